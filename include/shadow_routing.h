@@ -1,0 +1,146 @@
+/*
+ * shadow_routing.h -- C-ABI of the MI355X-native routing-table build for Shadow.
+ *
+ * Drop-in boundary: Shadow's routing module, /root/reference/src/main/routing/topology.h:17-28.
+ * The reference-signature entry points (topology_new, topology_attach, topology_getLatency, ...)
+ * are declared in include/topology.h and implemented on top of the srt_* functions below.
+ * Everything here uses plain C types (no glib, no torch): pointers, sizes, status codes.
+ *
+ * Table layout: row-major lat[n][n] in u32 quanta of `quantum_ns` nanoseconds
+ * and rel[n][n] f64, indexed by graph vertex index (GML order). The diagonal holds the
+ * "shortest path to self" rule (topology.c:1431-1576); undirected graphs are symmetric.
+ */
+#ifndef SHADOW_ROUTING_H
+#define SHADOW_ROUTING_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ----------------------------------------------------------------------- */
+enum {
+    SRT_OK = 0,
+    SRT_E_ARG = -1,       /* bad argument / shape */
+    SRT_E_PARSE = -2,     /* GML or unit parse error */
+    SRT_E_INVALID = -3,   /* graph failed validation (topology.c:659-1038) */
+    SRT_E_NOMEM = -4,     /* host or device allocation failed */
+    SRT_E_DEVICE = -5,    /* HIP error (never a silent CPU fallback) */
+    SRT_E_RANGE = -6,     /* path latencies exceed the u32-quantum table range */
+    SRT_E_COMM = -7,      /* RCCL error */
+    SRT_E_NOPATH = -8,    /* pair has no path (reference: utility_panic, topology.c:1970-1976) */
+    SRT_E_UNATTACHED = -9 /* address not attached (reference: returns -1, topology.c:1905-1915) */
+};
+
+/* ---- units grammar (restates src/main/core/support/units.rs:404-437, :776-837) ----------- */
+/* Nanoseconds, or -1 on a parse error / value > i64::MAX, or -2 where the reference's
+ * `.unwrap()` on the unit conversion would panic (u64 overflow, units.rs:821). */
+int64_t srt_parse_time_nanosec(const char* s);
+/* Bits per second, or -1 / -2 with the same meaning (units.rs:776-805). */
+int64_t srt_parse_bandwidth(const char* s);
+
+/* ---- device build ------------------------------------------------------------------------ */
+enum { SRT_ALGO_AUTO = 0, SRT_ALGO_DENSE_FW = 1, SRT_ALGO_SPARSE_SSSP = 2 };
+
+/* Graph handed over as canonical arrays (one arc per ordered vertex pair, see srt_canon_*). */
+typedef struct srt_edges {
+    int32_t n;
+    int32_t directed;
+    int64_t m;
+    const int32_t* src;    /* edge source vertex index (GML order) */
+    const int32_t* dst;    /* edge target vertex index */
+    const int64_t* lat_ns; /* parse_time_nanosec(latency) */
+    const double* loss;    /* packet_loss */
+} srt_edges;
+
+typedef struct srt_build_opts {
+    int32_t device;            /* HIP device ordinal */
+    int32_t algo;              /* SRT_ALGO_* */
+    int32_t use_shortest_path; /* network.use_shortest_path (configuration.rs:204-209) */
+    int32_t fw_block;          /* 0 = default pivot-block edge */
+} srt_build_opts;
+
+typedef struct srt_build_stats {
+    int32_t algo;        /* algorithm actually used */
+    int32_t fw_block;    /* pivot-block edge used by FW */
+    int64_t ess_arcs;    /* essential arcs found by the predecessor pass (dense) */
+    double ms_total;     /* wall time of the device build (HIP events), excl. host copies */
+    double ms_fw;        /* shortest-distance kernels */
+    double ms_post;      /* predecessor / reliability / diagonal / symmetry kernels */
+    int32_t max_depth;   /* deepest shortest-path tree seen by the reliability pass */
+} srt_build_stats;
+
+/* Build the full tables for an edge list on one GPU; outputs are host buffers of n*n entries.
+ * quantum_ns: the latency quantum (gcd of all edge latencies). Thread-safe per call. */
+int srt_build_tables(const srt_edges* g, const srt_build_opts* opts, uint32_t* lat_q,
+                     uint64_t* quantum_ns, double* rel, srt_build_stats* stats);
+
+/* Quantum and u32-range check used by srt_build_tables. Returns SRT_OK or SRT_E_RANGE. */
+int srt_latency_quantum(const srt_edges* g, uint64_t* quantum_ns, uint32_t* max_w_q);
+
+/* ---- device-resident dense build (benchmark / zero-copy path) ----------------------------
+ * All pointers are HIP device pointers on the current device; `stream` is a hipStream_t (NULL =
+ * default stream). Every matrix is ld x ld row-major with ld % 64 == 0 and ld >= n (rows and
+ * columns >= n are padding). w: u32 quanta, diagonal = self-loop (SRT_INF = no edge);
+ * r: f64 edge reliability (1 - loss). Outputs lat (u32 quanta) and rel (f64).
+ * The predecessor-pass workspace is allocated on first use and cached per device. */
+#define SRT_INF 0x7FFFFFFFu
+int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, const uint32_t* w,
+                           const double* r, uint32_t* lat, double* rel, void* stream,
+                           int32_t fw_block, srt_build_stats* stats);
+
+/* Synthetic graph generators on the device (seeded counter-based hash; identical to
+ * shadow_amd/graphs.py so tests can rebuild the same graph on the host). */
+int srt_gen_complete_device(int32_t n, int32_t ld, uint64_t seed, uint32_t lat_max_ms,
+                            uint32_t self_max_ms, uint32_t loss_max_e4, uint32_t* w, double* r,
+                            void* stream);
+
+/* ---- device-resident sparse build (CSR of canonical arcs, self-loops excluded) ----------
+ * Computes rows [src_begin, src_end) (row r of lat_rows/rel_rows = source src_begin + r, row
+ * stride n) with one workgroup per source and the distance row resident in LDS
+ * (n <= srt_sparse_max_n()). delta = bucket width in quanta (0 = default). */
+int srt_sparse_max_n(void);
+int srt_sparse_build_device(int32_t n, int32_t directed, const int32_t* rowptr,
+                            const int32_t* col, const uint32_t* w, const double* r,
+                            const int32_t* in_rowptr, const int32_t* in_col,
+                            const uint32_t* in_w, const double* in_r, const uint32_t* self_w,
+                            const double* self_r, int32_t src_begin, int32_t src_end,
+                            uint32_t delta, uint32_t* lat_rows, double* rel_rows, void* stream,
+                            srt_build_stats* stats);
+/* rel[s][t] <- rel[t][s] for s > t (undirected symmetry rule), ld x ld device matrix. */
+int srt_mirror_lower_device(int32_t n, int32_t ld, double* rel, void* stream);
+
+/* ---- multi-GPU (one process per GPU; RCCL over xGMI) ----------------------------------- */
+typedef struct srt_comm srt_comm;
+/* 128-byte RCCL unique id, created on rank 0 and shared by the caller (e.g. torch.distributed). */
+int srt_comm_unique_id(uint8_t out[128]);
+int srt_comm_init(const uint8_t id[128], int32_t nranks, int32_t rank, int32_t device,
+                  srt_comm** comm);
+void srt_comm_free(srt_comm* comm);
+/* Row-block partition used by every sharded build: rank r owns rows [begin, end). */
+void srt_shard_rows(int32_t n, int32_t align, int32_t nranks, int32_t rank, int32_t* begin,
+                    int32_t* end);
+/* Dense FW over row shards: each rank passes its rows [begin,end) of w/r (ld columns) and gets
+ * the same rows of lat/rel. Pivot-row panels are broadcast with RCCL once per round. */
+int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, int32_t directed,
+                            const uint32_t* w_rows, const double* r_rows, uint32_t* lat_rows,
+                            double* rel_rows, void* stream, int32_t fw_block,
+                            srt_build_stats* stats);
+/* Sparse: each rank computes its source rows, then ncclAllGather assembles the full tables
+ * (lat_all: n x n u32, rel_all: n x n f64, each rank's slice written in place). */
+int srt_sparse_allgather(srt_comm* comm, int32_t n, int32_t rows_per_rank, uint32_t* lat_all,
+                         double* rel_all, void* stream);
+
+/* ---- misc ------------------------------------------------------------------------------ */
+const char* srt_version(void);
+const char* srt_last_error(void); /* thread-local message for the last failing call */
+int srt_device_count(void);
+int srt_device_sync(int32_t device);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,88 @@
+/*
+ * topology.h -- drop-in replacement for Shadow's routing header.
+ *
+ * Reference interface: /root/reference/src/main/routing/topology.h:17-28 (same names, same
+ * argument meaning, same error behaviour). glib typedefs are restated with their ABI types
+ * (gchar = char, gboolean = int, gdouble = double, guint64 = uint64_t) so the header builds
+ * without glib; inside Shadow the glib definitions are ABI-identical.
+ *
+ * Address / Random stay opaque Shadow types: the implementation calls Shadow's own
+ * address_toNetworkIP() (address.h:78), address_toString(), random_nextDouble() (random.c:39)
+ * and worker_updateMinTimeJump() (worker.c:627). Weak fallbacks for standalone use live in
+ * shadow_amd/csrc/shadow_compat.c and are overridden by Shadow's strong symbols at link time.
+ */
+#ifndef SRT_TOPOLOGY_H
+#define SRT_TOPOLOGY_H
+
+#include <stdint.h>
+
+#include "shadow_routing.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct _Topology Topology;
+typedef struct _Address Address;
+typedef struct _Random Random;
+
+/* ---- reference signatures (topology.h:17-28) -------------------------------------------- */
+/* topology.c:2328-2354: load + validate the GML file, extract edge weights; NULL on failure. */
+Topology* topology_new(const char* graphPath, int useShortestPath);
+/* topology.c:2283-2326 */
+void topology_free(Topology* top);
+/* topology.c:2218-2272: choose a vertex for the address from the hints (exact IP > city >
+ * country > all; LPM or rand_r pick) and report the vertex bandwidths in KiB/s. */
+void topology_attach(Topology* top, Address* address, Random* randomSourcePool, char* ipHint,
+                     char* citycodeHint, char* countrycodeHint, uint64_t* bwDownOut,
+                     uint64_t* bwUpOut);
+/* topology.c:2274-2281 */
+void topology_detach(Topology* top, Address* address);
+/* topology.c:2019-2022 */
+int topology_isRoutable(Topology* top, Address* srcAddress, Address* dstAddress);
+/* topology.c:1995-2005: path latency in ms, -1 if an endpoint is not attached */
+double topology_getLatency(Topology* top, Address* srcAddress, Address* dstAddress);
+/* topology.c:2007-2017: path reliability in [0,1], -1 if an endpoint is not attached */
+double topology_getReliability(Topology* top, Address* srcAddress, Address* dstAddress);
+/* topology.c:1983-1993: panics (abort) if the path cannot be found */
+void topology_incrementPathPacketCounter(Topology* top, Address* srcAddress, Address* dstAddress);
+
+/* ---- additions behind the same ABI -------------------------------------- */
+/* Eager, idempotent all-pairs build on the GPU(s). The lookups call it lazily if needed.
+ * Calls worker_updateMinTimeJump() once with the minimum path latency (topology.c:1253-1264). */
+int topology_computeShortestPaths(Topology* top, int nGPUs);
+/* Zero-copy view of the finished tables (valid until topology_free). */
+int topology_getTable(Topology* top, const uint32_t** latQ, uint64_t* quantumNs,
+                      const double** rel, int* n);
+
+/* ---- network-order IP variants (no Shadow types; used by the Python mirror and tests) --- */
+Topology* srt_topology_new_from_string(const char* gmlText, int useShortestPath);
+int32_t srt_topology_attach_ip(Topology* top, uint32_t ipNet, uint32_t* randState,
+                               const char* ipHint, const char* citycodeHint,
+                               const char* countrycodeHint, uint64_t* bwDownOut,
+                               uint64_t* bwUpOut);
+void srt_topology_detach_ip(Topology* top, uint32_t ipNet);
+int32_t srt_topology_vertex_of_ip(Topology* top, uint32_t ipNet);
+double srt_topology_latency_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet);
+double srt_topology_reliability_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet);
+int srt_topology_increment_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet);
+uint64_t srt_topology_packet_count_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet);
+/* Graph facts established by validation (topology.c:659-716). */
+int32_t srt_topology_vertex_count(Topology* top);
+int64_t srt_topology_edge_count(Topology* top);
+int srt_topology_is_directed(Topology* top);
+int srt_topology_is_complete(Topology* top);
+/* Validated canonical edge arrays (GML order) -- the input of the device build. */
+int srt_topology_edges(Topology* top, srt_edges* out);
+/* Minimum latency (ms) over pairs of attached vertices incl. the diagonal (runahead export,
+ * controller.c:141-153); 0 if nothing is attached. */
+double srt_topology_min_latency_ms(Topology* top);
+/* Select the algorithm / device for topology_computeShortestPaths. */
+void srt_topology_set_build_opts(Topology* top, const srt_build_opts* opts);
+int srt_topology_last_stats(Topology* top, srt_build_stats* stats);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,121 @@
+"""TEST INFRASTRUCTURE ONLY -- CPU oracle for Shadow's routing precomputation.
+
+Python binding of oracle/oracle.c, the plain-C restatement of
+/root/reference/src/main/routing/topology.c (see oracle.h for the file:line map). Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg may import this package; the product
+(shadow_amd/) never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+
+ORC_INT_NS = 0
+ORC_F64_MS = 1
+U64_MAX = np.iinfo(np.uint64).max
+
+
+class _Graph(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int32),
+        ("directed", ctypes.c_int32),
+        ("m", ctypes.c_int64),
+        ("src", ctypes.c_void_p),
+        ("dst", ctypes.c_void_p),
+        ("lat_ns", ctypes.c_void_p),
+        ("loss", ctypes.c_void_p),
+    ]
+
+
+_lib = None
+
+
+def build() -> None:
+    """Compile liboracle.so in place (gcc)."""
+    import subprocess
+
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.orc_sssp_rows.restype = ctypes.c_int
+        L.orc_sssp_rows.argtypes = [ctypes.POINTER(_Graph), ctypes.c_int, ctypes.c_int32,
+                                    ctypes.c_int32, ctypes.c_int] + [ctypes.c_void_p] * 5
+        L.orc_table.restype = ctypes.c_int
+        L.orc_table.argtypes = [ctypes.POINTER(_Graph), ctypes.c_int, ctypes.c_int,
+                                ctypes.c_int] + [ctypes.c_void_p] * 4
+        _lib = L
+    return _lib
+
+
+class EdgeList:
+    """Edges in GML order: src/dst vertex indices, latency in ns, packet_loss."""
+
+    def __init__(self, n, directed, src, dst, lat_ns, loss):
+        self.n = int(n)
+        self.directed = int(bool(directed))
+        self.src = np.ascontiguousarray(src, dtype=np.int32)
+        self.dst = np.ascontiguousarray(dst, dtype=np.int32)
+        self.lat_ns = np.ascontiguousarray(lat_ns, dtype=np.int64)
+        self.loss = np.ascontiguousarray(loss, dtype=np.float64)
+        self.m = len(self.src)
+
+    def _c(self) -> _Graph:
+        return _Graph(self.n, self.directed, self.m, self.src.ctypes.data, self.dst.ctypes.data,
+                      self.lat_ns.ctypes.data, self.loss.ctypes.data)
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def sssp_rows(g: EdgeList, s0: int = 0, s1: int | None = None, mode: int = ORC_INT_NS,
+              nthreads: int = 1, want_pred: bool = False):
+    """Raw per-source rows [s0, s1): dict of lat_int, lat_ref, rel, lat_ms (, pred)."""
+    s1 = g.n if s1 is None else s1
+    rows = s1 - s0
+    out = {
+        "lat_int": np.empty((rows, g.n), np.uint64),
+        "lat_ref": np.empty((rows, g.n), np.uint64),
+        "rel": np.empty((rows, g.n), np.float64),
+        "lat_ms": np.empty((rows, g.n), np.float64),
+    }
+    pred = np.empty((rows, g.n), np.int32) if want_pred else None
+    cg = g._c()
+    rc = lib().orc_sssp_rows(ctypes.byref(cg), mode, s0, s1, nthreads, _ptr(out["lat_int"]),
+                             _ptr(out["lat_ref"]), _ptr(out["rel"]), _ptr(out["lat_ms"]),
+                             _ptr(pred))
+    if rc:
+        raise RuntimeError("orc_sssp_rows failed")
+    if want_pred:
+        out["pred"] = pred
+    return out
+
+
+def table(g: EdgeList, use_shortest_path: bool = True, mode: int = ORC_INT_NS,
+          nthreads: int = 1):
+    """Full n x n table as the reference's lookup API would return it for every vertex pair."""
+    n = g.n
+    out = {
+        "lat_int": np.empty((n, n), np.uint64),
+        "lat_ref": np.empty((n, n), np.uint64),
+        "rel": np.empty((n, n), np.float64),
+        "lat_ms": np.empty((n, n), np.float64),
+    }
+    cg = g._c()
+    rc = lib().orc_table(ctypes.byref(cg), int(bool(use_shortest_path)), mode, nthreads,
+                         _ptr(out["lat_int"]), _ptr(out["lat_ref"]), _ptr(out["rel"]),
+                         _ptr(out["lat_ms"]))
+    if rc:
+        raise RuntimeError("orc_table failed (direct mode needs a complete graph)")
+    return out

@@ -1,0 +1,995 @@
+/*
+ * dense.hip -- dense all-pairs build for gfx950: blocked min-plus Floyd-Warshall with LDS tiles,
+ * then the canonical-predecessor / path-order reliability pass, the symmetry mirror and the
+ * diagonal rule.
+ *
+ * Reference semantics (/root/reference/src/main/routing/topology.c):
+ *   distances      Dijkstra per source (:1682) -> here FW over integer latency quanta
+ *   predecessor    first-settled tight in-edge -> canonical argmin (D[s][u], u) over tight (u,t)
+ *   reliability    product of (1 - loss) in path order from the source (:1308-1309, :1365)
+ *   symmetry       one cached entry per unordered pair (:1194-1199) -> computed from min(s,t)
+ *   diagonal       shortest path to self (:1431-1576)
+ *
+ * Layout: every matrix is ld x ld row-major (ld % 64 == 0, rows/cols >= n are padding),
+ * distances u32 quanta with SRT_INF = 0x7FFFFFFF (a + b never wraps: both operands <= INF),
+ * reliabilities f64. No MFMA: min-plus is not an FMA contraction; the hot loop is
+ * v_add_u32 + v_min3_u32 over 4x4 register blocks fed by ds_read_b128 from LDS.
+ */
+#include "srt_device.h"
+
+#define B SRT_FW_B
+#define LDT SRT_FW_LDT
+
+/* ------------------------------------------------------------------------------------------ */
+/* synthetic complete graph (SURVEY.md §8d C1/C2/C4 generators)                               */
+/* ------------------------------------------------------------------------------------------ */
+__global__ void gen_complete_kernel(int n, int ld, uint64_t seed, uint32_t lat_max, uint32_t self_max,
+                                    uint32_t loss_max, uint32_t* __restrict__ w,
+                                    double* __restrict__ r) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y;
+    if (j >= ld) return;
+    size_t ix = (size_t)i * ld + j;
+    if (i >= n || j >= n) {
+        w[ix] = SRT_INF;
+        r[ix] = 0.0;
+        return;
+    }
+    uint32_t a = i < j ? i : j, b = i < j ? j : i;
+    uint32_t lat, k;
+    if (a == b) {
+        lat = 1u + (uint32_t)(srt_hash(seed, 2, a, a) % self_max);
+        k = (uint32_t)(srt_hash(seed, 3, a, a) % (loss_max + 1u));
+    } else {
+        lat = 1u + (uint32_t)(srt_hash(seed, 0, a, b) % lat_max);
+        k = (uint32_t)(srt_hash(seed, 1, a, b) % (loss_max + 1u));
+    }
+    w[ix] = lat;
+    double loss = (double)k / 10000.0;
+    r[ix] = 1.0 - loss;
+}
+
+extern "C" int srt_gen_complete_device(int32_t n, int32_t ld, uint64_t seed, uint32_t lat_max_ms,
+                                       uint32_t self_max_ms, uint32_t loss_max_e4, uint32_t* w,
+                                       double* r, void* stream) {
+    if (n <= 0 || ld < n || ld % B || !w || !r || lat_max_ms == 0 || self_max_ms == 0) {
+        srt_set_error("srt_gen_complete_device: bad arguments");
+        return SRT_E_ARG;
+    }
+    dim3 grid(srt_ceil_div(ld, 256), ld);
+    gen_complete_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(n, ld, seed, lat_max_ms, self_max_ms,
+                                                               loss_max_e4, w, r);
+    SRT_HIPCHK(hipGetLastError());
+    return SRT_OK;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* D <- W with a zero diagonal and INF padding                                                */
+/* ------------------------------------------------------------------------------------------ */
+__global__ void init_dist_kernel(int n, int ld, int row0, const uint32_t* __restrict__ w,
+                                 uint32_t* __restrict__ d) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = row0 + blockIdx.y; /* global row */
+    if (j >= ld) return;
+    size_t ix = (size_t)blockIdx.y * ld + j;
+    uint32_t v = (i < n && j < n) ? w[ix] : SRT_INF;
+    if (v > SRT_INF) v = SRT_INF;
+    d[ix] = (i == j) ? 0u : v;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* 64x64x64 min-plus tile product: C = min(C, A (x) Bm), 256 threads, 4x4 outputs per thread. */
+/* A is staged transposed (At[m][row]) so a thread's 4 rows are one ds_read_b128, Bm row-major. */
+/* ------------------------------------------------------------------------------------------ */
+__device__ __forceinline__ void stage_tile(uint32_t* __restrict__ s, const uint32_t* __restrict__ g,
+                                           int ldg, int tid) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        int idx = tid + it * 256; /* 1024 uint4 = 64 rows x 16 */
+        int row = idx >> 4, c4 = (idx & 15) << 2;
+        uint4 v = *reinterpret_cast<const uint4*>(g + (size_t)row * ldg + c4);
+        *reinterpret_cast<uint4*>(s + row * LDT + c4) = v;
+    }
+}
+
+__device__ __forceinline__ void stage_tile_T(uint32_t* __restrict__ s, const uint32_t* __restrict__ g,
+                                             int ldg, int tid) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        int idx = tid + it * 256;
+        int row = idx >> 4, c4 = (idx & 15) << 2;
+        uint4 v = *reinterpret_cast<const uint4*>(g + (size_t)row * ldg + c4);
+        s[(c4 + 0) * LDT + row] = v.x;
+        s[(c4 + 1) * LDT + row] = v.y;
+        s[(c4 + 2) * LDT + row] = v.z;
+        s[(c4 + 3) * LDT + row] = v.w;
+    }
+}
+
+__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) {
+    return min(a, min(b, c));
+}
+
+/* acc (4x4 in registers) <- min(acc, sAt (x) sB); LDS already staged and synchronized. */
+__device__ __forceinline__ void minplus_acc(uint32_t (&acc)[4][4], const uint32_t* __restrict__ sAt,
+                                            const uint32_t* __restrict__ sB, int tx, int ty) {
+#pragma unroll 8
+    for (int m = 0; m < B; m += 2) {
+        uint4 a0 = *reinterpret_cast<const uint4*>(sAt + m * LDT + 4 * ty);
+        uint4 b0 = *reinterpret_cast<const uint4*>(sB + m * LDT + 4 * tx);
+        uint4 a1 = *reinterpret_cast<const uint4*>(sAt + (m + 1) * LDT + 4 * ty);
+        uint4 b1 = *reinterpret_cast<const uint4*>(sB + (m + 1) * LDT + 4 * tx);
+        const uint32_t av0[4] = {a0.x, a0.y, a0.z, a0.w};
+        const uint32_t bv0[4] = {b0.x, b0.y, b0.z, b0.w};
+        const uint32_t av1[4] = {a1.x, a1.y, a1.z, a1.w};
+        const uint32_t bv1[4] = {b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                acc[a][b] = umin3(acc[a][b], av0[a] + bv0[b], av1[a] + bv1[b]);
+    }
+}
+
+__device__ __forceinline__ void load_acc(uint32_t (&acc)[4][4], const uint32_t* __restrict__ C,
+                                         int ldc, int tx, int ty) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        uint4 v = *reinterpret_cast<const uint4*>(C + (size_t)(4 * ty + a) * ldc + 4 * tx);
+        acc[a][0] = v.x;
+        acc[a][1] = v.y;
+        acc[a][2] = v.z;
+        acc[a][3] = v.w;
+    }
+}
+
+/* store only the 16-byte rows that changed: unchanged tiles cost no HBM write */
+__device__ __forceinline__ void store_acc(const uint32_t (&acc)[4][4], const uint32_t (&old)[4][4],
+                                          uint32_t* __restrict__ C, int ldc, int tx, int ty) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        uint4* p = reinterpret_cast<uint4*>(C + (size_t)(4 * ty + a) * ldc + 4 * tx);
+        if (old[a][0] != acc[a][0] || old[a][1] != acc[a][1] || old[a][2] != acc[a][2] ||
+            old[a][3] != acc[a][3])
+            *p = make_uint4(acc[a][0], acc[a][1], acc[a][2], acc[a][3]);
+    }
+}
+
+/* Phase 1: closure of the diagonal tile (pivots kB..kB+63), in LDS, one workgroup. */
+__global__ __launch_bounds__(256) void fw_diag_kernel(uint32_t* __restrict__ P, int ld, int k0) {
+    __shared__ __attribute__((aligned(16))) uint32_t s[B * LDT];
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    uint32_t* T = P + k0;
+    stage_tile(s, T, ld, tid);
+    __syncthreads();
+    for (int m = 0; m < B; ++m) {
+        uint4 bm = *reinterpret_cast<const uint4*>(s + m * LDT + 4 * tx);
+        uint32_t am[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) am[a] = s[(4 * ty + a) * LDT + m];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            uint4* row = reinterpret_cast<uint4*>(s + (4 * ty + a) * LDT + 4 * tx);
+            uint4 v = *row;
+            v.x = min(v.x, am[a] + bm.x);
+            v.y = min(v.y, am[a] + bm.y);
+            v.z = min(v.z, am[a] + bm.z);
+            v.w = min(v.w, am[a] + bm.w);
+            *row = v;
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        uint4 v = *reinterpret_cast<const uint4*>(s + (4 * ty + a) * LDT + 4 * tx);
+        *reinterpret_cast<uint4*>(T + (size_t)(4 * ty + a) * ld + 4 * tx) = v;
+    }
+}
+
+/* Phase 2: pivot-row panel tiles (k, j): X <- Dkk* (x) X, and pivot-column tiles (i, k):
+ * X <- X (x) Dkk*. P = the B x ld pivot-row panel (closed diagonal tile at column k0).
+ * D holds `nrow_tiles` local row tiles whose first global row is row0. */
+__global__ __launch_bounds__(256) void fw_panel_kernel(uint32_t* __restrict__ D, int ld, int row0,
+                                                       int nrow_tiles, uint32_t* __restrict__ P,
+                                                       int k0, int ncol_tiles, int do_row,
+                                                       int do_col) {
+    __shared__ __attribute__((aligned(16))) uint32_t sA[B * LDT];
+    __shared__ __attribute__((aligned(16))) uint32_t sB[B * LDT];
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    int bid = blockIdx.x;
+    uint32_t* C;
+    if (bid < ncol_tiles) {
+        if (!do_row || bid * B == k0) return;
+        C = P + bid * B;
+        stage_tile_T(sA, P + k0, ld, tid); /* Dkk* */
+        stage_tile(sB, C, ld, tid);
+    } else {
+        bid -= ncol_tiles;
+        if (!do_col || bid >= nrow_tiles || row0 + bid * B == k0) return;
+        C = D + (size_t)bid * B * ld + k0;
+        stage_tile_T(sA, C, ld, tid);
+        stage_tile(sB, P + k0, ld, tid);
+    }
+    __syncthreads();
+    uint32_t acc[4][4], old[4][4];
+    load_acc(old, C, ld, tx, ty);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = old[a][b];
+    minplus_acc(acc, sA, sB, tx, ty);
+    store_acc(acc, old, C, ld, tx, ty);
+}
+
+/* Phase 3: every other tile (i, j): D_ij <- min(D_ij, D_ik (x) P_kj). */
+__global__ __launch_bounds__(256) void fw_update_kernel(uint32_t* __restrict__ D, int ld, int row0,
+                                                        const uint32_t* __restrict__ P, int k0) {
+    __shared__ __attribute__((aligned(16))) uint32_t sA[B * LDT];
+    __shared__ __attribute__((aligned(16))) uint32_t sB[B * LDT];
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int J = blockIdx.x, I = blockIdx.y;
+    if (J * B == k0 || row0 + I * B == k0) return;
+    uint32_t* C = D + (size_t)I * B * ld + J * B;
+    stage_tile_T(sA, D + (size_t)I * B * ld + k0, ld, tid);
+    stage_tile(sB, P + J * B, ld, tid);
+    __syncthreads();
+    uint32_t acc[4][4], old[4][4];
+    load_acc(old, C, ld, tx, ty);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = old[a][b];
+    minplus_acc(acc, sA, sB, tx, ty);
+    store_acc(acc, old, C, ld, tx, ty);
+}
+
+/* One FW round on a row shard. P is the B x ld pivot-row panel: in place (D + (k0-row0)*ld) on
+ * the rank that owns rows [k0, k0+B), a received copy elsewhere. The owner part (diagonal closure
+ * + row panel) must finish before the panel is broadcast; the rest runs on every rank. */
+static int fw_owner_part(uint32_t* D, int ld, int row0, int nrows, uint32_t* P, int k0,
+                         hipStream_t st) {
+    const int nb = ld / B, nrb = nrows / B;
+    fw_diag_kernel<<<1, 256, 0, st>>>(P, ld, k0);
+    fw_panel_kernel<<<nb, 256, 0, st>>>(D, ld, row0, nrb, P, k0, nb, 1, 0);
+    SRT_HIPCHK(hipGetLastError());
+    return SRT_OK;
+}
+
+static int fw_shard_part(uint32_t* D, int ld, int row0, int nrows, const uint32_t* P, int k0,
+                         hipStream_t st) {
+    const int nb = ld / B, nrb = nrows / B;
+    if (nrb == 0) return SRT_OK;
+    fw_panel_kernel<<<nb + nrb, 256, 0, st>>>(D, ld, row0, nrb, (uint32_t*)P, k0, nb, 0, 1);
+    fw_update_kernel<<<dim3(nb, nrb), 256, 0, st>>>(D, ld, row0, P, k0);
+    SRT_HIPCHK(hipGetLastError());
+    return SRT_OK;
+}
+
+int srt_dense_fw_device(int32_t n, int32_t ld, uint32_t* d, hipStream_t st) {
+    (void)n;
+    for (int k0 = 0; k0 < ld; k0 += B) {
+        uint32_t* P = d + (size_t)k0 * ld;
+        int rc = fw_owner_part(d, ld, 0, ld, P, k0, st);
+        if (!rc) rc = fw_shard_part(d, ld, 0, ld, P, k0, st);
+        if (rc) return rc;
+    }
+    return SRT_OK;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Essential arcs: (u,t) with W[u][t] == D[u][t] (u != t). Every tight predecessor of any      */
+/* (s,t) is essential: D[s][u] + W[u][t] = D[s][t] <= D[s][u] + D[u][t] forces D[u][t] = W.    */
+/* Rows are local (global row = row0 + blockIdx.x); counts go to cnt[global row].            */
+/* ------------------------------------------------------------------------------------------ */
+__global__ __launch_bounds__(256) void ess_count_kernel(int n, int ld, int row0,
+                                                        const uint32_t* __restrict__ w,
+                                                        const uint32_t* __restrict__ d,
+                                                        int32_t* __restrict__ cnt) {
+    const int u = row0 + blockIdx.x;
+    if (u >= n) return;
+    const uint32_t* wr = w + (size_t)blockIdx.x * ld;
+    const uint32_t* dr = d + (size_t)blockIdx.x * ld;
+    int c = 0;
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        uint32_t x = wr[t];
+        c += (t != u && x < SRT_INF && x == dr[t]) ? 1 : 0;
+    }
+    __shared__ int red[256];
+    red[threadIdx.x] = c;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) cnt[u] = red[0];
+}
+
+/* exclusive scan of cnt[0..n) into ptr[0..n], one workgroup of 1024 threads */
+__global__ __launch_bounds__(1024) void scan_kernel(int n, const int32_t* __restrict__ cnt,
+                                                    int32_t* __restrict__ ptr) {
+    __shared__ int64_t part[1024];
+    const int tid = threadIdx.x;
+    const int chunk = (n + 1023) / 1024;
+    const int b = tid * chunk, e = min(n, b + chunk);
+    int64_t s = 0;
+    for (int i = b; i < e; ++i) s += cnt[i];
+    part[tid] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        int64_t v = tid >= off ? part[tid - off] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int64_t run = part[tid] - s;
+    for (int i = b; i < e; ++i) {
+        ptr[i] = (int32_t)run;
+        run += cnt[i];
+    }
+    if (tid == 1023) ptr[n] = (int32_t)part[1023];
+}
+
+/* fill essential out-arcs of local row u at ptr[u], ascending t (wave ballot compaction) */
+__global__ __launch_bounds__(256) void ess_fill_kernel(int n, int ld, int row0,
+                                                       const uint32_t* __restrict__ w,
+                                                       const double* __restrict__ r,
+                                                       const uint32_t* __restrict__ d,
+                                                       const int32_t* __restrict__ ptr,
+                                                       int32_t* __restrict__ col,
+                                                       uint32_t* __restrict__ aw,
+                                                       double* __restrict__ ar) {
+    const int u = row0 + blockIdx.x;
+    if (u >= n) return;
+    const uint32_t* wr = w + (size_t)blockIdx.x * ld;
+    const uint32_t* dr = d + (size_t)blockIdx.x * ld;
+    const double* rr = r + (size_t)blockIdx.x * ld;
+    __shared__ int wave_cnt[4];
+    __shared__ int base;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x == 0) base = ptr[u];
+    __syncthreads();
+    for (int t0 = 0; t0 < n; t0 += 256) {
+        int t = t0 + threadIdx.x;
+        bool ok = false;
+        uint32_t x = 0;
+        if (t < n) {
+            x = wr[t];
+            ok = (t != u && x < SRT_INF && x == dr[t]);
+        }
+        uint64_t mask = __ballot(ok);
+        int before = __popcll(mask & ((1ull << lane) - 1ull));
+        if (lane == 0) wave_cnt[wv] = __popcll(mask);
+        __syncthreads();
+        int off = base;
+        for (int q = 0; q < wv; ++q) off += wave_cnt[q];
+        if (ok) {
+            int o = off + before;
+            col[o] = t;
+            aw[o] = x;
+            ar[o] = rr[t];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) base += wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
+        __syncthreads();
+    }
+}
+
+/* transpose an arc list (directed graphs: In*(t) from Out*(u)) */
+__global__ void arc_count_by_col(int64_t arcs, const int32_t* __restrict__ col,
+                                 int32_t* __restrict__ cnt) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < arcs) atomicAdd(&cnt[col[i]], 1);
+}
+
+__global__ void arc_transpose_fill(int n, const int32_t* __restrict__ ptr,
+                                   const int32_t* __restrict__ col, const uint32_t* __restrict__ aw,
+                                   const double* __restrict__ ar, int32_t* __restrict__ cursor,
+                                   int32_t* __restrict__ tcol, uint32_t* __restrict__ tw,
+                                   double* __restrict__ tr) {
+    int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= n) return;
+    for (int k = ptr[u]; k < ptr[u + 1]; ++k) {
+        int t = col[k];
+        int o = atomicAdd(&cursor[t], 1);
+        tcol[o] = u;
+        tw[o] = aw[k];
+        tr[o] = ar[k];
+    }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Canonical predecessor + path-order reliability, one workgroup per source row s.            */
+/* pred(s,t) = argmin over essential in-arcs (u,t) with D[s][u] + w == D[s][t] of (D[s][u], u) */
+/* rel(s,t)  = rel(s,pred) * r(pred,t), rel(s,s) = 1  -> the product in path order.            */
+/* ------------------------------------------------------------------------------------------ */
+template <bool DROW_LDS>
+__global__ __launch_bounds__(512) void dense_predrel_kernel(int n, int ld, int row0,
+                                                            const uint32_t* __restrict__ d,
+                                                            const int32_t* __restrict__ iptr,
+                                                            const int32_t* __restrict__ icol,
+                                                            const uint32_t* __restrict__ iw,
+                                                            const double* __restrict__ ir,
+                                                            double* __restrict__ rel,
+                                                            int32_t* __restrict__ max_depth) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int s = row0 + blockIdx.x;
+    if (s >= n) return;
+    const uint32_t* dg = d + (size_t)blockIdx.x * ld;
+    uint32_t* drow = smem;
+    int32_t* arc = reinterpret_cast<int32_t*>(smem + (DROW_LDS ? ld : 0));
+    if (DROW_LDS)
+        for (int t = threadIdx.x; t < n; t += blockDim.x) drow[t] = dg[t];
+    __syncthreads();
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        int bk = -1;
+        if (t != s) {
+            const uint32_t dt = DROW_LDS ? drow[t] : dg[t];
+            uint64_t best = ~0ull;
+            const int kb = iptr[t], ke = iptr[t + 1];
+            for (int k = kb; k < ke; ++k) {
+                const int u = icol[k];
+                const uint32_t du = DROW_LDS ? drow[u] : dg[u];
+                if (du + iw[k] == dt) {
+                    uint64_t key = ((uint64_t)du << 32) | (uint32_t)u;
+                    if (key < best) {
+                        best = key;
+                        bk = k;
+                    }
+                }
+            }
+        }
+        arc[t] = bk;
+    }
+    __syncthreads();
+    double* rr = rel + (size_t)blockIdx.x * ld;
+    /* each thread owns t = tid + i*blockDim (i < 64 for n <= 32768) */
+    uint64_t pending = 0;
+    int nt = 0;
+    for (int t = threadIdx.x; t < n; t += blockDim.x, ++nt) {
+        if (t == s) {
+            rr[t] = 1.0;
+        } else {
+            rr[t] = -1.0;
+            pending |= 1ull << nt;
+        }
+    }
+    __syncthreads();
+    int depth = 0;
+    for (;;) {
+        int any = 0;
+        int i = 0;
+        for (int t = threadIdx.x; t < n; t += blockDim.x, ++i) {
+            if (!((pending >> i) & 1ull)) continue;
+            const int k = arc[t];
+            if (k < 0) { /* unreachable (cannot happen on a validated graph) */
+                rr[t] = 0.0;
+                pending &= ~(1ull << i);
+                continue;
+            }
+            const double rp = __hip_atomic_load(rr + icol[k], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (rp >= 0.0) {
+                __hip_atomic_store(rr + t, rp * ir[k], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                pending &= ~(1ull << i);
+            } else {
+                any = 1;
+            }
+        }
+        ++depth;
+        if (!__syncthreads_or(any)) break;
+    }
+    if (threadIdx.x == 0) atomicMax(max_depth, depth);
+}
+
+/* Diagonal rule (topology.c:1431-1576): min over incident OUT edges of (self-loop: L,
+ * other: 2L) with the first strict minimum in (neighbor, edge) order; rel r or r^2. */
+__global__ __launch_bounds__(256) void dense_diag_kernel(int n, int ld, int row0, int nrows,
+                                                         const uint32_t* __restrict__ w,
+                                                         const double* __restrict__ r,
+                                                         uint32_t* __restrict__ d,
+                                                         double* __restrict__ rel) {
+    const int lr = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int v = row0 + lr;
+    const int lane = threadIdx.x & 63;
+    if (lr >= nrows || v >= n) return;
+    const uint32_t* wr = w + (size_t)lr * ld;
+    uint64_t best = ~0ull;
+    for (int u = lane; u < n; u += 64) {
+        uint32_t x = wr[u];
+        if (x >= SRT_INF) continue;
+        uint64_t lat = (u == v) ? x : 2ull * x;
+        uint64_t key = (lat << 32) | (uint32_t)u;
+        best = key < best ? key : best;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        uint64_t o = __shfl_xor(best, off);
+        best = o < best ? o : best;
+    }
+    if (lane == 0) {
+        size_t ix = (size_t)lr * ld + v;
+        if (best == ~0ull) {
+            d[ix] = 0;
+            rel[ix] = 0.0;
+        } else {
+            int u = (int)(best & 0xffffffffu);
+            double x = r[(size_t)lr * ld + u];
+            d[ix] = (uint32_t)(best >> 32);
+            rel[ix] = (u == v) ? x : x * x;
+        }
+    }
+}
+
+/* rel[s][t] <- rel[t][s] for s > t inside one square block (rows/cols [b, e) of the matrix,
+ * local rows start at b). */
+__global__ __launch_bounds__(256) void mirror_block_kernel(int n, int ld, int b, int e,
+                                                           double* __restrict__ rel_rows) {
+    __shared__ double tile[64][65];
+    const int I = blockIdx.y, J = blockIdx.x;
+    if (J > I) return;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int a = ty; a < 64; a += 4) {
+        int t = b + J * 64 + a, s = b + I * 64 + tx;
+        tile[a][tx] = (t < e && s < e && t < n && s < n) ? rel_rows[(size_t)(t - b) * ld + s] : 0.0;
+    }
+    __syncthreads();
+    for (int a = ty; a < 64; a += 4) {
+        int s = b + I * 64 + a, t = b + J * 64 + tx;
+        if (s < e && t < e && s < n && s > t) rel_rows[(size_t)(s - b) * ld + t] = tile[tx][a];
+    }
+}
+
+/* pack rel_rows[:, c0:c1] (nrows x (c1-c0)) into a contiguous buffer */
+__global__ void pack_cols_kernel(int nrows, int ld, int c0, int c1, const double* __restrict__ src,
+                                 double* __restrict__ dst) {
+    const int w = c1 - c0;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)nrows * w) return;
+    const int r = (int)(i / w), c = (int)(i % w);
+    dst[i] = src[(size_t)r * ld + c0 + c];
+}
+
+/* rel_rows[s - b][c0 + t'] <- buf[t'][s - b] (buf = the peer's packed block, peer rows x our rows) */
+__global__ __launch_bounds__(256) void unpack_transpose_kernel(int nrows, int ld, int c0, int pw,
+                                                               const double* __restrict__ buf,
+                                                               double* __restrict__ rel_rows) {
+    __shared__ double tile[64][65];
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int R0 = blockIdx.y * 64; /* our local rows */
+    const int C0 = blockIdx.x * 64; /* peer rows = our columns c0.. */
+    for (int a = ty; a < 64; a += 4) {
+        int pr = C0 + a, lr = R0 + tx;
+        tile[a][tx] = (pr < pw && lr < nrows) ? buf[(size_t)pr * nrows + lr] : 0.0;
+    }
+    __syncthreads();
+    for (int a = ty; a < 64; a += 4) {
+        int lr = R0 + a, pr = C0 + tx;
+        if (lr < nrows && pr < pw) rel_rows[(size_t)lr * ld + c0 + pr] = tile[tx][a];
+    }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* host orchestration of the dense post pass (single GPU or one row shard)                    */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+    size_t n_cap, arc_cap, tarc_cap, x_cap;
+    int32_t *cnt, *ptr, *tptr, *cursor, *col, *tcol, *depth;
+    uint32_t *aw, *tw;
+    double *ar, *tr, *xsend, *xrecv;
+    uint32_t* panel;
+    size_t panel_cap;
+} dense_ws;
+
+static dense_ws g_ws[64];
+
+static int ws_grow(void** p, size_t* cap, size_t need, size_t elem) {
+    if (*cap >= need && *p) return SRT_OK;
+    if (*p) SRT_HIPCHK(hipFree(*p));
+    *p = NULL;
+    size_t c = need + need / 4 + 1024;
+    SRT_HIPCHK(hipMalloc(p, c * elem));
+    *cap = c;
+    return SRT_OK;
+}
+
+static int ws_get(dense_ws** out, int n) {
+    int dev = 0;
+    SRT_HIPCHK(hipGetDevice(&dev));
+    dense_ws* ws = &g_ws[dev & 63];
+    if (ws->n_cap < (size_t)n + 1 || !ws->cnt) {
+        if (ws->cnt) {
+            SRT_HIPCHK(hipFree(ws->cnt));
+            SRT_HIPCHK(hipFree(ws->ptr));
+            SRT_HIPCHK(hipFree(ws->tptr));
+            SRT_HIPCHK(hipFree(ws->cursor));
+            SRT_HIPCHK(hipFree(ws->depth));
+        }
+        size_t c = (size_t)n + 1;
+        SRT_HIPCHK(hipMalloc(&ws->cnt, c * sizeof(int32_t)));
+        SRT_HIPCHK(hipMalloc(&ws->ptr, c * sizeof(int32_t)));
+        SRT_HIPCHK(hipMalloc(&ws->tptr, c * sizeof(int32_t)));
+        SRT_HIPCHK(hipMalloc(&ws->cursor, c * sizeof(int32_t)));
+        SRT_HIPCHK(hipMalloc(&ws->depth, sizeof(int32_t)));
+        ws->n_cap = c;
+    }
+    *out = ws;
+    return SRT_OK;
+}
+
+static int grow_arcs(dense_ws* ws, size_t need) {
+    int rc;
+    size_t c1 = ws->arc_cap, c2 = ws->arc_cap, c3 = ws->arc_cap;
+    if ((rc = ws_grow((void**)&ws->col, &c1, need, sizeof(int32_t)))) return rc;
+    if ((rc = ws_grow((void**)&ws->aw, &c2, need, sizeof(uint32_t)))) return rc;
+    if ((rc = ws_grow((void**)&ws->ar, &c3, need, sizeof(double)))) return rc;
+    ws->arc_cap = c1;
+    return SRT_OK;
+}
+
+/* gather hook for sharded builds: makes the essential-arc counts / arcs global */
+typedef int (*ess_gather_fn)(void* ctx, dense_ws* ws, int n, int phase, int32_t total,
+                             hipStream_t st);
+
+static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_t directed,
+                      const uint32_t* w, const double* r, uint32_t* d, double* rel, hipStream_t st,
+                      srt_build_stats* stats, ess_gather_fn gather, void* gctx) {
+    dense_ws* ws;
+    int rc = ws_get(&ws, n);
+    if (rc) return rc;
+    const int lrows = max(0, min(nrows, n - row0)); /* real (non-padding) local rows */
+    SRT_HIPCHK(hipMemsetAsync(ws->cnt, 0, (size_t)(n + 1) * sizeof(int32_t), st));
+    if (lrows > 0) ess_count_kernel<<<lrows, 256, 0, st>>>(n, ld, row0, w, d, ws->cnt);
+    if (gather && (rc = gather(gctx, ws, n, 0, 0, st))) return rc; /* all-reduce counts */
+    scan_kernel<<<1, 1024, 0, st>>>(n, ws->cnt, ws->ptr);
+    SRT_HIPCHK(hipGetLastError());
+    int32_t total = 0;
+    SRT_HIPCHK(hipMemcpyAsync(&total, ws->ptr + n, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    SRT_HIPCHK(hipStreamSynchronize(st));
+    if (total < 0) {
+        srt_set_error("essential-arc count overflow");
+        return SRT_E_RANGE;
+    }
+    if ((rc = grow_arcs(ws, (size_t)total + 1))) return rc;
+    if (lrows > 0)
+        ess_fill_kernel<<<lrows, 256, 0, st>>>(n, ld, row0, w, r, d, ws->ptr, ws->col, ws->aw, ws->ar);
+    SRT_HIPCHK(hipGetLastError());
+    if (gather && (rc = gather(gctx, ws, n, 1, total, st))) return rc; /* share the arcs */
+    const int32_t *iptr = ws->ptr, *icol = ws->col;
+    const uint32_t* iw = ws->aw;
+    const double* ir = ws->ar;
+    if (directed) {
+        size_t t1 = ws->tarc_cap, t2 = ws->tarc_cap, t3 = ws->tarc_cap;
+        if ((rc = ws_grow((void**)&ws->tcol, &t1, (size_t)total + 1, sizeof(int32_t)))) return rc;
+        if ((rc = ws_grow((void**)&ws->tw, &t2, (size_t)total + 1, sizeof(uint32_t)))) return rc;
+        if ((rc = ws_grow((void**)&ws->tr, &t3, (size_t)total + 1, sizeof(double)))) return rc;
+        ws->tarc_cap = t1;
+        SRT_HIPCHK(hipMemsetAsync(ws->cnt, 0, (size_t)n * sizeof(int32_t), st));
+        if (total > 0)
+            arc_count_by_col<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, ws->col, ws->cnt);
+        scan_kernel<<<1, 1024, 0, st>>>(n, ws->cnt, ws->tptr);
+        SRT_HIPCHK(hipMemcpyAsync(ws->cursor, ws->tptr, (size_t)n * sizeof(int32_t),
+                                  hipMemcpyDeviceToDevice, st));
+        arc_transpose_fill<<<srt_ceil_div(n, 256), 256, 0, st>>>(n, ws->ptr, ws->col, ws->aw, ws->ar,
+                                                                ws->cursor, ws->tcol, ws->tw, ws->tr);
+        SRT_HIPCHK(hipGetLastError());
+        iptr = ws->tptr;
+        icol = ws->tcol;
+        iw = ws->tw;
+        ir = ws->tr;
+    }
+    SRT_HIPCHK(hipMemsetAsync(ws->depth, 0, sizeof(int32_t), st));
+    if (n > 512 * 64) {
+        srt_set_error("dense predecessor pass supports n <= 32768 (n = %d)", n);
+        return SRT_E_ARG;
+    }
+    if (lrows > 0) {
+        size_t lds_both = (size_t)2 * ld * sizeof(uint32_t);
+        if (lds_both <= 160 * 1024) {
+            SRT_HIPCHK(hipFuncSetAttribute((const void*)dense_predrel_kernel<true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds_both));
+            dense_predrel_kernel<true><<<lrows, 512, lds_both, st>>>(n, ld, row0, d, iptr, icol, iw,
+                                                                      ir, rel, ws->depth);
+        } else {
+            size_t lds = (size_t)ld * sizeof(uint32_t);
+            SRT_HIPCHK(hipFuncSetAttribute((const void*)dense_predrel_kernel<false>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            dense_predrel_kernel<false><<<lrows, 512, lds, st>>>(n, ld, row0, d, iptr, icol, iw, ir,
+                                                                  rel, ws->depth);
+        }
+        SRT_HIPCHK(hipGetLastError());
+    }
+    if (stats) {
+        stats->ess_arcs = total;
+    }
+    return SRT_OK;
+}
+
+static int dense_finish_rows(int32_t n, int32_t ld, int32_t row0, int32_t nrows, const uint32_t* w,
+                             const double* r, uint32_t* d, double* rel, hipStream_t st,
+                             srt_build_stats* stats) {
+    const int lrows = max(0, min(nrows, n - row0));
+    if (lrows > 0) dense_diag_kernel<<<srt_ceil_div(lrows, 4), 256, 0, st>>>(n, ld, row0, lrows, w, r, d, rel);
+    SRT_HIPCHK(hipGetLastError());
+    if (stats) {
+        dense_ws* ws;
+        int rc = ws_get(&ws, n);
+        if (rc) return rc;
+        int32_t depth = 0;
+        SRT_HIPCHK(hipMemcpyAsync(&depth, ws->depth, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipStreamSynchronize(st));
+        stats->max_depth = depth;
+    }
+    return SRT_OK;
+}
+
+int srt_dense_post_device(int32_t n, int32_t ld, int32_t directed, const uint32_t* w, const double* r,
+                          uint32_t* d, double* rel, hipStream_t st, srt_build_stats* stats) {
+    int rc = dense_post(n, ld, 0, ld, directed, w, r, d, rel, st, stats, NULL, NULL);
+    if (rc) return rc;
+    if (!directed) {
+        dim3 g(srt_ceil_div(n, 64), srt_ceil_div(n, 64));
+        mirror_block_kernel<<<g, 256, 0, st>>>(n, ld, 0, n, rel);
+        SRT_HIPCHK(hipGetLastError());
+    }
+    return dense_finish_rows(n, ld, 0, ld, w, r, d, rel, st, stats);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* public device-resident dense build                                                         */
+/* ------------------------------------------------------------------------------------------ */
+extern "C" int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, const uint32_t* w,
+                                      const double* r, uint32_t* lat, double* rel, void* stream,
+                                      int32_t fw_block, srt_build_stats* stats) {
+    if (n <= 0 || ld < n || ld % B || !w || !r || !lat || !rel) {
+        srt_set_error("srt_dense_build_device: bad arguments (n=%d ld=%d)", n, ld);
+        return SRT_E_ARG;
+    }
+    if (fw_block != 0 && fw_block != B) {
+        srt_set_error("srt_dense_build_device: fw_block must be 0 or %d", B);
+        return SRT_E_ARG;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    hipEvent_t e0, e1, e2;
+    SRT_HIPCHK(hipEventCreate(&e0));
+    SRT_HIPCHK(hipEventCreate(&e1));
+    SRT_HIPCHK(hipEventCreate(&e2));
+    SRT_HIPCHK(hipEventRecord(e0, st));
+    dim3 g(srt_ceil_div(ld, 256), ld);
+    init_dist_kernel<<<g, 256, 0, st>>>(n, ld, 0, w, lat);
+    SRT_HIPCHK(hipGetLastError());
+    int rc = srt_dense_fw_device(n, ld, lat, st);
+    if (rc) return rc;
+    SRT_HIPCHK(hipEventRecord(e1, st));
+    rc = srt_dense_post_device(n, ld, directed, w, r, lat, rel, st, stats);
+    if (rc) return rc;
+    SRT_HIPCHK(hipEventRecord(e2, st));
+    if (stats) {
+        SRT_HIPCHK(hipEventSynchronize(e2));
+        float a = 0, b = 0;
+        SRT_HIPCHK(hipEventElapsedTime(&a, e0, e1));
+        SRT_HIPCHK(hipEventElapsedTime(&b, e1, e2));
+        stats->algo = SRT_ALGO_DENSE_FW;
+        stats->fw_block = B;
+        stats->ms_fw = a;
+        stats->ms_post = b;
+        stats->ms_total = a + b;
+    }
+    SRT_HIPCHK(hipEventDestroy(e0));
+    SRT_HIPCHK(hipEventDestroy(e1));
+    SRT_HIPCHK(hipEventDestroy(e2));
+    return SRT_OK;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* row-sharded dense build over RCCL (one process per GPU)                                    */
+/* ------------------------------------------------------------------------------------------ */
+#include <rccl/rccl.h>
+
+int srt_comm_rank(const srt_comm* c);
+int srt_comm_size(const srt_comm* c);
+ncclComm_t srt_comm_nccl(const srt_comm* c);
+
+#define SRT_NCCLCHK(expr)                                                                  \
+    do {                                                                                   \
+        ncclResult_t r_ = (expr);                                                          \
+        if (r_ != ncclSuccess) {                                                           \
+            srt_set_error("RCCL error %s at %s:%d (%s)", ncclGetErrorString(r_), __FILE__, \
+                          __LINE__, #expr);                                                \
+            return SRT_E_COMM;                                                             \
+        }                                                                                  \
+    } while (0)
+
+typedef struct {
+    const srt_comm* comm;
+    int ld;
+} shard_ctx;
+
+static int shard_gather(void* vctx, dense_ws* ws, int n, int phase, int32_t total, hipStream_t st) {
+    (void)total;
+    shard_ctx* ctx = (shard_ctx*)vctx;
+    ncclComm_t nc = srt_comm_nccl(ctx->comm);
+    const int R = srt_comm_size(ctx->comm);
+    if (phase == 0) {
+        /* counts are zero outside each rank's rows: a sum all-reduce assembles them */
+        SRT_NCCLCHK(ncclAllReduce(ws->cnt, ws->cnt, (size_t)n, ncclInt32, ncclSum, nc, st));
+        return SRT_OK;
+    }
+    /* every rank filled its own rows' contiguous arc segment: broadcast each segment */
+    int32_t* hptr = (int32_t*)malloc((size_t)(n + 1) * sizeof(int32_t));
+    if (!hptr) return SRT_E_NOMEM;
+    if (hipMemcpyAsync(hptr, ws->ptr, (size_t)(n + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, st) !=
+            hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+        free(hptr);
+        srt_set_error("hipMemcpy of the essential-arc offsets failed");
+        return SRT_E_DEVICE;
+    }
+    ncclResult_t r = ncclGroupStart();
+    for (int q = 0; q < R && r == ncclSuccess; q++) {
+        int32_t b, e;
+        srt_shard_rows(ctx->ld, B, R, q, &b, &e);
+        b = min(b, n);
+        e = min(e, n);
+        const size_t o = (size_t)hptr[b], c = (size_t)(hptr[e] - hptr[b]);
+        if (c == 0) continue;
+        r = ncclBroadcast(ws->col + o, ws->col + o, c, ncclInt32, q, nc, st);
+        if (r == ncclSuccess) r = ncclBroadcast(ws->aw + o, ws->aw + o, c, ncclUint32, q, nc, st);
+        if (r == ncclSuccess) r = ncclBroadcast(ws->ar + o, ws->ar + o, c, ncclFloat64, q, nc, st);
+    }
+    ncclResult_t r2 = ncclGroupEnd();
+    free(hptr);
+    if (r != ncclSuccess || r2 != ncclSuccess) {
+        srt_set_error("RCCL broadcast of essential arcs failed: %s",
+                      ncclGetErrorString(r != ncclSuccess ? r : r2));
+        return SRT_E_COMM;
+    }
+    return SRT_OK;
+}
+
+/* undirected symmetry across shards: rank q sends rel[q rows][r cols] to every r > q, which
+ * stores its transpose into rel[r rows][q cols] (the entries with s > t). */
+static int shard_mirror(const srt_comm* comm, int n, int ld, int b, int e, double* rel_rows,
+                        hipStream_t st) {
+    ncclComm_t nc = srt_comm_nccl(comm);
+    const int R = srt_comm_size(comm), me = srt_comm_rank(comm);
+    const int nr = e - b;
+    dense_ws* ws;
+    int rc = ws_get(&ws, n);
+    if (rc) return rc;
+    size_t send_need = (size_t)nr * (size_t)(ld - e) + 1, recv_need = (size_t)nr * (size_t)b + 1;
+    size_t cs = ws->x_cap, cr = ws->x_cap;
+    size_t need = send_need > recv_need ? send_need : recv_need;
+    if ((rc = ws_grow((void**)&ws->xsend, &cs, need, sizeof(double)))) return rc;
+    if ((rc = ws_grow((void**)&ws->xrecv, &cr, need, sizeof(double)))) return rc;
+    ws->x_cap = cs;
+    size_t so = 0;
+    for (int q = me + 1; q < R; q++) {
+        int32_t qb, qe;
+        srt_shard_rows(ld, B, R, q, &qb, &qe);
+        const int64_t cnt = (int64_t)nr * (qe - qb);
+        if (cnt > 0)
+            pack_cols_kernel<<<srt_ceil_div(cnt, 256), 256, 0, st>>>(nr, ld, qb, qe, rel_rows,
+                                                                    ws->xsend + so);
+        so += (size_t)cnt;
+    }
+    SRT_HIPCHK(hipGetLastError());
+    SRT_NCCLCHK(ncclGroupStart());
+    so = 0;
+    for (int q = me + 1; q < R; q++) {
+        int32_t qb, qe;
+        srt_shard_rows(ld, B, R, q, &qb, &qe);
+        const size_t cnt = (size_t)nr * (qe - qb);
+        if (cnt) SRT_NCCLCHK(ncclSend(ws->xsend + so, cnt, ncclFloat64, q, nc, st));
+        so += cnt;
+    }
+    size_t ro = 0;
+    for (int q = 0; q < me; q++) {
+        int32_t qb, qe;
+        srt_shard_rows(ld, B, R, q, &qb, &qe);
+        const size_t cnt = (size_t)(qe - qb) * nr;
+        if (cnt) SRT_NCCLCHK(ncclRecv(ws->xrecv + ro, cnt, ncclFloat64, q, nc, st));
+        ro += cnt;
+    }
+    SRT_NCCLCHK(ncclGroupEnd());
+    ro = 0;
+    for (int q = 0; q < me; q++) {
+        int32_t qb, qe;
+        srt_shard_rows(ld, B, R, q, &qb, &qe);
+        const int pw = qe - qb;
+        if (pw > 0 && nr > 0) {
+            dim3 g(srt_ceil_div(pw, 64), srt_ceil_div(nr, 64));
+            unpack_transpose_kernel<<<g, 256, 0, st>>>(nr, ld, qb, pw, ws->xrecv + ro, rel_rows);
+        }
+        ro += (size_t)pw * nr;
+    }
+    if (nr > 0) {
+        dim3 g(srt_ceil_div(nr, 64), srt_ceil_div(nr, 64));
+        mirror_block_kernel<<<g, 256, 0, st>>>(n, ld, b, e, rel_rows);
+    }
+    SRT_HIPCHK(hipGetLastError());
+    return SRT_OK;
+}
+
+extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, int32_t directed,
+                                       const uint32_t* w_rows, const double* r_rows,
+                                       uint32_t* lat_rows, double* rel_rows, void* stream,
+                                       int32_t fw_block, srt_build_stats* stats) {
+    if (!comm || n <= 0 || ld < n || ld % B || !w_rows || !r_rows || !lat_rows || !rel_rows) {
+        srt_set_error("srt_dense_build_sharded: bad arguments");
+        return SRT_E_ARG;
+    }
+    if (fw_block != 0 && fw_block != B) {
+        srt_set_error("srt_dense_build_sharded: fw_block must be 0 or %d", B);
+        return SRT_E_ARG;
+    }
+    const int R = srt_comm_size(comm), me = srt_comm_rank(comm);
+    int32_t b, e;
+    srt_shard_rows(ld, B, R, me, &b, &e);
+    const int nr = e - b;
+    hipStream_t st = (hipStream_t)stream;
+    ncclComm_t nc = srt_comm_nccl(comm);
+    dense_ws* ws;
+    int rc = ws_get(&ws, n);
+    if (rc) return rc;
+    size_t pc = ws->panel_cap;
+    if ((rc = ws_grow((void**)&ws->panel, &pc, (size_t)B * ld, sizeof(uint32_t)))) return rc;
+    ws->panel_cap = pc;
+    hipEvent_t e0, e1, e2;
+    SRT_HIPCHK(hipEventCreate(&e0));
+    SRT_HIPCHK(hipEventCreate(&e1));
+    SRT_HIPCHK(hipEventCreate(&e2));
+    SRT_HIPCHK(hipEventRecord(e0, st));
+    if (nr > 0) {
+        dim3 g(srt_ceil_div(ld, 256), nr);
+        init_dist_kernel<<<g, 256, 0, st>>>(n, ld, b, w_rows, lat_rows);
+        SRT_HIPCHK(hipGetLastError());
+    }
+    for (int k0 = 0; k0 < ld; k0 += B) {
+        int owner = 0;
+        for (int q = 0; q < R; q++) {
+            int32_t qb, qe;
+            srt_shard_rows(ld, B, R, q, &qb, &qe);
+            if (k0 >= qb && k0 < qe) owner = q;
+        }
+        uint32_t* P;
+        if (owner == me) {
+            P = lat_rows + (size_t)(k0 - b) * ld;
+            if ((rc = fw_owner_part(lat_rows, ld, b, nr, P, k0, st))) return rc;
+        } else {
+            P = ws->panel;
+        }
+        if (R > 1) SRT_NCCLCHK(ncclBroadcast(P, P, (size_t)B * ld, ncclUint32, owner, nc, st));
+        if ((rc = fw_shard_part(lat_rows, ld, b, nr, P, k0, st))) return rc;
+    }
+    SRT_HIPCHK(hipEventRecord(e1, st));
+    shard_ctx ctx = {comm, ld};
+    rc = dense_post(n, ld, b, nr, directed, w_rows, r_rows, lat_rows, rel_rows, st, stats,
+                    R > 1 ? shard_gather : NULL, &ctx);
+    if (rc) return rc;
+    if (!directed) {
+        if (R > 1) {
+            if ((rc = shard_mirror(comm, n, ld, b, e, rel_rows, st))) return rc;
+        } else {
+            dim3 g(srt_ceil_div(n, 64), srt_ceil_div(n, 64));
+            mirror_block_kernel<<<g, 256, 0, st>>>(n, ld, 0, n, rel_rows);
+        }
+    }
+    if ((rc = dense_finish_rows(n, ld, b, nr, w_rows, r_rows, lat_rows, rel_rows, st, stats))) return rc;
+    SRT_HIPCHK(hipEventRecord(e2, st));
+    if (stats) {
+        SRT_HIPCHK(hipEventSynchronize(e2));
+        float a = 0, c = 0;
+        SRT_HIPCHK(hipEventElapsedTime(&a, e0, e1));
+        SRT_HIPCHK(hipEventElapsedTime(&c, e1, e2));
+        stats->algo = SRT_ALGO_DENSE_FW;
+        stats->fw_block = B;
+        stats->ms_fw = a;
+        stats->ms_post = c;
+        stats->ms_total = a + c;
+    }
+    SRT_HIPCHK(hipEventDestroy(e0));
+    SRT_HIPCHK(hipEventDestroy(e1));
+    SRT_HIPCHK(hipEventDestroy(e2));
+    return SRT_OK;
+}

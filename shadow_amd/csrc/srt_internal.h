@@ -1,0 +1,48 @@
+/*
+ * srt_internal.h -- private helpers shared by the host C layer and the HIP translation units.
+ */
+#ifndef SRT_INTERNAL_H
+#define SRT_INTERNAL_H
+
+#include <stdint.h>
+
+#include "shadow_routing.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { SRT_LOG_ERROR = 0, SRT_LOG_WARNING = 1, SRT_LOG_INFO = 2, SRT_LOG_DEBUG = 3 };
+void srt_log(int level, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+void srt_set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+
+/* Canonical dense / CSR forms of an edge list (host side, see graph.c). */
+typedef struct srt_canon {
+    int32_t n;
+    int32_t directed;
+    uint64_t quantum_ns;
+    uint32_t max_w_q;
+    /* CSR of canonical out-arcs (self-loops excluded), columns ascending */
+    int64_t arcs;
+    int32_t* rowptr;
+    int32_t* col;
+    uint32_t* w;
+    double* r;
+    /* CSR of canonical in-arcs (directed graphs only; aliases the out-CSR when undirected) */
+    int32_t* in_rowptr;
+    int32_t* in_col;
+    uint32_t* in_w;
+    double* in_r;
+    /* canonical self-loop per vertex (SRT_INF if none) */
+    uint32_t* self_w;
+    double* self_r;
+} srt_canon;
+
+int srt_canon_build(const srt_edges* g, srt_canon* c);
+void srt_canon_free(srt_canon* c);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,907 @@
+/*
+ * topology.c -- Shadow's routing module (drop-in for /root/reference/src/main/routing/topology.c)
+ * with the all-pairs tables built eagerly on MI355X.
+ *
+ * Load + validation restate topology.c:326-1122; attach restates :2024-2281; the lookup API keeps
+ * the semantics of :1900-2022 but reads one row-major table instead of running lazy Dijkstra
+ * under a global lock. Tables are immutable once built, so lookups are lock-free; only the
+ * IP -> vertex map (attach/detach) and the packet counters take locks.
+ */
+#define _GNU_SOURCE
+#include <arpa/inet.h>
+#include <math.h>
+#include <netinet/in.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <strings.h>
+
+#include "gml.h"
+#include "srt_internal.h"
+#include "topology.h"
+
+/* ---- Shadow entry points used by the reference-signature wrappers -----------------------
+ * Provided by Shadow when linked into it; weak fallbacks in shadow_compat.c otherwise. */
+extern uint32_t address_toNetworkIP(Address* address);
+extern double random_nextDouble(Random* random);
+extern void worker_updateMinTimeJump(double minPathLatency);
+
+#define TOPOLOGY_MAGIC 0x70b0109au
+
+/* ---- u32 -> i32 map (IP in network order -> vertex) --------------------------------------- */
+typedef struct {
+    uint32_t* keys;
+    int32_t* vals; /* -1 empty, -2 tombstone */
+    size_t cap, used;
+} ipmap_t;
+
+static size_t h32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+static int ipmap_put(ipmap_t* m, uint32_t k, int32_t v) {
+    if ((m->used + 1) * 2 > m->cap) {
+        size_t nc = m->cap ? m->cap * 2 : 64;
+        uint32_t* nk = (uint32_t*)malloc(nc * sizeof(uint32_t));
+        int32_t* nv = (int32_t*)malloc(nc * sizeof(int32_t));
+        if (!nk || !nv) {
+            free(nk);
+            free(nv);
+            return -1;
+        }
+        for (size_t i = 0; i < nc; i++) nv[i] = -1;
+        size_t used = 0;
+        for (size_t i = 0; i < m->cap; i++)
+            if (m->vals[i] >= 0) {
+                size_t h = h32(m->keys[i]) & (nc - 1);
+                while (nv[h] >= 0) h = (h + 1) & (nc - 1);
+                nk[h] = m->keys[i];
+                nv[h] = m->vals[i];
+                used++;
+            }
+        free(m->keys);
+        free(m->vals);
+        m->keys = nk;
+        m->vals = nv;
+        m->cap = nc;
+        m->used = used;
+    }
+    size_t h = h32(k) & (m->cap - 1);
+    size_t tomb = (size_t)-1;
+    while (m->vals[h] != -1) {
+        if (m->vals[h] >= 0 && m->keys[h] == k) {
+            m->vals[h] = v;
+            return 0;
+        }
+        if (m->vals[h] == -2 && tomb == (size_t)-1) tomb = h;
+        h = (h + 1) & (m->cap - 1);
+    }
+    if (tomb != (size_t)-1) h = tomb;
+    else m->used++;
+    m->keys[h] = k;
+    m->vals[h] = v;
+    return 0;
+}
+
+static int32_t ipmap_get(const ipmap_t* m, uint32_t k) {
+    if (!m->cap) return -1;
+    size_t h = h32(k) & (m->cap - 1);
+    while (m->vals[h] != -1) {
+        if (m->vals[h] >= 0 && m->keys[h] == k) return m->vals[h];
+        h = (h + 1) & (m->cap - 1);
+    }
+    return -1;
+}
+
+static void ipmap_del(ipmap_t* m, uint32_t k) {
+    if (!m->cap) return;
+    size_t h = h32(k) & (m->cap - 1);
+    while (m->vals[h] != -1) {
+        if (m->vals[h] >= 0 && m->keys[h] == k) {
+            m->vals[h] = -2;
+            return;
+        }
+        h = (h + 1) & (m->cap - 1);
+    }
+}
+
+/* ---- packet counters, keyed like the reference's cached Path (one per unordered pair) ---- */
+typedef struct {
+    uint64_t* keys;
+    uint64_t* cnt;
+    size_t cap, used;
+} cntmap_t;
+
+static uint64_t* cnt_slot(cntmap_t* m, uint64_t k) {
+    if ((m->used + 1) * 2 > m->cap) {
+        size_t nc = m->cap ? m->cap * 2 : 1024;
+        uint64_t* nk = (uint64_t*)calloc(nc, sizeof(uint64_t));
+        uint64_t* nv = (uint64_t*)calloc(nc, sizeof(uint64_t));
+        if (!nk || !nv) {
+            free(nk);
+            free(nv);
+            return NULL;
+        }
+        for (size_t i = 0; i < m->cap; i++)
+            if (m->keys[i]) {
+                size_t h = h32((uint32_t)(m->keys[i] ^ (m->keys[i] >> 32))) & (nc - 1);
+                while (nk[h]) h = (h + 1) & (nc - 1);
+                nk[h] = m->keys[i];
+                nv[h] = m->cnt[i];
+            }
+        free(m->keys);
+        free(m->cnt);
+        m->keys = nk;
+        m->cnt = nv;
+        m->cap = nc;
+    }
+    size_t h = h32((uint32_t)(k ^ (k >> 32))) & (m->cap - 1);
+    while (m->keys[h] && m->keys[h] != k) h = (h + 1) & (m->cap - 1);
+    if (!m->keys[h]) {
+        m->keys[h] = k;
+        m->used++;
+    }
+    return &m->cnt[h];
+}
+
+/* ---- the topology object -------------------------------------------------------------- */
+struct _Topology {
+    uint32_t magic;
+    int use_shortest_path;
+    int directed;
+    int complete;
+    int32_t n;
+    int64_t m;
+    /* validated attributes */
+    double* vid;
+    const char** vip;      /* "" if absent */
+    const char** vcity;    /* NULL if absent */
+    const char** vcountry; /* NULL if absent */
+    uint64_t* bw_down_kib;
+    uint64_t* bw_up_kib;
+    int has_ip_attr;
+    int32_t* esrc;
+    int32_t* edst;
+    int64_t* elat_ns;
+    double* eloss;
+    gml_graph gml; /* owns the attribute strings */
+    /* attach state (topology.c:37-42) */
+    pthread_rwlock_t ip_lock;
+    ipmap_t ipmap;
+    uint8_t* attached; /* verticesWithAttachedHosts */
+    /* tables (immutable once `built` is set) */
+    pthread_mutex_t build_lock;
+    atomic_int built;
+    int build_failed;
+    uint32_t* lat_q;
+    uint64_t quantum_ns;
+    double* rel;
+    srt_build_opts opts;
+    srt_build_stats stats;
+    /* counters */
+    pthread_mutex_t cnt_lock;
+    cntmap_t counters;
+};
+
+static int magic_ok(const Topology* t) { return t && t->magic == TOPOLOGY_MAGIC; }
+
+/* address_stringToIP (address.c:145-152): network order, INADDR_NONE on failure */
+static uint32_t string_to_ip(const char* s) {
+    struct in_addr a;
+    if (s && inet_pton(AF_INET, s, &a) == 1) return a.s_addr;
+    return INADDR_NONE;
+}
+
+/* ---- validation (topology.c:525-1038) -------------------------------------------------- */
+static int prefix_ci(const char* name, const char* expected) {
+    return strncasecmp(name, expected, strlen(expected)) == 0; /* topology.c:184-188 */
+}
+
+static int check_type(const gml_attr* a, int want_string) {
+    if (a->is_string == want_string) return 1;
+    srt_log(SRT_LOG_WARNING, "graph attribute '%s' with type '%s' is supported, but we found "
+            "unsupported type '%s'", a->name, want_string ? "STRING" : "NUMERIC",
+            a->is_string ? "STRING" : "NUMERIC");
+    return 0;
+}
+
+static int check_attributes(const gml_graph* g) {
+    int ok = 1;
+    for (int i = 0; i < g->nva; i++) {
+        const gml_attr* a = &g->va[i];
+        const char* nm = a->name;
+        if (prefix_ci(nm, "id"))
+            ok = ok && check_type(a, 0);
+        else if (prefix_ci(nm, "ip_address") || prefix_ci(nm, "city_code") ||
+                 prefix_ci(nm, "country_code") || prefix_ci(nm, "bandwidth_down") ||
+                 prefix_ci(nm, "bandwidth_up") || prefix_ci(nm, "label"))
+            ok = ok && check_type(a, 1);
+        else {
+            srt_log(SRT_LOG_ERROR, "vertex attribute '%s' is unsupported", nm);
+            ok = 0;
+        }
+    }
+    static const char* vreq[] = {"id", "bandwidth_down", "bandwidth_up"};
+    for (int i = 0; i < 3; i++)
+        if (!gml_vattr(g, vreq[i])) {
+            srt_log(SRT_LOG_WARNING, "the vertex attribute '%s' is required but not provided",
+                    vreq[i]);
+            ok = 0;
+        }
+    for (int i = 0; i < g->nea; i++) {
+        const gml_attr* a = &g->ea[i];
+        const char* nm = a->name;
+        if (prefix_ci(nm, "latency") || prefix_ci(nm, "jitter") || prefix_ci(nm, "label"))
+            ok = ok && check_type(a, 1);
+        else if (prefix_ci(nm, "packet_loss"))
+            ok = ok && check_type(a, 0);
+        else {
+            srt_log(SRT_LOG_ERROR, "edge attribute '%s' is unsupported", nm);
+            ok = 0;
+        }
+    }
+    static const char* ereq[] = {"latency", "packet_loss"};
+    for (int i = 0; i < 2; i++)
+        if (!gml_eattr(g, ereq[i])) {
+            srt_log(SRT_LOG_WARNING, "the edge attribute '%s' is required but not provided",
+                    ereq[i]);
+            ok = 0;
+        }
+    return ok;
+}
+
+/* BFS reachability over out-arcs (forward) or in-arcs (backward). */
+static int32_t reach_count(int32_t n, int64_t m, const int32_t* es, const int32_t* ed, int directed,
+                           int backward) {
+    int32_t* deg = (int32_t*)calloc((size_t)n + 1, sizeof(int32_t));
+    int32_t* adj = (int32_t*)malloc((size_t)(2 * m + 1) * sizeof(int32_t));
+    int32_t* q = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+    uint8_t* seen = (uint8_t*)calloc((size_t)n, 1);
+    if (!deg || !adj || !q || !seen) {
+        free(deg);
+        free(adj);
+        free(q);
+        free(seen);
+        return -1;
+    }
+    for (int64_t e = 0; e < m; e++) {
+        int32_t a = backward ? ed[e] : es[e], b = backward ? es[e] : ed[e];
+        deg[a + 1]++;
+        if (!directed) deg[b + 1]++;
+    }
+    for (int32_t i = 0; i < n; i++) deg[i + 1] += deg[i];
+    int32_t* pos = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+    if (!pos) {
+        free(deg);
+        free(adj);
+        free(q);
+        free(seen);
+        return -1;
+    }
+    memcpy(pos, deg, (size_t)n * sizeof(int32_t));
+    for (int64_t e = 0; e < m; e++) {
+        int32_t a = backward ? ed[e] : es[e], b = backward ? es[e] : ed[e];
+        adj[pos[a]++] = b;
+        if (!directed) adj[pos[b]++] = a;
+    }
+    int32_t head = 0, tail = 0, cnt = 0;
+    q[tail++] = 0;
+    seen[0] = 1;
+    while (head < tail) {
+        int32_t u = q[head++];
+        cnt++;
+        for (int32_t k = deg[u]; k < deg[u + 1]; k++)
+            if (!seen[adj[k]]) {
+                seen[adj[k]] = 1;
+                q[tail++] = adj[k];
+            }
+    }
+    free(deg);
+    free(adj);
+    free(q);
+    free(seen);
+    free(pos);
+    return cnt;
+}
+
+/* _topology_isComplete (topology.c:409-511): every vertex needs >= n incident OUT edges; an
+ * undirected self-loop is listed twice by igraph and corrected once (:464-480). */
+static int is_complete(const gml_graph* g) {
+    int32_t n = g->n;
+    int64_t* cnt = (int64_t*)calloc((size_t)n, sizeof(int64_t));
+    uint8_t* loop = (uint8_t*)calloc((size_t)n, 1);
+    if (!cnt || !loop) {
+        free(cnt);
+        free(loop);
+        return 0;
+    }
+    for (int64_t e = 0; e < g->m; e++) {
+        int32_t a = g->esrc[e], b = g->edst[e];
+        cnt[a]++;
+        if (!g->directed) cnt[b]++;
+        if (a == b) loop[a] = 1;
+    }
+    int complete = 1;
+    for (int32_t v = 0; v < n && complete; v++) {
+        int64_t c = cnt[v] - ((!g->directed && loop[v]) ? 1 : 0);
+        if (c < n) complete = 0;
+    }
+    free(cnt);
+    free(loop);
+    return complete;
+}
+
+static int bandwidth_kib(const gml_attr* a, int32_t v, uint64_t* out) {
+    /* _topology_findVertexAttributeStringBandwidth (topology.c:210-233) */
+    if (!a || !a->is_string) return 0;
+    const char* s = a->str[v];
+    if (!s || !s[0]) return 0;
+    int64_t bw = srt_parse_bandwidth(s);
+    if (bw == -2) {
+        srt_log(SRT_LOG_ERROR, "bandwidth '%s' overflows (the reference panics here)", s);
+        return 0;
+    }
+    if (bw < 0) return 0;
+    *out = (uint64_t)(bw / (8 * 1024));
+    return 1;
+}
+
+static int edge_time_ns(const gml_attr* a, int64_t e, int64_t* out) {
+    /* _topology_findEdgeAttributeStringTimeMs (topology.c:280-302) */
+    if (!a || !a->is_string) return 0;
+    const char* s = a->str[e];
+    if (!s || !s[0]) return 0;
+    int64_t ns = srt_parse_time_nanosec(s);
+    if (ns == -2) {
+        srt_log(SRT_LOG_ERROR, "time '%s' overflows (the reference panics here)", s);
+        return 0;
+    }
+    if (ns < 0) return 0;
+    *out = ns;
+    return 1;
+}
+
+static int validate_and_extract(Topology* t) {
+    const gml_graph* g = &t->gml;
+    srt_log(SRT_LOG_INFO, "checking graph attributes...");
+    if (!check_attributes(g)) {
+        srt_log(SRT_LOG_ERROR, "topology validation failed because of problem with graph, vertex, "
+                "or edge attributes");
+        return 0;
+    }
+    t->n = g->n;
+    t->m = g->m;
+    t->directed = g->directed;
+    /* strongly connected, one cluster (topology.c:671-713) */
+    int connected = g->n > 0;
+    if (connected) {
+        int32_t f = reach_count(g->n, g->m, g->esrc, g->edst, g->directed, 0);
+        connected = (f == g->n);
+        if (connected && g->directed) connected = reach_count(g->n, g->m, g->esrc, g->edst, 1, 1) == g->n;
+    }
+    t->complete = g->n > 0 && is_complete(g);
+    if (!t->complete && !t->use_shortest_path) {
+        srt_log(SRT_LOG_ERROR, "The 'use_shortest_path' feature is disabled/false, but the graph is "
+                "not complete");
+        return 0;
+    }
+    if (!connected) {
+        srt_log(SRT_LOG_ERROR, "topology must be strongly connected with a single cluster");
+        return 0;
+    }
+    /* vertices (topology.c:718-890) */
+    const gml_attr* aid = gml_vattr(g, "id");
+    const gml_attr* adown = gml_vattr(g, "bandwidth_down");
+    const gml_attr* aup = gml_vattr(g, "bandwidth_up");
+    const gml_attr* aip = gml_vattr(g, "ip_address");
+    const gml_attr* acity = gml_vattr(g, "city_code");
+    const gml_attr* acountry = gml_vattr(g, "country_code");
+    int32_t n = g->n;
+    t->vid = (double*)malloc((size_t)n * sizeof(double));
+    t->vip = (const char**)malloc((size_t)n * sizeof(char*));
+    t->vcity = (const char**)malloc((size_t)n * sizeof(char*));
+    t->vcountry = (const char**)malloc((size_t)n * sizeof(char*));
+    t->bw_down_kib = (uint64_t*)malloc((size_t)n * sizeof(uint64_t));
+    t->bw_up_kib = (uint64_t*)malloc((size_t)n * sizeof(uint64_t));
+    t->attached = (uint8_t*)calloc((size_t)n, 1);
+    if (!t->vid || !t->vip || !t->vcity || !t->vcountry || !t->bw_down_kib || !t->bw_up_kib ||
+        !t->attached)
+        return 0;
+    t->has_ip_attr = aip && aip->is_string;
+    int ok = 1;
+    for (int32_t v = 0; v < n; v++) {
+        double id = aid->num[v];
+        if (isnan(id)) {
+            srt_log(SRT_LOG_WARNING, "required attribute 'id' on vertex %d is NULL", v);
+            ok = 0;
+        }
+        t->vid[v] = id;
+        if (!(bandwidth_kib(adown, v, &t->bw_down_kib[v]) && t->bw_down_kib[v] > 0)) {
+            srt_log(SRT_LOG_WARNING, "required attribute 'bandwidth_down' on vertex %d is NAN or "
+                    "negative", v);
+            ok = 0;
+        }
+        if (!(bandwidth_kib(aup, v, &t->bw_up_kib[v]) && t->bw_up_kib[v] > 0)) {
+            srt_log(SRT_LOG_WARNING, "required attribute 'bandwidth_up' on vertex %d is NAN or "
+                    "negative", v);
+            ok = 0;
+        }
+        t->vip[v] = (aip && aip->is_string) ? aip->str[v] : "";
+        t->vcity[v] = (acity && acity->is_string && acity->str[v][0]) ? acity->str[v] : NULL;
+        t->vcountry[v] =
+            (acountry && acountry->is_string && acountry->str[v][0]) ? acountry->str[v] : NULL;
+    }
+    if (!ok) {
+        srt_log(SRT_LOG_WARNING, "unable to validate graph vertices");
+        return 0;
+    }
+    /* edges (topology.c:892-1038) + weight extraction (:1065-1122) */
+    const gml_attr* alat = gml_eattr(g, "latency");
+    const gml_attr* aloss = gml_eattr(g, "packet_loss");
+    const gml_attr* ajit = gml_eattr(g, "jitter");
+    int64_t m = g->m;
+    t->esrc = g->esrc;
+    t->edst = g->edst;
+    t->elat_ns = (int64_t*)malloc((size_t)(m > 0 ? m : 1) * sizeof(int64_t));
+    t->eloss = (double*)malloc((size_t)(m > 0 ? m : 1) * sizeof(double));
+    if (!t->elat_ns || !t->eloss) return 0;
+    for (int64_t e = 0; e < m; e++) {
+        int64_t ns = 0;
+        if (!(edge_time_ns(alat, e, &ns) && (double)ns / 1000000.0 > 0.0)) {
+            srt_log(SRT_LOG_WARNING, "required attribute 'latency' on edge %lld is missing, NAN or "
+                    "non-positive", (long long)e);
+            ok = 0;
+        }
+        t->elat_ns[e] = ns;
+        double loss = aloss->num ? aloss->num[e] : NAN;
+        if (isnan(loss) || !(loss >= 0.0f && loss <= 1.0f)) {
+            srt_log(SRT_LOG_WARNING, "required attribute 'packet_loss' on edge %lld is missing, NAN "
+                    "or out of range [0.0,1.0]", (long long)e);
+            ok = 0;
+        }
+        t->eloss[e] = loss;
+        int64_t jns;
+        (void)ajit;
+        (void)jns; /* jitter parses to ns >= 0 whenever present, so it can never fail (:956-970) */
+    }
+    if (!ok) {
+        srt_log(SRT_LOG_WARNING, "unable to validate graph edges");
+        return 0;
+    }
+    srt_log(SRT_LOG_INFO, "successfully parsed gml and validated topology: %d vertices, %lld edges, "
+            "%s, %s", n, (long long)m, t->directed ? "directed" : "undirected",
+            t->complete ? "complete" : "incomplete");
+    return 1;
+}
+
+static Topology* topology_from_text(const char* text, size_t len, int useShortestPath) {
+    Topology* t = (Topology*)calloc(1, sizeof(Topology));
+    if (!t) return NULL;
+    t->magic = TOPOLOGY_MAGIC;
+    t->use_shortest_path = useShortestPath ? 1 : 0;
+    pthread_rwlock_init(&t->ip_lock, NULL);
+    pthread_mutex_init(&t->build_lock, NULL);
+    pthread_mutex_init(&t->cnt_lock, NULL);
+    atomic_store(&t->built, 0);
+    t->opts.device = 0;
+    t->opts.algo = SRT_ALGO_AUTO;
+    char err[512];
+    if (gml_parse(text, len, &t->gml, err, sizeof(err))) {
+        srt_log(SRT_LOG_ERROR, "GML read failed: %s", err);
+        topology_free(t);
+        return NULL;
+    }
+    if (!validate_and_extract(t)) {
+        srt_log(SRT_LOG_ERROR, "we failed to create the simulation topology because we were unable "
+                "to validate the topology gml file");
+        topology_free(t);
+        return NULL;
+    }
+    return t;
+}
+
+Topology* srt_topology_new_from_string(const char* gmlText, int useShortestPath) {
+    if (!gmlText) return NULL;
+    return topology_from_text(gmlText, strlen(gmlText), useShortestPath);
+}
+
+Topology* topology_new(const char* graphPath, int useShortestPath) {
+    if (!graphPath) return NULL;
+    FILE* f = fopen(graphPath, "rb");
+    if (!f) {
+        srt_log(SRT_LOG_ERROR, "fopen returned NULL while attempting to open graph file path '%s'",
+                graphPath);
+        return NULL;
+    }
+    fseek(f, 0, SEEK_END);
+    long len = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    char* buf = (char*)malloc((size_t)(len > 0 ? len : 0) + 1);
+    if (!buf) {
+        fclose(f);
+        return NULL;
+    }
+    size_t got = fread(buf, 1, (size_t)(len > 0 ? len : 0), f);
+    fclose(f);
+    buf[got] = 0;
+    /* the path is not retained: the controller unlinks the temp file (controller.c:173-174) */
+    Topology* t = topology_from_text(buf, got, useShortestPath);
+    free(buf);
+    return t;
+}
+
+void topology_free(Topology* t) {
+    if (!t) return;
+    free(t->vid);
+    free(t->vip);
+    free(t->vcity);
+    free(t->vcountry);
+    free(t->bw_down_kib);
+    free(t->bw_up_kib);
+    free(t->attached);
+    free(t->elat_ns);
+    free(t->eloss);
+    free(t->ipmap.keys);
+    free(t->ipmap.vals);
+    free(t->lat_q);
+    free(t->rel);
+    free(t->counters.keys);
+    free(t->counters.cnt);
+    gml_free(&t->gml);
+    pthread_rwlock_destroy(&t->ip_lock);
+    pthread_mutex_destroy(&t->build_lock);
+    pthread_mutex_destroy(&t->cnt_lock);
+    t->magic = 0;
+    free(t);
+}
+
+/* ---- attach (topology.c:2024-2272) ----------------------------------------------------- */
+typedef struct {
+    int32_t* v;
+    int32_t len, head;
+} queue_t;
+
+static void q_push(queue_t* q, int32_t x) { q->v[q->len++] = x; }
+
+static int32_t find_attachment_vertex(Topology* t, uint32_t* rand_state, Random* rnd,
+                                      const char* ipHint, const char* cityHint,
+                                      const char* countryHint) {
+    int32_t n = t->n;
+    queue_t city = {(int32_t*)malloc((size_t)n * sizeof(int32_t)), 0, 0};
+    queue_t country = {(int32_t*)malloc((size_t)n * sizeof(int32_t)), 0, 0};
+    queue_t all = {(int32_t*)malloc((size_t)n * sizeof(int32_t)), 0, 0};
+    if (!city.v || !country.v || !all.v) {
+        free(city.v);
+        free(country.v);
+        free(all.v);
+        return -1;
+    }
+    uint32_t numIPsCity = 0, numIPsCountry = 0, numIPsAll = 0;
+    int requestedIPIsUsable = 0, foundExact = 0;
+    uint32_t requestedIP = 0;
+    if (ipHint) {
+        uint32_t ip = string_to_ip(ipHint);
+        /* INADDR_LOOPBACK is host order compared to a network-order value (topology.c:2146) */
+        if (ip != INADDR_NONE && ip != INADDR_ANY && ip != INADDR_LOOPBACK) {
+            requestedIPIsUsable = 1;
+            requestedIP = ip;
+        }
+    }
+    for (int32_t v = 0; v < n; v++) { /* _topology_findAttachmentVertexHelperHook :2024-2100 */
+        const char* ipStr = t->vip[v];
+        int ipFound = ipStr && ipStr[0];
+        int cityMatch = t->vcity[v] && cityHint && !strcasecmp(t->vcity[v], cityHint);
+        int countryMatch = t->vcountry[v] && countryHint && !strcasecmp(t->vcountry[v], countryHint);
+        int usable = 0;
+        uint32_t vip = INADDR_NONE;
+        if (ipFound) {
+            uint32_t ip = string_to_ip(ipStr);
+            if (ip != INADDR_NONE && ip != INADDR_ANY && ip != INADDR_LOOPBACK) {
+                usable = 1;
+                vip = ip;
+            }
+        }
+        if (requestedIPIsUsable && usable && vip == requestedIP) {
+            if (!foundExact) {
+                city.len = country.len = all.len = 0;
+            }
+            foundExact = 1;
+            q_push(&all, v);
+            numIPsAll++;
+        }
+        if (foundExact) continue;
+        q_push(&all, v);
+        if (usable) numIPsAll++;
+        if (cityMatch) {
+            q_push(&city, v);
+            if (usable) numIPsCity++;
+        }
+        if (countryMatch) {
+            q_push(&country, v);
+            if (usable) numIPsCountry++;
+        }
+    }
+    queue_t* cand;
+    int useLPM;
+    if (city.len > 0) {
+        cand = &city;
+        useLPM = requestedIPIsUsable && numIPsCity > 0;
+    } else if (country.len > 0) {
+        cand = &country;
+        useLPM = requestedIPIsUsable && numIPsCountry > 0;
+    } else {
+        cand = &all;
+        useLPM = ipHint && numIPsAll > 0; /* the hint's presence, not its usability (:2178) */
+    }
+    int32_t chosen = -1;
+    if (cand->len > 0) {
+        if (useLPM && !foundExact) { /* _topology_getLongestPrefixMatch :2102-2130 */
+            uint32_t bestMatch = 0;
+            for (int32_t i = 0; i < cand->len; i++) {
+                int32_t v = cand->v[i];
+                uint32_t vip = string_to_ip(t->vip[v]);
+                uint32_t match = ~(vip ^ requestedIP);
+                if (match > bestMatch || bestMatch == 0) {
+                    bestMatch = match;
+                    chosen = v;
+                }
+            }
+        } else { /* :2188-2196 */
+            double u;
+            if (rnd)
+                u = random_nextDouble(rnd);
+            else
+                u = (double)rand_r(rand_state) / (double)RAND_MAX; /* random.c:32-43 */
+            int indexRange = cand->len - 1;
+            int chosenIndex = (int)round((double)(indexRange * u));
+            chosen = cand->v[chosenIndex < cand->len ? chosenIndex : cand->len - 1];
+        }
+    }
+    free(city.v);
+    free(country.v);
+    free(all.v);
+    return chosen;
+}
+
+static int32_t attach_common(Topology* t, uint32_t ipNet, uint32_t* rand_state, Random* rnd,
+                             const char* ipHint, const char* cityHint, const char* countryHint,
+                             uint64_t* bwDownOut, uint64_t* bwUpOut) {
+    if (!magic_ok(t)) return SRT_E_ARG;
+    int32_t v = find_attachment_vertex(t, rand_state, rnd, ipHint, cityHint, countryHint);
+    if (v < 0) {
+        srt_log(SRT_LOG_ERROR, "no attachment vertex found");
+        abort(); /* utility_assert(numCandidates > 0), topology.c:2182 */
+    }
+    pthread_rwlock_wrlock(&t->ip_lock);
+    ipmap_put(&t->ipmap, ipNet, v);
+    t->attached[v] = 1;
+    pthread_rwlock_unlock(&t->ip_lock);
+    if (bwUpOut) *bwUpOut = t->bw_up_kib[v];
+    if (bwDownOut) *bwDownOut = t->bw_down_kib[v];
+    srt_log(SRT_LOG_INFO, "attached address to vertex %d ('%ld') using hints (ip=%s, citycode=%s, "
+            "countrycode=%s)", v, (long)t->vid[v], ipHint ? ipHint : "(null)",
+            cityHint ? cityHint : "(null)", countryHint ? countryHint : "(null)");
+    return v;
+}
+
+int32_t srt_topology_attach_ip(Topology* t, uint32_t ipNet, uint32_t* randState, const char* ipHint,
+                               const char* citycodeHint, const char* countrycodeHint,
+                               uint64_t* bwDownOut, uint64_t* bwUpOut) {
+    if (!randState) return SRT_E_ARG;
+    return attach_common(t, ipNet, randState, NULL, ipHint, citycodeHint, countrycodeHint,
+                         bwDownOut, bwUpOut);
+}
+
+void topology_attach(Topology* t, Address* address, Random* randomSourcePool, char* ipHint,
+                     char* citycodeHint, char* countrycodeHint, uint64_t* bwDownOut,
+                     uint64_t* bwUpOut) {
+    attach_common(t, address_toNetworkIP(address), NULL, randomSourcePool, ipHint, citycodeHint,
+                  countrycodeHint, bwDownOut, bwUpOut);
+}
+
+void srt_topology_detach_ip(Topology* t, uint32_t ipNet) {
+    if (!magic_ok(t)) return;
+    pthread_rwlock_wrlock(&t->ip_lock);
+    ipmap_del(&t->ipmap, ipNet); /* verticesWithAttachedHosts is left as is (:2274-2281) */
+    pthread_rwlock_unlock(&t->ip_lock);
+}
+
+void topology_detach(Topology* t, Address* address) {
+    srt_topology_detach_ip(t, address_toNetworkIP(address));
+}
+
+int32_t srt_topology_vertex_of_ip(Topology* t, uint32_t ipNet) {
+    if (!magic_ok(t)) return -1;
+    pthread_rwlock_rdlock(&t->ip_lock);
+    int32_t v = ipmap_get(&t->ipmap, ipNet);
+    pthread_rwlock_unlock(&t->ip_lock);
+    return v;
+}
+
+/* ---- build + lookups ------------------------------------------------------------------ */
+int srt_topology_edges(Topology* t, srt_edges* out) {
+    if (!magic_ok(t) || !out) return SRT_E_ARG;
+    out->n = t->n;
+    out->directed = t->directed;
+    out->m = t->m;
+    out->src = t->esrc;
+    out->dst = t->edst;
+    out->lat_ns = t->elat_ns;
+    out->loss = t->eloss;
+    return SRT_OK;
+}
+
+void srt_topology_set_build_opts(Topology* t, const srt_build_opts* opts) {
+    if (magic_ok(t) && opts) t->opts = *opts;
+}
+
+int srt_topology_last_stats(Topology* t, srt_build_stats* stats) {
+    if (!magic_ok(t) || !stats) return SRT_E_ARG;
+    *stats = t->stats;
+    return SRT_OK;
+}
+
+double srt_topology_min_latency_ms(Topology* t) {
+    if (!magic_ok(t) || !atomic_load(&t->built)) return 0.0;
+    int32_t n = t->n;
+    uint64_t best = UINT64_MAX;
+    for (int32_t s = 0; s < n; s++) {
+        if (!t->attached[s]) continue;
+        const uint32_t* row = t->lat_q + (size_t)s * n;
+        for (int32_t d = 0; d < n; d++)
+            if (t->attached[d] && row[d] < best) best = row[d];
+    }
+    if (best == UINT64_MAX) return 0.0;
+    return (double)(best * t->quantum_ns) / 1000000.0;
+}
+
+int topology_computeShortestPaths(Topology* t, int nGPUs) {
+    if (!magic_ok(t)) return SRT_E_ARG;
+    if (atomic_load_explicit(&t->built, memory_order_acquire)) return SRT_OK;
+    pthread_mutex_lock(&t->build_lock);
+    int rc = SRT_OK;
+    if (!atomic_load(&t->built)) {
+        if (t->build_failed) {
+            pthread_mutex_unlock(&t->build_lock);
+            return SRT_E_DEVICE;
+        }
+        if (nGPUs > 1)
+            srt_log(SRT_LOG_INFO, "in-process multi-GPU build not enabled; using device %d "
+                    "(sharded builds run one process per GPU, see bench.py)", t->opts.device);
+        size_t nn = (size_t)t->n * (size_t)t->n;
+        t->lat_q = (uint32_t*)malloc(nn * sizeof(uint32_t));
+        t->rel = (double*)malloc(nn * sizeof(double));
+        if (!t->lat_q || !t->rel) {
+            rc = SRT_E_NOMEM;
+        } else {
+            srt_edges e;
+            srt_topology_edges(t, &e);
+            srt_build_opts o = t->opts;
+            o.use_shortest_path = t->use_shortest_path;
+            rc = srt_build_tables(&e, &o, t->lat_q, &t->quantum_ns, t->rel, &t->stats);
+        }
+        if (rc == SRT_OK) {
+            atomic_store_explicit(&t->built, 1, memory_order_release);
+        } else {
+            t->build_failed = 1;
+            srt_log(SRT_LOG_ERROR, "routing table build failed (%d): %s", rc, srt_last_error());
+        }
+    }
+    pthread_mutex_unlock(&t->build_lock);
+    if (rc == SRT_OK) {
+        double mn = srt_topology_min_latency_ms(t);
+        if (mn > 0.0) worker_updateMinTimeJump(mn); /* once, global minimum (:1253-1264) */
+    }
+    return rc;
+}
+
+int topology_getTable(Topology* t, const uint32_t** latQ, uint64_t* quantumNs, const double** rel,
+                      int* n) {
+    if (!magic_ok(t)) return SRT_E_ARG;
+    int rc = topology_computeShortestPaths(t, 1);
+    if (rc) return rc;
+    if (latQ) *latQ = t->lat_q;
+    if (quantumNs) *quantumNs = t->quantum_ns;
+    if (rel) *rel = t->rel;
+    if (n) *n = t->n;
+    return SRT_OK;
+}
+
+/* _topology_getPathEntry (topology.c:1900-1981): table index of the pair, or an error code. */
+static int64_t path_index(Topology* t, uint32_t srcIp, uint32_t dstIp) {
+    int32_t s = srt_topology_vertex_of_ip(t, srcIp);
+    if (s < 0) {
+        srt_log(SRT_LOG_ERROR, "source address is not connected to topology");
+        return SRT_E_UNATTACHED;
+    }
+    int32_t d = srt_topology_vertex_of_ip(t, dstIp);
+    if (d < 0) {
+        srt_log(SRT_LOG_ERROR, "destination address is not connected to topology");
+        return SRT_E_UNATTACHED;
+    }
+    if (!atomic_load_explicit(&t->built, memory_order_acquire)) {
+        int rc = topology_computeShortestPaths(t, 1);
+        if (rc) {
+            srt_log(SRT_LOG_ERROR, "unable to find path between vertex %d and vertex %d", s, d);
+            abort(); /* utility_panic (topology.c:1970-1976) */
+        }
+    }
+    return (int64_t)s * t->n + d;
+}
+
+double srt_topology_latency_ip(Topology* t, uint32_t srcIp, uint32_t dstIp) {
+    if (!magic_ok(t)) return -1.0;
+    int64_t i = path_index(t, srcIp, dstIp);
+    if (i < 0) return -1.0;
+    return (double)((uint64_t)t->lat_q[i] * t->quantum_ns) / 1000000.0;
+}
+
+double srt_topology_reliability_ip(Topology* t, uint32_t srcIp, uint32_t dstIp) {
+    if (!magic_ok(t)) return -1.0;
+    int64_t i = path_index(t, srcIp, dstIp);
+    if (i < 0) return -1.0;
+    return t->rel[i];
+}
+
+static uint64_t counter_key(Topology* t, int64_t idx) {
+    int64_t s = idx / t->n, d = idx % t->n;
+    if (!t->directed && d < s) {
+        int64_t x = s;
+        s = d;
+        d = x;
+    }
+    return ((uint64_t)s << 32 | (uint64_t)d) + 1; /* 0 = empty slot */
+}
+
+int srt_topology_increment_ip(Topology* t, uint32_t srcIp, uint32_t dstIp) {
+    if (!magic_ok(t)) return SRT_E_ARG;
+    int64_t i = path_index(t, srcIp, dstIp);
+    if (i < 0) return (int)i;
+    pthread_mutex_lock(&t->cnt_lock);
+    uint64_t* c = cnt_slot(&t->counters, counter_key(t, i));
+    if (c) (*c)++;
+    pthread_mutex_unlock(&t->cnt_lock);
+    return c ? SRT_OK : SRT_E_NOMEM;
+}
+
+uint64_t srt_topology_packet_count_ip(Topology* t, uint32_t srcIp, uint32_t dstIp) {
+    if (!magic_ok(t)) return 0;
+    int64_t i = path_index(t, srcIp, dstIp);
+    if (i < 0) return 0;
+    pthread_mutex_lock(&t->cnt_lock);
+    uint64_t* c = cnt_slot(&t->counters, counter_key(t, i));
+    uint64_t v = c ? *c : 0;
+    pthread_mutex_unlock(&t->cnt_lock);
+    return v;
+}
+
+double topology_getLatency(Topology* t, Address* src, Address* dst) {
+    return srt_topology_latency_ip(t, address_toNetworkIP(src), address_toNetworkIP(dst));
+}
+
+double topology_getReliability(Topology* t, Address* src, Address* dst) {
+    return srt_topology_reliability_ip(t, address_toNetworkIP(src), address_toNetworkIP(dst));
+}
+
+int topology_isRoutable(Topology* t, Address* src, Address* dst) {
+    return topology_getLatency(t, src, dst) > -1 ? 1 : 0; /* topology.c:2019-2022 */
+}
+
+void topology_incrementPathPacketCounter(Topology* t, Address* src, Address* dst) {
+    if (srt_topology_increment_ip(t, address_toNetworkIP(src), address_toNetworkIP(dst))) {
+        srt_log(SRT_LOG_ERROR, "unable to find path between nodes");
+        abort(); /* utility_panic (topology.c:1990) */
+    }
+}
+
+int32_t srt_topology_vertex_count(Topology* t) { return magic_ok(t) ? t->n : -1; }
+int64_t srt_topology_edge_count(Topology* t) { return magic_ok(t) ? t->m : -1; }
+int srt_topology_is_directed(Topology* t) { return magic_ok(t) ? t->directed : -1; }
+int srt_topology_is_complete(Topology* t) { return magic_ok(t) ? t->complete : -1; }

@@ -1,0 +1,186 @@
+"""Python mirror of Shadow's routing interface (include/topology.h), over the C-ABI.
+
+Method names follow /root/reference/src/main/routing/topology.h:17-28 so the parity tests read
+like the reference's call sites (controller.c:173, host.c:172, worker.c:542-554):
+
+    top = Topology.new(path, use_shortest_path=True)        # topology_new
+    top.attach(ip, rand_state, ip_hint, city, country)      # topology_attach
+    top.get_latency(src_ip, dst_ip)                         # topology_getLatency (ms, -1)
+    top.get_reliability(src_ip, dst_ip)                     # topology_getReliability
+    top.is_routable(src_ip, dst_ip)                         # topology_isRoutable
+    top.increment_path_packet_counter(src_ip, dst_ip)       # topology_incrementPathPacketCounter
+    top.compute_shortest_paths()                            # eager GPU build (addition)
+    top.table()                                             # zero-copy (lat_ns, rel) view
+
+IPs are dotted strings or network-order u32, as Address.ip is (address.c:23-25).
+"""
+from __future__ import annotations
+
+import ctypes
+import socket
+import struct
+
+import numpy as np
+
+from . import _lib
+from ._lib import BuildOpts, BuildStats, Edges, check, lib
+
+
+def ip_to_net(ip) -> int:
+    """dotted string -> network-order u32 as stored in Address (inet_pton semantics)."""
+    if isinstance(ip, int):
+        return ip
+    return struct.unpack("=I", socket.inet_aton(ip))[0]
+
+
+class Topology:
+    def __init__(self, handle: int):
+        if not handle:
+            raise ValueError("topology_new failed (see the [shadow-routing] log)")
+        self._h = ctypes.c_void_p(handle)
+        self._keep = []
+
+    # -- construction ------------------------------------------------------------------------
+    @classmethod
+    def new(cls, graph_path: str, use_shortest_path: bool = True) -> "Topology":
+        return cls(lib().topology_new(graph_path.encode(), int(bool(use_shortest_path))))
+
+    @classmethod
+    def from_gml(cls, text: str, use_shortest_path: bool = True) -> "Topology":
+        return cls(lib().srt_topology_new_from_string(text.encode(), int(bool(use_shortest_path))))
+
+    @staticmethod
+    def try_from_gml(text: str, use_shortest_path: bool = True):
+        h = lib().srt_topology_new_from_string(text.encode(), int(bool(use_shortest_path)))
+        return Topology(h) if h else None
+
+    def free(self) -> None:
+        if self._h:
+            lib().topology_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    # -- graph facts ---------------------------------------------------------------------------
+    @property
+    def n(self) -> int:
+        return lib().srt_topology_vertex_count(self._h)
+
+    @property
+    def m(self) -> int:
+        return lib().srt_topology_edge_count(self._h)
+
+    @property
+    def directed(self) -> bool:
+        return bool(lib().srt_topology_is_directed(self._h))
+
+    @property
+    def complete(self) -> bool:
+        return bool(lib().srt_topology_is_complete(self._h))
+
+    def edges(self):
+        e = Edges()
+        check(lib().srt_topology_edges(self._h, ctypes.byref(e)), "srt_topology_edges")
+        m = e.m
+        def arr(ptr, ct, dt):
+            if m == 0:
+                return np.zeros(0, dt)
+            return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ct)), (m,)).astype(dt)
+        return (e.n, bool(e.directed), arr(e.src, ctypes.c_int32, np.int32),
+                arr(e.dst, ctypes.c_int32, np.int32), arr(e.lat_ns, ctypes.c_int64, np.int64),
+                arr(e.loss, ctypes.c_double, np.float64))
+
+    # -- attach --------------------------------------------------------------------------------
+    def attach(self, ip, rand_state: int = 1, ip_hint=None, city_hint=None, country_hint=None):
+        """Returns (vertex, bw_down_KiB, bw_up_KiB, new_rand_state)."""
+        st = ctypes.c_uint32(rand_state)
+        down, up = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        enc = lambda s: None if s is None else s.encode()
+        v = lib().srt_topology_attach_ip(self._h, ip_to_net(ip), ctypes.byref(st), enc(ip_hint),
+                                         enc(city_hint), enc(country_hint), ctypes.byref(down),
+                                         ctypes.byref(up))
+        if v < 0:
+            check(v, "attach")
+        return v, down.value, up.value, st.value
+
+    def detach(self, ip) -> None:
+        lib().srt_topology_detach_ip(self._h, ip_to_net(ip))
+
+    def vertex_of(self, ip) -> int:
+        return lib().srt_topology_vertex_of_ip(self._h, ip_to_net(ip))
+
+    # -- build + lookups -----------------------------------------------------------------------
+    def set_build_opts(self, device=0, algo=_lib.ALGO_AUTO, fw_block=0) -> None:
+        o = BuildOpts(device, algo, 1, fw_block)
+        lib().srt_topology_set_build_opts(self._h, ctypes.byref(o))
+
+    def compute_shortest_paths(self, n_gpus: int = 1) -> None:
+        check(lib().topology_computeShortestPaths(self._h, n_gpus), "topology_computeShortestPaths")
+
+    def stats(self) -> BuildStats:
+        s = BuildStats()
+        check(lib().srt_topology_last_stats(self._h, ctypes.byref(s)), "stats")
+        return s
+
+    def table(self):
+        """(lat_ns u64 [n,n], rel f64 [n,n]) copies of the finished tables."""
+        latp = ctypes.c_void_p()
+        relp = ctypes.c_void_p()
+        q = ctypes.c_uint64()
+        n = ctypes.c_int()
+        check(lib().topology_getTable(self._h, ctypes.byref(latp), ctypes.byref(q),
+                                      ctypes.byref(relp), ctypes.byref(n)), "topology_getTable")
+        nn = n.value
+        lat = np.ctypeslib.as_array(ctypes.cast(latp, ctypes.POINTER(ctypes.c_uint32)), (nn, nn))
+        rel = np.ctypeslib.as_array(ctypes.cast(relp, ctypes.POINTER(ctypes.c_double)), (nn, nn))
+        return lat.astype(np.uint64) * np.uint64(q.value), rel.copy()
+
+    def get_latency(self, src, dst) -> float:
+        return lib().srt_topology_latency_ip(self._h, ip_to_net(src), ip_to_net(dst))
+
+    def get_reliability(self, src, dst) -> float:
+        return lib().srt_topology_reliability_ip(self._h, ip_to_net(src), ip_to_net(dst))
+
+    def is_routable(self, src, dst) -> bool:
+        return self.get_latency(src, dst) > -1
+
+    def increment_path_packet_counter(self, src, dst) -> None:
+        check(lib().srt_topology_increment_ip(self._h, ip_to_net(src), ip_to_net(dst)),
+              "topology_incrementPathPacketCounter")
+
+    def packet_count(self, src, dst) -> int:
+        return lib().srt_topology_packet_count_ip(self._h, ip_to_net(src), ip_to_net(dst))
+
+    def min_latency_ms(self) -> float:
+        return lib().srt_topology_min_latency_ms(self._h)
+
+
+def parse_time_nanosec(s: str) -> int:
+    return lib().srt_parse_time_nanosec(s.encode())
+
+
+def parse_bandwidth(s: str) -> int:
+    return lib().srt_parse_bandwidth(s.encode())
+
+
+def build_tables(n, directed, src, dst, lat_ns, loss, use_shortest_path=True, device=0,
+                 algo=_lib.ALGO_AUTO):
+    """srt_build_tables on host arrays -> (lat_ns u64 [n,n], rel f64 [n,n], stats)."""
+    src = np.ascontiguousarray(src, np.int32)
+    dst = np.ascontiguousarray(dst, np.int32)
+    lat_ns = np.ascontiguousarray(lat_ns, np.int64)
+    loss = np.ascontiguousarray(loss, np.float64)
+    e = Edges(n, int(bool(directed)), len(src), src.ctypes.data, dst.ctypes.data,
+              lat_ns.ctypes.data, loss.ctypes.data)
+    o = BuildOpts(device, algo, int(bool(use_shortest_path)), 0)
+    lat = np.empty((n, n), np.uint32)
+    rel = np.empty((n, n), np.float64)
+    q = ctypes.c_uint64()
+    st = BuildStats()
+    check(lib().srt_build_tables(ctypes.byref(e), ctypes.byref(o), lat.ctypes.data, ctypes.byref(q),
+                                 rel.ctypes.data, ctypes.byref(st)), "srt_build_tables")
+    return lat.astype(np.uint64) * np.uint64(q.value), rel, st

@@ -1,0 +1,186 @@
+"""HIP path vs the CPU oracle, through the C-ABI (run on an MI355X with -m gpu).
+
+Latency tables must be bit-exact in integer ns; reliability must be within 1e-12 relative
+(north_star). Because the GPU forms the product in the same path order as the oracle
+(topology.c:1364-1365) the match is in fact exact; the tolerance is the contract.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import GOLDEN
+from shadow_amd import graphs
+from shadow_amd._lib import ALGO_DENSE_FW, ALGO_SPARSE_SSSP
+from shadow_amd.topology import Topology, build_tables
+
+pytestmark = pytest.mark.gpu
+REL_TOL = 1e-12
+MS = 1_000_000
+
+
+def assert_tables(lat_ns, rel, exp_lat, exp_rel, what=""):
+    exp_lat = np.asarray(exp_lat, dtype=np.uint64)
+    bad = np.argwhere(lat_ns != exp_lat)
+    assert bad.size == 0, f"{what}: {len(bad)} latency mismatches, first {bad[:5].tolist()}"
+    err = np.abs(rel - exp_rel) / np.maximum(np.abs(exp_rel), 1e-300)
+    assert float(err.max()) <= REL_TOL, f"{what}: max rel error {err.max()}"
+
+
+def _oracle(g, use_sp=True, nthreads=8):
+    el = oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
+    return oracle.table(el, use_sp, oracle.ORC_INT_NS, nthreads)
+
+
+def test_known_answers(gpu):
+    for c in json.load(open(os.path.join(GOLDEN, "known_answers.json"))):
+        top = Topology.from_gml(c["gml"])
+        lat, rel = top.table()
+        for s, d, lat_ns, r in c["pairs"]:
+            assert int(lat[s, d]) == lat_ns and rel[s, d] == r, c["name"]
+
+
+@pytest.mark.parametrize("algo", [ALGO_DENSE_FW, ALGO_SPARSE_SSSP])
+def test_tie_graphs(gpu, algo):
+    for c in json.load(open(os.path.join(GOLDEN, "ties.json"))):
+        e = np.array(c["edges"], dtype=np.float64)
+        lat, rel, _ = build_tables(c["n"], c["directed"], e[:, 0], e[:, 1],
+                                   (e[:, 2] * MS).astype(np.int64), e[:, 3], algo=algo)
+        for s, d, lat_ns, r in c["pairs"]:
+            assert int(lat[s, d]) == lat_ns, (c["name"], s, d)
+            assert rel[s, d] == r, (c["name"], s, d)
+
+
+def test_c1_golden_through_gml(gpu):
+    """C1: GML text -> topology_new path -> GPU tables == committed oracle/networkx tables."""
+    text = open(os.path.join(GOLDEN, "c1.gml")).read()
+    top = Topology.from_gml(text)
+    assert top.n == 50 and top.complete and not top.directed
+    lat, rel = top.table()
+    exp = np.load(os.path.join(GOLDEN, "c1_expected.npz"))
+    assert_tables(lat, rel, exp["lat_ns"], exp["rel"], "C1")
+    assert np.array_equal(rel, exp["rel"])  # same path, same multiplication order
+
+
+@pytest.mark.parametrize("algo", [ALGO_DENSE_FW, ALGO_SPARSE_SSSP])
+def test_c2_complete_1000(gpu, algo):
+    g = graphs.complete_graph(1000, seed=2)
+    lat, rel, st = build_tables(g.n, False, g.src, g.dst, g.lat_ns, g.loss, algo=algo)
+    exp = _oracle(g)
+    assert_tables(lat, rel, exp["lat_int"], exp["rel"], f"C2 algo={algo}")
+
+
+@pytest.mark.parametrize("n", [257, 3000])
+def test_sparse_rgg(gpu, n):
+    g = graphs.random_geometric(n, seed=3)
+    lat, rel, st = build_tables(g.n, False, g.src, g.dst, g.lat_ns, g.loss, algo=ALGO_SPARSE_SSSP)
+    exp = _oracle(g)
+    assert_tables(lat, rel, exp["lat_int"], exp["rel"], f"RGG{n} sparse")
+    lat2, rel2, _ = build_tables(g.n, False, g.src, g.dst, g.lat_ns, g.loss, algo=ALGO_DENSE_FW)
+    assert_tables(lat2, rel2, exp["lat_int"], exp["rel"], f"RGG{n} dense")
+
+
+def test_barabasi_albert_small(gpu):
+    g = graphs.barabasi_albert(2000, seed=5)
+    exp = _oracle(g)
+    for algo in (ALGO_SPARSE_SSSP, ALGO_DENSE_FW):
+        lat, rel, _ = build_tables(g.n, False, g.src, g.dst, g.lat_ns, g.loss, algo=algo)
+        assert_tables(lat, rel, exp["lat_int"], exp["rel"], f"BA2000 algo={algo}")
+
+
+@pytest.mark.parametrize("algo", [ALGO_DENSE_FW, ALGO_SPARSE_SSSP])
+def test_directed_random(gpu, algo):
+    rng = np.random.default_rng(11)
+    n, m = 300, 2400
+    src = rng.integers(0, n, m)
+    dst = rng.integers(0, n, m)
+    ring = np.arange(n)  # strongly connected backbone
+    src = np.concatenate([src, ring, ring]).astype(np.int32)
+    dst = np.concatenate([dst, (ring + 1) % n, ring]).astype(np.int32)
+    lat = (rng.integers(1, 20, len(src)) * MS).astype(np.int64)
+    loss = rng.integers(0, 300, len(src)) / 10000.0
+    g = graphs.Graph(n, True, src, dst, lat, loss)
+    lat_ns, rel, _ = build_tables(n, True, src, dst, lat, loss, algo=algo)
+    exp = _oracle(g)
+    assert_tables(lat_ns, rel, exp["lat_int"], exp["rel"], "directed")
+
+
+def test_direct_mode(gpu):
+    g = graphs.complete_graph(70, seed=4)
+    lat, rel, _ = build_tables(g.n, False, g.src, g.dst, g.lat_ns, g.loss, use_shortest_path=False)
+    exp = _oracle(g, use_sp=False)
+    assert_tables(lat, rel, exp["lat_int"], exp["rel"], "direct")
+
+
+def test_lookup_api_end_to_end(gpu):
+    """attach -> getLatency/getReliability/isRoutable/incrementPathPacketCounter (worker.c:542-554)."""
+    g = graphs.complete_graph(40, seed=7)
+    top = Topology.from_gml(graphs.to_gml(g))
+    exp = _oracle(g)
+    ips = []
+    for v in range(40):
+        ip = f"11.0.0.{v + 1}"
+        vert, down, up, _ = top.attach(f"100.0.{v}.1", 1, ip_hint=ip)
+        assert vert == v and down == up == 1_000_000_000 // 8192
+        ips.append(f"100.0.{v}.1")
+    for s in range(0, 40, 3):
+        for d in range(0, 40, 5):
+            assert top.get_latency(ips[s], ips[d]) == int(exp["lat_int"][s, d]) / 1e6
+            assert abs(top.get_reliability(ips[s], ips[d]) - exp["rel"][s, d]) <= REL_TOL
+            assert top.is_routable(ips[s], ips[d])
+    assert top.get_latency(ips[0], "9.9.9.9") == -1
+    assert not top.is_routable("9.9.9.9", ips[0])
+    top.increment_path_packet_counter(ips[1], ips[2])
+    top.increment_path_packet_counter(ips[2], ips[1])  # undirected: one counter per pair
+    assert top.packet_count(ips[1], ips[2]) == 2
+    # runahead export: min over attached pairs incl. the diagonal
+    assert top.min_latency_ms() == int(exp["lat_int"].min()) / 1e6
+
+
+def test_device_generator_matches_host(gpu):
+    import torch
+    from shadow_amd._lib import lib
+    n, ld = 300, 320
+    w = torch.empty((ld, ld), dtype=torch.int32, device="cuda")
+    r = torch.empty((ld, ld), dtype=torch.float64, device="cuda")
+    rc = lib().srt_gen_complete_device(n, ld, 4, 1000, 10, 500, w.data_ptr(), r.data_ptr(), None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    hw, hr = graphs.complete_dense(n, 4, lat_max=1000, self_max=10, loss_max=500)
+    assert np.array_equal(w[:n, :n].cpu().numpy().view(np.uint32), hw)
+    assert np.array_equal(r[:n, :n].cpu().numpy(), hr)
+
+
+def test_dense_device_api_and_sharded_single_rank(gpu):
+    """srt_dense_build_device and srt_dense_build_sharded (1-rank RCCL comm) on device data."""
+    import torch
+    from shadow_amd._lib import BuildStats, lib
+    n, ld = 700, 704
+    w = torch.empty((ld, ld), dtype=torch.int32, device="cuda")
+    r = torch.empty((ld, ld), dtype=torch.float64, device="cuda")
+    L = lib()
+    assert L.srt_gen_complete_device(n, ld, 8, 300, 10, 500, w.data_ptr(), r.data_ptr(), None) == 0
+    lat = torch.empty_like(w)
+    rel = torch.empty_like(r)
+    st = BuildStats()
+    assert L.srt_dense_build_device(n, ld, 0, w.data_ptr(), r.data_ptr(), lat.data_ptr(),
+                                    rel.data_ptr(), None, 0, ctypes.byref(st)) == 0
+    torch.cuda.synchronize()
+    g = graphs.complete_graph(n, seed=8)
+    exp = _oracle(g)
+    lat_ns = lat[:n, :n].cpu().numpy().view(np.uint32).astype(np.uint64) * np.uint64(MS)
+    assert_tables(lat_ns, rel[:n, :n].cpu().numpy(), exp["lat_int"], exp["rel"], "device api")
+    uid = (ctypes.c_uint8 * 128)()
+    assert L.srt_comm_unique_id(uid) == 0
+    comm = ctypes.c_void_p()
+    assert L.srt_comm_init(uid, 1, 0, torch.cuda.current_device(), ctypes.byref(comm)) == 0
+    lat2 = torch.empty_like(w)
+    rel2 = torch.empty_like(r)
+    assert L.srt_dense_build_sharded(comm, n, ld, 0, w.data_ptr(), r.data_ptr(), lat2.data_ptr(),
+                                     rel2.data_ptr(), None, 0, None) == 0
+    torch.cuda.synchronize()
+    L.srt_comm_free(comm)
+    assert torch.equal(lat2[:n, :n], lat[:n, :n]) and torch.equal(rel2[:n, :n], rel[:n, :n])
