@@ -63,6 +63,7 @@ typedef struct srt_build_opts {
 } srt_build_opts;
 
 typedef struct srt_build_stats {
+    int32_t time_kernels; /* input: 1 = bracket every FW update launch with HIP events */
     int32_t algo;        /* algorithm actually used */
     int32_t fw_block;    /* pivot-block edge used by FW */
     int64_t ess_arcs;    /* essential arcs found by the predecessor pass (dense) */
@@ -70,6 +71,9 @@ typedef struct srt_build_stats {
     double ms_fw;        /* shortest-distance kernels */
     double ms_post;      /* predecessor / reliability / diagonal / symmetry kernels */
     int32_t max_depth;   /* deepest shortest-path tree seen by the reliability pass */
+    int32_t n_update;    /* FW update-kernel launches timed (time_kernels = 1) */
+    double ms_update;    /* summed HIP-event duration of those launches */
+    double ms_comm;      /* host-observed time of the collective calls (sharded builds) */
 } srt_build_stats;
 
 /* Build the full tables for an edge list on one GPU; outputs are host buffers of n*n entries.
@@ -93,9 +97,9 @@ int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, const uint32
 
 /* Synthetic graph generators on the device (seeded counter-based hash; identical to
  * shadow_amd/graphs.py so tests can rebuild the same graph on the host). */
-int srt_gen_complete_device(int32_t n, int32_t ld, uint64_t seed, uint32_t lat_max_ms,
-                            uint32_t self_max_ms, uint32_t loss_max_e4, uint32_t* w, double* r,
-                            void* stream);
+int srt_gen_complete_device(int32_t n, int32_t ld, int32_t row0, int32_t nrows, uint64_t seed,
+                            uint32_t lat_max_ms, uint32_t self_max_ms, uint32_t loss_max_e4,
+                            uint32_t* w, double* r, void* stream);
 
 /* ---- device-resident sparse build (CSR of canonical arcs, self-loops excluded) ----------
  * Computes rows [src_begin, src_end) (row r of lat_rows/rel_rows = source src_begin + r, row

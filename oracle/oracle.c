@@ -10,6 +10,7 @@
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 /* ---------------------------------------------------------------------------------------------
  * Canonical arcs: one per ordered vertex pair (u != v), the (min latency, lowest index) edge.
@@ -395,5 +396,152 @@ int orc_table(const orc_graph* g, int use_shortest_path, int mode, int nthreads,
         size_t d = (size_t)v * n + v;
         orc_self_path(g, v, &lat_int[d], &lat_ref[d], &rel[d], lat_ms ? &lat_ms[d] : NULL);
     }
+    return 0;
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * CPU baseline on the dense synthetic complete graphs (C2 / C4 of SURVEY.md §8d): the weight
+ * matrix is generated from the same counter hash as shadow_amd/graphs.py and the device
+ * generator, then a dense O(n^2) Dijkstra (linear (dist, index) selection -- the canonical order,
+ * strict-< relaxation) runs per sampled source with path-order reliability.
+ * ------------------------------------------------------------------------------------------- */
+static inline uint64_t smix(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static inline uint64_t ghash(uint64_t seed, uint64_t stream, uint32_t i, uint32_t j) {
+    return smix(smix(seed * 4ull + stream) ^ (((uint64_t)i << 32) | j));
+}
+
+typedef struct {
+    int32_t n, r0, r1;
+    uint64_t seed;
+    uint32_t lat_max, self_max;
+    uint32_t* W;
+} genjob_t;
+
+static void* gen_worker(void* a) {
+    genjob_t* j = (genjob_t*)a;
+    for (int32_t i = j->r0; i < j->r1; i++)
+        for (int32_t k = 0; k < j->n; k++) {
+            uint32_t x = i < k ? i : k, y = i < k ? k : i;
+            j->W[(size_t)i * j->n + k] =
+                (x == y) ? 1u + (uint32_t)(ghash(j->seed, 2, x, x) % j->self_max)
+                         : 1u + (uint32_t)(ghash(j->seed, 0, x, y) % j->lat_max);
+        }
+    return NULL;
+}
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+typedef struct {
+    int32_t n;
+    uint64_t seed;
+    uint32_t loss_max;
+    const uint32_t* W;
+    const int32_t* sources;
+    int32_t k0, k1;
+    uint64_t* lat_out;
+    double* rel_out;
+} djob_t;
+
+static void* dense_worker(void* a) {
+    djob_t* j = (djob_t*)a;
+    const int32_t n = j->n;
+    uint32_t* dist = (uint32_t*)malloc((size_t)n * sizeof(uint32_t));
+    int32_t* pred = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+    uint8_t* done = (uint8_t*)malloc((size_t)n);
+    double* rel = (double*)malloc((size_t)n * sizeof(double));
+    for (int32_t q = j->k0; q < j->k1; q++) {
+        const int32_t s = j->sources[q];
+        for (int32_t v = 0; v < n; v++) {
+            dist[v] = 0xFFFFFFFFu;
+            pred[v] = -1;
+            done[v] = 0;
+        }
+        dist[s] = 0;
+        rel[s] = 1.0;
+        for (int32_t it = 0; it < n; it++) {
+            uint32_t best = 0xFFFFFFFFu;
+            int32_t u = -1;
+            for (int32_t v = 0; v < n; v++)
+                if (!done[v] && dist[v] < best) {
+                    best = dist[v];
+                    u = v;
+                }
+            if (u < 0) break;
+            done[u] = 1;
+            if (u != s) {
+                const int32_t p = pred[u];
+                const uint32_t x = p < u ? p : u, y = p < u ? u : p;
+                const double loss = (double)(ghash(j->seed, 1, x, y) % (j->loss_max + 1u)) / 10000.0;
+                rel[u] = rel[p] * (1.0 - loss);
+            }
+            const uint32_t* row = j->W + (size_t)u * n;
+            const uint32_t du = dist[u];
+            for (int32_t v = 0; v < n; v++) {
+                if (v == u || done[v]) continue;
+                const uint32_t nd = du + row[v];
+                if (nd < dist[v]) {
+                    dist[v] = nd;
+                    pred[v] = u;
+                }
+            }
+        }
+        for (int32_t v = 0; v < n; v++) {
+            j->lat_out[(size_t)q * n + v] = (uint64_t)dist[v] * 1000000ull;
+            j->rel_out[(size_t)q * n + v] = rel[v];
+        }
+    }
+    free(dist);
+    free(pred);
+    free(done);
+    free(rel);
+    return NULL;
+}
+
+int orc_complete_sample(int32_t n, uint64_t seed, uint32_t lat_max, uint32_t self_max,
+                        uint32_t loss_max, const int32_t* sources, int32_t k, int nthreads,
+                        uint64_t* lat_out, double* rel_out, double* gen_seconds,
+                        double* sssp_seconds) {
+    if (n <= 0 || k <= 0 || !sources || !lat_out || !rel_out) return -1;
+    uint32_t* W = (uint32_t*)malloc((size_t)n * (size_t)n * sizeof(uint32_t));
+    if (!W) return -1;
+    int gt = 16;
+    double t0 = now_s();
+    pthread_t th[64];
+    genjob_t gj[64];
+    for (int i = 0; i < gt; i++) {
+        gj[i] = (genjob_t){n, (int32_t)((int64_t)n * i / gt), (int32_t)((int64_t)n * (i + 1) / gt),
+                           seed, lat_max, self_max, W};
+        pthread_create(&th[i], NULL, gen_worker, &gj[i]);
+    }
+    for (int i = 0; i < gt; i++) pthread_join(th[i], NULL);
+    double t1 = now_s();
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 64) nthreads = 64;
+    djob_t dj[64];
+    for (int i = 0; i < nthreads; i++) {
+        dj[i] = (djob_t){n, seed, loss_max, W, sources, (int32_t)((int64_t)k * i / nthreads),
+                         (int32_t)((int64_t)k * (i + 1) / nthreads), lat_out, rel_out};
+        if (nthreads == 1)
+            dense_worker(&dj[i]);
+        else
+            pthread_create(&th[i], NULL, dense_worker, &dj[i]);
+    }
+    if (nthreads > 1)
+        for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+    double t2 = now_s();
+    free(W);
+    if (gen_seconds) *gen_seconds = t1 - t0;
+    if (sssp_seconds) *sssp_seconds = t2 - t1;
     return 0;
 }

@@ -72,6 +72,15 @@ int orc_table(const orc_graph* g, int use_shortest_path, int mode, int nthreads,
 void orc_self_path(const orc_graph* g, int32_t v, uint64_t* lat_int, uint64_t* lat_ref,
                    double* rel, double* lat_ms);
 
+/* CPU baseline on the synthetic complete graph (graphs.complete_graph / srt_gen_complete_device
+ * with the same seed and distributions): dense O(n^2) Dijkstra from k sampled sources.
+ * lat_out/rel_out are k x n raw per-source rows (lat in ns). Times exclude nothing but the
+ * matrix generation, reported separately. */
+int orc_complete_sample(int32_t n, uint64_t seed, uint32_t lat_max, uint32_t self_max,
+                        uint32_t loss_max, const int32_t* sources, int32_t k, int nthreads,
+                        uint64_t* lat_out, double* rel_out, double* gen_seconds,
+                        double* sssp_seconds);
+
 #ifdef __cplusplus
 }
 #endif

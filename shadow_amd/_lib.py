@@ -48,6 +48,7 @@ class BuildOpts(ctypes.Structure):
 
 class BuildStats(ctypes.Structure):
     _fields_ = [
+        ("time_kernels", ctypes.c_int32),
         ("algo", ctypes.c_int32),
         ("fw_block", ctypes.c_int32),
         ("ess_arcs", ctypes.c_int64),
@@ -55,6 +56,9 @@ class BuildStats(ctypes.Structure):
         ("ms_fw", ctypes.c_double),
         ("ms_post", ctypes.c_double),
         ("max_depth", ctypes.c_int32),
+        ("n_update", ctypes.c_int32),
+        ("ms_update", ctypes.c_double),
+        ("ms_comm", ctypes.c_double),
     ]
 
 
@@ -69,7 +73,8 @@ SIGNATURES = {
     "srt_build_tables": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
     "srt_latency_quantum": (ctypes.c_int, [_VP, _VP, _VP]),
     "srt_dense_build_device": (ctypes.c_int, [_I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _I32, _VP]),
-    "srt_gen_complete_device": (ctypes.c_int, [_I32, _I32, _U64, _U32, _U32, _U32, _VP, _VP, _VP]),
+    "srt_gen_complete_device": (ctypes.c_int, [_I32, _I32, _I32, _I32, _U64, _U32, _U32, _U32,
+                                                _VP, _VP, _VP]),
     "srt_sparse_max_n": (ctypes.c_int, []),
     "srt_sparse_build_device": (ctypes.c_int, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
                                                _VP, _VP, _I32, _I32, _U32, _VP, _VP, _VP, _VP]),

@@ -23,13 +23,13 @@
 /* ------------------------------------------------------------------------------------------ */
 /* synthetic complete graph (SURVEY.md §8d C1/C2/C4 generators)                               */
 /* ------------------------------------------------------------------------------------------ */
-__global__ void gen_complete_kernel(int n, int ld, uint64_t seed, uint32_t lat_max, uint32_t self_max,
-                                    uint32_t loss_max, uint32_t* __restrict__ w,
+__global__ void gen_complete_kernel(int n, int ld, int row0, uint64_t seed, uint32_t lat_max,
+                                    uint32_t self_max, uint32_t loss_max, uint32_t* __restrict__ w,
                                     double* __restrict__ r) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    const int i = blockIdx.y;
+    const int i = row0 + blockIdx.y;
     if (j >= ld) return;
-    size_t ix = (size_t)i * ld + j;
+    size_t ix = (size_t)blockIdx.y * ld + j;
     if (i >= n || j >= n) {
         w[ix] = SRT_INF;
         r[ix] = 0.0;
@@ -49,16 +49,18 @@ __global__ void gen_complete_kernel(int n, int ld, uint64_t seed, uint32_t lat_m
     r[ix] = 1.0 - loss;
 }
 
-extern "C" int srt_gen_complete_device(int32_t n, int32_t ld, uint64_t seed, uint32_t lat_max_ms,
-                                       uint32_t self_max_ms, uint32_t loss_max_e4, uint32_t* w,
-                                       double* r, void* stream) {
-    if (n <= 0 || ld < n || ld % B || !w || !r || lat_max_ms == 0 || self_max_ms == 0) {
+extern "C" int srt_gen_complete_device(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
+                                       uint64_t seed, uint32_t lat_max_ms, uint32_t self_max_ms,
+                                       uint32_t loss_max_e4, uint32_t* w, double* r, void* stream) {
+    if (n <= 0 || ld < n || ld % B || !w || !r || lat_max_ms == 0 || self_max_ms == 0 ||
+        row0 < 0 || nrows < 0 || row0 + nrows > ld) {
         srt_set_error("srt_gen_complete_device: bad arguments");
         return SRT_E_ARG;
     }
-    dim3 grid(srt_ceil_div(ld, 256), ld);
-    gen_complete_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(n, ld, seed, lat_max_ms, self_max_ms,
-                                                               loss_max_e4, w, r);
+    if (nrows == 0) return SRT_OK;
+    dim3 grid(srt_ceil_div(ld, 256), nrows);
+    gen_complete_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(n, ld, row0, seed, lat_max_ms,
+                                                               self_max_ms, loss_max_e4, w, r);
     SRT_HIPCHK(hipGetLastError());
     return SRT_OK;
 }
@@ -255,22 +257,62 @@ static int fw_owner_part(uint32_t* D, int ld, int row0, int nrows, uint32_t* P, 
     return SRT_OK;
 }
 
+/* HIP events bracketing every FW update launch (stats->time_kernels): the per-launch duration
+ * of the dominant kernel that bench.py reports against the roofline. */
+typedef struct {
+    hipEvent_t* ev;
+    int cap, used;
+} evpool_t;
+
+static evpool_t g_evp[64];
+
+static int evpool_begin(evpool_t** out, int rounds) {
+    int dev = 0;
+    SRT_HIPCHK(hipGetDevice(&dev));
+    evpool_t* p = &g_evp[dev & 63];
+    if (p->cap < 2 * rounds) {
+        hipEvent_t* ne = (hipEvent_t*)realloc(p->ev, sizeof(hipEvent_t) * 2 * rounds);
+        if (!ne) return SRT_E_NOMEM;
+        p->ev = ne;
+        for (int i = p->cap; i < 2 * rounds; i++) SRT_HIPCHK(hipEventCreate(&p->ev[i]));
+        p->cap = 2 * rounds;
+    }
+    p->used = 0;
+    *out = p;
+    return SRT_OK;
+}
+
+static int evpool_sum(evpool_t* p, hipEvent_t last, srt_build_stats* stats) {
+    SRT_HIPCHK(hipEventSynchronize(last));
+    double tot = 0;
+    for (int i = 0; i + 1 < p->used; i += 2) {
+        float ms = 0;
+        SRT_HIPCHK(hipEventElapsedTime(&ms, p->ev[i], p->ev[i + 1]));
+        tot += ms;
+    }
+    stats->ms_update = tot;
+    stats->n_update = p->used / 2;
+    return SRT_OK;
+}
+
 static int fw_shard_part(uint32_t* D, int ld, int row0, int nrows, const uint32_t* P, int k0,
-                         hipStream_t st) {
+                         hipStream_t st, evpool_t* evp) {
     const int nb = ld / B, nrb = nrows / B;
     if (nrb == 0) return SRT_OK;
     fw_panel_kernel<<<nb + nrb, 256, 0, st>>>(D, ld, row0, nrb, (uint32_t*)P, k0, nb, 0, 1);
+    if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
     fw_update_kernel<<<dim3(nb, nrb), 256, 0, st>>>(D, ld, row0, P, k0);
+    if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
     SRT_HIPCHK(hipGetLastError());
     return SRT_OK;
 }
 
-int srt_dense_fw_device(int32_t n, int32_t ld, uint32_t* d, hipStream_t st) {
+int srt_dense_fw_device(int32_t n, int32_t ld, uint32_t* d, hipStream_t st, evpool_t* evp) {
     (void)n;
     for (int k0 = 0; k0 < ld; k0 += B) {
         uint32_t* P = d + (size_t)k0 * ld;
         int rc = fw_owner_part(d, ld, 0, ld, P, k0, st);
-        if (!rc) rc = fw_shard_part(d, ld, 0, ld, P, k0, st);
+        if (!rc) rc = fw_shard_part(d, ld, 0, ld, P, k0, st, evp);
         if (rc) return rc;
     }
     return SRT_OK;
@@ -758,7 +800,10 @@ extern "C" int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, c
     dim3 g(srt_ceil_div(ld, 256), ld);
     init_dist_kernel<<<g, 256, 0, st>>>(n, ld, 0, w, lat);
     SRT_HIPCHK(hipGetLastError());
-    int rc = srt_dense_fw_device(n, ld, lat, st);
+    evpool_t* evp = NULL;
+    int rc;
+    if (stats && stats->time_kernels && (rc = evpool_begin(&evp, ld / B))) return rc;
+    rc = srt_dense_fw_device(n, ld, lat, st, evp);
     if (rc) return rc;
     SRT_HIPCHK(hipEventRecord(e1, st));
     rc = srt_dense_post_device(n, ld, directed, w, r, lat, rel, st, stats);
@@ -774,6 +819,7 @@ extern "C" int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, c
         stats->ms_fw = a;
         stats->ms_post = b;
         stats->ms_total = a + b;
+        if (evp && (rc = evpool_sum(evp, e2, stats))) return rc;
     }
     SRT_HIPCHK(hipEventDestroy(e0));
     SRT_HIPCHK(hipEventDestroy(e1));
@@ -945,6 +991,8 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
         init_dist_kernel<<<g, 256, 0, st>>>(n, ld, b, w_rows, lat_rows);
         SRT_HIPCHK(hipGetLastError());
     }
+    evpool_t* evp = NULL;
+    if (stats && stats->time_kernels && (rc = evpool_begin(&evp, ld / B))) return rc;
     for (int k0 = 0; k0 < ld; k0 += B) {
         int owner = 0;
         for (int q = 0; q < R; q++) {
@@ -960,7 +1008,7 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
             P = ws->panel;
         }
         if (R > 1) SRT_NCCLCHK(ncclBroadcast(P, P, (size_t)B * ld, ncclUint32, owner, nc, st));
-        if ((rc = fw_shard_part(lat_rows, ld, b, nr, P, k0, st))) return rc;
+        if ((rc = fw_shard_part(lat_rows, ld, b, nr, P, k0, st, evp))) return rc;
     }
     SRT_HIPCHK(hipEventRecord(e1, st));
     shard_ctx ctx = {comm, ld};
@@ -987,6 +1035,7 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
         stats->ms_fw = a;
         stats->ms_post = c;
         stats->ms_total = a + c;
+        if (evp && (rc = evpool_sum(evp, e2, stats))) return rc;
     }
     SRT_HIPCHK(hipEventDestroy(e0));
     SRT_HIPCHK(hipEventDestroy(e1));

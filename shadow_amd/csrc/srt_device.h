@@ -41,7 +41,6 @@ __host__ __device__ static inline uint64_t srt_hash(uint64_t seed, uint64_t stre
 static inline int srt_ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 /* internal (C++ linkage) entry points shared between translation units */
-int srt_dense_fw_device(int32_t n, int32_t ld, uint32_t* d, hipStream_t st);
 int srt_dense_post_device(int32_t n, int32_t ld, int32_t directed, const uint32_t* w,
                           const double* r, uint32_t* d, double* rel, hipStream_t st,
                           srt_build_stats* stats);

@@ -146,7 +146,8 @@ def test_device_generator_matches_host(gpu):
     n, ld = 300, 320
     w = torch.empty((ld, ld), dtype=torch.int32, device="cuda")
     r = torch.empty((ld, ld), dtype=torch.float64, device="cuda")
-    rc = lib().srt_gen_complete_device(n, ld, 4, 1000, 10, 500, w.data_ptr(), r.data_ptr(), None)
+    rc = lib().srt_gen_complete_device(n, ld, 0, ld, 4, 1000, 10, 500, w.data_ptr(), r.data_ptr(),
+                                       None)
     assert rc == 0
     torch.cuda.synchronize()
     hw, hr = graphs.complete_dense(n, 4, lat_max=1000, self_max=10, loss_max=500)
@@ -162,7 +163,8 @@ def test_dense_device_api_and_sharded_single_rank(gpu):
     w = torch.empty((ld, ld), dtype=torch.int32, device="cuda")
     r = torch.empty((ld, ld), dtype=torch.float64, device="cuda")
     L = lib()
-    assert L.srt_gen_complete_device(n, ld, 8, 300, 10, 500, w.data_ptr(), r.data_ptr(), None) == 0
+    assert L.srt_gen_complete_device(n, ld, 0, ld, 8, 300, 10, 500, w.data_ptr(), r.data_ptr(),
+                                     None) == 0
     lat = torch.empty_like(w)
     rel = torch.empty_like(r)
     st = BuildStats()

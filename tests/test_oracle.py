@@ -99,3 +99,16 @@ def test_rows_threads_agree():
     b = oracle.sssp_rows(el, 10, 60, nthreads=4, want_pred=True)
     for k in a:
         assert np.array_equal(a[k], b[k])
+
+
+def test_complete_sample_matches_edge_list_oracle():
+    """The dense CPU-baseline Dijkstra (bench.py cpu_baseline) equals the edge-list oracle."""
+    n, seed = 300, 2
+    g = graphs.complete_graph(n, seed=seed, lat_max=300, self_max=10, loss_max=500)
+    el = oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
+    src = np.array([0, 7, 150, 299], np.int32)
+    lat, rel, _, _ = oracle.complete_sample(n, seed, 300, 10, 500, src, nthreads=2)
+    for i, s in enumerate(src):
+        rows = oracle.sssp_rows(el, int(s), int(s) + 1)
+        assert np.array_equal(lat[i], rows["lat_int"][0])
+        assert np.array_equal(rel[i], rows["rel"][0])
