@@ -41,6 +41,7 @@ METRIC = "routing-table build time & node-pairs/sec (GB/s vs HBM peak), 1/2/4/8 
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md, HBM3E spec peak
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CU x 4 SIMD32 x 32 lanes x 2.4 GHz
 FW_B = 64
+SHARD_ALIGN = 128  # row-shard / update-tile alignment (srt_device.h SRT_SHARD_ALIGN)
 
 
 def log(rank, *a):
@@ -72,9 +73,9 @@ def main():
     L = _lib.lib()
     wl = WORKLOADS[args.workload]
     n = wl["n"]
-    ld = (n + FW_B - 1) // FW_B * FW_B
+    ld = (n + SHARD_ALIGN - 1) // SHARD_ALIGN * SHARD_ALIGN
     b, e = ctypes.c_int32(), ctypes.c_int32()
-    L.srt_shard_rows(ld, FW_B, world, rank, ctypes.byref(b), ctypes.byref(e))
+    L.srt_shard_rows(ld, SHARD_ALIGN, world, rank, ctypes.byref(b), ctypes.byref(e))
     b, e = b.value, e.value
     nr = e - b
     stream = torch.cuda.Stream(device=dev)
@@ -143,23 +144,28 @@ def main():
     n_upd = sum(s.n_update for s in stats)
     ms_upd = sum(s.ms_update for s in stats)
     avg_upd_ms = ms_upd / max(n_upd, 1)
-    bytes_per_launch = 2.0 * nr * ld * 4  # round-streaming model: read + write the local rows
+    packed = stats[-1].fw_block < 0  # packed-u16 distances (exact, else the u32 kernels ran)
+    s_d = 2 if packed else 4
+    ops_per_relax = 1.0 if packed else 1.5  # v_pk_add_u16+v_pk_min_u16 per 2 | v_add+v_min3/2
+    bytes_per_launch = 2.0 * nr * ld * s_d  # round-streaming model: read + write the local rows
     relax_per_launch = float(nr) * ld * FW_B
     achieved_gbs = bytes_per_launch / (avg_upd_ms * 1e-3) / 1e9
-    valu_tops = 1.5 * relax_per_launch / (avg_upd_ms * 1e-3) / 1e12
+    valu_tops = ops_per_relax * relax_per_launch / (avg_upd_ms * 1e-3) / 1e12
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.workload}_n{world}.json")
     if os.path.exists(pmc_path):
         traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
     roofline = {
-        "bound": "hbm", "kernel": "fw_update_kernel", "achieved": round(achieved_gbs, 1),
+        "bound": "hbm", "kernel": "fw16_update_kernel" if packed else "fw_update_kernel",
+        "achieved": round(achieved_gbs, 1),
         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
         "traffic": traffic, "bytes_per_launch": bytes_per_launch,
         "avg_launch_ms": round(avg_upd_ms, 4), "launches_timed": n_upd,
-        "model": "2*rows*ld*4 B per round (SURVEY §8d round-streaming, B=64)",
+        "model": f"2*rows*ld*{s_d} B per round (SURVEY §8d round-streaming, B=64, "
+                 f"{'u16' if packed else 'u32'} distances)",
         "valu": {"achieved": round(valu_tops, 2), "peak": round(VALU_PEAK_TOPS, 1),
                  "unit": "Tops/s", "frac": round(valu_tops / VALU_PEAK_TOPS, 4),
-                 "ops_per_relax": 1.5},
+                 "ops_per_relax": ops_per_relax},
     }
 
     cpu = None
@@ -198,7 +204,8 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "node-pairs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "u16" if packed else "u32",
             "data": "synthetic",
             "config": {"workload": wl["desc"], "n": n, "ld": ld, "fw_block": FW_B,
                        "parallelism": f"row-shard x{world}" + (" + RCCL pivot-panel broadcast"

@@ -17,6 +17,11 @@
  */
 #include "srt_device.h"
 
+evpool_t* srt_evpool(int dev) {
+    static evpool_t pools[64];
+    return &pools[dev & 63];
+}
+
 #define B SRT_FW_B
 #define LDT SRT_FW_LDT
 
@@ -257,44 +262,6 @@ static int fw_owner_part(uint32_t* D, int ld, int row0, int nrows, uint32_t* P, 
     return SRT_OK;
 }
 
-/* HIP events bracketing every FW update launch (stats->time_kernels): the per-launch duration
- * of the dominant kernel that bench.py reports against the roofline. */
-typedef struct {
-    hipEvent_t* ev;
-    int cap, used;
-} evpool_t;
-
-static evpool_t g_evp[64];
-
-static int evpool_begin(evpool_t** out, int rounds) {
-    int dev = 0;
-    SRT_HIPCHK(hipGetDevice(&dev));
-    evpool_t* p = &g_evp[dev & 63];
-    if (p->cap < 2 * rounds) {
-        hipEvent_t* ne = (hipEvent_t*)realloc(p->ev, sizeof(hipEvent_t) * 2 * rounds);
-        if (!ne) return SRT_E_NOMEM;
-        p->ev = ne;
-        for (int i = p->cap; i < 2 * rounds; i++) SRT_HIPCHK(hipEventCreate(&p->ev[i]));
-        p->cap = 2 * rounds;
-    }
-    p->used = 0;
-    *out = p;
-    return SRT_OK;
-}
-
-static int evpool_sum(evpool_t* p, hipEvent_t last, srt_build_stats* stats) {
-    SRT_HIPCHK(hipEventSynchronize(last));
-    double tot = 0;
-    for (int i = 0; i + 1 < p->used; i += 2) {
-        float ms = 0;
-        SRT_HIPCHK(hipEventElapsedTime(&ms, p->ev[i], p->ev[i + 1]));
-        tot += ms;
-    }
-    stats->ms_update = tot;
-    stats->n_update = p->used / 2;
-    return SRT_OK;
-}
-
 static int fw_shard_part(uint32_t* D, int ld, int row0, int nrows, const uint32_t* P, int k0,
                          hipStream_t st, evpool_t* evp) {
     const int nb = ld / B, nrb = nrows / B;
@@ -440,49 +407,94 @@ __global__ void arc_transpose_fill(int n, const int32_t* __restrict__ ptr,
 }
 
 /* ------------------------------------------------------------------------------------------ */
-/* Canonical predecessor + path-order reliability, one workgroup per source row s.            */
+/* Canonical predecessor, sources across lanes.                                               */
 /* pred(s,t) = argmin over essential in-arcs (u,t) with D[s][u] + w == D[s][t] of (D[s][u], u) */
-/* rel(s,t)  = rel(s,pred) * r(pred,t), rel(s,s) = 1  -> the product in path order.            */
+/* A wave takes 64 consecutive local sources; t and the arc list of t are wave-uniform (scalar */
+/* loads), and D[s][u] for the 64 sources is one coalesced 256-byte read of row u of DT, the   */
+/* transpose of the local row block. Blocks are mapped so that each XCD works on its own      */
+/* source block at a time (its 8 MB column slab stays in that XCD's L2 / the Infinity Cache). */
 /* ------------------------------------------------------------------------------------------ */
-template <bool DROW_LDS>
-__global__ __launch_bounds__(512) void dense_predrel_kernel(int n, int ld, int row0,
-                                                            const uint32_t* __restrict__ d,
-                                                            const int32_t* __restrict__ iptr,
-                                                            const int32_t* __restrict__ icol,
-                                                            const uint32_t* __restrict__ iw,
-                                                            const double* __restrict__ ir,
-                                                            double* __restrict__ rel,
-                                                            int32_t* __restrict__ max_depth) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const int s = row0 + blockIdx.x;
-    if (s >= n) return;
-    const uint32_t* dg = d + (size_t)blockIdx.x * ld;
-    uint32_t* drow = smem;
-    int32_t* arc = reinterpret_cast<int32_t*>(smem + (DROW_LDS ? ld : 0));
-    if (DROW_LDS)
-        for (int t = threadIdx.x; t < n; t += blockDim.x) drow[t] = dg[t];
-    __syncthreads();
-    for (int t = threadIdx.x; t < n; t += blockDim.x) {
-        int bk = -1;
-        if (t != s) {
-            const uint32_t dt = DROW_LDS ? drow[t] : dg[t];
-            uint64_t best = ~0ull;
-            const int kb = iptr[t], ke = iptr[t + 1];
-            for (int k = kb; k < ke; ++k) {
-                const int u = icol[k];
-                const uint32_t du = DROW_LDS ? drow[u] : dg[u];
-                if (du + iw[k] == dt) {
-                    uint64_t key = ((uint64_t)du << 32) | (uint32_t)u;
-                    if (key < best) {
-                        best = key;
-                        bk = k;
-                    }
-                }
-            }
-        }
-        arc[t] = bk;
+__global__ __launch_bounds__(256) void transpose_u32_kernel(int rows, int cols,
+                                                            const uint32_t* __restrict__ in,
+                                                            size_t ldi, uint32_t* __restrict__ out,
+                                                            size_t ldo) {
+    __shared__ uint32_t tile[64][65];
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+    for (int a = ty; a < 64; a += 4) {
+        const int r = r0 + a, c = c0 + tx;
+        tile[a][tx] = (r < rows && c < cols) ? in[(size_t)r * ldi + c] : 0u;
     }
     __syncthreads();
+    for (int a = ty; a < 64; a += 4) {
+        const int c = c0 + a, r = r0 + tx;
+        if (r < rows && c < cols) out[(size_t)c * ldo + r] = tile[tx][a];
+    }
+}
+
+__global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nloc, int ldT,
+                                                        const uint32_t* __restrict__ DT,
+                                                        const int32_t* __restrict__ iptr,
+                                                        const uint2* __restrict__ uw,
+                                                        int32_t* __restrict__ predT, int nsb,
+                                                        int tch, int tper) {
+    const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
+    const int sb = (j / tch) * 8 + xcd, tc = j % tch;
+    if (sb >= nsb) return;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int sl = sb * 64 + lane;
+    const int s = row0 + sl;
+    const bool valid = sl < nloc && s < n;
+    const int t1 = min(n, (tc + 1) * tper);
+    for (int t = tc * tper + wv; t < t1; t += 4) {
+        const uint32_t dst = DT[(size_t)t * ldT + sl];
+        const int kb = __builtin_amdgcn_readfirstlane(iptr[t]);
+        const int ke = __builtin_amdgcn_readfirstlane(iptr[t + 1]);
+        uint64_t best = ~0ull;
+        int bk = -1;
+        int k = kb;
+        for (; k + 4 <= ke; k += 4) {
+            const uint2 a0 = uw[k], a1 = uw[k + 1], a2 = uw[k + 2], a3 = uw[k + 3];
+            const uint32_t d0 = DT[(size_t)a0.x * ldT + sl], d1 = DT[(size_t)a1.x * ldT + sl];
+            const uint32_t d2 = DT[(size_t)a2.x * ldT + sl], d3 = DT[(size_t)a3.x * ldT + sl];
+#define SRT_PRED_TRY(dd, aa, kk)                                                  \
+    if ((dd) + (aa).y == dst) {                                                   \
+        const uint64_t key = ((uint64_t)(dd) << 32) | (aa).x;                     \
+        if (key < best) {                                                         \
+            best = key;                                                           \
+            bk = (kk);                                                            \
+        }                                                                         \
+    }
+            SRT_PRED_TRY(d0, a0, k)
+            SRT_PRED_TRY(d1, a1, k + 1)
+            SRT_PRED_TRY(d2, a2, k + 2)
+            SRT_PRED_TRY(d3, a3, k + 3)
+        }
+        for (; k < ke; ++k) {
+            const uint2 a0 = uw[k];
+            const uint32_t d0 = DT[(size_t)a0.x * ldT + sl];
+            SRT_PRED_TRY(d0, a0, k)
+        }
+#undef SRT_PRED_TRY
+        if (valid) predT[(size_t)t * ldT + sl] = (s == t) ? -1 : bk;
+    }
+}
+
+/* Path-order reliability, one workgroup per local source row:
+ * rel(s,t) = rel(s,pred) * r(pred,t), rel(s,s) = 1 -> the product in the order of
+ * topology.c:1364-1365. Sweeps until every target of the row is resolved (tree depth). */
+__global__ __launch_bounds__(512) void rel_rows_kernel(int n, int ld, int row0,
+                                                       const int32_t* __restrict__ pred,
+                                                       const int32_t* __restrict__ icol,
+                                                       const double* __restrict__ ir,
+                                                       double* __restrict__ rel,
+                                                       int32_t* __restrict__ max_depth) {
+    extern __shared__ __attribute__((aligned(16))) int32_t arc[];
+    const int s = row0 + blockIdx.x;
+    if (s >= n) return;
+    const int32_t* pg = pred + (size_t)blockIdx.x * ld;
+    for (int t = threadIdx.x; t < n; t += blockDim.x) arc[t] = pg[t];
     double* rr = rel + (size_t)blockIdx.x * ld;
     /* each thread owns t = tid + i*blockDim (i < 64 for n <= 32768) */
     uint64_t pending = 0;
@@ -522,6 +534,12 @@ __global__ __launch_bounds__(512) void dense_predrel_kernel(int n, int ld, int r
         if (!__syncthreads_or(any)) break;
     }
     if (threadIdx.x == 0) atomicMax(max_depth, depth);
+}
+
+__global__ void pack_uw_kernel(int64_t arcs, const int32_t* __restrict__ col,
+                               const uint32_t* __restrict__ w, uint2* __restrict__ uw) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < arcs) uw[i] = make_uint2((uint32_t)col[i], w[i]);
 }
 
 /* Diagonal rule (topology.c:1431-1576): min over incident OUT edges of (self-loop: L,
@@ -620,6 +638,11 @@ typedef struct {
     double *ar, *tr, *xsend, *xrecv;
     uint32_t* panel;
     size_t panel_cap;
+    uint2* uw;
+    size_t uw_cap;
+    uint32_t* dt;   /* transpose of the local row block, then the predecessor rows */
+    int32_t* predt; /* predecessors, sources across columns */
+    size_t dt_cap, predt_cap;
 } dense_ws;
 
 static dense_ws g_ws[64];
@@ -725,20 +748,34 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         return SRT_E_ARG;
     }
     if (lrows > 0) {
-        size_t lds_both = (size_t)2 * ld * sizeof(uint32_t);
-        if (lds_both <= 160 * 1024) {
-            SRT_HIPCHK(hipFuncSetAttribute((const void*)dense_predrel_kernel<true>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)lds_both));
-            dense_predrel_kernel<true><<<lrows, 512, lds_both, st>>>(n, ld, row0, d, iptr, icol, iw,
-                                                                      ir, rel, ws->depth);
-        } else {
-            size_t lds = (size_t)ld * sizeof(uint32_t);
-            SRT_HIPCHK(hipFuncSetAttribute((const void*)dense_predrel_kernel<false>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            dense_predrel_kernel<false><<<lrows, 512, lds, st>>>(n, ld, row0, d, iptr, icol, iw, ir,
-                                                                  rel, ws->depth);
-        }
+        const size_t slab = (size_t)ld * nrows;
+        size_t c1 = ws->dt_cap, c2 = ws->predt_cap, c3 = ws->uw_cap;
+        if ((rc = ws_grow((void**)&ws->dt, &c1, slab, sizeof(uint32_t)))) return rc;
+        ws->dt_cap = c1;
+        if ((rc = ws_grow((void**)&ws->predt, &c2, slab, sizeof(int32_t)))) return rc;
+        ws->predt_cap = c2;
+        if ((rc = ws_grow((void**)&ws->uw, &c3, (size_t)total + 1, sizeof(uint2)))) return rc;
+        ws->uw_cap = c3;
+        if (total > 0)
+            pack_uw_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, icol, iw, ws->uw);
+        /* DT[u][sl] = D[row0 + sl][u] */
+        transpose_u32_kernel<<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)), 256, 0, st>>>(
+            nrows, ld, d, (size_t)ld, ws->dt, (size_t)nrows);
+        const int nsb = nrows / 64;
+        const int tch = max(1, min(n, 256));
+        const int tper = srt_ceil_div(n, tch);
+        const int grid = srt_ceil_div(nsb, 8) * 8 * tch;
+        pred_cols_kernel<<<grid, 256, 0, st>>>(n, row0, lrows, nrows, ws->dt, iptr, ws->uw,
+                                               ws->predt, nsb, tch, tper);
+        /* predecessor rows: pred[sl][t] = predT[t][sl] (reuses the DT buffer) */
+        int32_t* pred = reinterpret_cast<int32_t*>(ws->dt);
+        transpose_u32_kernel<<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+            n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows,
+            reinterpret_cast<uint32_t*>(pred), (size_t)ld);
+        const size_t lds = (size_t)ld * sizeof(int32_t);
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_rows_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        rel_rows_kernel<<<lrows, 512, lds, st>>>(n, ld, row0, pred, icol, ir, rel, ws->depth);
         SRT_HIPCHK(hipGetLastError());
     }
     if (stats) {
@@ -797,14 +834,22 @@ extern "C" int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, c
     SRT_HIPCHK(hipEventCreate(&e1));
     SRT_HIPCHK(hipEventCreate(&e2));
     SRT_HIPCHK(hipEventRecord(e0, st));
-    dim3 g(srt_ceil_div(ld, 256), ld);
-    init_dist_kernel<<<g, 256, 0, st>>>(n, ld, 0, w, lat);
-    SRT_HIPCHK(hipGetLastError());
     evpool_t* evp = NULL;
     int rc;
     if (stats && stats->time_kernels && (rc = evpool_begin(&evp, ld / B))) return rc;
-    rc = srt_dense_fw_device(n, ld, lat, st, evp);
-    if (rc) return rc;
+    int exact = 0;
+    if (ld % 128 == 0) {
+        rc = srt_fw16_build(n, ld, 0, ld, w, lat, st, evp, NULL, NULL, NULL, 0, &exact);
+        if (rc) return rc;
+    }
+    if (!exact) { /* u32 path: ld not a multiple of 128, or a distance reached 0xFFFF quanta */
+        if (evp) evp->used = 0;
+        dim3 g(srt_ceil_div(ld, 256), ld);
+        init_dist_kernel<<<g, 256, 0, st>>>(n, ld, 0, w, lat);
+        SRT_HIPCHK(hipGetLastError());
+        rc = srt_dense_fw_device(n, ld, lat, st, evp);
+        if (rc) return rc;
+    }
     SRT_HIPCHK(hipEventRecord(e1, st));
     rc = srt_dense_post_device(n, ld, directed, w, r, lat, rel, st, stats);
     if (rc) return rc;
@@ -815,7 +860,7 @@ extern "C" int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, c
         SRT_HIPCHK(hipEventElapsedTime(&a, e0, e1));
         SRT_HIPCHK(hipEventElapsedTime(&b, e1, e2));
         stats->algo = SRT_ALGO_DENSE_FW;
-        stats->fw_block = B;
+        stats->fw_block = exact ? -B : B; /* negative: packed-u16 distances */
         stats->ms_fw = a;
         stats->ms_post = b;
         stats->ms_total = a + b;
@@ -851,6 +896,23 @@ typedef struct {
     int ld;
 } shard_ctx;
 
+static int shard_owner(void* vctx, int k0) {
+    const shard_ctx* ctx = (const shard_ctx*)vctx;
+    const int R = srt_comm_size(ctx->comm);
+    for (int q = 0; q < R; q++) {
+        int32_t qb, qe;
+        srt_shard_rows(ctx->ld, SRT_SHARD_ALIGN, R, q, &qb, &qe);
+        if (k0 >= qb && k0 < qe) return q;
+    }
+    return 0;
+}
+
+static int shard_bcast(void* vctx, void* panel, size_t bytes, int owner, hipStream_t st) {
+    const shard_ctx* ctx = (const shard_ctx*)vctx;
+    SRT_NCCLCHK(ncclBroadcast(panel, panel, bytes, ncclUint8, owner, srt_comm_nccl(ctx->comm), st));
+    return SRT_OK;
+}
+
 static int shard_gather(void* vctx, dense_ws* ws, int n, int phase, int32_t total, hipStream_t st) {
     (void)total;
     shard_ctx* ctx = (shard_ctx*)vctx;
@@ -874,7 +936,7 @@ static int shard_gather(void* vctx, dense_ws* ws, int n, int phase, int32_t tota
     ncclResult_t r = ncclGroupStart();
     for (int q = 0; q < R && r == ncclSuccess; q++) {
         int32_t b, e;
-        srt_shard_rows(ctx->ld, B, R, q, &b, &e);
+        srt_shard_rows(ctx->ld, SRT_SHARD_ALIGN, R, q, &b, &e);
         b = min(b, n);
         e = min(e, n);
         const size_t o = (size_t)hptr[b], c = (size_t)(hptr[e] - hptr[b]);
@@ -912,7 +974,7 @@ static int shard_mirror(const srt_comm* comm, int n, int ld, int b, int e, doubl
     size_t so = 0;
     for (int q = me + 1; q < R; q++) {
         int32_t qb, qe;
-        srt_shard_rows(ld, B, R, q, &qb, &qe);
+        srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &qb, &qe);
         const int64_t cnt = (int64_t)nr * (qe - qb);
         if (cnt > 0)
             pack_cols_kernel<<<srt_ceil_div(cnt, 256), 256, 0, st>>>(nr, ld, qb, qe, rel_rows,
@@ -924,7 +986,7 @@ static int shard_mirror(const srt_comm* comm, int n, int ld, int b, int e, doubl
     so = 0;
     for (int q = me + 1; q < R; q++) {
         int32_t qb, qe;
-        srt_shard_rows(ld, B, R, q, &qb, &qe);
+        srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &qb, &qe);
         const size_t cnt = (size_t)nr * (qe - qb);
         if (cnt) SRT_NCCLCHK(ncclSend(ws->xsend + so, cnt, ncclFloat64, q, nc, st));
         so += cnt;
@@ -932,7 +994,7 @@ static int shard_mirror(const srt_comm* comm, int n, int ld, int b, int e, doubl
     size_t ro = 0;
     for (int q = 0; q < me; q++) {
         int32_t qb, qe;
-        srt_shard_rows(ld, B, R, q, &qb, &qe);
+        srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &qb, &qe);
         const size_t cnt = (size_t)(qe - qb) * nr;
         if (cnt) SRT_NCCLCHK(ncclRecv(ws->xrecv + ro, cnt, ncclFloat64, q, nc, st));
         ro += cnt;
@@ -941,7 +1003,7 @@ static int shard_mirror(const srt_comm* comm, int n, int ld, int b, int e, doubl
     ro = 0;
     for (int q = 0; q < me; q++) {
         int32_t qb, qe;
-        srt_shard_rows(ld, B, R, q, &qb, &qe);
+        srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &qb, &qe);
         const int pw = qe - qb;
         if (pw > 0 && nr > 0) {
             dim3 g(srt_ceil_div(pw, 64), srt_ceil_div(nr, 64));
@@ -961,7 +1023,7 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
                                        const uint32_t* w_rows, const double* r_rows,
                                        uint32_t* lat_rows, double* rel_rows, void* stream,
                                        int32_t fw_block, srt_build_stats* stats) {
-    if (!comm || n <= 0 || ld < n || ld % B || !w_rows || !r_rows || !lat_rows || !rel_rows) {
+    if (!comm || n <= 0 || ld < n || ld % SRT_SHARD_ALIGN || !w_rows || !r_rows || !lat_rows || !rel_rows) {
         srt_set_error("srt_dense_build_sharded: bad arguments");
         return SRT_E_ARG;
     }
@@ -971,7 +1033,7 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
     }
     const int R = srt_comm_size(comm), me = srt_comm_rank(comm);
     int32_t b, e;
-    srt_shard_rows(ld, B, R, me, &b, &e);
+    srt_shard_rows(ld, SRT_SHARD_ALIGN, R, me, &b, &e);
     const int nr = e - b;
     hipStream_t st = (hipStream_t)stream;
     ncclComm_t nc = srt_comm_nccl(comm);
@@ -986,32 +1048,41 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
     SRT_HIPCHK(hipEventCreate(&e1));
     SRT_HIPCHK(hipEventCreate(&e2));
     SRT_HIPCHK(hipEventRecord(e0, st));
-    if (nr > 0) {
-        dim3 g(srt_ceil_div(ld, 256), nr);
-        init_dist_kernel<<<g, 256, 0, st>>>(n, ld, b, w_rows, lat_rows);
-        SRT_HIPCHK(hipGetLastError());
-    }
     evpool_t* evp = NULL;
     if (stats && stats->time_kernels && (rc = evpool_begin(&evp, ld / B))) return rc;
-    for (int k0 = 0; k0 < ld; k0 += B) {
-        int owner = 0;
-        for (int q = 0; q < R; q++) {
-            int32_t qb, qe;
-            srt_shard_rows(ld, B, R, q, &qb, &qe);
-            if (k0 >= qb && k0 < qe) owner = q;
+    shard_ctx ctx = {comm, ld};
+    int exact = 0;
+    rc = srt_fw16_build(n, ld, b, nr, w_rows, lat_rows, st, evp, shard_owner,
+                        R > 1 ? shard_bcast : NULL, &ctx, me, &exact);
+    if (rc) return rc;
+    if (R > 1) { /* every rank must agree before the u32 fallback */
+        int32_t* flag = ws->cnt;
+        SRT_HIPCHK(hipMemcpyAsync(flag, &exact, sizeof(int32_t), hipMemcpyHostToDevice, st));
+        SRT_NCCLCHK(ncclAllReduce(flag, flag, 1, ncclInt32, ncclMin, nc, st));
+        SRT_HIPCHK(hipMemcpyAsync(&exact, flag, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipStreamSynchronize(st));
+    }
+    if (!exact) {
+        if (evp) evp->used = 0;
+        if (nr > 0) {
+            dim3 g(srt_ceil_div(ld, 256), nr);
+            init_dist_kernel<<<g, 256, 0, st>>>(n, ld, b, w_rows, lat_rows);
+            SRT_HIPCHK(hipGetLastError());
         }
-        uint32_t* P;
-        if (owner == me) {
-            P = lat_rows + (size_t)(k0 - b) * ld;
-            if ((rc = fw_owner_part(lat_rows, ld, b, nr, P, k0, st))) return rc;
-        } else {
-            P = ws->panel;
+        for (int k0 = 0; k0 < ld; k0 += B) {
+            const int owner = shard_owner(&ctx, k0);
+            uint32_t* P;
+            if (owner == me) {
+                P = lat_rows + (size_t)(k0 - b) * ld;
+                if ((rc = fw_owner_part(lat_rows, ld, b, nr, P, k0, st))) return rc;
+            } else {
+                P = ws->panel;
+            }
+            if (R > 1) SRT_NCCLCHK(ncclBroadcast(P, P, (size_t)B * ld, ncclUint32, owner, nc, st));
+            if ((rc = fw_shard_part(lat_rows, ld, b, nr, P, k0, st, evp))) return rc;
         }
-        if (R > 1) SRT_NCCLCHK(ncclBroadcast(P, P, (size_t)B * ld, ncclUint32, owner, nc, st));
-        if ((rc = fw_shard_part(lat_rows, ld, b, nr, P, k0, st, evp))) return rc;
     }
     SRT_HIPCHK(hipEventRecord(e1, st));
-    shard_ctx ctx = {comm, ld};
     rc = dense_post(n, ld, b, nr, directed, w_rows, r_rows, lat_rows, rel_rows, st, stats,
                     R > 1 ? shard_gather : NULL, &ctx);
     if (rc) return rc;
@@ -1031,7 +1102,7 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
         SRT_HIPCHK(hipEventElapsedTime(&a, e0, e1));
         SRT_HIPCHK(hipEventElapsedTime(&c, e1, e2));
         stats->algo = SRT_ALGO_DENSE_FW;
-        stats->fw_block = B;
+        stats->fw_block = exact ? -B : B; /* negative: packed-u16 distances */
         stats->ms_fw = a;
         stats->ms_post = c;
         stats->ms_total = a + c;

@@ -1,0 +1,316 @@
+/*
+ * fw16.hip -- packed-u16 blocked Floyd-Warshall for gfx950.
+ *
+ * Distances are held as u16 quanta with saturating adds (v_pk_add_u16 ... clamp): two
+ * relaxations per VALU instruction (v_pk_add_u16 + v_pk_min_u16 per pair) and half the HBM / LDS
+ * / xGMI bytes of the u32 path. Saturation is exact: sat(sat(a)+b) = sat(a+b) and min commutes
+ * with sat, so the result is min(D, 0xFFFF) element-wise. If any real pair saturates the build
+ * reports inexact and the caller reruns the u32 kernels -- the table is never approximate.
+ *
+ * Kernels (pivot block KB = 64 rows/cols per round):
+ *   fw16_diag    closure of the 64x64 diagonal tile in LDS (64 dependent steps)
+ *   fw16_panel   pivot-row panel tiles Dkk* (x) X and pivot-column tiles X (x) Dkk* (64x64)
+ *   fw16_update  every 128x128 tile: C <- min(C, A (x) B), A = D[I][k-block], B = P[:, J]
+ * The 128x128 update tile gives each of 256 threads an 8x8 block: per pivot step 2 LDS reads
+ * (8 B of A, 16 B of B) feed 64 relaxations (0.5 B/relax, vs 2 B/relax for the u32 4x4 tile).
+ */
+#include "srt_device.h"
+
+typedef unsigned short u16;
+typedef u16 u16x2 __attribute__((ext_vector_type(2)));
+
+#define KB 64
+#define INF16 0xFFFFu
+#define LDA16 (KB + 8) /* u16 stride of an A row in LDS: 144 B, 16-byte aligned */
+
+static __device__ __forceinline__ u16x2 as2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+static __device__ __forceinline__ uint32_t as32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+static __device__ __forceinline__ u16x2 relax(u16x2 acc, u16x2 a, u16x2 b) {
+    return __builtin_elementwise_min(acc, __builtin_elementwise_add_sat(a, b));
+}
+
+/* ---- staging ------------------------------------------------------------------------------ */
+template <int TM>
+__device__ __forceinline__ void stage_A(u16* __restrict__ sA, const u16* __restrict__ g, size_t ldg,
+                                        int tid) {
+    for (int idx = tid; idx < TM * 8; idx += 256) { /* TM rows x 64 u16 = 8 uint4 per row */
+        const int row = idx >> 3, c8 = (idx & 7) * 8;
+        *reinterpret_cast<uint4*>(sA + row * LDA16 + c8) =
+            *reinterpret_cast<const uint4*>(g + (size_t)row * ldg + c8);
+    }
+}
+
+template <int TN>
+__device__ __forceinline__ void stage_B(u16* __restrict__ sB, const u16* __restrict__ g, size_t ldg,
+                                        int tid) {
+    constexpr int LDB = TN + 8;
+    constexpr int PER = TN / 8;
+    for (int idx = tid; idx < KB * PER; idx += 256) {
+        const int row = idx / PER, c8 = (idx % PER) * 8;
+        *reinterpret_cast<uint4*>(sB + row * LDB + c8) =
+            *reinterpret_cast<const uint4*>(g + (size_t)row * ldg + c8);
+    }
+}
+
+/* ---- register-blocked min-plus over the 64 pivots ------------------------------------------ */
+template <int TN, int RM, int RN>
+__device__ __forceinline__ void mp16(u16x2 (&acc)[RM][RN / 2], const u16* __restrict__ sA,
+                                     const u16* __restrict__ sB, int tx, int ty) {
+    constexpr int LDB = TN + 8;
+    const u16* pa = sA + ty * RM * LDA16;
+    const u16* pb = sB + tx * RN;
+#pragma unroll 1
+    for (int m = 0; m < KB; m += 4) {
+        uint2 av[RM];
+#pragma unroll
+        for (int r = 0; r < RM; ++r) av[r] = *reinterpret_cast<const uint2*>(pa + r * LDA16 + m);
+        uint32_t bv[4][RN / 2];
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+            if constexpr (RN == 8) {
+                uint4 v = *reinterpret_cast<const uint4*>(pb + (m + mm) * LDB);
+                bv[mm][0] = v.x;
+                bv[mm][1] = v.y;
+                bv[mm][2] = v.z;
+                bv[mm][3] = v.w;
+            } else {
+                uint2 v = *reinterpret_cast<const uint2*>(pb + (m + mm) * LDB);
+                bv[mm][0] = v.x;
+                bv[mm][1] = v.y;
+            }
+        }
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm)
+#pragma unroll
+            for (int r = 0; r < RM; ++r) {
+                const u16x2 a = as2(mm < 2 ? av[r].x : av[r].y);
+                const u16x2 as = (mm & 1) ? a.yy : a.xx;
+#pragma unroll
+                for (int c = 0; c < RN / 2; ++c) acc[r][c] = relax(acc[r][c], as, as2(bv[mm][c]));
+            }
+    }
+}
+
+template <int RM, int RN>
+__device__ __forceinline__ void load_acc16(u16x2 (&acc)[RM][RN / 2], const u16* __restrict__ C,
+                                           size_t ldc, int tx, int ty) {
+#pragma unroll
+    for (int r = 0; r < RM; ++r) {
+        const u16* p = C + (size_t)(ty * RM + r) * ldc + tx * RN;
+        if constexpr (RN == 8) {
+            uint4 v = *reinterpret_cast<const uint4*>(p);
+            acc[r][0] = as2(v.x);
+            acc[r][1] = as2(v.y);
+            acc[r][2] = as2(v.z);
+            acc[r][3] = as2(v.w);
+        } else {
+            uint2 v = *reinterpret_cast<const uint2*>(p);
+            acc[r][0] = as2(v.x);
+            acc[r][1] = as2(v.y);
+        }
+    }
+}
+
+/* store only the rows of the thread block that changed (unchanged tiles cost no HBM write) */
+template <int RM, int RN>
+__device__ __forceinline__ void store_acc16(const u16x2 (&acc)[RM][RN / 2],
+                                            const u16x2 (&old)[RM][RN / 2], u16* __restrict__ C,
+                                            size_t ldc, int tx, int ty) {
+#pragma unroll
+    for (int r = 0; r < RM; ++r) {
+        bool ch = false;
+#pragma unroll
+        for (int c = 0; c < RN / 2; ++c) ch |= as32(acc[r][c]) != as32(old[r][c]);
+        if (!ch) continue;
+        u16* p = C + (size_t)(ty * RM + r) * ldc + tx * RN;
+        if constexpr (RN == 8)
+            *reinterpret_cast<uint4*>(p) =
+                make_uint4(as32(acc[r][0]), as32(acc[r][1]), as32(acc[r][2]), as32(acc[r][3]));
+        else
+            *reinterpret_cast<uint2*>(p) = make_uint2(as32(acc[r][0]), as32(acc[r][1]));
+    }
+}
+
+/* old[] must already hold the tile (loaded before the LDS staging so its HBM latency overlaps) */
+template <int TM, int TN, int RM, int RN>
+__device__ __forceinline__ void tile_product(u16* __restrict__ C, size_t ldc,
+                                             const u16* __restrict__ sA, const u16* __restrict__ sB,
+                                             int tx, int ty, const u16x2 (&old)[RM][RN / 2]) {
+    u16x2 acc[RM][RN / 2];
+#pragma unroll
+    for (int r = 0; r < RM; ++r)
+#pragma unroll
+        for (int c = 0; c < RN / 2; ++c) acc[r][c] = old[r][c];
+    mp16<TN, RM, RN>(acc, sA, sB, tx, ty);
+    store_acc16<RM, RN>(acc, old, C, ldc, tx, ty);
+}
+
+/* ---- kernels --------------------------------------------------------------------------------- */
+__global__ void fw16_init_kernel(int n, int ld, int row0, const uint32_t* __restrict__ w,
+                                 u16* __restrict__ d) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = row0 + blockIdx.y;
+    if (j >= ld) return;
+    const uint32_t x = (i < n && j < n) ? w[(size_t)blockIdx.y * ld + j] : INF16;
+    d[(size_t)blockIdx.y * ld + j] = (i == j) ? (u16)0 : (u16)min(x, (uint32_t)INF16);
+}
+
+/* closure of the diagonal tile: 64 dependent pivot steps in LDS, 4x4 per thread */
+__global__ __launch_bounds__(256) void fw16_diag_kernel(u16* __restrict__ P, int ld, int k0) {
+    __shared__ __attribute__((aligned(16))) u16 s[KB * LDA16];
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    u16* T = P + k0;
+    for (int idx = tid; idx < KB * 8; idx += 256) {
+        const int row = idx >> 3, c8 = (idx & 7) * 8;
+        *reinterpret_cast<uint4*>(s + row * LDA16 + c8) =
+            *reinterpret_cast<const uint4*>(T + (size_t)row * ld + c8);
+    }
+    __syncthreads();
+    for (int m = 0; m < KB; ++m) {
+        const uint2 bm = *reinterpret_cast<const uint2*>(s + m * LDA16 + 4 * tx);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const u16 a = s[(4 * ty + r) * LDA16 + m];
+            const u16x2 as = {a, a};
+            uint2* row = reinterpret_cast<uint2*>(s + (4 * ty + r) * LDA16 + 4 * tx);
+            uint2 v = *row;
+            v.x = as32(relax(as2(v.x), as, as2(bm.x)));
+            v.y = as32(relax(as2(v.y), as, as2(bm.y)));
+            *row = v;
+        }
+        __syncthreads();
+    }
+    for (int idx = tid; idx < KB * 8; idx += 256) {
+        const int row = idx >> 3, c8 = (idx & 7) * 8;
+        *reinterpret_cast<uint4*>(T + (size_t)row * ld + c8) =
+            *reinterpret_cast<const uint4*>(s + row * LDA16 + c8);
+    }
+}
+
+/* pivot-row panel tiles (k, j): X <- Dkk* (x) X ; pivot-column tiles (i, k): X <- X (x) Dkk* */
+__global__ __launch_bounds__(256) void fw16_panel_kernel(u16* __restrict__ D, int ld, int row0,
+                                                         int nrow_tiles, u16* __restrict__ P, int k0,
+                                                         int ncol_tiles, int do_row, int do_col) {
+    __shared__ __attribute__((aligned(16))) u16 sA[KB * LDA16];
+    __shared__ __attribute__((aligned(16))) u16 sB[KB * (KB + 8)];
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    int bid = blockIdx.x;
+    u16* C;
+    if (bid < ncol_tiles) {
+        if (!do_row || bid * KB == k0) return;
+        C = P + bid * KB;
+        stage_A<KB>(sA, P + k0, ld, tid);
+        stage_B<KB>(sB, C, ld, tid);
+    } else {
+        bid -= ncol_tiles;
+        if (!do_col || bid >= nrow_tiles || row0 + bid * KB == k0) return;
+        C = D + (size_t)bid * KB * ld + k0;
+        stage_A<KB>(sA, C, ld, tid);
+        stage_B<KB>(sB, P + k0, ld, tid);
+    }
+    u16x2 old[4][2];
+    load_acc16<4, 4>(old, C, ld, tx, ty);
+    __syncthreads();
+    tile_product<KB, KB, 4, 4>(C, ld, sA, sB, tx, ty, old);
+}
+
+/* every 128x128 tile of the local rows: D_IJ <- min(D_IJ, D_I,k (x) P_k,J) */
+__global__ __launch_bounds__(256) void fw16_update_kernel(u16* __restrict__ D, int ld,
+                                                          const u16* __restrict__ P, int k0,
+                                                          int ncol_tiles) {
+    __shared__ __attribute__((aligned(16))) u16 sA[128 * LDA16];
+    __shared__ __attribute__((aligned(16))) u16 sB[KB * (128 + 8)];
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    /* XCD-aware order: consecutive blocks land on different XCDs; give each XCD a contiguous run
+     * of tiles in a row band so its L2 keeps the band's A slice and the panel columns. */
+    const int nb = gridDim.x;
+    const int per = nb >> 3;
+    const int bid = (nb & 7) == 0 ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
+    const int I = bid / ncol_tiles, J = bid % ncol_tiles;
+    u16* C = D + (size_t)I * 128 * ld + J * 128;
+    u16x2 old[8][4];
+    load_acc16<8, 8>(old, C, ld, tx, ty); /* HBM reads in flight during the staging */
+    stage_A<128>(sA, D + (size_t)I * 128 * ld + k0, ld, tid);
+    stage_B<128>(sB, P + J * 128, ld, tid);
+    __syncthreads();
+    tile_product<128, 128, 8, 8>(C, ld, sA, sB, tx, ty, old);
+}
+
+/* widen to the u32 table and flag saturation of a real pair (i, j < n) */
+__global__ void fw16_finish_kernel(int n, int ld, int row0, const u16* __restrict__ d16,
+                                   uint32_t* __restrict__ lat, int* __restrict__ saturated) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = row0 + blockIdx.y;
+    if (j >= ld) return;
+    const size_t ix = (size_t)blockIdx.y * ld + j;
+    const uint32_t v = d16[ix];
+    const bool real = i < n && j < n;
+    lat[ix] = (v == INF16) ? SRT_INF : v;
+    if (real && v == INF16) atomicOr(saturated, 1);
+}
+
+/* ---- orchestration --------------------------------------------------------------------------- */
+int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,
+                   hipStream_t st, evpool_t* evp, srt_owner_fn owner_of, srt_panel_bcast_fn bcast,
+                   void* ctx, int rank, int* exact) {
+    if (ld % 128 || nrows % 128) {
+        srt_set_error("u16 FW needs ld and the row shard to be multiples of 128");
+        return SRT_E_ARG;
+    }
+    static u16* bufs[64];
+    static size_t caps[64];
+    static u16* panels[64];
+    static int* flags[64];
+    int dev = 0;
+    SRT_HIPCHK(hipGetDevice(&dev));
+    dev &= 63;
+    const size_t need = (size_t)nrows * ld + (size_t)KB * ld;
+    if (caps[dev] < need) {
+        if (bufs[dev]) SRT_HIPCHK(hipFree(bufs[dev]));
+        SRT_HIPCHK(hipMalloc(&bufs[dev], need * sizeof(u16)));
+        caps[dev] = need;
+        panels[dev] = bufs[dev] + (size_t)nrows * ld;
+    }
+    panels[dev] = bufs[dev] + (size_t)nrows * ld;
+    if (!flags[dev]) SRT_HIPCHK(hipMalloc(&flags[dev], sizeof(int)));
+    u16* d = bufs[dev];
+    u16* pbuf = panels[dev];
+    if (nrows > 0) {
+        fw16_init_kernel<<<dim3(srt_ceil_div(ld, 256), nrows), 256, 0, st>>>(n, ld, row0, w_rows, d);
+        SRT_HIPCHK(hipGetLastError());
+    }
+    const int nb = ld / KB, nrb = nrows / KB, ncol128 = ld / 128, nrow128 = nrows / 128;
+    for (int k0 = 0; k0 < ld; k0 += KB) {
+        const int owner = owner_of ? owner_of(ctx, k0) : rank;
+        u16* P;
+        if (owner == rank) {
+            P = d + (size_t)(k0 - row0) * ld;
+            fw16_diag_kernel<<<1, 256, 0, st>>>(P, ld, k0);
+            fw16_panel_kernel<<<nb, 256, 0, st>>>(d, ld, row0, nrb, P, k0, nb, 1, 0);
+            SRT_HIPCHK(hipGetLastError());
+        } else {
+            P = pbuf;
+        }
+        if (bcast) {
+            int rc = bcast(ctx, P, (size_t)KB * ld * sizeof(u16), owner, st);
+            if (rc) return rc;
+        }
+        if (nrb > 0) {
+            fw16_panel_kernel<<<nb + nrb, 256, 0, st>>>(d, ld, row0, nrb, P, k0, nb, 0, 1);
+            if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
+            fw16_update_kernel<<<ncol128 * nrow128, 256, 0, st>>>(d, ld, P, k0, ncol128);
+            if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
+            SRT_HIPCHK(hipGetLastError());
+        }
+    }
+    SRT_HIPCHK(hipMemsetAsync(flags[dev], 0, sizeof(int), st));
+    if (nrows > 0)
+        fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 256), nrows), 256, 0, st>>>(n, ld, row0, d,
+                                                                             lat_rows, flags[dev]);
+    SRT_HIPCHK(hipGetLastError());
+    int sat = 0;
+    SRT_HIPCHK(hipMemcpyAsync(&sat, flags[dev], sizeof(int), hipMemcpyDeviceToHost, st));
+    SRT_HIPCHK(hipStreamSynchronize(st));
+    *exact = sat ? 0 : 1;
+    return SRT_OK;
+}

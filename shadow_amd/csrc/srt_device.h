@@ -6,6 +6,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "srt_internal.h"
 
@@ -21,6 +22,8 @@
 
 /* pivot-block edge of the blocked Floyd-Warshall and the output-tile edge of its kernels */
 #define SRT_FW_B 64
+/* row-shard alignment of every sharded dense build (the u16 update tile is 128 rows) */
+#define SRT_SHARD_ALIGN 128
 /* LDS row stride (u32) of a 64-wide tile: +4 keeps 16-byte alignment for ds_read_b128 */
 #define SRT_FW_LDT (SRT_FW_B + 4)
 
@@ -41,6 +44,55 @@ __host__ __device__ static inline uint64_t srt_hash(uint64_t seed, uint64_t stre
 static inline int srt_ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 /* internal (C++ linkage) entry points shared between translation units */
+/* HIP events bracketing every FW update launch (stats->time_kernels): the per-launch duration
+ * of the dominant kernel that bench.py reports against the roofline. */
+typedef struct {
+    hipEvent_t* ev;
+    int cap, used;
+} evpool_t;
+
+evpool_t* srt_evpool(int dev);
+
+
+static inline int evpool_begin(evpool_t** out, int rounds) {
+    int dev = 0;
+    SRT_HIPCHK(hipGetDevice(&dev));
+    evpool_t* p = srt_evpool(dev);
+    if (p->cap < 2 * rounds) {
+        hipEvent_t* ne = (hipEvent_t*)realloc(p->ev, sizeof(hipEvent_t) * 2 * rounds);
+        if (!ne) return SRT_E_NOMEM;
+        p->ev = ne;
+        for (int i = p->cap; i < 2 * rounds; i++) SRT_HIPCHK(hipEventCreate(&p->ev[i]));
+        p->cap = 2 * rounds;
+    }
+    p->used = 0;
+    *out = p;
+    return SRT_OK;
+}
+
+static inline int evpool_sum(evpool_t* p, hipEvent_t last, srt_build_stats* stats) {
+    SRT_HIPCHK(hipEventSynchronize(last));
+    double tot = 0;
+    for (int i = 0; i + 1 < p->used; i += 2) {
+        float ms = 0;
+        SRT_HIPCHK(hipEventElapsedTime(&ms, p->ev[i], p->ev[i + 1]));
+        tot += ms;
+    }
+    stats->ms_update = tot;
+    stats->n_update = p->used / 2;
+    return SRT_OK;
+}
+
+
+typedef int (*srt_panel_bcast_fn)(void* ctx, void* panel, size_t bytes, int owner, hipStream_t st);
+typedef int (*srt_owner_fn)(void* ctx, int k0);
+/* packed-u16 Floyd-Warshall over a row shard (fw16.hip). d16: nrows x ld u16. Returns SRT_OK and
+ * *exact = 1 when every distance fits below the u16 saturation value (else the caller reruns
+ * the u32 path). lat_rows receives the distances widened to u32 quanta. */
+int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,
+                   hipStream_t st, evpool_t* evp, srt_owner_fn owner_of, srt_panel_bcast_fn bcast,
+                   void* ctx, int rank, int* exact);
+
 int srt_dense_post_device(int32_t n, int32_t ld, int32_t directed, const uint32_t* w,
                           const double* r, uint32_t* d, double* rel, hipStream_t st,
                           srt_build_stats* stats);

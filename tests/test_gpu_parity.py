@@ -159,7 +159,7 @@ def test_dense_device_api_and_sharded_single_rank(gpu):
     """srt_dense_build_device and srt_dense_build_sharded (1-rank RCCL comm) on device data."""
     import torch
     from shadow_amd._lib import BuildStats, lib
-    n, ld = 700, 704
+    n, ld = 700, 768
     w = torch.empty((ld, ld), dtype=torch.int32, device="cuda")
     r = torch.empty((ld, ld), dtype=torch.float64, device="cuda")
     L = lib()
