@@ -1,0 +1,218 @@
+"""Multi-process (world_size 2, gloo, CPU) rehearsal of the sharded builds' decomposition.
+
+The GPU path (srt_dense_build_sharded / srt_sparse_allgather) runs one process per GPU over
+RCCL. Here the same schedule -- the library's own srt_shard_rows partition, the owner of each
+64-row pivot block, one pivot-panel broadcast per round, the essential-arc all-reduce/broadcast,
+the undirected mirror exchange (rank q sends rel[q rows][r cols] to every r > q) and the sparse
+source-shard all-gather -- is replayed with numpy compute and gloo collectives, and the
+assembled tables must equal the CPU oracle's.
+"""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+from shadow_amd import graphs
+
+INF = 0x7FFFFFFF
+KB = 64
+ALIGN = 128
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _shard(lib, ld, R, r):
+    b, e = ctypes.c_int32(), ctypes.c_int32()
+    lib.srt_shard_rows(ld, ALIGN, R, r, ctypes.byref(b), ctypes.byref(e))
+    return b.value, e.value
+
+
+def _minplus(A, B):
+    """min over m of A[:, m] + B[m, :] (int64 to avoid overflow)."""
+    return (A[:, :, None].astype(np.int64) + B[None, :, :].astype(np.int64)).min(axis=1)
+
+
+def _dense_worker(rank, R, port, n, seed, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=R)
+    from shadow_amd._lib import lib
+    L = lib()
+    ld = (n + ALIGN - 1) // ALIGN * ALIGN
+    b, e = _shard(L, ld, R, rank)
+    w, r = graphs.complete_dense(n, seed)
+    W = np.full((ld, ld), INF, np.int64)
+    W[:n, :n] = w
+    Rm = np.zeros((ld, ld))
+    Rm[:n, :n] = r
+    D = W[b:e].copy()
+    for i in range(b, e):
+        D[i - b, i] = 0
+    owners = [_shard(L, ld, R, x) for x in range(R)]
+    for k0 in range(0, ld, KB):
+        owner = [x for x, (qb, qe) in enumerate(owners) if qb <= k0 < qe][0]
+        P = torch.zeros((KB, ld), dtype=torch.int64)
+        if owner == rank:
+            Pk = D[k0 - b:k0 - b + KB]
+            T = Pk[:, k0:k0 + KB]
+            for m in range(KB):  # diagonal closure
+                T = np.minimum(T, T[:, m:m + 1] + T[m:m + 1, :])
+            Pk[:, k0:k0 + KB] = T
+            Pk[:] = np.minimum(Pk, _minplus(T, Pk))  # row panel
+            P = torch.from_numpy(Pk.copy())
+        dist.broadcast(P, owner)
+        Pn = P.numpy()
+        Dkk = Pn[:, k0:k0 + KB]
+        mine = np.array([not (k0 <= b + i < k0 + KB) for i in range(e - b)])
+        col = D[:, k0:k0 + KB]
+        col[mine] = np.minimum(col[mine], _minplus(col[mine], Dkk))  # column panel
+        D[mine] = np.minimum(D[mine], _minplus(D[mine][:, k0:k0 + KB], Pn))
+    # essential arcs (W[u][t] == D[u][t], u != t) of the local rows; all-reduce the counts
+    cnt = torch.zeros(ld, dtype=torch.int64)
+    arcs = {}
+    for i in range(e - b):
+        u = b + i
+        if u >= n:
+            continue
+        ts = [t for t in range(n) if t != u and W[u, t] < INF and W[u, t] == D[i, t]]
+        arcs[u] = ts
+        cnt[u] = len(ts)
+    dist.all_reduce(cnt)
+    # every rank broadcasts its rows' arcs (same segments as the RCCL broadcasts)
+    inarc = {}
+    for x, (qb, qe) in enumerate(owners):
+        seg = torch.zeros(int(cnt[qb:qe].sum()), dtype=torch.int64)
+        if x == rank:
+            seg = torch.tensor([t for u in range(qb, min(qe, n)) for t in arcs[u]], dtype=torch.int64)
+        dist.broadcast(seg, x)
+        o = 0
+        for u in range(qb, min(qe, n)):
+            inarc[u] = seg[o:o + int(cnt[u])].tolist()
+            o += int(cnt[u])
+    # canonical predecessor + path-order reliability for local rows (undirected: In* = Out*)
+    Dfull = np.zeros((ld, ld), np.int64)
+    Dt = torch.from_numpy(np.ascontiguousarray(D))
+    parts = [torch.zeros((qe - qb, ld), dtype=torch.int64) for qb, qe in owners]
+    dist.all_gather(parts, Dt)
+    Dfull = torch.cat(parts).numpy()  # only the lat check below uses the assembled D
+    rel = np.zeros((e - b, ld))
+    for i in range(e - b):
+        s = b + i
+        if s >= n:
+            continue
+        pred = {}
+        for t in range(n):
+            if t == s:
+                continue
+            best = None
+            for u in inarc[t]:
+                if D[i, u] + W[u, t] == D[i, t]:
+                    key = (D[i, u], u)
+                    best = key if best is None or key < best else best
+            pred[t] = best[1]
+        order = sorted(range(n), key=lambda t: D[i, t])
+        rr = np.full(n, -1.0)
+        rr[s] = 1.0
+        for t in order:
+            if t != s:
+                rr[t] = rr[pred[t]] * Rm[pred[t], t]
+        rel[i, :n] = rr
+    # mirror exchange: q sends rel[q rows][r cols] to r > q; r stores the transpose (s > t)
+    for x in range(R):
+        for y in range(x + 1, R):
+            yb, ye = owners[y]
+            xb, xe = owners[x]
+            if rank == x:
+                dist.send(torch.from_numpy(np.ascontiguousarray(rel[:, yb:ye])), y)
+            elif rank == y:
+                buf = torch.zeros((xe - xb, ye - yb), dtype=torch.float64)
+                dist.recv(buf, x)
+                rel[:, xb:xe] = buf.numpy().T
+    for i in range(e - b):  # local diagonal block mirror + diagonal rule
+        s = b + i
+        if s >= n:
+            continue
+        for t in range(b, s):
+            rel[i, t] = rel[t - b, s]
+        cands = [((W[s, u] if u == s else 2 * W[s, u]), u) for u in range(n)]
+        lat_d, u = min(cands)
+        D[i, s] = lat_d
+        rel[i, s] = Rm[s, s] if u == s else Rm[s, u] * Rm[s, u]
+    q.put((rank, b, e, D[:, :n].copy(), rel[:, :n].copy(), Dfull[:n, :n].copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _sparse_worker(rank, R, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=R)
+    g = graphs.random_geometric(300, seed=3)
+    el = oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
+    n = g.n
+    per = (n + R - 1) // R
+    s0, s1 = rank * per, min(n, (rank + 1) * per)
+    rows = oracle.sssp_rows(el, s0, s1)  # stands in for this rank's GPU rows
+    lat = torch.zeros((per, n), dtype=torch.int64)
+    rel = torch.zeros((per, n), dtype=torch.float64)
+    lat[:s1 - s0] = torch.from_numpy(rows["lat_int"].astype(np.int64))
+    rel[:s1 - s0] = torch.from_numpy(rows["rel"])
+    lat_all = [torch.zeros_like(lat) for _ in range(R)]
+    rel_all = [torch.zeros_like(rel) for _ in range(R)]
+    dist.all_gather(lat_all, lat)  # ncclAllGather layout: rank-major row slices
+    dist.all_gather(rel_all, rel)
+    q.put((rank, torch.cat(lat_all)[:n].numpy(), torch.cat(rel_all)[:n].numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_dense_sharded_schedule_gloo(native):
+    n, seed, R = 200, 6, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dense_worker, args=(r, R, port, n, seed, q)) for r in range(R)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=500) for _ in range(R)])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    lat = np.concatenate([x[3] for x in res])[:n].astype(np.uint64) * np.uint64(1_000_000)
+    rel = np.concatenate([x[4] for x in res])[:n]
+    g = graphs.complete_graph(n, seed=seed)
+    exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss))
+    assert np.array_equal(lat, exp["lat_int"])
+    assert np.array_equal(rel, exp["rel"])
+
+
+@pytest.mark.timeout(300)
+def test_sparse_source_shard_allgather_gloo(native):
+    R = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sparse_worker, args=(r, R, port, q)) for r in range(R)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=250) for _ in range(R)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    g = graphs.random_geometric(300, seed=3)
+    el = oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
+    full = oracle.sssp_rows(el)
+    for _, lat, rel in res:
+        assert np.array_equal(lat.astype(np.uint64), full["lat_int"])
+        assert np.array_equal(rel, full["rel"])

@@ -1,0 +1,190 @@
+"""Host-side C layer (no GPU): units grammar, GML reader + validation rules, attach, ABI."""
+import ctypes
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+from shadow_amd import graphs
+from shadow_amd.topology import Topology, parse_bandwidth, parse_time_nanosec
+
+MS = 1_000_000
+
+
+# ---- units.rs grammar (units.rs:404-437, :583-722, :776-837) -----------------------------------
+def test_units_known_answers(native):
+    cases = json.load(open(os.path.join(GOLDEN, "units_cases.json")))
+    for s, want in cases["time_ns"]:
+        assert parse_time_nanosec(s) == want, repr(s)
+    for s, want in cases["bandwidth_bps"]:
+        assert parse_bandwidth(s) == want, repr(s)
+
+
+def test_units_whitespace_and_newline(native):
+    assert parse_time_nanosec("10\tms") == 10 * MS
+    assert parse_time_nanosec("10 ms") == 10 * MS  # Unicode \s (NBSP) between value and unit
+    assert parse_time_nanosec("10 m\ns") == -1           # '.' does not match '\n' in (.*)$
+
+
+# ---- GML reader + validation (topology.c:525-1038) --------------------------------------------
+BASE_NODE = 'node [ id {id} bandwidth_down "1 Gbit" bandwidth_up "1 Gbit" {extra} ]'
+BASE_EDGE = 'edge [ source {a} target {b} latency "{lat}" packet_loss {loss} {extra} ]'
+
+
+def gml(nodes, edges, directed=0, header=""):
+    body = "\n".join([BASE_NODE.format(id=i, extra=x) for i, x in nodes] +
+                     [BASE_EDGE.format(a=a, b=b, lat=l, loss=p, extra=x) for a, b, l, p, x in edges])
+    return f"graph [ directed {directed} {header}\n{body}\n]"
+
+
+def tri(**kw):
+    nodes = [(0, ""), (1, ""), (2, "")]
+    edges = [(0, 1, "5 ms", 0.1, ""), (1, 2, "5 ms", 0.2, ""), (0, 2, "10 ms", 0.3, "")]
+    return gml(nodes, edges, **kw)
+
+
+def test_parse_accepts_reference_fixtures(native):
+    for c in json.load(open(os.path.join(GOLDEN, "known_answers.json"))):
+        t = Topology.from_gml(c["gml"])
+        assert t.n == 1 and t.m == 1
+    t = Topology.from_gml(open(os.path.join(GOLDEN, "c1.gml")).read())
+    n, directed, src, dst, lat, loss = t.edges()
+    g = graphs.complete_graph(50, seed=1)
+    assert n == 50 and not directed
+    assert np.array_equal(src, g.src) and np.array_equal(dst, g.dst)
+    assert np.array_equal(lat, g.lat_ns) and np.array_equal(loss, g.loss)
+    assert t.complete
+
+
+@pytest.mark.parametrize("text,ok,why", [
+    (tri(), True, "plain triangle"),
+    (gml([(0, ""), (1, "")], [(0, 1, "1 ms", 0.0, "")]), True, "two nodes"),
+    (gml([(0, ""), (1, "")], []), False, "disconnected (topology.c:707-713)"),
+    (gml([(0, ""), (1, "")], [(0, 1, "1 ms", 0.0, "")], directed=1), False,
+     "directed edge only one way: not strongly connected"),
+    (gml([(0, ""), (1, "")], [(0, 1, "0 ms", 0.0, "")]), False, "latency must be > 0 (:922)"),
+    (gml([(0, ""), (1, "")], [(0, 1, "1.5 ms", 0.0, "")]), False, "fractional value (units.rs)"),
+    (gml([(0, ""), (1, "")], [(0, 1, "1 ms", 1.5, "")]), False, "loss > 1 (:942)"),
+    (gml([(0, ""), (1, "")], [(0, 1, "1 ms", -0.1, "")]), False, "loss < 0"),
+    (gml([(0, ""), (1, "")], [(0, 1, "1 ms", 1.0, "")]), True, "loss == 1 allowed"),
+    (gml([(0, 'foo 1'), (1, "")], [(0, 1, "1 ms", 0.0, "")]), False, "unsupported vertex attr"),
+    (gml([(0, 'identifier 1'), (1, "")], [(0, 1, "1 ms", 0.0, "")]), True,
+     "prefix match of 'id' (topology.c:184-188)"),
+    (gml([(0, 'Label "x"'), (1, "")], [(0, 1, "1 ms", 0.0, "")]), True, "case-insensitive prefix"),
+    (gml([(0, 'ip_address 5'), (1, "")], [(0, 1, "1 ms", 0.0, "")]), False, "ip_address must be a string"),
+    (gml([(0, ""), (1, "")], [(0, 1, "1 ms", 0.0, 'jitter "2 ms"')]), True, "jitter ok"),
+    (gml([(0, ""), (1, "")], [(0, 1, "1 ms", 0.0, 'color "red"')]), False, "unsupported edge attr"),
+    (gml([(0, ""), (1, "")], [(0, 1, "1 ms", 0.0, 'graphics [ x 1 ]')]), True, "nested list skipped"),
+    ('graph [ node [ id 0 bandwidth_down "1 Gbit" bandwidth_up "1 Gbit" ] '
+     'edge [ source 0 target 0 latency 10 packet_loss 0.0 ] ]', False, "numeric latency"),
+    ('graph [ node [ id 0 bandwidth_down "1 Gbit" ] edge [ source 0 target 0 latency "1 ms" '
+     'packet_loss 0.0 ] ]', False, "missing bandwidth_up"),
+    ('graph [ node [ id 0 bandwidth_down "4 Kbit" bandwidth_up "1 Gbit" ] edge [ source 0 target 0 '
+     'latency "1 ms" packet_loss 0.0 ] ]', False, "bandwidth < 8 Kibit rounds to 0 KiB/s"),
+    ('graph [ node [ id 0 bandwidth_down "1 Gbit" bandwidth_up "1 Gbit" ] edge [ source 0 target 0 '
+     'latency "1 ms" ] ]', False, "missing packet_loss"),
+    ('graph [ node [ id 0 bandwidth_down "1 Gbit" bandwidth_up "1 Gbit" ] edge [ source 0 target 7 '
+     'latency "1 ms" packet_loss 0.0 ] ]', False, "unknown node id"),
+    ('# comment\nCreator "x"\ngraph [ node [ id 3 bandwidth_down "1 Gbit" bandwidth_up "1 Gbit" ] '
+     'edge [ source 3 target 3 latency "1 ms" packet_loss 0.0 ] ]', True, "comments, top-level keys"),
+])
+def test_validation_rules(native, text, ok, why):
+    t = Topology.try_from_gml(text)
+    assert (t is not None) == ok, why
+
+
+def test_complete_detection_and_direct_mode(native):
+    """_topology_isComplete (:409-511): self-loops required; !complete && !use_shortest_path
+    fails (:696-699)."""
+    g = graphs.complete_graph(6, seed=3)
+    assert Topology.from_gml(graphs.to_gml(g), use_shortest_path=False).complete
+    nose = graphs.Graph(g.n, False, g.src[g.src != g.dst], g.dst[g.src != g.dst],
+                        g.lat_ns[g.src != g.dst], g.loss[g.src != g.dst])
+    assert not Topology.from_gml(graphs.to_gml(nose)).complete
+    assert Topology.try_from_gml(graphs.to_gml(nose), use_shortest_path=False) is None
+
+
+def test_topology_new_from_file(native, tmp_path):
+    p = tmp_path / "g.gml"
+    p.write_text(tri())
+    t = Topology.new(str(p))
+    assert t.n == 3 and t.m == 3 and not t.directed
+    with pytest.raises(ValueError):
+        Topology.new(str(tmp_path / "missing.gml"))
+
+
+# ---- attach (topology.c:2024-2281) ---------------------------------------------------------
+def test_attach_matches_restatement(native):
+    fx = json.load(open(os.path.join(GOLDEN, "attach_cases.json")))
+    top = Topology.from_gml(fx["gml"])
+    for i, c in enumerate(fx["cases"]):
+        v, down, up, after = top.attach(f"100.64.{i // 250}.{i % 250 + 1}", c["seed_before"],
+                                        c["ip_hint"], c["city_hint"], c["country_hint"])
+        assert v == c["vertex"], c
+        assert after == c["seed_after"], c
+        assert down == fx["bw_down_kib"] and up == fx["bw_up_kib"]
+
+
+def test_attach_detach_lookup(native):
+    top = Topology.from_gml(tri())
+    v, _, _, _ = top.attach("11.0.0.9", 1, None, None, None)
+    assert top.vertex_of("11.0.0.9") == v
+    top.detach("11.0.0.9")
+    assert top.vertex_of("11.0.0.9") == -1
+    # unattached endpoints: -1, not routable (topology.c:1905-1915, :2019-2022); no build needed
+    assert top.get_latency("11.0.0.9", "11.0.0.10") == -1
+    assert not top.is_routable("11.0.0.9", "11.0.0.10")
+
+
+# ---- C-ABI exports ---------------------------------------------------------------------------
+def _declared(header):
+    text = open(os.path.join(ROOT, "include", header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return set(re.findall(r"\b([a-z_][a-zA-Z0-9_]*)\s*\(", text)) - {"if", "sizeof"}
+
+
+def test_library_exports_every_declared_symbol(native):
+    from shadow_amd import _lib
+    names = {n for n in _declared("shadow_routing.h") | _declared("topology.h")
+             if n.startswith(("srt_", "topology_"))}
+    assert len(names) > 40
+    for n in sorted(names):
+        assert hasattr(native, n), f"{n} declared in include/ but not exported"
+        assert n in _lib.SIGNATURES, f"{n} missing from the ctypes signature table"
+
+
+def test_version_and_device_count_without_gpu(native):
+    assert b"gfx950" in native.srt_version()
+    assert native.srt_device_count() >= 0
+
+
+def test_shard_rows_partition(native):
+    for n, align, R in [(32768, 128, 8), (1024, 128, 3), (1000, 64, 7), (130, 128, 4)]:
+        got = []
+        for r in range(R):
+            b, e = ctypes.c_int32(), ctypes.c_int32()
+            native.srt_shard_rows(n, align, R, r, ctypes.byref(b), ctypes.byref(e))
+            got.append((b.value, e.value))
+            assert b.value % align == 0 and e.value % align == 0
+        assert got[0][0] == 0 and got[-1][1] >= n and got[-1][1] < n + align
+        for (b0, e0), (b1, e1) in zip(got, got[1:]):
+            assert e0 == b1
+
+
+def test_range_check(native):
+    """Latencies beyond the u32 quantum range fail loudly (SRT_E_RANGE), never silently."""
+    from shadow_amd._lib import Edges
+    src = np.array([0], np.int32)
+    dst = np.array([1], np.int32)
+    lat = np.array([2**40], np.int64)
+    loss = np.array([0.0])
+    e = Edges(2, 0, 1, src.ctypes.data, dst.ctypes.data, lat.ctypes.data, loss.ctypes.data)
+    q, mw = ctypes.c_uint64(), ctypes.c_uint32()
+    assert native.srt_latency_quantum(ctypes.byref(e), ctypes.byref(q), ctypes.byref(mw)) == 0
+    lat2 = np.array([3, 2**40], np.int64)
+    src2, dst2 = np.array([0, 0], np.int32), np.array([1, 1], np.int32)
+    e2 = Edges(2, 0, 2, src2.ctypes.data, dst2.ctypes.data, lat2.ctypes.data, np.zeros(2).ctypes.data)
+    assert native.srt_latency_quantum(ctypes.byref(e2), ctypes.byref(q), ctypes.byref(mw)) == -6
