@@ -1,11 +1,17 @@
 /*
- * fw16.hip -- packed-u16 blocked Floyd-Warshall for gfx950.
+ * fw16.hip -- packed 15-bit blocked Floyd-Warshall for gfx950.
  *
- * Distances are held as u16 quanta with saturating adds (v_pk_add_u16 ... clamp): two
- * relaxations per VALU instruction (v_pk_add_u16 + v_pk_min_u16 per pair) and half the HBM / LDS
- * / xGMI bytes of the u32 path. Saturation is exact: sat(sat(a)+b) = sat(a+b) and min commutes
- * with sat, so the result is min(D, 0xFFFF) element-wise. If any real pair saturates the build
- * reports inexact and the caller reruns the u32 kernels -- the table is never approximate.
+ * Distances are held as u16 quanta capped at INF15 = 0x7FFF, two per 32-bit register. Because
+ * both halves are <= 0x7FFF, one plain v_add_u32 adds the two pairs without a carry crossing
+ * the half boundary (sums <= 0xFFFE), and v_pk_min_u16 keeps the minimum per half: two
+ * relaxations cost one v_add_u32 (~2.4 cycles per wave64 instruction on gfx950, measured by
+ * tools/valu_rate.hip) plus one v_pk_min_u16 (~4.2), against ~4.2 + 4.2 for
+ * v_pk_add_u16 + v_pk_min_u16 and ~2.4 + 4.1 per single relaxation for u32 add + min.
+ * Every stored value is min(candidate, previous) <= 0x7FFF, so the result is min(D, 0x7FFF)
+ * element-wise: exact wherever D < 0x7FFF. If any real pair reaches the cap the build reports
+ * inexact and the caller reruns the u32 kernels -- the table is never approximate.
+ * The A operand is staged pre-splatted, (a, a) per 32-bit LDS word, so the add needs no
+ * per-half operand select.
  *
  * Kernels (pivot block KB = 64 rows/cols per round):
  *   fw16_diag    closure of the 64x64 diagonal tile in LDS (64 dependent steps)
@@ -20,51 +26,59 @@ typedef unsigned short u16;
 typedef u16 u16x2 __attribute__((ext_vector_type(2)));
 
 #define KB 64
-#define INF16 0xFFFFu
+#define INF16 0x7FFFu  /* cap of the packed 15-bit distances */
 #define LDA16 (KB + 8) /* u16 stride of an A row in LDS: 144 B, 16-byte aligned */
+#define UKC 32          /* pivots per LDS stage in the update kernel (two stages per launch) */
 
 static __device__ __forceinline__ u16x2 as2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
 static __device__ __forceinline__ uint32_t as32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
-static __device__ __forceinline__ u16x2 relax(u16x2 acc, u16x2 a, u16x2 b) {
-    return __builtin_elementwise_min(acc, __builtin_elementwise_add_sat(a, b));
+/* a, b halves <= 0x7FFF: the 32-bit add is two independent 16-bit adds */
+static __device__ __forceinline__ u16x2 relax(u16x2 acc, uint32_t a2, uint32_t b2) {
+    return __builtin_elementwise_min(acc, as2(a2 + b2));
 }
+static __device__ __forceinline__ uint32_t splat(uint32_t h) { return h | (h << 16); }
 
 /* ---- staging ------------------------------------------------------------------------------ */
-template <int TM>
-__device__ __forceinline__ void stage_A(u16* __restrict__ sA, const u16* __restrict__ g, size_t ldg,
-                                        int tid) {
-    for (int idx = tid; idx < TM * 8; idx += 256) { /* TM rows x 64 u16 = 8 uint4 per row */
-        const int row = idx >> 3, c8 = (idx & 7) * 8;
-        *reinterpret_cast<uint4*>(sA + row * LDA16 + c8) =
-            *reinterpret_cast<const uint4*>(g + (size_t)row * ldg + c8);
+/* A (TM rows x KC pivots) into LDS as (a, a) words: row r, pivot m at sA[r * (KC + 4) + m]
+ * (row stride 16-byte aligned, offset by 4 banks per row) */
+template <int TM, int KC>
+__device__ __forceinline__ void stage_A(uint32_t* __restrict__ sA, const u16* __restrict__ g,
+                                        size_t ldg, int tid) {
+    constexpr int PER = KC / 8; /* uint4 per row */
+    for (int idx = tid; idx < TM * PER; idx += 256) {
+        const int row = idx / PER, c8 = (idx % PER) * 8;
+        const uint4 v = *reinterpret_cast<const uint4*>(g + (size_t)row * ldg + c8);
+        uint32_t* d = sA + row * (KC + 4) + c8;
+        *reinterpret_cast<uint4*>(d) = make_uint4(splat(v.x & 0xFFFFu), splat(v.x >> 16),
+                                                  splat(v.y & 0xFFFFu), splat(v.y >> 16));
+        *reinterpret_cast<uint4*>(d + 4) = make_uint4(splat(v.z & 0xFFFFu), splat(v.z >> 16),
+                                                      splat(v.w & 0xFFFFu), splat(v.w >> 16));
     }
 }
 
-template <int TN>
+/* B (KC pivot rows x TN columns) into LDS as packed u16 pairs */
+template <int TN, int KC>
 __device__ __forceinline__ void stage_B(u16* __restrict__ sB, const u16* __restrict__ g, size_t ldg,
                                         int tid) {
     constexpr int LDB = TN + 8;
     constexpr int PER = TN / 8;
-    for (int idx = tid; idx < KB * PER; idx += 256) {
+    for (int idx = tid; idx < KC * PER; idx += 256) {
         const int row = idx / PER, c8 = (idx % PER) * 8;
         *reinterpret_cast<uint4*>(sB + row * LDB + c8) =
             *reinterpret_cast<const uint4*>(g + (size_t)row * ldg + c8);
     }
 }
 
-/* ---- register-blocked min-plus over the 64 pivots ------------------------------------------ */
-template <int TN, int RM, int RN>
-__device__ __forceinline__ void mp16(u16x2 (&acc)[RM][RN / 2], const u16* __restrict__ sA,
+/* ---- register-blocked min-plus over KC staged pivots ---------------------------------------- */
+template <int TN, int RM, int RN, int KC>
+__device__ __forceinline__ void mp16(u16x2 (&acc)[RM][RN / 2], const uint32_t* __restrict__ sA,
                                      const u16* __restrict__ sB, int tx, int ty) {
-    constexpr int LDB = TN + 8;
-    const u16* pa = sA + ty * RM * LDA16;
+    constexpr int LDB = TN + 8, LDA = KC + 4;
+    const uint32_t* pa = sA + ty * RM * LDA;
     const u16* pb = sB + tx * RN;
 #pragma unroll 1
-    for (int m = 0; m < KB; m += 4) {
-        uint2 av[RM];
-#pragma unroll
-        for (int r = 0; r < RM; ++r) av[r] = *reinterpret_cast<const uint2*>(pa + r * LDA16 + m);
-        uint32_t bv[4][RN / 2];
+    for (int m = 0; m < KC; m += 4) {
+        uint32_t bv[4][RN / 2]; /* packed B pairs of pivots m..m+3 */
 #pragma unroll
         for (int mm = 0; mm < 4; ++mm) {
             if constexpr (RN == 8) {
@@ -79,15 +93,37 @@ __device__ __forceinline__ void mp16(u16x2 (&acc)[RM][RN / 2], const u16* __rest
                 bv[mm][1] = v.y;
             }
         }
+        /* rows in groups of four: (a, a) words of pivots m..m+3, one b128 read per row */
 #pragma unroll
-        for (int mm = 0; mm < 4; ++mm)
+        for (int rg = 0; rg < RM; rg += 4) {
+            uint4 av[4];
 #pragma unroll
-            for (int r = 0; r < RM; ++r) {
-                const u16x2 a = as2(mm < 2 ? av[r].x : av[r].y);
-                const u16x2 as = (mm & 1) ? a.yy : a.xx;
+            for (int r = 0; r < 4; ++r)
+                av[r] = *reinterpret_cast<const uint4*>(pa + (rg + r) * LDA + m);
 #pragma unroll
-                for (int c = 0; c < RN / 2; ++c) acc[r][c] = relax(acc[r][c], as, as2(bv[mm][c]));
-            }
+            for (int mm = 0; mm < 4; ++mm)
+#pragma unroll
+                for (int r = 0; r < 4; r += 2) {
+                    /* two rows at a time: RN independent adds, then RN mins, so every min is
+                     * several instructions behind the add it consumes */
+                    const uint32_t s0 = mm == 0 ? av[r].x : mm == 1 ? av[r].y : mm == 2 ? av[r].z : av[r].w;
+                    const uint32_t s1 = mm == 0   ? av[r + 1].x
+                                        : mm == 1 ? av[r + 1].y
+                                        : mm == 2 ? av[r + 1].z
+                                                  : av[r + 1].w;
+                    uint32_t t[2][RN / 2];
+#pragma unroll
+                    for (int c = 0; c < RN / 2; ++c) {
+                        t[0][c] = s0 + bv[mm][c];
+                        t[1][c] = s1 + bv[mm][c];
+                    }
+#pragma unroll
+                    for (int c = 0; c < RN / 2; ++c) {
+                        acc[rg + r][c] = __builtin_elementwise_min(acc[rg + r][c], as2(t[0][c]));
+                        acc[rg + r + 1][c] = __builtin_elementwise_min(acc[rg + r + 1][c], as2(t[1][c]));
+                    }
+                }
+        }
     }
 }
 
@@ -131,20 +167,6 @@ __device__ __forceinline__ void store_acc16(const u16x2 (&acc)[RM][RN / 2],
     }
 }
 
-/* old[] must already hold the tile (loaded before the LDS staging so its HBM latency overlaps) */
-template <int TM, int TN, int RM, int RN>
-__device__ __forceinline__ void tile_product(u16* __restrict__ C, size_t ldc,
-                                             const u16* __restrict__ sA, const u16* __restrict__ sB,
-                                             int tx, int ty, const u16x2 (&old)[RM][RN / 2]) {
-    u16x2 acc[RM][RN / 2];
-#pragma unroll
-    for (int r = 0; r < RM; ++r)
-#pragma unroll
-        for (int c = 0; c < RN / 2; ++c) acc[r][c] = old[r][c];
-    mp16<TN, RM, RN>(acc, sA, sB, tx, ty);
-    store_acc16<RM, RN>(acc, old, C, ldc, tx, ty);
-}
-
 /* ---- kernels --------------------------------------------------------------------------------- */
 __global__ void fw16_init_kernel(int n, int ld, int row0, const uint32_t* __restrict__ w,
                                  u16* __restrict__ d) {
@@ -170,12 +192,11 @@ __global__ __launch_bounds__(256) void fw16_diag_kernel(u16* __restrict__ P, int
         const uint2 bm = *reinterpret_cast<const uint2*>(s + m * LDA16 + 4 * tx);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const u16 a = s[(4 * ty + r) * LDA16 + m];
-            const u16x2 as = {a, a};
+            const uint32_t as = splat(s[(4 * ty + r) * LDA16 + m]);
             uint2* row = reinterpret_cast<uint2*>(s + (4 * ty + r) * LDA16 + 4 * tx);
             uint2 v = *row;
-            v.x = as32(relax(as2(v.x), as, as2(bm.x)));
-            v.y = as32(relax(as2(v.y), as, as2(bm.y)));
+            v.x = as32(relax(as2(v.x), as, bm.x));
+            v.y = as32(relax(as2(v.y), as, bm.y));
             *row = v;
         }
         __syncthreads();
@@ -191,7 +212,7 @@ __global__ __launch_bounds__(256) void fw16_diag_kernel(u16* __restrict__ P, int
 __global__ __launch_bounds__(256) void fw16_panel_kernel(u16* __restrict__ D, int ld, int row0,
                                                          int nrow_tiles, u16* __restrict__ P, int k0,
                                                          int ncol_tiles, int do_row, int do_col) {
-    __shared__ __attribute__((aligned(16))) u16 sA[KB * LDA16];
+    __shared__ __attribute__((aligned(16))) uint32_t sA[KB * (KB + 4)];
     __shared__ __attribute__((aligned(16))) u16 sB[KB * (KB + 8)];
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     int bid = blockIdx.x;
@@ -199,27 +220,32 @@ __global__ __launch_bounds__(256) void fw16_panel_kernel(u16* __restrict__ D, in
     if (bid < ncol_tiles) {
         if (!do_row || bid * KB == k0) return;
         C = P + bid * KB;
-        stage_A<KB>(sA, P + k0, ld, tid);
-        stage_B<KB>(sB, C, ld, tid);
+        stage_A<KB, KB>(sA, P + k0, ld, tid);
+        stage_B<KB, KB>(sB, C, ld, tid);
     } else {
         bid -= ncol_tiles;
         if (!do_col || bid >= nrow_tiles || row0 + bid * KB == k0) return;
         C = D + (size_t)bid * KB * ld + k0;
-        stage_A<KB>(sA, C, ld, tid);
-        stage_B<KB>(sB, P + k0, ld, tid);
+        stage_A<KB, KB>(sA, C, ld, tid);
+        stage_B<KB, KB>(sB, P + k0, ld, tid);
     }
-    u16x2 old[4][2];
+    u16x2 old[4][2], acc[4][2];
     load_acc16<4, 4>(old, C, ld, tx, ty);
     __syncthreads();
-    tile_product<KB, KB, 4, 4>(C, ld, sA, sB, tx, ty, old);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) acc[r][c] = old[r][c];
+    mp16<KB, 4, 4, KB>(acc, sA, sB, tx, ty);
+    store_acc16<4, 4>(acc, old, C, ld, tx, ty);
 }
 
 /* every 128x128 tile of the local rows: D_IJ <- min(D_IJ, D_I,k (x) P_k,J) */
-__global__ __launch_bounds__(256) void fw16_update_kernel(u16* __restrict__ D, int ld,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void fw16_update_kernel(u16* __restrict__ D, int ld,
                                                           const u16* __restrict__ P, int k0,
                                                           int ncol_tiles) {
-    __shared__ __attribute__((aligned(16))) u16 sA[128 * LDA16];
-    __shared__ __attribute__((aligned(16))) u16 sB[KB * (128 + 8)];
+    __shared__ __attribute__((aligned(16))) uint32_t sA[128 * (UKC + 4)];
+    __shared__ __attribute__((aligned(16))) u16 sB[UKC * (128 + 8)];
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     /* XCD-aware order: consecutive blocks land on different XCDs; give each XCD a contiguous run
      * of tiles in a row band so its L2 keeps the band's A slice and the panel columns. */
@@ -228,12 +254,24 @@ __global__ __launch_bounds__(256) void fw16_update_kernel(u16* __restrict__ D, i
     const int bid = (nb & 7) == 0 ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
     const int I = bid / ncol_tiles, J = bid % ncol_tiles;
     u16* C = D + (size_t)I * 128 * ld + J * 128;
-    u16x2 old[8][4];
+    u16x2 old[8][4], acc[8][4];
     load_acc16<8, 8>(old, C, ld, tx, ty); /* HBM reads in flight during the staging */
-    stage_A<128>(sA, D + (size_t)I * 128 * ld + k0, ld, tid);
-    stage_B<128>(sB, P + J * 128, ld, tid);
-    __syncthreads();
-    tile_product<128, 128, 8, 8>(C, ld, sA, sB, tx, ty, old);
+#pragma unroll
+    for (int h = 0; h < KB; h += UKC) {
+        /* two 32-pivot stages keep LDS at 27 KB per block (4 blocks per CU) */
+        if (h) __syncthreads();
+        stage_A<128, UKC>(sA, D + (size_t)I * 128 * ld + k0 + h, ld, tid);
+        stage_B<128, UKC>(sB, P + (size_t)h * ld + J * 128, ld, tid);
+        __syncthreads();
+        if (!h) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) acc[r][c] = old[r][c];
+        }
+        mp16<128, 8, 8, UKC>(acc, sA, sB, tx, ty);
+    }
+    store_acc16<8, 8>(acc, old, C, ld, tx, ty);
 }
 
 /* widen to the u32 table and flag saturation of a real pair (i, j < n) */
@@ -249,6 +287,7 @@ __global__ void fw16_finish_kernel(int n, int ld, int row0, const u16* __restric
     if (real && v == INF16) atomicOr(saturated, 1);
 }
 
+#ifndef SRT_FW16_DEVICE_ONLY
 /* ---- orchestration --------------------------------------------------------------------------- */
 int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,
                    hipStream_t st, evpool_t* evp, srt_owner_fn owner_of, srt_panel_bcast_fn bcast,
@@ -314,3 +353,4 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
     *exact = sat ? 0 : 1;
     return SRT_OK;
 }
+#endif /* SRT_FW16_DEVICE_ONLY */
