@@ -103,8 +103,12 @@ int srt_gen_complete_device(int32_t n, int32_t ld, int32_t row0, int32_t nrows, 
 
 /* ---- device-resident sparse build (CSR of canonical arcs, self-loops excluded) ----------
  * Computes rows [src_begin, src_end) (row r of lat_rows/rel_rows = source src_begin + r, row
- * stride n) with one workgroup per source and the distance row resident in LDS
- * (n <= srt_sparse_max_n()). delta = bucket width in quanta (0 = default). */
+ * stride n) with one workgroup per source. The per-source working set (distance row, frontier
+ * queue, bitmaps: ~8n + n/8 bytes) is LDS-resident for n <= srt_sparse_max_n() and lives in a
+ * per-workgroup HBM slot beyond (persistent grid of 2 workgroups per CU; environment variable
+ * SRT_SPARSE_WORKSET=hbm forces the HBM form for testing). delta = bucket width in quanta
+ * (0 = default). The undirected symmetry rule is NOT applied here: after the rows of every
+ * source are assembled, call srt_mirror_lower_device. */
 int srt_sparse_max_n(void);
 int srt_sparse_build_device(int32_t n, int32_t directed, const int32_t* rowptr,
                             const int32_t* col, const uint32_t* w, const double* r,
@@ -113,6 +117,17 @@ int srt_sparse_build_device(int32_t n, int32_t directed, const int32_t* rowptr,
                             const double* self_r, int32_t src_begin, int32_t src_end,
                             uint32_t delta, uint32_t* lat_rows, double* rel_rows, void* stream,
                             srt_build_stats* stats);
+/* Canonical CSR built on the host from an edge list and uploaded once to `device`; rows of any
+ * source range can then be computed on that device (one shard per rank in a sharded build).
+ * Replaces the per-source igraph Dijkstra of topology.c:1578-1814 (_topology_computeSourcePaths). */
+typedef struct srt_sparse_graph srt_sparse_graph;
+int srt_sparse_graph_new(const srt_edges* g, int32_t device, srt_sparse_graph** out);
+int srt_sparse_graph_info(const srt_sparse_graph* g, int32_t* n, int32_t* directed, int64_t* arcs,
+                          uint64_t* quantum_ns);
+int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src_end,
+                          uint32_t* lat_rows, double* rel_rows, void* stream,
+                          srt_build_stats* stats);
+void srt_sparse_graph_free(srt_sparse_graph* g);
 /* rel[s][t] <- rel[t][s] for s > t (undirected symmetry rule), ld x ld device matrix. */
 int srt_mirror_lower_device(int32_t n, int32_t ld, double* rel, void* stream);
 

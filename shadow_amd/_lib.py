@@ -79,6 +79,10 @@ SIGNATURES = {
     "srt_sparse_build_device": (ctypes.c_int, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
                                                _VP, _VP, _I32, _I32, _U32, _VP, _VP, _VP, _VP]),
     "srt_mirror_lower_device": (ctypes.c_int, [_I32, _I32, _VP, _VP]),
+    "srt_sparse_graph_new": (ctypes.c_int, [_VP, _I32, _VP]),
+    "srt_sparse_graph_info": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
+    "srt_sparse_graph_rows": (ctypes.c_int, [_VP, _I32, _I32, _VP, _VP, _VP, _VP]),
+    "srt_sparse_graph_free": (None, [_VP]),
     "srt_comm_unique_id": (ctypes.c_int, [_VP]),
     "srt_comm_init": (ctypes.c_int, [_VP, _I32, _I32, _I32, _VP]),
     "srt_comm_free": (None, [_VP]),

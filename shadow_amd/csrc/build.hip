@@ -104,6 +104,128 @@ static int choose_algo(const srt_canon* c, const srt_build_opts* o) {
     return SRT_ALGO_SPARSE_SSSP;
 }
 
+/* ---- device-resident sparse graph (canonical CSR uploaded once, rows computed per shard) ---- */
+struct srt_sparse_graph {
+    int device;
+    int32_t n, directed;
+    int64_t arcs;
+    uint64_t quantum_ns;
+    uint32_t delta;
+    int32_t *rp, *col, *irp, *icol;
+    uint32_t *w, *iw, *sw;
+    double *r, *ir, *sr;
+};
+
+static int up(void** d, const void* h, size_t bytes) {
+    *d = NULL;
+    if (hipMalloc(d, bytes ? bytes : 4) != hipSuccess) {
+        (void)hipGetLastError();
+        srt_set_error("hipMalloc of %zu bytes failed", bytes);
+        return SRT_E_NOMEM;
+    }
+    if (bytes && hipMemcpy(*d, h, bytes, hipMemcpyHostToDevice) != hipSuccess) {
+        srt_set_error("hipMemcpy of %zu bytes failed", bytes);
+        return SRT_E_DEVICE;
+    }
+    return SRT_OK;
+}
+
+extern "C" void srt_sparse_graph_free(srt_sparse_graph* g) {
+    if (!g) return;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(g->device);
+    void* ps[] = {g->rp, g->col, g->w, g->r, g->sw, g->sr};
+    for (void* p : ps)
+        if (p) (void)hipFree(p);
+    if (g->directed) {
+        void* qs[] = {g->irp, g->icol, g->iw, g->ir};
+        for (void* p : qs)
+            if (p) (void)hipFree(p);
+    }
+    (void)hipSetDevice(prev);
+    free(g);
+}
+
+static int sparse_graph_from_canon(const srt_canon* c, int device, srt_sparse_graph** out) {
+    *out = NULL;
+    srt_sparse_graph* g = (srt_sparse_graph*)calloc(1, sizeof(srt_sparse_graph));
+    if (!g) return SRT_E_NOMEM;
+    g->device = device;
+    g->n = c->n;
+    g->directed = c->directed;
+    g->arcs = c->arcs;
+    g->quantum_ns = c->quantum_ns;
+    /* bucket width of the label-correcting loop: the mean arc weight */
+    double sumw = 0;
+    for (int64_t k = 0; k < c->arcs; k++) sumw += c->w[k];
+    g->delta = c->arcs > 0 ? (uint32_t)(sumw / (double)c->arcs + 0.5) : 1u;
+    if (g->delta < 1) g->delta = 1;
+    int rc = hipSetDevice(device) == hipSuccess ? SRT_OK : SRT_E_DEVICE;
+    const size_t n1 = (size_t)(c->n + 1), na = (size_t)c->arcs, nv = (size_t)c->n;
+    if (!rc) rc = up((void**)&g->rp, c->rowptr, n1 * 4);
+    if (!rc) rc = up((void**)&g->col, c->col, na * 4);
+    if (!rc) rc = up((void**)&g->w, c->w, na * 4);
+    if (!rc) rc = up((void**)&g->r, c->r, na * 8);
+    if (!rc) rc = up((void**)&g->sw, c->self_w, nv * 4);
+    if (!rc) rc = up((void**)&g->sr, c->self_r, nv * 8);
+    if (c->directed) {
+        if (!rc) rc = up((void**)&g->irp, c->in_rowptr, n1 * 4);
+        if (!rc) rc = up((void**)&g->icol, c->in_col, na * 4);
+        if (!rc) rc = up((void**)&g->iw, c->in_w, na * 4);
+        if (!rc) rc = up((void**)&g->ir, c->in_r, na * 8);
+    } else {
+        g->irp = g->rp;
+        g->icol = g->col;
+        g->iw = g->w;
+        g->ir = g->r;
+    }
+    if (rc) {
+        srt_sparse_graph_free(g);
+        return rc;
+    }
+    *out = g;
+    return SRT_OK;
+}
+
+extern "C" int srt_sparse_graph_new(const srt_edges* e, int32_t device, srt_sparse_graph** out) {
+    if (!e || !out) {
+        srt_set_error("srt_sparse_graph_new: null argument");
+        return SRT_E_ARG;
+    }
+    srt_canon c;
+    int rc = srt_canon_build(e, &c);
+    if (rc) return rc;
+    rc = sparse_graph_from_canon(&c, device, out);
+    srt_canon_free(&c);
+    return rc;
+}
+
+extern "C" int srt_sparse_graph_info(const srt_sparse_graph* g, int32_t* n, int32_t* directed,
+                                     int64_t* arcs, uint64_t* quantum_ns) {
+    if (!g) {
+        srt_set_error("srt_sparse_graph_info: null graph");
+        return SRT_E_ARG;
+    }
+    if (n) *n = g->n;
+    if (directed) *directed = g->directed;
+    if (arcs) *arcs = g->arcs;
+    if (quantum_ns) *quantum_ns = g->quantum_ns;
+    return SRT_OK;
+}
+
+extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src_end,
+                                     uint32_t* lat_rows, double* rel_rows, void* stream,
+                                     srt_build_stats* stats) {
+    if (!g) {
+        srt_set_error("srt_sparse_graph_rows: null graph");
+        return SRT_E_ARG;
+    }
+    return srt_sparse_build_device(g->n, g->directed, g->rp, g->col, g->w, g->r, g->irp, g->icol,
+                                   g->iw, g->ir, g->sw, g->sr, src_begin, src_end, g->delta,
+                                   lat_rows, rel_rows, stream, stats);
+}
+
 extern "C" int srt_build_tables(const srt_edges* g, const srt_build_opts* opts, uint32_t* lat_q,
                                 uint64_t* quantum_ns, double* rel, srt_build_stats* stats) {
     if (!g || !lat_q || !quantum_ns || !rel) {
@@ -179,47 +301,16 @@ extern "C" int srt_build_tables(const srt_edges* g, const srt_build_opts* opts, 
         }
     } else {
         const size_t nn = (size_t)n * n;
-        const int64_t arcs = c.arcs;
-        int32_t *d_rp, *d_col, *d_irp, *d_icol;
-        uint32_t *d_w, *d_iw, *d_sw, *d_lat;
-        double *d_r, *d_ir, *d_sr, *d_rel;
-        TRY(dalloc(&B, (void**)&d_rp, (size_t)(n + 1) * sizeof(int32_t)));
-        TRY(dalloc(&B, (void**)&d_col, (size_t)arcs * sizeof(int32_t)));
-        TRY(dalloc(&B, (void**)&d_w, (size_t)arcs * sizeof(uint32_t)));
-        TRY(dalloc(&B, (void**)&d_r, (size_t)arcs * sizeof(double)));
-        TRY(dalloc(&B, (void**)&d_sw, (size_t)n * sizeof(uint32_t)));
-        TRY(dalloc(&B, (void**)&d_sr, (size_t)n * sizeof(double)));
-        TRY(dalloc(&B, (void**)&d_lat, nn * sizeof(uint32_t)));
-        TRY(dalloc(&B, (void**)&d_rel, nn * sizeof(double)));
-        TRYHIP(hipMemcpyAsync(d_rp, c.rowptr, (size_t)(n + 1) * sizeof(int32_t), hipMemcpyHostToDevice, st));
-        TRYHIP(hipMemcpyAsync(d_col, c.col, (size_t)arcs * sizeof(int32_t), hipMemcpyHostToDevice, st));
-        TRYHIP(hipMemcpyAsync(d_w, c.w, (size_t)arcs * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-        TRYHIP(hipMemcpyAsync(d_r, c.r, (size_t)arcs * sizeof(double), hipMemcpyHostToDevice, st));
-        TRYHIP(hipMemcpyAsync(d_sw, c.self_w, (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-        TRYHIP(hipMemcpyAsync(d_sr, c.self_r, (size_t)n * sizeof(double), hipMemcpyHostToDevice, st));
-        if (c.directed) {
-            TRY(dalloc(&B, (void**)&d_irp, (size_t)(n + 1) * sizeof(int32_t)));
-            TRY(dalloc(&B, (void**)&d_icol, (size_t)arcs * sizeof(int32_t)));
-            TRY(dalloc(&B, (void**)&d_iw, (size_t)arcs * sizeof(uint32_t)));
-            TRY(dalloc(&B, (void**)&d_ir, (size_t)arcs * sizeof(double)));
-            TRYHIP(hipMemcpyAsync(d_irp, c.in_rowptr, (size_t)(n + 1) * sizeof(int32_t), hipMemcpyHostToDevice, st));
-            TRYHIP(hipMemcpyAsync(d_icol, c.in_col, (size_t)arcs * sizeof(int32_t), hipMemcpyHostToDevice, st));
-            TRYHIP(hipMemcpyAsync(d_iw, c.in_w, (size_t)arcs * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-            TRYHIP(hipMemcpyAsync(d_ir, c.in_r, (size_t)arcs * sizeof(double), hipMemcpyHostToDevice, st));
-        } else {
-            d_irp = d_rp;
-            d_icol = d_col;
-            d_iw = d_w;
-            d_ir = d_r;
-        }
-        /* bucket width: the mean arc weight */
-        double sumw = 0;
-        for (int64_t k = 0; k < arcs; k++) sumw += c.w[k];
-        uint32_t delta = arcs > 0 ? (uint32_t)(sumw / (double)arcs + 0.5) : 1u;
-        if (delta < 1) delta = 1;
-        TRY(srt_sparse_build_device(n, c.directed, d_rp, d_col, d_w, d_r, d_irp, d_icol, d_iw, d_ir,
-                                    d_sw, d_sr, 0, n, delta, d_lat, d_rel, st, &local));
-        if (!c.directed) TRY(srt_mirror_lower_device(n, n, d_rel, st));
+        srt_sparse_graph* sg = NULL;
+        uint32_t* d_lat;
+        double* d_rel;
+        TRY(sparse_graph_from_canon(&c, opts ? opts->device : 0, &sg));
+        rc = dalloc(&B, (void**)&d_lat, nn * sizeof(uint32_t));
+        if (!rc) rc = dalloc(&B, (void**)&d_rel, nn * sizeof(double));
+        if (!rc) rc = srt_sparse_graph_rows(sg, 0, n, d_lat, d_rel, st, &local);
+        if (!rc && !c.directed) rc = srt_mirror_lower_device(n, n, d_rel, st);
+        srt_sparse_graph_free(sg);
+        if (rc) goto out;
         TRYHIP(hipMemcpyAsync(lat_q, d_lat, nn * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         TRYHIP(hipMemcpyAsync(rel, d_rel, nn * sizeof(double), hipMemcpyDeviceToHost, st));
         TRYHIP(hipStreamSynchronize(st));

@@ -14,10 +14,19 @@
  * (children of v are found among v's out-arcs), i.e. the product is formed in exactly the order
  * /root/reference/src/main/routing/topology.c:1342-1366 forms it.
  *
- * LDS layout (bytes): [A: 4n] dist during SSSP/pred, two frontier bitmaps during the tree walk;
- * [Bq: 4n] near queue during SSSP, predecessor arc index afterwards; [C: n/8] improved bitmap.
+ * Working-set layout (bytes): [A: 4n] dist during SSSP/pred, two frontier bitmaps during the tree
+ * walk; [Bq: 4n] near queue during SSSP, predecessor arc index afterwards; [C: n/8] improved
+ * bitmap. For n <= srt_sparse_max_n() (~20k) it is LDS (one workgroup per CU); beyond that the
+ * same layout lives in a per-workgroup slot of an HBM workspace and the grid is persistent
+ * (2 workgroups per CU, each looping over sources), with every relaxation an L2 atomic. All
+ * threads of a workgroup share one CU and its L1, so workgroup barriers order the slot's
+ * global-memory traffic exactly as they order LDS.
  */
 #include "srt_device.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 #define SP_THREADS 1024
 #define SP_WAVES (SP_THREADS / 64)
@@ -33,25 +42,30 @@ static __device__ __forceinline__ int wave_excl_scan(int v, int lane, int* total
     return x - v;
 }
 
-__global__ __launch_bounds__(SP_THREADS) void sssp_lds_kernel(
-    int n, int src_begin, uint32_t delta, const int32_t* __restrict__ rowptr,
+template <bool G>
+__global__ __launch_bounds__(SP_THREADS) void sssp_kernel(
+    int n, int src_begin, int nsrc, uint32_t delta, const int32_t* __restrict__ rowptr,
     const int32_t* __restrict__ col, const uint32_t* __restrict__ w,
     const int32_t* __restrict__ in_rowptr, const int32_t* __restrict__ in_col,
     const uint32_t* __restrict__ in_w, const double* __restrict__ in_r, uint32_t* __restrict__ lat,
-    double* __restrict__ rel, size_t ldo, int32_t* __restrict__ max_depth) {
+    double* __restrict__ rel, size_t ldo, int32_t* __restrict__ max_depth, uint32_t* ws,
+    size_t slot_words) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const int s = src_begin + blockIdx.x;
     const int nwords = (n + 31) >> 5;
     const int a_words = n > 2 * nwords ? n : 2 * nwords;
-    uint32_t* dist = smem;                                     /* region A */
-    uint32_t* queue = smem + a_words;                          /* region B */
-    int32_t* arc = reinterpret_cast<int32_t*>(smem + a_words); /* region B after SSSP */
-    uint32_t* bits = smem + a_words + n;                       /* region C */
+    uint32_t* base = G ? ws + (size_t)blockIdx.x * slot_words : smem;
+    uint32_t* dist = base;                                     /* region A */
+    uint32_t* queue = base + a_words;                          /* region B */
+    int32_t* arc = reinterpret_cast<int32_t*>(base + a_words); /* region B after SSSP */
+    uint32_t* bits = base + a_words + n;                       /* region C */
     __shared__ int s_qlen;
     __shared__ uint32_t s_minfar;
     __shared__ int s_any;
     const int tid = threadIdx.x, lane = tid & 63;
-
+    int depth = 0;
+  for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
+    const int s = src_begin + si;
+    __syncthreads(); /* the previous source's walk is done with the working set */
     for (int v = tid; v < n; v += SP_THREADS) dist[v] = SRT_INF;
     for (int q = tid; q < nwords; q += SP_THREADS) bits[q] = 0;
     __syncthreads();
@@ -125,7 +139,7 @@ __global__ __launch_bounds__(SP_THREADS) void sssp_lds_kernel(
     }
     __syncthreads();
     /* latency row + canonical predecessor arc of every target */
-    uint32_t* latrow = lat + (size_t)blockIdx.x * ldo;
+    uint32_t* latrow = lat + (size_t)si * ldo;
     for (int t = tid; t < n; t += SP_THREADS) {
         const uint32_t dt = dist[t];
         latrow[t] = (t == s) ? 0u : dt;
@@ -149,15 +163,15 @@ __global__ __launch_bounds__(SP_THREADS) void sssp_lds_kernel(
     }
     __syncthreads();
     /* breadth-first walk down the predecessor tree; frontier bitmaps reuse region A */
-    uint32_t* cur = smem;
-    uint32_t* nxt = smem + nwords;
-    double* relrow = rel + (size_t)blockIdx.x * ldo;
+    uint32_t* cur = base;
+    uint32_t* nxt = base + nwords;
+    double* relrow = rel + (size_t)si * ldo;
     for (int t = tid; t < n; t += SP_THREADS) relrow[t] = (t == s) ? 1.0 : 0.0;
-    for (int q = tid; q < 2 * nwords; q += SP_THREADS) smem[q] = 0u;
+    for (int q = tid; q < 2 * nwords; q += SP_THREADS) base[q] = 0u;
     __syncthreads();
     if (tid == 0) cur[s >> 5] = 1u << (s & 31);
     __syncthreads();
-    int depth = 0;
+    int sdepth = 0;
     for (;;) {
         if (tid == 0) s_any = 0;
         __syncthreads();
@@ -188,12 +202,14 @@ __global__ __launch_bounds__(SP_THREADS) void sssp_lds_kernel(
         if (any) s_any = 1;
         __syncthreads();
         if (!s_any) break;
-        ++depth;
+        ++sdepth;
         uint32_t* t = cur;
         cur = nxt;
         nxt = t;
         __syncthreads();
     }
+    depth = max(depth, sdepth);
+  }
     if (tid == 0) atomicMax(max_depth, depth);
 }
 
@@ -258,11 +274,6 @@ extern "C" int srt_sparse_build_device(int32_t n, int32_t directed, const int32_
         srt_set_error("srt_sparse_build_device: bad arguments");
         return SRT_E_ARG;
     }
-    if (n > srt_sparse_max_n()) {
-        srt_set_error("srt_sparse_build_device: n = %d exceeds the LDS-resident limit %d", n,
-                      srt_sparse_max_n());
-        return SRT_E_ARG;
-    }
     hipStream_t st = (hipStream_t)stream;
     int32_t* depth = NULL;
     SRT_HIPCHK(hipMalloc(&depth, sizeof(int32_t)));
@@ -271,14 +282,39 @@ extern "C" int srt_sparse_build_device(int32_t n, int32_t directed, const int32_
     SRT_HIPCHK(hipEventCreate(&e0));
     SRT_HIPCHK(hipEventCreate(&e1));
     SRT_HIPCHK(hipEventRecord(e0, st));
-    size_t lds = srt_sparse_lds_bytes(n);
-    SRT_HIPCHK(hipFuncSetAttribute((const void*)sssp_lds_kernel,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (delta == 0) delta = 8; /* bucket width of the label-correcting loop, in quanta */
     const size_t ldo = (size_t)n;
-    sssp_lds_kernel<<<src_end - src_begin, SP_THREADS, lds, st>>>(
-        n, src_begin, delta, rowptr, col, w, in_rowptr, in_col, in_w, in_r, lat_rows, rel_rows, ldo,
-        depth);
+    const int nsrc = src_end - src_begin;
+    const char* wsenv = getenv("SRT_SPARSE_WORKSET");
+    const bool force_hbm = wsenv && !strcmp(wsenv, "hbm");
+    if (n <= srt_sparse_max_n() && !force_hbm) {
+        const size_t lds = srt_sparse_lds_bytes(n);
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)sssp_kernel<false>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        sssp_kernel<false><<<nsrc, SP_THREADS, lds, st>>>(n, src_begin, nsrc, delta, rowptr, col, w,
+                                                          in_rowptr, in_col, in_w, in_r, lat_rows,
+                                                          rel_rows, ldo, depth, NULL, 0);
+    } else {
+        int cus = 256;
+        hipDeviceProp_t prop;
+        int dev = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+            cus = prop.multiProcessorCount;
+        const int slots = std::min(nsrc, 2 * cus);
+        const size_t slot_words = srt_sparse_lds_bytes(n) / 4 + 64; /* 256-B separated slots */
+        uint32_t* ws = NULL;
+        if (hipMallocAsync((void**)&ws, (size_t)slots * slot_words * 4, st) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipFree(depth);
+            srt_set_error("srt_sparse_build_device: workspace of %zu MiB failed",
+                          (size_t)slots * slot_words * 4 >> 20);
+            return SRT_E_NOMEM;
+        }
+        sssp_kernel<true><<<slots, SP_THREADS, 0, st>>>(n, src_begin, nsrc, delta, rowptr, col, w,
+                                                        in_rowptr, in_col, in_w, in_r, lat_rows,
+                                                        rel_rows, ldo, depth, ws, slot_words);
+        SRT_HIPCHK(hipFreeAsync(ws, st));
+    }
     SRT_HIPCHK(hipGetLastError());
     sparse_diag_kernel<<<srt_ceil_div(src_end - src_begin, 256), 256, 0, st>>>(
         n, src_begin, src_end, rowptr, col, w, r, self_w, self_r, lat_rows, rel_rows, ldo);

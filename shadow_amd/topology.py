@@ -184,3 +184,42 @@ def build_tables(n, directed, src, dst, lat_ns, loss, use_shortest_path=True, de
     check(lib().srt_build_tables(ctypes.byref(e), ctypes.byref(o), lat.ctypes.data, ctypes.byref(q),
                                  rel.ctypes.data, ctypes.byref(st)), "srt_build_tables")
     return lat.astype(np.uint64) * np.uint64(q.value), rel, st
+
+
+class SparseGraph:
+    """Device-resident canonical CSR (srt_sparse_graph_*): rows of any source range are computed
+    on the device into caller-provided device buffers (torch tensors or raw pointers)."""
+
+    def __init__(self, n, directed, src, dst, lat_ns, loss, device=0):
+        self._keep = [np.ascontiguousarray(src, np.int32), np.ascontiguousarray(dst, np.int32),
+                      np.ascontiguousarray(lat_ns, np.int64), np.ascontiguousarray(loss, np.float64)]
+        s, d, l, p = self._keep
+        e = Edges(n, int(bool(directed)), len(s), s.ctypes.data, d.ctypes.data, l.ctypes.data,
+                  p.ctypes.data)
+        h = ctypes.c_void_p()
+        check(lib().srt_sparse_graph_new(ctypes.byref(e), device, ctypes.byref(h)),
+              "srt_sparse_graph_new")
+        self._h = h
+        self._keep = None
+        nn, dd, aa, qq = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_uint64()
+        check(lib().srt_sparse_graph_info(h, ctypes.byref(nn), ctypes.byref(dd), ctypes.byref(aa),
+                                          ctypes.byref(qq)), "srt_sparse_graph_info")
+        self.n, self.directed, self.arcs, self.quantum_ns = nn.value, bool(dd.value), aa.value, qq.value
+
+    def rows(self, src_begin, src_end, lat_ptr, rel_ptr, stream=None, stats=None):
+        """srt_sparse_graph_rows into device pointers (row stride n)."""
+        st = ctypes.byref(stats) if stats is not None else None
+        check(lib().srt_sparse_graph_rows(self._h, src_begin, src_end, ctypes.c_void_p(lat_ptr),
+                                          ctypes.c_void_p(rel_ptr), ctypes.c_void_p(stream), st),
+              "srt_sparse_graph_rows")
+
+    def free(self):
+        if getattr(self, "_h", None):
+            lib().srt_sparse_graph_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

@@ -1,0 +1,84 @@
+"""Sparse multi-source SSSP through the device C-ABI (srt_sparse_graph_*), both working-set forms.
+
+* LDS-resident rows (n <= srt_sparse_max_n(), ~20k): C3-shaped random geometric graph.
+* HBM-resident rows (n beyond the LDS limit, or SRT_SPARSE_WORKSET=hbm): C5-shaped 100k-node
+  Barabasi-Albert graph, and the small graphs re-run with the HBM form forced.
+
+Latency bit-exact in integer ns, reliability within 1e-12 relative (north_star). Rows of a source
+subset are compared with oracle.sssp_rows; the undirected mirror (srt_mirror_lower_device) only
+moves the lower triangle, so the comparison of raw rows covers lat everywhere and rel for t > s.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from shadow_amd import graphs
+from shadow_amd._lib import ALGO_SPARSE_SSSP
+from shadow_amd.topology import SparseGraph, build_tables
+
+pytestmark = pytest.mark.gpu
+REL_TOL = 1e-12
+
+
+def _rows_on_gpu(sg, s0, s1, torch):
+    lat = torch.empty((s1 - s0, sg.n), dtype=torch.int32, device="cuda")
+    rel = torch.empty((s1 - s0, sg.n), dtype=torch.float64, device="cuda")
+    sg.rows(s0, s1, lat.data_ptr(), rel.data_ptr(), None)
+    torch.cuda.synchronize()
+    return (lat.cpu().numpy().view(np.uint32).astype(np.uint64) * np.uint64(sg.quantum_ns),
+            rel.cpu().numpy())
+
+
+def _check_rows(g, ranges, torch):
+    sg = SparseGraph(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
+    el = oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
+    for s0, s1 in ranges:
+        lat, rel = _rows_on_gpu(sg, s0, s1, torch)
+        exp = oracle.sssp_rows(el, s0, s1, nthreads=8)
+        off = np.arange(g.n)[None, :] != np.arange(s0, s1)[:, None]
+        assert np.array_equal(np.where(off, lat, 0), np.where(off, exp["lat_int"], 0)), (s0, s1)
+        upper = np.arange(g.n)[None, :] > np.arange(s0, s1)[:, None]
+        if not g.directed:
+            err = np.abs(rel - exp["rel"]) / np.maximum(exp["rel"], 1e-300)
+            assert float(err[upper].max() if upper.any() else 0.0) <= REL_TOL, (s0, s1)
+        else:
+            err = np.abs(rel - exp["rel"]) / np.maximum(exp["rel"], 1e-300)
+            assert float(err[off].max()) <= REL_TOL, (s0, s1)
+    sg.free()
+
+
+def test_c3_shape_rgg_20000_lds_rows(gpu):
+    import torch
+    g = graphs.random_geometric(20000, seed=3)
+    _check_rows(g, [(0, 96), (9_950, 10_050), (19_900, 20_000)], torch)
+
+
+def test_c5_shape_ba_100000_hbm_rows(gpu):
+    import torch
+    g = graphs.barabasi_albert(100_000, seed=5)
+    _check_rows(g, [(0, 48), (50_000, 50_016), (99_984, 100_000)], torch)
+
+
+@pytest.mark.parametrize("which", ["rgg3000", "ba2000", "directed"])
+def test_hbm_workset_forced_full_tables(gpu, monkeypatch, which):
+    monkeypatch.setenv("SRT_SPARSE_WORKSET", "hbm")
+    if which == "rgg3000":
+        g = graphs.random_geometric(3000, seed=3)
+    elif which == "ba2000":
+        g = graphs.barabasi_albert(2000, seed=5)
+    else:
+        rng = np.random.default_rng(12)
+        n, m = 400, 3000
+        ring = np.arange(n)
+        src = np.concatenate([rng.integers(0, n, m), ring, ring]).astype(np.int32)
+        dst = np.concatenate([rng.integers(0, n, m), (ring + 1) % n, ring]).astype(np.int32)
+        lat = (rng.integers(1, 20, len(src)) * 1_000_000).astype(np.int64)
+        loss = rng.integers(0, 300, len(src)) / 10000.0
+        g = graphs.Graph(n, True, src, dst, lat, loss)
+    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                algo=ALGO_SPARSE_SSSP)
+    exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss),
+                       True, oracle.ORC_INT_NS, 8)
+    assert np.array_equal(lat, exp["lat_int"])
+    err = np.abs(rel - exp["rel"]) / np.maximum(np.abs(exp["rel"]), 1e-300)
+    assert float(err.max()) <= REL_TOL
