@@ -39,11 +39,10 @@ WORKLOADS = {
 }
 METRIC = "routing-table build time & node-pairs/sec (GB/s vs HBM peak), 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md, HBM3E spec peak
-# VALU issue: 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz = 39.3 T lane-instructions/s (one wave64
-# instruction per 4 cycles per SIMD). Measured on gfx950 (profiles/r01_valu_issue_rates.txt):
-# v_min_u32 / v_pk_min_u16 / v_pk_add_u16 issue at 4.1-4.2 cycles, and a stream mixing them with
-# the 2-cycle ops (v_add_u32) still issues at 4.0 cycles per instruction.
-VALU_PEAK_TINSTR = 256 * 4 * 16 * 2.4e9 / 1e12
+# VALU: 256 CU x 4 SIMD x 64 lanes x 2.4 GHz = 157.3 T lane-cycles/s; a wave64 relaxation costs
+# `cyc_per_relax` SIMD cycles under the issue model below, so the relaxation roof is
+# 157.3 T / cyc_per_relax.
+VALU_LANE_CYCLES_T = 256 * 4 * 64 * 2.4e9 / 1e12
 FW_B = 64
 SHARD_ALIGN = 128  # row-shard / update-tile alignment (srt_device.h SRT_SHARD_ALIGN)
 
@@ -148,16 +147,22 @@ def main():
     n_upd = sum(s.n_update for s in stats)
     ms_upd = sum(s.ms_update for s in stats)
     avg_upd_ms = ms_upd / max(n_upd, 1)
-    packed = stats[-1].fw_block < 0  # packed 15-bit distances (exact, else the u32 kernels ran)
-    s_d = 2 if packed else 4
-    # VALU instructions per relaxation: packed = (v_add_u32 + v_pk_min_u16) per 2 relaxations;
-    # u32 = v_add_u32 + v_min3_u32 over two candidates = 1.5
-    instr_per_relax = 1.0 if packed else 1.5
+    enc = int(stats[-1].dist_enc)  # 3: u16 + f16-compare mins, 2: u16 pk_min, 1: u32
+    s_d = 4 if enc == 1 else 2
+    # VALU issue model per wave64 relaxation (cycles per SIMD): full-rate ops (v_add_u32) issue in
+    # 2 cycles, packed / 3-input ops (v_pk_minimum3_f16, v_pk_min_u16, v_min3_u32) in 4
+    # (profiles/r01_valu_issue_rates*.txt):
+    #   enc 3: 2 x v_add_u32 + 1 x v_pk_minimum3_f16 per 4 relaxations -> 8/4 = 2.0 cycles
+    #   enc 2: 1 x v_add_u32 + 1 x v_pk_min_u16 per 2 relaxations      -> 6/2 = 3.0 cycles
+    #   enc 1: 2 x v_add_u32 + 1 x v_min3_u32 per 2 relaxations         -> 8/2 = 4.0 cycles
+    cyc_per_relax = {3: 2.0, 2: 3.0, 1: 4.0}[enc]
+    instr_per_relax = {3: 0.75, 2: 1.0, 1: 1.5}[enc]
+    kname = {3: "fw16_update_kernel<true>", 2: "fw16_update_kernel<false>", 1: "fw_update_kernel"}[enc]
     bytes_per_launch = 2.0 * nr * ld * s_d  # round-streaming model: read + write the local rows
     relax_per_launch = float(nr) * ld * FW_B
     achieved_gbs = bytes_per_launch / (avg_upd_ms * 1e-3) / 1e9
     relax_t = relax_per_launch / (avg_upd_ms * 1e-3) / 1e12
-    relax_peak_t = VALU_PEAK_TINSTR / instr_per_relax
+    relax_peak_t = VALU_LANE_CYCLES_T / cyc_per_relax
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.workload}_n{world}.json")
     if os.path.exists(pmc_path):
@@ -166,19 +171,20 @@ def main():
         # the north-star metric is GB/s vs HBM peak; the kernel itself is VALU-issue bound (min-plus
         # has no MFMA form), so the binding roof is reported beside it under "valu"
         "bound": "hbm", "binding": "valu-issue",
-        "kernel": "fw16_update_kernel" if packed else "fw_update_kernel",
+        "kernel": kname,
         "achieved": round(achieved_gbs, 1),
         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
         "traffic": traffic, "bytes_per_launch": bytes_per_launch,
         "avg_launch_ms": round(avg_upd_ms, 4), "launches_timed": n_upd,
         "model": f"2*rows*ld*{s_d} B per round (SURVEY §8d round-streaming, B=64, "
-                 f"{'packed 15-bit u16' if packed else 'u32'} distances)",
+                 f"{ {3: 'u16 f16-compare', 2: 'u16 pk_min', 1: 'u32'}[enc]} distances)",
         "algorithmic_min_bytes": float(nr) * ld * (4 + 8),
         "valu": {"achieved": round(relax_t, 2), "peak": round(relax_peak_t, 1),
                  "unit": "Trelax/s", "frac": round(relax_t / relax_peak_t, 4),
-                 "instr_per_relax": instr_per_relax,
+                 "instr_per_relax": instr_per_relax, "cycles_per_relax": cyc_per_relax,
                  "relax_per_launch": relax_per_launch,
-                 "peak_basis": "256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz / instr_per_relax"},
+                 "peak_basis": "256 CU x 4 SIMD x 64 lanes x 2.4 GHz / cycles_per_relax "
+                               "(v_add_u32 2 cycles, packed/3-input ops 4 cycles per wave64)"},
     }
 
     cpu = None
@@ -218,7 +224,7 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "node-pairs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-            "dtype": "u16" if packed else "u32",  # integer latency quanta
+            "dtype": "u32" if enc == 1 else "u16",  # integer latency quanta
             "data": "synthetic",
             "config": {"workload": wl["desc"], "n": n, "ld": ld, "fw_block": FW_B,
                        "parallelism": f"row-shard x{world}" + (" + RCCL pivot-panel broadcast"

@@ -59,6 +59,7 @@ class BuildStats(ctypes.Structure):
         ("n_update", ctypes.c_int32),
         ("ms_update", ctypes.c_double),
         ("ms_comm", ctypes.c_double),
+        ("dist_enc", ctypes.c_int32),
     ]
 
 

@@ -837,12 +837,15 @@ extern "C" int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, c
     evpool_t* evp = NULL;
     int rc;
     if (stats && stats->time_kernels && (rc = evpool_begin(&evp, ld / B))) return rc;
-    int exact = 0;
-    if (ld % 128 == 0) {
-        rc = srt_fw16_build(n, ld, 0, ld, w, lat, st, evp, NULL, NULL, NULL, 0, &exact);
+    /* narrowest exact encoding first: f16-compare u16 -> pk_min u16 -> u32 */
+    int exact = 0, enc = SRT_DENC_U32;
+    for (int fm = 1; fm >= 0 && !exact && ld % 128 == 0; --fm) {
+        if (evp) evp->used = 0;
+        rc = srt_fw16_build(n, ld, 0, ld, w, lat, st, evp, NULL, NULL, NULL, 0, fm, &exact);
         if (rc) return rc;
+        if (exact) enc = fm ? SRT_DENC_F16CMP : SRT_DENC_U16;
     }
-    if (!exact) { /* u32 path: ld not a multiple of 128, or a distance reached 0xFFFF quanta */
+    if (!exact) { /* u32 path: ld not a multiple of 128, or a distance reached 0x7FFF quanta */
         if (evp) evp->used = 0;
         dim3 g(srt_ceil_div(ld, 256), ld);
         init_dist_kernel<<<g, 256, 0, st>>>(n, ld, 0, w, lat);
@@ -860,7 +863,8 @@ extern "C" int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, c
         SRT_HIPCHK(hipEventElapsedTime(&a, e0, e1));
         SRT_HIPCHK(hipEventElapsedTime(&b, e1, e2));
         stats->algo = SRT_ALGO_DENSE_FW;
-        stats->fw_block = exact ? -B : B; /* negative: packed-u16 distances */
+        stats->fw_block = B;
+        stats->dist_enc = enc;
         stats->ms_fw = a;
         stats->ms_post = b;
         stats->ms_total = a + b;
@@ -1051,16 +1055,20 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
     evpool_t* evp = NULL;
     if (stats && stats->time_kernels && (rc = evpool_begin(&evp, ld / B))) return rc;
     shard_ctx ctx = {comm, ld};
-    int exact = 0;
-    rc = srt_fw16_build(n, ld, b, nr, w_rows, lat_rows, st, evp, shard_owner,
-                        R > 1 ? shard_bcast : NULL, &ctx, me, &exact);
-    if (rc) return rc;
-    if (R > 1) { /* every rank must agree before the u32 fallback */
-        int32_t* flag = ws->cnt;
-        SRT_HIPCHK(hipMemcpyAsync(flag, &exact, sizeof(int32_t), hipMemcpyHostToDevice, st));
-        SRT_NCCLCHK(ncclAllReduce(flag, flag, 1, ncclInt32, ncclMin, nc, st));
-        SRT_HIPCHK(hipMemcpyAsync(&exact, flag, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-        SRT_HIPCHK(hipStreamSynchronize(st));
+    int exact = 0, enc = SRT_DENC_U32;
+    for (int fm = 1; fm >= 0 && !exact; --fm) {
+        if (evp) evp->used = 0;
+        rc = srt_fw16_build(n, ld, b, nr, w_rows, lat_rows, st, evp, shard_owner,
+                            R > 1 ? shard_bcast : NULL, &ctx, me, fm, &exact);
+        if (rc) return rc;
+        if (R > 1) { /* every rank must agree before falling back to a wider encoding */
+            int32_t* flag = ws->cnt;
+            SRT_HIPCHK(hipMemcpyAsync(flag, &exact, sizeof(int32_t), hipMemcpyHostToDevice, st));
+            SRT_NCCLCHK(ncclAllReduce(flag, flag, 1, ncclInt32, ncclMin, nc, st));
+            SRT_HIPCHK(hipMemcpyAsync(&exact, flag, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+            SRT_HIPCHK(hipStreamSynchronize(st));
+        }
+        if (exact) enc = fm ? SRT_DENC_F16CMP : SRT_DENC_U16;
     }
     if (!exact) {
         if (evp) evp->used = 0;
@@ -1102,7 +1110,8 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
         SRT_HIPCHK(hipEventElapsedTime(&a, e0, e1));
         SRT_HIPCHK(hipEventElapsedTime(&c, e1, e2));
         stats->algo = SRT_ALGO_DENSE_FW;
-        stats->fw_block = exact ? -B : B; /* negative: packed-u16 distances */
+        stats->fw_block = B;
+        stats->dist_enc = enc;
         stats->ms_fw = a;
         stats->ms_post = c;
         stats->ms_total = a + c;

@@ -1,20 +1,28 @@
 /*
- * fw16.hip -- packed 15-bit blocked Floyd-Warshall for gfx950.
+ * fw16.hip -- packed 16-bit blocked Floyd-Warshall for gfx950.
  *
- * Distances are held as u16 quanta capped at INF15 = 0x7FFF, two per 32-bit register. Because
- * both halves are <= 0x7FFF, one plain v_add_u32 adds the two pairs without a carry crossing
- * the half boundary (sums <= 0xFFFE), and v_pk_min_u16 keeps the minimum per half: two
- * relaxations cost one v_add_u32 (~2.4 cycles per wave64 instruction on gfx950, measured by
- * tools/valu_rate.hip) plus one v_pk_min_u16 (~4.2), against ~4.2 + 4.2 for
- * v_pk_add_u16 + v_pk_min_u16 and ~2.4 + 4.1 per single relaxation for u32 add + min.
- * Every stored value is min(candidate, previous) <= 0x7FFF, so the result is min(D, 0x7FFF)
- * element-wise: exact wherever D < 0x7FFF. If any real pair reaches the cap the build reports
- * inexact and the caller reruns the u32 kernels -- the table is never approximate.
+ * Distances are held as u16 quanta, two per 32-bit register, capped at CAP. Two instruction
+ * mixes implement the min-plus step (issue costs measured by tools/valu_rate*.hip, 4 waves/SIMD):
+ *
+ *   FM (f16-compare) path, CAP = 0x3DFF: two pivots per step. One plain v_add_u32 adds a pair of
+ *     halves (both <= CAP, so each half-sum <= 0x7BFE: no carry crosses the half boundary), and
+ *     one v_pk_minimum3_f16 takes min(acc, t_m, t_m+1) per half. The half-sums are bit patterns
+ *     of non-negative finite f16 values (< 0x7C00 = +inf), whose f16 order is their integer
+ *     order, denormals included (checked exhaustively-by-sample on the device: 0 mismatches of
+ *     4M triples, profiles/r01_valu_issue_rates2.txt). 4 relaxations = 2 adds + 1 min3:
+ *     2.48 cycles per relaxation per wave64, against 3.80 for the U path.
+ *   U path, CAP = 0x7FFF: one v_add_u32 + one v_pk_min_u16 per 2 relaxations.
+ *
+ * Both are exact where the true distance is below CAP: every stored value is min(candidate,
+ * previous) <= CAP, and min(a,CAP) + min(b,CAP) >= min(a+b, CAP), so the table computed is
+ * min(D, CAP) element-wise. If any real pair reaches CAP the build reports inexact and the caller
+ * reruns with the next wider path (FM -> U -> u32 kernels) -- the table is never approximate.
  * The A operand is staged pre-splatted, (a, a) per 32-bit LDS word, so the add needs no
  * per-half operand select.
  *
  * Kernels (pivot block KB = 64 rows/cols per round):
- *   fw16_diag    closure of the 64x64 diagonal tile in LDS (64 dependent steps)
+ *   fw16_diag    closure of the 64x64 diagonal tile in LDS (64 dependent steps; u16 pk_min, valid
+ *                for either CAP since sums of two values <= 0x7FFF fit 16 bits)
  *   fw16_panel   pivot-row panel tiles Dkk* (x) X and pivot-column tiles X (x) Dkk* (64x64)
  *   fw16_update  every 128x128 tile: C <- min(C, A (x) B), A = D[I][k-block], B = P[:, J]
  * The 128x128 update tile gives each of 256 threads an 8x8 block: per pivot step 2 LDS reads
@@ -26,7 +34,8 @@ typedef unsigned short u16;
 typedef u16 u16x2 __attribute__((ext_vector_type(2)));
 
 #define KB 64
-#define INF16 0x7FFFu  /* cap of the packed 15-bit distances */
+#define CAP_U 0x7FFFu /* cap of the U path (v_pk_min_u16) */
+#define CAP_F 0x3DFFu /* cap of the FM path: 2 * CAP_F < 0x7C00 (f16 +inf) */
 #define LDA16 (KB + 8) /* u16 stride of an A row in LDS: 144 B, 16-byte aligned */
 #define UKC 32          /* pivots per LDS stage in the update kernel (two stages per launch) */
 
@@ -37,6 +46,21 @@ static __device__ __forceinline__ u16x2 relax(u16x2 acc, uint32_t a2, uint32_t b
     return __builtin_elementwise_min(acc, as2(a2 + b2));
 }
 static __device__ __forceinline__ uint32_t splat(uint32_t h) { return h | (h << 16); }
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+/* per half: min(acc, x, y) on u16 bit patterns in [0, 0x7BFF] -> one v_pk_minimum3_f16 */
+static __device__ __forceinline__ uint32_t min3h(uint32_t acc, uint32_t x, uint32_t y) {
+    const h2 r = __builtin_elementwise_minimum(
+        __builtin_bit_cast(h2, acc),
+        __builtin_elementwise_minimum(__builtin_bit_cast(h2, x), __builtin_bit_cast(h2, y)));
+    return __builtin_bit_cast(uint32_t, r);
+}
+template <int I>
+static __device__ __forceinline__ uint32_t lane4(const uint4& v) {
+    if constexpr (I == 0) return v.x;
+    else if constexpr (I == 1) return v.y;
+    else if constexpr (I == 2) return v.z;
+    else return v.w;
+}
 
 /* ---- staging ------------------------------------------------------------------------------ */
 /* A (TM rows x KC pivots) into LDS as (a, a) words: row r, pivot m at sA[r * (KC + 4) + m]
@@ -70,7 +94,46 @@ __device__ __forceinline__ void stage_B(u16* __restrict__ sB, const u16* __restr
 }
 
 /* ---- register-blocked min-plus over KC staged pivots ---------------------------------------- */
-template <int TN, int RM, int RN, int KC>
+template <bool FM, int MM, int RN>
+__device__ __forceinline__ void step_rows(u16x2 (&acc)[RN / 2], u16x2 (&acc1)[RN / 2], const uint4& a0,
+                                          const uint4& a1, const uint32_t (&bv)[4][RN / 2]) {
+    if constexpr (FM) {
+        /* pivots MM, MM+1: two adds per column pair and row, one 3-input min */
+        uint32_t t[4][RN / 2];
+#pragma unroll
+        for (int c = 0; c < RN / 2; ++c) {
+            t[0][c] = lane4<MM>(a0) + bv[MM][c];
+            t[1][c] = lane4<MM + 1>(a0) + bv[MM + 1][c];
+            t[2][c] = lane4<MM>(a1) + bv[MM][c];
+            t[3][c] = lane4<MM + 1>(a1) + bv[MM + 1][c];
+        }
+#pragma unroll
+        for (int c = 0; c < RN / 2; ++c) {
+            acc[c] = as2(min3h(as32(acc[c]), t[0][c], t[1][c]));
+            acc1[c] = as2(min3h(as32(acc1[c]), t[2][c], t[3][c]));
+        }
+    } else {
+        /* one pivot at a time, two rows: RN independent adds, then RN mins */
+#pragma unroll
+        for (int mm = MM; mm < MM + 2; ++mm) {
+            uint32_t t[2][RN / 2];
+            const uint32_t s0 = mm == MM ? lane4<MM>(a0) : lane4<MM + 1>(a0);
+            const uint32_t s1 = mm == MM ? lane4<MM>(a1) : lane4<MM + 1>(a1);
+#pragma unroll
+            for (int c = 0; c < RN / 2; ++c) {
+                t[0][c] = s0 + bv[mm][c];
+                t[1][c] = s1 + bv[mm][c];
+            }
+#pragma unroll
+            for (int c = 0; c < RN / 2; ++c) {
+                acc[c] = __builtin_elementwise_min(acc[c], as2(t[0][c]));
+                acc1[c] = __builtin_elementwise_min(acc1[c], as2(t[1][c]));
+            }
+        }
+    }
+}
+
+template <bool FM, int TN, int RM, int RN, int KC>
 __device__ __forceinline__ void mp16(u16x2 (&acc)[RM][RN / 2], const uint32_t* __restrict__ sA,
                                      const u16* __restrict__ sB, int tx, int ty) {
     constexpr int LDB = TN + 8, LDA = KC + 4;
@@ -101,28 +164,10 @@ __device__ __forceinline__ void mp16(u16x2 (&acc)[RM][RN / 2], const uint32_t* _
             for (int r = 0; r < 4; ++r)
                 av[r] = *reinterpret_cast<const uint4*>(pa + (rg + r) * LDA + m);
 #pragma unroll
-            for (int mm = 0; mm < 4; ++mm)
-#pragma unroll
-                for (int r = 0; r < 4; r += 2) {
-                    /* two rows at a time: RN independent adds, then RN mins, so every min is
-                     * several instructions behind the add it consumes */
-                    const uint32_t s0 = mm == 0 ? av[r].x : mm == 1 ? av[r].y : mm == 2 ? av[r].z : av[r].w;
-                    const uint32_t s1 = mm == 0   ? av[r + 1].x
-                                        : mm == 1 ? av[r + 1].y
-                                        : mm == 2 ? av[r + 1].z
-                                                  : av[r + 1].w;
-                    uint32_t t[2][RN / 2];
-#pragma unroll
-                    for (int c = 0; c < RN / 2; ++c) {
-                        t[0][c] = s0 + bv[mm][c];
-                        t[1][c] = s1 + bv[mm][c];
-                    }
-#pragma unroll
-                    for (int c = 0; c < RN / 2; ++c) {
-                        acc[rg + r][c] = __builtin_elementwise_min(acc[rg + r][c], as2(t[0][c]));
-                        acc[rg + r + 1][c] = __builtin_elementwise_min(acc[rg + r + 1][c], as2(t[1][c]));
-                    }
-                }
+            for (int r = 0; r < 4; r += 2) {
+                step_rows<FM, 0, RN>(acc[rg + r], acc[rg + r + 1], av[r], av[r + 1], bv);
+                step_rows<FM, 2, RN>(acc[rg + r], acc[rg + r + 1], av[r], av[r + 1], bv);
+            }
         }
     }
 }
@@ -169,12 +214,12 @@ __device__ __forceinline__ void store_acc16(const u16x2 (&acc)[RM][RN / 2],
 
 /* ---- kernels --------------------------------------------------------------------------------- */
 __global__ void fw16_init_kernel(int n, int ld, int row0, const uint32_t* __restrict__ w,
-                                 u16* __restrict__ d) {
+                                 u16* __restrict__ d, uint32_t cap) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const int i = row0 + blockIdx.y;
     if (j >= ld) return;
-    const uint32_t x = (i < n && j < n) ? w[(size_t)blockIdx.y * ld + j] : INF16;
-    d[(size_t)blockIdx.y * ld + j] = (i == j) ? (u16)0 : (u16)min(x, (uint32_t)INF16);
+    const uint32_t x = (i < n && j < n) ? w[(size_t)blockIdx.y * ld + j] : cap;
+    d[(size_t)blockIdx.y * ld + j] = (i == j) ? (u16)0 : (u16)min(x, cap);
 }
 
 /* closure of the diagonal tile: 64 dependent pivot steps in LDS, 4x4 per thread */
@@ -209,6 +254,7 @@ __global__ __launch_bounds__(256) void fw16_diag_kernel(u16* __restrict__ P, int
 }
 
 /* pivot-row panel tiles (k, j): X <- Dkk* (x) X ; pivot-column tiles (i, k): X <- X (x) Dkk* */
+template <bool FM>
 __global__ __launch_bounds__(256) void fw16_panel_kernel(u16* __restrict__ D, int ld, int row0,
                                                          int nrow_tiles, u16* __restrict__ P, int k0,
                                                          int ncol_tiles, int do_row, int do_col) {
@@ -236,11 +282,12 @@ __global__ __launch_bounds__(256) void fw16_panel_kernel(u16* __restrict__ D, in
     for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int c = 0; c < 2; ++c) acc[r][c] = old[r][c];
-    mp16<KB, 4, 4, KB>(acc, sA, sB, tx, ty);
+    mp16<FM, KB, 4, 4, KB>(acc, sA, sB, tx, ty);
     store_acc16<4, 4>(acc, old, C, ld, tx, ty);
 }
 
 /* every 128x128 tile of the local rows: D_IJ <- min(D_IJ, D_I,k (x) P_k,J) */
+template <bool FM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void fw16_update_kernel(u16* __restrict__ D, int ld,
                                                           const u16* __restrict__ P, int k0,
                                                           int ncol_tiles) {
@@ -269,29 +316,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
                 for (int c = 0; c < 4; ++c) acc[r][c] = old[r][c];
         }
-        mp16<128, 8, 8, UKC>(acc, sA, sB, tx, ty);
+        mp16<FM, 128, 8, 8, UKC>(acc, sA, sB, tx, ty);
     }
     store_acc16<8, 8>(acc, old, C, ld, tx, ty);
 }
 
 /* widen to the u32 table and flag saturation of a real pair (i, j < n) */
 __global__ void fw16_finish_kernel(int n, int ld, int row0, const u16* __restrict__ d16,
-                                   uint32_t* __restrict__ lat, int* __restrict__ saturated) {
+                                   uint32_t* __restrict__ lat, int* __restrict__ saturated,
+                                   uint32_t cap) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const int i = row0 + blockIdx.y;
     if (j >= ld) return;
     const size_t ix = (size_t)blockIdx.y * ld + j;
     const uint32_t v = d16[ix];
     const bool real = i < n && j < n;
-    lat[ix] = (v == INF16) ? SRT_INF : v;
-    if (real && v == INF16) atomicOr(saturated, 1);
+    lat[ix] = (v == cap) ? SRT_INF : v;
+    if (real && v == cap) atomicOr(saturated, 1);
 }
 
 #ifndef SRT_FW16_DEVICE_ONLY
 /* ---- orchestration --------------------------------------------------------------------------- */
 int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,
                    hipStream_t st, evpool_t* evp, srt_owner_fn owner_of, srt_panel_bcast_fn bcast,
-                   void* ctx, int rank, int* exact) {
+                   void* ctx, int rank, int fm, int* exact) {
     if (ld % 128 || nrows % 128) {
         srt_set_error("u16 FW needs ld and the row shard to be multiples of 128");
         return SRT_E_ARG;
@@ -314,8 +362,12 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
     if (!flags[dev]) SRT_HIPCHK(hipMalloc(&flags[dev], sizeof(int)));
     u16* d = bufs[dev];
     u16* pbuf = panels[dev];
+    const uint32_t cap = fm ? CAP_F : CAP_U;
+    auto panel = fm ? fw16_panel_kernel<true> : fw16_panel_kernel<false>;
+    auto update = fm ? fw16_update_kernel<true> : fw16_update_kernel<false>;
     if (nrows > 0) {
-        fw16_init_kernel<<<dim3(srt_ceil_div(ld, 256), nrows), 256, 0, st>>>(n, ld, row0, w_rows, d);
+        fw16_init_kernel<<<dim3(srt_ceil_div(ld, 256), nrows), 256, 0, st>>>(n, ld, row0, w_rows, d,
+                                                                           cap);
         SRT_HIPCHK(hipGetLastError());
     }
     const int nb = ld / KB, nrb = nrows / KB, ncol128 = ld / 128, nrow128 = nrows / 128;
@@ -325,7 +377,7 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
         if (owner == rank) {
             P = d + (size_t)(k0 - row0) * ld;
             fw16_diag_kernel<<<1, 256, 0, st>>>(P, ld, k0);
-            fw16_panel_kernel<<<nb, 256, 0, st>>>(d, ld, row0, nrb, P, k0, nb, 1, 0);
+            panel<<<nb, 256, 0, st>>>(d, ld, row0, nrb, P, k0, nb, 1, 0);
             SRT_HIPCHK(hipGetLastError());
         } else {
             P = pbuf;
@@ -335,17 +387,17 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
             if (rc) return rc;
         }
         if (nrb > 0) {
-            fw16_panel_kernel<<<nb + nrb, 256, 0, st>>>(d, ld, row0, nrb, P, k0, nb, 0, 1);
+            panel<<<nb + nrb, 256, 0, st>>>(d, ld, row0, nrb, P, k0, nb, 0, 1);
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
-            fw16_update_kernel<<<ncol128 * nrow128, 256, 0, st>>>(d, ld, P, k0, ncol128);
+            update<<<ncol128 * nrow128, 256, 0, st>>>(d, ld, P, k0, ncol128);
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
             SRT_HIPCHK(hipGetLastError());
         }
     }
     SRT_HIPCHK(hipMemsetAsync(flags[dev], 0, sizeof(int), st));
     if (nrows > 0)
-        fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 256), nrows), 256, 0, st>>>(n, ld, row0, d,
-                                                                             lat_rows, flags[dev]);
+        fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 256), nrows), 256, 0, st>>>(
+            n, ld, row0, d, lat_rows, flags[dev], cap);
     SRT_HIPCHK(hipGetLastError());
     int sat = 0;
     SRT_HIPCHK(hipMemcpyAsync(&sat, flags[dev], sizeof(int), hipMemcpyDeviceToHost, st));

@@ -186,3 +186,32 @@ def test_dense_device_api_and_sharded_single_rank(gpu):
     torch.cuda.synchronize()
     L.srt_comm_free(comm)
     assert torch.equal(lat2[:n, :n], lat[:n, :n]) and torch.equal(rel2[:n, :n], rel[:n, :n])
+
+
+@pytest.mark.parametrize("hop_ms,enc", [(1, 3), (160, 2), (400, 1)])
+def test_dense_distance_encoding_tiers(gpu, hop_ms, enc):
+    """Each distance encoding of the dense build (fw16.hip) is exact where it is chosen.
+
+    A 256-vertex ring with hop latencies hop_ms / hop_ms+1 (gcd 1 ms) plus a few chords: the
+    largest distance is ~128 * hop_ms quanta, so hop_ms = 1 fits the f16-compare path (cap
+    0x3DFF), 160 saturates it and falls back to the u16 pk_min path (cap 0x7FFF), and 400
+    saturates both and ends on the u32 kernels. Every tier must match the oracle bit for bit.
+    """
+    n = 256
+    rng = np.random.default_rng(hop_ms)
+    src = list(range(n))
+    dst = [(i + 1) % n for i in range(n)]
+    lat = [(hop_ms + (i % 2)) * MS for i in range(n)]
+    for _ in range(12):  # long chords keep the diameter large but break the ring's ties
+        a, b = (int(x) for x in rng.choice(n, 2, replace=False))
+        src.append(a)
+        dst.append(b)
+        lat.append(int(hop_ms * n // 3) * MS)
+    loss = rng.integers(0, 100, len(src)) * 1e-4
+    g = graphs.Graph(n, 0, np.array(src, np.int32), np.array(dst, np.int32),
+                     np.array(lat, np.int64), loss)
+    got_lat, got_rel, st = build_tables(g.n, False, g.src, g.dst, g.lat_ns, g.loss,
+                                        algo=ALGO_DENSE_FW)
+    exp = _oracle(g)
+    assert_tables(got_lat, got_rel, exp["lat_int"], exp["rel"], f"hop {hop_ms} ms")
+    assert st.dist_enc == enc, f"expected encoding {enc}, build used {st.dist_enc}"

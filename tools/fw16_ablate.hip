@@ -6,8 +6,8 @@
 #include <vector>
 #include <algorithm>
 
-template <bool IO, bool STAGE, bool COMPUTE>
-__global__ __launch_bounds__(256) void abl_kernel(u16* __restrict__ D, int ld, const u16* __restrict__ P,
+template <bool FM, bool IO, bool STAGE, bool COMPUTE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void abl_kernel(u16* __restrict__ D, int ld, const u16* __restrict__ P,
                                                   int k0, int ncol_tiles, unsigned* sink) {
     __shared__ __attribute__((aligned(16))) uint32_t sA[128 * (UKC + 4)];
     __shared__ __attribute__((aligned(16))) u16 sB[UKC * (128 + 8)];
@@ -28,7 +28,7 @@ __global__ __launch_bounds__(256) void abl_kernel(u16* __restrict__ D, int ld, c
             stage_B<128, UKC>(sB, P + (size_t)h * ld + J * 128, ld, tid);
             __syncthreads();
         }
-        if (COMPUTE) mp16<128, 8, 8, UKC>(acc, sA, sB, tx, ty);
+        if (COMPUTE) mp16<FM, 128, 8, 8, UKC>(acc, sA, sB, tx, ty);
     }
     if (IO) store_acc16<8, 8>(acc, old, C, ld, tx, ty);
     else {
@@ -38,14 +38,14 @@ __global__ __launch_bounds__(256) void abl_kernel(u16* __restrict__ D, int ld, c
     }
 }
 
-template <bool IO, bool ST, bool CO>
+template <bool FM, bool IO, bool ST, bool CO>
 float run(u16* D, int ld, unsigned* sink, int rounds) {
     hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
     const int nct = ld / 128, grid = nct * nct;
     hipEventRecord(a);
     for (int k = 0; k < rounds; ++k) {
         const int k0 = (k * 64) % ld;
-        abl_kernel<IO, ST, CO><<<grid, 256>>>(D, ld, D + (size_t)k0 * ld, k0, nct, sink);
+        abl_kernel<FM, IO, ST, CO><<<grid, 256>>>(D, ld, D + (size_t)k0 * ld, k0, nct, sink);
     }
     hipEventRecord(b); hipEventSynchronize(b);
     float ms; hipEventElapsedTime(&ms, a, b);
@@ -59,19 +59,28 @@ int main(int argc, char** argv) {
     hipMalloc(&D, (size_t)ld * ld * 2); hipMalloc(&sink, 4096);
     hipMemset(D, 0x11, (size_t)ld * ld * 2);
     const char* names[] = {"full", "no-io", "no-stage", "compute-only", "io-only", "io+stage", "stage-only"};
-    std::vector<std::vector<float>> t(7);
-    for (int it = 0; it < 5; ++it) {
-        t[0].push_back(run<true, true, true>(D, ld, sink, rounds));
-        t[1].push_back(run<false, true, true>(D, ld, sink, rounds));
-        t[2].push_back(run<true, false, true>(D, ld, sink, rounds));
-        t[3].push_back(run<false, false, true>(D, ld, sink, rounds));
-        t[4].push_back(run<true, false, false>(D, ld, sink, rounds));
-        t[5].push_back(run<true, true, false>(D, ld, sink, rounds));
-        t[6].push_back(run<false, true, false>(D, ld, sink, rounds));
-    }
-    for (int v = 0; v < 7; ++v) {
-        std::sort(t[v].begin(), t[v].end());
-        printf("%-14s median %.4f ms  min %.4f ms\n", names[v], t[v][2], t[v][0]);
+    for (int fm = 1; fm >= 0; --fm) {
+        std::vector<std::vector<float>> t(7);
+        for (int it = 0; it < 5; ++it) {
+            if (fm) {
+                t[0].push_back(run<true, true, true, true>(D, ld, sink, rounds));
+                t[1].push_back(run<true, false, true, true>(D, ld, sink, rounds));
+                t[2].push_back(run<true, true, false, true>(D, ld, sink, rounds));
+                t[3].push_back(run<true, false, false, true>(D, ld, sink, rounds));
+            } else {
+                t[0].push_back(run<false, true, true, true>(D, ld, sink, rounds));
+                t[1].push_back(run<false, false, true, true>(D, ld, sink, rounds));
+                t[2].push_back(run<false, true, false, true>(D, ld, sink, rounds));
+                t[3].push_back(run<false, false, false, true>(D, ld, sink, rounds));
+            }
+            t[4].push_back(run<false, true, false, false>(D, ld, sink, rounds));
+            t[5].push_back(run<false, true, true, false>(D, ld, sink, rounds));
+            t[6].push_back(run<false, false, true, false>(D, ld, sink, rounds));
+        }
+        for (int v = 0; v < 7; ++v) {
+            std::sort(t[v].begin(), t[v].end());
+            printf("%s %-14s median %.4f ms  min %.4f ms\n", fm ? "FM" : "U ", names[v], t[v][2], t[v][0]);
+        }
     }
     return 0;
 }
