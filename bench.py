@@ -157,7 +157,7 @@ def main():
     #   enc 1: 2 x v_add_u32 + 1 x v_min3_u32 per 2 relaxations         -> 8/2 = 4.0 cycles
     cyc_per_relax = {3: 2.0, 2: 3.0, 1: 4.0}[enc]
     instr_per_relax = {3: 0.75, 2: 1.0, 1: 1.5}[enc]
-    kname = {3: "fw16_update_kernel<true>", 2: "fw16_update_kernel<false>", 1: "fw_update_kernel"}[enc]
+    kname = {3: "fwh_update_kernel", 2: "fw16_update_kernel<false>", 1: "fw_update_kernel"}[enc]
     bytes_per_launch = 2.0 * nr * ld * s_d  # round-streaming model: read + write the local rows
     relax_per_launch = float(nr) * ld * FW_B
     achieved_gbs = bytes_per_launch / (avg_upd_ms * 1e-3) / 1e9

@@ -46,13 +46,13 @@ static __device__ __forceinline__ u16x2 relax(u16x2 acc, uint32_t a2, uint32_t b
     return __builtin_elementwise_min(acc, as2(a2 + b2));
 }
 static __device__ __forceinline__ uint32_t splat(uint32_t h) { return h | (h << 16); }
-typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-/* per half: min(acc, x, y) on u16 bit patterns in [0, 0x7BFF] -> one v_pk_minimum3_f16 */
+/* per half: min(acc, x, y) on u16 bit patterns in [0, 0x7BFF] -> one v_pk_minimum3_f16.
+ * Inline asm: written with the generic minimum builtins, LLVM re-associates the chain across
+ * pivot pairs into two-input minimum3s with a duplicated operand (1.5x the min instructions). */
 static __device__ __forceinline__ uint32_t min3h(uint32_t acc, uint32_t x, uint32_t y) {
-    const h2 r = __builtin_elementwise_minimum(
-        __builtin_bit_cast(h2, acc),
-        __builtin_elementwise_minimum(__builtin_bit_cast(h2, x), __builtin_bit_cast(h2, y)));
-    return __builtin_bit_cast(uint32_t, r);
+    uint32_t r;
+    asm("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(acc), "v"(x), "v"(y));
+    return r;
 }
 template <int I>
 static __device__ __forceinline__ uint32_t lane4(const uint4& v) {
@@ -321,6 +321,159 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     store_acc16<8, 8>(acc, old, C, ld, tx, ty);
 }
 
+/* ---- f16-compare update, software-pipelined ------------------------------------------------ *
+ * Same tile as fw16_update_kernel<true> (128x128 outputs, 8x8 per thread, two 32-pivot stages)
+ * with the latencies taken off the critical path:
+ *   - the next stage's A/B slices are loaded into registers while the current stage computes;
+ *   - LDS operands of pivot pair p+1 are read while pair p computes (double-buffered registers);
+ *   - the unchanged-row test re-reads C at the end instead of holding a copy in 32 VGPRs.
+ * Per pivot pair and thread: 2 ds_read_b128 (B, 8 columns x 2 pivots) + 4 ds_read_b128 (A, 8 rows
+ * x 2 splatted pivots) feed 64 v_add_u32 + 32 v_pk_minimum3_f16 = 128 relaxations.
+ * A is laid out pivot-pair-major in LDS: word pair (splat A[r][2p], splat A[r][2p+1]) at
+ * sA[(p * 128 + r) * 2], so a thread's 4 consecutive rows are one 32-byte run (two full-rate
+ * ds_read_b128; a row-major A makes the compiler pair the reads into half-rate ds_read2_b64). */
+#define UBS (128 + 8) /* B row stride in LDS u16 */
+
+struct fwh_stage_regs {
+    uint4 a[2], b[2];
+};
+
+static __device__ __forceinline__ void fwh_gload(fwh_stage_regs& g, const u16* __restrict__ A,
+                                                 const u16* __restrict__ B, size_t ld, int tid) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int ia = tid + q * 256, ra = ia & 127, ca = (ia >> 7) * 8; /* 128 rows x 32 pivots */
+        const int ib = tid + q * 256, rb = ib >> 4, cb = (ib & 15) * 8;  /* 32 pivots x 128 cols */
+        g.a[q] = *reinterpret_cast<const uint4*>(A + (size_t)ra * ld + ca);
+        g.b[q] = *reinterpret_cast<const uint4*>(B + (size_t)rb * ld + cb);
+    }
+}
+
+static __device__ __forceinline__ void fwh_swrite(const fwh_stage_regs& g, uint32_t* __restrict__ sA,
+                                                  u16* __restrict__ sB, int tid) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int ia = tid + q * 256, ra = ia & 127, ca = (ia >> 7) * 8;
+        const int ib = tid + q * 256, rb = ib >> 4, cb = (ib & 15) * 8;
+        const uint4 v = g.a[q];
+        uint32_t* d = sA + ((ca >> 1) * 128 + ra) * 2; /* pairs ca/2 .. ca/2+3 of row ra */
+        *reinterpret_cast<uint2*>(d) = make_uint2(splat(v.x & 0xFFFFu), splat(v.x >> 16));
+        *reinterpret_cast<uint2*>(d + 256) = make_uint2(splat(v.y & 0xFFFFu), splat(v.y >> 16));
+        *reinterpret_cast<uint2*>(d + 512) = make_uint2(splat(v.z & 0xFFFFu), splat(v.z >> 16));
+        *reinterpret_cast<uint2*>(d + 768) = make_uint2(splat(v.w & 0xFFFFu), splat(v.w >> 16));
+        *reinterpret_cast<uint4*>(sB + rb * UBS + cb) = g.b[q];
+    }
+}
+
+/* LDS operand reads: B rows m, m+1 at the thread's 8 columns; A (splat pivots m, m+1) of 4 rows */
+static __device__ __forceinline__ void fwh_readB(uint4 (&b)[2], const u16* __restrict__ pb, int m) {
+    b[0] = *reinterpret_cast<const uint4*>(pb + m * UBS);
+    b[1] = *reinterpret_cast<const uint4*>(pb + (m + 1) * UBS);
+}
+static __device__ __forceinline__ void fwh_readA(uint2 (&a)[4], const uint32_t* __restrict__ pa, int m) {
+    const uint4 q0 = *reinterpret_cast<const uint4*>(pa + (m >> 1) * 256);
+    const uint4 q1 = *reinterpret_cast<const uint4*>(pa + (m >> 1) * 256 + 4);
+    a[0] = make_uint2(q0.x, q0.y);
+    a[1] = make_uint2(q0.z, q0.w);
+    a[2] = make_uint2(q1.x, q1.y);
+    a[3] = make_uint2(q1.z, q1.w);
+}
+/* rows r0..r0+3 of the thread's block, pivots m, m+1: 32 v_add_u32 + 16 v_pk_minimum3_f16 */
+template <int R0>
+static __device__ __forceinline__ void fwh_rows(uint32_t (&acc)[8][4], const uint2 (&a)[4],
+                                                const uint4 (&b)[2]) {
+    const uint32_t b0[4] = {b[0].x, b[0].y, b[0].z, b[0].w};
+    const uint32_t b1[4] = {b[1].x, b[1].y, b[1].z, b[1].w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        uint32_t t0[4], t1[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            t0[c] = a[r].x + b0[c];
+            t1[c] = a[r].y + b1[c];
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[R0 + r][c] = min3h(acc[R0 + r][c], t0[c], t1[c]);
+    }
+}
+
+#define FWH_PHASE __builtin_amdgcn_sched_barrier(0)
+static __device__ __forceinline__ void fwh_stage(uint32_t (&acc)[8][4], const uint32_t* __restrict__ sA,
+                                                 const u16* __restrict__ sB, int tx, int ty) {
+    const uint32_t* pa0 = sA + ty * 8 * 2; /* rows 0-3 of the thread's block (pair 0) */
+    const uint32_t* pa1 = pa0 + 4 * 2;     /* rows 4-7 */
+    const u16* pb = sB + tx * 8;
+    uint4 B0[2], B1[2];
+    uint2 A0[4], A1[4];
+    fwh_readB(B0, pb, 0);
+    fwh_readA(A0, pa0, 0);
+#pragma unroll 1
+    for (int m = 0; m < UKC; m += 4) {
+        /* every phase issues the reads the next phase needs, then computes on registers that
+         * were read one phase earlier (the clamped last reads are harmless re-reads) */
+        const int m2 = m + 2, m4 = min(m + 4, UKC - 2);
+        fwh_readA(A1, pa1, m);
+        FWH_PHASE;
+        fwh_rows<0>(acc, A0, B0);
+        FWH_PHASE;
+        fwh_readB(B1, pb, m2);
+        fwh_readA(A0, pa0, m2);
+        FWH_PHASE;
+        fwh_rows<4>(acc, A1, B0);
+        FWH_PHASE;
+        fwh_readA(A1, pa1, m2);
+        FWH_PHASE;
+        fwh_rows<0>(acc, A0, B1);
+        FWH_PHASE;
+        fwh_readB(B0, pb, m4);
+        fwh_readA(A0, pa0, m4);
+        FWH_PHASE;
+        fwh_rows<4>(acc, A1, B1);
+        FWH_PHASE;
+    }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void fwh_update_kernel(
+    u16* __restrict__ D, int ld, const u16* __restrict__ P, int k0, int ncol_tiles) {
+    __shared__ __attribute__((aligned(16))) uint32_t sA[UKC / 2 * 128 * 2];
+    __shared__ __attribute__((aligned(16))) u16 sB[UKC * UBS];
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int nb = gridDim.x;
+    const int per = nb >> 3;
+    const int bid = (nb & 7) == 0 ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
+    const int I = bid / ncol_tiles, J = bid % ncol_tiles;
+    u16* C = D + (size_t)I * 128 * ld + J * 128;
+    const u16* Ag = D + (size_t)I * 128 * ld + k0;
+    const u16* Bg = P + J * 128;
+    fwh_stage_regs g;
+    fwh_gload(g, Ag, Bg, ld, tid);
+    uint32_t acc[8][4];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const uint4 v = *reinterpret_cast<const uint4*>(C + (size_t)(ty * 8 + r) * ld + tx * 8);
+        acc[r][0] = v.x;
+        acc[r][1] = v.y;
+        acc[r][2] = v.z;
+        acc[r][3] = v.w;
+    }
+    fwh_swrite(g, sA, sB, tid);
+    __syncthreads();
+    fwh_gload(g, Ag + UKC, Bg + (size_t)UKC * ld, ld, tid); /* in flight during stage 0 */
+    fwh_stage(acc, sA, sB, tx, ty);
+    __syncthreads();
+    fwh_swrite(g, sA, sB, tid);
+    __syncthreads();
+    fwh_stage(acc, sA, sB, tx, ty);
+    /* store only the rows that changed (re-read: nothing else writes this tile in this launch) */
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        uint4* p = reinterpret_cast<uint4*>(C + (size_t)(ty * 8 + r) * ld + tx * 8);
+        const uint4 o = *p;
+        if (o.x != acc[r][0] || o.y != acc[r][1] || o.z != acc[r][2] || o.w != acc[r][3])
+            *p = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+    }
+}
+
 /* widen to the u32 table and flag saturation of a real pair (i, j < n) */
 __global__ void fw16_finish_kernel(int n, int ld, int row0, const u16* __restrict__ d16,
                                    uint32_t* __restrict__ lat, int* __restrict__ saturated,
@@ -364,7 +517,7 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
     u16* pbuf = panels[dev];
     const uint32_t cap = fm ? CAP_F : CAP_U;
     auto panel = fm ? fw16_panel_kernel<true> : fw16_panel_kernel<false>;
-    auto update = fm ? fw16_update_kernel<true> : fw16_update_kernel<false>;
+    auto update = fm ? fwh_update_kernel : fw16_update_kernel<false>;
     if (nrows > 0) {
         fw16_init_kernel<<<dim3(srt_ceil_div(ld, 256), nrows), 256, 0, st>>>(n, ld, row0, w_rows, d,
                                                                            cap);
