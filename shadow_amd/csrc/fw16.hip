@@ -287,10 +287,17 @@ __global__ __launch_bounds__(256) void fw16_panel_kernel(u16* __restrict__ D, in
 }
 
 /* every 128x128 tile of the local rows: D_IJ <- min(D_IJ, D_I,k (x) P_k,J) */
+/* Tile rows: I = i0 + bid / ncol_tiles, skipping tile row `skip` (-1: none) -- the lookahead
+ * schedule updates the next pivot block's tile row first and the others after it. */
+static __device__ __forceinline__ int tile_row(int bid, int ncol_tiles, int i0, int skip) {
+    const int I = i0 + bid / ncol_tiles;
+    return (skip >= 0 && I >= skip) ? I + 1 : I;
+}
+
 template <bool FM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void fw16_update_kernel(u16* __restrict__ D, int ld,
                                                           const u16* __restrict__ P, int k0,
-                                                          int ncol_tiles) {
+                                                          int ncol_tiles, int i0, int skip) {
     __shared__ __attribute__((aligned(16))) uint32_t sA[128 * (UKC + 4)];
     __shared__ __attribute__((aligned(16))) u16 sB[UKC * (128 + 8)];
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
@@ -299,7 +306,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const int nb = gridDim.x;
     const int per = nb >> 3;
     const int bid = (nb & 7) == 0 ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
-    const int I = bid / ncol_tiles, J = bid % ncol_tiles;
+    const int I = tile_row(bid, ncol_tiles, i0, skip), J = bid % ncol_tiles;
     u16* C = D + (size_t)I * 128 * ld + J * 128;
     u16x2 old[8][4], acc[8][4];
     load_acc16<8, 8>(old, C, ld, tx, ty); /* HBM reads in flight during the staging */
@@ -434,14 +441,14 @@ static __device__ __forceinline__ void fwh_stage(uint32_t (&acc)[8][4], const ui
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void fwh_update_kernel(
-    u16* __restrict__ D, int ld, const u16* __restrict__ P, int k0, int ncol_tiles) {
+    u16* __restrict__ D, int ld, const u16* __restrict__ P, int k0, int ncol_tiles, int i0, int skip) {
     __shared__ __attribute__((aligned(16))) uint32_t sA[UKC / 2 * 128 * 2];
     __shared__ __attribute__((aligned(16))) u16 sB[UKC * UBS];
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     const int nb = gridDim.x;
     const int per = nb >> 3;
     const int bid = (nb & 7) == 0 ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
-    const int I = bid / ncol_tiles, J = bid % ncol_tiles;
+    const int I = tile_row(bid, ncol_tiles, i0, skip), J = bid % ncol_tiles;
     u16* C = D + (size_t)I * 128 * ld + J * 128;
     const u16* Ag = D + (size_t)I * 128 * ld + k0;
     const u16* Bg = P + J * 128;
@@ -489,32 +496,71 @@ __global__ void fw16_finish_kernel(int n, int ld, int row0, const u16* __restric
 }
 
 #ifndef SRT_FW16_DEVICE_ONLY
-/* ---- orchestration --------------------------------------------------------------------------- */
+/* ---- orchestration --------------------------------------------------------------------------- *
+ * Lookahead schedule (one row shard per rank; a single GPU is the 1-rank case). Round k uses the
+ * 64-row pivot panel P_k (owner: in place in its rows; others: a double-buffered receive panel).
+ * Main stream st:      wait P_k ready -> pivot-column tiles of k -> update k
+ * Critical stream cs:  diagonal closure + pivot-row panel of k+1 -> broadcast P_k+1 -> P_k+1 ready
+ * On the owner of k+1 the update of round k is split: the 128-row tile row holding block k+1 goes
+ * first, cs starts the k+1 panel as soon as it is done, and the remaining tile rows of round k
+ * overlap the panel work and the RCCL broadcast. A receive panel is overwritten only after the
+ * update that last read it (round k-1) has finished.
+ * Without a broadcast to hide (one GPU) the split and the cross-stream events cost more than the
+ * overlap returns (C2: 1.01 -> 1.34 ms), so the single-GPU build runs the same rounds on one stream
+ * in order; SRT_FW_LOOKAHEAD=1 forces the two-stream schedule (tests exercise it on one GPU). */
+typedef struct {
+    hipStream_t cs;
+    hipEvent_t ready[2], row_done, upd_done[2], init_done;
+    int ok;
+} fw16_sched;
+
+static int sched_get(fw16_sched** out, int dev) {
+    static fw16_sched sc[64];
+    fw16_sched* x = &sc[dev & 63];
+    if (!x->ok) {
+        int lo = 0, hi = 0;
+        SRT_HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        SRT_HIPCHK(hipStreamCreateWithPriority(&x->cs, hipStreamNonBlocking, hi));
+        for (int i = 0; i < 2; ++i) {
+            SRT_HIPCHK(hipEventCreateWithFlags(&x->ready[i], hipEventDisableTiming));
+            SRT_HIPCHK(hipEventCreateWithFlags(&x->upd_done[i], hipEventDisableTiming));
+        }
+        SRT_HIPCHK(hipEventCreateWithFlags(&x->row_done, hipEventDisableTiming));
+        SRT_HIPCHK(hipEventCreateWithFlags(&x->init_done, hipEventDisableTiming));
+        x->ok = 1;
+    }
+    *out = x;
+    return SRT_OK;
+}
+
 int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,
                    hipStream_t st, evpool_t* evp, srt_owner_fn owner_of, srt_panel_bcast_fn bcast,
                    void* ctx, int rank, int fm, int* exact) {
-    if (ld % 128 || nrows % 128) {
+    if (ld % 128 || nrows % 128 || row0 % 128) {
         srt_set_error("u16 FW needs ld and the row shard to be multiples of 128");
         return SRT_E_ARG;
     }
     static u16* bufs[64];
     static size_t caps[64];
-    static u16* panels[64];
     static int* flags[64];
     int dev = 0;
     SRT_HIPCHK(hipGetDevice(&dev));
     dev &= 63;
-    const size_t need = (size_t)nrows * ld + (size_t)KB * ld;
+    const size_t need = (size_t)nrows * ld + 2 * (size_t)KB * ld;
     if (caps[dev] < need) {
         if (bufs[dev]) SRT_HIPCHK(hipFree(bufs[dev]));
         SRT_HIPCHK(hipMalloc(&bufs[dev], need * sizeof(u16)));
         caps[dev] = need;
-        panels[dev] = bufs[dev] + (size_t)nrows * ld;
     }
-    panels[dev] = bufs[dev] + (size_t)nrows * ld;
     if (!flags[dev]) SRT_HIPCHK(hipMalloc(&flags[dev], sizeof(int)));
+    fw16_sched* sc;
+    int rc = sched_get(&sc, dev);
+    if (rc) return rc;
+    const char* la_env = getenv("SRT_FW_LOOKAHEAD");
+    const bool lookahead = la_env ? atoi(la_env) != 0 : bcast != NULL;
+    hipStream_t cs = lookahead ? sc->cs : st;
     u16* d = bufs[dev];
-    u16* pbuf = panels[dev];
+    u16* pbuf[2] = {bufs[dev] + (size_t)nrows * ld, bufs[dev] + (size_t)nrows * ld + (size_t)KB * ld};
     const uint32_t cap = fm ? CAP_F : CAP_U;
     auto panel = fm ? fw16_panel_kernel<true> : fw16_panel_kernel<false>;
     auto update = fm ? fwh_update_kernel : fw16_update_kernel<false>;
@@ -524,28 +570,59 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
         SRT_HIPCHK(hipGetLastError());
     }
     const int nb = ld / KB, nrb = nrows / KB, ncol128 = ld / 128, nrow128 = nrows / 128;
-    for (int k0 = 0; k0 < ld; k0 += KB) {
-        const int owner = owner_of ? owner_of(ctx, k0) : rank;
-        u16* P;
-        if (owner == rank) {
-            P = d + (size_t)(k0 - row0) * ld;
-            fw16_diag_kernel<<<1, 256, 0, st>>>(P, ld, k0);
-            panel<<<nb, 256, 0, st>>>(d, ld, row0, nrb, P, k0, nb, 1, 0);
+    const int rounds = ld / KB;
+    auto owner = [&](int k) { return owner_of ? owner_of(ctx, k * KB) : rank; };
+    auto panel_of = [&](int k) -> u16* {
+        return owner(k) == rank ? d + (size_t)(k * KB - row0) * ld : pbuf[k & 1];
+    };
+    /* critical-stream part of round k: owner closes the diagonal tile and the pivot-row panel,
+     * then every rank takes part in the broadcast; P_k ready is signalled on cs */
+    auto produce = [&](int k) -> int {
+        u16* P = panel_of(k);
+        if (owner(k) == rank) {
+            fw16_diag_kernel<<<1, 256, 0, cs>>>(P, ld, k * KB);
+            panel<<<nb, 256, 0, cs>>>(d, ld, row0, nrb, P, k * KB, nb, 1, 0);
             SRT_HIPCHK(hipGetLastError());
-        } else {
-            P = pbuf;
+        } else if (k >= 2 && lookahead) {
+            SRT_HIPCHK(hipStreamWaitEvent(cs, sc->upd_done[k & 1], 0)); /* round k-2 read it */
         }
         if (bcast) {
-            int rc = bcast(ctx, P, (size_t)KB * ld * sizeof(u16), owner, st);
-            if (rc) return rc;
+            int r = bcast(ctx, P, (size_t)KB * ld * sizeof(u16), owner(k), cs);
+            if (r) return r;
         }
+        if (lookahead) SRT_HIPCHK(hipEventRecord(sc->ready[k & 1], cs));
+        return SRT_OK;
+    };
+    if (lookahead) {
+        SRT_HIPCHK(hipEventRecord(sc->init_done, st));
+        SRT_HIPCHK(hipStreamWaitEvent(cs, sc->init_done, 0));
+    }
+    if ((rc = produce(0))) return rc;
+    for (int k = 0; k < rounds; ++k) {
+        const int k0 = k * KB;
+        u16* P = panel_of(k);
+        if (lookahead) SRT_HIPCHK(hipStreamWaitEvent(st, sc->ready[k & 1], 0));
+        const bool next = k + 1 < rounds;
+        const int skip =
+            (lookahead && next && owner(k + 1) == rank) ? ((k + 1) * KB - row0) / 128 : -1;
         if (nrb > 0) {
             panel<<<nb + nrb, 256, 0, st>>>(d, ld, row0, nrb, P, k0, nb, 0, 1);
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
-            update<<<ncol128 * nrow128, 256, 0, st>>>(d, ld, P, k0, ncol128);
+            if (skip >= 0) {
+                update<<<ncol128, 256, 0, st>>>(d, ld, P, k0, ncol128, skip, -1);
+                SRT_HIPCHK(hipEventRecord(sc->row_done, st));
+                SRT_HIPCHK(hipStreamWaitEvent(cs, sc->row_done, 0));
+                if ((rc = produce(k + 1))) return rc;
+                if (nrow128 > 1)
+                    update<<<ncol128 * (nrow128 - 1), 256, 0, st>>>(d, ld, P, k0, ncol128, 0, skip);
+            } else {
+                update<<<ncol128 * nrow128, 256, 0, st>>>(d, ld, P, k0, ncol128, 0, -1);
+            }
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
             SRT_HIPCHK(hipGetLastError());
         }
+        if (lookahead) SRT_HIPCHK(hipEventRecord(sc->upd_done[k & 1], st));
+        if (next && skip < 0 && (rc = produce(k + 1))) return rc;
     }
     SRT_HIPCHK(hipMemsetAsync(flags[dev], 0, sizeof(int), st));
     if (nrows > 0)

@@ -2,7 +2,8 @@
 
 The GPU path (srt_dense_build_sharded / srt_sparse_allgather) runs one process per GPU over
 RCCL. Here the same schedule -- the library's own srt_shard_rows partition, the owner of each
-64-row pivot block, one pivot-panel broadcast per round, the essential-arc all-reduce/broadcast,
+64-row pivot block, one pivot-panel broadcast per round in the lookahead order (panel k+1 is
+produced from a partially updated round k), the essential-arc all-reduce/broadcast,
 the undirected mirror exchange (rank q sends rel[q rows][r cols] to every r > q) and the sparse
 source-shard all-gather -- is replayed with numpy compute and gloo collectives, and the
 assembled tables must equal the CPU oracle's.
@@ -60,10 +61,14 @@ def _dense_worker(rank, R, port, n, seed, q):
     for i in range(b, e):
         D[i - b, i] = 0
     owners = [_shard(L, ld, R, x) for x in range(R)]
-    for k0 in range(0, ld, KB):
-        owner = [x for x, (qb, qe) in enumerate(owners) if qb <= k0 < qe][0]
+
+    def owner(k0):
+        return [x for x, (qb, qe) in enumerate(owners) if qb <= k0 < qe][0]
+
+    def produce(k0):
+        """diagonal closure + pivot-row panel of block k0 (owner), broadcast to every rank"""
         P = torch.zeros((KB, ld), dtype=torch.int64)
-        if owner == rank:
+        if owner(k0) == rank:
             Pk = D[k0 - b:k0 - b + KB]
             T = Pk[:, k0:k0 + KB]
             for m in range(KB):  # diagonal closure
@@ -71,13 +76,34 @@ def _dense_worker(rank, R, port, n, seed, q):
             Pk[:, k0:k0 + KB] = T
             Pk[:] = np.minimum(Pk, _minplus(T, Pk))  # row panel
             P = torch.from_numpy(Pk.copy())
-        dist.broadcast(P, owner)
-        Pn = P.numpy()
+        dist.broadcast(P, owner(k0))
+        return P.numpy()
+
+    def update(Pn, k0, rows):
+        sel = np.zeros(e - b, bool)
+        sel[rows] = True
+        D[sel] = np.minimum(D[sel], _minplus(D[sel][:, k0:k0 + KB], Pn))
+
+    # lookahead order of srt_fw16_build (fw16.hip): the owner of block k+1 updates the 128-row
+    # tile row holding it first, produces and broadcasts panel k+1, then updates the other rows
+    Pn = produce(0)
+    for k0 in range(0, ld, KB):
         Dkk = Pn[:, k0:k0 + KB]
         mine = np.array([not (k0 <= b + i < k0 + KB) for i in range(e - b)])
         col = D[:, k0:k0 + KB]
         col[mine] = np.minimum(col[mine], _minplus(col[mine], Dkk))  # column panel
-        D[mine] = np.minimum(D[mine], _minplus(D[mine][:, k0:k0 + KB], Pn))
+        k1 = k0 + KB
+        rows = np.arange(e - b)
+        if k1 < ld and owner(k1) == rank:
+            t0 = (k1 - b) // ALIGN * ALIGN
+            first = rows[t0:t0 + ALIGN]
+            update(Pn, k0, first)
+            Pnext = produce(k1)
+            update(Pn, k0, np.setdiff1d(rows, first))
+        else:
+            update(Pn, k0, rows)
+            Pnext = produce(k1) if k1 < ld else None
+        Pn = Pnext
     # essential arcs (W[u][t] == D[u][t], u != t) of the local rows; all-reduce the counts
     cnt = torch.zeros(ld, dtype=torch.int64)
     arcs = {}
@@ -178,7 +204,7 @@ def _sparse_worker(rank, R, port, q):
 
 @pytest.mark.timeout(600)
 def test_dense_sharded_schedule_gloo(native):
-    n, seed, R = 200, 6, 2
+    n, seed, R = 400, 6, 2  # ld 512: two 128-row tile rows per rank, so the split update is real
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

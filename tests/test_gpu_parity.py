@@ -215,3 +215,38 @@ def test_dense_distance_encoding_tiers(gpu, hop_ms, enc):
     exp = _oracle(g)
     assert_tables(got_lat, got_rel, exp["lat_int"], exp["rel"], f"hop {hop_ms} ms")
     assert st.dist_enc == enc, f"expected encoding {enc}, build used {st.dist_enc}"
+
+
+@pytest.mark.parametrize("n,seed", [(700, 8), (1000, 2)])
+def test_dense_lookahead_schedule_one_gpu(gpu, monkeypatch, n, seed):
+    """The two-stream lookahead schedule of the sharded FW (fw16.hip srt_fw16_build: split update,
+    pivot panel k+1 on the high-priority stream, double-buffered receive panels) forced on one GPU
+    must give the oracle's tables, through both the single-GPU and the 1-rank sharded entry."""
+    import torch
+    from shadow_amd._lib import lib
+    monkeypatch.setenv("SRT_FW_LOOKAHEAD", "1")
+    ld = (n + 127) // 128 * 128
+    L = lib()
+    w = torch.empty((ld, ld), dtype=torch.int32, device="cuda")
+    r = torch.empty((ld, ld), dtype=torch.float64, device="cuda")
+    assert L.srt_gen_complete_device(n, ld, 0, ld, seed, 300, 10, 500, w.data_ptr(), r.data_ptr(),
+                                     None) == 0
+    exp = _oracle(graphs.complete_graph(n, seed=seed))
+    lat = torch.empty_like(w)
+    rel = torch.empty_like(r)
+    assert L.srt_dense_build_device(n, ld, 0, w.data_ptr(), r.data_ptr(), lat.data_ptr(),
+                                    rel.data_ptr(), None, 0, None) == 0
+    torch.cuda.synchronize()
+    lat_ns = lat[:n, :n].cpu().numpy().view(np.uint32).astype(np.uint64) * np.uint64(MS)
+    assert_tables(lat_ns, rel[:n, :n].cpu().numpy(), exp["lat_int"], exp["rel"], "lookahead")
+    uid = (ctypes.c_uint8 * 128)()
+    assert L.srt_comm_unique_id(uid) == 0
+    comm = ctypes.c_void_p()
+    assert L.srt_comm_init(uid, 1, 0, torch.cuda.current_device(), ctypes.byref(comm)) == 0
+    lat2 = torch.empty_like(w)
+    rel2 = torch.empty_like(r)
+    assert L.srt_dense_build_sharded(comm, n, ld, 0, w.data_ptr(), r.data_ptr(), lat2.data_ptr(),
+                                     rel2.data_ptr(), None, 0, None) == 0
+    torch.cuda.synchronize()
+    L.srt_comm_free(comm)
+    assert torch.equal(lat2[:n, :n], lat[:n, :n]) and torch.equal(rel2[:n, :n], rel[:n, :n])
