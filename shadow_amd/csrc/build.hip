@@ -110,11 +110,20 @@ struct srt_sparse_graph {
     int32_t n, directed;
     int64_t arcs;
     uint64_t quantum_ns;
-    uint32_t delta;
+    uint32_t delta, max_w;
     int32_t *rp, *col, *irp, *icol;
     uint32_t *w, *iw, *sw;
     double *r, *ir, *sr;
+    uint2 *cw, *icw; /* packed (col, w) arcs for the wave-per-source kernel */
 };
+
+int srt_wsssp_rows(int n, int directed, const int32_t* rowptr, const uint2* cw, const double* r,
+                   const int32_t* in_rowptr, const uint2* in_cw, const double* in_r,
+                   uint32_t max_w, int src_begin, int src_end, uint32_t* lat, double* rel,
+                   int* ovf, hipStream_t st);
+int srt_sparse_diag(int n, int src_begin, int src_end, const int32_t* rowptr, const int32_t* col,
+                    const uint32_t* w, const double* r, const uint32_t* self_w,
+                    const double* self_r, uint32_t* lat, double* rel, size_t ldo, hipStream_t st);
 
 static int up(void** d, const void* h, size_t bytes) {
     *d = NULL;
@@ -135,11 +144,11 @@ extern "C" void srt_sparse_graph_free(srt_sparse_graph* g) {
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(g->device);
-    void* ps[] = {g->rp, g->col, g->w, g->r, g->sw, g->sr};
+    void* ps[] = {g->rp, g->col, g->w, g->r, g->sw, g->sr, g->cw};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (g->directed) {
-        void* qs[] = {g->irp, g->icol, g->iw, g->ir};
+        void* qs[] = {g->irp, g->icol, g->iw, g->ir, g->icw};
         for (void* p : qs)
             if (p) (void)hipFree(p);
     }
@@ -156,6 +165,8 @@ static int sparse_graph_from_canon(const srt_canon* c, int device, srt_sparse_gr
     g->directed = c->directed;
     g->arcs = c->arcs;
     g->quantum_ns = c->quantum_ns;
+    g->max_w = 0;
+    for (int64_t k = 0; k < c->arcs; k++) g->max_w = c->w[k] > g->max_w ? c->w[k] : g->max_w;
     /* bucket width of the label-correcting loop: the mean arc weight */
     double sumw = 0;
     for (int64_t k = 0; k < c->arcs; k++) sumw += c->w[k];
@@ -169,17 +180,29 @@ static int sparse_graph_from_canon(const srt_canon* c, int device, srt_sparse_gr
     if (!rc) rc = up((void**)&g->r, c->r, na * 8);
     if (!rc) rc = up((void**)&g->sw, c->self_w, nv * 4);
     if (!rc) rc = up((void**)&g->sr, c->self_r, nv * 8);
+    uint2* hcw = (uint2*)malloc((na ? na : 1) * sizeof(uint2));
+    if (!hcw && !rc) rc = SRT_E_NOMEM;
+    if (!rc) {
+        for (size_t k = 0; k < na; k++) hcw[k] = make_uint2((uint32_t)c->col[k], c->w[k]);
+        rc = up((void**)&g->cw, hcw, na * sizeof(uint2));
+    }
     if (c->directed) {
         if (!rc) rc = up((void**)&g->irp, c->in_rowptr, n1 * 4);
         if (!rc) rc = up((void**)&g->icol, c->in_col, na * 4);
         if (!rc) rc = up((void**)&g->iw, c->in_w, na * 4);
         if (!rc) rc = up((void**)&g->ir, c->in_r, na * 8);
+        if (!rc) {
+            for (size_t k = 0; k < na; k++) hcw[k] = make_uint2((uint32_t)c->in_col[k], c->in_w[k]);
+            rc = up((void**)&g->icw, hcw, na * sizeof(uint2));
+        }
     } else {
         g->irp = g->rp;
         g->icol = g->col;
         g->iw = g->w;
         g->ir = g->r;
+        g->icw = g->cw;
     }
+    free(hcw);
     if (rc) {
         srt_sparse_graph_free(g);
         return rc;
@@ -214,6 +237,10 @@ extern "C" int srt_sparse_graph_info(const srt_sparse_graph* g, int32_t* n, int3
     return SRT_OK;
 }
 
+/* Rows of a source range: the wave-per-source bucket kernel (wsssp.hip) when the arc weights fit
+ * its bucket ring, with any source whose buckets overflowed recomputed by the
+ * workgroup-per-source kernel (sparse.hip); SRT_SPARSE_KERNEL=block (or SRT_SPARSE_WORKSET=hbm)
+ * selects the workgroup kernel for every source. */
 extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src_end,
                                      uint32_t* lat_rows, double* rel_rows, void* stream,
                                      srt_build_stats* stats) {
@@ -221,9 +248,64 @@ extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begi
         srt_set_error("srt_sparse_graph_rows: null graph");
         return SRT_E_ARG;
     }
-    return srt_sparse_build_device(g->n, g->directed, g->rp, g->col, g->w, g->r, g->irp, g->icol,
-                                   g->iw, g->ir, g->sw, g->sr, src_begin, src_end, g->delta,
-                                   lat_rows, rel_rows, stream, stats);
+    const char* kenv = getenv("SRT_SPARSE_KERNEL");
+    const char* wenv = getenv("SRT_SPARSE_WORKSET");
+    const bool block = (kenv && !strcmp(kenv, "block")) || (wenv && !strcmp(wenv, "hbm"));
+    if (block || g->max_w >= 256 || src_begin < 0 || src_end > g->n || src_begin >= src_end)
+        return srt_sparse_build_device(g->n, g->directed, g->rp, g->col, g->w, g->r, g->irp,
+                                       g->icol, g->iw, g->ir, g->sw, g->sr, src_begin, src_end,
+                                       g->delta, lat_rows, rel_rows, stream, stats);
+    hipStream_t st = (hipStream_t)stream;
+    const int nsrc = src_end - src_begin;
+    int* ovf = NULL;
+    SRT_HIPCHK(hipMallocAsync((void**)&ovf, (size_t)nsrc * sizeof(int), st));
+    hipEvent_t e0, e1, e2;
+    SRT_HIPCHK(hipEventCreate(&e0));
+    SRT_HIPCHK(hipEventCreate(&e1));
+    SRT_HIPCHK(hipEventCreate(&e2));
+    SRT_HIPCHK(hipEventRecord(e0, st));
+    int rc = srt_wsssp_rows(g->n, g->directed, g->rp, g->cw, g->r, g->irp, g->icw, g->ir, g->max_w,
+                            src_begin, src_end, lat_rows, rel_rows, ovf, st);
+    if (rc) return rc;
+    SRT_HIPCHK(hipEventRecord(e1, st));
+    rc = srt_sparse_diag(g->n, src_begin, src_end, g->rp, g->col, g->w, g->r, g->sw, g->sr,
+                         lat_rows, rel_rows, (size_t)g->n, st);
+    if (rc) return rc;
+    int* hov = (int*)malloc((size_t)nsrc * sizeof(int));
+    if (!hov) return SRT_E_NOMEM;
+    SRT_HIPCHK(hipMemcpyAsync(hov, ovf, (size_t)nsrc * sizeof(int), hipMemcpyDeviceToHost, st));
+    SRT_HIPCHK(hipFreeAsync(ovf, st));
+    SRT_HIPCHK(hipStreamSynchronize(st));
+    int nov = 0;
+    for (int i = 0; i < nsrc && !rc; i++) {
+        if (!hov[i]) continue;
+        ++nov;
+        rc = srt_sparse_build_device(g->n, g->directed, g->rp, g->col, g->w, g->r, g->irp, g->icol,
+                                     g->iw, g->ir, g->sw, g->sr, src_begin + i, src_begin + i + 1,
+                                     g->delta, lat_rows + (size_t)i * g->n,
+                                     rel_rows + (size_t)i * g->n, stream, NULL);
+    }
+    free(hov);
+    if (rc) return rc;
+    SRT_HIPCHK(hipEventRecord(e2, st));
+    SRT_HIPCHK(hipEventSynchronize(e2));
+    float a = 0, b = 0;
+    SRT_HIPCHK(hipEventElapsedTime(&a, e0, e1));
+    SRT_HIPCHK(hipEventElapsedTime(&b, e0, e2));
+    SRT_HIPCHK(hipEventDestroy(e0));
+    SRT_HIPCHK(hipEventDestroy(e1));
+    SRT_HIPCHK(hipEventDestroy(e2));
+    if (nov) srt_log(SRT_LOG_INFO, "wsssp: %d of %d sources overflowed their buckets and were "
+                     "recomputed by the workgroup kernel", nov, nsrc);
+    if (stats) {
+        stats->algo = SRT_ALGO_SPARSE_SSSP;
+        stats->ms_fw = b;
+        stats->ms_total = b;
+        stats->n_update = 1;
+        stats->ms_update = a;
+        stats->ess_arcs = nov; /* sparse builds: sources recomputed after a bucket overflow */
+    }
+    return SRT_OK;
 }
 
 extern "C" int srt_build_tables(const srt_edges* g, const srt_build_opts* opts, uint32_t* lat_q,

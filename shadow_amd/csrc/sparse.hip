@@ -248,6 +248,16 @@ __global__ void sparse_diag_kernel(int n, int src_begin, int src_end, const int3
     }
 }
 
+/* host wrapper so the wave-per-source kernel (wsssp.hip) shares the diagonal rule */
+int srt_sparse_diag(int n, int src_begin, int src_end, const int32_t* rowptr, const int32_t* col,
+                    const uint32_t* w, const double* r, const uint32_t* self_w,
+                    const double* self_r, uint32_t* lat, double* rel, size_t ldo, hipStream_t st) {
+    sparse_diag_kernel<<<srt_ceil_div(src_end - src_begin, 256), 256, 0, st>>>(
+        n, src_begin, src_end, rowptr, col, w, r, self_w, self_r, lat, rel, ldo);
+    SRT_HIPCHK(hipGetLastError());
+    return SRT_OK;
+}
+
 size_t srt_sparse_lds_bytes(int n) {
     const int nwords = (n + 31) / 32;
     const int a_words = n > 2 * nwords ? n : 2 * nwords;

@@ -82,3 +82,44 @@ def test_hbm_workset_forced_full_tables(gpu, monkeypatch, which):
     assert np.array_equal(lat, exp["lat_int"])
     err = np.abs(rel - exp["rel"]) / np.maximum(np.abs(exp["rel"]), 1e-300)
     assert float(err.max()) <= REL_TOL
+
+
+@pytest.mark.parametrize("which", ["rgg3000", "directed"])
+@pytest.mark.parametrize("bcap", ["3", "64"])
+def test_wave_kernel_bucket_overflow_fallback(gpu, monkeypatch, which, bcap):
+    """Wave-per-source bucket kernel (wsssp.hip) with tiny bucket capacities: sources whose
+    buckets overflow are recomputed by the workgroup kernel, and the table stays exact."""
+    monkeypatch.setenv("SRT_WSSSP_BCAP", bcap)
+    if which == "rgg3000":
+        g = graphs.random_geometric(3000, seed=3)
+    else:
+        rng = np.random.default_rng(12)
+        n, m = 400, 3000
+        ring = np.arange(n)
+        src = np.concatenate([rng.integers(0, n, m), ring, ring]).astype(np.int32)
+        dst = np.concatenate([rng.integers(0, n, m), (ring + 1) % n, ring]).astype(np.int32)
+        lat = (rng.integers(1, 20, len(src)) * 1_000_000).astype(np.int64)
+        loss = rng.integers(0, 300, len(src)) / 10000.0
+        g = graphs.Graph(n, True, src, dst, lat, loss)
+    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                algo=ALGO_SPARSE_SSSP)
+    exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss),
+                       True, oracle.ORC_INT_NS, 8)
+    assert np.array_equal(lat, exp["lat_int"])
+    err = np.abs(rel - exp["rel"]) / np.maximum(np.abs(exp["rel"]), 1e-300)
+    assert float(err.max()) <= REL_TOL
+    if bcap == "3":
+        assert st.ess_arcs > 0, "expected some sources to overflow and be recomputed"
+
+
+def test_wave_kernel_matches_block_kernel_c3_rows(gpu, monkeypatch):
+    """The two sparse kernels agree bit for bit on C3-shaped rows (the wave kernel is the default,
+    SRT_SPARSE_KERNEL=block selects the workgroup kernel)."""
+    import torch
+    g = graphs.random_geometric(20000, seed=3)
+    sg = SparseGraph(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
+    a = _rows_on_gpu(sg, 5000, 5256, torch)
+    monkeypatch.setenv("SRT_SPARSE_KERNEL", "block")
+    b = _rows_on_gpu(sg, 5000, 5256, torch)
+    sg.free()
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
