@@ -328,7 +328,8 @@ def run_sparse(c: Ctx, wl):
     s0st = stats[-1]
     config = {"workload": wl["desc"], "n": n, "edges": int(g.m), "arcs": int(arcs),
               "parallelism": f"source-shard x{world}" + (" + RCCL allgather" if world > 1 else ""),
-              "sources_per_rank": nsrc, "max_tree_depth": int(s0st.max_depth),
+              "sources_per_rank": nsrc,
+              "sources_recomputed_after_bucket_overflow": int(s0st.ess_arcs),
               "ms_sssp": round(s0st.ms_fw, 3)}
     return elapsed, "u32", "strong", config, roofline, cpu, parity
 

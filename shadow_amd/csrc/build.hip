@@ -12,6 +12,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+
 #include "srt_device.h"
 
 int srt_sparse_max_n(void);
@@ -115,12 +117,18 @@ struct srt_sparse_graph {
     uint32_t *w, *iw, *sw;
     double *r, *ir, *sr;
     uint2 *cw, *icw; /* packed (col, w) arcs for the wave-per-source kernel */
+    /* the same graph relabelled in Cuthill-McKee order for the wave-per-source kernel: perm[new] =
+     * old, inv[old] = new; rows keep their arcs sorted by ORIGINAL neighbour index */
+    int32_t *perm, *inv;
+    int2 *rp2, *irp2; /* (begin, end) of each relabelled row */
+    uint2 *cw2, *icw2;
+    double *r2, *ir2;
 };
 
-int srt_wsssp_rows(int n, int directed, const int32_t* rowptr, const uint2* cw, const double* r,
-                   const int32_t* in_rowptr, const uint2* in_cw, const double* in_r,
-                   uint32_t max_w, int src_begin, int src_end, uint32_t* lat, double* rel,
-                   int* ovf, hipStream_t st);
+int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, const double* r,
+                   const int2* in_rowptr, const uint2* in_cw, const double* in_r,
+                   const int32_t* perm, const int32_t* inv, uint32_t max_w, int src_begin,
+                   int src_end, uint32_t* lat, double* rel, int* ovf, hipStream_t st);
 int srt_sparse_diag(int n, int src_begin, int src_end, const int32_t* rowptr, const int32_t* col,
                     const uint32_t* w, const double* r, const uint32_t* self_w,
                     const double* self_r, uint32_t* lat, double* rel, size_t ldo, hipStream_t st);
@@ -144,16 +152,82 @@ extern "C" void srt_sparse_graph_free(srt_sparse_graph* g) {
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(g->device);
-    void* ps[] = {g->rp, g->col, g->w, g->r, g->sw, g->sr, g->cw};
+    void* ps[] = {g->rp, g->col, g->w, g->r, g->sw, g->sr, g->cw, g->perm, g->inv, g->rp2, g->cw2, g->r2};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (g->directed) {
-        void* qs[] = {g->irp, g->icol, g->iw, g->ir, g->icw};
+        void* qs[] = {g->irp, g->icol, g->iw, g->ir, g->icw, g->irp2, g->icw2, g->ir2};
         for (void* p : qs)
             if (p) (void)hipFree(p);
     }
     (void)hipSetDevice(prev);
     free(g);
+}
+
+/* Cuthill-McKee order of the undirected structure (out-arcs, plus in-arcs when directed):
+ * breadth-first from the lowest-degree unvisited vertex, neighbours in increasing degree. */
+static int cuthill_mckee(const srt_canon* c, int32_t* perm, int32_t* inv) {
+    const int n = c->n;
+    int32_t* deg = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+    int32_t* byd = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+    int32_t* nb = (int32_t*)malloc((size_t)(c->arcs * (c->directed ? 2 : 1) + 1) * sizeof(int32_t));
+    if (!deg || !byd || !nb) {
+        free(deg);
+        free(byd);
+        free(nb);
+        return SRT_E_NOMEM;
+    }
+    for (int v = 0; v < n; v++) {
+        deg[v] = c->rowptr[v + 1] - c->rowptr[v];
+        if (c->directed) deg[v] += c->in_rowptr[v + 1] - c->in_rowptr[v];
+        byd[v] = v;
+        inv[v] = -1;
+    }
+    std::stable_sort(byd, byd + n, [&](int32_t a, int32_t b) { return deg[a] < deg[b]; });
+    int head = 0, tail = 0, next_start = 0;
+    while (tail < n) {
+        while (inv[byd[next_start]] >= 0) next_start++;
+        const int st = byd[next_start];
+        inv[st] = tail;
+        perm[tail++] = st;
+        while (head < tail) {
+            const int v = perm[head++];
+            int m = 0;
+            for (int k = c->rowptr[v]; k < c->rowptr[v + 1]; k++)
+                if (inv[c->col[k]] < 0) nb[m++] = c->col[k];
+            if (c->directed)
+                for (int k = c->in_rowptr[v]; k < c->in_rowptr[v + 1]; k++)
+                    if (inv[c->in_col[k]] < 0) nb[m++] = c->in_col[k];
+            std::stable_sort(nb, nb + m, [&](int32_t a, int32_t b) {
+                return deg[a] != deg[b] ? deg[a] < deg[b] : a < b;
+            });
+            for (int i = 0; i < m; i++) {
+                if (inv[nb[i]] >= 0) continue; /* duplicate (out- and in-neighbour) */
+                inv[nb[i]] = tail;
+                perm[tail++] = nb[i];
+            }
+        }
+    }
+    free(deg);
+    free(byd);
+    free(nb);
+    return SRT_OK;
+}
+
+/* CSR rows in relabelled order; each row keeps its arcs in original-neighbour order */
+static void relabel_csr(int n, const int32_t* rp, const int32_t* col, const uint32_t* w,
+                        const double* r, const int32_t* perm, const int32_t* inv, int2* rp2,
+                        uint2* cw2, double* r2) {
+    int o = 0;
+    for (int i = 0; i < n; i++) {
+        const int v = perm[i];
+        const int b = o;
+        for (int k = rp[v]; k < rp[v + 1]; k++, o++) {
+            cw2[o] = make_uint2((uint32_t)inv[col[k]], w[k]);
+            r2[o] = r[k];
+        }
+        rp2[i] = make_int2(b, o);
+    }
 }
 
 static int sparse_graph_from_canon(const srt_canon* c, int device, srt_sparse_graph** out) {
@@ -202,6 +276,35 @@ static int sparse_graph_from_canon(const srt_canon* c, int device, srt_sparse_gr
         g->ir = g->r;
         g->icw = g->cw;
     }
+    /* relabelled copy for the wave-per-source kernel */
+    int32_t* hperm = (int32_t*)malloc(nv * sizeof(int32_t));
+    int32_t* hinv = (int32_t*)malloc(nv * sizeof(int32_t));
+    int2* hrp = (int2*)malloc(nv * sizeof(int2));
+    double* hr = (double*)malloc((na ? na : 1) * sizeof(double));
+    if (!rc && (!hperm || !hinv || !hrp || !hr || !hcw)) rc = SRT_E_NOMEM;
+    if (!rc) rc = cuthill_mckee(c, hperm, hinv);
+    if (!rc) {
+        relabel_csr(c->n, c->rowptr, c->col, c->w, c->r, hperm, hinv, hrp, hcw, hr);
+        rc = up((void**)&g->perm, hperm, nv * 4);
+        if (!rc) rc = up((void**)&g->inv, hinv, nv * 4);
+        if (!rc) rc = up((void**)&g->rp2, hrp, nv * sizeof(int2));
+        if (!rc) rc = up((void**)&g->cw2, hcw, na * sizeof(uint2));
+        if (!rc) rc = up((void**)&g->r2, hr, na * 8);
+    }
+    if (!rc && c->directed) {
+        relabel_csr(c->n, c->in_rowptr, c->in_col, c->in_w, c->in_r, hperm, hinv, hrp, hcw, hr);
+        rc = up((void**)&g->irp2, hrp, nv * sizeof(int2));
+        if (!rc) rc = up((void**)&g->icw2, hcw, na * sizeof(uint2));
+        if (!rc) rc = up((void**)&g->ir2, hr, na * 8);
+    } else if (!rc) {
+        g->irp2 = g->rp2;
+        g->icw2 = g->cw2;
+        g->ir2 = g->r2;
+    }
+    free(hperm);
+    free(hinv);
+    free(hrp);
+    free(hr);
     free(hcw);
     if (rc) {
         srt_sparse_graph_free(g);
@@ -264,8 +367,9 @@ extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begi
     SRT_HIPCHK(hipEventCreate(&e1));
     SRT_HIPCHK(hipEventCreate(&e2));
     SRT_HIPCHK(hipEventRecord(e0, st));
-    int rc = srt_wsssp_rows(g->n, g->directed, g->rp, g->cw, g->r, g->irp, g->icw, g->ir, g->max_w,
-                            src_begin, src_end, lat_rows, rel_rows, ovf, st);
+    int rc = srt_wsssp_rows(g->n, g->directed, g->rp2, g->cw2, g->r2, g->irp2, g->icw2, g->ir2,
+                            g->perm, g->inv, g->max_w, src_begin, src_end, lat_rows, rel_rows, ovf,
+                            st);
     if (rc) return rc;
     SRT_HIPCHK(hipEventRecord(e1, st));
     rc = srt_sparse_diag(g->n, src_begin, src_end, g->rp, g->col, g->w, g->r, g->sw, g->sr,

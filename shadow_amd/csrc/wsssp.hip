@@ -17,9 +17,14 @@
  * For undirected graphs the out-arcs scanned to relax t's neighbours are also t's in-arcs, so one
  * pass over them does both; directed graphs scan the in-arc CSR separately.
  *
- * Memory: the distance row is the output lat row (u32 quanta, L2-coherent loads and atomics),
- * the rel row is the output rel row; buckets live in a per-wave global slot (C x bcap vertex ids);
- * bucket counts and the non-empty mask live in LDS. A bucket overflow flags the source and the
+ * Vertex order: the kernel runs on a Cuthill-McKee relabelling of the graph (build.hip), so a
+ * frontier's neighbours sit in nearby words of the working distance row and each random access
+ * shares cache lines with the next ones (the C3 profile without it: 28% L2 hits, 245 GB fetched
+ * for 44 GB of algorithmic bytes). Arcs of a relabelled row stay sorted by ORIGINAL neighbour
+ * index, so the (D[u], arc index) key still breaks ties by original vertex index.
+ * Memory: a per-wave working distance row (u32 quanta, relabelled order, L2-coherent loads and
+ * atomics) and bucket ring (C x bcap vertex ids) in global memory; bucket counts and the
+ * non-empty mask in LDS. Settled values go straight to the output rows in original order. A bucket overflow flags the source and the
  * caller recomputes it with the workgroup-per-source kernel (sparse.hip) -- never approximate.
  *
  * Arc work inside one step is balanced across lanes merge-path style: the settled vertices of a
@@ -30,11 +35,14 @@
 
 #define WL 64
 
+/* Every row a wave touches is private to its workgroup (one wave), so workgroup-scope relaxed
+ * atomic loads are coherent with the wave's own stores and atomics and may be served by the
+ * CU's L1 / the XCD's L2 (agent scope would send every load past the per-XCD L2). */
 static __device__ __forceinline__ uint32_t ld_coherent(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 static __device__ __forceinline__ double ld_coherent(const double* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 static __device__ __forceinline__ int wave_scan_excl(int v, int lane, int* total) {
@@ -57,12 +65,13 @@ static __device__ __forceinline__ int wave_scan_max(int v, int lane) {
     return v;
 }
 
-template <bool DIRECTED>
+template <bool DIRECTED, bool LDSD>
 __global__ __launch_bounds__(WL) void wsssp_kernel(
-    int n, int src_begin, int nsrc, const int32_t* __restrict__ rowptr,
+    int n, int src_begin, int nsrc, const int2* __restrict__ rowptr,
     const uint2* __restrict__ cw, const double* __restrict__ r,
-    const int32_t* __restrict__ in_rowptr, const uint2* __restrict__ in_cw,
-    const double* __restrict__ in_r, uint32_t* __restrict__ lat, double* __restrict__ rel,
+    const int2* __restrict__ in_rowptr, const uint2* __restrict__ in_cw,
+    const double* __restrict__ in_r, const int32_t* __restrict__ perm,
+    const int32_t* __restrict__ inv, uint32_t* __restrict__ lat, double* __restrict__ rel,
     size_t ldo, uint32_t* __restrict__ ws, int nb, int bcap, int* __restrict__ overflow) {
     __shared__ uint32_t bcnt[256];
     __shared__ unsigned long long bmask[4];
@@ -70,15 +79,22 @@ __global__ __launch_bounds__(WL) void wsssp_kernel(
     __shared__ unsigned long long s_best[WL];
     __shared__ int s_ovf;
     const int lane = threadIdx.x;
-    uint32_t* buckets = ws + (size_t)blockIdx.x * nb * bcap;
+    extern __shared__ uint32_t sdist[]; /* LDSD: the working row lives in LDS */
+    uint32_t* buckets = ws + (size_t)blockIdx.x * ((size_t)nb * bcap + (LDSD ? 0 : n));
+    uint32_t* dist = LDSD ? sdist : buckets + (size_t)nb * bcap; /* working row, relabelled */
+    auto dload = [&](uint32_t i) -> uint32_t {
+        if constexpr (LDSD) return sdist[i];
+        else return ld_coherent(dist + i);
+    };
     const uint32_t bmaskm = (uint32_t)nb - 1u;
 
     for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
-        const int s = src_begin + si;
-        uint32_t* dist = lat + (size_t)si * ldo;
+        const int s = inv[src_begin + si];
+        uint32_t* ol = lat + (size_t)si * ldo; /* output rows, original order */
         double* rr = rel + (size_t)si * ldo;
         for (int v = lane; v < n; v += WL) {
             dist[v] = (v == s) ? 0u : SRT_INF;
+            ol[v] = SRT_INF;
             rr[v] = 0.0;
         }
         for (int b = lane; b < nb; b += WL) bcnt[b] = 0;
@@ -120,9 +136,10 @@ __global__ __launch_bounds__(WL) void wsssp_kernel(
                 int v = -1, beg = 0, deg = 0;
                 if (i < cnt) {
                     v = (int)ld_coherent(bk + i);
-                    if (ld_coherent(dist + v) == d) {
-                        beg = rowptr[v];
-                        deg = rowptr[v + 1] - beg;
+                    if (dload((uint32_t)v) == d) {
+                        const int2 be = rowptr[v];
+                        beg = be.x;
+                        deg = be.y - be.x;
                     } else {
                         v = -1; /* stale: improved after it was pushed */
                     }
@@ -148,10 +165,13 @@ __global__ __launch_bounds__(WL) void wsssp_kernel(
                         const int k = s_beg[own] + (a - s_excl[own]);
                         const uint2 e = cw[k];
                         const uint32_t u = e.x, wk = e.y;
-                        const uint32_t du = ld_coherent(dist + u);
+                        const uint32_t du = dload(u);
                         const uint32_t nd = d + wk;
                         if (nd < du) {
-                            const uint32_t old = atomicMin(dist + u, nd);
+                            const uint32_t old =
+                                LDSD ? atomicMin(sdist + u, nd)
+                                     : __hip_atomic_fetch_min(dist + u, nd, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_WORKGROUP);
                             if (nd < old) {
                                 const int b2 = (int)(nd & bmaskm);
                                 const int slot = (int)atomicAdd(&bcnt[b2], 1u);
@@ -172,8 +192,9 @@ __global__ __launch_bounds__(WL) void wsssp_kernel(
                     /* tight in-arcs (u -> v): the same merge-path walk over the in-CSR */
                     int ibeg = 0, ideg = 0;
                     if (v >= 0) {
-                        ibeg = in_rowptr[v];
-                        ideg = in_rowptr[v + 1] - ibeg;
+                        const int2 be = in_rowptr[v];
+                        ibeg = be.x;
+                        ideg = be.y - be.x;
                     }
                     int itotal;
                     const int iexcl = wave_scan_excl(ideg, lane, &itotal);
@@ -194,7 +215,7 @@ __global__ __launch_bounds__(WL) void wsssp_kernel(
                         if (a < itotal && own >= 0) {
                             const int k = s_beg[own] + (a - s_excl[own]);
                             const uint2 e = in_cw[k];
-                            const uint32_t du = ld_coherent(dist + e.x);
+                            const uint32_t du = dload(e.x);
                             if (du < SRT_INF && du + e.y == d)
                                 atomicMin(&s_best[own], ((unsigned long long)du << 32) | (uint32_t)k);
                         }
@@ -213,10 +234,12 @@ __global__ __launch_bounds__(WL) void wsssp_kernel(
                         if (key != ~0ull) {
                             const int k = (int)(uint32_t)key;
                             const uint32_t u = DIRECTED ? in_cw[k].x : cw[k].x;
-                            x = ld_coherent(rr + u) * (DIRECTED ? in_r[k] : r[k]);
+                            x = ld_coherent(rr + perm[u]) * (DIRECTED ? in_r[k] : r[k]);
                         }
                     }
-                    rr[v] = x;
+                    const int vo = perm[v];
+                    ol[vo] = d;
+                    rr[vo] = x;
                 }
                 __threadfence_block(); /* settled rel visible to the later steps of this wave */
                 __syncthreads();
@@ -235,10 +258,10 @@ int srt_sparse_diag(int n, int src_begin, int src_end, const int32_t* rowptr, co
 /* Rows [src_begin, src_end) by the wave-per-source kernel. *overflowed receives the number of
  * sources whose buckets overflowed; their indices (relative to src_begin) are flagged in ovf
  * (device, nsrc ints, zeroed here) for the caller to recompute. */
-int srt_wsssp_rows(int n, int directed, const int32_t* rowptr, const uint2* cw, const double* r,
-                   const int32_t* in_rowptr, const uint2* in_cw, const double* in_r,
-                   uint32_t max_w, int src_begin, int src_end, uint32_t* lat, double* rel,
-                   int* ovf, hipStream_t st) {
+int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, const double* r,
+                   const int2* in_rowptr, const uint2* in_cw, const double* in_r,
+                   const int32_t* perm, const int32_t* inv, uint32_t max_w, int src_begin,
+                   int src_end, uint32_t* lat, double* rel, int* ovf, hipStream_t st) {
     int nb = 1;
     while ((uint32_t)nb <= max_w) nb <<= 1;
     if (nb > 256) {
@@ -254,10 +277,21 @@ int srt_wsssp_rows(int n, int directed, const int32_t* rowptr, const uint2* cw, 
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
         cus = prop.multiProcessorCount;
-    /* 16 waves per CU, bounded by an 8 GiB bucket workspace */
-    const size_t per_slot = (size_t)nb * bcap * sizeof(uint32_t);
-    size_t slots = (size_t)16 * cus;
-    const size_t budget = (size_t)8 << 30;
+    /* working distance row in LDS when it fits (LDS atomics and gathers instead of divergent
+     * global ones -- the global form is bound by the texture path at one line per lane), else a
+     * global row with up to SRT_WSSSP_WAVES (default 16) waves per CU */
+    const size_t lds_row = (size_t)n * sizeof(uint32_t), lds_static = 4096;
+    const char* lenv = getenv("SRT_WSSSP_LDS");
+    /* the LDS form holds few waves per CU and each wave's bucket steps are a latency chain
+     * (C3, n = 20000: 2 waves/CU, 354 ms vs 70 ms for the global form at 16), so it is the
+     * default only while it still fits 8 waves per CU; SRT_WSSSP_LDS=1/0 forces either form */
+    const bool ldsd = lenv ? (atoi(lenv) != 0 && lds_row + lds_static <= 160 * 1024)
+                           : 8 * (lds_row + lds_static) <= 160 * 1024;
+    const size_t per_slot = ((size_t)nb * bcap + (ldsd ? 0 : n)) * sizeof(uint32_t);
+    const char* wenv = getenv("SRT_WSSSP_WAVES");
+    size_t slots = ldsd ? (size_t)cus * ((160 * 1024) / (lds_row + lds_static))
+                        : (size_t)(wenv && atoi(wenv) > 0 ? atoi(wenv) : 16) * cus;
+    const size_t budget = (size_t)16 << 30;
     if (slots * per_slot > budget) slots = budget / per_slot;
     if (slots > (size_t)nsrc) slots = nsrc;
     if (slots < 1) slots = 1;
@@ -268,14 +302,22 @@ int srt_wsssp_rows(int n, int directed, const int32_t* rowptr, const uint2* cw, 
         return SRT_E_NOMEM;
     }
     SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)nsrc * sizeof(int), st));
-    if (directed)
-        wsssp_kernel<true><<<(unsigned)slots, WL, 0, st>>>(n, src_begin, nsrc, rowptr, cw, r, in_rowptr,
-                                                           in_cw, in_r, lat, rel, (size_t)n, ws, nb,
-                                                           bcap, ovf);
-    else
-        wsssp_kernel<false><<<(unsigned)slots, WL, 0, st>>>(n, src_begin, nsrc, rowptr, cw, r, in_rowptr,
-                                                            in_cw, in_r, lat, rel, (size_t)n, ws, nb,
-                                                            bcap, ovf);
+    const size_t dyn = ldsd ? lds_row : 0;
+#define SRT_WSSSP_LAUNCH(D, L)                                                                   \
+    do {                                                                                         \
+        if (dyn) SRT_HIPCHK(hipFuncSetAttribute((const void*)wsssp_kernel<D, L>,                  \
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,       \
+                                                (int)dyn));                                       \
+        wsssp_kernel<D, L><<<(unsigned)slots, WL, dyn, st>>>(n, src_begin, nsrc, rowptr, cw, r,   \
+                                                            in_rowptr, in_cw, in_r, perm, inv,    \
+                                                            lat, rel, (size_t)n, ws, nb, bcap,    \
+                                                            ovf);                                 \
+    } while (0)
+    if (directed && ldsd) SRT_WSSSP_LAUNCH(true, true);
+    else if (directed) SRT_WSSSP_LAUNCH(true, false);
+    else if (ldsd) SRT_WSSSP_LAUNCH(false, true);
+    else SRT_WSSSP_LAUNCH(false, false);
+#undef SRT_WSSSP_LAUNCH
     SRT_HIPCHK(hipGetLastError());
     SRT_HIPCHK(hipFreeAsync(ws, st));
     return SRT_OK;

@@ -123,3 +123,31 @@ def test_wave_kernel_matches_block_kernel_c3_rows(gpu, monkeypatch):
     b = _rows_on_gpu(sg, 5000, 5256, torch)
     sg.free()
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("which", ["rgg3000", "ba2000", "directed"])
+@pytest.mark.parametrize("lds", ["0", "1"])
+def test_wave_kernel_working_row_forms(gpu, monkeypatch, which, lds):
+    """SRT_WSSSP_LDS=0/1: the wave kernel's working distance row in global memory or in LDS gives
+    the same exact tables."""
+    monkeypatch.setenv("SRT_WSSSP_LDS", lds)
+    if which == "rgg3000":
+        g = graphs.random_geometric(3000, seed=3)
+    elif which == "ba2000":
+        g = graphs.barabasi_albert(2000, seed=5)
+    else:
+        rng = np.random.default_rng(12)
+        n, m = 400, 3000
+        ring = np.arange(n)
+        src = np.concatenate([rng.integers(0, n, m), ring, ring]).astype(np.int32)
+        dst = np.concatenate([rng.integers(0, n, m), (ring + 1) % n, ring]).astype(np.int32)
+        lat = (rng.integers(1, 20, len(src)) * 1_000_000).astype(np.int64)
+        loss = rng.integers(0, 300, len(src)) / 10000.0
+        g = graphs.Graph(n, True, src, dst, lat, loss)
+    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                algo=ALGO_SPARSE_SSSP)
+    exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss),
+                       True, oracle.ORC_INT_NS, 8)
+    assert np.array_equal(lat, exp["lat_int"])
+    err = np.abs(rel - exp["rel"]) / np.maximum(np.abs(exp["rel"]), 1e-300)
+    assert float(err.max()) <= REL_TOL
