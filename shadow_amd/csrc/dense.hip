@@ -414,11 +414,10 @@ __global__ void arc_transpose_fill(int n, const int32_t* __restrict__ ptr,
 /* transpose of the local row block. Blocks are mapped so that each XCD works on its own      */
 /* source block at a time (its 8 MB column slab stays in that XCD's L2 / the Infinity Cache). */
 /* ------------------------------------------------------------------------------------------ */
-__global__ __launch_bounds__(256) void transpose_u32_kernel(int rows, int cols,
-                                                            const uint32_t* __restrict__ in,
-                                                            size_t ldi, uint32_t* __restrict__ out,
-                                                            size_t ldo) {
-    __shared__ uint32_t tile[64][65];
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, const T* __restrict__ in,
+                                                        size_t ldi, T* __restrict__ out, size_t ldo) {
+    __shared__ T tile[64][65];
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
     for (int a = ty; a < 64; a += 4) {
@@ -432,12 +431,17 @@ __global__ __launch_bounds__(256) void transpose_u32_kernel(int rows, int cols,
     }
 }
 
+template <typename T, bool UR>
 __global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nloc, int ldT,
-                                                        const uint32_t* __restrict__ DT,
+                                                        const T* __restrict__ DT,
                                                         const int32_t* __restrict__ iptr,
                                                         const uint2* __restrict__ uw,
-                                                        int32_t* __restrict__ predT, int nsb,
+                                                        const double* __restrict__ ar,
+                                                        int32_t* __restrict__ predT,
+                                                        double* __restrict__ rT, int nsb,
                                                         int tch, int tper) {
+    /* UR: write the predecessor vertex and the reliability of its arc (predT, rT) for the
+     * level-order pass; otherwise the arc index for the sweep pass */
     const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
     const int sb = (j / tch) * 8 + xcd, tc = j % tch;
     if (sb >= nsb) return;
@@ -453,60 +457,86 @@ __global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nlo
         const int ke = __builtin_amdgcn_readfirstlane(iptr[t + 1]);
         uint64_t best = ~0ull;
         int bk = -1;
+        double br = 0.0;
         int k = kb;
-        for (; k + 4 <= ke; k += 4) {
-            const uint2 a0 = uw[k], a1 = uw[k + 1], a2 = uw[k + 2], a3 = uw[k + 3];
-            const uint32_t d0 = DT[(size_t)a0.x * ldT + sl], d1 = DT[(size_t)a1.x * ldT + sl];
-            const uint32_t d2 = DT[(size_t)a2.x * ldT + sl], d3 = DT[(size_t)a3.x * ldT + sl];
-#define SRT_PRED_TRY(dd, aa, kk)                                                  \
+#define SRT_PRED_TRY(dd, aa, kk, rk)                                              \
     if ((dd) + (aa).y == dst) {                                                   \
         const uint64_t key = ((uint64_t)(dd) << 32) | (aa).x;                     \
         if (key < best) {                                                         \
             best = key;                                                           \
             bk = (kk);                                                            \
+            if (UR) br = (rk);                                                    \
         }                                                                         \
     }
-            SRT_PRED_TRY(d0, a0, k)
-            SRT_PRED_TRY(d1, a1, k + 1)
-            SRT_PRED_TRY(d2, a2, k + 2)
-            SRT_PRED_TRY(d3, a3, k + 3)
+        for (; k + 4 <= ke; k += 4) {
+            const uint2 a0 = uw[k], a1 = uw[k + 1], a2 = uw[k + 2], a3 = uw[k + 3];
+            double r0 = 0, r1 = 0, r2 = 0, r3 = 0; /* wave-uniform: scalar loads */
+            if (UR) {
+                r0 = ar[k];
+                r1 = ar[k + 1];
+                r2 = ar[k + 2];
+                r3 = ar[k + 3];
+            }
+            const uint32_t d0 = DT[(size_t)a0.x * ldT + sl], d1 = DT[(size_t)a1.x * ldT + sl];
+            const uint32_t d2 = DT[(size_t)a2.x * ldT + sl], d3 = DT[(size_t)a3.x * ldT + sl];
+            SRT_PRED_TRY(d0, a0, k, r0)
+            SRT_PRED_TRY(d1, a1, k + 1, r1)
+            SRT_PRED_TRY(d2, a2, k + 2, r2)
+            SRT_PRED_TRY(d3, a3, k + 3, r3)
         }
         for (; k < ke; ++k) {
             const uint2 a0 = uw[k];
+            const double r0 = UR ? ar[k] : 0.0;
             const uint32_t d0 = DT[(size_t)a0.x * ldT + sl];
-            SRT_PRED_TRY(d0, a0, k)
+            SRT_PRED_TRY(d0, a0, k, r0)
         }
 #undef SRT_PRED_TRY
-        if (valid) predT[(size_t)t * ldT + sl] = (s == t) ? -1 : bk;
+        if (valid) {
+            const size_t o = (size_t)t * ldT + sl;
+            if (UR) {
+                predT[o] = (s == t || bk < 0) ? -1 : (int32_t)(uint32_t)best;
+                rT[o] = br;
+            } else {
+                predT[o] = (s == t) ? -1 : bk;
+            }
+        }
     }
 }
 
-/* Path-order reliability, one workgroup per local source row:
- * rel(s,t) = rel(s,pred) * r(pred,t), rel(s,s) = 1 -> the product in the order of
- * topology.c:1364-1365. Sweeps until every target of the row is resolved (tree depth). */
-__global__ __launch_bounds__(512) void rel_rows_kernel(int n, int ld, int row0,
-                                                       const int32_t* __restrict__ pred,
-                                                       const int32_t* __restrict__ icol,
-                                                       const double* __restrict__ ir,
-                                                       double* __restrict__ rel,
-                                                       int32_t* __restrict__ max_depth) {
-    extern __shared__ __attribute__((aligned(16))) int32_t arc[];
+/* Path-order reliability by sweeps for rows with a large distance range (rel_levels_kernel
+ * flagged them), one workgroup per row, same in-place (u, r) input. A target resolves once its
+ * predecessor resolved in an earlier sweep (double-buffered LDS bitmaps; the sweeps = the depth
+ * of the row's predecessor tree). */
+__global__ __launch_bounds__(512) void rel_sweeps_kernel(int n, int ld, int row0,
+                                                         const int32_t* __restrict__ pred,
+                                                         double* __restrict__ rel,
+                                                         int32_t* __restrict__ max_depth,
+                                                         const int32_t* __restrict__ only) {
+    extern __shared__ __attribute__((aligned(16))) int32_t smem[];
     const int s = row0 + blockIdx.x;
-    if (s >= n) return;
+    if (s >= n || !only[blockIdx.x]) return;
+    const int nw = (n + 31) >> 5;
+    int32_t* pu = smem;                                   /* n predecessor vertices */
+    uint32_t* done = reinterpret_cast<uint32_t*>(smem + n); /* resolved before this sweep */
+    uint32_t* fresh = done + nw;                           /* resolved during this sweep */
     const int32_t* pg = pred + (size_t)blockIdx.x * ld;
-    for (int t = threadIdx.x; t < n; t += blockDim.x) arc[t] = pg[t];
     double* rr = rel + (size_t)blockIdx.x * ld;
+    for (int t = threadIdx.x; t < n; t += blockDim.x) pu[t] = pg[t];
+    for (int q = threadIdx.x; q < nw; q += blockDim.x) {
+        done[q] = 0u;
+        fresh[q] = 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        done[s >> 5] = 1u << (s & 31);
+        __hip_atomic_store(rr + s, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     /* each thread owns t = tid + i*blockDim (i < 64 for n <= 32768) */
     uint64_t pending = 0;
     int nt = 0;
-    for (int t = threadIdx.x; t < n; t += blockDim.x, ++nt) {
-        if (t == s) {
-            rr[t] = 1.0;
-        } else {
-            rr[t] = -1.0;
-            pending |= 1ull << nt;
-        }
-    }
+    for (int t = threadIdx.x; t < n; t += blockDim.x, ++nt)
+        if (t != s && pu[t] >= 0) pending |= 1ull << nt;
+    __threadfence_block();
     __syncthreads();
     int depth = 0;
     for (;;) {
@@ -514,26 +544,74 @@ __global__ __launch_bounds__(512) void rel_rows_kernel(int n, int ld, int row0,
         int i = 0;
         for (int t = threadIdx.x; t < n; t += blockDim.x, ++i) {
             if (!((pending >> i) & 1ull)) continue;
-            const int k = arc[t];
-            if (k < 0) { /* unreachable (cannot happen on a validated graph) */
-                rr[t] = 0.0;
-                pending &= ~(1ull << i);
+            const int u = pu[t];
+            if (!((done[u >> 5] >> (u & 31)) & 1u)) {
+                any = 1;
                 continue;
             }
-            const double rp = __hip_atomic_load(rr + icol[k], __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (rp >= 0.0) {
-                __hip_atomic_store(rr + t, rp * ir[k], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-                pending &= ~(1ull << i);
-            } else {
-                any = 1;
-            }
+            const double ru = __hip_atomic_load(rr + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const double rt = __hip_atomic_load(rr + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(rr + t, ru * rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            atomicOr(&fresh[t >> 5], 1u << (t & 31));
+            pending &= ~(1ull << i);
         }
         ++depth;
+        __threadfence_block();
         if (!__syncthreads_or(any)) break;
+        for (int q = threadIdx.x; q < nw; q += blockDim.x) {
+            done[q] |= fresh[q];
+            fresh[q] = 0u;
+        }
+        __syncthreads();
     }
     if (threadIdx.x == 0) atomicMax(max_depth, depth);
+}
+
+/* Reliability in increasing-distance order, one workgroup per local source row, in place: the
+ * rel row arrives holding r(pred(s,t), t) and the pred row the predecessor vertex (pred_cols
+ * UR form). Every arc is >= 1 quantum, so D[s][pred] < D[s][t] and pass L (targets with
+ * D[s][t] == L) only reads values final since an earlier pass: each entry is formed once,
+ * rel(s,t) = rel(s,pred) * r(pred,t), the left-to-right product of topology.c:1364-1365.
+ * Rows whose largest distance exceeds maxl passes are flagged for rel_sweeps_kernel. */
+__global__ __launch_bounds__(512) void rel_levels_kernel(int n, int ld, int row0,
+                                                         const uint32_t* __restrict__ lat,
+                                                         const int32_t* __restrict__ pred,
+                                                         double* __restrict__ rel, int maxl,
+                                                         int32_t* __restrict__ max_depth,
+                                                         int32_t* __restrict__ sweep) {
+    const int s = row0 + blockIdx.x;
+    if (s >= n) return;
+    const uint32_t* dl = lat + (size_t)blockIdx.x * ld;
+    const int32_t* pg = pred + (size_t)blockIdx.x * ld;
+    double* rr = rel + (size_t)blockIdx.x * ld;
+    __shared__ uint32_t red[8];
+    uint32_t mx = 0;
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        const uint32_t x = dl[t];
+        if (t != s && x < SRT_INF) mx = max(mx, x);
+    }
+    for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    if (threadIdx.x == 0) __hip_atomic_store(rr + s, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __threadfence_block();
+    __syncthreads();
+    mx = 0;
+    for (int i = 0; i < 8; ++i) mx = max(mx, red[i]);
+    if (threadIdx.x == 0) sweep[blockIdx.x] = (int)mx > maxl;
+    if ((int)mx > maxl) return; /* long distance range: rel_sweeps_kernel takes the row */
+    for (uint32_t L = 1; L <= mx; ++L) {
+        for (int t = threadIdx.x; t < n; t += blockDim.x) {
+            if (t == s || dl[t] != L) continue;
+            const int u = pg[t];
+            if (u < 0) continue; /* unreachable (cannot happen on a validated graph) */
+            const double ru = __hip_atomic_load(rr + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const double rt = __hip_atomic_load(rr + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(rr + t, ru * rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicMax(max_depth, (int)mx);
 }
 
 __global__ void pack_uw_kernel(int64_t arcs, const int32_t* __restrict__ col,
@@ -643,6 +721,8 @@ typedef struct {
     uint32_t* dt;   /* transpose of the local row block, then the predecessor rows */
     int32_t* predt; /* predecessors, sources across columns */
     size_t dt_cap, predt_cap;
+    double* rt; /* reliability of each predecessor arc, sources across columns */
+    size_t rt_cap;
 } dense_ws;
 
 static dense_ws g_ws[64];
@@ -696,8 +776,9 @@ typedef int (*ess_gather_fn)(void* ctx, dense_ws* ws, int n, int phase, int32_t 
                              hipStream_t st);
 
 static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_t directed,
-                      const uint32_t* w, const double* r, uint32_t* d, double* rel, hipStream_t st,
-                      srt_build_stats* stats, ess_gather_fn gather, void* gctx) {
+                      const uint32_t* w, const double* r, uint32_t* d, const uint16_t* d16,
+                      double* rel, hipStream_t st, srt_build_stats* stats, ess_gather_fn gather,
+                      void* gctx) {
     dense_ws* ws;
     int rc = ws_get(&ws, n);
     if (rc) return rc;
@@ -758,24 +839,46 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         ws->uw_cap = c3;
         if (total > 0)
             pack_uw_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, icol, iw, ws->uw);
-        /* DT[u][sl] = D[row0 + sl][u] */
-        transpose_u32_kernel<<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)), 256, 0, st>>>(
-            nrows, ld, d, (size_t)ld, ws->dt, (size_t)nrows);
+        /* DT[u][sl] = D[row0 + sl][u], from the u16 working matrix when the build kept one
+         * (half the bytes per candidate arc: the predecessor search is bound by these reads).
+         * With small distances (every local one <= 64 quanta) the search also emits the arc
+         * reliability and the reliability pass runs in level order in place; otherwise it emits
+         * arc indices for the sweep pass. */
         const int nsb = nrows / 64;
         const int tch = max(1, min(n, 256));
         const int tper = srt_ceil_div(n, tch);
         const int grid = srt_ceil_div(nsb, 8) * 8 * tch;
-        pred_cols_kernel<<<grid, 256, 0, st>>>(n, row0, lrows, nrows, ws->dt, iptr, ws->uw,
-                                               ws->predt, nsb, tch, tper);
-        /* predecessor rows: pred[sl][t] = predT[t][sl] (reuses the DT buffer) */
+        size_t c4 = ws->rt_cap;
+        if ((rc = ws_grow((void**)&ws->rt, &c4, slab, sizeof(double)))) return rc;
+        ws->rt_cap = c4;
+        if (d16) {
+            uint16_t* dt16 = reinterpret_cast<uint16_t*>(ws->dt);
+            transpose_kernel<uint16_t><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)), 256, 0,
+                                         st>>>(nrows, ld, d16, (size_t)ld, dt16, (size_t)nrows);
+            pred_cols_kernel<uint16_t, true><<<grid, 256, 0, st>>>(
+                n, row0, lrows, nrows, dt16, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper);
+        } else {
+            transpose_kernel<uint32_t><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)), 256, 0,
+                                         st>>>(nrows, ld, d, (size_t)ld, ws->dt, (size_t)nrows);
+            pred_cols_kernel<uint32_t, true><<<grid, 256, 0, st>>>(
+                n, row0, lrows, nrows, ws->dt, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper);
+        }
+        /* predecessor rows pred[sl][t] = predT[t][sl] (reuses the DT buffer) and the arc
+         * reliabilities straight into the rel rows, where the passes below finish them in place */
         int32_t* pred = reinterpret_cast<int32_t*>(ws->dt);
-        transpose_u32_kernel<<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+        transpose_kernel<uint32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
             n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows,
             reinterpret_cast<uint32_t*>(pred), (size_t)ld);
-        const size_t lds = (size_t)ld * sizeof(int32_t);
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_rows_kernel,
+        transpose_kernel<double><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+            n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
+        /* level order for rows whose distances span <= 64 quanta, sweeps for the rest
+         * (ws->cursor is free here and carries the per-row hand-over flags) */
+        rel_levels_kernel<<<lrows, 512, 0, st>>>(n, ld, row0, d, pred, rel, 64, ws->depth,
+                                                 ws->cursor);
+        const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        rel_rows_kernel<<<lrows, 512, lds, st>>>(n, ld, row0, pred, icol, ir, rel, ws->depth);
+        rel_sweeps_kernel<<<lrows, 512, lds, st>>>(n, ld, row0, pred, rel, ws->depth, ws->cursor);
         SRT_HIPCHK(hipGetLastError());
     }
     if (stats) {
@@ -803,8 +906,9 @@ static int dense_finish_rows(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
 }
 
 int srt_dense_post_device(int32_t n, int32_t ld, int32_t directed, const uint32_t* w, const double* r,
-                          uint32_t* d, double* rel, hipStream_t st, srt_build_stats* stats) {
-    int rc = dense_post(n, ld, 0, ld, directed, w, r, d, rel, st, stats, NULL, NULL);
+                          uint32_t* d, const uint16_t* d16, double* rel, hipStream_t st,
+                          srt_build_stats* stats) {
+    int rc = dense_post(n, ld, 0, ld, directed, w, r, d, d16, rel, st, stats, NULL, NULL);
     if (rc) return rc;
     if (!directed) {
         dim3 g(srt_ceil_div(n, 64), srt_ceil_div(n, 64));
@@ -854,7 +958,8 @@ extern "C" int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, c
         if (rc) return rc;
     }
     SRT_HIPCHK(hipEventRecord(e1, st));
-    rc = srt_dense_post_device(n, ld, directed, w, r, lat, rel, st, stats);
+    rc = srt_dense_post_device(n, ld, directed, w, r, lat, exact ? srt_fw16_matrix() : NULL, rel,
+                               st, stats);
     if (rc) return rc;
     SRT_HIPCHK(hipEventRecord(e2, st));
     if (stats) {
@@ -1091,7 +1196,8 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
         }
     }
     SRT_HIPCHK(hipEventRecord(e1, st));
-    rc = dense_post(n, ld, b, nr, directed, w_rows, r_rows, lat_rows, rel_rows, st, stats,
+    rc = dense_post(n, ld, b, nr, directed, w_rows, r_rows, lat_rows,
+                    exact ? srt_fw16_matrix() : NULL, rel_rows, st, stats,
                     R > 1 ? shard_gather : NULL, &ctx);
     if (rc) return rc;
     if (!directed) {

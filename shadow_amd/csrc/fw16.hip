@@ -333,13 +333,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
  * with the latencies taken off the critical path:
  *   - the next stage's A/B slices are loaded into registers while the current stage computes;
  *   - LDS operands of pivot pair p+1 are read while pair p computes (double-buffered registers);
- *   - the unchanged-row test re-reads C at the end instead of holding a copy in 32 VGPRs.
+ *   - the unchanged-row test compares per-row sums of the u16 values (8 VGPRs) instead of
+ *     holding a copy of C in 32 VGPRs or reading it again from HBM.
  * Per pivot pair and thread: 2 ds_read_b128 (B, 8 columns x 2 pivots) + 4 ds_read_b128 (A, 8 rows
  * x 2 splatted pivots) feed 64 v_add_u32 + 32 v_pk_minimum3_f16 = 128 relaxations.
  * A is laid out pivot-pair-major in LDS: word pair (splat A[r][2p], splat A[r][2p+1]) at
  * sA[(p * 128 + r) * 2], so a thread's 4 consecutive rows are one 32-byte run (two full-rate
  * ds_read_b128; a row-major A makes the compiler pair the reads into half-rate ds_read2_b64). */
 #define UBS (128 + 8) /* B row stride in LDS u16 */
+
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+/* sum of the eight u16 values of a thread-row (four packed words): 4 x v_dot2_u32_u16 */
+static __device__ __forceinline__ uint32_t rowsum16(const uint32_t (&w)[4]) {
+    const us2 one = {1, 1};
+    uint32_t s = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) s = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, w[c]), one, s, false);
+    return s;
+}
 
 struct fwh_stage_regs {
     uint4 a[2], b[2];
@@ -463,6 +474,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         acc[r][2] = v.z;
         acc[r][3] = v.w;
     }
+    /* unchanged-row test without a 32-VGPR copy of C or a second HBM read of it: values only
+     * decrease, so a row changed iff the sum of its eight u16 values decreased (v_dot2_u32_u16) */
+    uint32_t sum0[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) sum0[r] = rowsum16(acc[r]);
     fwh_swrite(g, sA, sB, tid);
     __syncthreads();
     fwh_gload(g, Ag + UKC, Bg + (size_t)UKC * ld, ld, tid); /* in flight during stage 0 */
@@ -471,14 +487,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     fwh_swrite(g, sA, sB, tid);
     __syncthreads();
     fwh_stage(acc, sA, sB, tx, ty);
-    /* store only the rows that changed (re-read: nothing else writes this tile in this launch) */
+    /* store only the rows that changed */
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        uint4* p = reinterpret_cast<uint4*>(C + (size_t)(ty * 8 + r) * ld + tx * 8);
-        const uint4 o = *p;
-        if (o.x != acc[r][0] || o.y != acc[r][1] || o.z != acc[r][2] || o.w != acc[r][3])
-            *p = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
-    }
+    for (int r = 0; r < 8; ++r)
+        if (rowsum16(acc[r]) != sum0[r])
+            *reinterpret_cast<uint4*>(C + (size_t)(ty * 8 + r) * ld + tx * 8) =
+                make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
 }
 
 /* widen to the u32 table and flag saturation of a real pair (i, j < n) */
@@ -508,6 +522,15 @@ __global__ void fw16_finish_kernel(int n, int ld, int row0, const u16* __restric
  * Without a broadcast to hide (one GPU) the split and the cross-stream events cost more than the
  * overlap returns (C2: 1.01 -> 1.34 ms), so the single-GPU build runs the same rounds on one stream
  * in order; SRT_FW_LOOKAHEAD=1 forces the two-stream schedule (tests exercise it on one GPU). */
+/* per-device u16 working matrix of the last build (rows of the shard, ld columns); the dense
+ * post pass reads it transposed for the predecessor search (half the bytes of the u32 table) */
+static u16* fw16_bufs[64];
+const uint16_t* srt_fw16_matrix(void) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return NULL;
+    return fw16_bufs[dev & 63];
+}
+
 typedef struct {
     hipStream_t cs;
     hipEvent_t ready[2], row_done, upd_done[2], init_done;
@@ -540,7 +563,7 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
         srt_set_error("u16 FW needs ld and the row shard to be multiples of 128");
         return SRT_E_ARG;
     }
-    static u16* bufs[64];
+    u16** bufs = fw16_bufs;
     static size_t caps[64];
     static int* flags[64];
     int dev = 0;
@@ -552,7 +575,7 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
         SRT_HIPCHK(hipMalloc(&bufs[dev], need * sizeof(u16)));
         caps[dev] = need;
     }
-    if (!flags[dev]) SRT_HIPCHK(hipMalloc(&flags[dev], sizeof(int)));
+    if (!flags[dev]) SRT_HIPCHK(hipMalloc(&flags[dev], 2 * sizeof(int)));
     fw16_sched* sc;
     int rc = sched_get(&sc, dev);
     if (rc) return rc;

@@ -93,11 +93,13 @@ typedef int (*srt_owner_fn)(void* ctx, int k0);
 int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,
                    hipStream_t st, evpool_t* evp, srt_owner_fn owner_of, srt_panel_bcast_fn bcast,
                    void* ctx, int rank, int fm, int* exact);
+/* the u16 working matrix of the last srt_fw16_build on the current device (row shard x ld) */
+const uint16_t* srt_fw16_matrix(void);
 /* distance encodings of the dense build, reported (negated) in srt_build_stats.fw_block */
 enum { SRT_DENC_U32 = 1, SRT_DENC_U16 = 2, SRT_DENC_F16CMP = 3 };
 
 int srt_dense_post_device(int32_t n, int32_t ld, int32_t directed, const uint32_t* w,
-                          const double* r, uint32_t* d, double* rel, hipStream_t st,
-                          srt_build_stats* stats);
+                          const double* r, uint32_t* d, const uint16_t* d16, double* rel,
+                          hipStream_t st, srt_build_stats* stats);
 
 #endif
