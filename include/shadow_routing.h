@@ -83,6 +83,14 @@ typedef struct srt_build_stats {
 int srt_build_tables(const srt_edges* g, const srt_build_opts* opts, uint32_t* lat_q,
                      uint64_t* quantum_ns, double* rel, srt_build_stats* stats);
 
+/* srt_build_tables over `ngpus` GPUs of this process (one host thread per GPU, RCCL over xGMI):
+ * dense graphs shard rows with the pivot-panel broadcast, sparse graphs shard sources and
+ * all-gather. The in-process form Shadow (one process) uses; bench.py runs the same kernels one
+ * process per GPU. */
+int srt_build_tables_multi(const srt_edges* g, const srt_build_opts* opts, int32_t ngpus,
+                           uint32_t* lat_q, uint64_t* quantum_ns, double* rel,
+                           srt_build_stats* stats);
+
 /* Quantum and u32-range check used by srt_build_tables. Returns SRT_OK or SRT_E_RANGE. */
 int srt_latency_quantum(const srt_edges* g, uint64_t* quantum_ns, uint32_t* max_w_q);
 
@@ -140,6 +148,8 @@ int srt_comm_unique_id(uint8_t out[128]);
 int srt_comm_init(const uint8_t id[128], int32_t nranks, int32_t rank, int32_t device,
                   srt_comm** comm);
 void srt_comm_free(srt_comm* comm);
+/* In-process communicators for `ndev` devices (ncclCommInitAll): comms[i] drives devices[i]. */
+int srt_comm_init_all(int32_t ndev, const int32_t* devices, srt_comm** comms);
 /* Row-block partition used by every sharded build: rank r owns rows [begin, end). */
 void srt_shard_rows(int32_t n, int32_t align, int32_t nranks, int32_t rank, int32_t* begin,
                     int32_t* end);

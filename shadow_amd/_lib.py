@@ -72,6 +72,7 @@ SIGNATURES = {
     "srt_parse_time_nanosec": (_I64, [_CP]),
     "srt_parse_bandwidth": (_I64, [_CP]),
     "srt_build_tables": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
+    "srt_build_tables_multi": (ctypes.c_int, [_VP, _VP, _I32, _VP, _VP, _VP, _VP]),
     "srt_latency_quantum": (ctypes.c_int, [_VP, _VP, _VP]),
     "srt_dense_build_device": (ctypes.c_int, [_I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _I32, _VP]),
     "srt_gen_complete_device": (ctypes.c_int, [_I32, _I32, _I32, _I32, _U64, _U32, _U32, _U32,
@@ -86,6 +87,7 @@ SIGNATURES = {
     "srt_sparse_graph_free": (None, [_VP]),
     "srt_comm_unique_id": (ctypes.c_int, [_VP]),
     "srt_comm_init": (ctypes.c_int, [_VP, _I32, _I32, _I32, _VP]),
+    "srt_comm_init_all": (ctypes.c_int, [_I32, _VP, _VP]),
     "srt_comm_free": (None, [_VP]),
     "srt_shard_rows": (None, [_I32, _I32, _I32, _I32, _VP, _VP]),
     "srt_dense_build_sharded": (ctypes.c_int, [_VP, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP,

@@ -435,7 +435,7 @@ extern "C" int srt_build_tables(const srt_edges* g, const srt_build_opts* opts, 
     TRYHIP(hipSetDevice(opts ? opts->device : 0));
     TRYHIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     if (algo == SRT_ALGO_DENSE_FW) {
-        const int ld = srt_ceil_div(n, 64) * 64;
+        const int ld = srt_ceil_div(n, 128) * 128; /* the u16 FW tiles need ld % 128 == 0 */
         const size_t ll = (size_t)ld * ld;
         hw = (uint32_t*)malloc(ll * sizeof(uint32_t));
         hr = (double*)malloc(ll * sizeof(double));
@@ -508,6 +508,211 @@ out:
         (void)hipStreamDestroy(st);
     }
     dfree(&B);
+    free(hw);
+    free(hr);
+    srt_canon_free(&c);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* In-process multi-GPU build (Shadow is one process): one host thread per GPU, RCCL           */
+/* communicators from ncclCommInitAll, the same sharded kernels as the one-process-per-GPU     */
+/* path (dense: row shards + pivot-panel broadcast; sparse: source shards + allgather).        */
+/* ------------------------------------------------------------------------------------------ */
+#include <pthread.h>
+
+typedef struct {
+    int rank, R, dev, directed, algo, n, ld;
+    srt_comm* comm;
+    const srt_canon* c;
+    const uint32_t* hw; /* dense: host w/r matrices, ld x ld */
+    const double* hr;
+    uint32_t* lat_q; /* host outputs, n x n */
+    double* rel;
+    int rc;
+    char err[256];
+    srt_build_stats st;
+} mjob;
+
+static void mjob_fail(mjob* j, int rc) {
+    j->rc = rc;
+    snprintf(j->err, sizeof(j->err), "%s", srt_last_error());
+}
+
+static void* mjob_dense(void* p) {
+    mjob* j = (mjob*)p;
+    int rc = SRT_OK;
+    dbufs B;
+    B.k = 0;
+    hipStream_t st = NULL;
+    int32_t b, e;
+    srt_shard_rows(j->ld, SRT_SHARD_ALIGN, j->R, j->rank, &b, &e);
+    const int nr = e - b;
+    const size_t rows = (size_t)(nr > 0 ? nr : 1) * j->ld;
+    uint32_t *dw, *dlat;
+    double *dr, *drel;
+    TRYHIP(hipSetDevice(j->dev));
+    TRYHIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    TRY(dalloc(&B, (void**)&dw, rows * sizeof(uint32_t)));
+    TRY(dalloc(&B, (void**)&dr, rows * sizeof(double)));
+    TRY(dalloc(&B, (void**)&dlat, rows * sizeof(uint32_t)));
+    TRY(dalloc(&B, (void**)&drel, rows * sizeof(double)));
+    if (nr > 0) {
+        TRYHIP(hipMemcpyAsync(dw, j->hw + (size_t)b * j->ld, (size_t)nr * j->ld * sizeof(uint32_t),
+                              hipMemcpyHostToDevice, st));
+        TRYHIP(hipMemcpyAsync(dr, j->hr + (size_t)b * j->ld, (size_t)nr * j->ld * sizeof(double),
+                              hipMemcpyHostToDevice, st));
+    }
+    TRY(srt_dense_build_sharded(j->comm, j->n, j->ld, j->directed, dw, dr, dlat, drel, st, 0, &j->st));
+    {
+        const int r1 = e < j->n ? e : j->n;
+        if (r1 > b) {
+            TRYHIP(hipMemcpy2DAsync(j->lat_q + (size_t)b * j->n, (size_t)j->n * sizeof(uint32_t), dlat,
+                                    (size_t)j->ld * sizeof(uint32_t), (size_t)j->n * sizeof(uint32_t),
+                                    r1 - b, hipMemcpyDeviceToHost, st));
+            TRYHIP(hipMemcpy2DAsync(j->rel + (size_t)b * j->n, (size_t)j->n * sizeof(double), drel,
+                                    (size_t)j->ld * sizeof(double), (size_t)j->n * sizeof(double),
+                                    r1 - b, hipMemcpyDeviceToHost, st));
+        }
+        TRYHIP(hipStreamSynchronize(st));
+    }
+out:
+    if (rc) mjob_fail(j, rc);
+    if (st) (void)hipStreamDestroy(st);
+    dfree(&B);
+    return NULL;
+}
+
+static void* mjob_sparse(void* p) {
+    mjob* j = (mjob*)p;
+    int rc = SRT_OK;
+    dbufs B;
+    B.k = 0;
+    hipStream_t st = NULL;
+    srt_sparse_graph* sg = NULL;
+    const int n = j->n, per = srt_ceil_div(n, j->R);
+    const int s0 = j->rank * per, s1 = (s0 + per < n) ? s0 + per : n;
+    const size_t all = (size_t)per * j->R * n;
+    uint32_t* dlat;
+    double* drel;
+    TRYHIP(hipSetDevice(j->dev));
+    TRYHIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    TRY(sparse_graph_from_canon(j->c, j->dev, &sg));
+    TRY(dalloc(&B, (void**)&dlat, all * sizeof(uint32_t)));
+    TRY(dalloc(&B, (void**)&drel, all * sizeof(double)));
+    if (s1 > s0)
+        TRY(srt_sparse_graph_rows(sg, s0, s1, dlat + (size_t)s0 * n, drel + (size_t)s0 * n, st, &j->st));
+    /* the symmetry rule needs the other shards' rows: gather, mirror, keep our block */
+    TRY(srt_sparse_allgather(j->comm, n, per, dlat, drel, st));
+    if (!j->directed) TRY(srt_mirror_lower_device(n, n, drel, st));
+    if (s1 > s0) {
+        TRYHIP(hipMemcpyAsync(j->lat_q + (size_t)s0 * n, dlat + (size_t)s0 * n,
+                              (size_t)(s1 - s0) * n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        TRYHIP(hipMemcpyAsync(j->rel + (size_t)s0 * n, drel + (size_t)s0 * n,
+                              (size_t)(s1 - s0) * n * sizeof(double), hipMemcpyDeviceToHost, st));
+    }
+    TRYHIP(hipStreamSynchronize(st));
+out:
+    if (rc) mjob_fail(j, rc);
+    if (sg) srt_sparse_graph_free(sg);
+    if (st) (void)hipStreamDestroy(st);
+    dfree(&B);
+    return NULL;
+}
+
+extern "C" int srt_build_tables_multi(const srt_edges* g, const srt_build_opts* opts, int32_t ngpus,
+                                      uint32_t* lat_q, uint64_t* quantum_ns, double* rel,
+                                      srt_build_stats* stats) {
+    if (!g || !lat_q || !quantum_ns || !rel || ngpus < 1) {
+        srt_set_error("srt_build_tables_multi: bad argument");
+        return SRT_E_ARG;
+    }
+    const int avail = srt_device_count();
+    if (avail < 1) {
+        srt_set_error("srt_build_tables_multi: no HIP device");
+        return SRT_E_DEVICE;
+    }
+    const int R = ngpus < avail ? ngpus : avail;
+    const int use_sp = opts ? opts->use_shortest_path : 1;
+    if (!use_sp) return srt_build_tables(g, opts, lat_q, quantum_ns, rel, stats);
+    srt_canon c;
+    int rc = srt_canon_build(g, &c);
+    if (rc) return rc;
+    *quantum_ns = c.quantum_ns;
+    const int n = c.n;
+    const int algo = choose_algo(&c, opts);
+    const int ld = srt_ceil_div(n, SRT_SHARD_ALIGN) * SRT_SHARD_ALIGN;
+    uint32_t* hw = NULL;
+    double* hr = NULL;
+    srt_comm** comms = (srt_comm**)calloc((size_t)R, sizeof(srt_comm*));
+    mjob* jobs = (mjob*)calloc((size_t)R, sizeof(mjob));
+    pthread_t* th = (pthread_t*)calloc((size_t)R, sizeof(pthread_t));
+    int* devs = (int*)calloc((size_t)R, sizeof(int));
+    if (!comms || !jobs || !th || !devs) {
+        rc = SRT_E_NOMEM;
+        goto done;
+    }
+    if (algo == SRT_ALGO_DENSE_FW) {
+        const size_t ll = (size_t)ld * ld;
+        hw = (uint32_t*)malloc(ll * sizeof(uint32_t));
+        hr = (double*)malloc(ll * sizeof(double));
+        if (!hw || !hr) {
+            rc = SRT_E_NOMEM;
+            goto done;
+        }
+        for (size_t i = 0; i < ll; i++) {
+            hw[i] = SRT_INF;
+            hr[i] = 0.0;
+        }
+        for (int u = 0; u < n; u++) {
+            for (int k = c.rowptr[u]; k < c.rowptr[u + 1]; k++) {
+                hw[(size_t)u * ld + c.col[k]] = c.w[k];
+                hr[(size_t)u * ld + c.col[k]] = c.r[k];
+            }
+            hw[(size_t)u * ld + u] = c.self_w[u];
+            hr[(size_t)u * ld + u] = c.self_r[u];
+        }
+    }
+    for (int i = 0; i < R; i++) devs[i] = i;
+    if ((rc = srt_comm_init_all(R, devs, comms))) goto done;
+    for (int i = 0; i < R; i++) {
+        mjob* j = &jobs[i];
+        j->rank = i;
+        j->R = R;
+        j->dev = devs[i];
+        j->directed = c.directed;
+        j->algo = algo;
+        j->n = n;
+        j->ld = ld;
+        j->comm = comms[i];
+        j->c = &c;
+        j->hw = hw;
+        j->hr = hr;
+        j->lat_q = lat_q;
+        j->rel = rel;
+        if (pthread_create(&th[i], NULL, algo == SRT_ALGO_DENSE_FW ? mjob_dense : mjob_sparse, j)) {
+            /* a collective would wait forever for the missing rank: refuse before any started */
+            for (int k = 0; k < i; k++) pthread_join(th[k], NULL);
+            rc = SRT_E_NOMEM;
+            srt_set_error("srt_build_tables_multi: pthread_create failed");
+            goto done;
+        }
+    }
+    for (int i = 0; i < R; i++) pthread_join(th[i], NULL);
+    for (int i = 0; i < R && !rc; i++)
+        if (jobs[i].rc) {
+            rc = jobs[i].rc;
+            srt_set_error("rank %d: %s", i, jobs[i].err);
+        }
+    if (!rc && stats) *stats = jobs[0].st;
+done:
+    if (comms)
+        for (int i = 0; i < R; i++)
+            if (comms[i]) srt_comm_free(comms[i]);
+    free(comms);
+    free(jobs);
+    free(th);
+    free(devs);
     free(hw);
     free(hr);
     srt_canon_free(&c);

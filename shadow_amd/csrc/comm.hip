@@ -59,6 +59,39 @@ extern "C" int srt_comm_init(const uint8_t id[128], int32_t nranks, int32_t rank
     return SRT_OK;
 }
 
+extern "C" int srt_comm_init_all(int32_t ndev, const int32_t* devices, srt_comm** comms) {
+    if (ndev < 1 || !devices || !comms) {
+        srt_set_error("srt_comm_init_all: bad arguments");
+        return SRT_E_ARG;
+    }
+    ncclComm_t* nc = (ncclComm_t*)calloc((size_t)ndev, sizeof(ncclComm_t));
+    if (!nc) return SRT_E_NOMEM;
+    ncclResult_t r = ncclCommInitAll(nc, ndev, devices);
+    if (r != ncclSuccess) {
+        free(nc);
+        srt_set_error("ncclCommInitAll: %s", ncclGetErrorString(r));
+        return SRT_E_COMM;
+    }
+    for (int i = 0; i < ndev; i++) {
+        comms[i] = (srt_comm*)calloc(1, sizeof(srt_comm));
+        if (!comms[i]) {
+            for (int k = 0; k < ndev; k++) {
+                (void)ncclCommDestroy(nc[k]);
+                free(comms[k]);
+                comms[k] = NULL;
+            }
+            free(nc);
+            return SRT_E_NOMEM;
+        }
+        comms[i]->nc = nc[i];
+        comms[i]->nranks = ndev;
+        comms[i]->rank = i;
+        comms[i]->device = devices[i];
+    }
+    free(nc);
+    return SRT_OK;
+}
+
 extern "C" void srt_comm_free(srt_comm* comm) {
     if (!comm) return;
     (void)ncclCommDestroy(comm->nc);

@@ -772,9 +772,6 @@ int topology_computeShortestPaths(Topology* t, int nGPUs) {
             pthread_mutex_unlock(&t->build_lock);
             return SRT_E_DEVICE;
         }
-        if (nGPUs > 1)
-            srt_log(SRT_LOG_INFO, "in-process multi-GPU build not enabled; using device %d "
-                    "(sharded builds run one process per GPU, see bench.py)", t->opts.device);
         size_t nn = (size_t)t->n * (size_t)t->n;
         t->lat_q = (uint32_t*)malloc(nn * sizeof(uint32_t));
         t->rel = (double*)malloc(nn * sizeof(double));
@@ -785,7 +782,10 @@ int topology_computeShortestPaths(Topology* t, int nGPUs) {
             srt_topology_edges(t, &e);
             srt_build_opts o = t->opts;
             o.use_shortest_path = t->use_shortest_path;
-            rc = srt_build_tables(&e, &o, t->lat_q, &t->quantum_ns, t->rel, &t->stats);
+            /* nGPUs > 1: one host thread per GPU of this process, RCCL between them */
+            rc = nGPUs > 1 ? srt_build_tables_multi(&e, &o, nGPUs, t->lat_q, &t->quantum_ns, t->rel,
+                                                    &t->stats)
+                           : srt_build_tables(&e, &o, t->lat_q, &t->quantum_ns, t->rel, &t->stats);
         }
         if (rc == SRT_OK) {
             atomic_store_explicit(&t->built, 1, memory_order_release);

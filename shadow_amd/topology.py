@@ -168,8 +168,9 @@ def parse_bandwidth(s: str) -> int:
 
 
 def build_tables(n, directed, src, dst, lat_ns, loss, use_shortest_path=True, device=0,
-                 algo=_lib.ALGO_AUTO):
-    """srt_build_tables on host arrays -> (lat_ns u64 [n,n], rel f64 [n,n], stats)."""
+                 algo=_lib.ALGO_AUTO, ngpus=None):
+    """srt_build_tables on host arrays -> (lat_ns u64 [n,n], rel f64 [n,n], stats).
+    ngpus: run srt_build_tables_multi (one host thread per GPU of this process, RCCL)."""
     src = np.ascontiguousarray(src, np.int32)
     dst = np.ascontiguousarray(dst, np.int32)
     lat_ns = np.ascontiguousarray(lat_ns, np.int64)
@@ -181,8 +182,14 @@ def build_tables(n, directed, src, dst, lat_ns, loss, use_shortest_path=True, de
     rel = np.empty((n, n), np.float64)
     q = ctypes.c_uint64()
     st = BuildStats()
-    check(lib().srt_build_tables(ctypes.byref(e), ctypes.byref(o), lat.ctypes.data, ctypes.byref(q),
-                                 rel.ctypes.data, ctypes.byref(st)), "srt_build_tables")
+    if ngpus is None:
+        check(lib().srt_build_tables(ctypes.byref(e), ctypes.byref(o), lat.ctypes.data,
+                                     ctypes.byref(q), rel.ctypes.data, ctypes.byref(st)),
+              "srt_build_tables")
+    else:
+        check(lib().srt_build_tables_multi(ctypes.byref(e), ctypes.byref(o), int(ngpus),
+                                           lat.ctypes.data, ctypes.byref(q), rel.ctypes.data,
+                                           ctypes.byref(st)), "srt_build_tables_multi")
     return lat.astype(np.uint64) * np.uint64(q.value), rel, st
 
 

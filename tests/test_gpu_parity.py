@@ -250,3 +250,31 @@ def test_dense_lookahead_schedule_one_gpu(gpu, monkeypatch, n, seed):
     torch.cuda.synchronize()
     L.srt_comm_free(comm)
     assert torch.equal(lat2[:n, :n], lat[:n, :n]) and torch.equal(rel2[:n, :n], rel[:n, :n])
+
+
+@pytest.mark.parametrize("kind", ["dense", "sparse", "directed"])
+@pytest.mark.parametrize("ngpus", [1, 8])
+def test_in_process_multi_gpu_build(gpu, kind, ngpus):
+    """srt_build_tables_multi (Shadow's one-process form: a host thread per GPU, communicators from
+    ncclCommInitAll, sharded kernels + RCCL) equals the oracle; ngpus is clamped to the devices
+    present, so on a one-GPU box both requests exercise the threaded path with one rank."""
+    if kind == "dense":
+        g = graphs.complete_graph(700, seed=9)
+        algo = ALGO_DENSE_FW
+    elif kind == "sparse":
+        g = graphs.random_geometric(1500, seed=3)
+        algo = ALGO_SPARSE_SSSP
+    else:
+        rng = np.random.default_rng(21)
+        n, m = 300, 2500
+        ring = np.arange(n)
+        src = np.concatenate([rng.integers(0, n, m), ring]).astype(np.int32)
+        dst = np.concatenate([rng.integers(0, n, m), (ring + 1) % n]).astype(np.int32)
+        lat = (rng.integers(1, 30, len(src)) * MS).astype(np.int64)
+        loss = rng.integers(0, 200, len(src)) / 10000.0
+        g = graphs.Graph(n, True, src, dst, lat, loss)
+        algo = ALGO_DENSE_FW
+    lat, rel, _ = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss, algo=algo,
+                               ngpus=ngpus)
+    exp = _oracle(g)
+    assert_tables(lat, rel, exp["lat_int"], exp["rel"], f"multi {kind} x{ngpus}")
