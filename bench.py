@@ -164,7 +164,9 @@ def run_dense(c: Ctx, wl):
     n_upd = sum(s.n_update for s in stats)
     ms_upd = sum(s.ms_update for s in stats)
     avg_upd_ms = ms_upd / max(n_upd, 1)
-    enc = int(stats[-1].dist_enc)  # 3: u16 + f16-compare mins, 2: u16 pk_min, 1: u32
+    # 4: u16 + f16-compare mins on upper-triangle tiles (undirected), 3: the same on every tile,
+    # 2: u16 pk_min, 1: u32
+    enc = int(stats[-1].dist_enc)
     s_d = 4 if enc == 1 else 2
     # VALU issue model per wave64 relaxation (cycles per SIMD): full-rate ops (v_add_u32) issue in
     # 2 cycles, packed / 3-input ops (v_pk_minimum3_f16, v_pk_min_u16, v_min3_u32) in 4
@@ -172,11 +174,15 @@ def run_dense(c: Ctx, wl):
     #   enc 3: 2 x v_add_u32 + 1 x v_pk_minimum3_f16 per 4 relaxations -> 8/4 = 2.0 cycles
     #   enc 2: 1 x v_add_u32 + 1 x v_pk_min_u16 per 2 relaxations      -> 6/2 = 3.0 cycles
     #   enc 1: 2 x v_add_u32 + 1 x v_min3_u32 per 2 relaxations         -> 8/2 = 4.0 cycles
-    cyc_per_relax = {3: 2.0, 2: 3.0, 1: 4.0}[enc]
-    instr_per_relax = {3: 0.75, 2: 1.0, 1: 1.5}[enc]
-    kname = {3: "fwh_update_kernel", 2: "fw16_update_kernel<false>", 1: "fw_update_kernel"}[enc]
-    bytes_per_round = 2.0 * nr * ld * s_d  # round-streaming model: read + write the local rows
-    relax_per_round = float(nr) * ld * FW_B
+    cyc_per_relax = {4: 2.0, 3: 2.0, 2: 3.0, 1: 4.0}[enc]
+    instr_per_relax = {4: 0.75, 3: 0.75, 2: 1.0, 1: 1.5}[enc]
+    kname = {4: "fwh_update_kernel<true>", 3: "fwh_update_kernel<false>",
+             2: "fw16_update_kernel<false>", 1: "fw_update_kernel"}[enc]
+    # elements a round updates: every local row, or (enc 4) the upper-triangle 128x128 tiles only
+    tiles = ld // 128
+    elems = float(tiles * (tiles + 1) // 2) * 128 * 128 if enc == 4 else float(nr) * ld
+    bytes_per_round = 2.0 * elems * s_d  # round-streaming model: read + write what is updated
+    relax_per_round = elems * FW_B
     achieved_gbs = bytes_per_round / (avg_upd_ms * 1e-3) / 1e9
     relax_t = relax_per_round / (avg_upd_ms * 1e-3) / 1e12
     relax_peak_t = VALU_LANE_CYCLES_T / cyc_per_relax
@@ -194,8 +200,9 @@ def run_dense(c: Ctx, wl):
         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
         "traffic": traffic, "bytes_per_launch": bytes_per_round,
         "avg_launch_ms": round(avg_upd_ms, 4), "launches_timed": n_upd,
-        "model": f"2*rows*ld*{s_d} B per round (SURVEY §8d round-streaming, B=64, "
-                 f"{ {3: 'u16 f16-compare', 2: 'u16 pk_min', 1: 'u32'}[enc]} distances)",
+        "model": f"2*elements*{s_d} B per round (SURVEY §8d round-streaming, B=64, "
+                 f"{ {4: 'u16 f16-compare, upper triangle', 3: 'u16 f16-compare', 2: 'u16 pk_min', 1: 'u32'}[enc]}"
+                 f" distances; elements updated per round = {int(elems)})",
         "algorithmic_min_bytes": float(nr) * ld * (4 + 8),
         "valu": {"achieved": round(relax_t, 2), "peak": round(relax_peak_t, 1),
                  "unit": "Trelax/s", "frac": round(relax_t / relax_peak_t, 4),

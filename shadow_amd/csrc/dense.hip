@@ -945,9 +945,10 @@ extern "C" int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, c
     int exact = 0, enc = SRT_DENC_U32;
     for (int fm = 1; fm >= 0 && !exact && ld % 128 == 0; --fm) {
         if (evp) evp->used = 0;
-        rc = srt_fw16_build(n, ld, 0, ld, w, lat, st, evp, NULL, NULL, NULL, 0, fm, &exact);
+        int sym = !directed;
+        rc = srt_fw16_build(n, ld, 0, ld, w, lat, st, evp, NULL, NULL, NULL, 0, fm, &sym, &exact);
         if (rc) return rc;
-        if (exact) enc = fm ? SRT_DENC_F16CMP : SRT_DENC_U16;
+        if (exact) enc = fm ? (sym ? SRT_DENC_F16CMP_SYM : SRT_DENC_F16CMP) : SRT_DENC_U16;
     }
     if (!exact) { /* u32 path: ld not a multiple of 128, or a distance reached 0x7FFF quanta */
         if (evp) evp->used = 0;
@@ -1164,7 +1165,7 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
     for (int fm = 1; fm >= 0 && !exact; --fm) {
         if (evp) evp->used = 0;
         rc = srt_fw16_build(n, ld, b, nr, w_rows, lat_rows, st, evp, shard_owner,
-                            R > 1 ? shard_bcast : NULL, &ctx, me, fm, &exact);
+                            R > 1 ? shard_bcast : NULL, &ctx, me, fm, NULL, &exact);
         if (rc) return rc;
         if (R > 1) { /* every rank must agree before falling back to a wider encoding */
             int32_t* flag = ws->cnt;

@@ -254,7 +254,10 @@ __global__ __launch_bounds__(256) void fw16_diag_kernel(u16* __restrict__ P, int
 }
 
 /* pivot-row panel tiles (k, j): X <- Dkk* (x) X ; pivot-column tiles (i, k): X <- X (x) Dkk* */
-template <bool FM>
+/* SYM (undirected graphs, one shard): only upper-triangle panel tiles -- row tiles right of the
+ * pivot block and column tiles above it -- are kept; fw16_refresh_kernel mirrors the column tiles
+ * into the lower part of the pivot rows so P is a full panel. */
+template <bool FM, bool SYM>
 __global__ __launch_bounds__(256) void fw16_panel_kernel(u16* __restrict__ D, int ld, int row0,
                                                          int nrow_tiles, u16* __restrict__ P, int k0,
                                                          int ncol_tiles, int do_row, int do_col) {
@@ -264,13 +267,14 @@ __global__ __launch_bounds__(256) void fw16_panel_kernel(u16* __restrict__ D, in
     int bid = blockIdx.x;
     u16* C;
     if (bid < ncol_tiles) {
-        if (!do_row || bid * KB == k0) return;
+        if (!do_row || bid * KB == k0 || (SYM && bid * KB < k0)) return;
         C = P + bid * KB;
         stage_A<KB, KB>(sA, P + k0, ld, tid);
         stage_B<KB, KB>(sB, C, ld, tid);
     } else {
         bid -= ncol_tiles;
-        if (!do_col || bid >= nrow_tiles || row0 + bid * KB == k0) return;
+        if (!do_col || bid >= nrow_tiles || row0 + bid * KB == k0 || (SYM && row0 + bid * KB > k0))
+            return;
         C = D + (size_t)bid * KB * ld + k0;
         stage_A<KB, KB>(sA, C, ld, tid);
         stage_B<KB, KB>(sB, P + k0, ld, tid);
@@ -284,6 +288,26 @@ __global__ __launch_bounds__(256) void fw16_panel_kernel(u16* __restrict__ D, in
         for (int c = 0; c < 2; ++c) acc[r][c] = old[r][c];
     mp16<FM, KB, 4, 4, KB>(acc, sA, sB, tx, ty);
     store_acc16<4, 4>(acc, old, C, ld, tx, ty);
+}
+
+/* SYM: pivot rows' lower part from the (upper) column tiles: D[k0+m][j0+c] = D[j0+c][k0+m] */
+__global__ __launch_bounds__(256) void fw16_refresh_kernel(u16* __restrict__ D, int ld, int k0) {
+    __shared__ u16 t[KB][KB + 2];
+    const int j0 = blockIdx.x * KB, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int a = ty; a < KB; a += 4) t[a][tx] = D[(size_t)(j0 + a) * ld + k0 + tx];
+    __syncthreads();
+    for (int a = ty; a < KB; a += 4) D[(size_t)(k0 + a) * ld + j0 + tx] = t[tx][a];
+}
+
+/* SYM, after the last round: lower triangle from the upper, 64x64 tiles (I > J) */
+__global__ __launch_bounds__(256) void fw16_mirror_kernel(u16* __restrict__ D, int ld) {
+    __shared__ u16 t[KB][KB + 2];
+    const int I = blockIdx.y, J = blockIdx.x;
+    if (I <= J) return;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int a = ty; a < KB; a += 4) t[a][tx] = D[(size_t)(J * KB + a) * ld + I * KB + tx];
+    __syncthreads();
+    for (int a = ty; a < KB; a += 4) D[(size_t)(I * KB + a) * ld + J * KB + tx] = t[tx][a];
 }
 
 /* every 128x128 tile of the local rows: D_IJ <- min(D_IJ, D_I,k (x) P_k,J) */
@@ -383,6 +407,51 @@ static __device__ __forceinline__ void fwh_swrite(const fwh_stage_regs& g, uint3
     }
 }
 
+/* SYM: the A slice of tile row I is the pivot panel transposed, A[r][m] = P[m][I0 + r]; a thread
+ * loads 8 rows of pivots 2p and 2p+1 (two coalesced 16-B pieces) and writes them pair-major */
+static __device__ __forceinline__ void fwh_gload_sym(fwh_stage_regs& g, const u16* __restrict__ Ph,
+                                                     int I0, const u16* __restrict__ B, size_t ld,
+                                                     int tid) {
+    const int p = tid >> 4, rg = tid & 15;
+    g.a[0] = *reinterpret_cast<const uint4*>(Ph + (size_t)(2 * p) * ld + I0 + rg * 8);
+    g.a[1] = *reinterpret_cast<const uint4*>(Ph + (size_t)(2 * p + 1) * ld + I0 + rg * 8);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int ib = tid + q * 256, rb = ib >> 4, cb = (ib & 15) * 8;
+        g.b[q] = *reinterpret_cast<const uint4*>(B + (size_t)rb * ld + cb);
+    }
+}
+
+static __device__ __forceinline__ void fwh_swrite_sym(const fwh_stage_regs& g,
+                                                      uint32_t* __restrict__ sA,
+                                                      u16* __restrict__ sB, int tid) {
+    const int p = tid >> 4, rg = tid & 15;
+    const uint32_t a0[4] = {g.a[0].x, g.a[0].y, g.a[0].z, g.a[0].w}; /* pivot 2p, rows 2i, 2i+1 */
+    const uint32_t a1[4] = {g.a[1].x, g.a[1].y, g.a[1].z, g.a[1].w}; /* pivot 2p+1 */
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<uint4*>(sA + ((p * 128) + rg * 8 + 2 * i) * 2) =
+            make_uint4(splat(a0[i] & 0xFFFFu), splat(a1[i] & 0xFFFFu), splat(a0[i] >> 16),
+                       splat(a1[i] >> 16));
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int ib = tid + q * 256, rb = ib >> 4, cb = (ib & 15) * 8;
+        *reinterpret_cast<uint4*>(sB + rb * UBS + cb) = g.b[q];
+    }
+}
+
+/* upper-triangle tile (I <= J) of linear index x among T tile rows: row I holds T - I tiles */
+static __device__ __forceinline__ void tri_decode(int x, int T, int* I, int* J) {
+    auto off = [T](int i) { return i * T - (i * (i - 1)) / 2; };
+    const double tt = T + 0.5;
+    int i = (int)(tt - sqrt(tt * tt - 2.0 * x));
+    i = max(0, min(i, T - 1));
+    while (i > 0 && off(i) > x) --i;
+    while (i + 1 < T && off(i + 1) <= x) ++i;
+    *I = i;
+    *J = i + (x - off(i));
+}
+
 /* LDS operand reads: B rows m, m+1 at the thread's 8 columns; A (splat pivots m, m+1) of 4 rows */
 static __device__ __forceinline__ void fwh_readB(uint4 (&b)[2], const u16* __restrict__ pb, int m) {
     b[0] = *reinterpret_cast<const uint4*>(pb + m * UBS);
@@ -451,6 +520,10 @@ static __device__ __forceinline__ void fwh_stage(uint32_t (&acc)[8][4], const ui
     }
 }
 
+/* SYM: only upper-triangle tiles (I <= J, grid T(T+1)/2) -- an undirected graph's distance
+ * matrix stays symmetric through every round, so the lower triangle is the transpose and half the
+ * relaxations are skipped; A comes from the pivot panel transposed. */
+template <bool SYM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void fwh_update_kernel(
     u16* __restrict__ D, int ld, const u16* __restrict__ P, int k0, int ncol_tiles, int i0, int skip) {
     __shared__ __attribute__((aligned(16))) uint32_t sA[UKC / 2 * 128 * 2];
@@ -459,12 +532,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const int nb = gridDim.x;
     const int per = nb >> 3;
     const int bid = (nb & 7) == 0 ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
-    const int I = tile_row(bid, ncol_tiles, i0, skip), J = bid % ncol_tiles;
+    int I, J;
+    if (SYM) {
+        tri_decode(bid, ncol_tiles, &I, &J);
+    } else {
+        I = tile_row(bid, ncol_tiles, i0, skip);
+        J = bid % ncol_tiles;
+    }
     u16* C = D + (size_t)I * 128 * ld + J * 128;
     const u16* Ag = D + (size_t)I * 128 * ld + k0;
     const u16* Bg = P + J * 128;
     fwh_stage_regs g;
-    fwh_gload(g, Ag, Bg, ld, tid);
+    if (SYM)
+        fwh_gload_sym(g, P, I * 128, Bg, ld, tid);
+    else
+        fwh_gload(g, Ag, Bg, ld, tid);
     uint32_t acc[8][4];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
@@ -479,12 +561,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     uint32_t sum0[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) sum0[r] = rowsum16(acc[r]);
-    fwh_swrite(g, sA, sB, tid);
+    if (SYM)
+        fwh_swrite_sym(g, sA, sB, tid);
+    else
+        fwh_swrite(g, sA, sB, tid);
     __syncthreads();
-    fwh_gload(g, Ag + UKC, Bg + (size_t)UKC * ld, ld, tid); /* in flight during stage 0 */
+    if (SYM) /* in flight during stage 0 */
+        fwh_gload_sym(g, P + (size_t)UKC * ld, I * 128, Bg + (size_t)UKC * ld, ld, tid);
+    else
+        fwh_gload(g, Ag + UKC, Bg + (size_t)UKC * ld, ld, tid);
     fwh_stage(acc, sA, sB, tx, ty);
     __syncthreads();
-    fwh_swrite(g, sA, sB, tid);
+    if (SYM)
+        fwh_swrite_sym(g, sA, sB, tid);
+    else
+        fwh_swrite(g, sA, sB, tid);
     __syncthreads();
     fwh_stage(acc, sA, sB, tx, ty);
     /* store only the rows that changed */
@@ -525,6 +616,8 @@ __global__ void fw16_finish_kernel(int n, int ld, int row0, const u16* __restric
 /* per-device u16 working matrix of the last build (rows of the shard, ld columns); the dense
  * post pass reads it transposed for the predecessor search (half the bytes of the u32 table) */
 static u16* fw16_bufs[64];
+static size_t fw16_caps[64]; /* elements allocated in fw16_bufs (shared by both build forms) */
+static int* fw16_flags[64];
 const uint16_t* srt_fw16_matrix(void) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return NULL;
@@ -556,16 +649,60 @@ static int sched_get(fw16_sched** out, int dev) {
     return SRT_OK;
 }
 
+/* Upper-triangle blocked FW for an undirected graph on one GPU (f16-compare kernels). */
+static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipStream_t st,
+                          evpool_t* evp, int* exact) {
+    int dev = 0;
+    SRT_HIPCHK(hipGetDevice(&dev));
+    dev &= 63;
+    size_t* caps = fw16_caps;
+    int** flags = fw16_flags;
+    const size_t need = (size_t)ld * ld;
+    if (caps[dev] < need || !fw16_bufs[dev]) {
+        if (fw16_bufs[dev]) SRT_HIPCHK(hipFree(fw16_bufs[dev]));
+        fw16_bufs[dev] = NULL;
+        caps[dev] = 0;
+        SRT_HIPCHK(hipMalloc(&fw16_bufs[dev], need * sizeof(u16)));
+        caps[dev] = need;
+    }
+    if (!flags[dev]) SRT_HIPCHK(hipMalloc(&flags[dev], sizeof(int)));
+    u16* d = fw16_bufs[dev];
+    fw16_init_kernel<<<dim3(srt_ceil_div(ld, 256), ld), 256, 0, st>>>(n, ld, 0, w, d, CAP_F);
+    SRT_HIPCHK(hipGetLastError());
+    const int nb = ld / KB, T = ld / 128;
+    const int ntri = T * (T + 1) / 2;
+    for (int k0 = 0; k0 < ld; k0 += KB) {
+        u16* P = d + (size_t)k0 * ld;
+        fw16_diag_kernel<<<1, 256, 0, st>>>(P, ld, k0);
+        fw16_panel_kernel<true, true><<<2 * nb, 256, 0, st>>>(d, ld, 0, nb, P, k0, nb, 1, 1);
+        if (k0 > 0) fw16_refresh_kernel<<<k0 / KB, 256, 0, st>>>(d, ld, k0);
+        if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
+        fwh_update_kernel<true><<<ntri, 256, 0, st>>>(d, ld, P, k0, T, 0, -1);
+        if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
+        SRT_HIPCHK(hipGetLastError());
+    }
+    fw16_mirror_kernel<<<dim3(nb, nb), 256, 0, st>>>(d, ld);
+    SRT_HIPCHK(hipMemsetAsync(flags[dev], 0, sizeof(int), st));
+    fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 256), ld), 256, 0, st>>>(n, ld, 0, d, lat, flags[dev],
+                                                                        CAP_F);
+    SRT_HIPCHK(hipGetLastError());
+    int sat = 0;
+    SRT_HIPCHK(hipMemcpyAsync(&sat, flags[dev], sizeof(int), hipMemcpyDeviceToHost, st));
+    SRT_HIPCHK(hipStreamSynchronize(st));
+    *exact = sat ? 0 : 1;
+    return SRT_OK;
+}
+
 int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,
                    hipStream_t st, evpool_t* evp, srt_owner_fn owner_of, srt_panel_bcast_fn bcast,
-                   void* ctx, int rank, int fm, int* exact) {
+                   void* ctx, int rank, int fm, int* sym, int* exact) {
     if (ld % 128 || nrows % 128 || row0 % 128) {
         srt_set_error("u16 FW needs ld and the row shard to be multiples of 128");
         return SRT_E_ARG;
     }
     u16** bufs = fw16_bufs;
-    static size_t caps[64];
-    static int* flags[64];
+    size_t* caps = fw16_caps;
+    int** flags = fw16_flags;
     int dev = 0;
     SRT_HIPCHK(hipGetDevice(&dev));
     dev &= 63;
@@ -581,12 +718,20 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
     if (rc) return rc;
     const char* la_env = getenv("SRT_FW_LOOKAHEAD");
     const bool lookahead = la_env ? atoi(la_env) != 0 : bcast != NULL;
+    /* upper-triangle rounds: undirected graph, f16-compare path, the whole matrix on one GPU */
+    const char* sym_env = getenv("SRT_FW_SYM");
+    const bool want_sym = sym && *sym && !(sym_env && atoi(sym_env) == 0);
+    if (sym) *sym = 0;
+    if (want_sym && fm && !lookahead && !bcast && !owner_of && row0 == 0 && nrows == ld) {
+        *sym = 1;
+        return fw16_build_sym(n, ld, w_rows, lat_rows, st, evp, exact);
+    }
     hipStream_t cs = lookahead ? sc->cs : st;
     u16* d = bufs[dev];
     u16* pbuf[2] = {bufs[dev] + (size_t)nrows * ld, bufs[dev] + (size_t)nrows * ld + (size_t)KB * ld};
     const uint32_t cap = fm ? CAP_F : CAP_U;
-    auto panel = fm ? fw16_panel_kernel<true> : fw16_panel_kernel<false>;
-    auto update = fm ? fwh_update_kernel : fw16_update_kernel<false>;
+    auto panel = fm ? fw16_panel_kernel<true, false> : fw16_panel_kernel<false, false>;
+    auto update = fm ? fwh_update_kernel<false> : fw16_update_kernel<false>;
     if (nrows > 0) {
         fw16_init_kernel<<<dim3(srt_ceil_div(ld, 256), nrows), 256, 0, st>>>(n, ld, row0, w_rows, d,
                                                                            cap);

@@ -86,17 +86,19 @@ static inline int evpool_sum(evpool_t* p, hipEvent_t last, srt_build_stats* stat
 
 typedef int (*srt_panel_bcast_fn)(void* ctx, void* panel, size_t bytes, int owner, hipStream_t st);
 typedef int (*srt_owner_fn)(void* ctx, int k0);
-/* packed-u16 Floyd-Warshall over a row shard (fw16.hip). d16: nrows x ld u16. fm = 1 selects the
+/* packed-u16 Floyd-Warshall over a row shard (fw16.hip). d16: nrows x ld u16. *sym = 1 on input
+ * (undirected, symmetric w) lets a single-shard f16-compare build update only upper-triangle tiles;
+ * on output it says whether that form ran (sym may be NULL). fm = 1 selects the
  * f16-compare instruction mix (cap 0x3DFF), fm = 0 the v_pk_min_u16 mix (cap 0x7FFF). Returns
  * SRT_OK and *exact = 1 when every distance is below the cap (else the caller reruns with the
  * next wider path). lat_rows receives the distances widened to u32 quanta. */
 int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,
                    hipStream_t st, evpool_t* evp, srt_owner_fn owner_of, srt_panel_bcast_fn bcast,
-                   void* ctx, int rank, int fm, int* exact);
+                   void* ctx, int rank, int fm, int* sym, int* exact);
 /* the u16 working matrix of the last srt_fw16_build on the current device (row shard x ld) */
 const uint16_t* srt_fw16_matrix(void);
 /* distance encodings of the dense build, reported (negated) in srt_build_stats.fw_block */
-enum { SRT_DENC_U32 = 1, SRT_DENC_U16 = 2, SRT_DENC_F16CMP = 3 };
+enum { SRT_DENC_U32 = 1, SRT_DENC_U16 = 2, SRT_DENC_F16CMP = 3, SRT_DENC_F16CMP_SYM = 4 };
 
 int srt_dense_post_device(int32_t n, int32_t ld, int32_t directed, const uint32_t* w,
                           const double* r, uint32_t* d, const uint16_t* d16, double* rel,

@@ -188,15 +188,18 @@ def test_dense_device_api_and_sharded_single_rank(gpu):
     assert torch.equal(lat2[:n, :n], lat[:n, :n]) and torch.equal(rel2[:n, :n], rel[:n, :n])
 
 
-@pytest.mark.parametrize("hop_ms,enc", [(1, 3), (160, 2), (400, 1)])
-def test_dense_distance_encoding_tiers(gpu, hop_ms, enc):
+@pytest.mark.parametrize("hop_ms,enc,sym", [(1, 4, "1"), (1, 3, "0"), (160, 2, "1"), (400, 1, "1")])
+def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym):
     """Each distance encoding of the dense build (fw16.hip) is exact where it is chosen.
 
     A 256-vertex ring with hop latencies hop_ms / hop_ms+1 (gcd 1 ms) plus a few chords: the
     largest distance is ~128 * hop_ms quanta, so hop_ms = 1 fits the f16-compare path (cap
     0x3DFF), 160 saturates it and falls back to the u16 pk_min path (cap 0x7FFF), and 400
     saturates both and ends on the u32 kernels. Every tier must match the oracle bit for bit.
+    The graph is undirected, so the f16-compare tier runs its upper-triangle form (encoding 4)
+    unless SRT_FW_SYM=0 forces every tile (encoding 3).
     """
+    monkeypatch.setenv("SRT_FW_SYM", sym)
     n = 256
     rng = np.random.default_rng(hop_ms)
     src = list(range(n))
