@@ -67,6 +67,14 @@ double srt_topology_latency_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpN
 double srt_topology_reliability_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet);
 int srt_topology_increment_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet);
 uint64_t srt_topology_packet_count_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet);
+/* Packet-path consumer (worker.c:541-555): deliver/drop decision, delay in ns and the packet
+ * counter for one packet (1 delivered, 0 dropped, < 0 error) or a trace of them. */
+int srt_topology_send_packet_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet, double chance,
+                                int bootstrapping, uint64_t payloadLength, uint64_t* delayNs);
+int srt_topology_send_packets_ip(Topology* top, int64_t count, const uint32_t* srcIpNet,
+                                 const uint32_t* dstIpNet, const double* chance,
+                                 const uint8_t* bootstrapping, const uint64_t* payloadLength,
+                                 uint8_t* delivered, uint64_t* delayNs);
 /* Graph facts established by validation (topology.c:659-716). */
 int32_t srt_topology_vertex_count(Topology* top);
 int64_t srt_topology_edge_count(Topology* top);

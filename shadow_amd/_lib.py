@@ -117,6 +117,10 @@ SIGNATURES = {
     "srt_topology_reliability_ip": (_D, [_VP, _U32, _U32]),
     "srt_topology_increment_ip": (ctypes.c_int, [_VP, _U32, _U32]),
     "srt_topology_packet_count_ip": (_U64, [_VP, _U32, _U32]),
+    "srt_topology_send_packet_ip": (ctypes.c_int, [_VP, _U32, _U32, ctypes.c_double, ctypes.c_int,
+                                                   _U64, _VP]),
+    "srt_topology_send_packets_ip": (ctypes.c_int, [_VP, ctypes.c_int64, _VP, _VP, _VP, _VP, _VP,
+                                                    _VP, _VP]),
     "srt_topology_vertex_count": (_I32, [_VP]),
     "srt_topology_edge_count": (_I64, [_VP]),
     "srt_topology_is_directed": (ctypes.c_int, [_VP]),

@@ -882,6 +882,46 @@ uint64_t srt_topology_packet_count_ip(Topology* t, uint32_t srcIp, uint32_t dstI
     return v;
 }
 
+/* worker_sendPacket (/root/reference/src/main/core/worker.c:541-555): the fate of one packet on
+ * the path src -> dst. Delivered when bootstrapping, when chance <= reliability (:548) or when
+ * the payload is empty; then *delayNs = (u64)ceil(latency_ms * SIMTIME_ONE_MILLISECOND) (:550-551)
+ * and the pair's packet counter is incremented (:554). Returns 1 delivered, 0 dropped, or a
+ * negative SRT_E_* code. `chance` is the caller's random_nextDouble(host random) draw (:543). */
+int srt_topology_send_packet_ip(Topology* t, uint32_t srcIp, uint32_t dstIp, double chance,
+                                int bootstrapping, uint64_t payloadLength, uint64_t* delayNs) {
+    if (!magic_ok(t)) return SRT_E_ARG;
+    const int64_t i = path_index(t, srcIp, dstIp);
+    if (i < 0) return (int)i;
+    const double reliability = t->rel[i];
+    if (bootstrapping || chance <= reliability || payloadLength == 0) {
+        const double latency = (double)((uint64_t)t->lat_q[i] * t->quantum_ns) / 1000000.0;
+        if (delayNs) *delayNs = (uint64_t)ceil(latency * 1000000.0);
+        const int rc = srt_topology_increment_ip(t, srcIp, dstIp);
+        return rc ? rc : 1;
+    }
+    return 0;
+}
+
+/* srt_topology_send_packet_ip over a trace of `count` packets (one lookup per packet, no locks
+ * but the counter's). delivered[k] = 1/0; delay[k] is written for delivered packets. Returns
+ * SRT_OK or the first negative code (stopping there). */
+int srt_topology_send_packets_ip(Topology* t, int64_t count, const uint32_t* srcIp,
+                                 const uint32_t* dstIp, const double* chance,
+                                 const uint8_t* bootstrapping, const uint64_t* payloadLength,
+                                 uint8_t* delivered, uint64_t* delayNs) {
+    if (!magic_ok(t) || count < 0 || (count && (!srcIp || !dstIp || !chance || !delivered)))
+        return SRT_E_ARG;
+    for (int64_t k = 0; k < count; k++) {
+        const int r = srt_topology_send_packet_ip(t, srcIp[k], dstIp[k], chance[k],
+                                                  bootstrapping ? bootstrapping[k] : 0,
+                                                  payloadLength ? payloadLength[k] : 1,
+                                                  delayNs ? delayNs + k : NULL);
+        if (r < 0) return r;
+        delivered[k] = (uint8_t)r;
+    }
+    return SRT_OK;
+}
+
 double topology_getLatency(Topology* t, Address* src, Address* dst) {
     return srt_topology_latency_ip(t, address_toNetworkIP(src), address_toNetworkIP(dst));
 }

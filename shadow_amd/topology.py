@@ -28,8 +28,8 @@ from ._lib import BuildOpts, BuildStats, Edges, check, lib
 
 def ip_to_net(ip) -> int:
     """dotted string -> network-order u32 as stored in Address (inet_pton semantics)."""
-    if isinstance(ip, int):
-        return ip
+    if isinstance(ip, (int, np.integer)):
+        return int(ip)
     return struct.unpack("=I", socket.inet_aton(ip))[0]
 
 
@@ -154,6 +154,33 @@ class Topology:
 
     def packet_count(self, src, dst) -> int:
         return lib().srt_topology_packet_count_ip(self._h, ip_to_net(src), ip_to_net(dst))
+
+    def send_packet(self, src, dst, chance: float, bootstrapping: bool = False,
+                    payload_length: int = 1):
+        """worker_sendPacket's decision (worker.c:541-555): (delivered, delay_ns or None)."""
+        d = ctypes.c_uint64(0)
+        r = lib().srt_topology_send_packet_ip(self._h, ip_to_net(src), ip_to_net(dst),
+                                              float(chance), int(bool(bootstrapping)),
+                                              int(payload_length), ctypes.byref(d))
+        if r < 0:
+            check(r, "send_packet")
+        return (True, d.value) if r == 1 else (False, None)
+
+    def send_packets(self, src_net, dst_net, chance, bootstrapping=None, payload_length=None):
+        """Trace replay: network-order u32 IP arrays -> (delivered bool[k], delay_ns u64[k])."""
+        src = np.ascontiguousarray(src_net, np.uint32)
+        dst = np.ascontiguousarray(dst_net, np.uint32)
+        ch = np.ascontiguousarray(chance, np.float64)
+        k = len(src)
+        boot = None if bootstrapping is None else np.ascontiguousarray(bootstrapping, np.uint8)
+        pay = None if payload_length is None else np.ascontiguousarray(payload_length, np.uint64)
+        out = np.zeros(k, np.uint8)
+        delay = np.zeros(k, np.uint64)
+        ptr = lambda a: None if a is None else a.ctypes.data
+        check(lib().srt_topology_send_packets_ip(self._h, k, ptr(src), ptr(dst), ptr(ch),
+                                                 ptr(boot), ptr(pay), ptr(out), ptr(delay)),
+              "send_packets")
+        return out.astype(bool), delay
 
     def min_latency_ms(self) -> float:
         return lib().srt_topology_min_latency_ms(self._h)

@@ -281,3 +281,52 @@ def test_in_process_multi_gpu_build(gpu, kind, ngpus):
                                ngpus=ngpus)
     exp = _oracle(g)
     assert_tables(lat, rel, exp["lat_int"], exp["rel"], f"multi {kind} x{ngpus}")
+
+
+def test_packet_path_trace_replay(gpu):
+    """the packet-path consumer (worker.c:541-555) on a recorded trace gives the
+    reference's drop decisions, delivery delays and per-pair packet counts. Expected values come
+    from the committed C1 oracle tables: delivered iff bootstrapping, chance <= rel or an empty
+    payload; delay = ceil(lat_ms * 1e6) ns (worker.c:550-551, the oracle's lat_ref)."""
+    from shadow_amd.topology import ip_to_net
+    text = open(os.path.join(GOLDEN, "c1.gml")).read()
+    top = Topology.from_gml(text)
+    exp = np.load(os.path.join(GOLDEN, "c1_expected.npz"))
+    rng = np.random.default_rng(2024)
+    hosts = []
+    for h in range(120):  # hosts spread over the vertices; some share a vertex
+        ip = f"12.{h // 250}.{h % 250}.7"
+        v, _, _, _ = top.attach(ip, rand_state=h + 1)
+        hosts.append((ip_to_net(ip), v))
+    k = 20000
+    si = rng.integers(0, len(hosts), k)
+    di = rng.integers(0, len(hosts), k)
+    src = np.array([hosts[i][0] for i in si], np.uint32)
+    dst = np.array([hosts[i][0] for i in di], np.uint32)
+    vs = np.array([hosts[i][1] for i in si])
+    vd = np.array([hosts[i][1] for i in di])
+    chance = rng.random(k)
+    boot = (rng.random(k) < 0.05).astype(np.uint8)
+    payload = np.where(rng.random(k) < 0.1, 0, 1400).astype(np.uint64)
+    delivered, delay = top.send_packets(src, dst, chance, boot, payload)
+    rel = exp["rel"][vs, vd]
+    want = (boot == 1) | (chance <= rel) | (payload == 0)
+    assert np.array_equal(delivered, want)
+    lat_ref = np.ceil(exp["lat_ms"][vs, vd] * 1e6).astype(np.uint64)
+    assert np.array_equal(delay[want], lat_ref[want])
+    # per-pair counters (topology.c:1983-1993) equal the delivered counts
+    pairs = {}
+    for a, b, ok in zip(si, di, want):
+        if ok:
+            pairs[(a, b)] = pairs.get((a, b), 0) + 1
+    for (a, b), c in list(pairs.items())[:200]:
+        got = top.packet_count(hosts[a][0], hosts[b][0])
+        # the reference keys counters per cached path, i.e. per unordered vertex pair when the
+        # graph is undirected (topology.c:1189-1215): sum both directions over the same vertices
+        va, vb = hosts[a][1], hosts[b][1]
+        same = sum(cnt for (x, y), cnt in pairs.items()
+                   if {hosts[x][1], hosts[y][1]} == {va, vb})
+        assert got == same, (a, b, got, same)
+    # single-packet form agrees with the trace form
+    ok, d = top.send_packet(src[0], dst[0], chance[0], bool(boot[0]), int(payload[0]))
+    assert ok == bool(want[0]) and (not ok or d == lat_ref[0])
