@@ -414,9 +414,9 @@ __global__ void arc_transpose_fill(int n, const int32_t* __restrict__ ptr,
 /* transpose of the local row block. Blocks are mapped so that each XCD works on its own      */
 /* source block at a time (its 8 MB column slab stays in that XCD's L2 / the Infinity Cache). */
 /* ------------------------------------------------------------------------------------------ */
-template <typename T>
+template <typename T, typename TO = T>
 __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, const T* __restrict__ in,
-                                                        size_t ldi, T* __restrict__ out, size_t ldo) {
+                                                        size_t ldi, TO* __restrict__ out, size_t ldo) {
     __shared__ T tile[64][65];
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
@@ -427,7 +427,7 @@ __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, cons
     __syncthreads();
     for (int a = ty; a < 64; a += 4) {
         const int c = c0 + a, r = r0 + tx;
-        if (r < rows && c < cols) out[(size_t)c * ldo + r] = tile[tx][a];
+        if (r < rows && c < cols) out[(size_t)c * ldo + r] = (TO)tile[tx][a];
     }
 }
 
@@ -439,9 +439,15 @@ __global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nlo
                                                         const double* __restrict__ ar,
                                                         int32_t* __restrict__ predT,
                                                         double* __restrict__ rT, int nsb,
-                                                        int tch, int tper) {
+                                                        int tch, int tper, int sorted) {
     /* UR: write the predecessor vertex and the reliability of its arc (predT, rT) for the
-     * level-order pass; otherwise the arc index for the sweep pass */
+     * level-order pass; otherwise the arc index.
+     * sorted: t's in-arc list is in ascending u (undirected: the out-lists of the ballot-compacted
+     * essential arcs); the transposed lists of a directed graph are not, and key on u itself.
+     * Narrow distances (u8/u16: D < 2^16) and in-degrees < 2^16 pack the key (D[s][u], arc rank
+     * in t's list) into 32 bits; the lists are sorted by u, so the rank orders like u. A check is
+     * then add, compare, pack, select, min; the winner's vertex and reliability are read once. */
+    constexpr bool NARROW = sizeof(T) <= 2;
     const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
     const int sb = (j / tch) * 8 + xcd, tc = j % tch;
     if (sb >= nsb) return;
@@ -455,47 +461,71 @@ __global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nlo
         const uint32_t dst = DT[(size_t)t * ldT + sl];
         const int kb = __builtin_amdgcn_readfirstlane(iptr[t]);
         const int ke = __builtin_amdgcn_readfirstlane(iptr[t + 1]);
-        uint64_t best = ~0ull;
         int bk = -1;
-        double br = 0.0;
-        int k = kb;
-#define SRT_PRED_TRY(dd, aa, kk, rk)                                              \
-    if ((dd) + (aa).y == dst) {                                                   \
-        const uint64_t key = ((uint64_t)(dd) << 32) | (aa).x;                     \
-        if (key < best) {                                                         \
-            best = key;                                                           \
-            bk = (kk);                                                            \
-            if (UR) br = (rk);                                                    \
-        }                                                                         \
-    }
-        for (; k + 4 <= ke; k += 4) {
-            const uint2 a0 = uw[k], a1 = uw[k + 1], a2 = uw[k + 2], a3 = uw[k + 3];
-            double r0 = 0, r1 = 0, r2 = 0, r3 = 0; /* wave-uniform: scalar loads */
-            if (UR) {
-                r0 = ar[k];
-                r1 = ar[k + 1];
-                r2 = ar[k + 2];
-                r3 = ar[k + 3];
+        if (NARROW && ke - kb <= 0xFFFF) {
+            uint32_t best = 0xFFFFFFFFu;
+            int k = kb;
+#define SRT_PRED_TRY32(dd, aa, kk)                                                              \
+    best = min(best, ((dd) + (aa).y == dst)                                                    \
+                         ? (((dd) << 16) | (sorted ? (uint32_t)((kk) - kb) : (aa).x))          \
+                         : 0xFFFFFFFFu);
+            /* 16 (then 4, 1) candidate arcs per step: one batch of scalar loads, then the gathers
+             * in flight together. The loop is latency bound: with 4 per step, u8 and u16 distances
+             * measured the same (47 ms on C4); 16 per step 37 ms; 32 per step no better. */
+            for (; k + 16 <= ke; k += 16) {
+                uint2 a[16];
+                uint32_t dd[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) a[q] = uw[k + q];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) dd[q] = DT[(size_t)a[q].x * ldT + sl];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) SRT_PRED_TRY32(dd[q], a[q], k + q)
             }
-            const uint32_t d0 = DT[(size_t)a0.x * ldT + sl], d1 = DT[(size_t)a1.x * ldT + sl];
-            const uint32_t d2 = DT[(size_t)a2.x * ldT + sl], d3 = DT[(size_t)a3.x * ldT + sl];
-            SRT_PRED_TRY(d0, a0, k, r0)
-            SRT_PRED_TRY(d1, a1, k + 1, r1)
-            SRT_PRED_TRY(d2, a2, k + 2, r2)
-            SRT_PRED_TRY(d3, a3, k + 3, r3)
+            for (; k + 4 <= ke; k += 4) {
+                const uint2 a0 = uw[k], a1 = uw[k + 1], a2 = uw[k + 2], a3 = uw[k + 3];
+                const uint32_t d0 = DT[(size_t)a0.x * ldT + sl], d1 = DT[(size_t)a1.x * ldT + sl];
+                const uint32_t d2 = DT[(size_t)a2.x * ldT + sl], d3 = DT[(size_t)a3.x * ldT + sl];
+                SRT_PRED_TRY32(d0, a0, k)
+                SRT_PRED_TRY32(d1, a1, k + 1)
+                SRT_PRED_TRY32(d2, a2, k + 2)
+                SRT_PRED_TRY32(d3, a3, k + 3)
+            }
+            for (; k < ke; ++k) {
+                const uint2 a0 = uw[k];
+                const uint32_t d0 = DT[(size_t)a0.x * ldT + sl];
+                SRT_PRED_TRY32(d0, a0, k)
+            }
+#undef SRT_PRED_TRY32
+            if (best != 0xFFFFFFFFu) {
+                if (sorted) {
+                    bk = kb + (int)(best & 0xFFFFu);
+                } else { /* find the winning vertex's arc in the (unsorted) list */
+                    const uint32_t u = best & 0xFFFFu;
+                    for (int q = kb; q < ke; ++q) bk = (uw[q].x == u) ? q : bk;
+                }
+            }
+        } else {
+            uint64_t best = ~0ull;
+            int k = kb;
+            for (; k < ke; ++k) {
+                const uint2 a0 = uw[k];
+                const uint32_t d0 = DT[(size_t)a0.x * ldT + sl];
+                if (d0 + a0.y == dst) {
+                    const uint64_t key = ((uint64_t)d0 << 32) | a0.x;
+                    if (key < best) {
+                        best = key;
+                        bk = k;
+                    }
+                }
+            }
         }
-        for (; k < ke; ++k) {
-            const uint2 a0 = uw[k];
-            const double r0 = UR ? ar[k] : 0.0;
-            const uint32_t d0 = DT[(size_t)a0.x * ldT + sl];
-            SRT_PRED_TRY(d0, a0, k, r0)
-        }
-#undef SRT_PRED_TRY
         if (valid) {
             const size_t o = (size_t)t * ldT + sl;
             if (UR) {
-                predT[o] = (s == t || bk < 0) ? -1 : (int32_t)(uint32_t)best;
-                rT[o] = br;
+                const bool has = s != t && bk >= 0;
+                predT[o] = has ? (int32_t)uw[bk].x : -1;
+                rT[o] = has ? ar[bk] : 0.0;
             } else {
                 predT[o] = (s == t) ? -1 : bk;
             }
@@ -851,17 +881,29 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         size_t c4 = ws->rt_cap;
         if ((rc = ws_grow((void**)&ws->rt, &c4, slab, sizeof(double)))) return rc;
         ws->rt_cap = c4;
-        if (d16) {
+        if (d16 && srt_fw16_small()) {
+            /* every distance fits a byte: the transposed slab of a 64-source block is 2 MB and
+             * stays in its XCD's L2 */
+            uint8_t* dt8 = reinterpret_cast<uint8_t*>(ws->dt);
+            transpose_kernel<uint16_t, uint8_t><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)),
+                                                  256, 0, st>>>(nrows, ld, d16, (size_t)ld, dt8,
+                                                                (size_t)nrows);
+            pred_cols_kernel<uint8_t, true><<<grid, 256, 0, st>>>(
+                n, row0, lrows, nrows, dt8, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper,
+                !directed);
+        } else if (d16) {
             uint16_t* dt16 = reinterpret_cast<uint16_t*>(ws->dt);
             transpose_kernel<uint16_t><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)), 256, 0,
                                          st>>>(nrows, ld, d16, (size_t)ld, dt16, (size_t)nrows);
             pred_cols_kernel<uint16_t, true><<<grid, 256, 0, st>>>(
-                n, row0, lrows, nrows, dt16, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper);
+                n, row0, lrows, nrows, dt16, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper,
+                !directed);
         } else {
             transpose_kernel<uint32_t><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)), 256, 0,
                                          st>>>(nrows, ld, d, (size_t)ld, ws->dt, (size_t)nrows);
             pred_cols_kernel<uint32_t, true><<<grid, 256, 0, st>>>(
-                n, row0, lrows, nrows, ws->dt, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper);
+                n, row0, lrows, nrows, ws->dt, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper,
+                !directed);
         }
         /* predecessor rows pred[sl][t] = predT[t][sl] (reuses the DT buffer) and the arc
          * reliabilities straight into the rel rows, where the passes below finish them in place */

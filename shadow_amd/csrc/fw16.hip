@@ -587,17 +587,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 }
 
 /* widen to the u32 table and flag saturation of a real pair (i, j < n) */
+/* flags[0]: a real pair reached the cap (inexact); flags[1]: a real distance exceeds 254 quanta
+ * (the post pass can read the distances as u8 otherwise) -- one atomic per wave at most, and none
+ * once the flag is seen set */
 __global__ void fw16_finish_kernel(int n, int ld, int row0, const u16* __restrict__ d16,
-                                   uint32_t* __restrict__ lat, int* __restrict__ saturated,
+                                   uint32_t* __restrict__ lat, int* __restrict__ flags,
                                    uint32_t cap) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const int i = row0 + blockIdx.y;
-    if (j >= ld) return;
-    const size_t ix = (size_t)blockIdx.y * ld + j;
-    const uint32_t v = d16[ix];
-    const bool real = i < n && j < n;
-    lat[ix] = (v == cap) ? SRT_INF : v;
-    if (real && v == cap) atomicOr(saturated, 1);
+    bool big = false;
+    if (j < ld) {
+        const size_t ix = (size_t)blockIdx.y * ld + j;
+        const uint32_t v = d16[ix];
+        const bool real = i < n && j < n;
+        lat[ix] = (v == cap) ? SRT_INF : v;
+        if (real && v == cap) atomicOr(flags, 1);
+        big = real && v > 254u;
+    }
+    if (__ballot(big) && (threadIdx.x & 63) == 0 &&
+        !__hip_atomic_load(flags + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicOr(flags + 1, 1);
 }
 
 #ifndef SRT_FW16_DEVICE_ONLY
@@ -618,6 +627,12 @@ __global__ void fw16_finish_kernel(int n, int ld, int row0, const u16* __restric
 static u16* fw16_bufs[64];
 static size_t fw16_caps[64]; /* elements allocated in fw16_bufs (shared by both build forms) */
 static int* fw16_flags[64];
+static int fw16_small[64]; /* last build: every real distance <= 254 quanta */
+int srt_fw16_small(void) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    return fw16_small[dev & 63];
+}
 const uint16_t* srt_fw16_matrix(void) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return NULL;
@@ -665,7 +680,7 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
         SRT_HIPCHK(hipMalloc(&fw16_bufs[dev], need * sizeof(u16)));
         caps[dev] = need;
     }
-    if (!flags[dev]) SRT_HIPCHK(hipMalloc(&flags[dev], sizeof(int)));
+    if (!flags[dev]) SRT_HIPCHK(hipMalloc(&flags[dev], 2 * sizeof(int)));
     u16* d = fw16_bufs[dev];
     fw16_init_kernel<<<dim3(srt_ceil_div(ld, 256), ld), 256, 0, st>>>(n, ld, 0, w, d, CAP_F);
     SRT_HIPCHK(hipGetLastError());
@@ -682,14 +697,15 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
         SRT_HIPCHK(hipGetLastError());
     }
     fw16_mirror_kernel<<<dim3(nb, nb), 256, 0, st>>>(d, ld);
-    SRT_HIPCHK(hipMemsetAsync(flags[dev], 0, sizeof(int), st));
+    SRT_HIPCHK(hipMemsetAsync(flags[dev], 0, 2 * sizeof(int), st));
     fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 256), ld), 256, 0, st>>>(n, ld, 0, d, lat, flags[dev],
                                                                         CAP_F);
     SRT_HIPCHK(hipGetLastError());
-    int sat = 0;
-    SRT_HIPCHK(hipMemcpyAsync(&sat, flags[dev], sizeof(int), hipMemcpyDeviceToHost, st));
+    int hf[2] = {0, 0};
+    SRT_HIPCHK(hipMemcpyAsync(hf, flags[dev], 2 * sizeof(int), hipMemcpyDeviceToHost, st));
     SRT_HIPCHK(hipStreamSynchronize(st));
-    *exact = sat ? 0 : 1;
+    *exact = hf[0] ? 0 : 1;
+    fw16_small[dev] = hf[1] ? 0 : 1;
     return SRT_OK;
 }
 
@@ -792,15 +808,16 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
         if (lookahead) SRT_HIPCHK(hipEventRecord(sc->upd_done[k & 1], st));
         if (next && skip < 0 && (rc = produce(k + 1))) return rc;
     }
-    SRT_HIPCHK(hipMemsetAsync(flags[dev], 0, sizeof(int), st));
+    SRT_HIPCHK(hipMemsetAsync(flags[dev], 0, 2 * sizeof(int), st));
     if (nrows > 0)
         fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 256), nrows), 256, 0, st>>>(
             n, ld, row0, d, lat_rows, flags[dev], cap);
     SRT_HIPCHK(hipGetLastError());
-    int sat = 0;
-    SRT_HIPCHK(hipMemcpyAsync(&sat, flags[dev], sizeof(int), hipMemcpyDeviceToHost, st));
+    int hf[2] = {0, 0};
+    SRT_HIPCHK(hipMemcpyAsync(hf, flags[dev], 2 * sizeof(int), hipMemcpyDeviceToHost, st));
     SRT_HIPCHK(hipStreamSynchronize(st));
-    *exact = sat ? 0 : 1;
+    *exact = hf[0] ? 0 : 1;
+    fw16_small[dev] = hf[1] ? 0 : 1;
     return SRT_OK;
 }
 #endif /* SRT_FW16_DEVICE_ONLY */

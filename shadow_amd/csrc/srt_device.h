@@ -97,6 +97,8 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
                    void* ctx, int rank, int fm, int* sym, int* exact);
 /* the u16 working matrix of the last srt_fw16_build on the current device (row shard x ld) */
 const uint16_t* srt_fw16_matrix(void);
+/* 1 when every real distance of that build is <= 254 quanta (the post pass then reads u8) */
+int srt_fw16_small(void);
 /* distance encodings of the dense build, reported (negated) in srt_build_stats.fw_block */
 enum { SRT_DENC_U32 = 1, SRT_DENC_U16 = 2, SRT_DENC_F16CMP = 3, SRT_DENC_F16CMP_SYM = 4 };
 
