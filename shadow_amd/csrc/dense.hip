@@ -414,7 +414,9 @@ __global__ void arc_transpose_fill(int n, const int32_t* __restrict__ ptr,
 /* transpose of the local row block. Blocks are mapped so that each XCD works on its own      */
 /* source block at a time (its 8 MB column slab stays in that XCD's L2 / the Infinity Cache). */
 /* ------------------------------------------------------------------------------------------ */
-template <typename T, typename TO = T>
+/* out[c][r] = in[r][c]; BM (block-major): out[r / 64][c][r % 64], ldo = the stride of a 64-row
+ * block, so each 64-row block's transpose is one contiguous slab */
+template <typename T, typename TO = T, bool BM = false>
 __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, const T* __restrict__ in,
                                                         size_t ldi, TO* __restrict__ out, size_t ldo) {
     __shared__ T tile[64][65];
@@ -427,13 +429,16 @@ __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, cons
     __syncthreads();
     for (int a = ty; a < 64; a += 4) {
         const int c = c0 + a, r = r0 + tx;
-        if (r < rows && c < cols) out[(size_t)c * ldo + r] = (TO)tile[tx][a];
+        if (r < rows && c < cols) {
+            if (BM) out[(size_t)blockIdx.y * ldo + (size_t)c * 64 + tx] = (TO)tile[tx][a];
+            else out[(size_t)c * ldo + r] = (TO)tile[tx][a];
+        }
     }
 }
 
 template <typename T, bool UR>
 __global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nloc, int ldT,
-                                                        const T* __restrict__ DT,
+                                                        size_t bsD, const T* __restrict__ DT,
                                                         const int32_t* __restrict__ iptr,
                                                         const uint2* __restrict__ uw,
                                                         const double* __restrict__ ar,
@@ -457,8 +462,10 @@ __global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nlo
     const int s = row0 + sl;
     const bool valid = sl < nloc && s < n;
     const int t1 = min(n, (tc + 1) * tper);
+    /* this source block's contiguous slab of the block-major transpose: DB[u * 64] = D[s][u] */
+    const T* __restrict__ DB = DT + (size_t)sb * bsD + lane;
     for (int t = tc * tper + wv; t < t1; t += 4) {
-        const uint32_t dst = DT[(size_t)t * ldT + sl];
+        const uint32_t dst = DB[(size_t)t * 64];
         const int kb = __builtin_amdgcn_readfirstlane(iptr[t]);
         const int ke = __builtin_amdgcn_readfirstlane(iptr[t + 1]);
         int bk = -1;
@@ -478,14 +485,14 @@ __global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nlo
 #pragma unroll
                 for (int q = 0; q < 16; ++q) a[q] = uw[k + q];
 #pragma unroll
-                for (int q = 0; q < 16; ++q) dd[q] = DT[(size_t)a[q].x * ldT + sl];
+                for (int q = 0; q < 16; ++q) dd[q] = DB[(size_t)a[q].x * 64];
 #pragma unroll
                 for (int q = 0; q < 16; ++q) SRT_PRED_TRY32(dd[q], a[q], k + q)
             }
             for (; k + 4 <= ke; k += 4) {
                 const uint2 a0 = uw[k], a1 = uw[k + 1], a2 = uw[k + 2], a3 = uw[k + 3];
-                const uint32_t d0 = DT[(size_t)a0.x * ldT + sl], d1 = DT[(size_t)a1.x * ldT + sl];
-                const uint32_t d2 = DT[(size_t)a2.x * ldT + sl], d3 = DT[(size_t)a3.x * ldT + sl];
+                const uint32_t d0 = DB[(size_t)a0.x * 64], d1 = DB[(size_t)a1.x * 64];
+                const uint32_t d2 = DB[(size_t)a2.x * 64], d3 = DB[(size_t)a3.x * 64];
                 SRT_PRED_TRY32(d0, a0, k)
                 SRT_PRED_TRY32(d1, a1, k + 1)
                 SRT_PRED_TRY32(d2, a2, k + 2)
@@ -493,7 +500,7 @@ __global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nlo
             }
             for (; k < ke; ++k) {
                 const uint2 a0 = uw[k];
-                const uint32_t d0 = DT[(size_t)a0.x * ldT + sl];
+                const uint32_t d0 = DB[(size_t)a0.x * 64];
                 SRT_PRED_TRY32(d0, a0, k)
             }
 #undef SRT_PRED_TRY32
@@ -510,7 +517,7 @@ __global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nlo
             int k = kb;
             for (; k < ke; ++k) {
                 const uint2 a0 = uw[k];
-                const uint32_t d0 = DT[(size_t)a0.x * ldT + sl];
+                const uint32_t d0 = DB[(size_t)a0.x * 64];
                 if (d0 + a0.y == dst) {
                     const uint64_t key = ((uint64_t)d0 << 32) | a0.x;
                     if (key < best) {
@@ -860,6 +867,11 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
     }
     if (lrows > 0) {
         const size_t slab = (size_t)ld * nrows;
+        /* the transpose is block-major (DT[s / 64][u][s % 64]): a 64-source block's slab is
+         * contiguous, so it spreads over every L2 set and fills whole lines (a row-major transpose
+         * with its power-of-two stride put the slab in a few sets: 37.6 vs 30.0 ms with one line
+         * of padding on C4) */
+        const size_t bsD = (size_t)ld * 64;
         size_t c1 = ws->dt_cap, c2 = ws->predt_cap, c3 = ws->uw_cap;
         if ((rc = ws_grow((void**)&ws->dt, &c1, slab, sizeof(uint32_t)))) return rc;
         ws->dt_cap = c1;
@@ -885,24 +897,24 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
             /* every distance fits a byte: the transposed slab of a 64-source block is 2 MB and
              * stays in its XCD's L2 */
             uint8_t* dt8 = reinterpret_cast<uint8_t*>(ws->dt);
-            transpose_kernel<uint16_t, uint8_t><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)),
+            transpose_kernel<uint16_t, uint8_t, true><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)),
                                                   256, 0, st>>>(nrows, ld, d16, (size_t)ld, dt8,
-                                                                (size_t)nrows);
+                                                                bsD);
             pred_cols_kernel<uint8_t, true><<<grid, 256, 0, st>>>(
-                n, row0, lrows, nrows, dt8, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper,
+                n, row0, lrows, nrows, bsD, dt8, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper,
                 !directed);
         } else if (d16) {
             uint16_t* dt16 = reinterpret_cast<uint16_t*>(ws->dt);
-            transpose_kernel<uint16_t><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)), 256, 0,
-                                         st>>>(nrows, ld, d16, (size_t)ld, dt16, (size_t)nrows);
+            transpose_kernel<uint16_t, uint16_t, true><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)),
+                                                         256, 0, st>>>(nrows, ld, d16, (size_t)ld, dt16, bsD);
             pred_cols_kernel<uint16_t, true><<<grid, 256, 0, st>>>(
-                n, row0, lrows, nrows, dt16, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper,
+                n, row0, lrows, nrows, bsD, dt16, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper,
                 !directed);
         } else {
-            transpose_kernel<uint32_t><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)), 256, 0,
-                                         st>>>(nrows, ld, d, (size_t)ld, ws->dt, (size_t)nrows);
+            transpose_kernel<uint32_t, uint32_t, true><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)),
+                                                         256, 0, st>>>(nrows, ld, d, (size_t)ld, ws->dt, bsD);
             pred_cols_kernel<uint32_t, true><<<grid, 256, 0, st>>>(
-                n, row0, lrows, nrows, ws->dt, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper,
+                n, row0, lrows, nrows, bsD, ws->dt, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper,
                 !directed);
         }
         /* predecessor rows pred[sl][t] = predT[t][sl] (reuses the DT buffer) and the arc

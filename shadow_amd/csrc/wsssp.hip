@@ -291,7 +291,13 @@ int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, con
     const char* wenv = getenv("SRT_WSSSP_WAVES");
     size_t slots = ldsd ? (size_t)cus * ((160 * 1024) / (lds_row + lds_static))
                         : (size_t)(wenv && atoi(wenv) > 0 ? atoi(wenv) : 16) * cus;
-    const size_t budget = (size_t)16 << 30;
+    /* workspace budget: what the tables and the graph leave free, up to 64 GiB (C5 at 32
+     * waves/CU: 8192 slots x 4.6 MB) */
+    size_t budget = (size_t)16 << 30, free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > ((size_t)8 << 30)) {
+        budget = free_b - ((size_t)8 << 30);
+        if (budget > ((size_t)64 << 30)) budget = (size_t)64 << 30;
+    }
     if (slots * per_slot > budget) slots = budget / per_slot;
     if (slots > (size_t)nsrc) slots = nsrc;
     if (slots < 1) slots = 1;
