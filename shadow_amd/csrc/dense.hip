@@ -414,9 +414,9 @@ __global__ void arc_transpose_fill(int n, const int32_t* __restrict__ ptr,
 /* transpose of the local row block. Blocks are mapped so that each XCD works on its own      */
 /* source block at a time (its 8 MB column slab stays in that XCD's L2 / the Infinity Cache). */
 /* ------------------------------------------------------------------------------------------ */
-/* out[c][r] = in[r][c]; BM (block-major): out[r / 64][c][r % 64], ldo = the stride of a 64-row
- * block, so each 64-row block's transpose is one contiguous slab */
-template <typename T, typename TO = T, bool BM = false>
+/* out[c][r] = in[r][c]; BM (block-major, 64 or 128): out[r / BM][c][r % BM], ldo = the stride of
+ * a BM-row block, so each block's transpose is one contiguous slab */
+template <typename T, typename TO = T, int BM = 0>
 __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, const T* __restrict__ in,
                                                         size_t ldi, TO* __restrict__ out, size_t ldo) {
     __shared__ T tile[64][65];
@@ -430,8 +430,10 @@ __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, cons
     for (int a = ty; a < 64; a += 4) {
         const int c = c0 + a, r = r0 + tx;
         if (r < rows && c < cols) {
-            if (BM) out[(size_t)blockIdx.y * ldo + (size_t)c * 64 + tx] = (TO)tile[tx][a];
-            else out[(size_t)c * ldo + r] = (TO)tile[tx][a];
+            if constexpr (BM != 0)
+                out[(size_t)(r / BM) * ldo + (size_t)c * BM + (r % BM)] = (TO)tile[tx][a];
+            else
+                out[(size_t)c * ldo + r] = (TO)tile[tx][a];
         }
     }
 }
@@ -540,6 +542,107 @@ __global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nlo
     }
 }
 
+/* Byte distances, two sources per lane: a wave covers a 128-source block, one 128-B line of its
+ * block-major slab (DT[s / 128][u][s % 128], 4 MB at n = 32,768) per candidate arc. Same keys and
+ * outputs as pred_cols_kernel<uint8_t, true> for each of the lane's two sources. */
+template <int U>
+__global__ __launch_bounds__(256) void pred_cols2_kernel(int n, int row0, int nloc, int ldT,
+                                                         size_t bsD, const uint8_t* __restrict__ DT,
+                                                         const int32_t* __restrict__ iptr,
+                                                         const uint2* __restrict__ uw,
+                                                         const double* __restrict__ ar,
+                                                         int32_t* __restrict__ predT,
+                                                         double* __restrict__ rT, int nsb, int tch,
+                                                         int tper, int sorted) {
+    const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
+    const int sb = (j / tch) * 8 + xcd, tc = j % tch;
+    if (sb >= nsb) return;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int sl = sb * 128 + 2 * lane;
+    const int s = row0 + sl;
+    const bool v0 = sl < nloc && s < n, v1 = sl + 1 < nloc && s + 1 < n;
+    const int t1 = min(n, (tc + 1) * tper);
+    /* the slab through a buffer descriptor: row u is the scalar offset u * 128, the lane's two
+     * bytes the constant vector offset, so no per-arc 64-bit address lives in VGPRs */
+    const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(DT) + (size_t)sb * bsD, 0, (int)bsD, 0x00020000);
+    const int voff = 2 * lane;
+#define SRT_DB(u) ((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(slab, voff, (int)(u) * 128, 0))
+    for (int t = tc * tper + wv; t < t1; t += 4) {
+        const uint32_t dst = SRT_DB(t);
+        const uint32_t dst0 = dst & 0xFFu, dst1 = dst >> 8;
+        const int kb = __builtin_amdgcn_readfirstlane(iptr[t]);
+        const int ke = __builtin_amdgcn_readfirstlane(iptr[t + 1]);
+        uint32_t best0 = 0xFFFFFFFFu, best1 = 0xFFFFFFFFu;
+        int k = kb;
+#define SRT_PRED_TRY2(dd, aa, kk)                                                               \
+    {                                                                                           \
+        const uint32_t lo = (dd) & 0xFFu, hi = (dd) >> 8;                                       \
+        const uint32_t id = sorted ? (uint32_t)((kk) - kb) : (aa).x;                            \
+        best0 = min(best0, (lo + (aa).y == dst0) ? ((lo << 16) | id) : 0xFFFFFFFFu);            \
+        best1 = min(best1, (hi + (aa).y == dst1) ? ((hi << 16) | id) : 0xFFFFFFFFu);            \
+    }
+        for (; k + U <= ke; k += U) {
+            uint2 a[U];
+            uint32_t dd[U];
+#pragma unroll
+            for (int q = 0; q < U; ++q) a[q] = uw[k + q];
+#pragma unroll
+            for (int q = 0; q < U; ++q) dd[q] = SRT_DB(a[q].x);
+#pragma unroll
+            for (int q = 0; q < U; ++q) SRT_PRED_TRY2(dd[q], a[q], k + q)
+        }
+        for (; k + 4 <= ke; k += 4) {
+            uint2 a[4];
+            uint32_t dd[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a[q] = uw[k + q];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dd[q] = SRT_DB(a[q].x);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) SRT_PRED_TRY2(dd[q], a[q], k + q)
+        }
+        for (; k < ke; ++k) {
+            const uint2 a0 = uw[k];
+            const uint32_t d0 = SRT_DB(a0.x);
+            SRT_PRED_TRY2(d0, a0, k)
+        }
+#undef SRT_PRED_TRY2
+        int bk0 = -1, bk1 = -1;
+        if (sorted) {
+            if (best0 != 0xFFFFFFFFu) bk0 = kb + (int)(best0 & 0xFFFFu);
+            if (best1 != 0xFFFFFFFFu) bk1 = kb + (int)(best1 & 0xFFFFu);
+        } else { /* find the winning vertices' arcs in the (unsorted) list */
+            const uint32_t u0 = best0 != 0xFFFFFFFFu ? (best0 & 0xFFFFu) : 0xFFFFFFFFu;
+            const uint32_t u1 = best1 != 0xFFFFFFFFu ? (best1 & 0xFFFFu) : 0xFFFFFFFFu;
+            for (int q = kb; q < ke; ++q) {
+                const uint32_t u = uw[q].x;
+                bk0 = (u == u0) ? q : bk0;
+                bk1 = (u == u1) ? q : bk1;
+            }
+        }
+        const size_t o = (size_t)t * ldT + sl;
+        const bool h0 = s != t && bk0 >= 0, h1 = s + 1 != t && bk1 >= 0;
+        if (v0 && v1 && (o & 1) == 0) {
+            *reinterpret_cast<int2*>(predT + o) =
+                make_int2(h0 ? (int32_t)uw[bk0].x : -1, h1 ? (int32_t)uw[bk1].x : -1);
+            rT[o] = h0 ? ar[bk0] : 0.0;
+            rT[o + 1] = h1 ? ar[bk1] : 0.0;
+        } else {
+            if (v0) {
+                predT[o] = h0 ? (int32_t)uw[bk0].x : -1;
+                rT[o] = h0 ? ar[bk0] : 0.0;
+            }
+            if (v1) {
+                predT[o + 1] = h1 ? (int32_t)uw[bk1].x : -1;
+                rT[o + 1] = h1 ? ar[bk1] : 0.0;
+            }
+        }
+    }
+#undef SRT_DB
+}
+
 /* Path-order reliability by sweeps for rows with a large distance range (rel_levels_kernel
  * flagged them), one workgroup per row, same in-place (u, r) input. A target resolves once its
  * predecessor resolved in an earlier sweep (double-buffered LDS bitmaps; the sweeps = the depth
@@ -610,45 +713,90 @@ __global__ __launch_bounds__(512) void rel_sweeps_kernel(int n, int ld, int row0
  * D[s][t] == L) only reads values final since an earlier pass: each entry is formed once,
  * rel(s,t) = rel(s,pred) * r(pred,t), the left-to-right product of topology.c:1364-1365.
  * Rows whose largest distance exceeds maxl passes are flagged for rel_sweeps_kernel. */
-__global__ __launch_bounds__(512) void rel_levels_kernel(int n, int ld, int row0,
+__global__ __launch_bounds__(512, 4) void rel_levels_kernel(int n, int ld, int row0,
                                                          const uint32_t* __restrict__ lat,
                                                          const int32_t* __restrict__ pred,
                                                          double* __restrict__ rel, int maxl,
                                                          int32_t* __restrict__ max_depth,
                                                          int32_t* __restrict__ sweep) {
+    /* each thread owns t = tid + i * 512 (i < 64, n <= 32768); the row's distances are read once
+     * and kept as bytes in registers (levels <= maxl <= 254 once the row qualifies), so a pass
+     * only compares registers and touches memory for its own targets. The row reads go through
+     * buffer descriptors (constant scalar offset per i, one vector offset), which keeps the 64
+     * unrolled loads from holding 64-bit addresses. */
+    constexpr int PER = 64;
     const int s = row0 + blockIdx.x;
     if (s >= n) return;
+    const int tid = threadIdx.x;
     const uint32_t* dl = lat + (size_t)blockIdx.x * ld;
     const int32_t* pg = pred + (size_t)blockIdx.x * ld;
     double* rr = rel + (size_t)blockIdx.x * ld;
+    const __amdgpu_buffer_rsrc_t rd =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(dl), 0, n * 4, 0x00020000);
     __shared__ uint32_t red[8];
+    extern __shared__ uint16_t s_wlist[]; /* 8 waves x 64 x PER target indices */
+    uint32_t lv[PER / 4];
     uint32_t mx = 0;
-    for (int t = threadIdx.x; t < n; t += blockDim.x) {
-        const uint32_t x = dl[t];
-        if (t != s && x < SRT_INF) mx = max(mx, x);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        /* out of range reads 0 (the descriptor's bound): not a target of any pass, like the
+         * source itself and unreachable vertices */
+        const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(rd, tid * 4, i * 2048, 0);
+        const uint32_t x = (tid + i * 512 != s && d < SRT_INF) ? d : 0u;
+        mx = max(mx, x);
+        const uint32_t b = min(x, 255u) << (8 * (i & 3));
+        lv[i >> 2] = (i & 3) ? (lv[i >> 2] | b) : b;
     }
     for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
-    if (threadIdx.x == 0) __hip_atomic_store(rr + s, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if ((tid & 63) == 0) red[tid >> 6] = mx;
+    if (tid == 0) rr[s] = 1.0;
     __threadfence_block();
     __syncthreads();
     mx = 0;
     for (int i = 0; i < 8; ++i) mx = max(mx, red[i]);
-    if (threadIdx.x == 0) sweep[blockIdx.x] = (int)mx > maxl;
+    if (tid == 0) sweep[blockIdx.x] = (int)mx > maxl;
     if ((int)mx > maxl) return; /* long distance range: rel_sweeps_kernel takes the row */
+    /* per pass, each wave compacts its targets of level L into its own LDS list (ballot +
+     * prefix popcount), then walks the list with its lanes: the loads of different targets are
+     * independent and stay in flight together */
+    const int lane = tid & 63;
+    uint16_t* wl = s_wlist + (size_t)(tid >> 6) * (64 * PER);
+    const uint64_t lt = (1ull << lane) - 1ull;
     for (uint32_t L = 1; L <= mx; ++L) {
-        for (int t = threadIdx.x; t < n; t += blockDim.x) {
-            if (t == s || dl[t] != L) continue;
-            const int u = pg[t];
-            if (u < 0) continue; /* unreachable (cannot happen on a validated graph) */
-            const double ru = __hip_atomic_load(rr + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const double rt = __hip_atomic_load(rr + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_store(rr + t, ru * rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        int cnt = 0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const bool hit = ((lv[i >> 2] >> (8 * (i & 3))) & 0xFFu) == L;
+            const uint64_t m = __ballot(hit);
+            if (hit) wl[cnt + __popcll(m & lt)] = (uint16_t)(tid + i * 512);
+            cnt += __popcll(m);
+        }
+        /* the list is written and read by this wave only */
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        /* eight targets per lane in flight: a pass costs about two dependent global latencies
+         * (pred, then rel of the predecessor) per 512 targets of the wave */
+        for (int j = lane; j < cnt; j += 512) {
+            int t[8], u[8];
+            double rt[8], ru[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) t[q] = j + 64 * q < cnt ? (int)wl[j + 64 * q] : -1;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) u[q] = t[q] >= 0 ? pg[t[q]] : -1;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) rt[q] = t[q] >= 0 ? rr[t[q]] : 0.0;
+            /* u < 0: unreachable, cannot happen on a validated graph; the entry is kept */
+#pragma unroll
+            for (int q = 0; q < 8; ++q) ru[q] = u[q] >= 0 ? rr[u[q]] : 1.0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (t[q] >= 0) rr[t[q]] = ru[q] * rt[q];
         }
         __threadfence_block();
         __syncthreads();
     }
-    if (threadIdx.x == 0) atomicMax(max_depth, (int)mx);
+    if (tid == 0) atomicMax(max_depth, (int)mx);
 }
 
 __global__ void pack_uw_kernel(int64_t arcs, const int32_t* __restrict__ col,
@@ -897,21 +1045,23 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
             /* every distance fits a byte: the transposed slab of a 64-source block is 2 MB and
              * stays in its XCD's L2 */
             uint8_t* dt8 = reinterpret_cast<uint8_t*>(ws->dt);
-            transpose_kernel<uint16_t, uint8_t, true><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)),
-                                                  256, 0, st>>>(nrows, ld, d16, (size_t)ld, dt8,
-                                                                bsD);
-            pred_cols_kernel<uint8_t, true><<<grid, 256, 0, st>>>(
-                n, row0, lrows, nrows, bsD, dt8, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper,
-                !directed);
+            const int nsb2 = srt_ceil_div(nrows, 128);
+            transpose_kernel<uint16_t, uint8_t, 128><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)),
+                                                     256, 0, st>>>(nrows, ld, d16, (size_t)ld, dt8,
+                                                                   (size_t)ld * 128);
+            /* 16 candidate arcs in flight per step: 17.3 ms on C4 against 18.7 (8) and 20.0 (32) */
+            pred_cols2_kernel<16><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
+                n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
+                nsb2, tch, tper, !directed);
         } else if (d16) {
             uint16_t* dt16 = reinterpret_cast<uint16_t*>(ws->dt);
-            transpose_kernel<uint16_t, uint16_t, true><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)),
+            transpose_kernel<uint16_t, uint16_t, 64><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)),
                                                          256, 0, st>>>(nrows, ld, d16, (size_t)ld, dt16, bsD);
             pred_cols_kernel<uint16_t, true><<<grid, 256, 0, st>>>(
                 n, row0, lrows, nrows, bsD, dt16, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper,
                 !directed);
         } else {
-            transpose_kernel<uint32_t, uint32_t, true><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)),
+            transpose_kernel<uint32_t, uint32_t, 64><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)),
                                                          256, 0, st>>>(nrows, ld, d, (size_t)ld, ws->dt, bsD);
             pred_cols_kernel<uint32_t, true><<<grid, 256, 0, st>>>(
                 n, row0, lrows, nrows, bsD, ws->dt, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper,
@@ -927,7 +1077,9 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
             n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
         /* level order for rows whose distances span <= 64 quanta, sweeps for the rest
          * (ws->cursor is free here and carries the per-row hand-over flags) */
-        rel_levels_kernel<<<lrows, 512, 0, st>>>(n, ld, row0, d, pred, rel, 64, ws->depth,
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
+        rel_levels_kernel<<<lrows, 512, 65536, st>>>(n, ld, row0, d, pred, rel, 64, ws->depth,
                                                  ws->cursor);
         const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
         SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel,
