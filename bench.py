@@ -291,8 +291,9 @@ def run_sparse(c: Ctx, wl):
     nsrc = s1 - s0
     k_ms = sum(s.ms_update for s in stats) / max(sum(s.n_update for s in stats), 1)
     achieved_gbs = nsrc * bytes_per_src / (k_ms * 1e-3) / 1e9
-    roofline = {"bound": "hbm", "kernel": "sssp_kernel<%s>" % (
-        "false" if n <= L.srt_sparse_max_n() else "true"),
+    lds_row = 8 * (n * 4 + 4096) <= 160 * 1024  # wsssp.hip: LDS working row when 8 waves/CU fit
+    roofline = {"bound": "hbm", "kernel": "wsssp_kernel<%s, %s>" % (
+        "true" if g.directed else "false", "true" if lds_row else "false"),
         "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None,
         "bytes_per_launch": float(nsrc * bytes_per_src), "avg_launch_ms": round(k_ms, 3),

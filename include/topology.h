@@ -61,6 +61,14 @@ int32_t srt_topology_attach_ip(Topology* top, uint32_t ipNet, uint32_t* randStat
                                const char* ipHint, const char* citycodeHint,
                                const char* countrycodeHint, uint64_t* bwDownOut,
                                uint64_t* bwUpOut);
+/* Batched attach of nhosts addresses, each exactly as srt_topology_attach_ip
+ * in order; per-host rand_r states; hint arrays and output arrays may be NULL. Returns the
+ * number attached or a negative SRT_E_* code. Replaces topology.c:2132-2272 per host. */
+int32_t srt_topology_attach_batch_ip(Topology* top, int32_t nhosts, const uint32_t* ipNet,
+                                     uint32_t* randStates, const char* const* ipHints,
+                                     const char* const* citycodeHints,
+                                     const char* const* countrycodeHints, int32_t* outVertex,
+                                     uint64_t* bwDownOut, uint64_t* bwUpOut);
 void srt_topology_detach_ip(Topology* top, uint32_t ipNet);
 int32_t srt_topology_vertex_of_ip(Topology* top, uint32_t ipNet);
 double srt_topology_latency_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet);

@@ -111,6 +111,7 @@ SIGNATURES = {
     # topology.h (IP-level additions)
     "srt_topology_new_from_string": (_VP, [_CP, ctypes.c_int]),
     "srt_topology_attach_ip": (_I32, [_VP, _U32, _VP, _CP, _CP, _CP, _VP, _VP]),
+    "srt_topology_attach_batch_ip": (_I32, [_VP, _I32, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "srt_topology_detach_ip": (None, [_VP, _U32]),
     "srt_topology_vertex_of_ip": (_I32, [_VP, _U32]),
     "srt_topology_latency_ip": (_D, [_VP, _U32, _U32]),

@@ -9,6 +9,7 @@
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
+#include <ctype.h>
 #include <math.h>
 #include <netinet/in.h>
 #include <pthread.h>
@@ -188,9 +189,13 @@ struct _Topology {
     /* counters */
     pthread_mutex_t cnt_lock;
     cntmap_t counters;
+    /* attach index (built on the first attach) */
+    pthread_mutex_t ax_lock;
+    void* ax;
 };
 
 static int magic_ok(const Topology* t) { return t && t->magic == TOPOLOGY_MAGIC; }
+static void attach_index_free(Topology* t);
 
 /* address_stringToIP (address.c:145-152): network order, INADDR_NONE on failure */
 static uint32_t string_to_ip(const char* s) {
@@ -489,6 +494,7 @@ static Topology* topology_from_text(const char* text, size_t len, int useShortes
     pthread_rwlock_init(&t->ip_lock, NULL);
     pthread_mutex_init(&t->build_lock, NULL);
     pthread_mutex_init(&t->cnt_lock, NULL);
+    pthread_mutex_init(&t->ax_lock, NULL);
     atomic_store(&t->built, 0);
     t->opts.device = 0;
     t->opts.algo = SRT_ALGO_AUTO;
@@ -558,116 +564,307 @@ void topology_free(Topology* t) {
     pthread_rwlock_destroy(&t->ip_lock);
     pthread_mutex_destroy(&t->build_lock);
     pthread_mutex_destroy(&t->cnt_lock);
+    attach_index_free(t);
+    pthread_mutex_destroy(&t->ax_lock);
     t->magic = 0;
     free(t);
 }
 
-/* ---- attach (topology.c:2024-2272) ----------------------------------------------------- */
+/* ---- attach (topology.c:2024-2272) ----------------------------------------------------- *
+ * The reference scans every vertex per host (hook :2024-2100), re-parsing its IP string and
+ * comparing hint strings, and then takes the longest prefix match (:2102-2130) or a random
+ * candidate (:2188-2196). The outcome depends only on the vertex attributes and the hints, so the
+ * attributes are indexed once (lazily, on the first attach) and every attach is O(log n):
+ *  - raw vertex IPs (string_to_ip of the attribute, INADDR_NONE when absent), all vertices
+ *    sorted by (ip, vertex);
+ *  - city and country codes interned case-insensitively (g_ascii_strcasecmp); per code the
+ *    vertices in index order (the candidate queue), the count with a usable IP, and the same
+ *    vertices sorted by (ip, vertex).
+ * Candidate queues are the reference's: an exact usable-IP match keeps only the exact matches
+ * (in index order); otherwise city, then country, then all vertices.
+ * LPM: match = ~(ip ^ key) is largest where ip ^ key is smallest; XOR with a fixed key is a
+ * bijection, so one IP value wins, found by a 32-step bit descent over the sorted queue (see
+ * lpm_pick; the nearest neighbours of key in sorted order are not enough: {0x0, 0x7} with key
+ * 0x8 is won by 0x0). The reference's update rule (match > best || best == 0) keeps the first
+ * candidate with the largest match when that match is > 0, which is the first vertex of the
+ * winning IP's (ip, vertex)-sorted run; when every match is 0 it ends on the last candidate of
+ * the queue. */
 typedef struct {
-    int32_t* v;
-    int32_t len, head;
-} queue_t;
+    uint32_t ip;
+    int32_t v;
+} ipv_t;
 
-static void q_push(queue_t* q, int32_t x) { q->v[q->len++] = x; }
+typedef struct {
+    char** names;    /* sorted, lowercase, unique */
+    int32_t count;
+    int32_t* ptr;    /* count + 1 */
+    int32_t* list;   /* vertices of each code, index order */
+    ipv_t* sorted;   /* the same segments sorted by (ip, vertex) */
+    int32_t* usable; /* per code: vertices with a usable IP */
+} code_index;
+
+typedef struct {
+    uint32_t* vip; /* raw IP per vertex */
+    ipv_t* all_sorted;
+    int32_t all_usable;
+    code_index city, country;
+} attach_index;
+
+static int ip_usable(uint32_t ip) {
+    /* INADDR_LOOPBACK is host order compared to a network-order value (topology.c:2051) */
+    return ip != INADDR_NONE && ip != INADDR_ANY && ip != INADDR_LOOPBACK;
+}
+
+static int ipv_cmp(const void* a, const void* b) {
+    const ipv_t* x = (const ipv_t*)a;
+    const ipv_t* y = (const ipv_t*)b;
+    if (x->ip != y->ip) return x->ip < y->ip ? -1 : 1;
+    return (x->v > y->v) - (x->v < y->v);
+}
+
+static char* lower_dup(const char* s) {
+    size_t n = strlen(s);
+    char* d = (char*)malloc(n + 1);
+    if (!d) return NULL;
+    for (size_t i = 0; i <= n; i++) d[i] = (char)tolower((unsigned char)s[i]);
+    return d;
+}
+
+typedef struct {
+    char* key;
+    int32_t v;
+} keyv_t;
+
+static int keyv_cmp(const void* a, const void* b) {
+    const keyv_t* x = (const keyv_t*)a;
+    const keyv_t* y = (const keyv_t*)b;
+    int c = strcmp(x->key, y->key);
+    if (c) return c;
+    return (x->v > y->v) - (x->v < y->v);
+}
+
+static int code_index_build(code_index* ci, const char** codes, int32_t n, const uint32_t* vip) {
+    memset(ci, 0, sizeof(*ci));
+    keyv_t* kv = (keyv_t*)malloc((size_t)(n > 0 ? n : 1) * sizeof(keyv_t));
+    if (!kv) return SRT_E_NOMEM;
+    int32_t m = 0;
+    for (int32_t v = 0; v < n; v++) {
+        if (!codes[v]) continue;
+        kv[m].key = lower_dup(codes[v]);
+        if (!kv[m].key) {
+            for (int32_t q = 0; q < m; q++) free(kv[q].key);
+            free(kv);
+            return SRT_E_NOMEM;
+        }
+        kv[m++].v = v;
+    }
+    qsort(kv, (size_t)m, sizeof(keyv_t), keyv_cmp); /* by code, then vertex index */
+    int32_t nc = 0;
+    for (int32_t q = 0; q < m; q++)
+        if (q == 0 || strcmp(kv[q].key, kv[q - 1].key)) nc++;
+    ci->names = (char**)calloc((size_t)(nc > 0 ? nc : 1), sizeof(char*));
+    ci->ptr = (int32_t*)calloc((size_t)nc + 1, sizeof(int32_t));
+    ci->list = (int32_t*)malloc((size_t)(m > 0 ? m : 1) * sizeof(int32_t));
+    ci->sorted = (ipv_t*)malloc((size_t)(m > 0 ? m : 1) * sizeof(ipv_t));
+    ci->usable = (int32_t*)calloc((size_t)(nc > 0 ? nc : 1), sizeof(int32_t));
+    if (!ci->names || !ci->ptr || !ci->list || !ci->sorted || !ci->usable) {
+        for (int32_t q = 0; q < m; q++) free(kv[q].key);
+        free(kv);
+        return SRT_E_NOMEM;
+    }
+    int32_t c = -1;
+    for (int32_t q = 0; q < m; q++) {
+        if (c < 0 || strcmp(kv[q].key, ci->names[c])) { /* duplicates are freed below */
+            ci->names[++c] = kv[q].key;
+            ci->ptr[c] = q;
+        } else {
+            free(kv[q].key);
+        }
+        ci->list[q] = kv[q].v;
+        ci->sorted[q].ip = vip[kv[q].v];
+        ci->sorted[q].v = kv[q].v;
+        ci->usable[c] += ip_usable(vip[kv[q].v]);
+    }
+    ci->count = nc;
+    ci->ptr[nc] = m;
+    for (int32_t k = 0; k < nc; k++)
+        qsort(ci->sorted + ci->ptr[k], (size_t)(ci->ptr[k + 1] - ci->ptr[k]), sizeof(ipv_t), ipv_cmp);
+    free(kv);
+    return SRT_OK;
+}
+
+static void code_index_free(code_index* ci) {
+    for (int32_t k = 0; k < ci->count; k++) free(ci->names[k]);
+    free(ci->names);
+    free(ci->ptr);
+    free(ci->list);
+    free(ci->sorted);
+    free(ci->usable);
+    memset(ci, 0, sizeof(*ci));
+}
+
+/* interned id of a hint (case-insensitive), -1 when no vertex carries it */
+static int32_t code_lookup(const code_index* ci, const char* hint) {
+    if (!hint || ci->count == 0) return -1;
+    char* key = lower_dup(hint);
+    if (!key) return -1;
+    int32_t lo = 0, hi = ci->count - 1, found = -1;
+    while (lo <= hi) {
+        int32_t mid = lo + (hi - lo) / 2;
+        int c = strcmp(ci->names[mid], key);
+        if (c == 0) {
+            found = mid;
+            break;
+        }
+        if (c < 0) lo = mid + 1;
+        else hi = mid - 1;
+    }
+    free(key);
+    return found;
+}
+
+/* first position in s[0, len) whose ip is >= key */
+static int32_t ipv_lower(const ipv_t* s, int32_t len, uint32_t key) {
+    int32_t lo = 0, hi = len;
+    while (lo < hi) {
+        int32_t mid = lo + (hi - lo) / 2;
+        if (s[mid].ip < key) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+/* first position in [lo, hi) whose ip is >= key */
+static int32_t ipv_lower_in(const ipv_t* s, int32_t lo, int32_t hi, uint32_t key) {
+    while (lo < hi) {
+        int32_t mid = lo + (hi - lo) / 2;
+        if (s[mid].ip < key) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+/* _topology_getLongestPrefixMatch over one candidate queue: `sorted` is the queue sorted by
+ * (ip, vertex), `last` the queue's last vertex in queue order. The smallest ip ^ key is found by
+ * descending the bits from the top, as in a binary trie: [lo, hi) holds the IPs that agree with
+ * the best choice so far above bit b, ordered so that bit b = 0 comes first; keep the half whose
+ * bit b equals key's when it is non-empty. The range ends on one IP value. */
+static int32_t lpm_pick(const ipv_t* sorted, int32_t len, int32_t last, uint32_t key) {
+    int32_t lo = 0, hi = len;
+    for (int b = 31; b >= 0; --b) {
+        const uint32_t bit = 1u << b;
+        const uint32_t high = b == 31 ? 0u : sorted[lo].ip & ~((bit << 1) - 1u);
+        const int32_t split = ipv_lower_in(sorted, lo, hi, high | bit);
+        if (key & bit) {
+            if (split < hi) lo = split;
+        } else {
+            if (split > lo) hi = split;
+        }
+    }
+    if (~(sorted[lo].ip ^ key) == 0u) return last; /* every match is 0: the update rule ends on the last */
+    return sorted[lo].v; /* the first vertex holding the best IP */
+}
+
+static void attach_index_free(Topology* t) {
+    attach_index* ax = (attach_index*)t->ax;
+    if (!ax) return;
+    free(ax->vip);
+    free(ax->all_sorted);
+    code_index_free(&ax->city);
+    code_index_free(&ax->country);
+    free(ax);
+    t->ax = NULL;
+}
+
+static attach_index* attach_index_of(Topology* t) {
+    pthread_mutex_lock(&t->ax_lock);
+    if (!t->ax) {
+        const int32_t n = t->n;
+        attach_index* ax = (attach_index*)calloc(1, sizeof(attach_index));
+        int ok = ax != NULL;
+        if (ok) {
+            ax->vip = (uint32_t*)malloc((size_t)(n > 0 ? n : 1) * sizeof(uint32_t));
+            ax->all_sorted = (ipv_t*)malloc((size_t)(n > 0 ? n : 1) * sizeof(ipv_t));
+            ok = ax->vip && ax->all_sorted;
+        }
+        if (ok) {
+            for (int32_t v = 0; v < n; v++) {
+                const char* ipStr = t->vip[v];
+                ax->vip[v] = (ipStr && ipStr[0]) ? string_to_ip(ipStr) : INADDR_NONE;
+                ax->all_sorted[v].ip = ax->vip[v];
+                ax->all_sorted[v].v = v;
+                ax->all_usable += ip_usable(ax->vip[v]);
+            }
+            qsort(ax->all_sorted, (size_t)n, sizeof(ipv_t), ipv_cmp);
+            ok = code_index_build(&ax->city, t->vcity, n, ax->vip) == SRT_OK &&
+                 code_index_build(&ax->country, t->vcountry, n, ax->vip) == SRT_OK;
+        }
+        t->ax = ax;
+        if (!ok) attach_index_free(t);
+    }
+    attach_index* r = (attach_index*)t->ax;
+    pthread_mutex_unlock(&t->ax_lock);
+    return r;
+}
 
 static int32_t find_attachment_vertex(Topology* t, uint32_t* rand_state, Random* rnd,
                                       const char* ipHint, const char* cityHint,
                                       const char* countryHint) {
-    int32_t n = t->n;
-    queue_t city = {(int32_t*)malloc((size_t)n * sizeof(int32_t)), 0, 0};
-    queue_t country = {(int32_t*)malloc((size_t)n * sizeof(int32_t)), 0, 0};
-    queue_t all = {(int32_t*)malloc((size_t)n * sizeof(int32_t)), 0, 0};
-    if (!city.v || !country.v || !all.v) {
-        free(city.v);
-        free(country.v);
-        free(all.v);
-        return -1;
-    }
-    uint32_t numIPsCity = 0, numIPsCountry = 0, numIPsAll = 0;
-    int requestedIPIsUsable = 0, foundExact = 0;
+    attach_index* ax = attach_index_of(t);
+    if (!ax) return -1;
+    const int32_t n = t->n;
+    int requestedIPIsUsable = 0;
     uint32_t requestedIP = 0;
     if (ipHint) {
         uint32_t ip = string_to_ip(ipHint);
-        /* INADDR_LOOPBACK is host order compared to a network-order value (topology.c:2146) */
-        if (ip != INADDR_NONE && ip != INADDR_ANY && ip != INADDR_LOOPBACK) {
+        if (ip_usable(ip)) {
             requestedIPIsUsable = 1;
             requestedIP = ip;
         }
     }
-    for (int32_t v = 0; v < n; v++) { /* _topology_findAttachmentVertexHelperHook :2024-2100 */
-        const char* ipStr = t->vip[v];
-        int ipFound = ipStr && ipStr[0];
-        int cityMatch = t->vcity[v] && cityHint && !strcasecmp(t->vcity[v], cityHint);
-        int countryMatch = t->vcountry[v] && countryHint && !strcasecmp(t->vcountry[v], countryHint);
-        int usable = 0;
-        uint32_t vip = INADDR_NONE;
-        if (ipFound) {
-            uint32_t ip = string_to_ip(ipStr);
-            if (ip != INADDR_NONE && ip != INADDR_ANY && ip != INADDR_LOOPBACK) {
-                usable = 1;
-                vip = ip;
-            }
-        }
-        if (requestedIPIsUsable && usable && vip == requestedIP) {
-            if (!foundExact) {
-                city.len = country.len = all.len = 0;
-            }
-            foundExact = 1;
-            q_push(&all, v);
-            numIPsAll++;
-        }
-        if (foundExact) continue;
-        q_push(&all, v);
-        if (usable) numIPsAll++;
-        if (cityMatch) {
-            q_push(&city, v);
-            if (usable) numIPsCity++;
-        }
-        if (countryMatch) {
-            q_push(&country, v);
-            if (usable) numIPsCountry++;
+    /* candidate queue: `seg` in queue order (NULL: all vertices), `sorted` by (ip, vertex) */
+    const int32_t* seg = NULL;
+    const ipv_t* sorted = ax->all_sorted;
+    int32_t len = n, useLPM = 0, exact = 0;
+    if (requestedIPIsUsable) {
+        const int32_t a = ipv_lower(ax->all_sorted, n, requestedIP);
+        const int32_t b = ipv_lower(ax->all_sorted, n, requestedIP + 1u);
+        if (b > a && ax->all_sorted[a].ip == requestedIP) { /* exact matches, index order */
+            exact = 1;
+            sorted = ax->all_sorted + a;
+            len = (requestedIP == 0xFFFFFFFFu ? n : b) - a;
         }
     }
-    queue_t* cand;
-    int useLPM;
-    if (city.len > 0) {
-        cand = &city;
-        useLPM = requestedIPIsUsable && numIPsCity > 0;
-    } else if (country.len > 0) {
-        cand = &country;
-        useLPM = requestedIPIsUsable && numIPsCountry > 0;
-    } else {
-        cand = &all;
-        useLPM = ipHint && numIPsAll > 0; /* the hint's presence, not its usability (:2178) */
-    }
-    int32_t chosen = -1;
-    if (cand->len > 0) {
-        if (useLPM && !foundExact) { /* _topology_getLongestPrefixMatch :2102-2130 */
-            uint32_t bestMatch = 0;
-            for (int32_t i = 0; i < cand->len; i++) {
-                int32_t v = cand->v[i];
-                uint32_t vip = string_to_ip(t->vip[v]);
-                uint32_t match = ~(vip ^ requestedIP);
-                if (match > bestMatch || bestMatch == 0) {
-                    bestMatch = match;
-                    chosen = v;
-                }
-            }
-        } else { /* :2188-2196 */
-            double u;
-            if (rnd)
-                u = random_nextDouble(rnd);
-            else
-                u = (double)rand_r(rand_state) / (double)RAND_MAX; /* random.c:32-43 */
-            int indexRange = cand->len - 1;
-            int chosenIndex = (int)round((double)(indexRange * u));
-            chosen = cand->v[chosenIndex < cand->len ? chosenIndex : cand->len - 1];
+    if (!exact) {
+        const int32_t c = code_lookup(&ax->city, cityHint);
+        const int32_t k = c < 0 ? code_lookup(&ax->country, countryHint) : -1;
+        if (c >= 0) {
+            seg = ax->city.list + ax->city.ptr[c];
+            sorted = ax->city.sorted + ax->city.ptr[c];
+            len = ax->city.ptr[c + 1] - ax->city.ptr[c];
+            useLPM = requestedIPIsUsable && ax->city.usable[c] > 0;
+        } else if (k >= 0) {
+            seg = ax->country.list + ax->country.ptr[k];
+            sorted = ax->country.sorted + ax->country.ptr[k];
+            len = ax->country.ptr[k + 1] - ax->country.ptr[k];
+            useLPM = requestedIPIsUsable && ax->country.usable[k] > 0;
+        } else {
+            useLPM = ipHint && ax->all_usable > 0; /* the hint's presence, not its usability (:2178) */
         }
     }
-    free(city.v);
-    free(country.v);
-    free(all.v);
-    return chosen;
+    if (len <= 0) return -1;
+    if (useLPM) return lpm_pick(sorted, len, seg ? seg[len - 1] : n - 1, requestedIP);
+    /* :2188-2196 */
+    double u;
+    if (rnd)
+        u = random_nextDouble(rnd);
+    else
+        u = (double)rand_r(rand_state) / (double)RAND_MAX; /* random.c:32-43 */
+    const int indexRange = len - 1;
+    int chosenIndex = (int)round((double)(indexRange * u));
+    if (chosenIndex >= len) chosenIndex = len - 1;
+    if (exact) return sorted[chosenIndex].v; /* the run is in vertex order */
+    return seg ? seg[chosenIndex] : chosenIndex;
 }
 
 static int32_t attach_common(Topology* t, uint32_t ipNet, uint32_t* rand_state, Random* rnd,
@@ -697,6 +894,49 @@ int32_t srt_topology_attach_ip(Topology* t, uint32_t ipNet, uint32_t* randState,
     if (!randState) return SRT_E_ARG;
     return attach_common(t, ipNet, randState, NULL, ipHint, citycodeHint, countrycodeHint,
                          bwDownOut, bwUpOut);
+}
+
+/* Batched attach: hosts in order, each exactly as srt_topology_attach_ip
+ * would attach it (host h draws from randStates[h] only when its pick is random), with one
+ * write-lock for the IP map. Hint arrays may be NULL or hold NULL entries; output arrays may
+ * be NULL. Returns the number of hosts attached, or a negative error code for a host without a
+ * candidate (the reference asserts, topology.c:2182) -- the hosts before it stay attached. */
+int32_t srt_topology_attach_batch_ip(Topology* t, int32_t nhosts, const uint32_t* ipNet,
+                                     uint32_t* randStates, const char* const* ipHints,
+                                     const char* const* citycodeHints,
+                                     const char* const* countrycodeHints, int32_t* outVertex,
+                                     uint64_t* bwDownOut, uint64_t* bwUpOut) {
+    if (!magic_ok(t) || nhosts < 0 || (nhosts > 0 && (!ipNet || !randStates))) return SRT_E_ARG;
+    if (!attach_index_of(t)) return SRT_E_NOMEM;
+    int32_t* vs = (int32_t*)malloc((size_t)(nhosts > 0 ? nhosts : 1) * sizeof(int32_t));
+    if (!vs) return SRT_E_NOMEM;
+    int32_t done = 0, rc = 0;
+    for (; done < nhosts; done++) {
+        const int32_t v = find_attachment_vertex(
+            t, randStates + done, NULL, ipHints ? ipHints[done] : NULL,
+            citycodeHints ? citycodeHints[done] : NULL,
+            countrycodeHints ? countrycodeHints[done] : NULL);
+        if (v < 0) {
+            srt_set_error("attach batch: no attachment vertex for host %d", done);
+            rc = SRT_E_ARG;
+            break;
+        }
+        vs[done] = v;
+    }
+    pthread_rwlock_wrlock(&t->ip_lock);
+    for (int32_t h = 0; h < done; h++) {
+        ipmap_put(&t->ipmap, ipNet[h], vs[h]);
+        t->attached[vs[h]] = 1;
+    }
+    pthread_rwlock_unlock(&t->ip_lock);
+    for (int32_t h = 0; h < done; h++) {
+        if (outVertex) outVertex[h] = vs[h];
+        if (bwDownOut) bwDownOut[h] = t->bw_down_kib[vs[h]];
+        if (bwUpOut) bwUpOut[h] = t->bw_up_kib[vs[h]];
+    }
+    free(vs);
+    srt_log(SRT_LOG_INFO, "attached %d addresses in one batch", done);
+    return rc ? rc : done;
 }
 
 void topology_attach(Topology* t, Address* address, Random* randomSourcePool, char* ipHint,

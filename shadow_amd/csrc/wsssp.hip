@@ -291,6 +291,13 @@ int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, con
     const char* wenv = getenv("SRT_WSSSP_WAVES");
     size_t slots = ldsd ? (size_t)cus * ((160 * 1024) / (lds_row + lds_static))
                         : (size_t)(wenv && atoi(wenv) > 0 ? atoi(wenv) : 16) * cus;
+    /* the random gathers into the working rows are served by L2 / Infinity Cache / HBM; past
+     * about 1.4 GB of rows in flight more waves only thrash (C5, n = 100,000: 16 waves/CU
+     * 2.90 s, 3,500 waves 2.6 s, 8/CU 2.66 s; C3, n = 20,000: 16/CU 73 ms, 8/CU 98 ms) */
+    if (!ldsd && !(wenv && atoi(wenv) > 0)) {
+        const size_t cap = ((size_t)1400 << 20) / ((size_t)n * sizeof(uint32_t));
+        if (slots > cap) slots = cap > (size_t)cus ? cap : (size_t)cus;
+    }
     /* workspace budget: what the tables and the graph leave free, up to 64 GiB (C5 at 32
      * waves/CU: 8192 slots x 4.6 MB) */
     size_t budget = (size_t)16 << 30, free_b = 0, total_b = 0;

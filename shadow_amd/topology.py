@@ -107,6 +107,32 @@ class Topology:
             check(v, "attach")
         return v, down.value, up.value, st.value
 
+    def attach_batch(self, ips, rand_states, ip_hints=None, city_hints=None, country_hints=None):
+        """Attach many hosts in order (srt_topology_attach_batch_ip). Returns (vertices, bw_down,
+        bw_up, new_rand_states) as numpy arrays."""
+        h = len(ips)
+        ipn = np.array([ip_to_net(x) for x in ips], dtype=np.uint32)
+        st = np.ascontiguousarray(np.asarray(rand_states, dtype=np.uint32).copy())
+        out = np.zeros(h, dtype=np.int32)
+        down = np.zeros(h, dtype=np.uint64)
+        up = np.zeros(h, dtype=np.uint64)
+
+        def strs(a):
+            if a is None:
+                return None
+            arr = (ctypes.c_char_p * h)()
+            for i, x in enumerate(a):
+                arr[i] = None if x is None else x.encode()
+            return arr
+
+        hints = [strs(ip_hints), strs(city_hints), strs(country_hints)]
+        ptr = lambda x: x.ctypes.data_as(ctypes.c_void_p)
+        r = lib().srt_topology_attach_batch_ip(self._h, h, ptr(ipn), ptr(st), *hints, ptr(out),
+                                               ptr(down), ptr(up))
+        if r < 0:
+            check(r, "attach_batch")
+        return out, down, up, st
+
     def detach(self, ip) -> None:
         lib().srt_topology_detach_ip(self._h, ip_to_net(ip))
 

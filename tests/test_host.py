@@ -139,6 +139,80 @@ def test_attach_detach_lookup(native):
     assert not top.is_routable("11.0.0.9", "11.0.0.10")
 
 
+def _attach_world(rng, n):
+    """Vertex attributes with duplicates, gaps and the special addresses the reference treats as
+    unusable (0.0.0.0, 255.255.255.255, an unparsable string, and 1.0.0.127, whose network-order
+    value equals the host-order INADDR_LOOPBACK constant, topology.c:2051)."""
+    pool = [f"10.{a}.{b}.{c}" for a, b, c in rng.integers(0, 4, size=(24, 3))]
+    special = ["0.0.0.0", "255.255.255.255", "bogus", "1.0.0.127", "127.0.0.1", "10.20.30.40"]
+    cities = ["Portland", "portland", "PORTLAND", "Berlin", "berlin", "Lima", "zz"]
+    countries = ["US", "us", "DE", "Pe", "pe"]
+    verts = []
+    for v in range(n):
+        a = {}
+        r = rng.random()
+        if r < 0.7:
+            a["ip"] = pool[rng.integers(len(pool))]
+        elif r < 0.85:
+            a["ip"] = special[rng.integers(len(special))]
+        if rng.random() < 0.6:
+            a["city"] = cities[rng.integers(len(cities) - 1)]
+        if rng.random() < 0.7:
+            a["country"] = countries[rng.integers(len(countries))]
+        verts.append(a)
+    for v in (n - 7, n - 3):  # the all-zero-match queue: city "zz", both at 10.20.30.40
+        verts[v] = {"ip": "10.20.30.40", "city": "zz", "country": "US"}
+    nodes = []
+    for v, a in enumerate(verts):
+        extra = " ".join(f'{k} "{a[x]}"' for x, k in (("ip", "ip_address"), ("city", "city_code"),
+                                                   ("country", "country_code")) if x in a)
+        nodes.append((v, extra))
+    edges = [(v, v, "1 ms", 0.0, "") for v in range(n)]
+    edges += [(v, v + 1, "2 ms", 0.0, "") for v in range(n - 1)]
+    return verts, gml(nodes, edges), pool
+
+
+def _attach_hosts(rng, h, pool):
+    ipish = pool + ["0.0.0.0", "127.0.0.1", "1.0.0.127", "bogus", "245.235.225.215", "10.9.9.9",
+                    "11.3.2.1", "200.1.2.3"]
+    out = []
+    for i in range(h):
+        ip = None if rng.random() < 0.25 else ipish[rng.integers(len(ipish))]
+        city = None if rng.random() < 0.5 else ["portland", "Berlin", "LIMA", "zz", "Oslo",
+                                                 "ZZ"][rng.integers(6)]
+        ctry = None if rng.random() < 0.5 else ["us", "De", "PE", "FR"][rng.integers(4)]
+        out.append((ip, city, ctry, int(rng.integers(1, 2**31))))
+    # 245.235.225.215 is ~10.20.30.40: every match in city "zz" is 0 -> the queue's last vertex
+    out.append(("245.235.225.215", "zz", None, 7))
+    return out
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3, 4, 5])
+def test_attach_indexed_matches_restatement(native, seed):
+    """The O(log n) indexed attach (single and batched) against the pure-Python restatement of
+    the reference's per-host vertex scan (oracle/attach.py), hints and seeds randomized."""
+    from oracle import attach as oa
+    rng = np.random.default_rng(seed)
+    verts, text, pool = _attach_world(rng, 257)
+    hosts = _attach_hosts(rng, 600, pool)
+    want, want_state = [], []
+    for ip, city, ctry, sd in hosts:
+        st = [sd]
+        want.append(oa.find_attachment_vertex(verts, st, ip, city, ctry))
+        want_state.append(st[0])
+    top = Topology.from_gml(text)
+    for i, (ip, city, ctry, sd) in enumerate(hosts):
+        v, _, _, after = top.attach(f"100.65.{i // 250}.{i % 250 + 1}", sd, ip, city, ctry)
+        assert (v, after) == (want[i], want_state[i]), hosts[i]
+    top2 = Topology.from_gml(text)
+    addrs = [f"100.66.{i // 250}.{i % 250 + 1}" for i in range(len(hosts))]
+    vs, down, up, states = top2.attach_batch(addrs, [h[3] for h in hosts], [h[0] for h in hosts],
+                                             [h[1] for h in hosts], [h[2] for h in hosts])
+    assert vs.tolist() == want and states.tolist() == want_state
+    assert top2.vertex_of(addrs[5]) == want[5]
+    assert hosts[-1][0] == "245.235.225.215" and want[-1] == 257 - 3
+
+
 # ---- C-ABI exports ---------------------------------------------------------------------------
 def _declared(header):
     text = open(os.path.join(ROOT, "include", header)).read()
