@@ -113,6 +113,7 @@ struct srt_sparse_graph {
     int64_t arcs;
     uint64_t quantum_ns;
     uint32_t delta, max_w;
+    int local; /* relabelled arcs span <= 4096 vertices on average (graph.c CM order) */
     int32_t *rp, *col, *irp, *icol;
     uint32_t *w, *iw, *sw;
     double *r, *ir, *sr;
@@ -127,7 +128,8 @@ struct srt_sparse_graph {
 
 int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, const double* r,
                    const int2* in_rowptr, const uint2* in_cw, const double* in_r,
-                   const int32_t* perm, const int32_t* inv, uint32_t max_w, int src_begin,
+                   const int32_t* perm, const int32_t* inv, uint32_t max_w, int local,
+                   int src_begin,
                    int src_end, uint32_t* lat, double* rel, int* ovf, hipStream_t st);
 int srt_sparse_diag(int n, int src_begin, int src_end, const int32_t* rowptr, const int32_t* col,
                     const uint32_t* w, const double* r, const uint32_t* self_w,
@@ -285,6 +287,13 @@ static int sparse_graph_from_canon(const srt_canon* c, int device, srt_sparse_gr
     if (!rc) rc = cuthill_mckee(c, hperm, hinv);
     if (!rc) {
         relabel_csr(c->n, c->rowptr, c->col, c->w, c->r, hperm, hinv, hrp, hcw, hr);
+        /* locality of the relabelled graph: the wave kernel keeps its reliability row in
+         * relabelled order when an arc's ends are close there (RGG-like graphs: the
+         * predecessor's entry is near), else writes the output rows at settle time */
+        double span = 0.0;
+        for (int32_t v = 0; v < c->n; v++)
+            for (int32_t k = hrp[v].x; k < hrp[v].y; k++) span += fabs((double)v - (double)hcw[k].x);
+        g->local = na == 0 || span / (double)na <= 4096.0;
         rc = up((void**)&g->perm, hperm, nv * 4);
         if (!rc) rc = up((void**)&g->inv, hinv, nv * 4);
         if (!rc) rc = up((void**)&g->rp2, hrp, nv * sizeof(int2));
@@ -368,7 +377,8 @@ extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begi
     SRT_HIPCHK(hipEventCreate(&e2));
     SRT_HIPCHK(hipEventRecord(e0, st));
     int rc = srt_wsssp_rows(g->n, g->directed, g->rp2, g->cw2, g->r2, g->irp2, g->icw2, g->ir2,
-                            g->perm, g->inv, g->max_w, src_begin, src_end, lat_rows, rel_rows, ovf,
+                            g->perm, g->inv, g->max_w, g->local, src_begin, src_end, lat_rows,
+                            rel_rows, ovf,
                             st);
     if (rc) return rc;
     SRT_HIPCHK(hipEventRecord(e1, st));

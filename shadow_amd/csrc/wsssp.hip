@@ -22,10 +22,14 @@
  * shares cache lines with the next ones (the C3 profile without it: 28% L2 hits, 245 GB fetched
  * for 44 GB of algorithmic bytes). Arcs of a relabelled row stay sorted by ORIGINAL neighbour
  * index, so the (D[u], arc index) key still breaks ties by original vertex index.
- * Memory: a per-wave working distance row (u32 quanta, relabelled order, L2-coherent loads and
- * atomics) and bucket ring (C x bcap vertex ids) in global memory; bucket counts and the
- * non-empty mask in LDS. Settled values go straight to the output rows in original order. A bucket overflow flags the source and the
- * caller recomputes it with the workgroup-per-source kernel (sparse.hip) -- never approximate.
+ * Memory: per wave a working distance row (u32 quanta) and a reliability row (f64), both in
+ * relabelled order, and a bucket ring (C x bcap vertex ids) in global memory; bucket counts and
+ * the non-empty mask in LDS. The predecessor's reliability is read from the relabelled row, where
+ * graph neighbours sit close together; when the source is done, one pass gathers both rows into
+ * the output rows in original order with whole-line writes (settle-time scattered 4- and 8-byte
+ * writes into the output rows were partial-line HBM writes). A bucket overflow flags the source
+ * and the caller recomputes it with the workgroup-per-source kernel (sparse.hip) -- never
+ * approximate.
  *
  * Arc work inside one step is balanced across lanes merge-path style: the settled vertices of a
  * 64-entry chunk are laid end to end by an exclusive scan of their degrees, and each lane finds
@@ -65,7 +69,7 @@ static __device__ __forceinline__ int wave_scan_max(int v, int lane) {
     return v;
 }
 
-template <bool DIRECTED, bool LDSD>
+template <bool DIRECTED, bool LDSD, bool RELP>
 __global__ __launch_bounds__(WL) void wsssp_kernel(
     int n, int src_begin, int nsrc, const int2* __restrict__ rowptr,
     const uint2* __restrict__ cw, const double* __restrict__ r,
@@ -80,7 +84,12 @@ __global__ __launch_bounds__(WL) void wsssp_kernel(
     __shared__ int s_ovf;
     const int lane = threadIdx.x;
     extern __shared__ uint32_t sdist[]; /* LDSD: the working row lives in LDS */
-    uint32_t* buckets = ws + (size_t)blockIdx.x * ((size_t)nb * bcap + (LDSD ? 0 : n));
+    /* per slot: the path-order reliability row (f64, relabelled order), the bucket ring, then
+     * (global form) the distance row (relabelled order) */
+    const size_t relw = RELP ? 2 * (size_t)n : 0;
+    const size_t slot_words = (relw + (size_t)nb * bcap + (LDSD ? 0 : n) + 1) & ~(size_t)1;
+    double* relp = reinterpret_cast<double*>(ws + (size_t)blockIdx.x * slot_words);
+    uint32_t* buckets = ws + (size_t)blockIdx.x * slot_words + relw;
     uint32_t* dist = LDSD ? sdist : buckets + (size_t)nb * bcap; /* working row, relabelled */
     auto dload = [&](uint32_t i) -> uint32_t {
         if constexpr (LDSD) return sdist[i];
@@ -94,8 +103,12 @@ __global__ __launch_bounds__(WL) void wsssp_kernel(
         double* rr = rel + (size_t)si * ldo;
         for (int v = lane; v < n; v += WL) {
             dist[v] = (v == s) ? 0u : SRT_INF;
-            ol[v] = SRT_INF;
-            rr[v] = 0.0;
+            if (RELP) {
+                relp[v] = 0.0;
+            } else {
+                ol[v] = SRT_INF;
+                rr[v] = 0.0;
+            }
         }
         for (int b = lane; b < nb; b += WL) bcnt[b] = 0;
         if (lane < 4) bmask[lane] = 0ull;
@@ -223,7 +236,9 @@ __global__ __launch_bounds__(WL) void wsssp_kernel(
                     }
                 }
                 __syncthreads();
-                /* settle: path-order reliability from the canonical predecessor */
+                /* settle: path-order reliability from the canonical predecessor, kept in the
+                 * relabelled row (the predecessor is a graph neighbour, so its entry is usually
+                 * near v's); the distance is already final in dist[v] */
                 if (v >= 0) {
                     double x = 1.0;
                     if (v != s) {
@@ -234,17 +249,33 @@ __global__ __launch_bounds__(WL) void wsssp_kernel(
                         if (key != ~0ull) {
                             const int k = (int)(uint32_t)key;
                             const uint32_t u = DIRECTED ? in_cw[k].x : cw[k].x;
-                            x = ld_coherent(rr + perm[u]) * (DIRECTED ? in_r[k] : r[k]);
+                            x = ld_coherent(RELP ? relp + u : rr + perm[u]) *
+                                (DIRECTED ? in_r[k] : r[k]);
                         }
                     }
-                    const int vo = perm[v];
-                    ol[vo] = d;
-                    rr[vo] = x;
+                    if (RELP) {
+                        relp[v] = x;
+                    } else {
+                        const int vo = perm[v];
+                        ol[vo] = d;
+                        rr[vo] = x;
+                    }
                 }
                 __threadfence_block(); /* settled rel visible to the later steps of this wave */
                 __syncthreads();
             }
             if (s_ovf) break;
+        }
+        /* output rows in original order: whole-line writes, the relabelled rows gathered
+         * (unreached vertices keep INF / 0) */
+        __threadfence_block();
+        __syncthreads();
+        if (RELP) {
+            for (int i = lane; i < n; i += WL) {
+                const int v = inv[i];
+                ol[i] = dload((uint32_t)v);
+                rr[i] = ld_coherent(relp + v);
+            }
         }
         if (s_ovf && lane == 0) overflow[si] = 1;
         __syncthreads();
@@ -260,8 +291,9 @@ int srt_sparse_diag(int n, int src_begin, int src_end, const int32_t* rowptr, co
  * (device, nsrc ints, zeroed here) for the caller to recompute. */
 int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, const double* r,
                    const int2* in_rowptr, const uint2* in_cw, const double* in_r,
-                   const int32_t* perm, const int32_t* inv, uint32_t max_w, int src_begin,
-                   int src_end, uint32_t* lat, double* rel, int* ovf, hipStream_t st) {
+                   const int32_t* perm, const int32_t* inv, uint32_t max_w, int local,
+                   int src_begin, int src_end, uint32_t* lat, double* rel, int* ovf,
+                   hipStream_t st) {
     int nb = 1;
     while ((uint32_t)nb <= max_w) nb <<= 1;
     if (nb > 256) {
@@ -287,7 +319,13 @@ int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, con
      * default only while it still fits 8 waves per CU; SRT_WSSSP_LDS=1/0 forces either form */
     const bool ldsd = lenv ? (atoi(lenv) != 0 && lds_row + lds_static <= 160 * 1024)
                            : 8 * (lds_row + lds_static) <= 160 * 1024;
-    const size_t per_slot = ((size_t)nb * bcap + (ldsd ? 0 : n)) * sizeof(uint32_t);
+    /* the kernel's slot layout: f64 reliability row, bucket ring, u32 distance row (global form),
+     * padded to 8 bytes */
+    const char* renv = getenv("SRT_WSSSP_RELROW"); /* tests: force either reliability form */
+    const bool relp = renv ? atoi(renv) != 0 : local != 0;
+    const size_t per_slot =
+        (((relp ? 2 * (size_t)n : 0) + (size_t)nb * bcap + (ldsd ? 0 : n) + 1) & ~(size_t)1) *
+        sizeof(uint32_t);
     const char* wenv = getenv("SRT_WSSSP_WAVES");
     size_t slots = ldsd ? (size_t)cus * ((160 * 1024) / (lds_row + lds_static))
                         : (size_t)(wenv && atoi(wenv) > 0 ? atoi(wenv) : 16) * cus;
@@ -316,20 +354,25 @@ int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, con
     }
     SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)nsrc * sizeof(int), st));
     const size_t dyn = ldsd ? lds_row : 0;
-#define SRT_WSSSP_LAUNCH(D, L)                                                                   \
+#define SRT_WSSSP_LAUNCH(D, L, R)                                                                \
     do {                                                                                         \
-        if (dyn) SRT_HIPCHK(hipFuncSetAttribute((const void*)wsssp_kernel<D, L>,                  \
+        if (dyn) SRT_HIPCHK(hipFuncSetAttribute((const void*)wsssp_kernel<D, L, R>,               \
                                                 hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                                 (int)dyn));                                       \
-        wsssp_kernel<D, L><<<(unsigned)slots, WL, dyn, st>>>(n, src_begin, nsrc, rowptr, cw, r,   \
-                                                            in_rowptr, in_cw, in_r, perm, inv,    \
-                                                            lat, rel, (size_t)n, ws, nb, bcap,    \
-                                                            ovf);                                 \
+        wsssp_kernel<D, L, R><<<(unsigned)slots, WL, dyn, st>>>(                                  \
+            n, src_begin, nsrc, rowptr, cw, r, in_rowptr, in_cw, in_r, perm, inv, lat, rel,       \
+            (size_t)n, ws, nb, bcap, ovf);                                                        \
     } while (0)
-    if (directed && ldsd) SRT_WSSSP_LAUNCH(true, true);
-    else if (directed) SRT_WSSSP_LAUNCH(true, false);
-    else if (ldsd) SRT_WSSSP_LAUNCH(false, true);
-    else SRT_WSSSP_LAUNCH(false, false);
+#define SRT_WSSSP_LAUNCH2(D, L)                                                                  \
+    do {                                                                                         \
+        if (relp) SRT_WSSSP_LAUNCH(D, L, true);                                                   \
+        else SRT_WSSSP_LAUNCH(D, L, false);                                                       \
+    } while (0)
+    if (directed && ldsd) SRT_WSSSP_LAUNCH2(true, true);
+    else if (directed) SRT_WSSSP_LAUNCH2(true, false);
+    else if (ldsd) SRT_WSSSP_LAUNCH2(false, true);
+    else SRT_WSSSP_LAUNCH2(false, false);
+#undef SRT_WSSSP_LAUNCH2
 #undef SRT_WSSSP_LAUNCH
     SRT_HIPCHK(hipGetLastError());
     SRT_HIPCHK(hipFreeAsync(ws, st));

@@ -126,11 +126,13 @@ def test_wave_kernel_matches_block_kernel_c3_rows(gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("which", ["rgg3000", "ba2000", "directed"])
-@pytest.mark.parametrize("lds", ["0", "1"])
-def test_wave_kernel_working_row_forms(gpu, monkeypatch, which, lds):
-    """SRT_WSSSP_LDS=0/1: the wave kernel's working distance row in global memory or in LDS gives
-    the same exact tables."""
+@pytest.mark.parametrize("lds,relrow", [("0", "0"), ("0", "1"), ("1", "0"), ("1", "1")])
+def test_wave_kernel_working_row_forms(gpu, monkeypatch, which, lds, relrow):
+    """SRT_WSSSP_LDS=0/1 (working distance row in global memory or in LDS) x SRT_WSSSP_RELROW=0/1
+    (reliability written to the output rows at settle time, or kept in a relabelled row and
+    gathered at the end): every form gives the same exact tables."""
     monkeypatch.setenv("SRT_WSSSP_LDS", lds)
+    monkeypatch.setenv("SRT_WSSSP_RELROW", relrow)
     if which == "rgg3000":
         g = graphs.random_geometric(3000, seed=3)
     elif which == "ba2000":
