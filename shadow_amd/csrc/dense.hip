@@ -713,18 +713,19 @@ __global__ __launch_bounds__(512) void rel_sweeps_kernel(int n, int ld, int row0
  * D[s][t] == L) only reads values final since an earlier pass: each entry is formed once,
  * rel(s,t) = rel(s,pred) * r(pred,t), the left-to-right product of topology.c:1364-1365.
  * Rows whose largest distance exceeds maxl passes are flagged for rel_sweeps_kernel. */
-__global__ __launch_bounds__(512, 4) void rel_levels_kernel(int n, int ld, int row0,
+template <int NT>
+__global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
                                                          const uint32_t* __restrict__ lat,
                                                          const int32_t* __restrict__ pred,
                                                          double* __restrict__ rel, int maxl,
                                                          int32_t* __restrict__ max_depth,
                                                          int32_t* __restrict__ sweep) {
-    /* each thread owns t = tid + i * 512 (i < 64, n <= 32768); the row's distances are read once
+    /* each thread owns t = tid + i * NT (i < PER, n <= 32768); the row's distances are read once
      * and kept as bytes in registers (levels <= maxl <= 254 once the row qualifies), so a pass
      * only compares registers and touches memory for its own targets. The row reads go through
      * buffer descriptors (constant scalar offset per i, one vector offset), which keeps the 64
      * unrolled loads from holding 64-bit addresses. */
-    constexpr int PER = 64;
+    constexpr int PER = 32768 / NT;
     const int s = row0 + blockIdx.x;
     if (s >= n) return;
     const int tid = threadIdx.x;
@@ -733,16 +734,16 @@ __global__ __launch_bounds__(512, 4) void rel_levels_kernel(int n, int ld, int r
     double* rr = rel + (size_t)blockIdx.x * ld;
     const __amdgpu_buffer_rsrc_t rd =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(dl), 0, n * 4, 0x00020000);
-    __shared__ uint32_t red[8];
-    extern __shared__ uint16_t s_wlist[]; /* 8 waves x 64 x PER target indices */
+    __shared__ uint32_t red[NT / 64];
+    extern __shared__ uint16_t s_wlist[]; /* NT / 64 waves x 64 x PER target indices */
     uint32_t lv[PER / 4];
     uint32_t mx = 0;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
         /* out of range reads 0 (the descriptor's bound): not a target of any pass, like the
          * source itself and unreachable vertices */
-        const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(rd, tid * 4, i * 2048, 0);
-        const uint32_t x = (tid + i * 512 != s && d < SRT_INF) ? d : 0u;
+        const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(rd, tid * 4, i * NT * 4, 0);
+        const uint32_t x = (tid + i * NT != s && d < SRT_INF) ? d : 0u;
         mx = max(mx, x);
         const uint32_t b = min(x, 255u) << (8 * (i & 3));
         lv[i >> 2] = (i & 3) ? (lv[i >> 2] | b) : b;
@@ -753,7 +754,7 @@ __global__ __launch_bounds__(512, 4) void rel_levels_kernel(int n, int ld, int r
     __threadfence_block();
     __syncthreads();
     mx = 0;
-    for (int i = 0; i < 8; ++i) mx = max(mx, red[i]);
+    for (int i = 0; i < NT / 64; ++i) mx = max(mx, red[i]);
     if (tid == 0) sweep[blockIdx.x] = (int)mx > maxl;
     if ((int)mx > maxl) return; /* long distance range: rel_sweeps_kernel takes the row */
     /* per pass, each wave compacts its targets of level L into its own LDS list (ballot +
@@ -768,29 +769,30 @@ __global__ __launch_bounds__(512, 4) void rel_levels_kernel(int n, int ld, int r
         for (int i = 0; i < PER; ++i) {
             const bool hit = ((lv[i >> 2] >> (8 * (i & 3))) & 0xFFu) == L;
             const uint64_t m = __ballot(hit);
-            if (hit) wl[cnt + __popcll(m & lt)] = (uint16_t)(tid + i * 512);
+            if (hit) wl[cnt + __popcll(m & lt)] = (uint16_t)(tid + i * NT);
             cnt += __popcll(m);
         }
         /* the list is written and read by this wave only */
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        /* eight targets per lane in flight: a pass costs about two dependent global latencies
-         * (pred, then rel of the predecessor) per 512 targets of the wave */
-        for (int j = lane; j < cnt; j += 512) {
-            int t[8], u[8];
-            double rt[8], ru[8];
+        /* QB targets per lane in flight: a pass costs about two dependent global latencies
+         * (pred, then rel of the predecessor) per 64 * QB targets of the wave */
+        constexpr int QB = 8;
+        for (int j = lane; j < cnt; j += 64 * QB) {
+            int t[QB], u[QB];
+            double rt[QB], ru[QB];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) t[q] = j + 64 * q < cnt ? (int)wl[j + 64 * q] : -1;
+            for (int q = 0; q < QB; ++q) t[q] = j + 64 * q < cnt ? (int)wl[j + 64 * q] : -1;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) u[q] = t[q] >= 0 ? pg[t[q]] : -1;
+            for (int q = 0; q < QB; ++q) u[q] = t[q] >= 0 ? pg[t[q]] : -1;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) rt[q] = t[q] >= 0 ? rr[t[q]] : 0.0;
+            for (int q = 0; q < QB; ++q) rt[q] = t[q] >= 0 ? rr[t[q]] : 0.0;
             /* u < 0: unreachable, cannot happen on a validated graph; the entry is kept */
 #pragma unroll
-            for (int q = 0; q < 8; ++q) ru[q] = u[q] >= 0 ? rr[u[q]] : 1.0;
+            for (int q = 0; q < QB; ++q) ru[q] = u[q] >= 0 ? rr[u[q]] : 1.0;
 #pragma unroll
-            for (int q = 0; q < 8; ++q)
+            for (int q = 0; q < QB; ++q)
                 if (t[q] >= 0) rr[t[q]] = ru[q] * rt[q];
         }
         __threadfence_block();
@@ -1077,9 +1079,11 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
             n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
         /* level order for rows whose distances span <= 64 quanta, sweeps for the rest
          * (ws->cursor is free here and carries the per-row hand-over flags) */
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel,
+        /* 1024 threads per row, one row per CU (128 VGPRs): 12.3 ms on C4 against 13.3 for 512
+         * threads at two rows per CU and 13.1 for 1024 at two (64 VGPRs, 4 targets in flight) */
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
-        rel_levels_kernel<<<lrows, 512, 65536, st>>>(n, ld, row0, d, pred, rel, 64, ws->depth,
+        rel_levels_kernel<1024><<<lrows, 1024, 65536, st>>>(n, ld, row0, d, pred, rel, 64, ws->depth,
                                                  ws->cursor);
         const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
         SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel,
