@@ -151,6 +151,11 @@ int srt_comm_init(const uint8_t id[128], int32_t nranks, int32_t rank, int32_t d
 void srt_comm_free(srt_comm* comm);
 /* In-process communicators for `ndev` devices (ncclCommInitAll): comms[i] drives devices[i]. */
 int srt_comm_init_all(int32_t ndev, const int32_t* devices, srt_comm** comms);
+/* `nranks` virtual ranks of one process on one device (tests of the sharded schedules on one
+ * GPU): each comms[i] is driven by its own host thread; collectives become device-to-device
+ * copies ordered by events and host barriers. srt_build_tables_multi uses them when the
+ * environment sets SRT_VIRTUAL_RANKS. */
+int srt_comm_init_virtual(int32_t nranks, int32_t device, srt_comm** comms);
 /* Row-block partition used by every sharded build: rank r owns rows [begin, end). */
 void srt_shard_rows(int32_t n, int32_t align, int32_t nranks, int32_t rank, int32_t* begin,
                     int32_t* end);

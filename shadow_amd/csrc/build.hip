@@ -533,6 +533,7 @@ out:
 
 typedef struct {
     int rank, R, dev, directed, algo, n, ld;
+    int virt; /* virtual ranks on one device: per-rank state slots */
     srt_comm* comm;
     const srt_canon* c;
     const uint32_t* hw; /* dense: host w/r matrices, ld x ld */
@@ -561,6 +562,7 @@ static void* mjob_dense(void* p) {
     const size_t rows = (size_t)(nr > 0 ? nr : 1) * j->ld;
     uint32_t *dw, *dlat;
     double *dr, *drel;
+    srt_set_virtual_slot(j->virt ? j->rank : -1);
     TRYHIP(hipSetDevice(j->dev));
     TRYHIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     TRY(dalloc(&B, (void**)&dw, rows * sizeof(uint32_t)));
@@ -605,6 +607,7 @@ static void* mjob_sparse(void* p) {
     const size_t all = (size_t)per * j->R * n;
     uint32_t* dlat;
     double* drel;
+    srt_set_virtual_slot(j->virt ? j->rank : -1);
     TRYHIP(hipSetDevice(j->dev));
     TRYHIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     TRY(sparse_graph_from_canon(j->c, j->dev, &sg));
@@ -642,7 +645,10 @@ extern "C" int srt_build_tables_multi(const srt_edges* g, const srt_build_opts* 
         srt_set_error("srt_build_tables_multi: no HIP device");
         return SRT_E_DEVICE;
     }
-    const int R = ngpus < avail ? ngpus : avail;
+    /* SRT_VIRTUAL_RANKS=R (tests): R ranks on device 0, collectives as device copies */
+    const char* venv = getenv("SRT_VIRTUAL_RANKS");
+    const int virt = venv && atoi(venv) > 0 ? (atoi(venv) < 64 ? atoi(venv) : 64) : 0;
+    const int R = virt ? virt : (ngpus < avail ? ngpus : avail);
     const int use_sp = opts ? opts->use_shortest_path : 1;
     if (!use_sp) return srt_build_tables(g, opts, lat_q, quantum_ns, rel, stats);
     srt_canon c;
@@ -683,12 +689,14 @@ extern "C" int srt_build_tables_multi(const srt_edges* g, const srt_build_opts* 
             hr[(size_t)u * ld + u] = c.self_r[u];
         }
     }
-    for (int i = 0; i < R; i++) devs[i] = i;
-    if ((rc = srt_comm_init_all(R, devs, comms))) goto done;
+    for (int i = 0; i < R; i++) devs[i] = virt ? 0 : i;
+    if ((rc = virt ? srt_comm_init_virtual(R, 0, comms) : srt_comm_init_all(R, devs, comms)))
+        goto done;
     for (int i = 0; i < R; i++) {
         mjob* j = &jobs[i];
         j->rank = i;
         j->R = R;
+        j->virt = virt;
         j->dev = devs[i];
         j->directed = c.directed;
         j->algo = algo;

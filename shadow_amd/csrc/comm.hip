@@ -6,16 +6,42 @@
  * Dense builds broadcast one pivot-row panel per Floyd-Warshall round; sparse builds shard the
  * sources and assemble the tables with one ncclAllGather.
  */
+#include <pthread.h>
 #include <rccl/rccl.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "srt_device.h"
 
+/* Virtual ranks: several ranks of one process on one device (tests of the sharded schedules on
+ * a one-GPU box; RCCL refuses two ranks on one device). Collectives become device-to-device
+ * copies on the callers' streams, ordered by events; host barriers line the ranks up at each
+ * call, which every rank makes in the same order (SPMD), as with RCCL. */
+typedef struct srt_loop {
+    int nranks, refs;
+    pthread_barrier_t bar;
+    pthread_mutex_t mu;
+    void** ptr;           /* per rank: its buffer of the current call */
+    void** sendp;         /* [from * R + to] */
+    size_t* sendb;        /* [from * R + to] */
+    hipEvent_t* ready;    /* per rank: its inputs are written */
+    hipEvent_t* done;     /* per rank: it has read what it needs */
+} srt_loop;
+
 struct srt_comm {
     ncclComm_t nc;
     int nranks, rank, device;
+    srt_loop* loop; /* non-NULL: virtual ranks */
 };
+
+static thread_local int t_vslot = -1;
+void srt_set_virtual_slot(int rank) { t_vslot = rank; }
+int srt_state_slot(void) {
+    if (t_vslot >= 0) return 64 + (t_vslot & 63);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    return dev & 63;
+}
 
 #define SRT_NCCLCHK(expr)                                                                  \
     do {                                                                                   \
@@ -92,10 +118,183 @@ extern "C" int srt_comm_init_all(int32_t ndev, const int32_t* devices, srt_comm*
     return SRT_OK;
 }
 
+extern "C" int srt_comm_init_virtual(int32_t nranks, int32_t device, srt_comm** comms) {
+    if (nranks < 1 || nranks > 64 || !comms) {
+        srt_set_error("srt_comm_init_virtual: bad arguments");
+        return SRT_E_ARG;
+    }
+    SRT_HIPCHK(hipSetDevice(device));
+    srt_loop* L = (srt_loop*)calloc(1, sizeof(srt_loop));
+    if (!L) return SRT_E_NOMEM;
+    const int R = nranks;
+    L->nranks = R;
+    L->refs = R;
+    L->ptr = (void**)calloc((size_t)R, sizeof(void*));
+    L->sendp = (void**)calloc((size_t)R * R, sizeof(void*));
+    L->sendb = (size_t*)calloc((size_t)R * R, sizeof(size_t));
+    L->ready = (hipEvent_t*)calloc((size_t)R, sizeof(hipEvent_t));
+    L->done = (hipEvent_t*)calloc((size_t)R, sizeof(hipEvent_t));
+    if (!L->ptr || !L->sendp || !L->sendb || !L->ready || !L->done) return SRT_E_NOMEM;
+    pthread_barrier_init(&L->bar, NULL, (unsigned)R);
+    pthread_mutex_init(&L->mu, NULL);
+    for (int i = 0; i < R; i++) {
+        SRT_HIPCHK(hipEventCreateWithFlags(&L->ready[i], hipEventDisableTiming));
+        SRT_HIPCHK(hipEventCreateWithFlags(&L->done[i], hipEventDisableTiming));
+        comms[i] = (srt_comm*)calloc(1, sizeof(srt_comm));
+        if (!comms[i]) return SRT_E_NOMEM;
+        comms[i]->nranks = R;
+        comms[i]->rank = i;
+        comms[i]->device = device;
+        comms[i]->loop = L;
+    }
+    return SRT_OK;
+}
+
 extern "C" void srt_comm_free(srt_comm* comm) {
     if (!comm) return;
-    (void)ncclCommDestroy(comm->nc);
+    if (comm->loop) {
+        srt_loop* L = comm->loop;
+        pthread_mutex_lock(&L->mu);
+        const int last = --L->refs == 0;
+        pthread_mutex_unlock(&L->mu);
+        if (last) {
+            for (int i = 0; i < L->nranks; i++) {
+                (void)hipEventDestroy(L->ready[i]);
+                (void)hipEventDestroy(L->done[i]);
+            }
+            pthread_barrier_destroy(&L->bar);
+            pthread_mutex_destroy(&L->mu);
+            free(L->ptr);
+            free(L->sendp);
+            free(L->sendb);
+            free(L->ready);
+            free(L->done);
+            free(L);
+        }
+    } else {
+        (void)ncclCommDestroy(comm->nc);
+    }
     free(comm);
+}
+
+/* ---- collectives ------------------------------------------------------------------------ */
+static void loop_wait(srt_loop* L) { pthread_barrier_wait(&L->bar); }
+
+__global__ void allreduce_i32_kernel(int32_t* __restrict__ dst, const int32_t* __restrict__ src,
+                                     size_t count, int op_min) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) dst[i] = op_min ? min(dst[i], src[i]) : dst[i] + src[i];
+}
+
+int srt_coll_bcast(const srt_comm* c, void* buf, size_t bytes, int root, hipStream_t st) {
+    if (!c->loop) {
+        SRT_NCCLCHK(ncclBroadcast(buf, buf, bytes, ncclUint8, root, c->nc, st));
+        return SRT_OK;
+    }
+    srt_loop* L = c->loop;
+    const int me = c->rank, R = c->nranks;
+    L->ptr[me] = buf;
+    SRT_HIPCHK(hipEventRecord(L->ready[me], st));
+    loop_wait(L);
+    if (me != root) {
+        SRT_HIPCHK(hipStreamWaitEvent(st, L->ready[root], 0));
+        if (bytes) SRT_HIPCHK(hipMemcpyAsync(buf, L->ptr[root], bytes, hipMemcpyDeviceToDevice, st));
+        SRT_HIPCHK(hipEventRecord(L->done[me], st));
+    }
+    loop_wait(L);
+    if (me == root)
+        for (int q = 0; q < R; q++)
+            if (q != root) SRT_HIPCHK(hipStreamWaitEvent(st, L->done[q], 0));
+    loop_wait(L);
+    return SRT_OK;
+}
+
+int srt_coll_allreduce_i32(const srt_comm* c, int32_t* buf, size_t count, int op_min,
+                           hipStream_t st) {
+    if (!c->loop) {
+        SRT_NCCLCHK(ncclAllReduce(buf, buf, count, ncclInt32, op_min ? ncclMin : ncclSum, c->nc, st));
+        return SRT_OK;
+    }
+    srt_loop* L = c->loop;
+    const int me = c->rank, R = c->nranks;
+    L->ptr[me] = buf;
+    SRT_HIPCHK(hipEventRecord(L->ready[me], st));
+    loop_wait(L);
+    if (me == 0) { /* rank 0 reduces every rank's buffer into its own */
+        for (int q = 1; q < R; q++) {
+            SRT_HIPCHK(hipStreamWaitEvent(st, L->ready[q], 0));
+            if (count)
+                allreduce_i32_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(
+                    buf, (const int32_t*)L->ptr[q], count, op_min);
+        }
+        SRT_HIPCHK(hipGetLastError());
+        SRT_HIPCHK(hipEventRecord(L->done[0], st));
+    }
+    loop_wait(L);
+    if (me != 0) {
+        SRT_HIPCHK(hipStreamWaitEvent(st, L->done[0], 0));
+        if (count)
+            SRT_HIPCHK(hipMemcpyAsync(buf, L->ptr[0], count * sizeof(int32_t),
+                                      hipMemcpyDeviceToDevice, st));
+        SRT_HIPCHK(hipEventRecord(L->ready[me], st));
+    }
+    loop_wait(L);
+    if (me == 0) /* rank 0's buffer stays untouched until every rank has its copy */
+        for (int q = 1; q < R; q++) SRT_HIPCHK(hipStreamWaitEvent(st, L->ready[q], 0));
+    loop_wait(L);
+    return SRT_OK;
+}
+
+int srt_coll_group_begin(const srt_comm* c) {
+    if (!c->loop) SRT_NCCLCHK(ncclGroupStart());
+    return SRT_OK;
+}
+
+int srt_coll_group_end(const srt_comm* c) {
+    if (!c->loop) SRT_NCCLCHK(ncclGroupEnd());
+    return SRT_OK;
+}
+
+int srt_coll_exchange(const srt_comm* c, void* const* send, const size_t* send_bytes,
+                      void* const* recv, const size_t* recv_bytes, hipStream_t st) {
+    const int me = c->rank, R = c->nranks;
+    if (!c->loop) {
+        SRT_NCCLCHK(ncclGroupStart());
+        for (int q = 0; q < R; q++)
+            if (q != me && send_bytes[q])
+                SRT_NCCLCHK(ncclSend(send[q], send_bytes[q], ncclUint8, q, c->nc, st));
+        for (int q = 0; q < R; q++)
+            if (q != me && recv_bytes[q])
+                SRT_NCCLCHK(ncclRecv(recv[q], recv_bytes[q], ncclUint8, q, c->nc, st));
+        SRT_NCCLCHK(ncclGroupEnd());
+        return SRT_OK;
+    }
+    srt_loop* L = c->loop;
+    for (int q = 0; q < R; q++) {
+        L->sendp[me * R + q] = send[q];
+        L->sendb[me * R + q] = q == me ? 0 : send_bytes[q];
+    }
+    SRT_HIPCHK(hipEventRecord(L->ready[me], st));
+    loop_wait(L);
+    for (int q = 0; q < R; q++) {
+        if (q == me || !recv_bytes[q]) continue;
+        if (L->sendb[q * R + me] != recv_bytes[q]) {
+            srt_set_error("virtual exchange: rank %d sends %zu bytes to %d, which expects %zu", q,
+                          L->sendb[q * R + me], me, recv_bytes[q]);
+            loop_wait(L);
+            loop_wait(L);
+            return SRT_E_COMM;
+        }
+        SRT_HIPCHK(hipStreamWaitEvent(st, L->ready[q], 0));
+        SRT_HIPCHK(hipMemcpyAsync(recv[q], L->sendp[q * R + me], recv_bytes[q],
+                                  hipMemcpyDeviceToDevice, st));
+    }
+    SRT_HIPCHK(hipEventRecord(L->done[me], st));
+    loop_wait(L);
+    for (int q = 0; q < R; q++) /* the send buffers stay untouched until the peers have read */
+        if (q != me && L->sendb[me * R + q]) SRT_HIPCHK(hipStreamWaitEvent(st, L->done[q], 0));
+    loop_wait(L);
+    return SRT_OK;
 }
 
 extern "C" void srt_shard_rows(int32_t n, int32_t align, int32_t nranks, int32_t rank,
@@ -110,7 +309,6 @@ extern "C" void srt_shard_rows(int32_t n, int32_t align, int32_t nranks, int32_t
 
 int srt_comm_rank(const srt_comm* c) { return c ? c->rank : -1; }
 int srt_comm_size(const srt_comm* c) { return c ? c->nranks : 0; }
-ncclComm_t srt_comm_nccl(const srt_comm* c) { return c->nc; }
 
 extern "C" int srt_sparse_allgather(srt_comm* comm, int32_t n, int32_t rows_per_rank,
                                     uint32_t* lat_all, double* rel_all, void* stream) {
@@ -120,6 +318,14 @@ extern "C" int srt_sparse_allgather(srt_comm* comm, int32_t n, int32_t rows_per_
     }
     hipStream_t st = (hipStream_t)stream;
     const size_t cnt = (size_t)rows_per_rank * n;
+    if (comm->loop) { /* every rank broadcasts its block in turn */
+        for (int q = 0; q < comm->nranks; q++) {
+            int rc = srt_coll_bcast(comm, lat_all + cnt * q, cnt * sizeof(uint32_t), q, st);
+            if (!rc) rc = srt_coll_bcast(comm, rel_all + cnt * q, cnt * sizeof(double), q, st);
+            if (rc) return rc;
+        }
+        return SRT_OK;
+    }
     SRT_NCCLCHK(ncclGroupStart());
     SRT_NCCLCHK(ncclAllGather(lat_all + cnt * comm->rank, lat_all, cnt, ncclUint32, comm->nc, st));
     SRT_NCCLCHK(ncclAllGather(rel_all + cnt * comm->rank, rel_all, cnt, ncclFloat64, comm->nc, st));

@@ -17,9 +17,9 @@
  */
 #include "srt_device.h"
 
-evpool_t* srt_evpool(int dev) {
-    static evpool_t pools[64];
-    return &pools[dev & 63];
+evpool_t* srt_evpool(int slot) {
+    static evpool_t pools[SRT_STATE_SLOTS];
+    return &pools[slot % SRT_STATE_SLOTS];
 }
 
 #define B SRT_FW_B
@@ -912,7 +912,7 @@ typedef struct {
     size_t rt_cap;
 } dense_ws;
 
-static dense_ws g_ws[64];
+static dense_ws g_ws[SRT_STATE_SLOTS];
 
 static int ws_grow(void** p, size_t* cap, size_t need, size_t elem) {
     if (*cap >= need && *p) return SRT_OK;
@@ -925,9 +925,7 @@ static int ws_grow(void** p, size_t* cap, size_t need, size_t elem) {
 }
 
 static int ws_get(dense_ws** out, int n) {
-    int dev = 0;
-    SRT_HIPCHK(hipGetDevice(&dev));
-    dense_ws* ws = &g_ws[dev & 63];
+    dense_ws* ws = &g_ws[srt_state_slot()];
     if (ws->n_cap < (size_t)n + 1 || !ws->cnt) {
         if (ws->cnt) {
             SRT_HIPCHK(hipFree(ws->cnt));
@@ -1195,21 +1193,7 @@ extern "C" int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, c
 /* ------------------------------------------------------------------------------------------ */
 /* row-sharded dense build over RCCL (one process per GPU)                                    */
 /* ------------------------------------------------------------------------------------------ */
-#include <rccl/rccl.h>
-
-int srt_comm_rank(const srt_comm* c);
-int srt_comm_size(const srt_comm* c);
-ncclComm_t srt_comm_nccl(const srt_comm* c);
-
-#define SRT_NCCLCHK(expr)                                                                  \
-    do {                                                                                   \
-        ncclResult_t r_ = (expr);                                                          \
-        if (r_ != ncclSuccess) {                                                           \
-            srt_set_error("RCCL error %s at %s:%d (%s)", ncclGetErrorString(r_), __FILE__, \
-                          __LINE__, #expr);                                                \
-            return SRT_E_COMM;                                                             \
-        }                                                                                  \
-    } while (0)
+/* collectives: srt_coll_* (comm.hip) -- RCCL, or virtual ranks sharing one device */
 
 typedef struct {
     const srt_comm* comm;
@@ -1229,20 +1213,15 @@ static int shard_owner(void* vctx, int k0) {
 
 static int shard_bcast(void* vctx, void* panel, size_t bytes, int owner, hipStream_t st) {
     const shard_ctx* ctx = (const shard_ctx*)vctx;
-    SRT_NCCLCHK(ncclBroadcast(panel, panel, bytes, ncclUint8, owner, srt_comm_nccl(ctx->comm), st));
-    return SRT_OK;
+    return srt_coll_bcast(ctx->comm, panel, bytes, owner, st);
 }
 
 static int shard_gather(void* vctx, dense_ws* ws, int n, int phase, int32_t total, hipStream_t st) {
     (void)total;
     shard_ctx* ctx = (shard_ctx*)vctx;
-    ncclComm_t nc = srt_comm_nccl(ctx->comm);
     const int R = srt_comm_size(ctx->comm);
-    if (phase == 0) {
-        /* counts are zero outside each rank's rows: a sum all-reduce assembles them */
-        SRT_NCCLCHK(ncclAllReduce(ws->cnt, ws->cnt, (size_t)n, ncclInt32, ncclSum, nc, st));
-        return SRT_OK;
-    }
+    if (phase == 0) /* counts are zero outside each rank's rows: a sum all-reduce assembles them */
+        return srt_coll_allreduce_i32(ctx->comm, ws->cnt, (size_t)n, 0, st);
     /* every rank filled its own rows' contiguous arc segment: broadcast each segment */
     int32_t* hptr = (int32_t*)malloc((size_t)(n + 1) * sizeof(int32_t));
     if (!hptr) return SRT_E_NOMEM;
@@ -1253,33 +1232,27 @@ static int shard_gather(void* vctx, dense_ws* ws, int n, int phase, int32_t tota
         srt_set_error("hipMemcpy of the essential-arc offsets failed");
         return SRT_E_DEVICE;
     }
-    ncclResult_t r = ncclGroupStart();
-    for (int q = 0; q < R && r == ncclSuccess; q++) {
+    int rc = srt_coll_group_begin(ctx->comm);
+    for (int q = 0; q < R && !rc; q++) {
         int32_t b, e;
         srt_shard_rows(ctx->ld, SRT_SHARD_ALIGN, R, q, &b, &e);
         b = min(b, n);
         e = min(e, n);
         const size_t o = (size_t)hptr[b], c = (size_t)(hptr[e] - hptr[b]);
         if (c == 0) continue;
-        r = ncclBroadcast(ws->col + o, ws->col + o, c, ncclInt32, q, nc, st);
-        if (r == ncclSuccess) r = ncclBroadcast(ws->aw + o, ws->aw + o, c, ncclUint32, q, nc, st);
-        if (r == ncclSuccess) r = ncclBroadcast(ws->ar + o, ws->ar + o, c, ncclFloat64, q, nc, st);
+        rc = srt_coll_bcast(ctx->comm, ws->col + o, c * sizeof(int32_t), q, st);
+        if (!rc) rc = srt_coll_bcast(ctx->comm, ws->aw + o, c * sizeof(uint32_t), q, st);
+        if (!rc) rc = srt_coll_bcast(ctx->comm, ws->ar + o, c * sizeof(double), q, st);
     }
-    ncclResult_t r2 = ncclGroupEnd();
+    const int rc2 = srt_coll_group_end(ctx->comm);
     free(hptr);
-    if (r != ncclSuccess || r2 != ncclSuccess) {
-        srt_set_error("RCCL broadcast of essential arcs failed: %s",
-                      ncclGetErrorString(r != ncclSuccess ? r : r2));
-        return SRT_E_COMM;
-    }
-    return SRT_OK;
+    return rc ? rc : rc2;
 }
 
 /* undirected symmetry across shards: rank q sends rel[q rows][r cols] to every r > q, which
  * stores its transpose into rel[r rows][q cols] (the entries with s > t). */
 static int shard_mirror(const srt_comm* comm, int n, int ld, int b, int e, double* rel_rows,
                         hipStream_t st) {
-    ncclComm_t nc = srt_comm_nccl(comm);
     const int R = srt_comm_size(comm), me = srt_comm_rank(comm);
     const int nr = e - b;
     dense_ws* ws;
@@ -1302,13 +1275,24 @@ static int shard_mirror(const srt_comm* comm, int n, int ld, int b, int e, doubl
         so += (size_t)cnt;
     }
     SRT_HIPCHK(hipGetLastError());
-    SRT_NCCLCHK(ncclGroupStart());
+    void** sp = (void**)calloc((size_t)R, sizeof(void*));
+    void** rp = (void**)calloc((size_t)R, sizeof(void*));
+    size_t* sb = (size_t*)calloc((size_t)R, sizeof(size_t));
+    size_t* rb = (size_t*)calloc((size_t)R, sizeof(size_t));
+    if (!sp || !rp || !sb || !rb) {
+        free(sp);
+        free(rp);
+        free(sb);
+        free(rb);
+        return SRT_E_NOMEM;
+    }
     so = 0;
     for (int q = me + 1; q < R; q++) {
         int32_t qb, qe;
         srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &qb, &qe);
         const size_t cnt = (size_t)nr * (qe - qb);
-        if (cnt) SRT_NCCLCHK(ncclSend(ws->xsend + so, cnt, ncclFloat64, q, nc, st));
+        sp[q] = ws->xsend + so;
+        sb[q] = cnt * sizeof(double);
         so += cnt;
     }
     size_t ro = 0;
@@ -1316,10 +1300,16 @@ static int shard_mirror(const srt_comm* comm, int n, int ld, int b, int e, doubl
         int32_t qb, qe;
         srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &qb, &qe);
         const size_t cnt = (size_t)(qe - qb) * nr;
-        if (cnt) SRT_NCCLCHK(ncclRecv(ws->xrecv + ro, cnt, ncclFloat64, q, nc, st));
+        rp[q] = ws->xrecv + ro;
+        rb[q] = cnt * sizeof(double);
         ro += cnt;
     }
-    SRT_NCCLCHK(ncclGroupEnd());
+    rc = srt_coll_exchange(comm, sp, sb, rp, rb, st);
+    free(sp);
+    free(rp);
+    free(sb);
+    free(rb);
+    if (rc) return rc;
     ro = 0;
     for (int q = 0; q < me; q++) {
         int32_t qb, qe;
@@ -1356,7 +1346,6 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
     srt_shard_rows(ld, SRT_SHARD_ALIGN, R, me, &b, &e);
     const int nr = e - b;
     hipStream_t st = (hipStream_t)stream;
-    ncclComm_t nc = srt_comm_nccl(comm);
     dense_ws* ws;
     int rc = ws_get(&ws, n);
     if (rc) return rc;
@@ -1380,7 +1369,7 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
         if (R > 1) { /* every rank must agree before falling back to a wider encoding */
             int32_t* flag = ws->cnt;
             SRT_HIPCHK(hipMemcpyAsync(flag, &exact, sizeof(int32_t), hipMemcpyHostToDevice, st));
-            SRT_NCCLCHK(ncclAllReduce(flag, flag, 1, ncclInt32, ncclMin, nc, st));
+            if ((rc = srt_coll_allreduce_i32(comm, flag, 1, 1, st))) return rc;
             SRT_HIPCHK(hipMemcpyAsync(&exact, flag, sizeof(int32_t), hipMemcpyDeviceToHost, st));
             SRT_HIPCHK(hipStreamSynchronize(st));
         }
@@ -1402,7 +1391,8 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
             } else {
                 P = ws->panel;
             }
-            if (R > 1) SRT_NCCLCHK(ncclBroadcast(P, P, (size_t)B * ld, ncclUint32, owner, nc, st));
+            if (R > 1 && (rc = srt_coll_bcast(comm, P, (size_t)B * ld * sizeof(uint32_t), owner, st)))
+                return rc;
             if ((rc = fw_shard_part(lat_rows, ld, b, nr, P, k0, st, evp))) return rc;
         }
     }

@@ -624,20 +624,12 @@ __global__ void fw16_finish_kernel(int n, int ld, int row0, const u16* __restric
  * in order; SRT_FW_LOOKAHEAD=1 forces the two-stream schedule (tests exercise it on one GPU). */
 /* per-device u16 working matrix of the last build (rows of the shard, ld columns); the dense
  * post pass reads it transposed for the predecessor search (half the bytes of the u32 table) */
-static u16* fw16_bufs[64];
-static size_t fw16_caps[64]; /* elements allocated in fw16_bufs (shared by both build forms) */
-static int* fw16_flags[64];
-static int fw16_small[64]; /* last build: every real distance <= 254 quanta */
-int srt_fw16_small(void) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    return fw16_small[dev & 63];
-}
-const uint16_t* srt_fw16_matrix(void) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return NULL;
-    return fw16_bufs[dev & 63];
-}
+static u16* fw16_bufs[SRT_STATE_SLOTS];
+static size_t fw16_caps[SRT_STATE_SLOTS]; /* elements allocated in fw16_bufs (shared by both build forms) */
+static int* fw16_flags[SRT_STATE_SLOTS];
+static int fw16_small[SRT_STATE_SLOTS]; /* last build: every real distance <= 254 quanta */
+int srt_fw16_small(void) { return fw16_small[srt_state_slot()]; }
+const uint16_t* srt_fw16_matrix(void) { return fw16_bufs[srt_state_slot()]; }
 
 typedef struct {
     hipStream_t cs;
@@ -646,8 +638,8 @@ typedef struct {
 } fw16_sched;
 
 static int sched_get(fw16_sched** out, int dev) {
-    static fw16_sched sc[64];
-    fw16_sched* x = &sc[dev & 63];
+    static fw16_sched sc[SRT_STATE_SLOTS];
+    fw16_sched* x = &sc[dev % SRT_STATE_SLOTS];
     if (!x->ok) {
         int lo = 0, hi = 0;
         SRT_HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -667,9 +659,7 @@ static int sched_get(fw16_sched** out, int dev) {
 /* Upper-triangle blocked FW for an undirected graph on one GPU (f16-compare kernels). */
 static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipStream_t st,
                           evpool_t* evp, int* exact) {
-    int dev = 0;
-    SRT_HIPCHK(hipGetDevice(&dev));
-    dev &= 63;
+    const int dev = srt_state_slot(); /* the device, or this virtual rank's slot */
     size_t* caps = fw16_caps;
     int** flags = fw16_flags;
     const size_t need = (size_t)ld * ld;
@@ -719,9 +709,7 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
     u16** bufs = fw16_bufs;
     size_t* caps = fw16_caps;
     int** flags = fw16_flags;
-    int dev = 0;
-    SRT_HIPCHK(hipGetDevice(&dev));
-    dev &= 63;
+    const int dev = srt_state_slot(); /* the device, or this virtual rank's slot */
     const size_t need = (size_t)nrows * ld + 2 * (size_t)KB * ld;
     if (caps[dev] < need) {
         if (bufs[dev]) SRT_HIPCHK(hipFree(bufs[dev]));

@@ -20,6 +20,27 @@
         }                                                                                  \
     } while (0)
 
+/* Per-thread slot of the static per-device state (workspaces, event pools, FW buffers and
+ * streams): the current device (0..63), or 64 + r for virtual rank r when several ranks share
+ * one device inside one process (srt_build_tables_multi with SRT_VIRTUAL_RANKS, comm.hip). */
+#define SRT_STATE_SLOTS 128
+int srt_state_slot(void);
+void srt_set_virtual_slot(int rank); /* -1: back to the device slot */
+
+/* Collectives over an srt_comm: RCCL, or (virtual ranks on one device) device-to-device copies
+ * ordered by events and host barriers. Every rank calls the same sequence. */
+int srt_coll_bcast(const srt_comm* c, void* buf, size_t bytes, int root, hipStream_t st);
+int srt_coll_allreduce_i32(const srt_comm* c, int32_t* buf, size_t count, int op_min,
+                           hipStream_t st);
+int srt_coll_group_begin(const srt_comm* c);
+int srt_coll_group_end(const srt_comm* c);
+/* point-to-point exchange: to each peer q send send_bytes[q] from send[q], receive
+ * recv_bytes[q] into recv[q] (arrays of comm size; zero bytes skip the pair) */
+int srt_coll_exchange(const srt_comm* c, void* const* send, const size_t* send_bytes,
+                      void* const* recv, const size_t* recv_bytes, hipStream_t st);
+int srt_comm_rank(const srt_comm* c);
+int srt_comm_size(const srt_comm* c);
+
 /* pivot-block edge of the blocked Floyd-Warshall and the output-tile edge of its kernels */
 #define SRT_FW_B 64
 /* row-shard alignment of every sharded dense build (the u16 update tile is 128 rows) */
@@ -55,9 +76,7 @@ evpool_t* srt_evpool(int dev);
 
 
 static inline int evpool_begin(evpool_t** out, int rounds) {
-    int dev = 0;
-    SRT_HIPCHK(hipGetDevice(&dev));
-    evpool_t* p = srt_evpool(dev);
+    evpool_t* p = srt_evpool(srt_state_slot());
     if (p->cap < 2 * rounds) {
         hipEvent_t* ne = (hipEvent_t*)realloc(p->ev, sizeof(hipEvent_t) * 2 * rounds);
         if (!ne) return SRT_E_NOMEM;

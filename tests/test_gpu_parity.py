@@ -283,6 +283,59 @@ def test_in_process_multi_gpu_build(gpu, kind, ngpus):
     assert_tables(lat, rel, exp["lat_int"], exp["rel"], f"multi {kind} x{ngpus}")
 
 
+def _ring_graph(n, hop_ms, seed):
+    """Ring with hop latencies hop_ms / hop_ms+1 plus long chords (test_dense_distance_encoding_tiers)."""
+    rng = np.random.default_rng(seed)
+    src, dst = list(range(n)), [(i + 1) % n for i in range(n)]
+    lat = [(hop_ms + (i % 2)) * MS for i in range(n)]
+    for _ in range(12):
+        a, b = (int(x) for x in rng.choice(n, 2, replace=False))
+        src.append(a)
+        dst.append(b)
+        lat.append(int(hop_ms * n // 3) * MS)
+    loss = rng.integers(0, 100, len(src)) * 1e-4
+    return graphs.Graph(n, 0, np.array(src, np.int32), np.array(dst, np.int32),
+                        np.array(lat, np.int64), loss)
+
+
+@pytest.mark.parametrize("kind", ["dense", "sparse", "directed", "ring_u16", "ring_u32"])
+@pytest.mark.parametrize("ranks", [2, 3, 4])
+def test_virtual_ranks_sharded_build(gpu, monkeypatch, kind, ranks):
+    """The multi-rank sharded builds on ONE GPU: SRT_VIRTUAL_RANKS=R runs R ranks of
+    srt_build_tables_multi on device 0, each with its own host thread, stream and workspaces, and
+    the collectives (pivot-panel broadcasts under the lookahead schedule, the exact-flag
+    all-reduce, the essential-arc count all-reduce and segment broadcasts, the symmetry
+    exchange, the sparse all-gather) as device-to-device copies. The C host logic of the
+    N-rank paths -- shard partition, owners, lookahead order, offsets of every exchange -- is
+    the code the RCCL runs use; the tables must equal the oracle's."""
+    monkeypatch.setenv("SRT_VIRTUAL_RANKS", str(ranks))
+    algo = ALGO_DENSE_FW
+    if kind == "dense":
+        g = graphs.complete_graph(700, seed=9)
+    elif kind == "sparse":
+        g = graphs.random_geometric(1500, seed=3)
+        algo = ALGO_SPARSE_SSSP
+    elif kind == "directed":
+        rng = np.random.default_rng(21)
+        n, m = 300, 2500
+        ring = np.arange(n)
+        src = np.concatenate([rng.integers(0, n, m), ring]).astype(np.int32)
+        dst = np.concatenate([rng.integers(0, n, m), (ring + 1) % n]).astype(np.int32)
+        lat = (rng.integers(1, 30, len(src)) * MS).astype(np.int64)
+        loss = rng.integers(0, 200, len(src)) / 10000.0
+        g = graphs.Graph(n, True, src, dst, lat, loss)
+    elif kind == "ring_u16":  # saturates the f16-compare cap: u16 pk_min tier on every rank
+        g = _ring_graph(384, 160, 160)  # max distance ~30.8k quanta < 0x7FFF; 3 row blocks
+    else:  # saturates both u16 caps: the u32 rounds with their own panel broadcasts
+        g = _ring_graph(640, 400, 400)
+    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss, algo=algo,
+                                ngpus=1)
+    exp = _oracle(g)
+    assert_tables(lat, rel, exp["lat_int"], exp["rel"], f"virtual x{ranks} {kind}")
+    if kind.startswith("ring"):
+        assert st.dist_enc == (2 if kind == "ring_u16" else 1)
+
+
 def test_packet_path_trace_replay(gpu):
     """the packet-path consumer (worker.c:541-555) on a recorded trace gives the
     reference's drop decisions, delivery delays and per-pair packet counts. Expected values come
