@@ -176,11 +176,23 @@ def run_dense(c: Ctx, wl):
     #   enc 1: 2 x v_add_u32 + 1 x v_min3_u32 per 2 relaxations         -> 8/2 = 4.0 cycles
     cyc_per_relax = {4: 2.0, 3: 2.0, 2: 3.0, 1: 4.0}[enc]
     instr_per_relax = {4: 0.75, 3: 0.75, 2: 1.0, 1: 1.5}[enc]
-    kname = {4: "fwh_update_kernel<true>", 3: "fwh_update_kernel<false>",
+    kname = {4: "fwh_update_kernel<true, 0>" if world == 1 else "fwh_update_kernel<true, 4>",
+             3: "fwh_update_kernel<false, 0>",
              2: "fw16_update_kernel<false>", 1: "fw_update_kernel"}[enc]
-    # elements a round updates: every local row, or (enc 4) the upper-triangle 128x128 tiles only
+    # elements a timed launch updates: every local row; (enc 4, one GPU) the upper-triangle 128x128
+    # tiles; (enc 4, sharded) this rank's kept tiles (fw16.hip sym_kept: one orientation of each
+    # tile pair) less the next pivot block's tile row and column, which run in their own launch
     tiles = ld // 128
-    elems = float(tiles * (tiles + 1) // 2) * 128 * 128 if enc == 4 else float(nr) * ld
+    if enc == 4 and world == 1:
+        elems = float(tiles * (tiles + 1) // 2) * 128 * 128
+    elif enc == 4:
+        kept = lambda i, j: i == j or ((i < j) == ((i + j) % 2 == 0))
+        tb, te = b // 128, e // 128
+        nkept = sum(1 for i in range(tb, te) for j in range(tiles) if kept(i, j))
+        cross = tiles // 2 / max(world, 1) + (te - tb) / 2  # average kept tiles of row/col K1
+        elems = float(max(nkept - cross, 1)) * 128 * 128
+    else:
+        elems = float(nr) * ld
     bytes_per_round = 2.0 * elems * s_d  # round-streaming model: read + write what is updated
     relax_per_round = elems * FW_B
     achieved_gbs = bytes_per_round / (avg_upd_ms * 1e-3) / 1e9

@@ -1361,10 +1361,15 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
     if (stats && stats->time_kernels && (rc = evpool_begin(&evp, ld / B))) return rc;
     shard_ctx ctx = {comm, ld};
     int exact = 0, enc = SRT_DENC_U32;
+    const char* sym_env = getenv("SRT_FW_SYM");
+    const bool sym = !directed && R > 1 && !(sym_env && atoi(sym_env) == 0);
     for (int fm = 1; fm >= 0 && !exact; --fm) {
         if (evp) evp->used = 0;
-        rc = srt_fw16_build(n, ld, b, nr, w_rows, lat_rows, st, evp, shard_owner,
-                            R > 1 ? shard_bcast : NULL, &ctx, me, fm, NULL, &exact);
+        if (fm && sym) /* undirected: each rank updates half of its row block (fw16.hip) */
+            rc = srt_fw16_build_sym_sharded(comm, n, ld, b, nr, w_rows, lat_rows, st, evp, &exact);
+        else
+            rc = srt_fw16_build(n, ld, b, nr, w_rows, lat_rows, st, evp, shard_owner,
+                                R > 1 ? shard_bcast : NULL, &ctx, me, fm, NULL, &exact);
         if (rc) return rc;
         if (R > 1) { /* every rank must agree before falling back to a wider encoding */
             int32_t* flag = ws->cnt;
@@ -1373,7 +1378,7 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
             SRT_HIPCHK(hipMemcpyAsync(&exact, flag, sizeof(int32_t), hipMemcpyDeviceToHost, st));
             SRT_HIPCHK(hipStreamSynchronize(st));
         }
-        if (exact) enc = fm ? SRT_DENC_F16CMP : SRT_DENC_U16;
+        if (exact) enc = fm ? (sym ? SRT_DENC_F16CMP_SYM : SRT_DENC_F16CMP) : SRT_DENC_U16;
     }
     if (!exact) {
         if (evp) evp->used = 0;

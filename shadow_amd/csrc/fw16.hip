@@ -321,7 +321,9 @@ static __device__ __forceinline__ int tile_row(int bid, int ncol_tiles, int i0, 
 template <bool FM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void fw16_update_kernel(u16* __restrict__ D, int ld,
                                                           const u16* __restrict__ P, int k0,
-                                                          int ncol_tiles, int i0, int skip) {
+                                                          int ncol_tiles, int i0, int skip,
+                                                          const uint32_t* __restrict__ /*tl*/,
+                                                          int /*te*/) {
     __shared__ __attribute__((aligned(16))) uint32_t sA[128 * (UKC + 4)];
     __shared__ __attribute__((aligned(16))) u16 sB[UKC * (128 + 8)];
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
@@ -520,26 +522,58 @@ static __device__ __forceinline__ void fwh_stage(uint32_t (&acc)[8][4], const ui
     }
 }
 
+/* Row-sharded symmetric rounds: of the tile pair (I, J) / (J, I), I != J, the rank owning row I
+ * keeps (I, J) when I < J and I + J is even, or I > J and I + J is odd; the other one is its
+ * transpose, filled in at the end. Every rank then holds about half of its row block's tiles,
+ * whatever its position. */
+static __host__ __device__ __forceinline__ bool sym_kept(int I, int J) {
+    return I == J || ((I < J) == (((I + J) & 1) == 0));
+}
+
 /* SYM: only upper-triangle tiles (I <= J, grid T(T+1)/2) -- an undirected graph's distance
  * matrix stays symmetric through every round, so the lower triangle is the transpose and half the
- * relaxations are skipped; A comes from the pivot panel transposed. */
-template <bool SYM>
+ * relaxations are skipped; A comes from the pivot panel transposed.
+ * XM (row-sharded SYM, D = the rank's rows from tile row i0 = tb, te = end tile row, skip = the
+ * tile row K1 of the next pivot block or -1): 3 = the kept tiles of tile row K1 (block b < T: J =
+ * b) and of tile column K1 in the rank's rows (b >= T: I = tb + b - T), which the next pivot
+ * panel is assembled from; 4 = the rank's kept-tile list tl minus those; 5 = the whole list. */
+template <bool SYM, int XM = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void fwh_update_kernel(
-    u16* __restrict__ D, int ld, const u16* __restrict__ P, int k0, int ncol_tiles, int i0, int skip) {
+    u16* __restrict__ D, int ld, const u16* __restrict__ P, int k0, int ncol_tiles, int i0, int skip,
+    const uint32_t* __restrict__ tl, int te) {
     __shared__ __attribute__((aligned(16))) uint32_t sA[UKC / 2 * 128 * 2];
     __shared__ __attribute__((aligned(16))) u16 sB[UKC * UBS];
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     const int nb = gridDim.x;
     const int per = nb >> 3;
     const int bid = (nb & 7) == 0 ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
-    int I, J;
-    if (SYM) {
+    int I, J, Iloc;
+    if (XM == 3) {
+        if (blockIdx.x < ncol_tiles) {
+            J = blockIdx.x;
+            I = skip;
+            if (I < i0 || I >= te || !sym_kept(I, J)) return;
+        } else {
+            I = i0 + (int)blockIdx.x - ncol_tiles;
+            J = skip;
+            if (I >= te || I == skip || !sym_kept(I, J)) return;
+        }
+        Iloc = I - i0;
+    } else if (XM == 4 || XM == 5) {
+        const uint32_t t = tl[bid];
+        I = (int)(t >> 16);
+        J = (int)(t & 0xFFFFu);
+        if (XM == 4 && (I == skip || J == skip)) return;
+        Iloc = I - i0;
+    } else if (SYM) {
         tri_decode(bid, ncol_tiles, &I, &J);
+        Iloc = I;
     } else {
         I = tile_row(bid, ncol_tiles, i0, skip);
         J = bid % ncol_tiles;
+        Iloc = I;
     }
-    u16* C = D + (size_t)I * 128 * ld + J * 128;
+    u16* C = D + (size_t)Iloc * 128 * ld + J * 128;
     const u16* Ag = D + (size_t)I * 128 * ld + k0;
     const u16* Bg = P + J * 128;
     fwh_stage_regs g;
@@ -607,6 +641,82 @@ __global__ void fw16_finish_kernel(int n, int ld, int row0, const u16* __restric
     if (__ballot(big) && (threadIdx.x & 63) == 0 &&
         !__hip_atomic_load(flags + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
         atomicOr(flags + 1, 1);
+}
+
+/* ---- row-sharded symmetric rounds: pivot-row gather and the final fill -------------------- */
+/* entries of the pivot rows in tile column J that K1's owner does not keep: (J, K1)^T */
+static __device__ __forceinline__ bool sym_gathered(int K1, int J) {
+    return J != K1 && !sym_kept(K1, J);
+}
+static __device__ int sym_gather_slot(int K1, int J) {
+    int c = 0;
+    for (int q = 0; q < J; ++q) c += sym_gathered(K1, q);
+    return c;
+}
+
+/* rows [J*128, J*128 + 128) of the rank (local from tile row tb), columns [c0, c0 + 64),
+ * transposed into a 64 x 128 block per gathered J at out + (slot(J) - slot(tb)) * 8192 */
+__global__ __launch_bounds__(256) void sym_gather_pack_kernel(const u16* __restrict__ D, int ld,
+                                                              int tb, int K1, int c0,
+                                                              u16* __restrict__ out) {
+    __shared__ u16 t[128][KB + 2];
+    const int J = tb + (int)blockIdx.x;
+    if (!sym_gathered(K1, J)) return;
+    const int slot = sym_gather_slot(K1, J) - sym_gather_slot(K1, tb);
+    const u16* src = D + (size_t)(J - tb) * 128 * ld + c0;
+    for (int i = threadIdx.x; i < 128 * KB; i += 256) t[i / KB][i % KB] = src[(size_t)(i / KB) * ld + i % KB];
+    __syncthreads();
+    u16* dst = out + (size_t)slot * (KB * 128);
+    for (int i = threadIdx.x; i < KB * 128; i += 256) dst[i] = t[i % 128][i / 128];
+}
+
+/* owner of K1: every gathered block into its pivot rows (local row row_off), column block J */
+__global__ __launch_bounds__(256) void sym_gather_unpack_kernel(u16* __restrict__ D, int ld,
+                                                                int row_off, int K1,
+                                                                const u16* __restrict__ in) {
+    const int J = (int)blockIdx.x;
+    if (!sym_gathered(K1, J)) return;
+    const u16* src = in + (size_t)sym_gather_slot(K1, J) * (KB * 128);
+    u16* dst = D + (size_t)row_off * ld + J * 128;
+    for (int i = threadIdx.x; i < KB * 128; i += 256) dst[(size_t)(i / 128) * ld + i % 128] = src[i];
+}
+
+/* final fill: kept tile (I, J) of the sender, transposed into a contiguous 128 x 128 block */
+__global__ __launch_bounds__(256) void sym_fill_pack_kernel(const u16* __restrict__ D, int ld, int tb,
+                                                            const uint32_t* __restrict__ pairs,
+                                                            u16* __restrict__ out) {
+    __shared__ u16 t[128][128 + 2];
+    const uint32_t p = pairs[blockIdx.x];
+    const int I = (int)(p >> 16), J = (int)(p & 0xFFFFu);
+    const u16* src = D + (size_t)(I - tb) * 128 * ld + (size_t)J * 128;
+    for (int i = threadIdx.x; i < 128 * 128; i += 256) t[i / 128][i % 128] = src[(size_t)(i / 128) * ld + i % 128];
+    __syncthreads();
+    u16* dst = out + (size_t)blockIdx.x * (128 * 128);
+    for (int i = threadIdx.x; i < 128 * 128; i += 256) dst[i] = t[i % 128][i / 128];
+}
+
+/* receiver: block b (the sender's pair (I, J), J in this rank's rows) becomes tile (J, I) */
+__global__ __launch_bounds__(256) void sym_fill_unpack_kernel(u16* __restrict__ D, int ld, int tb,
+                                                              const uint32_t* __restrict__ pairs,
+                                                              const u16* __restrict__ in) {
+    const uint32_t p = pairs[blockIdx.x];
+    const int I = (int)(p >> 16), J = (int)(p & 0xFFFFu);
+    const u16* src = in + (size_t)blockIdx.x * (128 * 128);
+    u16* dst = D + (size_t)(J - tb) * 128 * ld + (size_t)I * 128;
+    for (int i = threadIdx.x; i < 128 * 128; i += 256) dst[(size_t)(i / 128) * ld + i % 128] = src[i];
+}
+
+/* both tiles in this rank's rows: kept (I, J) transposed into (J, I) */
+__global__ __launch_bounds__(256) void sym_fill_local_kernel(u16* __restrict__ D, int ld, int tb,
+                                                             const uint32_t* __restrict__ pairs) {
+    __shared__ u16 t[128][128 + 2];
+    const uint32_t p = pairs[blockIdx.x];
+    const int I = (int)(p >> 16), J = (int)(p & 0xFFFFu);
+    const u16* src = D + (size_t)(I - tb) * 128 * ld + (size_t)J * 128;
+    for (int i = threadIdx.x; i < 128 * 128; i += 256) t[i / 128][i % 128] = src[(size_t)(i / 128) * ld + i % 128];
+    __syncthreads();
+    u16* dst = D + (size_t)(J - tb) * 128 * ld + (size_t)I * 128;
+    for (int i = threadIdx.x; i < 128 * 128; i += 256) dst[(size_t)(i / 128) * ld + i % 128] = t[i % 128][i / 128];
 }
 
 #ifndef SRT_FW16_DEVICE_ONLY
@@ -682,7 +792,7 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
         fw16_panel_kernel<true, true><<<2 * nb, 256, 0, st>>>(d, ld, 0, nb, P, k0, nb, 1, 1);
         if (k0 > 0) fw16_refresh_kernel<<<k0 / KB, 256, 0, st>>>(d, ld, k0);
         if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
-        fwh_update_kernel<true><<<ntri, 256, 0, st>>>(d, ld, P, k0, T, 0, -1);
+        fwh_update_kernel<true><<<ntri, 256, 0, st>>>(d, ld, P, k0, T, 0, -1, nullptr, 0);
         if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
         SRT_HIPCHK(hipGetLastError());
     }
@@ -697,6 +807,313 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
     *exact = hf[0] ? 0 : 1;
     fw16_small[dev] = hf[1] ? 0 : 1;
     return SRT_OK;
+}
+
+/* Row-sharded symmetric FW (undirected graph, f16-compare path, R > 1 ranks; SURVEY §8e with the
+ * one-GPU upper-triangle saving). Rows stay in the srt_shard_rows blocks; of each tile pair
+ * (I, J) / (J, I) one rank keeps and updates one orientation (sym_kept), so every rank updates
+ * about half of its row block whatever its position. Round k needs the full pivot panel P_k (64 x
+ * ld): its owner holds the kept tiles of tile row K; the other column blocks J are (J, K)^T,
+ * kept by the owners of rows J, who send their 64 x 128 transposed slices to the owner (one
+ * exchange, about half a panel). The owner then closes the diagonal block, updates the pivot-row
+ * panel and broadcasts it. Every rank updates its kept tiles with A = P^T (column block I) and
+ * B = P (column block J), as on one GPU. Lookahead as in srt_fw16_build: each round first
+ * updates the kept tiles of the next pivot block's tile row and column (XM 3), the
+ * high-priority stream cs gathers / closes / broadcasts the next panel under the rest of the
+ * round (XM 4). After the last round each rank receives the transposes of the tiles it does
+ * not keep (point-to-point) and fills them in locally. */
+static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0, int nrows,
+                                  const uint32_t* w_rows, uint32_t* lat_rows, hipStream_t st,
+                                  evpool_t* evp, int* exact) {
+    const int dev = srt_state_slot();
+    const int R = srt_comm_size(comm), me = srt_comm_rank(comm);
+    const int T = ld / 128, nb = ld / KB, nrb = nrows / KB;
+    const int tb = row0 / 128, te = (row0 + nrows) / 128;
+    size_t* caps = fw16_caps;
+    int** flags = fw16_flags;
+    const size_t need = (size_t)nrows * ld + 2 * (size_t)KB * ld;
+    if (caps[dev] < need || !fw16_bufs[dev]) {
+        if (fw16_bufs[dev]) SRT_HIPCHK(hipFree(fw16_bufs[dev]));
+        fw16_bufs[dev] = NULL;
+        caps[dev] = 0;
+        SRT_HIPCHK(hipMalloc(&fw16_bufs[dev], need * sizeof(u16)));
+        caps[dev] = need;
+    }
+    if (!flags[dev]) SRT_HIPCHK(hipMalloc(&flags[dev], 2 * sizeof(int)));
+    fw16_sched* sc;
+    int rc = sched_get(&sc, dev);
+    if (rc) return rc;
+    hipStream_t cs = sc->cs;
+    u16* d = fw16_bufs[dev];
+    u16* pbuf[2] = {d + (size_t)nrows * ld, d + (size_t)nrows * ld + (size_t)KB * ld};
+    /* tile-row ranges of every rank, the owner of each tile row, this rank's kept tiles */
+    int* qtb = (int*)malloc((size_t)R * sizeof(int));
+    int* qte = (int*)malloc((size_t)R * sizeof(int));
+    int* own = (int*)malloc((size_t)T * sizeof(int));
+    const size_t maxkept = (size_t)(te - tb) * T + 1;
+    uint32_t* hkept = (uint32_t*)malloc(maxkept * sizeof(uint32_t));
+    if (!qtb || !qte || !own || !hkept) {
+        free(qtb);
+        free(qte);
+        free(own);
+        free(hkept);
+        return SRT_E_NOMEM;
+    }
+    for (int q = 0; q < R; q++) {
+        int32_t qb, qe;
+        srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &qb, &qe);
+        qtb[q] = qb / 128;
+        qte[q] = qe / 128;
+        for (int K = qtb[q]; K < qte[q] && K < T; K++) own[K] = q;
+    }
+    size_t nkept = 0;
+    for (int I = tb; I < te; I++)
+        for (int J = 0; J < T; J++)
+            if (sym_kept(I, J)) hkept[nkept++] = ((uint32_t)I << 16) | (uint32_t)J;
+    auto gathered = [](int K1, int J) { return J != K1 && !sym_kept(K1, J); };
+    auto gather_count = [&](int K1, int a, int b) {
+        int c = 0;
+        for (int J = a; J < b; J++) c += gathered(K1, J);
+        return c;
+    };
+    /* device scratch: kept-tile list, gather send (this rank's rows) and receive (a panel) */
+    uint32_t* tl = NULL;
+    u16* gsend = NULL;
+    u16* grecv = NULL;
+    const size_t blk = (size_t)KB * 128;
+    bool ok = hipMalloc(&tl, (nkept + 1) * sizeof(uint32_t)) == hipSuccess &&
+              hipMalloc(&gsend, ((size_t)(te - tb) + 1) * blk * sizeof(u16)) == hipSuccess &&
+              hipMalloc(&grecv, ((size_t)T + 1) * blk * sizeof(u16)) == hipSuccess;
+    void** sp = (void**)calloc((size_t)R, sizeof(void*));
+    void** rp = (void**)calloc((size_t)R, sizeof(void*));
+    size_t* sbytes = (size_t*)calloc((size_t)R, sizeof(size_t));
+    size_t* rbytes = (size_t*)calloc((size_t)R, sizeof(size_t));
+    ok = ok && sp && rp && sbytes && rbytes;
+    if (ok && nkept) /* pageable source: finished before the host list can change */
+        ok = hipMemcpyAsync(tl, hkept, nkept * sizeof(uint32_t), hipMemcpyHostToDevice, st) ==
+                 hipSuccess &&
+             hipStreamSynchronize(st) == hipSuccess;
+#define SYM_FAIL(code)                                                                             \
+    do {                                                                                           \
+        rc = (code);                                                                               \
+        goto out;                                                                                  \
+    } while (0)
+#define SYM_HIP(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) {                                                                    \
+            srt_set_error("HIP error %s at %s:%d (%s)", hipGetErrorString(e_), __FILE__,           \
+                          __LINE__, #expr);                                                        \
+            SYM_FAIL(SRT_E_DEVICE);                                                                \
+        }                                                                                          \
+    } while (0)
+    {
+        if (!ok) {
+            srt_set_error("sharded symmetric FW: scratch allocation failed");
+            SYM_FAIL(SRT_E_NOMEM);
+        }
+        if (nrows > 0)
+            fw16_init_kernel<<<dim3(srt_ceil_div(ld, 256), nrows), 256, 0, st>>>(n, ld, row0, w_rows,
+                                                                               d, CAP_F);
+        SYM_HIP(hipGetLastError());
+        SYM_HIP(hipEventRecord(sc->init_done, st));
+        SYM_HIP(hipStreamWaitEvent(cs, sc->init_done, 0));
+        auto panel_of = [&](int k) -> u16* {
+            const int K = k * KB / 128;
+            return own[K] == me ? d + (size_t)(k * KB - row0) * ld : pbuf[k & 1];
+        };
+        /* on cs: assemble, close and broadcast P_k (its tiles' round k-1 values are final) */
+        auto produce = [&](int k) -> int {
+            const int k0 = k * KB, K = k0 / 128, o = own[K];
+            u16* P = panel_of(k);
+            for (int q = 0; q < R; q++) {
+                sp[q] = rp[q] = NULL;
+                sbytes[q] = rbytes[q] = 0;
+            }
+            const int mine = gather_count(K, tb, te);
+            if (me == o) {
+                if (mine)
+                    sym_gather_pack_kernel<<<te - tb, 256, 0, cs>>>(
+                        d, ld, tb, K, k0, grecv + (size_t)gather_count(K, 0, tb) * blk);
+                for (int q = 0; q < R; q++) {
+                    if (q == me) continue;
+                    rp[q] = grecv + (size_t)gather_count(K, 0, qtb[q]) * blk;
+                    rbytes[q] = (size_t)gather_count(K, qtb[q], qte[q]) * blk * sizeof(u16);
+                }
+            } else if (mine) {
+                sym_gather_pack_kernel<<<te - tb, 256, 0, cs>>>(d, ld, tb, K, k0, gsend);
+                sp[o] = gsend;
+                sbytes[o] = (size_t)mine * blk * sizeof(u16);
+            }
+            SRT_HIPCHK(hipGetLastError());
+            int r = srt_coll_exchange(comm, sp, sbytes, rp, rbytes, cs);
+            if (r) return r;
+            if (me == o) {
+                sym_gather_unpack_kernel<<<T, 256, 0, cs>>>(d, ld, k0 - row0, K, grecv);
+                fw16_diag_kernel<<<1, 256, 0, cs>>>(P, ld, k0);
+                fw16_panel_kernel<true, false><<<nb, 256, 0, cs>>>(d, ld, row0, nrb, P, k0, nb, 1, 0);
+                SRT_HIPCHK(hipGetLastError());
+            } else if (k >= 2) {
+                SRT_HIPCHK(hipStreamWaitEvent(cs, sc->upd_done[k & 1], 0)); /* round k-2 read it */
+            }
+            if ((r = srt_coll_bcast(comm, P, (size_t)KB * ld * sizeof(u16), o, cs))) return r;
+            SRT_HIPCHK(hipEventRecord(sc->ready[k & 1], cs));
+            return SRT_OK;
+        };
+        if ((rc = produce(0))) goto out;
+        for (int k = 0; k < nb; ++k) {
+            const int k0 = k * KB;
+            u16* P = panel_of(k);
+            SYM_HIP(hipStreamWaitEvent(st, sc->ready[k & 1], 0));
+            const bool next = k + 1 < nb;
+            const int K1 = next ? (k + 1) * KB / 128 : -1;
+            if (next) {
+                fwh_update_kernel<true, 3><<<T + (te - tb), 256, 0, st>>>(d, ld, P, k0, T, tb, K1,
+                                                                          nullptr, te);
+                SYM_HIP(hipEventRecord(sc->row_done, st));
+                SYM_HIP(hipStreamWaitEvent(cs, sc->row_done, 0));
+                if ((rc = produce(k + 1))) goto out;
+            }
+            if (evp && next) SYM_HIP(hipEventRecord(evp->ev[evp->used++], st));
+            if (nkept) {
+                if (next)
+                    fwh_update_kernel<true, 4><<<(unsigned)nkept, 256, 0, st>>>(d, ld, P, k0, T, tb,
+                                                                               K1, tl, te);
+                else
+                    fwh_update_kernel<true, 5><<<(unsigned)nkept, 256, 0, st>>>(d, ld, P, k0, T, tb,
+                                                                               -1, tl, te);
+            }
+            if (evp && next) SYM_HIP(hipEventRecord(evp->ev[evp->used++], st));
+            SYM_HIP(hipGetLastError());
+            SYM_HIP(hipEventRecord(sc->upd_done[k & 1], st));
+        }
+        /* fill the tiles this rank does not keep: transposes from their keepers */
+        {
+            size_t nloc = 0;
+            size_t* scount = (size_t*)calloc((size_t)R, sizeof(size_t));
+            size_t* rcount = (size_t*)calloc((size_t)R, sizeof(size_t));
+            if (!scount || !rcount) {
+                free(scount);
+                free(rcount);
+                SYM_FAIL(SRT_E_NOMEM);
+            }
+            for (int q = 0; q < R; q++) {
+                for (int I = tb; I < te; I++) /* this rank keeps (I, J), J in q's rows */
+                    for (int J = qtb[q]; J < qte[q]; J++)
+                        if (I != J && sym_kept(I, J)) (q == me ? nloc : scount[q])++;
+                if (q != me)
+                    for (int I = qtb[q]; I < qte[q]; I++) /* q keeps (I, J), J in this rank's rows */
+                        for (int J = tb; J < te; J++)
+                            if (sym_kept(I, J)) rcount[q]++;
+            }
+            size_t stot = 0, rtot = 0;
+            for (int q = 0; q < R; q++) {
+                stot += scount[q];
+                rtot += rcount[q];
+            }
+            const size_t npairs = nloc + stot + rtot;
+            uint32_t* hp = (uint32_t*)malloc((npairs + 1) * sizeof(uint32_t));
+            uint32_t* dp = NULL;
+            u16* fsend = NULL;
+            u16* frecv = NULL;
+            const size_t tile = 128 * 128;
+            bool fok = hp && hipMalloc(&dp, (npairs + 1) * sizeof(uint32_t)) == hipSuccess &&
+                       hipMalloc(&fsend, (stot + 1) * tile * sizeof(u16)) == hipSuccess &&
+                       hipMalloc(&frecv, (rtot + 1) * tile * sizeof(u16)) == hipSuccess;
+            if (fok) {
+                /* layout of hp: local pairs, then send pairs by peer, then receive pairs by peer */
+                size_t o = 0;
+                for (int I = tb; I < te; I++)
+                    for (int J = tb; J < te; J++)
+                        if (I != J && sym_kept(I, J)) hp[o++] = ((uint32_t)I << 16) | (uint32_t)J;
+                for (int q = 0; q < R; q++)
+                    if (q != me)
+                        for (int I = tb; I < te; I++)
+                            for (int J = qtb[q]; J < qte[q]; J++)
+                                if (sym_kept(I, J)) hp[o++] = ((uint32_t)I << 16) | (uint32_t)J;
+                for (int q = 0; q < R; q++)
+                    if (q != me)
+                        for (int I = qtb[q]; I < qte[q]; I++)
+                            for (int J = tb; J < te; J++)
+                                if (sym_kept(I, J)) hp[o++] = ((uint32_t)I << 16) | (uint32_t)J;
+                fok = hipMemcpyAsync(dp, hp, npairs * sizeof(uint32_t), hipMemcpyHostToDevice, st) ==
+                      hipSuccess;
+                /* the copy reads pageable host memory: finish it before hp is freed */
+                fok = fok && hipStreamSynchronize(st) == hipSuccess;
+            }
+            if (fok) {
+                if (nloc) sym_fill_local_kernel<<<(unsigned)nloc, 256, 0, st>>>(d, ld, tb, dp);
+                if (stot)
+                    sym_fill_pack_kernel<<<(unsigned)stot, 256, 0, st>>>(d, ld, tb, dp + nloc, fsend);
+                size_t so = 0, ro = 0;
+                for (int q = 0; q < R; q++) {
+                    sp[q] = fsend + so * tile;
+                    sbytes[q] = q == me ? 0 : scount[q] * tile * sizeof(u16);
+                    rp[q] = frecv + ro * tile;
+                    rbytes[q] = q == me ? 0 : rcount[q] * tile * sizeof(u16);
+                    so += q == me ? 0 : scount[q];
+                    ro += q == me ? 0 : rcount[q];
+                }
+                fok = hipGetLastError() == hipSuccess;
+                if (fok && (rc = srt_coll_exchange(comm, sp, sbytes, rp, rbytes, st))) fok = false;
+                if (fok && rtot)
+                    sym_fill_unpack_kernel<<<(unsigned)rtot, 256, 0, st>>>(d, ld, tb,
+                                                                          dp + nloc + stot, frecv);
+                fok = fok && hipGetLastError() == hipSuccess &&
+                      hipStreamSynchronize(st) == hipSuccess;
+            }
+            if (dp) (void)hipFree(dp);
+            if (fsend) (void)hipFree(fsend);
+            if (frecv) (void)hipFree(frecv);
+            free(hp);
+            free(scount);
+            free(rcount);
+            if (!fok) {
+                if (!rc) {
+                    srt_set_error("sharded symmetric FW: final fill failed");
+                    rc = SRT_E_DEVICE;
+                }
+                goto out;
+            }
+        }
+        SYM_HIP(hipMemsetAsync(flags[dev], 0, 2 * sizeof(int), st));
+        if (nrows > 0)
+            fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 256), nrows), 256, 0, st>>>(
+                n, ld, row0, d, lat_rows, flags[dev], CAP_F);
+        SYM_HIP(hipGetLastError());
+        int hf[2] = {0, 0};
+        SYM_HIP(hipMemcpyAsync(hf, flags[dev], 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+        SYM_HIP(hipStreamSynchronize(st));
+        *exact = hf[0] ? 0 : 1;
+        fw16_small[dev] = hf[1] ? 0 : 1;
+    }
+out:
+#undef SYM_HIP
+#undef SYM_FAIL
+    (void)hipStreamSynchronize(cs);
+    (void)hipStreamSynchronize(st);
+    if (tl) (void)hipFree(tl);
+    if (gsend) (void)hipFree(gsend);
+    if (grecv) (void)hipFree(grecv);
+    free(sp);
+    free(rp);
+    free(sbytes);
+    free(rbytes);
+    free(qtb);
+    free(qte);
+    free(own);
+    free(hkept);
+    return rc;
+}
+
+int srt_fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0, int nrows,
+                               const uint32_t* w_rows, uint32_t* lat_rows, hipStream_t st,
+                               evpool_t* evp, int* exact) {
+    if (ld % 128 || nrows % 128 || row0 % 128 || srt_comm_size(comm) < 2) {
+        srt_set_error("sharded symmetric FW needs 128-aligned shards and two or more ranks");
+        return SRT_E_ARG;
+    }
+    return fw16_build_sym_sharded(comm, n, ld, row0, nrows, w_rows, lat_rows, st, evp, exact);
 }
 
 int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,
@@ -781,14 +1198,15 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
             panel<<<nb + nrb, 256, 0, st>>>(d, ld, row0, nrb, P, k0, nb, 0, 1);
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
             if (skip >= 0) {
-                update<<<ncol128, 256, 0, st>>>(d, ld, P, k0, ncol128, skip, -1);
+                update<<<ncol128, 256, 0, st>>>(d, ld, P, k0, ncol128, skip, -1, nullptr, 0);
                 SRT_HIPCHK(hipEventRecord(sc->row_done, st));
                 SRT_HIPCHK(hipStreamWaitEvent(cs, sc->row_done, 0));
                 if ((rc = produce(k + 1))) return rc;
                 if (nrow128 > 1)
-                    update<<<ncol128 * (nrow128 - 1), 256, 0, st>>>(d, ld, P, k0, ncol128, 0, skip);
+                    update<<<ncol128 * (nrow128 - 1), 256, 0, st>>>(d, ld, P, k0, ncol128, 0, skip,
+                                                                   nullptr, 0);
             } else {
-                update<<<ncol128 * nrow128, 256, 0, st>>>(d, ld, P, k0, ncol128, 0, -1);
+                update<<<ncol128 * nrow128, 256, 0, st>>>(d, ld, P, k0, ncol128, 0, -1, nullptr, 0);
             }
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
             SRT_HIPCHK(hipGetLastError());

@@ -111,6 +111,10 @@ typedef int (*srt_owner_fn)(void* ctx, int k0);
  * f16-compare instruction mix (cap 0x3DFF), fm = 0 the v_pk_min_u16 mix (cap 0x7FFF). Returns
  * SRT_OK and *exact = 1 when every distance is below the cap (else the caller reruns with the
  * next wider path). lat_rows receives the distances widened to u32 quanta. */
+/* row-sharded symmetric rounds (undirected, f16-compare path, >= 2 ranks; fw16.hip) */
+int srt_fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0, int nrows,
+                               const uint32_t* w_rows, uint32_t* lat_rows, hipStream_t st,
+                               evpool_t* evp, int* exact);
 int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,
                    hipStream_t st, evpool_t* evp, srt_owner_fn owner_of, srt_panel_bcast_fn bcast,
                    void* ctx, int rank, int fm, int* sym, int* exact);

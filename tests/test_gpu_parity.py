@@ -298,7 +298,8 @@ def _ring_graph(n, hop_ms, seed):
                         np.array(lat, np.int64), loss)
 
 
-@pytest.mark.parametrize("kind", ["dense", "sparse", "directed", "ring_u16", "ring_u32"])
+@pytest.mark.parametrize("kind", ["dense", "dense2000", "ring_f16", "sparse", "directed",
+                                  "ring_u16", "ring_u32"])
 @pytest.mark.parametrize("ranks", [2, 3, 4])
 def test_virtual_ranks_sharded_build(gpu, monkeypatch, kind, ranks):
     """The multi-rank sharded builds on ONE GPU: SRT_VIRTUAL_RANKS=R runs R ranks of
@@ -307,11 +308,17 @@ def test_virtual_ranks_sharded_build(gpu, monkeypatch, kind, ranks):
     all-reduce, the essential-arc count all-reduce and segment broadcasts, the symmetry
     exchange, the sparse all-gather) as device-to-device copies. The C host logic of the
     N-rank paths -- shard partition, owners, lookahead order, offsets of every exchange -- is
-    the code the RCCL runs use; the tables must equal the oracle's."""
+    the code the RCCL runs use; the tables must equal the oracle's. Undirected graphs on the
+    f16-compare tier take the row-sharded symmetric rounds (kept-tile checkerboard, pivot-row
+    gather, final transpose fill: encoding 4)."""
     monkeypatch.setenv("SRT_VIRTUAL_RANKS", str(ranks))
     algo = ALGO_DENSE_FW
     if kind == "dense":
         g = graphs.complete_graph(700, seed=9)
+    elif kind == "dense2000":
+        g = graphs.complete_graph(2000, seed=13)
+    elif kind == "ring_f16":
+        g = _ring_graph(1000, 1, 1)
     elif kind == "sparse":
         g = graphs.random_geometric(1500, seed=3)
         algo = ALGO_SPARSE_SSSP
@@ -332,8 +339,10 @@ def test_virtual_ranks_sharded_build(gpu, monkeypatch, kind, ranks):
                                 ngpus=1)
     exp = _oracle(g)
     assert_tables(lat, rel, exp["lat_int"], exp["rel"], f"virtual x{ranks} {kind}")
-    if kind.startswith("ring"):
-        assert st.dist_enc == (2 if kind == "ring_u16" else 1)
+    want_enc = {"dense": 4, "dense2000": 4, "ring_f16": 4, "directed": 3, "ring_u16": 2,
+                "ring_u32": 1}
+    if kind in want_enc:
+        assert st.dist_enc == want_enc[kind], f"encoding {st.dist_enc}"
 
 
 def test_packet_path_trace_replay(gpu):

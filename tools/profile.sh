@@ -13,9 +13,9 @@ mkdir -p $OUT
 BENCH="python3 $ROOT/bench.py --workload $WL --steps 1 --warmup 0 --no-cpu-baseline"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $BENCH > $OUT/trace.log 2>&1
 echo trace-done
-timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex $KREGEX --output-format csv -d $OUT/fetch -o run -- $BENCH > $OUT/fetch.log 2>&1
+timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KREGEX" --output-format csv -d $OUT/fetch -o run -- $BENCH > $OUT/fetch.log 2>&1
 echo fetch-done
-timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex $KREGEX --output-format csv -d $OUT/write -o run -- $BENCH > $OUT/write.log 2>&1
+timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KREGEX" --output-format csv -d $OUT/write -o run -- $BENCH > $OUT/write.log 2>&1
 echo write-done
-python3 $ROOT/tools/pmc_summary.py $OUT $KREGEX $OUT/pmc_summary.json --stats-out $OUT/kernel_stats.csv
+python3 $ROOT/tools/pmc_summary.py $OUT "$KREGEX" $OUT/pmc_summary.json --stats-out $OUT/kernel_stats.csv
 echo profile-done
