@@ -6,7 +6,8 @@ RCCL. Here the same schedule -- the library's own srt_shard_rows partition, the 
 produced from a partially updated round k), the essential-arc all-reduce/broadcast,
 the undirected mirror exchange (rank q sends rel[q rows][r cols] to every r > q) and the sparse
 source-shard all-gather -- is replayed with numpy compute and gloo collectives, and the
-assembled tables must equal the CPU oracle's.
+assembled tables must equal the CPU oracle's. The row-sharded symmetric rounds (kept-tile
+checkerboard, pivot-row gather, final transpose fill) are replayed the same way.
 """
 import ctypes
 import os
@@ -180,6 +181,113 @@ def _dense_worker(rank, R, port, n, seed, q):
     dist.destroy_process_group()
 
 
+def _dense_sym_worker(rank, R, port, n, seed, q):
+    """The row-sharded symmetric rounds of fw16.hip fw16_build_sym_sharded, distances only: each
+    rank keeps one orientation of every 128-tile pair (sym_kept), the next pivot rows are
+    gathered from their keepers (transposed 64 x 128 slices, sent to the owner), the owner closes
+    the diagonal block and the row panel and broadcasts it, every rank updates its kept tiles
+    with A = P^T and B = P, the next pivot block's tile row / column first; at the end each
+    rank receives the transposes of the tiles it does not keep."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=R)
+    from shadow_amd._lib import lib
+    L = lib()
+    ld = (n + ALIGN - 1) // ALIGN * ALIGN
+    T = ld // ALIGN
+    b, e = _shard(L, ld, R, rank)
+    tb, te = b // ALIGN, e // ALIGN
+    w, _ = graphs.complete_dense(n, seed)
+    W = np.full((ld, ld), INF, np.int64)
+    W[:n, :n] = w
+    D = W[b:e].copy()
+    for i in range(b, e):
+        D[i - b, i] = 0
+    ranges = [_shard(L, ld, R, x) for x in range(R)]
+    own = {K: x for x, (qb, qe) in enumerate(ranges) for K in range(qb // ALIGN, qe // ALIGN)}
+
+    def kept(I, J):
+        return I == J or ((I < J) == ((I + J) % 2 == 0))
+
+    def gathered(K, J):
+        return J != K and not kept(K, J)
+
+    def tile(I, J):  # view of this rank's tile (I, J)
+        return D[(I - tb) * ALIGN:(I - tb + 1) * ALIGN, J * ALIGN:(J + 1) * ALIGN]
+
+    def produce(k0):
+        K, o = k0 // ALIGN, own[k0 // ALIGN]
+        if rank != o:
+            blocks = [D[(J - tb) * ALIGN:(J - tb + 1) * ALIGN, k0:k0 + KB].T for J in range(tb, te)
+                      if gathered(K, J)]
+            if blocks:
+                dist.send(torch.from_numpy(np.ascontiguousarray(np.concatenate(blocks, axis=1))), o)
+            P = torch.zeros((KB, ld), dtype=torch.int64)
+        else:
+            rows = D[k0 - b:k0 - b + KB]
+            for J in range(tb, te):
+                if gathered(K, J):
+                    rows[:, J * ALIGN:(J + 1) * ALIGN] = D[(J - tb) * ALIGN:(J - tb + 1) * ALIGN,
+                                                           k0:k0 + KB].T
+            for x, (qb, qe) in enumerate(ranges):
+                js = [J for J in range(qb // ALIGN, qe // ALIGN) if gathered(K, J)]
+                if x == rank or not js:
+                    continue
+                buf = torch.zeros((KB, ALIGN * len(js)), dtype=torch.int64)
+                dist.recv(buf, x)
+                for i, J in enumerate(js):
+                    rows[:, J * ALIGN:(J + 1) * ALIGN] = buf[:, i * ALIGN:(i + 1) * ALIGN].numpy()
+            Tk = rows[:, k0:k0 + KB]
+            for m in range(KB):  # diagonal closure
+                Tk = np.minimum(Tk, Tk[:, m:m + 1] + Tk[m:m + 1, :])
+            rows[:, k0:k0 + KB] = Tk
+            rows[:] = np.minimum(rows, _minplus(Tk, rows))  # row panel
+            P = torch.from_numpy(rows.copy())
+        dist.broadcast(P, o)
+        return P.numpy()
+
+    def update(P, tiles):
+        for I, J in tiles:
+            C = tile(I, J)
+            C[:] = np.minimum(C, _minplus(P[:, I * ALIGN:(I + 1) * ALIGN].T,
+                                          P[:, J * ALIGN:(J + 1) * ALIGN]))
+
+    mine = [(I, J) for I in range(tb, te) for J in range(T) if kept(I, J)]
+    P = produce(0)
+    for k0 in range(0, ld, KB):
+        k1 = k0 + KB
+        if k1 < ld:
+            K1 = k1 // ALIGN
+            cross = [t for t in mine if K1 in t]
+            update(P, cross)
+            Pn = produce(k1)
+            update(P, [t for t in mine if K1 not in t])
+        else:
+            update(P, mine)
+            Pn = None
+        P = Pn
+    # fill: x sends the transposes of its kept tiles (I in x, J in y) to y, in one global order
+    for x, (xb, xe) in enumerate(ranges):
+        for y, (yb, ye) in enumerate(ranges):
+            pairs = [(I, J) for I in range(xb // ALIGN, xe // ALIGN)
+                     for J in range(yb // ALIGN, ye // ALIGN) if I != J and kept(I, J)]
+            if not pairs:
+                continue
+            if x == y == rank:
+                for I, J in pairs:
+                    tile(J, I)[:] = tile(I, J).T
+            elif rank == x:
+                dist.send(torch.from_numpy(np.ascontiguousarray(
+                    np.concatenate([tile(I, J).T for I, J in pairs], axis=1))), y)
+            elif rank == y:
+                buf = torch.zeros((ALIGN, ALIGN * len(pairs)), dtype=torch.int64)
+                dist.recv(buf, x)
+                for i, (I, J) in enumerate(pairs):
+                    tile(J, I)[:] = buf[:, i * ALIGN:(i + 1) * ALIGN].numpy()
+    q.put((rank, D[:, :n].copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def _sparse_worker(rank, R, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=R)
@@ -221,6 +329,27 @@ def test_dense_sharded_schedule_gloo(native):
     exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss))
     assert np.array_equal(lat, exp["lat_int"])
     assert np.array_equal(rel, exp["rel"])
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("n,R", [(400, 2), (700, 3)])
+def test_dense_symmetric_sharded_schedule_gloo(native, n, R):
+    seed = 7
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dense_sym_worker, args=(r, R, port, n, seed, q)) for r in range(R)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=500) for _ in range(R)], key=lambda x: x[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    D = np.concatenate([x[1] for x in res])[:n].astype(np.uint64) * np.uint64(1_000_000)
+    g = graphs.complete_graph(n, seed=seed)
+    exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss))
+    off = ~np.eye(n, dtype=bool)  # the diagonal follows its own rule after the rounds
+    assert np.array_equal(D[off], exp["lat_int"][off])
 
 
 @pytest.mark.timeout(300)
