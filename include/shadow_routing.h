@@ -156,6 +156,10 @@ int srt_comm_init_all(int32_t ndev, const int32_t* devices, srt_comm** comms);
  * copies ordered by events and host barriers. srt_build_tables_multi uses them when the
  * environment sets SRT_VIRTUAL_RANKS. */
 int srt_comm_init_virtual(int32_t nranks, int32_t device, srt_comm** comms);
+/* Bind the calling host thread to virtual rank `rank` on `device` (its own workspaces and
+ * streams) before it drives that rank's srt_dense_build_sharded / srt_sparse_graph_rows;
+ * rank < 0 returns the thread to the per-device state. */
+int srt_virtual_rank_bind(int32_t rank, int32_t device);
 /* Row-block partition used by every sharded build: rank r owns rows [begin, end). */
 void srt_shard_rows(int32_t n, int32_t align, int32_t nranks, int32_t rank, int32_t* begin,
                     int32_t* end);

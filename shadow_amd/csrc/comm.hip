@@ -150,6 +150,12 @@ extern "C" int srt_comm_init_virtual(int32_t nranks, int32_t device, srt_comm** 
     return SRT_OK;
 }
 
+extern "C" int srt_virtual_rank_bind(int32_t rank, int32_t device) {
+    srt_set_virtual_slot(rank);
+    SRT_HIPCHK(hipSetDevice(device));
+    return SRT_OK;
+}
+
 extern "C" void srt_comm_free(srt_comm* comm) {
     if (!comm) return;
     if (comm->loop) {
