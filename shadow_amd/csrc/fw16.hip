@@ -643,41 +643,51 @@ __global__ void fw16_finish_kernel(int n, int ld, int row0, const u16* __restric
         atomicOr(flags + 1, 1);
 }
 
-/* ---- row-sharded symmetric rounds: pivot-row gather and the final fill -------------------- */
-/* entries of the pivot rows in tile column J that K1's owner does not keep: (J, K1)^T */
-static __device__ __forceinline__ bool sym_gathered(int K1, int J) {
-    return J != K1 && !sym_kept(K1, J);
+/* ---- row-sharded symmetric rounds: pivot panel from every rank, final transpose fill -------- */
+/* Pivot panel of block k (tile row K) as R broadcasts: column block J comes from its contributor
+ * (K's owner when it keeps (K, J), else the owner of row J, as (J, K)^T); blocks are staged in
+ * (contributor, J) order, so each contributor's blocks are one contiguous broadcast. */
+static __device__ __forceinline__ int sym_contrib(int K, int J, const int* __restrict__ own) {
+    return sym_kept(K, J) ? own[K] : own[J];
 }
-static __device__ int sym_gather_slot(int K1, int J) {
-    int c = 0;
-    for (int q = 0; q < J; ++q) c += sym_gathered(K1, q);
-    return c;
+static __device__ int sym_contrib_pos(int K, int J, int T, const int* __restrict__ own) {
+    const int c = sym_contrib(K, J, own);
+    int pos = 0;
+    for (int q = 0; q < T; ++q) {
+        const int cq = sym_contrib(K, q, own);
+        pos += cq < c || (cq == c && q < J);
+    }
+    return pos;
 }
 
-/* rows [J*128, J*128 + 128) of the rank (local from tile row tb), columns [c0, c0 + 64),
- * transposed into a 64 x 128 block per gathered J at out + (slot(J) - slot(tb)) * 8192 */
-__global__ __launch_bounds__(256) void sym_gather_pack_kernel(const u16* __restrict__ D, int ld,
-                                                              int tb, int K1, int c0,
-                                                              u16* __restrict__ out) {
+/* this rank's blocks of panel k into the staging buffer (64 x 128 each) */
+__global__ __launch_bounds__(256) void sym_contrib_pack_kernel(const u16* __restrict__ D, int ld,
+                                                               int row0, int tb, int K, int k0,
+                                                               int T, const int* __restrict__ own,
+                                                               int me, u16* __restrict__ stage) {
     __shared__ u16 t[128][KB + 2];
-    const int J = tb + (int)blockIdx.x;
-    if (!sym_gathered(K1, J)) return;
-    const int slot = sym_gather_slot(K1, J) - sym_gather_slot(K1, tb);
-    const u16* src = D + (size_t)(J - tb) * 128 * ld + c0;
+    const int J = (int)blockIdx.x;
+    if (J >= T || sym_contrib(K, J, own) != me) return;
+    u16* dst = stage + (size_t)sym_contrib_pos(K, J, T, own) * (KB * 128);
+    if (sym_kept(K, J)) { /* this rank owns the pivot rows: straight copy */
+        const u16* src = D + (size_t)(k0 - row0) * ld + (size_t)J * 128;
+        for (int i = threadIdx.x; i < KB * 128; i += 256) dst[i] = src[(size_t)(i / 128) * ld + i % 128];
+        return;
+    }
+    const u16* src = D + (size_t)(J - tb) * 128 * ld + k0; /* tile (J, K), the pivot columns */
     for (int i = threadIdx.x; i < 128 * KB; i += 256) t[i / KB][i % KB] = src[(size_t)(i / KB) * ld + i % KB];
     __syncthreads();
-    u16* dst = out + (size_t)slot * (KB * 128);
     for (int i = threadIdx.x; i < KB * 128; i += 256) dst[i] = t[i % 128][i / 128];
 }
 
-/* owner of K1: every gathered block into its pivot rows (local row row_off), column block J */
-__global__ __launch_bounds__(256) void sym_gather_unpack_kernel(u16* __restrict__ D, int ld,
-                                                                int row_off, int K1,
-                                                                const u16* __restrict__ in) {
+/* every rank: staged blocks into its panel buffer P (64 x ld) */
+__global__ __launch_bounds__(256) void sym_contrib_unpack_kernel(u16* __restrict__ P, int ld, int K,
+                                                                 int T, const int* __restrict__ own,
+                                                                 const u16* __restrict__ stage) {
     const int J = (int)blockIdx.x;
-    if (!sym_gathered(K1, J)) return;
-    const u16* src = in + (size_t)sym_gather_slot(K1, J) * (KB * 128);
-    u16* dst = D + (size_t)row_off * ld + J * 128;
+    if (J >= T) return;
+    const u16* src = stage + (size_t)sym_contrib_pos(K, J, T, own) * (KB * 128);
+    u16* dst = P + (size_t)J * 128;
     for (int i = threadIdx.x; i < KB * 128; i += 256) dst[(size_t)(i / 128) * ld + i % 128] = src[i];
 }
 
@@ -813,15 +823,16 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
  * one-GPU upper-triangle saving). Rows stay in the srt_shard_rows blocks; of each tile pair
  * (I, J) / (J, I) one rank keeps and updates one orientation (sym_kept), so every rank updates
  * about half of its row block whatever its position. Round k needs the full pivot panel P_k (64 x
- * ld): its owner holds the kept tiles of tile row K; the other column blocks J are (J, K)^T,
- * kept by the owners of rows J, who send their 64 x 128 transposed slices to the owner (one
- * exchange, about half a panel). The owner then closes the diagonal block, updates the pivot-row
- * panel and broadcasts it. Every rank updates its kept tiles with A = P^T (column block I) and
- * B = P (column block J), as on one GPU. Lookahead as in srt_fw16_build: each round first
- * updates the kept tiles of the next pivot block's tile row and column (XM 3), the
- * high-priority stream cs gathers / closes / broadcasts the next panel under the rest of the
- * round (XM 4). After the last round each rank receives the transposes of the tiles it does
- * not keep (point-to-point) and fills them in locally. */
+ * ld): column block J is in the kept tile (K, J) at the owner of tile row K, or is (J, K)^T at
+ * the owner of row J. Every rank stages the blocks it holds (transposing the latter) and
+ * broadcasts them, one grouped broadcast per round (4 MiB in all at C4); each rank then closes
+ * the diagonal block and updates the row panel itself (24 us, instead of a second collective
+ * in the chain), and the owner writes the result back into its pivot rows. Every rank updates
+ * its kept tiles with A = P^T (column block I) and B = P (column block J), as on one GPU.
+ * Lookahead as in srt_fw16_build: each round first updates the kept tiles of the next pivot
+ * block's tile row and column (XM 3), the high-priority stream cs assembles and closes the next
+ * panel under the rest of the round (XM 4). After the last round each rank receives the
+ * transposes of the tiles it does not keep (point-to-point) and fills them in locally. */
 static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0, int nrows,
                                   const uint32_t* w_rows, uint32_t* lat_rows, hipStream_t st,
                                   evpool_t* evp, int* exact) {
@@ -870,20 +881,19 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
     for (int I = tb; I < te; I++)
         for (int J = 0; J < T; J++)
             if (sym_kept(I, J)) hkept[nkept++] = ((uint32_t)I << 16) | (uint32_t)J;
-    auto gathered = [](int K1, int J) { return J != K1 && !sym_kept(K1, J); };
-    auto gather_count = [&](int K1, int a, int b) {
-        int c = 0;
-        for (int J = a; J < b; J++) c += gathered(K1, J);
-        return c;
-    };
     /* device scratch: kept-tile list, gather send (this rank's rows) and receive (a panel) */
     uint32_t* tl = NULL;
-    u16* gsend = NULL;
-    u16* grecv = NULL;
+    int* down = NULL; /* owner of each tile row, on the device */
+    u16* grecv = NULL; /* staged panel blocks in (contributor, J) order */
+    int* cnt = (int*)calloc((size_t)R, sizeof(int));
     const size_t blk = (size_t)KB * 128;
-    bool ok = hipMalloc(&tl, (nkept + 1) * sizeof(uint32_t)) == hipSuccess &&
-              hipMalloc(&gsend, ((size_t)(te - tb) + 1) * blk * sizeof(u16)) == hipSuccess &&
+    bool ok = cnt && hipMalloc(&tl, (nkept + 1) * sizeof(uint32_t)) == hipSuccess &&
+              hipMalloc(&down, (size_t)T * sizeof(int)) == hipSuccess &&
               hipMalloc(&grecv, ((size_t)T + 1) * blk * sizeof(u16)) == hipSuccess;
+    if (ok)
+        ok = hipMemcpyAsync(down, own, (size_t)T * sizeof(int), hipMemcpyHostToDevice, st) ==
+                 hipSuccess &&
+             hipStreamSynchronize(st) == hipSuccess;
     void** sp = (void**)calloc((size_t)R, sizeof(void*));
     void** rp = (void**)calloc((size_t)R, sizeof(void*));
     size_t* sbytes = (size_t*)calloc((size_t)R, sizeof(size_t));
@@ -918,45 +928,35 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
         SYM_HIP(hipGetLastError());
         SYM_HIP(hipEventRecord(sc->init_done, st));
         SYM_HIP(hipStreamWaitEvent(cs, sc->init_done, 0));
-        auto panel_of = [&](int k) -> u16* {
-            const int K = k * KB / 128;
-            return own[K] == me ? d + (size_t)(k * KB - row0) * ld : pbuf[k & 1];
-        };
-        /* on cs: assemble, close and broadcast P_k (its tiles' round k-1 values are final) */
+        auto panel_of = [&](int k) -> u16* { return pbuf[k & 1]; };
+        /* on cs: assemble P_k from every rank's blocks (its tiles' round k-1 values are final),
+         * then every rank closes the diagonal block and updates the row panel itself; the owner
+         * also writes the result back into its pivot rows */
         auto produce = [&](int k) -> int {
             const int k0 = k * KB, K = k0 / 128, o = own[K];
-            u16* P = panel_of(k);
-            for (int q = 0; q < R; q++) {
-                sp[q] = rp[q] = NULL;
-                sbytes[q] = rbytes[q] = 0;
-            }
-            const int mine = gather_count(K, tb, te);
-            if (me == o) {
-                if (mine)
-                    sym_gather_pack_kernel<<<te - tb, 256, 0, cs>>>(
-                        d, ld, tb, K, k0, grecv + (size_t)gather_count(K, 0, tb) * blk);
-                for (int q = 0; q < R; q++) {
-                    if (q == me) continue;
-                    rp[q] = grecv + (size_t)gather_count(K, 0, qtb[q]) * blk;
-                    rbytes[q] = (size_t)gather_count(K, qtb[q], qte[q]) * blk * sizeof(u16);
-                }
-            } else if (mine) {
-                sym_gather_pack_kernel<<<te - tb, 256, 0, cs>>>(d, ld, tb, K, k0, gsend);
-                sp[o] = gsend;
-                sbytes[o] = (size_t)mine * blk * sizeof(u16);
-            }
+            u16* P = pbuf[k & 1];
+            if (k >= 2) SRT_HIPCHK(hipStreamWaitEvent(cs, sc->upd_done[k & 1], 0)); /* k-2 read P */
+            for (int q = 0; q < R; q++) cnt[q] = 0;
+            for (int J = 0; J < T; J++) cnt[sym_kept(K, J) ? o : own[J]]++;
+            if (cnt[me])
+                sym_contrib_pack_kernel<<<T, 256, 0, cs>>>(d, ld, row0, tb, K, k0, T, down, me, grecv);
             SRT_HIPCHK(hipGetLastError());
-            int r = srt_coll_exchange(comm, sp, sbytes, rp, rbytes, cs);
-            if (r) return r;
-            if (me == o) {
-                sym_gather_unpack_kernel<<<T, 256, 0, cs>>>(d, ld, k0 - row0, K, grecv);
-                fw16_diag_kernel<<<1, 256, 0, cs>>>(P, ld, k0);
-                fw16_panel_kernel<true, false><<<nb, 256, 0, cs>>>(d, ld, row0, nrb, P, k0, nb, 1, 0);
-                SRT_HIPCHK(hipGetLastError());
-            } else if (k >= 2) {
-                SRT_HIPCHK(hipStreamWaitEvent(cs, sc->upd_done[k & 1], 0)); /* round k-2 read it */
+            int r = srt_coll_group_begin(comm);
+            size_t off = 0;
+            for (int q = 0; q < R && !r; q++) {
+                if (cnt[q])
+                    r = srt_coll_bcast(comm, grecv + off * blk, (size_t)cnt[q] * blk * sizeof(u16), q, cs);
+                off += (size_t)cnt[q];
             }
-            if ((r = srt_coll_bcast(comm, P, (size_t)KB * ld * sizeof(u16), o, cs))) return r;
+            const int r2 = srt_coll_group_end(comm);
+            if (r || r2) return r ? r : r2;
+            sym_contrib_unpack_kernel<<<T, 256, 0, cs>>>(P, ld, K, T, down, grecv);
+            fw16_diag_kernel<<<1, 256, 0, cs>>>(P, ld, k0);
+            fw16_panel_kernel<true, false><<<nb, 256, 0, cs>>>(d, ld, row0, nrb, P, k0, nb, 1, 0);
+            SRT_HIPCHK(hipGetLastError());
+            if (me == o)
+                SRT_HIPCHK(hipMemcpyAsync(d + (size_t)(k0 - row0) * ld, P, (size_t)KB * ld * sizeof(u16),
+                                          hipMemcpyDeviceToDevice, cs));
             SRT_HIPCHK(hipEventRecord(sc->ready[k & 1], cs));
             return SRT_OK;
         };
@@ -1093,8 +1093,9 @@ out:
     (void)hipStreamSynchronize(cs);
     (void)hipStreamSynchronize(st);
     if (tl) (void)hipFree(tl);
-    if (gsend) (void)hipFree(gsend);
+    if (down) (void)hipFree(down);
     if (grecv) (void)hipFree(grecv);
+    free(cnt);
     free(sp);
     free(rp);
     free(sbytes);

@@ -7,7 +7,8 @@ produced from a partially updated round k), the essential-arc all-reduce/broadca
 the undirected mirror exchange (rank q sends rel[q rows][r cols] to every r > q) and the sparse
 source-shard all-gather -- is replayed with numpy compute and gloo collectives, and the
 assembled tables must equal the CPU oracle's. The row-sharded symmetric rounds (kept-tile
-checkerboard, pivot-row gather, final transpose fill) are replayed the same way.
+checkerboard, panel blocks broadcast by their holders, final transpose fill) are replayed the
+same way.
 """
 import ctypes
 import os
@@ -183,11 +184,12 @@ def _dense_worker(rank, R, port, n, seed, q):
 
 def _dense_sym_worker(rank, R, port, n, seed, q):
     """The row-sharded symmetric rounds of fw16.hip fw16_build_sym_sharded, distances only: each
-    rank keeps one orientation of every 128-tile pair (sym_kept), the next pivot rows are
-    gathered from their keepers (transposed 64 x 128 slices, sent to the owner), the owner closes
-    the diagonal block and the row panel and broadcasts it, every rank updates its kept tiles
-    with A = P^T and B = P, the next pivot block's tile row / column first; at the end each
-    rank receives the transposes of the tiles it does not keep."""
+    rank keeps one orientation of every 128-tile pair (sym_kept); every rank broadcasts the
+    pivot-panel blocks it holds (its kept row blocks, or transposed 64 x 128 slices of its tiles
+    in the pivot column), every rank closes the diagonal block and the row panel itself and the
+    owner writes them back; every rank updates its kept tiles with A = P^T and B = P, the next
+    pivot block's tile row / column first; at the end each rank receives the transposes of the
+    tiles it does not keep."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=R)
     from shadow_amd._lib import lib
@@ -208,42 +210,35 @@ def _dense_sym_worker(rank, R, port, n, seed, q):
     def kept(I, J):
         return I == J or ((I < J) == ((I + J) % 2 == 0))
 
-    def gathered(K, J):
-        return J != K and not kept(K, J)
-
     def tile(I, J):  # view of this rank's tile (I, J)
         return D[(I - tb) * ALIGN:(I - tb + 1) * ALIGN, J * ALIGN:(J + 1) * ALIGN]
 
     def produce(k0):
+        """P_k from every rank's blocks (one broadcast per contributor, in (contributor, J)
+        order); every rank closes the diagonal block and the row panel itself"""
         K, o = k0 // ALIGN, own[k0 // ALIGN]
-        if rank != o:
-            blocks = [D[(J - tb) * ALIGN:(J - tb + 1) * ALIGN, k0:k0 + KB].T for J in range(tb, te)
-                      if gathered(K, J)]
-            if blocks:
-                dist.send(torch.from_numpy(np.ascontiguousarray(np.concatenate(blocks, axis=1))), o)
-            P = torch.zeros((KB, ld), dtype=torch.int64)
-        else:
-            rows = D[k0 - b:k0 - b + KB]
-            for J in range(tb, te):
-                if gathered(K, J):
-                    rows[:, J * ALIGN:(J + 1) * ALIGN] = D[(J - tb) * ALIGN:(J - tb + 1) * ALIGN,
-                                                           k0:k0 + KB].T
-            for x, (qb, qe) in enumerate(ranges):
-                js = [J for J in range(qb // ALIGN, qe // ALIGN) if gathered(K, J)]
-                if x == rank or not js:
-                    continue
-                buf = torch.zeros((KB, ALIGN * len(js)), dtype=torch.int64)
-                dist.recv(buf, x)
-                for i, J in enumerate(js):
-                    rows[:, J * ALIGN:(J + 1) * ALIGN] = buf[:, i * ALIGN:(i + 1) * ALIGN].numpy()
-            Tk = rows[:, k0:k0 + KB]
-            for m in range(KB):  # diagonal closure
-                Tk = np.minimum(Tk, Tk[:, m:m + 1] + Tk[m:m + 1, :])
-            rows[:, k0:k0 + KB] = Tk
-            rows[:] = np.minimum(rows, _minplus(Tk, rows))  # row panel
-            P = torch.from_numpy(rows.copy())
-        dist.broadcast(P, o)
-        return P.numpy()
+        contrib = [o if kept(K, J) else own[J] for J in range(T)]
+        P = np.zeros((KB, ld), np.int64)
+        for x in range(R):
+            js = [J for J in range(T) if contrib[J] == x]
+            if not js:
+                continue
+            buf = torch.zeros((KB, ALIGN * len(js)), dtype=torch.int64)
+            if x == rank:
+                blocks = [D[k0 - b:k0 - b + KB, J * ALIGN:(J + 1) * ALIGN] if kept(K, J) else
+                          D[(J - tb) * ALIGN:(J - tb + 1) * ALIGN, k0:k0 + KB].T for J in js]
+                buf = torch.from_numpy(np.ascontiguousarray(np.concatenate(blocks, axis=1)))
+            dist.broadcast(buf, x)
+            for i, J in enumerate(js):
+                P[:, J * ALIGN:(J + 1) * ALIGN] = buf[:, i * ALIGN:(i + 1) * ALIGN].numpy()
+        Tk = P[:, k0:k0 + KB]
+        for m in range(KB):  # diagonal closure
+            Tk = np.minimum(Tk, Tk[:, m:m + 1] + Tk[m:m + 1, :])
+        P[:, k0:k0 + KB] = Tk
+        P[:] = np.minimum(P, _minplus(Tk, P))  # row panel
+        if rank == o:
+            D[k0 - b:k0 - b + KB] = P
+        return P
 
     def update(P, tiles):
         for I, J in tiles:
