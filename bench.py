@@ -174,16 +174,21 @@ def run_dense(c: Ctx, wl):
     #   enc 3: 2 x v_add_u32 + 1 x v_pk_minimum3_f16 per 4 relaxations -> 8/4 = 2.0 cycles
     #   enc 2: 1 x v_add_u32 + 1 x v_pk_min_u16 per 2 relaxations      -> 6/2 = 3.0 cycles
     #   enc 1: 2 x v_add_u32 + 1 x v_min3_u32 per 2 relaxations         -> 8/2 = 4.0 cycles
-    cyc_per_relax = {4: 2.0, 3: 2.0, 2: 3.0, 1: 4.0}[enc]
-    instr_per_relax = {4: 0.75, 3: 0.75, 2: 1.0, 1: 1.5}[enc]
-    kname = {4: "fwh_update_kernel<true, 0>" if world == 1 else "fwh_update_kernel<true, 4>",
+    cyc_per_relax = {5: 2.0, 4: 2.0, 3: 2.0, 2: 3.0, 1: 4.0}[enc]
+    instr_per_relax = {5: 0.75, 4: 0.75, 3: 0.75, 2: 1.0, 1: 1.5}[enc]
+    kname = {5: "fwh_update_kernel<true, 4>",
+             4: "fwh_update_kernel<true, 0>" if world == 1 else "fwh_update_kernel<true, 4>",
              3: "fwh_update_kernel<false, 0>",
              2: "fw16_update_kernel<false>", 1: "fw_update_kernel"}[enc]
     # elements a timed launch updates: every local row; (enc 4, one GPU) the upper-triangle 128x128
     # tiles; (enc 4, sharded) this rank's kept tiles (fw16.hip sym_kept: one orientation of each
     # tile pair) less the next pivot block's tile row and column, which run in their own launch
     tiles = ld // 128
-    if enc == 4 and world == 1:
+    if enc == 5:  # one GPU, two update streams: a timed unit is the pair of rest-of-round
+        # launches (first start to last end), all upper-triangle tiles but the next pivot
+        # block's tile row and column (T tiles, their own launches)
+        elems = float(tiles * (tiles + 1) // 2 - tiles) * 128 * 128
+    elif enc == 4 and world == 1:
         elems = float(tiles * (tiles + 1) // 2) * 128 * 128
     elif enc == 4:
         kept = lambda i, j: i == j or ((i < j) == ((i + j) % 2 == 0))
@@ -204,6 +209,8 @@ def run_dense(c: Ctx, wl):
         pmc = json.load(open(pmc_path))
         if pmc.get("kernel") == kname:
             traffic = pmc.get("hbm_bytes_per_launch")
+            if enc == 5 and traffic is not None:  # the timed unit is two launches
+                traffic = 2.0 * traffic
     roofline = {
         # the north-star metric is GB/s vs HBM peak; the kernel itself is VALU-issue bound (min-plus
         # has no MFMA form), so the binding roof is reported beside it under "valu"
@@ -213,7 +220,7 @@ def run_dense(c: Ctx, wl):
         "traffic": traffic, "bytes_per_launch": bytes_per_round,
         "avg_launch_ms": round(avg_upd_ms, 4), "launches_timed": n_upd,
         "model": f"2*elements*{s_d} B per round (SURVEY §8d round-streaming, B=64, "
-                 f"{ {4: 'u16 f16-compare, upper triangle', 3: 'u16 f16-compare', 2: 'u16 pk_min', 1: 'u32'}[enc]}"
+                 f"{ {5: 'u16 f16-compare, upper triangle on two streams (unit: both rest launches)', 4: 'u16 f16-compare, upper triangle', 3: 'u16 f16-compare', 2: 'u16 pk_min', 1: 'u32'}[enc]}"
                  f" distances; elements updated per round = {int(elems)})",
         "algorithmic_min_bytes": float(nr) * ld * (4 + 8),
         "valu": {"achieved": round(relax_t, 2), "peak": round(relax_peak_t, 1),

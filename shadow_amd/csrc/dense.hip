@@ -1152,14 +1152,23 @@ extern "C" int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, c
     /* narrowest exact encoding first: f16-compare u16 -> pk_min u16 -> u32 */
     int exact = 0, enc = SRT_DENC_U32;
     for (int fm = 1; fm >= 0 && !exact && ld % 128 == 0; --fm) {
-        if (evp) evp->used = 0;
+        if (evp) {
+            evp->used = 0;
+            evp->group = 2;
+        }
         int sym = !directed;
         rc = srt_fw16_build(n, ld, 0, ld, w, lat, st, evp, NULL, NULL, NULL, 0, fm, &sym, &exact);
         if (rc) return rc;
-        if (exact) enc = fm ? (sym ? SRT_DENC_F16CMP_SYM : SRT_DENC_F16CMP) : SRT_DENC_U16;
+        if (exact)
+            enc = !fm ? SRT_DENC_U16
+                      : sym == 2 ? SRT_DENC_F16CMP_SYM2
+                                 : sym ? SRT_DENC_F16CMP_SYM : SRT_DENC_F16CMP;
     }
     if (!exact) { /* u32 path: ld not a multiple of 128, or a distance reached 0x7FFF quanta */
-        if (evp) evp->used = 0;
+        if (evp) {
+            evp->used = 0;
+            evp->group = 2;
+        }
         dim3 g(srt_ceil_div(ld, 256), ld);
         init_dist_kernel<<<g, 256, 0, st>>>(n, ld, 0, w, lat);
         SRT_HIPCHK(hipGetLastError());
@@ -1364,7 +1373,10 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
     const char* sym_env = getenv("SRT_FW_SYM");
     const bool sym = !directed && R > 1 && !(sym_env && atoi(sym_env) == 0);
     for (int fm = 1; fm >= 0 && !exact; --fm) {
-        if (evp) evp->used = 0;
+        if (evp) {
+            evp->used = 0;
+            evp->group = 2;
+        }
         if (fm && sym) /* undirected: each rank updates half of its row block (fw16.hip) */
             rc = srt_fw16_build_sym_sharded(comm, n, ld, b, nr, w_rows, lat_rows, st, evp, &exact);
         else
@@ -1381,7 +1393,10 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
         if (exact) enc = fm ? (sym ? SRT_DENC_F16CMP_SYM : SRT_DENC_F16CMP) : SRT_DENC_U16;
     }
     if (!exact) {
-        if (evp) evp->used = 0;
+        if (evp) {
+            evp->used = 0;
+            evp->group = 2;
+        }
         if (nr > 0) {
             dim3 g(srt_ceil_div(ld, 256), nr);
             init_dist_kernel<<<g, 256, 0, st>>>(n, ld, b, w_rows, lat_rows);

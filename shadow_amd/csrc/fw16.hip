@@ -536,7 +536,9 @@ static __host__ __device__ __forceinline__ bool sym_kept(int I, int J) {
  * XM (row-sharded SYM, D = the rank's rows from tile row i0 = tb, te = end tile row, skip = the
  * tile row K1 of the next pivot block or -1): 3 = the kept tiles of tile row K1 (block b < T: J =
  * b) and of tile column K1 in the rank's rows (b >= T: I = tb + b - T), which the next pivot
- * panel is assembled from; 4 = the rank's kept-tile list tl minus those; 5 = the whole list. */
+ * panel is assembled from; 4 = the rank's kept-tile list tl minus those; 5 = the whole list;
+ * 6 = (one GPU, two update streams) the upper-triangle tiles of tile row / column K1 whose
+ * I + J has the parity i0. */
 template <bool SYM, int XM = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void fwh_update_kernel(
     u16* __restrict__ D, int ld, const u16* __restrict__ P, int k0, int ncol_tiles, int i0, int skip,
@@ -559,6 +561,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             if (I >= te || I == skip || !sym_kept(I, J)) return;
         }
         Iloc = I - i0;
+    } else if (XM == 6) { /* one GPU, upper triangle: the cross of K1 restricted to I + J = i0 mod 2 */
+        I = min((int)blockIdx.x, skip);
+        J = max((int)blockIdx.x, skip);
+        if (((I + J) & 1) != i0) return;
+        Iloc = I;
     } else if (XM == 4 || XM == 5) {
         const uint32_t t = tl[bid];
         I = (int)(t >> 16);
@@ -754,6 +761,11 @@ const uint16_t* srt_fw16_matrix(void) { return fw16_bufs[srt_state_slot()]; }
 typedef struct {
     hipStream_t cs;
     hipEvent_t ready[2], row_done, upd_done[2], init_done;
+    /* one-GPU symmetric rounds on two update streams (st, xs) */
+    hipStream_t xs;
+    hipEvent_t e_set[2][2]; /* [round & 1][tile set]: the set's next-row tiles are done */
+    uint32_t* tl2;
+    size_t tl2_cap;
     int ok;
 } fw16_sched;
 
@@ -770,6 +782,9 @@ static int sched_get(fw16_sched** out, int dev) {
         }
         SRT_HIPCHK(hipEventCreateWithFlags(&x->row_done, hipEventDisableTiming));
         SRT_HIPCHK(hipEventCreateWithFlags(&x->init_done, hipEventDisableTiming));
+        SRT_HIPCHK(hipStreamCreateWithFlags(&x->xs, hipStreamNonBlocking));
+        for (int i = 0; i < 4; ++i)
+            SRT_HIPCHK(hipEventCreateWithFlags(&x->e_set[i / 2][i % 2], hipEventDisableTiming));
         x->ok = 1;
     }
     *out = x;
@@ -777,8 +792,17 @@ static int sched_get(fw16_sched** out, int dev) {
 }
 
 /* Upper-triangle blocked FW for an undirected graph on one GPU (f16-compare kernels). */
+/* Upper-triangle blocked FW for an undirected graph on one GPU (f16-compare kernels).
+ * two: the upper-triangle tiles are split by the parity of I + J into two static sets, each
+ * updated by its own stream (st, xs) every round, while the high-priority stream cs closes the
+ * next diagonal block, builds the next panel and refreshes it as soon as both streams have
+ * updated their tiles of the next pivot block's tile row and column (launched first). A stream
+ * depends only on its own previous launches and on the panel, so one stream's next round starts
+ * in the other's tail and the panel work overlaps the update. A stream may then read pivot rows
+ * that the other stream has already relaxed in the next round: those values are still lengths
+ * of real paths, no larger than the round requires, so the result is the same exact matrix. */
 static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipStream_t st,
-                          evpool_t* evp, int* exact) {
+                          evpool_t* evp, int* exact, bool two) {
     const int dev = srt_state_slot(); /* the device, or this virtual rank's slot */
     size_t* caps = fw16_caps;
     int** flags = fw16_flags;
@@ -796,15 +820,98 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
     SRT_HIPCHK(hipGetLastError());
     const int nb = ld / KB, T = ld / 128;
     const int ntri = T * (T + 1) / 2;
-    for (int k0 = 0; k0 < ld; k0 += KB) {
-        u16* P = d + (size_t)k0 * ld;
-        fw16_diag_kernel<<<1, 256, 0, st>>>(P, ld, k0);
-        fw16_panel_kernel<true, true><<<2 * nb, 256, 0, st>>>(d, ld, 0, nb, P, k0, nb, 1, 1);
-        if (k0 > 0) fw16_refresh_kernel<<<k0 / KB, 256, 0, st>>>(d, ld, k0);
-        if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
-        fwh_update_kernel<true><<<ntri, 256, 0, st>>>(d, ld, P, k0, T, 0, -1, nullptr, 0);
-        if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
-        SRT_HIPCHK(hipGetLastError());
+    if (!two) {
+        for (int k0 = 0; k0 < ld; k0 += KB) {
+            u16* P = d + (size_t)k0 * ld;
+            fw16_diag_kernel<<<1, 256, 0, st>>>(P, ld, k0);
+            fw16_panel_kernel<true, true><<<2 * nb, 256, 0, st>>>(d, ld, 0, nb, P, k0, nb, 1, 1);
+            if (k0 > 0) fw16_refresh_kernel<<<k0 / KB, 256, 0, st>>>(d, ld, k0);
+            if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
+            fwh_update_kernel<true><<<ntri, 256, 0, st>>>(d, ld, P, k0, T, 0, -1, nullptr, 0);
+            if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
+            SRT_HIPCHK(hipGetLastError());
+        }
+    } else {
+        fw16_sched* sc;
+        int rc = sched_get(&sc, dev);
+        if (rc) return rc;
+        hipStream_t cs = sc->cs, xs = sc->xs;
+        /* the two tile sets, row-major, as device lists */
+        uint32_t* h = (uint32_t*)malloc((size_t)ntri * sizeof(uint32_t));
+        if (!h) return SRT_E_NOMEM;
+        int nset[2] = {0, 0};
+        for (int p = 0, o = 0; p < 2; p++)
+            for (int I = 0; I < T; I++)
+                for (int J = I; J < T; J++)
+                    if (((I + J) & 1) == p) {
+                        h[o++] = ((uint32_t)I << 16) | (uint32_t)J;
+                        nset[p]++;
+                    }
+        if (!sc->tl2 || sc->tl2_cap < (size_t)ntri) {
+            if (sc->tl2) SRT_HIPCHK(hipFree(sc->tl2));
+            sc->tl2 = NULL;
+            SRT_HIPCHK(hipMalloc(&sc->tl2, (size_t)ntri * sizeof(uint32_t)));
+            sc->tl2_cap = (size_t)ntri;
+        }
+        const hipError_t ce = hipMemcpyAsync(sc->tl2, h, (size_t)ntri * sizeof(uint32_t),
+                                             hipMemcpyHostToDevice, st);
+        const hipError_t se = ce == hipSuccess ? hipStreamSynchronize(st) : ce;
+        free(h);
+        SRT_HIPCHK(se);
+        const uint32_t* tls[2] = {sc->tl2, sc->tl2 + nset[0]};
+        hipStream_t ss[2] = {st, xs};
+        auto produce = [&](int k) -> int {
+            const int k0 = k * KB;
+            u16* P = d + (size_t)k0 * ld;
+            fw16_diag_kernel<<<1, 256, 0, cs>>>(P, ld, k0);
+            fw16_panel_kernel<true, true><<<2 * nb, 256, 0, cs>>>(d, ld, 0, nb, P, k0, nb, 1, 1);
+            if (k0 > 0) fw16_refresh_kernel<<<k0 / KB, 256, 0, cs>>>(d, ld, k0);
+            SRT_HIPCHK(hipGetLastError());
+            SRT_HIPCHK(hipEventRecord(sc->ready[k & 1], cs));
+            return SRT_OK;
+        };
+        SRT_HIPCHK(hipEventRecord(sc->init_done, st));
+        SRT_HIPCHK(hipStreamWaitEvent(cs, sc->init_done, 0));
+        SRT_HIPCHK(hipStreamWaitEvent(xs, sc->init_done, 0));
+        if ((rc = produce(0))) return rc;
+        for (int k = 0; k < nb; ++k) {
+            const int k0 = k * KB;
+            u16* P = d + (size_t)k0 * ld;
+            const bool next = k + 1 < nb;
+            const int K1 = next ? ((k + 1) * KB) / 128 : -1;
+            for (int p = 0; p < 2; p++) {
+                SRT_HIPCHK(hipStreamWaitEvent(ss[p], sc->ready[k & 1], 0));
+                if (next) {
+                    fwh_update_kernel<true, 6><<<T, 256, 0, ss[p]>>>(d, ld, P, k0, T, p, K1, nullptr, 0);
+                    SRT_HIPCHK(hipEventRecord(sc->e_set[k & 1][p], ss[p]));
+                }
+            }
+            if (next) {
+                SRT_HIPCHK(hipStreamWaitEvent(cs, sc->e_set[k & 1][0], 0));
+                SRT_HIPCHK(hipStreamWaitEvent(cs, sc->e_set[k & 1][1], 0));
+                if ((rc = produce(k + 1))) return rc;
+            }
+            /* timed as one unit: the two rest-of-round launches, from the first start to the
+             * last end (evpool group 4: start A, start B, end A, end B) */
+            const int e0 = evp ? evp->used : 0;
+            if (evp && next) {
+                evp->group = 4;
+                evp->used += 4;
+            }
+            for (int p = 0; p < 2; p++) {
+                if (evp && next) SRT_HIPCHK(hipEventRecord(evp->ev[e0 + p], ss[p]));
+                if (next)
+                    fwh_update_kernel<true, 4><<<(unsigned)nset[p], 256, 0, ss[p]>>>(
+                        d, ld, P, k0, T, 0, K1, tls[p], T);
+                else
+                    fwh_update_kernel<true, 5><<<(unsigned)nset[p], 256, 0, ss[p]>>>(
+                        d, ld, P, k0, T, 0, -1, tls[p], T);
+                if (evp && next) SRT_HIPCHK(hipEventRecord(evp->ev[e0 + 2 + p], ss[p]));
+            }
+            SRT_HIPCHK(hipGetLastError());
+        }
+        SRT_HIPCHK(hipEventRecord(sc->row_done, xs));
+        SRT_HIPCHK(hipStreamWaitEvent(st, sc->row_done, 0));
     }
     fw16_mirror_kernel<<<dim3(nb, nb), 256, 0, st>>>(d, ld);
     SRT_HIPCHK(hipMemsetAsync(flags[dev], 0, 2 * sizeof(int), st));
@@ -1144,9 +1251,12 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
     const char* sym_env = getenv("SRT_FW_SYM");
     const bool want_sym = sym && *sym && !(sym_env && atoi(sym_env) == 0);
     if (sym) *sym = 0;
-    if (want_sym && fm && !lookahead && !bcast && !owner_of && row0 == 0 && nrows == ld) {
-        *sym = 1;
-        return fw16_build_sym(n, ld, w_rows, lat_rows, st, evp, exact);
+    if (want_sym && fm && !bcast && !owner_of && row0 == 0 && nrows == ld) {
+        /* two update streams once the rounds are long enough to hide their event waits;
+         * SRT_FW_LOOKAHEAD=0/1 forces either form */
+        const bool two = la_env ? atoi(la_env) != 0 : ld >= 8192;
+        *sym = two ? 2 : 1;
+        return fw16_build_sym(n, ld, w_rows, lat_rows, st, evp, exact, two);
     }
     hipStream_t cs = lookahead ? sc->cs : st;
     u16* d = bufs[dev];

@@ -70,6 +70,10 @@ static inline int srt_ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) 
 typedef struct {
     hipEvent_t* ev;
     int cap, used;
+    /* 2: (start, end) per timed launch; 4: (start A, start B, end A, end B) per round for the
+     * launch pairs of two update streams, which drift apart and overlap across rounds: the unit's
+     * time is their period, (last end - first start) / pairs */
+    int group;
 } evpool_t;
 
 evpool_t* srt_evpool(int dev);
@@ -77,14 +81,15 @@ evpool_t* srt_evpool(int dev);
 
 static inline int evpool_begin(evpool_t** out, int rounds) {
     evpool_t* p = srt_evpool(srt_state_slot());
-    if (p->cap < 2 * rounds) {
-        hipEvent_t* ne = (hipEvent_t*)realloc(p->ev, sizeof(hipEvent_t) * 2 * rounds);
+    if (p->cap < 4 * rounds) {
+        hipEvent_t* ne = (hipEvent_t*)realloc(p->ev, sizeof(hipEvent_t) * 4 * rounds);
         if (!ne) return SRT_E_NOMEM;
         p->ev = ne;
-        for (int i = p->cap; i < 2 * rounds; i++) SRT_HIPCHK(hipEventCreate(&p->ev[i]));
-        p->cap = 2 * rounds;
+        for (int i = p->cap; i < 4 * rounds; i++) SRT_HIPCHK(hipEventCreate(&p->ev[i]));
+        p->cap = 4 * rounds;
     }
     p->used = 0;
+    p->group = 2;
     *out = p;
     return SRT_OK;
 }
@@ -92,13 +97,23 @@ static inline int evpool_begin(evpool_t** out, int rounds) {
 static inline int evpool_sum(evpool_t* p, hipEvent_t last, srt_build_stats* stats) {
     SRT_HIPCHK(hipEventSynchronize(last));
     double tot = 0;
-    for (int i = 0; i + 1 < p->used; i += 2) {
-        float ms = 0;
-        SRT_HIPCHK(hipEventElapsedTime(&ms, p->ev[i], p->ev[i + 1]));
-        tot += ms;
+    const int g = p->group == 4 ? 4 : 2;
+    if (g == 2) {
+        for (int i = 0; i + 1 < p->used; i += 2) {
+            float ms = 0;
+            SRT_HIPCHK(hipEventElapsedTime(&ms, p->ev[i], p->ev[i + 1]));
+            tot += ms;
+        }
+    } else if (p->used >= 4) { /* relative to the first start A */
+        const int l = p->used - 4;
+        float sb = 0, ea = 0, eb = 0;
+        SRT_HIPCHK(hipEventElapsedTime(&sb, p->ev[0], p->ev[1]));
+        SRT_HIPCHK(hipEventElapsedTime(&ea, p->ev[0], p->ev[l + 2]));
+        SRT_HIPCHK(hipEventElapsedTime(&eb, p->ev[0], p->ev[l + 3]));
+        tot = (ea > eb ? ea : eb) - (sb < 0 ? sb : 0);
     }
     stats->ms_update = tot;
-    stats->n_update = p->used / 2;
+    stats->n_update = p->used / g;
     return SRT_OK;
 }
 
@@ -123,7 +138,13 @@ const uint16_t* srt_fw16_matrix(void);
 /* 1 when every real distance of that build is <= 254 quanta (the post pass then reads u8) */
 int srt_fw16_small(void);
 /* distance encodings of the dense build, reported (negated) in srt_build_stats.fw_block */
-enum { SRT_DENC_U32 = 1, SRT_DENC_U16 = 2, SRT_DENC_F16CMP = 3, SRT_DENC_F16CMP_SYM = 4 };
+enum {
+    SRT_DENC_U32 = 1,
+    SRT_DENC_U16 = 2,
+    SRT_DENC_F16CMP = 3,
+    SRT_DENC_F16CMP_SYM = 4,
+    SRT_DENC_F16CMP_SYM2 = 5 /* one GPU, upper triangle on two update streams */
+};
 
 int srt_dense_post_device(int32_t n, int32_t ld, int32_t directed, const uint32_t* w,
                           const double* r, uint32_t* d, const uint16_t* d16, double* rel,

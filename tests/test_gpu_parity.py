@@ -188,8 +188,9 @@ def test_dense_device_api_and_sharded_single_rank(gpu):
     assert torch.equal(lat2[:n, :n], lat[:n, :n]) and torch.equal(rel2[:n, :n], rel[:n, :n])
 
 
-@pytest.mark.parametrize("hop_ms,enc,sym", [(1, 4, "1"), (1, 3, "0"), (160, 2, "1"), (400, 1, "1")])
-def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym):
+@pytest.mark.parametrize("hop_ms,enc,sym,la", [(1, 4, "1", None), (1, 5, "1", "1"), (1, 3, "0", None),
+                                               (160, 2, "1", None), (400, 1, "1", None)])
+def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym, la):
     """Each distance encoding of the dense build (fw16.hip) is exact where it is chosen.
 
     A 256-vertex ring with hop latencies hop_ms / hop_ms+1 (gcd 1 ms) plus a few chords: the
@@ -197,9 +198,12 @@ def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym):
     0x3DFF), 160 saturates it and falls back to the u16 pk_min path (cap 0x7FFF), and 400
     saturates both and ends on the u32 kernels. Every tier must match the oracle bit for bit.
     The graph is undirected, so the f16-compare tier runs its upper-triangle form (encoding 4)
-    unless SRT_FW_SYM=0 forces every tile (encoding 3).
+    unless SRT_FW_SYM=0 forces every tile (encoding 3); SRT_FW_LOOKAHEAD=1 forces its two
+    update streams (encoding 5, the default from n = 8192).
     """
     monkeypatch.setenv("SRT_FW_SYM", sym)
+    if la is not None:
+        monkeypatch.setenv("SRT_FW_LOOKAHEAD", la)
     n = 256
     rng = np.random.default_rng(hop_ms)
     src = list(range(n))
@@ -222,9 +226,11 @@ def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym):
 
 @pytest.mark.parametrize("n,seed", [(700, 8), (1000, 2)])
 def test_dense_lookahead_schedule_one_gpu(gpu, monkeypatch, n, seed):
-    """The two-stream lookahead schedule of the sharded FW (fw16.hip srt_fw16_build: split update,
-    pivot panel k+1 on the high-priority stream, double-buffered receive panels) forced on one GPU
-    must give the oracle's tables, through both the single-GPU and the 1-rank sharded entry."""
+    """The lookahead schedules forced on one GPU must give the oracle's tables: through the
+    single-GPU entry the symmetric rounds on two update streams (fw16_build_sym: static tile
+    sets by I + J parity, next diagonal / panel / refresh on the high-priority stream), through
+    the 1-rank sharded entry the sharded FW's two-stream schedule (split update, pivot panel k+1
+    on the high-priority stream, double-buffered receive panels)."""
     import torch
     from shadow_amd._lib import lib
     monkeypatch.setenv("SRT_FW_LOOKAHEAD", "1")

@@ -58,7 +58,7 @@ float run_fwh(u16* D, int ld, int rounds) {
     hipEventRecord(a);
     for (int k = 0; k < rounds; ++k) {
         const int k0 = (k * 64) % ld;
-        fwh_update_kernel<false><<<grid, 256>>>(D, ld, D + (size_t)k0 * ld, k0, nct, 0, -1);
+        fwh_update_kernel<false><<<grid, 256>>>(D, ld, D + (size_t)k0 * ld, k0, nct, 0, -1, nullptr, 0);
     }
     hipEventRecord(b); hipEventSynchronize(b);
     float ms; hipEventElapsedTime(&ms, a, b);
