@@ -538,7 +538,8 @@ static __host__ __device__ __forceinline__ bool sym_kept(int I, int J) {
  * b) and of tile column K1 in the rank's rows (b >= T: I = tb + b - T), which the next pivot
  * panel is assembled from; 4 = the rank's kept-tile list tl minus those; 5 = the whole list;
  * 6 = (one GPU, two update streams) the upper-triangle tiles of tile row / column K1 whose
- * I + J has the parity i0. */
+ * I + J has the parity i0; 7 / 8 = mode 3 restricted to even / odd J (the sharded rounds' two
+ * update streams). */
 template <bool SYM, int XM = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void fwh_update_kernel(
     u16* __restrict__ D, int ld, const u16* __restrict__ P, int k0, int ncol_tiles, int i0, int skip,
@@ -550,7 +551,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const int per = nb >> 3;
     const int bid = (nb & 7) == 0 ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
     int I, J, Iloc;
-    if (XM == 3) {
+    if (XM == 3 || XM == 7 || XM == 8) {
         if (blockIdx.x < ncol_tiles) {
             J = blockIdx.x;
             I = skip;
@@ -560,6 +561,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             J = skip;
             if (I >= te || I == skip || !sym_kept(I, J)) return;
         }
+        if (XM != 3 && (J & 1) != XM - 7) return; /* two update streams: tile set J mod 2 */
         Iloc = I - i0;
     } else if (XM == 6) { /* one GPU, upper triangle: the cross of K1 restricted to I + J = i0 mod 2 */
         I = min((int)blockIdx.x, skip);
@@ -764,6 +766,7 @@ typedef struct {
     /* one-GPU symmetric rounds on two update streams (st, xs) */
     hipStream_t xs;
     hipEvent_t e_set[2][2]; /* [round & 1][tile set]: the set's next-row tiles are done */
+    hipEvent_t xs_done[2];  /* sharded symmetric rounds: stream xs finished round k's update */
     uint32_t* tl2;
     size_t tl2_cap;
     int ok;
@@ -785,6 +788,8 @@ static int sched_get(fw16_sched** out, int dev) {
         SRT_HIPCHK(hipStreamCreateWithFlags(&x->xs, hipStreamNonBlocking));
         for (int i = 0; i < 4; ++i)
             SRT_HIPCHK(hipEventCreateWithFlags(&x->e_set[i / 2][i % 2], hipEventDisableTiming));
+        for (int i = 0; i < 2; ++i)
+            SRT_HIPCHK(hipEventCreateWithFlags(&x->xs_done[i], hipEventDisableTiming));
         x->ok = 1;
     }
     *out = x;
@@ -984,10 +989,15 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
         qte[q] = qe / 128;
         for (int K = qtb[q]; K < qte[q] && K < T; K++) own[K] = q;
     }
-    size_t nkept = 0;
-    for (int I = tb; I < te; I++)
-        for (int J = 0; J < T; J++)
-            if (sym_kept(I, J)) hkept[nkept++] = ((uint32_t)I << 16) | (uint32_t)J;
+    /* kept tiles, even J first, then odd J: the lists of the two update streams */
+    size_t nkept = 0, nset[2] = {0, 0};
+    for (int p = 0; p < 2; p++)
+        for (int I = tb; I < te; I++)
+            for (int J = p; J < T; J += 2)
+                if (sym_kept(I, J)) {
+                    hkept[nkept++] = ((uint32_t)I << 16) | (uint32_t)J;
+                    nset[p]++;
+                }
     /* device scratch: kept-tile list, gather send (this rank's rows) and receive (a panel) */
     uint32_t* tl = NULL;
     int* down = NULL; /* owner of each tile row, on the device */
@@ -1042,7 +1052,10 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
         auto produce = [&](int k) -> int {
             const int k0 = k * KB, K = k0 / 128, o = own[K];
             u16* P = pbuf[k & 1];
-            if (k >= 2) SRT_HIPCHK(hipStreamWaitEvent(cs, sc->upd_done[k & 1], 0)); /* k-2 read P */
+            if (k >= 2) { /* both streams' round k-2 read P */
+                SRT_HIPCHK(hipStreamWaitEvent(cs, sc->upd_done[k & 1], 0));
+                SRT_HIPCHK(hipStreamWaitEvent(cs, sc->xs_done[k & 1], 0));
+            }
             for (int q = 0; q < R; q++) cnt[q] = 0;
             for (int J = 0; J < T; J++) cnt[sym_kept(K, J) ? o : own[J]]++;
             if (cnt[me])
@@ -1068,32 +1081,55 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
             return SRT_OK;
         };
         if ((rc = produce(0))) goto out;
+        /* two update streams (st: even J, xs: odd J), as on one GPU (fw16_build_sym): each
+         * depends on its own launches and the panel, so their rounds overlap */
+        hipStream_t ss[2] = {st, sc->xs};
+        const uint32_t* tls[2] = {tl, tl + nset[0]};
+        SYM_HIP(hipStreamWaitEvent(sc->xs, sc->init_done, 0));
         for (int k = 0; k < nb; ++k) {
             const int k0 = k * KB;
             u16* P = panel_of(k);
-            SYM_HIP(hipStreamWaitEvent(st, sc->ready[k & 1], 0));
             const bool next = k + 1 < nb;
             const int K1 = next ? (k + 1) * KB / 128 : -1;
+            for (int p = 0; p < 2; p++) {
+                SYM_HIP(hipStreamWaitEvent(ss[p], sc->ready[k & 1], 0));
+                if (!next) continue;
+                if (p == 0)
+                    fwh_update_kernel<true, 7><<<T + (te - tb), 256, 0, ss[p]>>>(d, ld, P, k0, T, tb,
+                                                                                 K1, nullptr, te);
+                else
+                    fwh_update_kernel<true, 8><<<T + (te - tb), 256, 0, ss[p]>>>(d, ld, P, k0, T, tb,
+                                                                                 K1, nullptr, te);
+                SYM_HIP(hipEventRecord(sc->e_set[k & 1][p], ss[p]));
+            }
             if (next) {
-                fwh_update_kernel<true, 3><<<T + (te - tb), 256, 0, st>>>(d, ld, P, k0, T, tb, K1,
-                                                                          nullptr, te);
-                SYM_HIP(hipEventRecord(sc->row_done, st));
-                SYM_HIP(hipStreamWaitEvent(cs, sc->row_done, 0));
+                SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[k & 1][0], 0));
+                SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[k & 1][1], 0));
                 if ((rc = produce(k + 1))) goto out;
             }
-            if (evp && next) SYM_HIP(hipEventRecord(evp->ev[evp->used++], st));
-            if (nkept) {
-                if (next)
-                    fwh_update_kernel<true, 4><<<(unsigned)nkept, 256, 0, st>>>(d, ld, P, k0, T, tb,
-                                                                               K1, tl, te);
-                else
-                    fwh_update_kernel<true, 5><<<(unsigned)nkept, 256, 0, st>>>(d, ld, P, k0, T, tb,
-                                                                               -1, tl, te);
+            /* timed as one unit per round: the two rest launches (evpool group 4) */
+            const int e0 = evp ? evp->used : 0;
+            if (evp && next) {
+                evp->group = 4;
+                evp->used += 4;
             }
-            if (evp && next) SYM_HIP(hipEventRecord(evp->ev[evp->used++], st));
+            for (int p = 0; p < 2; p++) {
+                if (evp && next) SYM_HIP(hipEventRecord(evp->ev[e0 + p], ss[p]));
+                if (nset[p]) {
+                    if (next)
+                        fwh_update_kernel<true, 4><<<(unsigned)nset[p], 256, 0, ss[p]>>>(
+                            d, ld, P, k0, T, tb, K1, tls[p], te);
+                    else
+                        fwh_update_kernel<true, 5><<<(unsigned)nset[p], 256, 0, ss[p]>>>(
+                            d, ld, P, k0, T, tb, -1, tls[p], te);
+                }
+                if (evp && next) SYM_HIP(hipEventRecord(evp->ev[e0 + 2 + p], ss[p]));
+            }
             SYM_HIP(hipGetLastError());
             SYM_HIP(hipEventRecord(sc->upd_done[k & 1], st));
+            SYM_HIP(hipEventRecord(sc->xs_done[k & 1], sc->xs));
         }
+        SYM_HIP(hipStreamWaitEvent(st, sc->xs_done[(nb - 1) & 1], 0));
         /* fill the tiles this rank does not keep: transposes from their keepers */
         {
             size_t nloc = 0;
