@@ -74,7 +74,9 @@ typedef struct srt_build_stats {
     int32_t n_update;    /* FW update-kernel launches timed (time_kernels = 1) */
     double ms_update;    /* summed HIP-event duration of those launches */
     double ms_comm;      /* host-observed time of the collective calls (sharded builds) */
-    int32_t dist_enc;    /* distance encoding the dense build finished with: 5 = 4 on two
+    int32_t dist_enc;    /* sparse builds: 2 = workgroup-per-source kernel (LDS-packed rows),
+                          * 1 = wave-per-source kernel, 0 = workgroup kernel for every source.
+                          * Dense: the distance encoding the build finished with: 5 = 4 on two
                           * update streams (one GPU, n >= 8192), 4 = u16 with
                           * f16-compare mins, upper-triangle rounds (undirected, one shard),
                           * 3 = u16 f16-compare (cap 0x3DFF), 2 = u16 pk_min (cap 0x7FFF), 1 = u32 */

@@ -126,6 +126,10 @@ struct srt_sparse_graph {
     double *r2, *ir2;
 };
 
+int srt_wgsssp_max_n(void);
+int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r, const int32_t* inv,
+                    uint32_t max_w, int src_begin, int src_end, uint32_t* lat, double* rel,
+                    int* ovf, hipStream_t st);
 int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, const double* r,
                    const int2* in_rowptr, const uint2* in_cw, const double* in_r,
                    const int32_t* perm, const int32_t* inv, uint32_t max_w, int local,
@@ -376,10 +380,39 @@ extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begi
     SRT_HIPCHK(hipEventCreate(&e1));
     SRT_HIPCHK(hipEventCreate(&e2));
     SRT_HIPCHK(hipEventRecord(e0, st));
-    int rc = srt_wsssp_rows(g->n, g->directed, g->rp2, g->cw2, g->r2, g->irp2, g->icw2, g->ir2,
+    /* large power-law graphs (relabelled arcs far apart): the workgroup kernel with the distance
+     * row packed in LDS, once a probe source shows every distance fits its 10-bit fields
+     * (d(a, b) <= 2 ecc(s0)); SRT_SPARSE_WG=0/1 disables / allows it at any size */
+    const char* genv = getenv("SRT_SPARSE_WG");
+    bool wg = !g->directed && g->n <= srt_wgsssp_max_n() &&
+              (genv ? atoi(genv) != 0 : (g->n > 32768 && !g->local));
+    int rc = SRT_OK;
+    if (wg) {
+        rc = srt_wgsssp_rows(g->n, g->rp2, g->cw2, g->r2, g->inv, g->max_w, src_begin,
+                             src_begin + 1, lat_rows, rel_rows, ovf, st);
+        if (rc) return rc;
+        uint32_t* row = (uint32_t*)malloc((size_t)g->n * sizeof(uint32_t));
+        int pov = 1;
+        if (!row) return SRT_E_NOMEM;
+        SRT_HIPCHK(hipMemcpyAsync(row, lat_rows, (size_t)g->n * sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipMemcpyAsync(&pov, ovf, sizeof(int), hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipStreamSynchronize(st));
+        uint32_t ecc = 0;
+        for (int32_t i = 0; i < g->n; i++)
+            if (row[i] != SRT_INF && row[i] > ecc) ecc = row[i];
+        free(row);
+        wg = !pov && 2ull * ecc <= 1022ull;
+        if (wg && nsrc > 1)
+            rc = srt_wgsssp_rows(g->n, g->rp2, g->cw2, g->r2, g->inv, g->max_w, src_begin + 1,
+                                 src_end, lat_rows + (size_t)g->n, rel_rows + (size_t)g->n, ovf + 1,
+                                 st);
+        if (rc) return rc;
+    }
+    if (!wg)
+        rc = srt_wsssp_rows(g->n, g->directed, g->rp2, g->cw2, g->r2, g->irp2, g->icw2, g->ir2,
                             g->perm, g->inv, g->max_w, g->local, src_begin, src_end, lat_rows,
-                            rel_rows, ovf,
-                            st);
+                            rel_rows, ovf, st);
     if (rc) return rc;
     SRT_HIPCHK(hipEventRecord(e1, st));
     rc = srt_sparse_diag(g->n, src_begin, src_end, g->rp, g->col, g->w, g->r, g->sw, g->sr,
@@ -391,14 +424,34 @@ extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begi
     SRT_HIPCHK(hipFreeAsync(ovf, st));
     SRT_HIPCHK(hipStreamSynchronize(st));
     int nov = 0;
+    int* ovf1 = NULL;
     for (int i = 0; i < nsrc && !rc; i++) {
         if (!hov[i]) continue;
         ++nov;
-        rc = srt_sparse_build_device(g->n, g->directed, g->rp, g->col, g->w, g->r, g->irp, g->icol,
-                                     g->iw, g->ir, g->sw, g->sr, src_begin + i, src_begin + i + 1,
-                                     g->delta, lat_rows + (size_t)i * g->n,
-                                     rel_rows + (size_t)i * g->n, stream, NULL);
+        int again = 1;
+        if (wg) { /* the workgroup kernel's overflow: the wave kernel first */
+            if (!ovf1) SRT_HIPCHK(hipMalloc((void**)&ovf1, sizeof(int)));
+            rc = srt_wsssp_rows(g->n, g->directed, g->rp2, g->cw2, g->r2, g->irp2, g->icw2, g->ir2,
+                                g->perm, g->inv, g->max_w, g->local, src_begin + i,
+                                src_begin + i + 1, lat_rows + (size_t)i * g->n,
+                                rel_rows + (size_t)i * g->n, ovf1, st);
+            if (!rc && hipMemcpyAsync(&again, ovf1, sizeof(int), hipMemcpyDeviceToHost, st) ==
+                           hipSuccess &&
+                hipStreamSynchronize(st) != hipSuccess)
+                rc = SRT_E_DEVICE;
+            if (!rc && !again) /* the wave kernel wrote the row; the diagonal rule again */
+                rc = srt_sparse_diag(g->n, src_begin + i, src_begin + i + 1, g->rp, g->col, g->w,
+                                     g->r, g->sw, g->sr, lat_rows + (size_t)i * g->n,
+                                     rel_rows + (size_t)i * g->n, (size_t)g->n, st);
+        }
+        if (!rc && again)
+            rc = srt_sparse_build_device(g->n, g->directed, g->rp, g->col, g->w, g->r, g->irp,
+                                         g->icol, g->iw, g->ir, g->sw, g->sr, src_begin + i,
+                                         src_begin + i + 1, g->delta,
+                                         lat_rows + (size_t)i * g->n, rel_rows + (size_t)i * g->n,
+                                         stream, NULL);
     }
+    if (ovf1) (void)hipFree(ovf1);
     free(hov);
     if (rc) return rc;
     SRT_HIPCHK(hipEventRecord(e2, st));
@@ -418,6 +471,7 @@ extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begi
         stats->n_update = 1;
         stats->ms_update = a;
         stats->ess_arcs = nov; /* sparse builds: sources recomputed after a bucket overflow */
+        stats->dist_enc = wg ? 2 : 1; /* sparse builds: 2 = workgroup kernel, 1 = wave kernel */
     }
     return SRT_OK;
 }

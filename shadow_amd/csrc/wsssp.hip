@@ -378,3 +378,246 @@ int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, con
     SRT_HIPCHK(hipFreeAsync(ws, st));
     return SRT_OK;
 }
+
+/* ------------------------------------------------------------------------------------------ *
+ * Workgroup-per-source form for large power-law graphs (C5: n = 100,000, Barabasi-Albert).
+ * The wave kernel above keeps its working distance row in HBM; on such graphs the frontier has
+ * no locality, so nearly every relaxation is a random line fetch beyond L2 and the kernel is bound
+ * by that traffic (C5 profile: ~7 TB of lines for 2.7 s). Here one 512-thread workgroup owns a
+ * source and keeps the whole distance row in LDS, packed three 10-bit values per word (133 KB at
+ * n = 100,000; code 1023 = unreached), so relaxations, staleness checks and the canonical
+ * predecessor search touch only LDS; one bucket step spreads its arcs over 1024 lanes instead of
+ * 64 (C5: 1.07 s with 1024 threads, 1.43 s with 512, 2.7 s for the wave kernel). Reliability lives in a private relabelled f64 row (L2 / Infinity Cache), the output rows are
+ * written once at the end with whole lines. Same Dial bucket order, settle-time canonical
+ * predecessor argmin (D[u], arc rank) and path-order reliability as wsssp_kernel, so the tables
+ * are identical. A distance above 1022 quanta or a full bucket flags the source, which the caller
+ * recomputes with the wave kernel; the caller only picks this form when a probe source shows every
+ * distance fits (d(a, b) <= 2 ecc(s0)). Undirected graphs only.
+ * ------------------------------------------------------------------------------------------ */
+#define WG_INF 1023u
+
+static __device__ __forceinline__ uint32_t wg_get(const uint32_t* sd, uint32_t v) {
+    return (sd[v / 3] >> (10 * (v % 3))) & 1023u;
+}
+
+/* lower the 10-bit field of v to nd if that is smaller; true when this call lowered it */
+static __device__ __forceinline__ bool wg_lower(uint32_t* sd, uint32_t v, uint32_t nd) {
+    uint32_t* p = sd + v / 3;
+    const uint32_t sh = 10 * (v % 3);
+    uint32_t old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (;;) {
+        const uint32_t cur = (old >> sh) & 1023u;
+        if (nd >= cur) return false;
+        const uint32_t nw = (old & ~(1023u << sh)) | (nd << sh);
+        const uint32_t prev = atomicCAS(p, old, nw);
+        if (prev == old) return true;
+        old = prev;
+    }
+}
+
+template <int WG>
+__global__ __launch_bounds__(WG) void wgsssp_kernel(
+    int n, int src_begin, int nsrc, const int2* __restrict__ rowptr, const uint2* __restrict__ cw,
+    const double* __restrict__ r, const int32_t* __restrict__ inv, uint32_t* __restrict__ lat,
+    double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ ws, int nb, int bcap,
+    int* __restrict__ overflow) {
+    extern __shared__ uint32_t sd[]; /* packed distances, relabelled order */
+    __shared__ uint32_t bcnt[256];
+    __shared__ unsigned long long bmask[4];
+    __shared__ int s_beg[WG], s_excl[WG], s_wtot[WG / WL];
+    __shared__ unsigned long long s_best[WG];
+    __shared__ int s_found, s_ovf;
+    const int tid = threadIdx.x, lane = tid & (WL - 1), wv = tid >> 6;
+    const int words = (n + 2) / 3;
+    const size_t slot_words = ((size_t)nb * bcap + 2 * (size_t)n + 1) & ~(size_t)1;
+    uint32_t* buckets = ws + (size_t)blockIdx.x * slot_words;
+    double* relp = reinterpret_cast<double*>(buckets + (((size_t)nb * bcap + 1) & ~(size_t)1));
+    const uint32_t bm = (uint32_t)nb - 1u;
+    for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
+        const int s = inv[src_begin + si];
+        uint32_t* ol = lat + (size_t)si * ldo;
+        double* rr = rel + (size_t)si * ldo;
+        for (int q = tid; q < words; q += WG) sd[q] = 0x3FFFFFFFu; /* three unreached fields */
+        for (int v = tid; v < n; v += WG) relp[v] = 0.0;
+        for (int b = tid; b < nb; b += WG) bcnt[b] = 0;
+        if (tid < 4) bmask[tid] = 0ull;
+        __syncthreads();
+        if (tid == 0) {
+            s_ovf = 0;
+            sd[s / 3] &= ~(1023u << (10 * (s % 3))); /* D[s] = 0 */
+            buckets[0] = (uint32_t)s;
+            bcnt[0] = 1;
+            bmask[0] = 1ull;
+        }
+        __threadfence_block();
+        __syncthreads();
+        uint32_t d = 0;
+        for (;;) {
+            if (wv == 0) { /* next non-empty bucket at or after d (circular) */
+                const uint32_t p0 = d & bm;
+                int found = -1;
+                for (int q = 0; q < nb && found < 0; q += WL) {
+                    const int pos = (int)((p0 + (uint32_t)q + (uint32_t)lane) & bm);
+                    const bool set = (bmask[pos >> 6] >> (pos & 63)) & 1ull;
+                    const unsigned long long bal = __ballot(set && q + lane < nb);
+                    if (bal) found = q + __ffsll((long long)bal) - 1;
+                }
+                if (lane == 0) s_found = found;
+            }
+            __syncthreads();
+            const int found = s_found;
+            if (found < 0) break;
+            d += (uint32_t)found;
+            const int b = (int)(d & bm);
+            const int cnt = min((int)bcnt[b], bcap);
+            __syncthreads();
+            if (tid == 0) {
+                bcnt[b] = 0;
+                bmask[b >> 6] &= ~(1ull << (b & 63));
+            }
+            __syncthreads();
+            const uint32_t* bk = buckets + (size_t)b * bcap;
+            for (int c0 = 0; c0 < cnt; c0 += WG) {
+                const int i = c0 + tid;
+                int v = -1, beg = 0, deg = 0;
+                if (i < cnt) {
+                    v = (int)ld_coherent(bk + i);
+                    if (wg_get(sd, (uint32_t)v) == d) {
+                        const int2 be = rowptr[v];
+                        beg = be.x;
+                        deg = be.y - be.x;
+                    } else {
+                        v = -1; /* stale: improved after it was pushed */
+                    }
+                }
+                /* workgroup exclusive scan of the degrees */
+                int wtot;
+                const int wex = wave_scan_excl(deg, lane, &wtot);
+                if (lane == 0) s_wtot[wv] = wtot;
+                __syncthreads();
+                int base = 0, total = 0;
+                for (int q = 0; q < WG / WL; ++q) {
+                    base += q < wv ? s_wtot[q] : 0;
+                    total += s_wtot[q];
+                }
+                s_beg[tid] = beg;
+                s_excl[tid] = base + wex;
+                s_best[tid] = ~0ull;
+                __syncthreads();
+                for (int a0 = 0; a0 < total; a0 += WG) {
+                    const int a = a0 + tid;
+                    if (a < total) {
+                        /* owner: the last entry whose exclusive offset is <= a */
+                        int lo = 0, hi = WG;
+                        while (hi - lo > 1) {
+                            const int mid = (lo + hi) >> 1;
+                            if (s_excl[mid] <= a) lo = mid;
+                            else hi = mid;
+                        }
+                        const int own = lo;
+                        const int k = s_beg[own] + (a - s_excl[own]);
+                        const uint2 e = cw[k];
+                        const uint32_t u = e.x, wk = e.y;
+                        const uint32_t du = wg_get(sd, u);
+                        const uint32_t nd = d + wk;
+                        if (nd < du) {
+                            if (nd >= WG_INF) {
+                                s_ovf = 1; /* not representable in 10 bits */
+                            } else if (wg_lower(sd, u, nd)) {
+                                const int b2 = (int)(nd & bm);
+                                const int slot = (int)atomicAdd(&bcnt[b2], 1u);
+                                if (slot < bcap) {
+                                    buckets[(size_t)b2 * bcap + slot] = u;
+                                    atomicOr(&bmask[b2 >> 6], 1ull << (b2 & 63));
+                                } else {
+                                    s_ovf = 1;
+                                }
+                            }
+                        }
+                        if (du != WG_INF && du + wk == d)
+                            atomicMin(&s_best[own], ((unsigned long long)du << 32) | (uint32_t)k);
+                    }
+                }
+                __threadfence_block();
+                __syncthreads();
+                /* settle: path-order reliability from the canonical predecessor */
+                if (v >= 0) {
+                    double x = 1.0;
+                    if (v != s) {
+                        const unsigned long long key = s_best[tid];
+                        x = 0.0;
+                        if (key != ~0ull) {
+                            const int k = (int)(uint32_t)key;
+                            x = ld_coherent(relp + cw[k].x) * r[k];
+                        }
+                    }
+                    relp[v] = x;
+                }
+                __threadfence_block();
+                __syncthreads();
+            }
+            if (s_ovf) break;
+        }
+        /* output rows in original order, whole lines */
+        for (int i = tid; i < n; i += WG) {
+            const int v = inv[i];
+            const uint32_t dv = wg_get(sd, (uint32_t)v);
+            ol[i] = dv == WG_INF ? SRT_INF : dv;
+            rr[i] = ld_coherent(relp + v);
+        }
+        if (s_ovf && tid == 0) overflow[si] = 1;
+        __syncthreads();
+    }
+}
+
+/* largest n the packed LDS row holds beside the kernel's static LDS (1024 threads: ~18 KB) */
+int srt_wgsssp_max_n(void) { return 3 * ((140 * 1024) / 4); }
+
+/* Rows [src_begin, src_end) by the workgroup kernel (undirected graphs, n <= srt_wgsssp_max_n,
+ * max arc weight < 256 quanta). ovf[i] = 1 marks a source to recompute (distance above 1022 or a
+ * full bucket). */
+int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r, const int32_t* inv,
+                    uint32_t max_w, int src_begin, int src_end, uint32_t* lat, double* rel,
+                    int* ovf, hipStream_t st) {
+    int nb = 1;
+    while ((uint32_t)nb <= max_w) nb <<= 1;
+    if (nb > 256 || n > srt_wgsssp_max_n()) {
+        srt_set_error("wgsssp: n = %d or max arc weight %u outside the kernel's range", n, max_w);
+        return SRT_E_ARG;
+    }
+    const int nsrc = src_end - src_begin;
+    int bcap = n < 65536 ? n : 65536;
+    const char* env = getenv("SRT_WSSSP_BCAP"); /* tests: force bucket overflows */
+    if (env && atoi(env) > 0) bcap = atoi(env);
+    int cus = 256, dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+        cus = prop.multiProcessorCount;
+    const size_t slot_words = ((size_t)nb * bcap + 2 * (size_t)n + 1) & ~(size_t)1;
+    size_t slots = (size_t)cus; /* one workgroup per CU: the packed row takes most of the LDS */
+    if (slots > (size_t)nsrc) slots = nsrc;
+    uint32_t* ws = NULL;
+    if (hipMallocAsync((void**)&ws, slots * (slot_words + 2) * sizeof(uint32_t), st) != hipSuccess) {
+        (void)hipGetLastError();
+        srt_set_error("wgsssp: workspace of %zu MiB failed", (slots * slot_words * 4) >> 20);
+        return SRT_E_NOMEM;
+    }
+    SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)nsrc * sizeof(int), st));
+    const size_t dyn = (size_t)((n + 2) / 3) * sizeof(uint32_t);
+    const char* tenv = getenv("SRT_WGSSSP_THREADS");
+    if (tenv && atoi(tenv) == 512) {
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<512>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+        wgsssp_kernel<512><<<(unsigned)slots, 512, dyn, st>>>(n, src_begin, nsrc, rowptr, cw, r, inv,
+                                                             lat, rel, (size_t)n, ws, nb, bcap, ovf);
+    } else {
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+        wgsssp_kernel<1024><<<(unsigned)slots, 1024, dyn, st>>>(n, src_begin, nsrc, rowptr, cw, r,
+                                                               inv, lat, rel, (size_t)n, ws, nb, bcap,
+                                                               ovf);
+    }
+    SRT_HIPCHK(hipGetLastError());
+    SRT_HIPCHK(hipFreeAsync(ws, st));
+    return SRT_OK;
+}

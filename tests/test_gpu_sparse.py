@@ -153,3 +153,40 @@ def test_wave_kernel_working_row_forms(gpu, monkeypatch, which, lds, relrow):
     assert np.array_equal(lat, exp["lat_int"])
     err = np.abs(rel - exp["rel"]) / np.maximum(np.abs(exp["rel"]), 1e-300)
     assert float(err.max()) <= REL_TOL
+
+
+@pytest.mark.parametrize("which", ["ba2000", "ba3000_w20", "rgg3000"])
+def test_workgroup_kernel_packed_rows(gpu, monkeypatch, which):
+    """SRT_SPARSE_WG=1: the workgroup-per-source kernel (distance row packed 3 x 10 bits in LDS)
+    on any undirected graph whose probe source shows every distance fits (2 ecc <= 1022); else
+    the wave kernel. Either way the exact tables."""
+    monkeypatch.setenv("SRT_SPARSE_WG", "1")
+    if which == "ba2000":
+        g = graphs.barabasi_albert(2000, seed=5)
+    elif which == "ba3000_w20":
+        g = graphs.barabasi_albert(3000, seed=8, lat_max=20)
+    else:
+        g = graphs.random_geometric(3000, seed=3)
+    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                algo=ALGO_SPARSE_SSSP)
+    exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss),
+                       True, oracle.ORC_INT_NS, 8)
+    assert np.array_equal(lat, exp["lat_int"])
+    assert np.array_equal(rel, exp["rel"])
+    if which.startswith("ba"):
+        assert st.dist_enc == 2, "the workgroup kernel should take power-law graphs with small distances"
+
+
+@pytest.mark.parametrize("bcap", ["3", "64"])
+def test_workgroup_kernel_overflow_fallback(gpu, monkeypatch, bcap):
+    """Forced bucket overflows in the workgroup kernel: flagged sources go to the wave kernel and,
+    when that overflows too, to the block kernel; the tables stay exact."""
+    monkeypatch.setenv("SRT_SPARSE_WG", "1")
+    monkeypatch.setenv("SRT_WSSSP_BCAP", bcap)
+    g = graphs.barabasi_albert(1500, seed=6)
+    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                algo=ALGO_SPARSE_SSSP)
+    exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss),
+                       True, oracle.ORC_INT_NS, 8)
+    assert np.array_equal(lat, exp["lat_int"])
+    assert np.array_equal(rel, exp["rel"])
