@@ -383,12 +383,13 @@ int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, con
  * Workgroup-per-source form for large power-law graphs (C5: n = 100,000, Barabasi-Albert).
  * The wave kernel above keeps its working distance row in HBM; on such graphs the frontier has
  * no locality, so nearly every relaxation is a random line fetch beyond L2 and the kernel is bound
- * by that traffic (C5 profile: ~7 TB of lines for 2.7 s). Here one 512-thread workgroup owns a
+ * by that traffic (C5 profile: ~7 TB of lines for 2.7 s). Here one 1024-thread workgroup owns a
  * source and keeps the whole distance row in LDS, packed three 10-bit values per word (133 KB at
  * n = 100,000; code 1023 = unreached), so relaxations, staleness checks and the canonical
  * predecessor search touch only LDS; one bucket step spreads its arcs over 1024 lanes instead of
- * 64 (C5: 1.07 s with 1024 threads, 1.43 s with 512, 2.7 s for the wave kernel). Reliability lives in a private relabelled f64 row (L2 / Infinity Cache), the output rows are
- * written once at the end with whole lines. Same Dial bucket order, settle-time canonical
+ * 64 (C5: 1.07 s with 1024 threads, 1.43 s with 512, 2.7 s for the wave kernel). Reliability
+ * lives in a private relabelled f64 row (L2 / Infinity Cache), the output rows are written once
+ * at the end with whole lines. Same Dial bucket order, settle-time canonical
  * predecessor argmin (D[u], arc rank) and path-order reliability as wsssp_kernel, so the tables
  * are identical. A distance above 1022 quanta or a full bucket flags the source, which the caller
  * recomputes with the wave kernel; the caller only picks this form when a probe source shows every
