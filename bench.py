@@ -311,8 +311,13 @@ def run_sparse(c: Ctx, wl):
     k_ms = sum(s.ms_update for s in stats) / max(sum(s.n_update for s in stats), 1)
     achieved_gbs = nsrc * bytes_per_src / (k_ms * 1e-3) / 1e9
     lds_row = 8 * (n * 4 + 4096) <= 160 * 1024  # wsssp.hip: LDS working row when 8 waves/CU fit
-    roofline = {"bound": "hbm", "kernel": "wsssp_kernel<%s, %s>" % (
-        "true" if g.directed else "false", "true" if lds_row else "false"),
+    # the kernel the build used (srt_build_stats.dist_enc for sparse builds): 2 = workgroup per
+    # source with the LDS-packed distance row, 1 = wave per source, 0 = the block kernel
+    enc = int(stats[-1].dist_enc)
+    kname = {2: "wgsssp_kernel<1024>",
+             1: "wsssp_kernel<%s, %s>" % ("true" if g.directed else "false",
+                                          "true" if lds_row else "false")}.get(enc, "sssp_kernel")
+    roofline = {"bound": "hbm", "kernel": kname,
         "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None,
         "bytes_per_launch": float(nsrc * bytes_per_src), "avg_launch_ms": round(k_ms, 3),

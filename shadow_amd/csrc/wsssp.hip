@@ -396,6 +396,7 @@ int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, con
  * distance fits (d(a, b) <= 2 ecc(s0)). Undirected graphs only.
  * ------------------------------------------------------------------------------------------ */
 #define WG_INF 1023u
+#define WG_AK 4 /* arc windows in flight per lane */
 
 static __device__ __forceinline__ uint32_t wg_get(const uint32_t* sd, uint32_t v) {
     return (sd[v / 3] >> (10 * (v % 3))) & 1023u;
@@ -416,23 +417,68 @@ static __device__ __forceinline__ bool wg_lower(uint32_t* sd, uint32_t v, uint32
     }
 }
 
-template <int WG>
+/* bucket entry: x = v | min(deg, WG_DEGC) << 17 (v < 2^17: srt_wgsssp_max_n), y = row begin, so a
+ * popped entry needs no row-pointer load; a degree at the clamp reloads rowptr[v] */
+#define WG_DEGC 32767u
+/* workgroup barrier ordering LDS only (no wait for outstanding global stores); the barriers that
+ * must publish global stores to the other waves stay __syncthreads() */
+#define WG_LDS_BARRIER()                                                \
+    do {                                                                \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); \
+        __builtin_amdgcn_s_barrier();                                   \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); \
+    } while (0)
+static __device__ __forceinline__ uint2 wg_entry(uint32_t v, uint32_t beg, uint32_t deg) {
+    return make_uint2(v | (min(deg, WG_DEGC) << 17), beg);
+}
+static __device__ __forceinline__ uint2 ld_coherent2(const uint2* p) {
+    const unsigned long long x = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return make_uint2((uint32_t)x, (uint32_t)(x >> 32));
+}
+
+/* arcs for the workgroup kernel: (neighbour u, weight, begin of u's row, degree of u), relabelled */
+__global__ void wg_arcs_kernel(int n, const int2* __restrict__ rowptr, const uint2* __restrict__ cw,
+                               uint4* __restrict__ ca) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const int2 be = rowptr[v];
+    for (int k = be.x; k < be.y; ++k) {
+        const uint2 e = cw[k];
+        const int2 bu = rowptr[e.x];
+        ca[k] = make_uint4(e.x, e.y, (uint32_t)bu.x, (uint32_t)(bu.y - bu.x));
+    }
+}
+
+/* PROF (tools only, SRT_WGSSSP_PROF=1): thread 0 accumulates shader-clock cycles per phase and
+ * step counts into prof[block * 10 + k]: 0 init, 1 bucket search, 2 chunk head, 3 arcs,
+ * 4 settle, 5 output, 6 steps, 7 chunks, 8 arc windows, 9 sources */
+#define WG_PT(k)                                                        \
+    do {                                                                \
+        if (PROF && tid == 0) {                                         \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+            pacc[k] += t_ - pt;                                         \
+            pt = t_;                                                    \
+        }                                                               \
+    } while (0)
+template <int WG, bool PROF = false>
 __global__ __launch_bounds__(WG) void wgsssp_kernel(
-    int n, int src_begin, int nsrc, const int2* __restrict__ rowptr, const uint2* __restrict__ cw,
+    int n, int src_begin, int nsrc, const int2* __restrict__ rowptr, const uint4* __restrict__ ca,
     const double* __restrict__ r, const int32_t* __restrict__ inv, uint32_t* __restrict__ lat,
     double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ ws, int nb, int bcap,
-    int* __restrict__ overflow) {
+    int* __restrict__ overflow, unsigned long long* __restrict__ prof = nullptr) {
+    unsigned long long pacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long pt = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     extern __shared__ uint32_t sd[]; /* packed distances, relabelled order */
-    __shared__ uint32_t bcnt[256];
-    __shared__ unsigned long long bmask[4];
+    __shared__ uint32_t bcnt[256]; /* entries per bucket; the search ballots on bcnt > 0 */
     __shared__ int s_beg[WG], s_excl[WG], s_wtot[WG / WL];
     __shared__ unsigned long long s_best[WG];
     __shared__ int s_found, s_ovf;
     const int tid = threadIdx.x, lane = tid & (WL - 1), wv = tid >> 6;
     const int words = (n + 2) / 3;
-    const size_t slot_words = ((size_t)nb * bcap + 2 * (size_t)n + 1) & ~(size_t)1;
-    uint32_t* buckets = ws + (size_t)blockIdx.x * slot_words;
-    double* relp = reinterpret_cast<double*>(buckets + (((size_t)nb * bcap + 1) & ~(size_t)1));
+    const size_t slot_words = ((size_t)nb * bcap * 2 + 2 * (size_t)n + 1) & ~(size_t)1;
+    uint2* buckets = reinterpret_cast<uint2*>(ws + (size_t)blockIdx.x * slot_words);
+    double* relp = reinterpret_cast<double*>(buckets + (size_t)nb * bcap);
     const uint32_t bm = (uint32_t)nb - 1u;
     for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
         const int s = inv[src_begin + si];
@@ -441,17 +487,24 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
         for (int q = tid; q < words; q += WG) sd[q] = 0x3FFFFFFFu; /* three unreached fields */
         for (int v = tid; v < n; v += WG) relp[v] = 0.0;
         for (int b = tid; b < nb; b += WG) bcnt[b] = 0;
-        if (tid < 4) bmask[tid] = 0ull;
         __syncthreads();
         if (tid == 0) {
             s_ovf = 0;
             sd[s / 3] &= ~(1023u << (10 * (s % 3))); /* D[s] = 0 */
-            buckets[0] = (uint32_t)s;
+            const int2 be = rowptr[s];
+            buckets[0] = wg_entry((uint32_t)s, (uint32_t)be.x, (uint32_t)(be.y - be.x));
             bcnt[0] = 1;
-            bmask[0] = 1ull;
         }
         __threadfence_block();
         __syncthreads();
+        WG_PT(0);
+        if (PROF && tid == 0) pacc[9]++;
+        /* deferred settle: the reliability of the lane's last settled vertex pv is stored at the
+         * next chunk's head (or after the last step), so its two loads overlap the bucket search
+         * and the next entry load; nothing reads rel(s, pv) before a larger distance value is
+         * settled, and that chunk's head barrier orders the store before it */
+        int pv = -1;
+        double pa = 0.0, pb = 0.0;
         uint32_t d = 0;
         for (;;) {
             if (wv == 0) { /* next non-empty bucket at or after d (circular) */
@@ -459,34 +512,43 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                 int found = -1;
                 for (int q = 0; q < nb && found < 0; q += WL) {
                     const int pos = (int)((p0 + (uint32_t)q + (uint32_t)lane) & bm);
-                    const bool set = (bmask[pos >> 6] >> (pos & 63)) & 1ull;
-                    const unsigned long long bal = __ballot(set && q + lane < nb);
+                    const bool set = q + lane < nb && bcnt[pos] != 0u;
+                    const unsigned long long bal = __ballot(set);
                     if (bal) found = q + __ffsll((long long)bal) - 1;
                 }
                 if (lane == 0) s_found = found;
             }
-            __syncthreads();
+            __syncthreads(); /* full: the last arc pass's bucket stores are visible from here */
             const int found = s_found;
             if (found < 0) break;
             d += (uint32_t)found;
             const int b = (int)(d & bm);
             const int cnt = min((int)bcnt[b], bcap);
-            __syncthreads();
-            if (tid == 0) {
-                bcnt[b] = 0;
-                bmask[b >> 6] &= ~(1ull << (b & 63));
-            }
-            __syncthreads();
-            const uint32_t* bk = buckets + (size_t)b * bcap;
+            WG_LDS_BARRIER();
+            if (tid == 0) bcnt[b] = 0;
+            WG_LDS_BARRIER();
+            WG_PT(1);
+            if (PROF && tid == 0) pacc[6]++;
+            const uint2* bk = buckets + (size_t)b * bcap;
             for (int c0 = 0; c0 < cnt; c0 += WG) {
+                if (PROF && tid == 0) pacc[7]++;
                 const int i = c0 + tid;
                 int v = -1, beg = 0, deg = 0;
+                uint2 en = make_uint2(0u, 0u);
+                if (i < cnt) en = ld_coherent2(bk + i);
+                if (pv >= 0) { /* the lane's vertex of the previous chunk */
+                    relp[pv] = pa * pb;
+                    pv = -1;
+                }
                 if (i < cnt) {
-                    v = (int)ld_coherent(bk + i);
+                    v = (int)(en.x & 0x1FFFFu);
                     if (wg_get(sd, (uint32_t)v) == d) {
-                        const int2 be = rowptr[v];
-                        beg = be.x;
-                        deg = be.y - be.x;
+                        beg = (int)en.y;
+                        deg = (int)(en.x >> 17);
+                        if ((uint32_t)deg == WG_DEGC) {
+                            const int2 be = rowptr[v];
+                            deg = be.y - be.x;
+                        }
                     } else {
                         v = -1; /* stale: improved after it was pushed */
                     }
@@ -495,7 +557,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                 int wtot;
                 const int wex = wave_scan_excl(deg, lane, &wtot);
                 if (lane == 0) s_wtot[wv] = wtot;
-                __syncthreads();
+                WG_LDS_BARRIER();
                 int base = 0, total = 0;
                 for (int q = 0; q < WG / WL; ++q) {
                     base += q < wv ? s_wtot[q] : 0;
@@ -504,21 +566,35 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                 s_beg[tid] = beg;
                 s_excl[tid] = base + wex;
                 s_best[tid] = ~0ull;
-                __syncthreads();
-                for (int a0 = 0; a0 < total; a0 += WG) {
-                    const int a = a0 + tid;
-                    if (a < total) {
-                        /* owner: the last entry whose exclusive offset is <= a */
-                        int lo = 0, hi = WG;
-                        while (hi - lo > 1) {
-                            const int mid = (lo + hi) >> 1;
-                            if (s_excl[mid] <= a) lo = mid;
-                            else hi = mid;
-                        }
-                        const int own = lo;
-                        const int k = s_beg[own] + (a - s_excl[own]);
-                        const uint2 e = cw[k];
-                        const uint32_t u = e.x, wk = e.y;
+                if (c0 == 0) /* full: the previous step's deferred reliability stores */
+                    __syncthreads();
+                else
+                    WG_LDS_BARRIER();
+                WG_PT(2);
+                /* WG_AK arc windows per pass: the owner searches (fixed-step, unrolled) and the
+                 * arc loads of every window are issued before any of them is used, so their
+                 * latencies overlap instead of adding up */
+                for (int a0 = 0; a0 < total; a0 += WG * WG_AK) {
+                    if (PROF && tid == 0) pacc[8]++;
+                    int own[WG_AK], rk[WG_AK];
+                    uint4 e[WG_AK];
+#pragma unroll
+                    for (int j = 0; j < WG_AK; ++j) {
+                        const int a = a0 + j * WG + tid;
+                        int lo = 0; /* owner: the last entry whose exclusive offset is <= a */
+#pragma unroll
+                        for (int step = WG / 2; step >= 1; step >>= 1)
+                            if (s_excl[lo + step] <= a) lo = lo + step;
+                        own[j] = lo;
+                        rk[j] = a - s_excl[lo];
+                    }
+#pragma unroll
+                    for (int j = 0; j < WG_AK; ++j)
+                        if (a0 + j * WG + tid < total) e[j] = ca[s_beg[own[j]] + rk[j]];
+#pragma unroll
+                    for (int j = 0; j < WG_AK; ++j) {
+                        if (a0 + j * WG + tid >= total) continue;
+                        const uint32_t u = e[j].x, wk = e[j].y;
                         const uint32_t du = wg_get(sd, u);
                         const uint32_t nd = d + wk;
                         if (nd < du) {
@@ -528,37 +604,44 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                                 const int b2 = (int)(nd & bm);
                                 const int slot = (int)atomicAdd(&bcnt[b2], 1u);
                                 if (slot < bcap) {
-                                    buckets[(size_t)b2 * bcap + slot] = u;
-                                    atomicOr(&bmask[b2 >> 6], 1ull << (b2 & 63));
+                                    buckets[(size_t)b2 * bcap + slot] = wg_entry(u, e[j].z, e[j].w);
                                 } else {
                                     s_ovf = 1;
                                 }
                             }
                         }
+                        /* canonical predecessor key (D[u], rank of the arc in the row), with u
+                         * carried along so the settle step needs no second arc load */
                         if (du != WG_INF && du + wk == d)
-                            atomicMin(&s_best[own], ((unsigned long long)du << 32) | (uint32_t)k);
+                            atomicMin(&s_best[own[j]], ((unsigned long long)du << 40) |
+                                                           ((unsigned long long)rk[j] << 20) | u);
                     }
                 }
-                __threadfence_block();
-                __syncthreads();
-                /* settle: path-order reliability from the canonical predecessor */
+                WG_LDS_BARRIER(); /* the bucket stores drain by the next step's search barrier */
+                WG_PT(3);
+                /* settle: path-order reliability from the canonical predecessor, issued now and
+                 * stored one chunk later */
                 if (v >= 0) {
-                    double x = 1.0;
+                    pv = v;
+                    pa = 1.0;
+                    pb = 1.0;
                     if (v != s) {
                         const unsigned long long key = s_best[tid];
-                        x = 0.0;
+                        pa = 0.0;
                         if (key != ~0ull) {
-                            const int k = (int)(uint32_t)key;
-                            x = ld_coherent(relp + cw[k].x) * r[k];
+                            pa = ld_coherent(relp + (uint32_t)(key & 0xFFFFFu));
+                            pb = r[beg + (int)((key >> 20) & 0xFFFFFu)];
                         }
                     }
-                    relp[v] = x;
                 }
-                __threadfence_block();
-                __syncthreads();
+                WG_PT(4);
             }
             if (s_ovf) break;
         }
+        if (pv >= 0) relp[pv] = pa * pb;
+        __threadfence_block();
+        __syncthreads();
+        WG_PT(1);
         /* output rows in original order, whole lines */
         for (int i = tid; i < n; i += WG) {
             const int v = inv[i];
@@ -568,7 +651,10 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
         }
         if (s_ovf && tid == 0) overflow[si] = 1;
         __syncthreads();
+        WG_PT(5);
     }
+    if (PROF && tid == 0)
+        for (int k = 0; k < 10; ++k) prof[blockIdx.x * 10 + k] = pacc[k];
 }
 
 /* largest n the packed LDS row holds beside the kernel's static LDS (1024 threads: ~18 KB) */
@@ -587,38 +673,77 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
         return SRT_E_ARG;
     }
     const int nsrc = src_end - src_begin;
-    int bcap = n < 65536 ? n : 65536;
+    int bcap = n < 32768 ? n : 32768; /* entries per bucket (uint2) */
     const char* env = getenv("SRT_WSSSP_BCAP"); /* tests: force bucket overflows */
     if (env && atoi(env) > 0) bcap = atoi(env);
     int cus = 256, dev = 0;
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
         cus = prop.multiProcessorCount;
-    const size_t slot_words = ((size_t)nb * bcap + 2 * (size_t)n + 1) & ~(size_t)1;
+    /* arcs carrying their head's row bounds (built per call: a few MB, microseconds) */
+    int2 last;
+    SRT_HIPCHK(hipMemcpyAsync(&last, rowptr + (n - 1), sizeof(int2), hipMemcpyDeviceToHost, st));
+    SRT_HIPCHK(hipStreamSynchronize(st));
+    uint4* ca = NULL;
+    if (hipMallocAsync((void**)&ca, ((size_t)last.y + 1) * sizeof(uint4), st) != hipSuccess) {
+        (void)hipGetLastError();
+        srt_set_error("wgsssp: arc array of %d arcs failed", last.y);
+        return SRT_E_NOMEM;
+    }
+    wg_arcs_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rowptr, cw, ca);
+    SRT_HIPCHK(hipGetLastError());
+    const size_t slot_words = ((size_t)nb * bcap * 2 + 2 * (size_t)n + 1) & ~(size_t)1;
     size_t slots = (size_t)cus; /* one workgroup per CU: the packed row takes most of the LDS */
     if (slots > (size_t)nsrc) slots = nsrc;
     uint32_t* ws = NULL;
     if (hipMallocAsync((void**)&ws, slots * (slot_words + 2) * sizeof(uint32_t), st) != hipSuccess) {
         (void)hipGetLastError();
+        (void)hipFreeAsync(ca, st);
         srt_set_error("wgsssp: workspace of %zu MiB failed", (slots * slot_words * 4) >> 20);
         return SRT_E_NOMEM;
     }
     SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)nsrc * sizeof(int), st));
     const size_t dyn = (size_t)((n + 2) / 3) * sizeof(uint32_t);
     const char* tenv = getenv("SRT_WGSSSP_THREADS");
-    if (tenv && atoi(tenv) == 512) {
+    const char* penv = getenv("SRT_WGSSSP_PROF"); /* tools: per-phase cycle counts on stderr */
+    if (penv && atoi(penv) > 0) {
+        unsigned long long* prof = NULL;
+        SRT_HIPCHK(hipMalloc((void**)&prof, slots * 10 * sizeof(unsigned long long)));
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+        wgsssp_kernel<1024, true><<<(unsigned)slots, 1024, dyn, st>>>(
+            n, src_begin, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf, prof);
+        SRT_HIPCHK(hipGetLastError());
+        unsigned long long* h = (unsigned long long*)calloc(slots * 10, sizeof(*h));
+        SRT_HIPCHK(hipMemcpyAsync(h, prof, slots * 10 * sizeof(*h), hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipStreamSynchronize(st));
+        double tot[10] = {0};
+        for (size_t b = 0; b < slots; ++b)
+            for (int k = 0; k < 10; ++k) tot[k] += (double)h[b * 10 + k];
+        const double cyc = tot[0] + tot[1] + tot[2] + tot[3] + tot[4] + tot[5];
+        fprintf(stderr,
+                "[wgsssp prof] blocks %zu sources %.0f: cycles/source %.0f = init %.1f%% search "
+                "%.1f%% head %.1f%% arcs %.1f%% settle %.1f%% output %.1f%%; per source: steps "
+                "%.1f chunks %.1f arc windows %.1f; cycles per step %.0f\n",
+                slots, tot[9], cyc / tot[9], 100 * tot[0] / cyc, 100 * tot[1] / cyc,
+                100 * tot[2] / cyc, 100 * tot[3] / cyc, 100 * tot[4] / cyc, 100 * tot[5] / cyc,
+                tot[6] / tot[9], tot[7] / tot[9], tot[8] / tot[9], cyc / tot[6]);
+        free(h);
+        SRT_HIPCHK(hipFree(prof));
+    } else if (tenv && atoi(tenv) == 512) {
         SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<512>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-        wgsssp_kernel<512><<<(unsigned)slots, 512, dyn, st>>>(n, src_begin, nsrc, rowptr, cw, r, inv,
+        wgsssp_kernel<512><<<(unsigned)slots, 512, dyn, st>>>(n, src_begin, nsrc, rowptr, ca, r, inv,
                                                              lat, rel, (size_t)n, ws, nb, bcap, ovf);
     } else {
         SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-        wgsssp_kernel<1024><<<(unsigned)slots, 1024, dyn, st>>>(n, src_begin, nsrc, rowptr, cw, r,
+        wgsssp_kernel<1024><<<(unsigned)slots, 1024, dyn, st>>>(n, src_begin, nsrc, rowptr, ca, r,
                                                                inv, lat, rel, (size_t)n, ws, nb, bcap,
                                                                ovf);
     }
     SRT_HIPCHK(hipGetLastError());
     SRT_HIPCHK(hipFreeAsync(ws, st));
+    SRT_HIPCHK(hipFreeAsync(ca, st));
     return SRT_OK;
 }
