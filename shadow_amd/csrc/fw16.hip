@@ -35,6 +35,10 @@ typedef u16 u16x2 __attribute__((ext_vector_type(2)));
 
 #define KB 64
 #define CAP_U 0x7FFFu /* cap of the U path (v_pk_min_u16) */
+/* kernels on the round-to-round critical chain (next pivot block's tiles, diagonal closure,
+ * panel, panel assembly) raise their waves' issue priority above the bulk update's, which
+ * shares every SIMD with them; stream priority alone only orders dispatch */
+#define FW_CHAIN_PRIO() __builtin_amdgcn_s_setprio(3)
 #define CAP_F 0x3DFFu /* cap of the FM path: 2 * CAP_F < 0x7C00 (f16 +inf) */
 #define LDA16 (KB + 8) /* u16 stride of an A row in LDS: 144 B, 16-byte aligned */
 #define UKC 32          /* pivots per LDS stage in the update kernel (two stages per launch) */
@@ -225,6 +229,7 @@ __global__ void fw16_init_kernel(int n, int ld, int row0, const uint32_t* __rest
 /* closure of the diagonal tile: 64 dependent pivot steps in LDS, 4x4 per thread */
 __global__ __launch_bounds__(256) void fw16_diag_kernel(u16* __restrict__ P, int ld, int k0) {
     __shared__ __attribute__((aligned(16))) u16 s[KB * LDA16];
+    FW_CHAIN_PRIO();
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     u16* T = P + k0;
     for (int idx = tid; idx < KB * 8; idx += 256) {
@@ -263,6 +268,7 @@ __global__ __launch_bounds__(256) void fw16_panel_kernel(u16* __restrict__ D, in
                                                          int ncol_tiles, int do_row, int do_col) {
     __shared__ __attribute__((aligned(16))) uint32_t sA[KB * (KB + 4)];
     __shared__ __attribute__((aligned(16))) u16 sB[KB * (KB + 8)];
+    FW_CHAIN_PRIO();
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     int bid = blockIdx.x;
     u16* C;
@@ -293,6 +299,7 @@ __global__ __launch_bounds__(256) void fw16_panel_kernel(u16* __restrict__ D, in
 /* SYM: pivot rows' lower part from the (upper) column tiles: D[k0+m][j0+c] = D[j0+c][k0+m] */
 __global__ __launch_bounds__(256) void fw16_refresh_kernel(u16* __restrict__ D, int ld, int k0) {
     __shared__ u16 t[KB][KB + 2];
+    FW_CHAIN_PRIO();
     const int j0 = blockIdx.x * KB, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     for (int a = ty; a < KB; a += 4) t[a][tx] = D[(size_t)(j0 + a) * ld + k0 + tx];
     __syncthreads();
@@ -546,6 +553,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const uint32_t* __restrict__ tl, int te) {
     __shared__ __attribute__((aligned(16))) uint32_t sA[UKC / 2 * 128 * 2];
     __shared__ __attribute__((aligned(16))) u16 sB[UKC * UBS];
+    if constexpr (XM == 3 || XM == 6 || XM == 7 || XM == 8) FW_CHAIN_PRIO(); /* next-row tiles */
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     const int nb = gridDim.x;
     const int per = nb >> 3;
@@ -675,6 +683,7 @@ __global__ __launch_bounds__(256) void sym_contrib_pack_kernel(const u16* __rest
                                                                int T, const int* __restrict__ own,
                                                                int me, u16* __restrict__ stage) {
     __shared__ u16 t[128][KB + 2];
+    FW_CHAIN_PRIO();
     const int J = (int)blockIdx.x;
     if (J >= T || sym_contrib(K, J, own) != me) return;
     u16* dst = stage + (size_t)sym_contrib_pos(K, J, T, own) * (KB * 128);
@@ -693,6 +702,7 @@ __global__ __launch_bounds__(256) void sym_contrib_pack_kernel(const u16* __rest
 __global__ __launch_bounds__(256) void sym_contrib_unpack_kernel(u16* __restrict__ P, int ld, int K,
                                                                  int T, const int* __restrict__ own,
                                                                  const u16* __restrict__ stage) {
+    FW_CHAIN_PRIO();
     const int J = (int)blockIdx.x;
     if (J >= T) return;
     const u16* src = stage + (size_t)sym_contrib_pos(K, J, T, own) * (KB * 128);
