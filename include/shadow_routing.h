@@ -158,6 +158,10 @@ int srt_comm_init_all(int32_t ndev, const int32_t* devices, srt_comm** comms);
  * GPU): each comms[i] is driven by its own host thread; collectives become device-to-device
  * copies ordered by events and host barriers. srt_build_tables_multi uses them when the
  * environment sets SRT_VIRTUAL_RANKS. */
+/* Timing only (tools/solo_rank.py): rank `rank` of `nranks` alone on `device`, every collective a
+ * no-op, so one rank's compute and critical chain at N ranks is measured without the wire. The
+ * tables it produces are NOT correct. */
+int srt_comm_init_solo(int32_t nranks, int32_t rank, int32_t device, srt_comm** comm);
 int srt_comm_init_virtual(int32_t nranks, int32_t device, srt_comm** comms);
 /* Bind the calling host thread to virtual rank `rank` on `device` (its own workspaces and
  * streams) before it drives that rank's srt_dense_build_sharded / srt_sparse_graph_rows;

@@ -32,6 +32,7 @@ struct srt_comm {
     ncclComm_t nc;
     int nranks, rank, device;
     srt_loop* loop; /* non-NULL: virtual ranks */
+    int solo;       /* timing only: one rank alone, every collective a no-op (srt_comm_init_solo) */
 };
 
 static thread_local int t_vslot = -1;
@@ -150,6 +151,26 @@ extern "C" int srt_comm_init_virtual(int32_t nranks, int32_t device, srt_comm** 
     return SRT_OK;
 }
 
+/* Timing-only communicator: rank `rank` of `nranks` runs its own schedule alone on `device` and
+ * every collective returns at once without moving data, so the tables are NOT correct. It
+ * measures one rank's compute and critical chain at N ranks without the wire
+ * (tools/solo_rank.py); never used by a build that returns tables. */
+extern "C" int srt_comm_init_solo(int32_t nranks, int32_t rank, int32_t device, srt_comm** comm) {
+    if (nranks < 1 || rank < 0 || rank >= nranks || !comm) {
+        srt_set_error("srt_comm_init_solo: bad arguments");
+        return SRT_E_ARG;
+    }
+    SRT_HIPCHK(hipSetDevice(device));
+    srt_comm* c = (srt_comm*)calloc(1, sizeof(srt_comm));
+    if (!c) return SRT_E_NOMEM;
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = device;
+    c->solo = 1;
+    *comm = c;
+    return SRT_OK;
+}
+
 extern "C" int srt_virtual_rank_bind(int32_t rank, int32_t device) {
     srt_set_virtual_slot(rank);
     SRT_HIPCHK(hipSetDevice(device));
@@ -177,7 +198,7 @@ extern "C" void srt_comm_free(srt_comm* comm) {
             free(L->done);
             free(L);
         }
-    } else {
+    } else if (!comm->solo) {
         (void)ncclCommDestroy(comm->nc);
     }
     free(comm);
@@ -193,6 +214,7 @@ __global__ void allreduce_i32_kernel(int32_t* __restrict__ dst, const int32_t* _
 }
 
 int srt_coll_bcast(const srt_comm* c, void* buf, size_t bytes, int root, hipStream_t st) {
+    if (c->solo) return SRT_OK;
     if (!c->loop) {
         SRT_NCCLCHK(ncclBroadcast(buf, buf, bytes, ncclUint8, root, c->nc, st));
         return SRT_OK;
@@ -217,6 +239,7 @@ int srt_coll_bcast(const srt_comm* c, void* buf, size_t bytes, int root, hipStre
 
 int srt_coll_allreduce_i32(const srt_comm* c, int32_t* buf, size_t count, int op_min,
                            hipStream_t st) {
+    if (c->solo) return SRT_OK;
     if (!c->loop) {
         SRT_NCCLCHK(ncclAllReduce(buf, buf, count, ncclInt32, op_min ? ncclMin : ncclSum, c->nc, st));
         return SRT_OK;
@@ -252,18 +275,19 @@ int srt_coll_allreduce_i32(const srt_comm* c, int32_t* buf, size_t count, int op
 }
 
 int srt_coll_group_begin(const srt_comm* c) {
-    if (!c->loop) SRT_NCCLCHK(ncclGroupStart());
+    if (!c->loop && !c->solo) SRT_NCCLCHK(ncclGroupStart());
     return SRT_OK;
 }
 
 int srt_coll_group_end(const srt_comm* c) {
-    if (!c->loop) SRT_NCCLCHK(ncclGroupEnd());
+    if (!c->loop && !c->solo) SRT_NCCLCHK(ncclGroupEnd());
     return SRT_OK;
 }
 
 int srt_coll_exchange(const srt_comm* c, void* const* send, const size_t* send_bytes,
                       void* const* recv, const size_t* recv_bytes, hipStream_t st) {
     const int me = c->rank, R = c->nranks;
+    if (c->solo) return SRT_OK;
     if (!c->loop) {
         SRT_NCCLCHK(ncclGroupStart());
         for (int q = 0; q < R; q++)
@@ -314,6 +338,7 @@ extern "C" void srt_shard_rows(int32_t n, int32_t align, int32_t nranks, int32_t
 }
 
 int srt_comm_rank(const srt_comm* c) { return c ? c->rank : -1; }
+int srt_comm_is_solo(const srt_comm* c) { return c ? c->solo : 0; }
 int srt_comm_size(const srt_comm* c) { return c ? c->nranks : 0; }
 
 extern "C" int srt_sparse_allgather(srt_comm* comm, int32_t n, int32_t rows_per_rank,
@@ -324,6 +349,7 @@ extern "C" int srt_sparse_allgather(srt_comm* comm, int32_t n, int32_t rows_per_
     }
     hipStream_t st = (hipStream_t)stream;
     const size_t cnt = (size_t)rows_per_rank * n;
+    if (comm->solo) return SRT_OK;
     if (comm->loop) { /* every rank broadcasts its block in turn */
         for (int q = 0; q < comm->nranks; q++) {
             int rc = srt_coll_bcast(comm, lat_all + cnt * q, cnt * sizeof(uint32_t), q, st);

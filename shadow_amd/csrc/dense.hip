@@ -1371,7 +1371,8 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
     shard_ctx ctx = {comm, ld};
     int exact = 0, enc = SRT_DENC_U32;
     const char* sym_env = getenv("SRT_FW_SYM");
-    const bool sym = !directed && R > 1 && !(sym_env && atoi(sym_env) == 0);
+    /* symmetric rounds up to 1,024 tile columns (fw16.hip SYM_TMAX, the panel-position table) */
+    const bool sym = !directed && R > 1 && ld <= 1024 * 128 && !(sym_env && atoi(sym_env) == 0);
     for (int fm = 1; fm >= 0 && !exact; --fm) {
         if (evp) {
             evp->used = 0;

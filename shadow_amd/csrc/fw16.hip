@@ -667,14 +667,23 @@ __global__ void fw16_finish_kernel(int n, int ld, int row0, const u16* __restric
 static __device__ __forceinline__ int sym_contrib(int K, int J, const int* __restrict__ own) {
     return sym_kept(K, J) ? own[K] : own[J];
 }
-static __device__ int sym_contrib_pos(int K, int J, int T, const int* __restrict__ own) {
-    const int c = sym_contrib(K, J, own);
-    int pos = 0;
-    for (int q = 0; q < T; ++q) {
-        const int cq = sym_contrib(K, q, own);
-        pos += cq < c || (cq == c && q < J);
+/* position of column block J in the staged panel: blocks in (contributor, J) order. The owner
+ * table is staged in LDS and the count spread over the workgroup (T <= SYM_TMAX tile columns). */
+#define SYM_TMAX 1024
+static __device__ int sym_contrib_pos(int K, int J, int T, const int* __restrict__ own, int* s_own,
+                                      int* s_cnt) {
+    for (int q = threadIdx.x; q < T; q += blockDim.x) s_own[q] = own[q];
+    if (threadIdx.x == 0) *s_cnt = 0;
+    __syncthreads();
+    const int c = sym_contrib(K, J, s_own);
+    int mine = 0;
+    for (int q = threadIdx.x; q < T; q += blockDim.x) {
+        const int cq = sym_contrib(K, q, s_own);
+        mine += cq < c || (cq == c && q < J);
     }
-    return pos;
+    if (mine) atomicAdd(s_cnt, mine);
+    __syncthreads();
+    return *s_cnt;
 }
 
 /* this rank's blocks of panel k into the staging buffer (64 x 128 each) */
@@ -682,32 +691,135 @@ __global__ __launch_bounds__(256) void sym_contrib_pack_kernel(const u16* __rest
                                                                int row0, int tb, int K, int k0,
                                                                int T, const int* __restrict__ own,
                                                                int me, u16* __restrict__ stage) {
-    __shared__ u16 t[128][KB + 2];
+    __shared__ u16 t[128][KB + 8];
+    __shared__ int s_own[SYM_TMAX], s_cnt;
     FW_CHAIN_PRIO();
-    const int J = (int)blockIdx.x;
+    const int J = (int)blockIdx.x, tid = threadIdx.x;
     if (J >= T || sym_contrib(K, J, own) != me) return;
-    u16* dst = stage + (size_t)sym_contrib_pos(K, J, T, own) * (KB * 128);
-    if (sym_kept(K, J)) { /* this rank owns the pivot rows: straight copy */
+    u16* dst = stage + (size_t)sym_contrib_pos(K, J, T, own, s_own, &s_cnt) * (KB * 128);
+    if (sym_kept(K, J)) { /* this rank owns the pivot rows: straight copy, 16 B per access */
         const u16* src = D + (size_t)(k0 - row0) * ld + (size_t)J * 128;
-        for (int i = threadIdx.x; i < KB * 128; i += 256) dst[i] = src[(size_t)(i / 128) * ld + i % 128];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = tid + q * 256, row = i >> 4, c8 = (i & 15) * 8;
+            *reinterpret_cast<uint4*>(dst + row * 128 + c8) =
+                *reinterpret_cast<const uint4*>(src + (size_t)row * ld + c8);
+        }
         return;
     }
-    const u16* src = D + (size_t)(J - tb) * 128 * ld + k0; /* tile (J, K), the pivot columns */
-    for (int i = threadIdx.x; i < 128 * KB; i += 256) t[i / KB][i % KB] = src[(size_t)(i / KB) * ld + i % KB];
+    /* tile (J, K): rows r of block J, pivot columns m -> staged [m][r] */
+    const u16* src = D + (size_t)(J - tb) * 128 * ld + k0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int i = tid + q * 256, r = i >> 3, m8 = (i & 7) * 8;
+        *reinterpret_cast<uint4*>(&t[r][m8]) = *reinterpret_cast<const uint4*>(src + (size_t)r * ld + m8);
+    }
     __syncthreads();
-    for (int i = threadIdx.x; i < KB * 128; i += 256) dst[i] = t[i % 128][i / 128];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int i = tid + q * 256, m = i >> 4, r8 = (i & 15) * 8;
+        u16 v[8];
+#pragma unroll
+        for (int x = 0; x < 8; ++x) v[x] = t[r8 + x][m];
+        uint4 o;
+        o.x = v[0] | ((uint32_t)v[1] << 16);
+        o.y = v[2] | ((uint32_t)v[3] << 16);
+        o.z = v[4] | ((uint32_t)v[5] << 16);
+        o.w = v[6] | ((uint32_t)v[7] << 16);
+        *reinterpret_cast<uint4*>(dst + m * 128 + r8) = o;
+    }
 }
 
-/* every rank: staged blocks into its panel buffer P (64 x ld) */
-__global__ __launch_bounds__(256) void sym_contrib_unpack_kernel(u16* __restrict__ P, int ld, int K,
-                                                                 int T, const int* __restrict__ own,
-                                                                 const u16* __restrict__ stage) {
+/* Panel of block k from the staged blocks in two launches (replacing unpack + diagonal + panel +
+ * the owner's copy). Staged position of tile column J: blocks in (contributor, J) order. */
+static __device__ int sym_stage_pos(int K, int J, int T, const int* __restrict__ own, int* s_own,
+                                    int* s_cnt) {
+    return sym_contrib_pos(K, J, T, own, s_own, s_cnt);
+}
+
+/* one workgroup: the diagonal block from its staged tile column, closed in LDS (64 dependent
+ * steps, as fw16_diag_kernel), into P and, on the owner (prow != NULL), its pivot rows */
+__global__ __launch_bounds__(256) void sym_diag_stage_kernel(u16* __restrict__ P, int ld, int K,
+                                                             int k0, int T,
+                                                             const int* __restrict__ own,
+                                                             const u16* __restrict__ stage,
+                                                             u16* __restrict__ prow) {
+    __shared__ __attribute__((aligned(16))) u16 s[KB * LDA16];
+    __shared__ int s_own[SYM_TMAX], s_cnt;
     FW_CHAIN_PRIO();
-    const int J = (int)blockIdx.x;
-    if (J >= T) return;
-    const u16* src = stage + (size_t)sym_contrib_pos(K, J, T, own) * (KB * 128);
-    u16* dst = P + (size_t)J * 128;
-    for (int i = threadIdx.x; i < KB * 128; i += 256) dst[(size_t)(i / 128) * ld + i % 128] = src[i];
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const u16* src = stage + (size_t)sym_stage_pos(K, K, T, own, s_own, &s_cnt) * (KB * 128) + (k0 & 127);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int i = tid + q * 256, row = i >> 3, c8 = (i & 7) * 8;
+        *reinterpret_cast<uint4*>(s + row * LDA16 + c8) = *reinterpret_cast<const uint4*>(src + row * 128 + c8);
+    }
+    __syncthreads();
+    for (int m = 0; m < KB; ++m) {
+        const uint2 bm = *reinterpret_cast<const uint2*>(s + m * LDA16 + 4 * tx);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t as = splat(s[(4 * ty + r) * LDA16 + m]);
+            uint2* row = reinterpret_cast<uint2*>(s + (4 * ty + r) * LDA16 + 4 * tx);
+            uint2 v = *row;
+            v.x = as32(relax(as2(v.x), as, bm.x));
+            v.y = as32(relax(as2(v.y), as, bm.y));
+            *row = v;
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int i = tid + q * 256, row = i >> 3, c8 = (i & 7) * 8;
+        const uint4 v = *reinterpret_cast<const uint4*>(s + row * LDA16 + c8);
+        *reinterpret_cast<uint4*>(P + (size_t)row * ld + k0 + c8) = v;
+        if (prow) *reinterpret_cast<uint4*>(prow + (size_t)row * ld + k0 + c8) = v;
+    }
+}
+
+/* workgroup j (columns j0 = 64 j, j0 != k0): P[:, j0..j0+63] = min(X, Dkk* (x) X) from its staged
+ * block X and the closed diagonal block in P (as fw16_panel_kernel), into P and the owner's rows */
+__global__ __launch_bounds__(256) void sym_panel_stage_kernel(u16* __restrict__ P, int ld, int K,
+                                                              int k0, int T,
+                                                              const int* __restrict__ own,
+                                                              const u16* __restrict__ stage,
+                                                              u16* __restrict__ prow) {
+    __shared__ __attribute__((aligned(16))) u16 s[KB * LDA16]; /* Dkk* */
+    __shared__ __attribute__((aligned(16))) u16 x[KB * LDA16]; /* this workgroup's block */
+    __shared__ int s_own[SYM_TMAX], s_cnt;
+    FW_CHAIN_PRIO();
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int j0 = (int)blockIdx.x * KB;
+    if (j0 == k0) return;
+    const u16* xsrc = stage + (size_t)sym_stage_pos(K, j0 >> 7, T, own, s_own, &s_cnt) * (KB * 128) +
+                      (j0 & 127);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int i = tid + q * 256, row = i >> 3, c8 = (i & 7) * 8;
+        *reinterpret_cast<uint4*>(s + row * LDA16 + c8) =
+            *reinterpret_cast<const uint4*>(P + (size_t)row * ld + k0 + c8);
+        *reinterpret_cast<uint4*>(x + row * LDA16 + c8) =
+            *reinterpret_cast<const uint4*>(xsrc + row * 128 + c8);
+    }
+    __syncthreads();
+    uint2 acc[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = *reinterpret_cast<const uint2*>(x + (4 * ty + r) * LDA16 + 4 * tx);
+    for (int m = 0; m < KB; ++m) {
+        const uint2 bm = *reinterpret_cast<const uint2*>(x + m * LDA16 + 4 * tx);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t as = splat(s[(4 * ty + r) * LDA16 + m]);
+            acc[r].x = as32(relax(as2(acc[r].x), as, bm.x));
+            acc[r].y = as32(relax(as2(acc[r].y), as, bm.y));
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const size_t o = (size_t)(4 * ty + r) * ld + j0 + 4 * tx;
+        *reinterpret_cast<uint2*>(P + o) = acc[r];
+        if (prow) *reinterpret_cast<uint2*>(prow + o) = acc[r];
+    }
 }
 
 /* final fill: kept tile (I, J) of the sender, transposed into a contiguous 128 x 128 block */
@@ -960,7 +1072,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
                                   evpool_t* evp, int* exact) {
     const int dev = srt_state_slot();
     const int R = srt_comm_size(comm), me = srt_comm_rank(comm);
-    const int T = ld / 128, nb = ld / KB, nrb = nrows / KB;
+    const int T = ld / 128, nb = ld / KB;
     const int tb = row0 / 128, te = (row0 + nrows) / 128;
     size_t* caps = fw16_caps;
     int** flags = fw16_flags;
@@ -1021,6 +1133,10 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
         ok = hipMemcpyAsync(down, own, (size_t)T * sizeof(int), hipMemcpyHostToDevice, st) ==
                  hipSuccess &&
              hipStreamSynchronize(st) == hipSuccess;
+    /* timing-only communicator: the blocks other ranks would send stay a small constant, so the
+     * arithmetic keeps the u16 tier and the u8 post pass (the tables are not correct) */
+    if (ok && srt_comm_is_solo(comm))
+        ok = hipMemsetD16Async((hipDeviceptr_t)grecv, 3, ((size_t)T + 1) * blk, st) == hipSuccess;
     void** sp = (void**)calloc((size_t)R, sizeof(void*));
     void** rp = (void**)calloc((size_t)R, sizeof(void*));
     size_t* sbytes = (size_t*)calloc((size_t)R, sizeof(size_t));
@@ -1061,11 +1177,9 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
          * also writes the result back into its pivot rows */
         auto produce = [&](int k) -> int {
             const int k0 = k * KB, K = k0 / 128, o = own[K];
+            /* P was last read by round k-2's rest launches, which precede round k-1's next-row
+             * launches on both update streams; cs waited for those (e_set), so it is free */
             u16* P = pbuf[k & 1];
-            if (k >= 2) { /* both streams' round k-2 read P */
-                SRT_HIPCHK(hipStreamWaitEvent(cs, sc->upd_done[k & 1], 0));
-                SRT_HIPCHK(hipStreamWaitEvent(cs, sc->xs_done[k & 1], 0));
-            }
             for (int q = 0; q < R; q++) cnt[q] = 0;
             for (int J = 0; J < T; J++) cnt[sym_kept(K, J) ? o : own[J]]++;
             if (cnt[me])
@@ -1080,13 +1194,11 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
             }
             const int r2 = srt_coll_group_end(comm);
             if (r || r2) return r ? r : r2;
-            sym_contrib_unpack_kernel<<<T, 256, 0, cs>>>(P, ld, K, T, down, grecv);
-            fw16_diag_kernel<<<1, 256, 0, cs>>>(P, ld, k0);
-            fw16_panel_kernel<true, false><<<nb, 256, 0, cs>>>(d, ld, row0, nrb, P, k0, nb, 1, 0);
+            /* straight from the staged blocks: closure, then row panel (+ the owner's rows) */
+            u16* prow = me == o ? d + (size_t)(k0 - row0) * ld : nullptr;
+            sym_diag_stage_kernel<<<1, 256, 0, cs>>>(P, ld, K, k0, T, down, grecv, prow);
+            sym_panel_stage_kernel<<<nb, 256, 0, cs>>>(P, ld, K, k0, T, down, grecv, prow);
             SRT_HIPCHK(hipGetLastError());
-            if (me == o)
-                SRT_HIPCHK(hipMemcpyAsync(d + (size_t)(k0 - row0) * ld, P, (size_t)KB * ld * sizeof(u16),
-                                          hipMemcpyDeviceToDevice, cs));
             SRT_HIPCHK(hipEventRecord(sc->ready[k & 1], cs));
             return SRT_OK;
         };
@@ -1096,6 +1208,11 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
         hipStream_t ss[2] = {st, sc->xs};
         const uint32_t* tls[2] = {tl, tl + nset[0]};
         SYM_HIP(hipStreamWaitEvent(sc->xs, sc->init_done, 0));
+        /* Host enqueue order per round: next-row launches, the rest launches, then the next
+         * panel on cs. At N ranks a round is ~100 us of GPU work and ~20 HIP calls, so the host
+         * is the bottleneck if the bulk update waits behind the chain's calls; the chain kernels
+         * run at raised wave priority wherever they land (FW_CHAIN_PRIO). */
+        int timed = 0; /* rounds timed as one unit: the first start and the last end (evpool) */
         for (int k = 0; k < nb; ++k) {
             const int k0 = k * KB;
             u16* P = panel_of(k);
@@ -1112,19 +1229,15 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
                                                                                  K1, nullptr, te);
                 SYM_HIP(hipEventRecord(sc->e_set[k & 1][p], ss[p]));
             }
-            if (next) {
-                SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[k & 1][0], 0));
-                SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[k & 1][1], 0));
-                if ((rc = produce(k + 1))) goto out;
-            }
-            /* timed as one unit per round: the two rest launches (evpool group 4) */
-            const int e0 = evp ? evp->used : 0;
+            /* the unit's period only needs the first round's starts and the last round's ends
+             * (evpool_sum, group 4): two records per round fewer on the host's critical path */
+            const bool t_first = evp && next && timed == 0, t_last = evp && k + 2 == nb;
             if (evp && next) {
                 evp->group = 4;
-                evp->used += 4;
+                evp->used = 4 * ++timed;
             }
             for (int p = 0; p < 2; p++) {
-                if (evp && next) SYM_HIP(hipEventRecord(evp->ev[e0 + p], ss[p]));
+                if (t_first) SYM_HIP(hipEventRecord(evp->ev[p], ss[p]));
                 if (nset[p]) {
                     if (next)
                         fwh_update_kernel<true, 4><<<(unsigned)nset[p], 256, 0, ss[p]>>>(
@@ -1133,13 +1246,17 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
                         fwh_update_kernel<true, 5><<<(unsigned)nset[p], 256, 0, ss[p]>>>(
                             d, ld, P, k0, T, tb, -1, tls[p], te);
                 }
-                if (evp && next) SYM_HIP(hipEventRecord(evp->ev[e0 + 2 + p], ss[p]));
+                if (t_last) SYM_HIP(hipEventRecord(evp->ev[evp->used - 2 + p], ss[p]));
             }
             SYM_HIP(hipGetLastError());
-            SYM_HIP(hipEventRecord(sc->upd_done[k & 1], st));
-            SYM_HIP(hipEventRecord(sc->xs_done[k & 1], sc->xs));
+            if (next) {
+                SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[k & 1][0], 0));
+                SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[k & 1][1], 0));
+                if ((rc = produce(k + 1))) goto out;
+            }
         }
-        SYM_HIP(hipStreamWaitEvent(st, sc->xs_done[(nb - 1) & 1], 0));
+        SYM_HIP(hipEventRecord(sc->xs_done[0], sc->xs));
+        SYM_HIP(hipStreamWaitEvent(st, sc->xs_done[0], 0));
         /* fill the tiles this rank does not keep: transposes from their keepers */
         {
             size_t nloc = 0;
@@ -1208,6 +1325,9 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
                     ro += q == me ? 0 : rcount[q];
                 }
                 fok = hipGetLastError() == hipSuccess;
+                if (fok && srt_comm_is_solo(comm)) /* timing only: see grecv */
+                    fok = hipMemsetD16Async((hipDeviceptr_t)frecv, 3, (rtot + 1) * tile, st) ==
+                          hipSuccess;
                 if (fok && (rc = srt_coll_exchange(comm, sp, sbytes, rp, rbytes, st))) fok = false;
                 if (fok && rtot)
                     sym_fill_unpack_kernel<<<(unsigned)rtot, 256, 0, st>>>(d, ld, tb,
@@ -1263,8 +1383,9 @@ out:
 int srt_fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0, int nrows,
                                const uint32_t* w_rows, uint32_t* lat_rows, hipStream_t st,
                                evpool_t* evp, int* exact) {
-    if (ld % 128 || nrows % 128 || row0 % 128 || srt_comm_size(comm) < 2) {
-        srt_set_error("sharded symmetric FW needs 128-aligned shards and two or more ranks");
+    if (ld % 128 || nrows % 128 || row0 % 128 || srt_comm_size(comm) < 2 || ld / 128 > SYM_TMAX) {
+        srt_set_error("sharded symmetric FW needs 128-aligned shards, two or more ranks and at "
+                      "most %d tile columns", SYM_TMAX);
         return SRT_E_ARG;
     }
     return fw16_build_sym_sharded(comm, n, ld, row0, nrows, w_rows, lat_rows, st, evp, exact);

@@ -39,6 +39,7 @@ int srt_coll_group_end(const srt_comm* c);
 int srt_coll_exchange(const srt_comm* c, void* const* send, const size_t* send_bytes,
                       void* const* recv, const size_t* recv_bytes, hipStream_t st);
 int srt_comm_rank(const srt_comm* c);
+int srt_comm_is_solo(const srt_comm* c); /* timing-only communicator (srt_comm_init_solo) */
 int srt_comm_size(const srt_comm* c);
 
 /* pivot-block edge of the blocked Floyd-Warshall and the output-tile edge of its kernels */

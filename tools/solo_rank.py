@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""One rank of the N-rank sharded dense build, alone on one GPU, without the wire (timing only).
+
+srt_comm_init_solo gives rank r of R a communicator whose collectives return at once: the rank
+runs exactly its own schedule of the sharded build -- its row block, its kept tiles, the
+next-row tiles first, panel assembly + closure on the high-priority stream, the final fill and
+its share of the post pass -- on an otherwise idle GPU. Blocks other ranks would send stay a
+small constant, so the tables are NOT correct and nothing is checked; what it measures is one
+rank's compute plus its round-to-round critical chain at N ranks, i.e. the N-GPU build time
+minus the collectives' own cost. The N-GPU runs themselves are the driver's.
+
+usage: python tools/solo_rank.py [--ranks 8] [--which 0,3,7] [--workload c4]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from shadow_amd import _lib  # noqa: E402
+
+WORKLOADS = {
+    "c4": dict(n=32768, seed=4, lat_max=1000, self_max=10, loss_max=500),
+    "c2": dict(n=1000, seed=2, lat_max=300, self_max=10, loss_max=500),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
+    ap.add_argument("--ranks", type=int, default=8)
+    ap.add_argument("--which", default=None, help="comma-separated ranks (default: 0, R/2, R-1)")
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--time-kernels", type=int, default=1,
+                    help="1: HIP events around the update launches, as bench.py times them")
+    a = ap.parse_args()
+    wl = WORKLOADS[a.workload]
+    n, R = wl["n"], a.ranks
+    which = sorted({0, R // 2, R - 1}) if a.which is None else [int(x) for x in a.which.split(",")]
+    L = _lib.lib()
+    ld = (n + 127) // 128 * 128
+    st = torch.cuda.Stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    for r in which:
+        b, e = ctypes.c_int32(), ctypes.c_int32()
+        L.srt_shard_rows(ld, 128, R, r, ctypes.byref(b), ctypes.byref(e))
+        b, e = b.value, e.value
+        nr = e - b
+        comm = ctypes.c_void_p()
+        _lib.check(L.srt_comm_init_solo(R, r, 0, ctypes.byref(comm)), "srt_comm_init_solo")
+        w = torch.empty((nr, ld), dtype=torch.int32, device="cuda")
+        rr = torch.empty((nr, ld), dtype=torch.float64, device="cuda")
+        lat = torch.empty_like(w)
+        rel = torch.empty_like(rr)
+        _lib.check(L.srt_gen_complete_device(n, ld, b, nr, wl["seed"], wl["lat_max"],
+                                             wl["self_max"], wl["loss_max"], w.data_ptr(),
+                                             rr.data_ptr(), sp), "gen")
+        torch.cuda.synchronize()
+        best = None
+        for _ in range(a.reps):
+            s = _lib.BuildStats()
+            s.time_kernels = a.time_kernels
+            _lib.check(L.srt_dense_build_sharded(comm, n, ld, 0, w.data_ptr(), rr.data_ptr(),
+                                                 lat.data_ptr(), rel.data_ptr(), sp, 0,
+                                                 ctypes.byref(s)), f"rank {r}")
+            torch.cuda.synchronize()
+            if best is None or s.ms_total < best.ms_total:
+                best = s
+        rounds = ld // 64
+        print(json.dumps({
+            "workload": a.workload, "n": n, "ranks": R, "rank": r, "rows": nr,
+            "time_kernels": a.time_kernels,
+            "dist_enc": int(best.dist_enc), "ms_total": round(best.ms_total, 2),
+            "ms_fw": round(best.ms_fw, 2), "ms_post": round(best.ms_post, 2),
+            "us_per_round": round(best.ms_fw * 1e3 / rounds, 1),
+            "update_unit_us": round(best.ms_update * 1e3 / max(best.n_update, 1), 1)}), flush=True)
+        L.srt_comm_free(comm)
+        del w, rr, lat, rel
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
