@@ -57,6 +57,14 @@ FW_B = 64
 SHARD_ALIGN = 128  # row-shard / update-tile alignment (srt_device.h SRT_SHARD_ALIGN)
 
 
+def cpu_threads() -> int:
+    """Host threads of the all-cores CPU leg: this process's CPU share (OMP_NUM_THREADS on the
+    GPU box, 16 there; os.cpu_count() reports the whole machine), capped by the affinity set."""
+    avail = len(os.sched_getaffinity(0))
+    want = int(os.environ.get("OMP_NUM_THREADS") or avail)
+    return max(1, min(want, avail, 64))
+
+
 def log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -246,6 +254,15 @@ def run_dense(c: Ctx, wl):
                          f"(oracle/oracle.c orc_complete_sample), {sssp_s:.1f} s, 1 thread "
                          f"(the reference serializes Dijkstra on graphLock, topology.c:130-148); "
                          f"matrix generation ({gen_s:.1f} s) excluded"}
+        # all-cores leg (SURVEY §8d ii): the same per-source Dijkstra sharded over host threads
+        nt = cpu_threads()
+        kk = int(max(nt, min(32 * nt, nt * c.args.cpu_seconds / 2 / max(t1, 1e-3))))
+        msrcs = np.unique(np.linspace(0, n - 1, kk).astype(np.int32))
+        _, _, _, mt_s = oracle.complete_sample(n, wl["seed"], wl["lat_max"], wl["self_max"],
+                                               wl["loss_max"], msrcs, nt)
+        cpu["all_cores"] = {"value": round(len(msrcs) * n / mt_s, 1), "cores": nt,
+                            "sample": f"{len(msrcs)} of {n} sources over {nt} threads, "
+                                      f"{mt_s:.1f} s (no graphLock: the reference cannot do this)"}
         # full-size parity spot check of the last step's rows against the oracle
         glat = lat[srcs.astype(np.int64)].cpu().numpy().view(np.uint32)[:, :n].astype(np.uint64) \
             * np.uint64(1_000_000)
@@ -342,6 +359,15 @@ def run_sparse(c: Ctx, wl):
                "sample": f"{3 * kk} of {n} sources (3 blocks of {kk}), binary-heap Dijkstra per "
                          f"source (oracle/oracle.c orc_sssp_rows), {cs:.1f} s, 1 thread (the "
                          f"reference serializes Dijkstra on graphLock, topology.c:130-148)"}
+        nt = cpu_threads()
+        mk = int(max(nt, min(64 * nt, nt * c.args.cpu_seconds / 2 / one)))
+        a0 = max(0, n // 2 - mk // 2)
+        t1 = time.perf_counter()
+        oracle.sssp_rows(el, a0, min(n, a0 + mk), nthreads=nt)
+        mt_s = time.perf_counter() - t1
+        cpu["all_cores"] = {"value": round(min(mk, n - a0) * n / mt_s, 1), "cores": nt,
+                            "sample": f"{min(mk, n - a0)} of {n} sources over {nt} threads, "
+                                      f"{mt_s:.1f} s (no graphLock: the reference cannot do this)"}
         ok, worst, exact = True, 0.0, 1.0
         for a, ex in rows:
             glat = lat[a:a + kk].cpu().numpy().view(np.uint32).astype(np.uint64) \

@@ -226,11 +226,65 @@ __global__ void fw16_init_kernel(int n, int ld, int row0, const uint32_t* __rest
     d[(size_t)blockIdx.y * ld + j] = (i == j) ? (u16)0 : (u16)min(x, cap);
 }
 
-/* closure of the diagonal tile: 64 dependent pivot steps in LDS, 4x4 per thread */
+/* Closure of the 64x64 block in LDS (stride LDA16, zero diagonal) by in-place min-plus squaring,
+ * D <- min(D, D (x) D), until a pass changes nothing -- at most 6 passes (a simple path inside
+ * the block has <= 63 hops; after pass t every path of <= 2^t hops is covered). Every value read
+ * or written is the length of a real path inside the block (u16 sums of two values <= CAP never
+ * carry across halves), so entries read while a neighbour writes its new (smaller) values only
+ * speed convergence; a pass that changes nothing leaves D = min(D, D (x) D), which with the zero
+ * diagonal is the closure -- the same matrix as 64 dependent FW steps, in ~3-4 barriers instead
+ * of 64 (the block's shortest paths have few hops: C4's trees are <= 5 deep). 4x4 per thread. */
+template <bool FM>
+static __device__ __forceinline__ void close64(u16* __restrict__ s, int tid) {
+    const int tx = tid & 15, ty = tid >> 4;
+#pragma unroll 1
+    for (int pass = 0; pass < 6; ++pass) {
+        uint2 acc[4], old[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) old[r] = acc[r] = *reinterpret_cast<const uint2*>(s + (4 * ty + r) * LDA16 + 4 * tx);
+#pragma unroll 2
+        for (int m = 0; m < KB; m += 4) {
+            uint2 a[4], b[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) a[r] = *reinterpret_cast<const uint2*>(s + (4 * ty + r) * LDA16 + m);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b[q] = *reinterpret_cast<const uint2*>(s + (m + q) * LDA16 + 4 * tx);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t p[4] = {splat(a[r].x & 0xFFFFu), splat(a[r].x >> 16),
+                                       splat(a[r].y & 0xFFFFu), splat(a[r].y >> 16)};
+                if constexpr (FM) {
+#pragma unroll
+                    for (int q = 0; q < 4; q += 2) {
+                        acc[r].x = min3h(acc[r].x, p[q] + b[q].x, p[q + 1] + b[q + 1].x);
+                        acc[r].y = min3h(acc[r].y, p[q] + b[q].y, p[q + 1] + b[q + 1].y);
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        acc[r].x = as32(relax(as2(acc[r].x), p[q], b[q].x));
+                        acc[r].y = as32(relax(as2(acc[r].y), p[q], b[q].y));
+                    }
+                }
+            }
+        }
+        int ch = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (acc[r].x != old[r].x || acc[r].y != old[r].y) {
+                ch = 1;
+                *reinterpret_cast<uint2*>(s + (4 * ty + r) * LDA16 + 4 * tx) = acc[r];
+            }
+        if (!__syncthreads_or(ch)) break;
+    }
+}
+
+/* closure of the diagonal tile in LDS (close64) */
+template <bool FM>
 __global__ __launch_bounds__(256) void fw16_diag_kernel(u16* __restrict__ P, int ld, int k0) {
     __shared__ __attribute__((aligned(16))) u16 s[KB * LDA16];
     FW_CHAIN_PRIO();
-    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int tid = threadIdx.x;
     u16* T = P + k0;
     for (int idx = tid; idx < KB * 8; idx += 256) {
         const int row = idx >> 3, c8 = (idx & 7) * 8;
@@ -238,19 +292,7 @@ __global__ __launch_bounds__(256) void fw16_diag_kernel(u16* __restrict__ P, int
             *reinterpret_cast<const uint4*>(T + (size_t)row * ld + c8);
     }
     __syncthreads();
-    for (int m = 0; m < KB; ++m) {
-        const uint2 bm = *reinterpret_cast<const uint2*>(s + m * LDA16 + 4 * tx);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint32_t as = splat(s[(4 * ty + r) * LDA16 + m]);
-            uint2* row = reinterpret_cast<uint2*>(s + (4 * ty + r) * LDA16 + 4 * tx);
-            uint2 v = *row;
-            v.x = as32(relax(as2(v.x), as, bm.x));
-            v.y = as32(relax(as2(v.y), as, bm.y));
-            *row = v;
-        }
-        __syncthreads();
-    }
+    close64<FM>(s, tid);
     for (int idx = tid; idx < KB * 8; idx += 256) {
         const int row = idx >> 3, c8 = (idx & 7) * 8;
         *reinterpret_cast<uint4*>(T + (size_t)row * ld + c8) =
@@ -747,7 +789,7 @@ __global__ __launch_bounds__(256) void sym_diag_stage_kernel(u16* __restrict__ P
     __shared__ __attribute__((aligned(16))) u16 s[KB * LDA16];
     __shared__ int s_own[SYM_TMAX], s_cnt;
     FW_CHAIN_PRIO();
-    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int tid = threadIdx.x;
     const u16* src = stage + (size_t)sym_stage_pos(K, K, T, own, s_own, &s_cnt) * (KB * 128) + (k0 & 127);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -755,19 +797,7 @@ __global__ __launch_bounds__(256) void sym_diag_stage_kernel(u16* __restrict__ P
         *reinterpret_cast<uint4*>(s + row * LDA16 + c8) = *reinterpret_cast<const uint4*>(src + row * 128 + c8);
     }
     __syncthreads();
-    for (int m = 0; m < KB; ++m) {
-        const uint2 bm = *reinterpret_cast<const uint2*>(s + m * LDA16 + 4 * tx);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint32_t as = splat(s[(4 * ty + r) * LDA16 + m]);
-            uint2* row = reinterpret_cast<uint2*>(s + (4 * ty + r) * LDA16 + 4 * tx);
-            uint2 v = *row;
-            v.x = as32(relax(as2(v.x), as, bm.x));
-            v.y = as32(relax(as2(v.y), as, bm.y));
-            *row = v;
-        }
-        __syncthreads();
-    }
+    close64<true>(s, tid);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int i = tid + q * 256, row = i >> 3, c8 = (i & 7) * 8;
@@ -777,48 +807,74 @@ __global__ __launch_bounds__(256) void sym_diag_stage_kernel(u16* __restrict__ P
     }
 }
 
-/* workgroup j (columns j0 = 64 j, j0 != k0): P[:, j0..j0+63] = min(X, Dkk* (x) X) from its staged
- * block X and the closed diagonal block in P (as fw16_panel_kernel), into P and the owner's rows */
+/* P[:, j0..j0+63] = min(X, Dkk* (x) X) for every 64-column block j0 != k0, from the staged block X
+ * and the closed diagonal block in P (as fw16_panel_kernel), into P and the owner's rows */
 __global__ __launch_bounds__(256) void sym_panel_stage_kernel(u16* __restrict__ P, int ld, int K,
                                                               int k0, int T,
                                                               const int* __restrict__ own,
                                                               const u16* __restrict__ stage,
                                                               u16* __restrict__ prow) {
-    __shared__ __attribute__((aligned(16))) u16 s[KB * LDA16]; /* Dkk* */
-    __shared__ __attribute__((aligned(16))) u16 x[KB * LDA16]; /* this workgroup's block */
+    /* workgroup J: the 64 x 128 staged block of tile column J (both 64-column halves; the half
+     * holding the diagonal block is not written), 4 rows x 8 columns per thread. Per 4 pivots a
+     * thread reads 4 b64 of Dkk* (its rows) and 4 b128 of X (its columns) for 128 relaxations. */
+    __shared__ __attribute__((aligned(16))) u16 s[KB * LDA16];       /* Dkk* */
+    __shared__ __attribute__((aligned(16))) u16 x[KB * (128 + 8)];   /* this workgroup's block */
     __shared__ int s_own[SYM_TMAX], s_cnt;
     FW_CHAIN_PRIO();
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
-    const int j0 = (int)blockIdx.x * KB;
-    if (j0 == k0) return;
-    const u16* xsrc = stage + (size_t)sym_stage_pos(K, j0 >> 7, T, own, s_own, &s_cnt) * (KB * 128) +
-                      (j0 & 127);
+    const int J = (int)blockIdx.x;
+    const u16* xsrc = stage + (size_t)sym_stage_pos(K, J, T, own, s_own, &s_cnt) * (KB * 128);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int i = tid + q * 256, row = i >> 3, c8 = (i & 7) * 8;
         *reinterpret_cast<uint4*>(s + row * LDA16 + c8) =
             *reinterpret_cast<const uint4*>(P + (size_t)row * ld + k0 + c8);
-        *reinterpret_cast<uint4*>(x + row * LDA16 + c8) =
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int i = tid + q * 256, row = i >> 4, c8 = (i & 15) * 8;
+        *reinterpret_cast<uint4*>(x + row * (128 + 8) + c8) =
             *reinterpret_cast<const uint4*>(xsrc + row * 128 + c8);
     }
     __syncthreads();
-    uint2 acc[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc[r] = *reinterpret_cast<const uint2*>(x + (4 * ty + r) * LDA16 + 4 * tx);
-    for (int m = 0; m < KB; ++m) {
-        const uint2 bm = *reinterpret_cast<const uint2*>(x + m * LDA16 + 4 * tx);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint32_t as = splat(s[(4 * ty + r) * LDA16 + m]);
-            acc[r].x = as32(relax(as2(acc[r].x), as, bm.x));
-            acc[r].y = as32(relax(as2(acc[r].y), as, bm.y));
-        }
-    }
+    uint32_t acc[4][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const size_t o = (size_t)(4 * ty + r) * ld + j0 + 4 * tx;
-        *reinterpret_cast<uint2*>(P + o) = acc[r];
-        if (prow) *reinterpret_cast<uint2*>(prow + o) = acc[r];
+        const uint4 v = *reinterpret_cast<const uint4*>(x + (4 * ty + r) * (128 + 8) + 8 * tx);
+        acc[r][0] = v.x;
+        acc[r][1] = v.y;
+        acc[r][2] = v.z;
+        acc[r][3] = v.w;
+    }
+#pragma unroll 2
+    for (int m = 0; m < KB; m += 4) {
+        uint2 a[4];
+        uint4 b[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a[r] = *reinterpret_cast<const uint2*>(s + (4 * ty + r) * LDA16 + m);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b[q] = *reinterpret_cast<const uint4*>(x + (m + q) * (128 + 8) + 8 * tx);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t p[4] = {splat(a[r].x & 0xFFFFu), splat(a[r].x >> 16),
+                                   splat(a[r].y & 0xFFFFu), splat(a[r].y >> 16)};
+#pragma unroll
+            for (int q = 0; q < 4; q += 2) {
+                const uint32_t b0[4] = {b[q].x, b[q].y, b[q].z, b[q].w};
+                const uint32_t b1[4] = {b[q + 1].x, b[q + 1].y, b[q + 1].z, b[q + 1].w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) acc[r][c] = min3h(acc[r][c], p[q] + b0[c], p[q + 1] + b1[c]);
+            }
+        }
+    }
+    const int j0 = J * 128 + 8 * tx;
+    if ((j0 & ~(KB - 1)) == k0) return; /* the diagonal block: sym_diag_stage_kernel's */
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const size_t o = (size_t)(4 * ty + r) * ld + j0;
+        const uint4 v = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+        *reinterpret_cast<uint4*>(P + o) = v;
+        if (prow) *reinterpret_cast<uint4*>(prow + o) = v;
     }
 }
 
@@ -950,7 +1006,7 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
     if (!two) {
         for (int k0 = 0; k0 < ld; k0 += KB) {
             u16* P = d + (size_t)k0 * ld;
-            fw16_diag_kernel<<<1, 256, 0, st>>>(P, ld, k0);
+            fw16_diag_kernel<true><<<1, 256, 0, st>>>(P, ld, k0);
             fw16_panel_kernel<true, true><<<2 * nb, 256, 0, st>>>(d, ld, 0, nb, P, k0, nb, 1, 1);
             if (k0 > 0) fw16_refresh_kernel<<<k0 / KB, 256, 0, st>>>(d, ld, k0);
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
@@ -990,7 +1046,7 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
         auto produce = [&](int k) -> int {
             const int k0 = k * KB;
             u16* P = d + (size_t)k0 * ld;
-            fw16_diag_kernel<<<1, 256, 0, cs>>>(P, ld, k0);
+            fw16_diag_kernel<true><<<1, 256, 0, cs>>>(P, ld, k0);
             fw16_panel_kernel<true, true><<<2 * nb, 256, 0, cs>>>(d, ld, 0, nb, P, k0, nb, 1, 1);
             if (k0 > 0) fw16_refresh_kernel<<<k0 / KB, 256, 0, cs>>>(d, ld, k0);
             SRT_HIPCHK(hipGetLastError());
@@ -1197,7 +1253,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
             /* straight from the staged blocks: closure, then row panel (+ the owner's rows) */
             u16* prow = me == o ? d + (size_t)(k0 - row0) * ld : nullptr;
             sym_diag_stage_kernel<<<1, 256, 0, cs>>>(P, ld, K, k0, T, down, grecv, prow);
-            sym_panel_stage_kernel<<<nb, 256, 0, cs>>>(P, ld, K, k0, T, down, grecv, prow);
+            sym_panel_stage_kernel<<<T, 256, 0, cs>>>(P, ld, K, k0, T, down, grecv, prow);
             SRT_HIPCHK(hipGetLastError());
             SRT_HIPCHK(hipEventRecord(sc->ready[k & 1], cs));
             return SRT_OK;
@@ -1447,7 +1503,7 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
     auto produce = [&](int k) -> int {
         u16* P = panel_of(k);
         if (owner(k) == rank) {
-            fw16_diag_kernel<<<1, 256, 0, cs>>>(P, ld, k * KB);
+            (fm ? fw16_diag_kernel<true> : fw16_diag_kernel<false>)<<<1, 256, 0, cs>>>(P, ld, k * KB);
             panel<<<nb, 256, 0, cs>>>(d, ld, row0, nrb, P, k * KB, nb, 1, 0);
             SRT_HIPCHK(hipGetLastError());
         } else if (k >= 2 && lookahead) {
