@@ -360,7 +360,8 @@ def run_sparse(c: Ctx, wl):
                          f"source (oracle/oracle.c orc_sssp_rows), {cs:.1f} s, 1 thread (the "
                          f"reference serializes Dijkstra on graphLock, topology.c:130-148)"}
         nt = cpu_threads()
-        mk = int(max(nt, min(64 * nt, nt * c.args.cpu_seconds / 2 / one)))
+        mk = int(max(nt, min(256 * nt, nt * c.args.cpu_seconds / 2 / one)))
+        mk = min(mk, max(nt, int(2e9 / (n * 32))))  # the oracle's output rows: <= ~2 GB
         a0 = max(0, n // 2 - mk // 2)
         t1 = time.perf_counter()
         oracle.sssp_rows(el, a0, min(n, a0 + mk), nthreads=nt)
