@@ -217,13 +217,31 @@ __device__ __forceinline__ void store_acc16(const u16x2 (&acc)[RM][RN / 2],
 }
 
 /* ---- kernels --------------------------------------------------------------------------------- */
+/* 8 columns per thread (ld is a multiple of 128): two 16-B loads of w, one 16-B store of d */
 __global__ void fw16_init_kernel(int n, int ld, int row0, const uint32_t* __restrict__ w,
                                  u16* __restrict__ d, uint32_t cap) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j8 = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
     const int i = row0 + blockIdx.y;
-    if (j >= ld) return;
-    const uint32_t x = (i < n && j < n) ? w[(size_t)blockIdx.y * ld + j] : cap;
-    d[(size_t)blockIdx.y * ld + j] = (i == j) ? (u16)0 : (u16)min(x, cap);
+    if (j8 >= ld) return;
+    const size_t ix = (size_t)blockIdx.y * ld + j8;
+    uint32_t x[8];
+    if (i < n && j8 + 8 <= n) {
+        const uint4 a = *reinterpret_cast<const uint4*>(w + ix);
+        const uint4 b = *reinterpret_cast<const uint4*>(w + ix + 4);
+        x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+        x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) x[q] = (i < n && j8 + q < n) ? w[ix + q] : cap;
+    }
+    uint32_t o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t lo = (i == j8 + 2 * q) ? 0u : min(x[2 * q], cap);
+        const uint32_t hi = (i == j8 + 2 * q + 1) ? 0u : min(x[2 * q + 1], cap);
+        o[q] = lo | (hi << 16);
+    }
+    *reinterpret_cast<uint4*>(d + ix) = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 /* Closure of the 64x64 block in LDS (stride LDA16, zero diagonal) by in-place min-plus squaring,
@@ -686,17 +704,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 __global__ void fw16_finish_kernel(int n, int ld, int row0, const u16* __restrict__ d16,
                                    uint32_t* __restrict__ lat, int* __restrict__ flags,
                                    uint32_t cap) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    /* 8 columns per thread (ld is a multiple of 128): one 16-B load, two 16-B stores */
+    const int j8 = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
     const int i = row0 + blockIdx.y;
-    bool big = false;
-    if (j < ld) {
-        const size_t ix = (size_t)blockIdx.y * ld + j;
-        const uint32_t v = d16[ix];
-        const bool real = i < n && j < n;
-        lat[ix] = (v == cap) ? SRT_INF : v;
-        if (real && v == cap) atomicOr(flags, 1);
-        big = real && v > 254u;
+    bool big = false, sat = false;
+    if (j8 < ld) {
+        const size_t ix = (size_t)blockIdx.y * ld + j8;
+        const uint4 v = *reinterpret_cast<const uint4*>(d16 + ix);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+        uint32_t o[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t x = (w4[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+            const bool real = i < n && j8 + q < n;
+            o[q] = (x == cap) ? SRT_INF : x;
+            sat |= real && x == cap;
+            big |= real && x > 254u;
+        }
+        *reinterpret_cast<uint4*>(lat + ix) = make_uint4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<uint4*>(lat + ix + 4) = make_uint4(o[4], o[5], o[6], o[7]);
     }
+    if (sat) atomicOr(flags, 1);
     if (__ballot(big) && (threadIdx.x & 63) == 0 &&
         !__hip_atomic_load(flags + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
         atomicOr(flags + 1, 1);
@@ -999,7 +1027,7 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
     }
     if (!flags[dev]) SRT_HIPCHK(hipMalloc(&flags[dev], 2 * sizeof(int)));
     u16* d = fw16_bufs[dev];
-    fw16_init_kernel<<<dim3(srt_ceil_div(ld, 256), ld), 256, 0, st>>>(n, ld, 0, w, d, CAP_F);
+    fw16_init_kernel<<<dim3(srt_ceil_div(ld, 2048), ld), 256, 0, st>>>(n, ld, 0, w, d, CAP_F);
     SRT_HIPCHK(hipGetLastError());
     const int nb = ld / KB, T = ld / 128;
     const int ntri = T * (T + 1) / 2;
@@ -1098,7 +1126,7 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
     }
     fw16_mirror_kernel<<<dim3(nb, nb), 256, 0, st>>>(d, ld);
     SRT_HIPCHK(hipMemsetAsync(flags[dev], 0, 2 * sizeof(int), st));
-    fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 256), ld), 256, 0, st>>>(n, ld, 0, d, lat, flags[dev],
+    fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 2048), ld), 256, 0, st>>>(n, ld, 0, d, lat, flags[dev],
                                                                         CAP_F);
     SRT_HIPCHK(hipGetLastError());
     int hf[2] = {0, 0};
@@ -1222,7 +1250,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
             SYM_FAIL(SRT_E_NOMEM);
         }
         if (nrows > 0)
-            fw16_init_kernel<<<dim3(srt_ceil_div(ld, 256), nrows), 256, 0, st>>>(n, ld, row0, w_rows,
+            fw16_init_kernel<<<dim3(srt_ceil_div(ld, 2048), nrows), 256, 0, st>>>(n, ld, row0, w_rows,
                                                                                d, CAP_F);
         SYM_HIP(hipGetLastError());
         SYM_HIP(hipEventRecord(sc->init_done, st));
@@ -1407,7 +1435,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
         }
         SYM_HIP(hipMemsetAsync(flags[dev], 0, 2 * sizeof(int), st));
         if (nrows > 0)
-            fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 256), nrows), 256, 0, st>>>(
+            fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 2048), nrows), 256, 0, st>>>(
                 n, ld, row0, d, lat_rows, flags[dev], CAP_F);
         SYM_HIP(hipGetLastError());
         int hf[2] = {0, 0};
@@ -1488,7 +1516,7 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
     auto panel = fm ? fw16_panel_kernel<true, false> : fw16_panel_kernel<false, false>;
     auto update = fm ? fwh_update_kernel<false> : fw16_update_kernel<false>;
     if (nrows > 0) {
-        fw16_init_kernel<<<dim3(srt_ceil_div(ld, 256), nrows), 256, 0, st>>>(n, ld, row0, w_rows, d,
+        fw16_init_kernel<<<dim3(srt_ceil_div(ld, 2048), nrows), 256, 0, st>>>(n, ld, row0, w_rows, d,
                                                                            cap);
         SRT_HIPCHK(hipGetLastError());
     }
@@ -1550,7 +1578,7 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
     }
     SRT_HIPCHK(hipMemsetAsync(flags[dev], 0, 2 * sizeof(int), st));
     if (nrows > 0)
-        fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 256), nrows), 256, 0, st>>>(
+        fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 2048), nrows), 256, 0, st>>>(
             n, ld, row0, d, lat_rows, flags[dev], cap);
     SRT_HIPCHK(hipGetLastError());
     int hf[2] = {0, 0};
