@@ -299,7 +299,14 @@ __global__ __launch_bounds__(256) void ess_count_kernel(int n, int ld, int row0,
     const uint32_t* wr = w + (size_t)blockIdx.x * ld;
     const uint32_t* dr = d + (size_t)blockIdx.x * ld;
     int c = 0;
-    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+    const int n4 = n & ~3; /* rows are 16-B aligned (ld % 64 == 0): 4 columns per load */
+    for (int t = threadIdx.x * 4; t < n4; t += blockDim.x * 4) {
+        const uint4 x = *reinterpret_cast<const uint4*>(wr + t);
+        const uint4 y = *reinterpret_cast<const uint4*>(dr + t);
+        c += (t != u && x.x < SRT_INF && x.x == y.x) + (t + 1 != u && x.y < SRT_INF && x.y == y.y) +
+             (t + 2 != u && x.z < SRT_INF && x.z == y.z) + (t + 3 != u && x.w < SRT_INF && x.w == y.w);
+    }
+    for (int t = n4 + threadIdx.x; t < n; t += blockDim.x) {
         uint32_t x = wr[t];
         c += (t != u && x < SRT_INF && x == dr[t]) ? 1 : 0;
     }
@@ -357,26 +364,47 @@ __global__ __launch_bounds__(256) void ess_fill_kernel(int n, int ld, int row0,
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (threadIdx.x == 0) base = ptr[u];
     __syncthreads();
-    for (int t0 = 0; t0 < n; t0 += 256) {
-        int t = t0 + threadIdx.x;
-        bool ok = false;
-        uint32_t x = 0;
-        if (t < n) {
-            x = wr[t];
-            ok = (t != u && x < SRT_INF && x == dr[t]);
+    /* 4 consecutive columns per lane (one 16-B load of w and of d), 1024 per pass; arcs stay in
+     * ascending t: lane-major, then the lane's 4. A lane's count (0..4) is spread over three
+     * ballots, so its exclusive prefix in the wave is three masked popcounts. */
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int t0 = 0; t0 < n; t0 += 1024) {
+        const int t = t0 + threadIdx.x * 4;
+        uint32_t x[4] = {0, 0, 0, 0}, y[4] = {1, 1, 1, 1};
+        if (t + 4 <= n) {
+            const uint4 a = *reinterpret_cast<const uint4*>(wr + t);
+            const uint4 b = *reinterpret_cast<const uint4*>(dr + t);
+            x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+            y[0] = b.x; y[1] = b.y; y[2] = b.z; y[3] = b.w;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (t + q < n) {
+                    x[q] = wr[t + q];
+                    y[q] = dr[t + q];
+                }
         }
-        uint64_t mask = __ballot(ok);
-        int before = __popcll(mask & ((1ull << lane) - 1ull));
-        if (lane == 0) wave_cnt[wv] = __popcll(mask);
+        bool ok[4];
+        int c = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            ok[q] = t + q < n && t + q != u && x[q] < SRT_INF && x[q] == y[q];
+            c += ok[q];
+        }
+        const uint64_t b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
+        const int before = __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
+        if (lane == 0) wave_cnt[wv] = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
         __syncthreads();
-        int off = base;
-        for (int q = 0; q < wv; ++q) off += wave_cnt[q];
-        if (ok) {
-            int o = off + before;
-            col[o] = t;
-            aw[o] = x;
-            ar[o] = rr[t];
-        }
+        int o = base + before;
+        for (int q = 0; q < wv; ++q) o += wave_cnt[q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (ok[q]) {
+                col[o] = t + q;
+                aw[o] = x[q];
+                ar[o] = rr[t + q];
+                ++o;
+            }
         __syncthreads();
         if (threadIdx.x == 0) base += wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
         __syncthreads();
