@@ -877,9 +877,13 @@ __global__ __launch_bounds__(256) void dense_diag_kernel(int n, int ld, int row0
  * local rows start at b). */
 __global__ __launch_bounds__(256) void mirror_block_kernel(int n, int ld, int b, int e,
                                                            double* __restrict__ rel_rows) {
+    /* one workgroup per lower-triangle block (I >= J): x = I (I + 1) / 2 + J */
     __shared__ double tile[64][65];
-    const int I = blockIdx.y, J = blockIdx.x;
-    if (J > I) return;
+    const int x = (int)blockIdx.x;
+    int I = (int)((sqrt(8.0 * x + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= x) ++I;
+    while (I * (I + 1) / 2 > x) --I;
+    const int J = x - I * (I + 1) / 2;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     for (int a = ty; a < 64; a += 4) {
         int t = b + J * 64 + a, s = b + I * 64 + tx;
@@ -1147,8 +1151,8 @@ int srt_dense_post_device(int32_t n, int32_t ld, int32_t directed, const uint32_
     int rc = dense_post(n, ld, 0, ld, directed, w, r, d, d16, rel, st, stats, NULL, NULL);
     if (rc) return rc;
     if (!directed) {
-        dim3 g(srt_ceil_div(n, 64), srt_ceil_div(n, 64));
-        mirror_block_kernel<<<g, 256, 0, st>>>(n, ld, 0, n, rel);
+        const int nbk = srt_ceil_div(n, 64);
+        mirror_block_kernel<<<nbk * (nbk + 1) / 2, 256, 0, st>>>(n, ld, 0, n, rel);
         SRT_HIPCHK(hipGetLastError());
     }
     return dense_finish_rows(n, ld, 0, ld, w, r, d, rel, st, stats);
@@ -1359,8 +1363,8 @@ static int shard_mirror(const srt_comm* comm, int n, int ld, int b, int e, doubl
         ro += (size_t)pw * nr;
     }
     if (nr > 0) {
-        dim3 g(srt_ceil_div(nr, 64), srt_ceil_div(nr, 64));
-        mirror_block_kernel<<<g, 256, 0, st>>>(n, ld, b, e, rel_rows);
+        const int nbk = srt_ceil_div(nr, 64);
+        mirror_block_kernel<<<nbk * (nbk + 1) / 2, 256, 0, st>>>(n, ld, b, e, rel_rows);
     }
     SRT_HIPCHK(hipGetLastError());
     return SRT_OK;
@@ -1454,8 +1458,8 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
         if (R > 1) {
             if ((rc = shard_mirror(comm, n, ld, b, e, rel_rows, st))) return rc;
         } else {
-            dim3 g(srt_ceil_div(n, 64), srt_ceil_div(n, 64));
-            mirror_block_kernel<<<g, 256, 0, st>>>(n, ld, 0, n, rel_rows);
+            const int nbk = srt_ceil_div(n, 64);
+            mirror_block_kernel<<<nbk * (nbk + 1) / 2, 256, 0, st>>>(n, ld, 0, n, rel_rows);
         }
     }
     if ((rc = dense_finish_rows(n, ld, b, nr, w_rows, r_rows, lat_rows, rel_rows, st, stats))) return rc;
