@@ -373,12 +373,30 @@ extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begi
                                        g->delta, lat_rows, rel_rows, stream, stats);
     hipStream_t st = (hipStream_t)stream;
     const int nsrc = src_end - src_begin;
-    int* ovf = NULL;
-    SRT_HIPCHK(hipMallocAsync((void**)&ovf, (size_t)nsrc * sizeof(int), st));
-    hipEvent_t e0, e1, e2;
-    SRT_HIPCHK(hipEventCreate(&e0));
-    SRT_HIPCHK(hipEventCreate(&e1));
-    SRT_HIPCHK(hipEventCreate(&e2));
+    /* events, the overflow flags and host buffers are released on every return path */
+    struct rows_scratch {
+        hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+        int* ovf = nullptr;
+        int* ovf1 = nullptr;
+        uint32_t* row = nullptr;
+        int* hov = nullptr;
+        hipStream_t st = nullptr;
+        ~rows_scratch() {
+            for (hipEvent_t e : ev)
+                if (e) (void)hipEventDestroy(e);
+            if (ovf) (void)hipFreeAsync(ovf, st);
+            if (ovf1) (void)hipFree(ovf1);
+            free(row);
+            free(hov);
+        }
+    } sc;
+    sc.st = st;
+    SRT_HIPCHK(hipMallocAsync((void**)&sc.ovf, (size_t)nsrc * sizeof(int), st));
+    int* const ovf = sc.ovf;
+    SRT_HIPCHK(hipEventCreate(&sc.ev[0]));
+    SRT_HIPCHK(hipEventCreate(&sc.ev[1]));
+    SRT_HIPCHK(hipEventCreate(&sc.ev[2]));
+    hipEvent_t e0 = sc.ev[0], e1 = sc.ev[1], e2 = sc.ev[2];
     SRT_HIPCHK(hipEventRecord(e0, st));
     /* large power-law graphs (relabelled arcs far apart): the workgroup kernel with the distance
      * row packed in LDS, once a probe source shows every distance fits its 10-bit fields
@@ -391,7 +409,7 @@ extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begi
         rc = srt_wgsssp_rows(g->n, g->rp2, g->cw2, g->r2, g->inv, g->max_w, src_begin,
                              src_begin + 1, lat_rows, rel_rows, ovf, st);
         if (rc) return rc;
-        uint32_t* row = (uint32_t*)malloc((size_t)g->n * sizeof(uint32_t));
+        uint32_t* row = sc.row = (uint32_t*)malloc((size_t)g->n * sizeof(uint32_t));
         int pov = 1;
         if (!row) return SRT_E_NOMEM;
         SRT_HIPCHK(hipMemcpyAsync(row, lat_rows, (size_t)g->n * sizeof(uint32_t),
@@ -401,7 +419,6 @@ extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begi
         uint32_t ecc = 0;
         for (int32_t i = 0; i < g->n; i++)
             if (row[i] != SRT_INF && row[i] > ecc) ecc = row[i];
-        free(row);
         wg = !pov && 2ull * ecc <= 1022ull;
         if (wg && nsrc > 1)
             rc = srt_wgsssp_rows(g->n, g->rp2, g->cw2, g->r2, g->inv, g->max_w, src_begin + 1,
@@ -418,13 +435,14 @@ extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begi
     rc = srt_sparse_diag(g->n, src_begin, src_end, g->rp, g->col, g->w, g->r, g->sw, g->sr,
                          lat_rows, rel_rows, (size_t)g->n, st);
     if (rc) return rc;
-    int* hov = (int*)malloc((size_t)nsrc * sizeof(int));
+    int* hov = sc.hov = (int*)malloc((size_t)nsrc * sizeof(int));
     if (!hov) return SRT_E_NOMEM;
     SRT_HIPCHK(hipMemcpyAsync(hov, ovf, (size_t)nsrc * sizeof(int), hipMemcpyDeviceToHost, st));
+    sc.ovf = nullptr;
     SRT_HIPCHK(hipFreeAsync(ovf, st));
     SRT_HIPCHK(hipStreamSynchronize(st));
     int nov = 0;
-    int* ovf1 = NULL;
+    int*& ovf1 = sc.ovf1;
     for (int i = 0; i < nsrc && !rc; i++) {
         if (!hov[i]) continue;
         ++nov;
@@ -451,17 +469,12 @@ extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begi
                                          lat_rows + (size_t)i * g->n, rel_rows + (size_t)i * g->n,
                                          stream, NULL);
     }
-    if (ovf1) (void)hipFree(ovf1);
-    free(hov);
     if (rc) return rc;
     SRT_HIPCHK(hipEventRecord(e2, st));
     SRT_HIPCHK(hipEventSynchronize(e2));
     float a = 0, b = 0;
     SRT_HIPCHK(hipEventElapsedTime(&a, e0, e1));
     SRT_HIPCHK(hipEventElapsedTime(&b, e0, e2));
-    SRT_HIPCHK(hipEventDestroy(e0));
-    SRT_HIPCHK(hipEventDestroy(e1));
-    SRT_HIPCHK(hipEventDestroy(e2));
     if (nov) srt_log(SRT_LOG_INFO, "wsssp: %d of %d sources overflowed their buckets and were "
                      "recomputed by the workgroup kernel", nov, nsrc);
     if (stats) {
