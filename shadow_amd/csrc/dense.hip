@@ -450,13 +450,18 @@ __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, cons
     __shared__ T tile[64][65];
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
-    for (int a = ty; a < 64; a += 4) {
-        const int r = r0 + a, c = c0 + tx;
-        tile[a][tx] = (r < rows && c < cols) ? in[(size_t)r * ldi + c] : 0u;
+    T v[16]; /* all 16 loads in flight before the LDS stores */
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int r = r0 + ty + 4 * q, c = c0 + tx;
+        v[q] = (r < rows && c < cols) ? in[(size_t)r * ldi + c] : (T)0;
     }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) tile[ty + 4 * q][tx] = v[q];
     __syncthreads();
-    for (int a = ty; a < 64; a += 4) {
-        const int c = c0 + a, r = r0 + tx;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int a = ty + 4 * q, c = c0 + a, r = r0 + tx;
         if (r < rows && c < cols) {
             if constexpr (BM != 0)
                 out[(size_t)(r / BM) * ldo + (size_t)c * BM + (r % BM)] = (TO)tile[tx][a];
