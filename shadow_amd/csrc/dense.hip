@@ -890,13 +890,18 @@ __global__ __launch_bounds__(256) void mirror_block_kernel(int n, int ld, int b,
     while (I * (I + 1) / 2 > x) --I;
     const int J = x - I * (I + 1) / 2;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    for (int a = ty; a < 64; a += 4) {
-        int t = b + J * 64 + a, s = b + I * 64 + tx;
-        tile[a][tx] = (t < e && s < e && t < n && s < n) ? rel_rows[(size_t)(t - b) * ld + s] : 0.0;
+    double v[16]; /* all 16 loads in flight before the LDS stores */
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int t = b + J * 64 + ty + 4 * q, s = b + I * 64 + tx;
+        v[q] = (t < e && s < e && t < n && s < n) ? rel_rows[(size_t)(t - b) * ld + s] : 0.0;
     }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) tile[ty + 4 * q][tx] = v[q];
     __syncthreads();
-    for (int a = ty; a < 64; a += 4) {
-        int s = b + I * 64 + a, t = b + J * 64 + tx;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int a = ty + 4 * q, s = b + I * 64 + a, t = b + J * 64 + tx;
         if (s < e && t < e && s < n && s > t) rel_rows[(size_t)(s - b) * ld + t] = tile[tx][a];
     }
 }
