@@ -361,9 +361,14 @@ __global__ __launch_bounds__(256) void fw16_refresh_kernel(u16* __restrict__ D, 
     __shared__ u16 t[KB][KB + 2];
     FW_CHAIN_PRIO();
     const int j0 = blockIdx.x * KB, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    for (int a = ty; a < KB; a += 4) t[a][tx] = D[(size_t)(j0 + a) * ld + k0 + tx];
+    u16 v[KB / 4]; /* all loads in flight before the LDS stores */
+#pragma unroll
+    for (int q = 0; q < KB / 4; ++q) v[q] = D[(size_t)(j0 + ty + 4 * q) * ld + k0 + tx];
+#pragma unroll
+    for (int q = 0; q < KB / 4; ++q) t[ty + 4 * q][tx] = v[q];
     __syncthreads();
-    for (int a = ty; a < KB; a += 4) D[(size_t)(k0 + a) * ld + j0 + tx] = t[tx][a];
+#pragma unroll
+    for (int q = 0; q < KB / 4; ++q) D[(size_t)(k0 + ty + 4 * q) * ld + j0 + tx] = t[tx][ty + 4 * q];
 }
 
 /* SYM, after the last round: lower triangle from the upper, 64x64 tiles (I > J) */
@@ -372,9 +377,14 @@ __global__ __launch_bounds__(256) void fw16_mirror_kernel(u16* __restrict__ D, i
     const int I = blockIdx.y, J = blockIdx.x;
     if (I <= J) return;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    for (int a = ty; a < KB; a += 4) t[a][tx] = D[(size_t)(J * KB + a) * ld + I * KB + tx];
+    u16 v[KB / 4];
+#pragma unroll
+    for (int q = 0; q < KB / 4; ++q) v[q] = D[(size_t)(J * KB + ty + 4 * q) * ld + I * KB + tx];
+#pragma unroll
+    for (int q = 0; q < KB / 4; ++q) t[ty + 4 * q][tx] = v[q];
     __syncthreads();
-    for (int a = ty; a < KB; a += 4) D[(size_t)(I * KB + a) * ld + J * KB + tx] = t[tx][a];
+#pragma unroll
+    for (int q = 0; q < KB / 4; ++q) D[(size_t)(I * KB + ty + 4 * q) * ld + J * KB + tx] = t[tx][ty + 4 * q];
 }
 
 /* every 128x128 tile of the local rows: D_IJ <- min(D_IJ, D_I,k (x) P_k,J) */
