@@ -853,13 +853,21 @@ __global__ __launch_bounds__(256) void dense_diag_kernel(int n, int ld, int row0
     if (lr >= nrows || v >= n) return;
     const uint32_t* wr = w + (size_t)lr * ld;
     uint64_t best = ~0ull;
-    for (int u = lane; u < n; u += 64) {
-        uint32_t x = wr[u];
-        if (x >= SRT_INF) continue;
-        uint64_t lat = (u == v) ? x : 2ull * x;
-        uint64_t key = (lat << 32) | (uint32_t)u;
+    auto take = [&](uint32_t x, int u) {
+        if (x >= SRT_INF) return;
+        const uint64_t lat = (u == v) ? x : 2ull * x;
+        const uint64_t key = (lat << 32) | (uint32_t)u;
         best = key < best ? key : best;
+    };
+    const int n4 = n & ~3; /* rows are 16-B aligned (ld % 64 == 0): 4 columns per load */
+    for (int u = lane * 4; u < n4; u += 256) {
+        const uint4 x = *reinterpret_cast<const uint4*>(wr + u);
+        take(x.x, u);
+        take(x.y, u + 1);
+        take(x.z, u + 2);
+        take(x.w, u + 3);
     }
+    for (int u = n4 + lane; u < n; u += 64) take(wr[u], u);
     for (int off = 32; off > 0; off >>= 1) {
         uint64_t o = __shfl_xor(best, off);
         best = o < best ? o : best;
