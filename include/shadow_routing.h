@@ -95,6 +95,24 @@ int srt_build_tables_multi(const srt_edges* g, const srt_build_opts* opts, int32
                            uint32_t* lat_q, uint64_t* quantum_ns, double* rel,
                            srt_build_stats* stats);
 
+/* Tables over a vertex subset -- the vertices with attached hosts, which are the only targets the
+ * reference ever computes paths to (topology.c:1604-1656): outputs are nsub x nsub host tables
+ * whose entry [i][j] is the pair (verts[i], verts[j]); verts strictly increasing (NULL with
+ * nsub = n: every vertex). ngpus > 1 shards the build like srt_build_tables_multi.
+ * lat_ms (optional, may be NULL): the path latency as the reference's f64 millisecond sum in path
+ * order (topology.c:1308, :1364) -- differs from lat_q * quantum / 1e6 only when some edge latency
+ * has a sub-millisecond part. min_lat_q (optional): the smallest table entry, diagonal included
+ * (the runahead minimum, topology.c:1253-1264). */
+int srt_build_tables_subset(const srt_edges* g, const srt_build_opts* opts, int32_t ngpus,
+                            int32_t nsub, const int32_t* verts, uint32_t* lat_q,
+                            uint64_t* quantum_ns, double* rel, double* lat_ms, uint32_t* min_lat_q,
+                            srt_build_stats* stats);
+
+/* Largest n of the dense (Floyd-Warshall) form; SRT_ALGO_AUTO sends larger graphs, and sparse
+ * ones of any size, to the SSSP; an explicit SRT_ALGO_DENSE_FW beyond it fails with SRT_E_RANGE
+ * before any work. */
+int srt_dense_max_n(void);
+
 /* Quantum and u32-range check used by srt_build_tables. Returns SRT_OK or SRT_E_RANGE. */
 int srt_latency_quantum(const srt_edges* g, uint64_t* quantum_ns, uint32_t* max_w_q);
 
@@ -141,6 +159,11 @@ int srt_sparse_graph_info(const srt_sparse_graph* g, int32_t* n, int32_t* direct
 int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src_end,
                           uint32_t* lat_rows, double* rel_rows, void* stream,
                           srt_build_stats* stats);
+/* Rows of an arbitrary source list (srcs: nsrc device ints; row r = source srcs[r], stride n),
+ * e.g. the attached vertices. lat_ms_rows (optional): the f64 path-order ms rows. */
+int srt_sparse_graph_rows_list(const srt_sparse_graph* g, int32_t nsrc, const int32_t* srcs,
+                               uint32_t* lat_rows, double* rel_rows, double* lat_ms_rows,
+                               void* stream, srt_build_stats* stats);
 void srt_sparse_graph_free(srt_sparse_graph* g);
 /* rel[s][t] <- rel[t][s] for s > t (undirected symmetry rule), ld x ld device matrix. */
 int srt_mirror_lower_device(int32_t n, int32_t ld, double* rel, void* stream);

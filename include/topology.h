@@ -48,12 +48,25 @@ double topology_getReliability(Topology* top, Address* srcAddress, Address* dstA
 void topology_incrementPathPacketCounter(Topology* top, Address* srcAddress, Address* dstAddress);
 
 /* ---- additions behind the same ABI -------------------------------------- */
-/* Eager, idempotent all-pairs build on the GPU(s). The lookups call it lazily if needed.
- * Calls worker_updateMinTimeJump() once with the minimum path latency (topology.c:1253-1264). */
+/* Eager build on the GPU(s) of the tables over the vertices with attached hosts -- the only
+ * targets the reference computes paths to (topology.c:1604-1656) -- or over every vertex while
+ * nothing is attached. Call it after the hosts are attached (controller.c:367); it is idempotent,
+ * and the lookups call it lazily: a lookup whose vertex joined the attached set after the last
+ * build rebuilds (the reference's cache miss, topology.c:1923-1961). Hands the minimum latency
+ * over attached pairs to worker_updateMinTimeJump() (topology.c:1253-1264) once per attach
+ * generation, and only when it is below the last value handed over. */
 int topology_computeShortestPaths(Topology* top, int nGPUs);
-/* Zero-copy view of the finished tables (valid until topology_free). */
+/* Zero-copy view of the current tables (valid until topology_free): n x n over the table's
+ * vertices (srt_topology_table_info gives them; every vertex when the table is full). */
 int topology_getTable(Topology* top, const uint32_t** latQ, uint64_t* quantumNs,
                       const double** rel, int* n);
+/* The current table's vertices (increasing), their count, and the f64 path-order ms table (NULL
+ * when every edge latency is whole ms: lat_q * quantum / 1e6 is then the reference's value). */
+int srt_topology_table_info(Topology* top, const int32_t** verts, int32_t* nslot,
+                            const double** latMs);
+/* Receive the runahead minimum instead of worker_updateMinTimeJump (tests, embedders); NULL
+ * restores the Shadow call. Process-wide. */
+void srt_set_min_time_jump_hook(void (*fn)(double minPathLatencyMs));
 
 /* ---- network-order IP variants (no Shadow types; used by the Python mirror and tests) --- */
 Topology* srt_topology_new_from_string(const char* gmlText, int useShortestPath);

@@ -51,6 +51,9 @@ def lib() -> ctypes.CDLL:
         L.orc_sssp_rows.restype = ctypes.c_int
         L.orc_sssp_rows.argtypes = [ctypes.POINTER(_Graph), ctypes.c_int, ctypes.c_int32,
                                     ctypes.c_int32, ctypes.c_int] + [ctypes.c_void_p] * 5
+        L.orc_sssp_list.restype = ctypes.c_int
+        L.orc_sssp_list.argtypes = [ctypes.POINTER(_Graph), ctypes.c_int, ctypes.c_void_p,
+                                    ctypes.c_int32, ctypes.c_int] + [ctypes.c_void_p] * 5
         L.orc_table.restype = ctypes.c_int
         L.orc_table.argtypes = [ctypes.POINTER(_Graph), ctypes.c_int, ctypes.c_int,
                                 ctypes.c_int] + [ctypes.c_void_p] * 4
@@ -99,6 +102,25 @@ def sssp_rows(g: EdgeList, s0: int = 0, s1: int | None = None, mode: int = ORC_I
         raise RuntimeError("orc_sssp_rows failed")
     if want_pred:
         out["pred"] = pred
+    return out
+
+
+def sssp_list(g: EdgeList, sources, mode: int = ORC_INT_NS, nthreads: int = 1):
+    """Raw rows of an arbitrary source list: row i belongs to sources[i]."""
+    src = np.ascontiguousarray(sources, dtype=np.int32)
+    k = len(src)
+    out = {
+        "lat_int": np.empty((k, g.n), np.uint64),
+        "lat_ref": np.empty((k, g.n), np.uint64),
+        "rel": np.empty((k, g.n), np.float64),
+        "lat_ms": np.empty((k, g.n), np.float64),
+    }
+    cg = g._c()
+    rc = lib().orc_sssp_list(ctypes.byref(cg), mode, src.ctypes.data, k, nthreads,
+                             _ptr(out["lat_int"]), _ptr(out["lat_ref"]), _ptr(out["rel"]),
+                             _ptr(out["lat_ms"]), None)
+    if rc:
+        raise RuntimeError("orc_sssp_list failed")
     return out
 
 

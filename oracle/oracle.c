@@ -222,6 +222,7 @@ typedef struct {
     const orc_csr* c;
     int mode;
     int32_t s0, s1, stride, first;
+    const int32_t* list; /* sources list[i - s0] instead of i, when set */
     uint64_t* lat_int;
     uint64_t* lat_ref;
     double* rel;
@@ -242,12 +243,13 @@ static void* worker(void* arg) {
     double* rl = (double*)malloc((size_t)n * sizeof(double));
     int32_t* pr = (int32_t*)malloc((size_t)n * sizeof(int32_t));
     j->rc = (!di || !dd || !st || !li || !lm || !rl || !pr) ? -1 : 0;
-    for (int32_t s = j->s0 + j->first; s < j->s1 && j->rc == 0; s += j->stride) {
+    for (int32_t i = j->s0 + j->first; i < j->s1 && j->rc == 0; i += j->stride) {
+        const int32_t s = j->list ? j->list[i - j->s0] : i;
         if (sssp_one(j->g, j->c, j->mode, s, &H, di, dd, st, li, rl, lm, pr)) {
             j->rc = -1;
             break;
         }
-        size_t off = (size_t)(s - j->s0) * (size_t)n;
+        size_t off = (size_t)(i - j->s0) * (size_t)n;
         for (int32_t t = 0; t < n; t++) {
             if (j->lat_int) j->lat_int[off + t] = li[t];
             if (j->lat_ref) j->lat_ref[off + t] = (li[t] == UINT64_MAX) ? UINT64_MAX : ms_to_ns_ref(lm[t]);
@@ -277,7 +279,36 @@ int orc_sssp_rows(const orc_graph* g, int mode, int32_t s0, int32_t s1, int nthr
     pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
     int rc = 0;
     for (int i = 0; i < nthreads; i++) {
-        jobs[i] = (job_t){g, &c, mode, s0, s1, nthreads, i, lat_int, lat_ref, rel, lat_ms, pred, 0};
+        jobs[i] = (job_t){g, &c, mode, s0, s1, nthreads, i, NULL, lat_int, lat_ref, rel, lat_ms, pred, 0};
+        if (nthreads == 1)
+            worker(&jobs[i]);
+        else
+            pthread_create(&th[i], NULL, worker, &jobs[i]);
+    }
+    for (int i = 0; i < nthreads; i++) {
+        if (nthreads > 1) pthread_join(th[i], NULL);
+        if (jobs[i].rc) rc = -1;
+    }
+    free(jobs);
+    free(th);
+    free_csr(&c);
+    return rc;
+}
+
+/* orc_sssp_rows for an arbitrary source list: row i is source srcs[i] (sources in [0, n)) */
+int orc_sssp_list(const orc_graph* g, int mode, const int32_t* srcs, int32_t k, int nthreads,
+                  uint64_t* lat_int, uint64_t* lat_ref, double* rel, double* lat_ms, int32_t* pred) {
+    if (!g || g->n <= 0 || !srcs || k < 0) return -1;
+    for (int32_t i = 0; i < k; i++)
+        if (srcs[i] < 0 || srcs[i] >= g->n) return -1;
+    orc_csr c;
+    if (build_csr(g, &c)) return -1;
+    if (nthreads < 1) nthreads = 1;
+    job_t* jobs = (job_t*)calloc((size_t)nthreads, sizeof(job_t));
+    pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+    int rc = 0;
+    for (int i = 0; i < nthreads; i++) {
+        jobs[i] = (job_t){g, &c, mode, 0, k, nthreads, i, srcs, lat_int, lat_ref, rel, lat_ms, pred, 0};
         if (nthreads == 1)
             worker(&jobs[i]);
         else

@@ -61,6 +61,9 @@ enum { ORC_INT_NS = 0, ORC_F64_MS = 1 };
  * nthreads > 1 shards sources over pthreads. Returns 0 on success. */
 int orc_sssp_rows(const orc_graph* g, int mode, int32_t s0, int32_t s1, int nthreads,
                   uint64_t* lat_int, uint64_t* lat_ref, double* rel, double* lat_ms, int32_t* pred);
+/* orc_sssp_rows for the sources srcs[0..k): row i belongs to srcs[i] */
+int orc_sssp_list(const orc_graph* g, int mode, const int32_t* srcs, int32_t k, int nthreads,
+                  uint64_t* lat_int, uint64_t* lat_ref, double* rel, double* lat_ms, int32_t* pred);
 
 /* Full n*n table as the reference's lookup API would return it for every vertex pair:
  * shortest-path or direct mode, diagonal rule, symmetry rule. lat_ms (optional) is the f64

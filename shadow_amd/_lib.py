@@ -73,6 +73,9 @@ SIGNATURES = {
     "srt_parse_bandwidth": (_I64, [_CP]),
     "srt_build_tables": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
     "srt_build_tables_multi": (ctypes.c_int, [_VP, _VP, _I32, _VP, _VP, _VP, _VP]),
+    "srt_build_tables_subset": (ctypes.c_int, [_VP, _VP, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP,
+                                               _VP]),
+    "srt_dense_max_n": (ctypes.c_int, []),
     "srt_latency_quantum": (ctypes.c_int, [_VP, _VP, _VP]),
     "srt_dense_build_device": (ctypes.c_int, [_I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _I32, _VP]),
     "srt_gen_complete_device": (ctypes.c_int, [_I32, _I32, _I32, _I32, _U64, _U32, _U32, _U32,
@@ -84,6 +87,7 @@ SIGNATURES = {
     "srt_sparse_graph_new": (ctypes.c_int, [_VP, _I32, _VP]),
     "srt_sparse_graph_info": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
     "srt_sparse_graph_rows": (ctypes.c_int, [_VP, _I32, _I32, _VP, _VP, _VP, _VP]),
+    "srt_sparse_graph_rows_list": (ctypes.c_int, [_VP, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "srt_sparse_graph_free": (None, [_VP]),
     "srt_comm_unique_id": (ctypes.c_int, [_VP]),
     "srt_comm_init": (ctypes.c_int, [_VP, _I32, _I32, _I32, _VP]),
@@ -131,6 +135,8 @@ SIGNATURES = {
     "srt_topology_is_complete": (ctypes.c_int, [_VP]),
     "srt_topology_edges": (ctypes.c_int, [_VP, _VP]),
     "srt_topology_min_latency_ms": (_D, [_VP]),
+    "srt_topology_table_info": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
+    "srt_set_min_time_jump_hook": (None, [_VP]),
     "srt_topology_set_build_opts": (None, [_VP, _VP]),
     "srt_topology_last_stats": (ctypes.c_int, [_VP, _VP]),
 }

@@ -16,7 +16,12 @@
 
 #include "srt_device.h"
 
-int srt_sparse_max_n(void);
+int srt_sparse_block_rows(int32_t n, const int32_t* rowptr, const int32_t* col, const uint32_t* w,
+                          const double* r, const int32_t* in_rowptr, const int32_t* in_col,
+                          const uint32_t* in_w, const double* in_r, const uint32_t* self_w,
+                          const double* self_r, int32_t src_begin, int32_t src_end,
+                          const int32_t* srcs, uint32_t delta, uint32_t* lat_rows,
+                          double* rel_rows, void* stream, srt_build_stats* stats);
 
 extern "C" int srt_device_count(void) {
     int c = 0;
@@ -95,15 +100,17 @@ static void dfree(dbufs* b) {
         }                                                                                  \
     } while (0)
 
+/* AUTO: FW costs n^3 cheap register/LDS relaxations, the SSSP ~ n * arcs gathers, so dense wins
+ * once arcs are within ~1/16 of n^2 (or the graph is tiny) -- up to the dense form's size limit
+ * (srt_dense_max_n: 16-bit predecessor keys, int32 arc offsets). Everything else, of any size,
+ * takes the sparse SSSP, like the reference's per-source Dijkstra (topology.c:1578-1814). An
+ * explicit DENSE_FW request beyond the limit is refused before any work (SRT_E_RANGE). */
 static int choose_algo(const srt_canon* c, const srt_build_opts* o) {
     if (o && o->algo == SRT_ALGO_DENSE_FW) return SRT_ALGO_DENSE_FW;
     if (o && o->algo == SRT_ALGO_SPARSE_SSSP) return SRT_ALGO_SPARSE_SSSP;
     const double n = c->n;
-    /* FW costs n^3 cheap LDS relaxations; the SSSP costs ~n * arcs * (re-relaxation factor)
-     * gathers. Dense wins once arcs are within ~1/16 of n^2, or the graph is tiny. */
-    if (c->n <= 2048 || (double)c->arcs * 16.0 >= n * n) return SRT_ALGO_DENSE_FW;
-    if (c->n > srt_sparse_max_n()) return SRT_ALGO_DENSE_FW;
-    return SRT_ALGO_SPARSE_SSSP;
+    const bool dense_shape = c->n <= 2048 || (double)c->arcs * 16.0 >= n * n;
+    return dense_shape && c->n <= SRT_DENSE_MAX_N ? SRT_ALGO_DENSE_FW : SRT_ALGO_SPARSE_SSSP;
 }
 
 /* ---- device-resident sparse graph (canonical CSR uploaded once, rows computed per shard) ---- */
@@ -128,15 +135,15 @@ struct srt_sparse_graph {
 
 int srt_wgsssp_max_n(void);
 int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r, const int32_t* inv,
-                    uint32_t max_w, int src_begin, int src_end, uint32_t* lat, double* rel,
-                    int* ovf, hipStream_t st);
+                    uint32_t max_w, int src_begin, int src_end, const int32_t* srcs, uint32_t* lat,
+                    double* rel, int* ovf, hipStream_t st);
 int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, const double* r,
                    const int2* in_rowptr, const uint2* in_cw, const double* in_r,
                    const int32_t* perm, const int32_t* inv, uint32_t max_w, int local,
-                   int src_begin,
-                   int src_end, uint32_t* lat, double* rel, int* ovf, hipStream_t st);
-int srt_sparse_diag(int n, int src_begin, int src_end, const int32_t* rowptr, const int32_t* col,
-                    const uint32_t* w, const double* r, const uint32_t* self_w,
+                   int src_begin, int src_end, const int32_t* srcs, uint32_t* lat, double* rel,
+                   int* ovf, hipStream_t st);
+int srt_sparse_diag(int n, int src_begin, int src_end, const int32_t* srcs, const int32_t* rowptr,
+                    const int32_t* col, const uint32_t* w, const double* r, const uint32_t* self_w,
                     const double* self_r, uint32_t* lat, double* rel, size_t ldo, hipStream_t st);
 
 static int up(void** d, const void* h, size_t bytes) {
@@ -353,26 +360,36 @@ extern "C" int srt_sparse_graph_info(const srt_sparse_graph* g, int32_t* n, int3
     return SRT_OK;
 }
 
-/* Rows of a source range: the wave-per-source bucket kernel (wsssp.hip) when the arc weights fit
- * its bucket ring, with any source whose buckets overflowed recomputed by the
- * workgroup-per-source kernel (sparse.hip); SRT_SPARSE_KERNEL=block (or SRT_SPARSE_WORKSET=hbm)
- * selects the workgroup kernel for every source. */
-extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src_end,
-                                     uint32_t* lat_rows, double* rel_rows, void* stream,
-                                     srt_build_stats* stats) {
-    if (!g) {
-        srt_set_error("srt_sparse_graph_rows: null graph");
+/* Rows of nsrc sources (the device list srcs, or [src_begin, src_end) when srcs is NULL): the
+ * wave-per-source bucket kernel (wsssp.hip) when the arc weights fit its bucket ring, or the
+ * workgroup kernel with the row packed in LDS on large power-law graphs; any source whose buckets
+ * overflowed is recomputed (wave kernel, then the workgroup-per-source kernel of sparse.hip).
+ * SRT_SPARSE_KERNEL=block (or SRT_SPARSE_WORKSET=hbm) selects the sparse.hip kernel for every
+ * source. lms (optional): the f64 path-order ms rows (tables.hip), q the quantum in ns. */
+static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src_end,
+                       const int32_t* srcs, uint32_t* lat_rows, double* rel_rows, double* lms,
+                       hipStream_t st, srt_build_stats* stats) {
+    if (!g || src_begin < 0 || src_begin >= src_end || (!srcs && src_end > g->n)) {
+        srt_set_error("sparse rows: bad source range [%d, %d)", src_begin, src_end);
         return SRT_E_ARG;
     }
+    const int nsrc = src_end - src_begin;
+    /* source i of this call: srcs + i, or the range */
+    auto one = [&](int i) { return srcs ? srcs + i : (const int32_t*)NULL; };
+    const int b0 = srcs ? 0 : src_begin;
     const char* kenv = getenv("SRT_SPARSE_KERNEL");
     const char* wenv = getenv("SRT_SPARSE_WORKSET");
     const bool block = (kenv && !strcmp(kenv, "block")) || (wenv && !strcmp(wenv, "hbm"));
-    if (block || g->max_w >= 256 || src_begin < 0 || src_end > g->n || src_begin >= src_end)
-        return srt_sparse_build_device(g->n, g->directed, g->rp, g->col, g->w, g->r, g->irp,
-                                       g->icol, g->iw, g->ir, g->sw, g->sr, src_begin, src_end,
-                                       g->delta, lat_rows, rel_rows, stream, stats);
-    hipStream_t st = (hipStream_t)stream;
-    const int nsrc = src_end - src_begin;
+    int rc = SRT_OK;
+    if (block || g->max_w >= 256) {
+        rc = srt_sparse_block_rows(g->n, g->rp, g->col, g->w, g->r, g->irp, g->icol, g->iw, g->ir,
+                                   g->sw, g->sr, b0, b0 + nsrc, srcs, g->delta, lat_rows, rel_rows,
+                                   st, stats);
+        if (!rc && lms)
+            rc = srt_path_ms_rows(g->n, nsrc, srcs, b0, lat_rows, (size_t)g->n, NULL, 0, g->irp,
+                                  g->icol, g->iw, g->quantum_ns, lms, (size_t)g->n, st);
+        return rc;
+    }
     /* events, the overflow flags and host buffers are released on every return path */
     struct rows_scratch {
         hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -404,10 +421,9 @@ extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begi
     const char* genv = getenv("SRT_SPARSE_WG");
     bool wg = !g->directed && g->n <= srt_wgsssp_max_n() &&
               (genv ? atoi(genv) != 0 : (g->n > 32768 && !g->local));
-    int rc = SRT_OK;
     if (wg) {
-        rc = srt_wgsssp_rows(g->n, g->rp2, g->cw2, g->r2, g->inv, g->max_w, src_begin,
-                             src_begin + 1, lat_rows, rel_rows, ovf, st);
+        rc = srt_wgsssp_rows(g->n, g->rp2, g->cw2, g->r2, g->inv, g->max_w, b0, b0 + 1, one(0),
+                             lat_rows, rel_rows, ovf, st);
         if (rc) return rc;
         uint32_t* row = sc.row = (uint32_t*)malloc((size_t)g->n * sizeof(uint32_t));
         int pov = 1;
@@ -421,18 +437,18 @@ extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begi
             if (row[i] != SRT_INF && row[i] > ecc) ecc = row[i];
         wg = !pov && 2ull * ecc <= 1022ull;
         if (wg && nsrc > 1)
-            rc = srt_wgsssp_rows(g->n, g->rp2, g->cw2, g->r2, g->inv, g->max_w, src_begin + 1,
-                                 src_end, lat_rows + (size_t)g->n, rel_rows + (size_t)g->n, ovf + 1,
+            rc = srt_wgsssp_rows(g->n, g->rp2, g->cw2, g->r2, g->inv, g->max_w, b0 + 1, b0 + nsrc,
+                                 one(1), lat_rows + (size_t)g->n, rel_rows + (size_t)g->n, ovf + 1,
                                  st);
         if (rc) return rc;
     }
     if (!wg)
         rc = srt_wsssp_rows(g->n, g->directed, g->rp2, g->cw2, g->r2, g->irp2, g->icw2, g->ir2,
-                            g->perm, g->inv, g->max_w, g->local, src_begin, src_end, lat_rows,
+                            g->perm, g->inv, g->max_w, g->local, b0, b0 + nsrc, srcs, lat_rows,
                             rel_rows, ovf, st);
     if (rc) return rc;
     SRT_HIPCHK(hipEventRecord(e1, st));
-    rc = srt_sparse_diag(g->n, src_begin, src_end, g->rp, g->col, g->w, g->r, g->sw, g->sr,
+    rc = srt_sparse_diag(g->n, b0, b0 + nsrc, srcs, g->rp, g->col, g->w, g->r, g->sw, g->sr,
                          lat_rows, rel_rows, (size_t)g->n, st);
     if (rc) return rc;
     int* hov = sc.hov = (int*)malloc((size_t)nsrc * sizeof(int));
@@ -446,37 +462,39 @@ extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begi
     for (int i = 0; i < nsrc && !rc; i++) {
         if (!hov[i]) continue;
         ++nov;
+        uint32_t* lr = lat_rows + (size_t)i * g->n;
+        double* rr = rel_rows + (size_t)i * g->n;
         int again = 1;
         if (wg) { /* the workgroup kernel's overflow: the wave kernel first */
             if (!ovf1) SRT_HIPCHK(hipMalloc((void**)&ovf1, sizeof(int)));
             rc = srt_wsssp_rows(g->n, g->directed, g->rp2, g->cw2, g->r2, g->irp2, g->icw2, g->ir2,
-                                g->perm, g->inv, g->max_w, g->local, src_begin + i,
-                                src_begin + i + 1, lat_rows + (size_t)i * g->n,
-                                rel_rows + (size_t)i * g->n, ovf1, st);
+                                g->perm, g->inv, g->max_w, g->local, b0 + i, b0 + i + 1, one(i), lr,
+                                rr, ovf1, st);
             if (!rc && hipMemcpyAsync(&again, ovf1, sizeof(int), hipMemcpyDeviceToHost, st) ==
                            hipSuccess &&
                 hipStreamSynchronize(st) != hipSuccess)
                 rc = SRT_E_DEVICE;
             if (!rc && !again) /* the wave kernel wrote the row; the diagonal rule again */
-                rc = srt_sparse_diag(g->n, src_begin + i, src_begin + i + 1, g->rp, g->col, g->w,
-                                     g->r, g->sw, g->sr, lat_rows + (size_t)i * g->n,
-                                     rel_rows + (size_t)i * g->n, (size_t)g->n, st);
+                rc = srt_sparse_diag(g->n, b0 + i, b0 + i + 1, one(i), g->rp, g->col, g->w, g->r,
+                                     g->sw, g->sr, lr, rr, (size_t)g->n, st);
         }
         if (!rc && again)
-            rc = srt_sparse_build_device(g->n, g->directed, g->rp, g->col, g->w, g->r, g->irp,
-                                         g->icol, g->iw, g->ir, g->sw, g->sr, src_begin + i,
-                                         src_begin + i + 1, g->delta,
-                                         lat_rows + (size_t)i * g->n, rel_rows + (size_t)i * g->n,
-                                         stream, NULL);
+            rc = srt_sparse_block_rows(g->n, g->rp, g->col, g->w, g->r, g->irp, g->icol, g->iw,
+                                       g->ir, g->sw, g->sr, b0 + i, b0 + i + 1, one(i), g->delta,
+                                       lr, rr, st, NULL);
     }
     if (rc) return rc;
+    if (lms &&
+        (rc = srt_path_ms_rows(g->n, nsrc, srcs, b0, lat_rows, (size_t)g->n, NULL, 0, g->irp,
+                               g->icol, g->iw, g->quantum_ns, lms, (size_t)g->n, st)))
+        return rc;
     SRT_HIPCHK(hipEventRecord(e2, st));
     SRT_HIPCHK(hipEventSynchronize(e2));
     float a = 0, b = 0;
     SRT_HIPCHK(hipEventElapsedTime(&a, e0, e1));
     SRT_HIPCHK(hipEventElapsedTime(&b, e0, e2));
     if (nov) srt_log(SRT_LOG_INFO, "wsssp: %d of %d sources overflowed their buckets and were "
-                     "recomputed by the workgroup kernel", nov, nsrc);
+                     "recomputed", nov, nsrc);
     if (stats) {
         stats->algo = SRT_ALGO_SPARSE_SSSP;
         stats->ms_fw = b;
@@ -489,29 +507,120 @@ extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begi
     return SRT_OK;
 }
 
-extern "C" int srt_build_tables(const srt_edges* g, const srt_build_opts* opts, uint32_t* lat_q,
-                                uint64_t* quantum_ns, double* rel, srt_build_stats* stats) {
-    if (!g || !lat_q || !quantum_ns || !rel) {
-        srt_set_error("srt_build_tables: null argument");
+extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src_end,
+                                     uint32_t* lat_rows, double* rel_rows, void* stream,
+                                     srt_build_stats* stats) {
+    if (!g) {
+        srt_set_error("srt_sparse_graph_rows: null graph");
         return SRT_E_ARG;
     }
-    srt_canon c;
-    int rc = srt_canon_build(g, &c);
-    if (rc) return rc;
-    *quantum_ns = c.quantum_ns;
-    const int n = c.n;
+    return sparse_rows(g, src_begin, src_end, NULL, lat_rows, rel_rows, NULL, (hipStream_t)stream,
+                       stats);
+}
+
+extern "C" int srt_sparse_graph_rows_list(const srt_sparse_graph* g, int32_t nsrc,
+                                          const int32_t* srcs, uint32_t* lat_rows, double* rel_rows,
+                                          double* lat_ms_rows, void* stream,
+                                          srt_build_stats* stats) {
+    if (!g || nsrc <= 0 || !srcs || !lat_rows || !rel_rows) {
+        srt_set_error("srt_sparse_graph_rows_list: bad arguments");
+        return SRT_E_ARG;
+    }
+    return sparse_rows(g, 0, nsrc, srcs, lat_rows, rel_rows, lat_ms_rows, (hipStream_t)stream, stats);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Table build over a vertex subset (the attached vertices, topology.c:1604-1656): entry [i][j]  */
+/* is the pair (verts[i], verts[j]); verts strictly increasing, so the subset keeps vertex       */
+/* order and the undirected rule "pair computed from min(s, t)" is the sub-table's upper         */
+/* triangle. verts == NULL: every vertex (nsub = n).                                             */
+/* ------------------------------------------------------------------------------------------ */
+static void merge_stats(srt_build_stats* acc, const srt_build_stats* s, int first) {
+    if (first) {
+        *acc = *s;
+        return;
+    }
+    acc->ms_total += s->ms_total;
+    acc->ms_fw += s->ms_fw;
+    acc->ms_post += s->ms_post;
+    acc->ms_update += s->ms_update;
+    acc->n_update += s->n_update;
+    acc->ess_arcs += s->ess_arcs;
+    acc->max_depth = s->max_depth > acc->max_depth ? s->max_depth : acc->max_depth;
+    if (s->dist_enc < acc->dist_enc) acc->dist_enc = s->dist_enc;
+}
+
+static int check_verts(int n, int nsub, const int32_t* verts) {
+    if (!verts) return nsub == n ? SRT_OK : SRT_E_ARG;
+    if (nsub < 1 || nsub > n) return SRT_E_ARG;
+    for (int i = 0; i < nsub; i++)
+        if (verts[i] < 0 || verts[i] >= n || (i && verts[i] <= verts[i - 1])) return SRT_E_ARG;
+    return SRT_OK;
+}
+
+/* device memory left for row chunks after `reserved` bytes, capped */
+static size_t chunk_budget(size_t reserved) {
+    size_t free_b = 0, total_b = 0;
+    size_t budget = (size_t)8 << 30;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > reserved + ((size_t)12 << 30)) {
+        budget = free_b - reserved - ((size_t)12 << 30);
+        if (budget > ((size_t)48 << 30)) budget = (size_t)48 << 30;
+    }
+    return budget;
+}
+
+static void dense_host_matrices(const srt_canon* c, int ld, uint32_t* hw, double* hr) {
+    const size_t ll = (size_t)ld * ld;
+    for (size_t i = 0; i < ll; i++) {
+        hw[i] = SRT_INF;
+        hr[i] = 0.0;
+    }
+    for (int u = 0; u < c->n; u++) {
+        for (int k = c->rowptr[u]; k < c->rowptr[u + 1]; k++) {
+            hw[(size_t)u * ld + c->col[k]] = c->w[k];
+            hr[(size_t)u * ld + c->col[k]] = c->r[k];
+        }
+        hw[(size_t)u * ld + u] = c->self_w[u];
+        hr[(size_t)u * ld + u] = c->self_r[u];
+    }
+}
+
+/* one GPU */
+static int build_one(const srt_canon* c, const srt_build_opts* opts, int algo, int nsub,
+                     const int32_t* verts, uint32_t* lat_q, double* rel, double* lat_ms,
+                     uint32_t* min_q, srt_build_stats* stats) {
+    const int n = c->n;
     const int use_sp = opts ? opts->use_shortest_path : 1;
-    int algo = use_sp ? choose_algo(&c, opts) : SRT_ALGO_DENSE_FW;
+    const uint64_t q = c->quantum_ns;
     srt_build_stats local;
     memset(&local, 0, sizeof(local));
+    if (stats) local.time_kernels = stats->time_kernels;
     dbufs B;
     B.k = 0;
     hipStream_t st = NULL;
     uint32_t* hw = NULL;
     double* hr = NULL;
+    int32_t* dverts = NULL;
+    uint32_t* dmin = NULL;
+    uint32_t *slat = NULL, *dlat = NULL;
+    double *srel = NULL, *sms = NULL, *drel = NULL, *dms = NULL;
+    const size_t ns2 = (size_t)nsub * nsub;
+    int rc = SRT_OK;
     TRYHIP(hipSetDevice(opts ? opts->device : 0));
     TRYHIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    if (algo == SRT_ALGO_DENSE_FW) {
+    TRY(dalloc(&B, (void**)&dmin, sizeof(uint32_t)));
+    TRYHIP(hipMemsetAsync(dmin, 0xFF, sizeof(uint32_t), st));
+    if (verts) {
+        TRY(dalloc(&B, (void**)&dverts, (size_t)nsub * sizeof(int32_t)));
+        TRYHIP(hipMemcpyAsync(dverts, verts, (size_t)nsub * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    }
+    if (!use_sp || algo == SRT_ALGO_DENSE_FW) {
+        if (n > SRT_DENSE_MAX_N) {
+            srt_set_error("dense build supports n <= %d (n = %d); use the sparse SSSP",
+                          SRT_DENSE_MAX_N, n);
+            rc = SRT_E_RANGE;
+            goto out;
+        }
         const int ld = srt_ceil_div(n, 128) * 128; /* the u16 FW tiles need ld % 128 == 0 */
         const size_t ll = (size_t)ld * ld;
         hw = (uint32_t*)malloc(ll * sizeof(uint32_t));
@@ -520,42 +629,54 @@ extern "C" int srt_build_tables(const srt_edges* g, const srt_build_opts* opts, 
             rc = SRT_E_NOMEM;
             goto out;
         }
-        for (size_t i = 0; i < ll; i++) {
-            hw[i] = SRT_INF;
-            hr[i] = 0.0;
-        }
-        for (int u = 0; u < n; u++) {
-            for (int k = c.rowptr[u]; k < c.rowptr[u + 1]; k++) {
-                hw[(size_t)u * ld + c.col[k]] = c.w[k];
-                hr[(size_t)u * ld + c.col[k]] = c.r[k];
-            }
-            hw[(size_t)u * ld + u] = c.self_w[u];
-            hr[(size_t)u * ld + u] = c.self_r[u];
-        }
-        uint32_t *dw, *dlat;
-        double *dr, *drel;
+        dense_host_matrices(c, ld, hw, hr);
+        uint32_t* dw;
+        double* dr;
         TRY(dalloc(&B, (void**)&dw, ll * sizeof(uint32_t)));
         TRY(dalloc(&B, (void**)&dr, ll * sizeof(double)));
         TRY(dalloc(&B, (void**)&dlat, ll * sizeof(uint32_t)));
         TRY(dalloc(&B, (void**)&drel, ll * sizeof(double)));
+        if (lat_ms) TRY(dalloc(&B, (void**)&dms, ll * sizeof(double)));
         TRYHIP(hipMemcpyAsync(dw, hw, ll * sizeof(uint32_t), hipMemcpyHostToDevice, st));
         TRYHIP(hipMemcpyAsync(dr, hr, ll * sizeof(double), hipMemcpyHostToDevice, st));
         if (use_sp) {
-            TRY(srt_dense_build_device(n, ld, c.directed, dw, dr, dlat, drel, st,
-                                       opts ? opts->fw_block : 0, &local));
+            TRY(srt_dense_build_device_ms(n, ld, c->directed, dw, dr, dlat, drel, dms, q, st,
+                                          opts ? opts->fw_block : 0, &local));
         } else {
-            /* direct mode: the (complete) graph's own edges, self-loop on the diagonal */
+            /* direct mode (topology.c:1816-1858): the (complete) graph's own edges, the self-loop
+             * on the diagonal */
             TRYHIP(hipMemcpyAsync(dlat, dw, ll * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
             TRYHIP(hipMemcpyAsync(drel, dr, ll * sizeof(double), hipMemcpyDeviceToDevice, st));
+            if (dms) TRY(srt_quanta_to_ms(n, n, dw, ld, q, dms, ld, st));
             local.algo = SRT_ALGO_DENSE_FW;
         }
-        TRYHIP(hipMemcpy2DAsync(lat_q, (size_t)n * sizeof(uint32_t), dlat, (size_t)ld * sizeof(uint32_t),
-                                (size_t)n * sizeof(uint32_t), n, hipMemcpyDeviceToHost, st));
-        TRYHIP(hipMemcpy2DAsync(rel, (size_t)n * sizeof(double), drel, (size_t)ld * sizeof(double),
-                                (size_t)n * sizeof(double), n, hipMemcpyDeviceToHost, st));
+        if (verts) {
+            TRY(dalloc(&B, (void**)&slat, ns2 * sizeof(uint32_t)));
+            TRY(dalloc(&B, (void**)&srel, ns2 * sizeof(double)));
+            TRY(srt_gather_sub_u32(nsub, nsub, dverts, dverts, dlat, ld, slat, nsub, st));
+            TRY(srt_gather_sub_f64(nsub, nsub, dverts, dverts, drel, ld, srel, nsub, st));
+            if (dms) {
+                TRY(dalloc(&B, (void**)&sms, ns2 * sizeof(double)));
+                TRY(srt_gather_sub_f64(nsub, nsub, dverts, dverts, dms, ld, sms, nsub, st));
+            }
+            TRY(srt_table_min(nsub, nsub, slat, nsub, dmin, st));
+            TRYHIP(hipMemcpyAsync(lat_q, slat, ns2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+            TRYHIP(hipMemcpyAsync(rel, srel, ns2 * sizeof(double), hipMemcpyDeviceToHost, st));
+            if (sms) TRYHIP(hipMemcpyAsync(lat_ms, sms, ns2 * sizeof(double), hipMemcpyDeviceToHost, st));
+        } else {
+            TRY(srt_table_min(n, n, dlat, ld, dmin, st));
+            TRYHIP(hipMemcpy2DAsync(lat_q, (size_t)n * sizeof(uint32_t), dlat, (size_t)ld * sizeof(uint32_t),
+                                    (size_t)n * sizeof(uint32_t), n, hipMemcpyDeviceToHost, st));
+            TRYHIP(hipMemcpy2DAsync(rel, (size_t)n * sizeof(double), drel, (size_t)ld * sizeof(double),
+                                    (size_t)n * sizeof(double), n, hipMemcpyDeviceToHost, st));
+            if (dms)
+                TRYHIP(hipMemcpy2DAsync(lat_ms, (size_t)n * sizeof(double), dms, (size_t)ld * sizeof(double),
+                                        (size_t)n * sizeof(double), n, hipMemcpyDeviceToHost, st));
+        }
+        TRYHIP(hipMemcpyAsync(min_q, dmin, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         TRYHIP(hipStreamSynchronize(st));
         if (!use_sp) {
-            for (size_t i = 0; i < (size_t)n * n; i++)
+            for (size_t i = 0; i < ns2; i++)
                 if (lat_q[i] >= SRT_INF) {
                     srt_set_error("use_shortest_path=false requires a complete graph");
                     rc = SRT_E_INVALID;
@@ -563,19 +684,46 @@ extern "C" int srt_build_tables(const srt_edges* g, const srt_build_opts* opts, 
                 }
         }
     } else {
-        const size_t nn = (size_t)n * n;
         srt_sparse_graph* sg = NULL;
-        uint32_t* d_lat;
-        double* d_rel;
-        TRY(sparse_graph_from_canon(&c, opts ? opts->device : 0, &sg));
-        rc = dalloc(&B, (void**)&d_lat, nn * sizeof(uint32_t));
-        if (!rc) rc = dalloc(&B, (void**)&d_rel, nn * sizeof(double));
-        if (!rc) rc = srt_sparse_graph_rows(sg, 0, n, d_lat, d_rel, st, &local);
-        if (!rc && !c.directed) rc = srt_mirror_lower_device(n, n, d_rel, st);
+        TRY(sparse_graph_from_canon(c, opts ? opts->device : 0, &sg));
+        /* the sub-table (every source row of the subset, its columns) stays on the device for the
+         * symmetry mirror; the full-width rows of a chunk of sources are gathered into it */
+        const size_t per_row = (size_t)n * (sizeof(uint32_t) + sizeof(double) + (lat_ms ? sizeof(double) : 0));
+        rc = dalloc(&B, (void**)&slat, ns2 * sizeof(uint32_t));
+        if (!rc) rc = dalloc(&B, (void**)&srel, ns2 * sizeof(double));
+        if (!rc && lat_ms) rc = dalloc(&B, (void**)&sms, ns2 * sizeof(double));
+        int chunk = nsub;
+        if (!rc && verts) {
+            const size_t cb = chunk_budget(0) / per_row;
+            chunk = (int)(cb < (size_t)nsub ? (cb > 0 ? cb : 1) : (size_t)nsub);
+            rc = dalloc(&B, (void**)&dlat, (size_t)chunk * n * sizeof(uint32_t));
+            if (!rc) rc = dalloc(&B, (void**)&drel, (size_t)chunk * n * sizeof(double));
+            if (!rc && lat_ms) rc = dalloc(&B, (void**)&dms, (size_t)chunk * n * sizeof(double));
+        }
+        for (int r0 = 0; r0 < nsub && !rc; r0 += chunk) {
+            const int r1 = r0 + chunk < nsub ? r0 + chunk : nsub;
+            srt_build_stats cs;
+            memset(&cs, 0, sizeof(cs));
+            if (verts) {
+                rc = sparse_rows(sg, 0, r1 - r0, dverts + r0, dlat, drel, dms, st, &cs);
+                if (!rc) rc = srt_gather_sub_u32(r1 - r0, nsub, NULL, dverts, dlat, n, slat + (size_t)r0 * nsub, nsub, st);
+                if (!rc) rc = srt_gather_sub_f64(r1 - r0, nsub, NULL, dverts, drel, n, srel + (size_t)r0 * nsub, nsub, st);
+                if (!rc && dms) rc = srt_gather_sub_f64(r1 - r0, nsub, NULL, dverts, dms, n, sms + (size_t)r0 * nsub, nsub, st);
+            } else {
+                rc = sparse_rows(sg, r0, r1, NULL, slat + (size_t)r0 * n, srel + (size_t)r0 * n,
+                                 sms ? sms + (size_t)r0 * n : NULL, st, &cs);
+            }
+            merge_stats(&local, &cs, r0 == 0);
+        }
+        if (!rc && !c->directed) rc = srt_mirror_lower_device(nsub, nsub, srel, st);
+        if (!rc && !c->directed && sms) rc = srt_mirror_lower_device(nsub, nsub, sms, st);
+        if (!rc) rc = srt_table_min(nsub, nsub, slat, nsub, dmin, st);
         srt_sparse_graph_free(sg);
         if (rc) goto out;
-        TRYHIP(hipMemcpyAsync(lat_q, d_lat, nn * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        TRYHIP(hipMemcpyAsync(rel, d_rel, nn * sizeof(double), hipMemcpyDeviceToHost, st));
+        TRYHIP(hipMemcpyAsync(lat_q, slat, ns2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        TRYHIP(hipMemcpyAsync(rel, srel, ns2 * sizeof(double), hipMemcpyDeviceToHost, st));
+        if (sms) TRYHIP(hipMemcpyAsync(lat_ms, sms, ns2 * sizeof(double), hipMemcpyDeviceToHost, st));
+        TRYHIP(hipMemcpyAsync(min_q, dmin, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         TRYHIP(hipStreamSynchronize(st));
     }
     if (stats) *stats = local;
@@ -587,26 +735,36 @@ out:
     dfree(&B);
     free(hw);
     free(hr);
-    srt_canon_free(&c);
     return rc;
 }
 
 /* ------------------------------------------------------------------------------------------ */
 /* In-process multi-GPU build (Shadow is one process): one host thread per GPU, RCCL           */
 /* communicators from ncclCommInitAll, the same sharded kernels as the one-process-per-GPU     */
-/* path (dense: row shards + pivot-panel broadcast; sparse: source shards + allgather).        */
+/* path (dense: row shards + pivot-panel broadcast; sparse: source shards + all-gather).       */
 /* ------------------------------------------------------------------------------------------ */
 #include <pthread.h>
 
 typedef struct {
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    int state; /* 0 wait, 1 go, -1 abort */
+} start_gate;
+
+typedef struct {
     int rank, R, dev, directed, algo, n, ld;
     int virt; /* virtual ranks on one device: per-rank state slots */
+    start_gate* gate;
     srt_comm* comm;
     const srt_canon* c;
     const uint32_t* hw; /* dense: host w/r matrices, ld x ld */
     const double* hr;
-    uint32_t* lat_q; /* host outputs, n x n */
+    int nsub;
+    const int32_t* verts; /* host subset (NULL: all vertices) */
+    uint32_t* lat_q;      /* host outputs, nsub x nsub */
     double* rel;
+    double* lat_ms;
+    uint32_t min_q;
     int rc;
     char err[256];
     srt_build_stats st;
@@ -617,18 +775,29 @@ static void mjob_fail(mjob* j, int rc) {
     snprintf(j->err, sizeof(j->err), "%s", srt_last_error());
 }
 
+/* every rank thread starts only once all R exist: a rank that never started cannot leave the
+ * others waiting in a collective */
+static int gate_wait(start_gate* g) {
+    pthread_mutex_lock(&g->mu);
+    while (g->state == 0) pthread_cond_wait(&g->cv, &g->mu);
+    const int s = g->state;
+    pthread_mutex_unlock(&g->mu);
+    return s;
+}
+
 static void* mjob_dense(void* p) {
     mjob* j = (mjob*)p;
+    if (gate_wait(j->gate) < 0) return NULL;
     int rc = SRT_OK;
     dbufs B;
     B.k = 0;
     hipStream_t st = NULL;
     int32_t b, e;
     srt_shard_rows(j->ld, SRT_SHARD_ALIGN, j->R, j->rank, &b, &e);
-    const int nr = e - b;
+    const int nr = e - b, n = j->n, nsub = j->nsub;
     const size_t rows = (size_t)(nr > 0 ? nr : 1) * j->ld;
-    uint32_t *dw, *dlat;
-    double *dr, *drel;
+    uint32_t *dw, *dlat, *dmin;
+    double *dr, *drel, *dms = NULL;
     srt_set_virtual_slot(j->virt ? j->rank : -1);
     TRYHIP(hipSetDevice(j->dev));
     TRYHIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -636,23 +805,79 @@ static void* mjob_dense(void* p) {
     TRY(dalloc(&B, (void**)&dr, rows * sizeof(double)));
     TRY(dalloc(&B, (void**)&dlat, rows * sizeof(uint32_t)));
     TRY(dalloc(&B, (void**)&drel, rows * sizeof(double)));
+    TRY(dalloc(&B, (void**)&dmin, sizeof(uint32_t)));
+    if (j->lat_ms) TRY(dalloc(&B, (void**)&dms, rows * sizeof(double)));
+    TRYHIP(hipMemsetAsync(dmin, 0xFF, sizeof(uint32_t), st));
     if (nr > 0) {
         TRYHIP(hipMemcpyAsync(dw, j->hw + (size_t)b * j->ld, (size_t)nr * j->ld * sizeof(uint32_t),
                               hipMemcpyHostToDevice, st));
         TRYHIP(hipMemcpyAsync(dr, j->hr + (size_t)b * j->ld, (size_t)nr * j->ld * sizeof(double),
                               hipMemcpyHostToDevice, st));
     }
-    TRY(srt_dense_build_sharded(j->comm, j->n, j->ld, j->directed, dw, dr, dlat, drel, st, 0, &j->st));
+    TRY(srt_dense_build_sharded_ms(j->comm, n, j->ld, j->directed, dw, dr, dlat, drel, dms,
+                                   j->c->quantum_ns, st, 0, &j->st));
     {
-        const int r1 = e < j->n ? e : j->n;
-        if (r1 > b) {
-            TRYHIP(hipMemcpy2DAsync(j->lat_q + (size_t)b * j->n, (size_t)j->n * sizeof(uint32_t), dlat,
-                                    (size_t)j->ld * sizeof(uint32_t), (size_t)j->n * sizeof(uint32_t),
-                                    r1 - b, hipMemcpyDeviceToHost, st));
-            TRYHIP(hipMemcpy2DAsync(j->rel + (size_t)b * j->n, (size_t)j->n * sizeof(double), drel,
-                                    (size_t)j->ld * sizeof(double), (size_t)j->n * sizeof(double),
-                                    r1 - b, hipMemcpyDeviceToHost, st));
+        /* this rank's rows of the (sub-)table: slots whose vertex lies in [b, min(e, n)) */
+        const int r1 = e < n ? e : n;
+        int i0 = 0, i1 = 0;
+        if (j->verts) {
+            while (i0 < nsub && j->verts[i0] < b) i0++;
+            i1 = i0;
+            while (i1 < nsub && j->verts[i1] < r1) i1++;
+        } else {
+            i0 = b < n ? b : n;
+            i1 = r1 > i0 ? r1 : i0;
         }
+        const int cnt = i1 - i0;
+        if (cnt > 0 && j->verts) {
+            int32_t* hrows = (int32_t*)malloc((size_t)cnt * sizeof(int32_t));
+            if (!hrows) {
+                rc = SRT_E_NOMEM;
+                goto out;
+            }
+            for (int i = 0; i < cnt; i++) hrows[i] = j->verts[i0 + i] - b;
+            int32_t *drows, *dcols;
+            uint32_t* sl;
+            double *sr, *sm = NULL;
+            rc = dalloc(&B, (void**)&drows, (size_t)cnt * sizeof(int32_t));
+            if (!rc) rc = dalloc(&B, (void**)&dcols, (size_t)nsub * sizeof(int32_t));
+            if (!rc && hipMemcpyAsync(drows, hrows, (size_t)cnt * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess)
+                rc = SRT_E_DEVICE;
+            if (!rc && hipMemcpyAsync(dcols, j->verts, (size_t)nsub * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess)
+                rc = SRT_E_DEVICE;
+            if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = SRT_E_DEVICE;
+            free(hrows);
+            if (rc) goto out;
+            TRY(dalloc(&B, (void**)&sl, (size_t)cnt * nsub * sizeof(uint32_t)));
+            TRY(dalloc(&B, (void**)&sr, (size_t)cnt * nsub * sizeof(double)));
+            TRY(srt_gather_sub_u32(cnt, nsub, drows, dcols, dlat, j->ld, sl, nsub, st));
+            TRY(srt_gather_sub_f64(cnt, nsub, drows, dcols, drel, j->ld, sr, nsub, st));
+            if (dms) {
+                TRY(dalloc(&B, (void**)&sm, (size_t)cnt * nsub * sizeof(double)));
+                TRY(srt_gather_sub_f64(cnt, nsub, drows, dcols, dms, j->ld, sm, nsub, st));
+            }
+            TRY(srt_table_min(cnt, nsub, sl, nsub, dmin, st));
+            TRYHIP(hipMemcpyAsync(j->lat_q + (size_t)i0 * nsub, sl, (size_t)cnt * nsub * sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost, st));
+            TRYHIP(hipMemcpyAsync(j->rel + (size_t)i0 * nsub, sr, (size_t)cnt * nsub * sizeof(double),
+                                  hipMemcpyDeviceToHost, st));
+            if (sm)
+                TRYHIP(hipMemcpyAsync(j->lat_ms + (size_t)i0 * nsub, sm, (size_t)cnt * nsub * sizeof(double),
+                                      hipMemcpyDeviceToHost, st));
+        } else if (cnt > 0) {
+            TRY(srt_table_min(cnt, n, dlat, j->ld, dmin, st));
+            TRYHIP(hipMemcpy2DAsync(j->lat_q + (size_t)i0 * n, (size_t)n * sizeof(uint32_t), dlat,
+                                    (size_t)j->ld * sizeof(uint32_t), (size_t)n * sizeof(uint32_t),
+                                    cnt, hipMemcpyDeviceToHost, st));
+            TRYHIP(hipMemcpy2DAsync(j->rel + (size_t)i0 * n, (size_t)n * sizeof(double), drel,
+                                    (size_t)j->ld * sizeof(double), (size_t)n * sizeof(double), cnt,
+                                    hipMemcpyDeviceToHost, st));
+            if (dms)
+                TRYHIP(hipMemcpy2DAsync(j->lat_ms + (size_t)i0 * n, (size_t)n * sizeof(double), dms,
+                                        (size_t)j->ld * sizeof(double), (size_t)n * sizeof(double),
+                                        cnt, hipMemcpyDeviceToHost, st));
+        }
+        TRYHIP(hipMemcpyAsync(&j->min_q, dmin, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         TRYHIP(hipStreamSynchronize(st));
     }
 out:
@@ -664,33 +889,71 @@ out:
 
 static void* mjob_sparse(void* p) {
     mjob* j = (mjob*)p;
+    if (gate_wait(j->gate) < 0) return NULL;
     int rc = SRT_OK;
     dbufs B;
     B.k = 0;
     hipStream_t st = NULL;
     srt_sparse_graph* sg = NULL;
-    const int n = j->n, per = srt_ceil_div(n, j->R);
-    const int s0 = j->rank * per, s1 = (s0 + per < n) ? s0 + per : n;
-    const size_t all = (size_t)per * j->R * n;
-    uint32_t* dlat;
-    double* drel;
+    const int n = j->n, nsub = j->nsub, per = srt_ceil_div(nsub, j->R);
+    const int s0 = j->rank * per < nsub ? j->rank * per : nsub;
+    const int s1 = (s0 + per < nsub) ? s0 + per : nsub;
+    const size_t all = (size_t)per * j->R * nsub;
+    uint32_t *slat, *dlat = NULL, *dmin;
+    double *srel, *sms = NULL, *drel = NULL, *dms = NULL;
+    int32_t* dverts = NULL;
+    int chunk = s1 - s0;
     srt_set_virtual_slot(j->virt ? j->rank : -1);
     TRYHIP(hipSetDevice(j->dev));
     TRYHIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     TRY(sparse_graph_from_canon(j->c, j->dev, &sg));
-    TRY(dalloc(&B, (void**)&dlat, all * sizeof(uint32_t)));
-    TRY(dalloc(&B, (void**)&drel, all * sizeof(double)));
-    if (s1 > s0)
-        TRY(srt_sparse_graph_rows(sg, s0, s1, dlat + (size_t)s0 * n, drel + (size_t)s0 * n, st, &j->st));
-    /* the symmetry rule needs the other shards' rows: gather, mirror, keep our block */
-    TRY(srt_sparse_allgather(j->comm, n, per, dlat, drel, st));
-    if (!j->directed) TRY(srt_mirror_lower_device(n, n, drel, st));
-    if (s1 > s0) {
-        TRYHIP(hipMemcpyAsync(j->lat_q + (size_t)s0 * n, dlat + (size_t)s0 * n,
-                              (size_t)(s1 - s0) * n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        TRYHIP(hipMemcpyAsync(j->rel + (size_t)s0 * n, drel + (size_t)s0 * n,
-                              (size_t)(s1 - s0) * n * sizeof(double), hipMemcpyDeviceToHost, st));
+    TRY(dalloc(&B, (void**)&slat, all * sizeof(uint32_t)));
+    TRY(dalloc(&B, (void**)&srel, all * sizeof(double)));
+    TRY(dalloc(&B, (void**)&dmin, sizeof(uint32_t)));
+    if (j->lat_ms) TRY(dalloc(&B, (void**)&sms, all * sizeof(double)));
+    TRYHIP(hipMemsetAsync(dmin, 0xFF, sizeof(uint32_t), st));
+    if (j->verts && s1 > s0) {
+        const size_t per_row = (size_t)n * (sizeof(uint32_t) + sizeof(double) + (sms ? sizeof(double) : 0));
+        const size_t cb = chunk_budget(0) / per_row;
+        chunk = (int)(cb < (size_t)(s1 - s0) ? (cb > 0 ? cb : 1) : (size_t)(s1 - s0));
+        TRY(dalloc(&B, (void**)&dverts, (size_t)nsub * sizeof(int32_t)));
+        TRYHIP(hipMemcpyAsync(dverts, j->verts, (size_t)nsub * sizeof(int32_t), hipMemcpyHostToDevice, st));
+        TRY(dalloc(&B, (void**)&dlat, (size_t)chunk * n * sizeof(uint32_t)));
+        TRY(dalloc(&B, (void**)&drel, (size_t)chunk * n * sizeof(double)));
+        if (sms) TRY(dalloc(&B, (void**)&dms, (size_t)chunk * n * sizeof(double)));
     }
+    for (int r0 = s0; r0 < s1; r0 += chunk) {
+        const int r1 = r0 + chunk < s1 ? r0 + chunk : s1;
+        srt_build_stats cs;
+        memset(&cs, 0, sizeof(cs));
+        if (j->verts) {
+            TRY(sparse_rows(sg, 0, r1 - r0, dverts + r0, dlat, drel, dms, st, &cs));
+            TRY(srt_gather_sub_u32(r1 - r0, nsub, NULL, dverts, dlat, n, slat + (size_t)r0 * nsub, nsub, st));
+            TRY(srt_gather_sub_f64(r1 - r0, nsub, NULL, dverts, drel, n, srel + (size_t)r0 * nsub, nsub, st));
+            if (dms) TRY(srt_gather_sub_f64(r1 - r0, nsub, NULL, dverts, dms, n, sms + (size_t)r0 * nsub, nsub, st));
+        } else {
+            TRY(sparse_rows(sg, r0, r1, NULL, slat + (size_t)r0 * n, srel + (size_t)r0 * n,
+                            sms ? sms + (size_t)r0 * n : NULL, st, &cs));
+        }
+        merge_stats(&j->st, &cs, r0 == s0);
+    }
+    if (s1 > s0) TRY(srt_table_min(s1 - s0, nsub, slat + (size_t)s0 * nsub, nsub, dmin, st));
+    /* the symmetry rule needs the other shards' rows: gather (ncclAllGather), mirror, keep ours */
+    TRY(srt_coll_allgather(j->comm, slat, (size_t)per * nsub * sizeof(uint32_t), st));
+    TRY(srt_coll_allgather(j->comm, srel, (size_t)per * nsub * sizeof(double), st));
+    if (sms) TRY(srt_coll_allgather(j->comm, sms, (size_t)per * nsub * sizeof(double), st));
+    if (!j->directed) TRY(srt_mirror_lower_device(nsub, nsub, srel, st));
+    if (!j->directed && sms) TRY(srt_mirror_lower_device(nsub, nsub, sms, st));
+    if (s1 > s0) {
+        TRYHIP(hipMemcpyAsync(j->lat_q + (size_t)s0 * nsub, slat + (size_t)s0 * nsub,
+                              (size_t)(s1 - s0) * nsub * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        TRYHIP(hipMemcpyAsync(j->rel + (size_t)s0 * nsub, srel + (size_t)s0 * nsub,
+                              (size_t)(s1 - s0) * nsub * sizeof(double), hipMemcpyDeviceToHost, st));
+        if (sms)
+            TRYHIP(hipMemcpyAsync(j->lat_ms + (size_t)s0 * nsub, sms + (size_t)s0 * nsub,
+                                  (size_t)(s1 - s0) * nsub * sizeof(double), hipMemcpyDeviceToHost, st));
+    }
+    TRYHIP(hipMemcpyAsync(&j->min_q, dmin, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     TRYHIP(hipStreamSynchronize(st));
 out:
     if (rc) mjob_fail(j, rc);
@@ -700,33 +963,19 @@ out:
     return NULL;
 }
 
-extern "C" int srt_build_tables_multi(const srt_edges* g, const srt_build_opts* opts, int32_t ngpus,
-                                      uint32_t* lat_q, uint64_t* quantum_ns, double* rel,
-                                      srt_build_stats* stats) {
-    if (!g || !lat_q || !quantum_ns || !rel || ngpus < 1) {
-        srt_set_error("srt_build_tables_multi: bad argument");
-        return SRT_E_ARG;
-    }
-    const int avail = srt_device_count();
-    if (avail < 1) {
-        srt_set_error("srt_build_tables_multi: no HIP device");
-        return SRT_E_DEVICE;
-    }
-    /* SRT_VIRTUAL_RANKS=R (tests): R ranks on device 0, collectives as device copies */
-    const char* venv = getenv("SRT_VIRTUAL_RANKS");
-    const int virt = venv && atoi(venv) > 0 ? (atoi(venv) < 64 ? atoi(venv) : 64) : 0;
-    const int R = virt ? virt : (ngpus < avail ? ngpus : avail);
-    const int use_sp = opts ? opts->use_shortest_path : 1;
-    if (!use_sp) return srt_build_tables(g, opts, lat_q, quantum_ns, rel, stats);
-    srt_canon c;
-    int rc = srt_canon_build(g, &c);
-    if (rc) return rc;
-    *quantum_ns = c.quantum_ns;
-    const int n = c.n;
-    const int algo = choose_algo(&c, opts);
+static int build_multi(const srt_canon* c, const srt_build_opts* opts, int algo, int R, int virt,
+                       int nsub, const int32_t* verts, uint32_t* lat_q, double* rel,
+                       double* lat_ms, uint32_t* min_q, srt_build_stats* stats) {
+    const int n = c->n;
     const int ld = srt_ceil_div(n, SRT_SHARD_ALIGN) * SRT_SHARD_ALIGN;
+    int rc = SRT_OK;
     uint32_t* hw = NULL;
     double* hr = NULL;
+    start_gate gate;
+    pthread_mutex_init(&gate.mu, NULL);
+    pthread_cond_init(&gate.cv, NULL);
+    gate.state = 0;
+    int started = 0;
     srt_comm** comms = (srt_comm**)calloc((size_t)R, sizeof(srt_comm*));
     mjob* jobs = (mjob*)calloc((size_t)R, sizeof(mjob));
     pthread_t* th = (pthread_t*)calloc((size_t)R, sizeof(pthread_t));
@@ -736,6 +985,12 @@ extern "C" int srt_build_tables_multi(const srt_edges* g, const srt_build_opts* 
         goto done;
     }
     if (algo == SRT_ALGO_DENSE_FW) {
+        if (n > SRT_DENSE_MAX_N) {
+            srt_set_error("dense build supports n <= %d (n = %d); use the sparse SSSP",
+                          SRT_DENSE_MAX_N, n);
+            rc = SRT_E_RANGE;
+            goto done;
+        }
         const size_t ll = (size_t)ld * ld;
         hw = (uint32_t*)malloc(ll * sizeof(uint32_t));
         hr = (double*)malloc(ll * sizeof(double));
@@ -743,18 +998,7 @@ extern "C" int srt_build_tables_multi(const srt_edges* g, const srt_build_opts* 
             rc = SRT_E_NOMEM;
             goto done;
         }
-        for (size_t i = 0; i < ll; i++) {
-            hw[i] = SRT_INF;
-            hr[i] = 0.0;
-        }
-        for (int u = 0; u < n; u++) {
-            for (int k = c.rowptr[u]; k < c.rowptr[u + 1]; k++) {
-                hw[(size_t)u * ld + c.col[k]] = c.w[k];
-                hr[(size_t)u * ld + c.col[k]] = c.r[k];
-            }
-            hw[(size_t)u * ld + u] = c.self_w[u];
-            hr[(size_t)u * ld + u] = c.self_r[u];
-        }
+        dense_host_matrices(c, ld, hw, hr);
     }
     for (int i = 0; i < R; i++) devs[i] = virt ? 0 : i;
     if ((rc = virt ? srt_comm_init_virtual(R, 0, comms) : srt_comm_init_all(R, devs, comms)))
@@ -765,41 +1009,133 @@ extern "C" int srt_build_tables_multi(const srt_edges* g, const srt_build_opts* 
         j->R = R;
         j->virt = virt;
         j->dev = devs[i];
-        j->directed = c.directed;
+        j->directed = c->directed;
         j->algo = algo;
         j->n = n;
         j->ld = ld;
+        j->gate = &gate;
         j->comm = comms[i];
-        j->c = &c;
+        j->c = c;
         j->hw = hw;
         j->hr = hr;
+        j->nsub = nsub;
+        j->verts = verts;
         j->lat_q = lat_q;
         j->rel = rel;
+        j->lat_ms = lat_ms;
+        j->min_q = 0xFFFFFFFFu;
         if (pthread_create(&th[i], NULL, algo == SRT_ALGO_DENSE_FW ? mjob_dense : mjob_sparse, j)) {
-            /* a collective would wait forever for the missing rank: refuse before any started */
-            for (int k = 0; k < i; k++) pthread_join(th[k], NULL);
             rc = SRT_E_NOMEM;
-            srt_set_error("srt_build_tables_multi: pthread_create failed");
-            goto done;
+            srt_set_error("srt_build_tables_multi: pthread_create failed for rank %d", i);
+            break;
         }
+        started++;
     }
-    for (int i = 0; i < R; i++) pthread_join(th[i], NULL);
+    /* open the gate only when every rank exists; otherwise the started ones leave at once */
+    pthread_mutex_lock(&gate.mu);
+    gate.state = rc ? -1 : 1;
+    pthread_cond_broadcast(&gate.cv);
+    pthread_mutex_unlock(&gate.mu);
+    for (int i = 0; i < started; i++) pthread_join(th[i], NULL);
+    if (rc) goto done;
     for (int i = 0; i < R && !rc; i++)
         if (jobs[i].rc) {
             rc = jobs[i].rc;
             srt_set_error("rank %d: %s", i, jobs[i].err);
         }
-    if (!rc && stats) *stats = jobs[0].st;
+    if (!rc) {
+        uint32_t m = 0xFFFFFFFFu;
+        for (int i = 0; i < R; i++) m = jobs[i].min_q < m ? jobs[i].min_q : m;
+        *min_q = m;
+        if (stats) *stats = jobs[0].st;
+    }
 done:
     if (comms)
         for (int i = 0; i < R; i++)
             if (comms[i]) srt_comm_free(comms[i]);
+    pthread_mutex_destroy(&gate.mu);
+    pthread_cond_destroy(&gate.cv);
     free(comms);
     free(jobs);
     free(th);
     free(devs);
     free(hw);
     free(hr);
+    return rc;
+}
+
+extern "C" int srt_build_tables_subset(const srt_edges* g, const srt_build_opts* opts, int32_t ngpus,
+                                       int32_t nsub, const int32_t* verts, uint32_t* lat_q,
+                                       uint64_t* quantum_ns, double* rel, double* lat_ms,
+                                       uint32_t* min_lat_q, srt_build_stats* stats) {
+    if (!g || !lat_q || !quantum_ns || !rel || ngpus < 1) {
+        srt_set_error("srt_build_tables_subset: null argument");
+        return SRT_E_ARG;
+    }
+    if (check_verts(g->n, nsub, verts)) {
+        srt_set_error("srt_build_tables_subset: the subset must be 1..n strictly increasing vertex "
+                      "indices (or NULL with nsub = n)");
+        return SRT_E_ARG;
+    }
+    const int avail = srt_device_count();
+    if (avail < 1) {
+        srt_set_error("srt_build_tables: no HIP device");
+        return SRT_E_DEVICE;
+    }
+    srt_canon c;
+    int rc = srt_canon_build(g, &c);
+    if (rc) return rc;
+    *quantum_ns = c.quantum_ns;
+    const int use_sp = opts ? opts->use_shortest_path : 1;
+    const int algo = use_sp ? choose_algo(&c, opts) : SRT_ALGO_DENSE_FW;
+    /* SRT_VIRTUAL_RANKS=R (tests): R ranks on device 0, collectives as device copies */
+    const char* venv = getenv("SRT_VIRTUAL_RANKS");
+    const int virt = ngpus > 1 && venv && atoi(venv) > 0 ? (atoi(venv) < 64 ? atoi(venv) : 64) : 0;
+    const int R = virt ? virt : (ngpus < avail ? ngpus : avail);
+    uint32_t mq = 0xFFFFFFFFu;
+    if (R > 1 && use_sp)
+        rc = build_multi(&c, opts, algo, R, virt, nsub, verts, lat_q, rel, lat_ms, &mq, stats);
+    else
+        rc = build_one(&c, opts, algo, nsub, verts, lat_q, rel, lat_ms, &mq, stats);
+    if (!rc && min_lat_q) *min_lat_q = mq;
     srt_canon_free(&c);
     return rc;
+}
+
+extern "C" int srt_build_tables(const srt_edges* g, const srt_build_opts* opts, uint32_t* lat_q,
+                                uint64_t* quantum_ns, double* rel, srt_build_stats* stats) {
+    if (!g) {
+        srt_set_error("srt_build_tables: null argument");
+        return SRT_E_ARG;
+    }
+    return srt_build_tables_subset(g, opts, 1, g->n, NULL, lat_q, quantum_ns, rel, NULL, NULL, stats);
+}
+
+extern "C" int srt_build_tables_multi(const srt_edges* g, const srt_build_opts* opts, int32_t ngpus,
+                                      uint32_t* lat_q, uint64_t* quantum_ns, double* rel,
+                                      srt_build_stats* stats) {
+    if (!g || ngpus < 1) {
+        srt_set_error("srt_build_tables_multi: bad argument");
+        return SRT_E_ARG;
+    }
+    /* ngpus == 1 still runs the threaded, communicator-driven form (tests of that path) */
+    const int avail = srt_device_count();
+    const char* venv = getenv("SRT_VIRTUAL_RANKS");
+    if (ngpus == 1 && !(venv && atoi(venv) > 0) && avail >= 1) {
+        srt_canon c;
+        int rc = srt_canon_build(g, &c);
+        if (rc) return rc;
+        *quantum_ns = c.quantum_ns;
+        const int use_sp = opts ? opts->use_shortest_path : 1;
+        uint32_t mq;
+        if (!use_sp)
+            rc = build_one(&c, opts, SRT_ALGO_DENSE_FW, g->n, NULL, lat_q, rel, NULL, &mq, stats);
+        else
+            rc = build_multi(&c, opts, choose_algo(&c, opts), 1, 0, g->n, NULL, lat_q, rel, NULL,
+                             &mq, stats);
+        srt_canon_free(&c);
+        return rc;
+    }
+    return srt_build_tables_subset(g, opts, ngpus, g->n, NULL, lat_q, quantum_ns, rel, NULL, NULL,
+                                   stats);
 }

@@ -341,6 +341,19 @@ int srt_comm_rank(const srt_comm* c) { return c ? c->rank : -1; }
 int srt_comm_is_solo(const srt_comm* c) { return c ? c->solo : 0; }
 int srt_comm_size(const srt_comm* c) { return c ? c->nranks : 0; }
 
+int srt_coll_allgather(const srt_comm* c, void* buf, size_t bytes, hipStream_t st) {
+    if (c->solo || bytes == 0) return SRT_OK;
+    if (c->loop) { /* every rank broadcasts its block in turn */
+        for (int q = 0; q < c->nranks; q++) {
+            const int rc = srt_coll_bcast(c, (uint8_t*)buf + bytes * q, bytes, q, st);
+            if (rc) return rc;
+        }
+        return SRT_OK;
+    }
+    SRT_NCCLCHK(ncclAllGather((uint8_t*)buf + bytes * c->rank, buf, bytes, ncclUint8, c->nc, st));
+    return SRT_OK;
+}
+
 extern "C" int srt_sparse_allgather(srt_comm* comm, int32_t n, int32_t rows_per_rank,
                                     uint32_t* lat_all, double* rel_all, void* stream) {
     if (!comm || n <= 0 || rows_per_rank <= 0 || !lat_all || !rel_all) {

@@ -746,19 +746,19 @@ __global__ __launch_bounds__(512) void rel_sweeps_kernel(int n, int ld, int row0
  * D[s][t] == L) only reads values final since an earlier pass: each entry is formed once,
  * rel(s,t) = rel(s,pred) * r(pred,t), the left-to-right product of topology.c:1364-1365.
  * Rows whose largest distance exceeds maxl passes are flagged for rel_sweeps_kernel. */
-template <int NT>
+template <int NT, int MAXN>
 __global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
                                                          const uint32_t* __restrict__ lat,
                                                          const int32_t* __restrict__ pred,
                                                          double* __restrict__ rel, int maxl,
                                                          int32_t* __restrict__ max_depth,
                                                          int32_t* __restrict__ sweep) {
-    /* each thread owns t = tid + i * NT (i < PER, n <= 32768); the row's distances are read once
+    /* each thread owns t = tid + i * NT (i < PER, n <= MAXN); the row's distances are read once
      * and kept as bytes in registers (levels <= maxl <= 254 once the row qualifies), so a pass
      * only compares registers and touches memory for its own targets. The row reads go through
      * buffer descriptors (constant scalar offset per i, one vector offset), which keeps the 64
      * unrolled loads from holding 64-bit addresses. */
-    constexpr int PER = 32768 / NT;
+    constexpr int PER = MAXN / NT;
     const int s = row0 + blockIdx.x;
     if (s >= n) return;
     const int tid = threadIdx.x;
@@ -1059,9 +1059,9 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         ir = ws->tr;
     }
     SRT_HIPCHK(hipMemsetAsync(ws->depth, 0, sizeof(int32_t), st));
-    if (n > 512 * 64) {
-        srt_set_error("dense predecessor pass supports n <= 32768 (n = %d)", n);
-        return SRT_E_ARG;
+    if (n > srt_dense_max_n()) { /* the entry points refuse such n before FW */
+        srt_set_error("dense predecessor pass supports n <= %d (n = %d)", srt_dense_max_n(), n);
+        return SRT_E_RANGE;
     }
     if (lrows > 0) {
         const size_t slab = (size_t)ld * nrows;
@@ -1129,15 +1129,28 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
          * (ws->cursor is free here and carries the per-row hand-over flags) */
         /* 1024 threads per row, one row per CU (128 VGPRs): 12.3 ms on C4 against 13.3 for 512
          * threads at two rows per CU and 13.1 for 1024 at two (64 VGPRs, 4 targets in flight) */
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
-        rel_levels_kernel<1024><<<lrows, 1024, 65536, st>>>(n, ld, row0, d, pred, rel, 64, ws->depth,
-                                                 ws->cursor);
-        const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        rel_sweeps_kernel<<<lrows, 512, lds, st>>>(n, ld, row0, pred, rel, ws->depth, ws->cursor);
-        SRT_HIPCHK(hipGetLastError());
+        if (n <= 32768) {
+            SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 32768>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
+            rel_levels_kernel<1024, 32768><<<lrows, 1024, 65536, st>>>(n, ld, row0, d, pred, rel, 64,
+                                                                     ws->depth, ws->cursor);
+            const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
+            SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            rel_sweeps_kernel<<<lrows, 512, lds, st>>>(n, ld, row0, pred, rel, ws->depth, ws->cursor);
+            SRT_HIPCHK(hipGetLastError());
+        } else {
+            /* n beyond 32768: 64 entries per thread (128 KB of per-wave target lists), and the
+             * flagged rows sweep with their predecessor rows in HBM (tables.hip) */
+            SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 65536>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
+            rel_levels_kernel<1024, 65536><<<lrows, 1024, 131072, st>>>(n, ld, row0, d, pred, rel, 64,
+                                                                      ws->depth, ws->cursor);
+            SRT_HIPCHK(hipGetLastError());
+            if ((rc = srt_rel_sweeps_rows(n, lrows, row0, pred, (size_t)ld, rel, (size_t)ld,
+                                          ws->cursor, ws->depth, st)))
+                return rc;
+        }
     }
     if (stats) {
         stats->ess_arcs = total;
@@ -1179,25 +1192,56 @@ int srt_dense_post_device(int32_t n, int32_t ld, int32_t directed, const uint32_
 /* ------------------------------------------------------------------------------------------ */
 /* public device-resident dense build                                                         */
 /* ------------------------------------------------------------------------------------------ */
-extern "C" int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, const uint32_t* w,
-                                      const double* r, uint32_t* lat, double* rel, void* stream,
-                                      int32_t fw_block, srt_build_stats* stats) {
+extern "C" int srt_dense_max_n(void) { return SRT_DENSE_MAX_N; }
+
+/* HIP events of one build, released on every return path */
+struct build_events {
+    hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+    ~build_events() {
+        for (hipEvent_t x : e)
+            if (x) (void)hipEventDestroy(x);
+    }
+    int create() {
+        for (hipEvent_t& x : e) SRT_HIPCHK(hipEventCreate(&x));
+        return SRT_OK;
+    }
+};
+
+/* f64 path-order ms rows [row0, row0 + lrows) from the predecessor rows the post pass left in the
+ * workspace (tables.hip); runs after the diagonal rule */
+static int dense_path_ms(int32_t n, int32_t ld, int32_t row0, int32_t nrows, const uint32_t* d,
+                         uint64_t q, double* lms, hipStream_t st) {
+    const int lrows = max(0, min(nrows, n - row0));
+    if (lrows == 0) return SRT_OK;
+    dense_ws* ws;
+    int rc = ws_get(&ws, n);
+    if (rc) return rc;
+    return srt_path_ms_rows(n, lrows, NULL, row0, d, (size_t)ld, reinterpret_cast<const int32_t*>(ws->dt),
+                            (size_t)ld, NULL, NULL, NULL, q, lms, (size_t)ld, st);
+}
+
+int srt_dense_build_device_ms(int32_t n, int32_t ld, int32_t directed, const uint32_t* w,
+                              const double* r, uint32_t* lat, double* rel, double* lat_ms,
+                              uint64_t quantum_ns, hipStream_t st, int32_t fw_block,
+                              srt_build_stats* stats) {
     if (n <= 0 || ld < n || ld % B || !w || !r || !lat || !rel) {
         srt_set_error("srt_dense_build_device: bad arguments (n=%d ld=%d)", n, ld);
         return SRT_E_ARG;
+    }
+    if (n > srt_dense_max_n()) { /* refused before any FW round runs */
+        srt_set_error("dense build supports n <= %d (n = %d); use the sparse SSSP", srt_dense_max_n(), n);
+        return SRT_E_RANGE;
     }
     if (fw_block != 0 && fw_block != B) {
         srt_set_error("srt_dense_build_device: fw_block must be 0 or %d", B);
         return SRT_E_ARG;
     }
-    hipStream_t st = (hipStream_t)stream;
-    hipEvent_t e0, e1, e2;
-    SRT_HIPCHK(hipEventCreate(&e0));
-    SRT_HIPCHK(hipEventCreate(&e1));
-    SRT_HIPCHK(hipEventCreate(&e2));
+    build_events ev;
+    int rc = ev.create();
+    if (rc) return rc;
+    hipEvent_t e0 = ev.e[0], e1 = ev.e[1], e2 = ev.e[2];
     SRT_HIPCHK(hipEventRecord(e0, st));
     evpool_t* evp = NULL;
-    int rc;
     if (stats && stats->time_kernels && (rc = evpool_begin(&evp, ld / B))) return rc;
     /* narrowest exact encoding first: f16-compare u16 -> pk_min u16 -> u32 */
     int exact = 0, enc = SRT_DENC_U32;
@@ -1229,6 +1273,14 @@ extern "C" int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, c
     rc = srt_dense_post_device(n, ld, directed, w, r, lat, exact ? srt_fw16_matrix() : NULL, rel,
                                st, stats);
     if (rc) return rc;
+    if (lat_ms) {
+        if ((rc = dense_path_ms(n, ld, 0, ld, lat, quantum_ns, lat_ms, st))) return rc;
+        if (!directed) {
+            const int nbk = srt_ceil_div(n, 64);
+            mirror_block_kernel<<<nbk * (nbk + 1) / 2, 256, 0, st>>>(n, ld, 0, n, lat_ms);
+            SRT_HIPCHK(hipGetLastError());
+        }
+    }
     SRT_HIPCHK(hipEventRecord(e2, st));
     if (stats) {
         SRT_HIPCHK(hipEventSynchronize(e2));
@@ -1243,10 +1295,14 @@ extern "C" int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, c
         stats->ms_total = a + b;
         if (evp && (rc = evpool_sum(evp, e2, stats))) return rc;
     }
-    SRT_HIPCHK(hipEventDestroy(e0));
-    SRT_HIPCHK(hipEventDestroy(e1));
-    SRT_HIPCHK(hipEventDestroy(e2));
     return SRT_OK;
+}
+
+extern "C" int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, const uint32_t* w,
+                                      const double* r, uint32_t* lat, double* rel, void* stream,
+                                      int32_t fw_block, srt_build_stats* stats) {
+    return srt_dense_build_device_ms(n, ld, directed, w, r, lat, rel, NULL, 0, (hipStream_t)stream,
+                                     fw_block, stats);
 }
 
 /* ------------------------------------------------------------------------------------------ */
@@ -1388,13 +1444,17 @@ static int shard_mirror(const srt_comm* comm, int n, int ld, int b, int e, doubl
     return SRT_OK;
 }
 
-extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, int32_t directed,
-                                       const uint32_t* w_rows, const double* r_rows,
-                                       uint32_t* lat_rows, double* rel_rows, void* stream,
-                                       int32_t fw_block, srt_build_stats* stats) {
+int srt_dense_build_sharded_ms(srt_comm* comm, int32_t n, int32_t ld, int32_t directed,
+                               const uint32_t* w_rows, const double* r_rows, uint32_t* lat_rows,
+                               double* rel_rows, double* lms_rows, uint64_t quantum_ns,
+                               hipStream_t st, int32_t fw_block, srt_build_stats* stats) {
     if (!comm || n <= 0 || ld < n || ld % SRT_SHARD_ALIGN || !w_rows || !r_rows || !lat_rows || !rel_rows) {
         srt_set_error("srt_dense_build_sharded: bad arguments");
         return SRT_E_ARG;
+    }
+    if (n > srt_dense_max_n()) { /* refused before any FW round runs */
+        srt_set_error("dense build supports n <= %d (n = %d); use the sparse SSSP", srt_dense_max_n(), n);
+        return SRT_E_RANGE;
     }
     if (fw_block != 0 && fw_block != B) {
         srt_set_error("srt_dense_build_sharded: fw_block must be 0 or %d", B);
@@ -1404,17 +1464,15 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
     int32_t b, e;
     srt_shard_rows(ld, SRT_SHARD_ALIGN, R, me, &b, &e);
     const int nr = e - b;
-    hipStream_t st = (hipStream_t)stream;
     dense_ws* ws;
     int rc = ws_get(&ws, n);
     if (rc) return rc;
     size_t pc = ws->panel_cap;
     if ((rc = ws_grow((void**)&ws->panel, &pc, (size_t)B * ld, sizeof(uint32_t)))) return rc;
     ws->panel_cap = pc;
-    hipEvent_t e0, e1, e2;
-    SRT_HIPCHK(hipEventCreate(&e0));
-    SRT_HIPCHK(hipEventCreate(&e1));
-    SRT_HIPCHK(hipEventCreate(&e2));
+    build_events ev;
+    if ((rc = ev.create())) return rc;
+    hipEvent_t e0 = ev.e[0], e1 = ev.e[1], e2 = ev.e[2];
     SRT_HIPCHK(hipEventRecord(e0, st));
     evpool_t* evp = NULL;
     if (stats && stats->time_kernels && (rc = evpool_begin(&evp, ld / B))) return rc;
@@ -1481,6 +1539,18 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
         }
     }
     if ((rc = dense_finish_rows(n, ld, b, nr, w_rows, r_rows, lat_rows, rel_rows, st, stats))) return rc;
+    if (lms_rows) {
+        if ((rc = dense_path_ms(n, ld, b, nr, lat_rows, quantum_ns, lms_rows, st))) return rc;
+        if (!directed) {
+            if (R > 1) {
+                if ((rc = shard_mirror(comm, n, ld, b, e, lms_rows, st))) return rc;
+            } else {
+                const int nbk = srt_ceil_div(n, 64);
+                mirror_block_kernel<<<nbk * (nbk + 1) / 2, 256, 0, st>>>(n, ld, 0, n, lms_rows);
+                SRT_HIPCHK(hipGetLastError());
+            }
+        }
+    }
     SRT_HIPCHK(hipEventRecord(e2, st));
     if (stats) {
         SRT_HIPCHK(hipEventSynchronize(e2));
@@ -1495,8 +1565,13 @@ extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, in
         stats->ms_total = a + c;
         if (evp && (rc = evpool_sum(evp, e2, stats))) return rc;
     }
-    SRT_HIPCHK(hipEventDestroy(e0));
-    SRT_HIPCHK(hipEventDestroy(e1));
-    SRT_HIPCHK(hipEventDestroy(e2));
     return SRT_OK;
+}
+
+extern "C" int srt_dense_build_sharded(srt_comm* comm, int32_t n, int32_t ld, int32_t directed,
+                                       const uint32_t* w_rows, const double* r_rows,
+                                       uint32_t* lat_rows, double* rel_rows, void* stream,
+                                       int32_t fw_block, srt_build_stats* stats) {
+    return srt_dense_build_sharded_ms(comm, n, ld, directed, w_rows, r_rows, lat_rows, rel_rows,
+                                      NULL, 0, (hipStream_t)stream, fw_block, stats);
 }

@@ -44,7 +44,8 @@ static __device__ __forceinline__ int wave_excl_scan(int v, int lane, int* total
 
 template <bool G>
 __global__ __launch_bounds__(SP_THREADS) void sssp_kernel(
-    int n, int src_begin, int nsrc, uint32_t delta, const int32_t* __restrict__ rowptr,
+    int n, int src_begin, const int32_t* __restrict__ srcs, int nsrc, uint32_t delta,
+    const int32_t* __restrict__ rowptr,
     const int32_t* __restrict__ col, const uint32_t* __restrict__ w,
     const int32_t* __restrict__ in_rowptr, const int32_t* __restrict__ in_col,
     const uint32_t* __restrict__ in_w, const double* __restrict__ in_r, uint32_t* __restrict__ lat,
@@ -64,7 +65,7 @@ __global__ __launch_bounds__(SP_THREADS) void sssp_kernel(
     const int tid = threadIdx.x, lane = tid & 63;
     int depth = 0;
   for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
-    const int s = src_begin + si;
+    const int s = srcs ? srcs[si] : src_begin + si;
     __syncthreads(); /* the previous source's walk is done with the working set */
     for (int v = tid; v < n; v += SP_THREADS) dist[v] = SRT_INF;
     for (int q = tid; q < nwords; q += SP_THREADS) bits[q] = 0;
@@ -215,13 +216,15 @@ __global__ __launch_bounds__(SP_THREADS) void sssp_kernel(
 
 /* Diagonal rule (topology.c:1431-1576) from the canonical CSR: min over (self-loop L, v) and
  * (2L, u) for out-arcs (v,u), first strict minimum in neighbor order. */
-__global__ void sparse_diag_kernel(int n, int src_begin, int src_end, const int32_t* __restrict__ rowptr,
+__global__ void sparse_diag_kernel(int n, int src_begin, int src_end, const int32_t* __restrict__ srcs,
+                                   const int32_t* __restrict__ rowptr,
                                    const int32_t* __restrict__ col, const uint32_t* __restrict__ w,
                                    const double* __restrict__ r, const uint32_t* __restrict__ self_w,
                                    const double* __restrict__ self_r, uint32_t* __restrict__ lat,
                                    double* __restrict__ rel, size_t ldo) {
-    const int v = src_begin + blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= src_end) return;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= src_end - src_begin) return;
+    const int v = srcs ? srcs[i] : src_begin + i;
     uint64_t best = ~0ull;
     int bk = -2;
     if (self_w[v] < SRT_INF) {
@@ -235,7 +238,7 @@ __global__ void sparse_diag_kernel(int n, int src_begin, int src_end, const int3
             bk = k;
         }
     }
-    const size_t ix = (size_t)(v - src_begin) * ldo + v;
+    const size_t ix = (size_t)i * ldo + v;
     if (bk == -2) {
         lat[ix] = 0;
         rel[ix] = 0.0;
@@ -249,11 +252,11 @@ __global__ void sparse_diag_kernel(int n, int src_begin, int src_end, const int3
 }
 
 /* host wrapper so the wave-per-source kernel (wsssp.hip) shares the diagonal rule */
-int srt_sparse_diag(int n, int src_begin, int src_end, const int32_t* rowptr, const int32_t* col,
-                    const uint32_t* w, const double* r, const uint32_t* self_w,
+int srt_sparse_diag(int n, int src_begin, int src_end, const int32_t* srcs, const int32_t* rowptr,
+                    const int32_t* col, const uint32_t* w, const double* r, const uint32_t* self_w,
                     const double* self_r, uint32_t* lat, double* rel, size_t ldo, hipStream_t st) {
     sparse_diag_kernel<<<srt_ceil_div(src_end - src_begin, 256), 256, 0, st>>>(
-        n, src_begin, src_end, rowptr, col, w, r, self_w, self_r, lat, rel, ldo);
+        n, src_begin, src_end, srcs, rowptr, col, w, r, self_w, self_r, lat, rel, ldo);
     SRT_HIPCHK(hipGetLastError());
     return SRT_OK;
 }
@@ -269,16 +272,15 @@ int srt_sparse_max_n(void) {
     return (160 * 1024 - 256) * 8 / 65;
 }
 
-extern "C" int srt_sparse_build_device(int32_t n, int32_t directed, const int32_t* rowptr,
-                                       const int32_t* col, const uint32_t* w, const double* r,
-                                       const int32_t* in_rowptr, const int32_t* in_col,
-                                       const uint32_t* in_w, const double* in_r,
-                                       const uint32_t* self_w, const double* self_r,
-                                       int32_t src_begin, int32_t src_end, uint32_t delta,
-                                       uint32_t* lat_rows, double* rel_rows, void* stream,
-                                       srt_build_stats* stats) {
-    (void)directed;
-    if (n <= 0 || src_begin < 0 || src_end > n || src_begin >= src_end || !rowptr || !col || !w ||
+/* rows of sources srcs[0 .. src_end - src_begin) (device list), or of [src_begin, src_end) when
+ * srcs is NULL */
+int srt_sparse_block_rows(int32_t n, const int32_t* rowptr, const int32_t* col, const uint32_t* w,
+                          const double* r, const int32_t* in_rowptr, const int32_t* in_col,
+                          const uint32_t* in_w, const double* in_r, const uint32_t* self_w,
+                          const double* self_r, int32_t src_begin, int32_t src_end,
+                          const int32_t* srcs, uint32_t delta, uint32_t* lat_rows,
+                          double* rel_rows, void* stream, srt_build_stats* stats) {
+    if (n <= 0 || src_begin < 0 || (!srcs && src_end > n) || src_begin >= src_end || !rowptr || !col || !w ||
         !r || !in_rowptr || !in_col || !in_w || !in_r || !self_w || !self_r || !lat_rows ||
         !rel_rows) {
         srt_set_error("srt_sparse_build_device: bad arguments");
@@ -302,7 +304,7 @@ extern "C" int srt_sparse_build_device(int32_t n, int32_t directed, const int32_
         const size_t lds = srt_sparse_lds_bytes(n);
         SRT_HIPCHK(hipFuncSetAttribute((const void*)sssp_kernel<false>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        sssp_kernel<false><<<nsrc, SP_THREADS, lds, st>>>(n, src_begin, nsrc, delta, rowptr, col, w,
+        sssp_kernel<false><<<nsrc, SP_THREADS, lds, st>>>(n, src_begin, srcs, nsrc, delta, rowptr, col, w,
                                                           in_rowptr, in_col, in_w, in_r, lat_rows,
                                                           rel_rows, ldo, depth, NULL, 0);
     } else {
@@ -321,7 +323,7 @@ extern "C" int srt_sparse_build_device(int32_t n, int32_t directed, const int32_
                           (size_t)slots * slot_words * 4 >> 20);
             return SRT_E_NOMEM;
         }
-        sssp_kernel<true><<<slots, SP_THREADS, 0, st>>>(n, src_begin, nsrc, delta, rowptr, col, w,
+        sssp_kernel<true><<<slots, SP_THREADS, 0, st>>>(n, src_begin, srcs, nsrc, delta, rowptr, col, w,
                                                         in_rowptr, in_col, in_w, in_r, lat_rows,
                                                         rel_rows, ldo, depth, ws, slot_words);
         SRT_HIPCHK(hipFreeAsync(ws, st));
@@ -329,7 +331,7 @@ extern "C" int srt_sparse_build_device(int32_t n, int32_t directed, const int32_
     SRT_HIPCHK(hipGetLastError());
     SRT_HIPCHK(hipEventRecord(ek, st)); /* end of the SSSP kernel (the dominant launch) */
     sparse_diag_kernel<<<srt_ceil_div(src_end - src_begin, 256), 256, 0, st>>>(
-        n, src_begin, src_end, rowptr, col, w, r, self_w, self_r, lat_rows, rel_rows, ldo);
+        n, src_begin, src_end, srcs, rowptr, col, w, r, self_w, self_r, lat_rows, rel_rows, ldo);
     SRT_HIPCHK(hipGetLastError());
     SRT_HIPCHK(hipEventRecord(e1, st));
     SRT_HIPCHK(hipEventSynchronize(e1));
@@ -351,4 +353,17 @@ extern "C" int srt_sparse_build_device(int32_t n, int32_t directed, const int32_
         stats->ms_update = msk;
     }
     return SRT_OK;
+}
+
+extern "C" int srt_sparse_build_device(int32_t n, int32_t directed, const int32_t* rowptr,
+                                       const int32_t* col, const uint32_t* w, const double* r,
+                                       const int32_t* in_rowptr, const int32_t* in_col,
+                                       const uint32_t* in_w, const double* in_r,
+                                       const uint32_t* self_w, const double* self_r,
+                                       int32_t src_begin, int32_t src_end, uint32_t delta,
+                                       uint32_t* lat_rows, double* rel_rows, void* stream,
+                                       srt_build_stats* stats) {
+    (void)directed;
+    return srt_sparse_block_rows(n, rowptr, col, w, r, in_rowptr, in_col, in_w, in_r, self_w, self_r,
+                                 src_begin, src_end, NULL, delta, lat_rows, rel_rows, stream, stats);
 }

@@ -151,4 +151,37 @@ int srt_dense_post_device(int32_t n, int32_t ld, int32_t directed, const uint32_
                           const double* r, uint32_t* d, const uint16_t* d16, double* rel,
                           hipStream_t st, srt_build_stats* stats);
 
+/* Largest dense n: the predecessor keys pack a 16-bit rank and the essential-arc offsets are
+ * int32 (n^2 < 2^31), rounded down to the 128 tile. */
+#define SRT_DENSE_MAX_N 46336
+/* Dense builds with the optional f64 path-order ms table (lat_ms / lms_rows may be NULL). */
+int srt_dense_build_device_ms(int32_t n, int32_t ld, int32_t directed, const uint32_t* w,
+                              const double* r, uint32_t* lat, double* rel, double* lat_ms,
+                              uint64_t quantum_ns, hipStream_t st, int32_t fw_block,
+                              srt_build_stats* stats);
+int srt_dense_build_sharded_ms(srt_comm* comm, int32_t n, int32_t ld, int32_t directed,
+                               const uint32_t* w_rows, const double* r_rows, uint32_t* lat_rows,
+                               double* rel_rows, double* lms_rows, uint64_t quantum_ns,
+                               hipStream_t st, int32_t fw_block, srt_build_stats* stats);
+
+/* tables.hip: path-order passes, sub-table gathers, table minimum */
+int srt_path_sweeps_max_n(void);
+/* out rows (f64 ms, path order) of nrows sources (srcs[r], or src_begin + r) from their distance
+ * rows D (diagonal rule applied) and either predecessor rows or the in-arc CSR */
+int srt_path_ms_rows(int n, int nrows, const int32_t* srcs, int src_begin, const uint32_t* D,
+                     size_t ldd, const int32_t* pred, size_t ldp, const int32_t* irp,
+                     const int32_t* icol, const uint32_t* iw, uint64_t quantum_ns, double* out,
+                     size_t ldo, hipStream_t st);
+int srt_rel_sweeps_rows(int n, int nrows, int row0, const int32_t* pred, size_t ldp, double* rel,
+                        size_t ldr, const int32_t* only, int32_t* max_depth, hipStream_t st);
+int srt_gather_sub_u32(int nr, int nc, const int32_t* rows, const int32_t* cols, const uint32_t* in,
+                       size_t ldi, uint32_t* out, size_t ldo, hipStream_t st);
+int srt_gather_sub_f64(int nr, int nc, const int32_t* rows, const int32_t* cols, const double* in,
+                       size_t ldi, double* out, size_t ldo, hipStream_t st);
+int srt_table_min(int rows, int cols, const uint32_t* t, size_t ld, uint32_t* dmin, hipStream_t st);
+int srt_quanta_to_ms(int rows, int cols, const uint32_t* w, size_t ldw, uint64_t q, double* out,
+                     size_t ldo, hipStream_t st);
+/* collectives: all-gather of equal byte blocks, rank q's block at buf + q * bytes */
+int srt_coll_allgather(const srt_comm* c, void* buf, size_t bytes, hipStream_t st);
+
 #endif

@@ -177,13 +177,19 @@ struct _Topology {
     pthread_rwlock_t ip_lock;
     ipmap_t ipmap;
     uint8_t* attached; /* verticesWithAttachedHosts */
-    /* tables (immutable once `built` is set) */
+    atomic_int attach_gen; /* bumped whenever a vertex joins the attached set */
+    /* tables: one immutable generation per build, published through `tb` (acquire/release);
+     * replaced generations stay allocated until topology_free, so a lookup that loaded the
+     * previous pointer keeps reading valid memory */
     pthread_mutex_t build_lock;
-    atomic_int built;
+    _Atomic(struct tables*) tb;
     int build_failed;
-    uint32_t* lat_q;
+    int ngpus;
     uint64_t quantum_ns;
-    double* rel;
+    /* runahead export (topology.c:1253-1264): the attach generation it covers, the last value */
+    pthread_mutex_t min_lock;
+    atomic_int min_gen;
+    double min_exported;
     srt_build_opts opts;
     srt_build_stats stats;
     /* counters */
@@ -195,6 +201,34 @@ struct _Topology {
 };
 
 static int magic_ok(const Topology* t) { return t && t->magic == TOPOLOGY_MAGIC; }
+
+/* One generation of routing tables over a vertex subset: the vertices with attached hosts (the
+ * reference computes paths towards those only, topology.c:1604-1656), or every vertex when the
+ * build ran before any attach. Entry [i][j] is the pair (verts[i], verts[j]). */
+typedef struct tables {
+    int32_t nslot;
+    int all;            /* every vertex, slot == vertex */
+    int32_t* slot_of;   /* n entries: slot of a vertex, -1 when not in the table */
+    int32_t* verts;     /* nslot vertices, increasing */
+    uint32_t* lat_q;    /* nslot x nslot quanta */
+    double* rel;        /* nslot x nslot */
+    double* lat_ms;     /* f64 path-order ms (sub-ms edge latencies), else NULL */
+    uint32_t min_q;     /* smallest entry (diagonal included) */
+    struct tables* prev;
+} tables_t;
+
+static void tables_free_all(tables_t* tb) {
+    while (tb) {
+        tables_t* p = tb->prev;
+        free(tb->slot_of);
+        free(tb->verts);
+        free(tb->lat_q);
+        free(tb->rel);
+        free(tb->lat_ms);
+        free(tb);
+        tb = p;
+    }
+}
 static void attach_index_free(Topology* t);
 
 /* address_stringToIP (address.c:145-152): network order, INADDR_NONE on failure */
@@ -495,7 +529,12 @@ static Topology* topology_from_text(const char* text, size_t len, int useShortes
     pthread_mutex_init(&t->build_lock, NULL);
     pthread_mutex_init(&t->cnt_lock, NULL);
     pthread_mutex_init(&t->ax_lock, NULL);
-    atomic_store(&t->built, 0);
+    pthread_mutex_init(&t->min_lock, NULL);
+    atomic_store(&t->tb, NULL);
+    atomic_store(&t->attach_gen, 0);
+    atomic_store(&t->min_gen, 0);
+    t->min_exported = -1.0;
+    t->ngpus = 1;
     t->opts.device = 0;
     t->opts.algo = SRT_ALGO_AUTO;
     char err[512];
@@ -556,8 +595,7 @@ void topology_free(Topology* t) {
     free(t->eloss);
     free(t->ipmap.keys);
     free(t->ipmap.vals);
-    free(t->lat_q);
-    free(t->rel);
+    tables_free_all(atomic_load(&t->tb));
     free(t->counters.keys);
     free(t->counters.cnt);
     gml_free(&t->gml);
@@ -566,6 +604,7 @@ void topology_free(Topology* t) {
     pthread_mutex_destroy(&t->cnt_lock);
     attach_index_free(t);
     pthread_mutex_destroy(&t->ax_lock);
+    pthread_mutex_destroy(&t->min_lock);
     t->magic = 0;
     free(t);
 }
@@ -878,7 +917,10 @@ static int32_t attach_common(Topology* t, uint32_t ipNet, uint32_t* rand_state, 
     }
     pthread_rwlock_wrlock(&t->ip_lock);
     ipmap_put(&t->ipmap, ipNet, v);
-    t->attached[v] = 1;
+    if (!t->attached[v]) {
+        t->attached[v] = 1;
+        atomic_fetch_add(&t->attach_gen, 1);
+    }
     pthread_rwlock_unlock(&t->ip_lock);
     if (bwUpOut) *bwUpOut = t->bw_up_kib[v];
     if (bwDownOut) *bwDownOut = t->bw_down_kib[v];
@@ -926,7 +968,10 @@ int32_t srt_topology_attach_batch_ip(Topology* t, int32_t nhosts, const uint32_t
     pthread_rwlock_wrlock(&t->ip_lock);
     for (int32_t h = 0; h < done; h++) {
         ipmap_put(&t->ipmap, ipNet[h], vs[h]);
-        t->attached[vs[h]] = 1;
+        if (!t->attached[vs[h]]) {
+            t->attached[vs[h]] = 1;
+            atomic_fetch_add(&t->attach_gen, 1);
+        }
     }
     pthread_rwlock_unlock(&t->ip_lock);
     for (int32_t h = 0; h < done; h++) {
@@ -988,110 +1033,247 @@ int srt_topology_last_stats(Topology* t, srt_build_stats* stats) {
     return SRT_OK;
 }
 
-double srt_topology_min_latency_ms(Topology* t) {
-    if (!magic_ok(t) || !atomic_load(&t->built)) return 0.0;
-    int32_t n = t->n;
-    uint64_t best = UINT64_MAX;
-    for (int32_t s = 0; s < n; s++) {
-        if (!t->attached[s]) continue;
-        const uint32_t* row = t->lat_q + (size_t)s * n;
-        for (int32_t d = 0; d < n; d++)
-            if (t->attached[d] && row[d] < best) best = row[d];
+/* runahead hook: tests (and embedders without Shadow's worker) receive the exported minimum
+ * here instead of worker_updateMinTimeJump */
+static void (*g_min_hook)(double) = NULL;
+
+void srt_set_min_time_jump_hook(void (*fn)(double)) { g_min_hook = fn; }
+
+static double tables_latency_ms(const Topology* t, const tables_t* tb, size_t i) {
+    return tb->lat_ms ? tb->lat_ms[i] : (double)((uint64_t)tb->lat_q[i] * t->quantum_ns) / 1000000.0;
+}
+
+/* minimum path latency (ms) over pairs of attached vertices, diagonal included; < 0 if none */
+static double attached_min_ms(Topology* t, const tables_t* tb) {
+    const int32_t n = t->n;
+    int32_t na = 0;
+    for (int32_t v = 0; v < n; v++) na += t->attached[v] != 0;
+    if (na == 0) return -1.0;
+    if (na == tb->nslot && !tb->lat_ms) /* the table is the attached set: the device minimum */
+        return (double)((uint64_t)tb->min_q * t->quantum_ns) / 1000000.0;
+    double best = -1.0;
+    for (int32_t a = 0; a < tb->nslot; a++) {
+        if (!t->attached[tb->verts[a]]) continue;
+        const size_t row = (size_t)a * tb->nslot;
+        for (int32_t b = 0; b < tb->nslot; b++) {
+            if (!t->attached[tb->verts[b]]) continue;
+            const double ms = tables_latency_ms(t, tb, row + b);
+            if (best < 0 || ms < best) best = ms;
+        }
     }
-    if (best == UINT64_MAX) return 0.0;
-    return (double)(best * t->quantum_ns) / 1000000.0;
+    return best;
+}
+
+double srt_topology_min_latency_ms(Topology* t) {
+    if (!magic_ok(t)) return 0.0;
+    const tables_t* tb = atomic_load_explicit(&t->tb, memory_order_acquire);
+    if (!tb) return 0.0;
+    pthread_rwlock_rdlock(&t->ip_lock);
+    const double m = attached_min_ms(t, tb);
+    pthread_rwlock_unlock(&t->ip_lock);
+    return m < 0 ? 0.0 : m;
+}
+
+/* The reference hands every new smallest path latency to worker_updateMinTimeJump as it caches
+ * paths (topology.c:1253-1264, controller.c:141-153). The tables hold every attached pair at
+ * once, so the minimum over them is handed over once per attach generation, and only when it
+ * is below the last value handed over. */
+static void export_min(Topology* t) {
+    const int gen = atomic_load(&t->attach_gen);
+    if (atomic_load(&t->min_gen) == gen) return;
+    pthread_mutex_lock(&t->min_lock);
+    const tables_t* tb = atomic_load_explicit(&t->tb, memory_order_acquire);
+    if (tb && atomic_load(&t->min_gen) != gen) {
+        pthread_rwlock_rdlock(&t->ip_lock);
+        const double m = attached_min_ms(t, tb);
+        pthread_rwlock_unlock(&t->ip_lock);
+        if (m >= 0 && (t->min_exported < 0 || m < t->min_exported)) {
+            t->min_exported = m;
+            if (g_min_hook)
+                g_min_hook(m);
+            else
+                worker_updateMinTimeJump(m);
+        }
+        atomic_store(&t->min_gen, gen);
+    }
+    pthread_mutex_unlock(&t->min_lock);
+}
+
+static int tables_cover_attached(const Topology* t, const tables_t* tb) {
+    if (!tb) return 0;
+    if (tb->all) return 1;
+    for (int32_t v = 0; v < t->n; v++)
+        if (t->attached[v] && tb->slot_of[v] < 0) return 0;
+    return 1;
+}
+
+/* Build a new generation over the attached vertices (every vertex when none is attached yet).
+ * Caller holds build_lock. */
+static int build_generation(Topology* t, int nGPUs) {
+    const int32_t n = t->n;
+    tables_t* tb = (tables_t*)calloc(1, sizeof(tables_t));
+    if (!tb) return SRT_E_NOMEM;
+    tb->slot_of = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+    tb->verts = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+    if (!tb->slot_of || !tb->verts) {
+        tables_free_all(tb);
+        return SRT_E_NOMEM;
+    }
+    pthread_rwlock_rdlock(&t->ip_lock);
+    int32_t k = 0;
+    for (int32_t v = 0; v < n; v++) {
+        tb->slot_of[v] = t->attached[v] ? k : -1;
+        if (t->attached[v]) tb->verts[k++] = v;
+    }
+    pthread_rwlock_unlock(&t->ip_lock);
+    if (k == 0 || k == n) { /* nothing attached yet, or everything: the full table */
+        tb->all = 1;
+        for (int32_t v = 0; v < n; v++) {
+            tb->slot_of[v] = v;
+            tb->verts[v] = v;
+        }
+        k = n;
+    }
+    tb->nslot = k;
+    srt_edges e;
+    srt_topology_edges(t, &e);
+    uint64_t q = 0;
+    uint32_t mx = 0;
+    int rc = srt_latency_quantum(&e, &q, &mx);
+    if (rc) {
+        tables_free_all(tb);
+        return rc;
+    }
+    const size_t nn = (size_t)k * (size_t)k;
+    tb->lat_q = (uint32_t*)malloc(nn * sizeof(uint32_t));
+    tb->rel = (double*)malloc(nn * sizeof(double));
+    /* whole-ms edges: f64 ms sums are exact integers, lat_q * q / 1e6 is the reference's value */
+    if (q % 1000000u) tb->lat_ms = (double*)malloc(nn * sizeof(double));
+    if (!tb->lat_q || !tb->rel || ((q % 1000000u) && !tb->lat_ms)) {
+        tables_free_all(tb);
+        return SRT_E_NOMEM;
+    }
+    srt_build_opts o = t->opts;
+    o.use_shortest_path = t->use_shortest_path;
+    /* nGPUs > 1: one host thread per GPU of this process, RCCL between them */
+    rc = srt_build_tables_subset(&e, &o, nGPUs > 1 ? nGPUs : 1, k, tb->all ? NULL : tb->verts,
+                                 tb->lat_q, &t->quantum_ns, tb->rel, tb->lat_ms, &tb->min_q,
+                                 &t->stats);
+    if (rc) {
+        tables_free_all(tb);
+        return rc;
+    }
+    tb->prev = atomic_load(&t->tb);
+    atomic_store_explicit(&t->tb, tb, memory_order_release);
+    srt_log(SRT_LOG_INFO, "routing tables built over %d of %d vertices (%s)", k, n,
+            tb->all ? "all" : "attached");
+    return SRT_OK;
+}
+
+/* tables covering every attached vertex; builds (lazily, like _topology_getPathEntry's cache miss
+ * at topology.c:1923-1961) when there are none or an attach added a vertex since */
+static const tables_t* ensure_tables(Topology* t, int nGPUs) {
+    const tables_t* tb = atomic_load_explicit(&t->tb, memory_order_acquire);
+    pthread_mutex_lock(&t->build_lock);
+    tb = atomic_load_explicit(&t->tb, memory_order_acquire);
+    pthread_rwlock_rdlock(&t->ip_lock);
+    const int ok = tables_cover_attached(t, tb);
+    pthread_rwlock_unlock(&t->ip_lock);
+    if (!ok && !t->build_failed) {
+        const int rc = build_generation(t, nGPUs);
+        if (rc) {
+            t->build_failed = 1;
+            srt_log(SRT_LOG_ERROR, "routing table build failed (%d): %s", rc, srt_last_error());
+        }
+        tb = atomic_load_explicit(&t->tb, memory_order_acquire);
+    }
+    pthread_mutex_unlock(&t->build_lock);
+    return t->build_failed ? NULL : tb;
 }
 
 int topology_computeShortestPaths(Topology* t, int nGPUs) {
     if (!magic_ok(t)) return SRT_E_ARG;
-    if (atomic_load_explicit(&t->built, memory_order_acquire)) return SRT_OK;
-    pthread_mutex_lock(&t->build_lock);
-    int rc = SRT_OK;
-    if (!atomic_load(&t->built)) {
-        if (t->build_failed) {
-            pthread_mutex_unlock(&t->build_lock);
-            return SRT_E_DEVICE;
-        }
-        size_t nn = (size_t)t->n * (size_t)t->n;
-        t->lat_q = (uint32_t*)malloc(nn * sizeof(uint32_t));
-        t->rel = (double*)malloc(nn * sizeof(double));
-        if (!t->lat_q || !t->rel) {
-            rc = SRT_E_NOMEM;
-        } else {
-            srt_edges e;
-            srt_topology_edges(t, &e);
-            srt_build_opts o = t->opts;
-            o.use_shortest_path = t->use_shortest_path;
-            /* nGPUs > 1: one host thread per GPU of this process, RCCL between them */
-            rc = nGPUs > 1 ? srt_build_tables_multi(&e, &o, nGPUs, t->lat_q, &t->quantum_ns, t->rel,
-                                                    &t->stats)
-                           : srt_build_tables(&e, &o, t->lat_q, &t->quantum_ns, t->rel, &t->stats);
-        }
-        if (rc == SRT_OK) {
-            atomic_store_explicit(&t->built, 1, memory_order_release);
-        } else {
-            t->build_failed = 1;
-            srt_log(SRT_LOG_ERROR, "routing table build failed (%d): %s", rc, srt_last_error());
-        }
-    }
-    pthread_mutex_unlock(&t->build_lock);
-    if (rc == SRT_OK) {
-        double mn = srt_topology_min_latency_ms(t);
-        if (mn > 0.0) worker_updateMinTimeJump(mn); /* once, global minimum (:1253-1264) */
-    }
-    return rc;
+    t->ngpus = nGPUs > 1 ? nGPUs : 1;
+    if (!ensure_tables(t, t->ngpus)) return t->build_failed ? SRT_E_DEVICE : SRT_E_NOMEM;
+    export_min(t);
+    return SRT_OK;
 }
 
 int topology_getTable(Topology* t, const uint32_t** latQ, uint64_t* quantumNs, const double** rel,
                       int* n) {
     if (!magic_ok(t)) return SRT_E_ARG;
-    int rc = topology_computeShortestPaths(t, 1);
+    int rc = topology_computeShortestPaths(t, t->ngpus);
     if (rc) return rc;
-    if (latQ) *latQ = t->lat_q;
+    const tables_t* tb = atomic_load_explicit(&t->tb, memory_order_acquire);
+    if (latQ) *latQ = tb->lat_q;
     if (quantumNs) *quantumNs = t->quantum_ns;
-    if (rel) *rel = t->rel;
-    if (n) *n = t->n;
+    if (rel) *rel = tb->rel;
+    if (n) *n = tb->nslot;
     return SRT_OK;
 }
 
-/* _topology_getPathEntry (topology.c:1900-1981): table index of the pair, or an error code. */
-static int64_t path_index(Topology* t, uint32_t srcIp, uint32_t dstIp) {
+int srt_topology_table_info(Topology* t, const int32_t** verts, int32_t* nslot, const double** latMs) {
+    if (!magic_ok(t)) return SRT_E_ARG;
+    const tables_t* tb = atomic_load_explicit(&t->tb, memory_order_acquire);
+    if (!tb) return SRT_E_ARG;
+    if (verts) *verts = tb->verts;
+    if (nslot) *nslot = tb->nslot;
+    if (latMs) *latMs = tb->lat_ms;
+    return SRT_OK;
+}
+
+/* _topology_getPathEntry (topology.c:1900-1981): the tables holding the pair and its index, or
+ * NULL with *err set. */
+static const tables_t* path_entry(Topology* t, uint32_t srcIp, uint32_t dstIp, size_t* idx,
+                                  int32_t* sv, int32_t* dv, int* err) {
     int32_t s = srt_topology_vertex_of_ip(t, srcIp);
     if (s < 0) {
         srt_log(SRT_LOG_ERROR, "source address is not connected to topology");
-        return SRT_E_UNATTACHED;
+        *err = SRT_E_UNATTACHED;
+        return NULL;
     }
     int32_t d = srt_topology_vertex_of_ip(t, dstIp);
     if (d < 0) {
         srt_log(SRT_LOG_ERROR, "destination address is not connected to topology");
-        return SRT_E_UNATTACHED;
+        *err = SRT_E_UNATTACHED;
+        return NULL;
     }
-    if (!atomic_load_explicit(&t->built, memory_order_acquire)) {
-        int rc = topology_computeShortestPaths(t, 1);
-        if (rc) {
+    const tables_t* tb = atomic_load_explicit(&t->tb, memory_order_acquire);
+    if (!tb || tb->slot_of[s] < 0 || tb->slot_of[d] < 0) {
+        tb = ensure_tables(t, t->ngpus);
+        if (!tb || tb->slot_of[s] < 0 || tb->slot_of[d] < 0) {
             srt_log(SRT_LOG_ERROR, "unable to find path between vertex %d and vertex %d", s, d);
             abort(); /* utility_panic (topology.c:1970-1976) */
         }
     }
-    return (int64_t)s * t->n + d;
+    if (atomic_load_explicit(&t->min_gen, memory_order_relaxed) !=
+        atomic_load_explicit(&t->attach_gen, memory_order_relaxed))
+        export_min(t);
+    *idx = (size_t)tb->slot_of[s] * tb->nslot + tb->slot_of[d];
+    if (sv) *sv = s;
+    if (dv) *dv = d;
+    return tb;
 }
 
 double srt_topology_latency_ip(Topology* t, uint32_t srcIp, uint32_t dstIp) {
     if (!magic_ok(t)) return -1.0;
-    int64_t i = path_index(t, srcIp, dstIp);
-    if (i < 0) return -1.0;
-    return (double)((uint64_t)t->lat_q[i] * t->quantum_ns) / 1000000.0;
+    size_t i;
+    int err;
+    const tables_t* tb = path_entry(t, srcIp, dstIp, &i, NULL, NULL, &err);
+    if (!tb) return -1.0;
+    return tables_latency_ms(t, tb, i);
 }
 
 double srt_topology_reliability_ip(Topology* t, uint32_t srcIp, uint32_t dstIp) {
     if (!magic_ok(t)) return -1.0;
-    int64_t i = path_index(t, srcIp, dstIp);
-    if (i < 0) return -1.0;
-    return t->rel[i];
+    size_t i;
+    int err;
+    const tables_t* tb = path_entry(t, srcIp, dstIp, &i, NULL, NULL, &err);
+    if (!tb) return -1.0;
+    return tb->rel[i];
 }
 
-static uint64_t counter_key(Topology* t, int64_t idx) {
-    int64_t s = idx / t->n, d = idx % t->n;
+static uint64_t counter_key(Topology* t, int64_t s, int64_t d) {
     if (!t->directed && d < s) {
         int64_t x = s;
         s = d;
@@ -1100,23 +1282,31 @@ static uint64_t counter_key(Topology* t, int64_t idx) {
     return ((uint64_t)s << 32 | (uint64_t)d) + 1; /* 0 = empty slot */
 }
 
-int srt_topology_increment_ip(Topology* t, uint32_t srcIp, uint32_t dstIp) {
-    if (!magic_ok(t)) return SRT_E_ARG;
-    int64_t i = path_index(t, srcIp, dstIp);
-    if (i < 0) return (int)i;
+static int increment_pair(Topology* t, int32_t s, int32_t d) {
     pthread_mutex_lock(&t->cnt_lock);
-    uint64_t* c = cnt_slot(&t->counters, counter_key(t, i));
+    uint64_t* c = cnt_slot(&t->counters, counter_key(t, s, d));
     if (c) (*c)++;
     pthread_mutex_unlock(&t->cnt_lock);
     return c ? SRT_OK : SRT_E_NOMEM;
 }
 
+int srt_topology_increment_ip(Topology* t, uint32_t srcIp, uint32_t dstIp) {
+    if (!magic_ok(t)) return SRT_E_ARG;
+    size_t i;
+    int32_t s, d;
+    int err;
+    if (!path_entry(t, srcIp, dstIp, &i, &s, &d, &err)) return err;
+    return increment_pair(t, s, d);
+}
+
 uint64_t srt_topology_packet_count_ip(Topology* t, uint32_t srcIp, uint32_t dstIp) {
     if (!magic_ok(t)) return 0;
-    int64_t i = path_index(t, srcIp, dstIp);
-    if (i < 0) return 0;
+    size_t i;
+    int32_t s, d;
+    int err;
+    if (!path_entry(t, srcIp, dstIp, &i, &s, &d, &err)) return 0;
     pthread_mutex_lock(&t->cnt_lock);
-    uint64_t* c = cnt_slot(&t->counters, counter_key(t, i));
+    uint64_t* c = cnt_slot(&t->counters, counter_key(t, s, d));
     uint64_t v = c ? *c : 0;
     pthread_mutex_unlock(&t->cnt_lock);
     return v;
@@ -1130,13 +1320,16 @@ uint64_t srt_topology_packet_count_ip(Topology* t, uint32_t srcIp, uint32_t dstI
 int srt_topology_send_packet_ip(Topology* t, uint32_t srcIp, uint32_t dstIp, double chance,
                                 int bootstrapping, uint64_t payloadLength, uint64_t* delayNs) {
     if (!magic_ok(t)) return SRT_E_ARG;
-    const int64_t i = path_index(t, srcIp, dstIp);
-    if (i < 0) return (int)i;
-    const double reliability = t->rel[i];
+    size_t i;
+    int32_t s, d;
+    int err;
+    const tables_t* tb = path_entry(t, srcIp, dstIp, &i, &s, &d, &err);
+    if (!tb) return err;
+    const double reliability = tb->rel[i];
     if (bootstrapping || chance <= reliability || payloadLength == 0) {
-        const double latency = (double)((uint64_t)t->lat_q[i] * t->quantum_ns) / 1000000.0;
+        const double latency = tables_latency_ms(t, tb, i);
         if (delayNs) *delayNs = (uint64_t)ceil(latency * 1000000.0);
-        const int rc = srt_topology_increment_ip(t, srcIp, dstIp);
+        const int rc = increment_pair(t, s, d);
         return rc ? rc : 1;
     }
     return 0;

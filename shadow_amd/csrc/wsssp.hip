@@ -71,8 +71,8 @@ static __device__ __forceinline__ int wave_scan_max(int v, int lane) {
 
 template <bool DIRECTED, bool LDSD, bool RELP>
 __global__ __launch_bounds__(WL) void wsssp_kernel(
-    int n, int src_begin, int nsrc, const int2* __restrict__ rowptr,
-    const uint2* __restrict__ cw, const double* __restrict__ r,
+    int n, int src_begin, const int32_t* __restrict__ srcs, int nsrc,
+    const int2* __restrict__ rowptr, const uint2* __restrict__ cw, const double* __restrict__ r,
     const int2* __restrict__ in_rowptr, const uint2* __restrict__ in_cw,
     const double* __restrict__ in_r, const int32_t* __restrict__ perm,
     const int32_t* __restrict__ inv, uint32_t* __restrict__ lat, double* __restrict__ rel,
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(WL) void wsssp_kernel(
     const uint32_t bmaskm = (uint32_t)nb - 1u;
 
     for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
-        const int s = inv[src_begin + si];
+        const int s = inv[srcs ? srcs[si] : src_begin + si];
         uint32_t* ol = lat + (size_t)si * ldo; /* output rows, original order */
         double* rr = rel + (size_t)si * ldo;
         for (int v = lane; v < n; v += WL) {
@@ -282,9 +282,6 @@ __global__ __launch_bounds__(WL) void wsssp_kernel(
     }
 }
 
-int srt_sparse_diag(int n, int src_begin, int src_end, const int32_t* rowptr, const int32_t* col,
-                    const uint32_t* w, const double* r, const uint32_t* self_w,
-                    const double* self_r, uint32_t* lat, double* rel, size_t ldo, hipStream_t st);
 
 /* Rows [src_begin, src_end) by the wave-per-source kernel. *overflowed receives the number of
  * sources whose buckets overflowed; their indices (relative to src_begin) are flagged in ovf
@@ -292,8 +289,8 @@ int srt_sparse_diag(int n, int src_begin, int src_end, const int32_t* rowptr, co
 int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, const double* r,
                    const int2* in_rowptr, const uint2* in_cw, const double* in_r,
                    const int32_t* perm, const int32_t* inv, uint32_t max_w, int local,
-                   int src_begin, int src_end, uint32_t* lat, double* rel, int* ovf,
-                   hipStream_t st) {
+                   int src_begin, int src_end, const int32_t* srcs, uint32_t* lat, double* rel,
+                   int* ovf, hipStream_t st) {
     int nb = 1;
     while ((uint32_t)nb <= max_w) nb <<= 1;
     if (nb > 256) {
@@ -360,7 +357,7 @@ int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, con
                                                 hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                                 (int)dyn));                                       \
         wsssp_kernel<D, L, R><<<(unsigned)slots, WL, dyn, st>>>(                                  \
-            n, src_begin, nsrc, rowptr, cw, r, in_rowptr, in_cw, in_r, perm, inv, lat, rel,       \
+            n, src_begin, srcs, nsrc, rowptr, cw, r, in_rowptr, in_cw, in_r, perm, inv, lat, rel, \
             (size_t)n, ws, nb, bcap, ovf);                                                        \
     } while (0)
 #define SRT_WSSSP_LAUNCH2(D, L)                                                                  \
@@ -463,7 +460,8 @@ __global__ void wg_arcs_kernel(int n, const int2* __restrict__ rowptr, const uin
     } while (0)
 template <int WG, bool PROF = false>
 __global__ __launch_bounds__(WG) void wgsssp_kernel(
-    int n, int src_begin, int nsrc, const int2* __restrict__ rowptr, const uint4* __restrict__ ca,
+    int n, int src_begin, const int32_t* __restrict__ srcs, int nsrc,
+    const int2* __restrict__ rowptr, const uint4* __restrict__ ca,
     const double* __restrict__ r, const int32_t* __restrict__ inv, uint32_t* __restrict__ lat,
     double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ ws, int nb, int bcap,
     int* __restrict__ overflow, unsigned long long* __restrict__ prof = nullptr) {
@@ -481,7 +479,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
     double* relp = reinterpret_cast<double*>(buckets + (size_t)nb * bcap);
     const uint32_t bm = (uint32_t)nb - 1u;
     for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
-        const int s = inv[src_begin + si];
+        const int s = inv[srcs ? srcs[si] : src_begin + si];
         uint32_t* ol = lat + (size_t)si * ldo;
         double* rr = rel + (size_t)si * ldo;
         for (int q = tid; q < words; q += WG) sd[q] = 0x3FFFFFFFu; /* three unreached fields */
@@ -664,8 +662,8 @@ int srt_wgsssp_max_n(void) { return 3 * ((140 * 1024) / 4); }
  * max arc weight < 256 quanta). ovf[i] = 1 marks a source to recompute (distance above 1022 or a
  * full bucket). */
 int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r, const int32_t* inv,
-                    uint32_t max_w, int src_begin, int src_end, uint32_t* lat, double* rel,
-                    int* ovf, hipStream_t st) {
+                    uint32_t max_w, int src_begin, int src_end, const int32_t* srcs, uint32_t* lat,
+                    double* rel, int* ovf, hipStream_t st) {
     int nb = 1;
     while ((uint32_t)nb <= max_w) nb <<= 1;
     if (nb > 256 || n > srt_wgsssp_max_n()) {
@@ -712,7 +710,7 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
         SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
         wgsssp_kernel<1024, true><<<(unsigned)slots, 1024, dyn, st>>>(
-            n, src_begin, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf, prof);
+            n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf, prof);
         SRT_HIPCHK(hipGetLastError());
         unsigned long long* h = (unsigned long long*)calloc(slots * 10, sizeof(*h));
         SRT_HIPCHK(hipMemcpyAsync(h, prof, slots * 10 * sizeof(*h), hipMemcpyDeviceToHost, st));
@@ -733,12 +731,12 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     } else if (tenv && atoi(tenv) == 512) {
         SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<512>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-        wgsssp_kernel<512><<<(unsigned)slots, 512, dyn, st>>>(n, src_begin, nsrc, rowptr, ca, r, inv,
+        wgsssp_kernel<512><<<(unsigned)slots, 512, dyn, st>>>(n, src_begin, srcs, nsrc, rowptr, ca, r, inv,
                                                              lat, rel, (size_t)n, ws, nb, bcap, ovf);
     } else {
         SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-        wgsssp_kernel<1024><<<(unsigned)slots, 1024, dyn, st>>>(n, src_begin, nsrc, rowptr, ca, r,
+        wgsssp_kernel<1024><<<(unsigned)slots, 1024, dyn, st>>>(n, src_begin, srcs, nsrc, rowptr, ca, r,
                                                                inv, lat, rel, (size_t)n, ws, nb, bcap,
                                                                ovf);
     }

@@ -153,7 +153,8 @@ class Topology:
         return s
 
     def table(self):
-        """(lat_ns u64 [n,n], rel f64 [n,n]) copies of the finished tables."""
+        """(lat_ns u64 [k,k], rel f64 [k,k]) copies of the current tables over their k vertices
+        (table_vertices(); every vertex while nothing is attached)."""
         latp = ctypes.c_void_p()
         relp = ctypes.c_void_p()
         q = ctypes.c_uint64()
@@ -164,6 +165,20 @@ class Topology:
         lat = np.ctypeslib.as_array(ctypes.cast(latp, ctypes.POINTER(ctypes.c_uint32)), (nn, nn))
         rel = np.ctypeslib.as_array(ctypes.cast(relp, ctypes.POINTER(ctypes.c_double)), (nn, nn))
         return lat.astype(np.uint64) * np.uint64(q.value), rel.copy()
+
+    def table_vertices(self):
+        """(vertices int32 [k], lat_ms f64 [k,k] or None) of the current tables."""
+        vp, mp = ctypes.c_void_p(), ctypes.c_void_p()
+        k = ctypes.c_int32()
+        check(lib().srt_topology_table_info(self._h, ctypes.byref(vp), ctypes.byref(k),
+                                            ctypes.byref(mp)), "srt_topology_table_info")
+        kk = k.value
+        verts = np.ctypeslib.as_array(ctypes.cast(vp, ctypes.POINTER(ctypes.c_int32)), (kk,)).copy()
+        ms = None
+        if mp.value:
+            ms = np.ctypeslib.as_array(ctypes.cast(mp, ctypes.POINTER(ctypes.c_double)),
+                                       (kk, kk)).copy()
+        return verts, ms
 
     def get_latency(self, src, dst) -> float:
         return lib().srt_topology_latency_ip(self._h, ip_to_net(src), ip_to_net(dst))
@@ -212,12 +227,50 @@ class Topology:
         return lib().srt_topology_min_latency_ms(self._h)
 
 
+MIN_HOOK = ctypes.CFUNCTYPE(None, ctypes.c_double)
+
+
+def set_min_time_jump_hook(fn):
+    """Route the runahead export (worker_updateMinTimeJump) to fn(ms); None restores it. Returns
+    the ctypes callback, which the caller must keep alive while it is installed."""
+    cb = MIN_HOOK(fn) if fn is not None else None
+    lib().srt_set_min_time_jump_hook(ctypes.cast(cb, ctypes.c_void_p) if cb else None)
+    return cb
+
+
 def parse_time_nanosec(s: str) -> int:
     return lib().srt_parse_time_nanosec(s.encode())
 
 
 def parse_bandwidth(s: str) -> int:
     return lib().srt_parse_bandwidth(s.encode())
+
+
+def build_tables_subset(n, directed, src, dst, lat_ns, loss, verts=None, use_shortest_path=True,
+                        device=0, algo=_lib.ALGO_AUTO, ngpus=1, want_ms=False):
+    """srt_build_tables_subset -> (lat_ns u64 [k,k], rel f64 [k,k], lat_ms f64 [k,k] or None,
+    min_lat_ns, stats) over the vertices `verts` (increasing; None = all)."""
+    src = np.ascontiguousarray(src, np.int32)
+    dst = np.ascontiguousarray(dst, np.int32)
+    lat_ns = np.ascontiguousarray(lat_ns, np.int64)
+    loss = np.ascontiguousarray(loss, np.float64)
+    e = Edges(n, int(bool(directed)), len(src), src.ctypes.data, dst.ctypes.data,
+              lat_ns.ctypes.data, loss.ctypes.data)
+    o = BuildOpts(device, algo, int(bool(use_shortest_path)), 0)
+    vv = None if verts is None else np.ascontiguousarray(verts, np.int32)
+    k = n if vv is None else len(vv)
+    lat = np.empty((k, k), np.uint32)
+    rel = np.empty((k, k), np.float64)
+    ms = np.empty((k, k), np.float64) if want_ms else None
+    q = ctypes.c_uint64()
+    mn = ctypes.c_uint32()
+    st = BuildStats()
+    check(lib().srt_build_tables_subset(ctypes.byref(e), ctypes.byref(o), int(ngpus), k,
+                                        None if vv is None else vv.ctypes.data, lat.ctypes.data,
+                                        ctypes.byref(q), rel.ctypes.data,
+                                        None if ms is None else ms.ctypes.data, ctypes.byref(mn),
+                                        ctypes.byref(st)), "srt_build_tables_subset")
+    return lat.astype(np.uint64) * np.uint64(q.value), rel, ms, int(mn.value) * q.value, st
 
 
 def build_tables(n, directed, src, dst, lat_ns, loss, use_shortest_path=True, device=0,
