@@ -135,6 +135,90 @@ class Ctx:
 
 
 # ------------------------------------------------------------------------------------------
+# parity helpers (outside the timed region)
+# ------------------------------------------------------------------------------------------
+def all_sum(c: Ctx, v: int) -> int:
+    if c.world == 1:
+        return v
+    t = torch.tensor([v], dtype=torch.int64, device=c.dev)
+    dist.all_reduce(t)
+    return int(t.item())
+
+
+def parity_rows(c: Ctx, rank_range, n: int, k_per_rank: int) -> np.ndarray:
+    """Sample sources: k_per_rank spread over rank 0's rows and over the last rank's
+    (rank_range(q) -> [a, z)), always including the last row of each."""
+    out = set()
+    for q in sorted({0, c.world - 1}):
+        a, z = rank_range(q)
+        z = min(z, n)
+        if z > a:
+            out.update(np.linspace(a, z - 1, k_per_rank).astype(int).tolist())
+    return np.array(sorted(out), np.int32)
+
+
+def dense_range(c: Ctx, n: int):
+    def f(q):
+        bq, eq = ctypes.c_int32(), ctypes.c_int32()
+        c.L.srt_shard_rows(ld_of(n), SHARD_ALIGN, c.world, q, ctypes.byref(bq), ctypes.byref(eq))
+        return bq.value, eq.value
+    return f
+
+
+def gather_rows(c: Ctx, sample, get_lat, get_rel, n, quantum_ns):
+    """Rows of `sample` from the ranks that own them, on rank 0 (numpy): lat in ns, rel f64.
+    Dense shards hold rows [b, e) locally; the last rank sends its sampled rows over the
+    process group."""
+    rng = dense_range(c, n)
+    ld_rows = []
+    owner = []
+    for s in sample:
+        for q in range(c.world):
+            bq, eq = rng(q)
+            if bq <= s < eq:
+                owner.append(q)
+                ld_rows.append(int(s) - bq)
+                break
+    owner = np.array(owner)
+    glat = np.zeros((len(sample), n), np.uint64)
+    grel = np.zeros((len(sample), n), np.float64)
+    for q in sorted(set(owner.tolist())):
+        sel = np.nonzero(owner == q)[0]
+        loc = torch.tensor([ld_rows[i] for i in sel], dtype=torch.int64, device=c.dev)
+        if c.rank == q:
+            tl = get_lat(loc)[:, :n].contiguous()
+            tr = get_rel(loc)[:, :n].contiguous()
+        else:
+            tl = torch.empty((len(sel), n), dtype=torch.int32, device=c.dev)
+            tr = torch.empty((len(sel), n), dtype=torch.float64, device=c.dev)
+        if q != 0 and c.world > 1:
+            dist.broadcast(tl, src=q)
+            dist.broadcast(tr, src=q)
+        if c.rank == 0:
+            glat[sel] = tl.cpu().numpy().view(np.uint32).astype(np.uint64) * np.uint64(quantum_ns)
+            grel[sel] = tr.cpu().numpy()
+    return glat, grel
+
+
+def ld_of(n: int) -> int:
+    return (n + SHARD_ALIGN - 1) // SHARD_ALIGN * SHARD_ALIGN
+
+
+def compare_rows(sample, n, glat, grel, clat, crel) -> dict:
+    """Latency bit-exact off the diagonal; reliability on the entries the row's own source
+    computed (t > s: the lower triangle is the symmetry mirror)."""
+    upper = np.arange(n)[None, :] > sample[:, None]
+    diag = np.arange(n)[None, :] == sample[:, None]
+    lat_ok = bool(np.array_equal(np.where(diag, 0, glat), np.where(diag, 0, clat)))
+    rerr = np.abs(grel - crel) / np.maximum(crel, 1e-300)
+    return {"rows_checked": int(len(sample)), "rows": [int(x) for x in sample],
+            "lat_bit_exact": lat_ok,
+            "rel_max_rel_err_upper": float(rerr[upper].max()) if upper.any() else 0.0,
+            "rel_exact_frac_upper": float((grel[upper] == crel[upper]).mean())
+            if upper.any() else 1.0}
+
+
+# ------------------------------------------------------------------------------------------
 # dense: blocked Floyd-Warshall (C2, C4)
 # ------------------------------------------------------------------------------------------
 def run_dense(c: Ctx, wl):
@@ -238,43 +322,47 @@ def run_dense(c: Ctx, wl):
                  "peak_basis": "256 CU x 4 SIMD x 64 lanes x 2.4 GHz / cycles_per_relax "
                                "(v_add_u32 2 cycles, packed/3-input ops 4 cycles per wave64)"},
     }
+    # untimed check build: the tied-pair count (srt_build_stats.tied_pairs), summed over ranks
+    chk = _lib.BuildStats()
+    chk.count_ties = 1
+    step(chk)
+    tied = all_sum(c, int(chk.tied_pairs))
+    # parity rows: rank 0's first / middle / last rows and the last rank's (gathered to rank 0)
+    sample = parity_rows(c, dense_range(c, n), n, k_per_rank=8)
+    glat, grel = gather_rows(c, sample, lambda rr: lat[rr], lambda rr: rel[rr], n, 1_000_000)
     cpu = parity = None
-    if rank == 0 and world == 1 and not c.args.no_cpu_baseline:
-        import oracle  # cpu_baseline leg only
-        one = np.array([17 % n], np.int32)
-        _, _, _, t1 = oracle.complete_sample(n, wl["seed"], wl["lat_max"], wl["self_max"],
-                                             wl["loss_max"], one, 1)
-        k = int(max(2, min(64, c.args.cpu_seconds / max(t1, 1e-3))))
-        srcs = np.unique(np.linspace(0, n - 1, k).astype(np.int32))
-        clat, crel, gen_s, sssp_s = oracle.complete_sample(n, wl["seed"], wl["lat_max"],
-                                                           wl["self_max"], wl["loss_max"], srcs, 1)
-        cpu = {"value": round(len(srcs) * n / sssp_s, 1), "unit": "node-pairs/s", "cores": 1,
-               "kind": "port",
-               "sample": f"{len(srcs)} of {n} sources, dense O(n^2) Dijkstra per source "
-                         f"(oracle/oracle.c orc_complete_sample), {sssp_s:.1f} s, 1 thread "
-                         f"(the reference serializes Dijkstra on graphLock, topology.c:130-148); "
-                         f"matrix generation ({gen_s:.1f} s) excluded"}
-        # all-cores leg (SURVEY §8d ii): the same per-source Dijkstra sharded over host threads
-        nt = cpu_threads()
-        kk = int(max(nt, min(32 * nt, nt * c.args.cpu_seconds / 2 / max(t1, 1e-3))))
-        msrcs = np.unique(np.linspace(0, n - 1, kk).astype(np.int32))
-        _, _, _, mt_s = oracle.complete_sample(n, wl["seed"], wl["lat_max"], wl["self_max"],
-                                               wl["loss_max"], msrcs, nt)
-        cpu["all_cores"] = {"value": round(len(msrcs) * n / mt_s, 1), "cores": nt,
-                            "sample": f"{len(msrcs)} of {n} sources over {nt} threads, "
-                                      f"{mt_s:.1f} s (no graphLock: the reference cannot do this)"}
-        # full-size parity spot check of the last step's rows against the oracle
-        glat = lat[srcs.astype(np.int64)].cpu().numpy().view(np.uint32)[:, :n].astype(np.uint64) \
-            * np.uint64(1_000_000)
-        grel = rel[srcs.astype(np.int64)].cpu().numpy()[:, :n]
-        upper = np.arange(n)[None, :] > srcs[:, None]
-        diag = np.arange(n)[None, :] == srcs[:, None]
-        lat_ok = bool(np.array_equal(np.where(diag, 0, glat), np.where(diag, 0, clat)))
-        rerr = np.abs(grel - crel) / np.maximum(crel, 1e-300)
-        parity = {"rows_checked": int(len(srcs)), "lat_bit_exact": lat_ok,
-                  "rel_max_rel_err_upper": float(rerr[upper].max()) if upper.any() else 0.0,
-                  "rel_exact_frac_upper": float((grel[upper] == crel[upper]).mean())
-                  if upper.any() else 1.0}
+    if rank == 0 and not c.args.no_cpu_baseline:
+        import oracle  # cpu_baseline leg and the parity check only
+        if world == 1:
+            one = np.array([17 % n], np.int32)
+            _, _, _, t1 = oracle.complete_sample(n, wl["seed"], wl["lat_max"], wl["self_max"],
+                                                 wl["loss_max"], one, 1)
+            k = int(max(2, min(64, c.args.cpu_seconds / max(t1, 1e-3))))
+            srcs = np.unique(np.linspace(0, n - 1, k).astype(np.int32))
+            _, _, gen_s, sssp_s = oracle.complete_sample(n, wl["seed"], wl["lat_max"],
+                                                         wl["self_max"], wl["loss_max"], srcs, 1)
+            cpu = {"value": round(len(srcs) * n / sssp_s, 1), "unit": "node-pairs/s", "cores": 1,
+                   "kind": "port",
+                   "sample": f"{len(srcs)} of {n} sources, dense O(n^2) Dijkstra per source "
+                             f"(oracle/oracle.c orc_complete_sample), {sssp_s:.1f} s, 1 thread "
+                             f"(the reference serializes Dijkstra on graphLock, topology.c:130-148); "
+                             f"matrix generation ({gen_s:.1f} s) excluded"}
+            # all-cores leg (SURVEY §8d ii): the same per-source Dijkstra sharded over host threads
+            nt = cpu_threads()
+            kk = int(max(nt, min(32 * nt, nt * c.args.cpu_seconds / 2 / max(t1, 1e-3))))
+            msrcs = np.unique(np.linspace(0, n - 1, kk).astype(np.int32))
+            _, _, _, mt_s = oracle.complete_sample(n, wl["seed"], wl["lat_max"], wl["self_max"],
+                                                   wl["loss_max"], msrcs, nt)
+            cpu["all_cores"] = {"value": round(len(msrcs) * n / mt_s, 1), "cores": nt,
+                                "sample": f"{len(msrcs)} of {n} sources over {nt} threads, "
+                                          f"{mt_s:.1f} s (no graphLock: the reference cannot do "
+                                          f"this)"}
+        # full-size parity of the last build's rows against the oracle
+        clat, crel, _, _ = oracle.complete_sample(n, wl["seed"], wl["lat_max"], wl["self_max"],
+                                                  wl["loss_max"], sample, cpu_threads())
+        parity = compare_rows(sample, n, glat, grel, clat, crel)
+    if parity is not None:
+        parity.update({"tied_pairs": tied, "tied_frac": tied / float(n * (n - 1))})
     s0 = stats[-1]
     config = {"workload": wl["desc"], "n": n, "ld": ld, "fw_block": FW_B,
               "parallelism": f"row-shard x{world}" + (" + RCCL pivot-panel broadcast"
@@ -341,48 +429,56 @@ def run_sparse(c: Ctx, wl):
         "launches_timed": len(stats),
         "model": "per source: (n+1)*4 + arcs*16 + n*12 B (SURVEY §8d work-efficient gather model)",
         "relax_per_launch": float(nsrc) * arcs}
+    # untimed check build: the tied-pair count over this rank's rows, summed over ranks
+    chk = _lib.BuildStats()
+    chk.count_ties = 1
+    step(chk)
+    tied = all_sum(c, int(chk.tied_pairs))
+    # after the all-gather every rank holds every row: rank 0 checks its own block's and the
+    # last rank's block's rows
+    sample = parity_rows(c, lambda q: (q * per, (q + 1) * per), n, k_per_rank=8)
+    glat = rel_rows = None
+    if rank == 0:
+        idx = torch.from_numpy(sample.astype(np.int64)).to(c.dev)
+        glat = lat.index_select(0, idx).cpu().numpy().view(np.uint32).astype(np.uint64) \
+            * np.uint64(sg.quantum_ns)
+        rel_rows = rel.index_select(0, idx).cpu().numpy()
     cpu = parity = None
-    if rank == 0 and world == 1 and not c.args.no_cpu_baseline:
-        import oracle  # cpu_baseline leg only
+    if rank == 0 and not c.args.no_cpu_baseline:
+        import oracle  # cpu_baseline leg and the parity check only
         el = oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
-        t1 = time.perf_counter()
-        oracle.sssp_rows(el, 0, 1)
-        one = max(time.perf_counter() - t1, 1e-4)
-        k = int(max(2, min(2000, c.args.cpu_seconds / one)))
-        srcs = np.linspace(0, n - k, 3).astype(np.int64)  # three contiguous sample blocks
-        kk = max(1, k // 3)
-        t1 = time.perf_counter()
-        rows = [(int(a), oracle.sssp_rows(el, int(a), int(a) + kk)) for a in srcs]
-        cs = time.perf_counter() - t1
-        cpu = {"value": round(3 * kk * n / cs, 1), "unit": "node-pairs/s", "cores": 1,
-               "kind": "port",
-               "sample": f"{3 * kk} of {n} sources (3 blocks of {kk}), binary-heap Dijkstra per "
-                         f"source (oracle/oracle.c orc_sssp_rows), {cs:.1f} s, 1 thread (the "
-                         f"reference serializes Dijkstra on graphLock, topology.c:130-148)"}
-        nt = cpu_threads()
-        mk = int(max(nt, min(256 * nt, nt * c.args.cpu_seconds / 2 / one)))
-        mk = min(mk, max(nt, int(2e9 / (n * 32))))  # the oracle's output rows: <= ~2 GB
-        a0 = max(0, n // 2 - mk // 2)
-        t1 = time.perf_counter()
-        oracle.sssp_rows(el, a0, min(n, a0 + mk), nthreads=nt)
-        mt_s = time.perf_counter() - t1
-        cpu["all_cores"] = {"value": round(min(mk, n - a0) * n / mt_s, 1), "cores": nt,
-                            "sample": f"{min(mk, n - a0)} of {n} sources over {nt} threads, "
-                                      f"{mt_s:.1f} s (no graphLock: the reference cannot do this)"}
-        ok, worst, exact = True, 0.0, 1.0
-        for a, ex in rows:
-            glat = lat[a:a + kk].cpu().numpy().view(np.uint32).astype(np.uint64) \
-                * np.uint64(sg.quantum_ns)
-            grel = rel[a:a + kk].cpu().numpy()
-            off = np.arange(n)[None, :] != np.arange(a, a + kk)[:, None]
-            upper = np.arange(n)[None, :] > np.arange(a, a + kk)[:, None]
-            ok &= bool(np.array_equal(np.where(off, glat, 0), np.where(off, ex["lat_int"], 0)))
-            err = np.abs(grel - ex["rel"]) / np.maximum(ex["rel"], 1e-300)
-            worst = max(worst, float(err[upper].max()) if upper.any() else 0.0)
-            exact = min(exact, float((grel[upper] == ex["rel"][upper]).mean()) if upper.any()
-                        else 1.0)
-        parity = {"rows_checked": 3 * kk, "lat_bit_exact": ok, "rel_max_rel_err_upper": worst,
-                  "rel_exact_frac_upper": exact}
+        if world == 1:
+            t1 = time.perf_counter()
+            oracle.sssp_rows(el, 0, 1)
+            one = max(time.perf_counter() - t1, 1e-4)
+            k = int(max(2, min(2000, c.args.cpu_seconds / one)))
+            srcs = np.linspace(0, n - k, 3).astype(np.int64)  # three contiguous sample blocks
+            kk = max(1, k // 3)
+            t1 = time.perf_counter()
+            for a in srcs:
+                oracle.sssp_rows(el, int(a), int(a) + kk)
+            cs = time.perf_counter() - t1
+            cpu = {"value": round(3 * kk * n / cs, 1), "unit": "node-pairs/s", "cores": 1,
+                   "kind": "port",
+                   "sample": f"{3 * kk} of {n} sources (3 blocks of {kk}), binary-heap Dijkstra "
+                             f"per source (oracle/oracle.c orc_sssp_rows), {cs:.1f} s, 1 thread "
+                             f"(the reference serializes Dijkstra on graphLock, "
+                             f"topology.c:130-148)"}
+            nt = cpu_threads()
+            mk = int(max(nt, min(256 * nt, nt * c.args.cpu_seconds / 2 / one)))
+            mk = min(mk, max(nt, int(2e9 / (n * 32))))  # the oracle's output rows: <= ~2 GB
+            a0 = max(0, n // 2 - mk // 2)
+            t1 = time.perf_counter()
+            oracle.sssp_rows(el, a0, min(n, a0 + mk), nthreads=nt)
+            mt_s = time.perf_counter() - t1
+            cpu["all_cores"] = {"value": round(min(mk, n - a0) * n / mt_s, 1), "cores": nt,
+                                "sample": f"{min(mk, n - a0)} of {n} sources over {nt} threads, "
+                                          f"{mt_s:.1f} s (no graphLock: the reference cannot do "
+                                          f"this)"}
+        ex = oracle.sssp_list(el, sample, nthreads=cpu_threads())
+        parity = compare_rows(sample, n, glat, rel_rows, ex["lat_int"], ex["rel"])
+    if parity is not None:
+        parity.update({"tied_pairs": tied, "tied_frac": tied / float(n * (n - 1))})
     sg.free()
     s0st = stats[-1]
     config = {"workload": wl["desc"], "n": n, "edges": int(g.m), "arcs": int(arcs),

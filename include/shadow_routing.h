@@ -80,6 +80,11 @@ typedef struct srt_build_stats {
                           * update streams (one GPU, n >= 8192), 4 = u16 with
                           * f16-compare mins, upper-triangle rounds (undirected, one shard),
                           * 3 = u16 f16-compare (cap 0x3DFF), 2 = u16 pk_min (cap 0x7FFF), 1 = u32 */
+    int32_t count_ties;  /* input: 1 = count tied pairs (below) */
+    int64_t tied_pairs;  /* pairs (s, t), s != t, whose smallest D[s][u] over the tight
+                          * predecessors u of t is reached by two or more u: igraph's heap order
+                          * picks the reference's predecessor there (topology.c:1679-1701), the
+                          * build takes the smallest u -- the class where reliability can differ */
 } srt_build_stats;
 
 /* Build the full tables for an edge list on one GPU; outputs are host buffers of n*n entries.

@@ -60,6 +60,8 @@ class BuildStats(ctypes.Structure):
         ("ms_update", ctypes.c_double),
         ("ms_comm", ctypes.c_double),
         ("dist_enc", ctypes.c_int32),
+        ("count_ties", ctypes.c_int32),
+        ("tied_pairs", ctypes.c_int64),
     ]
 
 

@@ -382,9 +382,16 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
     const bool block = (kenv && !strcmp(kenv, "block")) || (wenv && !strcmp(wenv, "hbm"));
     int rc = SRT_OK;
     if (block || g->max_w >= 256) {
+        const int ct = stats && stats->count_ties;
         rc = srt_sparse_block_rows(g->n, g->rp, g->col, g->w, g->r, g->irp, g->icol, g->iw, g->ir,
                                    g->sw, g->sr, b0, b0 + nsrc, srcs, g->delta, lat_rows, rel_rows,
                                    st, stats);
+        if (!rc && ct) {
+            stats->count_ties = 1;
+            stats->tied_pairs = 0;
+            rc = srt_tie_count_rows(g->n, nsrc, srcs, b0, lat_rows, (size_t)g->n, g->irp, g->icol,
+                                    g->iw, &stats->tied_pairs, st);
+        }
         if (!rc && lms)
             rc = srt_path_ms_rows(g->n, nsrc, srcs, b0, lat_rows, (size_t)g->n, NULL, 0, g->irp,
                                   g->icol, g->iw, g->quantum_ns, lms, (size_t)g->n, st);
@@ -493,6 +500,11 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
     float a = 0, b = 0;
     SRT_HIPCHK(hipEventElapsedTime(&a, e0, e1));
     SRT_HIPCHK(hipEventElapsedTime(&b, e0, e2));
+    int64_t tied = 0; /* outside the timed span: a check pass, not part of the build */
+    if (stats && stats->count_ties &&
+        (rc = srt_tie_count_rows(g->n, nsrc, srcs, b0, lat_rows, (size_t)g->n, g->irp, g->icol,
+                                 g->iw, &tied, st)))
+        return rc;
     if (nov) srt_log(SRT_LOG_INFO, "wsssp: %d of %d sources overflowed their buckets and were "
                      "recomputed", nov, nsrc);
     if (stats) {
@@ -503,6 +515,7 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
         stats->ms_update = a;
         stats->ess_arcs = nov; /* sparse builds: sources recomputed after a bucket overflow */
         stats->dist_enc = wg ? 2 : 1; /* sparse builds: 2 = workgroup kernel, 1 = wave kernel */
+        stats->tied_pairs = tied;
     }
     return SRT_OK;
 }
@@ -546,6 +559,7 @@ static void merge_stats(srt_build_stats* acc, const srt_build_stats* s, int firs
     acc->ms_update += s->ms_update;
     acc->n_update += s->n_update;
     acc->ess_arcs += s->ess_arcs;
+    acc->tied_pairs += s->tied_pairs;
     acc->max_depth = s->max_depth > acc->max_depth ? s->max_depth : acc->max_depth;
     if (s->dist_enc < acc->dist_enc) acc->dist_enc = s->dist_enc;
 }
@@ -594,7 +608,10 @@ static int build_one(const srt_canon* c, const srt_build_opts* opts, int algo, i
     const uint64_t q = c->quantum_ns;
     srt_build_stats local;
     memset(&local, 0, sizeof(local));
-    if (stats) local.time_kernels = stats->time_kernels;
+    if (stats) {
+        local.time_kernels = stats->time_kernels;
+        local.count_ties = stats->count_ties;
+    }
     dbufs B;
     B.k = 0;
     hipStream_t st = NULL;
@@ -704,6 +721,7 @@ static int build_one(const srt_canon* c, const srt_build_opts* opts, int algo, i
             const int r1 = r0 + chunk < nsub ? r0 + chunk : nsub;
             srt_build_stats cs;
             memset(&cs, 0, sizeof(cs));
+            cs.count_ties = local.count_ties;
             if (verts) {
                 rc = sparse_rows(sg, 0, r1 - r0, dverts + r0, dlat, drel, dms, st, &cs);
                 if (!rc) rc = srt_gather_sub_u32(r1 - r0, nsub, NULL, dverts, dlat, n, slat + (size_t)r0 * nsub, nsub, st);
@@ -926,6 +944,7 @@ static void* mjob_sparse(void* p) {
         const int r1 = r0 + chunk < s1 ? r0 + chunk : s1;
         srt_build_stats cs;
         memset(&cs, 0, sizeof(cs));
+        cs.count_ties = j->st.count_ties;
         if (j->verts) {
             TRY(sparse_rows(sg, 0, r1 - r0, dverts + r0, dlat, drel, dms, st, &cs));
             TRY(srt_gather_sub_u32(r1 - r0, nsub, NULL, dverts, dlat, n, slat + (size_t)r0 * nsub, nsub, st));
@@ -1024,6 +1043,10 @@ static int build_multi(const srt_canon* c, const srt_build_opts* opts, int algo,
         j->rel = rel;
         j->lat_ms = lat_ms;
         j->min_q = 0xFFFFFFFFu;
+        if (stats) {
+            j->st.count_ties = stats->count_ties;
+            j->st.time_kernels = stats->time_kernels;
+        }
         if (pthread_create(&th[i], NULL, algo == SRT_ALGO_DENSE_FW ? mjob_dense : mjob_sparse, j)) {
             rc = SRT_E_NOMEM;
             srt_set_error("srt_build_tables_multi: pthread_create failed for rank %d", i);
@@ -1047,7 +1070,10 @@ static int build_multi(const srt_canon* c, const srt_build_opts* opts, int algo,
         uint32_t m = 0xFFFFFFFFu;
         for (int i = 0; i < R; i++) m = jobs[i].min_q < m ? jobs[i].min_q : m;
         *min_q = m;
-        if (stats) *stats = jobs[0].st;
+        if (stats) {
+            *stats = jobs[0].st;
+            for (int i = 1; i < R; i++) stats->tied_pairs += jobs[i].st.tied_pairs;
+        }
     }
 done:
     if (comms)

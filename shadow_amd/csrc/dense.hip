@@ -471,7 +471,27 @@ __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, cons
     }
 }
 
-template <typename T, bool UR>
+/* Running minimum of canonical keys (high part D[s][u], low part u or its rank); with TIES, *tie
+ * records whether the minimum D is reached by two different candidates -- the pairs whose
+ * predecessor igraph's heap order decides (equal tentative distances settle in an
+ * order the build cannot reproduce), reported as srt_build_stats.tied_pairs. */
+template <bool TIES, int SH, typename K>
+__device__ __forceinline__ void key_min(K& best, uint32_t& tie, K key) {
+    if constexpr (TIES) {
+        const bool same = key != ~(K)0 && (key >> SH) == (best >> SH);
+        tie = key < best ? (uint32_t)same : (tie | (uint32_t)same);
+    }
+    best = min(best, key);
+}
+
+/* one atomic per wave: the wave's tie count */
+static __device__ __forceinline__ void add_ties(unsigned long long* out, uint32_t c) {
+    unsigned long long v = c;
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(out, v);
+}
+
+template <typename T, bool UR, bool TIES>
 __global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nloc, int ldT,
                                                         size_t bsD, const T* __restrict__ DT,
                                                         const int32_t* __restrict__ iptr,
@@ -479,7 +499,8 @@ __global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nlo
                                                         const double* __restrict__ ar,
                                                         int32_t* __restrict__ predT,
                                                         double* __restrict__ rT, int nsb,
-                                                        int tch, int tper, int sorted) {
+                                                        int tch, int tper, int sorted,
+                                                        unsigned long long* __restrict__ ties) {
     /* UR: write the predecessor vertex and the reliability of its arc (predT, rT) for the
      * level-order pass; otherwise the arc index.
      * sorted: t's in-arc list is in ascending u (undirected: the out-lists of the ballot-compacted
@@ -499,8 +520,10 @@ __global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nlo
     const int t1 = min(n, (tc + 1) * tper);
     /* this source block's contiguous slab of the block-major transpose: DB[u * 64] = D[s][u] */
     const T* __restrict__ DB = DT + (size_t)sb * bsD + lane;
+    uint32_t nties = 0;
     for (int t = tc * tper + wv; t < t1; t += 4) {
         const uint32_t dst = DB[(size_t)t * 64];
+        uint32_t tie = 0;
         const int kb = __builtin_amdgcn_readfirstlane(iptr[t]);
         const int ke = __builtin_amdgcn_readfirstlane(iptr[t + 1]);
         int bk = -1;
@@ -508,9 +531,10 @@ __global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nlo
             uint32_t best = 0xFFFFFFFFu;
             int k = kb;
 #define SRT_PRED_TRY32(dd, aa, kk)                                                              \
-    best = min(best, ((dd) + (aa).y == dst)                                                    \
-                         ? (((dd) << 16) | (sorted ? (uint32_t)((kk) - kb) : (aa).x))          \
-                         : 0xFFFFFFFFu);
+    key_min<TIES, 16>(best, tie,                                                               \
+                      ((dd) + (aa).y == dst)                                                   \
+                          ? (((dd) << 16) | (sorted ? (uint32_t)((kk) - kb) : (aa).x))         \
+                          : 0xFFFFFFFFu);
             /* 16 (then 4, 1) candidate arcs per step: one batch of scalar loads, then the gathers
              * in flight together. The loop is latency bound: with 4 per step, u8 and u16 distances
              * measured the same (47 ms on C4); 16 per step 37 ms; 32 per step no better. */
@@ -555,13 +579,12 @@ __global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nlo
                 const uint32_t d0 = DB[(size_t)a0.x * 64];
                 if (d0 + a0.y == dst) {
                     const uint64_t key = ((uint64_t)d0 << 32) | a0.x;
-                    if (key < best) {
-                        best = key;
-                        bk = k;
-                    }
+                    if (key < best) bk = k;
+                    key_min<TIES, 32>(best, tie, key);
                 }
             }
         }
+        if (TIES && valid && s != t) nties += tie;
         if (valid) {
             const size_t o = (size_t)t * ldT + sl;
             if (UR) {
@@ -573,12 +596,13 @@ __global__ __launch_bounds__(256) void pred_cols_kernel(int n, int row0, int nlo
             }
         }
     }
+    if (TIES) add_ties(ties, nties);
 }
 
 /* Byte distances, two sources per lane: a wave covers a 128-source block, one 128-B line of its
  * block-major slab (DT[s / 128][u][s % 128], 4 MB at n = 32,768) per candidate arc. Same keys and
  * outputs as pred_cols_kernel<uint8_t, true> for each of the lane's two sources. */
-template <int U>
+template <int U, bool TIES>
 __global__ __launch_bounds__(256) void pred_cols2_kernel(int n, int row0, int nloc, int ldT,
                                                          size_t bsD, const uint8_t* __restrict__ DT,
                                                          const int32_t* __restrict__ iptr,
@@ -586,7 +610,8 @@ __global__ __launch_bounds__(256) void pred_cols2_kernel(int n, int row0, int nl
                                                          const double* __restrict__ ar,
                                                          int32_t* __restrict__ predT,
                                                          double* __restrict__ rT, int nsb, int tch,
-                                                         int tper, int sorted) {
+                                                         int tper, int sorted,
+                                                         unsigned long long* __restrict__ ties) {
     const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
     const int sb = (j / tch) * 8 + xcd, tc = j % tch;
     if (sb >= nsb) return;
@@ -602,7 +627,9 @@ __global__ __launch_bounds__(256) void pred_cols2_kernel(int n, int row0, int nl
         const_cast<uint8_t*>(DT) + (size_t)sb * bsD, 0, (int)bsD, 0x00020000);
     const int voff = 2 * lane;
 #define SRT_DB(u) ((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(slab, voff, (int)(u) * 128, 0))
+    uint32_t nties = 0;
     for (int t = tc * tper + wv; t < t1; t += 4) {
+        uint32_t tie0 = 0, tie1 = 0;
         const uint32_t dst = SRT_DB(t);
         const uint32_t dst0 = dst & 0xFFu, dst1 = dst >> 8;
         const int kb = __builtin_amdgcn_readfirstlane(iptr[t]);
@@ -613,8 +640,8 @@ __global__ __launch_bounds__(256) void pred_cols2_kernel(int n, int row0, int nl
     {                                                                                           \
         const uint32_t lo = (dd) & 0xFFu, hi = (dd) >> 8;                                       \
         const uint32_t id = sorted ? (uint32_t)((kk) - kb) : (aa).x;                            \
-        best0 = min(best0, (lo + (aa).y == dst0) ? ((lo << 16) | id) : 0xFFFFFFFFu);            \
-        best1 = min(best1, (hi + (aa).y == dst1) ? ((hi << 16) | id) : 0xFFFFFFFFu);            \
+        key_min<TIES, 16>(best0, tie0, (lo + (aa).y == dst0) ? ((lo << 16) | id) : 0xFFFFFFFFu); \
+        key_min<TIES, 16>(best1, tie1, (hi + (aa).y == dst1) ? ((hi << 16) | id) : 0xFFFFFFFFu); \
     }
         for (; k + U <= ke; k += U) {
             uint2 a[U];
@@ -657,6 +684,7 @@ __global__ __launch_bounds__(256) void pred_cols2_kernel(int n, int row0, int nl
         }
         const size_t o = (size_t)t * ldT + sl;
         const bool h0 = s != t && bk0 >= 0, h1 = s + 1 != t && bk1 >= 0;
+        if (TIES) nties += (v0 && h0 ? tie0 : 0u) + (v1 && h1 ? tie1 : 0u);
         if (v0 && v1 && (o & 1) == 0) {
             *reinterpret_cast<int2*>(predT + o) =
                 make_int2(h0 ? (int32_t)uw[bk0].x : -1, h1 ? (int32_t)uw[bk1].x : -1);
@@ -674,6 +702,7 @@ __global__ __launch_bounds__(256) void pred_cols2_kernel(int n, int row0, int nl
         }
     }
 #undef SRT_DB
+    if (TIES) add_ties(ties, nties);
 }
 
 /* Path-order reliability by sweeps for rows with a large distance range (rel_levels_kernel
@@ -949,6 +978,7 @@ __global__ __launch_bounds__(256) void unpack_transpose_kernel(int nrows, int ld
 typedef struct {
     size_t n_cap, arc_cap, tarc_cap, x_cap;
     int32_t *cnt, *ptr, *tptr, *cursor, *col, *tcol, *depth;
+    unsigned long long* ties; /* tied-pair count of the predecessor pass */
     uint32_t *aw, *tw;
     double *ar, *tr, *xsend, *xrecv;
     uint32_t* panel;
@@ -983,6 +1013,7 @@ static int ws_get(dense_ws** out, int n) {
             SRT_HIPCHK(hipFree(ws->tptr));
             SRT_HIPCHK(hipFree(ws->cursor));
             SRT_HIPCHK(hipFree(ws->depth));
+            SRT_HIPCHK(hipFree(ws->ties));
         }
         size_t c = (size_t)n + 1;
         SRT_HIPCHK(hipMalloc(&ws->cnt, c * sizeof(int32_t)));
@@ -990,6 +1021,7 @@ static int ws_get(dense_ws** out, int n) {
         SRT_HIPCHK(hipMalloc(&ws->tptr, c * sizeof(int32_t)));
         SRT_HIPCHK(hipMalloc(&ws->cursor, c * sizeof(int32_t)));
         SRT_HIPCHK(hipMalloc(&ws->depth, sizeof(int32_t)));
+        SRT_HIPCHK(hipMalloc(&ws->ties, sizeof(unsigned long long)));
         ws->n_cap = c;
     }
     *out = ws;
@@ -1059,6 +1091,8 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         ir = ws->tr;
     }
     SRT_HIPCHK(hipMemsetAsync(ws->depth, 0, sizeof(int32_t), st));
+    const bool ties = stats && stats->count_ties;
+    if (ties) SRT_HIPCHK(hipMemsetAsync(ws->ties, 0, sizeof(unsigned long long), st));
     if (n > srt_dense_max_n()) { /* the entry points refuse such n before FW */
         srt_set_error("dense predecessor pass supports n <= %d (n = %d)", srt_dense_max_n(), n);
         return SRT_E_RANGE;
@@ -1100,22 +1134,37 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
                                                      256, 0, st>>>(nrows, ld, d16, (size_t)ld, dt8,
                                                                    (size_t)ld * 128);
             /* 16 candidate arcs in flight per step: 17.3 ms on C4 against 18.7 (8) and 20.0 (32) */
-            pred_cols2_kernel<16><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
-                n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
-                nsb2, tch, tper, !directed);
+            if (ties)
+                pred_cols2_kernel<16, true><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
+                    n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
+                    nsb2, tch, tper, !directed, ws->ties);
+            else
+                pred_cols2_kernel<16, false><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
+                    n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
+                    nsb2, tch, tper, !directed, ws->ties);
         } else if (d16) {
             uint16_t* dt16 = reinterpret_cast<uint16_t*>(ws->dt);
             transpose_kernel<uint16_t, uint16_t, 64><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)),
                                                          256, 0, st>>>(nrows, ld, d16, (size_t)ld, dt16, bsD);
-            pred_cols_kernel<uint16_t, true><<<grid, 256, 0, st>>>(
-                n, row0, lrows, nrows, bsD, dt16, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper,
-                !directed);
+            if (ties)
+                pred_cols_kernel<uint16_t, true, true><<<grid, 256, 0, st>>>(
+                    n, row0, lrows, nrows, bsD, dt16, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch,
+                    tper, !directed, ws->ties);
+            else
+                pred_cols_kernel<uint16_t, true, false><<<grid, 256, 0, st>>>(
+                    n, row0, lrows, nrows, bsD, dt16, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch,
+                    tper, !directed, ws->ties);
         } else {
             transpose_kernel<uint32_t, uint32_t, 64><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)),
                                                          256, 0, st>>>(nrows, ld, d, (size_t)ld, ws->dt, bsD);
-            pred_cols_kernel<uint32_t, true><<<grid, 256, 0, st>>>(
-                n, row0, lrows, nrows, bsD, ws->dt, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch, tper,
-                !directed);
+            if (ties)
+                pred_cols_kernel<uint32_t, true, true><<<grid, 256, 0, st>>>(
+                    n, row0, lrows, nrows, bsD, ws->dt, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch,
+                    tper, !directed, ws->ties);
+            else
+                pred_cols_kernel<uint32_t, true, false><<<grid, 256, 0, st>>>(
+                    n, row0, lrows, nrows, bsD, ws->dt, iptr, ws->uw, ir, ws->predt, ws->rt, nsb, tch,
+                    tper, !directed, ws->ties);
         }
         /* predecessor rows pred[sl][t] = predT[t][sl] (reuses the DT buffer) and the arc
          * reliabilities straight into the rel rows, where the passes below finish them in place */
@@ -1169,9 +1218,13 @@ static int dense_finish_rows(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
         int rc = ws_get(&ws, n);
         if (rc) return rc;
         int32_t depth = 0;
+        unsigned long long nt = 0;
         SRT_HIPCHK(hipMemcpyAsync(&depth, ws->depth, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        if (stats->count_ties)
+            SRT_HIPCHK(hipMemcpyAsync(&nt, ws->ties, sizeof(nt), hipMemcpyDeviceToHost, st));
         SRT_HIPCHK(hipStreamSynchronize(st));
         stats->max_depth = depth;
+        stats->tied_pairs = (int64_t)nt;
     }
     return SRT_OK;
 }

@@ -179,6 +179,10 @@ int srt_gather_sub_u32(int nr, int nc, const int32_t* rows, const int32_t* cols,
 int srt_gather_sub_f64(int nr, int nc, const int32_t* rows, const int32_t* cols, const double* in,
                        size_t ldi, double* out, size_t ldo, hipStream_t st);
 int srt_table_min(int rows, int cols, const uint32_t* t, size_t ld, uint32_t* dmin, hipStream_t st);
+/* adds the tied pairs of nrows distance rows (diagonal rule applied) to *tied */
+int srt_tie_count_rows(int n, int nrows, const int32_t* srcs, int src_begin, const uint32_t* D,
+                       size_t ldd, const int32_t* irp, const int32_t* icol, const uint32_t* iw,
+                       int64_t* tied, hipStream_t st);
 int srt_quanta_to_ms(int rows, int cols, const uint32_t* w, size_t ldw, uint64_t q, double* out,
                      size_t ldo, hipStream_t st);
 /* collectives: all-gather of equal byte blocks, rank q's block at buf + q * bytes */

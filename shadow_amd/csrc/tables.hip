@@ -290,3 +290,55 @@ int srt_quanta_to_ms(int rows, int cols, const uint32_t* w, size_t ldw, uint64_t
     SRT_HIPCHK(hipGetLastError());
     return SRT_OK;
 }
+
+/* Tied pairs of rows built by the SSSP kernels (srt_build_stats.tied_pairs): targets t != s whose
+ * smallest D[s][u] over tight in-arcs u -> t is reached by two or more u (with D[s][s] = 0) --
+ * the class where igraph's heap order, not the canonical rule, picks the reference's predecessor. */
+__global__ __launch_bounds__(256) void tie_count_kernel(int n, int nrows, const int32_t* __restrict__ srcs,
+                                                        int src_begin, const uint32_t* __restrict__ D,
+                                                        size_t ldd, const int32_t* __restrict__ irp,
+                                                        const int32_t* __restrict__ icol,
+                                                        const uint32_t* __restrict__ iw,
+                                                        unsigned long long* __restrict__ out) {
+    unsigned long long c = 0;
+    for (int r = blockIdx.y; r < nrows; r += gridDim.y) {
+        const int s = srcs ? srcs[r] : src_begin + r;
+        const uint32_t* Dr = D + (size_t)r * ldd;
+        for (int t = blockIdx.x * 256 + threadIdx.x; t < n; t += gridDim.x * 256) {
+            const uint32_t dt = Dr[t];
+            if (t == s || dt >= SRT_INF) continue;
+            uint32_t best = SRT_INF, cnt = 0;
+            const int ke = irp[t + 1];
+            for (int k = irp[t]; k < ke; ++k) {
+                const int u = icol[k];
+                const uint32_t du = u == s ? 0u : Dr[u];
+                if (du < SRT_INF && du + iw[k] == dt) {
+                    cnt = du < best ? 1u : cnt + (du == best);
+                    best = min(best, du);
+                }
+            }
+            c += cnt >= 2;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
+
+int srt_tie_count_rows(int n, int nrows, const int32_t* srcs, int src_begin, const uint32_t* D,
+                       size_t ldd, const int32_t* irp, const int32_t* icol, const uint32_t* iw,
+                       int64_t* tied, hipStream_t st) {
+    if (nrows <= 0) return SRT_OK;
+    unsigned long long* d = NULL;
+    SRT_HIPCHK(hipMallocAsync((void**)&d, sizeof(*d), st));
+    SRT_HIPCHK(hipMemsetAsync(d, 0, sizeof(*d), st));
+    dim3 g((unsigned)(srt_ceil_div(n, 256) < 8 ? srt_ceil_div(n, 256) : 8),
+           (unsigned)(nrows < 8192 ? nrows : 8192));
+    tie_count_kernel<<<g, 256, 0, st>>>(n, nrows, srcs, src_begin, D, ldd, irp, icol, iw, d);
+    SRT_HIPCHK(hipGetLastError());
+    unsigned long long h = 0;
+    SRT_HIPCHK(hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, st));
+    SRT_HIPCHK(hipFreeAsync(d, st));
+    SRT_HIPCHK(hipStreamSynchronize(st));
+    *tied += (int64_t)h;
+    return SRT_OK;
+}

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("workload", ["c2"])
+@pytest.mark.parametrize("workload", ["c2", "c3"])
 def test_bench_json_line_contract(workload):
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--workload", workload,
                           "--steps", "2", "--warmup", "1", "--cpu-seconds", "1"],
@@ -35,3 +35,5 @@ def test_bench_json_line_contract(workload):
     assert cb["all_cores"]["cores"] >= 1 and cb["all_cores"]["value"] > 0
     assert d["parity"]["lat_bit_exact"] is True
     assert d["parity"]["rel_max_rel_err_upper"] <= 1e-12
+    assert d["parity"]["rows_checked"] >= 4 and d["parity"]["tied_pairs"] >= 0
+    assert 0.0 <= d["parity"]["tied_frac"] < 0.5
