@@ -268,9 +268,11 @@ def run_dense(c: Ctx, wl):
     #   enc 1: 2 x v_add_u32 + 1 x v_min3_u32 per 2 relaxations         -> 8/2 = 4.0 cycles
     cyc_per_relax = {5: 2.0, 4: 2.0, 3: 2.0, 2: 3.0, 1: 4.0}[enc]
     instr_per_relax = {5: 0.75, 4: 0.75, 3: 0.75, 2: 1.0, 1: 1.5}[enc]
-    kname = {5: "fwh_update_kernel<true, 4>",
-             4: "fwh_update_kernel<true, 0>" if world == 1 else "fwh_update_kernel<true, 4>",
-             3: "fwh_update_kernel<false, 0>",
+    # the 8-wave update kernel (fwq_update_kernel) unless SRT_FW_WAVES=4 selects the 4-wave one
+    uk = "fwh_update_kernel" if os.environ.get("SRT_FW_WAVES") == "4" else "fwq_update_kernel"
+    kname = {5: f"{uk}<true, 4>",
+             4: f"{uk}<true, 0>" if world == 1 else f"{uk}<true, 4>",
+             3: f"{uk}<false, 0>",
              2: "fw16_update_kernel<false>", 1: "fw_update_kernel"}[enc]
     # elements a timed launch updates: every local row; (enc 4, one GPU) the upper-triangle 128x128
     # tiles; (enc 4, sharded) this rank's kept tiles (fw16.hip sym_kept: one orientation of each

@@ -617,40 +617,37 @@ static __host__ __device__ __forceinline__ bool sym_kept(int I, int J) {
  * 6 = (one GPU, two update streams) the upper-triangle tiles of tile row / column K1 whose
  * I + J has the parity i0; 7 / 8 = mode 3 restricted to even / odd J (the sharded rounds' two
  * update streams). */
-template <bool SYM, int XM = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void fwh_update_kernel(
-    u16* __restrict__ D, int ld, const u16* __restrict__ P, int k0, int ncol_tiles, int i0, int skip,
-    const uint32_t* __restrict__ tl, int te) {
-    __shared__ __attribute__((aligned(16))) uint32_t sA[UKC / 2 * 128 * 2];
-    __shared__ __attribute__((aligned(16))) u16 sB[UKC * UBS];
-    if constexpr (XM == 3 || XM == 6 || XM == 7 || XM == 8) FW_CHAIN_PRIO(); /* next-row tiles */
-    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+/* The tile (I, J) the calling block of a mode-XM launch updates and its local tile row Iloc;
+ * false when the block has nothing to do (see fwh_update_kernel for the modes). */
+template <bool SYM, int XM>
+static __device__ __forceinline__ bool fw_tile_of(int ncol_tiles, int i0, int skip,
+                                                  const uint32_t* __restrict__ tl, int te, int& I,
+                                                  int& J, int& Iloc) {
     const int nb = gridDim.x;
     const int per = nb >> 3;
     const int bid = (nb & 7) == 0 ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
-    int I, J, Iloc;
     if (XM == 3 || XM == 7 || XM == 8) {
         if (blockIdx.x < ncol_tiles) {
             J = blockIdx.x;
             I = skip;
-            if (I < i0 || I >= te || !sym_kept(I, J)) return;
+            if (I < i0 || I >= te || !sym_kept(I, J)) return false;
         } else {
             I = i0 + (int)blockIdx.x - ncol_tiles;
             J = skip;
-            if (I >= te || I == skip || !sym_kept(I, J)) return;
+            if (I >= te || I == skip || !sym_kept(I, J)) return false;
         }
-        if (XM != 3 && (J & 1) != XM - 7) return; /* two update streams: tile set J mod 2 */
+        if (XM != 3 && (J & 1) != XM - 7) return false; /* two update streams: tile set J mod 2 */
         Iloc = I - i0;
     } else if (XM == 6) { /* one GPU, upper triangle: the cross of K1 restricted to I + J = i0 mod 2 */
         I = min((int)blockIdx.x, skip);
         J = max((int)blockIdx.x, skip);
-        if (((I + J) & 1) != i0) return;
+        if (((I + J) & 1) != i0) return false;
         Iloc = I;
     } else if (XM == 4 || XM == 5) {
         const uint32_t t = tl[bid];
         I = (int)(t >> 16);
         J = (int)(t & 0xFFFFu);
-        if (XM == 4 && (I == skip || J == skip)) return;
+        if (XM == 4 && (I == skip || J == skip)) return false;
         Iloc = I - i0;
     } else if (SYM) {
         tri_decode(bid, ncol_tiles, &I, &J);
@@ -660,6 +657,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         J = bid % ncol_tiles;
         Iloc = I;
     }
+    return true;
+}
+
+template <bool SYM, int XM = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void fwh_update_kernel(
+    u16* __restrict__ D, int ld, const u16* __restrict__ P, int k0, int ncol_tiles, int i0, int skip,
+    const uint32_t* __restrict__ tl, int te) {
+    __shared__ __attribute__((aligned(16))) uint32_t sA[UKC / 2 * 128 * 2];
+    __shared__ __attribute__((aligned(16))) u16 sB[UKC * UBS];
+    if constexpr (XM == 3 || XM == 6 || XM == 7 || XM == 8) FW_CHAIN_PRIO(); /* next-row tiles */
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    int I, J, Iloc;
+    if (!fw_tile_of<SYM, XM>(ncol_tiles, i0, skip, tl, te, I, J, Iloc)) return;
     u16* C = D + (size_t)Iloc * 128 * ld + J * 128;
     const u16* Ag = D + (size_t)I * 128 * ld + k0;
     const u16* Bg = P + J * 128;
@@ -704,6 +714,149 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     for (int r = 0; r < 8; ++r)
         if (rowsum16(acc[r]) != sum0[r])
             *reinterpret_cast<uint4*>(C + (size_t)(ty * 8 + r) * ld + tx * 8) =
+                make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+}
+
+/* ---- the same update at 8 waves per SIMD --------------------------------------------------- *
+ * 512 threads per 128x128 tile, 4 rows x 8 columns per thread: 16 accumulator VGPRs, <= 64 in
+ * all, so 8 waves share each SIMD (4 for fwh_update_kernel's 8x8 blocks at 119 VGPRs). The
+ * f16-compare mix issues at 2.29 cycles per relaxation with 8 waves against 2.48 with 4
+ * (profiles/r01_valu_issue_rates2.txt), and the tile's C load, staging and stores are spread
+ * over twice the waves. Per pivot pair and thread: 2 ds_read_b128 of B + 2 of A feed 32 v_add_u32
+ * + 16 v_pk_minimum3_f16 (LDS: 4 ds_read_b128 per 64 relaxations, 44% of the array's rate at
+ * the VALU issue rate). Same LDS image, modes and results as fwh_update_kernel
+ * (tools/fwh_variants.hip: 67.3% vs 64.2% of the issue model on a full 32k update). */
+struct fwq_stage_regs {
+    uint4 a, b; /* SYM: a = (pivot 2p rows 4g..4g+3, pivot 2p+1 rows 4g..4g+3) */
+};
+
+static __device__ __forceinline__ void fwq_gload(fwq_stage_regs& g, const u16* __restrict__ A,
+                                                 const u16* __restrict__ B, size_t ld, int tid) {
+    const int ra = tid & 127, ca = (tid >> 7) * 8; /* 128 rows x 32 pivots */
+    const int rb = tid >> 4, cb = (tid & 15) * 8;  /* 32 pivots x 128 columns */
+    g.a = *reinterpret_cast<const uint4*>(A + (size_t)ra * ld + ca);
+    g.b = *reinterpret_cast<const uint4*>(B + (size_t)rb * ld + cb);
+}
+
+static __device__ __forceinline__ void fwq_gload_sym(fwq_stage_regs& g, const u16* __restrict__ Ph,
+                                                     int I0, const u16* __restrict__ B, size_t ld,
+                                                     int tid) {
+    const int p = tid >> 5, rg = tid & 31;
+    const uint2 a0 = *reinterpret_cast<const uint2*>(Ph + (size_t)(2 * p) * ld + I0 + rg * 4);
+    const uint2 a1 = *reinterpret_cast<const uint2*>(Ph + (size_t)(2 * p + 1) * ld + I0 + rg * 4);
+    g.a = make_uint4(a0.x, a0.y, a1.x, a1.y);
+    const int rb = tid >> 4, cb = (tid & 15) * 8;
+    g.b = *reinterpret_cast<const uint4*>(B + (size_t)rb * ld + cb);
+}
+
+template <bool SYM>
+static __device__ __forceinline__ void fwq_swrite(const fwq_stage_regs& g, uint32_t* __restrict__ sA,
+                                                  u16* __restrict__ sB, int tid) {
+    if constexpr (SYM) {
+        const int p = tid >> 5, rg = tid & 31;
+        const uint32_t a0[2] = {g.a.x, g.a.y}, a1[2] = {g.a.z, g.a.w};
+#pragma unroll
+        for (int i = 0; i < 2; ++i) /* rows 4rg + 2i (low halves) and 4rg + 2i + 1 (high) */
+            *reinterpret_cast<uint4*>(sA + ((p * 128) + rg * 4 + 2 * i) * 2) =
+                make_uint4(splat(a0[i] & 0xFFFFu), splat(a1[i] & 0xFFFFu), splat(a0[i] >> 16),
+                           splat(a1[i] >> 16));
+    } else {
+        const int ra = tid & 127, ca = (tid >> 7) * 8;
+        const uint4 v = g.a;
+        uint32_t* d = sA + ((ca >> 1) * 128 + ra) * 2; /* pairs ca/2 .. ca/2+3 of row ra */
+        *reinterpret_cast<uint2*>(d) = make_uint2(splat(v.x & 0xFFFFu), splat(v.x >> 16));
+        *reinterpret_cast<uint2*>(d + 256) = make_uint2(splat(v.y & 0xFFFFu), splat(v.y >> 16));
+        *reinterpret_cast<uint2*>(d + 512) = make_uint2(splat(v.z & 0xFFFFu), splat(v.z >> 16));
+        *reinterpret_cast<uint2*>(d + 768) = make_uint2(splat(v.w & 0xFFFFu), splat(v.w >> 16));
+    }
+    const int rb = tid >> 4, cb = (tid & 15) * 8;
+    *reinterpret_cast<uint4*>(sB + rb * UBS + cb) = g.b;
+}
+
+/* rows 0..3 of the thread's 4x8 block, pivots m, m+1: 32 v_add_u32 + 16 v_pk_minimum3_f16 */
+static __device__ __forceinline__ void fwq_rows(uint32_t (&acc)[4][4], const uint2 (&a)[4],
+                                                const uint4 (&b)[2]) {
+    const uint32_t b0[4] = {b[0].x, b[0].y, b[0].z, b[0].w};
+    const uint32_t b1[4] = {b[1].x, b[1].y, b[1].z, b[1].w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        uint32_t t0[4], t1[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            t0[c] = a[r].x + b0[c];
+            t1[c] = a[r].y + b1[c];
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = min3h(acc[r][c], t0[c], t1[c]);
+    }
+}
+
+static __device__ __forceinline__ void fwq_stage(uint32_t (&acc)[4][4], const uint32_t* __restrict__ sA,
+                                                 const u16* __restrict__ sB, int tx, int ty) {
+    const uint32_t* pa = sA + ty * 4 * 2;
+    const u16* pb = sB + tx * 8;
+    /* no register double-buffering (it spills at 64 VGPRs): the other 7 waves of the SIMD hide the
+     * LDS latency */
+#pragma unroll 2
+    for (int m = 0; m < UKC; m += 2) {
+        uint4 b[2];
+        uint2 a[4];
+        fwh_readB(b, pb, m);
+        fwh_readA(a, pa, m);
+        fwq_rows(acc, a, b);
+    }
+}
+
+template <bool SYM, int XM = 0>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) void fwq_update_kernel(
+    u16* __restrict__ D, int ld, const u16* __restrict__ P, int k0, int ncol_tiles, int i0, int skip,
+    const uint32_t* __restrict__ tl, int te) {
+    __shared__ __attribute__((aligned(16))) uint32_t sA[UKC / 2 * 128 * 2];
+    __shared__ __attribute__((aligned(16))) u16 sB[UKC * UBS];
+    if constexpr (XM == 3 || XM == 6 || XM == 7 || XM == 8) FW_CHAIN_PRIO(); /* next-row tiles */
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    int I, J, Iloc;
+    if (!fw_tile_of<SYM, XM>(ncol_tiles, i0, skip, tl, te, I, J, Iloc)) return;
+    u16* C = D + (size_t)Iloc * 128 * ld + J * 128;
+    const u16* Ag = D + (size_t)I * 128 * ld + k0;
+    const u16* Bg = P + J * 128;
+    fwq_stage_regs g;
+    if (SYM)
+        fwq_gload_sym(g, P, I * 128, Bg, ld, tid);
+    else
+        fwq_gload(g, Ag, Bg, ld, tid);
+    uint32_t acc[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint4 v = *reinterpret_cast<const uint4*>(C + (size_t)(ty * 4 + r) * ld + tx * 8);
+        acc[r][0] = v.x;
+        acc[r][1] = v.y;
+        acc[r][2] = v.z;
+        acc[r][3] = v.w;
+    }
+    uint32_t sum0[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        sum0[r] = rowsum16(acc[r]);
+        /* keep the four sums live, not the sixteen loaded words they came from (the compiler
+         * otherwise sinks the sums to the stores and spills the rows) */
+        asm volatile("" : "+v"(sum0[r]));
+    }
+    fwq_swrite<SYM>(g, sA, sB, tid);
+    __syncthreads();
+    if (SYM) /* in flight during stage 0 */
+        fwq_gload_sym(g, P + (size_t)UKC * ld, I * 128, Bg + (size_t)UKC * ld, ld, tid);
+    else
+        fwq_gload(g, Ag + UKC, Bg + (size_t)UKC * ld, ld, tid);
+    fwq_stage(acc, sA, sB, tx, ty);
+    __syncthreads();
+    fwq_swrite<SYM>(g, sA, sB, tid);
+    __syncthreads();
+    fwq_stage(acc, sA, sB, tx, ty);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        if (rowsum16(acc[r]) != sum0[r])
+            *reinterpret_cast<uint4*>(C + (size_t)(ty * 4 + r) * ld + tx * 8) =
                 make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
 }
 
@@ -955,6 +1108,22 @@ __global__ __launch_bounds__(256) void sym_fill_local_kernel(u16* __restrict__ D
 }
 
 #ifndef SRT_FW16_DEVICE_ONLY
+/* 8-wave update kernel (fwq_update_kernel) unless SRT_FW_WAVES=4 selects the 4-wave one */
+static bool fw_waves8(void) {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("SRT_FW_WAVES");
+        v = (e && atoi(e) == 4) ? 0 : 1;
+    }
+    return v != 0;
+}
+#define FW_UPDATE(SYMV, XMV, GRID, STREAM, ...)                                                   \
+    do {                                                                                          \
+        if (fw_waves8())                                                                          \
+            fwq_update_kernel<SYMV, XMV><<<(GRID), 512, 0, (STREAM)>>>(__VA_ARGS__);              \
+        else                                                                                      \
+            fwh_update_kernel<SYMV, XMV><<<(GRID), 256, 0, (STREAM)>>>(__VA_ARGS__);              \
+    } while (0)
 /* ---- orchestration --------------------------------------------------------------------------- *
  * Lookahead schedule (one row shard per rank; a single GPU is the 1-rank case). Round k uses the
  * 64-row pivot panel P_k (owner: in place in its rows; others: a double-buffered receive panel).
@@ -1048,7 +1217,7 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
             fw16_panel_kernel<true, true><<<2 * nb, 256, 0, st>>>(d, ld, 0, nb, P, k0, nb, 1, 1);
             if (k0 > 0) fw16_refresh_kernel<<<k0 / KB, 256, 0, st>>>(d, ld, k0);
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
-            fwh_update_kernel<true><<<ntri, 256, 0, st>>>(d, ld, P, k0, T, 0, -1, nullptr, 0);
+            FW_UPDATE(true, 0, ntri, st, d, ld, P, k0, T, 0, -1, nullptr, 0);
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
             SRT_HIPCHK(hipGetLastError());
         }
@@ -1103,7 +1272,7 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
             for (int p = 0; p < 2; p++) {
                 SRT_HIPCHK(hipStreamWaitEvent(ss[p], sc->ready[k & 1], 0));
                 if (next) {
-                    fwh_update_kernel<true, 6><<<T, 256, 0, ss[p]>>>(d, ld, P, k0, T, p, K1, nullptr, 0);
+                    FW_UPDATE(true, 6, T, ss[p], d, ld, P, k0, T, p, K1, nullptr, 0);
                     SRT_HIPCHK(hipEventRecord(sc->e_set[k & 1][p], ss[p]));
                 }
             }
@@ -1122,10 +1291,10 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
             for (int p = 0; p < 2; p++) {
                 if (evp && next) SRT_HIPCHK(hipEventRecord(evp->ev[e0 + p], ss[p]));
                 if (next)
-                    fwh_update_kernel<true, 4><<<(unsigned)nset[p], 256, 0, ss[p]>>>(
+                    FW_UPDATE(true, 4, (unsigned)nset[p], ss[p],
                         d, ld, P, k0, T, 0, K1, tls[p], T);
                 else
-                    fwh_update_kernel<true, 5><<<(unsigned)nset[p], 256, 0, ss[p]>>>(
+                    FW_UPDATE(true, 5, (unsigned)nset[p], ss[p],
                         d, ld, P, k0, T, 0, -1, tls[p], T);
                 if (evp && next) SRT_HIPCHK(hipEventRecord(evp->ev[e0 + 2 + p], ss[p]));
             }
@@ -1316,10 +1485,10 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
                 SYM_HIP(hipStreamWaitEvent(ss[p], sc->ready[k & 1], 0));
                 if (!next) continue;
                 if (p == 0)
-                    fwh_update_kernel<true, 7><<<T + (te - tb), 256, 0, ss[p]>>>(d, ld, P, k0, T, tb,
+                    FW_UPDATE(true, 7, T + (te - tb), ss[p], d, ld, P, k0, T, tb,
                                                                                  K1, nullptr, te);
                 else
-                    fwh_update_kernel<true, 8><<<T + (te - tb), 256, 0, ss[p]>>>(d, ld, P, k0, T, tb,
+                    FW_UPDATE(true, 8, T + (te - tb), ss[p], d, ld, P, k0, T, tb,
                                                                                  K1, nullptr, te);
                 SYM_HIP(hipEventRecord(sc->e_set[k & 1][p], ss[p]));
             }
@@ -1334,10 +1503,10 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
                 if (t_first) SYM_HIP(hipEventRecord(evp->ev[p], ss[p]));
                 if (nset[p]) {
                     if (next)
-                        fwh_update_kernel<true, 4><<<(unsigned)nset[p], 256, 0, ss[p]>>>(
+                        FW_UPDATE(true, 4, (unsigned)nset[p], ss[p],
                             d, ld, P, k0, T, tb, K1, tls[p], te);
                     else
-                        fwh_update_kernel<true, 5><<<(unsigned)nset[p], 256, 0, ss[p]>>>(
+                        FW_UPDATE(true, 5, (unsigned)nset[p], ss[p],
                             d, ld, P, k0, T, tb, -1, tls[p], te);
                 }
                 if (t_last) SYM_HIP(hipEventRecord(evp->ev[evp->used - 2 + p], ss[p]));
@@ -1524,7 +1693,9 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
     u16* pbuf[2] = {bufs[dev] + (size_t)nrows * ld, bufs[dev] + (size_t)nrows * ld + (size_t)KB * ld};
     const uint32_t cap = fm ? CAP_F : CAP_U;
     auto panel = fm ? fw16_panel_kernel<true, false> : fw16_panel_kernel<false, false>;
-    auto update = fm ? fwh_update_kernel<false> : fw16_update_kernel<false>;
+    auto update = fm ? (fw_waves8() ? fwq_update_kernel<false> : fwh_update_kernel<false>)
+                     : fw16_update_kernel<false>;
+    const int uthr = fm && fw_waves8() ? 512 : 256; /* threads of an update block */
     if (nrows > 0) {
         fw16_init_kernel<<<dim3(srt_ceil_div(ld, 2048), nrows), 256, 0, st>>>(n, ld, row0, w_rows, d,
                                                                            cap);
@@ -1570,15 +1741,15 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
             panel<<<nb + nrb, 256, 0, st>>>(d, ld, row0, nrb, P, k0, nb, 0, 1);
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
             if (skip >= 0) {
-                update<<<ncol128, 256, 0, st>>>(d, ld, P, k0, ncol128, skip, -1, nullptr, 0);
+                update<<<ncol128, uthr, 0, st>>>(d, ld, P, k0, ncol128, skip, -1, nullptr, 0);
                 SRT_HIPCHK(hipEventRecord(sc->row_done, st));
                 SRT_HIPCHK(hipStreamWaitEvent(cs, sc->row_done, 0));
                 if ((rc = produce(k + 1))) return rc;
                 if (nrow128 > 1)
-                    update<<<ncol128 * (nrow128 - 1), 256, 0, st>>>(d, ld, P, k0, ncol128, 0, skip,
+                    update<<<ncol128 * (nrow128 - 1), uthr, 0, st>>>(d, ld, P, k0, ncol128, 0, skip,
                                                                    nullptr, 0);
             } else {
-                update<<<ncol128 * nrow128, 256, 0, st>>>(d, ld, P, k0, ncol128, 0, -1, nullptr, 0);
+                update<<<ncol128 * nrow128, uthr, 0, st>>>(d, ld, P, k0, ncol128, 0, -1, nullptr, 0);
             }
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
             SRT_HIPCHK(hipGetLastError());
