@@ -266,11 +266,11 @@ def run_dense(c: Ctx, wl):
     #   enc 3: 2 x v_add_u32 + 1 x v_pk_minimum3_f16 per 4 relaxations -> 8/4 = 2.0 cycles
     #   enc 2: 1 x v_add_u32 + 1 x v_pk_min_u16 per 2 relaxations      -> 6/2 = 3.0 cycles
     #   enc 1: 2 x v_add_u32 + 1 x v_min3_u32 per 2 relaxations         -> 8/2 = 4.0 cycles
-    cyc_per_relax = {5: 2.0, 4: 2.0, 3: 2.0, 2: 3.0, 1: 4.0}[enc]
-    instr_per_relax = {5: 0.75, 4: 0.75, 3: 0.75, 2: 1.0, 1: 1.5}[enc]
+    cyc_per_relax = {6: 2.0, 5: 2.0, 4: 2.0, 3: 2.0, 2: 3.0, 1: 4.0}[enc]
+    instr_per_relax = {6: 0.75, 5: 0.75, 4: 0.75, 3: 0.75, 2: 1.0, 1: 1.5}[enc]
     # the 8-wave update kernel (fwq_update_kernel) unless SRT_FW_WAVES=4 selects the 4-wave one
     uk = "fwh_update_kernel" if os.environ.get("SRT_FW_WAVES") == "4" else "fwq_update_kernel"
-    kname = {5: f"{uk}<true, 4>",
+    kname = {6: "fwq_update_kernel<true, 4, 4>", 5: f"{uk}<true, 4>",
              4: f"{uk}<true, 0>" if world == 1 else f"{uk}<true, 4>",
              3: f"{uk}<false, 0>",
              2: "fw16_update_kernel<false>", 1: "fw_update_kernel"}[enc]
@@ -278,7 +278,14 @@ def run_dense(c: Ctx, wl):
     # tiles; (enc 4, sharded) this rank's kept tiles (fw16.hip sym_kept: one orientation of each
     # tile pair) less the next pivot block's tile row and column, which run in their own launch
     tiles = ld // 128
-    if enc == 5:  # one GPU, two update streams: a timed unit is the pair of rest-of-round
+    pivots = FW_B  # pivots applied per element per timed unit
+    if enc == 6:  # one GPU, 128-pivot rounds on two update streams: a timed unit is the pair of
+        # rest launches of a round j, every upper-triangle tile but the cross of j + 1; the cross
+        # of j (T - 1 tiles of it) takes only the second 64-pivot panel
+        rest = tiles * (tiles + 1) // 2 - tiles
+        elems = float(rest) * 128 * 128
+        pivots = (float(rest - (tiles - 1)) * 128 + float(tiles - 1) * 64) / rest
+    elif enc == 5:  # one GPU, two update streams: a timed unit is the pair of rest-of-round
         # launches (first start to last end), all upper-triangle tiles but the next pivot
         # block's tile row and column (T tiles, their own launches)
         elems = float(tiles * (tiles + 1) // 2 - tiles) * 128 * 128
@@ -293,7 +300,7 @@ def run_dense(c: Ctx, wl):
     else:
         elems = float(nr) * ld
     bytes_per_round = 2.0 * elems * s_d  # round-streaming model: read + write what is updated
-    relax_per_round = elems * FW_B
+    relax_per_round = elems * pivots
     achieved_gbs = bytes_per_round / (avg_upd_ms * 1e-3) / 1e9
     relax_t = relax_per_round / (avg_upd_ms * 1e-3) / 1e12
     relax_peak_t = VALU_LANE_CYCLES_T / cyc_per_relax
@@ -303,7 +310,7 @@ def run_dense(c: Ctx, wl):
         pmc = json.load(open(pmc_path))
         if pmc.get("kernel") == kname:
             traffic = pmc.get("hbm_bytes_per_launch")
-            if enc == 5 and traffic is not None:  # the timed unit is two launches
+            if enc in (5, 6) and traffic is not None:  # the timed unit is two launches
                 traffic = 2.0 * traffic
     roofline = {
         # the north-star metric is GB/s vs HBM peak; the kernel itself is VALU-issue bound (min-plus
@@ -313,9 +320,11 @@ def run_dense(c: Ctx, wl):
         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
         "traffic": traffic, "bytes_per_launch": bytes_per_round,
         "avg_launch_ms": round(avg_upd_ms, 4), "launches_timed": n_upd,
-        "model": f"2*elements*{s_d} B per round (SURVEY §8d round-streaming, B=64, "
-                 f"{ {5: 'u16 f16-compare, upper triangle on two streams (unit: both rest launches)', 4: 'u16 f16-compare, upper triangle', 3: 'u16 f16-compare', 2: 'u16 pk_min', 1: 'u32'}[enc]}"
-                 f" distances; elements updated per round = {int(elems)})",
+        "model": f"2*elements*{s_d} B per timed unit (SURVEY §8d round-streaming, "
+                 f"{'B=128 (two 64-pivot panels per C-tile residency)' if enc == 6 else 'B=64'}, "
+                 f"{ {6: 'u16 f16-compare, upper triangle on two streams, 128-pivot rounds (unit: both rest launches)', 5: 'u16 f16-compare, upper triangle on two streams (unit: both rest launches)', 4: 'u16 f16-compare, upper triangle', 3: 'u16 f16-compare', 2: 'u16 pk_min', 1: 'u32'}[enc]}"
+                 f" distances; elements updated per unit = {int(elems)}, "
+                 f"pivots per element = {pivots:.2f})",
         "algorithmic_min_bytes": float(nr) * ld * (4 + 8),
         "valu": {"achieved": round(relax_t, 2), "peak": round(relax_peak_t, 1),
                  "unit": "Trelax/s", "frac": round(relax_t / relax_peak_t, 4),

@@ -807,24 +807,37 @@ static __device__ __forceinline__ void fwq_stage(uint32_t (&acc)[4][4], const ui
     }
 }
 
-template <bool SYM, int XM = 0>
+/* NST stages of UKC pivots per C-tile residency: 2 (a 64-pivot round) or 4 (two rounds, the
+ * 128-row panel P = P_a over P_b). prev >= 0 (128-pivot rounds): the tiles of tile row / column
+ * prev already hold P_a (the chain stream applied it to them before closing P_b) and take P_b only.
+ * XM 9: the cross of tile `skip` (tile row and column, upper triangle), every tile. */
+template <bool SYM, int XM = 0, int NST = 2>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) void fwq_update_kernel(
     u16* __restrict__ D, int ld, const u16* __restrict__ P, int k0, int ncol_tiles, int i0, int skip,
-    const uint32_t* __restrict__ tl, int te) {
+    const uint32_t* __restrict__ tl, int te, int prev = -1) {
     __shared__ __attribute__((aligned(16))) uint32_t sA[UKC / 2 * 128 * 2];
     __shared__ __attribute__((aligned(16))) u16 sB[UKC * UBS];
-    if constexpr (XM == 3 || XM == 6 || XM == 7 || XM == 8) FW_CHAIN_PRIO(); /* next-row tiles */
+    if constexpr (XM == 3 || XM == 6 || XM == 7 || XM == 8 || XM == 9)
+        FW_CHAIN_PRIO(); /* next-row tiles */
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     int I, J, Iloc;
-    if (!fw_tile_of<SYM, XM>(ncol_tiles, i0, skip, tl, te, I, J, Iloc)) return;
+    if constexpr (XM == 9) {
+        I = min((int)blockIdx.x, skip);
+        J = max((int)blockIdx.x, skip);
+        Iloc = I;
+    } else if (!fw_tile_of<SYM, XM>(ncol_tiles, i0, skip, tl, te, I, J, Iloc)) {
+        return;
+    }
+    /* wave-uniform first stage */
+    const int s0 = (NST == 4 && prev >= 0 && (I == prev || J == prev)) ? NST / 2 : 0;
     u16* C = D + (size_t)Iloc * 128 * ld + J * 128;
     const u16* Ag = D + (size_t)I * 128 * ld + k0;
     const u16* Bg = P + J * 128;
     fwq_stage_regs g;
     if (SYM)
-        fwq_gload_sym(g, P, I * 128, Bg, ld, tid);
+        fwq_gload_sym(g, P + (size_t)s0 * UKC * ld, I * 128, Bg + (size_t)s0 * UKC * ld, ld, tid);
     else
-        fwq_gload(g, Ag, Bg, ld, tid);
+        fwq_gload(g, Ag + s0 * UKC, Bg + (size_t)s0 * UKC * ld, ld, tid);
     uint32_t acc[4][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -842,17 +855,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
          * otherwise sinks the sums to the stores and spills the rows) */
         asm volatile("" : "+v"(sum0[r]));
     }
-    fwq_swrite<SYM>(g, sA, sB, tid);
-    __syncthreads();
-    if (SYM) /* in flight during stage 0 */
-        fwq_gload_sym(g, P + (size_t)UKC * ld, I * 128, Bg + (size_t)UKC * ld, ld, tid);
-    else
-        fwq_gload(g, Ag + UKC, Bg + (size_t)UKC * ld, ld, tid);
-    fwq_stage(acc, sA, sB, tx, ty);
-    __syncthreads();
-    fwq_swrite<SYM>(g, sA, sB, tid);
-    __syncthreads();
-    fwq_stage(acc, sA, sB, tx, ty);
+#pragma unroll 1
+    for (int s = s0; s < NST; ++s) {
+        if (s > s0) __syncthreads(); /* the previous stage's LDS reads are done */
+        fwq_swrite<SYM>(g, sA, sB, tid);
+        __syncthreads();
+        if (s + 1 < NST) { /* in flight during this stage */
+            if (SYM)
+                fwq_gload_sym(g, P + (size_t)(s + 1) * UKC * ld, I * 128,
+                              Bg + (size_t)(s + 1) * UKC * ld, ld, tid);
+            else
+                fwq_gload(g, Ag + (s + 1) * UKC, Bg + (size_t)(s + 1) * UKC * ld, ld, tid);
+        }
+        fwq_stage(acc, sA, sB, tx, ty);
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r)
         if (rowsum16(acc[r]) != sum0[r])
@@ -1110,12 +1126,8 @@ __global__ __launch_bounds__(256) void sym_fill_local_kernel(u16* __restrict__ D
 #ifndef SRT_FW16_DEVICE_ONLY
 /* 8-wave update kernel (fwq_update_kernel) unless SRT_FW_WAVES=4 selects the 4-wave one */
 static bool fw_waves8(void) {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("SRT_FW_WAVES");
-        v = (e && atoi(e) == 4) ? 0 : 1;
-    }
-    return v != 0;
+    const char* e = getenv("SRT_FW_WAVES");
+    return !(e && atoi(e) == 4);
 }
 #define FW_UPDATE(SYMV, XMV, GRID, STREAM, ...)                                                   \
     do {                                                                                          \
@@ -1192,7 +1204,7 @@ static int sched_get(fw16_sched** out, int dev) {
  * that the other stream has already relaxed in the next round: those values are still lengths
  * of real paths, no larger than the round requires, so the result is the same exact matrix. */
 static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipStream_t st,
-                          evpool_t* evp, int* exact, bool two) {
+                          evpool_t* evp, int* exact, bool two, bool r128) {
     const int dev = srt_state_slot(); /* the device, or this virtual rank's slot */
     size_t* caps = fw16_caps;
     int** flags = fw16_flags;
@@ -1263,6 +1275,68 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
         SRT_HIPCHK(hipEventRecord(sc->init_done, st));
         SRT_HIPCHK(hipStreamWaitEvent(cs, sc->init_done, 0));
         SRT_HIPCHK(hipStreamWaitEvent(xs, sc->init_done, 0));
+        if (r128) {
+            /* 128-pivot rounds (pivot blocks a = 2j, b = 2j + 1: tile row j): every C tile stays
+             * resident for both panels (four 32-pivot stages), which halves the per-pivot C loads,
+             * row sums and stores and the bulk launches. Chain stream cs, per round j:
+             * close P_a, apply it to the cross of tile j (its row and column, XM 9), close P_b ->
+             * ready[j]. Update stream p, per round j: (after ready[j]) the cross of tile j + 1
+             * with P_a and P_b, then the rest with both, where the cross of j takes P_b only (it
+             * has P_a). The cross of j + 1 is excluded from round j's rest and updated first, so
+             * cs can close P_a' of round j + 1 under the rest; cs's cross updates touch no tile
+             * of the rest launch still running (round j - 1 excludes the cross of j). */
+            auto produce2 = [&](int j) -> int {
+                const int ka = 2 * j * KB;
+                u16* Pa = d + (size_t)ka * ld;
+                fw16_diag_kernel<true><<<1, 256, 0, cs>>>(Pa, ld, ka);
+                fw16_panel_kernel<true, true><<<2 * nb, 256, 0, cs>>>(d, ld, 0, nb, Pa, ka, nb, 1, 1);
+                if (ka > 0) fw16_refresh_kernel<<<ka / KB, 256, 0, cs>>>(d, ld, ka);
+                fwq_update_kernel<true, 9, 2><<<T, 512, 0, cs>>>(d, ld, Pa, ka, T, 0, j, nullptr, 0, -1);
+                const int kb = ka + KB;
+                u16* Pb = d + (size_t)kb * ld;
+                fw16_diag_kernel<true><<<1, 256, 0, cs>>>(Pb, ld, kb);
+                fw16_panel_kernel<true, true><<<2 * nb, 256, 0, cs>>>(d, ld, 0, nb, Pb, kb, nb, 1, 1);
+                fw16_refresh_kernel<<<kb / KB, 256, 0, cs>>>(d, ld, kb);
+                SRT_HIPCHK(hipGetLastError());
+                SRT_HIPCHK(hipEventRecord(sc->ready[j & 1], cs));
+                return SRT_OK;
+            };
+            if ((rc = produce2(0))) return rc;
+            for (int j = 0; j < T; ++j) {
+                const int ka = 2 * j * KB;
+                u16* Pa = d + (size_t)ka * ld;
+                const bool next = j + 1 < T;
+                for (int p = 0; p < 2; p++) {
+                    SRT_HIPCHK(hipStreamWaitEvent(ss[p], sc->ready[j & 1], 0));
+                    if (next) {
+                        fwq_update_kernel<true, 6, 4><<<T, 512, 0, ss[p]>>>(d, ld, Pa, ka, T, p, j + 1,
+                                                                          nullptr, 0, -1);
+                        SRT_HIPCHK(hipEventRecord(sc->e_set[j & 1][p], ss[p]));
+                    }
+                }
+                if (next) {
+                    SRT_HIPCHK(hipStreamWaitEvent(cs, sc->e_set[j & 1][0], 0));
+                    SRT_HIPCHK(hipStreamWaitEvent(cs, sc->e_set[j & 1][1], 0));
+                    if ((rc = produce2(j + 1))) return rc;
+                }
+                const int e0 = evp ? evp->used : 0;
+                if (evp && next) {
+                    evp->group = 4;
+                    evp->used += 4;
+                }
+                for (int p = 0; p < 2; p++) {
+                    if (evp && next) SRT_HIPCHK(hipEventRecord(evp->ev[e0 + p], ss[p]));
+                    if (next)
+                        fwq_update_kernel<true, 4, 4><<<(unsigned)nset[p], 512, 0, ss[p]>>>(
+                            d, ld, Pa, ka, T, 0, j + 1, tls[p], T, j);
+                    else
+                        fwq_update_kernel<true, 5, 4><<<(unsigned)nset[p], 512, 0, ss[p]>>>(
+                            d, ld, Pa, ka, T, 0, -1, tls[p], T, j);
+                    if (evp && next) SRT_HIPCHK(hipEventRecord(evp->ev[e0 + 2 + p], ss[p]));
+                }
+                SRT_HIPCHK(hipGetLastError());
+            }
+        } else {
         if ((rc = produce(0))) return rc;
         for (int k = 0; k < nb; ++k) {
             const int k0 = k * KB;
@@ -1299,6 +1373,7 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
                 if (evp && next) SRT_HIPCHK(hipEventRecord(evp->ev[e0 + 2 + p], ss[p]));
             }
             SRT_HIPCHK(hipGetLastError());
+        }
         }
         SRT_HIPCHK(hipEventRecord(sc->row_done, xs));
         SRT_HIPCHK(hipStreamWaitEvent(st, sc->row_done, 0));
@@ -1685,17 +1760,29 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
         /* two update streams once the rounds are long enough to hide their event waits;
          * SRT_FW_LOOKAHEAD=0/1 forces either form */
         const bool two = la_env ? atoi(la_env) != 0 : ld >= 8192;
-        *sym = two ? 2 : 1;
-        return fw16_build_sym(n, ld, w_rows, lat_rows, st, evp, exact, two);
+        /* SRT_FW_KB=128: 128-pivot rounds on the two update streams (8-wave kernel). Measured on
+         * C4: the same period per 64 pivots as the 64-pivot rounds (1.315 ms per 128-pivot pair
+         * vs 0.657 per 64; build 380.5 vs 380.1 ms), so the simpler 64-pivot rounds stay the
+         * default */
+        const char* kb_env = getenv("SRT_FW_KB");
+        const bool r128 = two && fw_waves8() && ld >= 256 && kb_env && atoi(kb_env) == 128;
+        *sym = r128 ? 3 : two ? 2 : 1;
+        return fw16_build_sym(n, ld, w_rows, lat_rows, st, evp, exact, two, r128);
     }
     hipStream_t cs = lookahead ? sc->cs : st;
     u16* d = bufs[dev];
     u16* pbuf[2] = {bufs[dev] + (size_t)nrows * ld, bufs[dev] + (size_t)nrows * ld + (size_t)KB * ld};
     const uint32_t cap = fm ? CAP_F : CAP_U;
     auto panel = fm ? fw16_panel_kernel<true, false> : fw16_panel_kernel<false, false>;
-    auto update = fm ? (fw_waves8() ? fwq_update_kernel<false> : fwh_update_kernel<false>)
-                     : fw16_update_kernel<false>;
-    const int uthr = fm && fw_waves8() ? 512 : 256; /* threads of an update block */
+    /* the update of round k0 on this shard's tile rows (i0, skip as in tile_row) */
+    auto update = [&](unsigned grid, const u16* P, int k0, int ncol, int i0, int skip) {
+        if (!fm)
+            fw16_update_kernel<false><<<grid, 256, 0, st>>>(d, ld, P, k0, ncol, i0, skip, nullptr, 0);
+        else if (fw_waves8())
+            fwq_update_kernel<false><<<grid, 512, 0, st>>>(d, ld, P, k0, ncol, i0, skip, nullptr, 0);
+        else
+            fwh_update_kernel<false><<<grid, 256, 0, st>>>(d, ld, P, k0, ncol, i0, skip, nullptr, 0);
+    };
     if (nrows > 0) {
         fw16_init_kernel<<<dim3(srt_ceil_div(ld, 2048), nrows), 256, 0, st>>>(n, ld, row0, w_rows, d,
                                                                            cap);
@@ -1741,15 +1828,14 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
             panel<<<nb + nrb, 256, 0, st>>>(d, ld, row0, nrb, P, k0, nb, 0, 1);
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
             if (skip >= 0) {
-                update<<<ncol128, uthr, 0, st>>>(d, ld, P, k0, ncol128, skip, -1, nullptr, 0);
+                update(ncol128, P, k0, ncol128, skip, -1);
                 SRT_HIPCHK(hipEventRecord(sc->row_done, st));
                 SRT_HIPCHK(hipStreamWaitEvent(cs, sc->row_done, 0));
                 if ((rc = produce(k + 1))) return rc;
                 if (nrow128 > 1)
-                    update<<<ncol128 * (nrow128 - 1), uthr, 0, st>>>(d, ld, P, k0, ncol128, 0, skip,
-                                                                   nullptr, 0);
+                    update(ncol128 * (nrow128 - 1), P, k0, ncol128, 0, skip);
             } else {
-                update<<<ncol128 * nrow128, uthr, 0, st>>>(d, ld, P, k0, ncol128, 0, -1, nullptr, 0);
+                update(ncol128 * nrow128, P, k0, ncol128, 0, -1);
             }
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
             SRT_HIPCHK(hipGetLastError());

@@ -1,5 +1,6 @@
 """C4 at full size in -m gpu: the 32,768-node complete graph through the default one-GPU schedule
-(encoding 5: u16 f16-compare upper-triangle rounds on two update streams, XCD-remapped grid, u8
+(encoding 5: u16 f16-compare upper-triangle rounds on two update streams, the 8-wave update
+kernel, XCD-remapped grid, u8
 predecessor slab, rel_levels_kernel<1024>), against the CPU oracle's dense Dijkstra
 (oracle.complete_sample) on rows spread over every 4k block, including the last tile row.
 

@@ -188,9 +188,12 @@ def test_dense_device_api_and_sharded_single_rank(gpu):
     assert torch.equal(lat2[:n, :n], lat[:n, :n]) and torch.equal(rel2[:n, :n], rel[:n, :n])
 
 
-@pytest.mark.parametrize("hop_ms,enc,sym,la", [(1, 4, "1", None), (1, 5, "1", "1"), (1, 3, "0", None),
-                                               (160, 2, "1", None), (400, 1, "1", None)])
-def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym, la):
+@pytest.mark.parametrize("hop_ms,enc,sym,la,env", [
+    (1, 4, "1", None, {}), (1, 5, "1", "1", {}), (1, 6, "1", "1", {"SRT_FW_KB": "128"}),
+    (1, 5, "1", "1", {"SRT_FW_WAVES": "4"}), (1, 4, "1", None, {"SRT_FW_WAVES": "4"}),
+    (1, 3, "0", None, {}), (1, 3, "0", None, {"SRT_FW_WAVES": "4"}),
+    (160, 2, "1", None, {}), (400, 1, "1", None, {})])
+def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym, la, env):
     """Each distance encoding of the dense build (fw16.hip) is exact where it is chosen.
 
     A 256-vertex ring with hop latencies hop_ms / hop_ms+1 (gcd 1 ms) plus a few chords: the
@@ -199,9 +202,13 @@ def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym, la):
     saturates both and ends on the u32 kernels. Every tier must match the oracle bit for bit.
     The graph is undirected, so the f16-compare tier runs its upper-triangle form (encoding 4)
     unless SRT_FW_SYM=0 forces every tile (encoding 3); SRT_FW_LOOKAHEAD=1 forces its two
-    update streams (encoding 5, the default from n = 8192).
+    update streams (encoding 5, the default from n = 8192), with 128-pivot rounds under
+    SRT_FW_KB=128 (encoding 6). SRT_FW_WAVES=4 selects the 4-wave update kernel
+    (fwh_update_kernel) over the 8-wave one (fwq_update_kernel).
     """
     monkeypatch.setenv("SRT_FW_SYM", sym)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     if la is not None:
         monkeypatch.setenv("SRT_FW_LOOKAHEAD", la)
     n = 256
