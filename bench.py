@@ -49,6 +49,7 @@ WORKLOADS = {
 }
 METRIC = "routing-table build time & node-pairs/sec (GB/s vs HBM peak), 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md, HBM3E spec peak
+LDS_PEAK_TBS = 256 * 256 * 2.4e9 / 1e12  # 256 B/clk/CU x 256 CUs x 2.4 GHz = 157.3 TB/s
 # VALU: 256 CU x 4 SIMD x 64 lanes x 2.4 GHz = 157.3 T lane-cycles/s; a wave64 relaxation costs
 # `cyc_per_relax` SIMD cycles under the issue model below, so the relaxation roof is
 # 157.3 T / cyc_per_relax.
@@ -269,11 +270,17 @@ def run_dense(c: Ctx, wl):
     cyc_per_relax = {6: 2.0, 5: 2.0, 4: 2.0, 3: 2.0, 2: 3.0, 1: 4.0}[enc]
     instr_per_relax = {6: 0.75, 5: 0.75, 4: 0.75, 3: 0.75, 2: 1.0, 1: 1.5}[enc]
     # the 8-wave update kernel (fwq_update_kernel) unless SRT_FW_WAVES=4 selects the 4-wave one
-    uk = "fwh_update_kernel" if os.environ.get("SRT_FW_WAVES") == "4" else "fwq_update_kernel"
-    kname = {6: "fwq_update_kernel<true, 4, 4>", 5: f"{uk}<true, 4>",
-             4: f"{uk}<true, 0>" if world == 1 else f"{uk}<true, 4>",
-             3: f"{uk}<false, 0>",
+    w4 = os.environ.get("SRT_FW_WAVES") == "4"
+    uk = "fwh_update_kernel" if w4 else "fwq_update_kernel"
+    st2 = "" if w4 else ", 2"  # fwq's third template argument: 32-pivot stages per tile
+    kname = {6: "fwq_update_kernel<true, 4, 4>", 5: f"{uk}<true, 4{st2}>",
+             4: f"{uk}<true, 0{st2}>" if world == 1 else f"{uk}<true, 4{st2}>",
+             3: f"{uk}<false, 0{st2}>",
              2: "fw16_update_kernel<false>", 1: "fw_update_kernel"}[enc]
+    # LDS bytes per relaxation: operand reads (fwq: 4 ds_read_b128 per 64 relaxations per lane =
+    # 1 B; fwh: 6 per 128 = 0.75 B) + the staged A/B slices (sA 16 KB + sB 8 KB per 32 pivots per
+    # 128x128 tile = 0.047 B)
+    lds_b_per_relax = (0.75 if w4 else 1.0) + 24576.0 / (32 * 128 * 128)
     # elements a timed launch updates: every local row; (enc 4, one GPU) the upper-triangle 128x128
     # tiles; (enc 4, sharded) this rank's kept tiles (fw16.hip sym_kept: one orientation of each
     # tile pair) less the next pivot block's tile row and column, which run in their own launch
@@ -305,6 +312,7 @@ def run_dense(c: Ctx, wl):
     relax_t = relax_per_round / (avg_upd_ms * 1e-3) / 1e12
     relax_peak_t = VALU_LANE_CYCLES_T / cyc_per_relax
     traffic = None
+    pmc = {}
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{c.args.workload}_n{world}.json")
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
@@ -312,6 +320,16 @@ def run_dense(c: Ctx, wl):
             traffic = pmc.get("hbm_bytes_per_launch")
             if enc in (5, 6) and traffic is not None:  # the timed unit is two launches
                 traffic = 2.0 * traffic
+    lds = None
+    if enc >= 3:
+        lds_tbs = relax_per_round * lds_b_per_relax / (avg_upd_ms * 1e-3) / 1e12
+        lds = {"achieved": round(lds_tbs, 2), "peak": LDS_PEAK_TBS, "unit": "TB/s",
+               "frac": round(lds_tbs / LDS_PEAK_TBS, 4), "bytes_per_relax": lds_b_per_relax,
+               "peak_basis": "256 B/clk/CU (ds_read_b128) x 256 CUs x 2.4 GHz "
+                             "(MI355X_MICROARCH.md §LDS)"}
+        if traffic is not None and pmc.get("lds_array_busy_frac") is not None:
+            lds["pmc_lds_array_busy_frac"] = round(pmc["lds_array_busy_frac"], 4)
+            lds["pmc_clock_ghz"] = round(pmc.get("clock_ghz", 0.0), 3)
     roofline = {
         # the north-star metric is GB/s vs HBM peak; the kernel itself is VALU-issue bound (min-plus
         # has no MFMA form), so the binding roof is reported beside it under "valu"
@@ -326,6 +344,7 @@ def run_dense(c: Ctx, wl):
                  f" distances; elements updated per unit = {int(elems)}, "
                  f"pivots per element = {pivots:.2f})",
         "algorithmic_min_bytes": float(nr) * ld * (4 + 8),
+        "lds": lds,
         "valu": {"achieved": round(relax_t, 2), "peak": round(relax_peak_t, 1),
                  "unit": "Trelax/s", "frac": round(relax_t / relax_peak_t, 4),
                  "instr_per_relax": instr_per_relax, "cycles_per_relax": cyc_per_relax,
@@ -426,16 +445,24 @@ def run_sparse(c: Ctx, wl):
     nsrc = s1 - s0
     k_ms = sum(s.ms_update for s in stats) / max(sum(s.n_update for s in stats), 1)
     achieved_gbs = nsrc * bytes_per_src / (k_ms * 1e-3) / 1e9
-    lds_row = 8 * (n * 4 + 4096) <= 160 * 1024  # wsssp.hip: LDS working row when 8 waves/CU fit
     # the kernel the build used (srt_build_stats.dist_enc for sparse builds): 2 = workgroup per
     # source with the LDS-packed distance row, 1 = wave per source, 0 = the block kernel
     enc = int(stats[-1].dist_enc)
-    kname = {2: "wgsssp_kernel<1024>",
-             1: "wsssp_kernel<%s, %s>" % ("true" if g.directed else "false",
-                                          "true" if lds_row else "false")}.get(enc, "sssp_kernel")
+    # the kernel's form from the build (srt_build_stats.fw_block of sparse builds)
+    form = int(stats[-1].fw_block)
+    tf = lambda b: "true" if b else "false"
+    kname = {2: f"wgsssp_kernel<1024, false, {tf(form & 1)}, {tf(form & 2)}>",
+             1: f"wsssp_kernel<{tf(g.directed)}, {tf(form & 1)}, {tf(form & 2)}>"
+             }.get(enc, "sssp_kernel")
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{c.args.workload}_n{world}.json")
+    if os.path.exists(pmc_path):
+        pmc = json.load(open(pmc_path))
+        if pmc.get("kernel") == kname:
+            traffic = pmc.get("hbm_bytes_per_launch")
     roofline = {"bound": "hbm", "kernel": kname,
         "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+        "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
         "bytes_per_launch": float(nsrc * bytes_per_src), "avg_launch_ms": round(k_ms, 3),
         "launches_timed": len(stats),
         "model": "per source: (n+1)*4 + arcs*16 + n*12 B (SURVEY §8d work-efficient gather model)",

@@ -65,7 +65,10 @@ typedef struct srt_build_opts {
 typedef struct srt_build_stats {
     int32_t time_kernels; /* input: 1 = bracket every FW update launch with HIP events */
     int32_t algo;        /* algorithm actually used */
-    int32_t fw_block;    /* pivot-block edge used by FW */
+    int32_t fw_block;    /* dense: pivot-block edge used by FW; sparse: the kernel's form --
+                          * wave kernel 1 = working row in LDS | 2 = private relabelled
+                          * reliability row; workgroup kernel 4 | 1 = original vertex order
+                          * | 2 = compact 8-byte arcs */
     int64_t ess_arcs;    /* essential arcs found by the predecessor pass (dense) */
     double ms_total;     /* wall time of the device build (HIP events), excl. host copies */
     double ms_fw;        /* shortest-distance kernels */

@@ -129,6 +129,10 @@ struct srt_sparse_graph {
      * old, inv[old] = new; rows keep their arcs sorted by ORIGINAL neighbour index */
     int32_t *perm, *inv;
     int2 *rp2, *irp2; /* (begin, end) of each relabelled row */
+    int2* rpo;        /* (begin, end) of each original row (the workgroup kernel's order) */
+    /* the distinct arc reliabilities (<= 256 of them, else NULL) and each arc's index into them */
+    double* rtab;
+    uint8_t* ridx;
     uint2 *cw2, *icw2;
     double *r2, *ir2;
 };
@@ -136,12 +140,14 @@ struct srt_sparse_graph {
 int srt_wgsssp_max_n(void);
 int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r, const int32_t* inv,
                     uint32_t max_w, int src_begin, int src_end, const int32_t* srcs, uint32_t* lat,
-                    double* rel, int* ovf, hipStream_t st);
+                    double* rel, int* ovf, hipStream_t st, const uint8_t* ridx,
+                    const double* rtab);
 int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, const double* r,
                    const int2* in_rowptr, const uint2* in_cw, const double* in_r,
                    const int32_t* perm, const int32_t* inv, uint32_t max_w, int local,
                    int src_begin, int src_end, const int32_t* srcs, uint32_t* lat, double* rel,
                    int* ovf, hipStream_t st);
+int srt_sparse_last_form(void);
 int srt_sparse_diag(int n, int src_begin, int src_end, const int32_t* srcs, const int32_t* rowptr,
                     const int32_t* col, const uint32_t* w, const double* r, const uint32_t* self_w,
                     const double* self_r, uint32_t* lat, double* rel, size_t ldo, hipStream_t st);
@@ -165,7 +171,8 @@ extern "C" void srt_sparse_graph_free(srt_sparse_graph* g) {
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(g->device);
-    void* ps[] = {g->rp, g->col, g->w, g->r, g->sw, g->sr, g->cw, g->perm, g->inv, g->rp2, g->cw2, g->r2};
+    void* ps[] = {g->rp, g->col, g->w, g->r, g->sw, g->sr, g->cw, g->perm, g->inv, g->rp2, g->cw2, g->r2,
+                  g->rpo, g->rtab, g->ridx};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (g->directed) {
@@ -305,7 +312,32 @@ static int sparse_graph_from_canon(const srt_canon* c, int device, srt_sparse_gr
         for (int32_t v = 0; v < c->n; v++)
             for (int32_t k = hrp[v].x; k < hrp[v].y; k++) span += fabs((double)v - (double)hcw[k].x);
         g->local = na == 0 || span / (double)na <= 4096.0;
-        rc = up((void**)&g->perm, hperm, nv * 4);
+        for (int32_t v = 0; v < c->n; v++) hrp[v] = make_int2(c->rowptr[v], c->rowptr[v + 1]);
+        rc = up((void**)&g->rpo, hrp, nv * sizeof(int2));
+        /* table of the distinct arc reliabilities when there are few (generators draw loss from a
+         * grid of 1e-4 steps; the workgroup kernel then carries an 8-bit index per arc) */
+        if (!rc && na > 0) {
+            double* tab = (double*)malloc(na * sizeof(double));
+            uint8_t* idx = (uint8_t*)malloc(na);
+            if (!tab || !idx) {
+                rc = SRT_E_NOMEM;
+            } else {
+                memcpy(tab, c->r, na * sizeof(double));
+                std::sort(tab, tab + na);
+                /* bitwise-distinct values (every r is a finite value in [0, 1]) */
+                const size_t nt = (size_t)(std::unique(tab, tab + na) - tab);
+                if (nt <= 256) {
+                    for (size_t k = 0; k < na; k++)
+                        idx[k] = (uint8_t)(std::lower_bound(tab, tab + nt, c->r[k]) - tab);
+                    rc = up((void**)&g->rtab, tab, nt * sizeof(double));
+                    if (!rc) rc = up((void**)&g->ridx, idx, na);
+                }
+            }
+            free(tab);
+            free(idx);
+        }
+        if (!rc) relabel_csr(c->n, c->rowptr, c->col, c->w, c->r, hperm, hinv, hrp, hcw, hr);
+        if (!rc) rc = up((void**)&g->perm, hperm, nv * 4);
         if (!rc) rc = up((void**)&g->inv, hinv, nv * 4);
         if (!rc) rc = up((void**)&g->rp2, hrp, nv * sizeof(int2));
         if (!rc) rc = up((void**)&g->cw2, hcw, na * sizeof(uint2));
@@ -428,9 +460,18 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
     const char* genv = getenv("SRT_SPARSE_WG");
     bool wg = !g->directed && g->n <= srt_wgsssp_max_n() &&
               (genv ? atoi(genv) != 0 : (g->n > 32768 && !g->local));
+    /* the workgroup kernel keeps its row in LDS (any order serves), so it runs on the original
+     * vertex order and writes reliability straight into the output rows; SRT_WG_ORDER=cm runs it
+     * on the Cuthill-McKee relabelling with a private row gathered at the end */
+    const char* oenv = getenv("SRT_WG_ORDER");
+    const bool wg_cm = oenv && !strcmp(oenv, "cm");
+    const int2* wrp = wg_cm ? g->rp2 : g->rpo;
+    const uint2* wcw = wg_cm ? g->cw2 : g->cw;
+    const double* wr = wg_cm ? g->r2 : g->r;
+    const int32_t* winv = wg_cm ? g->inv : NULL;
     if (wg) {
-        rc = srt_wgsssp_rows(g->n, g->rp2, g->cw2, g->r2, g->inv, g->max_w, b0, b0 + 1, one(0),
-                             lat_rows, rel_rows, ovf, st);
+        rc = srt_wgsssp_rows(g->n, wrp, wcw, wr, winv, g->max_w, b0, b0 + 1, one(0),
+                             lat_rows, rel_rows, ovf, st, g->ridx, g->rtab);
         if (rc) return rc;
         uint32_t* row = sc.row = (uint32_t*)malloc((size_t)g->n * sizeof(uint32_t));
         int pov = 1;
@@ -444,9 +485,9 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
             if (row[i] != SRT_INF && row[i] > ecc) ecc = row[i];
         wg = !pov && 2ull * ecc <= 1022ull;
         if (wg && nsrc > 1)
-            rc = srt_wgsssp_rows(g->n, g->rp2, g->cw2, g->r2, g->inv, g->max_w, b0 + 1, b0 + nsrc,
+            rc = srt_wgsssp_rows(g->n, wrp, wcw, wr, winv, g->max_w, b0 + 1, b0 + nsrc,
                                  one(1), lat_rows + (size_t)g->n, rel_rows + (size_t)g->n, ovf + 1,
-                                 st);
+                                 st, g->ridx, g->rtab);
         if (rc) return rc;
     }
     if (!wg)
@@ -454,6 +495,7 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
                             g->perm, g->inv, g->max_w, g->local, b0, b0 + nsrc, srcs, lat_rows,
                             rel_rows, ovf, st);
     if (rc) return rc;
+    const int form = srt_sparse_last_form();
     SRT_HIPCHK(hipEventRecord(e1, st));
     rc = srt_sparse_diag(g->n, b0, b0 + nsrc, srcs, g->rp, g->col, g->w, g->r, g->sw, g->sr,
                          lat_rows, rel_rows, (size_t)g->n, st);
@@ -515,6 +557,7 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
         stats->ms_update = a;
         stats->ess_arcs = nov; /* sparse builds: sources recomputed after a bucket overflow */
         stats->dist_enc = wg ? 2 : 1; /* sparse builds: 2 = workgroup kernel, 1 = wave kernel */
+        stats->fw_block = form;       /* sparse builds: the kernel's form (srt_sparse_last_form) */
         stats->tied_pairs = tied;
     }
     return SRT_OK;

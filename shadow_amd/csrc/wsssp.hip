@@ -286,6 +286,12 @@ __global__ __launch_bounds__(WL) void wsssp_kernel(
 /* Rows [src_begin, src_end) by the wave-per-source kernel. *overflowed receives the number of
  * sources whose buckets overflowed; their indices (relative to src_begin) are flagged in ovf
  * (device, nsrc ints, zeroed here) for the caller to recompute. */
+/* the form of the last sparse launch on this thread (srt_build_stats.fw_block of sparse builds):
+ * wave kernel: 1 = working row in LDS, 2 = private relabelled reliability row; workgroup kernel:
+ * 4 | 1 = original vertex order, 4 | 2 = compact arcs */
+static thread_local int g_sparse_form = 0;
+int srt_sparse_last_form(void) { return g_sparse_form; }
+
 int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, const double* r,
                    const int2* in_rowptr, const uint2* in_cw, const double* in_r,
                    const int32_t* perm, const int32_t* inv, uint32_t max_w, int local,
@@ -320,6 +326,7 @@ int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, con
      * padded to 8 bytes */
     const char* renv = getenv("SRT_WSSSP_RELROW"); /* tests: force either reliability form */
     const bool relp = renv ? atoi(renv) != 0 : local != 0;
+    g_sparse_form = (ldsd ? 1 : 0) | (relp ? 2 : 0);
     const size_t per_slot =
         (((relp ? 2 * (size_t)n : 0) + (size_t)nb * bcap + (ldsd ? 0 : n) + 1) & ~(size_t)1) *
         sizeof(uint32_t);
@@ -447,6 +454,24 @@ __global__ void wg_arcs_kernel(int n, const int2* __restrict__ rowptr, const uin
     }
 }
 
+/* compact arcs (CMP form of the workgroup kernel, original vertex order): 8 bytes per arc,
+ * x = u | w << 17 | ridx << 24 (u < 2^17, w < 128, ridx = index of the arc's reliability in the
+ * graph's table of distinct values, <= 256 of them), y = begin of u's row | min(deg u, 4095) << 20
+ * (arcs < 2^20). Half the bytes of the uint4 arcs, and the settle step reads its reliability from
+ * the 2-KB table instead of a random line of r[] */
+__global__ void wg_arcs_cmp_kernel(int n, const int2* __restrict__ rowptr, const uint2* __restrict__ cw,
+                                   const uint8_t* __restrict__ ridx, uint2* __restrict__ ca) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const int2 be = rowptr[v];
+    for (int k = be.x; k < be.y; ++k) {
+        const uint2 e = cw[k];
+        const int2 bu = rowptr[e.x];
+        const uint32_t deg = (uint32_t)min(bu.y - bu.x, 4095);
+        ca[k] = make_uint2(e.x | (e.y << 17) | ((uint32_t)ridx[k] << 24), (uint32_t)bu.x | (deg << 20));
+    }
+}
+
 /* PROF (tools only, SRT_WGSSSP_PROF=1): thread 0 accumulates shader-clock cycles per phase and
  * step counts into prof[block * 10 + k]: 0 init, 1 bucket search, 2 chunk head, 3 arcs,
  * 4 settle, 5 output, 6 steps, 7 chunks, 8 arc windows, 9 sources */
@@ -458,13 +483,21 @@ __global__ void wg_arcs_kernel(int n, const int2* __restrict__ rowptr, const uin
             pt = t_;                                                    \
         }                                                               \
     } while (0)
-template <int WG, bool PROF = false>
+/* ORIG: the graph in its original vertex order (inv == NULL): the reliability row is the output
+ * row itself (settle-time stores and predecessor loads go to rr), so no end-of-source gather of a
+ * private relabelled row (one random line per vertex: ~40% of the kernel's memory traffic on C5,
+ * profiles/r02_c5) */
+template <int WG, bool PROF = false, bool ORIG = false, bool CMP = false>
 __global__ __launch_bounds__(WG) void wgsssp_kernel(
     int n, int src_begin, const int32_t* __restrict__ srcs, int nsrc,
-    const int2* __restrict__ rowptr, const uint4* __restrict__ ca,
+    const int2* __restrict__ rowptr, const void* __restrict__ cav,
     const double* __restrict__ r, const int32_t* __restrict__ inv, uint32_t* __restrict__ lat,
     double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ ws, int nb, int bcap,
     int* __restrict__ overflow, unsigned long long* __restrict__ prof = nullptr) {
+    /* CMP: cav holds the compact arcs and r the table of distinct reliabilities */
+    static_assert(!CMP || ORIG, "compact arcs key ties on u: original vertex order only");
+    const uint4* __restrict__ ca = reinterpret_cast<const uint4*>(cav);
+    const uint2* __restrict__ cc = reinterpret_cast<const uint2*>(cav);
     unsigned long long pacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long pt = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     extern __shared__ uint32_t sd[]; /* packed distances, relabelled order */
@@ -474,16 +507,21 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
     __shared__ int s_found, s_ovf;
     const int tid = threadIdx.x, lane = tid & (WL - 1), wv = tid >> 6;
     const int words = (n + 2) / 3;
-    const size_t slot_words = ((size_t)nb * bcap * 2 + 2 * (size_t)n + 1) & ~(size_t)1;
+    const size_t slot_words = ((size_t)nb * bcap * 2 + (ORIG ? 0 : 2 * (size_t)n) + 1) & ~(size_t)1;
     uint2* buckets = reinterpret_cast<uint2*>(ws + (size_t)blockIdx.x * slot_words);
-    double* relp = reinterpret_cast<double*>(buckets + (size_t)nb * bcap);
+    double* relp = ORIG ? nullptr : reinterpret_cast<double*>(buckets + (size_t)nb * bcap);
     const uint32_t bm = (uint32_t)nb - 1u;
     for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
-        const int s = inv[srcs ? srcs[si] : src_begin + si];
+        const int s0 = srcs ? srcs[si] : src_begin + si;
+        const int s = ORIG ? s0 : inv[s0];
         uint32_t* ol = lat + (size_t)si * ldo;
         double* rr = rel + (size_t)si * ldo;
+        if (ORIG) relp = rr;
         for (int q = tid; q < words; q += WG) sd[q] = 0x3FFFFFFFu; /* three unreached fields */
-        for (int v = tid; v < n; v += WG) relp[v] = 0.0;
+        /* ORIG: the output row is written at settle time; unreached entries get their 0 at the
+         * end (no full-row initialisation pass) */
+        if (!ORIG)
+            for (int v = tid; v < n; v += WG) relp[v] = 0.0;
         for (int b = tid; b < nb; b += WG) bcnt[b] = 0;
         __syncthreads();
         if (tid == 0) {
@@ -576,6 +614,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                     if (PROF && tid == 0) pacc[8]++;
                     int own[WG_AK], rk[WG_AK];
                     uint4 e[WG_AK];
+                    uint2 ec[WG_AK];
 #pragma unroll
                     for (int j = 0; j < WG_AK; ++j) {
                         const int a = a0 + j * WG + tid;
@@ -588,11 +627,29 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                     }
 #pragma unroll
                     for (int j = 0; j < WG_AK; ++j)
-                        if (a0 + j * WG + tid < total) e[j] = ca[s_beg[own[j]] + rk[j]];
+                        if (a0 + j * WG + tid < total) {
+                            if constexpr (CMP)
+                                ec[j] = cc[s_beg[own[j]] + rk[j]];
+                            else
+                                e[j] = ca[s_beg[own[j]] + rk[j]];
+                        }
 #pragma unroll
                     for (int j = 0; j < WG_AK; ++j) {
                         if (a0 + j * WG + tid >= total) continue;
-                        const uint32_t u = e[j].x, wk = e[j].y;
+                        uint32_t u, wk, ridx = 0, begu, degu;
+                        if constexpr (CMP) {
+                            u = ec[j].x & 0x1FFFFu;
+                            wk = (ec[j].x >> 17) & 0x7Fu;
+                            ridx = ec[j].x >> 24;
+                            begu = ec[j].y & 0xFFFFFu;
+                            degu = ec[j].y >> 20;
+                            if (degu == 4095u) degu = WG_DEGC; /* clamped: reloaded at pop */
+                        } else {
+                            u = e[j].x;
+                            wk = e[j].y;
+                            begu = e[j].z;
+                            degu = e[j].w;
+                        }
                         const uint32_t du = wg_get(sd, u);
                         const uint32_t nd = d + wk;
                         if (nd < du) {
@@ -602,7 +659,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                                 const int b2 = (int)(nd & bm);
                                 const int slot = (int)atomicAdd(&bcnt[b2], 1u);
                                 if (slot < bcap) {
-                                    buckets[(size_t)b2 * bcap + slot] = wg_entry(u, e[j].z, e[j].w);
+                                    buckets[(size_t)b2 * bcap + slot] = wg_entry(u, begu, degu);
                                 } else {
                                     s_ovf = 1;
                                 }
@@ -610,9 +667,14 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                         }
                         /* canonical predecessor key (D[u], rank of the arc in the row), with u
                          * carried along so the settle step needs no second arc load */
-                        if (du != WG_INF && du + wk == d)
-                            atomicMin(&s_best[own[j]], ((unsigned long long)du << 40) |
-                                                           ((unsigned long long)rk[j] << 20) | u);
+                        if (du != WG_INF && du + wk == d) {
+                            if constexpr (CMP) /* (D[u], u) with the arc's reliability index */
+                                atomicMin(&s_best[own[j]], ((unsigned long long)du << 40) |
+                                                               ((unsigned long long)u << 8) | ridx);
+                            else
+                                atomicMin(&s_best[own[j]], ((unsigned long long)du << 40) |
+                                                               ((unsigned long long)rk[j] << 20) | u);
+                        }
                     }
                 }
                 WG_LDS_BARRIER(); /* the bucket stores drain by the next step's search barrier */
@@ -627,8 +689,13 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                         const unsigned long long key = s_best[tid];
                         pa = 0.0;
                         if (key != ~0ull) {
-                            pa = ld_coherent(relp + (uint32_t)(key & 0xFFFFFu));
-                            pb = r[beg + (int)((key >> 20) & 0xFFFFFu)];
+                            if constexpr (CMP) {
+                                pa = ld_coherent(relp + (uint32_t)((key >> 8) & 0x1FFFFu));
+                                pb = r[key & 0xFFu];
+                            } else {
+                                pa = ld_coherent(relp + (uint32_t)(key & 0xFFFFFu));
+                                pb = r[beg + (int)((key >> 20) & 0xFFFFFu)];
+                            }
                         }
                     }
                 }
@@ -642,10 +709,13 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
         WG_PT(1);
         /* output rows in original order, whole lines */
         for (int i = tid; i < n; i += WG) {
-            const int v = inv[i];
+            const int v = ORIG ? i : inv[i];
             const uint32_t dv = wg_get(sd, (uint32_t)v);
             ol[i] = dv == WG_INF ? SRT_INF : dv;
-            rr[i] = ld_coherent(relp + v);
+            if (!ORIG)
+                rr[i] = ld_coherent(relp + v);
+            else if (dv == WG_INF)
+                rr[i] = 0.0; /* unreached */
         }
         if (s_ovf && tid == 0) overflow[si] = 1;
         __syncthreads();
@@ -663,7 +733,8 @@ int srt_wgsssp_max_n(void) { return 3 * ((140 * 1024) / 4); }
  * full bucket). */
 int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r, const int32_t* inv,
                     uint32_t max_w, int src_begin, int src_end, const int32_t* srcs, uint32_t* lat,
-                    double* rel, int* ovf, hipStream_t st) {
+                    double* rel, int* ovf, hipStream_t st, const uint8_t* ridx,
+                    const double* rtab) {
     int nb = 1;
     while ((uint32_t)nb <= max_w) nb <<= 1;
     if (nb > 256 || n > srt_wgsssp_max_n()) {
@@ -682,15 +753,25 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     int2 last;
     SRT_HIPCHK(hipMemcpyAsync(&last, rowptr + (n - 1), sizeof(int2), hipMemcpyDeviceToHost, st));
     SRT_HIPCHK(hipStreamSynchronize(st));
-    uint4* ca = NULL;
-    if (hipMallocAsync((void**)&ca, ((size_t)last.y + 1) * sizeof(uint4), st) != hipSuccess) {
+    /* compact 8-byte arcs: original order, a reliability table, w < 128, arcs < 2^20 */
+    const char* cenv = getenv("SRT_WG_COMPACT");
+    const bool cmp = !inv && ridx && rtab && max_w < 128 && last.y < (1 << 20) &&
+                     !(cenv && atoi(cenv) == 0);
+    g_sparse_form = 4 | (inv ? 0 : 1) | (cmp ? 2 : 0);
+    void* ca = NULL;
+    const size_t arc_bytes = cmp ? sizeof(uint2) : sizeof(uint4);
+    if (hipMallocAsync(&ca, ((size_t)last.y + 1) * arc_bytes, st) != hipSuccess) {
         (void)hipGetLastError();
         srt_set_error("wgsssp: arc array of %d arcs failed", last.y);
         return SRT_E_NOMEM;
     }
-    wg_arcs_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rowptr, cw, ca);
+    if (cmp)
+        wg_arcs_cmp_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rowptr, cw, ridx,
+                                                                        (uint2*)ca);
+    else
+        wg_arcs_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, rowptr, cw, (uint4*)ca);
     SRT_HIPCHK(hipGetLastError());
-    const size_t slot_words = ((size_t)nb * bcap * 2 + 2 * (size_t)n + 1) & ~(size_t)1;
+    const size_t slot_words = ((size_t)nb * bcap * 2 + (inv ? 2 * (size_t)n : 0) + 1) & ~(size_t)1;
     size_t slots = (size_t)cus; /* one workgroup per CU: the packed row takes most of the LDS */
     if (slots > (size_t)nsrc) slots = nsrc;
     uint32_t* ws = NULL;
@@ -707,10 +788,19 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     if (penv && atoi(penv) > 0) {
         unsigned long long* prof = NULL;
         SRT_HIPCHK(hipMalloc((void**)&prof, slots * 10 * sizeof(unsigned long long)));
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-        wgsssp_kernel<1024, true><<<(unsigned)slots, 1024, dyn, st>>>(
-            n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf, prof);
+        if (cmp) {
+            SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true, true, true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+            wgsssp_kernel<1024, true, true, true><<<(unsigned)slots, 1024, dyn, st>>>(
+                n, src_begin, srcs, nsrc, rowptr, ca, rtab, inv, lat, rel, (size_t)n, ws, nb, bcap,
+                ovf, prof);
+        } else {
+            SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+            wgsssp_kernel<1024, true><<<(unsigned)slots, 1024, dyn, st>>>(
+                n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap,
+                ovf, prof);
+        }
         SRT_HIPCHK(hipGetLastError());
         unsigned long long* h = (unsigned long long*)calloc(slots * 10, sizeof(*h));
         SRT_HIPCHK(hipMemcpyAsync(h, prof, slots * 10 * sizeof(*h), hipMemcpyDeviceToHost, st));
@@ -733,6 +823,16 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
         wgsssp_kernel<512><<<(unsigned)slots, 512, dyn, st>>>(n, src_begin, srcs, nsrc, rowptr, ca, r, inv,
                                                              lat, rel, (size_t)n, ws, nb, bcap, ovf);
+    } else if (cmp) { /* original order, compact arcs, reliabilities from the table */
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, false, true, true>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+        wgsssp_kernel<1024, false, true, true><<<(unsigned)slots, 1024, dyn, st>>>(
+            n, src_begin, srcs, nsrc, rowptr, ca, rtab, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf);
+    } else if (!inv) { /* the graph in original order: reliability straight into the output rows */
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, false, true>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+        wgsssp_kernel<1024, false, true><<<(unsigned)slots, 1024, dyn, st>>>(
+            n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf);
     } else {
         SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));

@@ -190,3 +190,26 @@ def test_workgroup_kernel_overflow_fallback(gpu, monkeypatch, bcap):
                        True, oracle.ORC_INT_NS, 8)
     assert np.array_equal(lat, exp["lat_int"])
     assert np.array_equal(rel, exp["rel"])
+
+
+@pytest.mark.parametrize("form", [{}, {"SRT_WG_COMPACT": "0"}, {"SRT_WG_ORDER": "cm"}])
+@pytest.mark.parametrize("which", ["ba2000", "ba2500_many_losses"])
+def test_workgroup_kernel_forms(gpu, monkeypatch, form, which):
+    """The workgroup kernel's forms give the same exact tables: original vertex order with compact
+    8-byte arcs and the table of distinct reliabilities (default when the graph has <= 256 of
+    them), original order with 16-byte arcs (SRT_WG_COMPACT=0, or > 256 distinct losses), and the
+    Cuthill-McKee relabelling with a private reliability row (SRT_WG_ORDER=cm)."""
+    monkeypatch.setenv("SRT_SPARSE_WG", "1")
+    for k, v in form.items():
+        monkeypatch.setenv(k, v)
+    g = graphs.barabasi_albert(2000 if which == "ba2000" else 2500, seed=7)
+    if which == "ba2500_many_losses":  # continuous losses: one distinct reliability per edge
+        rng = np.random.default_rng(3)
+        g = graphs.Graph(g.n, g.directed, g.src, g.dst, g.lat_ns, rng.random(g.m) * 0.05)
+    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                algo=ALGO_SPARSE_SSSP)
+    exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss),
+                       True, oracle.ORC_INT_NS, 8)
+    assert st.dist_enc == 2
+    assert np.array_equal(lat, exp["lat_int"])
+    assert np.array_equal(rel, exp["rel"])

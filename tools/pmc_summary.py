@@ -49,7 +49,34 @@ def main():
             mean[name] = sum(v) / len(v)
             res[name] = {"launches": len(v), "mean_kb": mean[name], "first_kb": v[0],
                          "last_kb": v[-1], "min_kb": min(v), "max_kb": max(v)}
-    if len(mean) == 2:
+    # SQ / GRBM passes (optional): LDS, VALU and the clock held under load
+    for sub, names in (("sq", ("SQ_INSTS_LDS", "SQ_LDS_IDX_ACTIVE", "SQ_LDS_BANK_CONFLICT",
+                               "SQ_WAIT_INST_LDS", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU",
+                               "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES")),
+                       ("grbm", ("GRBM_GUI_ACTIVE", "GRBM_COUNT"))):
+        path = os.path.join(prof, sub, "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        for name in names:
+            v = counters(path, kernel, name)
+            if v:
+                mean[name] = sum(v) / len(v)
+                res.setdefault("pmc_mean_per_launch", {})[name] = mean[name]
+    # the GRBM pass carries its own kernel trace: under --pmc launches are serialized, so the
+    # clock is taken over the durations of those same launches
+    gst = stats_row(os.path.join(prof, "grbm", "run_kernel_stats.csv"), kernel) \
+        if os.path.exists(os.path.join(prof, "grbm", "run_kernel_stats.csv")) else None
+    if "GRBM_GUI_ACTIVE" in mean and gst:
+        # MI355X_MICROARCH.md 'DVFS give-back': clock ~= GRBM_GUI_ACTIVE / 8 (XCDs) / wall time
+        gdur = float(gst["AverageNs"]) * 1e-9
+        res["pmc_serialized_avg_ms"] = gdur * 1e3
+        res["clock_ghz"] = mean["GRBM_GUI_ACTIVE"] / 8.0 / gdur / 1e9
+        if "SQ_LDS_IDX_ACTIVE" in mean:
+            cyc = mean["GRBM_GUI_ACTIVE"] / 8.0
+            res["lds_array_busy_frac"] = mean["SQ_LDS_IDX_ACTIVE"] / (cyc * 256.0)
+            res["lds_note"] = ("SQ_LDS_IDX_ACTIVE (all LDS-array cycles, summed over CUs) / "
+                               "(GRBM_GUI_ACTIVE / 8 x 256 CUs)")
+    if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
         res["hbm_bytes_per_launch"] = (2.0 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0
         res["note"] = ("rocprofv3 --pmc, one pass per counter; FETCH_SIZE reads 1/2 of wide "
                        "coalesced streams on gfx950 (MI355X_MICROARCH.md §HBM) -> hbm bytes = "
