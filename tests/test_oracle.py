@@ -75,8 +75,9 @@ def test_c1_against_networkx():
 
 def test_sub_ms_quirk_documented():
     """Sub-millisecond latencies: the reference sums f64 ms and rounds up (worker.c:551), which
-    can exceed the exact integer sum by 1 ns (0.1 + 0.2 ms). The GPU tables hold the exact integer
-    ns; this pins the divergence class on a 3-vertex path."""
+    can exceed the exact integer sum by 1 ns (0.1 + 0.2 ms). This pins that class on a 3-vertex
+    path. The GPU build reproduces lat_ref: with a sub-ms quantum it also forms the path-order f64
+    ms table (tables.hip path_sweeps_kernel), checked in tests/test_gpu_dropin.py."""
     el = oracle.EdgeList(3, False, [0, 1], [1, 2], [100_000, 200_000], [0.0, 0.0])
     t = oracle.table(el)
     assert int(t["lat_int"][0, 2]) == 300_000
