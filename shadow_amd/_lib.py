@@ -11,7 +11,8 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libshadow_routing.so")
+# SRT_LIB_PATH: a side-by-side build of the same sources (tools: A/B of build-time variants)
+LIB_PATH = os.environ.get("SRT_LIB_PATH") or os.path.join(_HERE, "libshadow_routing.so")
 CSRC = os.path.join(_HERE, "csrc")
 
 SRT_OK = 0

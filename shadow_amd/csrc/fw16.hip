@@ -58,6 +58,31 @@ static __device__ __forceinline__ uint32_t min3h(uint32_t acc, uint32_t x, uint3
     asm("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(acc), "v"(x), "v"(y));
     return r;
 }
+/* acc = min(acc, a0 + b0, a1 + b1) per half as one fixed add, add, min3 triple: left to the
+ * scheduler, the adds of a whole row pair are hoisted ahead of their mins, and the update loop
+ * issues 5% slower (tools/fwh_variants.hip "qa": 72.7% vs 68.9% of the issue model) */
+static __device__ __forceinline__ uint32_t relax2h(uint32_t acc, uint32_t a0, uint32_t b0, uint32_t a1,
+                                                   uint32_t b1) {
+    uint32_t t0, t1;
+    asm("v_add_u32 %1, %3, %4\n\tv_add_u32 %2, %5, %6\n\tv_pk_minimum3_f16 %0, %0, %1, %2"
+        : "+v"(acc), "=&v"(t0), "=&v"(t1)
+        : "v"(a0), "v"(b0), "v"(a1), "v"(b1));
+    return acc;
+}
+/* relax2h over a thread-row of four words in one block, each triple with its own temporaries (no
+ * false dependence between consecutive triples through reused registers) */
+static __device__ __forceinline__ void relax_row4(uint32_t (&acc)[4], uint32_t a0, uint32_t a1,
+                                                  const uint32_t (&b0)[4], const uint32_t (&b1)[4]) {
+    uint32_t t0, t1, t2, t3, t4, t5, t6, t7;
+    asm("v_add_u32 %4, %12, %14\n\tv_add_u32 %5, %13, %18\n\tv_pk_minimum3_f16 %0, %0, %4, %5\n\t"
+        "v_add_u32 %6, %12, %15\n\tv_add_u32 %7, %13, %19\n\tv_pk_minimum3_f16 %1, %1, %6, %7\n\t"
+        "v_add_u32 %8, %12, %16\n\tv_add_u32 %9, %13, %20\n\tv_pk_minimum3_f16 %2, %2, %8, %9\n\t"
+        "v_add_u32 %10, %12, %17\n\tv_add_u32 %11, %13, %21\n\tv_pk_minimum3_f16 %3, %3, %10, %11"
+        : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "=&v"(t0), "=&v"(t1), "=&v"(t2),
+          "=&v"(t3), "=&v"(t4), "=&v"(t5), "=&v"(t6), "=&v"(t7)
+        : "v"(a0), "v"(a1), "v"(b0[0]), "v"(b0[1]), "v"(b0[2]), "v"(b0[3]), "v"(b1[0]), "v"(b1[1]),
+          "v"(b1[2]), "v"(b1[3]));
+}
 template <int I>
 static __device__ __forceinline__ uint32_t lane4(const uint4& v) {
     if constexpr (I == 0) return v.x;
@@ -773,11 +798,25 @@ static __device__ __forceinline__ void fwq_swrite(const fwq_stage_regs& g, uint3
     *reinterpret_cast<uint4*>(sB + rb * UBS + cb) = g.b;
 }
 
-/* rows 0..3 of the thread's 4x8 block, pivots m, m+1: 32 v_add_u32 + 16 v_pk_minimum3_f16 */
+/* rows 0..3 of the thread's 4x8 block, pivots m, m+1: 32 v_add_u32 + 16 v_pk_minimum3_f16.
+ * FWQ_ROWS_FORM (build-time A/B): 1 = fixed add, add, min3 triples; 2 = one asm block per row;
+ * 0 = plain C (the scheduler hoists the adds) */
+#ifndef FWQ_ROWS_FORM
+#define FWQ_ROWS_FORM 1
+#endif
 static __device__ __forceinline__ void fwq_rows(uint32_t (&acc)[4][4], const uint2 (&a)[4],
                                                 const uint4 (&b)[2]) {
     const uint32_t b0[4] = {b[0].x, b[0].y, b[0].z, b[0].w};
     const uint32_t b1[4] = {b[1].x, b[1].y, b[1].z, b[1].w};
+#if FWQ_ROWS_FORM == 2
+#pragma unroll
+    for (int r = 0; r < 4; ++r) relax_row4(acc[r], a[r].x, a[r].y, b0, b1);
+#elif FWQ_ROWS_FORM == 1
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = relax2h(acc[r][c], a[r].x, b0[c], a[r].y, b1[c]);
+#else
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         uint32_t t0[4], t1[4];
@@ -789,6 +828,7 @@ static __device__ __forceinline__ void fwq_rows(uint32_t (&acc)[4][4], const uin
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[r][c] = min3h(acc[r][c], t0[c], t1[c]);
     }
+#endif
 }
 
 static __device__ __forceinline__ void fwq_stage(uint32_t (&acc)[4][4], const uint32_t* __restrict__ sA,
@@ -869,10 +909,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         }
         fwq_stage(acc, sA, sB, tx, ty);
     }
+    /* the store addresses are formed again here (an opaque copy of the thread index): kept from
+     * the C load, the four 64-bit row addresses spill across the loop */
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
+    u16* Cq = C + (size_t)((tq >> 4) * 4) * ld + (tq & 15) * 8;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
         if (rowsum16(acc[r]) != sum0[r])
-            *reinterpret_cast<uint4*>(C + (size_t)(ty * 4 + r) * ld + tx * 8) =
+            *reinterpret_cast<uint4*>(Cq + (size_t)r * ld) =
                 make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
 }
 

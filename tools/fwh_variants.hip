@@ -6,6 +6,8 @@
 #define SRT_FW16_DEVICE_ONLY
 #include "../shadow_amd/csrc/fw16.hip"
 #include <algorithm>
+#include <cstring>
+#include <cstdlib>
 #include <cstdio>
 #include <vector>
 
@@ -343,6 +345,290 @@ float runqb(u16* D, int ld, unsigned* sink, int rounds) {
 }
 
 
+/* DPP operand broadcast (qd): the 16 lanes of a DPP row share their 4 output rows (tx = lane & 15
+ * picks the columns), so lane l holds the splatted A of pivot m0 + l for those rows and
+ * v_add_u32_dpp row_newbcast:k hands pivot m0 + k to the whole row. Per pivot pair and thread:
+ * 2 ds_read_b128 of B, and one ds_read_b128 of A per 16 pivots (against 2 per pair). A layout
+ * [row group g][pivot m][4 rows] (u32 splat), so the 16 lanes of a row read 256 contiguous B.
+ * Staging follows the SYM form: A[r][m] = P[m][I0 + r] (two pivots x 4 rows per thread). */
+#define QD_AS(g, m) (((g) * UKC + (m)) * 4)
+static __device__ __forceinline__ void qd_gload(uint4& ga, uint4& gb, const u16* __restrict__ Ph, int I0,
+                                                const u16* __restrict__ B, size_t ld, int tid) {
+    const int p = tid >> 5, rg = tid & 31;
+    const uint2 a0 = *reinterpret_cast<const uint2*>(Ph + (size_t)(2 * p) * ld + I0 + rg * 4);
+    const uint2 a1 = *reinterpret_cast<const uint2*>(Ph + (size_t)(2 * p + 1) * ld + I0 + rg * 4);
+    ga = make_uint4(a0.x, a0.y, a1.x, a1.y);
+    const int rb = tid >> 4, cb = (tid & 15) * 8;
+    gb = *reinterpret_cast<const uint4*>(B + (size_t)rb * ld + cb);
+}
+static __device__ __forceinline__ void qd_swrite(const uint4& ga, const uint4& gb, uint32_t* __restrict__ sA,
+                                                 u16* __restrict__ sB, int tid) {
+    const int p = tid >> 5, rg = tid & 31;
+    *reinterpret_cast<uint4*>(sA + QD_AS(rg, 2 * p)) =
+        make_uint4(splat(ga.x & 0xFFFFu), splat(ga.x >> 16), splat(ga.y & 0xFFFFu), splat(ga.y >> 16));
+    *reinterpret_cast<uint4*>(sA + QD_AS(rg, 2 * p + 1)) =
+        make_uint4(splat(ga.z & 0xFFFFu), splat(ga.z >> 16), splat(ga.w & 0xFFFFu), splat(ga.w >> 16));
+    const int rb = tid >> 4, cb = (tid & 15) * 8;
+    *reinterpret_cast<uint4*>(sB + rb * UBS + cb) = gb;
+}
+template <int K>
+static __device__ __forceinline__ void qd_pair(uint32_t (&acc)[4][4], const uint4& a, const uint4 (&b)[2]) {
+    const uint32_t av[4] = {a.x, a.y, a.z, a.w};
+    const uint32_t b0[4] = {b[0].x, b[0].y, b[0].z, b[0].w};
+    const uint32_t b1[4] = {b[1].x, b[1].y, b[1].z, b[1].w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t x0 = __builtin_amdgcn_mov_dpp(av[r], 0x150 + K, 0xf, 0xf, true);
+        const uint32_t x1 = __builtin_amdgcn_mov_dpp(av[r], 0x151 + K, 0xf, 0xf, true);
+        uint32_t t0[4], t1[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            t0[c] = x0 + b0[c];
+            t1[c] = x1 + b1[c];
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = min3h(acc[r][c], t0[c], t1[c]);
+    }
+}
+template <int K>
+static __device__ __forceinline__ void qd_group(uint32_t (&acc)[4][4], const uint4& a, const u16* __restrict__ pb,
+                                                int m0) {
+    if constexpr (K < 16) {
+        uint4 b[2];
+        fwh_readB(b, pb, m0 + K);
+        qd_pair<K>(acc, a, b);
+        qd_group<K + 2>(acc, a, pb, m0);
+    }
+}
+static __device__ __forceinline__ void qd_stage(uint32_t (&acc)[4][4], const uint32_t* __restrict__ sA,
+                                                const u16* __restrict__ sB, int tx, int ty) {
+    const u16* pb = sB + tx * 8;
+#pragma unroll 1
+    for (int m0 = 0; m0 < UKC; m0 += 16) {
+        const uint4 a = *reinterpret_cast<const uint4*>(sA + QD_AS(ty, m0 + tx));
+        qd_group<0>(acc, a, pb, m0);
+    }
+}
+template <int NST, bool IO, bool STAGE, bool DPP>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) void qd_kernel(
+    u16* __restrict__ D, int ld, const u16* __restrict__ P, int k0, int nct, unsigned* __restrict__ sink) {
+    __shared__ __attribute__((aligned(16))) uint32_t sA[UKC / 2 * 128 * 2];
+    __shared__ __attribute__((aligned(16))) u16 sB[UKC * UBS];
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int nb = gridDim.x, per = nb >> 3;
+    const int bid = (nb & 7) == 0 ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
+    const int I = bid / nct, J = bid % nct;
+    u16* C = D + (size_t)I * 128 * ld + J * 128;
+    const u16* Bg = P + J * 128;
+    uint4 ga, gb;
+    if (STAGE) qd_gload(ga, gb, P, I * 128, Bg, ld, tid);
+    uint32_t acc[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        if (IO) {
+            const uint4 v = *reinterpret_cast<const uint4*>(C + (size_t)(ty * 4 + r) * ld + tx * 8);
+            acc[r][0] = v.x;
+            acc[r][1] = v.y;
+            acc[r][2] = v.z;
+            acc[r][3] = v.w;
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[r][c] = 0x30003000u + r * 4 + c + tid;
+        }
+    }
+    uint32_t sum0[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        sum0[r] = rowsum16(acc[r]);
+        asm volatile("" : "+v"(sum0[r]));
+    }
+#pragma unroll 1
+    for (int s = 0; s < NST; ++s) {
+        if (STAGE) {
+            if (s) __syncthreads();
+            if (DPP) {
+                qd_swrite(ga, gb, sA, sB, tid);
+            } else { /* the fwq SYM image */
+                const int p = tid >> 5, rg = tid & 31;
+                const uint32_t a0[2] = {ga.x, ga.y}, a1[2] = {ga.z, ga.w};
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    *reinterpret_cast<uint4*>(sA + ((p * 128) + rg * 4 + 2 * i) * 2) =
+                        make_uint4(splat(a0[i] & 0xFFFFu), splat(a1[i] & 0xFFFFu), splat(a0[i] >> 16),
+                                   splat(a1[i] >> 16));
+                const int rb = tid >> 4, cb = (tid & 15) * 8;
+                *reinterpret_cast<uint4*>(sB + rb * UBS + cb) = gb;
+            }
+            __syncthreads();
+            if (s + 1 < NST)
+                qd_gload(ga, gb, P + (size_t)(s + 1) * UKC * ld, I * 128, Bg + (size_t)(s + 1) * UKC * ld, ld, tid);
+        }
+        if (DPP)
+            qd_stage(acc, sA, sB, tx, ty);
+        else
+            q_stage<false>(acc, sA, sB, tx, ty);
+    }
+    if (IO) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (rowsum16(acc[r]) != sum0[r])
+                *reinterpret_cast<uint4*>(C + (size_t)(ty * 4 + r) * ld + tx * 8) =
+                    make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+    } else {
+        unsigned x = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) x ^= acc[r][c];
+        if (x == 0x12345678u) sink[tid] = x;
+    }
+}
+
+template <int NST, bool IO, bool ST, bool DPP>
+float runqd(u16* D, int ld, unsigned* sink, int rounds) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    const int nct = ld / 128, grid = nct * nct;
+    hipEventRecord(a);
+    for (int k = 0; k < rounds; ++k) {
+        const int k0 = (k * NST * UKC) % ld;
+        qd_kernel<NST, IO, ST, DPP><<<grid, 512>>>(D, ld, D + (size_t)k0 * ld, k0, nct, sink);
+    }
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    return ms / rounds;
+}
+
+/* the compute-only loop with the LDS operand reads taken out: operands read once per stage, then
+ * re-marked as modified per pivot pair (an empty asm, no instruction), so the adds stay -- the
+ * instruction stream of fwq_rows alone */
+static __device__ __forceinline__ void qr_stage(uint32_t (&acc)[4][4], const uint32_t* __restrict__ sA,
+                                                const u16* __restrict__ sB, int tx, int ty) {
+    const uint32_t* pa = sA + ty * 4 * 2;
+    const u16* pb = sB + tx * 8;
+    uint4 b[2];
+    uint2 a[4];
+    fwh_readB(b, pb, 0);
+    fwh_readA(a, pa, 0);
+#pragma unroll 2
+    for (int m = 0; m < UKC; m += 2) {
+        asm volatile("" : "+v"(b[0].x), "+v"(b[0].y), "+v"(b[0].z), "+v"(b[0].w));
+        asm volatile("" : "+v"(b[1].x), "+v"(b[1].y), "+v"(b[1].z), "+v"(b[1].w));
+        asm volatile("" : "+v"(a[0].x), "+v"(a[0].y), "+v"(a[1].x), "+v"(a[1].y));
+        asm volatile("" : "+v"(a[2].x), "+v"(a[2].y), "+v"(a[3].x), "+v"(a[3].y));
+        q_rows(acc, a, b);
+    }
+}
+/* fwq_rows as fixed add, add, min3 triples (the order of the pure-mix microbenchmark) */
+static __device__ __forceinline__ void q_rows_asm(uint32_t (&acc)[4][4], const uint2 (&a)[4],
+                                                  const uint4 (&b)[2]) {
+    const uint32_t b0[4] = {b[0].x, b[0].y, b[0].z, b[0].w};
+    const uint32_t b1[4] = {b[1].x, b[1].y, b[1].z, b[1].w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            uint32_t t0, t1;
+            asm volatile("v_add_u32 %1, %3, %4\n\tv_add_u32 %2, %5, %6\n\tv_pk_minimum3_f16 %0, %0, %1, %2"
+                         : "+v"(acc[r][c]), "=&v"(t0), "=&v"(t1)
+                         : "v"(a[r].x), "v"(b0[c]), "v"(a[r].y), "v"(b1[c]));
+        }
+}
+template <bool ASM>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) void qa_kernel(
+    unsigned* __restrict__ sink, int nst, int lds) {
+    __shared__ __attribute__((aligned(16))) uint32_t sA[UKC / 2 * 128 * 2];
+    __shared__ __attribute__((aligned(16))) u16 sB[UKC * UBS];
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    uint32_t acc[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = 0x30003000u + r * 4 + c + tid;
+    const uint32_t* pa = sA + ty * 4 * 2;
+    const u16* pb = sB + tx * 8;
+    for (int w = tid; w < UKC / 2 * 128 * 2; w += 512) sA[w] = 0x10001u * (w & 7);
+    for (int w = tid; w < UKC * UBS; w += 512) sB[w] = (u16)(w & 15);
+    __syncthreads();
+    for (int s = 0; s < nst; ++s) {
+        uint4 b[2];
+        uint2 a[4];
+        fwh_readB(b, pb, 0);
+        fwh_readA(a, pa, 0);
+#pragma unroll 2
+        for (int m = 0; m < UKC; m += 2) {
+            if (lds) { /* with the LDS operand reads of fwq_stage */
+                fwh_readB(b, pb, m);
+                fwh_readA(a, pa, m);
+            } else {
+                asm volatile("" : "+v"(b[0].x), "+v"(b[0].y), "+v"(b[0].z), "+v"(b[0].w));
+                asm volatile("" : "+v"(b[1].x), "+v"(b[1].y), "+v"(b[1].z), "+v"(b[1].w));
+                asm volatile("" : "+v"(a[0].x), "+v"(a[0].y), "+v"(a[1].x), "+v"(a[1].y));
+                asm volatile("" : "+v"(a[2].x), "+v"(a[2].y), "+v"(a[3].x), "+v"(a[3].y));
+            }
+            if (ASM)
+                q_rows_asm(acc, a, b);
+            else
+                q_rows(acc, a, b);
+        }
+    }
+    unsigned x = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) x ^= acc[r][c];
+    if (x == 0x12345678u) sink[tid] = x;
+}
+template <bool ASM>
+float runqa(int ld, unsigned* sink, int rounds, int lds) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    const int nct = ld / 128, grid = nct * nct / 4;
+    hipEventRecord(a);
+    for (int k = 0; k < rounds; ++k) qa_kernel<ASM><<<grid, 512>>>(sink, 8, lds);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    return ms / rounds;
+}
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) void qr_kernel(
+    unsigned* __restrict__ sink, int nst) {
+    __shared__ __attribute__((aligned(16))) uint32_t sA[UKC / 2 * 128 * 2];
+    __shared__ __attribute__((aligned(16))) u16 sB[UKC * UBS];
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    uint32_t acc[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = 0x30003000u + r * 4 + c + tid;
+    for (int s = 0; s < nst; ++s) qr_stage(acc, sA, sB, tx, ty);
+    unsigned x = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) x ^= acc[r][c];
+    if (x == 0x12345678u) sink[tid] = x;
+}
+float runqr(int ld, unsigned* sink, int rounds, int nst = 2, int div = 1) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    const int nct = ld / 128, grid = nct * nct / div;
+    hipEventRecord(a);
+    for (int k = 0; k < rounds; ++k) qr_kernel<<<grid, 512>>>(sink, nst);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    return ms / rounds;
+}
+
 /* clock probe: the compute-only 8-wave loop, thread 0 of each block records shader-clock and
  * 100 MHz real-time stamps around its work */
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) void clk_kernel(
@@ -453,6 +739,24 @@ int main(int argc, char** argv) {
                cyc / rt * 0.1, relax / (ms * 1e-3) / 1e12, 100.0 * relax / (ms * 1e-3) / 1e12 / 78.64,
                100.0 * relax / (ms * 1e-3) / 1e12 / (78.64 * cyc / rt * 0.1 / 2.4));
         fflush(stdout);
+    }
+    const char* only = getenv("FWV_ONLY"); /* "qd": just the DPP comparison */
+    if (only && !strcmp(only, "qd")) {
+        report("qs8w (fwq SYM image) full", 64, el, [&] { return runqd<2, true, true, false>(D, ld, sink, rounds); });
+        report("qs8w compute-only", 64, el, [&] { return runqd<2, false, false, false>(D, ld, sink, rounds); });
+        report("qd8w DPP full", 64, el, [&] { return runqd<2, true, true, true>(D, ld, sink, rounds); });
+        report("qd8w DPP no-io", 64, el, [&] { return runqd<2, false, true, true>(D, ld, sink, rounds); });
+        report("qd8w DPP compute-only", 64, el, [&] { return runqd<2, false, false, true>(D, ld, sink, rounds); });
+        report("q8w regs-only (no LDS reads)", 64, el, [&] { return runqr(ld, sink, rounds); });
+        report("q8w regs-only, 32 stages per block, grid/16", 64, el, [&] { return runqr(ld, sink, rounds, 32, 16); });
+        report("q8w regs-only, 8 stages per block, grid/4", 64, el, [&] { return runqr(ld, sink, rounds, 8, 4); });
+        report("qa regs, compiler order", 64, el, [&] { return runqa<false>(ld, sink, rounds, 0); });
+        report("qa regs, add-add-min3 asm", 64, el, [&] { return runqa<true>(ld, sink, rounds, 0); });
+        report("qa lds, compiler order", 64, el, [&] { return runqa<false>(ld, sink, rounds, 1); });
+        report("qa lds, add-add-min3 asm", 64, el, [&] { return runqa<true>(ld, sink, rounds, 1); });
+        report("q8w compute-only", 64, el, [&] { return runq<2, false, false, false>(D, ld, sink, rounds); });
+        report("qd8w DPP 4 stages full", 128, el, [&] { return runqd<4, true, true, true>(D, ld, sink, rounds); });
+        return 0;
     }
     report("ref fwh_update_kernel<false>", 64, el, [&] { return run_ref(D, ld, rounds); });
     report("var 2 stages full", 64, el, [&] { return run<2, true, true, false>(D, ld, sink, rounds, 0); });
