@@ -58,13 +58,16 @@ static __device__ __forceinline__ uint32_t min3h(uint32_t acc, uint32_t x, uint3
     asm("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(acc), "v"(x), "v"(y));
     return r;
 }
-/* acc = min(acc, a0 + b0, a1 + b1) per half as one fixed add, add, min3 triple: left to the
- * scheduler, the adds of a whole row pair are hoisted ahead of their mins, and the update loop
- * issues 5% slower (tools/fwh_variants.hip "qa": 72.7% vs 68.9% of the issue model) */
+/* acc = min(acc, a0 + b0, a1 + b1) per half as one fixed add, add, s_nop 0, min3 group. A packed
+ * (VOP3P) instruction issued right after the VALU write of its operand is held by the hardware
+ * interlock, which stalls the SIMD; one s_nop 0 in that wave lets the other waves issue instead:
+ * the update's instruction stream runs at 85.7% of the issue model with it against 67.6% without
+ * (tools/valu_banks.hip, 8 waves per SIMD; VGPR bank placement measured no effect). Left to the
+ * scheduler, the adds of a row pair are also hoisted ahead of their mins (5% slower). */
 static __device__ __forceinline__ uint32_t relax2h(uint32_t acc, uint32_t a0, uint32_t b0, uint32_t a1,
                                                    uint32_t b1) {
     uint32_t t0, t1;
-    asm("v_add_u32 %1, %3, %4\n\tv_add_u32 %2, %5, %6\n\tv_pk_minimum3_f16 %0, %0, %1, %2"
+    asm("v_add_u32 %1, %3, %4\n\tv_add_u32 %2, %5, %6\n\ts_nop 0\n\tv_pk_minimum3_f16 %0, %0, %1, %2"
         : "+v"(acc), "=&v"(t0), "=&v"(t1)
         : "v"(a0), "v"(b0), "v"(a1), "v"(b1));
     return acc;
@@ -74,10 +77,10 @@ static __device__ __forceinline__ uint32_t relax2h(uint32_t acc, uint32_t a0, ui
 static __device__ __forceinline__ void relax_row4(uint32_t (&acc)[4], uint32_t a0, uint32_t a1,
                                                   const uint32_t (&b0)[4], const uint32_t (&b1)[4]) {
     uint32_t t0, t1, t2, t3, t4, t5, t6, t7;
-    asm("v_add_u32 %4, %12, %14\n\tv_add_u32 %5, %13, %18\n\tv_pk_minimum3_f16 %0, %0, %4, %5\n\t"
-        "v_add_u32 %6, %12, %15\n\tv_add_u32 %7, %13, %19\n\tv_pk_minimum3_f16 %1, %1, %6, %7\n\t"
-        "v_add_u32 %8, %12, %16\n\tv_add_u32 %9, %13, %20\n\tv_pk_minimum3_f16 %2, %2, %8, %9\n\t"
-        "v_add_u32 %10, %12, %17\n\tv_add_u32 %11, %13, %21\n\tv_pk_minimum3_f16 %3, %3, %10, %11"
+    asm("v_add_u32 %4, %12, %14\n\tv_add_u32 %5, %13, %18\n\ts_nop 0\n\tv_pk_minimum3_f16 %0, %0, %4, %5\n\t"
+        "v_add_u32 %6, %12, %15\n\tv_add_u32 %7, %13, %19\n\ts_nop 0\n\tv_pk_minimum3_f16 %1, %1, %6, %7\n\t"
+        "v_add_u32 %8, %12, %16\n\tv_add_u32 %9, %13, %20\n\ts_nop 0\n\tv_pk_minimum3_f16 %2, %2, %8, %9\n\t"
+        "v_add_u32 %10, %12, %17\n\tv_add_u32 %11, %13, %21\n\ts_nop 0\n\tv_pk_minimum3_f16 %3, %3, %10, %11"
         : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "=&v"(t0), "=&v"(t1), "=&v"(t2),
           "=&v"(t3), "=&v"(t4), "=&v"(t5), "=&v"(t6), "=&v"(t7)
         : "v"(a0), "v"(a1), "v"(b0[0]), "v"(b0[1]), "v"(b0[2]), "v"(b0[3]), "v"(b1[0]), "v"(b1[1]),
@@ -802,7 +805,7 @@ static __device__ __forceinline__ void fwq_swrite(const fwq_stage_regs& g, uint3
  * FWQ_ROWS_FORM (build-time A/B): 1 = fixed add, add, min3 triples; 2 = one asm block per row;
  * 0 = plain C (the scheduler hoists the adds) */
 #ifndef FWQ_ROWS_FORM
-#define FWQ_ROWS_FORM 1
+#define FWQ_ROWS_FORM 2
 #endif
 static __device__ __forceinline__ void fwq_rows(uint32_t (&acc)[4][4], const uint2 (&a)[4],
                                                 const uint4 (&b)[2]) {

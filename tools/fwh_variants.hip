@@ -111,19 +111,7 @@ static __device__ __forceinline__ void q_swrite(const uint4& v, const uint4& gb,
 }
 static __device__ __forceinline__ void q_rows(uint32_t (&acc)[4][4], const uint2 (&a)[4],
                                               const uint4 (&b)[2]) {
-    const uint32_t b0[4] = {b[0].x, b[0].y, b[0].z, b[0].w};
-    const uint32_t b1[4] = {b[1].x, b[1].y, b[1].z, b[1].w};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        uint32_t t0[4], t1[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            t0[c] = a[r].x + b0[c];
-            t1[c] = a[r].y + b1[c];
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[r][c] = min3h(acc[r][c], t0[c], t1[c]);
-    }
+    fwq_rows(acc, a, b); /* the library's row step (FWQ_ROWS_FORM) */
 }
 template <bool PF, bool CAST = false>
 static __device__ __forceinline__ void q_stage(uint32_t (&acc)[4][4], const uint32_t* __restrict__ sA,
