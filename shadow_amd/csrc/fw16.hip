@@ -72,6 +72,13 @@ static __device__ __forceinline__ uint32_t relax2h(uint32_t acc, uint32_t a0, ui
         : "v"(a0), "v"(b0), "v"(a1), "v"(b1));
     return acc;
 }
+/* acc = min(acc, a + b) per half on the U path (v_pk_min_u16), with the same s_nop 0 before the
+ * packed min */
+static __device__ __forceinline__ uint32_t relax1u(uint32_t acc, uint32_t a, uint32_t b) {
+    uint32_t t;
+    asm("v_add_u32 %1, %2, %3\n\ts_nop 0\n\tv_pk_min_u16 %0, %0, %1" : "+v"(acc), "=&v"(t) : "v"(a), "v"(b));
+    return acc;
+}
 /* relax2h over a thread-row of four words in one block, each triple with its own temporaries (no
  * false dependence between consecutive triples through reused registers) */
 static __device__ __forceinline__ void relax_row4(uint32_t (&acc)[4], uint32_t a0, uint32_t a1,
@@ -131,35 +138,21 @@ __device__ __forceinline__ void step_rows(u16x2 (&acc)[RN / 2], u16x2 (&acc1)[RN
                                           const uint4& a1, const uint32_t (&bv)[4][RN / 2]) {
     if constexpr (FM) {
         /* pivots MM, MM+1: two adds per column pair and row, one 3-input min */
-        uint32_t t[4][RN / 2];
 #pragma unroll
         for (int c = 0; c < RN / 2; ++c) {
-            t[0][c] = lane4<MM>(a0) + bv[MM][c];
-            t[1][c] = lane4<MM + 1>(a0) + bv[MM + 1][c];
-            t[2][c] = lane4<MM>(a1) + bv[MM][c];
-            t[3][c] = lane4<MM + 1>(a1) + bv[MM + 1][c];
-        }
-#pragma unroll
-        for (int c = 0; c < RN / 2; ++c) {
-            acc[c] = as2(min3h(as32(acc[c]), t[0][c], t[1][c]));
-            acc1[c] = as2(min3h(as32(acc1[c]), t[2][c], t[3][c]));
+            acc[c] = as2(relax2h(as32(acc[c]), lane4<MM>(a0), bv[MM][c], lane4<MM + 1>(a0), bv[MM + 1][c]));
+            acc1[c] = as2(relax2h(as32(acc1[c]), lane4<MM>(a1), bv[MM][c], lane4<MM + 1>(a1), bv[MM + 1][c]));
         }
     } else {
         /* one pivot at a time, two rows: RN independent adds, then RN mins */
 #pragma unroll
         for (int mm = MM; mm < MM + 2; ++mm) {
-            uint32_t t[2][RN / 2];
             const uint32_t s0 = mm == MM ? lane4<MM>(a0) : lane4<MM + 1>(a0);
             const uint32_t s1 = mm == MM ? lane4<MM>(a1) : lane4<MM + 1>(a1);
 #pragma unroll
             for (int c = 0; c < RN / 2; ++c) {
-                t[0][c] = s0 + bv[mm][c];
-                t[1][c] = s1 + bv[mm][c];
-            }
-#pragma unroll
-            for (int c = 0; c < RN / 2; ++c) {
-                acc[c] = __builtin_elementwise_min(acc[c], as2(t[0][c]));
-                acc1[c] = __builtin_elementwise_min(acc1[c], as2(t[1][c]));
+                acc[c] = as2(relax1u(as32(acc[c]), s0, bv[mm][c]));
+                acc1[c] = as2(relax1u(as32(acc1[c]), s1, bv[mm][c]));
             }
         }
     }
@@ -302,14 +295,14 @@ static __device__ __forceinline__ void close64(u16* __restrict__ s, int tid) {
                 if constexpr (FM) {
 #pragma unroll
                     for (int q = 0; q < 4; q += 2) {
-                        acc[r].x = min3h(acc[r].x, p[q] + b[q].x, p[q + 1] + b[q + 1].x);
-                        acc[r].y = min3h(acc[r].y, p[q] + b[q].y, p[q + 1] + b[q + 1].y);
+                        acc[r].x = relax2h(acc[r].x, p[q], b[q].x, p[q + 1], b[q + 1].x);
+                        acc[r].y = relax2h(acc[r].y, p[q], b[q].y, p[q + 1], b[q + 1].y);
                     }
                 } else {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        acc[r].x = as32(relax(as2(acc[r].x), p[q], b[q].x));
-                        acc[r].y = as32(relax(as2(acc[r].y), p[q], b[q].y));
+                        acc[r].x = relax1u(acc[r].x, p[q], b[q].x);
+                        acc[r].y = relax1u(acc[r].y, p[q], b[q].y);
                     }
                 }
             }
@@ -579,16 +572,7 @@ static __device__ __forceinline__ void fwh_rows(uint32_t (&acc)[8][4], const uin
     const uint32_t b0[4] = {b[0].x, b[0].y, b[0].z, b[0].w};
     const uint32_t b1[4] = {b[1].x, b[1].y, b[1].z, b[1].w};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        uint32_t t0[4], t1[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            t0[c] = a[r].x + b0[c];
-            t1[c] = a[r].y + b1[c];
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[R0 + r][c] = min3h(acc[R0 + r][c], t0[c], t1[c]);
-    }
+    for (int r = 0; r < 4; ++r) relax_row4(acc[R0 + r], a[r].x, a[r].y, b0, b1);
 }
 
 #define FWH_PHASE __builtin_amdgcn_sched_barrier(0)
@@ -1118,7 +1102,7 @@ __global__ __launch_bounds__(256) void sym_panel_stage_kernel(u16* __restrict__ 
                 const uint32_t b0[4] = {b[q].x, b[q].y, b[q].z, b[q].w};
                 const uint32_t b1[4] = {b[q + 1].x, b[q + 1].y, b[q + 1].z, b[q + 1].w};
 #pragma unroll
-                for (int c = 0; c < 4; ++c) acc[r][c] = min3h(acc[r][c], p[q] + b0[c], p[q + 1] + b1[c]);
+                for (int c = 0; c < 4; ++c) acc[r][c] = relax2h(acc[r][c], p[q], b0[c], p[q + 1], b1[c]);
             }
         }
     }
@@ -1808,12 +1792,13 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
         /* two update streams once the rounds are long enough to hide their event waits;
          * SRT_FW_LOOKAHEAD=0/1 forces either form */
         const bool two = la_env ? atoi(la_env) != 0 : ld >= 8192;
-        /* SRT_FW_KB=128: 128-pivot rounds on the two update streams (8-wave kernel). Measured on
-         * C4: the same period per 64 pivots as the 64-pivot rounds (1.315 ms per 128-pivot pair
-         * vs 0.657 per 64; build 380.5 vs 380.1 ms), so the simpler 64-pivot rounds stay the
-         * default */
+        /* 128-pivot rounds on the two update streams (8-wave kernel; SRT_FW_KB=64 selects the
+         * 64-pivot rounds). With the update's compute loop at ~85% of the issue model, the per-tile
+         * C load, row sums, staging and store are what is left to amortize: C4 332.2 vs 344.1 ms
+         * per build on one box (before that loop change the two measured the same, 380.5 vs
+         * 380.1 ms) */
         const char* kb_env = getenv("SRT_FW_KB");
-        const bool r128 = two && fw_waves8() && ld >= 256 && kb_env && atoi(kb_env) == 128;
+        const bool r128 = two && fw_waves8() && ld >= 256 && !(kb_env && atoi(kb_env) == 64);
         *sym = r128 ? 3 : two ? 2 : 1;
         return fw16_build_sym(n, ld, w_rows, lat_rows, st, evp, exact, two, r128);
     }

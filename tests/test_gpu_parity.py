@@ -189,7 +189,7 @@ def test_dense_device_api_and_sharded_single_rank(gpu):
 
 
 @pytest.mark.parametrize("hop_ms,enc,sym,la,env", [
-    (1, 4, "1", None, {}), (1, 5, "1", "1", {}), (1, 6, "1", "1", {"SRT_FW_KB": "128"}),
+    (1, 4, "1", None, {}), (1, 6, "1", "1", {}), (1, 5, "1", "1", {"SRT_FW_KB": "64"}),
     (1, 5, "1", "1", {"SRT_FW_WAVES": "4"}), (1, 4, "1", None, {"SRT_FW_WAVES": "4"}),
     (1, 3, "0", None, {}), (1, 3, "0", None, {"SRT_FW_WAVES": "4"}),
     (160, 2, "1", None, {}), (400, 1, "1", None, {})])
@@ -202,8 +202,8 @@ def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym, la, e
     saturates both and ends on the u32 kernels. Every tier must match the oracle bit for bit.
     The graph is undirected, so the f16-compare tier runs its upper-triangle form (encoding 4)
     unless SRT_FW_SYM=0 forces every tile (encoding 3); SRT_FW_LOOKAHEAD=1 forces its two
-    update streams (encoding 5, the default from n = 8192), with 128-pivot rounds under
-    SRT_FW_KB=128 (encoding 6). SRT_FW_WAVES=4 selects the 4-wave update kernel
+    update streams, with 128-pivot rounds (encoding 6, the default from n = 8192) or 64-pivot
+    rounds under SRT_FW_KB=64 (encoding 5). SRT_FW_WAVES=4 selects the 4-wave update kernel
     (fwh_update_kernel) over the 8-wave one (fwq_update_kernel).
     """
     monkeypatch.setenv("SRT_FW_SYM", sym)
