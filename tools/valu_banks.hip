@@ -75,6 +75,34 @@
     TF(8, 49, 50) "s_nop 0\n\t" TF(9, 54, 55) "s_nop 0\n\t" TF(10, 51, 48) "s_nop 0\n\t" TF(11, 52, 53) "s_nop 0\n\t" \
     TF(12, 49, 50) "s_nop 0\n\t" TF(13, 54, 55) "s_nop 0\n\t" TF(14, 51, 48) "s_nop 0\n\t" TF(15, 52, 53) "s_nop 0\n\t"
 
+/* D1 / D2: s_nop 1 / s_nop 2 (two / three wait states) instead of s_nop 0 */
+#define TN1(acc, a, b, c, d, t0, t1) \
+    "v_add_u32 v" #t0 ", v" #a ", v" #b "\n\tv_add_u32 v" #t1 ", v" #c ", v" #d \
+    "\n\ts_nop 1\n\tv_pk_minimum3_f16 v" #acc ", v" #acc ", v" #t0 ", v" #t1 "\n\t"
+#define TN2(acc, a, b, c, d, t0, t1) \
+    "v_add_u32 v" #t0 ", v" #a ", v" #b "\n\tv_add_u32 v" #t1 ", v" #c ", v" #d \
+    "\n\ts_nop 2\n\tv_pk_minimum3_f16 v" #acc ", v" #acc ", v" #t0 ", v" #t1 "\n\t"
+#define BODY_X(TT) \
+    TT(0, 32, 26, 33, 18, 49, 50) TT(1, 32, 27, 33, 19, 54, 55) TT(2, 32, 30, 33, 22, 51, 48) TT(3, 32, 31, 33, 23, 52, 53) \
+    TT(4, 36, 26, 37, 18, 49, 50) TT(5, 36, 27, 37, 19, 54, 55) TT(6, 36, 30, 37, 22, 51, 48) TT(7, 36, 31, 37, 23, 52, 53) \
+    TT(8, 40, 26, 41, 18, 49, 50) TT(9, 40, 27, 41, 19, 54, 55) TT(10, 40, 30, 41, 22, 51, 48) TT(11, 40, 31, 41, 23, 52, 53) \
+    TT(12, 44, 26, 45, 18, 49, 50) TT(13, 44, 27, 45, 19, 54, 55) TT(14, 44, 30, 45, 22, 51, 48) TT(15, 44, 31, 45, 23, 52, 53)
+/* J: four groups' adds (8), then their four min3s: the nearest operand is written 4 slots back */
+#define TJ(a0, ax, b0, ay, c0, t0, t1, a1, b1, c1, t2, t3, a2, b2, c2, t4, t5, a3, b3, c3, t6, t7, ax2, ay2) \
+    "v_add_u32 v" #t0 ", v" #ax ", v" #b0 "\n\tv_add_u32 v" #t1 ", v" #ay ", v" #c0 "\n\t" \
+    "v_add_u32 v" #t2 ", v" #ax ", v" #b1 "\n\tv_add_u32 v" #t3 ", v" #ay ", v" #c1 "\n\t" \
+    "v_add_u32 v" #t4 ", v" #ax ", v" #b2 "\n\tv_add_u32 v" #t5 ", v" #ay ", v" #c2 "\n\t" \
+    "v_add_u32 v" #t6 ", v" #ax ", v" #b3 "\n\tv_add_u32 v" #t7 ", v" #ay ", v" #c3 "\n\t" \
+    "v_pk_minimum3_f16 v" #a0 ", v" #a0 ", v" #t0 ", v" #t1 "\n\t" \
+    "v_pk_minimum3_f16 v" #a1 ", v" #a1 ", v" #t2 ", v" #t3 "\n\t" \
+    "v_pk_minimum3_f16 v" #a2 ", v" #a2 ", v" #t4 ", v" #t5 "\n\t" \
+    "v_pk_minimum3_f16 v" #a3 ", v" #a3 ", v" #t6 ", v" #t7 "\n\t"
+#define BODY_J \
+    TJ(0, 32, 26, 33, 18, 48, 49, 1, 27, 19, 50, 51, 2, 30, 22, 52, 53, 3, 31, 23, 54, 55, 0, 0) \
+    TJ(4, 36, 26, 37, 18, 48, 49, 5, 27, 19, 50, 51, 6, 30, 22, 52, 53, 7, 31, 23, 54, 55, 0, 0) \
+    TJ(8, 40, 26, 41, 18, 48, 49, 9, 27, 19, 50, 51, 10, 30, 22, 52, 53, 11, 31, 23, 54, 55, 0, 0) \
+    TJ(12, 44, 26, 45, 18, 48, 49, 13, 27, 19, 50, 51, 14, 30, 22, 52, 53, 15, 31, 23, 54, 55, 0, 0)
+
 #define INIT "v_mov_b32 v0, 0x30003000\n\tv_mov_b32 v1, v0\n\tv_mov_b32 v2, v0\n\tv_mov_b32 v3, v0\n\t" \
     "v_mov_b32 v4, v0\n\tv_mov_b32 v5, v0\n\tv_mov_b32 v6, v0\n\tv_mov_b32 v7, v0\n\t"              \
     "v_mov_b32 v8, v0\n\tv_mov_b32 v9, v0\n\tv_mov_b32 v10, v0\n\tv_mov_b32 v11, v0\n\t"             \
@@ -97,6 +125,9 @@ KERNEL(k_d, BODY_D)
 KERNEL(k_e, BODY_E)
 KERNEL(k_f, BODY_F)
 KERNEL(k_fn, BODY_FN)
+KERNEL(k_d1, BODY_X(TN1))
+KERNEL(k_d2, BODY_X(TN2))
+KERNEL(k_j, BODY_J)
 
 typedef void (*kfn)(unsigned*, unsigned long long*);
 static void run(const char* name, kfn f, int w, unsigned* out, unsigned long long* clk) {
@@ -130,6 +161,9 @@ int main() {
         run("B bank-free operands and temps", k_b, w, out, clk);
         run("C bank-free, rotating temps", k_c, w, out, clk);
         run("D = C + s_nop 0 before each min3", k_d, w, out, clk);
+        run("D1 = C + s_nop 1 before each min3", k_d1, w, out, clk);
+        run("D2 = C + s_nop 2 before each min3", k_d2, w, out, clk);
+        run("J = 8 adds then 4 min3s (4 back)", k_j, w, out, clk);
         run("E = C, two triples interleaved", k_e, w, out, clk);
         run("F adds read the accumulator (valu_rate2)", k_f, w, out, clk);
         run("F + s_nop 0 after each triple", k_fn, w, out, clk);
