@@ -446,10 +446,13 @@ __global__ void arc_transpose_fill(int n, const int32_t* __restrict__ ptr,
  * a BM-row block, so each block's transpose is one contiguous slab */
 template <typename T, typename TO = T, int BM = 0>
 __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, const T* __restrict__ in,
-                                                        size_t ldi, TO* __restrict__ out, size_t ldo) {
+                                                        size_t ldi, TO* __restrict__ out, size_t ldo,
+                                                        int upper = 0) {
     __shared__ T tile[64][65];
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+    /* upper: a (t-major) block whose every t precedes every s holds no pair the build keeps */
+    if (upper && r0 + 64 <= c0) return;
     T v[16]; /* all 16 loads in flight before the LDS stores */
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -775,13 +778,24 @@ __global__ __launch_bounds__(512) void rel_sweeps_kernel(int n, int ld, int row0
  * D[s][t] == L) only reads values final since an earlier pass: each entry is formed once,
  * rel(s,t) = rel(s,pred) * r(pred,t), the left-to-right product of topology.c:1364-1365.
  * Rows whose largest distance exceeds maxl passes are flagged for rel_sweeps_kernel. */
-template <int NT, int MAXN>
+/* SYM (one GPU, undirected): the predecessor and reliability rows were transposed for the pairs
+ * t > s only (transpose_kernel upper); the lower entries are the mirror of rows t < s and are
+ * overwritten after this pass. The row still needs the lower vertices that are ancestors of its
+ * upper targets: they are marked from the upper predecessors (an LDS bitmap), their predecessor
+ * and arc reliability read from the source-column arrays of the predecessor pass (predT / rT,
+ * column s), transitively, and only upper and marked targets take the level passes; every other
+ * lower predecessor entry is set to -1. A row flagged for the sweep kernel marks every lower
+ * vertex (the sweeps walk whole rows). */
+template <int NT, int MAXN, bool SYM = false>
 __global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
                                                          const uint32_t* __restrict__ lat,
-                                                         const int32_t* __restrict__ pred,
+                                                         int32_t* __restrict__ pred,
                                                          double* __restrict__ rel, int maxl,
                                                          int32_t* __restrict__ max_depth,
-                                                         int32_t* __restrict__ sweep) {
+                                                         int32_t* __restrict__ sweep,
+                                                         const int32_t* __restrict__ predT = nullptr,
+                                                         const double* __restrict__ rT = nullptr,
+                                                         size_t ldT = 0) {
     /* each thread owns t = tid + i * NT (i < PER, n <= MAXN); the row's distances are read once
      * and kept as bytes in registers (levels <= maxl <= 254 once the row qualifies), so a pass
      * only compares registers and touches memory for its own targets. The row reads go through
@@ -792,12 +806,17 @@ __global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
     if (s >= n) return;
     const int tid = threadIdx.x;
     const uint32_t* dl = lat + (size_t)blockIdx.x * ld;
-    const int32_t* pg = pred + (size_t)blockIdx.x * ld;
+    int32_t* pg = pred + (size_t)blockIdx.x * ld;
     double* rr = rel + (size_t)blockIdx.x * ld;
     const __amdgpu_buffer_rsrc_t rd =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(dl), 0, n * 4, 0x00020000);
     __shared__ uint32_t red[NT / 64];
     extern __shared__ uint16_t s_wlist[]; /* NT / 64 waves x 64 x PER target indices */
+    constexpr int NWD = MAXN / 32;
+    /* SYM: the marked and processed bitmaps */
+    uint32_t* mk = reinterpret_cast<uint32_t*>(s_wlist + (NT / 64) * 64 * PER);
+    uint32_t* dn = mk + NWD;
+    uint32_t* nwb = dn + NWD;
     uint32_t lv[PER / 4];
     uint32_t mx = 0;
 #pragma unroll
@@ -818,6 +837,63 @@ __global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
     mx = 0;
     for (int i = 0; i < NT / 64; ++i) mx = max(mx, red[i]);
     if (tid == 0) sweep[blockIdx.x] = (int)mx > maxl;
+    if constexpr (SYM) {
+        const bool full = (int)mx > maxl; /* the sweeps need every lower predecessor */
+        for (int q = tid; q < NWD; q += NT) {
+            uint32_t m = 0u;
+            if (full) { /* every lower vertex (t < s, t < n) */
+                const int lo = q * 32;
+                m = lo + 32 <= s ? 0xFFFFFFFFu : lo >= s ? 0u : (1u << (s - lo)) - 1u;
+            }
+            mk[q] = m;
+            dn[q] = 0u;
+        }
+        __syncthreads();
+        if (!full) { /* the lower predecessors of the upper targets */
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int t = tid + i * NT;
+                if (t > s && t < n && ((lv[i >> 2] >> (8 * (i & 3))) & 0xFFu)) {
+                    const int u = pg[t];
+                    if (u >= 0 && u < s) atomicOr(&mk[u >> 5], 1u << (u & 31));
+                }
+            }
+        }
+        /* closure: each newly marked vertex takes its predecessor and arc reliability from
+         * column s of the predecessor pass's arrays; a lower predecessor is marked in turn */
+        for (;;) {
+            __syncthreads();
+            int any = 0;
+            for (int q = tid; q < NWD; q += NT) {
+                const uint32_t nb = mk[q] & ~dn[q];
+                nwb[q] = nb;
+                dn[q] |= nb;
+                any |= nb != 0u;
+            }
+            if (!__syncthreads_or(any)) break;
+            for (int q = tid; q < NWD; q += NT) {
+                uint32_t bits = nwb[q];
+                while (bits) {
+                    const int u = q * 32 + __ffs(bits) - 1;
+                    bits &= bits - 1u;
+                    if (u >= n || u == s) continue;
+                    const size_t o = (size_t)u * ldT + (size_t)(s - row0);
+                    const int p = predT[o];
+                    pg[u] = p;
+                    rr[u] = rT[o];
+                    if (p >= 0 && p < s) atomicOr(&mk[p >> 5], 1u << (p & 31));
+                }
+            }
+        }
+        /* the other lower entries: no predecessor (the path-order ms pass skips them) */
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int t = tid + i * NT;
+            if (t < s && !((dn[t >> 5] >> (t & 31)) & 1u)) pg[t] = -1;
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
     if ((int)mx > maxl) return; /* long distance range: rel_sweeps_kernel takes the row */
     /* per pass, each wave compacts its targets of level L into its own LDS list (ballot +
      * prefix popcount), then walks the list with its lanes: the loads of different targets are
@@ -829,7 +905,9 @@ __global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
         int cnt = 0;
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
-            const bool hit = ((lv[i >> 2] >> (8 * (i & 3))) & 0xFFu) == L;
+            const int t = tid + i * NT;
+            const bool hit = ((lv[i >> 2] >> (8 * (i & 3))) & 0xFFu) == L &&
+                             (!SYM || t > s || ((dn[t >> 5] >> (t & 31)) & 1u));
             const uint64_t m = __ballot(hit);
             if (hit) wl[cnt + __popcll(m & lt)] = (uint16_t)(tid + i * NT);
             cnt += __popcll(m);
@@ -1097,6 +1175,7 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         srt_set_error("dense predecessor pass supports n <= %d (n = %d)", srt_dense_max_n(), n);
         return SRT_E_RANGE;
     }
+    bool upper = false;
     if (lrows > 0) {
         const size_t slab = (size_t)ld * nrows;
         /* the transpose is block-major (DT[s / 64][u][s % 64]): a 64-source block's slab is
@@ -1125,6 +1204,11 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         size_t c4 = ws->rt_cap;
         if ((rc = ws_grow((void**)&ws->rt, &c4, slab, sizeof(double)))) return rc;
         ws->rt_cap = c4;
+        /* upper-only (one GPU, undirected, byte distances): the transposes and the reliability
+         * levels cover the pairs t > s, plus the lower ancestors rel_levels_kernel<SYM> marks;
+         * the lower triangle is the mirror (srt_dense_post_device) */
+        upper = !directed && !gather && row0 == 0 && lrows == n && d16 && srt_fw16_small() &&
+                n <= 32768 && !(getenv("SRT_DENSE_UPPER") && !atoi(getenv("SRT_DENSE_UPPER")));
         if (d16 && srt_fw16_small()) {
             /* every distance fits a byte: the transposed slab of a 64-source block is 2 MB and
              * stays in its XCD's L2 */
@@ -1171,14 +1255,27 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         int32_t* pred = reinterpret_cast<int32_t*>(ws->dt);
         transpose_kernel<uint32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
             n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows,
-            reinterpret_cast<uint32_t*>(pred), (size_t)ld);
+            reinterpret_cast<uint32_t*>(pred), (size_t)ld, upper ? 1 : 0);
         transpose_kernel<double><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
-            n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
+            n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld, upper ? 1 : 0);
         /* level order for rows whose distances span <= 64 quanta, sweeps for the rest
          * (ws->cursor is free here and carries the per-row hand-over flags) */
         /* 1024 threads per row, one row per CU (128 VGPRs): 12.3 ms on C4 against 13.3 for 512
          * threads at two rows per CU and 13.1 for 1024 at two (64 VGPRs, 4 targets in flight) */
-        if (n <= 32768) {
+        if (upper) {
+            /* + three bitmaps (12 KB) */
+            const int lds = 65536 + 3 * 4096;
+            SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 32768, true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+            rel_levels_kernel<1024, 32768, true><<<lrows, 1024, lds, st>>>(
+                n, ld, row0, d, pred, rel, 64, ws->depth, ws->cursor, ws->predt, ws->rt,
+                (size_t)nrows);
+            const size_t lds2 = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
+            SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+            rel_sweeps_kernel<<<lrows, 512, lds2, st>>>(n, ld, row0, pred, rel, ws->depth, ws->cursor);
+            SRT_HIPCHK(hipGetLastError());
+        } else if (n <= 32768) {
             SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 32768>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
             rel_levels_kernel<1024, 32768><<<lrows, 1024, 65536, st>>>(n, ld, row0, d, pred, rel, 64,
