@@ -267,13 +267,13 @@ def run_dense(c: Ctx, wl):
     #   enc 3: 2 x v_add_u32 + 1 x v_pk_minimum3_f16 per 4 relaxations -> 8/4 = 2.0 cycles
     #   enc 2: 1 x v_add_u32 + 1 x v_pk_min_u16 per 2 relaxations      -> 6/2 = 3.0 cycles
     #   enc 1: 2 x v_add_u32 + 1 x v_min3_u32 per 2 relaxations         -> 8/2 = 4.0 cycles
-    cyc_per_relax = {6: 2.0, 5: 2.0, 4: 2.0, 3: 2.0, 2: 3.0, 1: 4.0}[enc]
-    instr_per_relax = {6: 0.75, 5: 0.75, 4: 0.75, 3: 0.75, 2: 1.0, 1: 1.5}[enc]
+    cyc_per_relax = {7: 2.0, 6: 2.0, 5: 2.0, 4: 2.0, 3: 2.0, 2: 3.0, 1: 4.0}[enc]
+    instr_per_relax = {7: 0.75, 6: 0.75, 5: 0.75, 4: 0.75, 3: 0.75, 2: 1.0, 1: 1.5}[enc]
     # the 8-wave update kernel (fwq_update_kernel) unless SRT_FW_WAVES=4 selects the 4-wave one
     w4 = os.environ.get("SRT_FW_WAVES") == "4"
     uk = "fwh_update_kernel" if w4 else "fwq_update_kernel"
     st2 = "" if w4 else ", 2"  # fwq's third template argument: 32-pivot stages per tile
-    kname = {6: "fwq_update_kernel<true, 4, 4>", 5: f"{uk}<true, 4{st2}>",
+    kname = {7: "fwq_update_kernel<true, 4, 8>", 6: "fwq_update_kernel<true, 4, 4>", 5: f"{uk}<true, 4{st2}>",
              4: f"{uk}<true, 0{st2}>" if world == 1 else f"{uk}<true, 4{st2}>",
              3: f"{uk}<false, 0{st2}>",
              2: "fw16_update_kernel<false>", 1: "fw_update_kernel"}[enc]
@@ -286,7 +286,17 @@ def run_dense(c: Ctx, wl):
     # tile pair) less the next pivot block's tile row and column, which run in their own launch
     tiles = ld // 128
     pivots = FW_B  # pivots applied per element per timed unit
-    if enc == 6:  # one GPU, 128-pivot rounds on two update streams: a timed unit is the pair of
+    if enc == 7:  # one GPU, 256-pivot rounds on two update streams: a timed unit is the pair of
+        # rest launches of a round j, every upper-triangle tile but the crosses of tile rows
+        # 2j + 2 and 2j + 3; of the crosses of 2j and 2j + 1 (which the chain stream updated),
+        # the tiles of 2j + 1's take the last 64-pivot panel, the others of 2j's the last three
+        cross2 = 2 * tiles - 1  # tiles in the crosses of two adjacent tile rows (upper)
+        rest = tiles * (tiles + 1) // 2 - cross2
+        c1 = tiles - 2   # cross of 2j + 1 less the next round's two tiles in it
+        c0 = tiles - 3   # cross of 2j less (2j, 2j + 1) and the next round's two tiles in it
+        elems = float(rest) * 128 * 128
+        pivots = (float(rest - c1 - c0) * 256 + float(c1) * 64 + float(c0) * 192) / rest
+    elif enc == 6:  # one GPU, 128-pivot rounds on two update streams: a timed unit is the pair of
         # rest launches of a round j, every upper-triangle tile but the cross of j + 1; the cross
         # of j (T - 1 tiles of it) takes only the second 64-pivot panel
         rest = tiles * (tiles + 1) // 2 - tiles
@@ -318,7 +328,7 @@ def run_dense(c: Ctx, wl):
         pmc = json.load(open(pmc_path))
         if pmc.get("kernel") == kname:
             traffic = pmc.get("hbm_bytes_per_launch")
-            if enc in (5, 6) and traffic is not None:  # the timed unit is two launches
+            if enc in (5, 6, 7) and traffic is not None:  # the timed unit is two launches
                 traffic = 2.0 * traffic
     lds = None
     if enc >= 3:
@@ -339,8 +349,8 @@ def run_dense(c: Ctx, wl):
         "traffic": traffic, "bytes_per_launch": bytes_per_round,
         "avg_launch_ms": round(avg_upd_ms, 4), "launches_timed": n_upd,
         "model": f"2*elements*{s_d} B per timed unit (SURVEY §8d round-streaming, "
-                 f"{'B=128 (two 64-pivot panels per C-tile residency)' if enc == 6 else 'B=64'}, "
-                 f"{ {6: 'u16 f16-compare, upper triangle on two streams, 128-pivot rounds (unit: both rest launches)', 5: 'u16 f16-compare, upper triangle on two streams (unit: both rest launches)', 4: 'u16 f16-compare, upper triangle', 3: 'u16 f16-compare', 2: 'u16 pk_min', 1: 'u32'}[enc]}"
+                 f"{ {7: 'B=256 (four 64-pivot panels per C-tile residency)', 6: 'B=128 (two 64-pivot panels per C-tile residency)'}.get(enc, 'B=64')}, "
+                 f"{ {7: 'u16 f16-compare, upper triangle on two streams, 256-pivot rounds (unit: both rest launches)', 6: 'u16 f16-compare, upper triangle on two streams, 128-pivot rounds (unit: both rest launches)', 5: 'u16 f16-compare, upper triangle on two streams (unit: both rest launches)', 4: 'u16 f16-compare, upper triangle', 3: 'u16 f16-compare', 2: 'u16 pk_min', 1: 'u32'}[enc]}"
                  f" distances; elements updated per unit = {int(elems)}, "
                  f"pivots per element = {pivots:.2f})",
         "algorithmic_min_bytes": float(nr) * ld * (4 + 8),

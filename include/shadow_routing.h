@@ -79,7 +79,8 @@ typedef struct srt_build_stats {
     double ms_comm;      /* host-observed time of the collective calls (sharded builds) */
     int32_t dist_enc;    /* sparse builds: 2 = workgroup-per-source kernel (LDS-packed rows),
                           * 1 = wave-per-source kernel, 0 = workgroup kernel for every source.
-                          * Dense: the distance encoding the build finished with: 6 = 5 with
+                          * Dense: the distance encoding the build finished with: 7 = 5 with
+                          * 256-pivot rounds (four panels per C-tile residency), 6 = 5 with
                           * 128-pivot rounds (two panels per C-tile residency), 5 = 4 on two
                           * update streams (one GPU, n >= 8192), 4 = u16 with
                           * f16-compare mins, upper-triangle rounds (undirected, one shard),

@@ -1405,6 +1405,7 @@ int srt_dense_build_device_ms(int32_t n, int32_t ld, int32_t directed, const uin
         if (rc) return rc;
         if (exact)
             enc = !fm ? SRT_DENC_U16
+                      : sym == 4 ? SRT_DENC_F16CMP_SYM256
                       : sym == 3 ? SRT_DENC_F16CMP_SYM128
                       : sym == 2 ? SRT_DENC_F16CMP_SYM2
                                  : sym ? SRT_DENC_F16CMP_SYM : SRT_DENC_F16CMP;

@@ -834,17 +834,22 @@ static __device__ __forceinline__ void fwq_stage(uint32_t (&acc)[4][4], const ui
     }
 }
 
-/* NST stages of UKC pivots per C-tile residency: 2 (a 64-pivot round) or 4 (two rounds, the
- * 128-row panel P = P_a over P_b). prev >= 0 (128-pivot rounds): the tiles of tile row / column
- * prev already hold P_a (the chain stream applied it to them before closing P_b) and take P_b only.
- * XM 9: the cross of tile `skip` (tile row and column, upper triangle), every tile. */
+/* NST stages of UKC pivots per C-tile residency: 2 (a 64-pivot round), 4 (the 128-row panel
+ * P = P_a over P_b) or 8 (256 rows, P_a..P_d). prev >= 0: the cross tiles the chain stream updated
+ * while closing the round's later panels start past them -- 128-pivot rounds: the cross of prev
+ * holds P_a; 256-pivot rounds: the cross of prev + 1 holds P_a..P_c, the rest of the cross of prev
+ * holds P_a. (Applying a panel a tile already took is harmless -- min-plus with the same operands
+ * is idempotent -- so the small cross launches do not track it.)
+ * XM 9: the cross of tile `skip` (tile row and column, upper triangle), every tile.
+ * XM 13: the cross of tiles skip and skip + 1 whose I + J has the parity i0 (256-pivot rounds:
+ * the next round's two pivot tile rows). XM 4 with NST 8 leaves out both crosses. */
 template <bool SYM, int XM = 0, int NST = 2>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) void fwq_update_kernel(
     u16* __restrict__ D, int ld, const u16* __restrict__ P, int k0, int ncol_tiles, int i0, int skip,
     const uint32_t* __restrict__ tl, int te, int prev = -1) {
     __shared__ __attribute__((aligned(16))) uint32_t sA[UKC / 2 * 128 * 2];
     __shared__ __attribute__((aligned(16))) u16 sB[UKC * UBS];
-    if constexpr (XM == 3 || XM == 6 || XM == 7 || XM == 8 || XM == 9)
+    if constexpr (XM == 3 || XM == 6 || XM == 7 || XM == 8 || XM == 9 || XM == 13)
         FW_CHAIN_PRIO(); /* next-row tiles */
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     int I, J, Iloc;
@@ -852,11 +857,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         I = min((int)blockIdx.x, skip);
         J = max((int)blockIdx.x, skip);
         Iloc = I;
+    } else if constexpr (XM == 13) {
+        const int b = (int)blockIdx.x, second = b >= ncol_tiles;
+        const int c = second ? b - ncol_tiles : b, k = skip + second;
+        if (second && c == skip) return; /* (skip, skip + 1) is in the first set */
+        I = min(c, k);
+        J = max(c, k);
+        if (((I + J) & 1) != i0) return;
+        Iloc = I;
     } else if (!fw_tile_of<SYM, XM>(ncol_tiles, i0, skip, tl, te, I, J, Iloc)) {
         return;
     }
+    if constexpr (XM == 4 && NST == 8)
+        if (I == skip + 1 || J == skip + 1) return;
     /* wave-uniform first stage */
-    const int s0 = (NST == 4 && prev >= 0 && (I == prev || J == prev)) ? NST / 2 : 0;
+    int s0 = 0;
+    if (NST == 4 && prev >= 0 && (I == prev || J == prev)) s0 = NST / 2;
+    if (NST == 8 && prev >= 0)
+        s0 = (I == prev + 1 || J == prev + 1) ? 6 : (I == prev || J == prev) ? 2 : 0;
     u16* C = D + (size_t)Iloc * 128 * ld + J * 128;
     const u16* Ag = D + (size_t)I * 128 * ld + k0;
     const u16* Bg = P + J * 128;
@@ -1236,7 +1254,8 @@ static int sched_get(fw16_sched** out, int dev) {
  * that the other stream has already relaxed in the next round: those values are still lengths
  * of real paths, no larger than the round requires, so the result is the same exact matrix. */
 static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipStream_t st,
-                          evpool_t* evp, int* exact, bool two, bool r128) {
+                          evpool_t* evp, int* exact, bool two, int round_pivots) {
+    const bool r128 = round_pivots == 128, r256 = round_pivots == 256;
     const int dev = srt_state_slot(); /* the device, or this virtual rank's slot */
     size_t* caps = fw16_caps;
     int** flags = fw16_flags;
@@ -1307,7 +1326,76 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
         SRT_HIPCHK(hipEventRecord(sc->init_done, st));
         SRT_HIPCHK(hipStreamWaitEvent(cs, sc->init_done, 0));
         SRT_HIPCHK(hipStreamWaitEvent(xs, sc->init_done, 0));
-        if (r128) {
+        if (r256) {
+            /* 256-pivot rounds (pivot blocks a..d = 4j..4j+3: tile rows R0 = 2j, R1 = 2j + 1):
+             * every C tile stays resident for four panels (eight 32-pivot stages). Chain stream cs,
+             * per round j: close P_a, apply it to the cross of R0; close P_b, apply P_a and P_b to
+             * the cross of R1; close P_c, apply it to the cross of R1; close P_d -> ready[j].
+             * Update stream p, per round j (after ready[j]): the crosses of the next round's tile
+             * rows with all four panels, then the rest, whose tiles in the crosses of R0 / R1 start
+             * past the panels the chain already applied (fwq_update_kernel prev). */
+            auto closep = [&](int k0) -> int {
+                u16* P = d + (size_t)k0 * ld;
+                fw16_diag_kernel<true><<<1, 256, 0, cs>>>(P, ld, k0);
+                fw16_panel_kernel<true, true><<<2 * nb, 256, 0, cs>>>(d, ld, 0, nb, P, k0, nb, 1, 1);
+                if (k0 > 0) fw16_refresh_kernel<<<k0 / KB, 256, 0, cs>>>(d, ld, k0);
+                SRT_HIPCHK(hipGetLastError());
+                return SRT_OK;
+            };
+            auto produce4 = [&](int j) -> int {
+                const int ka = 4 * j * KB, R0 = 2 * j;
+                int rc2;
+                if ((rc2 = closep(ka))) return rc2;
+                fwq_update_kernel<true, 9, 2><<<T, 512, 0, cs>>>(d, ld, d + (size_t)ka * ld, ka, T, 0,
+                                                               R0, nullptr, 0, -1);
+                if ((rc2 = closep(ka + KB))) return rc2;
+                fwq_update_kernel<true, 9, 4><<<T, 512, 0, cs>>>(d, ld, d + (size_t)ka * ld, ka, T, 0,
+                                                               R0 + 1, nullptr, 0, -1);
+                if ((rc2 = closep(ka + 2 * KB))) return rc2;
+                fwq_update_kernel<true, 9, 2><<<T, 512, 0, cs>>>(
+                    d, ld, d + (size_t)(ka + 2 * KB) * ld, ka + 2 * KB, T, 0, R0 + 1, nullptr, 0, -1);
+                if ((rc2 = closep(ka + 3 * KB))) return rc2;
+                SRT_HIPCHK(hipGetLastError());
+                SRT_HIPCHK(hipEventRecord(sc->ready[j & 1], cs));
+                return SRT_OK;
+            };
+            const int R = T / 2;
+            if ((rc = produce4(0))) return rc;
+            for (int j = 0; j < R; ++j) {
+                const int ka = 4 * j * KB;
+                u16* Pa = d + (size_t)ka * ld;
+                const bool next = j + 1 < R;
+                for (int p = 0; p < 2; p++) {
+                    SRT_HIPCHK(hipStreamWaitEvent(ss[p], sc->ready[j & 1], 0));
+                    if (next) {
+                        fwq_update_kernel<true, 13, 8><<<2 * T, 512, 0, ss[p]>>>(
+                            d, ld, Pa, ka, T, p, 2 * j + 2, nullptr, 0, -1);
+                        SRT_HIPCHK(hipEventRecord(sc->e_set[j & 1][p], ss[p]));
+                    }
+                }
+                if (next) {
+                    SRT_HIPCHK(hipStreamWaitEvent(cs, sc->e_set[j & 1][0], 0));
+                    SRT_HIPCHK(hipStreamWaitEvent(cs, sc->e_set[j & 1][1], 0));
+                    if ((rc = produce4(j + 1))) return rc;
+                }
+                const int e0 = evp ? evp->used : 0;
+                if (evp && next) {
+                    evp->group = 4;
+                    evp->used += 4;
+                }
+                for (int p = 0; p < 2; p++) {
+                    if (evp && next) SRT_HIPCHK(hipEventRecord(evp->ev[e0 + p], ss[p]));
+                    if (next)
+                        fwq_update_kernel<true, 4, 8><<<(unsigned)nset[p], 512, 0, ss[p]>>>(
+                            d, ld, Pa, ka, T, 0, 2 * j + 2, tls[p], T, 2 * j);
+                    else
+                        fwq_update_kernel<true, 5, 8><<<(unsigned)nset[p], 512, 0, ss[p]>>>(
+                            d, ld, Pa, ka, T, 0, -1, tls[p], T, 2 * j);
+                    if (evp && next) SRT_HIPCHK(hipEventRecord(evp->ev[e0 + 2 + p], ss[p]));
+                }
+                SRT_HIPCHK(hipGetLastError());
+            }
+        } else if (r128) {
             /* 128-pivot rounds (pivot blocks a = 2j, b = 2j + 1: tile row j): every C tile stays
              * resident for both panels (four 32-pivot stages), which halves the per-pivot C loads,
              * row sums and stores and the bulk launches. Chain stream cs, per round j:
@@ -1798,9 +1886,11 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
          * per build on one box (before that loop change the two measured the same, 380.5 vs
          * 380.1 ms) */
         const char* kb_env = getenv("SRT_FW_KB");
-        const bool r128 = two && fw_waves8() && ld >= 256 && !(kb_env && atoi(kb_env) == 64);
-        *sym = r128 ? 3 : two ? 2 : 1;
-        return fw16_build_sym(n, ld, w_rows, lat_rows, st, evp, exact, two, r128);
+        const int kbw = kb_env ? atoi(kb_env) : 256;
+        const bool big = two && fw_waves8();
+        const int rp = big && kbw >= 256 && ld % 256 == 0 ? 256 : big && kbw >= 128 && ld >= 256 ? 128 : 64;
+        *sym = rp == 256 ? 4 : rp == 128 ? 3 : two ? 2 : 1;
+        return fw16_build_sym(n, ld, w_rows, lat_rows, st, evp, exact, two, rp);
     }
     hipStream_t cs = lookahead ? sc->cs : st;
     u16* d = bufs[dev];

@@ -145,7 +145,8 @@ enum {
     SRT_DENC_F16CMP = 3,
     SRT_DENC_F16CMP_SYM = 4,
     SRT_DENC_F16CMP_SYM2 = 5, /* one GPU, upper triangle on two update streams */
-    SRT_DENC_F16CMP_SYM128 = 6 /* 5 with 128-pivot rounds (8-wave update, 4 stages per tile) */
+    SRT_DENC_F16CMP_SYM128 = 6, /* 5 with 128-pivot rounds (8-wave update, 4 stages per tile) */
+    SRT_DENC_F16CMP_SYM256 = 7  /* 5 with 256-pivot rounds (8 stages per tile) */
 };
 
 int srt_dense_post_device(int32_t n, int32_t ld, int32_t directed, const uint32_t* w,

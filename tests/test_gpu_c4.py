@@ -1,5 +1,5 @@
 """C4 at full size in -m gpu: the 32,768-node complete graph through the default one-GPU schedule
-(encoding 6: u16 f16-compare upper-triangle 128-pivot rounds on two update streams, the 8-wave
+(encoding 7: u16 f16-compare upper-triangle 256-pivot rounds on two update streams, the 8-wave
 update kernel, XCD-remapped grid, u8
 predecessor slab, rel_levels_kernel<1024>), against the CPU oracle's dense Dijkstra
 (oracle.complete_sample) on rows spread over every 4k block, including the last tile row.
@@ -37,7 +37,7 @@ def test_c4_full_size_default_schedule(gpu):
                                         rel.data_ptr(), None, 0, ctypes.byref(st)), "C4 build")
     torch.cuda.synchronize()
     del w, r
-    assert st.dist_enc == 6, "the default one-GPU schedule (two update streams, 128-pivot rounds)"
+    assert st.dist_enc == 7, "the default one-GPU schedule (two update streams, 256-pivot rounds)"
     # 4 rows in each 4k block (first, middle, two in its last 128-row tile) + the last tile row
     rows = sorted({b + o for b in range(0, n, 4096) for o in (0, 2049, 4096 - 128, 4095)}
                   | {32640, 32700, 32767})

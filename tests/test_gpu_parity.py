@@ -189,7 +189,8 @@ def test_dense_device_api_and_sharded_single_rank(gpu):
 
 
 @pytest.mark.parametrize("hop_ms,enc,sym,la,env", [
-    (1, 4, "1", None, {}), (1, 6, "1", "1", {}), (1, 5, "1", "1", {"SRT_FW_KB": "64"}),
+    (1, 4, "1", None, {}), (1, 7, "1", "1", {}), (1, 6, "1", "1", {"SRT_FW_KB": "128"}),
+    (1, 5, "1", "1", {"SRT_FW_KB": "64"}),
     (1, 5, "1", "1", {"SRT_FW_WAVES": "4"}), (1, 4, "1", None, {"SRT_FW_WAVES": "4"}),
     (1, 3, "0", None, {}), (1, 3, "0", None, {"SRT_FW_WAVES": "4"}),
     (160, 2, "1", None, {}), (400, 1, "1", None, {})])
@@ -202,8 +203,9 @@ def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym, la, e
     saturates both and ends on the u32 kernels. Every tier must match the oracle bit for bit.
     The graph is undirected, so the f16-compare tier runs its upper-triangle form (encoding 4)
     unless SRT_FW_SYM=0 forces every tile (encoding 3); SRT_FW_LOOKAHEAD=1 forces its two
-    update streams, with 128-pivot rounds (encoding 6, the default from n = 8192) or 64-pivot
-    rounds under SRT_FW_KB=64 (encoding 5). SRT_FW_WAVES=4 selects the 4-wave update kernel
+    update streams, with 256-pivot rounds (encoding 7, the default from n = 8192), 128-pivot
+    rounds under SRT_FW_KB=128 (encoding 6) or 64-pivot rounds under SRT_FW_KB=64 (encoding 5).
+    SRT_FW_WAVES=4 selects the 4-wave update kernel
     (fwh_update_kernel) over the 8-wave one (fwq_update_kernel).
     """
     monkeypatch.setenv("SRT_FW_SYM", sym)
@@ -229,6 +231,33 @@ def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym, la, e
     exp = _oracle(g)
     assert_tables(got_lat, got_rel, exp["lat_int"], exp["rel"], f"hop {hop_ms} ms")
     assert st.dist_enc == enc, f"expected encoding {enc}, build used {st.dist_enc}"
+
+
+@pytest.mark.parametrize("n,kb", [(1000, "256"), (1000, "128"), (1536, "256")])
+def test_dense_round_sizes_multi_round(gpu, monkeypatch, n, kb):
+    """The two-stream schedules with several 256- / 128-pivot rounds (the encoding-tier test has
+    one or two): a ring with chords, long enough for distances of a few hundred quanta, against
+    the oracle bit for bit. Covers the chain stream's cross updates between a round's panels and
+    the rest launches that start past them."""
+    monkeypatch.setenv("SRT_FW_LOOKAHEAD", "1")
+    monkeypatch.setenv("SRT_FW_KB", kb)
+    rng = np.random.default_rng(n)
+    src = list(range(n))
+    dst = [(i + 1) % n for i in range(n)]
+    lat = [(1 + (i % 3)) * MS for i in range(n)]
+    for _ in range(40):
+        a, b = (int(x) for x in rng.choice(n, 2, replace=False))
+        src.append(a)
+        dst.append(b)
+        lat.append(int(rng.integers(5, 60)) * MS)
+    loss = rng.integers(0, 100, len(src)) * 1e-4
+    g = graphs.Graph(n, 0, np.array(src, np.int32), np.array(dst, np.int32),
+                     np.array(lat, np.int64), loss)
+    got_lat, got_rel, st = build_tables(g.n, False, g.src, g.dst, g.lat_ns, g.loss,
+                                        algo=ALGO_DENSE_FW)
+    assert st.dist_enc == (7 if kb == "256" else 6)
+    exp = _oracle(g)
+    assert_tables(got_lat, got_rel, exp["lat_int"], exp["rel"], f"rounds of {kb}, n={n}")
 
 
 @pytest.mark.parametrize("n,seed", [(700, 8), (1000, 2)])

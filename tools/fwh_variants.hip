@@ -732,6 +732,11 @@ int main(int argc, char** argv) {
     if (only && !strcmp(only, "qd")) {
         report("qs8w (fwq SYM image) full", 64, el, [&] { return runqd<2, true, true, false>(D, ld, sink, rounds); });
         report("qs8w compute-only", 64, el, [&] { return runqd<2, false, false, false>(D, ld, sink, rounds); });
+        report("qs8w NST=4 full", 128, el, [&] { return runqd<4, true, true, false>(D, ld, sink, rounds); });
+        report("qs8w NST=4 no-io", 128, el, [&] { return runqd<4, false, true, false>(D, ld, sink, rounds); });
+        report("qs8w NST=4 no-stage", 128, el, [&] { return runqd<4, true, false, false>(D, ld, sink, rounds); });
+        report("qs8w NST=4 compute-only", 128, el, [&] { return runqd<4, false, false, false>(D, ld, sink, rounds); });
+        report("qs8w NST=8 full", 256, el, [&] { return runqd<8, true, true, false>(D, ld, sink, rounds); });
         report("qd8w DPP full", 64, el, [&] { return runqd<2, true, true, true>(D, ld, sink, rounds); });
         report("qd8w DPP no-io", 64, el, [&] { return runqd<2, false, true, true>(D, ld, sink, rounds); });
         report("qd8w DPP compute-only", 64, el, [&] { return runqd<2, false, false, true>(D, ld, sink, rounds); });
