@@ -473,7 +473,8 @@ __global__ void wg_arcs_cmp_kernel(int n, const int2* __restrict__ rowptr, const
 }
 
 /* PROF (tools only, SRT_WGSSSP_PROF=1): thread 0 accumulates shader-clock cycles per phase and
- * step counts into prof[block * 10 + k]: 0 init, 1 bucket search, 2 chunk head, 3 arcs,
+ * step counts into prof[block * 12 + k]: 0 init, 1 bucket search, 2 chunk head (sums and the
+ * full barrier; 10 entry load, 11 scan barrier), 3 arcs,
  * 4 settle, 5 output, 6 steps, 7 chunks, 8 arc windows, 9 sources */
 #define WG_PT(k)                                                        \
     do {                                                                \
@@ -498,7 +499,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
     static_assert(!CMP || ORIG, "compact arcs key ties on u: original vertex order only");
     const uint4* __restrict__ ca = reinterpret_cast<const uint4*>(cav);
     const uint2* __restrict__ cc = reinterpret_cast<const uint2*>(cav);
-    unsigned long long pacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long pacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long pt = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     extern __shared__ uint32_t sd[]; /* packed distances, relabelled order */
     __shared__ uint32_t bcnt[256]; /* entries per bucket; the search ballots on bcnt > 0 */
@@ -589,11 +590,13 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                         v = -1; /* stale: improved after it was pushed */
                     }
                 }
+                WG_PT(10);
                 /* workgroup exclusive scan of the degrees */
                 int wtot;
                 const int wex = wave_scan_excl(deg, lane, &wtot);
                 if (lane == 0) s_wtot[wv] = wtot;
                 WG_LDS_BARRIER();
+                WG_PT(11);
                 int base = 0, total = 0;
                 for (int q = 0; q < WG / WL; ++q) {
                     base += q < wv ? s_wtot[q] : 0;
@@ -722,7 +725,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
         WG_PT(5);
     }
     if (PROF && tid == 0)
-        for (int k = 0; k < 10; ++k) prof[blockIdx.x * 10 + k] = pacc[k];
+        for (int k = 0; k < 12; ++k) prof[blockIdx.x * 12 + k] = pacc[k];
 }
 
 /* largest n the packed LDS row holds beside the kernel's static LDS (1024 threads: ~18 KB) */
@@ -787,7 +790,7 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     const char* penv = getenv("SRT_WGSSSP_PROF"); /* tools: per-phase cycle counts on stderr */
     if (penv && atoi(penv) > 0) {
         unsigned long long* prof = NULL;
-        SRT_HIPCHK(hipMalloc((void**)&prof, slots * 10 * sizeof(unsigned long long)));
+        SRT_HIPCHK(hipMalloc((void**)&prof, slots * 12 * sizeof(unsigned long long)));
         if (cmp) {
             SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true, true, true>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
@@ -802,18 +805,20 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
                 ovf, prof);
         }
         SRT_HIPCHK(hipGetLastError());
-        unsigned long long* h = (unsigned long long*)calloc(slots * 10, sizeof(*h));
-        SRT_HIPCHK(hipMemcpyAsync(h, prof, slots * 10 * sizeof(*h), hipMemcpyDeviceToHost, st));
+        unsigned long long* h = (unsigned long long*)calloc(slots * 12, sizeof(*h));
+        SRT_HIPCHK(hipMemcpyAsync(h, prof, slots * 12 * sizeof(*h), hipMemcpyDeviceToHost, st));
         SRT_HIPCHK(hipStreamSynchronize(st));
-        double tot[10] = {0};
+        double tot[12] = {0};
         for (size_t b = 0; b < slots; ++b)
-            for (int k = 0; k < 10; ++k) tot[k] += (double)h[b * 10 + k];
-        const double cyc = tot[0] + tot[1] + tot[2] + tot[3] + tot[4] + tot[5];
+            for (int k = 0; k < 12; ++k) tot[k] += (double)h[b * 12 + k];
+        const double cyc = tot[0] + tot[1] + tot[2] + tot[3] + tot[4] + tot[5] + tot[10] + tot[11];
         fprintf(stderr,
                 "[wgsssp prof] blocks %zu sources %.0f: cycles/source %.0f = init %.1f%% search "
-                "%.1f%% head %.1f%% arcs %.1f%% settle %.1f%% output %.1f%%; per source: steps "
+                "%.1f%% head %.1f%% (entry load %.1f%%, scan barrier %.1f%%, sums + full "
+                "barrier %.1f%%) arcs %.1f%% settle %.1f%% output %.1f%%; per source: steps "
                 "%.1f chunks %.1f arc windows %.1f; cycles per step %.0f\n",
                 slots, tot[9], cyc / tot[9], 100 * tot[0] / cyc, 100 * tot[1] / cyc,
+                100 * (tot[2] + tot[10] + tot[11]) / cyc, 100 * tot[10] / cyc, 100 * tot[11] / cyc,
                 100 * tot[2] / cyc, 100 * tot[3] / cyc, 100 * tot[4] / cyc, 100 * tot[5] / cyc,
                 tot[6] / tot[9], tot[7] / tot[9], tot[8] / tot[9], cyc / tot[6]);
         free(h);
