@@ -536,10 +536,11 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
         __syncthreads();
         WG_PT(0);
         if (PROF && tid == 0) pacc[9]++;
-        /* deferred settle: the reliability of the lane's last settled vertex pv is stored at the
-         * next chunk's head (or after the last step), so its two loads overlap the bucket search
-         * and the next entry load; nothing reads rel(s, pv) before a larger distance value is
-         * settled, and that chunk's head barrier orders the store before it */
+        /* deferred settle: the reliability of the lane's last settled vertex pv is stored after
+         * the next chunk's arcs (or after the last step), so its two loads overlap the bucket
+         * search, the next entry load and the arcs; nothing reads rel(s, pv) before a larger
+         * distance value is settled -- a later step, whose first chunk's post-arcs barrier is a
+         * full one that orders the store before that chunk's settle loads */
         int pv = -1;
         double pa = 0.0, pb = 0.0;
         uint32_t d = 0;
@@ -573,10 +574,6 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                 int v = -1, beg = 0, deg = 0;
                 uint2 en = make_uint2(0u, 0u);
                 if (i < cnt) en = ld_coherent2(bk + i);
-                if (pv >= 0) { /* the lane's vertex of the previous chunk */
-                    relp[pv] = pa * pb;
-                    pv = -1;
-                }
                 if (i < cnt) {
                     v = (int)(en.x & 0x1FFFFu);
                     if (wg_get(sd, (uint32_t)v) == d) {
@@ -605,10 +602,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                 s_beg[tid] = beg;
                 s_excl[tid] = base + wex;
                 s_best[tid] = ~0ull;
-                if (c0 == 0) /* full: the previous step's deferred reliability stores */
-                    __syncthreads();
-                else
-                    WG_LDS_BARRIER();
+                WG_LDS_BARRIER();
                 WG_PT(2);
                 /* WG_AK arc windows per pass: the owner searches (fixed-step, unrolled) and the
                  * arc loads of every window are issued before any of them is used, so their
@@ -680,7 +674,19 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                         }
                     }
                 }
-                WG_LDS_BARRIER(); /* the bucket stores drain by the next step's search barrier */
+                /* the lane's vertex of the previous chunk: its two loads (issued at that chunk's
+                 * settle) have had this chunk's head and arcs to arrive */
+                if (pv >= 0) {
+                    relp[pv] = pa * pb;
+                    pv = -1;
+                }
+                /* a step's first chunk may settle children of the previous chunk's vertices: full
+                 * barrier (their reliability stores, and this pass's bucket stores, visible);
+                 * otherwise the bucket stores drain by the next step's search barrier */
+                if (c0 == 0)
+                    __syncthreads();
+                else
+                    WG_LDS_BARRIER();
                 WG_PT(3);
                 /* settle: path-order reliability from the canonical predecessor, issued now and
                  * stored one chunk later */
