@@ -1157,9 +1157,10 @@ extern "C" int srt_build_tables_subset(const srt_edges* g, const srt_build_opts*
     *quantum_ns = c.quantum_ns;
     const int use_sp = opts ? opts->use_shortest_path : 1;
     const int algo = use_sp ? choose_algo(&c, opts) : SRT_ALGO_DENSE_FW;
-    /* SRT_VIRTUAL_RANKS=R (tests): R ranks on device 0, collectives as device copies */
+    /* SRT_VIRTUAL_RANKS=R (tests): R ranks on device 0, collectives as device copies, whatever
+     * ngpus says (srt_build_tables_multi hands ngpus = 1 down here when it is set) */
     const char* venv = getenv("SRT_VIRTUAL_RANKS");
-    const int virt = ngpus > 1 && venv && atoi(venv) > 0 ? (atoi(venv) < 64 ? atoi(venv) : 64) : 0;
+    const int virt = venv && atoi(venv) > 0 ? (atoi(venv) < 64 ? atoi(venv) : 64) : 0;
     const int R = virt ? virt : (ngpus < avail ? ngpus : avail);
     uint32_t mq = 0xFFFFFFFFu;
     if (R > 1 && use_sp)

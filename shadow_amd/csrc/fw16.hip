@@ -1135,6 +1135,73 @@ __global__ __launch_bounds__(256) void sym_panel_stage_kernel(u16* __restrict__ 
     }
 }
 
+/* 128-pivot sharded rounds: the staged blocks of rows b (the second 64-row half of pivot tile row
+ * K, 64 x 128 per tile column J, in the staging order) take pivot block a before P_b is closed:
+ * X[J] = min(X[J], X_K[:, 0:64] (x) P_a[:, J]), where X_K[:, 0:64] = D[b][a] is the staged block of
+ * tile column K and P_a the closed row panel a. The workgroup of J = K rewrites the D[b][a] the
+ * others read: either value is a valid operand (P_a is closed, so old and updated D[b][a] give the
+ * same minimum), as in blocked FW's column-panel/rest split. */
+__global__ __launch_bounds__(256) void sym_cross_stage_kernel(const u16* __restrict__ Pa, int ld, int K,
+                                                              int T, const int* __restrict__ own,
+                                                              u16* __restrict__ stage) {
+    __shared__ __attribute__((aligned(16))) u16 s[KB * LDA16];     /* D[b][a] */
+    __shared__ __attribute__((aligned(16))) u16 x[KB * (128 + 8)]; /* P_a[:, J] */
+    __shared__ int s_own[SYM_TMAX], s_cnt;
+    FW_CHAIN_PRIO();
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int J = (int)blockIdx.x;
+    const u16* ak = stage + (size_t)sym_stage_pos(K, K, T, own, s_own, &s_cnt) * (KB * 128);
+    __syncthreads(); /* s_cnt is reused by the second position */
+    u16* xj = stage + (size_t)sym_stage_pos(K, J, T, own, s_own, &s_cnt) * (KB * 128);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int i = tid + q * 256, row = i >> 3, c8 = (i & 7) * 8;
+        *reinterpret_cast<uint4*>(s + row * LDA16 + c8) =
+            *reinterpret_cast<const uint4*>(ak + row * 128 + c8);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int i = tid + q * 256, row = i >> 4, c8 = (i & 15) * 8;
+        *reinterpret_cast<uint4*>(x + row * (128 + 8) + c8) =
+            *reinterpret_cast<const uint4*>(Pa + (size_t)row * ld + (size_t)J * 128 + c8);
+    }
+    uint32_t acc[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint4 v = *reinterpret_cast<const uint4*>(xj + (4 * ty + r) * 128 + 8 * tx);
+        acc[r][0] = v.x;
+        acc[r][1] = v.y;
+        acc[r][2] = v.z;
+        acc[r][3] = v.w;
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int m = 0; m < KB; m += 4) {
+        uint2 a[4];
+        uint4 b[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a[r] = *reinterpret_cast<const uint2*>(s + (4 * ty + r) * LDA16 + m);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b[q] = *reinterpret_cast<const uint4*>(x + (m + q) * (128 + 8) + 8 * tx);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t p[4] = {splat(a[r].x & 0xFFFFu), splat(a[r].x >> 16),
+                                   splat(a[r].y & 0xFFFFu), splat(a[r].y >> 16)};
+#pragma unroll
+            for (int q = 0; q < 4; q += 2) {
+                const uint32_t b0[4] = {b[q].x, b[q].y, b[q].z, b[q].w};
+                const uint32_t b1[4] = {b[q + 1].x, b[q + 1].y, b[q + 1].z, b[q + 1].w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) acc[r][c] = relax2h(acc[r][c], p[q], b0[c], p[q + 1], b1[c]);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        *reinterpret_cast<uint4*>(xj + (4 * ty + r) * 128 + 8 * tx) =
+            make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+}
+
 /* final fill: kept tile (I, J) of the sender, transposed into a contiguous 128 x 128 block */
 __global__ __launch_bounds__(256) void sym_fill_pack_kernel(const u16* __restrict__ D, int ld, int tb,
                                                             const uint32_t* __restrict__ pairs,
@@ -1205,6 +1272,7 @@ static size_t fw16_caps[SRT_STATE_SLOTS]; /* elements allocated in fw16_bufs (sh
 static int* fw16_flags[SRT_STATE_SLOTS];
 static int fw16_small[SRT_STATE_SLOTS]; /* last build: every real distance <= 254 quanta */
 int srt_fw16_small(void) { return fw16_small[srt_state_slot()]; }
+static thread_local int g_sharded_rp = 64; /* pivots per round of this thread's last sharded build */
 const uint16_t* srt_fw16_matrix(void) { return fw16_bufs[srt_state_slot()]; }
 
 typedef struct {
@@ -1527,14 +1595,17 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
  * transposes of the tiles it does not keep (point-to-point) and fills them in locally. */
 static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0, int nrows,
                                   const uint32_t* w_rows, uint32_t* lat_rows, hipStream_t st,
-                                  evpool_t* evp, int* exact) {
+                                  evpool_t* evp, int* exact, int kbr) {
     const int dev = srt_state_slot();
     const int R = srt_comm_size(comm), me = srt_comm_rank(comm);
-    const int T = ld / 128, nb = ld / KB;
+    /* kbr = 128: 128-pivot rounds (pivot block = tile row K, panels P_a over P_b, four 32-pivot
+     * stages per C-tile residency); kbr = 64: 64-pivot rounds */
+    const bool r128 = kbr == 128;
+    const int T = ld / 128, nb = ld / kbr;
     const int tb = row0 / 128, te = (row0 + nrows) / 128;
     size_t* caps = fw16_caps;
     int** flags = fw16_flags;
-    const size_t need = (size_t)nrows * ld + 2 * (size_t)KB * ld;
+    const size_t need = (size_t)nrows * ld + 2 * (size_t)kbr * ld;
     if (caps[dev] < need || !fw16_bufs[dev]) {
         if (fw16_bufs[dev]) SRT_HIPCHK(hipFree(fw16_bufs[dev]));
         fw16_bufs[dev] = NULL;
@@ -1548,7 +1619,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
     if (rc) return rc;
     hipStream_t cs = sc->cs;
     u16* d = fw16_bufs[dev];
-    u16* pbuf[2] = {d + (size_t)nrows * ld, d + (size_t)nrows * ld + (size_t)KB * ld};
+    u16* pbuf[2] = {d + (size_t)nrows * ld, d + (size_t)nrows * ld + (size_t)kbr * ld};
     /* tile-row ranges of every rank, the owner of each tile row, this rank's kept tiles */
     int* qtb = (int*)malloc((size_t)R * sizeof(int));
     int* qte = (int*)malloc((size_t)R * sizeof(int));
@@ -1581,12 +1652,13 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
     /* device scratch: kept-tile list, gather send (this rank's rows) and receive (a panel) */
     uint32_t* tl = NULL;
     int* down = NULL; /* owner of each tile row, on the device */
-    u16* grecv = NULL; /* staged panel blocks in (contributor, J) order */
+    u16* grecv = NULL; /* staged panel blocks in (contributor, J) order (r128: rows a, then b) */
     int* cnt = (int*)calloc((size_t)R, sizeof(int));
     const size_t blk = (size_t)KB * 128;
+    const size_t nstage = (size_t)(kbr / KB) * ((size_t)T + 1) * blk;
     bool ok = cnt && hipMalloc(&tl, (nkept + 1) * sizeof(uint32_t)) == hipSuccess &&
               hipMalloc(&down, (size_t)T * sizeof(int)) == hipSuccess &&
-              hipMalloc(&grecv, ((size_t)T + 1) * blk * sizeof(u16)) == hipSuccess;
+              hipMalloc(&grecv, nstage * sizeof(u16)) == hipSuccess;
     if (ok)
         ok = hipMemcpyAsync(down, own, (size_t)T * sizeof(int), hipMemcpyHostToDevice, st) ==
                  hipSuccess &&
@@ -1594,7 +1666,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
     /* timing-only communicator: the blocks other ranks would send stay a small constant, so the
      * arithmetic keeps the u16 tier and the u8 post pass (the tables are not correct) */
     if (ok && srt_comm_is_solo(comm))
-        ok = hipMemsetD16Async((hipDeviceptr_t)grecv, 3, ((size_t)T + 1) * blk, st) == hipSuccess;
+        ok = hipMemsetD16Async((hipDeviceptr_t)grecv, 3, nstage, st) == hipSuccess;
     void** sp = (void**)calloc((size_t)R, sizeof(void*));
     void** rp = (void**)calloc((size_t)R, sizeof(void*));
     size_t* sbytes = (size_t*)calloc((size_t)R, sizeof(size_t));
@@ -1660,7 +1732,47 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
             SRT_HIPCHK(hipEventRecord(sc->ready[k & 1], cs));
             return SRT_OK;
         };
-        if ((rc = produce(0))) goto out;
+        /* 128-pivot rounds: the band of tile row K (rows a, then b) is staged and broadcast as
+         * two half-panels; every rank closes P_a, applies it to the staged b rows
+         * (sym_cross_stage_kernel), then closes P_b -- P = P_a over P_b, 128 x ld */
+        auto produce128 = [&](int k) -> int {
+            const int k0 = k * 128, K = k, o = own[K];
+            u16* P = pbuf[k & 1];
+            u16* sa = grecv;
+            u16* sb = grecv + ((size_t)T + 1) * blk;
+            for (int q = 0; q < R; q++) cnt[q] = 0;
+            for (int J = 0; J < T; J++) cnt[sym_kept(K, J) ? o : own[J]]++;
+            if (cnt[me]) {
+                sym_contrib_pack_kernel<<<T, 256, 0, cs>>>(d, ld, row0, tb, K, k0, T, down, me, sa);
+                sym_contrib_pack_kernel<<<T, 256, 0, cs>>>(d, ld, row0, tb, K, k0 + KB, T, down, me,
+                                                           sb);
+            }
+            SRT_HIPCHK(hipGetLastError());
+            int r = srt_coll_group_begin(comm);
+            size_t off = 0;
+            for (int q = 0; q < R && !r; q++) {
+                if (cnt[q]) {
+                    const size_t bytes = (size_t)cnt[q] * blk * sizeof(u16);
+                    r = srt_coll_bcast(comm, sa + off * blk, bytes, q, cs);
+                    if (!r) r = srt_coll_bcast(comm, sb + off * blk, bytes, q, cs);
+                }
+                off += (size_t)cnt[q];
+            }
+            const int r2 = srt_coll_group_end(comm);
+            if (r || r2) return r ? r : r2;
+            u16* prow_a = me == o ? d + (size_t)(k0 - row0) * ld : nullptr;
+            u16* prow_b = me == o ? prow_a + (size_t)KB * ld : nullptr;
+            u16* Pb = P + (size_t)KB * ld;
+            sym_diag_stage_kernel<<<1, 256, 0, cs>>>(P, ld, K, k0, T, down, sa, prow_a);
+            sym_panel_stage_kernel<<<T, 256, 0, cs>>>(P, ld, K, k0, T, down, sa, prow_a);
+            sym_cross_stage_kernel<<<T, 256, 0, cs>>>(P, ld, K, T, down, sb);
+            sym_diag_stage_kernel<<<1, 256, 0, cs>>>(Pb, ld, K, k0 + KB, T, down, sb, prow_b);
+            sym_panel_stage_kernel<<<T, 256, 0, cs>>>(Pb, ld, K, k0 + KB, T, down, sb, prow_b);
+            SRT_HIPCHK(hipGetLastError());
+            SRT_HIPCHK(hipEventRecord(sc->ready[k & 1], cs));
+            return SRT_OK;
+        };
+        if ((rc = r128 ? produce128(0) : produce(0))) goto out;
         /* two update streams (st: even J, xs: odd J), as on one GPU (fw16_build_sym): each
          * depends on its own launches and the panel, so their rounds overlap */
         hipStream_t ss[2] = {st, sc->xs};
@@ -1672,14 +1784,21 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
          * run at raised wave priority wherever they land (FW_CHAIN_PRIO). */
         int timed = 0; /* rounds timed as one unit: the first start and the last end (evpool) */
         for (int k = 0; k < nb; ++k) {
-            const int k0 = k * KB;
+            const int k0 = k * kbr;
             u16* P = panel_of(k);
             const bool next = k + 1 < nb;
-            const int K1 = next ? (k + 1) * KB / 128 : -1;
+            const int K1 = next ? (k + 1) * kbr / 128 : -1;
             for (int p = 0; p < 2; p++) {
                 SYM_HIP(hipStreamWaitEvent(ss[p], sc->ready[k & 1], 0));
                 if (!next) continue;
-                if (p == 0)
+                if (r128) {
+                    if (p == 0)
+                        fwq_update_kernel<true, 7, 4><<<T + (te - tb), 512, 0, ss[p]>>>(
+                            d, ld, P, k0, T, tb, K1, nullptr, te);
+                    else
+                        fwq_update_kernel<true, 8, 4><<<T + (te - tb), 512, 0, ss[p]>>>(
+                            d, ld, P, k0, T, tb, K1, nullptr, te);
+                } else if (p == 0)
                     FW_UPDATE(true, 7, T + (te - tb), ss[p], d, ld, P, k0, T, tb,
                                                                                  K1, nullptr, te);
                 else
@@ -1696,7 +1815,14 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
             }
             for (int p = 0; p < 2; p++) {
                 if (t_first) SYM_HIP(hipEventRecord(evp->ev[p], ss[p]));
-                if (nset[p]) {
+                if (nset[p] && r128) {
+                    if (next)
+                        fwq_update_kernel<true, 4, 4><<<(unsigned)nset[p], 512, 0, ss[p]>>>(
+                            d, ld, P, k0, T, tb, K1, tls[p], te);
+                    else
+                        fwq_update_kernel<true, 5, 4><<<(unsigned)nset[p], 512, 0, ss[p]>>>(
+                            d, ld, P, k0, T, tb, -1, tls[p], te);
+                } else if (nset[p]) {
                     if (next)
                         FW_UPDATE(true, 4, (unsigned)nset[p], ss[p],
                             d, ld, P, k0, T, tb, K1, tls[p], te);
@@ -1710,7 +1836,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
             if (next) {
                 SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[k & 1][0], 0));
                 SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[k & 1][1], 0));
-                if ((rc = produce(k + 1))) goto out;
+                if ((rc = r128 ? produce128(k + 1) : produce(k + 1))) goto out;
             }
         }
         SYM_HIP(hipEventRecord(sc->xs_done[0], sc->xs));
@@ -1846,8 +1972,13 @@ int srt_fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0, in
                       "most %d tile columns", SYM_TMAX);
         return SRT_E_ARG;
     }
-    return fw16_build_sym_sharded(comm, n, ld, row0, nrows, w_rows, lat_rows, st, evp, exact);
+    /* 128-pivot rounds with the 8-wave update unless SRT_FW_SH_KB=64 */
+    const char* kb_env = getenv("SRT_FW_SH_KB");
+    const int rp = (kb_env && atoi(kb_env) == 64) || !fw_waves8() ? 64 : 128;
+    g_sharded_rp = rp;
+    return fw16_build_sym_sharded(comm, n, ld, row0, nrows, w_rows, lat_rows, st, evp, exact, rp);
 }
+int srt_fw16_sharded_round_pivots(void) { return g_sharded_rp; }
 
 int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,
                    hipStream_t st, evpool_t* evp, srt_owner_fn owner_of, srt_panel_bcast_fn bcast,

@@ -352,7 +352,8 @@ def test_virtual_ranks_sharded_build(gpu, monkeypatch, kind, ranks):
     N-rank paths -- shard partition, owners, lookahead order, offsets of every exchange -- is
     the code the RCCL runs use; the tables must equal the oracle's. Undirected graphs on the
     f16-compare tier take the row-sharded symmetric rounds (kept-tile checkerboard, pivot-row
-    gather, final transpose fill: encoding 4)."""
+    gather, final transpose fill) in 128-pivot rounds (encoding 8: the band of tile row K staged
+    as two half-panels, P_a closed and applied to the b rows, then P_b closed)."""
     monkeypatch.setenv("SRT_VIRTUAL_RANKS", str(ranks))
     algo = ALGO_DENSE_FW
     if kind == "dense":
@@ -381,10 +382,29 @@ def test_virtual_ranks_sharded_build(gpu, monkeypatch, kind, ranks):
                                 ngpus=1)
     exp = _oracle(g)
     assert_tables(lat, rel, exp["lat_int"], exp["rel"], f"virtual x{ranks} {kind}")
-    want_enc = {"dense": 4, "dense2000": 4, "ring_f16": 4, "directed": 3, "ring_u16": 2,
+    want_enc = {"dense": 8, "dense2000": 8, "ring_f16": 8, "directed": 3, "ring_u16": 2,
                 "ring_u32": 1}
     if kind in want_enc:
         assert st.dist_enc == want_enc[kind], f"encoding {st.dist_enc}"
+
+
+@pytest.mark.parametrize("kind", ["dense", "dense2000", "ring_f16"])
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_virtual_ranks_sharded_64_pivot_rounds(gpu, monkeypatch, kind, ranks):
+    """SRT_FW_SH_KB=64 keeps the 64-pivot sharded symmetric rounds (encoding 4): same tables."""
+    monkeypatch.setenv("SRT_VIRTUAL_RANKS", str(ranks))
+    monkeypatch.setenv("SRT_FW_SH_KB", "64")
+    if kind == "dense":
+        g = graphs.complete_graph(700, seed=9)
+    elif kind == "dense2000":
+        g = graphs.complete_graph(2000, seed=13)
+    else:
+        g = _ring_graph(1000, 1, 1)
+    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                algo=ALGO_DENSE_FW, ngpus=1)
+    exp = _oracle(g)
+    assert_tables(lat, rel, exp["lat_int"], exp["rel"], f"virtual x{ranks} {kind} 64-pivot")
+    assert st.dist_enc == 4, f"encoding {st.dist_enc}"
 
 
 def test_packet_path_trace_replay(gpu):
