@@ -287,13 +287,21 @@ int srt_sparse_block_rows(int32_t n, const int32_t* rowptr, const int32_t* col, 
         return SRT_E_ARG;
     }
     hipStream_t st = (hipStream_t)stream;
-    int32_t* depth = NULL;
-    SRT_HIPCHK(hipMalloc(&depth, sizeof(int32_t)));
+    /* the depth counter and events, released on every return path */
+    struct guard_t {
+        int32_t* depth = nullptr;
+        hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+        ~guard_t() {
+            if (depth) (void)hipFree(depth);
+            for (hipEvent_t x : e)
+                if (x) (void)hipEventDestroy(x);
+        }
+    } g;
+    SRT_HIPCHK(hipMalloc(&g.depth, sizeof(int32_t)));
+    int32_t* depth = g.depth;
     SRT_HIPCHK(hipMemsetAsync(depth, 0, sizeof(int32_t), st));
-    hipEvent_t e0, e1, ek;
-    SRT_HIPCHK(hipEventCreate(&e0));
-    SRT_HIPCHK(hipEventCreate(&e1));
-    SRT_HIPCHK(hipEventCreate(&ek));
+    for (hipEvent_t& x : g.e) SRT_HIPCHK(hipEventCreate(&x));
+    hipEvent_t e0 = g.e[0], e1 = g.e[1], ek = g.e[2];
     SRT_HIPCHK(hipEventRecord(e0, st));
     if (delta == 0) delta = 8; /* bucket width of the label-correcting loop, in quanta */
     const size_t ldo = (size_t)n;
@@ -318,7 +326,6 @@ int srt_sparse_block_rows(int32_t n, const int32_t* rowptr, const int32_t* col, 
         uint32_t* ws = NULL;
         if (hipMallocAsync((void**)&ws, (size_t)slots * slot_words * 4, st) != hipSuccess) {
             (void)hipGetLastError();
-            (void)hipFree(depth);
             srt_set_error("srt_sparse_build_device: workspace of %zu MiB failed",
                           (size_t)slots * slot_words * 4 >> 20);
             return SRT_E_NOMEM;
@@ -340,10 +347,6 @@ int srt_sparse_block_rows(int32_t n, const int32_t* rowptr, const int32_t* col, 
     SRT_HIPCHK(hipEventElapsedTime(&msk, e0, ek));
     int32_t dmax = 0;
     SRT_HIPCHK(hipMemcpy(&dmax, depth, sizeof(int32_t), hipMemcpyDeviceToHost));
-    SRT_HIPCHK(hipFree(depth));
-    SRT_HIPCHK(hipEventDestroy(e0));
-    SRT_HIPCHK(hipEventDestroy(e1));
-    SRT_HIPCHK(hipEventDestroy(ek));
     if (stats) {
         stats->algo = SRT_ALGO_SPARSE_SSSP;
         stats->ms_fw = ms;
