@@ -182,14 +182,18 @@ def _dense_worker(rank, R, port, n, seed, q):
     dist.destroy_process_group()
 
 
-def _dense_sym_worker(rank, R, port, n, seed, q):
+def _dense_sym_worker(rank, R, port, n, seed, q, rp=KB):
     """The row-sharded symmetric rounds of fw16.hip fw16_build_sym_sharded, distances only: each
     rank keeps one orientation of every 128-tile pair (sym_kept); every rank broadcasts the
     pivot-panel blocks it holds (its kept row blocks, or transposed 64 x 128 slices of its tiles
     in the pivot column), every rank closes the diagonal block and the row panel itself and the
     owner writes them back; every rank updates its kept tiles with A = P^T and B = P, the next
     pivot block's tile row / column first; at the end each rank receives the transposes of the
-    tiles it does not keep."""
+    tiles it does not keep.
+    rp = 128 (encoding 8): a round's pivot block is one tile row K; its band is staged as two
+    half-panels (rows a, then rows b, two broadcasts per contributor); every rank closes P_a,
+    applies it to the staged b rows (sym_cross_stage_kernel), closes P_b, and the kept tiles take
+    both panels (min-plus over the 128 rows of P = P_a over P_b, as the four stages do)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=R)
     from shadow_amd._lib import lib
@@ -240,6 +244,42 @@ def _dense_sym_worker(rank, R, port, n, seed, q):
             D[k0 - b:k0 - b + KB] = P
         return P
 
+    def close(X, k0):
+        """diagonal closure of columns k0..k0+63 of the 64-row block X, then its row panel"""
+        Tk = X[:, k0:k0 + KB]
+        for m in range(KB):
+            Tk = np.minimum(Tk, Tk[:, m:m + 1] + Tk[m:m + 1, :])
+        X[:, k0:k0 + KB] = Tk
+        X[:] = np.minimum(X, _minplus(Tk, X))
+        return X
+
+    def produce128(k0):
+        K, o = k0 // ALIGN, own[k0 // ALIGN]
+        contrib = [o if kept(K, J) else own[J] for J in range(T)]
+        Pa = np.zeros((KB, ld), np.int64)
+        Xb = np.zeros((KB, ld), np.int64)
+        for x in range(R):
+            js = [J for J in range(T) if contrib[J] == x]
+            if not js:
+                continue
+            for half, out in ((0, Pa), (KB, Xb)):
+                buf = torch.zeros((KB, ALIGN * len(js)), dtype=torch.int64)
+                if x == rank:
+                    r0 = k0 + half
+                    blocks = [D[r0 - b:r0 - b + KB, J * ALIGN:(J + 1) * ALIGN] if kept(K, J) else
+                              D[(J - tb) * ALIGN:(J - tb + 1) * ALIGN, r0:r0 + KB].T for J in js]
+                    buf = torch.from_numpy(np.ascontiguousarray(np.concatenate(blocks, axis=1)))
+                dist.broadcast(buf, x)
+                for i, J in enumerate(js):
+                    out[:, J * ALIGN:(J + 1) * ALIGN] = buf[:, i * ALIGN:(i + 1) * ALIGN].numpy()
+        close(Pa, k0)
+        Xb[:] = np.minimum(Xb, _minplus(Xb[:, k0:k0 + KB], Pa))  # the b rows take pivot block a
+        close(Xb, k0 + KB)
+        P = np.concatenate([Pa, Xb])
+        if rank == o:
+            D[k0 - b:k0 - b + ALIGN] = P
+        return P
+
     def update(P, tiles):
         for I, J in tiles:
             C = tile(I, J)
@@ -247,14 +287,15 @@ def _dense_sym_worker(rank, R, port, n, seed, q):
                                           P[:, J * ALIGN:(J + 1) * ALIGN]))
 
     mine = [(I, J) for I in range(tb, te) for J in range(T) if kept(I, J)]
-    P = produce(0)
-    for k0 in range(0, ld, KB):
-        k1 = k0 + KB
+    make = produce128 if rp == 128 else produce
+    P = make(0)
+    for k0 in range(0, ld, rp):
+        k1 = k0 + rp
         if k1 < ld:
             K1 = k1 // ALIGN
             cross = [t for t in mine if K1 in t]
             update(P, cross)
-            Pn = produce(k1)
+            Pn = make(k1)
             update(P, [t for t in mine if K1 not in t])
         else:
             update(P, mine)
@@ -327,13 +368,14 @@ def test_dense_sharded_schedule_gloo(native):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("n,R", [(400, 2), (700, 3)])
-def test_dense_symmetric_sharded_schedule_gloo(native, n, R):
+@pytest.mark.parametrize("n,R,rp", [(400, 2, 64), (700, 3, 64), (400, 2, 128), (700, 3, 128)])
+def test_dense_symmetric_sharded_schedule_gloo(native, n, R, rp):
     seed = 7
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_dense_sym_worker, args=(r, R, port, n, seed, q)) for r in range(R)]
+    procs = [ctx.Process(target=_dense_sym_worker, args=(r, R, port, n, seed, q, rp))
+             for r in range(R)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=500) for _ in range(R)], key=lambda x: x[0])
