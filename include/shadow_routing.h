@@ -79,11 +79,14 @@ typedef struct srt_build_stats {
     double ms_comm;      /* host-observed time of the collective calls (sharded builds) */
     int32_t dist_enc;    /* sparse builds: 2 = workgroup-per-source kernel (LDS-packed rows),
                           * 1 = wave-per-source kernel, 0 = workgroup kernel for every source.
-                          * Dense: the distance encoding the build finished with: 7 = 5 with
+                          * Dense: the distance encoding the build finished with: 8 = u16
+                          * f16-compare row-sharded symmetric rounds of 128 pivots (N > 1;
+                          * 4 with SRT_FW_SH_KB=64), 7 = 5 with
                           * 256-pivot rounds (four panels per C-tile residency), 6 = 5 with
                           * 128-pivot rounds (two panels per C-tile residency), 5 = 4 on two
                           * update streams (one GPU, n >= 8192), 4 = u16 with
-                          * f16-compare mins, upper-triangle rounds (undirected, one shard),
+                          * f16-compare mins, upper-triangle rounds (undirected; one GPU, or
+                          * row-sharded kept tiles in 64-pivot rounds),
                           * 3 = u16 f16-compare (cap 0x3DFF), 2 = u16 pk_min (cap 0x7FFF), 1 = u32 */
     int32_t count_ties;  /* input: 1 = count tied pairs (below) */
     int64_t tied_pairs;  /* pairs (s, t), s != t, whose smallest D[s][u] over the tight
