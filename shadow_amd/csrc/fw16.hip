@@ -1428,20 +1428,38 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
                 return SRT_OK;
             };
             const int R = T / 2;
+            /* SRT_FW_NRCS=1: the next round's crosses run on the chain stream after both streams'
+             * rest of the round before (as in the sharded form), not at the head of each update
+             * stream's round */
+            const char* nrenv = getenv("SRT_FW_NRCS");
+            const bool nr_cs = nrenv ? atoi(nrenv) != 0 : false;
             if ((rc = produce4(0))) return rc;
             for (int j = 0; j < R; ++j) {
                 const int ka = 4 * j * KB;
                 u16* Pa = d + (size_t)ka * ld;
                 const bool next = j + 1 < R;
+                if (nr_cs && next) {
+                    /* cs: the crosses of tile rows 2j + 2, 2j + 3 with round j's panels follow
+                     * rest(j - 1) of both streams; round j + 1's panels follow them */
+                    if (j >= 1) {
+                        SRT_HIPCHK(hipStreamWaitEvent(cs, sc->e_set[(j - 1) & 1][0], 0));
+                        SRT_HIPCHK(hipStreamWaitEvent(cs, sc->e_set[(j - 1) & 1][1], 0));
+                    }
+                    for (int p = 0; p < 2; p++)
+                        fwq_update_kernel<true, 13, 8><<<2 * T, 512, 0, cs>>>(d, ld, Pa, ka, T, p,
+                                                                            2 * j + 2, nullptr, 0, -1);
+                    SRT_HIPCHK(hipGetLastError());
+                    if ((rc = produce4(j + 1))) return rc;
+                }
                 for (int p = 0; p < 2; p++) {
                     SRT_HIPCHK(hipStreamWaitEvent(ss[p], sc->ready[j & 1], 0));
-                    if (next) {
+                    if (next && !nr_cs) {
                         fwq_update_kernel<true, 13, 8><<<2 * T, 512, 0, ss[p]>>>(
                             d, ld, Pa, ka, T, p, 2 * j + 2, nullptr, 0, -1);
                         SRT_HIPCHK(hipEventRecord(sc->e_set[j & 1][p], ss[p]));
                     }
                 }
-                if (next) {
+                if (next && !nr_cs) {
                     SRT_HIPCHK(hipStreamWaitEvent(cs, sc->e_set[j & 1][0], 0));
                     SRT_HIPCHK(hipStreamWaitEvent(cs, sc->e_set[j & 1][1], 0));
                     if ((rc = produce4(j + 1))) return rc;
@@ -1460,6 +1478,7 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
                         fwq_update_kernel<true, 5, 8><<<(unsigned)nset[p], 512, 0, ss[p]>>>(
                             d, ld, Pa, ka, T, 0, -1, tls[p], T, 2 * j);
                     if (evp && next) SRT_HIPCHK(hipEventRecord(evp->ev[e0 + 2 + p], ss[p]));
+                    if (nr_cs) SRT_HIPCHK(hipEventRecord(sc->e_set[j & 1][p], ss[p])); /* rest(j) */
                 }
                 SRT_HIPCHK(hipGetLastError());
             }

@@ -113,3 +113,61 @@ def test_complete_sample_matches_edge_list_oracle():
         rows = oracle.sssp_rows(el, int(s), int(s) + 1)
         assert np.array_equal(lat[i], rows["lat_int"][0])
         assert np.array_equal(rel[i], rows["rel"][0])
+
+
+def _scipy_crosscheck(g):
+    """An independent implementation pins the oracle: scipy's Dijkstra gives every distance, and
+    on every pair whose shortest path is unique (where igraph's heap order and the canonical tie
+    rule cannot differ) the path-order product of (1 - loss) along scipy's predecessor chain,
+    formed left to right from the source (topology.c:1364-1365), gives the reliability."""
+    sp = pytest.importorskip("scipy.sparse")
+    csgraph = pytest.importorskip("scipy.sparse.csgraph")
+    n = g.n
+    off = g.src != g.dst
+    w = (g.lat_ns[off] // MS).astype(np.float64)
+    W = sp.coo_matrix((w, (g.src[off], g.dst[off])), shape=(n, n)).tocsr()
+    R = {(int(a), int(b)): 1.0 - float(x) for a, b, x in zip(g.src[off], g.dst[off], g.loss[off])}
+    if not g.directed:
+        W = W.maximum(W.T)
+        R.update({(b, a): x for (a, b), x in list(R.items())})
+    D, P = csgraph.dijkstra(W, directed=True, return_predecessors=True)
+    el = oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
+    t = oracle.table(el, nthreads=4)
+    Wd = W.toarray()
+    checked = 0
+    for s in range(n):
+        reach = np.isfinite(D[s])
+        for v in range(n):
+            if v != s and reach[v]:
+                assert int(t["lat_int"][s, v]) == int(D[s, v]) * MS, (s, v)
+        # uniqueness and the path product, in increasing distance order
+        order = np.argsort(D[s], kind="stable")
+        uniq = np.zeros(n, bool)
+        rel = np.zeros(n)
+        uniq[s], rel[s] = True, 1.0
+        for v in order:
+            if v == s or not reach[v]:
+                continue
+            tight = [u for u in np.nonzero(Wd[:, v])[0]
+                     if reach[u] and D[s, u] + Wd[u, v] == D[s, v] and u != v]
+            u = int(P[s, v])
+            uniq[v] = len(tight) == 1 and uniq[u]
+            rel[v] = rel[u] * R[(u, v)]
+            if uniq[v] and (g.directed or s < v):
+                assert t["rel"][s, v] == rel[v], (s, v)
+                checked += 1
+    return checked
+
+
+@pytest.mark.parametrize("which", ["c1", "rgg300", "ba400", "complete120_ties"])
+def test_oracle_against_scipy_dijkstra(which):
+    if which == "c1":
+        g = graphs.complete_graph(50, seed=1)
+    elif which == "rgg300":
+        g = graphs.random_geometric(300, seed=3)
+    elif which == "ba400":
+        g = graphs.barabasi_albert(400, seed=5)
+    else:  # small latencies: many equal-length paths, so many pairs are skipped as tied
+        g = graphs.complete_graph(120, seed=11, lat_max=8)
+    checked = _scipy_crosscheck(g)
+    assert checked > 0
