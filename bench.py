@@ -267,13 +267,13 @@ def run_dense(c: Ctx, wl):
     #   enc 3: 2 x v_add_u32 + 1 x v_pk_minimum3_f16 per 4 relaxations -> 8/4 = 2.0 cycles
     #   enc 2: 1 x v_add_u32 + 1 x v_pk_min_u16 per 2 relaxations      -> 6/2 = 3.0 cycles
     #   enc 1: 2 x v_add_u32 + 1 x v_min3_u32 per 2 relaxations         -> 8/2 = 4.0 cycles
-    cyc_per_relax = {8: 2.0, 7: 2.0, 6: 2.0, 5: 2.0, 4: 2.0, 3: 2.0, 2: 3.0, 1: 4.0}[enc]
-    instr_per_relax = {8: 0.75, 7: 0.75, 6: 0.75, 5: 0.75, 4: 0.75, 3: 0.75, 2: 1.0, 1: 1.5}[enc]
+    cyc_per_relax = {9: 2.0, 8: 2.0, 7: 2.0, 6: 2.0, 5: 2.0, 4: 2.0, 3: 2.0, 2: 3.0, 1: 4.0}[enc]
+    instr_per_relax = {9: 0.75, 8: 0.75, 7: 0.75, 6: 0.75, 5: 0.75, 4: 0.75, 3: 0.75, 2: 1.0, 1: 1.5}[enc]
     # the 8-wave update kernel (fwq_update_kernel) unless SRT_FW_WAVES=4 selects the 4-wave one
     w4 = os.environ.get("SRT_FW_WAVES") == "4"
     uk = "fwh_update_kernel" if w4 else "fwq_update_kernel"
     st2 = "" if w4 else ", 2"  # fwq's third template argument: 32-pivot stages per tile
-    kname = {8: "fwq_update_kernel<true, 4, 4>", 7: "fwq_update_kernel<true, 4, 8>", 6: "fwq_update_kernel<true, 4, 4>", 5: f"{uk}<true, 4{st2}>",
+    kname = {9: "fwq_update_kernel<true, 4, 8>", 8: "fwq_update_kernel<true, 4, 4>", 7: "fwq_update_kernel<true, 4, 8>", 6: "fwq_update_kernel<true, 4, 4>", 5: f"{uk}<true, 4{st2}>",
              4: f"{uk}<true, 0{st2}>" if world == 1 else f"{uk}<true, 4{st2}>",
              3: f"{uk}<false, 0{st2}>",
              2: "fw16_update_kernel<false>", 1: "fw_update_kernel"}[enc]
@@ -308,13 +308,13 @@ def run_dense(c: Ctx, wl):
         elems = float(tiles * (tiles + 1) // 2 - tiles) * 128 * 128
     elif enc == 4 and world == 1:
         elems = float(tiles * (tiles + 1) // 2) * 128 * 128
-    elif enc in (4, 8):  # row-sharded symmetric rounds (8: 128 pivots per round)
-        if enc == 8:
-            pivots = 128
+    elif enc in (4, 8, 9):  # row-sharded symmetric rounds (8: 128, 9: 256 pivots per round)
+        if enc in (8, 9):
+            pivots = 128 if enc == 8 else 256
         kept = lambda i, j: i == j or ((i < j) == ((i + j) % 2 == 0))
         tb, te = b // 128, e // 128
         nkept = sum(1 for i in range(tb, te) for j in range(tiles) if kept(i, j))
-        cross = tiles // 2 / max(world, 1) + (te - tb) / 2  # average kept tiles of row/col K1
+        cross = (tiles // 2 / max(world, 1) + (te - tb) / 2) * (2 if enc == 9 else 1)  # row/col K1 (and K1 + 1)
         elems = float(max(nkept - cross, 1)) * 128 * 128
     else:
         elems = float(nr) * ld
@@ -351,8 +351,8 @@ def run_dense(c: Ctx, wl):
         "traffic": traffic, "bytes_per_launch": bytes_per_round,
         "avg_launch_ms": round(avg_upd_ms, 4), "launches_timed": n_upd,
         "model": f"2*elements*{s_d} B per timed unit (SURVEY §8d round-streaming, "
-                 f"{ {7: 'B=256 (four 64-pivot panels per C-tile residency)', 6: 'B=128 (two 64-pivot panels per C-tile residency)', 8: 'B=128 (two 64-pivot panels per C-tile residency)'}.get(enc, 'B=64')}, "
-                 f"{ {8: 'u16 f16-compare, row-sharded kept tiles, 128-pivot rounds (unit: one round, first start to last end)', 7: 'u16 f16-compare, upper triangle on two streams, 256-pivot rounds (unit: both rest launches)', 6: 'u16 f16-compare, upper triangle on two streams, 128-pivot rounds (unit: both rest launches)', 5: 'u16 f16-compare, upper triangle on two streams (unit: both rest launches)', 4: 'u16 f16-compare, upper triangle', 3: 'u16 f16-compare', 2: 'u16 pk_min', 1: 'u32'}[enc]}"
+                 f"{ {7: 'B=256 (four 64-pivot panels per C-tile residency)', 6: 'B=128 (two 64-pivot panels per C-tile residency)', 8: 'B=128 (two 64-pivot panels per C-tile residency)', 9: 'B=256 (four 64-pivot panels per C-tile residency)'}.get(enc, 'B=64')}, "
+                 f"{ {9: 'u16 f16-compare, row-sharded kept tiles, 256-pivot rounds (unit: one round, first start to last end)', 8: 'u16 f16-compare, row-sharded kept tiles, 128-pivot rounds (unit: one round, first start to last end)', 7: 'u16 f16-compare, upper triangle on two streams, 256-pivot rounds (unit: both rest launches)', 6: 'u16 f16-compare, upper triangle on two streams, 128-pivot rounds (unit: both rest launches)', 5: 'u16 f16-compare, upper triangle on two streams (unit: both rest launches)', 4: 'u16 f16-compare, upper triangle', 3: 'u16 f16-compare', 2: 'u16 pk_min', 1: 'u32'}[enc]}"
                  f" distances; elements updated per unit = {int(elems)}, "
                  f"pivots per element = {pivots:.2f})",
         "algorithmic_min_bytes": float(nr) * ld * (4 + 8),

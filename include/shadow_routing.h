@@ -79,7 +79,8 @@ typedef struct srt_build_stats {
     double ms_comm;      /* host-observed time of the collective calls (sharded builds) */
     int32_t dist_enc;    /* sparse builds: 2 = workgroup-per-source kernel (LDS-packed rows),
                           * 1 = wave-per-source kernel, 0 = workgroup kernel for every source.
-                          * Dense: the distance encoding the build finished with: 8 = u16
+                          * Dense: the distance encoding the build finished with: 9 = 8 with
+                          * 256-pivot rounds (SRT_FW_SH_KB=256), 8 = u16
                           * f16-compare row-sharded symmetric rounds of 128 pivots (N > 1;
                           * 4 with SRT_FW_SH_KB=64), 7 = 5 with
                           * 256-pivot rounds (four panels per C-tile residency), 6 = 5 with

@@ -1652,8 +1652,9 @@ int srt_dense_build_sharded_ms(srt_comm* comm, int32_t n, int32_t ld, int32_t di
             SRT_HIPCHK(hipStreamSynchronize(st));
         }
         if (exact)
-            enc = fm ? (sym ? (srt_fw16_sharded_round_pivots() == 128 ? SRT_DENC_F16CMP_SYMSH128
-                                                                     : SRT_DENC_F16CMP_SYM)
+            enc = fm ? (sym ? (srt_fw16_sharded_round_pivots() == 256   ? SRT_DENC_F16CMP_SYMSH256
+                               : srt_fw16_sharded_round_pivots() == 128 ? SRT_DENC_F16CMP_SYMSH128
+                                                                        : SRT_DENC_F16CMP_SYM)
                             : SRT_DENC_F16CMP)
                      : SRT_DENC_U16;
     }

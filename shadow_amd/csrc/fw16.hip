@@ -1135,22 +1135,23 @@ __global__ __launch_bounds__(256) void sym_panel_stage_kernel(u16* __restrict__ 
     }
 }
 
-/* 128-pivot sharded rounds: the staged blocks of rows b (the second 64-row half of pivot tile row
- * K, 64 x 128 per tile column J, in the staging order) take pivot block a before P_b is closed:
- * X[J] = min(X[J], X_K[:, 0:64] (x) P_a[:, J]), where X_K[:, 0:64] = D[b][a] is the staged block of
- * tile column K and P_a the closed row panel a. The workgroup of J = K rewrites the D[b][a] the
- * others read: either value is a valid operand (P_a is closed, so old and updated D[b][a] give the
- * same minimum), as in blocked FW's column-panel/rest split. */
+/* 128/256-pivot sharded rounds: the staged blocks of a later 64-row quarter y of the band (tile
+ * row Ky, 64 x 128 per tile column J, in Ky's staging order) take a closed earlier pivot block x
+ * (tile column Kx, columns cx..cx+63 of it) before P_y is closed:
+ * X[J] = min(X[J], X_Kx[:, cx:cx+64] (x) P_x[:, J]), where X_Kx[:, cx:cx+64] = D[y][x] is the staged
+ * block of tile column Kx and P_x the closed row panel x. The workgroup of J = Kx rewrites the
+ * D[y][x] the others read: either value is a valid operand (P_x is closed, so old and updated
+ * D[y][x] give the same minimum), as in blocked FW's column-panel/rest split. */
 __global__ __launch_bounds__(256) void sym_cross_stage_kernel(const u16* __restrict__ Pa, int ld, int K,
                                                               int T, const int* __restrict__ own,
-                                                              u16* __restrict__ stage) {
+                                                              u16* __restrict__ stage, int Kx, int cx) {
     __shared__ __attribute__((aligned(16))) u16 s[KB * LDA16];     /* D[b][a] */
     __shared__ __attribute__((aligned(16))) u16 x[KB * (128 + 8)]; /* P_a[:, J] */
     __shared__ int s_own[SYM_TMAX], s_cnt;
     FW_CHAIN_PRIO();
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     const int J = (int)blockIdx.x;
-    const u16* ak = stage + (size_t)sym_stage_pos(K, K, T, own, s_own, &s_cnt) * (KB * 128);
+    const u16* ak = stage + (size_t)sym_stage_pos(K, Kx, T, own, s_own, &s_cnt) * (KB * 128) + cx;
     __syncthreads(); /* s_cnt is reused by the second position */
     u16* xj = stage + (size_t)sym_stage_pos(K, J, T, own, s_own, &s_cnt) * (KB * 128);
 #pragma unroll
@@ -1619,7 +1620,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
     const int R = srt_comm_size(comm), me = srt_comm_rank(comm);
     /* kbr = 128: 128-pivot rounds (pivot block = tile row K, panels P_a over P_b, four 32-pivot
      * stages per C-tile residency); kbr = 64: 64-pivot rounds */
-    const bool r128 = kbr == 128;
+    const bool r128 = kbr == 128, r256 = kbr == 256;
     const int T = ld / 128, nb = ld / kbr;
     const int tb = row0 / 128, te = (row0 + nrows) / 128;
     size_t* caps = fw16_caps;
@@ -1672,7 +1673,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
     uint32_t* tl = NULL;
     int* down = NULL; /* owner of each tile row, on the device */
     u16* grecv = NULL; /* staged panel blocks in (contributor, J) order (r128: rows a, then b) */
-    int* cnt = (int*)calloc((size_t)R, sizeof(int));
+    int* cnt = (int*)calloc(2 * (size_t)R, sizeof(int)); /* per contributor (256: two tile rows) */
     const size_t blk = (size_t)KB * 128;
     const size_t nstage = (size_t)(kbr / KB) * ((size_t)T + 1) * blk;
     bool ok = cnt && hipMalloc(&tl, (nkept + 1) * sizeof(uint32_t)) == hipSuccess &&
@@ -1784,14 +1785,60 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
             u16* Pb = P + (size_t)KB * ld;
             sym_diag_stage_kernel<<<1, 256, 0, cs>>>(P, ld, K, k0, T, down, sa, prow_a);
             sym_panel_stage_kernel<<<T, 256, 0, cs>>>(P, ld, K, k0, T, down, sa, prow_a);
-            sym_cross_stage_kernel<<<T, 256, 0, cs>>>(P, ld, K, T, down, sb);
+            sym_cross_stage_kernel<<<T, 256, 0, cs>>>(P, ld, K, T, down, sb, K, 0);
             sym_diag_stage_kernel<<<1, 256, 0, cs>>>(Pb, ld, K, k0 + KB, T, down, sb, prow_b);
             sym_panel_stage_kernel<<<T, 256, 0, cs>>>(Pb, ld, K, k0 + KB, T, down, sb, prow_b);
             SRT_HIPCHK(hipGetLastError());
             SRT_HIPCHK(hipEventRecord(sc->ready[k & 1], cs));
             return SRT_OK;
         };
-        if ((rc = r128 ? produce128(0) : produce(0))) goto out;
+        /* 256-pivot rounds: the band is tile rows K0 = 2j and K1 = 2j + 1 (quarters a, b of K0,
+         * c, d of K1, each staged in its tile row's contributor order: four half-panel
+         * broadcasts per contributor); every rank closes the quarters in order, each one's
+         * closed panel applied to the staged rows of the later quarters first */
+        auto produce256 = [&](int j) -> int {
+            const int k0 = j * 256, K0 = 2 * j;
+            u16* P = pbuf[j & 1];
+            u16* sq[4];
+            for (int q = 0; q < 4; q++) sq[q] = grecv + (size_t)q * ((size_t)T + 1) * blk;
+            int* cq[2] = {cnt, cnt + R};
+            for (int h = 0; h < 2; h++) {
+                const int K = K0 + h, o = own[K];
+                for (int q = 0; q < R; q++) cq[h][q] = 0;
+                for (int J = 0; J < T; J++) cq[h][sym_kept(K, J) ? o : own[J]]++;
+            }
+            for (int q = 0; q < 4; q++)
+                if (cq[q >> 1][me])
+                    sym_contrib_pack_kernel<<<T, 256, 0, cs>>>(d, ld, row0, tb, K0 + (q >> 1),
+                                                               k0 + q * KB, T, down, me, sq[q]);
+            SRT_HIPCHK(hipGetLastError());
+            int r = srt_coll_group_begin(comm);
+            for (int q = 0; q < 4 && !r; q++) {
+                size_t off = 0;
+                for (int x = 0; x < R && !r; x++) {
+                    const int c = cq[q >> 1][x];
+                    if (c) r = srt_coll_bcast(comm, sq[q] + off * blk, (size_t)c * blk * sizeof(u16), x, cs);
+                    off += (size_t)c;
+                }
+            }
+            const int r2 = srt_coll_group_end(comm);
+            if (r || r2) return r ? r : r2;
+            for (int q = 0; q < 4; q++) {
+                const int K = K0 + (q >> 1), kq = k0 + q * KB;
+                u16* Pq = P + (size_t)q * KB * ld;
+                u16* prow = me == own[K] ? d + (size_t)(kq - row0) * ld : nullptr;
+                sym_diag_stage_kernel<<<1, 256, 0, cs>>>(Pq, ld, K, kq, T, down, sq[q], prow);
+                sym_panel_stage_kernel<<<T, 256, 0, cs>>>(Pq, ld, K, kq, T, down, sq[q], prow);
+                for (int y = q + 1; y < 4; y++) /* P_q into the later quarters' staged rows */
+                    sym_cross_stage_kernel<<<T, 256, 0, cs>>>(Pq, ld, K0 + (y >> 1), T, down, sq[y], K,
+                                                              (q & 1) * KB);
+            }
+            SRT_HIPCHK(hipGetLastError());
+            SRT_HIPCHK(hipEventRecord(sc->ready[j & 1], cs));
+            return SRT_OK;
+        };
+        auto make = [&](int k) -> int { return r256 ? produce256(k) : r128 ? produce128(k) : produce(k); };
+        if ((rc = make(0))) goto out;
         /* two update streams (st: even J, xs: odd J), as on one GPU (fw16_build_sym): each
          * depends on its own launches and the panel, so their rounds overlap */
         hipStream_t ss[2] = {st, sc->xs};
@@ -1808,7 +1855,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
          * 49.2 -> 46.0 ms, N = 4 unchanged (83.5 ms). SRT_FW_SH_NRCS=0 keeps NR on the update
          * streams. */
         const char* nrenv = getenv("SRT_FW_SH_NRCS");
-        const bool nr_cs = nrenv ? atoi(nrenv) != 0 : true;
+        const bool nr_cs = r256 || (nrenv ? atoi(nrenv) != 0 : true); /* 256: only this form */
         for (int k = 0; k < nb; ++k) {
             const int k0 = k * kbr;
             u16* P = panel_of(k);
@@ -1841,7 +1888,14 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
             }
             for (int p = 0; p < 2; p++) {
                 if (t_first) SYM_HIP(hipEventRecord(evp->ev[p], ss[p]));
-                if (nset[p] && r128) {
+                if (nset[p] && r256) { /* XM 4 with NST 8 leaves out both crosses K1, K1 + 1 */
+                    if (next)
+                        fwq_update_kernel<true, 4, 8><<<(unsigned)nset[p], 512, 0, ss[p]>>>(
+                            d, ld, P, k0, T, tb, K1, tls[p], te);
+                    else
+                        fwq_update_kernel<true, 5, 8><<<(unsigned)nset[p], 512, 0, ss[p]>>>(
+                            d, ld, P, k0, T, tb, -1, tls[p], te);
+                } else if (nset[p] && r128) {
                     if (next)
                         fwq_update_kernel<true, 4, 4><<<(unsigned)nset[p], 512, 0, ss[p]>>>(
                             d, ld, P, k0, T, tb, K1, tls[p], te);
@@ -1868,17 +1922,21 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
                     SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[(k - 1) & 1][0], 0));
                     SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[(k - 1) & 1][1], 0));
                 }
-                if (r128)
+                if (r256) /* the next band's two tile rows and columns */
+                    for (int h = 0; h < 2; h++)
+                        fwq_update_kernel<true, 3, 8><<<T + (te - tb), 512, 0, cs>>>(
+                            d, ld, P, k0, T, tb, K1 + h, nullptr, te);
+                else if (r128)
                     fwq_update_kernel<true, 3, 4><<<T + (te - tb), 512, 0, cs>>>(d, ld, P, k0, T, tb,
                                                                                 K1, nullptr, te);
                 else
                     FW_UPDATE(true, 3, T + (te - tb), cs, d, ld, P, k0, T, tb, K1, nullptr, te);
                 SYM_HIP(hipGetLastError());
-                if ((rc = r128 ? produce128(k + 1) : produce(k + 1))) goto out;
+                if ((rc = make(k + 1))) goto out;
             } else if (next) {
                 SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[k & 1][0], 0));
                 SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[k & 1][1], 0));
-                if ((rc = r128 ? produce128(k + 1) : produce(k + 1))) goto out;
+                if ((rc = make(k + 1))) goto out;
             }
         }
         SYM_HIP(hipEventRecord(sc->xs_done[0], sc->xs));
@@ -2014,9 +2072,11 @@ int srt_fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0, in
                       "most %d tile columns", SYM_TMAX);
         return SRT_E_ARG;
     }
-    /* 128-pivot rounds with the 8-wave update unless SRT_FW_SH_KB=64 */
+    /* 128-pivot rounds with the 8-wave update; SRT_FW_SH_KB=64 or 256 selects the others (256
+     * needs ld % 256 == 0) */
     const char* kb_env = getenv("SRT_FW_SH_KB");
-    const int rp = (kb_env && atoi(kb_env) == 64) || !fw_waves8() ? 64 : 128;
+    const int want = kb_env ? atoi(kb_env) : 128;
+    const int rp = want == 64 || !fw_waves8() ? 64 : want == 256 && ld % 256 == 0 ? 256 : 128;
     g_sharded_rp = rp;
     return fw16_build_sym_sharded(comm, n, ld, row0, nrows, w_rows, lat_rows, st, evp, exact, rp);
 }

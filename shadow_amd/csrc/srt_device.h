@@ -147,7 +147,8 @@ enum {
     SRT_DENC_F16CMP_SYM2 = 5, /* one GPU, upper triangle on two update streams */
     SRT_DENC_F16CMP_SYM128 = 6, /* 5 with 128-pivot rounds (8-wave update, 4 stages per tile) */
     SRT_DENC_F16CMP_SYM256 = 7, /* 5 with 256-pivot rounds (8 stages per tile) */
-    SRT_DENC_F16CMP_SYMSH128 = 8 /* 4 (row-sharded, >= 2 ranks) with 128-pivot rounds */
+    SRT_DENC_F16CMP_SYMSH128 = 8, /* 4 (row-sharded, >= 2 ranks) with 128-pivot rounds */
+    SRT_DENC_F16CMP_SYMSH256 = 9  /* 4 (row-sharded) with 256-pivot rounds */
 };
 /* pivots per round of this thread's last srt_fw16_build_sym_sharded (64 or 128) */
 int srt_fw16_sharded_round_pivots(void);
