@@ -505,7 +505,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
     __shared__ uint32_t bcnt[256]; /* entries per bucket; the search ballots on bcnt > 0 */
     __shared__ int s_beg[WG], s_excl[WG], s_wtot[WG / WL];
     __shared__ unsigned long long s_best[WG];
-    __shared__ int s_found, s_ovf;
+    __shared__ int s_ovf;
     const int tid = threadIdx.x, lane = tid & (WL - 1), wv = tid >> 6;
     const int words = (n + 2) / 3;
     const size_t slot_words = ((size_t)nb * bcap * 2 + (ORIG ? 0 : 2 * (size_t)n) + 1) & ~(size_t)1;
@@ -545,26 +545,27 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
         double pa = 0.0, pb = 0.0;
         uint32_t d = 0;
         for (;;) {
-            if (wv == 0) { /* next non-empty bucket at or after d (circular) */
+            /* next non-empty bucket at or after d (circular), found by every wave itself: bcnt
+             * is final since the step's last post-arc barrier, a full one (the pushed entries
+             * are visible), and nothing writes it before every wave has passed the next scan
+             * barrier -- no workgroup barrier and broadcast here */
+            int found = -1;
+            {
                 const uint32_t p0 = d & bm;
-                int found = -1;
                 for (int q = 0; q < nb && found < 0; q += WL) {
                     const int pos = (int)((p0 + (uint32_t)q + (uint32_t)lane) & bm);
                     const bool set = q + lane < nb && bcnt[pos] != 0u;
                     const unsigned long long bal = __ballot(set);
                     if (bal) found = q + __ffsll((long long)bal) - 1;
                 }
-                if (lane == 0) s_found = found;
             }
-            __syncthreads(); /* full: the last arc pass's bucket stores are visible from here */
-            const int found = s_found;
             if (found < 0) break;
             d += (uint32_t)found;
             const int b = (int)(d & bm);
             const int cnt = min((int)bcnt[b], bcap);
-            WG_LDS_BARRIER();
-            if (tid == 0) bcnt[b] = 0;
-            WG_LDS_BARRIER();
+            /* bcnt[b] is zeroed after the first chunk's scan barrier (every thread has read cnt
+             * by then): no push of this step targets b (nd >= d + 1, and the ring is longer than
+             * the largest weight), and the next search follows this step's last barrier */
             WG_PT(1);
             if (PROF && tid == 0) pacc[6]++;
             const uint2* bk = buckets + (size_t)b * bcap;
@@ -594,6 +595,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                 if (lane == 0) s_wtot[wv] = wtot;
                 WG_LDS_BARRIER();
                 WG_PT(11);
+                if (c0 == 0 && tid == 0) bcnt[b] = 0;
                 int base = 0, total = 0;
                 for (int q = 0; q < WG / WL; ++q) {
                     base += q < wv ? s_wtot[q] : 0;
@@ -680,10 +682,11 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                     relp[pv] = pa * pb;
                     pv = -1;
                 }
-                /* a step's first chunk may settle children of the previous chunk's vertices: full
-                 * barrier (their reliability stores, and this pass's bucket stores, visible);
-                 * otherwise the bucket stores drain by the next step's search barrier */
-                if (c0 == 0)
+                /* full barrier after a step's first chunk (it may settle children of the previous
+                 * chunk's vertices: their reliability stores visible) and after its last (the
+                 * next step's search and entry loads follow with no other barrier: this pass's
+                 * bucket stores visible); an LDS barrier in between */
+                if (c0 == 0 || c0 + WG >= cnt)
                     __syncthreads();
                 else
                     WG_LDS_BARRIER();
