@@ -985,15 +985,29 @@ static __device__ int sym_contrib_pos(int K, int J, int T, const int* __restrict
     return *s_cnt;
 }
 
-/* this rank's blocks of panel k into the staging buffer (64 x 128 each) */
+/* rows of the staged-panel chain kernels per thread (sym_panel_stage_kernel, sym_cross_stage_kernel:
+ * 1024 / SYM_RM threads per workgroup) */
+#ifndef SYM_RM
+#define SYM_RM 2
+#endif
+
+/* this rank's blocks of panel k into the staging buffer (64 x 128 each); with stage_b, a grid of
+ * 2T also packs the band's second half (rows k0 + 64..) into stage_b (128-pivot rounds: one launch) */
 __global__ __launch_bounds__(256) void sym_contrib_pack_kernel(const u16* __restrict__ D, int ld,
                                                                int row0, int tb, int K, int k0,
                                                                int T, const int* __restrict__ own,
-                                                               int me, u16* __restrict__ stage) {
+                                                               int me, u16* __restrict__ stage,
+                                                               u16* __restrict__ stage_b = nullptr) {
     __shared__ u16 t[128][KB + 8];
     __shared__ int s_own[SYM_TMAX], s_cnt;
     FW_CHAIN_PRIO();
-    const int J = (int)blockIdx.x, tid = threadIdx.x;
+    int J = (int)blockIdx.x;
+    const int tid = threadIdx.x;
+    if (J >= T) { /* the second half (uniform per workgroup) */
+        J -= T;
+        k0 += KB;
+        stage = stage_b;
+    }
     if (J >= T || sym_contrib(K, J, own) != me) return;
     u16* dst = stage + (size_t)sym_contrib_pos(K, J, T, own, s_own, &s_cnt) * (KB * 128);
     if (sym_kept(K, J)) { /* this rank owns the pivot rows: straight copy, 16 B per access */
@@ -1065,15 +1079,18 @@ __global__ __launch_bounds__(256) void sym_diag_stage_kernel(u16* __restrict__ P
 }
 
 /* P[:, j0..j0+63] = min(X, Dkk* (x) X) for every 64-column block j0 != k0, from the staged block X
- * and the closed diagonal block in P (as fw16_panel_kernel), into P and the owner's rows */
-__global__ __launch_bounds__(256) void sym_panel_stage_kernel(u16* __restrict__ P, int ld, int K,
-                                                              int k0, int T,
-                                                              const int* __restrict__ own,
-                                                              const u16* __restrict__ stage,
-                                                              u16* __restrict__ prow) {
-    /* workgroup J: the 64 x 128 staged block of tile column J (both 64-column halves; the half
-     * holding the diagonal block is not written), 4 rows x 8 columns per thread. Per 4 pivots a
-     * thread reads 4 b64 of Dkk* (its rows) and 4 b128 of X (its columns) for 128 relaxations. */
+ * and the closed diagonal block in P (as fw16_panel_kernel), into P and the owner's rows.
+ * Workgroup J: the 64 x 128 staged block of tile column J (both 64-column halves; the half holding
+ * the diagonal block is not written), RM rows x 8 columns per thread (1024 / RM threads). The
+ * chain kernels run one workgroup per CU beside the bulk update, so fewer rows per thread (RM = 2)
+ * put twice the waves on the latency-bound pivot loop. */
+template <int RM>
+__global__ __launch_bounds__(1024 / RM) void sym_panel_stage_kernel(u16* __restrict__ P, int ld, int K,
+                                                                   int k0, int T,
+                                                                   const int* __restrict__ own,
+                                                                   const u16* __restrict__ stage,
+                                                                   u16* __restrict__ prow) {
+    constexpr int NT = 1024 / RM;
     __shared__ __attribute__((aligned(16))) u16 s[KB * LDA16];       /* Dkk* */
     __shared__ __attribute__((aligned(16))) u16 x[KB * (128 + 8)];   /* this workgroup's block */
     __shared__ int s_own[SYM_TMAX], s_cnt;
@@ -1082,22 +1099,22 @@ __global__ __launch_bounds__(256) void sym_panel_stage_kernel(u16* __restrict__ 
     const int J = (int)blockIdx.x;
     const u16* xsrc = stage + (size_t)sym_stage_pos(K, J, T, own, s_own, &s_cnt) * (KB * 128);
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int i = tid + q * 256, row = i >> 3, c8 = (i & 7) * 8;
+    for (int q = 0; q < 512 / NT; ++q) {
+        const int i = tid + q * NT, row = i >> 3, c8 = (i & 7) * 8;
         *reinterpret_cast<uint4*>(s + row * LDA16 + c8) =
             *reinterpret_cast<const uint4*>(P + (size_t)row * ld + k0 + c8);
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int i = tid + q * 256, row = i >> 4, c8 = (i & 15) * 8;
+    for (int q = 0; q < 1024 / NT; ++q) {
+        const int i = tid + q * NT, row = i >> 4, c8 = (i & 15) * 8;
         *reinterpret_cast<uint4*>(x + row * (128 + 8) + c8) =
             *reinterpret_cast<const uint4*>(xsrc + row * 128 + c8);
     }
     __syncthreads();
-    uint32_t acc[4][4];
+    uint32_t acc[RM][4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const uint4 v = *reinterpret_cast<const uint4*>(x + (4 * ty + r) * (128 + 8) + 8 * tx);
+    for (int r = 0; r < RM; ++r) {
+        const uint4 v = *reinterpret_cast<const uint4*>(x + (RM * ty + r) * (128 + 8) + 8 * tx);
         acc[r][0] = v.x;
         acc[r][1] = v.y;
         acc[r][2] = v.z;
@@ -1105,14 +1122,14 @@ __global__ __launch_bounds__(256) void sym_panel_stage_kernel(u16* __restrict__ 
     }
 #pragma unroll 2
     for (int m = 0; m < KB; m += 4) {
-        uint2 a[4];
+        uint2 a[RM];
         uint4 b[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) a[r] = *reinterpret_cast<const uint2*>(s + (4 * ty + r) * LDA16 + m);
+        for (int r = 0; r < RM; ++r) a[r] = *reinterpret_cast<const uint2*>(s + (RM * ty + r) * LDA16 + m);
 #pragma unroll
         for (int q = 0; q < 4; ++q) b[q] = *reinterpret_cast<const uint4*>(x + (m + q) * (128 + 8) + 8 * tx);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < RM; ++r) {
             const uint32_t p[4] = {splat(a[r].x & 0xFFFFu), splat(a[r].x >> 16),
                                    splat(a[r].y & 0xFFFFu), splat(a[r].y >> 16)};
 #pragma unroll
@@ -1127,8 +1144,8 @@ __global__ __launch_bounds__(256) void sym_panel_stage_kernel(u16* __restrict__ 
     const int j0 = J * 128 + 8 * tx;
     if ((j0 & ~(KB - 1)) == k0) return; /* the diagonal block: sym_diag_stage_kernel's */
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const size_t o = (size_t)(4 * ty + r) * ld + j0;
+    for (int r = 0; r < RM; ++r) {
+        const size_t o = (size_t)(RM * ty + r) * ld + j0;
         const uint4 v = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
         *reinterpret_cast<uint4*>(P + o) = v;
         if (prow) *reinterpret_cast<uint4*>(prow + o) = v;
@@ -1142,11 +1159,15 @@ __global__ __launch_bounds__(256) void sym_panel_stage_kernel(u16* __restrict__ 
  * block of tile column Kx and P_x the closed row panel x. The workgroup of J = Kx rewrites the
  * D[y][x] the others read: either value is a valid operand (P_x is closed, so old and updated
  * D[y][x] give the same minimum), as in blocked FW's column-panel/rest split. */
-__global__ __launch_bounds__(256) void sym_cross_stage_kernel(const u16* __restrict__ Pa, int ld, int K,
-                                                              int T, const int* __restrict__ own,
-                                                              u16* __restrict__ stage, int Kx, int cx) {
-    __shared__ __attribute__((aligned(16))) u16 s[KB * LDA16];     /* D[b][a] */
-    __shared__ __attribute__((aligned(16))) u16 x[KB * (128 + 8)]; /* P_a[:, J] */
+template <int RM>
+__global__ __launch_bounds__(1024 / RM) void sym_cross_stage_kernel(const u16* __restrict__ Pa, int ld,
+                                                                   int K, int T,
+                                                                   const int* __restrict__ own,
+                                                                   u16* __restrict__ stage, int Kx,
+                                                                   int cx) {
+    constexpr int NT = 1024 / RM;
+    __shared__ __attribute__((aligned(16))) u16 s[KB * LDA16];     /* D[y][x] */
+    __shared__ __attribute__((aligned(16))) u16 x[KB * (128 + 8)]; /* P_x[:, J] */
     __shared__ int s_own[SYM_TMAX], s_cnt;
     FW_CHAIN_PRIO();
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
@@ -1155,21 +1176,21 @@ __global__ __launch_bounds__(256) void sym_cross_stage_kernel(const u16* __restr
     __syncthreads(); /* s_cnt is reused by the second position */
     u16* xj = stage + (size_t)sym_stage_pos(K, J, T, own, s_own, &s_cnt) * (KB * 128);
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int i = tid + q * 256, row = i >> 3, c8 = (i & 7) * 8;
+    for (int q = 0; q < 512 / NT; ++q) {
+        const int i = tid + q * NT, row = i >> 3, c8 = (i & 7) * 8;
         *reinterpret_cast<uint4*>(s + row * LDA16 + c8) =
             *reinterpret_cast<const uint4*>(ak + row * 128 + c8);
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int i = tid + q * 256, row = i >> 4, c8 = (i & 15) * 8;
+    for (int q = 0; q < 1024 / NT; ++q) {
+        const int i = tid + q * NT, row = i >> 4, c8 = (i & 15) * 8;
         *reinterpret_cast<uint4*>(x + row * (128 + 8) + c8) =
             *reinterpret_cast<const uint4*>(Pa + (size_t)row * ld + (size_t)J * 128 + c8);
     }
-    uint32_t acc[4][4];
+    uint32_t acc[RM][4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const uint4 v = *reinterpret_cast<const uint4*>(xj + (4 * ty + r) * 128 + 8 * tx);
+    for (int r = 0; r < RM; ++r) {
+        const uint4 v = *reinterpret_cast<const uint4*>(xj + (RM * ty + r) * 128 + 8 * tx);
         acc[r][0] = v.x;
         acc[r][1] = v.y;
         acc[r][2] = v.z;
@@ -1178,14 +1199,14 @@ __global__ __launch_bounds__(256) void sym_cross_stage_kernel(const u16* __restr
     __syncthreads();
 #pragma unroll 2
     for (int m = 0; m < KB; m += 4) {
-        uint2 a[4];
+        uint2 a[RM];
         uint4 b[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) a[r] = *reinterpret_cast<const uint2*>(s + (4 * ty + r) * LDA16 + m);
+        for (int r = 0; r < RM; ++r) a[r] = *reinterpret_cast<const uint2*>(s + (RM * ty + r) * LDA16 + m);
 #pragma unroll
         for (int q = 0; q < 4; ++q) b[q] = *reinterpret_cast<const uint4*>(x + (m + q) * (128 + 8) + 8 * tx);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < RM; ++r) {
             const uint32_t p[4] = {splat(a[r].x & 0xFFFFu), splat(a[r].x >> 16),
                                    splat(a[r].y & 0xFFFFu), splat(a[r].y >> 16)};
 #pragma unroll
@@ -1198,8 +1219,8 @@ __global__ __launch_bounds__(256) void sym_cross_stage_kernel(const u16* __restr
         }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-        *reinterpret_cast<uint4*>(xj + (4 * ty + r) * 128 + 8 * tx) =
+    for (int r = 0; r < RM; ++r)
+        *reinterpret_cast<uint4*>(xj + (RM * ty + r) * 128 + 8 * tx) =
             make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
 }
 
@@ -1747,7 +1768,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
             /* straight from the staged blocks: closure, then row panel (+ the owner's rows) */
             u16* prow = me == o ? d + (size_t)(k0 - row0) * ld : nullptr;
             sym_diag_stage_kernel<<<1, 256, 0, cs>>>(P, ld, K, k0, T, down, grecv, prow);
-            sym_panel_stage_kernel<<<T, 256, 0, cs>>>(P, ld, K, k0, T, down, grecv, prow);
+            sym_panel_stage_kernel<SYM_RM><<<T, 1024 / SYM_RM, 0, cs>>>(P, ld, K, k0, T, down, grecv, prow);
             SRT_HIPCHK(hipGetLastError());
             SRT_HIPCHK(hipEventRecord(sc->ready[k & 1], cs));
             return SRT_OK;
@@ -1762,11 +1783,9 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
             u16* sb = grecv + ((size_t)T + 1) * blk;
             for (int q = 0; q < R; q++) cnt[q] = 0;
             for (int J = 0; J < T; J++) cnt[sym_kept(K, J) ? o : own[J]]++;
-            if (cnt[me]) {
-                sym_contrib_pack_kernel<<<T, 256, 0, cs>>>(d, ld, row0, tb, K, k0, T, down, me, sa);
-                sym_contrib_pack_kernel<<<T, 256, 0, cs>>>(d, ld, row0, tb, K, k0 + KB, T, down, me,
-                                                           sb);
-            }
+            if (cnt[me]) /* both halves in one launch */
+                sym_contrib_pack_kernel<<<2 * T, 256, 0, cs>>>(d, ld, row0, tb, K, k0, T, down, me, sa,
+                                                               sb);
             SRT_HIPCHK(hipGetLastError());
             int r = srt_coll_group_begin(comm);
             size_t off = 0;
@@ -1784,10 +1803,10 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
             u16* prow_b = me == o ? prow_a + (size_t)KB * ld : nullptr;
             u16* Pb = P + (size_t)KB * ld;
             sym_diag_stage_kernel<<<1, 256, 0, cs>>>(P, ld, K, k0, T, down, sa, prow_a);
-            sym_panel_stage_kernel<<<T, 256, 0, cs>>>(P, ld, K, k0, T, down, sa, prow_a);
-            sym_cross_stage_kernel<<<T, 256, 0, cs>>>(P, ld, K, T, down, sb, K, 0);
+            sym_panel_stage_kernel<SYM_RM><<<T, 1024 / SYM_RM, 0, cs>>>(P, ld, K, k0, T, down, sa, prow_a);
+            sym_cross_stage_kernel<SYM_RM><<<T, 1024 / SYM_RM, 0, cs>>>(P, ld, K, T, down, sb, K, 0);
             sym_diag_stage_kernel<<<1, 256, 0, cs>>>(Pb, ld, K, k0 + KB, T, down, sb, prow_b);
-            sym_panel_stage_kernel<<<T, 256, 0, cs>>>(Pb, ld, K, k0 + KB, T, down, sb, prow_b);
+            sym_panel_stage_kernel<SYM_RM><<<T, 1024 / SYM_RM, 0, cs>>>(Pb, ld, K, k0 + KB, T, down, sb, prow_b);
             SRT_HIPCHK(hipGetLastError());
             SRT_HIPCHK(hipEventRecord(sc->ready[k & 1], cs));
             return SRT_OK;
@@ -1828,9 +1847,9 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
                 u16* Pq = P + (size_t)q * KB * ld;
                 u16* prow = me == own[K] ? d + (size_t)(kq - row0) * ld : nullptr;
                 sym_diag_stage_kernel<<<1, 256, 0, cs>>>(Pq, ld, K, kq, T, down, sq[q], prow);
-                sym_panel_stage_kernel<<<T, 256, 0, cs>>>(Pq, ld, K, kq, T, down, sq[q], prow);
+                sym_panel_stage_kernel<SYM_RM><<<T, 1024 / SYM_RM, 0, cs>>>(Pq, ld, K, kq, T, down, sq[q], prow);
                 for (int y = q + 1; y < 4; y++) /* P_q into the later quarters' staged rows */
-                    sym_cross_stage_kernel<<<T, 256, 0, cs>>>(Pq, ld, K0 + (y >> 1), T, down, sq[y], K,
+                    sym_cross_stage_kernel<SYM_RM><<<T, 1024 / SYM_RM, 0, cs>>>(Pq, ld, K0 + (y >> 1), T, down, sq[y], K,
                                                               (q & 1) * KB);
             }
             SRT_HIPCHK(hipGetLastError());
