@@ -1800,7 +1800,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
             const int r2 = srt_coll_group_end(comm);
             if (r || r2) return r ? r : r2;
             u16* prow_a = me == o ? d + (size_t)(k0 - row0) * ld : nullptr;
-            u16* prow_b = me == o ? prow_a + (size_t)KB * ld : nullptr;
+            u16* prow_b = prow_a ? prow_a + (size_t)KB * ld : nullptr;
             u16* Pb = P + (size_t)KB * ld;
             sym_diag_stage_kernel<<<1, 256, 0, cs>>>(P, ld, K, k0, T, down, sa, prow_a);
             sym_panel_stage_kernel<SYM_RM><<<T, 1024 / SYM_RM, 0, cs>>>(P, ld, K, k0, T, down, sa, prow_a);
