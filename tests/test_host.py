@@ -262,3 +262,34 @@ def test_range_check(native):
     src2, dst2 = np.array([0, 0], np.int32), np.array([1, 1], np.int32)
     e2 = Edges(2, 0, 2, src2.ctypes.data, dst2.ctypes.data, lat2.ctypes.data, np.zeros(2).ctypes.data)
     assert native.srt_latency_quantum(ctypes.byref(e2), ctypes.byref(q), ctypes.byref(mw)) == -6
+
+
+# ---- bench.py parity helpers (the N > 1 check of the driver's scaling run) ------------------------
+def test_bench_parity_rows_cover_first_and_last_rank(native):
+    """At N ranks the bench checks rows of rank 0 and of the last rank (including each one's
+    last row), gathered to rank 0; the kernel-free helpers are plain host code."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+
+    class FakeCtx:
+        world, rank = 8, 0
+    n = 32768
+    blocks = [(q * 4096, (q + 1) * 4096) for q in range(8)]
+    rows = bench.parity_rows(FakeCtx(), lambda q: blocks[q], n, 4)
+    assert rows[0] == 0 and 4095 in rows and 28672 in rows and n - 1 in rows
+    assert all(r < 4096 or r >= 28672 for r in rows)
+    # compare_rows: the diagonal is ignored, reliability is judged on t > s only
+    sample = np.array([0, 3], np.int32)
+    lat = np.arange(2 * 6, dtype=np.uint64).reshape(2, 6)
+    rel = np.linspace(0.5, 1.0, 12).reshape(2, 6)
+    lat2, rel2 = lat.copy(), rel.copy()
+    lat2[0, 0] += 7          # diagonal: own rule, not compared
+    rel2[1, 1] = 0.0         # lower triangle of row 3: the mirror, not compared
+    r = bench.compare_rows(sample, 6, lat2, rel2, lat, rel)
+    assert r["lat_bit_exact"] and r["rel_max_rel_err_upper"] == 0.0 and r["rel_exact_frac_upper"] == 1.0
+    lat2[1, 5] += 1
+    rel2[1, 4] *= 1.0 + 1e-9
+    r = bench.compare_rows(sample, 6, lat2, rel2, lat, rel)
+    assert not r["lat_bit_exact"] and r["rel_max_rel_err_upper"] > 0.0
