@@ -494,15 +494,22 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
     const int2* __restrict__ rowptr, const void* __restrict__ cav,
     const double* __restrict__ r, const int32_t* __restrict__ inv, uint32_t* __restrict__ lat,
     double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ ws, int nb, int bcap,
-    int* __restrict__ overflow, unsigned long long* __restrict__ prof = nullptr) {
+    int* __restrict__ overflow, unsigned long long* __restrict__ prof = nullptr, int two = 0) {
     /* CMP: cav holds the compact arcs and r the table of distinct reliabilities */
+    /* two (SRT_WG_TWO): a step settles the entries of buckets d and d + 1 present at its start.
+     * An entry at d + 1 is final then (every unsettled vertex is at >= d and arcs are >= 1
+     * quantum), and its tight predecessors are at <= d: settled, or level 0 of this step. The
+     * level-0 entries come first in the step's index order; a chunk holding both levels stores its
+     * level-0 reliabilities before a full barrier and only then loads the level-1 ones. Pushes
+     * during the step may append to bucket d + 1: bst[] keeps each bucket's consumed prefix. */
     static_assert(!CMP || ORIG, "compact arcs key ties on u: original vertex order only");
     const uint4* __restrict__ ca = reinterpret_cast<const uint4*>(cav);
     const uint2* __restrict__ cc = reinterpret_cast<const uint2*>(cav);
     unsigned long long pacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long pt = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     extern __shared__ uint32_t sd[]; /* packed distances, relabelled order */
-    __shared__ uint32_t bcnt[256]; /* entries per bucket; the search ballots on bcnt > 0 */
+    __shared__ uint32_t bcnt[256]; /* entries per bucket; the search ballots on bcnt > bst */
+    __shared__ uint32_t bst[256];  /* consumed prefix of each bucket (two-level steps) */
     __shared__ int s_beg[WG], s_excl[WG], s_wtot[WG / WL];
     __shared__ unsigned long long s_best[WG];
     __shared__ int s_ovf;
@@ -523,7 +530,10 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
          * end (no full-row initialisation pass) */
         if (!ORIG)
             for (int v = tid; v < n; v += WG) relp[v] = 0.0;
-        for (int b = tid; b < nb; b += WG) bcnt[b] = 0;
+        for (int b = tid; b < nb; b += WG) {
+            bcnt[b] = 0;
+            bst[b] = 0;
+        }
         __syncthreads();
         if (tid == 0) {
             s_ovf = 0;
@@ -550,34 +560,45 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
              * are visible), and nothing writes it before every wave has passed the next scan
              * barrier -- no workgroup barrier and broadcast here */
             int found = -1;
-            {
-                const uint32_t p0 = d & bm;
-                for (int q = 0; q < nb && found < 0; q += WL) {
-                    const int pos = (int)((p0 + (uint32_t)q + (uint32_t)lane) & bm);
-                    const bool set = q + lane < nb && bcnt[pos] != 0u;
-                    const unsigned long long bal = __ballot(set);
-                    if (bal) found = q + __ffsll((long long)bal) - 1;
-                }
+            const uint32_t p0 = d & bm;
+            for (int q = 0; q < nb && found < 0; q += WL) {
+                const int pos = (int)((p0 + (uint32_t)q + (uint32_t)lane) & bm);
+                const bool set = q + lane < nb && bcnt[pos] > bst[pos];
+                const unsigned long long bal = __ballot(set);
+                if (bal) found = q + __ffsll((long long)bal) - 1;
             }
             if (found < 0) break;
+            /* the buckets skipped over are empty (a searching wave reads either their old or
+             * their zeroed counts: empty both ways) and take no push before their value wraps */
+            if (two && tid < found) {
+                bcnt[(p0 + (uint32_t)tid) & bm] = 0;
+                bst[(p0 + (uint32_t)tid) & bm] = 0;
+            }
             d += (uint32_t)found;
-            const int b = (int)(d & bm);
-            const int cnt = min((int)bcnt[b], bcap);
-            /* bcnt[b] is zeroed after the first chunk's scan barrier (every thread has read cnt
-             * by then): no push of this step targets b (nd >= d + 1, and the ring is longer than
-             * the largest weight), and the next search follows this step's last barrier */
+            const int b = (int)(d & bm), b1 = (int)((d + 1u) & bm);
+            const int st0 = (int)bst[b], st1 = two ? (int)bst[b1] : 0;
+            const int n0 = max(0, min((int)bcnt[b], bcap) - st0);
+            const int n1 = two ? max(0, min((int)bcnt[b1], bcap) - st1) : 0;
+            const int cnt = n0 + n1;
+            /* bucket b is reset after the first chunk's scan barrier (every thread has read its
+             * counts by then): no push of this step targets b (nd >= d + 1, and the ring is longer
+             * than the largest weight), and the next search follows this step's last barrier;
+             * bucket d + 1 keeps its count and records the consumed prefix */
             WG_PT(1);
             if (PROF && tid == 0) pacc[6]++;
-            const uint2* bk = buckets + (size_t)b * bcap;
+            const uint2* bk = buckets + (size_t)b * bcap + st0;
+            const uint2* bk1 = buckets + (size_t)b1 * bcap + st1;
             for (int c0 = 0; c0 < cnt; c0 += WG) {
                 if (PROF && tid == 0) pacc[7]++;
                 const int i = c0 + tid;
+                const int lvl = i >= n0; /* 1: an entry of bucket d + 1 */
+                const uint32_t dl = d + (uint32_t)lvl;
                 int v = -1, beg = 0, deg = 0;
                 uint2 en = make_uint2(0u, 0u);
-                if (i < cnt) en = ld_coherent2(bk + i);
+                if (i < cnt) en = ld_coherent2(lvl ? bk1 + (i - n0) : bk + i);
                 if (i < cnt) {
                     v = (int)(en.x & 0x1FFFFu);
-                    if (wg_get(sd, (uint32_t)v) == d) {
+                    if (wg_get(sd, (uint32_t)v) == dl) {
                         beg = (int)en.y;
                         deg = (int)(en.x >> 17);
                         if ((uint32_t)deg == WG_DEGC) {
@@ -595,13 +616,17 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                 if (lane == 0) s_wtot[wv] = wtot;
                 WG_LDS_BARRIER();
                 WG_PT(11);
-                if (c0 == 0 && tid == 0) bcnt[b] = 0;
+                if (c0 == 0 && tid == 0) {
+                    bcnt[b] = 0;
+                    bst[b] = 0;
+                    if (two) bst[b1] = (uint32_t)(st1 + n1);
+                }
                 int base = 0, total = 0;
                 for (int q = 0; q < WG / WL; ++q) {
                     base += q < wv ? s_wtot[q] : 0;
                     total += s_wtot[q];
                 }
-                s_beg[tid] = beg;
+                s_beg[tid] = beg | (lvl << 31); /* the owner's level rides in the top bit */
                 s_excl[tid] = base + wex;
                 s_best[tid] = ~0ull;
                 WG_LDS_BARRIER();
@@ -628,9 +653,9 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                     for (int j = 0; j < WG_AK; ++j)
                         if (a0 + j * WG + tid < total) {
                             if constexpr (CMP)
-                                ec[j] = cc[s_beg[own[j]] + rk[j]];
+                                ec[j] = cc[(s_beg[own[j]] & 0x7FFFFFFF) + rk[j]];
                             else
-                                e[j] = ca[s_beg[own[j]] + rk[j]];
+                                e[j] = ca[(s_beg[own[j]] & 0x7FFFFFFF) + rk[j]];
                         }
 #pragma unroll
                     for (int j = 0; j < WG_AK; ++j) {
@@ -650,7 +675,8 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                             degu = e[j].w;
                         }
                         const uint32_t du = wg_get(sd, u);
-                        const uint32_t nd = d + wk;
+                        const uint32_t dow = d + ((uint32_t)s_beg[own[j]] >> 31); /* owner's D */
+                        const uint32_t nd = dow + wk;
                         if (nd < du) {
                             if (nd >= WG_INF) {
                                 s_ovf = 1; /* not representable in 10 bits */
@@ -666,7 +692,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                         }
                         /* canonical predecessor key (D[u], rank of the arc in the row), with u
                          * carried along so the settle step needs no second arc load */
-                        if (du != WG_INF && du + wk == d) {
+                        if (du != WG_INF && du + wk == dow) {
                             if constexpr (CMP) /* (D[u], u) with the arc's reliability index */
                                 atomicMin(&s_best[own[j]], ((unsigned long long)du << 40) |
                                                                ((unsigned long long)u << 8) | ridx);
@@ -686,11 +712,37 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                  * chunk's vertices: their reliability stores visible) and after its last (the
                  * next step's search and entry loads follow with no other barrier: this pass's
                  * bucket stores visible); an LDS barrier in between */
-                if (c0 == 0 || c0 + WG >= cnt)
+                const bool mixed = two && n1 > 0 && c0 + WG > n0; /* level-1 lanes in this chunk */
+                if (c0 == 0 || c0 + WG >= cnt || mixed)
                     __syncthreads();
                 else
                     WG_LDS_BARRIER();
                 WG_PT(3);
+                /* a chunk with level-1 lanes: its level-0 lanes store their reliability now, and
+                 * the level-1 lanes (children of any level-0 vertex of the step) load theirs after
+                 * a full barrier */
+                if (mixed) {
+                    if (v >= 0 && !lvl) {
+                        double xa = 1.0, xb = 1.0;
+                        if (v != s) {
+                            const unsigned long long key = s_best[tid];
+                            xa = 0.0;
+                            if (key != ~0ull) {
+                                if constexpr (CMP) {
+                                    xa = ld_coherent(relp + (uint32_t)((key >> 8) & 0x1FFFFu));
+                                    xb = r[key & 0xFFu];
+                                } else {
+                                    xa = ld_coherent(relp + (uint32_t)(key & 0xFFFFFu));
+                                    xb = r[beg + (int)((key >> 20) & 0xFFFFFu)];
+                                }
+                            }
+                        }
+                        relp[v] = xa * xb;
+                        v = -1; /* settled: no deferred store */
+                    }
+                    __threadfence_block();
+                    __syncthreads();
+                }
                 /* settle: path-order reliability from the canonical predecessor, issued now and
                  * stored one chunk later */
                 if (v >= 0) {
@@ -738,7 +790,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
 }
 
 /* largest n the packed LDS row holds beside the kernel's static LDS (1024 threads: ~18 KB) */
-int srt_wgsssp_max_n(void) { return 3 * ((140 * 1024) / 4); }
+int srt_wgsssp_max_n(void) { return 3 * ((138 * 1024) / 4); }
 
 /* Rows [src_begin, src_end) by the workgroup kernel (undirected graphs, n <= srt_wgsssp_max_n,
  * max arc weight < 256 quanta). ovf[i] = 1 marks a source to recompute (distance above 1022 or a
@@ -747,8 +799,12 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
                     uint32_t max_w, int src_begin, int src_end, const int32_t* srcs, uint32_t* lat,
                     double* rel, int* ovf, hipStream_t st, const uint8_t* ridx,
                     const double* rtab) {
+    /* two-level steps push up to d + 1 + max_w: the ring then needs max_w + 2 buckets */
+    const char* twoenv = getenv("SRT_WG_TWO");
+    int two = twoenv ? atoi(twoenv) != 0 : 1;
+    if (max_w + 2u > 256u) two = 0;
     int nb = 1;
-    while ((uint32_t)nb <= max_w) nb <<= 1;
+    while ((uint32_t)nb <= max_w + (uint32_t)two) nb <<= 1;
     if (nb > 256 || n > srt_wgsssp_max_n()) {
         srt_set_error("wgsssp: n = %d or max arc weight %u outside the kernel's range", n, max_w);
         return SRT_E_ARG;
@@ -805,13 +861,13 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
             wgsssp_kernel<1024, true, true, true><<<(unsigned)slots, 1024, dyn, st>>>(
                 n, src_begin, srcs, nsrc, rowptr, ca, rtab, inv, lat, rel, (size_t)n, ws, nb, bcap,
-                ovf, prof);
+                ovf, prof, two);
         } else {
             SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
             wgsssp_kernel<1024, true><<<(unsigned)slots, 1024, dyn, st>>>(
                 n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap,
-                ovf, prof);
+                ovf, prof, two);
         }
         SRT_HIPCHK(hipGetLastError());
         unsigned long long* h = (unsigned long long*)calloc(slots * 12, sizeof(*h));
@@ -841,18 +897,20 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
         SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, false, true, true>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
         wgsssp_kernel<1024, false, true, true><<<(unsigned)slots, 1024, dyn, st>>>(
-            n, src_begin, srcs, nsrc, rowptr, ca, rtab, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf);
+            n, src_begin, srcs, nsrc, rowptr, ca, rtab, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf,
+            nullptr, two);
     } else if (!inv) { /* the graph in original order: reliability straight into the output rows */
         SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, false, true>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
         wgsssp_kernel<1024, false, true><<<(unsigned)slots, 1024, dyn, st>>>(
-            n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf);
+            n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf,
+            nullptr, two);
     } else {
         SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
         wgsssp_kernel<1024><<<(unsigned)slots, 1024, dyn, st>>>(n, src_begin, srcs, nsrc, rowptr, ca, r,
                                                                inv, lat, rel, (size_t)n, ws, nb, bcap,
-                                                               ovf);
+                                                               ovf, nullptr, two);
     }
     SRT_HIPCHK(hipGetLastError());
     SRT_HIPCHK(hipFreeAsync(ws, st));
