@@ -400,7 +400,8 @@ int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, con
  * distance fits (d(a, b) <= 2 ecc(s0)). Undirected graphs only.
  * ------------------------------------------------------------------------------------------ */
 #define WG_INF 1023u
-#define WG_AK 4 /* arc windows in flight per lane */
+#define WG_AK 4     /* arc windows in flight per lane */
+#define WG_NBLK 256 /* 64-arc blocks indexed per chunk (arcs beyond: whole-chunk search) */
 
 static __device__ __forceinline__ uint32_t wg_get(const uint32_t* sd, uint32_t v) {
     return (sd[v / 3] >> (10 * (v % 3))) & 1023u;
@@ -473,8 +474,9 @@ __global__ void wg_arcs_cmp_kernel(int n, const int2* __restrict__ rowptr, const
 }
 
 /* PROF (tools only, SRT_WGSSSP_PROF=1): thread 0 accumulates shader-clock cycles per phase and
- * step counts into prof[block * 12 + k]: 0 init, 1 bucket search, 2 chunk head (sums and the
- * full barrier; 10 entry load, 11 scan barrier), 3 arcs,
+ * step counts into prof[block * 16 + k]: 0 init, 1 bucket search, 2 chunk head (sums and the
+ * full barrier; 10 entry load, 11 scan barrier), 3 arcs (12 owner search, 13 arc-load wait, 14
+ * relaxations; 3 itself: the deferred store and the post-arc barrier),
  * 4 settle, 5 output, 6 steps, 7 chunks, 8 arc windows, 9 sources */
 #define WG_PT(k)                                                        \
     do {                                                                \
@@ -505,12 +507,16 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
     static_assert(!CMP || ORIG, "compact arcs key ties on u: original vertex order only");
     const uint4* __restrict__ ca = reinterpret_cast<const uint4*>(cav);
     const uint2* __restrict__ cc = reinterpret_cast<const uint2*>(cav);
-    unsigned long long pacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long pacc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long pt = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     extern __shared__ uint32_t sd[]; /* packed distances, relabelled order */
     __shared__ uint32_t bcnt[256]; /* entries per bucket; the search ballots on bcnt > bst */
     __shared__ uint32_t bst[256];  /* consumed prefix of each bucket (two-level steps) */
-    __shared__ int s_beg[WG], s_excl[WG], s_wtot[WG / WL];
+    /* s_off[i] = row begin - exclusive arc offset of chunk entry i (arc a of owner i is at
+     * a + s_off[i]); s_blk[B] = the owner of chunk arc 64 B, so a wave's owner search runs over
+     * [s_blk[B], s_blk[B + 1]] (a few entries) instead of the whole chunk */
+    __shared__ int s_off[WG], s_excl[WG], s_wtot[WG / WL];
+    __shared__ uint16_t s_blk[WG_NBLK];
     __shared__ unsigned long long s_best[WG];
     __shared__ int s_ovf;
     const int tid = threadIdx.x, lane = tid & (WL - 1), wv = tid >> 6;
@@ -626,9 +632,21 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                     base += q < wv ? s_wtot[q] : 0;
                     total += s_wtot[q];
                 }
-                s_beg[tid] = beg | (lvl << 31); /* the owner's level rides in the top bit */
-                s_excl[tid] = base + wex;
+                const int x = base + wex;
+                s_off[tid] = beg - x;
+                s_excl[tid] = x;
                 s_best[tid] = ~0ull;
+                {
+                    int B = (x + 63) >> 6; /* first block start in [x, x + deg): usually 0 or 1 */
+                    const int Be = min((x + deg - 1) >> 6, WG_NBLK - 1);
+                    if (deg > 0 && B <= Be) {
+                        s_blk[B] = (uint16_t)tid;
+                        for (++B; B <= Be; ++B) s_blk[B] = (uint16_t)tid; /* hubs */
+                    }
+                }
+                /* the owner of the last arc closes the last block's range */
+                if (deg > 0 && x + deg == total && (total - 1) / WL + 1 < WG_NBLK)
+                    s_blk[(total - 1) / WL + 1] = (uint16_t)tid;
                 WG_LDS_BARRIER();
                 WG_PT(2);
                 /* WG_AK arc windows per pass: the owner searches (fixed-step, unrolled) and the
@@ -636,27 +654,64 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                  * latencies overlap instead of adding up */
                 for (int a0 = 0; a0 < total; a0 += WG * WG_AK) {
                     if (PROF && tid == 0) pacc[8]++;
-                    int own[WG_AK], rk[WG_AK];
+                    int own[WG_AK];
                     uint4 e[WG_AK];
                     uint2 ec[WG_AK];
+                    /* owner: the last entry whose exclusive offset is <= a, searched between the
+                     * owners of the wave's block start and of the next block start (wave-uniform
+                     * bounds, one step count for all windows) */
+                    int hi[WG_AK], len = 0;
+                    const int totu = __builtin_amdgcn_readfirstlane(total);
+#pragma unroll
+                    for (int j = 0; j < WG_AK; ++j) { /* all the bound reads issued together */
+                        const int B = min((a0 + j * WG) / WL + __builtin_amdgcn_readfirstlane(wv),
+                                          WG_NBLK - 2);
+                        own[j] = s_blk[B];
+                        hi[j] = s_blk[B + 1];
+                    }
 #pragma unroll
                     for (int j = 0; j < WG_AK; ++j) {
-                        const int a = a0 + j * WG + tid;
-                        int lo = 0; /* owner: the last entry whose exclusive offset is <= a */
-#pragma unroll
-                        for (int step = WG / 2; step >= 1; step >>= 1)
-                            if (s_excl[lo + step] <= a) lo = lo + step;
-                        own[j] = lo;
-                        rk[j] = a - s_excl[lo];
+                        const int B = (a0 + j * WG) / WL + __builtin_amdgcn_readfirstlane(wv);
+                        if (B * WL >= totu) { /* no arcs for this wave in the window */
+                            own[j] = 0;
+                            hi[j] = 0;
+                        } else if (B + 1 < WG_NBLK) {
+                            own[j] = __builtin_amdgcn_readfirstlane(own[j]);
+                            hi[j] = __builtin_amdgcn_readfirstlane(hi[j]);
+                        } else {
+                            own[j] = 0;
+                            hi[j] = WG - 1;
+                        }
+                        len = max(len, hi[j] - own[j]);
                     }
+                    len = __builtin_amdgcn_readfirstlane(len);
+                    for (int step = len > 0 ? 1 << (31 - __builtin_clz(len)) : 0; step >= 1;
+                         step >>= 1) {
+                        /* clamped at hi: taking hi when s_excl[hi] <= a is the answer (the owner
+                         * is at most hi), so the lifting stays exact */
+                        int q[WG_AK];
+#pragma unroll
+                        for (int j = 0; j < WG_AK; ++j) {
+                            q[j] = min(own[j] + step, hi[j]);
+                            q[j] = s_excl[q[j]] <= a0 + j * WG + tid ? q[j] : own[j];
+                        }
+#pragma unroll
+                        for (int j = 0; j < WG_AK; ++j) own[j] = q[j];
+                    }
+                    WG_PT(12);
 #pragma unroll
                     for (int j = 0; j < WG_AK; ++j)
                         if (a0 + j * WG + tid < total) {
+                            const int arc = a0 + j * WG + tid + s_off[own[j]];
                             if constexpr (CMP)
-                                ec[j] = cc[(s_beg[own[j]] & 0x7FFFFFFF) + rk[j]];
+                                ec[j] = cc[arc];
                             else
-                                e[j] = ca[(s_beg[own[j]] & 0x7FFFFFFF) + rk[j]];
+                                e[j] = ca[arc];
                         }
+                    if (PROF) {
+                        __builtin_amdgcn_s_waitcnt(0); /* profile only: the arc loads' wait */
+                        WG_PT(13);
+                    }
 #pragma unroll
                     for (int j = 0; j < WG_AK; ++j) {
                         if (a0 + j * WG + tid >= total) continue;
@@ -675,7 +730,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                             degu = e[j].w;
                         }
                         const uint32_t du = wg_get(sd, u);
-                        const uint32_t dow = d + ((uint32_t)s_beg[own[j]] >> 31); /* owner's D */
+                        const uint32_t dow = d + (uint32_t)(c0 + own[j] >= n0); /* owner's D */
                         const uint32_t nd = dow + wk;
                         if (nd < du) {
                             if (nd >= WG_INF) {
@@ -697,10 +752,13 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                                 atomicMin(&s_best[own[j]], ((unsigned long long)du << 40) |
                                                                ((unsigned long long)u << 8) | ridx);
                             else
-                                atomicMin(&s_best[own[j]], ((unsigned long long)du << 40) |
-                                                               ((unsigned long long)rk[j] << 20) | u);
+                                atomicMin(&s_best[own[j]],
+                                          ((unsigned long long)du << 40) |
+                                              ((unsigned long long)(a0 + j * WG + tid - s_excl[own[j]]) << 20) |
+                                              u);
                         }
                     }
+                    WG_PT(14);
                 }
                 /* the lane's vertex of the previous chunk: its two loads (issued at that chunk's
                  * settle) have had this chunk's head and arcs to arrive */
@@ -786,11 +844,11 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
         WG_PT(5);
     }
     if (PROF && tid == 0)
-        for (int k = 0; k < 12; ++k) prof[blockIdx.x * 12 + k] = pacc[k];
+        for (int k = 0; k < 16; ++k) prof[blockIdx.x * 16 + k] = pacc[k];
 }
 
 /* largest n the packed LDS row holds beside the kernel's static LDS (1024 threads: ~18 KB) */
-int srt_wgsssp_max_n(void) { return 3 * ((138 * 1024) / 4); }
+int srt_wgsssp_max_n(void) { return 3 * ((137 * 1024) / 4); }
 
 /* Rows [src_begin, src_end) by the workgroup kernel (undirected graphs, n <= srt_wgsssp_max_n,
  * max arc weight < 256 quanta). ovf[i] = 1 marks a source to recompute (distance above 1022 or a
@@ -855,7 +913,7 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     const char* penv = getenv("SRT_WGSSSP_PROF"); /* tools: per-phase cycle counts on stderr */
     if (penv && atoi(penv) > 0) {
         unsigned long long* prof = NULL;
-        SRT_HIPCHK(hipMalloc((void**)&prof, slots * 12 * sizeof(unsigned long long)));
+        SRT_HIPCHK(hipMalloc((void**)&prof, slots * 16 * sizeof(unsigned long long)));
         if (cmp) {
             SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true, true, true>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
@@ -870,13 +928,14 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
                 ovf, prof, two);
         }
         SRT_HIPCHK(hipGetLastError());
-        unsigned long long* h = (unsigned long long*)calloc(slots * 12, sizeof(*h));
-        SRT_HIPCHK(hipMemcpyAsync(h, prof, slots * 12 * sizeof(*h), hipMemcpyDeviceToHost, st));
+        unsigned long long* h = (unsigned long long*)calloc(slots * 16, sizeof(*h));
+        SRT_HIPCHK(hipMemcpyAsync(h, prof, slots * 16 * sizeof(*h), hipMemcpyDeviceToHost, st));
         SRT_HIPCHK(hipStreamSynchronize(st));
-        double tot[12] = {0};
+        double tot[16] = {0};
         for (size_t b = 0; b < slots; ++b)
-            for (int k = 0; k < 12; ++k) tot[k] += (double)h[b * 12 + k];
-        const double cyc = tot[0] + tot[1] + tot[2] + tot[3] + tot[4] + tot[5] + tot[10] + tot[11];
+            for (int k = 0; k < 16; ++k) tot[k] += (double)h[b * 16 + k];
+        const double cyc = tot[0] + tot[1] + tot[2] + tot[3] + tot[4] + tot[5] + tot[10] + tot[11] +
+                           tot[12] + tot[13] + tot[14];
         fprintf(stderr,
                 "[wgsssp prof] blocks %zu sources %.0f: cycles/source %.0f = init %.1f%% search "
                 "%.1f%% head %.1f%% (entry load %.1f%%, scan barrier %.1f%%, sums + full "
@@ -884,8 +943,13 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
                 "%.1f chunks %.1f arc windows %.1f; cycles per step %.0f\n",
                 slots, tot[9], cyc / tot[9], 100 * tot[0] / cyc, 100 * tot[1] / cyc,
                 100 * (tot[2] + tot[10] + tot[11]) / cyc, 100 * tot[10] / cyc, 100 * tot[11] / cyc,
-                100 * tot[2] / cyc, 100 * tot[3] / cyc, 100 * tot[4] / cyc, 100 * tot[5] / cyc,
-                tot[6] / tot[9], tot[7] / tot[9], tot[8] / tot[9], cyc / tot[6]);
+                100 * tot[2] / cyc, 100 * (tot[3] + tot[12] + tot[13] + tot[14]) / cyc,
+                100 * tot[4] / cyc, 100 * tot[5] / cyc, tot[6] / tot[9], tot[7] / tot[9],
+                tot[8] / tot[9], cyc / tot[6]);
+        fprintf(stderr,
+                "[wgsssp prof] arcs: owner search %.1f%% arc-load wait %.1f%% relaxations %.1f%% "
+                "deferred store + post-arc barrier %.1f%%\n",
+                100 * tot[12] / cyc, 100 * tot[13] / cyc, 100 * tot[14] / cyc, 100 * tot[3] / cyc);
         free(h);
         SRT_HIPCHK(hipFree(prof));
     } else if (tenv && atoi(tenv) == 512) {
