@@ -407,11 +407,11 @@ static __device__ __forceinline__ uint32_t wg_get(const uint32_t* sd, uint32_t v
     return (sd[v / 3] >> (10 * (v % 3))) & 1023u;
 }
 
-/* lower the 10-bit field of v to nd if that is smaller; true when this call lowered it */
-static __device__ __forceinline__ bool wg_lower(uint32_t* sd, uint32_t v, uint32_t nd) {
+/* lower the 10-bit field of v to nd if that is smaller; true when this call lowered it. old: the
+ * word as the caller last read it (a stale value only costs one failed CAS) */
+static __device__ __forceinline__ bool wg_lower(uint32_t* sd, uint32_t v, uint32_t nd, uint32_t old) {
     uint32_t* p = sd + v / 3;
     const uint32_t sh = 10 * (v % 3);
-    uint32_t old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     for (;;) {
         const uint32_t cur = (old >> sh) & 1023u;
         if (nd >= cur) return false;
@@ -729,13 +729,14 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                             begu = e[j].z;
                             degu = e[j].w;
                         }
-                        const uint32_t du = wg_get(sd, u);
+                        const uint32_t wu = sd[u / 3];
+                        const uint32_t du = (wu >> (10 * (u % 3))) & 1023u;
                         const uint32_t dow = d + (uint32_t)(c0 + own[j] >= n0); /* owner's D */
                         const uint32_t nd = dow + wk;
                         if (nd < du) {
                             if (nd >= WG_INF) {
                                 s_ovf = 1; /* not representable in 10 bits */
-                            } else if (wg_lower(sd, u, nd)) {
+                            } else if (wg_lower(sd, u, nd, wu)) {
                                 const int b2 = (int)(nd & bm);
                                 const int slot = (int)atomicAdd(&bcnt[b2], 1u);
                                 if (slot < bcap) {
