@@ -213,3 +213,22 @@ def test_workgroup_kernel_forms(gpu, monkeypatch, form, which):
     assert st.dist_enc == 2
     assert np.array_equal(lat, exp["lat_int"])
     assert np.array_equal(rel, exp["rel"])
+
+
+@pytest.mark.parametrize("two", ["0", "1"])
+@pytest.mark.parametrize("lat_max", [2, 20, 127])
+def test_workgroup_kernel_two_level_steps(gpu, monkeypatch, two, lat_max):
+    """SRT_WG_TWO: a Dial step of the workgroup kernel settles buckets d and d + 1 together (the
+    default) or bucket d alone. Weights of 1..2 quanta push into d + 1 during nearly every step
+    (the consumed-prefix counts); 127 quanta is the largest compact-arc weight, where the bucket
+    ring must hold max_w + 2 buckets. Both forms give the exact tables."""
+    monkeypatch.setenv("SRT_SPARSE_WG", "1")
+    monkeypatch.setenv("SRT_WG_TWO", two)
+    g = graphs.barabasi_albert(2000, seed=9, lat_max=lat_max)
+    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                algo=ALGO_SPARSE_SSSP)
+    exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss),
+                       True, oracle.ORC_INT_NS, 8)
+    assert st.dist_enc == 2
+    assert np.array_equal(lat, exp["lat_int"])
+    assert np.array_equal(rel, exp["rel"])
