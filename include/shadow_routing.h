@@ -153,8 +153,8 @@ int srt_gen_complete_device(int32_t n, int32_t ld, int32_t row0, int32_t nrows, 
  * queue, bitmaps: ~8n + n/8 bytes) is LDS-resident for n <= srt_sparse_max_n() and lives in a
  * per-workgroup HBM slot beyond (persistent grid of 2 workgroups per CU; environment variable
  * SRT_SPARSE_WORKSET=hbm forces the HBM form for testing). delta = bucket width in quanta
- * (0 = default). The undirected symmetry rule is NOT applied here: after the rows of every
- * source are assembled, call srt_mirror_lower_device. */
+ * (0 = default). Each row is its own source's (no symmetry rule is applied: see
+ * srt_pair_order). */
 int srt_sparse_max_n(void);
 int srt_sparse_build_device(int32_t n, int32_t directed, const int32_t* rowptr,
                             const int32_t* col, const uint32_t* w, const double* r,
@@ -179,8 +179,6 @@ int srt_sparse_graph_rows_list(const srt_sparse_graph* g, int32_t nsrc, const in
                                uint32_t* lat_rows, double* rel_rows, double* lat_ms_rows,
                                void* stream, srt_build_stats* stats);
 void srt_sparse_graph_free(srt_sparse_graph* g);
-/* rel[s][t] <- rel[t][s] for s > t (undirected symmetry rule), ld x ld device matrix. */
-int srt_mirror_lower_device(int32_t n, int32_t ld, double* rel, void* stream);
 
 /* ---- multi-GPU (one process per GPU; RCCL over xGMI) ----------------------------------- */
 typedef struct srt_comm srt_comm;
@@ -221,6 +219,29 @@ int srt_sparse_allgather(srt_comm* comm, int32_t n, int32_t rows_per_rank, uint3
 /* ---- misc ------------------------------------------------------------------------------ */
 const char* srt_version(void);
 const char* srt_last_error(void); /* thread-local message for the last failing call */
+/* ---- pair order: which cached path the reference serves (pairorder.c) -------------------
+ * Restates the lazy cache of topology.c:1166-1265 + :1900-1981 over tables holding every
+ * source's raw row: a pair is served, in both directions, from the first source run (or, with
+ * use_shortest_path = false, the first direct-edge lookup) that stored it. per_source = 1 for
+ * shortest-path mode (a miss runs source s for every attached target, :1578-1814), 0 for direct
+ * mode (a miss stores the pair s -> t, :1816-1858). Thread-safe; lookups are lock-free once
+ * their pair is stored. */
+typedef struct srt_pair_order srt_pair_order;
+/* called (under the object's lock) with the paths a lookup stored: src -> targets[i] */
+typedef void (*srt_pair_store_fn)(void* ctx, int32_t src, const int32_t* targets, int32_t count);
+srt_pair_order* srt_pair_order_new(int32_t n, int32_t directed, int32_t per_source);
+void srt_pair_order_free(srt_pair_order* po);
+/* v joins the attached set (verticesWithAttachedHosts, topology.c:2231); idempotent */
+int srt_pair_order_attach(srt_pair_order* po, int32_t v);
+/* lookup (s, t): the source vertex of the path served (s or t), after recording the run or store
+ * a miss causes; SRT_E_UNATTACHED if an end is not attached */
+int32_t srt_pair_order_lookup(srt_pair_order* po, int32_t s, int32_t t, srt_pair_store_fn on_store,
+                              void* ctx);
+/* the same without recording anything: -1 while the pair is not stored */
+int32_t srt_pair_order_peek(srt_pair_order* po, int32_t s, int32_t t);
+/* recorded source runs of v (one per attach epoch it ran in) */
+int32_t srt_pair_order_runs(srt_pair_order* po, int32_t v);
+
 int srt_device_count(void);
 int srt_device_sync(int32_t device);
 

@@ -52,12 +52,15 @@ void topology_incrementPathPacketCounter(Topology* top, Address* srcAddress, Add
  * targets the reference computes paths to (topology.c:1604-1656) -- or over every vertex while
  * nothing is attached. Call it after the hosts are attached (controller.c:367); it is idempotent,
  * and the lookups call it lazily: a lookup whose vertex joined the attached set after the last
- * build rebuilds (the reference's cache miss, topology.c:1923-1961). Hands the minimum latency
- * over attached pairs to worker_updateMinTimeJump() (topology.c:1253-1264) once per attach
- * generation, and only when it is below the last value handed over. */
+ * build rebuilds. The tables hold every source's own row; which row serves a pair follows the
+ * reference's lazy cache (the first source run that stored the pair, topology.c:1189-1215,
+ * :1900-1981; see srt_pair_order in shadow_routing.h). Runahead: the lookups hand
+ * worker_updateMinTimeJump() each smaller path latency as their runs store paths, as
+ * _topology_storePathInCache does (topology.c:1253-1264); the eager build itself stores none. */
 int topology_computeShortestPaths(Topology* top, int nGPUs);
 /* Zero-copy view of the current tables (valid until topology_free): n x n over the table's
- * vertices (srt_topology_table_info gives them; every vertex when the table is full). */
+ * vertices (srt_topology_table_info gives them; every vertex when the table is full). Entry
+ * [i][j] is source verts[i]'s own path to verts[j]; a lookup may be served the [j][i] entry. */
 int topology_getTable(Topology* top, const uint32_t** latQ, uint64_t* quantumNs,
                       const double** rel, int* n);
 /* The current table's vertices (increasing), their count, and the f64 path-order ms table (NULL
@@ -87,7 +90,11 @@ int32_t srt_topology_vertex_of_ip(Topology* top, uint32_t ipNet);
 double srt_topology_latency_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet);
 double srt_topology_reliability_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet);
 int srt_topology_increment_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet);
+/* packets counted on the path a lookup (src, dst) is served from; 0 while it is not stored
+ * (computes nothing) */
 uint64_t srt_topology_packet_count_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet);
+/* source vertex of the path a lookup (src, dst) is served from, -1 while not stored (peek) */
+int32_t srt_topology_path_source_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet);
 /* Packet-path consumer (worker.c:541-555): deliver/drop decision, delay in ns and the packet
  * counter for one packet (1 delivered, 0 dropped, < 0 error) or a trace of them. */
 int srt_topology_send_packet_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet, double chance,

@@ -54,9 +54,10 @@ def lib() -> ctypes.CDLL:
         L.orc_sssp_list.restype = ctypes.c_int
         L.orc_sssp_list.argtypes = [ctypes.POINTER(_Graph), ctypes.c_int, ctypes.c_void_p,
                                     ctypes.c_int32, ctypes.c_int] + [ctypes.c_void_p] * 5
-        L.orc_table.restype = ctypes.c_int
-        L.orc_table.argtypes = [ctypes.POINTER(_Graph), ctypes.c_int, ctypes.c_int,
-                                ctypes.c_int] + [ctypes.c_void_p] * 4
+        for fn in (L.orc_table, L.orc_table_raw):
+            fn.restype = ctypes.c_int
+            fn.argtypes = [ctypes.POINTER(_Graph), ctypes.c_int, ctypes.c_int,
+                           ctypes.c_int] + [ctypes.c_void_p] * 4
         _lib = L
     return _lib
 
@@ -125,8 +126,10 @@ def sssp_list(g: EdgeList, sources, mode: int = ORC_INT_NS, nthreads: int = 1):
 
 
 def table(g: EdgeList, use_shortest_path: bool = True, mode: int = ORC_INT_NS,
-          nthreads: int = 1):
-    """Full n x n table as the reference's lookup API would return it for every vertex pair."""
+          nthreads: int = 1, raw: bool = False):
+    """Full n x n table. raw=False: as the reference's lookup API returns every pair when sources
+    run in increasing vertex order (undirected: the row of min(s, t)). raw=True: entry (s, t) is
+    source s's own row (what the product's tables hold; lazy_cache.py picks the serving row)."""
     n = g.n
     out = {
         "lat_int": np.empty((n, n), np.uint64),
@@ -135,7 +138,8 @@ def table(g: EdgeList, use_shortest_path: bool = True, mode: int = ORC_INT_NS,
         "lat_ms": np.empty((n, n), np.float64),
     }
     cg = g._c()
-    rc = lib().orc_table(ctypes.byref(cg), int(bool(use_shortest_path)), mode, nthreads,
+    fn = lib().orc_table_raw if raw else lib().orc_table
+    rc = fn(ctypes.byref(cg), int(bool(use_shortest_path)), mode, nthreads,
                          _ptr(out["lat_int"]), _ptr(out["lat_ref"]), _ptr(out["rel"]),
                          _ptr(out["lat_ms"]))
     if rc:

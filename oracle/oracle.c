@@ -372,8 +372,8 @@ void orc_self_path(const orc_graph* g, int32_t v, uint64_t* lat_int, uint64_t* l
     if (lat_ms) *lat_ms = best_ms;
 }
 
-int orc_table(const orc_graph* g, int use_shortest_path, int mode, int nthreads, uint64_t* lat_int,
-              uint64_t* lat_ref, double* rel, double* lat_ms) {
+static int table_impl(const orc_graph* g, int use_shortest_path, int mode, int nthreads, int raw,
+                      uint64_t* lat_int, uint64_t* lat_ref, double* rel, double* lat_ms) {
     const int32_t n = g->n;
     const size_t nn = (size_t)n * (size_t)n;
     if (!use_shortest_path) {
@@ -412,7 +412,7 @@ int orc_table(const orc_graph* g, int use_shortest_path, int mode, int nthreads,
         return rc;
     }
     if (orc_sssp_rows(g, mode, 0, n, nthreads, lat_int, lat_ref, rel, lat_ms, NULL)) return -1;
-    if (!g->directed) {
+    if (!g->directed && !raw) {
         /* one cache entry per unordered pair, computed from min(s,t) (topology.c:1194-1199) */
         for (int32_t s = 0; s < n; s++)
             for (int32_t t = 0; t < s; t++) {
@@ -428,6 +428,16 @@ int orc_table(const orc_graph* g, int use_shortest_path, int mode, int nthreads,
         orc_self_path(g, v, &lat_int[d], &lat_ref[d], &rel[d], lat_ms ? &lat_ms[d] : NULL);
     }
     return 0;
+}
+
+int orc_table(const orc_graph* g, int use_shortest_path, int mode, int nthreads, uint64_t* lat_int,
+              uint64_t* lat_ref, double* rel, double* lat_ms) {
+    return table_impl(g, use_shortest_path, mode, nthreads, 0, lat_int, lat_ref, rel, lat_ms);
+}
+
+int orc_table_raw(const orc_graph* g, int use_shortest_path, int mode, int nthreads,
+                  uint64_t* lat_int, uint64_t* lat_ref, double* rel, double* lat_ms) {
+    return table_impl(g, use_shortest_path, mode, nthreads, 1, lat_int, lat_ref, rel, lat_ms);
 }
 
 /* ---------------------------------------------------------------------------------------------

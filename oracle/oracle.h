@@ -13,12 +13,18 @@
  *   - diagonal ("shortest path to self") rule          topology.c:1431-1576
  *   - direct mode (use_shortest_path = false)          topology.c:1816-1858, :1948-1958
  *   - one cached entry per unordered pair (symmetry)   topology.c:1189-1215, :1918-1921, :1964-1967
+ *     (orc_table: the pairs as served when sources run in increasing vertex order; the lazy-cache
+ *     order itself is restated in oracle/lazy_cache.py over orc_table_raw's per-source rows)
  *   - delay = ceil(latency_ms * 1e6) ns                worker.c:550-551
  *
  * Tie rule: igraph's Dijkstra keeps the first-settled tight predecessor; igraph
  * is absent from this container, so the canonical rule is Dijkstra with a (distance, vertex index)
  * heap and strict-< relaxation, i.e. pred(s,t) = argmin over tight in-edges (u,t) of (D[s][u], u).
- * Symmetry rule for undirected graphs: the pair {s,t} is computed from source min(s,t) and mirrored.
+ * Which row serves a pair: the reference serves {s,t} from whichever end's source ran first (with
+ * the other end attached), for directed graphs too (topology.c:1194-1199, :1964-1967). orc_table
+ * fixes that order to increasing vertex index (undirected: the row of min(s,t), mirrored);
+ * orc_table_raw keeps every source's own row, and oracle/lazy_cache.py replays a lookup trace in
+ * the reference's order over it.
  * Parallel edges collapse to the (min latency, lowest edge index) edge for a vertex pair.
  *
  * Parity status: multi-vertex routing is "parity unpinned" by the reference's own tests (every
@@ -70,6 +76,11 @@ int orc_sssp_list(const orc_graph* g, int mode, const int32_t* srcs, int32_t k, 
  * value topology_getLatency() returns. Returns 0 on success, -1 if direct mode lacks an edge. */
 int orc_table(const orc_graph* g, int use_shortest_path, int mode, int nthreads,
               uint64_t* lat_int, uint64_t* lat_ref, double* rel, double* lat_ms);
+
+/* orc_table without the pair rule: entry (s, t) is what source s computes for t (its raw row),
+ * the diagonal rule on the diagonal; direct mode: the direct edge s -> t. */
+int orc_table_raw(const orc_graph* g, int use_shortest_path, int mode, int nthreads,
+                  uint64_t* lat_int, uint64_t* lat_ref, double* rel, double* lat_ms);
 
 /* Diagonal rule only (topology.c:1431-1576) for vertex v. */
 void orc_self_path(const orc_graph* g, int32_t v, uint64_t* lat_int, uint64_t* lat_ref,

@@ -86,7 +86,6 @@ SIGNATURES = {
     "srt_sparse_max_n": (ctypes.c_int, []),
     "srt_sparse_build_device": (ctypes.c_int, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
                                                _VP, _VP, _I32, _I32, _U32, _VP, _VP, _VP, _VP]),
-    "srt_mirror_lower_device": (ctypes.c_int, [_I32, _I32, _VP, _VP]),
     "srt_sparse_graph_new": (ctypes.c_int, [_VP, _I32, _VP]),
     "srt_sparse_graph_info": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
     "srt_sparse_graph_rows": (ctypes.c_int, [_VP, _I32, _I32, _VP, _VP, _VP, _VP]),
@@ -105,6 +104,12 @@ SIGNATURES = {
     "srt_sparse_allgather": (ctypes.c_int, [_VP, _I32, _I32, _VP, _VP, _VP]),
     "srt_version": (_CP, []),
     "srt_last_error": (_CP, []),
+    "srt_pair_order_new": (_VP, [_I32, _I32, _I32]),
+    "srt_pair_order_free": (None, [_VP]),
+    "srt_pair_order_attach": (ctypes.c_int, [_VP, _I32]),
+    "srt_pair_order_lookup": (_I32, [_VP, _I32, _I32, _VP, _VP]),
+    "srt_pair_order_peek": (_I32, [_VP, _I32, _I32]),
+    "srt_pair_order_runs": (_I32, [_VP, _I32]),
     "srt_device_count": (ctypes.c_int, []),
     "srt_device_sync": (ctypes.c_int, [_I32]),
     # topology.h (reference signatures)
@@ -128,6 +133,7 @@ SIGNATURES = {
     "srt_topology_reliability_ip": (_D, [_VP, _U32, _U32]),
     "srt_topology_increment_ip": (ctypes.c_int, [_VP, _U32, _U32]),
     "srt_topology_packet_count_ip": (_U64, [_VP, _U32, _U32]),
+    "srt_topology_path_source_ip": (_I32, [_VP, _U32, _U32]),
     "srt_topology_send_packet_ip": (ctypes.c_int, [_VP, _U32, _U32, ctypes.c_double, ctypes.c_int,
                                                    _U64, _VP]),
     "srt_topology_send_packets_ip": (ctypes.c_int, [_VP, ctypes.c_int64, _VP, _VP, _VP, _VP, _VP,
@@ -143,6 +149,10 @@ SIGNATURES = {
     "srt_topology_set_build_opts": (None, [_VP, _VP]),
     "srt_topology_last_stats": (ctypes.c_int, [_VP, _VP]),
 }
+
+# srt_pair_store_fn: (ctx, src, targets, count)
+PAIR_STORE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int32,
+                                 ctypes.POINTER(ctypes.c_int32), ctypes.c_int32)
 
 _lib = None
 

@@ -4,8 +4,11 @@
  * Replaces the lazy per-source Dijkstra of /root/reference/src/main/routing/topology.c:1578-1814
  * (run on a cache miss from _topology_getPathEntry, :1923-1961) with one eager all-pairs build:
  *   use_shortest_path == false : direct edge gather (topology.c:1816-1858)
- *   dense graphs               : blocked Floyd-Warshall + predecessor/reliability pass (dense.hip)
- *   sparse graphs              : multi-source LDS SSSP + tree walk (sparse.hip)
+ *   dense graphs               : blocked Floyd-Warshall (fw16.hip) + predecessor/reliability pass
+ *                                (dense.hip)
+ *   sparse graphs              : per-source bucket SSSP with settle-time predecessor and
+ *                                reliability (wsssp.hip; sparse.hip for overflowing sources)
+ * Every table row is its own source's row; pairorder.c decides which row serves a pair.
  * Every path runs on the GPU; a device failure is returned as SRT_E_DEVICE, never replaced by a
  * host computation.
  */
@@ -32,33 +35,6 @@ extern "C" int srt_device_count(void) {
 extern "C" int srt_device_sync(int32_t device) {
     SRT_HIPCHK(hipSetDevice(device));
     SRT_HIPCHK(hipDeviceSynchronize());
-    return SRT_OK;
-}
-
-__global__ void mirror_lower_tiles(int n, int ld, double* __restrict__ rel) {
-    __shared__ double tile[64][65];
-    const int I = blockIdx.y, J = blockIdx.x;
-    if (J > I) return;
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    for (int a = ty; a < 64; a += 4) {
-        int t = J * 64 + a, s = I * 64 + tx;
-        tile[a][tx] = (t < n && s < n) ? rel[(size_t)t * ld + s] : 0.0;
-    }
-    __syncthreads();
-    for (int a = ty; a < 64; a += 4) {
-        int s = I * 64 + a, t = J * 64 + tx;
-        if (s < n && t < n && s > t) rel[(size_t)s * ld + t] = tile[tx][a];
-    }
-}
-
-extern "C" int srt_mirror_lower_device(int32_t n, int32_t ld, double* rel, void* stream) {
-    if (n <= 0 || ld < n || !rel) {
-        srt_set_error("srt_mirror_lower_device: bad arguments");
-        return SRT_E_ARG;
-    }
-    dim3 g(srt_ceil_div(n, 64), srt_ceil_div(n, 64));
-    mirror_lower_tiles<<<g, 256, 0, (hipStream_t)stream>>>(n, ld, rel);
-    SRT_HIPCHK(hipGetLastError());
     return SRT_OK;
 }
 
@@ -615,15 +591,23 @@ static int check_verts(int n, int nsub, const int32_t* verts) {
     return SRT_OK;
 }
 
-/* device memory left for row chunks after `reserved` bytes, capped */
-static size_t chunk_budget(size_t reserved) {
+/* device memory for row chunks after `reserved` bytes: what is free beyond a 12 GiB reserve,
+ * capped at 48 GiB; when less than that reserve is free, half of what is free. `sharers` ranks
+ * (virtual ranks on one device) read the same free figure at once, so each takes its share. */
+static size_t chunk_budget(size_t reserved, int sharers) {
     size_t free_b = 0, total_b = 0;
-    size_t budget = (size_t)8 << 30;
-    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > reserved + ((size_t)12 << 30)) {
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+        (void)hipGetLastError();
+        return (size_t)1 << 30;
+    }
+    size_t budget;
+    if (free_b > reserved + ((size_t)12 << 30)) {
         budget = free_b - reserved - ((size_t)12 << 30);
         if (budget > ((size_t)48 << 30)) budget = (size_t)48 << 30;
+    } else {
+        budget = free_b > reserved ? (free_b - reserved) / 2 : 0;
     }
-    return budget;
+    return budget / (size_t)(sharers > 1 ? sharers : 1);
 }
 
 static void dense_host_matrices(const srt_canon* c, int ld, uint32_t* hw, double* hr) {
@@ -746,15 +730,15 @@ static int build_one(const srt_canon* c, const srt_build_opts* opts, int algo, i
     } else {
         srt_sparse_graph* sg = NULL;
         TRY(sparse_graph_from_canon(c, opts ? opts->device : 0, &sg));
-        /* the sub-table (every source row of the subset, its columns) stays on the device for the
-         * symmetry mirror; the full-width rows of a chunk of sources are gathered into it */
+        /* the sub-table (every source row of the subset, its columns) on the device; the
+         * full-width rows of a chunk of sources are gathered into it */
         const size_t per_row = (size_t)n * (sizeof(uint32_t) + sizeof(double) + (lat_ms ? sizeof(double) : 0));
         rc = dalloc(&B, (void**)&slat, ns2 * sizeof(uint32_t));
         if (!rc) rc = dalloc(&B, (void**)&srel, ns2 * sizeof(double));
         if (!rc && lat_ms) rc = dalloc(&B, (void**)&sms, ns2 * sizeof(double));
         int chunk = nsub;
         if (!rc && verts) {
-            const size_t cb = chunk_budget(0) / per_row;
+            const size_t cb = chunk_budget(0, 1) / per_row;
             chunk = (int)(cb < (size_t)nsub ? (cb > 0 ? cb : 1) : (size_t)nsub);
             rc = dalloc(&B, (void**)&dlat, (size_t)chunk * n * sizeof(uint32_t));
             if (!rc) rc = dalloc(&B, (void**)&drel, (size_t)chunk * n * sizeof(double));
@@ -776,8 +760,6 @@ static int build_one(const srt_canon* c, const srt_build_opts* opts, int algo, i
             }
             merge_stats(&local, &cs, r0 == 0);
         }
-        if (!rc && !c->directed) rc = srt_mirror_lower_device(nsub, nsub, srel, st);
-        if (!rc && !c->directed && sms) rc = srt_mirror_lower_device(nsub, nsub, sms, st);
         if (!rc) rc = srt_table_min(nsub, nsub, slat, nsub, dmin, st);
         srt_sparse_graph_free(sg);
         if (rc) goto out;
@@ -959,7 +941,9 @@ static void* mjob_sparse(void* p) {
     const int n = j->n, nsub = j->nsub, per = srt_ceil_div(nsub, j->R);
     const int s0 = j->rank * per < nsub ? j->rank * per : nsub;
     const int s1 = (s0 + per < nsub) ? s0 + per : nsub;
-    const size_t all = (size_t)per * j->R * nsub;
+    /* this rank's source rows only: every row is its own source's (no mirror), and the host
+     * table the ranks of this process share receives each shard directly */
+    const size_t all = (size_t)(s1 > s0 ? s1 - s0 : 1) * nsub;
     uint32_t *slat, *dlat = NULL, *dmin;
     double *srel, *sms = NULL, *drel = NULL, *dms = NULL;
     int32_t* dverts = NULL;
@@ -975,7 +959,7 @@ static void* mjob_sparse(void* p) {
     TRYHIP(hipMemsetAsync(dmin, 0xFF, sizeof(uint32_t), st));
     if (j->verts && s1 > s0) {
         const size_t per_row = (size_t)n * (sizeof(uint32_t) + sizeof(double) + (sms ? sizeof(double) : 0));
-        const size_t cb = chunk_budget(0) / per_row;
+        const size_t cb = chunk_budget(0, j->virt ? j->R : 1) / per_row;
         chunk = (int)(cb < (size_t)(s1 - s0) ? (cb > 0 ? cb : 1) : (size_t)(s1 - s0));
         TRY(dalloc(&B, (void**)&dverts, (size_t)nsub * sizeof(int32_t)));
         TRYHIP(hipMemcpyAsync(dverts, j->verts, (size_t)nsub * sizeof(int32_t), hipMemcpyHostToDevice, st));
@@ -989,30 +973,25 @@ static void* mjob_sparse(void* p) {
         memset(&cs, 0, sizeof(cs));
         cs.count_ties = j->st.count_ties;
         if (j->verts) {
+            const size_t o = (size_t)(r0 - s0) * nsub;
             TRY(sparse_rows(sg, 0, r1 - r0, dverts + r0, dlat, drel, dms, st, &cs));
-            TRY(srt_gather_sub_u32(r1 - r0, nsub, NULL, dverts, dlat, n, slat + (size_t)r0 * nsub, nsub, st));
-            TRY(srt_gather_sub_f64(r1 - r0, nsub, NULL, dverts, drel, n, srel + (size_t)r0 * nsub, nsub, st));
-            if (dms) TRY(srt_gather_sub_f64(r1 - r0, nsub, NULL, dverts, dms, n, sms + (size_t)r0 * nsub, nsub, st));
+            TRY(srt_gather_sub_u32(r1 - r0, nsub, NULL, dverts, dlat, n, slat + o, nsub, st));
+            TRY(srt_gather_sub_f64(r1 - r0, nsub, NULL, dverts, drel, n, srel + o, nsub, st));
+            if (dms) TRY(srt_gather_sub_f64(r1 - r0, nsub, NULL, dverts, dms, n, sms + o, nsub, st));
         } else {
-            TRY(sparse_rows(sg, r0, r1, NULL, slat + (size_t)r0 * n, srel + (size_t)r0 * n,
-                            sms ? sms + (size_t)r0 * n : NULL, st, &cs));
+            const size_t o = (size_t)(r0 - s0) * n;
+            TRY(sparse_rows(sg, r0, r1, NULL, slat + o, srel + o, sms ? sms + o : NULL, st, &cs));
         }
         merge_stats(&j->st, &cs, r0 == s0);
     }
-    if (s1 > s0) TRY(srt_table_min(s1 - s0, nsub, slat + (size_t)s0 * nsub, nsub, dmin, st));
-    /* the symmetry rule needs the other shards' rows: gather (ncclAllGather), mirror, keep ours */
-    TRY(srt_coll_allgather(j->comm, slat, (size_t)per * nsub * sizeof(uint32_t), st));
-    TRY(srt_coll_allgather(j->comm, srel, (size_t)per * nsub * sizeof(double), st));
-    if (sms) TRY(srt_coll_allgather(j->comm, sms, (size_t)per * nsub * sizeof(double), st));
-    if (!j->directed) TRY(srt_mirror_lower_device(nsub, nsub, srel, st));
-    if (!j->directed && sms) TRY(srt_mirror_lower_device(nsub, nsub, sms, st));
     if (s1 > s0) {
-        TRYHIP(hipMemcpyAsync(j->lat_q + (size_t)s0 * nsub, slat + (size_t)s0 * nsub,
+        TRY(srt_table_min(s1 - s0, nsub, slat, nsub, dmin, st));
+        TRYHIP(hipMemcpyAsync(j->lat_q + (size_t)s0 * nsub, slat,
                               (size_t)(s1 - s0) * nsub * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        TRYHIP(hipMemcpyAsync(j->rel + (size_t)s0 * nsub, srel + (size_t)s0 * nsub,
+        TRYHIP(hipMemcpyAsync(j->rel + (size_t)s0 * nsub, srel,
                               (size_t)(s1 - s0) * nsub * sizeof(double), hipMemcpyDeviceToHost, st));
         if (sms)
-            TRYHIP(hipMemcpyAsync(j->lat_ms + (size_t)s0 * nsub, sms + (size_t)s0 * nsub,
+            TRYHIP(hipMemcpyAsync(j->lat_ms + (size_t)s0 * nsub, sms,
                                   (size_t)(s1 - s0) * nsub * sizeof(double), hipMemcpyDeviceToHost, st));
     }
     TRYHIP(hipMemcpyAsync(&j->min_q, dmin, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -1133,10 +1112,17 @@ done:
     return rc;
 }
 
-extern "C" int srt_build_tables_subset(const srt_edges* g, const srt_build_opts* opts, int32_t ngpus,
-                                       int32_t nsub, const int32_t* verts, uint32_t* lat_q,
-                                       uint64_t* quantum_ns, double* rel, double* lat_ms,
-                                       uint32_t* min_lat_q, srt_build_stats* stats) {
+/* SRT_VIRTUAL_RANKS=R (tests): R ranks on device 0, collectives as device copies */
+static int virtual_ranks_env(void) {
+    const char* venv = getenv("SRT_VIRTUAL_RANKS");
+    const int v = venv ? atoi(venv) : 0;
+    return v > 0 ? (v < 64 ? v : 64) : 0;
+}
+
+static int build_tables_subset_impl(const srt_edges* g, const srt_build_opts* opts, int32_t ngpus,
+                                    int virt, int32_t nsub, const int32_t* verts, uint32_t* lat_q,
+                                    uint64_t* quantum_ns, double* rel, double* lat_ms,
+                                    uint32_t* min_lat_q, srt_build_stats* stats) {
     if (!g || !lat_q || !quantum_ns || !rel || ngpus < 1) {
         srt_set_error("srt_build_tables_subset: null argument");
         return SRT_E_ARG;
@@ -1157,10 +1143,6 @@ extern "C" int srt_build_tables_subset(const srt_edges* g, const srt_build_opts*
     *quantum_ns = c.quantum_ns;
     const int use_sp = opts ? opts->use_shortest_path : 1;
     const int algo = use_sp ? choose_algo(&c, opts) : SRT_ALGO_DENSE_FW;
-    /* SRT_VIRTUAL_RANKS=R (tests): R ranks on device 0, collectives as device copies, whatever
-     * ngpus says (srt_build_tables_multi hands ngpus = 1 down here when it is set) */
-    const char* venv = getenv("SRT_VIRTUAL_RANKS");
-    const int virt = venv && atoi(venv) > 0 ? (atoi(venv) < 64 ? atoi(venv) : 64) : 0;
     const int R = virt ? virt : (ngpus < avail ? ngpus : avail);
     uint32_t mq = 0xFFFFFFFFu;
     if (R > 1 && use_sp)
@@ -1170,6 +1152,16 @@ extern "C" int srt_build_tables_subset(const srt_edges* g, const srt_build_opts*
     if (!rc && min_lat_q) *min_lat_q = mq;
     srt_canon_free(&c);
     return rc;
+}
+
+/* SRT_VIRTUAL_RANKS applies only to a multi-GPU request (ngpus > 1): a variable left set must not
+ * turn the one-GPU builds (every lazy topology build) into the virtual multi-rank path */
+extern "C" int srt_build_tables_subset(const srt_edges* g, const srt_build_opts* opts, int32_t ngpus,
+                                       int32_t nsub, const int32_t* verts, uint32_t* lat_q,
+                                       uint64_t* quantum_ns, double* rel, double* lat_ms,
+                                       uint32_t* min_lat_q, srt_build_stats* stats) {
+    return build_tables_subset_impl(g, opts, ngpus, ngpus > 1 ? virtual_ranks_env() : 0, nsub,
+                                    verts, lat_q, quantum_ns, rel, lat_ms, min_lat_q, stats);
 }
 
 extern "C" int srt_build_tables(const srt_edges* g, const srt_build_opts* opts, uint32_t* lat_q,
@@ -1188,10 +1180,11 @@ extern "C" int srt_build_tables_multi(const srt_edges* g, const srt_build_opts* 
         srt_set_error("srt_build_tables_multi: bad argument");
         return SRT_E_ARG;
     }
-    /* ngpus == 1 still runs the threaded, communicator-driven form (tests of that path) */
+    /* ngpus == 1 still runs the threaded, communicator-driven form (tests of that path);
+     * SRT_VIRTUAL_RANKS (tests) runs that many virtual ranks on device 0 */
     const int avail = srt_device_count();
-    const char* venv = getenv("SRT_VIRTUAL_RANKS");
-    if (ngpus == 1 && !(venv && atoi(venv) > 0) && avail >= 1) {
+    const int virt = virtual_ranks_env();
+    if (ngpus == 1 && !virt && avail >= 1) {
         srt_canon c;
         int rc = srt_canon_build(g, &c);
         if (rc) return rc;
@@ -1206,6 +1199,6 @@ extern "C" int srt_build_tables_multi(const srt_edges* g, const srt_build_opts* 
         srt_canon_free(&c);
         return rc;
     }
-    return srt_build_tables_subset(g, opts, ngpus, g->n, NULL, lat_q, quantum_ns, rel, NULL, NULL,
-                                   stats);
+    return build_tables_subset_impl(g, opts, ngpus, virt, g->n, NULL, lat_q, quantum_ns, rel, NULL,
+                                    NULL, stats);
 }

@@ -1,13 +1,13 @@
 /*
  * dense.hip -- dense all-pairs build for gfx950: blocked min-plus Floyd-Warshall with LDS tiles,
- * then the canonical-predecessor / path-order reliability pass, the symmetry mirror and the
- * diagonal rule.
+ * then the canonical-predecessor / path-order reliability pass and the diagonal rule. Every
+ * source row is its own (the lookup layer picks which row serves a pair, pairorder.c).
  *
  * Reference semantics (/root/reference/src/main/routing/topology.c):
  *   distances      Dijkstra per source (:1682) -> here FW over integer latency quanta
  *   predecessor    first-settled tight in-edge -> canonical argmin (D[s][u], u) over tight (u,t)
  *   reliability    product of (1 - loss) in path order from the source (:1308-1309, :1365)
- *   symmetry       one cached entry per unordered pair (:1194-1199) -> computed from min(s,t)
+ *   pair cache     the first source run serves a pair (:1194-1199) -> raw rows + pairorder.c
  *   diagonal       shortest path to self (:1431-1576)
  *
  * Layout: every matrix is ld x ld row-major (ld % 64 == 0, rows/cols >= n are padding),
@@ -446,13 +446,10 @@ __global__ void arc_transpose_fill(int n, const int32_t* __restrict__ ptr,
  * a BM-row block, so each block's transpose is one contiguous slab */
 template <typename T, typename TO = T, int BM = 0>
 __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, const T* __restrict__ in,
-                                                        size_t ldi, TO* __restrict__ out, size_t ldo,
-                                                        int upper = 0) {
+                                                        size_t ldi, TO* __restrict__ out, size_t ldo) {
     __shared__ T tile[64][65];
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
-    /* upper: a (t-major) block whose every t precedes every s holds no pair the build keeps */
-    if (upper && r0 + 64 <= c0) return;
     T v[16]; /* all 16 loads in flight before the LDS stores */
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -778,24 +775,13 @@ __global__ __launch_bounds__(512) void rel_sweeps_kernel(int n, int ld, int row0
  * D[s][t] == L) only reads values final since an earlier pass: each entry is formed once,
  * rel(s,t) = rel(s,pred) * r(pred,t), the left-to-right product of topology.c:1364-1365.
  * Rows whose largest distance exceeds maxl passes are flagged for rel_sweeps_kernel. */
-/* SYM (one GPU, undirected): the predecessor and reliability rows were transposed for the pairs
- * t > s only (transpose_kernel upper); the lower entries are the mirror of rows t < s and are
- * overwritten after this pass. The row still needs the lower vertices that are ancestors of its
- * upper targets: they are marked from the upper predecessors (an LDS bitmap), their predecessor
- * and arc reliability read from the source-column arrays of the predecessor pass (predT / rT,
- * column s), transitively, and only upper and marked targets take the level passes; every other
- * lower predecessor entry is set to -1. A row flagged for the sweep kernel marks every lower
- * vertex (the sweeps walk whole rows). */
-template <int NT, int MAXN, bool SYM = false>
+template <int NT, int MAXN>
 __global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
                                                          const uint32_t* __restrict__ lat,
                                                          int32_t* __restrict__ pred,
                                                          double* __restrict__ rel, int maxl,
                                                          int32_t* __restrict__ max_depth,
-                                                         int32_t* __restrict__ sweep,
-                                                         const int32_t* __restrict__ predT = nullptr,
-                                                         const double* __restrict__ rT = nullptr,
-                                                         size_t ldT = 0) {
+                                                         int32_t* __restrict__ sweep) {
     /* each thread owns t = tid + i * NT (i < PER, n <= MAXN); the row's distances are read once
      * and kept as bytes in registers (levels <= maxl <= 254 once the row qualifies), so a pass
      * only compares registers and touches memory for its own targets. The row reads go through
@@ -812,11 +798,6 @@ __global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(dl), 0, n * 4, 0x00020000);
     __shared__ uint32_t red[NT / 64];
     extern __shared__ uint16_t s_wlist[]; /* NT / 64 waves x 64 x PER target indices */
-    constexpr int NWD = MAXN / 32;
-    /* SYM: the marked and processed bitmaps */
-    uint32_t* mk = reinterpret_cast<uint32_t*>(s_wlist + (NT / 64) * 64 * PER);
-    uint32_t* dn = mk + NWD;
-    uint32_t* nwb = dn + NWD;
     uint32_t lv[PER / 4];
     uint32_t mx = 0;
 #pragma unroll
@@ -837,63 +818,6 @@ __global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
     mx = 0;
     for (int i = 0; i < NT / 64; ++i) mx = max(mx, red[i]);
     if (tid == 0) sweep[blockIdx.x] = (int)mx > maxl;
-    if constexpr (SYM) {
-        const bool full = (int)mx > maxl; /* the sweeps need every lower predecessor */
-        for (int q = tid; q < NWD; q += NT) {
-            uint32_t m = 0u;
-            if (full) { /* every lower vertex (t < s, t < n) */
-                const int lo = q * 32;
-                m = lo + 32 <= s ? 0xFFFFFFFFu : lo >= s ? 0u : (1u << (s - lo)) - 1u;
-            }
-            mk[q] = m;
-            dn[q] = 0u;
-        }
-        __syncthreads();
-        if (!full) { /* the lower predecessors of the upper targets */
-#pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                const int t = tid + i * NT;
-                if (t > s && t < n && ((lv[i >> 2] >> (8 * (i & 3))) & 0xFFu)) {
-                    const int u = pg[t];
-                    if (u >= 0 && u < s) atomicOr(&mk[u >> 5], 1u << (u & 31));
-                }
-            }
-        }
-        /* closure: each newly marked vertex takes its predecessor and arc reliability from
-         * column s of the predecessor pass's arrays; a lower predecessor is marked in turn */
-        for (;;) {
-            __syncthreads();
-            int any = 0;
-            for (int q = tid; q < NWD; q += NT) {
-                const uint32_t nb = mk[q] & ~dn[q];
-                nwb[q] = nb;
-                dn[q] |= nb;
-                any |= nb != 0u;
-            }
-            if (!__syncthreads_or(any)) break;
-            for (int q = tid; q < NWD; q += NT) {
-                uint32_t bits = nwb[q];
-                while (bits) {
-                    const int u = q * 32 + __ffs(bits) - 1;
-                    bits &= bits - 1u;
-                    if (u >= n || u == s) continue;
-                    const size_t o = (size_t)u * ldT + (size_t)(s - row0);
-                    const int p = predT[o];
-                    pg[u] = p;
-                    rr[u] = rT[o];
-                    if (p >= 0 && p < s) atomicOr(&mk[p >> 5], 1u << (p & 31));
-                }
-            }
-        }
-        /* the other lower entries: no predecessor (the path-order ms pass skips them) */
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int t = tid + i * NT;
-            if (t < s && !((dn[t >> 5] >> (t & 31)) & 1u)) pg[t] = -1;
-        }
-        __threadfence_block();
-        __syncthreads();
-    }
     if ((int)mx > maxl) return; /* long distance range: rel_sweeps_kernel takes the row */
     /* per pass, each wave compacts its targets of level L into its own LDS list (ballot +
      * prefix popcount), then walks the list with its lanes: the loads of different targets are
@@ -905,9 +829,7 @@ __global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
         int cnt = 0;
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
-            const int t = tid + i * NT;
-            const bool hit = ((lv[i >> 2] >> (8 * (i & 3))) & 0xFFu) == L &&
-                             (!SYM || t > s || ((dn[t >> 5] >> (t & 31)) & 1u));
+            const bool hit = ((lv[i >> 2] >> (8 * (i & 3))) & 0xFFu) == L;
             const uint64_t m = __ballot(hit);
             if (hit) wl[cnt + __popcll(m & lt)] = (uint16_t)(tid + i * NT);
             cnt += __popcll(m);
@@ -993,72 +915,16 @@ __global__ __launch_bounds__(256) void dense_diag_kernel(int n, int ld, int row0
     }
 }
 
-/* rel[s][t] <- rel[t][s] for s > t inside one square block (rows/cols [b, e) of the matrix,
- * local rows start at b). */
-__global__ __launch_bounds__(256) void mirror_block_kernel(int n, int ld, int b, int e,
-                                                           double* __restrict__ rel_rows) {
-    /* one workgroup per lower-triangle block (I >= J): x = I (I + 1) / 2 + J */
-    __shared__ double tile[64][65];
-    const int x = (int)blockIdx.x;
-    int I = (int)((sqrt(8.0 * x + 1.0) - 1.0) * 0.5);
-    while ((I + 1) * (I + 2) / 2 <= x) ++I;
-    while (I * (I + 1) / 2 > x) --I;
-    const int J = x - I * (I + 1) / 2;
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    double v[16]; /* all 16 loads in flight before the LDS stores */
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int t = b + J * 64 + ty + 4 * q, s = b + I * 64 + tx;
-        v[q] = (t < e && s < e && t < n && s < n) ? rel_rows[(size_t)(t - b) * ld + s] : 0.0;
-    }
-#pragma unroll
-    for (int q = 0; q < 16; ++q) tile[ty + 4 * q][tx] = v[q];
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int a = ty + 4 * q, s = b + I * 64 + a, t = b + J * 64 + tx;
-        if (s < e && t < e && s < n && s > t) rel_rows[(size_t)(s - b) * ld + t] = tile[tx][a];
-    }
-}
-
-/* pack rel_rows[:, c0:c1] (nrows x (c1-c0)) into a contiguous buffer */
-__global__ void pack_cols_kernel(int nrows, int ld, int c0, int c1, const double* __restrict__ src,
-                                 double* __restrict__ dst) {
-    const int w = c1 - c0;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)nrows * w) return;
-    const int r = (int)(i / w), c = (int)(i % w);
-    dst[i] = src[(size_t)r * ld + c0 + c];
-}
-
-/* rel_rows[s - b][c0 + t'] <- buf[t'][s - b] (buf = the peer's packed block, peer rows x our rows) */
-__global__ __launch_bounds__(256) void unpack_transpose_kernel(int nrows, int ld, int c0, int pw,
-                                                               const double* __restrict__ buf,
-                                                               double* __restrict__ rel_rows) {
-    __shared__ double tile[64][65];
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    const int R0 = blockIdx.y * 64; /* our local rows */
-    const int C0 = blockIdx.x * 64; /* peer rows = our columns c0.. */
-    for (int a = ty; a < 64; a += 4) {
-        int pr = C0 + a, lr = R0 + tx;
-        tile[a][tx] = (pr < pw && lr < nrows) ? buf[(size_t)pr * nrows + lr] : 0.0;
-    }
-    __syncthreads();
-    for (int a = ty; a < 64; a += 4) {
-        int lr = R0 + a, pr = C0 + tx;
-        if (lr < nrows && pr < pw) rel_rows[(size_t)lr * ld + c0 + pr] = tile[tx][a];
-    }
-}
 
 /* ------------------------------------------------------------------------------------------ */
 /* host orchestration of the dense post pass (single GPU or one row shard)                    */
 /* ------------------------------------------------------------------------------------------ */
 typedef struct {
-    size_t n_cap, arc_cap, tarc_cap, x_cap;
+    size_t n_cap, arc_cap, tarc_cap;
     int32_t *cnt, *ptr, *tptr, *cursor, *col, *tcol, *depth;
     unsigned long long* ties; /* tied-pair count of the predecessor pass */
     uint32_t *aw, *tw;
-    double *ar, *tr, *xsend, *xrecv;
+    double *ar, *tr;
     uint32_t* panel;
     size_t panel_cap;
     uint2* uw;
@@ -1175,7 +1041,6 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         srt_set_error("dense predecessor pass supports n <= %d (n = %d)", srt_dense_max_n(), n);
         return SRT_E_RANGE;
     }
-    bool upper = false;
     if (lrows > 0) {
         const size_t slab = (size_t)ld * nrows;
         /* the transpose is block-major (DT[s / 64][u][s % 64]): a 64-source block's slab is
@@ -1204,11 +1069,6 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         size_t c4 = ws->rt_cap;
         if ((rc = ws_grow((void**)&ws->rt, &c4, slab, sizeof(double)))) return rc;
         ws->rt_cap = c4;
-        /* upper-only (one GPU, undirected, byte distances): the transposes and the reliability
-         * levels cover the pairs t > s, plus the lower ancestors rel_levels_kernel<SYM> marks;
-         * the lower triangle is the mirror (srt_dense_post_device) */
-        upper = !directed && !gather && row0 == 0 && lrows == n && d16 && srt_fw16_small() &&
-                n <= 32768 && !(getenv("SRT_DENSE_UPPER") && !atoi(getenv("SRT_DENSE_UPPER")));
         if (d16 && srt_fw16_small()) {
             /* every distance fits a byte: the transposed slab of a 64-source block is 2 MB and
              * stays in its XCD's L2 */
@@ -1255,27 +1115,14 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         int32_t* pred = reinterpret_cast<int32_t*>(ws->dt);
         transpose_kernel<uint32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
             n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows,
-            reinterpret_cast<uint32_t*>(pred), (size_t)ld, upper ? 1 : 0);
+            reinterpret_cast<uint32_t*>(pred), (size_t)ld);
         transpose_kernel<double><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
-            n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld, upper ? 1 : 0);
+            n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
         /* level order for rows whose distances span <= 64 quanta, sweeps for the rest
          * (ws->cursor is free here and carries the per-row hand-over flags) */
         /* 1024 threads per row, one row per CU (128 VGPRs): 12.3 ms on C4 against 13.3 for 512
          * threads at two rows per CU and 13.1 for 1024 at two (64 VGPRs, 4 targets in flight) */
-        if (upper) {
-            /* + three bitmaps (12 KB) */
-            const int lds = 65536 + 3 * 4096;
-            SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 32768, true>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-            rel_levels_kernel<1024, 32768, true><<<lrows, 1024, lds, st>>>(
-                n, ld, row0, d, pred, rel, 64, ws->depth, ws->cursor, ws->predt, ws->rt,
-                (size_t)nrows);
-            const size_t lds2 = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
-            SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
-            rel_sweeps_kernel<<<lrows, 512, lds2, st>>>(n, ld, row0, pred, rel, ws->depth, ws->cursor);
-            SRT_HIPCHK(hipGetLastError());
-        } else if (n <= 32768) {
+        if (n <= 32768) {
             SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 32768>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
             rel_levels_kernel<1024, 32768><<<lrows, 1024, 65536, st>>>(n, ld, row0, d, pred, rel, 64,
@@ -1331,11 +1178,6 @@ int srt_dense_post_device(int32_t n, int32_t ld, int32_t directed, const uint32_
                           srt_build_stats* stats) {
     int rc = dense_post(n, ld, 0, ld, directed, w, r, d, d16, rel, st, stats, NULL, NULL);
     if (rc) return rc;
-    if (!directed) {
-        const int nbk = srt_ceil_div(n, 64);
-        mirror_block_kernel<<<nbk * (nbk + 1) / 2, 256, 0, st>>>(n, ld, 0, n, rel);
-        SRT_HIPCHK(hipGetLastError());
-    }
     return dense_finish_rows(n, ld, 0, ld, w, r, d, rel, st, stats);
 }
 
@@ -1427,11 +1269,6 @@ int srt_dense_build_device_ms(int32_t n, int32_t ld, int32_t directed, const uin
     if (rc) return rc;
     if (lat_ms) {
         if ((rc = dense_path_ms(n, ld, 0, ld, lat, quantum_ns, lat_ms, st))) return rc;
-        if (!directed) {
-            const int nbk = srt_ceil_div(n, 64);
-            mirror_block_kernel<<<nbk * (nbk + 1) / 2, 256, 0, st>>>(n, ld, 0, n, lat_ms);
-            SRT_HIPCHK(hipGetLastError());
-        }
     }
     SRT_HIPCHK(hipEventRecord(e2, st));
     if (stats) {
@@ -1514,86 +1351,6 @@ static int shard_gather(void* vctx, dense_ws* ws, int n, int phase, int32_t tota
     const int rc2 = srt_coll_group_end(ctx->comm);
     free(hptr);
     return rc ? rc : rc2;
-}
-
-/* undirected symmetry across shards: rank q sends rel[q rows][r cols] to every r > q, which
- * stores its transpose into rel[r rows][q cols] (the entries with s > t). */
-static int shard_mirror(const srt_comm* comm, int n, int ld, int b, int e, double* rel_rows,
-                        hipStream_t st) {
-    const int R = srt_comm_size(comm), me = srt_comm_rank(comm);
-    const int nr = e - b;
-    dense_ws* ws;
-    int rc = ws_get(&ws, n);
-    if (rc) return rc;
-    size_t send_need = (size_t)nr * (size_t)(ld - e) + 1, recv_need = (size_t)nr * (size_t)b + 1;
-    size_t cs = ws->x_cap, cr = ws->x_cap;
-    size_t need = send_need > recv_need ? send_need : recv_need;
-    if ((rc = ws_grow((void**)&ws->xsend, &cs, need, sizeof(double)))) return rc;
-    if ((rc = ws_grow((void**)&ws->xrecv, &cr, need, sizeof(double)))) return rc;
-    ws->x_cap = cs;
-    size_t so = 0;
-    for (int q = me + 1; q < R; q++) {
-        int32_t qb, qe;
-        srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &qb, &qe);
-        const int64_t cnt = (int64_t)nr * (qe - qb);
-        if (cnt > 0)
-            pack_cols_kernel<<<srt_ceil_div(cnt, 256), 256, 0, st>>>(nr, ld, qb, qe, rel_rows,
-                                                                    ws->xsend + so);
-        so += (size_t)cnt;
-    }
-    SRT_HIPCHK(hipGetLastError());
-    void** sp = (void**)calloc((size_t)R, sizeof(void*));
-    void** rp = (void**)calloc((size_t)R, sizeof(void*));
-    size_t* sb = (size_t*)calloc((size_t)R, sizeof(size_t));
-    size_t* rb = (size_t*)calloc((size_t)R, sizeof(size_t));
-    if (!sp || !rp || !sb || !rb) {
-        free(sp);
-        free(rp);
-        free(sb);
-        free(rb);
-        return SRT_E_NOMEM;
-    }
-    so = 0;
-    for (int q = me + 1; q < R; q++) {
-        int32_t qb, qe;
-        srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &qb, &qe);
-        const size_t cnt = (size_t)nr * (qe - qb);
-        sp[q] = ws->xsend + so;
-        sb[q] = cnt * sizeof(double);
-        so += cnt;
-    }
-    size_t ro = 0;
-    for (int q = 0; q < me; q++) {
-        int32_t qb, qe;
-        srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &qb, &qe);
-        const size_t cnt = (size_t)(qe - qb) * nr;
-        rp[q] = ws->xrecv + ro;
-        rb[q] = cnt * sizeof(double);
-        ro += cnt;
-    }
-    rc = srt_coll_exchange(comm, sp, sb, rp, rb, st);
-    free(sp);
-    free(rp);
-    free(sb);
-    free(rb);
-    if (rc) return rc;
-    ro = 0;
-    for (int q = 0; q < me; q++) {
-        int32_t qb, qe;
-        srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &qb, &qe);
-        const int pw = qe - qb;
-        if (pw > 0 && nr > 0) {
-            dim3 g(srt_ceil_div(pw, 64), srt_ceil_div(nr, 64));
-            unpack_transpose_kernel<<<g, 256, 0, st>>>(nr, ld, qb, pw, ws->xrecv + ro, rel_rows);
-        }
-        ro += (size_t)pw * nr;
-    }
-    if (nr > 0) {
-        const int nbk = srt_ceil_div(nr, 64);
-        mirror_block_kernel<<<nbk * (nbk + 1) / 2, 256, 0, st>>>(n, ld, b, e, rel_rows);
-    }
-    SRT_HIPCHK(hipGetLastError());
-    return SRT_OK;
 }
 
 int srt_dense_build_sharded_ms(srt_comm* comm, int32_t n, int32_t ld, int32_t directed,
@@ -1687,26 +1444,9 @@ int srt_dense_build_sharded_ms(srt_comm* comm, int32_t n, int32_t ld, int32_t di
                     exact ? srt_fw16_matrix() : NULL, rel_rows, st, stats,
                     R > 1 ? shard_gather : NULL, &ctx);
     if (rc) return rc;
-    if (!directed) {
-        if (R > 1) {
-            if ((rc = shard_mirror(comm, n, ld, b, e, rel_rows, st))) return rc;
-        } else {
-            const int nbk = srt_ceil_div(n, 64);
-            mirror_block_kernel<<<nbk * (nbk + 1) / 2, 256, 0, st>>>(n, ld, 0, n, rel_rows);
-        }
-    }
     if ((rc = dense_finish_rows(n, ld, b, nr, w_rows, r_rows, lat_rows, rel_rows, st, stats))) return rc;
     if (lms_rows) {
         if ((rc = dense_path_ms(n, ld, b, nr, lat_rows, quantum_ns, lms_rows, st))) return rc;
-        if (!directed) {
-            if (R > 1) {
-                if ((rc = shard_mirror(comm, n, ld, b, e, lms_rows, st))) return rc;
-            } else {
-                const int nbk = srt_ceil_div(n, 64);
-                mirror_block_kernel<<<nbk * (nbk + 1) / 2, 256, 0, st>>>(n, ld, 0, n, lms_rows);
-                SRT_HIPCHK(hipGetLastError());
-            }
-        }
     }
     SRT_HIPCHK(hipEventRecord(e2, st));
     if (stats) {

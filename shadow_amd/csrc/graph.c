@@ -87,6 +87,46 @@ static int32_t uf_find(int32_t* p, int32_t x) {
     return x;
 }
 
+/* Largest hop count of a breadth-first search from `root` over the k arcs (u -> v, or v -> u when
+ * backward); -1 if some vertex is unreachable. */
+static int64_t hop_ecc(int32_t n, const carc* a, int64_t k, int32_t root, int backward) {
+    int32_t* ptr = (int32_t*)calloc((size_t)n + 1, sizeof(int32_t));
+    int32_t* adj = (int32_t*)malloc((size_t)(k > 0 ? k : 1) * sizeof(int32_t));
+    int32_t* q = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+    int32_t* dep = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+    int64_t ecc = -2;
+    if (ptr && adj && q && dep) {
+        for (int64_t i = 0; i < k; i++) ptr[(backward ? a[i].v : a[i].u) + 1]++;
+        for (int32_t v = 0; v < n; v++) ptr[v + 1] += ptr[v];
+        for (int64_t i = 0; i < k; i++) {
+            const int32_t x = backward ? a[i].v : a[i].u;
+            adj[ptr[x]++] = backward ? a[i].u : a[i].v;
+        }
+        for (int32_t v = n; v > 0; v--) ptr[v] = ptr[v - 1];
+        ptr[0] = 0;
+        for (int32_t v = 0; v < n; v++) dep[v] = -1;
+        int32_t head = 0, tail = 0;
+        dep[root] = 0;
+        q[tail++] = root;
+        ecc = 0;
+        while (head < tail) {
+            const int32_t u = q[head++];
+            if (dep[u] > ecc) ecc = dep[u];
+            for (int32_t j = ptr[u]; j < ptr[u + 1]; j++)
+                if (dep[adj[j]] < 0) {
+                    dep[adj[j]] = dep[u] + 1;
+                    q[tail++] = adj[j];
+                }
+        }
+        if (tail < n) ecc = -1;
+    }
+    free(ptr);
+    free(adj);
+    free(q);
+    free(dep);
+    return ecc;
+}
+
 static int lat_cmp(const void* a, const void* b) {
     const carc* x = (const carc*)a;
     const carc* y = (const carc*)b;
@@ -208,7 +248,10 @@ int srt_canon_build(const srt_edges* g, srt_canon* c) {
         c->self_r[v] = self_e[v] < 0 ? 0.0 : 1.0f - g->loss[self_e[v]];
     }
     free(self_e);
-    /* Range bound on any shortest distance: undirected -> MST weight, directed -> (n-1)*max. */
+    /* Range bound on any shortest distance: the smaller of (undirected) the MST weight or
+     * (directed) (n - 1) * max_w, and the hop bound through the highest-degree vertex p:
+     * D(a, b) <= D(a, p) + D(p, b) <= (ecc_in(p) + ecc_out(p)) * max_w in hops, which keeps
+     * small-world graphs with fine quanta (a 100k power-law graph at 1 us) in the u32 tables. */
     uint64_t bound;
     if (!g->directed) {
         carc* b = (carc*)malloc((size_t)(k > 0 ? k : 1) * sizeof(carc));
@@ -235,6 +278,22 @@ int srt_canon_build(const srt_edges* g, srt_canon* c) {
         free(par);
     } else {
         bound = (uint64_t)(g->n - 1) * (uint64_t)c->max_w_q;
+    }
+    {
+        int32_t* deg = (int32_t*)calloc((size_t)g->n, sizeof(int32_t));
+        if (deg) {
+            for (int64_t i = 0; i < k; i++) deg[a[i].u]++;
+            int32_t p = 0;
+            for (int32_t v = 1; v < g->n; v++)
+                if (deg[v] > deg[p]) p = v;
+            free(deg);
+            const int64_t eo = hop_ecc(g->n, a, k, p, 0);
+            const int64_t ei = g->directed ? hop_ecc(g->n, a, k, p, 1) : eo;
+            if (eo >= 0 && ei >= 0) {
+                const uint64_t hb = (uint64_t)(eo + ei) * (uint64_t)c->max_w_q;
+                if (hb < bound) bound = hb;
+            }
+        }
     }
     if (bound >= SRT_INF || 2ull * c->max_w_q >= SRT_INF) {
         free(a);

@@ -1,0 +1,285 @@
+/*
+ * pairorder.c -- which cached path the reference serves for a vertex pair.
+ *
+ * Restates the lazy path cache of /root/reference/src/main/routing/topology.c over tables that
+ * hold every source's raw row:
+ *   - a lookup (s, t) checks the cache for (s, t), and for (t, s) unless the graph is directed
+ *     (_topology_getPathEntry, :1917-1921);
+ *   - a miss computes source s for every attached target (_topology_computeSourcePaths,
+ *     :1578-1814; targets = verticesWithAttachedHosts at that moment, :1604) or, with
+ *     use_shortest_path = false, the one direct edge s -> t (_topology_lookupDirectPath,
+ *     :1816-1858); the self pair takes _topology_computeShortestPathToSelf (:1597-1599);
+ *   - a path (x, y) is stored only if neither (x, y) nor (y, x) is cached
+ *     (_topology_shouldStorePath, :1194-1199), and the lookup after the miss falls back to
+ *     (t, s) for any graph (:1963-1967).
+ * So the first source computed for a pair (with the other end attached) serves it for good, in
+ * both directions, with its own row's latency and reliability: a directed lookup (s, t) whose
+ * pair t computed first returns the t -> s path (and still runs source s, :1919).
+ *
+ * Model: per vertex, the sequence numbers of its source runs, one per attach epoch (the attached
+ * set only grows: topology_detach leaves verticesWithAttachedHosts alone, :2274-2281; a second
+ * run in the same epoch stores nothing new). The pair {x, y} is stored by the earliest run of x
+ * or y made while both were attached. Reads are lock-free (a seqlock over the per-vertex run
+ * lists); runs are recorded under a mutex. Direct mode keeps two bits per unordered pair (stored,
+ * and which end stored it), set by compare-and-swap.
+ */
+#define _GNU_SOURCE
+#include <pthread.h>
+#include <sched.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "srt_internal.h"
+
+typedef struct {
+    int32_t epoch; /* attach epoch of the run */
+    int32_t pad;
+    int64_t seq;   /* global order of runs */
+} po_run;
+
+typedef struct {
+    int32_t count;
+    int32_t pad;
+    po_run r[];
+} po_list;
+
+struct srt_pair_order {
+    int32_t n, directed, per_source;
+    pthread_mutex_t mu;
+    atomic_uint_fast64_t version; /* seqlock: odd while a run list is being replaced */
+    int64_t next_seq;
+    atomic_int epoch;           /* bumped when the attached set grows */
+    _Atomic int32_t* att_epoch; /* epoch from which v is attached; INT32_MAX = never */
+    int32_t* att_list;          /* attached vertices, in attach order */
+    int32_t natt;
+    _Atomic(po_list*)* runs; /* per-source mode */
+    po_list** retired;       /* replaced lists: lock-free readers may still hold them */
+    size_t nretired, cap_retired;
+    int32_t* scratch;            /* targets stored by one run */
+    atomic_uchar* self_done;     /* (v, v) stored */
+    _Atomic uint64_t* pairbits;  /* direct mode: 2 bits per unordered pair {a < b} */
+};
+
+srt_pair_order* srt_pair_order_new(int32_t n, int32_t directed, int32_t per_source) {
+    if (n <= 0) return NULL;
+    srt_pair_order* po = (srt_pair_order*)calloc(1, sizeof(*po));
+    if (!po) return NULL;
+    po->n = n;
+    po->directed = directed ? 1 : 0;
+    po->per_source = per_source ? 1 : 0;
+    pthread_mutex_init(&po->mu, NULL);
+    atomic_init(&po->version, 0);
+    atomic_init(&po->epoch, 0);
+    po->att_epoch = (_Atomic int32_t*)malloc((size_t)n * sizeof(*po->att_epoch));
+    po->att_list = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+    po->self_done = (atomic_uchar*)calloc((size_t)n, sizeof(atomic_uchar));
+    int ok = po->att_epoch && po->att_list && po->self_done;
+    if (ok && po->per_source) {
+        po->runs = (_Atomic(po_list*)*)calloc((size_t)n, sizeof(*po->runs));
+        po->scratch = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+        ok = po->runs && po->scratch;
+    } else if (ok) {
+        /* n (n - 1) / 2 pairs, 32 per word; calloc'd pages stay untouched until used */
+        const uint64_t pairs = (uint64_t)n * (uint64_t)(n - 1) / 2;
+        po->pairbits = (_Atomic uint64_t*)calloc((size_t)(pairs / 32 + 1), sizeof(uint64_t));
+        ok = po->pairbits != NULL;
+    }
+    if (!ok) {
+        srt_pair_order_free(po);
+        return NULL;
+    }
+    for (int32_t v = 0; v < n; v++) atomic_init(&po->att_epoch[v], INT32_MAX);
+    return po;
+}
+
+void srt_pair_order_free(srt_pair_order* po) {
+    if (!po) return;
+    if (po->runs)
+        for (int32_t v = 0; v < po->n; v++) free(atomic_load(&po->runs[v]));
+    for (size_t i = 0; i < po->nretired; i++) free(po->retired[i]);
+    free(po->retired);
+    free(po->runs);
+    free(po->scratch);
+    free((void*)po->att_epoch);
+    free(po->att_list);
+    free((void*)po->self_done);
+    free((void*)po->pairbits);
+    pthread_mutex_destroy(&po->mu);
+    free(po);
+}
+
+int srt_pair_order_attach(srt_pair_order* po, int32_t v) {
+    if (!po || v < 0 || v >= po->n) return SRT_E_ARG;
+    pthread_mutex_lock(&po->mu);
+    if (atomic_load_explicit(&po->att_epoch[v], memory_order_relaxed) == INT32_MAX) {
+        const int e = atomic_load_explicit(&po->epoch, memory_order_relaxed) + 1;
+        atomic_store_explicit(&po->epoch, e, memory_order_release);
+        atomic_store_explicit(&po->att_epoch[v], e, memory_order_release);
+        po->att_list[po->natt++] = v;
+    }
+    pthread_mutex_unlock(&po->mu);
+    return SRT_OK;
+}
+
+/* seq of the first run in L made while both ends were attached (epoch >= a), or INT64_MAX */
+static int64_t valid_run(const po_list* L, int32_t a) {
+    if (!L) return INT64_MAX;
+    for (int32_t i = 0; i < L->count; i++)
+        if (L->r[i].epoch >= a) return L->r[i].seq;
+    return INT64_MAX;
+}
+
+static int32_t att_of(const srt_pair_order* po, int32_t v) {
+    return atomic_load_explicit(&po->att_epoch[v], memory_order_acquire);
+}
+
+/* per-source mode: the end whose run stored {x, y} (-1: not stored yet) */
+static int32_t stored_from_raw(const srt_pair_order* po, int32_t x, int32_t y) {
+    const int32_t ax = att_of(po, x), ay = att_of(po, y);
+    const int32_t a = ax > ay ? ax : ay;
+    const int64_t sx = valid_run(atomic_load_explicit(&po->runs[x], memory_order_acquire), a);
+    const int64_t sy = valid_run(atomic_load_explicit(&po->runs[y], memory_order_acquire), a);
+    if (sx == INT64_MAX && sy == INT64_MAX) return -1;
+    return sx < sy ? x : y;
+}
+
+/* the same, as one consistent snapshot of both run lists */
+static int32_t stored_from(srt_pair_order* po, int32_t x, int32_t y) {
+    for (;;) {
+        const uint64_t v1 = atomic_load_explicit(&po->version, memory_order_acquire);
+        if (v1 & 1u) {
+            sched_yield();
+            continue;
+        }
+        const int32_t f = stored_from_raw(po, x, y);
+        atomic_thread_fence(memory_order_acquire);
+        if (atomic_load_explicit(&po->version, memory_order_relaxed) == v1) return f;
+    }
+}
+
+static int32_t last_epoch(const srt_pair_order* po, int32_t v) {
+    const po_list* L = atomic_load_explicit(&po->runs[v], memory_order_acquire);
+    return L && L->count ? L->r[L->count - 1].epoch : -1;
+}
+
+/* Record a source run of x in the current epoch and list the targets it stores (caller holds
+ * mu). Returns the number of stored targets (in po->scratch), or a negative error. */
+static int32_t record_run(srt_pair_order* po, int32_t x) {
+    const int32_t e = atomic_load_explicit(&po->epoch, memory_order_acquire);
+    po_list* old = atomic_load_explicit(&po->runs[x], memory_order_relaxed);
+    const int32_t cnt = old ? old->count : 0;
+    po_list* L = (po_list*)malloc(sizeof(po_list) + (size_t)(cnt + 1) * sizeof(po_run));
+    if (!L) return SRT_E_NOMEM;
+    if (old && po->nretired == po->cap_retired) {
+        const size_t nc = po->cap_retired ? 2 * po->cap_retired : 64;
+        po_list** nr = (po_list**)realloc(po->retired, nc * sizeof(po_list*));
+        if (!nr) {
+            free(L);
+            return SRT_E_NOMEM;
+        }
+        po->retired = nr;
+        po->cap_retired = nc;
+    }
+    L->count = cnt + 1;
+    if (cnt) memcpy(L->r, old->r, (size_t)cnt * sizeof(po_run));
+    const int64_t seq = ++po->next_seq;
+    L->r[cnt].epoch = e;
+    L->r[cnt].pad = 0;
+    L->r[cnt].seq = seq;
+    /* seqlock write: readers retry across the swap */
+    atomic_fetch_add_explicit(&po->version, 1, memory_order_relaxed);
+    atomic_thread_fence(memory_order_release);
+    atomic_store_explicit(&po->runs[x], L, memory_order_release);
+    atomic_fetch_add_explicit(&po->version, 1, memory_order_release);
+    if (old) po->retired[po->nretired++] = old;
+    /* targets stored by this run: attached y != x whose pair this run decides */
+    int32_t k = 0;
+    for (int32_t i = 0; i < po->natt; i++) {
+        const int32_t y = po->att_list[i];
+        if (y == x) continue;
+        const int32_t ay = att_of(po, y), ax = att_of(po, x);
+        const int32_t a = ax > ay ? ax : ay;
+        if (valid_run(L, a) != seq) continue; /* stored by an earlier run of x, or y not attached */
+        if (valid_run(atomic_load_explicit(&po->runs[y], memory_order_relaxed), a) < seq) continue;
+        po->scratch[k++] = y;
+    }
+    return k;
+}
+
+static void pair_index(int32_t s, int32_t t, size_t* word, unsigned* shift, int32_t* lo, int32_t* hi) {
+    const int32_t a = s < t ? s : t, b = s < t ? t : s;
+    const uint64_t idx = (uint64_t)b * (uint64_t)(b - 1) / 2 + (uint64_t)a;
+    *word = (size_t)(idx / 32);
+    *shift = (unsigned)(2 * (idx % 32));
+    *lo = a;
+    *hi = b;
+}
+
+int32_t srt_pair_order_lookup(srt_pair_order* po, int32_t s, int32_t t, srt_pair_store_fn on_store,
+                              void* ctx) {
+    if (!po || s < 0 || t < 0 || s >= po->n || t >= po->n) return SRT_E_ARG;
+    if (att_of(po, s) == INT32_MAX || att_of(po, t) == INT32_MAX) return SRT_E_UNATTACHED;
+    if (s == t) { /* (s, s): the self path, stored on its first lookup (:1597-1599, :1573) */
+        if (!atomic_exchange_explicit(&po->self_done[s], 1, memory_order_acq_rel) && on_store)
+            on_store(ctx, s, &s, 1);
+        return s;
+    }
+    if (!po->per_source) { /* direct mode: the pair itself (:1816-1858) */
+        size_t w;
+        unsigned sh;
+        int32_t lo, hi;
+        pair_index(s, t, &w, &sh, &lo, &hi);
+        uint64_t old = atomic_load_explicit(&po->pairbits[w], memory_order_acquire);
+        for (;;) {
+            const uint64_t bits = (old >> sh) & 3u;
+            if (bits & 1u) return (bits & 2u) ? hi : lo;
+            const uint64_t want = 1u | (s == hi ? 2u : 0u);
+            if (atomic_compare_exchange_weak_explicit(&po->pairbits[w], &old, old | (want << sh),
+                                                      memory_order_acq_rel, memory_order_acquire)) {
+                if (on_store) on_store(ctx, s, &t, 1);
+                return s;
+            }
+        }
+    }
+    int32_t f = stored_from(po, s, t);
+    if (f == s) return s;
+    if (f == t && (!po->directed || last_epoch(po, s) == atomic_load(&po->epoch))) return t;
+    /* a miss: source s runs (undirected: the pair is not stored; directed: (s, t) is not, and s
+     * has not run since the attached set last grew) */
+    pthread_mutex_lock(&po->mu);
+    f = stored_from_raw(po, s, t);
+    const int run = po->directed ? (f != s && last_epoch(po, s) != atomic_load(&po->epoch)) : f < 0;
+    if (run) {
+        const int32_t k = record_run(po, s);
+        if (k < 0) {
+            pthread_mutex_unlock(&po->mu);
+            return k;
+        }
+        if (on_store && k > 0) on_store(ctx, s, po->scratch, k);
+        f = stored_from_raw(po, s, t);
+    }
+    pthread_mutex_unlock(&po->mu);
+    return f;
+}
+
+int32_t srt_pair_order_peek(srt_pair_order* po, int32_t s, int32_t t) {
+    if (!po || s < 0 || t < 0 || s >= po->n || t >= po->n) return SRT_E_ARG;
+    if (s == t) return atomic_load(&po->self_done[s]) ? s : -1;
+    if (!po->per_source) {
+        size_t w;
+        unsigned sh;
+        int32_t lo, hi;
+        pair_index(s, t, &w, &sh, &lo, &hi);
+        const uint64_t bits = (atomic_load(&po->pairbits[w]) >> sh) & 3u;
+        return (bits & 1u) ? ((bits & 2u) ? hi : lo) : -1;
+    }
+    return stored_from(po, s, t);
+}
+
+int32_t srt_pair_order_runs(srt_pair_order* po, int32_t v) {
+    if (!po || v < 0 || v >= po->n || !po->per_source) return 0;
+    const po_list* L = atomic_load(&po->runs[v]);
+    return L ? L->count : 0;
+}

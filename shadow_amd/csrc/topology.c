@@ -3,9 +3,12 @@
  * with the all-pairs tables built eagerly on MI355X.
  *
  * Load + validation restate topology.c:326-1122; attach restates :2024-2281; the lookup API keeps
- * the semantics of :1900-2022 but reads one row-major table instead of running lazy Dijkstra
- * under a global lock. Tables are immutable once built, so lookups are lock-free; only the
- * IP -> vertex map (attach/detach) and the packet counters take locks.
+ * the semantics of :1900-2022 but reads row-major tables holding every source's own row instead of
+ * running lazy Dijkstra under a global lock. Which row serves a pair -- the first source run that
+ * stored it, as in the reference's lazy cache (:1189-1215, :1917-1967) -- is decided by
+ * pairorder.c. Tables are immutable once built, so lookups are lock-free once their pair is
+ * stored; the IP -> vertex map (attach/detach), a first run per source and the packet counters
+ * take locks.
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -113,7 +116,7 @@ static void ipmap_del(ipmap_t* m, uint32_t k) {
     }
 }
 
-/* ---- packet counters, keyed like the reference's cached Path (one per unordered pair) ---- */
+/* ---- packet counters, one per cached Path (the served pair's source, target) ------------ */
 typedef struct {
     uint64_t* keys;
     uint64_t* cnt;
@@ -186,10 +189,11 @@ struct _Topology {
     int build_failed;
     int ngpus;
     uint64_t quantum_ns;
-    /* runahead export (topology.c:1253-1264): the attach generation it covers, the last value */
+    /* which cached path serves a pair (pairorder.c) */
+    srt_pair_order* po;
+    /* runahead (topology.c:1253-1264): minimumPathLatency over the stored paths, 0 = none yet */
     pthread_mutex_t min_lock;
-    atomic_int min_gen;
-    double min_exported;
+    double min_path_ms;
     srt_build_opts opts;
     srt_build_stats stats;
     /* counters */
@@ -214,6 +218,7 @@ typedef struct tables {
     double* rel;        /* nslot x nslot */
     double* lat_ms;     /* f64 path-order ms (sub-ms edge latencies), else NULL */
     uint32_t min_q;     /* smallest entry (diagonal included) */
+    atomic_int checked_gen; /* attach generation this table was last found to cover */
     struct tables* prev;
 } tables_t;
 
@@ -532,8 +537,7 @@ static Topology* topology_from_text(const char* text, size_t len, int useShortes
     pthread_mutex_init(&t->min_lock, NULL);
     atomic_store(&t->tb, NULL);
     atomic_store(&t->attach_gen, 0);
-    atomic_store(&t->min_gen, 0);
-    t->min_exported = -1.0;
+    t->min_path_ms = 0.0;
     t->ngpus = 1;
     t->opts.device = 0;
     t->opts.algo = SRT_ALGO_AUTO;
@@ -546,6 +550,12 @@ static Topology* topology_from_text(const char* text, size_t len, int useShortes
     if (!validate_and_extract(t)) {
         srt_log(SRT_LOG_ERROR, "we failed to create the simulation topology because we were unable "
                 "to validate the topology gml file");
+        topology_free(t);
+        return NULL;
+    }
+    t->po = srt_pair_order_new(t->n, t->directed, t->use_shortest_path);
+    if (!t->po) {
+        srt_log(SRT_LOG_ERROR, "out of memory for the path order of %d vertices", t->n);
         topology_free(t);
         return NULL;
     }
@@ -603,6 +613,7 @@ void topology_free(Topology* t) {
     pthread_mutex_destroy(&t->build_lock);
     pthread_mutex_destroy(&t->cnt_lock);
     attach_index_free(t);
+    srt_pair_order_free(t->po);
     pthread_mutex_destroy(&t->ax_lock);
     pthread_mutex_destroy(&t->min_lock);
     t->magic = 0;
@@ -919,6 +930,7 @@ static int32_t attach_common(Topology* t, uint32_t ipNet, uint32_t* rand_state, 
     ipmap_put(&t->ipmap, ipNet, v);
     if (!t->attached[v]) {
         t->attached[v] = 1;
+        srt_pair_order_attach(t->po, v);
         atomic_fetch_add(&t->attach_gen, 1);
     }
     pthread_rwlock_unlock(&t->ip_lock);
@@ -970,6 +982,7 @@ int32_t srt_topology_attach_batch_ip(Topology* t, int32_t nhosts, const uint32_t
         ipmap_put(&t->ipmap, ipNet[h], vs[h]);
         if (!t->attached[vs[h]]) {
             t->attached[vs[h]] = 1;
+            srt_pair_order_attach(t->po, vs[h]);
             atomic_fetch_add(&t->attach_gen, 1);
         }
     }
@@ -1074,29 +1087,48 @@ double srt_topology_min_latency_ms(Topology* t) {
     return m < 0 ? 0.0 : m;
 }
 
-/* The reference hands every new smallest path latency to worker_updateMinTimeJump as it caches
- * paths (topology.c:1253-1264, controller.c:141-153). The tables hold every attached pair at
- * once, so the minimum over them is handed over once per attach generation, and only when it
- * is below the last value handed over. */
-static void export_min(Topology* t) {
-    const int gen = atomic_load(&t->attach_gen);
-    if (atomic_load(&t->min_gen) == gen) return;
+/* _topology_storePathInCache's minimum (topology.c:1253-1264): a stored path below the minimum so
+ * far (or the first one: 0 means none) becomes the minimum and goes to worker_updateMinTimeJump.
+ * The reference hands it over once per stored path; here one source run offers the smallest of
+ * the paths it stored, which leaves the controller's minimum (controller.c:141-153) the same after
+ * every run. A 0-ms path (a vertex without edges) would trip controller.c:144's assertion in the
+ * reference; it is logged and not handed over. */
+static void offer_min(Topology* t, double ms) {
     pthread_mutex_lock(&t->min_lock);
-    const tables_t* tb = atomic_load_explicit(&t->tb, memory_order_acquire);
-    if (tb && atomic_load(&t->min_gen) != gen) {
-        pthread_rwlock_rdlock(&t->ip_lock);
-        const double m = attached_min_ms(t, tb);
-        pthread_rwlock_unlock(&t->ip_lock);
-        if (m >= 0 && (t->min_exported < 0 || m < t->min_exported)) {
-            t->min_exported = m;
+    if (t->min_path_ms == 0.0 || ms < t->min_path_ms) {
+        t->min_path_ms = ms;
+        if (ms > 0.0) {
             if (g_min_hook)
-                g_min_hook(m);
+                g_min_hook(ms);
             else
-                worker_updateMinTimeJump(m);
+                worker_updateMinTimeJump(ms);
+        } else {
+            srt_log(SRT_LOG_WARNING, "a stored path has latency %g ms: not handed to "
+                    "worker_updateMinTimeJump (it requires > 0, controller.c:144)", ms);
         }
-        atomic_store(&t->min_gen, gen);
     }
     pthread_mutex_unlock(&t->min_lock);
+}
+
+typedef struct {
+    Topology* t;
+    const tables_t* tb;
+} store_ctx;
+
+/* srt_pair_store_fn: the paths src -> targets[] a lookup just stored (under the pair order's
+ * lock, so runs offer their minima in run order) */
+static void on_paths_stored(void* vctx, int32_t src, const int32_t* targets, int32_t count) {
+    const store_ctx* c = (const store_ctx*)vctx;
+    const int32_t a = c->tb->slot_of[src];
+    if (a < 0) return;
+    double best = -1.0;
+    for (int32_t i = 0; i < count; i++) {
+        const int32_t b = c->tb->slot_of[targets[i]];
+        if (b < 0) continue; /* attached after this table was built (a concurrent attach) */
+        const double ms = tables_latency_ms(c->t, c->tb, (size_t)a * c->tb->nslot + b);
+        if (best < 0.0 || ms < best) best = ms;
+    }
+    if (best >= 0.0) offer_min(c->t, best);
 }
 
 static int tables_cover_attached(const Topology* t, const tables_t* tb) {
@@ -1125,6 +1157,7 @@ static int build_generation(Topology* t, int nGPUs) {
         tb->slot_of[v] = t->attached[v] ? k : -1;
         if (t->attached[v]) tb->verts[k++] = v;
     }
+    atomic_store(&tb->checked_gen, atomic_load(&t->attach_gen));
     pthread_rwlock_unlock(&t->ip_lock);
     if (k == 0 || k == n) { /* nothing attached yet, or everything: the full table */
         tb->all = 1;
@@ -1178,6 +1211,7 @@ static const tables_t* ensure_tables(Topology* t, int nGPUs) {
     tb = atomic_load_explicit(&t->tb, memory_order_acquire);
     pthread_rwlock_rdlock(&t->ip_lock);
     const int ok = tables_cover_attached(t, tb);
+    if (ok) atomic_store(&((tables_t*)tb)->checked_gen, atomic_load(&t->attach_gen));
     pthread_rwlock_unlock(&t->ip_lock);
     if (!ok && !t->build_failed) {
         const int rc = build_generation(t, nGPUs);
@@ -1195,7 +1229,6 @@ int topology_computeShortestPaths(Topology* t, int nGPUs) {
     if (!magic_ok(t)) return SRT_E_ARG;
     t->ngpus = nGPUs > 1 ? nGPUs : 1;
     if (!ensure_tables(t, t->ngpus)) return t->build_failed ? SRT_E_DEVICE : SRT_E_NOMEM;
-    export_min(t);
     return SRT_OK;
 }
 
@@ -1222,8 +1255,9 @@ int srt_topology_table_info(Topology* t, const int32_t** verts, int32_t* nslot, 
     return SRT_OK;
 }
 
-/* _topology_getPathEntry (topology.c:1900-1981): the tables holding the pair and its index, or
- * NULL with *err set. */
+/* _topology_getPathEntry (topology.c:1900-1981): the tables holding the pair, the index of the
+ * path it is served from (row of the path's source) and that path's ends (*sv = its source, *dv =
+ * the other end), or NULL with *err set. */
 static const tables_t* path_entry(Topology* t, uint32_t srcIp, uint32_t dstIp, size_t* idx,
                                   int32_t* sv, int32_t* dv, int* err) {
     int32_t s = srt_topology_vertex_of_ip(t, srcIp);
@@ -1238,20 +1272,27 @@ static const tables_t* path_entry(Topology* t, uint32_t srcIp, uint32_t dstIp, s
         *err = SRT_E_UNATTACHED;
         return NULL;
     }
+    /* a miss stores paths to every attached vertex (topology.c:1604), so the tables must cover
+     * every vertex attached so far, not only s and d */
     const tables_t* tb = atomic_load_explicit(&t->tb, memory_order_acquire);
-    if (!tb || tb->slot_of[s] < 0 || tb->slot_of[d] < 0) {
+    if (!tb || atomic_load_explicit(&tb->checked_gen, memory_order_relaxed) !=
+                   atomic_load_explicit(&t->attach_gen, memory_order_relaxed)) {
         tb = ensure_tables(t, t->ngpus);
         if (!tb || tb->slot_of[s] < 0 || tb->slot_of[d] < 0) {
             srt_log(SRT_LOG_ERROR, "unable to find path between vertex %d and vertex %d", s, d);
             abort(); /* utility_panic (topology.c:1970-1976) */
         }
     }
-    if (atomic_load_explicit(&t->min_gen, memory_order_relaxed) !=
-        atomic_load_explicit(&t->attach_gen, memory_order_relaxed))
-        export_min(t);
-    *idx = (size_t)tb->slot_of[s] * tb->nslot + tb->slot_of[d];
-    if (sv) *sv = s;
-    if (dv) *dv = d;
+    store_ctx ctx = {t, tb};
+    const int32_t from = srt_pair_order_lookup(t->po, s, d, on_paths_stored, &ctx);
+    if (from < 0) {
+        srt_log(SRT_LOG_ERROR, "unable to find path between vertex %d and vertex %d (%d)", s, d, from);
+        abort(); /* utility_panic (topology.c:1970-1976) */
+    }
+    const int32_t to = from == s ? d : s;
+    *idx = (size_t)tb->slot_of[from] * tb->nslot + tb->slot_of[to];
+    if (sv) *sv = from;
+    if (dv) *dv = to;
     return tb;
 }
 
@@ -1273,18 +1314,15 @@ double srt_topology_reliability_ip(Topology* t, uint32_t srcIp, uint32_t dstIp) 
     return tb->rel[i];
 }
 
-static uint64_t counter_key(Topology* t, int64_t s, int64_t d) {
-    if (!t->directed && d < s) {
-        int64_t x = s;
-        s = d;
-        d = x;
-    }
-    return ((uint64_t)s << 32 | (uint64_t)d) + 1; /* 0 = empty slot */
+/* the served Path (source, target) -- path_incrementPacketCount on the cached object (:1983-1993);
+ * a pair has one Path whichever direction is looked up */
+static uint64_t counter_key(int64_t from, int64_t to) {
+    return ((uint64_t)from << 32 | (uint64_t)to) + 1; /* 0 = empty slot */
 }
 
-static int increment_pair(Topology* t, int32_t s, int32_t d) {
+static int increment_pair(Topology* t, int32_t from, int32_t to) {
     pthread_mutex_lock(&t->cnt_lock);
-    uint64_t* c = cnt_slot(&t->counters, counter_key(t, s, d));
+    uint64_t* c = cnt_slot(&t->counters, counter_key(from, to));
     if (c) (*c)++;
     pthread_mutex_unlock(&t->cnt_lock);
     return c ? SRT_OK : SRT_E_NOMEM;
@@ -1299,14 +1337,22 @@ int srt_topology_increment_ip(Topology* t, uint32_t srcIp, uint32_t dstIp) {
     return increment_pair(t, s, d);
 }
 
+int32_t srt_topology_path_source_ip(Topology* t, uint32_t srcIp, uint32_t dstIp) {
+    if (!magic_ok(t)) return -1;
+    const int32_t s = srt_topology_vertex_of_ip(t, srcIp), d = srt_topology_vertex_of_ip(t, dstIp);
+    if (s < 0 || d < 0) return -1;
+    const int32_t from = srt_pair_order_peek(t->po, s, d);
+    return from < 0 ? -1 : from;
+}
+
 uint64_t srt_topology_packet_count_ip(Topology* t, uint32_t srcIp, uint32_t dstIp) {
     if (!magic_ok(t)) return 0;
-    size_t i;
-    int32_t s, d;
-    int err;
-    if (!path_entry(t, srcIp, dstIp, &i, &s, &d, &err)) return 0;
+    const int32_t s = srt_topology_vertex_of_ip(t, srcIp), d = srt_topology_vertex_of_ip(t, dstIp);
+    if (s < 0 || d < 0) return 0;
+    const int32_t from = srt_pair_order_peek(t->po, s, d);
+    if (from < 0) return 0;
     pthread_mutex_lock(&t->cnt_lock);
-    uint64_t* c = cnt_slot(&t->counters, counter_key(t, s, d));
+    uint64_t* c = cnt_slot(&t->counters, counter_key(from, from == s ? d : s));
     uint64_t v = c ? *c : 0;
     pthread_mutex_unlock(&t->cnt_lock);
     return v;

@@ -566,9 +566,10 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
         uint32_t d = 0;
         for (;;) {
             /* next non-empty bucket at or after d (circular), found by every wave itself: bcnt
-             * is final since the step's last post-arc barrier, a full one (the pushed entries
-             * are visible), and nothing writes it before every wave has passed the next scan
-             * barrier -- no workgroup barrier and broadcast here */
+             * and bst are final since the step's last post-arc barrier, a full one (the pushed
+             * entries are visible), and nothing writes either before every wave has passed the
+             * first chunk's scan barrier (the popped and the skipped buckets are reset there), so
+             * every wave finds the same bucket -- no workgroup barrier and broadcast here */
             int found = -1;
             const uint32_t p0 = d & bm;
             for (int q = 0; q < nb && found < 0; q += WL) {
@@ -578,12 +579,6 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                 if (bal) found = q + __ffsll((long long)bal) - 1;
             }
             if (found < 0) break;
-            /* the buckets skipped over are empty (a searching wave reads either their old or
-             * their zeroed counts: empty both ways) and take no push before their value wraps */
-            if (two && tid < found) {
-                bcnt[(p0 + (uint32_t)tid) & bm] = 0;
-                bst[(p0 + (uint32_t)tid) & bm] = 0;
-            }
             d += (uint32_t)found;
             const int b = (int)(d & bm), b1 = (int)((d + 1u) & bm);
             const int st0 = (int)bst[b], st1 = two ? (int)bst[b1] : 0;
@@ -630,6 +625,14 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                     bcnt[b] = 0;
                     bst[b] = 0;
                     if (two) bst[b1] = (uint32_t)(st1 + n1);
+                }
+                /* the buckets the search skipped over (bcnt == bst: consumed, or empty) restart
+                 * at 0/0 for their next wrap; reset only here, after every wave's search, so no
+                 * wave can read an old bcnt beside a zeroed bst. No push targets them before the
+                 * arcs below, which follow the next barrier. */
+                if (c0 == 0 && two && tid < found) {
+                    bcnt[(p0 + (uint32_t)tid) & bm] = 0;
+                    bst[(p0 + (uint32_t)tid) & bm] = 0;
                 }
                 int base = 0, total = 0;
                 for (int q = 0; q < WG / WL; ++q) {
@@ -886,8 +889,10 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     SRT_HIPCHK(hipStreamSynchronize(st));
     /* compact 8-byte arcs: original order, a reliability table, w < 128, arcs < 2^20 */
     const char* cenv = getenv("SRT_WG_COMPACT");
+    const char* tenv = getenv("SRT_WGSSSP_THREADS"); /* 512: the 16-byte-arc form only */
+    const bool t512 = tenv && atoi(tenv) == 512;
     const bool cmp = !inv && ridx && rtab && max_w < 128 && last.y < (1 << 20) &&
-                     !(cenv && atoi(cenv) == 0);
+                     !(cenv && atoi(cenv) == 0) && !t512;
     g_sparse_form = 4 | (inv ? 0 : 1) | (cmp ? 2 : 0);
     void* ca = NULL;
     const size_t arc_bytes = cmp ? sizeof(uint2) : sizeof(uint4);
@@ -914,7 +919,6 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     }
     SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)nsrc * sizeof(int), st));
     const size_t dyn = (size_t)((n + 2) / 3) * sizeof(uint32_t);
-    const char* tenv = getenv("SRT_WGSSSP_THREADS");
     const char* penv = getenv("SRT_WGSSSP_PROF"); /* tools: per-phase cycle counts on stderr */
     if (penv && atoi(penv) > 0) {
         unsigned long long* prof = NULL;
@@ -924,6 +928,12 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
             wgsssp_kernel<1024, true, true, true><<<(unsigned)slots, 1024, dyn, st>>>(
                 n, src_begin, srcs, nsrc, rowptr, ca, rtab, inv, lat, rel, (size_t)n, ws, nb, bcap,
+                ovf, prof, two);
+        } else if (!inv) { /* original order: the output row is the working row */
+            SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true, true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+            wgsssp_kernel<1024, true, true><<<(unsigned)slots, 1024, dyn, st>>>(
+                n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap,
                 ovf, prof, two);
         } else {
             SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true>,
@@ -957,11 +967,20 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
                 100 * tot[12] / cyc, 100 * tot[13] / cyc, 100 * tot[14] / cyc, 100 * tot[3] / cyc);
         free(h);
         SRT_HIPCHK(hipFree(prof));
-    } else if (tenv && atoi(tenv) == 512) {
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<512>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-        wgsssp_kernel<512><<<(unsigned)slots, 512, dyn, st>>>(n, src_begin, srcs, nsrc, rowptr, ca, r, inv,
-                                                             lat, rel, (size_t)n, ws, nb, bcap, ovf);
+    } else if (t512) { /* 16-byte arcs; ORIG follows inv as below */
+        if (!inv) {
+            SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<512, false, true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+            wgsssp_kernel<512, false, true><<<(unsigned)slots, 512, dyn, st>>>(
+                n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf,
+                nullptr, two);
+        } else {
+            SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<512>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+            wgsssp_kernel<512><<<(unsigned)slots, 512, dyn, st>>>(
+                n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf,
+                nullptr, two);
+        }
     } else if (cmp) { /* original order, compact arcs, reliabilities from the table */
         SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, false, true, true>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));

@@ -173,6 +173,37 @@ def random_geometric(n: int, seed: int = 3, avg_degree: float = 8.0, loss_max: i
     return Graph(n, False, src, dst, lat.astype(np.int64), loss, name or f"rgg{n}")
 
 
+def directed_rgg(n: int, seed: int = 3, avg_degree: float = 8.0, loss_max: int = 100,
+                 lat_max: int = 300, name: str = "") -> Graph:
+    """random_geometric's structure with both orientations of every edge as separate directed
+    edges of independent latency and loss (strongly connected), self-loops kept."""
+    g = random_geometric(n, seed=seed, avg_degree=avg_degree, loss_max=loss_max)
+    off = g.src != g.dst
+    a, b = g.src[off].astype(np.uint64), g.dst[off].astype(np.uint64)
+    src = np.concatenate([a, b, g.src[~off].astype(np.uint64)])
+    dst = np.concatenate([b, a, g.dst[~off].astype(np.uint64)])
+    lat = np.concatenate([(np.uint64(1) + hash_u64(seed, 7, src[:2 * len(a)], dst[:2 * len(a)])
+                           % np.uint64(lat_max)).astype(np.int64) * MS, g.lat_ns[~off]])
+    k = hash_u64(seed, 8, src[:2 * len(a)], dst[:2 * len(a)]) % np.uint64(loss_max + 1)
+    loss = np.concatenate([k.astype(np.float64) / 10000.0, g.loss[~off]])
+    return Graph(n, True, src.astype(np.int32), dst.astype(np.int32), lat, loss,
+                 name or f"drgg{n}")
+
+
+def complete_directed(n: int, seed: int, lat_max: int = 300, self_max: int = 10,
+                      loss_max: int = 500, name: str = "") -> Graph:
+    """Complete directed graph with self-loops: edge (i, j) for every ordered pair, i -> j and
+    j -> i drawn independently (topology.c:409-511 calls it complete)."""
+    i, j = np.meshgrid(np.arange(n, dtype=np.uint64), np.arange(n, dtype=np.uint64), indexing="ij")
+    i, j = i.ravel(), j.ravel()
+    self_loop = i == j
+    lat = np.where(self_loop, np.uint64(1) + hash_u64(seed, 2, i, j) % np.uint64(self_max),
+                   np.uint64(1) + hash_u64(seed, 9, i, j) % np.uint64(lat_max))
+    k = hash_u64(seed, 10, i, j) % np.uint64(loss_max + 1)
+    return Graph(n, True, i.astype(np.int32), j.astype(np.int32), lat.astype(np.int64) * MS,
+                 k.astype(np.float64) / 10000.0, name or f"dcomplete{n}")
+
+
 def barabasi_albert(n: int, m: int = 3, seed: int = 5, lat_max: int = 100, loss_max: int = 100,
                     self_max: int = 10, name: str = "") -> Graph:
     """Preferential attachment: clique on m+1 vertices, each new vertex links to m distinct

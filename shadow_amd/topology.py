@@ -196,6 +196,11 @@ class Topology:
     def packet_count(self, src, dst) -> int:
         return lib().srt_topology_packet_count_ip(self._h, ip_to_net(src), ip_to_net(dst))
 
+    def path_source(self, src, dst) -> int:
+        """Vertex whose source run stored the path a lookup (src, dst) is served from (-1: none
+        yet); the lazy-cache order of topology.c:1189-1215, :1900-1981."""
+        return lib().srt_topology_path_source_ip(self._h, ip_to_net(src), ip_to_net(dst))
+
     def send_packet(self, src, dst, chance: float, bootstrapping: bool = False,
                     payload_length: int = 1):
         """worker_sendPacket's decision (worker.c:541-555): (delivered, delay_ns or None)."""

@@ -7,9 +7,11 @@ Sources of truth, in order of strength:
      docs/network_graph_spec.md:16-37, src/test/config/convert/topology.expected.gml (directed)
      -- the GML texts are data fixtures copied from those files;
   2. the units-grammar known answers of src/main/core/support/units.rs:583-722;
-  3. C1 (50-node tor-style complete graph): the C oracle's table, with the latency matrix
-     cross-checked against networkx (third-party Dijkstra) and, for pairs whose shortest path is
-     unique, the reliability cross-checked against the product along networkx's path;
+  3. C1 (50-node tor-style complete graph): the C oracle's raw per-source table, with the latency
+     matrix cross-checked against networkx (third-party Dijkstra) and, for pairs whose shortest
+     path is unique, the reliability of both directions cross-checked against the products along
+     networkx's path (forward for s -> t, reversed for t -> s); rel_served_ascending is the table
+     the reference serves when sources run in increasing vertex order;
   4. hand-built tie graphs whose expected values are derived by hand below (the canonical tie
      rule of SURVEY.md §8a-4);
   5. attach cases from oracle/attach.py (restatement of topology.c:2024-2216).
@@ -151,7 +153,8 @@ def known_answers():
 
 
 def tie_graphs():
-    """Hand-derived expectations for the canonical tie rule."""
+    """Hand-derived expectations for the canonical tie rule. Every pair (s, t)
+    is source s's own path (the raw row; which row serves a lookup is the lazy-cache order)."""
     def gml(n, edges, directed=False):
         edge_store.append({"n": n, "directed": directed, "edges": edges})
         g = ["graph [", f"  directed {1 if directed else 0}"]
@@ -179,15 +182,23 @@ def tie_graphs():
     e = [(0, 1, 2, 0.1), (1, 3, 3, 0.2), (0, 2, 3, 0.3), (2, 3, 2, 0.4)] + \
         [(v, v, 50, 0.0) for v in range(4)]
     cases.append({"name": "square_pred_by_distance", "gml": gml(4, e), "pairs": [
-        [0, 3, 5 * MS, (1.0 * 0.9) * 0.8], [3, 0, 5 * MS, (1.0 * 0.9) * 0.8],
+        [0, 3, 5 * MS, (1.0 * 0.9) * 0.8],
+        # (3,0) from source 3: 3-1-0 (3+2) ties 3-2-0 (2+3); pred(3,0)=2 (D[3][2]=2 < D[3][1]=3)
+        [3, 0, 5 * MS, (1.0 * 0.6) * 0.7],
         # (1,2) from source 1: 1-0-2 (2+3) ties 1-3-2 (3+2); pred(1,2)=0 (D[1][0]=2 < D[1][3]=3)
-        [1, 2, 5 * MS, (1.0 * 0.9) * 0.7], [2, 1, 5 * MS, (1.0 * 0.9) * 0.7]]})
+        [1, 2, 5 * MS, (1.0 * 0.9) * 0.7],
+        # (2,1) from source 2: 2-0-1 (3+2) ties 2-3-1 (2+3); pred(2,1)=3 (D[2][3]=2 < D[2][0]=3)
+        [2, 1, 5 * MS, (1.0 * 0.6) * 0.8]]})
     # T3 diamond with equal D[u]: pred(0,3) among u=1,2 (both D=1) -> lower index 1
     e = [(0, 1, 1, 0.1), (0, 2, 1, 0.2), (1, 3, 1, 0.3), (2, 3, 1, 0.4)] + \
         [(v, v, 50, 0.0) for v in range(4)]
     cases.append({"name": "diamond_pred_by_index", "gml": gml(4, e), "pairs": [
-        [0, 3, 2 * MS, (1.0 * 0.9) * 0.7], [3, 0, 2 * MS, (1.0 * 0.9) * 0.7],
-        [1, 2, 2 * MS, (1.0 * 0.9) * 0.8], [2, 1, 2 * MS, (1.0 * 0.9) * 0.8],
+        [0, 3, 2 * MS, (1.0 * 0.9) * 0.7],
+        # (3,0) from source 3: D[3][1] = D[3][2] = 1 -> lower index 1: 3-1-0
+        [3, 0, 2 * MS, (1.0 * 0.7) * 0.9],
+        [1, 2, 2 * MS, (1.0 * 0.9) * 0.8],
+        # (2,1) from source 2: D[2][0] = D[2][3] = 1 -> lower index 0: 2-0-1
+        [2, 1, 2 * MS, (1.0 * 0.8) * 0.9],
         [0, 0, 2 * MS, 0.9 * 0.9], [3, 3, 2 * MS, 0.7 * 0.7]]})
     # T4 directed: the true directed table (no reference symmetry quirk)
     e = [(0, 1, 1, 0.1), (1, 0, 5, 0.2), (1, 2, 1, 0.3), (2, 0, 1, 0.4), (0, 2, 10, 0.5),
@@ -200,7 +211,7 @@ def tie_graphs():
     # T5 no self-loops: diagonal from the cheapest incident edge, doubled
     e = [(0, 1, 7, 0.1), (1, 2, 3, 0.2)]
     cases.append({"name": "path_no_selfloops", "gml": gml(3, e), "pairs": [
-        [0, 2, 10 * MS, (1.0 * 0.9) * 0.8], [2, 0, 10 * MS, (1.0 * 0.9) * 0.8],
+        [0, 2, 10 * MS, (1.0 * 0.9) * 0.8], [2, 0, 10 * MS, (1.0 * 0.8) * 0.9],
         [0, 0, 14 * MS, 0.9 * 0.9], [1, 1, 6 * MS, 0.8 * 0.8], [2, 2, 6 * MS, 0.8 * 0.8]]})
     # T6 parallel edges collapse to the (min latency, lowest index) edge
     e = [(0, 1, 9, 0.5), (0, 1, 4, 0.3), (0, 1, 4, 0.1), (1, 2, 1, 0.0), (0, 0, 50, 0.0),
@@ -259,8 +270,9 @@ def c1():
     g = graphs.complete_graph(50, seed=1, lat_max=300, self_max=10, loss_max=500, name="C1")
     gml = graphs.to_gml(g)
     el = oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
-    t = oracle.table(el, True, oracle.ORC_INT_NS)
-    tf = oracle.table(el, True, oracle.ORC_F64_MS)
+    t = oracle.table(el, True, oracle.ORC_INT_NS, raw=True)
+    tf = oracle.table(el, True, oracle.ORC_F64_MS, raw=True)
+    served = oracle.table(el, True, oracle.ORC_INT_NS)  # sources in increasing vertex order
     assert np.array_equal(t["lat_int"], tf["lat_int"]) and np.array_equal(t["rel"], tf["rel"])
     assert np.array_equal(t["lat_int"], t["lat_ref"]), "whole-ms graph: integer ns == ceil(ms*1e6)"
     import networkx as nx
@@ -270,6 +282,7 @@ def c1():
         if a != b:
             G.add_edge(a, b, weight=int(g.lat_ns[e]), r=1.0 - float(g.loss[e]))
     nx_unique = 0
+    unique_dir_differ = 0  # unique shortest path, yet rel(s->t) != rel(t->s) bitwise
     for s in range(g.n):
         dist = nx.single_source_dijkstra_path_length(G, s, weight="weight")
         for t_, d in dist.items():
@@ -282,14 +295,22 @@ def c1():
                 rel = 1.0
                 for a, b in zip(p[:-1], p[1:]):
                     rel *= G[a][b]["r"]
-                assert t["rel"][s, t_] == rel and t["rel"][t_, s] == rel
+                back = 1.0  # source t_'s own row multiplies the same hops in reverse order
+                for a, b in zip(p[::-1][:-1], p[::-1][1:]):
+                    back *= G[a][b]["r"]
+                assert t["rel"][s, t_] == rel and t["rel"][t_, s] == back
                 nx_unique += 1
+                unique_dir_differ += int(rel != back)
+    off = ~np.eye(g.n, dtype=bool)
+    dir_differ = int((t["rel"][off] != t["rel"].T[off]).sum()) // 2
     np.savez_compressed(os.path.join(HERE, "c1_expected.npz"), lat_ns=t["lat_int"],
-                        rel=t["rel"], lat_ms=t["lat_ms"])
+                        rel=t["rel"], lat_ms=t["lat_ms"], rel_served_ascending=served["rel"])
     with open(os.path.join(HERE, "c1.gml"), "w") as f:
         f.write(gml)
     return {"n": g.n, "edges": g.m, "networkx_version": nx.__version__,
-            "pairs_with_unique_path_checked": nx_unique}
+            "pairs_with_unique_path_checked": nx_unique,
+            "unique_path_pairs_rel_direction_differs": unique_dir_differ,
+            "pairs_rel_direction_differs": dir_differ}
 
 
 def main():
@@ -303,7 +324,7 @@ def main():
         e = np.array(case["edges"], dtype=np.float64)
         el = oracle.EdgeList(case["n"], case["directed"], e[:, 0].astype(np.int32),
                              e[:, 1].astype(np.int32), (e[:, 2] * MS).astype(np.int64), e[:, 3])
-        t = oracle.table(el, True)
+        t = oracle.table(el, True, raw=True)
         for s_, t_, lat, rel in case["pairs"]:
             assert int(t["lat_int"][s_, t_]) == lat and t["rel"][s_, t_] == rel, (case["name"], s_, t_)
     with open(os.path.join(HERE, "ties.json"), "w") as f:

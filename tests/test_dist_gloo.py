@@ -3,10 +3,10 @@
 The GPU path (srt_dense_build_sharded / srt_sparse_allgather) runs one process per GPU over
 RCCL. Here the same schedule -- the library's own srt_shard_rows partition, the owner of each
 64-row pivot block, one pivot-panel broadcast per round in the lookahead order (panel k+1 is
-produced from a partially updated round k), the essential-arc all-reduce/broadcast,
-the undirected mirror exchange (rank q sends rel[q rows][r cols] to every r > q) and the sparse
-source-shard all-gather -- is replayed with numpy compute and gloo collectives, and the
-assembled tables must equal the CPU oracle's. The row-sharded symmetric rounds (kept-tile
+produced from a partially updated round k), the essential-arc all-reduce/broadcast and the
+sparse source-shard all-gather -- is replayed with numpy compute and gloo collectives, and the
+assembled tables must equal the CPU oracle's raw per-source rows (no mirror exchange: each rank's
+rows are its own sources', and the lookup layer picks the serving row, pairorder.c). The row-sharded symmetric rounds (kept-tile
 checkerboard, panel blocks broadcast by their holders, final transpose fill) are replayed the
 same way.
 """
@@ -156,23 +156,10 @@ def _dense_worker(rank, R, port, n, seed, q):
             if t != s:
                 rr[t] = rr[pred[t]] * Rm[pred[t], t]
         rel[i, :n] = rr
-    # mirror exchange: q sends rel[q rows][r cols] to r > q; r stores the transpose (s > t)
-    for x in range(R):
-        for y in range(x + 1, R):
-            yb, ye = owners[y]
-            xb, xe = owners[x]
-            if rank == x:
-                dist.send(torch.from_numpy(np.ascontiguousarray(rel[:, yb:ye])), y)
-            elif rank == y:
-                buf = torch.zeros((xe - xb, ye - yb), dtype=torch.float64)
-                dist.recv(buf, x)
-                rel[:, xb:xe] = buf.numpy().T
-    for i in range(e - b):  # local diagonal block mirror + diagonal rule
+    for i in range(e - b):  # diagonal rule
         s = b + i
         if s >= n:
             continue
-        for t in range(b, s):
-            rel[i, t] = rel[t - b, s]
         cands = [((W[s, u] if u == s else 2 * W[s, u]), u) for u in range(n)]
         lat_d, u = min(cands)
         D[i, s] = lat_d
@@ -362,7 +349,7 @@ def test_dense_sharded_schedule_gloo(native):
     lat = np.concatenate([x[3] for x in res])[:n].astype(np.uint64) * np.uint64(1_000_000)
     rel = np.concatenate([x[4] for x in res])[:n]
     g = graphs.complete_graph(n, seed=seed)
-    exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss))
+    exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss), raw=True)
     assert np.array_equal(lat, exp["lat_int"])
     assert np.array_equal(rel, exp["rel"])
 

@@ -34,6 +34,6 @@ def test_bench_json_line_contract(workload):
     assert cb["kind"] in ("port", "reference") and cb["cores"] == 1 and cb["value"] > 0
     assert cb["all_cores"]["cores"] >= 1 and cb["all_cores"]["value"] > 0
     assert d["parity"]["lat_bit_exact"] is True
-    assert d["parity"]["rel_max_rel_err_upper"] <= 1e-12
+    assert d["parity"]["rel_max_rel_err"] <= 1e-12
     assert d["parity"]["rows_checked"] >= 4 and d["parity"]["tied_pairs"] >= 0
     assert 0.0 <= d["parity"]["tied_frac"] < 0.5

@@ -1,12 +1,13 @@
 """C4 at full size in -m gpu: the 32,768-node complete graph through the default one-GPU schedule
 (encoding 7: u16 f16-compare upper-triangle 256-pivot rounds on two update streams, the 8-wave
-update kernel, XCD-remapped grid, u8
-predecessor slab, rel_levels_kernel<1024>), against the CPU oracle's dense Dijkstra
-(oracle.complete_sample) on rows spread over every 4k block, including the last tile row.
+update kernel, XCD-remapped grid, u8 predecessor slab, rel_levels_kernel<1024>), against the CPU
+oracle's dense Dijkstra (oracle.complete_sample) on rows spread over every 4k block, including the
+last tile row.
 
-Latency bit-exact in integer ns; reliability within 1e-12 relative (north_star) on the entries the
-row's own source computed (t > s; the lower triangle is the symmetry mirror, checked against the
-transposed rows).
+Latency bit-exact in integer ns; reliability within 1e-12 relative (north_star) on every entry off
+the diagonal: each row is its own source's row (no mirror; the lookup layer serves a pair from the
+row of whichever end ran first, pairorder.c). The test also reports how often the two directions'
+reliabilities differ, which is what makes the serving order observable.
 """
 import ctypes
 
@@ -47,7 +48,7 @@ def test_c4_full_size_default_schedule(gpu):
     glat = lat.index_select(0, idx).cpu().numpy().view(np.uint32).astype(np.uint64) \
         * np.uint64(1_000_000)
     grel = rel.index_select(0, idx).cpu().numpy()
-    # the mirrored columns of the same sources (rel[t][s] for t < s comes from row t)
+    # the other direction of the same pairs (rel[t][s]: row t's own path to s)
     gcol = rel.index_select(1, idx).cpu().numpy().T
     tied = int(st.tied_pairs)
     del lat, rel
@@ -55,13 +56,94 @@ def test_c4_full_size_default_schedule(gpu):
     diag = np.arange(n)[None, :] == rows[:, None]
     bad = np.argwhere(np.where(diag, 0, glat) != np.where(diag, 0, clat))
     assert bad.size == 0, f"{len(bad)} latency mismatches, first {bad[:5].tolist()}"
-    upper = np.arange(n)[None, :] > rows[:, None]
+    off = ~diag
     err = np.abs(grel - crel) / np.maximum(crel, 1e-300)
-    assert float(err[upper].max()) <= REL_TOL
-    # symmetry rule: the lower triangle of row s equals the column s of the rows t < s
-    lower = np.arange(n)[None, :] < rows[:, None]
-    assert np.array_equal(grel[lower], gcol[lower])
+    assert float(err[off].max()) <= REL_TOL
+    # the two directions of a pair: ties and the reversed product order can make them differ
+    differ = int((grel[off] != gcol[off]).sum())
+    print(f"C4 sampled pairs whose rel(s->t) != rel(t->s) bitwise: {differ} of {int(off.sum())}")
     # tied pairs (canonical rule vs igraph's heap order) are counted: on C4 about half of the
     # pairs have two or more tight predecessors at the same smallest D[s][u] (many 1-2 ms arcs)
     assert 0 < tied < n * (n - 1)
     print(f"C4 tied pairs: {tied} ({tied / (n * (n - 1)):.4f} of the pairs)")
+
+
+@pytest.mark.parametrize("ranks", [4, 8])
+def test_c4_virtual_ranks_sharded_schedule(gpu, ranks):
+    """The N-GPU C4 schedule at full size on ONE GPU (VERDICT r02 "configs_untested"): `ranks`
+    host threads, each a virtual rank on device 0 with its own streams and workspaces, generate
+    their row block of C4 on the device and run srt_dense_build_sharded over a virtual
+    communicator (the broadcasts, all-reduces and the final transpose fill as device copies
+    ordered by events and host barriers) -- the host logic of the 4- and 8-GPU runs: partition,
+    owners, 128-pivot row-sharded symmetric rounds (encoding 8), band staging and the post pass's
+    essential-arc exchange. Checked against the oracle: >= 4 rows of every rank (its first, last,
+    and two inside), the last tile row (32640-32767) and the rows either side of every rank
+    boundary."""
+    import threading
+    import torch
+    L = _lib.lib()
+    n = ld = N
+    comms = (ctypes.c_void_p * ranks)()
+    _lib.check(L.srt_comm_init_virtual(ranks, 0, comms), "srt_comm_init_virtual")
+    shards, bufs, streams = [], [], []
+    try:
+        for r in range(ranks):
+            b, e = ctypes.c_int32(), ctypes.c_int32()
+            L.srt_shard_rows(ld, 128, ranks, r, ctypes.byref(b), ctypes.byref(e))
+            b, e = b.value, e.value
+            assert e > b
+            w = torch.empty((e - b, ld), dtype=torch.int32, device="cuda")
+            rr = torch.empty((e - b, ld), dtype=torch.float64, device="cuda")
+            st = torch.cuda.Stream()
+            _lib.check(L.srt_gen_complete_device(n, ld, b, e - b, SEED, LAT_MAX, SELF_MAX, LOSS_MAX,
+                                                 w.data_ptr(), rr.data_ptr(),
+                                                 ctypes.c_void_p(st.cuda_stream)), "generate")
+            shards.append((b, e))
+            bufs.append((w, rr, torch.empty_like(w), torch.empty_like(rr)))
+            streams.append(st)
+        torch.cuda.synchronize()
+        rcs = [None] * ranks
+        stats = [_lib.BuildStats() for _ in range(ranks)]
+
+        def work(r):
+            L.srt_virtual_rank_bind(r, 0)
+            w, rr, lat, rel = bufs[r]
+            rcs[r] = L.srt_dense_build_sharded(ctypes.c_void_p(comms[r]), n, ld, 0, w.data_ptr(),
+                                               rr.data_ptr(), lat.data_ptr(), rel.data_ptr(),
+                                               ctypes.c_void_p(streams[r].cuda_stream), 0,
+                                               ctypes.byref(stats[r]))
+            L.srt_virtual_rank_bind(-1, 0)
+
+        th = [threading.Thread(target=work, args=(r,)) for r in range(ranks)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        torch.cuda.synchronize()
+        for r in range(ranks):
+            _lib.check(rcs[r], f"rank {r}")
+            assert stats[r].dist_enc == 8, (r, stats[r].dist_enc)
+        rows = set(range(32640, 32768, 37)) | {32767}
+        for b, e in shards:
+            rows |= {b, e - 1, b + (e - b) // 3, b + 2 * (e - b) // 3}
+            if b > 0:
+                rows |= {b - 1, b - 64, b + 63}  # a 128-row band straddling the boundary
+        rows = np.array(sorted(rows), np.int32)
+        glat = np.empty((len(rows), n), np.uint64)
+        grel = np.empty((len(rows), n))
+        for i, s in enumerate(rows):
+            r = [q for q, (b, e) in enumerate(shards) if b <= s < e][0]
+            b = shards[r][0]
+            glat[i] = bufs[r][2][s - b, :n].cpu().numpy().view(np.uint32).astype(np.uint64) \
+                * np.uint64(1_000_000)
+            grel[i] = bufs[r][3][s - b, :n].cpu().numpy()
+    finally:
+        for r in range(ranks):
+            L.srt_comm_free(ctypes.c_void_p(comms[r]))
+    del bufs
+    clat, crel, _, _ = oracle.complete_sample(n, SEED, LAT_MAX, SELF_MAX, LOSS_MAX, rows, 16)
+    off = np.arange(n)[None, :] != rows[:, None]
+    bad = np.argwhere(np.where(off, glat, 0) != np.where(off, clat, 0))
+    assert bad.size == 0, f"{len(bad)} latency mismatches, first {bad[:5].tolist()}"
+    err = np.abs(grel - crel) / np.maximum(crel, 1e-300)
+    assert float(err[off].max()) <= REL_TOL

@@ -9,8 +9,9 @@ order, against the CPU oracle.
   full table restricted to the subset, for dense / sparse / directed graphs and virtual ranks.
 * f64 path-order milliseconds (topology.c:1308, :1364): sub-millisecond edges give the
   reference's latency and worker.c:551's ceil(ms * 1e6) delay exactly.
-* Runahead export (topology.c:1253-1264): worker_updateMinTimeJump receives the minimum over
-  attached pairs under the documented build order and after later attaches.
+* Runahead export (topology.c:1253-1264): worker_updateMinTimeJump receives each smaller path
+  latency as the lookups' source runs store paths (the eager build stores none), in both build
+  orders and after later attaches.
 * The reference-signature entry points (topology_attach / getLatency / getReliability /
   isRoutable / incrementPathPacketCounter / detach) with Address and Random laid out as
   address.c:23-25 and random.c:15-18.
@@ -36,28 +37,22 @@ def _el(g):
 
 
 def _check_sampled_rows(lat, rel, g, rows, what):
-    """Full-table rows vs the oracle's raw rows: latency off the diagonal, reliability where the
-    row's own source computed it (t > s for undirected, every t for directed)."""
+    """Full-table rows vs the oracle's raw rows off the diagonal (every row is its own
+    source's)."""
     exp = oracle.sssp_list(_el(g), rows, nthreads=16)
     for i, s in enumerate(rows):
         off = np.arange(g.n) != s
         assert np.array_equal(lat[s][off], exp["lat_int"][i][off]), (what, s)
-        keep = (np.arange(g.n) > s) if not g.directed else off
-        err = np.abs(rel[s][keep] - exp["rel"][i][keep]) / np.maximum(exp["rel"][i][keep], 1e-300)
+        err = np.abs(rel[s][off] - exp["rel"][i][off]) / np.maximum(exp["rel"][i][off], 1e-300)
         assert float(err.max() if err.size else 0.0) <= REL_TOL, (what, s)
 
 
 def _expected_sub(g, verts, nthreads=16):
-    """The oracle's table restricted to the subset, built from raw rows of the subset's sources:
-    latency [i][j] = row(verts[i])[verts[j]]; reliability from the row of min(s, t) when
-    undirected (the symmetry rule). The diagonal is left out (NaN / 0)."""
-    k = len(verts)
+    """The oracle's raw rows of the subset's sources restricted to the subset:
+    [i][j] = row(verts[i])[verts[j]]. The diagonal is left out (0)."""
     rows = oracle.sssp_list(_el(g), verts, nthreads=nthreads)
     lat = rows["lat_int"][:, verts].copy()
     rel = rows["rel"][:, verts].copy()
-    if not g.directed:
-        low = np.tril_indices(k, -1)
-        rel[low] = rel.T[low]
     np.fill_diagonal(lat, 0)
     np.fill_diagonal(rel, 0.0)
     return lat, rel
@@ -70,7 +65,9 @@ def test_auto_dispatch_c3_rgg_20000_full_table(gpu):
     lat, rel, st = build_tables(g.n, False, g.src, g.dst, g.lat_ns, g.loss, algo=ALGO_AUTO)
     assert st.algo == ALGO_SPARSE_SSSP and st.dist_enc == 1
     _check_sampled_rows(lat, rel, g, rows, "C3 AUTO")
-    assert np.array_equal(rel, rel.T)
+    assert np.array_equal(lat, lat.T)
+    off = ~np.eye(g.n, dtype=bool)
+    print(f"C3 pairs whose rel(s->t) != rel(t->s) bitwise: {int((rel != rel.T)[off].sum()) // 2}")
     lat2, rel2, st2 = build_tables(g.n, False, g.src, g.dst, g.lat_ns, g.loss, algo=ALGO_AUTO,
                                    ngpus=1)
     assert st2.algo == ALGO_SPARSE_SSSP
@@ -144,7 +141,7 @@ def test_subset_tables_equal_restricted_full_table(gpu, which, algo):
     g = {"complete300": lambda: graphs.complete_graph(300, seed=21),
          "rgg2000": lambda: graphs.random_geometric(2000, seed=3),
          "directed": _directed_graph}[which]()
-    full = oracle.table(_el(g), True, oracle.ORC_INT_NS, 8)
+    full = oracle.table(_el(g), True, oracle.ORC_INT_NS, 8, raw=True)
     rng = np.random.default_rng(3)
     verts = np.sort(rng.choice(g.n, min(g.n, 77), replace=False)).astype(np.int32)
     lat, rel, ms, mn, st = build_tables_subset(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
@@ -185,7 +182,7 @@ def _sub_ms_graph(kind):
                                        ("directed", ALGO_SPARSE_SSSP)])
 def test_f64_ms_path_order_latency(gpu, kind, algo):
     g = _sub_ms_graph(kind)
-    full = oracle.table(_el(g), True, oracle.ORC_INT_NS, 8)
+    full = oracle.table(_el(g), True, oracle.ORC_INT_NS, 8, raw=True)
     lat, rel, ms, _, st = build_tables_subset(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
                                               algo=algo, want_ms=True)
     assert np.array_equal(lat, full["lat_int"])
@@ -208,60 +205,74 @@ def test_f64_ms_path_order_latency(gpu, kind, algo):
 
 
 def test_sub_ms_latency_through_topology_and_packet_path(gpu):
-    """GML with microsecond latencies -> getLatency == the reference's f64 ms sum and the packet
-    delay == ceil(ms * 1e6) (worker.c:551) on every attached pair."""
+    """GML with microsecond latencies -> getLatency == the reference's f64 ms sum along the serving
+    source's path, and the packet delay == ceil(ms * 1e6) (worker.c:551), on every looked-up pair
+    (lazy-cache order, oracle/lazy_cache.py)."""
+    from oracle.lazy_cache import LazyPathCache
     g = _sub_ms_graph("complete")
     top = Topology.from_gml(graphs.to_gml(g))
-    full = oracle.table(_el(g), True, oracle.ORC_INT_NS, 8)
+    full = oracle.table(_el(g), True, oracle.ORC_INT_NS, 8, raw=True)
+    sim = LazyPathCache(full, directed=False)
     ips = [f"100.1.{v}.1" for v in range(g.n)]
     hosts = list(range(0, g.n, 3))
     for v in hosts:
         vert, _, _, _ = top.attach(ips[v], 1, ip_hint=f"11.0.0.{v + 1}")
         assert vert == v
+        sim.attach(ips[v], v)
     top.compute_shortest_paths()
     verts, ms = top.table_vertices()
     assert np.array_equal(verts, np.array(hosts)) and ms is not None
     for s in hosts[::4]:
-        for d in hosts[::3]:
-            assert top.get_latency(ips[s], ips[d]) == full["lat_ms"][s, d]
+        for d in hosts[::3][::-1]:
+            assert top.get_latency(ips[s], ips[d]) == sim.get_latency(ips[s], ips[d])
             ok, delay = top.send_packet(ips[s], ips[d], 0.0)
-            assert ok and delay == int(full["lat_ref"][s, d])
+            assert (ok, delay) == sim.send_packet(ips[s], ips[d], 0.0)
 
 
 def test_runahead_export_documented_order(gpu):
-    """Attach first, then build (controller.c:367 before the eager build): one export, the
-    minimum over attached pairs; a later attach of a new vertex exports again only if smaller."""
+    """Attach first, then build (controller.c:367 before the eager build): the build stores no
+    path, so nothing is exported; each lookup that runs a source hands over the smallest latency
+    it stored when that is below the minimum so far (topology.c:1253-1264), as the reference's
+    lazy cache does (oracle/lazy_cache.py). A later attach of a new vertex changes nothing until
+    a run stores its pairs."""
+    from oracle.lazy_cache import LazyPathCache
     calls = []
     cb = set_min_time_jump_hook(lambda ms: calls.append(ms))
     try:
         g = graphs.complete_graph(60, seed=13)
         top = Topology.from_gml(graphs.to_gml(g))
-        full = oracle.table(_el(g), True, oracle.ORC_INT_NS, 8)
+        full = oracle.table(_el(g), True, oracle.ORC_INT_NS, 8, raw=True)
+        sim = LazyPathCache(full, directed=False)
         ips = [f"100.2.{v}.1" for v in range(g.n)]
         first = [3, 7, 11, 20, 41]
         for v in first:
             top.attach(ips[v], 1, ip_hint=f"11.0.0.{v + 1}")
-        assert calls == []
+            sim.attach(ips[v], v)
         top.compute_shortest_paths()
         verts, _ = top.table_vertices()
         assert list(verts) == first  # tables over the attached vertices only
-        m1 = int(full["lat_int"][np.ix_(first, first)].min()) / 1e6
-        assert calls == [m1]
-        top.get_latency(ips[3], ips[41])
+        assert calls == []
+        assert top.get_latency(ips[3], ips[41]) == sim.get_latency(ips[3], ips[41])
+        m1 = min(full["lat_ms"][3, t] for t in first if t != 3)
+        assert calls == [m1] and sim.minimum_path_latency == m1
         top.compute_shortest_paths()
-        assert calls == [m1]  # nothing new attached: no second export
-        # a host on a new vertex: the next lookup rebuilds over the grown set and exports
-        # the new minimum only when it is smaller
+        assert calls == [m1]  # nothing new stored
+        for s, d in ((41, 3), (7, 7), (20, 11), (11, 7)):
+            top.get_reliability(ips[s], ips[d])
+            sim.get_reliability(ips[s], ips[d])
+            assert calls[-1] == sim.minimum_path_latency
+        # a host on a new vertex: the next lookup rebuilds over the grown set
         v_new = int(np.argmin(np.diag(full["lat_int"])))
         if v_new in first:
             v_new = 0
         top.attach(ips[v_new], 1, ip_hint=f"11.0.0.{v_new + 1}")
-        both = sorted(first + [v_new])
-        assert top.get_latency(ips[v_new], ips[3]) == int(full["lat_int"][v_new, 3]) / 1e6
+        sim.attach(ips[v_new], v_new)
+        before = list(calls)
+        assert top.get_latency(ips[v_new], ips[3]) == sim.get_latency(ips[v_new], ips[3])
         verts, _ = top.table_vertices()
-        assert list(verts) == both
-        m2 = int(full["lat_int"][np.ix_(both, both)].min()) / 1e6
-        assert calls == ([m1, m2] if m2 < m1 else [m1])
+        assert list(verts) == sorted(first + [v_new])
+        assert (calls[-1] if calls else 0.0) == sim.minimum_path_latency
+        assert calls[:len(before)] == before and all(x > y for x, y in zip(calls, calls[1:]))
         top.free()
     finally:
         set_min_time_jump_hook(None)
@@ -269,14 +280,14 @@ def test_runahead_export_documented_order(gpu):
 
 
 def test_runahead_export_build_before_attach(gpu):
-    """Eager build before any attach (tables over every vertex): nothing exported until hosts
-    attach; the first lookup after the attaches exports the minimum over attached pairs."""
+    """Eager build before any attach (tables over every vertex): nothing exported until a lookup
+    runs a source; then the minimum over the paths it stored (the self path on its own lookup)."""
     calls = []
     cb = set_min_time_jump_hook(lambda ms: calls.append(ms))
     try:
         g = graphs.complete_graph(50, seed=14)
         top = Topology.from_gml(graphs.to_gml(g))
-        full = oracle.table(_el(g), True, oracle.ORC_INT_NS, 8)
+        full = oracle.table(_el(g), True, oracle.ORC_INT_NS, 8, raw=True)
         top.compute_shortest_paths()
         assert calls == []
         ips = [f"100.3.{v}.1" for v in range(g.n)]
@@ -284,7 +295,10 @@ def test_runahead_export_build_before_attach(gpu):
         for v in att:
             top.attach(ips[v], 1, ip_hint=f"11.0.0.{v + 1}")
         top.get_reliability(ips[2], ips[30])
-        assert calls == [int(full["lat_int"][np.ix_(att, att)].min()) / 1e6]
+        assert calls == [min(full["lat_ms"][2, 9], full["lat_ms"][2, 30])]
+        top.get_latency(ips[9], ips[9])  # the self path of 9 is stored on its own lookup
+        if full["lat_ms"][9, 9] < calls[0]:
+            assert calls[-1] == full["lat_ms"][9, 9]
         verts, _ = top.table_vertices()
         assert len(verts) == g.n  # the full table covers the attached set: no rebuild
         top.free()
@@ -342,3 +356,60 @@ def test_reference_signature_entry_points(gpu):
     assert L.topology_isRoutable(a._h, ctypes.byref(addrs[5]), ctypes.byref(addrs[6])) == 0
     a.free()
     b.free()
+
+
+def _both_orientations(g, seed):
+    """Directed variant: each undirected edge becomes two directed edges with independent
+    latencies (1..100,000 us) and losses; self-loops kept."""
+    rng = np.random.default_rng(seed)
+    off = g.src != g.dst
+    src = np.concatenate([g.src[off], g.dst[off], g.src[~off]]).astype(np.int32)
+    dst = np.concatenate([g.dst[off], g.src[off], g.dst[~off]]).astype(np.int32)
+    lat = np.concatenate([rng.integers(1, 100_001, 2 * int(off.sum())) * 1_000,
+                          g.lat_ns[~off]]).astype(np.int64)
+    loss = np.concatenate([rng.integers(0, 101, 2 * int(off.sum())) / 10000.0, g.loss[~off]])
+    return graphs.Graph(g.n, True, src, dst, lat, loss)
+
+
+@pytest.mark.parametrize("directed", [False, True])
+def test_fine_quantum_range_lifted(gpu, directed):
+    """a 100k power-law graph with 1..100,000 us latencies (quantum 1 us, so the
+    MST / (n - 1) * max_w bounds reach ~1e9-1e10 quanta) builds through AUTO: the hop bound
+    through the hub (graph.c) keeps every distance provably inside the u32 tables. Rows of 64
+    attached sources against the oracle."""
+    g = graphs.barabasi_albert(100_000, seed=15)
+    rng = np.random.default_rng(16)
+    if directed:
+        g = _both_orientations(g, 17)
+    else:
+        off = g.src != g.dst
+        lat = g.lat_ns.copy()
+        lat[off] = rng.integers(1, 100_001, int(off.sum())) * 1_000
+        g = graphs.Graph(g.n, False, g.src, g.dst, lat, g.loss)
+    q = ctypes.c_uint64()
+    mw = ctypes.c_uint32()
+    e = _lib_edges(g)
+    assert lib().srt_latency_quantum(ctypes.byref(e[0]), ctypes.byref(q), ctypes.byref(mw)) == 0
+    assert q.value == 1_000 and mw.value >= 99_000
+    verts = np.unique(np.concatenate([rng.choice(g.n, 62, replace=False), [0, g.n - 1]]))
+    verts = verts.astype(np.int32)
+    lat, rel, ms, mn, st = build_tables_subset(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                               verts=verts, algo=ALGO_AUTO, want_ms=True)
+    assert st.algo == ALGO_SPARSE_SSSP and ms is not None
+    rows = oracle.sssp_list(_el(g), verts, nthreads=16)
+    ix = np.ix_(np.arange(len(verts)), verts)
+    off = ~np.eye(len(verts), dtype=bool)
+    assert np.array_equal(lat[off], rows["lat_int"][ix][off])
+    assert np.array_equal(rel[off], rows["rel"][ix][off])
+    assert np.array_equal(ms[off], rows["lat_ms"][ix][off])  # f64 path-order ms (q = 1 us)
+    # the undirected MST bound here is ~2.15e9 quanta and the directed (n - 1) * max_w ~1e10,
+    # both past the u32 range; real distances reach ~2e5 quanta
+    assert int(lat[off].max()) // 1_000 > 100_000
+
+
+def _lib_edges(g):
+    from shadow_amd._lib import Edges
+    arrs = (np.ascontiguousarray(g.src, np.int32), np.ascontiguousarray(g.dst, np.int32),
+            np.ascontiguousarray(g.lat_ns, np.int64), np.ascontiguousarray(g.loss, np.float64))
+    e = Edges(g.n, int(g.directed), len(g.src), *(a.ctypes.data for a in arrs))
+    return e, arrs

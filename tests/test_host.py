@@ -280,16 +280,18 @@ def test_bench_parity_rows_cover_first_and_last_rank(native):
     rows = bench.parity_rows(FakeCtx(), lambda q: blocks[q], n, 4)
     assert rows[0] == 0 and 4095 in rows and 28672 in rows and n - 1 in rows
     assert all(r < 4096 or r >= 28672 for r in rows)
-    # compare_rows: the diagonal is ignored, reliability is judged on t > s only
+    # compare_rows: the diagonal is ignored, every other entry of a row is its source's own
     sample = np.array([0, 3], np.int32)
     lat = np.arange(2 * 6, dtype=np.uint64).reshape(2, 6)
     rel = np.linspace(0.5, 1.0, 12).reshape(2, 6)
     lat2, rel2 = lat.copy(), rel.copy()
     lat2[0, 0] += 7          # diagonal: own rule, not compared
-    rel2[1, 1] = 0.0         # lower triangle of row 3: the mirror, not compared
+    rel2[1, 3] = 0.0
     r = bench.compare_rows(sample, 6, lat2, rel2, lat, rel)
-    assert r["lat_bit_exact"] and r["rel_max_rel_err_upper"] == 0.0 and r["rel_exact_frac_upper"] == 1.0
+    assert r["lat_bit_exact"] and r["rel_max_rel_err"] == 0.0 and r["rel_exact_frac"] == 1.0
+    rel2[1, 1] *= 1.0 + 1e-9  # t < s: compared too (no mirror)
+    r = bench.compare_rows(sample, 6, lat2, rel2, lat, rel)
+    assert r["lat_bit_exact"] and r["rel_max_rel_err"] > 0.0
     lat2[1, 5] += 1
-    rel2[1, 4] *= 1.0 + 1e-9
     r = bench.compare_rows(sample, 6, lat2, rel2, lat, rel)
-    assert not r["lat_bit_exact"] and r["rel_max_rel_err_upper"] > 0.0
+    assert not r["lat_bit_exact"]

@@ -38,7 +38,7 @@ def test_known_answers_single_vertex():
 @pytest.mark.parametrize("case", json.load(open(os.path.join(GOLDEN, "ties.json"))),
                          ids=lambda c: c["name"])
 def test_tie_graphs(case):
-    t = oracle.table(_edges_from_case(case))
+    t = oracle.table(_edges_from_case(case), raw=True)
     for s, d, lat_ns, rel in case["pairs"]:
         assert int(t["lat_int"][s, d]) == lat_ns, (s, d)
         assert t["rel"][s, d] == rel, (s, d)
@@ -49,14 +49,18 @@ def test_c1_regression_and_modes():
     el = oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
     exp = np.load(os.path.join(GOLDEN, "c1_expected.npz"))
     for mode in (oracle.ORC_INT_NS, oracle.ORC_F64_MS):
-        t = oracle.table(el, True, mode, nthreads=2)
+        t = oracle.table(el, True, mode, nthreads=2, raw=True)
         assert np.array_equal(t["lat_int"], exp["lat_ns"])
         assert np.array_equal(t["rel"], exp["rel"])
+        served = oracle.table(el, True, mode, nthreads=2)
+        assert np.array_equal(served["rel"], exp["rel_served_ascending"])
     # whole-ms graph: exact integer ns equals the reference's ceil(ms * 1e6) (worker.c:551)
     assert np.array_equal(t["lat_ref"], t["lat_int"])
-    # undirected: one cached entry per pair
+    # undirected: latency is symmetric; each source's own reliability is not, bit for bit (the
+    # reversed product, and ties): the first source run decides what a pair serves
     assert np.array_equal(exp["lat_ns"], exp["lat_ns"].T)
-    assert np.array_equal(exp["rel"], exp["rel"].T)
+    assert np.array_equal(exp["rel_served_ascending"], exp["rel_served_ascending"].T)
+    assert not np.array_equal(exp["rel"], exp["rel"].T)
 
 
 def test_c1_against_networkx():
@@ -132,7 +136,7 @@ def _scipy_crosscheck(g):
         R.update({(b, a): x for (a, b), x in list(R.items())})
     D, P = csgraph.dijkstra(W, directed=True, return_predecessors=True)
     el = oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
-    t = oracle.table(el, nthreads=4)
+    t = oracle.table(el, nthreads=4, raw=True)
     Wd = W.toarray()
     checked = 0
     for s in range(n):
@@ -153,7 +157,7 @@ def _scipy_crosscheck(g):
             u = int(P[s, v])
             uniq[v] = len(tight) == 1 and uniq[u]
             rel[v] = rel[u] * R[(u, v)]
-            if uniq[v] and (g.directed or s < v):
+            if uniq[v]:  # every row is its own source's
                 assert t["rel"][s, v] == rel[v], (s, v)
                 checked += 1
     return checked
@@ -171,3 +175,50 @@ def test_oracle_against_scipy_dijkstra(which):
         g = graphs.complete_graph(120, seed=11, lat_max=8)
     checked = _scipy_crosscheck(g)
     assert checked > 0
+
+
+def test_lazy_cache_ascending_order_is_the_served_table():
+    """oracle/lazy_cache.py (the reference's lazy cache, topology.c:1900-1981) pinned on C1: with
+    every vertex attached and lookups (s, t) issued in increasing source order, each pair is served
+    from the row of min(s, t) -- exactly orc_table's served table; the reverse order serves the
+    row of max(s, t). Every source runs once, and the packet counts land on one Path per pair."""
+    from oracle.lazy_cache import LazyPathCache
+    g = graphs.complete_graph(50, seed=1, lat_max=300, self_max=10, loss_max=500)
+    el = oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
+    raw = oracle.table(el, True, raw=True)
+    exp = np.load(os.path.join(GOLDEN, "c1_expected.npz"))
+    for order in (1, -1):
+        sim = LazyPathCache(raw, directed=False)
+        for v in range(g.n):
+            sim.attach(v, v)
+        got = np.empty((g.n, g.n))
+        for s in range(g.n)[::order]:
+            for t in range(g.n)[::order]:
+                got[s, t] = sim.get_reliability(s, t)
+                sim.increment(t, s)
+        if order == 1:
+            assert np.array_equal(got, exp["rel_served_ascending"])
+        else:  # the row of max(s, t): the transpose of the ascending lower triangle
+            up = np.triu_indices(g.n, 1)
+            assert np.array_equal(got[up], raw["rel"].T[up])
+        assert sim.source_runs == g.n - 1  # the last source finds every pair cached
+        assert all(p.packets == (2 if p.src != p.dst else 1)
+                   for c in sim.cache.values() for p in c.values())
+
+
+def test_lazy_cache_directed_serves_the_first_run():
+    """Directed: the reference checks only (s, t) before computing (topology.c:1919), but falls
+    back to (t, s) after (:1963-1967) -- so lookup(s, t) after t's source ran returns t -> s."""
+    from oracle.lazy_cache import LazyPathCache
+    el = oracle.EdgeList(3, True, [0, 1, 1, 2, 0, 0, 1, 2], [1, 0, 2, 0, 2, 0, 1, 2],
+                         np.array([1, 5, 1, 1, 10, 50, 50, 50]) * MS, [0.1, 0.2, 0.3, 0.4, 0.5,
+                                                                       0.0, 0.0, 0.0])
+    raw = oracle.table(el, True, raw=True)
+    sim = LazyPathCache(raw, directed=True)
+    for v in range(3):
+        sim.attach(v, v)
+    assert sim.get_latency(1, 0) == 2.0            # source 1 runs: 1 -> 2 -> 0
+    assert sim.get_latency(0, 1) == 2.0            # served the 1 -> 0 path, not 0 -> 1 (1 ms)
+    assert raw["lat_ms"][0, 1] == 1.0
+    assert sim.get_latency(0, 2) == 2.0            # source 0 ran too: its own 0 -> 1 -> 2
+    assert sim.source_runs == 2
