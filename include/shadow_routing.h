@@ -143,6 +143,14 @@ int srt_dense_build_device(int32_t n, int32_t ld, int32_t directed, const uint32
 
 /* Synthetic graph generators on the device (seeded counter-based hash; identical to
  * shadow_amd/graphs.py so tests can rebuild the same graph on the host). */
+/* Rows of nsub sources (device vertex list dverts) on a dense device graph (w, r: ld x ld, as for
+ * srt_dense_build_device) without the all-pairs FW: Bellman-Ford passes on u16 quanta, canonical
+ * predecessors, path-order reliability, the diagonal rule. lat_rows / rel_rows: nsub x ld (row i =
+ * source dverts[i]). SRT_E_RANGE when n > 32768 or a distance reaches the u16 cap. The table
+ * builds take this path by themselves when at most n / 12 vertices are attached. */
+int srt_dense_rows_build(int32_t n, int32_t ld, int32_t nsub, const int32_t* dverts,
+                         const uint32_t* w, const double* r, uint32_t* lat_rows, double* rel_rows,
+                         void* stream, srt_build_stats* stats);
 int srt_gen_complete_device(int32_t n, int32_t ld, int32_t row0, int32_t nrows, uint64_t seed,
                             uint32_t lat_max_ms, uint32_t self_max_ms, uint32_t loss_max_e4,
                             uint32_t* w, double* r, void* stream);
@@ -197,6 +205,12 @@ int srt_comm_init_all(int32_t ndev, const int32_t* devices, srt_comm** comms);
  * no-op, so one rank's compute and critical chain at N ranks is measured without the wire. The
  * tables it produces are NOT correct. */
 int srt_comm_init_solo(int32_t nranks, int32_t rank, int32_t device, srt_comm** comm);
+/* srt_comm_init_solo with a wire model: each collective holds its stream for lat_us + the bytes
+ * this rank receives / gbps (GB/s), spun on the device wall clock; a group pays once, at its end.
+ * srt_comm_wire_ms: the modelled wire time issued so far. Timing only, like srt_comm_init_solo. */
+int srt_comm_init_solo_wire(int32_t nranks, int32_t rank, int32_t device, double gbps,
+                            double lat_us, srt_comm** comm);
+double srt_comm_wire_ms(const srt_comm* comm);
 int srt_comm_init_virtual(int32_t nranks, int32_t device, srt_comm** comms);
 /* Bind the calling host thread to virtual rank `rank` on `device` (its own workspaces and
  * streams) before it drives that rank's srt_dense_build_sharded / srt_sparse_graph_rows;

@@ -81,6 +81,7 @@ SIGNATURES = {
     "srt_dense_max_n": (ctypes.c_int, []),
     "srt_latency_quantum": (ctypes.c_int, [_VP, _VP, _VP]),
     "srt_dense_build_device": (ctypes.c_int, [_I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _I32, _VP]),
+    "srt_dense_rows_build": (ctypes.c_int, [_I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "srt_gen_complete_device": (ctypes.c_int, [_I32, _I32, _I32, _I32, _U64, _U32, _U32, _U32,
                                                 _VP, _VP, _VP]),
     "srt_sparse_max_n": (ctypes.c_int, []),
@@ -96,6 +97,8 @@ SIGNATURES = {
     "srt_comm_init_all": (ctypes.c_int, [_I32, _VP, _VP]),
     "srt_comm_init_virtual": (ctypes.c_int, [_I32, _I32, _VP]),
     "srt_comm_init_solo": (ctypes.c_int, [_I32, _I32, _I32, _VP]),
+    "srt_comm_init_solo_wire": (ctypes.c_int, [_I32, _I32, _I32, _D, _D, _VP]),
+    "srt_comm_wire_ms": (_D, [_VP]),
     "srt_virtual_rank_bind": (ctypes.c_int, [_I32, _I32]),
     "srt_comm_free": (None, [_VP]),
     "srt_shard_rows": (None, [_I32, _I32, _I32, _I32, _VP, _VP]),

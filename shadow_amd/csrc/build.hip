@@ -678,12 +678,47 @@ static int build_one(const srt_canon* c, const srt_build_opts* opts, int algo, i
         double* dr;
         TRY(dalloc(&B, (void**)&dw, ll * sizeof(uint32_t)));
         TRY(dalloc(&B, (void**)&dr, ll * sizeof(double)));
-        TRY(dalloc(&B, (void**)&dlat, ll * sizeof(uint32_t)));
-        TRY(dalloc(&B, (void**)&drel, ll * sizeof(double)));
-        if (lat_ms) TRY(dalloc(&B, (void**)&dms, ll * sizeof(double)));
         TRYHIP(hipMemcpyAsync(dw, hw, ll * sizeof(uint32_t), hipMemcpyHostToDevice, st));
         TRYHIP(hipMemcpyAsync(dr, hr, ll * sizeof(double), hipMemcpyHostToDevice, st));
-        if (use_sp) {
+        /* a few attached vertices: their rows alone (Bellman-Ford passes, ~6 nsub n^2 work)
+         * instead of the all-pairs FW (n^3 / 2), as the reference computes paths from attached
+         * sources only (topology.c:1604-1656); SRT_DENSE_ROWS=0 keeps the FW */
+        const char* renv = getenv("SRT_DENSE_ROWS");
+        int rows_used = 0;
+        if (use_sp && verts && (size_t)nsub * 12 <= (size_t)n && !(renv && atoi(renv) == 0)) {
+            uint32_t* rl;
+            double *rr, *rm = NULL;
+            TRY(dalloc(&B, (void**)&rl, (size_t)nsub * ld * sizeof(uint32_t)));
+            TRY(dalloc(&B, (void**)&rr, (size_t)nsub * ld * sizeof(double)));
+            if (lat_ms) TRY(dalloc(&B, (void**)&rm, (size_t)nsub * ld * sizeof(double)));
+            TRY(srt_dense_rows_build_device(n, ld, nsub, dverts, dw, dr, rl, rr, rm, q, c->directed,
+                                            st, &local, &rows_used));
+            if (rows_used) {
+                TRY(dalloc(&B, (void**)&slat, ns2 * sizeof(uint32_t)));
+                TRY(dalloc(&B, (void**)&srel, ns2 * sizeof(double)));
+                TRY(srt_gather_sub_u32(nsub, nsub, NULL, dverts, rl, ld, slat, nsub, st));
+                TRY(srt_gather_sub_f64(nsub, nsub, NULL, dverts, rr, ld, srel, nsub, st));
+                if (rm) {
+                    TRY(dalloc(&B, (void**)&sms, ns2 * sizeof(double)));
+                    TRY(srt_gather_sub_f64(nsub, nsub, NULL, dverts, rm, ld, sms, nsub, st));
+                }
+                TRY(srt_table_min(nsub, nsub, slat, nsub, dmin, st));
+                TRYHIP(hipMemcpyAsync(lat_q, slat, ns2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+                TRYHIP(hipMemcpyAsync(rel, srel, ns2 * sizeof(double), hipMemcpyDeviceToHost, st));
+                if (sms)
+                    TRYHIP(hipMemcpyAsync(lat_ms, sms, ns2 * sizeof(double), hipMemcpyDeviceToHost, st));
+                TRYHIP(hipMemcpyAsync(min_q, dmin, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+                TRYHIP(hipStreamSynchronize(st));
+            }
+        }
+        if (!rows_used) {
+            TRY(dalloc(&B, (void**)&dlat, ll * sizeof(uint32_t)));
+            TRY(dalloc(&B, (void**)&drel, ll * sizeof(double)));
+            if (lat_ms) TRY(dalloc(&B, (void**)&dms, ll * sizeof(double)));
+        }
+        if (rows_used) {
+            /* done: the attached rows */
+        } else if (use_sp) {
             TRY(srt_dense_build_device_ms(n, ld, c->directed, dw, dr, dlat, drel, dms, q, st,
                                           opts ? opts->fw_block : 0, &local));
         } else {
@@ -694,7 +729,8 @@ static int build_one(const srt_canon* c, const srt_build_opts* opts, int algo, i
             if (dms) TRY(srt_quanta_to_ms(n, n, dw, ld, q, dms, ld, st));
             local.algo = SRT_ALGO_DENSE_FW;
         }
-        if (verts) {
+        if (rows_used) {
+        } else if (verts) {
             TRY(dalloc(&B, (void**)&slat, ns2 * sizeof(uint32_t)));
             TRY(dalloc(&B, (void**)&srel, ns2 * sizeof(double)));
             TRY(srt_gather_sub_u32(nsub, nsub, dverts, dverts, dlat, ld, slat, nsub, st));
@@ -717,8 +753,10 @@ static int build_one(const srt_canon* c, const srt_build_opts* opts, int algo, i
                 TRYHIP(hipMemcpy2DAsync(lat_ms, (size_t)n * sizeof(double), dms, (size_t)ld * sizeof(double),
                                         (size_t)n * sizeof(double), n, hipMemcpyDeviceToHost, st));
         }
-        TRYHIP(hipMemcpyAsync(min_q, dmin, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        TRYHIP(hipStreamSynchronize(st));
+        if (!rows_used) {
+            TRYHIP(hipMemcpyAsync(min_q, dmin, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+            TRYHIP(hipStreamSynchronize(st));
+        }
         if (!use_sp) {
             for (size_t i = 0; i < ns2; i++)
                 if (lat_q[i] >= SRT_INF) {

@@ -33,6 +33,12 @@ struct srt_comm {
     int nranks, rank, device;
     srt_loop* loop; /* non-NULL: virtual ranks */
     int solo;       /* timing only: one rank alone, every collective a no-op (srt_comm_init_solo) */
+    /* solo wire model (srt_comm_init_solo_wire): each collective occupies its stream for
+     * wire_lat_us + bytes received / wire_gbps; a group's bytes are summed and paid at its end */
+    double wire_gbps, wire_lat_us, wire_ticks_per_us;
+    int in_group;
+    size_t group_bytes;
+    double wire_us_total; /* modelled wire time issued on the streams (ms_comm of a solo build) */
 };
 
 static thread_local int t_vslot = -1;
@@ -171,6 +177,54 @@ extern "C" int srt_comm_init_solo(int32_t nranks, int32_t rank, int32_t device, 
     return SRT_OK;
 }
 
+/* srt_comm_init_solo plus a wire model: every collective holds its stream for
+ * lat_us + (bytes this rank receives) / gbps, as a spin on the device's constant-rate wall clock,
+ * so one rank's schedule feels a wire of that speed without the peers (the other ranks' sends
+ * are what it waits for on a real node). gbps <= 0: no wire (srt_comm_init_solo). */
+extern "C" int srt_comm_init_solo_wire(int32_t nranks, int32_t rank, int32_t device, double gbps,
+                                       double lat_us, srt_comm** comm) {
+    int rc = srt_comm_init_solo(nranks, rank, device, comm);
+    if (rc) return rc;
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess ||
+        khz <= 0) {
+        srt_comm_free(*comm);
+        *comm = NULL;
+        srt_set_error("srt_comm_init_solo_wire: no wall-clock rate on device %d", device);
+        return SRT_E_DEVICE;
+    }
+    (*comm)->wire_gbps = gbps;
+    (*comm)->wire_lat_us = lat_us > 0 ? lat_us : 0.0;
+    (*comm)->wire_ticks_per_us = (double)khz / 1000.0;
+    return SRT_OK;
+}
+
+/* one wave spins until `ticks` of the constant-rate wall clock have passed (s_memrealtime) */
+__global__ __launch_bounds__(64) void wire_spin_kernel(uint64_t ticks) {
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+
+/* the stream a solo group's wire time is paid on: the one its first collective names */
+static thread_local hipStream_t t_group_stream = nullptr;
+
+static int solo_wire(const srt_comm* cc, size_t bytes, hipStream_t st) {
+    srt_comm* c = const_cast<srt_comm*>(cc);
+    if (c->wire_gbps <= 0.0) return SRT_OK;
+    if (c->in_group) {
+        c->group_bytes += bytes;
+        if (!t_group_stream) t_group_stream = st;
+        return SRT_OK;
+    }
+    const double us = c->wire_lat_us + (double)bytes / (c->wire_gbps * 1e3);
+    c->wire_us_total += us;
+    wire_spin_kernel<<<1, 64, 0, st>>>((uint64_t)(us * c->wire_ticks_per_us + 0.5));
+    SRT_HIPCHK(hipGetLastError());
+    return SRT_OK;
+}
+
+extern "C" double srt_comm_wire_ms(const srt_comm* c) { return c ? c->wire_us_total * 1e-3 : 0.0; }
+
 extern "C" int srt_virtual_rank_bind(int32_t rank, int32_t device) {
     srt_set_virtual_slot(rank);
     SRT_HIPCHK(hipSetDevice(device));
@@ -214,7 +268,7 @@ __global__ void allreduce_i32_kernel(int32_t* __restrict__ dst, const int32_t* _
 }
 
 int srt_coll_bcast(const srt_comm* c, void* buf, size_t bytes, int root, hipStream_t st) {
-    if (c->solo) return SRT_OK;
+    if (c->solo) return root == c->rank ? solo_wire(c, 0, st) : solo_wire(c, bytes, st);
     if (!c->loop) {
         SRT_NCCLCHK(ncclBroadcast(buf, buf, bytes, ncclUint8, root, c->nc, st));
         return SRT_OK;
@@ -239,7 +293,9 @@ int srt_coll_bcast(const srt_comm* c, void* buf, size_t bytes, int root, hipStre
 
 int srt_coll_allreduce_i32(const srt_comm* c, int32_t* buf, size_t count, int op_min,
                            hipStream_t st) {
-    if (c->solo) return SRT_OK;
+    /* ring all-reduce: 2 (R - 1) / R of the buffer in */
+    if (c->solo)
+        return solo_wire(c, 2 * (size_t)(c->nranks - 1) * count * sizeof(int32_t) / c->nranks, st);
     if (!c->loop) {
         SRT_NCCLCHK(ncclAllReduce(buf, buf, count, ncclInt32, op_min ? ncclMin : ncclSum, c->nc, st));
         return SRT_OK;
@@ -276,18 +332,34 @@ int srt_coll_allreduce_i32(const srt_comm* c, int32_t* buf, size_t count, int op
 
 int srt_coll_group_begin(const srt_comm* c) {
     if (!c->loop && !c->solo) SRT_NCCLCHK(ncclGroupStart());
+    if (c->solo) {
+        srt_comm* m = const_cast<srt_comm*>(c);
+        m->in_group = 1;
+        m->group_bytes = 0;
+        t_group_stream = nullptr;
+    }
     return SRT_OK;
 }
 
 int srt_coll_group_end(const srt_comm* c) {
     if (!c->loop && !c->solo) SRT_NCCLCHK(ncclGroupEnd());
+    if (c->solo && c->in_group) {
+        srt_comm* m = const_cast<srt_comm*>(c);
+        m->in_group = 0;
+        if (t_group_stream) return solo_wire(c, m->group_bytes, t_group_stream);
+    }
     return SRT_OK;
 }
 
 int srt_coll_exchange(const srt_comm* c, void* const* send, const size_t* send_bytes,
                       void* const* recv, const size_t* recv_bytes, hipStream_t st) {
     const int me = c->rank, R = c->nranks;
-    if (c->solo) return SRT_OK;
+    if (c->solo) {
+        size_t in = 0;
+        for (int q = 0; q < R; q++)
+            if (q != me) in += recv_bytes[q];
+        return solo_wire(c, in, st);
+    }
     if (!c->loop) {
         SRT_NCCLCHK(ncclGroupStart());
         for (int q = 0; q < R; q++)
@@ -342,7 +414,8 @@ int srt_comm_is_solo(const srt_comm* c) { return c ? c->solo : 0; }
 int srt_comm_size(const srt_comm* c) { return c ? c->nranks : 0; }
 
 int srt_coll_allgather(const srt_comm* c, void* buf, size_t bytes, hipStream_t st) {
-    if (c->solo || bytes == 0) return SRT_OK;
+    if (c->solo) return solo_wire(c, (size_t)(c->nranks - 1) * bytes, st);
+    if (bytes == 0) return SRT_OK;
     if (c->loop) { /* every rank broadcasts its block in turn */
         for (int q = 0; q < c->nranks; q++) {
             const int rc = srt_coll_bcast(c, (uint8_t*)buf + bytes * q, bytes, q, st);
@@ -362,7 +435,7 @@ extern "C" int srt_sparse_allgather(srt_comm* comm, int32_t n, int32_t rows_per_
     }
     hipStream_t st = (hipStream_t)stream;
     const size_t cnt = (size_t)rows_per_rank * n;
-    if (comm->solo) return SRT_OK;
+    if (comm->solo) return solo_wire(comm, (size_t)(comm->nranks - 1) * cnt * 12, st);
     if (comm->loop) { /* every rank broadcasts its block in turn */
         for (int q = 0; q < comm->nranks; q++) {
             int rc = srt_coll_bcast(comm, lat_all + cnt * q, cnt * sizeof(uint32_t), q, st);

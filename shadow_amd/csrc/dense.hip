@@ -713,9 +713,10 @@ __global__ __launch_bounds__(512) void rel_sweeps_kernel(int n, int ld, int row0
                                                          const int32_t* __restrict__ pred,
                                                          double* __restrict__ rel,
                                                          int32_t* __restrict__ max_depth,
-                                                         const int32_t* __restrict__ only) {
+                                                         const int32_t* __restrict__ only,
+                                                         const int32_t* __restrict__ srcs = nullptr) {
     extern __shared__ __attribute__((aligned(16))) int32_t smem[];
-    const int s = row0 + blockIdx.x;
+    const int s = srcs ? srcs[blockIdx.x] : row0 + blockIdx.x; /* srcs: row i is source srcs[i] */
     if (s >= n || !only[blockIdx.x]) return;
     const int nw = (n + 31) >> 5;
     int32_t* pu = smem;                                   /* n predecessor vertices */
@@ -781,14 +782,15 @@ __global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
                                                          int32_t* __restrict__ pred,
                                                          double* __restrict__ rel, int maxl,
                                                          int32_t* __restrict__ max_depth,
-                                                         int32_t* __restrict__ sweep) {
+                                                         int32_t* __restrict__ sweep,
+                                                         const int32_t* __restrict__ srcs = nullptr) {
     /* each thread owns t = tid + i * NT (i < PER, n <= MAXN); the row's distances are read once
      * and kept as bytes in registers (levels <= maxl <= 254 once the row qualifies), so a pass
      * only compares registers and touches memory for its own targets. The row reads go through
      * buffer descriptors (constant scalar offset per i, one vector offset), which keeps the 64
      * unrolled loads from holding 64-bit addresses. */
     constexpr int PER = MAXN / NT;
-    const int s = row0 + blockIdx.x;
+    const int s = srcs ? srcs[blockIdx.x] : row0 + blockIdx.x; /* srcs: row i is source srcs[i] */
     if (s >= n) return;
     const int tid = threadIdx.x;
     const uint32_t* dl = lat + (size_t)blockIdx.x * ld;
@@ -875,12 +877,16 @@ __global__ __launch_bounds__(256) void dense_diag_kernel(int n, int ld, int row0
                                                          const uint32_t* __restrict__ w,
                                                          const double* __restrict__ r,
                                                          uint32_t* __restrict__ d,
-                                                         double* __restrict__ rel) {
+                                                         double* __restrict__ rel,
+                                                         const int32_t* __restrict__ srcs = nullptr) {
+    /* srcs: output row lr is source srcs[lr], whose edges are row srcs[lr] of the full w / r */
     const int lr = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int v = row0 + lr;
+    if (lr >= nrows) return;
+    const int v = srcs ? srcs[lr] : row0 + lr;
     const int lane = threadIdx.x & 63;
-    if (lr >= nrows || v >= n) return;
-    const uint32_t* wr = w + (size_t)lr * ld;
+    if (v >= n) return;
+    const size_t wrow = (size_t)(srcs ? v : lr) * ld;
+    const uint32_t* wr = w + wrow;
     uint64_t best = ~0ull;
     auto take = [&](uint32_t x, int u) {
         if (x >= SRT_INF) return;
@@ -908,7 +914,7 @@ __global__ __launch_bounds__(256) void dense_diag_kernel(int n, int ld, int row0
             rel[ix] = 0.0;
         } else {
             int u = (int)(best & 0xffffffffu);
-            double x = r[(size_t)lr * ld + u];
+            double x = r[wrow + u];
             d[ix] = (uint32_t)(best >> 32);
             rel[ix] = (u == v) ? x : x * x;
         }
@@ -1173,6 +1179,286 @@ static int dense_finish_rows(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
     return SRT_OK;
 }
 
+/* ---- a few source rows on a dense graph (srt_dense_rows_build_device) ---------------------- */
+/* The canonical predecessor of (source row i, target t) is argmin over u with
+ * D[i][u] + W[u][t] == D[i][t] of (D[i][u], u) -- pred_cols_kernel's rule. Without every row of D
+ * the essential-arc filter is not available; an arc can only be tight for some row if
+ * W[u][t] <= max_i D[i][t], which keeps a few percent of a complete graph's arcs (distances are a
+ * few hops of the shortest arcs). Those candidates are listed per target (CSR over t, u
+ * ascending), the rows are transposed 64 sources to a 128-byte line, and one wave per (t, source
+ * block) walks t's candidates with the sources across its lanes, as pred_cols2_kernel does. */
+#define ROWS_CAP 0x3DFFu
+__global__ void rows_maxd_kernel(int nsub, int ld, const uint16_t* __restrict__ ds,
+                                 uint32_t* __restrict__ maxd) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ld) return;
+    uint32_t m = 0;
+    for (int i = 0; i < nsub; ++i) {
+        const uint32_t d = ds[(size_t)i * ld + t];
+        if (d < ROWS_CAP && d > m) m = d;
+    }
+    maxd[t] = m;
+}
+
+/* one wave per target t: wt row t is column t of W (the u16 matrix itself when W is symmetric);
+ * FILL = 0 counts the candidates u != t with W[u][t] <= maxd[t], FILL = 1 writes them in order */
+template <bool FILL>
+__global__ __launch_bounds__(256) void rows_cand_kernel(int n, int ld, const uint16_t* __restrict__ wt,
+                                                       const uint32_t* __restrict__ maxd,
+                                                       int32_t* __restrict__ cnt,
+                                                       const int32_t* __restrict__ ptr,
+                                                       uint32_t* __restrict__ cand) {
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (t >= n) return;
+    const uint32_t lim = maxd[t];
+    const uint16_t* row = wt + (size_t)t * ld;
+    int base = FILL ? ptr[t] : 0;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int u0 = 0; u0 < n; u0 += 512) {
+        const int u = u0 + lane * 8;
+        uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        if (u < ld) v = *reinterpret_cast<const uint4*>(row + u);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+        uint32_t m = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t w = (w4[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+            if (u + q < n && u + q != t && w <= lim) m |= 1u << q;
+        }
+        const int c = __popc(m);
+        /* a lane's count (0..8) in four ballots: its exclusive prefix is four masked popcounts */
+        int pre = 0, tot = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint64_t bal = __ballot((c >> b) & 1);
+            pre += __popcll(bal & lt) << b;
+            tot += __popcll(bal) << b;
+        }
+        if (FILL) {
+            int o = base + pre;
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if ((m >> q) & 1u) {
+                    const uint32_t w = (w4[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+                    cand[o++] = (uint32_t)(u + q) | (w << 16);
+                }
+        }
+        base += tot;
+    }
+    if (!FILL && lane == 0) cnt[t] = base;
+}
+
+/* DT[b][u][l] = ds[b * 64 + l][u] (rows past nsub: the cap) */
+__global__ void rows_dt_kernel(int nsub, int ld, const uint16_t* __restrict__ ds,
+                               uint16_t* __restrict__ dt) {
+    const int l = threadIdx.x & 63, b = blockIdx.y;
+    const int u = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (u >= ld) return;
+    const int i = b * 64 + l;
+    dt[((size_t)b * ld + u) * 64 + l] = i < nsub ? ds[(size_t)i * ld + u] : (uint16_t)ROWS_CAP;
+}
+
+template <bool TIES>
+__global__ __launch_bounds__(256) void rows_pred_kernel(int n, int ld, int nsub,
+                                                        const int32_t* __restrict__ verts,
+                                                        const uint16_t* __restrict__ dt,
+                                                        const int32_t* __restrict__ ptr,
+                                                        const uint32_t* __restrict__ cand,
+                                                        const double* __restrict__ r,
+                                                        int32_t* __restrict__ pred,
+                                                        double* __restrict__ rel,
+                                                        unsigned long long* __restrict__ ties) {
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63, b = blockIdx.y;
+    if (t >= n) return;
+    const int i = b * 64 + lane;
+    const uint16_t* db = dt + (size_t)b * ld * 64 + lane;
+    const uint32_t tgt = db[(size_t)t * 64];
+    uint32_t best = 0xFFFFFFFFu, tie = 0;
+    const int e = ptr[t + 1];
+    for (int j0 = ptr[t]; j0 < e; j0 += 8) {
+        uint32_t cu[8], d[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) cu[q] = j0 + q < e ? cand[j0 + q] : 0xFFFFFFFFu;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) d[q] = cu[q] != 0xFFFFFFFFu ? db[(size_t)(cu[q] & 0xFFFFu) * 64] : 0xFFFFu;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (cu[q] == 0xFFFFFFFFu || d[q] + (cu[q] >> 16) != tgt) continue;
+            const uint32_t key = (d[q] << 16) | (cu[q] & 0xFFFFu);
+            if (TIES && ((key ^ best) >> 16) == 0) tie = 1;
+            if (key < best) {
+                if (TIES && (key >> 16) < (best >> 16)) tie = 0;
+                best = key;
+            }
+        }
+    }
+    if (i >= nsub) return;
+    const int s = verts[i];
+    const bool has = best != 0xFFFFFFFFu && t != s;
+    const int u = has ? (int)(best & 0xFFFFu) : -1;
+    pred[(size_t)i * ld + t] = u;
+    rel[(size_t)i * ld + t] = has ? r[(size_t)u * ld + t] : 0.0;
+    if (TIES) {
+        const uint64_t tb = __ballot(has && tie);
+        if (lane == 0 && tb) atomicAdd(ties, (unsigned long long)__popcll(tb));
+    }
+}
+
+/* Tables of nsub sources (device list dverts, host copy hverts) on a dense graph without the
+ * all-pairs FW: distance rows by Bellman-Ford passes (srt_fw16_rows), canonical predecessors
+ * (rows_pred_kernel), path-order reliability (rel_levels_kernel / rel_sweeps_kernel), the diagonal
+ * rule and, with lat_ms, the f64 path-order ms rows. Rows are full width (ld); *used = 0 (and
+ * nothing written) when a distance reaches the u16 cap or n is beyond the LDS forms -- the caller
+ * then runs the FW. w, r: ld x ld device matrices. */
+int srt_dense_rows_build_device(int32_t n, int32_t ld, int32_t nsub, const int32_t* dverts,
+                                const uint32_t* w, const double* r, uint32_t* lat_rows,
+                                double* rel_rows, double* lms_rows, uint64_t quantum_ns,
+                                int32_t directed, hipStream_t st, srt_build_stats* stats, int* used) {
+    *used = 0;
+    if (n > 32768 || ld % 128 || nsub < 1 || nsub > n) return SRT_OK;
+    const int nsp = srt_ceil_div(nsub, 128) * 128, nb64 = srt_ceil_div(nsub, 64);
+    struct scratch {
+        void* p[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+        hipStream_t s;
+        ~scratch() {
+            for (void* x : p)
+                if (x) (void)hipFreeAsync(x, s);
+        }
+        int get(int k, size_t bytes) {
+            if (hipMallocAsync(&p[k], bytes ? bytes : 16, s) != hipSuccess) {
+                (void)hipGetLastError();
+                srt_set_error("dense rows build: scratch of %zu MiB failed", bytes >> 20);
+                return SRT_E_NOMEM;
+            }
+            return SRT_OK;
+        }
+    } sc;
+    sc.s = st;
+    int rc;
+    if ((rc = sc.get(0, (size_t)ld * ld * sizeof(uint16_t))) ||
+        (rc = sc.get(1, (size_t)nsp * ld * sizeof(uint16_t))) ||
+        (rc = sc.get(2, ((size_t)ld * nsub + 2 * (size_t)nsub + 2) * sizeof(int32_t))) ||
+        (rc = sc.get(3, sizeof(unsigned long long))) ||
+        (rc = sc.get(4, (size_t)nb64 * ld * 64 * sizeof(uint16_t))) ||
+        (rc = sc.get(5, (size_t)(3 * ld + 3) * sizeof(int32_t))))
+        return rc;
+    uint16_t* w16 = (uint16_t*)sc.p[0];
+    uint16_t* ds = (uint16_t*)sc.p[1];
+    int32_t* pred = (int32_t*)sc.p[2];
+    int32_t* sweep = pred + (size_t)ld * nsub;
+    int32_t* depth = sweep + nsub;
+    unsigned long long* ties = (unsigned long long*)sc.p[3];
+    uint16_t* dt = (uint16_t*)sc.p[4];
+    uint32_t* maxd = (uint32_t*)sc.p[5];
+    int32_t* ccnt = (int32_t*)sc.p[5] + ld;
+    int32_t* ptr = ccnt + ld + 1; /* n + 1 candidate offsets */
+    hipEvent_t e0, e1, e2;
+    SRT_HIPCHK(hipEventCreate(&e0));
+    SRT_HIPCHK(hipEventCreate(&e1));
+    SRT_HIPCHK(hipEventCreate(&e2));
+    struct evs {
+        hipEvent_t* e[3];
+        ~evs() {
+            for (hipEvent_t* x : e) (void)hipEventDestroy(*x);
+        }
+    } ev{{&e0, &e1, &e2}};
+    SRT_HIPCHK(hipEventRecord(e0, st));
+    int exact = 0, small = 0, passes = 0;
+    rc = srt_fw16_rows(n, ld, nsub, dverts, w, w16, ds, lat_rows, st, &exact, &small, &passes);
+    if (rc) return rc;
+    if (!exact) return SRT_OK; /* a distance at the u16 cap: the FW's wider tiers take it */
+    SRT_HIPCHK(hipEventRecord(e1, st));
+    const bool ct = stats && stats->count_ties;
+    SRT_HIPCHK(hipMemsetAsync(ties, 0, sizeof(unsigned long long), st));
+    SRT_HIPCHK(hipMemsetAsync(depth, 0, sizeof(int32_t), st));
+    /* candidate arcs per target: column t of W is row t of W (symmetric) or of its transpose */
+    const uint16_t* wt = w16;
+    if (directed) {
+        if ((rc = sc.get(6, (size_t)ld * ld * sizeof(uint16_t)))) return rc;
+        transpose_kernel<uint16_t><<<dim3(ld / 64, ld / 64), 256, 0, st>>>(ld, ld, w16, (size_t)ld,
+                                                                           (uint16_t*)sc.p[6],
+                                                                           (size_t)ld);
+        wt = (const uint16_t*)sc.p[6];
+    }
+    rows_maxd_kernel<<<srt_ceil_div(ld, 256), 256, 0, st>>>(nsub, ld, ds, maxd);
+    rows_cand_kernel<false><<<srt_ceil_div(n, 4), 256, 0, st>>>(n, ld, wt, maxd, ccnt, NULL, NULL);
+    scan_kernel<<<1, 1024, 0, st>>>(n, ccnt, ptr);
+    SRT_HIPCHK(hipGetLastError());
+    int32_t total = 0;
+    SRT_HIPCHK(hipMemcpyAsync(&total, ptr + n, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    SRT_HIPCHK(hipStreamSynchronize(st));
+    if ((rc = sc.get(7, ((size_t)total + 1) * sizeof(uint32_t)))) return rc;
+    uint32_t* cand = (uint32_t*)sc.p[7];
+    rows_cand_kernel<true><<<srt_ceil_div(n, 4), 256, 0, st>>>(n, ld, wt, maxd, NULL, ptr, cand);
+    rows_dt_kernel<<<dim3(ld / 4, nb64), 256, 0, st>>>(nsub, ld, ds, dt);
+    dim3 pg(srt_ceil_div(n, 4), nb64);
+    if (ct)
+        rows_pred_kernel<true><<<pg, 256, 0, st>>>(n, ld, nsub, dverts, dt, ptr, cand, r, pred,
+                                                    rel_rows, ties);
+    else
+        rows_pred_kernel<false><<<pg, 256, 0, st>>>(n, ld, nsub, dverts, dt, ptr, cand, r, pred,
+                                                     rel_rows, ties);
+    SRT_HIPCHK(hipGetLastError());
+    SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 32768>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
+    rel_levels_kernel<1024, 32768><<<nsub, 1024, 65536, st>>>(n, ld, 0, lat_rows, pred, rel_rows, 64,
+                                                             depth, sweep, dverts);
+    const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
+    SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    rel_sweeps_kernel<<<nsub, 512, lds, st>>>(n, ld, 0, pred, rel_rows, depth, sweep, dverts);
+    dense_diag_kernel<<<srt_ceil_div(nsub, 4), 256, 0, st>>>(n, ld, 0, nsub, w, r, lat_rows, rel_rows,
+                                                             dverts);
+    SRT_HIPCHK(hipGetLastError());
+    if (lms_rows &&
+        (rc = srt_path_ms_rows(n, nsub, dverts, 0, lat_rows, (size_t)ld, pred, (size_t)ld, NULL, NULL,
+                               NULL, quantum_ns, lms_rows, (size_t)ld, st)))
+        return rc;
+    SRT_HIPCHK(hipEventRecord(e2, st));
+    SRT_HIPCHK(hipEventSynchronize(e2));
+    if (stats) {
+        float a = 0, b = 0;
+        SRT_HIPCHK(hipEventElapsedTime(&a, e0, e1));
+        SRT_HIPCHK(hipEventElapsedTime(&b, e1, e2));
+        unsigned long long nt = 0;
+        int32_t dep = 0;
+        SRT_HIPCHK(hipMemcpy(&nt, ties, sizeof(nt), hipMemcpyDeviceToHost));
+        SRT_HIPCHK(hipMemcpy(&dep, depth, sizeof(dep), hipMemcpyDeviceToHost));
+        stats->algo = SRT_ALGO_DENSE_FW;
+        stats->dist_enc = SRT_DENC_ROWS;
+        stats->fw_block = passes; /* dense rows builds: the Bellman-Ford passes */
+        stats->ms_fw = a;
+        stats->ms_post = b;
+        stats->ms_total = a + b;
+        stats->n_update = passes;
+        stats->ms_update = a;
+        stats->max_depth = dep;
+        stats->tied_pairs = ct ? (int64_t)nt : 0;
+        stats->ess_arcs = total; /* dense rows builds: the candidate arcs */
+    }
+    *used = 1;
+    return SRT_OK;
+}
+
+extern "C" int srt_dense_rows_build(int32_t n, int32_t ld, int32_t nsub, const int32_t* dverts,
+                                    const uint32_t* w, const double* r, uint32_t* lat_rows,
+                                    double* rel_rows, void* stream, srt_build_stats* stats) {
+    if (n <= 0 || ld < n || ld % 128 || nsub < 1 || !dverts || !w || !r || !lat_rows || !rel_rows) {
+        srt_set_error("srt_dense_rows_build: bad arguments");
+        return SRT_E_ARG;
+    }
+    int used = 0;
+    /* symmetric w assumed unknown here: the candidate lists come from the transpose */
+    const int rc = srt_dense_rows_build_device(n, ld, nsub, dverts, w, r, lat_rows, rel_rows, NULL, 0,
+                                               1, (hipStream_t)stream, stats, &used);
+    if (rc) return rc;
+    if (!used) {
+        srt_set_error("srt_dense_rows_build: n = %d beyond 32768 or a distance at the u16 cap", n);
+        return SRT_E_RANGE;
+    }
+    return SRT_OK;
+}
+
 int srt_dense_post_device(int32_t n, int32_t ld, int32_t directed, const uint32_t* w, const double* r,
                           uint32_t* d, const uint16_t* d16, double* rel, hipStream_t st,
                           srt_build_stats* stats) {
@@ -1247,6 +1533,7 @@ int srt_dense_build_device_ms(int32_t n, int32_t ld, int32_t directed, const uin
         if (rc) return rc;
         if (exact)
             enc = !fm ? SRT_DENC_U16
+                      : sym == 5 ? SRT_DENC_SQUARE
                       : sym == 4 ? SRT_DENC_F16CMP_SYM256
                       : sym == 3 ? SRT_DENC_F16CMP_SYM128
                       : sym == 2 ? SRT_DENC_F16CMP_SYM2

@@ -1224,6 +1224,52 @@ __global__ __launch_bounds__(1024 / RM) void sym_cross_stage_kernel(const u16* _
             make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
 }
 
+/* Two-deep sharded rounds (fw16_build_sym_sharded, deep): a closed 128-row panel P (rows P_a over
+ * P_b, 128 x ld) applied to a band that was staged early -- the two 64-row halves sa / sb of tile
+ * row Kb, 64 x 128 per tile column J in Kb's staging order. In symmetric rounds the A operand of a
+ * row-Kb tile is P's own columns at Kb (D[i][k] = D[k][i] = P[k][i]), so the band needs nothing but
+ * P: X[:, J] = min(X[:, J], P[:, Kb]^T (x) P[:, J]), the fwq_update_kernel<true> tile with C in the
+ * staging buffer (row stride 128). One workgroup per tile column, 128 pivots in four stages. */
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) void fwq_band_kernel(
+    const u16* __restrict__ P, int ld, int Kb, int T, const int* __restrict__ own,
+    u16* __restrict__ sa, u16* __restrict__ sb) {
+    __shared__ __attribute__((aligned(16))) uint32_t sA[UKC / 2 * 128 * 2];
+    __shared__ __attribute__((aligned(16))) u16 sB[UKC * UBS];
+    __shared__ int s_own[SYM_TMAX], s_cnt;
+    FW_CHAIN_PRIO();
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int J = (int)blockIdx.x;
+    const size_t pos = (size_t)sym_stage_pos(Kb, J, T, own, s_own, &s_cnt) * (KB * 128);
+    /* rows 4 ty .. 4 ty + 3 of the 128-row tile: the a half below 64, the b half above */
+    u16* C = (ty < 16 ? sa + pos + (size_t)(ty * 4) * 128 : sb + pos + (size_t)(ty * 4 - 64) * 128) +
+             tx * 8;
+    const u16* Bg = P + J * 128;
+    fwq_stage_regs g;
+    fwq_gload_sym(g, P, Kb * 128, Bg, ld, tid);
+    uint32_t acc[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint4 v = *reinterpret_cast<const uint4*>(C + r * 128);
+        acc[r][0] = v.x;
+        acc[r][1] = v.y;
+        acc[r][2] = v.z;
+        acc[r][3] = v.w;
+    }
+#pragma unroll 1
+    for (int s = 0; s < 4; ++s) {
+        if (s > 0) __syncthreads();
+        fwq_swrite<true>(g, sA, sB, tid);
+        __syncthreads();
+        if (s + 1 < 4)
+            fwq_gload_sym(g, P + (size_t)(s + 1) * UKC * ld, Kb * 128, Bg + (size_t)(s + 1) * UKC * ld,
+                          ld, tid);
+        fwq_stage(acc, sA, sB, tx, ty);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        *reinterpret_cast<uint4*>(C + r * 128) = make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+}
+
 /* final fill: kept tile (I, J) of the sender, transposed into a contiguous 128 x 128 block */
 __global__ __launch_bounds__(256) void sym_fill_pack_kernel(const u16* __restrict__ D, int ld, int tb,
                                                             const uint32_t* __restrict__ pairs,
@@ -1304,6 +1350,9 @@ typedef struct {
     hipStream_t xs;
     hipEvent_t e_set[2][2]; /* [round & 1][tile set]: the set's next-row tiles are done */
     hipEvent_t xs_done[2];  /* sharded symmetric rounds: stream xs finished round k's update */
+    /* two-deep sharded rounds: the band stream (pack + broadcast) and its staged-band arrivals */
+    hipStream_t ms;
+    hipEvent_t arr[3], applied[3];
     uint32_t* tl2;
     size_t tl2_cap;
     int ok;
@@ -1327,6 +1376,11 @@ static int sched_get(fw16_sched** out, int dev) {
             SRT_HIPCHK(hipEventCreateWithFlags(&x->e_set[i / 2][i % 2], hipEventDisableTiming));
         for (int i = 0; i < 2; ++i)
             SRT_HIPCHK(hipEventCreateWithFlags(&x->xs_done[i], hipEventDisableTiming));
+        SRT_HIPCHK(hipStreamCreateWithPriority(&x->ms, hipStreamNonBlocking, hi));
+        for (int i = 0; i < 3; ++i) {
+            SRT_HIPCHK(hipEventCreateWithFlags(&x->arr[i], hipEventDisableTiming));
+            SRT_HIPCHK(hipEventCreateWithFlags(&x->applied[i], hipEventDisableTiming));
+        }
         x->ok = 1;
     }
     *out = x;
@@ -1696,7 +1750,12 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
     u16* grecv = NULL; /* staged panel blocks in (contributor, J) order (r128: rows a, then b) */
     int* cnt = (int*)calloc(2 * (size_t)R, sizeof(int)); /* per contributor (256: two tile rows) */
     const size_t blk = (size_t)KB * 128;
-    const size_t nstage = (size_t)(kbr / KB) * ((size_t)T + 1) * blk;
+    /* two-deep 128-pivot rounds (N > 1 default; SRT_FW_SH_DEEP=0: one-deep): band k + 3 is staged
+     * and broadcast on its own stream right after round k's update, three rounds ahead, and each
+     * rank applies the two panels it missed to the staged band itself (fwq_band_kernel) */
+    const char* deep_env = getenv("SRT_FW_SH_DEEP");
+    const bool deep = r128 && R > 1 && T >= 2 && (deep_env ? atoi(deep_env) != 0 : true);
+    const size_t nstage = (size_t)(kbr / KB) * ((size_t)T + 1) * blk * (deep ? 3 : 1);
     bool ok = cnt && hipMalloc(&tl, (nkept + 1) * sizeof(uint32_t)) == hipSuccess &&
               hipMalloc(&down, (size_t)T * sizeof(int)) == hipSuccess &&
               hipMalloc(&grecv, nstage * sizeof(u16)) == hipSuccess;
@@ -1857,12 +1916,126 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
             return SRT_OK;
         };
         auto make = [&](int k) -> int { return r256 ? produce256(k) : r128 ? produce128(k) : produce(k); };
-        if ((rc = make(0))) goto out;
         /* two update streams (st: even J, xs: odd J), as on one GPU (fw16_build_sym): each
          * depends on its own launches and the panel, so their rounds overlap */
         hipStream_t ss[2] = {st, sc->xs};
         const uint32_t* tls[2] = {tl, tl + nset[0]};
         SYM_HIP(hipStreamWaitEvent(sc->xs, sc->init_done, 0));
+        if (deep) {
+            /* Two-deep rounds. Band j (tile row j, rows a then b) is packed from the real tiles
+             * after round j - 3's update (panels <= j - 3; the update of round j - 2 may already
+             * be writing them -- every value read is a real path length no larger than what the
+             * round needs, as with the two update streams), broadcast on the band stream ms, and
+             * takes P_{j-2} and P_{j-1} on arrival (fwq_band_kernel, on cs) before it is closed
+             * into P_j. The broadcast then has a whole round of the update to hide under, and the
+             * chain from P_k to P_{k+1} is one band apply plus the closures. The update launches
+             * cover every kept tile (no cross exclusions): the pivot rows take their own closed
+             * panel there (min-plus with a closed panel is idempotent), so the closures write no
+             * pivot rows. */
+            hipStream_t ms = sc->ms;
+            auto sa_of = [&](int j) { return grecv + (size_t)(j % 3) * 2 * ((size_t)T + 1) * blk; };
+            auto sb_of = [&](int j) { return sa_of(j) + ((size_t)T + 1) * blk; };
+            auto send = [&](int j) -> int { /* on ms: pack band j, broadcast, mark its arrival */
+                const int o = own[j];
+                u16* sa = sa_of(j);
+                u16* sb = sb_of(j);
+                for (int q = 0; q < R; q++) cnt[q] = 0;
+                for (int J = 0; J < T; J++) cnt[sym_kept(j, J) ? o : own[J]]++;
+                if (cnt[me])
+                    sym_contrib_pack_kernel<<<2 * T, 256, 0, ms>>>(d, ld, row0, tb, j, j * 128, T, down,
+                                                                   me, sa, sb);
+                SRT_HIPCHK(hipGetLastError());
+                int r = srt_coll_group_begin(comm);
+                size_t off = 0;
+                for (int q = 0; q < R && !r; q++) {
+                    if (cnt[q]) {
+                        const size_t bytes = (size_t)cnt[q] * blk * sizeof(u16);
+                        r = srt_coll_bcast(comm, sa + off * blk, bytes, q, ms);
+                        if (!r) r = srt_coll_bcast(comm, sb + off * blk, bytes, q, ms);
+                    }
+                    off += (size_t)cnt[q];
+                }
+                const int r2 = srt_coll_group_end(comm);
+                if (r || r2) return r ? r : r2;
+                SRT_HIPCHK(hipEventRecord(sc->arr[j % 3], ms));
+                return SRT_OK;
+            };
+            auto close = [&](int j) -> int { /* on cs: the staged band j (complete) -> P_j */
+                const int j0 = j * 128;
+                u16* P = pbuf[j & 1];
+                u16* Pb = P + (size_t)KB * ld;
+                u16* sa = sa_of(j);
+                u16* sb = sb_of(j);
+                sym_diag_stage_kernel<<<1, 256, 0, cs>>>(P, ld, j, j0, T, down, sa, nullptr);
+                sym_panel_stage_kernel<SYM_RM><<<T, 1024 / SYM_RM, 0, cs>>>(P, ld, j, j0, T, down, sa, nullptr);
+                sym_cross_stage_kernel<SYM_RM><<<T, 1024 / SYM_RM, 0, cs>>>(P, ld, j, T, down, sb, j, 0);
+                sym_diag_stage_kernel<<<1, 256, 0, cs>>>(Pb, ld, j, j0 + KB, T, down, sb, nullptr);
+                sym_panel_stage_kernel<SYM_RM><<<T, 1024 / SYM_RM, 0, cs>>>(Pb, ld, j, j0 + KB, T, down, sb, nullptr);
+                SRT_HIPCHK(hipGetLastError());
+                SRT_HIPCHK(hipEventRecord(sc->ready[j & 1], cs));
+                return SRT_OK;
+            };
+            /* P_k into the staged band j: the band's last panel (j = k + 1) on cs, on the chain from
+             * P_k to P_{k+1}; its first (j = k + 2) on the band stream ms, which has broadcast the
+             * band and then idles until round k's update ends (its next send): off the chain, and
+             * no fifth stream (four hardware queues per process: a fifth would share one, and a
+             * wait there stalls an update stream). The last apply of band j waits for it
+             * (applied[j]). */
+            auto apply = [&](int k, int j) -> int {
+                hipStream_t as = j == k + 1 ? cs : ms;
+                if (j == k + 1) {
+                    SRT_HIPCHK(hipStreamWaitEvent(cs, sc->arr[j % 3], 0));
+                    if (j >= 2) SRT_HIPCHK(hipStreamWaitEvent(cs, sc->applied[j % 3], 0));
+                } else {
+                    SRT_HIPCHK(hipStreamWaitEvent(ms, sc->ready[k & 1], 0));
+                }
+                fwq_band_kernel<<<T, 512, 0, as>>>(pbuf[k & 1], ld, j, T, down, sa_of(j), sb_of(j));
+                SRT_HIPCHK(hipGetLastError());
+                if (j == k + 2) SRT_HIPCHK(hipEventRecord(sc->applied[j % 3], ms));
+                return SRT_OK;
+            };
+            SYM_HIP(hipStreamWaitEvent(ms, sc->init_done, 0));
+            for (int j = 0; j < 3 && j < nb; j++)
+                if ((rc = send(j))) goto out;
+            SYM_HIP(hipStreamWaitEvent(cs, sc->arr[0], 0));
+            if ((rc = close(0))) goto out;
+            int timed = 0;
+            for (int k = 0; k < nb; ++k) {
+                u16* P = panel_of(k);
+                const bool next = k + 1 < nb;
+                const bool t_first = evp && next && timed == 0, t_last = evp && k + 2 == nb;
+                if (evp && next) {
+                    evp->group = 4;
+                    evp->used = 4 * ++timed;
+                }
+                for (int p = 0; p < 2; p++) {
+                    SYM_HIP(hipStreamWaitEvent(ss[p], sc->ready[k & 1], 0));
+                    if (t_first) SYM_HIP(hipEventRecord(evp->ev[p], ss[p]));
+                    if (nset[p])
+                        fwq_update_kernel<true, 5, 4><<<(unsigned)nset[p], 512, 0, ss[p]>>>(
+                            d, ld, P, k * 128, T, tb, -1, tls[p], te);
+                    if (t_last) SYM_HIP(hipEventRecord(evp->ev[evp->used - 2 + p], ss[p]));
+                    SYM_HIP(hipEventRecord(sc->e_set[k & 1][p], ss[p]));
+                }
+                SYM_HIP(hipGetLastError());
+                /* band stream: P_k into band k + 2 (arrived), then band k + 3 once round k's
+                 * update has (at least) passed over its tiles */
+                if (k + 2 < nb && (rc = apply(k, k + 2))) goto out;
+                if (k + 3 < nb) {
+                    SYM_HIP(hipStreamWaitEvent(ms, sc->e_set[k & 1][0], 0));
+                    SYM_HIP(hipStreamWaitEvent(ms, sc->e_set[k & 1][1], 0));
+                    if ((rc = send(k + 3))) goto out;
+                }
+                if (!next) continue;
+                if ((rc = apply(k, k + 1))) goto out;
+                if (k >= 1) { /* P_{k+1} overwrites P_{k-1}: its update launches are done */
+                    SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[(k - 1) & 1][0], 0));
+                    SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[(k - 1) & 1][1], 0));
+                }
+                if ((rc = close(k + 1))) goto out;
+            }
+        } else {
+        if ((rc = make(0))) goto out;
         /* Host enqueue order per round: next-row launches, the rest launches, then the next
          * panel on cs. At N ranks a round is ~100 us of GPU work and ~20 HIP calls, so the host
          * is the bottleneck if the bulk update waits behind the chain's calls; the chain kernels
@@ -1958,6 +2131,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
                 if ((rc = make(k + 1))) goto out;
             }
         }
+        } /* one-deep rounds */
         SYM_HIP(hipEventRecord(sc->xs_done[0], sc->xs));
         SYM_HIP(hipStreamWaitEvent(st, sc->xs_done[0], 0));
         /* fill the tiles this rank does not keep: transposes from their keepers */
@@ -2067,6 +2241,7 @@ out:
 #undef SYM_HIP
 #undef SYM_FAIL
     (void)hipStreamSynchronize(cs);
+    (void)hipStreamSynchronize(sc->ms);
     (void)hipStreamSynchronize(st);
     if (tl) (void)hipFree(tl);
     if (down) (void)hipFree(down);
@@ -2101,12 +2276,23 @@ int srt_fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0, in
 }
 int srt_fw16_sharded_round_pivots(void) { return g_sharded_rp; }
 
+static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStream_t st,
+                       evpool_t* evp, int* exact);
+
 int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,
                    hipStream_t st, evpool_t* evp, srt_owner_fn owner_of, srt_panel_bcast_fn bcast,
                    void* ctx, int rank, int fm, int* sym, int* exact) {
     if (ld % 128 || nrows % 128 || row0 % 128) {
         srt_set_error("u16 FW needs ld and the row shard to be multiples of 128");
         return SRT_E_ARG;
+    }
+    /* small matrices on one GPU (ld <= 2048, C2's 1,000 vertices): min-plus squaring to a fixed
+     * point instead of ld / 64 latency-bound FW rounds; SRT_FW_SQUARE=0 keeps the rounds */
+    const char* sq_env = getenv("SRT_FW_SQUARE");
+    if (fm && !bcast && !owner_of && row0 == 0 && nrows == ld && ld <= 2048 &&
+        !(sq_env && atoi(sq_env) == 0)) {
+        if (sym) *sym = 5;
+        return fw16_square(n, ld, w_rows, lat_rows, st, evp, exact);
     }
     u16** bufs = fw16_bufs;
     size_t* caps = fw16_caps;
@@ -2225,6 +2411,182 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
     SRT_HIPCHK(hipGetLastError());
     int hf[2] = {0, 0};
     SRT_HIPCHK(hipMemcpyAsync(hf, flags[dev], 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+    SRT_HIPCHK(hipStreamSynchronize(st));
+    *exact = hf[0] ? 0 : 1;
+    fw16_small[dev] = hf[1] ? 0 : 1;
+    return SRT_OK;
+}
+
+/* ---- distance rows of a few sources on a dense graph (no all-pairs FW) -------------------- */
+/* w16 = min(w, cap) (the B operand: every arc, the self-loop on the diagonal) */
+__global__ void rows_w16_kernel(int ld, const uint32_t* __restrict__ w, u16* __restrict__ w16,
+                                uint32_t cap) {
+    const size_t i8 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+    if (i8 >= (size_t)ld * ld) return;
+    const uint4 a = *reinterpret_cast<const uint4*>(w + i8);
+    const uint4 b = *reinterpret_cast<const uint4*>(w + i8 + 4);
+    auto c = [&](uint32_t x) { return x < cap ? x : cap; };
+    *reinterpret_cast<uint4*>(w16 + i8) = make_uint4(c(a.x) | (c(a.y) << 16), c(a.z) | (c(a.w) << 16),
+                                                     c(b.x) | (c(b.y) << 16), c(b.z) | (c(b.w) << 16));
+}
+
+/* D_S row i = the arcs of source verts[i] (capped), 0 at the source; padding rows stay at cap */
+__global__ void rows_init_kernel(int ld, int nsub, const int32_t* __restrict__ verts,
+                                 const u16* __restrict__ w16, u16* __restrict__ ds, uint32_t cap) {
+    const int i = blockIdx.y;
+    const int j8 = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+    if (j8 >= ld) return;
+    uint4 v = make_uint4(cap | (cap << 16), cap | (cap << 16), cap | (cap << 16), cap | (cap << 16));
+    int s = -1;
+    if (i < nsub) {
+        s = verts[i];
+        v = *reinterpret_cast<const uint4*>(w16 + (size_t)s * ld + j8);
+    }
+    *reinterpret_cast<uint4*>(ds + (size_t)i * ld + j8) = v;
+    if (s >= j8 && s < j8 + 8) ds[(size_t)i * ld + s] = 0;
+}
+
+/* sum of the rows (values only decrease: an unchanged sum is a fixed point) */
+__global__ void rows_sum_kernel(size_t count, const u16* __restrict__ ds,
+                                unsigned long long* __restrict__ sum) {
+    unsigned long long acc = 0;
+    for (size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < count;
+         i += (size_t)gridDim.x * blockDim.x * 8) {
+        const uint4 v = *reinterpret_cast<const uint4*>(ds + i);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc += (w4[q] & 0xFFFFu) + (w4[q] >> 16);
+    }
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if ((threadIdx.x & 63) == 0) atomicAdd(sum, acc);
+}
+
+/* Shortest-distance rows of nsub sources (device list dverts) on a dense graph with n vertices:
+ * Bellman-Ford on u16 quanta, D_S <- min(D_S, D_S (x) W), in place (the update kernel of the FW,
+ * fwq_update_kernel<false>, with A = the rows' own columns and B = the rows of W), until a pass
+ * changes nothing. Each pass extends every path by at least one arc in pivot order, so it ends
+ * after (fewest hops of a shortest path) + 1 passes; a complete graph's shortest paths have a few
+ * hops. Cost nsub * n^2 per pass, against the FW's n^3: it wins for few sources (the attached
+ * vertices, topology.c:1604-1656). ds: nsp x ld (nsp = nsub rounded up to 128); lat_rows: nsub x
+ * ld u32 quanta. *exact = 0 when a real distance reached the cap (the caller runs the FW). */
+int srt_fw16_rows(int n, int ld, int nsub, const int32_t* dverts, const uint32_t* w, u16* w16,
+                  u16* ds, uint32_t* lat_rows, hipStream_t st, int* exact, int* small, int* passes) {
+    if (ld % 128 || nsub < 1 || n > ld) {
+        srt_set_error("srt_fw16_rows: bad arguments");
+        return SRT_E_ARG;
+    }
+    const int dev = srt_state_slot();
+    const int nsp = srt_ceil_div(nsub, 128) * 128, T = ld / 128;
+    const size_t ll = (size_t)ld * ld;
+    rows_w16_kernel<<<(unsigned)srt_ceil_div((long long)(ll / 8), 256), 256, 0, st>>>(ld, w, w16, CAP_F);
+    rows_init_kernel<<<dim3(srt_ceil_div(ld, 2048), nsp), 256, 0, st>>>(ld, nsub, dverts, w16, ds, CAP_F);
+    SRT_HIPCHK(hipGetLastError());
+    unsigned long long* dsum = nullptr;
+    SRT_HIPCHK(hipMallocAsync((void**)&dsum, sizeof(unsigned long long), st));
+    struct freer {
+        unsigned long long* p;
+        hipStream_t s;
+        ~freer() { (void)hipFreeAsync(p, s); }
+    } fr{dsum, st};
+    unsigned long long prev = ~0ull;
+    int it = 0;
+    for (; it < n + 1; ++it) {
+        for (int k0 = 0; k0 < ld; k0 += 256) {
+            if (k0 + 256 <= ld)
+                fwq_update_kernel<false, 0, 8><<<(unsigned)(nsp / 128 * T), 512, 0, st>>>(
+                    ds, ld, w16 + (size_t)k0 * ld, k0, T, 0, -1, nullptr, 0);
+            else
+                fwq_update_kernel<false, 0, 4><<<(unsigned)(nsp / 128 * T), 512, 0, st>>>(
+                    ds, ld, w16 + (size_t)k0 * ld, k0, T, 0, -1, nullptr, 0);
+        }
+        SRT_HIPCHK(hipMemsetAsync(dsum, 0, sizeof(unsigned long long), st));
+        rows_sum_kernel<<<256, 256, 0, st>>>((size_t)nsp * ld, ds, dsum);
+        SRT_HIPCHK(hipGetLastError());
+        unsigned long long cur = 0;
+        SRT_HIPCHK(hipMemcpyAsync(&cur, dsum, sizeof(cur), hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipStreamSynchronize(st));
+        if (cur == prev) break;
+        prev = cur;
+    }
+    if (passes) *passes = it + 1;
+    int* flags = fw16_flags[dev];
+    if (!flags) {
+        SRT_HIPCHK(hipMalloc(&fw16_flags[dev], 2 * sizeof(int)));
+        flags = fw16_flags[dev];
+    }
+    SRT_HIPCHK(hipMemsetAsync(flags, 0, 2 * sizeof(int), st));
+    fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 2048), nsub), 256, 0, st>>>(n, ld, 0, ds, lat_rows, flags,
+                                                                          CAP_F);
+    SRT_HIPCHK(hipGetLastError());
+    int hf[2] = {0, 0};
+    SRT_HIPCHK(hipMemcpyAsync(hf, flags, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+    SRT_HIPCHK(hipStreamSynchronize(st));
+    *exact = hf[0] ? 0 : 1;
+    if (small) *small = hf[1] ? 0 : 1;
+    return SRT_OK;
+}
+
+/* Min-plus squaring to a fixed point on one GPU: D <- min(D, D (x) D) in place, every tile and
+ * every pivot per pass (the update kernel with A and B both from D), until a pass changes
+ * nothing. Values only decrease and are always lengths of real paths, so the concurrent in-place
+ * reads are harmless (as in the FW rounds); a pass that changes nothing leaves D = min(D, D (x) D)
+ * with a zero diagonal, which is the closure. Pass p covers every path of up to 2^p arcs (more,
+ * with the in-place updates), so a graph whose shortest paths have h arcs takes about
+ * log2(h) + 2 passes of four launches: for small n that replaces ld / 64 FW rounds, each a chain
+ * of dependent launches (C2: 16 rounds). */
+static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStream_t st,
+                       evpool_t* evp, int* exact) {
+    const int dev = srt_state_slot();
+    const size_t need = (size_t)ld * ld + 2 * (size_t)KB * ld;
+    if (fw16_caps[dev] < need) {
+        if (fw16_bufs[dev]) SRT_HIPCHK(hipFree(fw16_bufs[dev]));
+        SRT_HIPCHK(hipMalloc(&fw16_bufs[dev], need * sizeof(u16)));
+        fw16_caps[dev] = need;
+    }
+    if (!fw16_flags[dev]) SRT_HIPCHK(hipMalloc(&fw16_flags[dev], 2 * sizeof(int)));
+    u16* d = fw16_bufs[dev];
+    int* flags = fw16_flags[dev];
+    const int T = ld / 128;
+    fw16_init_kernel<<<dim3(srt_ceil_div(ld, 2048), ld), 256, 0, st>>>(n, ld, 0, w, d, CAP_F);
+    SRT_HIPCHK(hipGetLastError());
+    unsigned long long* dsum = nullptr;
+    SRT_HIPCHK(hipMallocAsync((void**)&dsum, 2 * sizeof(unsigned long long), st));
+    struct freer {
+        unsigned long long* p;
+        hipStream_t s;
+        ~freer() { (void)hipFreeAsync(p, s); }
+    } fr{dsum, st};
+    unsigned long long prev = ~0ull;
+    for (int it = 0; it < 64; ++it) {
+        if (evp && evp->used + 2 <= evp->cap) {
+            SRT_HIPCHK(hipEventRecord(evp->ev[evp->used], st));
+        }
+        for (int k0 = 0; k0 < ld; k0 += 256) {
+            if (k0 + 256 <= ld)
+                fwq_update_kernel<false, 0, 8><<<(unsigned)(T * T), 512, 0, st>>>(
+                    d, ld, d + (size_t)k0 * ld, k0, T, 0, -1, nullptr, 0);
+            else
+                fwq_update_kernel<false, 0, 4><<<(unsigned)(T * T), 512, 0, st>>>(
+                    d, ld, d + (size_t)k0 * ld, k0, T, 0, -1, nullptr, 0);
+        }
+        if (evp && evp->used + 2 <= evp->cap) {
+            SRT_HIPCHK(hipEventRecord(evp->ev[evp->used + 1], st));
+            evp->used += 2;
+        }
+        SRT_HIPCHK(hipMemsetAsync(dsum, 0, sizeof(unsigned long long), st));
+        rows_sum_kernel<<<64, 256, 0, st>>>((size_t)ld * ld, d, dsum);
+        SRT_HIPCHK(hipGetLastError());
+        unsigned long long cur = 0;
+        SRT_HIPCHK(hipMemcpyAsync(&cur, dsum, sizeof(cur), hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipStreamSynchronize(st));
+        if (cur == prev) break;
+        prev = cur;
+    }
+    SRT_HIPCHK(hipMemsetAsync(flags, 0, 2 * sizeof(int), st));
+    fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 2048), ld), 256, 0, st>>>(n, ld, 0, d, lat, flags, CAP_F);
+    SRT_HIPCHK(hipGetLastError());
+    int hf[2] = {0, 0};
+    SRT_HIPCHK(hipMemcpyAsync(hf, flags, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
     SRT_HIPCHK(hipStreamSynchronize(st));
     *exact = hf[0] ? 0 : 1;
     fw16_small[dev] = hf[1] ? 0 : 1;

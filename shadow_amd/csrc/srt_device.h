@@ -148,10 +148,21 @@ enum {
     SRT_DENC_F16CMP_SYM128 = 6, /* 5 with 128-pivot rounds (8-wave update, 4 stages per tile) */
     SRT_DENC_F16CMP_SYM256 = 7, /* 5 with 256-pivot rounds (8 stages per tile) */
     SRT_DENC_F16CMP_SYMSH128 = 8, /* 4 (row-sharded, >= 2 ranks) with 128-pivot rounds */
-    SRT_DENC_F16CMP_SYMSH256 = 9  /* 4 (row-sharded) with 256-pivot rounds */
+    SRT_DENC_F16CMP_SYMSH256 = 9, /* 4 (row-sharded) with 256-pivot rounds */
+    SRT_DENC_ROWS = 10,           /* a few source rows by Bellman-Ford passes, no FW */
+    SRT_DENC_SQUARE = 11          /* ld <= 2048 on one GPU: min-plus squaring to a fixed point */
 };
+int srt_dense_rows_build_device(int32_t n, int32_t ld, int32_t nsub, const int32_t* dverts,
+                                const uint32_t* w, const double* r, uint32_t* lat_rows,
+                                double* rel_rows, double* lms_rows, uint64_t quantum_ns,
+                                int32_t directed, hipStream_t st, srt_build_stats* stats, int* used);
 /* pivots per round of this thread's last srt_fw16_build_sym_sharded (64 or 128) */
 int srt_fw16_sharded_round_pivots(void);
+/* distance rows of nsub sources on a dense graph by Bellman-Ford passes on u16 quanta (fw16.hip);
+ * w16: ld x ld scratch, ds: (nsub rounded up to 128) x ld scratch, lat_rows: nsub x ld u32 */
+int srt_fw16_rows(int n, int ld, int nsub, const int32_t* dverts, const uint32_t* w, uint16_t* w16,
+                  uint16_t* ds, uint32_t* lat_rows, hipStream_t st, int* exact, int* small,
+                  int* passes);
 
 int srt_dense_post_device(int32_t n, int32_t ld, int32_t directed, const uint32_t* w,
                           const double* r, uint32_t* d, const uint16_t* d16, double* rel,

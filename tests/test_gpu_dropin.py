@@ -413,3 +413,81 @@ def _lib_edges(g):
             np.ascontiguousarray(g.lat_ns, np.int64), np.ascontiguousarray(g.loss, np.float64))
     e = Edges(g.n, int(g.directed), len(g.src), *(a.ctypes.data for a in arrs))
     return e, arrs
+
+
+@pytest.mark.parametrize("kind", ["complete", "directed", "sub_ms"])
+def test_dense_rows_few_attached(gpu, kind):
+    """a dense graph with few attached vertices (<= n / 12) builds their rows by
+    Bellman-Ford passes (srt_dense_rows_build_device, encoding 10) instead of the all-pairs FW;
+    the sub-table equals the oracle's raw rows, the f64 ms table included."""
+    if kind == "complete":
+        g = graphs.complete_graph(600, seed=31)
+    elif kind == "directed":
+        g = graphs.complete_directed(480, seed=32)
+    else:
+        g = graphs.complete_graph(360, seed=33)
+        rng = np.random.default_rng(34)
+        g = graphs.Graph(g.n, False, g.src, g.dst, rng.integers(1, 900, g.m).astype(np.int64) * 1_000,
+                         g.loss)
+    rng = np.random.default_rng(35)
+    verts = np.sort(rng.choice(g.n, g.n // 12, replace=False)).astype(np.int32)
+    lat, rel, ms, mn, st = build_tables_subset(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                               verts=verts, algo=ALGO_AUTO, want_ms=kind == "sub_ms")
+    assert st.dist_enc == 10, st.dist_enc
+    rows = oracle.sssp_list(_el(g), verts, nthreads=16)
+    ix = np.ix_(np.arange(len(verts)), verts)
+    off = ~np.eye(len(verts), dtype=bool)
+    assert np.array_equal(lat[off], rows["lat_int"][ix][off])
+    assert np.array_equal(rel[off], rows["rel"][ix][off])
+    full = oracle.table(_el(g), True, oracle.ORC_INT_NS, 8, raw=True)
+    sub = np.ix_(verts, verts)
+    assert np.array_equal(lat, full["lat_int"][sub]) and np.array_equal(rel, full["rel"][sub])
+    if kind == "sub_ms":
+        assert np.array_equal(ms, full["lat_ms"][sub])
+    # the same request with the rows path off takes the FW and agrees
+    import os
+    os.environ["SRT_DENSE_ROWS"] = "0"
+    try:
+        lat2, rel2, _, _, st2 = build_tables_subset(g.n, g.directed, g.src, g.dst, g.lat_ns,
+                                                    g.loss, verts=verts, algo=ALGO_AUTO)
+    finally:
+        del os.environ["SRT_DENSE_ROWS"]
+    assert st2.dist_enc != 10 and np.array_equal(lat, lat2) and np.array_equal(rel, rel2)
+
+
+def test_dense_rows_c4_50_attached(gpu):
+    """C4 (n = 32,768 complete graph) with 50 attached vertices: their rows without the FW
+    (<= 20 ms against the 322-ms all-pairs build), checked against the oracle's
+    dense Dijkstra on every row."""
+    import torch
+    from shadow_amd._lib import BuildStats, check
+    n = ld = 32768
+    L = lib()
+    w = torch.empty((ld, ld), dtype=torch.int32, device="cuda")
+    r = torch.empty((ld, ld), dtype=torch.float64, device="cuda")
+    check(L.srt_gen_complete_device(n, ld, 0, ld, 4, 1000, 10, 500, w.data_ptr(), r.data_ptr(),
+                                    None), "generate")
+    rng = np.random.default_rng(50)
+    verts = np.sort(rng.choice(n, 50, replace=False)).astype(np.int32)
+    dv = torch.from_numpy(verts).cuda()
+    lat = torch.empty((50, ld), dtype=torch.int32, device="cuda")
+    rel = torch.empty((50, ld), dtype=torch.float64, device="cuda")
+    times = []
+    for _ in range(3):
+        st = BuildStats()
+        st.count_ties = 0
+        torch.cuda.synchronize()
+        check(L.srt_dense_rows_build(n, ld, 50, dv.data_ptr(), w.data_ptr(), r.data_ptr(),
+                                     lat.data_ptr(), rel.data_ptr(), None, ctypes.byref(st)),
+              "rows build")
+        torch.cuda.synchronize()
+        times.append(st.ms_total)
+    print(f"C4 rows of 50 attached vertices: {min(times):.2f} ms (distances {st.ms_fw:.2f} ms in "
+          f"{st.n_update} passes, post {st.ms_post:.2f} ms)")
+    glat = lat.cpu().numpy().view(np.uint32).astype(np.uint64) * np.uint64(1_000_000)
+    grel = rel.cpu().numpy()
+    del w, r
+    clat, crel, _, _ = oracle.complete_sample(n, 4, 1000, 10, 500, verts, 16)
+    offd = np.arange(n)[None, :] != verts[:, None]
+    assert np.array_equal(np.where(offd, glat, 0), np.where(offd, clat, 0))
+    assert np.array_equal(grel[offd], crel[offd])

@@ -66,12 +66,18 @@ def test_c1_golden_through_gml(gpu):
     assert np.array_equal(rel, exp["rel"])  # same path, same multiplication order
 
 
-@pytest.mark.parametrize("algo", [ALGO_DENSE_FW, ALGO_SPARSE_SSSP])
-def test_c2_complete_1000(gpu, algo):
+@pytest.mark.parametrize("algo,square", [(ALGO_DENSE_FW, "1"), (ALGO_DENSE_FW, "0"),
+                                          (ALGO_SPARSE_SSSP, "1")])
+def test_c2_complete_1000(gpu, monkeypatch, algo, square):
+    """C2's full table; the dense build by min-plus squaring (its default at ld <= 2048, encoding
+    11) and by the 256-pivot FW rounds (SRT_FW_SQUARE=0)."""
+    monkeypatch.setenv("SRT_FW_SQUARE", square)
     g = graphs.complete_graph(1000, seed=2)
     lat, rel, st = build_tables(g.n, False, g.src, g.dst, g.lat_ns, g.loss, algo=algo)
     exp = _oracle(g)
     assert_tables(lat, rel, exp["lat_int"], exp["rel"], f"C2 algo={algo}")
+    if algo == ALGO_DENSE_FW:
+        assert (st.dist_enc == 11) == (square == "1"), st.dist_enc
 
 
 @pytest.mark.parametrize("n", [257, 3000])
@@ -199,7 +205,9 @@ def test_dense_device_api_and_sharded_single_rank(gpu):
     (1, 5, "1", "1", {"SRT_FW_KB": "64"}),
     (1, 5, "1", "1", {"SRT_FW_WAVES": "4"}), (1, 4, "1", None, {"SRT_FW_WAVES": "4"}),
     (1, 3, "0", None, {}), (1, 3, "0", None, {"SRT_FW_WAVES": "4"}),
-    (160, 2, "1", None, {}), (400, 1, "1", None, {})])
+    (160, 2, "1", None, {}), (400, 1, "1", None, {}),
+    (1, 11, "1", None, {"SRT_FW_SQUARE": "1"}), (1, 11, "0", None, {"SRT_FW_SQUARE": "1"}),
+    (160, 2, "1", None, {"SRT_FW_SQUARE": "1"})])
 def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym, la, env):
     """Each distance encoding of the dense build (fw16.hip) is exact where it is chosen.
 
@@ -212,9 +220,13 @@ def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym, la, e
     update streams, with 256-pivot rounds (encoding 7, the default from n = 8192), 128-pivot
     rounds under SRT_FW_KB=128 (encoding 6) or 64-pivot rounds under SRT_FW_KB=64 (encoding 5).
     SRT_FW_WAVES=4 selects the 4-wave update kernel
-    (fwh_update_kernel) over the 8-wave one (fwq_update_kernel).
+    (fwh_update_kernel) over the 8-wave one (fwq_update_kernel). The round schedules are forced
+    with SRT_FW_SQUARE=0: by default a matrix of ld <= 2048 takes min-plus squaring to a fixed
+    point (encoding 11) -- on this ring, ~128-arc paths, so seven or more passes; at hop 160 the
+    squaring saturates the f16-compare cap and the build falls back to the u16 rounds (2).
     """
     monkeypatch.setenv("SRT_FW_SYM", sym)
+    monkeypatch.setenv("SRT_FW_SQUARE", "0")
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     if la is not None:
@@ -244,7 +256,8 @@ def test_dense_round_sizes_multi_round(gpu, monkeypatch, n, kb):
     """The two-stream schedules with several 256- / 128-pivot rounds (the encoding-tier test has
     one or two): a ring with chords, long enough for distances of a few hundred quanta, against
     the oracle bit for bit. Covers the chain stream's cross updates between a round's panels and
-    the rest launches that start past them."""
+    the rest launches that start past them (SRT_FW_SQUARE=0: not the small-matrix squaring)."""
+    monkeypatch.setenv("SRT_FW_SQUARE", "0")
     monkeypatch.setenv("SRT_FW_LOOKAHEAD", "1")
     monkeypatch.setenv("SRT_FW_KB", kb)
     rng = np.random.default_rng(n)
@@ -275,6 +288,7 @@ def test_dense_lookahead_schedule_one_gpu(gpu, monkeypatch, n, seed):
     on the high-priority stream, double-buffered receive panels)."""
     import torch
     from shadow_amd._lib import lib
+    monkeypatch.setenv("SRT_FW_SQUARE", "0")
     monkeypatch.setenv("SRT_FW_LOOKAHEAD", "1")
     ld = (n + 127) // 128 * 128
     L = lib()

@@ -9,7 +9,11 @@ small constant, so the tables are NOT correct and nothing is checked; what it me
 rank's compute plus its round-to-round critical chain at N ranks, i.e. the N-GPU build time
 minus the collectives' own cost. The N-GPU runs themselves are the driver's.
 
-usage: python tools/solo_rank.py [--ranks 8] [--which 0,3,7] [--workload c4]
+--wire-gbps 0,50,64,100,150 adds a wire model (srt_comm_init_solo_wire): each collective holds
+its stream for --wire-lat-us + the bytes this rank would receive / GB/s, so the schedule feels
+where a wire of that speed would sit on its critical chain.
+
+usage: python tools/solo_rank.py [--ranks 8] [--which 0,3,7] [--workload c4] [--wire-gbps 0,64]
 """
 import argparse
 import ctypes
@@ -38,6 +42,8 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--time-kernels", type=int, default=1,
                     help="1: HIP events around the update launches, as bench.py times them")
+    ap.add_argument("--wire-gbps", default="0", help="comma-separated effective GB/s (0: no wire)")
+    ap.add_argument("--wire-lat-us", type=float, default=10.0, help="per-collective latency")
     a = ap.parse_args()
     wl = WORKLOADS[a.workload]
     n, R = wl["n"], a.ranks
@@ -46,13 +52,15 @@ def main():
     ld = (n + 127) // 128 * 128
     st = torch.cuda.Stream()
     sp = ctypes.c_void_p(st.cuda_stream)
-    for r in which:
+    wires = [float(x) for x in a.wire_gbps.split(",")]
+    for r, gbps in [(r, g) for r in which for g in wires]:
         b, e = ctypes.c_int32(), ctypes.c_int32()
         L.srt_shard_rows(ld, 128, R, r, ctypes.byref(b), ctypes.byref(e))
         b, e = b.value, e.value
         nr = e - b
         comm = ctypes.c_void_p()
-        _lib.check(L.srt_comm_init_solo(R, r, 0, ctypes.byref(comm)), "srt_comm_init_solo")
+        _lib.check(L.srt_comm_init_solo_wire(R, r, 0, gbps, a.wire_lat_us if gbps > 0 else 0.0,
+                                             ctypes.byref(comm)), "srt_comm_init_solo_wire")
         w = torch.empty((nr, ld), dtype=torch.int32, device="cuda")
         rr = torch.empty((nr, ld), dtype=torch.float64, device="cuda")
         lat = torch.empty_like(w)
@@ -62,6 +70,7 @@ def main():
                                              rr.data_ptr(), sp), "gen")
         torch.cuda.synchronize()
         best = None
+        wire0 = L.srt_comm_wire_ms(comm)
         for _ in range(a.reps):
             s = _lib.BuildStats()
             s.time_kernels = a.time_kernels
@@ -74,6 +83,8 @@ def main():
         rounds = ld // 64
         print(json.dumps({
             "workload": a.workload, "n": n, "ranks": R, "rank": r, "rows": nr,
+            "wire_gbps": gbps, "wire_lat_us": a.wire_lat_us if gbps > 0 else 0.0,
+            "wire_ms_per_build": round((L.srt_comm_wire_ms(comm) - wire0) / a.reps, 2),
             "time_kernels": a.time_kernels,
             "dist_enc": int(best.dist_enc), "ms_total": round(best.ms_total, 2),
             "ms_fw": round(best.ms_fw, 2), "ms_post": round(best.ms_post, 2),
