@@ -265,13 +265,15 @@ def run_dense(c: Ctx, wl):
     #   enc 3: 2 x v_add_u32 + 1 x v_pk_minimum3_f16 per 4 relaxations -> 8/4 = 2.0 cycles
     #   enc 2: 1 x v_add_u32 + 1 x v_pk_min_u16 per 2 relaxations      -> 6/2 = 3.0 cycles
     #   enc 1: 2 x v_add_u32 + 1 x v_min3_u32 per 2 relaxations         -> 8/2 = 4.0 cycles
-    cyc_per_relax = {9: 2.0, 8: 2.0, 7: 2.0, 6: 2.0, 5: 2.0, 4: 2.0, 3: 2.0, 2: 3.0, 1: 4.0}[enc]
-    instr_per_relax = {9: 0.75, 8: 0.75, 7: 0.75, 6: 0.75, 5: 0.75, 4: 0.75, 3: 0.75, 2: 1.0, 1: 1.5}[enc]
+    cyc_per_relax = {11: 2.0, 9: 2.0, 8: 2.0, 7: 2.0, 6: 2.0, 5: 2.0, 4: 2.0, 3: 2.0, 2: 3.0,
+                     1: 4.0}[enc]
+    instr_per_relax = {11: 0.75, 9: 0.75, 8: 0.75, 7: 0.75, 6: 0.75, 5: 0.75, 4: 0.75, 3: 0.75,
+                       2: 1.0, 1: 1.5}[enc]
     # the 8-wave update kernel (fwq_update_kernel) unless SRT_FW_WAVES=4 selects the 4-wave one
     w4 = os.environ.get("SRT_FW_WAVES") == "4"
     uk = "fwh_update_kernel" if w4 else "fwq_update_kernel"
     st2 = "" if w4 else ", 2"  # fwq's third template argument: 32-pivot stages per tile
-    kname = {9: "fwq_update_kernel<true, 4, 8>", 8: "fwq_update_kernel<true, 4, 4>", 7: "fwq_update_kernel<true, 4, 8>", 6: "fwq_update_kernel<true, 4, 4>", 5: f"{uk}<true, 4{st2}>",
+    kname = {11: "fwq_update_kernel<false, 0, 8>", 9: "fwq_update_kernel<true, 4, 8>", 8: "fwq_update_kernel<true, 4, 4>", 7: "fwq_update_kernel<true, 4, 8>", 6: "fwq_update_kernel<true, 4, 4>", 5: f"{uk}<true, 4{st2}>",
              4: f"{uk}<true, 0{st2}>" if world == 1 else f"{uk}<true, 4{st2}>",
              3: f"{uk}<false, 0{st2}>",
              2: "fw16_update_kernel<false>", 1: "fw_update_kernel"}[enc]
@@ -284,7 +286,11 @@ def run_dense(c: Ctx, wl):
     # tile pair) less the next pivot block's tile row and column, which run in their own launch
     tiles = ld // 128
     pivots = FW_B  # pivots applied per element per timed unit
-    if enc == 7:  # one GPU, 256-pivot rounds on two update streams: a timed unit is the pair of
+    if enc == 11:  # ld <= 2048, one GPU: min-plus squaring D <- min(D, D (x) D); a timed unit
+        # is one squaring (ld / 256 launches over every tile, ld pivots per element)
+        elems = float(ld) * ld
+        pivots = ld
+    elif enc == 7:  # one GPU, 256-pivot rounds on two update streams: a timed unit is the pair of
         # rest launches of a round j, every upper-triangle tile but the crosses of tile rows
         # 2j + 2 and 2j + 3; of the crosses of 2j and 2j + 1 (which the chain stream updated),
         # the tiles of 2j + 1's take the last 64-pivot panel, the others of 2j's the last three
@@ -406,7 +412,7 @@ def run_dense(c: Ctx, wl):
     s0 = stats[-1]
     # pivots per round (one C-tile residency): 256 (enc 7, 9), 128 (enc 6, 8), else the 64-pivot
     # diagonal block FW_B
-    round_pivots = {7: 256, 9: 256, 6: 128, 8: 128}.get(enc, FW_B)
+    round_pivots = {7: 256, 9: 256, 6: 128, 8: 128, 11: ld}.get(enc, FW_B)
     config = {"workload": wl["desc"], "n": n, "ld": ld, "pivots_per_round": round_pivots,
               "diag_block": FW_B,
               "parallelism": f"row-shard x{world}" + (" + RCCL pivot-panel broadcast"
@@ -462,9 +468,21 @@ def run_sparse(c: Ctx, wl):
     # the kernel's form from the build (srt_build_stats.fw_block of sparse builds)
     form = int(stats[-1].fw_block)
     tf = lambda b: "true" if b else "false"
-    kname = {2: f"wgsssp_kernel<1024, false, {tf(form & 1)}, {tf(form & 2)}>",
+    kname = {3: f"msssp_kernel<{tf(g.directed)}>",
+             2: f"wgsssp_kernel<1024, false, {tf(form & 1)}, {tf(form & 2)}>",
              1: f"wsssp_kernel<{tf(g.directed)}, {tf(form & 1)}, {tf(form & 2)}>"
              }.get(enc, "sssp_kernel")
+    model = "per source: (n+1)*4 + arcs*16 + n*12 B (SURVEY §8d work-efficient gather model)"
+    bytes_launch = float(nsrc * bytes_per_src)
+    if enc == 3:
+        # multi-source kernel: the graph and each vertex's 64-lane working state are shared by
+        # the 64 sources of a batch
+        nb = (nsrc + 63) // 64
+        bytes_launch = float(nsrc * n * 12 + nb * (2 * n * 64 * 12 + (n + 1) * 8 + arcs * 16))
+        model = ("per 64-source batch: each vertex's 64-lane state (u32 D + f64 R) written and "
+                 "read once, the graph once ((n+1)*8 + arcs*16 B); per source its output row "
+                 "(n*12 B)")
+        achieved_gbs = bytes_launch / (k_ms * 1e-3) / 1e9
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{c.args.workload}_n{world}.json")
     if os.path.exists(pmc_path):
@@ -474,9 +492,9 @@ def run_sparse(c: Ctx, wl):
     roofline = {"bound": "hbm", "kernel": kname,
         "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-        "bytes_per_launch": float(nsrc * bytes_per_src), "avg_launch_ms": round(k_ms, 3),
+        "bytes_per_launch": bytes_launch, "avg_launch_ms": round(k_ms, 3),
         "launches_timed": len(stats),
-        "model": "per source: (n+1)*4 + arcs*16 + n*12 B (SURVEY §8d work-efficient gather model)",
+        "model": model,
         "relax_per_launch": float(nsrc) * arcs}
     # untimed check build: the tied-pair count over this rank's rows, summed over ranks
     chk = _lib.BuildStats()

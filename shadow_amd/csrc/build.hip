@@ -6,8 +6,11 @@
  *   use_shortest_path == false : direct edge gather (topology.c:1816-1858)
  *   dense graphs               : blocked Floyd-Warshall (fw16.hip) + predecessor/reliability pass
  *                                (dense.hip)
- *   sparse graphs              : per-source bucket SSSP with settle-time predecessor and
- *                                reliability (wsssp.hip; sparse.hip for overflowing sources)
+ *   sparse graphs              : multi-source shared-frontier SSSP, 64 sources per workgroup,
+ *                                on local graphs (msssp.hip); otherwise per-source bucket SSSP
+ *                                with settle-time predecessor and reliability (wsssp.hip, one
+ *                                wave or one workgroup per source; sparse.hip for overflowing
+ *                                sources)
  * Every table row is its own source's row; pairorder.c decides which row serves a pair.
  * Every path runs on the GPU; a device failure is returned as SRT_E_DEVICE, never replaced by a
  * host computation.
@@ -16,6 +19,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "srt_device.h"
 
@@ -111,6 +115,10 @@ struct srt_sparse_graph {
     uint8_t* ridx;
     uint2 *cw2, *icw2;
     double *r2, *ir2;
+    /* host copy of the relabelled out-rows, for the multi-source kernel's source clusters */
+    int2* h_rp2;
+    uint2* h_cw2;
+    int32_t* h_inv;
 };
 
 int srt_wgsssp_max_n(void);
@@ -157,6 +165,9 @@ extern "C" void srt_sparse_graph_free(srt_sparse_graph* g) {
             if (p) (void)hipFree(p);
     }
     (void)hipSetDevice(prev);
+    free(g->h_rp2);
+    free(g->h_cw2);
+    free(g->h_inv);
     free(g);
 }
 
@@ -313,6 +324,18 @@ static int sparse_graph_from_canon(const srt_canon* c, int device, srt_sparse_gr
             free(idx);
         }
         if (!rc) relabel_csr(c->n, c->rowptr, c->col, c->w, c->r, hperm, hinv, hrp, hcw, hr);
+        if (!rc) {
+            g->h_rp2 = (int2*)malloc(nv * sizeof(int2));
+            g->h_cw2 = (uint2*)malloc((na ? na : 1) * sizeof(uint2));
+            g->h_inv = (int32_t*)malloc(nv * sizeof(int32_t));
+            if (!g->h_rp2 || !g->h_cw2 || !g->h_inv) {
+                rc = SRT_E_NOMEM;
+            } else {
+                memcpy(g->h_rp2, hrp, nv * sizeof(int2));
+                memcpy(g->h_cw2, hcw, na * sizeof(uint2));
+                memcpy(g->h_inv, hinv, nv * sizeof(int32_t));
+            }
+        }
         if (!rc) rc = up((void**)&g->perm, hperm, nv * 4);
         if (!rc) rc = up((void**)&g->inv, hinv, nv * 4);
         if (!rc) rc = up((void**)&g->rp2, hrp, nv * sizeof(int2));
@@ -368,6 +391,103 @@ extern "C" int srt_sparse_graph_info(const srt_sparse_graph* g, int32_t* n, int3
     return SRT_OK;
 }
 
+int srt_msssp_max_n(void);
+int srt_ms_scatter_rows(int nr, int n, const int32_t* rows, const uint32_t* tl, const double* tr,
+                        uint32_t* lat, double* rel, size_t ldo, hipStream_t st);
+int srt_msssp_rows(int n, int directed, const int2* orp, const uint2* ocw, const int2* irp,
+                   const uint2* icw, const double* ir, const int32_t* inv, uint32_t delta,
+                   int nbatch, const int32_t* bsrc, const int32_t* brow, uint32_t* lat, double* rel,
+                   size_t ldo, hipStream_t st);
+
+/* Sweep order for the source clusters: breadth-first from a pseudo-peripheral vertex of each
+ * component (the far end of a breadth-first search from the component's first vertex), so clusters
+ * are cut off a front that moves across the graph and leave no scattered remainders behind it. */
+static void ms_sweep_order(const srt_sparse_graph* g, std::vector<int32_t>& order) {
+    const int n = g->n;
+    std::vector<int32_t> seen((size_t)n, -1), q;
+    q.reserve((size_t)n);
+    order.clear();
+    order.reserve((size_t)n);
+    int tag = 0;
+    auto bfs = [&](int s, std::vector<int32_t>& out) {
+        out.clear();
+        out.push_back(s);
+        seen[s] = tag;
+        for (size_t h = 0; h < out.size(); h++)
+            for (int a = g->h_rp2[out[h]].x; a < g->h_rp2[out[h]].y; a++) {
+                const int v = (int)g->h_cw2[a].x;
+                if (seen[v] != tag) {
+                    seen[v] = tag;
+                    out.push_back(v);
+                }
+            }
+    };
+    std::vector<char> placed((size_t)n, 0);
+    for (int v0 = 0; v0 < n; v0++) {
+        if (placed[v0]) continue;
+        ++tag;
+        bfs(v0, q); /* the component of v0; its last vertex is far from v0 */
+        const int far = q.back();
+        ++tag;
+        bfs(far, q);
+        for (int v : q) placed[v] = 1;
+        order.insert(order.end(), q.begin(), q.end());
+    }
+}
+
+/* Batches of the multi-source kernel (msssp.hip): the sources in groups of 64, each a compact
+ * cluster, grown breadth-first (hop radius <= rmax) from the first unassigned source in the sweep
+ * order, so the 64 distance fields of a batch stay close everywhere and their frontiers overlap. A
+ * group that cannot fill 48 of its 64 lanes within that radius (scattered sources, e.g. a few
+ * attached hosts on a large graph) goes to `rest`, for the single-source kernels: the shared
+ * frontier only pays when the sources are close. rowof[v] (relabelled v): the output row of source
+ * v, -1 when v is not a source; rest receives output rows. */
+static void ms_clusters(const srt_sparse_graph* g, const int32_t* rowof, int nsrc, int rmax,
+                        std::vector<int32_t>& bsrc, std::vector<int32_t>& brow,
+                        std::vector<int32_t>& rest) {
+    const int n = g->n;
+    std::vector<int32_t> order, stamp((size_t)n, -1), queue, depth((size_t)n, 0), found;
+    std::vector<char> done((size_t)n, 0);
+    ms_sweep_order(g, order);
+    int assigned = 0, cl = 0;
+    for (int p = 0; p < n && assigned < nsrc; p++) {
+        const int seed = order[p];
+        if (rowof[seed] < 0 || done[seed]) continue;
+        found.clear();
+        queue.clear();
+        queue.push_back(seed);
+        stamp[seed] = cl;
+        depth[seed] = 0;
+        for (size_t h = 0; h < queue.size() && found.size() < 64; h++) {
+            const int u = queue[h];
+            if (rowof[u] >= 0 && !done[u]) found.push_back(u);
+            if (depth[u] >= rmax) continue;
+            for (int a = g->h_rp2[u].x; a < g->h_rp2[u].y; a++) {
+                const int v = (int)g->h_cw2[a].x;
+                if (stamp[v] != cl) {
+                    stamp[v] = cl;
+                    depth[v] = depth[u] + 1;
+                    queue.push_back(v);
+                }
+            }
+        }
+        for (int v : found) done[v] = 1;
+        assigned += (int)found.size();
+        if (found.size() >= 48) {
+            const size_t base = bsrc.size();
+            bsrc.resize(base + 64, -1);
+            brow.resize(base + 64, -1);
+            for (size_t k = 0; k < found.size(); k++) {
+                bsrc[base + k] = found[k];
+                brow[base + k] = rowof[found[k]];
+            }
+        } else {
+            for (int v : found) rest.push_back(rowof[v]);
+        }
+        cl++;
+    }
+}
+
 /* Rows of nsrc sources (the device list srcs, or [src_begin, src_end) when srcs is NULL): the
  * wave-per-source bucket kernel (wsssp.hip) when the arc weights fit its bucket ring, or the
  * workgroup kernel with the row packed in LDS on large power-law graphs; any source whose buckets
@@ -376,7 +496,7 @@ extern "C" int srt_sparse_graph_info(const srt_sparse_graph* g, int32_t* n, int3
  * source. lms (optional): the f64 path-order ms rows (tables.hip), q the quantum in ns. */
 static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src_end,
                        const int32_t* srcs, uint32_t* lat_rows, double* rel_rows, double* lms,
-                       hipStream_t st, srt_build_stats* stats) {
+                       hipStream_t st, srt_build_stats* stats, int allow_ms = 1) {
     if (!g || src_begin < 0 || src_begin >= src_end || (!srcs && src_end > g->n)) {
         srt_set_error("sparse rows: bad source range [%d, %d)", src_begin, src_end);
         return SRT_E_ARG;
@@ -389,7 +509,29 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
     const char* wenv = getenv("SRT_SPARSE_WORKSET");
     const bool block = (kenv && !strcmp(kenv, "block")) || (wenv && !strcmp(wenv, "hbm"));
     int rc = SRT_OK;
-    if (block || g->max_w >= 256) {
+    /* the multi-source kernel (msssp.hip) where the relabelled graph is local (RGG-like, where
+     * the 64 frontiers of a source cluster overlap); SRT_SPARSE_MS=0/1 disables / forces it.
+     * Sources are clustered here, on the host, before the timed span */
+    const char* menv = getenv("SRT_SPARSE_MS");
+    bool ms = allow_ms && !block && g->n <= srt_msssp_max_n() && g->h_rp2 &&
+              (menv ? atoi(menv) != 0 : g->local != 0);
+    std::vector<int32_t> ms_bsrc, ms_brow, ms_rest, hs;
+    if (ms) {
+        std::vector<int32_t> rowof((size_t)g->n, -1);
+        hs.resize((size_t)nsrc);
+        if (srcs) SRT_HIPCHK(hipMemcpy(hs.data(), srcs, (size_t)nsrc * 4, hipMemcpyDeviceToHost));
+        for (int i = 0; i < nsrc && ms; i++) {
+            const int s = srcs ? hs[i] : b0 + i;
+            if (s < 0 || s >= g->n || rowof[g->h_inv[s]] >= 0) ms = false; /* duplicates */
+            else rowof[g->h_inv[s]] = i;
+        }
+        /* SRT_MSSSP_RMAX: the hop radius of a cluster (tests force it to 0 / large) */
+        const char* renv = getenv("SRT_MSSSP_RMAX");
+        const int rmax = renv ? atoi(renv) : 24;
+        if (ms) ms_clusters(g, rowof.data(), nsrc, rmax, ms_bsrc, ms_brow, ms_rest);
+        if (ms_bsrc.empty()) ms = false; /* every source scattered: the single-source kernels */
+    }
+    if (block || (g->max_w >= 256 && !ms)) {
         const int ct = stats && stats->count_ties;
         rc = srt_sparse_block_rows(g->n, g->rp, g->col, g->w, g->r, g->irp, g->icol, g->iw, g->ir,
                                    g->sw, g->sr, b0, b0 + nsrc, srcs, g->delta, lat_rows, rel_rows,
@@ -433,8 +575,48 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
     /* large power-law graphs (relabelled arcs far apart): the workgroup kernel with the distance
      * row packed in LDS, once a probe source shows every distance fits its 10-bit fields
      * (d(a, b) <= 2 ecc(s0)); SRT_SPARSE_WG=0/1 disables / allows it at any size */
+    int32_t* ms_dev = NULL; /* bsrc then brow, freed on the stream after the launch */
+    if (ms) {
+        const int nb = (int)(ms_bsrc.size() / 64);
+        const size_t bb = ms_bsrc.size() * sizeof(int32_t);
+        SRT_HIPCHK(hipMallocAsync((void**)&ms_dev, 2 * bb, st));
+        SRT_HIPCHK(hipMemcpyAsync(ms_dev, ms_bsrc.data(), bb, hipMemcpyHostToDevice, st));
+        SRT_HIPCHK(hipMemcpyAsync(ms_dev + ms_bsrc.size(), ms_brow.data(), bb,
+                                  hipMemcpyHostToDevice, st));
+        const char* denv = getenv("SRT_MSSSP_DELTA");
+        const uint32_t delta = denv && atoi(denv) > 0 ? (uint32_t)atoi(denv) : 2u * g->delta;
+        rc = srt_msssp_rows(g->n, g->directed, g->rp2, g->cw2, g->irp2, g->icw2, g->ir2, g->inv,
+                            delta, nb, ms_dev, ms_dev + ms_bsrc.size(), lat_rows, rel_rows,
+                            (size_t)g->n, st);
+        if (rc) return rc;
+        SRT_HIPCHK(hipFreeAsync(ms_dev, st));
+        SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)nsrc * sizeof(int), st));
+        if (!ms_rest.empty()) {
+            /* scattered sources: the single-source kernels into scratch rows, scattered after */
+            const int nr = (int)ms_rest.size();
+            std::vector<int32_t> rs((size_t)nr);
+            for (int i = 0; i < nr; i++) rs[i] = srcs ? hs[ms_rest[i]] : b0 + ms_rest[i];
+            int32_t* dr = NULL;
+            uint32_t* tl = NULL;
+            double* tr = NULL;
+            SRT_HIPCHK(hipMallocAsync((void**)&dr, 2 * (size_t)nr * 4, st));
+            SRT_HIPCHK(hipMallocAsync((void**)&tl, (size_t)nr * g->n * 4, st));
+            SRT_HIPCHK(hipMallocAsync((void**)&tr, (size_t)nr * g->n * 8, st));
+            SRT_HIPCHK(hipMemcpyAsync(dr, rs.data(), (size_t)nr * 4, hipMemcpyHostToDevice, st));
+            SRT_HIPCHK(hipMemcpyAsync(dr + nr, ms_rest.data(), (size_t)nr * 4,
+                                      hipMemcpyHostToDevice, st));
+            rc = sparse_rows(g, 0, nr, dr, tl, tr, NULL, st, NULL, 0);
+            if (!rc)
+                rc = srt_ms_scatter_rows(nr, g->n, dr + nr, tl, tr, lat_rows, rel_rows,
+                                         (size_t)g->n, st);
+            (void)hipFreeAsync(tr, st);
+            (void)hipFreeAsync(tl, st);
+            (void)hipFreeAsync(dr, st);
+            if (rc) return rc;
+        }
+    }
     const char* genv = getenv("SRT_SPARSE_WG");
-    bool wg = !g->directed && g->n <= srt_wgsssp_max_n() &&
+    bool wg = !ms && !g->directed && g->n <= srt_wgsssp_max_n() &&
               (genv ? atoi(genv) != 0 : (g->n > 32768 && !g->local));
     /* the workgroup kernel keeps its row in LDS (any order serves), so it runs on the original
      * vertex order and writes reliability straight into the output rows; SRT_WG_ORDER=cm runs it
@@ -466,12 +648,12 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
                                  st, g->ridx, g->rtab);
         if (rc) return rc;
     }
-    if (!wg)
+    if (!wg && !ms)
         rc = srt_wsssp_rows(g->n, g->directed, g->rp2, g->cw2, g->r2, g->irp2, g->icw2, g->ir2,
                             g->perm, g->inv, g->max_w, g->local, b0, b0 + nsrc, srcs, lat_rows,
                             rel_rows, ovf, st);
     if (rc) return rc;
-    const int form = srt_sparse_last_form();
+    const int form = ms ? 8 : srt_sparse_last_form();
     SRT_HIPCHK(hipEventRecord(e1, st));
     rc = srt_sparse_diag(g->n, b0, b0 + nsrc, srcs, g->rp, g->col, g->w, g->r, g->sw, g->sr,
                          lat_rows, rel_rows, (size_t)g->n, st);
@@ -532,7 +714,8 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
         stats->n_update = 1;
         stats->ms_update = a;
         stats->ess_arcs = nov; /* sparse builds: sources recomputed after a bucket overflow */
-        stats->dist_enc = wg ? 2 : 1; /* sparse builds: 2 = workgroup kernel, 1 = wave kernel */
+        /* sparse builds: 3 = multi-source kernel, 2 = workgroup kernel, 1 = wave kernel */
+        stats->dist_enc = ms ? 3 : wg ? 2 : 1;
         stats->fw_block = form;       /* sparse builds: the kernel's form (srt_sparse_last_form) */
         stats->tied_pairs = tied;
     }

@@ -331,6 +331,15 @@ class SparseGraph:
                                           ctypes.c_void_p(rel_ptr), ctypes.c_void_p(stream), st),
               "srt_sparse_graph_rows")
 
+    def rows_list(self, srcs_ptr, nsrc, lat_ptr, rel_ptr, stream=None, stats=None):
+        """srt_sparse_graph_rows_list: row i of the device buffers is source srcs[i] (a device
+        int32 array of nsrc vertices)."""
+        st = ctypes.byref(stats) if stats is not None else None
+        check(lib().srt_sparse_graph_rows_list(self._h, int(nsrc), ctypes.c_void_p(srcs_ptr),
+                                               ctypes.c_void_p(lat_ptr), ctypes.c_void_p(rel_ptr),
+                                               None, ctypes.c_void_p(stream), st),
+              "srt_sparse_graph_rows_list")
+
     def free(self):
         if getattr(self, "_h", None):
             lib().srt_sparse_graph_free(self._h)

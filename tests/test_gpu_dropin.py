@@ -59,11 +59,12 @@ def _expected_sub(g, verts, nthreads=16):
 
 
 def test_auto_dispatch_c3_rgg_20000_full_table(gpu):
-    """C3 through srt_build_tables (AUTO) and srt_build_tables_multi(ngpus=1): the wave SSSP."""
+    """C3 through srt_build_tables (AUTO) and srt_build_tables_multi(ngpus=1): the multi-source
+    SSSP (msssp.hip)."""
     g = graphs.random_geometric(20000, seed=3)
     rows = np.r_[0:8, 9_996:10_004, 19_992:20_000, np.linspace(8, 19_990, 24).astype(int)]
     lat, rel, st = build_tables(g.n, False, g.src, g.dst, g.lat_ns, g.loss, algo=ALGO_AUTO)
-    assert st.algo == ALGO_SPARSE_SSSP and st.dist_enc == 1
+    assert st.algo == ALGO_SPARSE_SSSP and st.dist_enc == 3
     _check_sampled_rows(lat, rel, g, rows, "C3 AUTO")
     assert np.array_equal(lat, lat.T)
     off = ~np.eye(g.n, dtype=bool)

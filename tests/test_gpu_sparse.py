@@ -19,6 +19,13 @@ pytestmark = pytest.mark.gpu
 REL_TOL = 1e-12
 
 
+@pytest.fixture(autouse=True)
+def _single_source_kernels(monkeypatch):
+    """These tests pin the single-source kernels; the multi-source kernel that AUTO gives local
+    graphs (msssp.hip, dist_enc 3) has its own file, tests/test_gpu_msssp.py."""
+    monkeypatch.setenv("SRT_SPARSE_MS", "0")
+
+
 def _rows_on_gpu(sg, s0, s1, torch, stats=None):
     lat = torch.empty((s1 - s0, sg.n), dtype=torch.int32, device="cuda")
     rel = torch.empty((s1 - s0, sg.n), dtype=torch.float64, device="cuda")
