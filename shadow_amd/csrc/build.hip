@@ -18,6 +18,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <pthread.h>
+
 #include <algorithm>
 #include <vector>
 
@@ -100,6 +102,7 @@ struct srt_sparse_graph {
     int64_t arcs;
     uint64_t quantum_ns;
     uint32_t delta, max_w;
+    uint64_t dist_bound; /* srt_canon.dist_bound */
     int local; /* relabelled arcs span <= 4096 vertices on average (graph.c CM order) */
     int32_t *rp, *col, *irp, *icol;
     uint32_t *w, *iw, *sw;
@@ -119,6 +122,12 @@ struct srt_sparse_graph {
     int2* h_rp2;
     uint2* h_cw2;
     int32_t* h_inv;
+    /* the clusters of the last source set (the same rows are usually asked for again): the
+     * sources (original ids, or the range [ck_b0, ck_b0 + ck_n) when ck_list is 0), the radius,
+     * then nbatch x 64 sources and rows and the rows left to the single-source kernels */
+    int32_t ck_n, ck_b0, ck_list, ck_rmax, ck_maxb, ck_nb, ck_nrest;
+    int32_t *ck_srcs, *ck_bsrc, *ck_brow, *ck_rest;
+    pthread_mutex_t ck_mu; /* all-zero (calloc) is the default mutex */
 };
 
 int srt_wgsssp_max_n(void);
@@ -168,6 +177,10 @@ extern "C" void srt_sparse_graph_free(srt_sparse_graph* g) {
     free(g->h_rp2);
     free(g->h_cw2);
     free(g->h_inv);
+    free(g->ck_srcs);
+    free(g->ck_bsrc);
+    free(g->ck_brow);
+    free(g->ck_rest);
     free(g);
 }
 
@@ -246,6 +259,7 @@ static int sparse_graph_from_canon(const srt_canon* c, int device, srt_sparse_gr
     g->directed = c->directed;
     g->arcs = c->arcs;
     g->quantum_ns = c->quantum_ns;
+    g->dist_bound = c->dist_bound;
     g->max_w = 0;
     for (int64_t k = 0; k < c->arcs; k++) g->max_w = c->w[k] > g->max_w ? c->w[k] : g->max_w;
     /* bucket width of the label-correcting loop: the mean arc weight */
@@ -397,7 +411,7 @@ int srt_ms_scatter_rows(int nr, int n, const int32_t* rows, const uint32_t* tl, 
 int srt_msssp_rows(int n, int directed, const int2* orp, const uint2* ocw, const int2* irp,
                    const uint2* icw, const double* ir, const int32_t* inv, uint32_t delta,
                    int nbatch, const int32_t* bsrc, const int32_t* brow, uint32_t* lat, double* rel,
-                   size_t ldo, hipStream_t st);
+                   size_t ldo, int d16, hipStream_t st);
 
 /* Sweep order for the source clusters: breadth-first from a pseudo-peripheral vertex of each
  * component (the far end of a breadth-first search from the component's first vertex), so clusters
@@ -439,12 +453,15 @@ static void ms_sweep_order(const srt_sparse_graph* g, std::vector<int32_t>& orde
  * cluster, grown breadth-first (hop radius <= rmax) from the first unassigned source in the sweep
  * order, so the 64 distance fields of a batch stay close everywhere and their frontiers overlap. A
  * group that cannot fill 48 of its 64 lanes within that radius (scattered sources, e.g. a few
- * attached hosts on a large graph) goes to `rest`, for the single-source kernels: the shared
+ * attached hosts on a large graph; or 8,192 vertices visited first) becomes a batch of its own
+ * while all batches fit max_batches (the kernel's concurrent slots), else goes to `rest`, for the
+ * single-source kernels: the shared
  * frontier only pays when the sources are close. rowof[v] (relabelled v): the output row of source
  * v, -1 when v is not a source; rest receives output rows. */
 static void ms_clusters(const srt_sparse_graph* g, const int32_t* rowof, int nsrc, int rmax,
-                        std::vector<int32_t>& bsrc, std::vector<int32_t>& brow,
+                        int max_batches, std::vector<int32_t>& bsrc, std::vector<int32_t>& brow,
                         std::vector<int32_t>& rest) {
+    std::vector<int32_t> small_src, small_cnt; /* clusters under 48 sources, in order */
     const int n = g->n;
     std::vector<int32_t> order, stamp((size_t)n, -1), queue, depth((size_t)n, 0), found;
     std::vector<char> done((size_t)n, 0);
@@ -461,7 +478,8 @@ static void ms_clusters(const srt_sparse_graph* g, const int32_t* rowof, int nsr
         for (size_t h = 0; h < queue.size() && found.size() < 64; h++) {
             const int u = queue[h];
             if (rowof[u] >= 0 && !done[u]) found.push_back(u);
-            if (depth[u] >= rmax) continue;
+            /* hop radius, and a visit budget that bounds the host work on small-world graphs */
+            if (depth[u] >= rmax || queue.size() >= 8192) continue;
             for (int a = g->h_rp2[u].x; a < g->h_rp2[u].y; a++) {
                 const int v = (int)g->h_cw2[a].x;
                 if (stamp[v] != cl) {
@@ -482,9 +500,30 @@ static void ms_clusters(const srt_sparse_graph* g, const int32_t* rowof, int nsr
                 brow[base + k] = rowof[found[k]];
             }
         } else {
-            for (int v : found) rest.push_back(rowof[v]);
+            small_cnt.push_back((int32_t)found.size());
+            small_src.insert(small_src.end(), found.begin(), found.end());
         }
         cl++;
+    }
+    /* the small clusters (the sweep's remainders, or sources scattered over the graph) still ride
+     * the multi-source kernel while every batch fits the kernel's concurrent slots: a batch costs
+     * about the same wall time whatever its lane count, and the single-source kernels would run
+     * after it */
+    const bool fit = (int)(bsrc.size() / 64 + small_cnt.size()) <= max_batches;
+    size_t o = 0;
+    for (int32_t c : small_cnt) {
+        if (fit) {
+            const size_t base = bsrc.size();
+            bsrc.resize(base + 64, -1);
+            brow.resize(base + 64, -1);
+            for (int32_t k = 0; k < c; k++) {
+                bsrc[base + k] = small_src[o + k];
+                brow[base + k] = rowof[small_src[o + k]];
+            }
+        } else {
+            for (int32_t k = 0; k < c; k++) rest.push_back(rowof[small_src[o + k]]);
+        }
+        o += (size_t)c;
     }
 }
 
@@ -528,7 +567,51 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
         /* SRT_MSSSP_RMAX: the hop radius of a cluster (tests force it to 0 / large) */
         const char* renv = getenv("SRT_MSSSP_RMAX");
         const int rmax = renv ? atoi(renv) : 24;
-        if (ms) ms_clusters(g, rowof.data(), nsrc, rmax, ms_bsrc, ms_brow, ms_rest);
+        int cus = 256, dev = 0;
+        hipDeviceProp_t prop;
+        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+            cus = prop.multiProcessorCount;
+        const char* benv = getenv("SRT_MSSSP_MAXB"); /* tests: the batch budget */
+        const int maxb = benv ? atoi(benv) : 2 * cus;
+        srt_sparse_graph* gm = const_cast<srt_sparse_graph*>(g); /* the cluster cache */
+        pthread_mutex_lock(&gm->ck_mu);
+        const bool hit = ms && gm->ck_bsrc && gm->ck_n == nsrc && gm->ck_rmax == rmax &&
+                         gm->ck_maxb == maxb &&
+                         gm->ck_list == (srcs != NULL) &&
+                         (srcs ? !memcmp(gm->ck_srcs, hs.data(), (size_t)nsrc * 4)
+                               : gm->ck_b0 == b0);
+        if (hit) {
+            ms_bsrc.assign(gm->ck_bsrc, gm->ck_bsrc + (size_t)gm->ck_nb * 64);
+            ms_brow.assign(gm->ck_brow, gm->ck_brow + (size_t)gm->ck_nb * 64);
+            ms_rest.assign(gm->ck_rest, gm->ck_rest + gm->ck_nrest);
+        } else if (ms) {
+            ms_clusters(g, rowof.data(), nsrc, rmax, maxb, ms_bsrc, ms_brow, ms_rest);
+            free(gm->ck_srcs);
+            free(gm->ck_bsrc);
+            free(gm->ck_brow);
+            free(gm->ck_rest);
+            gm->ck_n = nsrc;
+            gm->ck_b0 = b0;
+            gm->ck_list = srcs != NULL;
+            gm->ck_rmax = rmax;
+            gm->ck_maxb = maxb;
+            gm->ck_nb = (int32_t)(ms_bsrc.size() / 64);
+            gm->ck_nrest = (int32_t)ms_rest.size();
+            gm->ck_srcs = (int32_t*)malloc((size_t)(srcs ? nsrc : 1) * 4);
+            gm->ck_bsrc = (int32_t*)malloc((ms_bsrc.size() + 1) * 4);
+            gm->ck_brow = (int32_t*)malloc((ms_brow.size() + 1) * 4);
+            gm->ck_rest = (int32_t*)malloc((ms_rest.size() + 1) * 4);
+            if (gm->ck_srcs && gm->ck_bsrc && gm->ck_brow && gm->ck_rest) {
+                if (srcs) memcpy(gm->ck_srcs, hs.data(), (size_t)nsrc * 4);
+                memcpy(gm->ck_bsrc, ms_bsrc.data(), ms_bsrc.size() * 4);
+                memcpy(gm->ck_brow, ms_brow.data(), ms_brow.size() * 4);
+                memcpy(gm->ck_rest, ms_rest.data(), ms_rest.size() * 4);
+            } else { /* no cache, no harm */
+                free(gm->ck_bsrc);
+                gm->ck_bsrc = NULL;
+            }
+        }
+        pthread_mutex_unlock(&gm->ck_mu);
         if (ms_bsrc.empty()) ms = false; /* every source scattered: the single-source kernels */
     }
     if (block || (g->max_w >= 256 && !ms)) {
@@ -583,11 +666,16 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
         SRT_HIPCHK(hipMemcpyAsync(ms_dev, ms_bsrc.data(), bb, hipMemcpyHostToDevice, st));
         SRT_HIPCHK(hipMemcpyAsync(ms_dev + ms_bsrc.size(), ms_brow.data(), bb,
                                   hipMemcpyHostToDevice, st));
+        /* bucket width: 8 mean arc weights (C3: 64 quanta; same-box sweep in DESIGN §5.4) */
         const char* denv = getenv("SRT_MSSSP_DELTA");
-        const uint32_t delta = denv && atoi(denv) > 0 ? (uint32_t)atoi(denv) : 2u * g->delta;
+        const uint32_t delta = denv && atoi(denv) > 0 ? (uint32_t)atoi(denv) : 8u * g->delta;
+        /* 16-bit working distances when every finite distance provably fits (half the bytes of
+         * every row access); SRT_MSSSP_U16=0 keeps 32 */
+        const char* uenv = getenv("SRT_MSSSP_U16");
+        const int d16 = g->dist_bound < 0xFFFFull && !(uenv && atoi(uenv) == 0);
         rc = srt_msssp_rows(g->n, g->directed, g->rp2, g->cw2, g->irp2, g->icw2, g->ir2, g->inv,
                             delta, nb, ms_dev, ms_dev + ms_bsrc.size(), lat_rows, rel_rows,
-                            (size_t)g->n, st);
+                            (size_t)g->n, d16, st);
         if (rc) return rc;
         SRT_HIPCHK(hipFreeAsync(ms_dev, st));
         SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)nsrc * sizeof(int), st));

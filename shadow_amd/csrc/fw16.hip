@@ -846,14 +846,26 @@ static __device__ __forceinline__ void fwq_stage(uint32_t (&acc)[4][4], const ui
 template <bool SYM, int XM = 0, int NST = 2>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) void fwq_update_kernel(
     u16* __restrict__ D, int ld, const u16* __restrict__ P, int k0, int ncol_tiles, int i0, int skip,
-    const uint32_t* __restrict__ tl, int te, int prev = -1) {
+    const uint32_t* __restrict__ tl, int te, int prev = -1, u16* __restrict__ outq = nullptr) {
     __shared__ __attribute__((aligned(16))) uint32_t sA[UKC / 2 * 128 * 2];
     __shared__ __attribute__((aligned(16))) u16 sB[UKC * UBS];
     if constexpr (XM == 3 || XM == 6 || XM == 7 || XM == 8 || XM == 9 || XM == 13)
         FW_CHAIN_PRIO(); /* next-row tiles */
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     int I, J, Iloc;
-    if constexpr (XM == 9) {
+    int q20 = 0;
+    if constexpr (XM == 20) {
+        /* split-k squaring (ld <= 2048): tile (I, J) x pivot block q of NST * UKC pivots from
+         * k0, C read from D, min(C, A (x) B) written whole to outq's slice q */
+        const int tiles = ncol_tiles * ncol_tiles;
+        const int bid = (int)blockIdx.x % tiles;
+        q20 = (int)blockIdx.x / tiles;
+        I = bid / ncol_tiles;
+        J = bid % ncol_tiles;
+        Iloc = I;
+        k0 += q20 * NST * UKC;
+        P = D + (size_t)k0 * ld;
+    } else if constexpr (XM == 9) {
         I = min((int)blockIdx.x, skip);
         J = max((int)blockIdx.x, skip);
         Iloc = I;
@@ -918,6 +930,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
      * the C load, the four 64-bit row addresses spill across the loop */
     int tq = tid;
     asm volatile("" : "+v"(tq));
+    if constexpr (XM == 20) {
+        u16* Oq = outq + (size_t)q20 * ld * ld + (size_t)Iloc * 128 * ld + J * 128 +
+                  (size_t)((tq >> 4) * 4) * ld + (tq & 15) * 8;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            *reinterpret_cast<uint4*>(Oq + (size_t)r * ld) =
+                make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+        (void)sum0;
+        return;
+    }
     u16* Cq = C + (size_t)((tq >> 4) * 4) * ld + (tq & 15) * 8;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -2534,6 +2556,33 @@ int srt_fw16_rows(int n, int ld, int nsub, const int32_t* dverts, const uint32_t
  * with the in-place updates), so a graph whose shortest paths have h arcs takes about
  * log2(h) + 2 passes of four launches: for small n that replaces ld / 64 FW rounds, each a chain
  * of dependent launches (C2: 16 rounds). */
+static __device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+    return min(a & 0xFFFFu, b & 0xFFFFu) | (min(a >> 16, b >> 16) << 16);
+}
+
+/* D = min over q < nq of the split-k partials (each already <= D); flag: any entry changed */
+__global__ void sq_reduce_kernel(size_t count, int nq, const u16* __restrict__ part,
+                                 u16* __restrict__ d, int* __restrict__ flag) {
+    bool ch = false;
+    for (size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < count;
+         i += (size_t)gridDim.x * blockDim.x * 8) {
+        uint4 m = *reinterpret_cast<const uint4*>(part + i);
+        for (int q = 1; q < nq; ++q) {
+            const uint4 x = *reinterpret_cast<const uint4*>(part + (size_t)q * count + i);
+            m.x = pk_min_u16(m.x, x.x);
+            m.y = pk_min_u16(m.y, x.y);
+            m.z = pk_min_u16(m.z, x.z);
+            m.w = pk_min_u16(m.w, x.w);
+        }
+        const uint4 o = *reinterpret_cast<const uint4*>(d + i);
+        if (m.x != o.x || m.y != o.y || m.z != o.z || m.w != o.w) {
+            *reinterpret_cast<uint4*>(d + i) = m;
+            ch = true;
+        }
+    }
+    if (__ballot(ch) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
 static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStream_t st,
                        evpool_t* evp, int* exact) {
     const int dev = srt_state_slot();
@@ -2556,22 +2605,57 @@ static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStrea
         hipStream_t s;
         ~freer() { (void)hipFreeAsync(p, s); }
     } fr{dsum, st};
+    /* split-k: one launch per squaring over every (tile, 256-pivot block) -- T^2 ld / 256
+     * workgroups, every CU busy at C2's T = 8 -- into per-block partials, then one reduce pass
+     * that also says whether anything changed (SRT_FW_SQUARE_SPLIT=0: the in-place launches per
+     * block, one workgroup per tile) */
+    const char* sp_env = getenv("SRT_FW_SQUARE_SPLIT");
+    const bool split = !(sp_env && atoi(sp_env) == 0);
+    const int nq8 = ld / 256, tail = (ld % 256) ? 1 : 0;
+    u16* part = nullptr;
+    if (split) SRT_HIPCHK(hipMallocAsync((void**)&part, (size_t)(nq8 + tail) * ld * ld * 2, st));
+    struct freer2 {
+        u16* p;
+        hipStream_t s;
+        ~freer2() {
+            if (p) (void)hipFreeAsync(p, s);
+        }
+    } fr2{part, st};
     unsigned long long prev = ~0ull;
     for (int it = 0; it < 64; ++it) {
         if (evp && evp->used + 2 <= evp->cap) {
             SRT_HIPCHK(hipEventRecord(evp->ev[evp->used], st));
         }
-        for (int k0 = 0; k0 < ld; k0 += 256) {
-            if (k0 + 256 <= ld)
-                fwq_update_kernel<false, 0, 8><<<(unsigned)(T * T), 512, 0, st>>>(
-                    d, ld, d + (size_t)k0 * ld, k0, T, 0, -1, nullptr, 0);
-            else
-                fwq_update_kernel<false, 0, 4><<<(unsigned)(T * T), 512, 0, st>>>(
-                    d, ld, d + (size_t)k0 * ld, k0, T, 0, -1, nullptr, 0);
+        if (split) {
+            if (nq8)
+                fwq_update_kernel<false, 20, 8><<<(unsigned)(T * T * nq8), 512, 0, st>>>(
+                    d, ld, d, 0, T, 0, 0, nullptr, 0, -1, part);
+            if (tail)
+                fwq_update_kernel<false, 20, 4><<<(unsigned)(T * T), 512, 0, st>>>(
+                    d, ld, d, nq8 * 256, T, 0, 0, nullptr, 0, -1, part + (size_t)nq8 * ld * ld);
+            SRT_HIPCHK(hipMemsetAsync(flags, 0, sizeof(int), st));
+            sq_reduce_kernel<<<256, 256, 0, st>>>((size_t)ld * ld, nq8 + tail, part, d, flags);
+        } else {
+            for (int k0 = 0; k0 < ld; k0 += 256) {
+                if (k0 + 256 <= ld)
+                    fwq_update_kernel<false, 0, 8><<<(unsigned)(T * T), 512, 0, st>>>(
+                        d, ld, d + (size_t)k0 * ld, k0, T, 0, -1, nullptr, 0);
+                else
+                    fwq_update_kernel<false, 0, 4><<<(unsigned)(T * T), 512, 0, st>>>(
+                        d, ld, d + (size_t)k0 * ld, k0, T, 0, -1, nullptr, 0);
+            }
         }
         if (evp && evp->used + 2 <= evp->cap) {
             SRT_HIPCHK(hipEventRecord(evp->ev[evp->used + 1], st));
             evp->used += 2;
+        }
+        SRT_HIPCHK(hipGetLastError());
+        if (split) {
+            int ch = 0;
+            SRT_HIPCHK(hipMemcpyAsync(&ch, flags, sizeof(int), hipMemcpyDeviceToHost, st));
+            SRT_HIPCHK(hipStreamSynchronize(st));
+            if (!ch) break;
+            continue;
         }
         SRT_HIPCHK(hipMemsetAsync(dsum, 0, sizeof(unsigned long long), st));
         rows_sum_kernel<<<64, 256, 0, st>>>((size_t)ld * ld, d, dsum);

@@ -303,6 +303,7 @@ int srt_canon_build(const srt_edges* g, srt_canon* c) {
                       (unsigned long long)bound, (unsigned long long)q);
         return SRT_E_RANGE;
     }
+    c->dist_bound = bound;
     rc = fill_csr(g, a, k, q, &c->rowptr, &c->col, &c->w, &c->r, &c->arcs);
     if (rc == SRT_OK && g->directed) {
         for (int64_t i = 0; i < k; i++) {

@@ -54,6 +54,9 @@
 static __device__ __forceinline__ uint32_t ms_ld(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+static __device__ __forceinline__ uint32_t ms_ld(const uint16_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 static __device__ __forceinline__ double ms_ld(const double* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -113,7 +116,7 @@ static __device__ __forceinline__ void ms_compact(uint32_t* bm, int nw, int* lis
  * for undirected graphs); inv[original] = relabelled; bsrc / brow: per batch and lane the
  * relabelled source and the output row (-1 = empty lane); ws: per slot D (n x 64 u32), R (n x 64
  * f64) and the lane minimum of every vertex (n u32). */
-template <bool DIRECTED, bool PROF>
+template <bool DIRECTED, bool PROF, typename DT>
 __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
     int n, const int2* __restrict__ orp, const uint2* __restrict__ ocw,
     const int2* __restrict__ irp, const uint2* __restrict__ icw, const double* __restrict__ ir,
@@ -130,9 +133,14 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
     uint32_t* const bmB = sm + nw;
     uint32_t* const pend = sm + 2 * nw;
     const int tid = threadIdx.x, lane = tid & (MS_L - 1), wave = tid >> 6;
-    uint32_t* const D = ws + (size_t)blockIdx.x * slot_words;
-    double* const R = reinterpret_cast<double*>(D + (size_t)n * MS_L);
-    uint32_t* const mind = D + (size_t)n * MS_L * 3;
+    /* DT: u32 quanta, or u16 when every finite distance is below 0xFFFF (the caller's bound);
+     * DINF marks an unreached lane, and a u16 candidate saturates at DINF - 1 -- still an upper
+     * bound of the true distance (<= the bound), so the fixed point is unchanged */
+    constexpr uint32_t DINF = sizeof(DT) == 2 ? 0xFFFFu : SRT_INF;
+    uint32_t* const wsb = ws + (size_t)blockIdx.x * slot_words;
+    DT* const D = reinterpret_cast<DT*>(wsb);
+    double* const R = reinterpret_cast<double*>(wsb + (size_t)n * MS_L);
+    uint32_t* const mind = wsb + (size_t)n * MS_L * 3;
 
     /* PROF (SRT_MSSSP_PROF=1): per batch, passes, pulls, bucket advances, then the cycles of
      * wave 0 in the compaction, pull, advance, output and initialisation phases */
@@ -153,8 +161,9 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
         for (int i = tid; i < 3 * nw; i += MS_WG) sm[i] = 0u;
         {
             uint4* d4 = reinterpret_cast<uint4*>(D);
-            const uint4 inf4 = make_uint4(SRT_INF, SRT_INF, SRT_INF, SRT_INF);
-            for (size_t i = tid; i < (size_t)n * (MS_L / 4); i += MS_WG) d4[i] = inf4;
+            const uint32_t iw = sizeof(DT) == 2 ? 0xFFFFFFFFu : SRT_INF;
+            const uint4 inf4 = make_uint4(iw, iw, iw, iw);
+            for (size_t i = tid; i < (size_t)n * MS_L * sizeof(DT) / 16; i += MS_WG) d4[i] = inf4;
         }
         __syncthreads();
         const int mysrc = bsrc[(size_t)b * MS_L + lane];
@@ -164,7 +173,7 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
             const int s = bsrc[(size_t)b * MS_L + l];
             if (s < 0) continue;
             if (lane == l) {
-                D[(size_t)s * MS_L + l] = 0u;
+                D[(size_t)s * MS_L + l] = (DT)0;
                 R[(size_t)s * MS_L + l] = 1.0;
             }
             const int2 be = orp[s];
@@ -224,8 +233,8 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                     int bk[MS_G];
 #pragma unroll
                     for (int j = 0; j < MS_G; j++) {
-                        bc[j] = SRT_INF;
-                        bdu[j] = SRT_INF;
+                        bc[j] = DINF;
+                        bdu[j] = DINF;
                         bu[j] = 0u;
                         bk[j] = -1;
                     }
@@ -249,12 +258,13 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
 #pragma unroll
                                 for (int a = 0; a < MS_AK; a++) {
                                     const int k = c0 + h + a;
-                                    if (k >= dg[j] || du[j][a] >= SRT_INF) continue;
+                                    if (k >= dg[j] || du[j][a] >= DINF) continue;
                                     const uint32_t col =
                                         (uint32_t)__builtin_amdgcn_readlane((int)ea.x, j * MS_AC + h + a);
                                     const uint32_t w =
                                         (uint32_t)__builtin_amdgcn_readlane((int)ea.y, j * MS_AC + h + a);
-                                    const uint32_t c = du[j][a] + w;
+                                    const uint32_t c =
+                                        sizeof(DT) == 2 ? min(du[j][a] + w, DINF - 1u) : du[j][a] + w;
                                     if (c < bc[j] || (c == bc[j] && du[j][a] < bdu[j])) {
                                         bc[j] = c;
                                         bdu[j] = du[j][a];
@@ -268,7 +278,7 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                     double nr[MS_G];
 #pragma unroll
                     for (int j = 0; j < MS_G; j++) {
-                        nd[j] = SRT_INF;
+                        nd[j] = DINF;
                         nr[j] = 0.0;
                         if ((int)v[j] == mysrc) {
                             nd[j] = 0u;
@@ -282,12 +292,12 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                     for (int j = 0; j < MS_G; j++) {
                         if (j >= ng) break;
                         /* an unreached lane's R is not initialised: it reads as 0 */
-                        const double ol = od[j] < SRT_INF ? orl[j] : 0.0;
+                        const double ol = od[j] < DINF ? orl[j] : 0.0;
                         const bool ch = nd[j] != od[j] ||
                                         __double_as_longlong(nr[j]) != __double_as_longlong(ol);
                         if (!__ballot(ch)) continue;
                         const uint32_t vj = v[j];
-                        D[(size_t)vj * MS_L + lane] = nd[j];
+                        D[(size_t)vj * MS_L + lane] = (DT)nd[j];
                         R[(size_t)vj * MS_L + lane] = nr[j];
                         const uint32_t mn = ms_wave_min(nd[j]);
                         if (lane == 0) mind[vj] = mn;
@@ -297,7 +307,7 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                             if (DIRECTED) {
                                 const int2 ob = orp[vj];
                                 for (int k = ob.x + lane; k < ob.y; k += MS_L) ms_set(nxt, ocw[k].x);
-                            } else if (dg[j] <= MS_AC) { /* the arcs of the (only) chunk */
+                            } else if (maxdeg <= MS_AC) { /* the arcs of the (only) chunk */
                                 if (aj == j && aa < dg[j]) ms_set(nxt, ea.x);
                             } else {
                                 for (int k = bx[j] + lane; k < bx[j] + dg[j]; k += MS_L)
@@ -367,17 +377,30 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
             const int t = t0 + lane;
             const bool ok = t < n;
             const uint32_t v = ok ? (uint32_t)inv[t] : 0u;
+            /* E lanes per 16-byte piece of the D row: 4 (u32) or 8 (u16) */
+            constexpr int E = 16 / (int)sizeof(DT);
             const uint4* d4 = reinterpret_cast<const uint4*>(D + (size_t)v * MS_L);
             const double2* r2 = reinterpret_cast<const double2*>(R + (size_t)v * MS_L);
-#pragma unroll 4
-            for (int q = 0; q < MS_L / 4; q++) {
-                const uint4 d = d4[q];
-                const double2 ra = r2[2 * q], rb = r2[2 * q + 1];
-                const uint32_t dd[4] = {d.x, d.y, d.z, d.w};
-                const double rr[4] = {ra.x, ra.y, rb.x, rb.y};
+#pragma unroll 2
+            for (int q = 0; q < MS_L / E; q++) {
+                const uint4 dq = d4[q];
+                const uint32_t w4[4] = {dq.x, dq.y, dq.z, dq.w};
+                uint32_t dd[E];
+                double rr[E];
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const int row = br[4 * q + i];
+                for (int i = 0; i < E; i++) {
+                    dd[i] = sizeof(DT) == 2 ? (w4[i >> 1] >> (16 * (i & 1))) & 0xFFFFu : w4[i];
+                    if (dd[i] >= DINF) dd[i] = SRT_INF;
+                }
+#pragma unroll
+                for (int i = 0; i < E; i += 2) {
+                    const double2 x = r2[(q * E + i) >> 1];
+                    rr[i] = x.x;
+                    rr[i + 1] = x.y;
+                }
+#pragma unroll
+                for (int i = 0; i < E; i++) {
+                    const int row = br[q * E + i];
                     if (row < 0 || !ok) continue;
                     lat[(size_t)row * ldo + t] = dd[i];
                     rel[(size_t)row * ldo + t] = dd[i] < SRT_INF ? rr[i] : 0.0;
@@ -406,10 +429,15 @@ int srt_msssp_max_n(void) {
  * nbatch x 64 relabelled sources and output rows, -1 = empty lane); graph arrays as for the
  * kernel. Rows get the distances (u32 quanta, SRT_INF unreached) and the path-order reliability;
  * the diagonal is the caller's (srt_sparse_diag). */
+/* the working rows stay allocated between builds (per device or virtual-rank slot): a fresh
+ * multi-GB allocation per call costs milliseconds of mapping */
+static uint32_t* g_ms_ws[SRT_STATE_SLOTS];
+static size_t g_ms_cap[SRT_STATE_SLOTS];
+
 int srt_msssp_rows(int n, int directed, const int2* orp, const uint2* ocw, const int2* irp,
                    const uint2* icw, const double* ir, const int32_t* inv, uint32_t delta,
                    int nbatch, const int32_t* bsrc, const int32_t* brow, uint32_t* lat, double* rel,
-                   size_t ldo, hipStream_t st) {
+                   size_t ldo, int d16, hipStream_t st) {
     if (n > srt_msssp_max_n()) {
         srt_set_error("msssp: %d vertices exceed the LDS bitmaps (%d)", n, srt_msssp_max_n());
         return SRT_E_ARG;
@@ -419,25 +447,39 @@ int srt_msssp_rows(int n, int directed, const int2* orp, const uint2* ocw, const
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
         cus = prop.multiProcessorCount;
-    /* D, R and the lane minimum, rounded to 16 bytes (the uint4 initialisation of D) */
+    /* D (u32-sized slots; a u16 row uses half), R and the lane minimum, rounded to 16 bytes */
     const size_t slot_words = ((size_t)n * MS_L * 3 + (size_t)n + 3) & ~(size_t)3;
     const size_t per_slot = slot_words * sizeof(uint32_t);
     const char* wenv = getenv("SRT_MSSSP_SLOTS");
     size_t slots = wenv && atoi(wenv) > 0 ? (size_t)atoi(wenv) : 2 * (size_t)cus;
-    size_t budget = (size_t)16 << 30, free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > ((size_t)8 << 30)) {
-        budget = free_b - ((size_t)8 << 30);
-        if (budget > ((size_t)64 << 30)) budget = (size_t)64 << 30;
-    }
-    if (slots * per_slot > budget) slots = budget / per_slot;
     if (slots > (size_t)nbatch) slots = nbatch;
-    if (slots < 1) slots = 1;
-    uint32_t* ws = NULL;
-    if (hipMallocAsync((void**)&ws, slots * per_slot, st) != hipSuccess) {
-        (void)hipGetLastError();
-        srt_set_error("msssp: workspace of %zu MiB failed", (slots * per_slot) >> 20);
-        return SRT_E_NOMEM;
+    const int sl = srt_state_slot();
+    if (g_ms_cap[sl] < slots * per_slot) {
+        size_t budget = (size_t)16 << 30, free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > ((size_t)8 << 30)) {
+            budget = free_b + g_ms_cap[sl] - ((size_t)8 << 30);
+            if (budget > ((size_t)64 << 30)) budget = (size_t)64 << 30;
+        }
+        if (slots * per_slot > budget) slots = budget / per_slot;
+        if (slots < 1) slots = 1;
+        if (g_ms_ws[sl] && g_ms_cap[sl] < slots * per_slot) {
+            SRT_HIPCHK(hipStreamSynchronize(st));
+            SRT_HIPCHK(hipFree(g_ms_ws[sl]));
+            g_ms_ws[sl] = NULL;
+            g_ms_cap[sl] = 0;
+        }
+        if (!g_ms_ws[sl]) {
+            if (hipMalloc((void**)&g_ms_ws[sl], slots * per_slot) != hipSuccess) {
+                (void)hipGetLastError();
+                g_ms_ws[sl] = NULL;
+                srt_set_error("msssp: workspace of %zu MiB failed", (slots * per_slot) >> 20);
+                return SRT_E_NOMEM;
+            }
+            g_ms_cap[sl] = slots * per_slot;
+        }
     }
+    if (slots * per_slot > g_ms_cap[sl]) slots = g_ms_cap[sl] / per_slot;
+    uint32_t* ws = g_ms_ws[sl];
     const uint32_t dl = delta < 1 ? 1u : delta;
     const size_t dyn = ms_lds_bytes(n);
     const char* penv = getenv("SRT_MSSSP_PROF");
@@ -448,21 +490,26 @@ int srt_msssp_rows(int n, int directed, const int2* orp, const uint2* ocw, const
         (void)hipGetLastError();
         prof = NULL;
     }
-#define SRT_MSSSP_LAUNCH(DIR, PR)                                                                \
+#define SRT_MSSSP_LAUNCH(DIR, PR, DT)                                                            \
     do {                                                                                         \
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)msssp_kernel<DIR, PR>,                        \
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)msssp_kernel<DIR, PR, DT>,                    \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));    \
-        msssp_kernel<DIR, PR><<<(unsigned)slots, MS_WG, dyn, st>>>(                               \
+        msssp_kernel<DIR, PR, DT><<<(unsigned)slots, MS_WG, dyn, st>>>(                           \
             n, orp, ocw, irp, icw, ir, inv, nbatch, bsrc, brow, lat, rel, ldo, ws, slot_words,    \
             dl, prof);                                                                            \
     } while (0)
-    if (directed && prof) SRT_MSSSP_LAUNCH(true, true);
-    else if (directed) SRT_MSSSP_LAUNCH(true, false);
-    else if (prof) SRT_MSSSP_LAUNCH(false, true);
-    else SRT_MSSSP_LAUNCH(false, false);
+#define SRT_MSSSP_LAUNCH2(DIR, PR)                                                               \
+    do {                                                                                         \
+        if (d16) SRT_MSSSP_LAUNCH(DIR, PR, uint16_t);                                             \
+        else SRT_MSSSP_LAUNCH(DIR, PR, uint32_t);                                                 \
+    } while (0)
+    if (directed && prof) SRT_MSSSP_LAUNCH2(true, true);
+    else if (directed) SRT_MSSSP_LAUNCH2(true, false);
+    else if (prof) SRT_MSSSP_LAUNCH2(false, true);
+    else SRT_MSSSP_LAUNCH2(false, false);
+#undef SRT_MSSSP_LAUNCH2
 #undef SRT_MSSSP_LAUNCH
     SRT_HIPCHK(hipGetLastError());
-    SRT_HIPCHK(hipFreeAsync(ws, st));
     if (prof) { /* per-batch means on stderr (a measurement aid, not part of the build) */
         const size_t words = (size_t)nbatch * MS_PROF;
         unsigned long long* h = (unsigned long long*)malloc(words * 8);
@@ -485,11 +532,11 @@ int srt_msssp_rows(int n, int directed, const int2* orp, const uint2* ocw, const
             }
             const double span = (double)(t_hi - t_lo) / 100.0;
             fprintf(stderr,
-                    "[msssp] %d batches, slots %zu, delta %u: per batch %.1f passes, %.0f pulls, "
+                    "[msssp] %d batches, slots %zu, delta %u, u%d: per batch %.1f passes, %.0f pulls, "
                     "%.1f advances; wave-0 kcycles: compaction %.0f, pulls %.0f, advance %.0f, "
                     "output %.0f, init %.0f; batch us mean %.0f, worst %.0f (batch %d: %llu passes,"
                     " %llu pulls); span %.0f us, mean concurrency %.1f\n",
-                    nbatch, slots, dl, m[0], m[1], m[2], m[3] / 1e3, m[4] / 1e3, m[5] / 1e3,
+                    nbatch, slots, dl, d16 ? 16 : 32, m[0], m[1], m[2], m[3] / 1e3, m[4] / 1e3, m[5] / 1e3,
                     m[6] / 1e3, m[7] / 1e3, busy / nbatch, worst, wb, h[(size_t)wb * MS_PROF],
                     h[(size_t)wb * MS_PROF + 1], span, span > 0 ? busy / span : 0.0);
         }

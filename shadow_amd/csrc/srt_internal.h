@@ -22,6 +22,9 @@ typedef struct srt_canon {
     int32_t directed;
     uint64_t quantum_ns;
     uint32_t max_w_q;
+    /* upper bound on every finite shortest distance, in quanta (graph.c: MST, (n - 1) max_w or
+     * the hop bound through the highest-degree vertex); < SRT_INF */
+    uint64_t dist_bound;
     /* CSR of canonical out-arcs (self-loops excluded), columns ascending */
     int64_t arcs;
     int32_t* rowptr;

@@ -91,6 +91,21 @@ def test_msssp_full_tables(gpu, monkeypatch, which):
     assert np.array_equal(rel.view(np.uint64), exp["rel"].view(np.uint64)), which
 
 
+@pytest.mark.parametrize("u16", ["0", "1"])
+def test_msssp_distance_widths(gpu, monkeypatch, u16):
+    """SRT_MSSSP_U16=0/1: 32-bit working distances, or 16-bit ones (the default when the graph's
+    distance bound is below 0xFFFF; candidates saturate one below the 16-bit INF), same tables."""
+    monkeypatch.setenv("SRT_SPARSE_MS", "1")
+    monkeypatch.setenv("SRT_MSSSP_U16", u16)
+    g = graphs.random_geometric(2200, seed=13)
+    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                algo=ALGO_SPARSE_SSSP)
+    assert st.dist_enc == 3
+    exp = oracle.table(_el(g), True, oracle.ORC_INT_NS, 8, raw=True)
+    assert np.array_equal(lat, exp["lat_int"])
+    assert np.array_equal(rel.view(np.uint64), exp["rel"].view(np.uint64))
+
+
 @pytest.mark.parametrize("delta", ["1", "3", "100000"])
 def test_msssp_bucket_widths(gpu, monkeypatch, delta):
     """SRT_MSSSP_DELTA: bucket width 1 (Dial-like), 3, and one bucket for everything (plain
@@ -120,47 +135,77 @@ def test_msssp_persistent_slots(gpu, monkeypatch, slots):
     assert np.array_equal(rel.view(np.uint64), exp["rel"].view(np.uint64))
 
 
-def test_msssp_c3_rows_and_ties(gpu):
-    """C3 itself (n = 20,000): AUTO picks the multi-source kernel; sampled row ranges, including
-    a partial last batch, are exact, and the tied-pair count equals the wave kernel's."""
+def _near(g_n, seed, x0, y0, k):
+    """The k vertices of random_geometric(g_n, seed) nearest (x0, y0): a compact source set."""
+    idx = np.arange(g_n, dtype=np.uint64)
+    x, y = graphs._rand01(seed, 4, idx), graphs._rand01(seed, 5, idx)
+    return np.argsort((x - x0) ** 2 + (y - y0) ** 2)[:k].astype(np.int32)
+
+
+def test_msssp_c3_compact_sources_and_ties(gpu):
+    """C3 itself (n = 20,000) with AUTO: a compact set of 300 sources (five batches, the last one
+    partial) takes the multi-source kernel and is exact, with the tied-pair count equal to the
+    wave kernel's on the same rows. A range of original ids is scattered across the square
+    (random positions): small batches within the batch budget, the single-source kernels with a
+    zero budget; both exact."""
+    import os
     import torch
     g = graphs.random_geometric(20000, seed=3)
     sg = SparseGraph(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
     el = _el(g)
-    for s0, s1 in [(0, 100), (9_950, 10_050), (19_963, 20_000)]:
-        st = BuildStats()
-        st.count_ties = 1
-        lat = torch.empty((s1 - s0, g.n), dtype=torch.int32, device="cuda")
-        rel = torch.empty((s1 - s0, g.n), dtype=torch.float64, device="cuda")
-        sg.rows(s0, s1, lat.data_ptr(), rel.data_ptr(), None, st)
+    srcs = _near(g.n, 3, 0.62, 0.41, 300)
+    ds = torch.from_numpy(srcs).cuda()
+    lat = torch.empty((len(srcs), g.n), dtype=torch.int32, device="cuda")
+    rel = torch.empty((len(srcs), g.n), dtype=torch.float64, device="cuda")
+    st = BuildStats()
+    st.count_ties = 1
+    sg.rows_list(ds.data_ptr(), len(srcs), lat.data_ptr(), rel.data_ptr(), None, st)
+    torch.cuda.synchronize()
+    assert st.dist_enc == 3, st.dist_enc
+    got = lat.cpu().numpy().view(np.uint32).astype(np.uint64) * np.uint64(sg.quantum_ns)
+    exp = oracle.sssp_list(el, srcs, nthreads=16)
+    off = np.arange(g.n)[None, :] != srcs[:, None]
+    assert np.array_equal(np.where(off, got, 0), np.where(off, exp["lat_int"], 0))
+    r = rel.cpu().numpy()
+    assert np.array_equal(r[off].view(np.uint64), exp["rel"][off].view(np.uint64))
+    os.environ["SRT_SPARSE_MS"] = "0"
+    try:
+        st1 = BuildStats()
+        st1.count_ties = 1
+        sg.rows_list(ds.data_ptr(), len(srcs), lat.data_ptr(), rel.data_ptr(), None, st1)
         torch.cuda.synchronize()
-        assert st.dist_enc == 3, st.dist_enc
-        got = lat.cpu().numpy().view(np.uint32).astype(np.uint64) * np.uint64(sg.quantum_ns)
-        exp = oracle.sssp_rows(el, s0, s1, nthreads=16)
-        off = np.arange(g.n)[None, :] != np.arange(s0, s1)[:, None]
-        assert np.array_equal(np.where(off, got, 0), np.where(off, exp["lat_int"], 0)), (s0, s1)
-        r = rel.cpu().numpy()
-        assert np.array_equal(r[off].view(np.uint64), exp["rel"][off].view(np.uint64)), (s0, s1)
-        tied_ms = st.tied_pairs
-        import os
-        os.environ["SRT_SPARSE_MS"] = "0"
+    finally:
+        del os.environ["SRT_SPARSE_MS"]
+    assert st1.dist_enc == 1 and st1.tied_pairs == st.tied_pairs, (st1.tied_pairs, st.tied_pairs)
+    # 100 original ids: random positions, so small clusters -- batches of their own within the
+    # batch budget, the single-source kernels without one
+    exp = oracle.sssp_rows(el, 0, 100, nthreads=16)
+    off = np.arange(g.n)[None, :] != np.arange(100)[:, None]
+    for maxb, enc in ((None, 3), ("0", 1)):
+        if maxb is not None:
+            os.environ["SRT_MSSSP_MAXB"] = maxb
         try:
-            st1 = BuildStats()
-            st1.count_ties = 1
-            sg.rows(s0, s1, lat.data_ptr(), rel.data_ptr(), None, st1)
+            st2 = BuildStats()
+            sg.rows(0, 100, lat.data_ptr(), rel.data_ptr(), None, st2)
             torch.cuda.synchronize()
         finally:
-            del os.environ["SRT_SPARSE_MS"]
-        assert st1.dist_enc == 1 and st1.tied_pairs == tied_ms, (st1.dist_enc, st1.tied_pairs, tied_ms)
+            os.environ.pop("SRT_MSSSP_MAXB", None)
+        assert st2.dist_enc == enc, (maxb, st2.dist_enc)
+        got = lat[:100].cpu().numpy().view(np.uint32).astype(np.uint64) * np.uint64(sg.quantum_ns)
+        assert np.array_equal(np.where(off, got, 0), np.where(off, exp["lat_int"], 0)), maxb
+        r = rel[:100].cpu().numpy()
+        assert np.array_equal(r[off].view(np.uint64), exp["rel"][off].view(np.uint64)), maxb
     sg.free()
 
 
 @pytest.mark.parametrize("which", ["rgg3000", "dring"])
 def test_msssp_source_list(gpu, monkeypatch, which):
     """srt_sparse_graph_rows_list with an unordered source list of 150 vertices (three batches,
-    the last one partial): row i is source srcs[i]."""
+    the last one partial; the hop radius lifted so the scattered sources still share batches):
+    row i is source srcs[i]."""
     import torch
     monkeypatch.setenv("SRT_SPARSE_MS", "1")
+    monkeypatch.setenv("SRT_MSSSP_RMAX", "100000")  # cluster even scattered sources
     g = _graph(which)
     rng = np.random.default_rng(77)
     srcs = rng.choice(g.n, 150, replace=False).astype(np.int32)
@@ -181,15 +226,19 @@ def test_msssp_source_list(gpu, monkeypatch, which):
     sg.free()
 
 
-@pytest.mark.parametrize("rmax", ["0", "24"])
-def test_msssp_compact_and_scattered_sources(gpu, monkeypatch, rmax):
+@pytest.mark.parametrize("rmax,maxb,enc", [("0", "0", 1), ("24", "4", 3), ("24", None, 3)])
+def test_msssp_compact_and_scattered_sources(gpu, monkeypatch, rmax, maxb, enc):
     """A source list mixing a compact region (the 200 vertices nearest a point of the unit
-    square) with 40 scattered vertices: compact clusters take the multi-source kernel, sources
-    that cannot fill a batch within the hop radius take the single-source kernels and are
-    scattered to their rows. SRT_MSSSP_RMAX=0 sends every source there."""
+    square) with 40 scattered vertices. Clusters that fill 48 lanes within the hop radius take the
+    multi-source kernel; the small ones do too while all batches fit the batch budget
+    (SRT_MSSSP_MAXB, default two per CU), else they take the single-source kernels and are
+    scattered to their rows: budget 4 splits the set, radius 0 with budget 0 sends every source
+    there (dist_enc 1)."""
     import torch
     monkeypatch.setenv("SRT_SPARSE_MS", "1")
     monkeypatch.setenv("SRT_MSSSP_RMAX", rmax)
+    if maxb is not None:
+        monkeypatch.setenv("SRT_MSSSP_MAXB", maxb)
     n = 4000
     g = graphs.random_geometric(n, seed=3)
     idx = np.arange(n, dtype=np.uint64)
@@ -205,7 +254,7 @@ def test_msssp_compact_and_scattered_sources(gpu, monkeypatch, rmax):
     st = BuildStats()
     sg.rows_list(ds.data_ptr(), len(srcs), lat.data_ptr(), rel.data_ptr(), None, st)
     torch.cuda.synchronize()
-    assert st.dist_enc == (1 if rmax == "0" else 3), st.dist_enc
+    assert st.dist_enc == enc, st.dist_enc
     got = lat.cpu().numpy().view(np.uint32).astype(np.uint64) * np.uint64(sg.quantum_ns)
     exp = oracle.sssp_list(_el(g), srcs, nthreads=16)
     off = np.arange(g.n)[None, :] != srcs[:, None]

@@ -19,7 +19,7 @@
 #define INF 0xFFFFFFFFu
 
 typedef struct {
-    int64_t pulls, passes, buckets, arcs;
+    int64_t pulls, passes, buckets, arcs, hub_arcs, hub_pulls;
 } sim_counts;
 
 int msssp_sim_batch(int n, const int32_t* irp, const int32_t* icol, const uint32_t* iw,
@@ -80,6 +80,10 @@ int msssp_sim_batch(int n, const int32_t* irp, const int32_t* icol, const uint32
                 const int v = C[i];
                 cand[v] = 0;
                 cnt->arcs += irp[v + 1] - irp[v];
+                if (irp[v + 1] - irp[v] > 64) {
+                    cnt->hub_arcs += irp[v + 1] - irp[v];
+                    cnt->hub_pulls++;
+                }
                 int changed = 0;
                 uint32_t mn = INF;
                 for (int l = 0; l < L; l++) {

@@ -21,7 +21,8 @@ SO = "/tmp/libmsssp_sim.so"
 
 class Counts(ctypes.Structure):
     _fields_ = [("pulls", ctypes.c_int64), ("passes", ctypes.c_int64),
-                ("buckets", ctypes.c_int64), ("arcs", ctypes.c_int64)]
+                ("buckets", ctypes.c_int64), ("arcs", ctypes.c_int64),
+                ("hub_arcs", ctypes.c_int64), ("hub_pulls", ctypes.c_int64)]
 
 
 def load():
@@ -116,7 +117,8 @@ def main():
         tp += c.pulls
         tq += c.passes
         line = (f"batch {ci}: pulls/n {c.pulls / n:.2f} passes {c.passes} buckets {c.buckets} "
-                f"arcs/arcs {c.arcs / len(icol):.2f}")
+                f"arcs/arcs {c.arcs / len(icol):.2f} (in-degree > 64: {c.hub_pulls} pulls, "
+                f"{c.hub_arcs / len(icol):.2f} arcs/arcs)")
         if a.check:
             import oracle
             e = oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
