@@ -478,9 +478,10 @@ def run_sparse(c: Ctx, wl):
         # multi-source kernel: the graph and each vertex's 64-lane working state are shared by
         # the 64 sources of a batch
         nb = (nsrc + 63) // 64
-        bytes_launch = float(nsrc * n * 12 + nb * (2 * n * 64 * 12 + (n + 1) * 8 + arcs * 16))
-        model = ("per 64-source batch: each vertex's 64-lane state (u32 D + f64 R) written and "
-                 "read once, the graph once ((n+1)*8 + arcs*16 B); per source its output row "
+        sd = 2 if form & 16 else 4  # 16-bit working distances (form bit 16)
+        bytes_launch = float(nsrc * n * 12 + nb * (2 * n * 64 * (sd + 8) + (n + 1) * 8 + arcs * 16))
+        model = (f"per 64-source batch: each vertex's 64-lane state (u{8 * sd} D + f64 R) written "
+                 "and read once, the graph once ((n+1)*8 + arcs*16 B); per source its output row "
                  "(n*12 B)")
         achieved_gbs = bytes_launch / (k_ms * 1e-3) / 1e9
     traffic = None

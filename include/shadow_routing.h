@@ -68,7 +68,8 @@ typedef struct srt_build_stats {
     int32_t fw_block;    /* dense: pivot-block edge used by FW; sparse: the kernel's form --
                           * wave kernel 1 = working row in LDS | 2 = private relabelled
                           * reliability row; workgroup kernel 4 | 1 = original vertex order
-                          * | 2 = compact 8-byte arcs */
+                          * | 2 = compact 8-byte arcs; multi-source kernel 8 | 16 = 16-bit
+                          * working distances */
     int64_t ess_arcs;    /* essential arcs found by the predecessor pass (dense) */
     double ms_total;     /* wall time of the device build (HIP events), excl. host copies */
     double ms_fw;        /* shortest-distance kernels */
@@ -77,7 +78,8 @@ typedef struct srt_build_stats {
     int32_t n_update;    /* FW update-kernel launches timed (time_kernels = 1) */
     double ms_update;    /* summed HIP-event duration of those launches */
     double ms_comm;      /* host-observed time of the collective calls (sharded builds) */
-    int32_t dist_enc;    /* sparse builds: 2 = workgroup-per-source kernel (LDS-packed rows),
+    int32_t dist_enc;    /* sparse builds: 3 = multi-source kernel (64 sources per workgroup),
+                          * 2 = workgroup-per-source kernel (LDS-packed rows),
                           * 1 = wave-per-source kernel, 0 = workgroup kernel for every source.
                           * Dense: the distance encoding the build finished with: 9 = 8 with
                           * 256-pivot rounds (SRT_FW_SH_KB=256), 8 = u16

@@ -118,6 +118,9 @@ struct srt_sparse_graph {
     uint8_t* ridx;
     uint2 *cw2, *icw2;
     double *r2, *ir2;
+    /* the relabelled in-arcs packed col | w << 24 for the multi-source kernel (max_w < 256,
+     * n < 2^24; 8 words of padding), else NULL */
+    uint32_t* ca2;
     /* host copy of the relabelled out-rows, for the multi-source kernel's source clusters */
     int2* h_rp2;
     uint2* h_cw2;
@@ -165,7 +168,7 @@ extern "C" void srt_sparse_graph_free(srt_sparse_graph* g) {
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(g->device);
     void* ps[] = {g->rp, g->col, g->w, g->r, g->sw, g->sr, g->cw, g->perm, g->inv, g->rp2, g->cw2, g->r2,
-                  g->rpo, g->rtab, g->ridx};
+                  g->rpo, g->rtab, g->ridx, g->ca2};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (g->directed) {
@@ -361,7 +364,19 @@ static int sparse_graph_from_canon(const srt_canon* c, int device, srt_sparse_gr
         rc = up((void**)&g->irp2, hrp, nv * sizeof(int2));
         if (!rc) rc = up((void**)&g->icw2, hcw, na * sizeof(uint2));
         if (!rc) rc = up((void**)&g->ir2, hr, na * 8);
-    } else if (!rc) {
+    }
+    /* packed in-arcs (hcw holds the relabelled in-arcs now: the out-arcs when undirected) */
+    if (!rc && g->max_w < 256 && c->n < (1 << 24)) {
+        uint32_t* pk = (uint32_t*)calloc(na + 8, sizeof(uint32_t));
+        if (!pk) {
+            rc = SRT_E_NOMEM;
+        } else {
+            for (size_t k = 0; k < na; k++) pk[k] = hcw[k].x | (hcw[k].y << 24);
+            rc = up((void**)&g->ca2, pk, (na + 8) * sizeof(uint32_t));
+            free(pk);
+        }
+    }
+    if (!rc && !c->directed) {
         g->irp2 = g->rp2;
         g->icw2 = g->cw2;
         g->ir2 = g->r2;
@@ -409,9 +424,9 @@ int srt_msssp_max_n(void);
 int srt_ms_scatter_rows(int nr, int n, const int32_t* rows, const uint32_t* tl, const double* tr,
                         uint32_t* lat, double* rel, size_t ldo, hipStream_t st);
 int srt_msssp_rows(int n, int directed, const int2* orp, const uint2* ocw, const int2* irp,
-                   const uint2* icw, const double* ir, const int32_t* inv, uint32_t delta,
-                   int nbatch, const int32_t* bsrc, const int32_t* brow, uint32_t* lat, double* rel,
-                   size_t ldo, int d16, hipStream_t st);
+                   const uint2* icw, const uint32_t* ica, const double* ir, const int32_t* inv,
+                   uint32_t delta, int nbatch, const int32_t* bsrc, const int32_t* brow,
+                   uint32_t* lat, double* rel, size_t ldo, int d16, hipStream_t st);
 
 /* Sweep order for the source clusters: breadth-first from a pseudo-peripheral vertex of each
  * component (the far end of a breadth-first search from the component's first vertex), so clusters
@@ -659,6 +674,7 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
      * row packed in LDS, once a probe source shows every distance fits its 10-bit fields
      * (d(a, b) <= 2 ecc(s0)); SRT_SPARSE_WG=0/1 disables / allows it at any size */
     int32_t* ms_dev = NULL; /* bsrc then brow, freed on the stream after the launch */
+    int ms_d16 = 0;
     if (ms) {
         const int nb = (int)(ms_bsrc.size() / 64);
         const size_t bb = ms_bsrc.size() * sizeof(int32_t);
@@ -673,8 +689,13 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
          * every row access); SRT_MSSSP_U16=0 keeps 32 */
         const char* uenv = getenv("SRT_MSSSP_U16");
         const int d16 = g->dist_bound < 0xFFFFull && !(uenv && atoi(uenv) == 0);
-        rc = srt_msssp_rows(g->n, g->directed, g->rp2, g->cw2, g->irp2, g->icw2, g->ir2, g->inv,
-                            delta, nb, ms_dev, ms_dev + ms_bsrc.size(), lat_rows, rel_rows,
+        ms_d16 = d16;
+        /* SRT_MSSSP_A32=1: arcs packed in one word (one lane read per arc instead of two, but
+         * a scalar split on the address chain: C3 26.4 vs 25.2 ms for the pairs, same box) */
+        const char* aenv = getenv("SRT_MSSSP_A32");
+        const uint32_t* ca = aenv && atoi(aenv) != 0 ? g->ca2 : NULL;
+        rc = srt_msssp_rows(g->n, g->directed, g->rp2, g->cw2, g->irp2, g->icw2, ca, g->ir2,
+                            g->inv, delta, nb, ms_dev, ms_dev + ms_bsrc.size(), lat_rows, rel_rows,
                             (size_t)g->n, d16, st);
         if (rc) return rc;
         SRT_HIPCHK(hipFreeAsync(ms_dev, st));
@@ -741,7 +762,8 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
                             g->perm, g->inv, g->max_w, g->local, b0, b0 + nsrc, srcs, lat_rows,
                             rel_rows, ovf, st);
     if (rc) return rc;
-    const int form = ms ? 8 : srt_sparse_last_form();
+    /* the multi-source kernel's form: 8, | 16 with 16-bit working distances */
+    const int form = ms ? 8 | (ms_d16 ? 16 : 0) : srt_sparse_last_form();
     SRT_HIPCHK(hipEventRecord(e1, st));
     rc = srt_sparse_diag(g->n, b0, b0 + nsrc, srcs, g->rp, g->col, g->w, g->r, g->sw, g->sr,
                          lat_rows, rel_rows, (size_t)g->n, st);

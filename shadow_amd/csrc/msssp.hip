@@ -40,6 +40,8 @@
  * loaded). Output: the rows are transposed into lat[row][t] / rel[row][t] in original vertex
  * order with coalesced stores.
  */
+#include <type_traits>
+
 #include "srt_device.h"
 
 #define MS_L 64     /* sources per batch (lanes) */
@@ -116,10 +118,11 @@ static __device__ __forceinline__ void ms_compact(uint32_t* bm, int nw, int* lis
  * for undirected graphs); inv[original] = relabelled; bsrc / brow: per batch and lane the
  * relabelled source and the output row (-1 = empty lane); ws: per slot D (n x 64 u32), R (n x 64
  * f64) and the lane minimum of every vertex (n u32). */
-template <bool DIRECTED, bool PROF, typename DT>
+template <bool DIRECTED, bool PROF, typename DT, bool A32>
 __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
     int n, const int2* __restrict__ orp, const uint2* __restrict__ ocw,
-    const int2* __restrict__ irp, const uint2* __restrict__ icw, const double* __restrict__ ir,
+    const int2* __restrict__ irp, const uint2* __restrict__ icw, const uint32_t* __restrict__ ica,
+    const double* __restrict__ ir,
     const int32_t* __restrict__ inv, int nbatch, const int32_t* __restrict__ bsrc,
     const int32_t* __restrict__ brow, uint32_t* __restrict__ lat, double* __restrict__ rel,
     size_t ldo, uint32_t* __restrict__ ws, size_t slot_words, uint32_t delta,
@@ -205,17 +208,50 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                  * distance loads share round trips: lane j < MS_G loads candidate j's in-row,
                  * lanes j * MS_AC + a its arcs a, a + MS_AC, ..., and the 64-lane distance rows
                  * of MS_G x MS_AK arcs are loaded back to back */
-                for (int g0 = wave * MS_G; g0 < cnt; g0 += MS_NWAVE * MS_G) {
+                /* this lane's arc slot: candidate lane / MS_AC, arc lane % MS_AC of a chunk */
+                const int aj = lane / MS_AC, aa = lane % MS_AC;
+                /* software pipeline: the next group's list entries, in-rows and first arc chunk
+                 * are loaded while this group's distance rows are in flight, so a group's chain
+                 * is its distance rows, then its reliability gathers */
+                constexpr int GS = MS_NWAVE * MS_G;
+                /* a lane's arc of a chunk: A32 one word col | w << 24, else the (col, w) pair */
+                using arc_t = typename std::conditional<A32, uint32_t, uint2>::type;
+                auto arc_at = [&](int k) -> arc_t {
+                    if constexpr (A32) return ica[k];
+                    else return icw[k];
+                };
+                auto arc_none = []() -> arc_t {
+                    if constexpr (A32) return 0u;
+                    else return make_uint2(0u, 0u);
+                };
+                int vl_n = 0;
+                int2 bel_n = make_int2(0, 0);
+                arc_t ea_n = arc_none();
+                {
+                    const int g1 = wave * MS_G;
+                    if (g1 < cnt && lane < min(MS_G, cnt - g1)) {
+                        vl_n = s_list[g1 + lane];
+                        bel_n = irp[vl_n];
+                    }
+                    const int bx1 = __shfl(bel_n.x, aj), dg1 = __shfl(bel_n.y, aj) - bx1;
+                    if (aa < dg1) ea_n = arc_at(bx1 + aa);
+                }
+                for (int g0 = wave * MS_G; g0 < cnt; g0 += GS) {
                     const int ng = min(MS_G, cnt - g0);
-                    int vl = 0;
-                    int2 bel = make_int2(0, 0);
-                    if (lane < ng) {
-                        vl = s_list[g0 + lane];
-                        bel = irp[vl];
+                    const int vl = vl_n;
+                    const int2 bel = bel_n;
+                    const arc_t ea0 = ea_n;
+                    {
+                        const int g1 = g0 + GS;
+                        vl_n = 0;
+                        bel_n = make_int2(0, 0);
+                        if (g1 < cnt && lane < min(MS_G, cnt - g1)) {
+                            vl_n = s_list[g1 + lane];
+                            bel_n = irp[vl_n];
+                        }
                     }
                     uint32_t v[MS_G], od[MS_G];
                     int bx[MS_G], dg[MS_G];
-                    double orl[MS_G];
                     int maxdeg = 0;
 #pragma unroll
                     for (int j = 0; j < MS_G; j++) {
@@ -224,10 +260,7 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                         dg[j] = j < ng ? __builtin_amdgcn_readlane(bel.y, j) - bx[j] : 0;
                         maxdeg = max(maxdeg, dg[j]);
                         od[j] = ms_ld(D + (size_t)v[j] * MS_L + lane);
-                        orl[j] = ms_ld(R + (size_t)v[j] * MS_L + lane);
                     }
-                    /* this lane's arc slot: candidate lane / MS_AC, arc lane % MS_AC of a chunk */
-                    const int aj = lane / MS_AC, aa = lane % MS_AC;
                     const int abx = __shfl(bel.x, aj), adg = aj < ng ? __shfl(bel.y, aj) - abx : 0;
                     uint32_t bc[MS_G], bdu[MS_G], bu[MS_G];
                     int bk[MS_G];
@@ -238,9 +271,21 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                         bu[j] = 0u;
                         bk[j] = -1;
                     }
-                    uint2 ea = make_uint2(0u, 0u);
+                    /* the arc in slot j * MS_AC + h of the chunk: its column and weight, as
+                     * wave-uniform values (one lane read, the split is scalar) */
+                    auto arc_of = [&](const arc_t& e, int slot, uint32_t& col, uint32_t& w) {
+                        if constexpr (A32) {
+                            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)e, slot);
+                            col = x & 0xFFFFFFu;
+                            w = x >> 24;
+                        } else {
+                            col = (uint32_t)__builtin_amdgcn_readlane((int)e.x, slot);
+                            w = (uint32_t)__builtin_amdgcn_readlane((int)e.y, slot);
+                        }
+                    };
+                    arc_t ea = ea0;
                     for (int c0 = 0; c0 < maxdeg; c0 += MS_AC) {
-                        ea = aa + c0 < adg ? icw[abx + c0 + aa] : make_uint2(0u, 0u);
+                        if (c0 > 0) ea = aa + c0 < adg ? arc_at(abx + c0 + aa) : arc_none();
 #pragma unroll
                         for (int h = 0; h < MS_AC; h += MS_AK) {
                             if (c0 + h >= maxdeg) break;
@@ -249,8 +294,8 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                             for (int j = 0; j < MS_G; j++)
 #pragma unroll
                                 for (int a = 0; a < MS_AK; a++) {
-                                    const uint32_t col =
-                                        (uint32_t)__builtin_amdgcn_readlane((int)ea.x, j * MS_AC + h + a);
+                                    uint32_t col, w;
+                                    arc_of(ea, j * MS_AC + h + a, col, w);
                                     du[j][a] = ms_ld(D + (size_t)col * MS_L + lane);
                                 }
 #pragma unroll
@@ -259,10 +304,8 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                                 for (int a = 0; a < MS_AK; a++) {
                                     const int k = c0 + h + a;
                                     if (k >= dg[j] || du[j][a] >= DINF) continue;
-                                    const uint32_t col =
-                                        (uint32_t)__builtin_amdgcn_readlane((int)ea.x, j * MS_AC + h + a);
-                                    const uint32_t w =
-                                        (uint32_t)__builtin_amdgcn_readlane((int)ea.y, j * MS_AC + h + a);
+                                    uint32_t col, w;
+                                    arc_of(ea, j * MS_AC + h + a, col, w);
                                     const uint32_t c =
                                         sizeof(DT) == 2 ? min(du[j][a] + w, DINF - 1u) : du[j][a] + w;
                                     if (c < bc[j] || (c == bc[j] && du[j][a] < bdu[j])) {
@@ -274,10 +317,16 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                                 }
                         }
                     }
+                    {   /* the next group's first arc chunk (its in-rows arrived meanwhile) */
+                        const int bx1 = __shfl(bel_n.x, aj), dg1 = __shfl(bel_n.y, aj) - bx1;
+                        ea_n = aa < dg1 ? arc_at(bx1 + aa) : arc_none();
+                    }
                     uint32_t nd[MS_G];
-                    double nr[MS_G];
+                    double nr[MS_G], orl[MS_G];
 #pragma unroll
                     for (int j = 0; j < MS_G; j++) {
+                        /* the old reliability rides with the predecessor gathers */
+                        orl[j] = ms_ld(R + (size_t)v[j] * MS_L + lane);
                         nd[j] = DINF;
                         nr[j] = 0.0;
                         if ((int)v[j] == mysrc) {
@@ -308,7 +357,10 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                                 const int2 ob = orp[vj];
                                 for (int k = ob.x + lane; k < ob.y; k += MS_L) ms_set(nxt, ocw[k].x);
                             } else if (maxdeg <= MS_AC) { /* the arcs of the (only) chunk */
-                                if (aj == j && aa < dg[j]) ms_set(nxt, ea.x);
+                                if (aj == j && aa < dg[j]) {
+                                    if constexpr (A32) ms_set(nxt, ea & 0xFFFFFFu);
+                                    else ms_set(nxt, ea.x);
+                                }
                             } else {
                                 for (int k = bx[j] + lane; k < bx[j] + dg[j]; k += MS_L)
                                     ms_set(nxt, icw[k].x);
@@ -435,9 +487,9 @@ static uint32_t* g_ms_ws[SRT_STATE_SLOTS];
 static size_t g_ms_cap[SRT_STATE_SLOTS];
 
 int srt_msssp_rows(int n, int directed, const int2* orp, const uint2* ocw, const int2* irp,
-                   const uint2* icw, const double* ir, const int32_t* inv, uint32_t delta,
-                   int nbatch, const int32_t* bsrc, const int32_t* brow, uint32_t* lat, double* rel,
-                   size_t ldo, int d16, hipStream_t st) {
+                   const uint2* icw, const uint32_t* ica, const double* ir, const int32_t* inv,
+                   uint32_t delta, int nbatch, const int32_t* bsrc, const int32_t* brow,
+                   uint32_t* lat, double* rel, size_t ldo, int d16, hipStream_t st) {
     if (n > srt_msssp_max_n()) {
         srt_set_error("msssp: %d vertices exceed the LDS bitmaps (%d)", n, srt_msssp_max_n());
         return SRT_E_ARG;
@@ -490,18 +542,20 @@ int srt_msssp_rows(int n, int directed, const int2* orp, const uint2* ocw, const
         (void)hipGetLastError();
         prof = NULL;
     }
-#define SRT_MSSSP_LAUNCH(DIR, PR, DT)                                                            \
+#define SRT_MSSSP_LAUNCH(DIR, PR, DT, A)                                                         \
     do {                                                                                         \
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)msssp_kernel<DIR, PR, DT>,                    \
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)msssp_kernel<DIR, PR, DT, A>,                 \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));    \
-        msssp_kernel<DIR, PR, DT><<<(unsigned)slots, MS_WG, dyn, st>>>(                           \
-            n, orp, ocw, irp, icw, ir, inv, nbatch, bsrc, brow, lat, rel, ldo, ws, slot_words,    \
-            dl, prof);                                                                            \
+        msssp_kernel<DIR, PR, DT, A><<<(unsigned)slots, MS_WG, dyn, st>>>(                        \
+            n, orp, ocw, irp, icw, ica, ir, inv, nbatch, bsrc, brow, lat, rel, ldo, ws,           \
+            slot_words, dl, prof);                                                                \
     } while (0)
 #define SRT_MSSSP_LAUNCH2(DIR, PR)                                                               \
     do {                                                                                         \
-        if (d16) SRT_MSSSP_LAUNCH(DIR, PR, uint16_t);                                             \
-        else SRT_MSSSP_LAUNCH(DIR, PR, uint32_t);                                                 \
+        if (d16 && ica) SRT_MSSSP_LAUNCH(DIR, PR, uint16_t, true);                                \
+        else if (d16) SRT_MSSSP_LAUNCH(DIR, PR, uint16_t, false);                                 \
+        else if (ica) SRT_MSSSP_LAUNCH(DIR, PR, uint32_t, true);                                  \
+        else SRT_MSSSP_LAUNCH(DIR, PR, uint32_t, false);                                          \
     } while (0)
     if (directed && prof) SRT_MSSSP_LAUNCH2(true, true);
     else if (directed) SRT_MSSSP_LAUNCH2(true, false);

@@ -91,12 +91,16 @@ def test_msssp_full_tables(gpu, monkeypatch, which):
     assert np.array_equal(rel.view(np.uint64), exp["rel"].view(np.uint64)), which
 
 
+@pytest.mark.parametrize("a32", ["0", "1"])
 @pytest.mark.parametrize("u16", ["0", "1"])
-def test_msssp_distance_widths(gpu, monkeypatch, u16):
+def test_msssp_distance_widths(gpu, monkeypatch, u16, a32):
     """SRT_MSSSP_U16=0/1: 32-bit working distances, or 16-bit ones (the default when the graph's
-    distance bound is below 0xFFFF; candidates saturate one below the 16-bit INF), same tables."""
+    distance bound is below 0xFFFF; a candidate past it reads as not reached yet), and
+    SRT_MSSSP_A32=0/1: (col, w) pair arcs or col | w << 24 words (the default when every weight is
+    below 256), all four forms give the same tables."""
     monkeypatch.setenv("SRT_SPARSE_MS", "1")
     monkeypatch.setenv("SRT_MSSSP_U16", u16)
+    monkeypatch.setenv("SRT_MSSSP_A32", a32)
     g = graphs.random_geometric(2200, seed=13)
     lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
                                 algo=ALGO_SPARSE_SSSP)
