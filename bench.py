@@ -355,8 +355,8 @@ def run_dense(c: Ctx, wl):
         "traffic": traffic, "bytes_per_launch": bytes_per_round,
         "avg_launch_ms": round(avg_upd_ms, 4), "launches_timed": n_upd,
         "model": f"2*elements*{s_d} B per timed unit (SURVEY §8d round-streaming, "
-                 f"{ {7: 'B=256 (four 64-pivot panels per C-tile residency)', 6: 'B=128 (two 64-pivot panels per C-tile residency)', 8: 'B=128 (two 64-pivot panels per C-tile residency)', 9: 'B=256 (four 64-pivot panels per C-tile residency)'}.get(enc, 'B=64')}, "
-                 f"{ {9: 'u16 f16-compare, row-sharded kept tiles, 256-pivot rounds (unit: one round, first start to last end)', 8: 'u16 f16-compare, row-sharded kept tiles, 128-pivot rounds (unit: one round, first start to last end)', 7: 'u16 f16-compare, upper triangle on two streams, 256-pivot rounds (unit: both rest launches)', 6: 'u16 f16-compare, upper triangle on two streams, 128-pivot rounds (unit: both rest launches)', 5: 'u16 f16-compare, upper triangle on two streams (unit: both rest launches)', 4: 'u16 f16-compare, upper triangle', 3: 'u16 f16-compare', 2: 'u16 pk_min', 1: 'u32'}[enc]}"
+                 f"{ {7: 'B=256 (four 64-pivot panels per C-tile residency)', 6: 'B=128 (two 64-pivot panels per C-tile residency)', 8: 'B=128 (two 64-pivot panels per C-tile residency)', 9: 'B=256 (four 64-pivot panels per C-tile residency)', 11: f'B=256 (one 256-pivot block per C-tile residency; a squaring applies all {ld} pivots)'}.get(enc, 'B=64')}, "
+                 f"{ {9: 'u16 f16-compare, row-sharded kept tiles, 256-pivot rounds (unit: one round, first start to last end)', 8: 'u16 f16-compare, row-sharded kept tiles, 128-pivot rounds (unit: one round, first start to last end)', 7: 'u16 f16-compare, upper triangle on two streams, 256-pivot rounds (unit: both rest launches)', 6: 'u16 f16-compare, upper triangle on two streams, 128-pivot rounds (unit: both rest launches)', 5: 'u16 f16-compare, upper triangle on two streams (unit: both rest launches)', 4: 'u16 f16-compare, upper triangle', 3: 'u16 f16-compare', 2: 'u16 pk_min', 1: 'u32', 11: 'u16 f16-compare, min-plus squaring split over 256-pivot blocks (unit: one squaring, all its launches)'}[enc]}"
                  f" distances; elements updated per unit = {int(elems)}, "
                  f"pivots per element = {pivots:.2f})",
         "algorithmic_min_bytes": float(nr) * ld * (4 + 8),
