@@ -273,7 +273,7 @@ def run_dense(c: Ctx, wl):
     w4 = os.environ.get("SRT_FW_WAVES") == "4"
     uk = "fwh_update_kernel" if w4 else "fwq_update_kernel"
     st2 = "" if w4 else ", 2"  # fwq's third template argument: 32-pivot stages per tile
-    kname = {11: "fwq_update_kernel<false, 0, 8>", 9: "fwq_update_kernel<true, 4, 8>", 8: "fwq_update_kernel<true, 4, 4>", 7: "fwq_update_kernel<true, 4, 8>", 6: "fwq_update_kernel<true, 4, 4>", 5: f"{uk}<true, 4{st2}>",
+    kname = {11: "fwq_update_kernel<false, 20, 8>", 9: "fwq_update_kernel<true, 4, 8>", 8: "fwq_update_kernel<true, 4, 4>", 7: "fwq_update_kernel<true, 4, 8>", 6: "fwq_update_kernel<true, 4, 4>", 5: f"{uk}<true, 4{st2}>",
              4: f"{uk}<true, 0{st2}>" if world == 1 else f"{uk}<true, 4{st2}>",
              3: f"{uk}<false, 0{st2}>",
              2: "fw16_update_kernel<false>", 1: "fw_update_kernel"}[enc]

@@ -556,6 +556,7 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
         return SRT_E_ARG;
     }
     const int nsrc = src_end - src_begin;
+    (void)srt_state_slot(); /* also keeps the device's scratch pool mapped (comm.hip) */
     /* source i of this call: srcs + i, or the range */
     auto one = [&](int i) { return srcs ? srcs + i : (const int32_t*)NULL; };
     const int b0 = srcs ? 0 : src_begin;

@@ -1129,10 +1129,20 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         /* 1024 threads per row, one row per CU (128 VGPRs): 12.3 ms on C4 against 13.3 for 512
          * threads at two rows per CU and 13.1 for 1024 at two (64 VGPRs, 4 targets in flight) */
         if (n <= 32768) {
-            SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 32768>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
-            rel_levels_kernel<1024, 32768><<<lrows, 1024, 65536, st>>>(n, ld, row0, d, pred, rel, 64,
-                                                                     ws->depth, ws->cursor);
+            /* small rows take small workgroups (C2, n = 1,000: 256 threads of 4 entries, four
+             * rows per CU, instead of 1,024 threads that scan 32 mostly empty entries per level) */
+            if (n <= 1024)
+                rel_levels_kernel<256, 1024><<<lrows, 256, 2048, st>>>(n, ld, row0, d, pred, rel, 64,
+                                                                      ws->depth, ws->cursor);
+            else if (n <= 4096)
+                rel_levels_kernel<512, 4096><<<lrows, 512, 8192, st>>>(n, ld, row0, d, pred, rel, 64,
+                                                                      ws->depth, ws->cursor);
+            else {
+                SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 32768>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
+                rel_levels_kernel<1024, 32768><<<lrows, 1024, 65536, st>>>(
+                    n, ld, row0, d, pred, rel, 64, ws->depth, ws->cursor);
+            }
             const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
             SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

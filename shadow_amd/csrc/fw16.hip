@@ -2560,14 +2560,18 @@ static __device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
     return min(a & 0xFFFFu, b & 0xFFFFu) | (min(a >> 16, b >> 16) << 16);
 }
 
-/* D = min over q < nq of the split-k partials (each already <= D); flag: any entry changed */
+/* D = min over q < nq of the split-k partials (each already <= D); flag: any entry changed.
+ * NQ > 0: the partial count is a compile-time constant and all loads issue together */
+template <int NQ>
 __global__ void sq_reduce_kernel(size_t count, int nq, const u16* __restrict__ part,
                                  u16* __restrict__ d, int* __restrict__ flag) {
+    if (NQ > 0) nq = NQ;
     bool ch = false;
     for (size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < count;
          i += (size_t)gridDim.x * blockDim.x * 8) {
         uint4 m = *reinterpret_cast<const uint4*>(part + i);
-        for (int q = 1; q < nq; ++q) {
+#pragma unroll
+        for (int q = 1; q < (NQ > 0 ? NQ : nq); ++q) {
             const uint4 x = *reinterpret_cast<const uint4*>(part + (size_t)q * count + i);
             m.x = pk_min_u16(m.x, x.x);
             m.y = pk_min_u16(m.y, x.y);
@@ -2580,7 +2584,9 @@ __global__ void sq_reduce_kernel(size_t count, int nq, const u16* __restrict__ p
             ch = true;
         }
     }
-    if (__ballot(ch) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+    /* one flag write per workgroup: same-address atomics serialise in L2 (one per wave over
+     * 2048 waves cost 12 us of a 20 us pass at C2) */
+    if (__syncthreads_or(ch) && threadIdx.x == 0) atomicOr(flag, 1);
 }
 
 static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStream_t st,
@@ -2612,6 +2618,7 @@ static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStrea
     const char* sp_env = getenv("SRT_FW_SQUARE_SPLIT");
     const bool split = !(sp_env && atoi(sp_env) == 0);
     const int nq8 = ld / 256, tail = (ld % 256) ? 1 : 0;
+    int* sflag = reinterpret_cast<int*>(dsum); /* four change flags (dsum holds 16 bytes) */
     u16* part = nullptr;
     if (split) SRT_HIPCHK(hipMallocAsync((void**)&part, (size_t)(nq8 + tail) * ld * ld * 2, st));
     struct freer2 {
@@ -2633,8 +2640,15 @@ static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStrea
             if (tail)
                 fwq_update_kernel<false, 20, 4><<<(unsigned)(T * T), 512, 0, st>>>(
                     d, ld, d, nq8 * 256, T, 0, 0, nullptr, 0, -1, part + (size_t)nq8 * ld * ld);
-            SRT_HIPCHK(hipMemsetAsync(flags, 0, sizeof(int), st));
-            sq_reduce_kernel<<<256, 256, 0, st>>>((size_t)ld * ld, nq8 + tail, part, d, flags);
+            if (!(it & 3)) SRT_HIPCHK(hipMemsetAsync(sflag, 0, 4 * sizeof(int), st));
+            const size_t cnt = (size_t)ld * ld;
+            static const char* rg_env = getenv("SRT_SQ_REDUCE_BLOCKS");
+            const unsigned rg = rg_env ? (unsigned)std::max(1, atoi(rg_env))
+                                       : (unsigned)std::min<size_t>(256, srt_ceil_div((long long)(cnt / 8), 256));
+            if (nq8 + tail == 4)
+                sq_reduce_kernel<4><<<rg, 256, 0, st>>>(cnt, 4, part, d, sflag + (it & 3));
+            else
+                sq_reduce_kernel<0><<<rg, 256, 0, st>>>(cnt, nq8 + tail, part, d, sflag + (it & 3));
         } else {
             for (int k0 = 0; k0 < ld; k0 += 256) {
                 if (k0 + 256 <= ld)
@@ -2651,10 +2665,14 @@ static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStrea
         }
         SRT_HIPCHK(hipGetLastError());
         if (split) {
-            int ch = 0;
-            SRT_HIPCHK(hipMemcpyAsync(&ch, flags, sizeof(int), hipMemcpyDeviceToHost, st));
+            /* the change flags are read every fourth pass (one host round trip per four
+             * passes; complete graphs converge in 3-4): a pass after the fixed point changes
+             * nothing and costs only its time */
+            if ((it & 3) != 3) continue;
+            int ch[4] = {0, 0, 0, 0};
+            SRT_HIPCHK(hipMemcpyAsync(ch, sflag, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
             SRT_HIPCHK(hipStreamSynchronize(st));
-            if (!ch) break;
+            if (!ch[0] || !ch[1] || !ch[2] || !ch[3]) break;
             continue;
         }
         SRT_HIPCHK(hipMemsetAsync(dsum, 0, sizeof(unsigned long long), st));
