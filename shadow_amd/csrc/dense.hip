@@ -705,6 +705,118 @@ __global__ __launch_bounds__(256) void pred_cols2_kernel(int n, int row0, int nl
     if (TIES) add_ties(ties, nties);
 }
 
+/* Byte distances without the tie count: the canonical predecessor as ONE 32-bit minimum per arc
+ * and source. Every distance fits a byte (<= 254) and the arcs come with A = (w' << 23) | id,
+ * w' = min(w, 257), id = the arc's rank in t's list (sorted lists) or its tail (n <= 32,768, so
+ * both fit 15 bits), and the row offset u * 128 (pack_uk_kernel). The key
+ *   key = ((D[s][u] + w') << 23) | (D[s][u] << 15) | id = D[s][u] * (2^23 + 2^15) + A
+ * is one v_mad_u32_u24, and its minimum over t's in-arcs orders first by D[s][u] + w -- the
+ * smallest is D[s][t] exactly when some arc lies on a shortest path, which the winner is checked
+ * for -- then by (D[s][u], id): pred_cols2_kernel's (D[s][u], rank) rule among the arcs with
+ * D[s][u] + w = D[s][t], without its per-arc compare and select (12 -> 5 VALU per arc and wave). */
+__global__ void pack_uk_kernel(int n, const int32_t* __restrict__ iptr, const int32_t* __restrict__ col,
+                               const uint32_t* __restrict__ w, int sorted, uint2* __restrict__ uk) {
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= n) return;
+    const int kb = iptr[t], ke = iptr[t + 1];
+    for (int k = kb + (threadIdx.x & 63); k < ke; k += 64) {
+        const uint32_t u = (uint32_t)col[k];
+        const uint32_t id = sorted ? (uint32_t)(k - kb) : u;
+        uk[k] = make_uint2(u << 7, (min(w[k], 257u) << 23) | id);
+    }
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void pred_cols3_kernel(int n, int row0, int nloc, int ldT,
+                                                         size_t bsD, const uint8_t* __restrict__ DT,
+                                                         const int32_t* __restrict__ iptr,
+                                                         const uint2* __restrict__ uk,
+                                                         const double* __restrict__ ar,
+                                                         int32_t* __restrict__ predT,
+                                                         double* __restrict__ rT, int nsb, int tch,
+                                                         int tper, int sorted) {
+    const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
+    const int sb = (j / tch) * 8 + xcd, tc = j % tch;
+    if (sb >= nsb) return;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int sl = sb * 128 + 2 * lane;
+    const int s = row0 + sl;
+    const bool v0 = sl < nloc && s < n, v1 = sl + 1 < nloc && s + 1 < n;
+    const int t1 = min(n, (tc + 1) * tper);
+    const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(DT) + (size_t)sb * bsD, 0, (int)bsD, 0x00020000);
+    const int voff = 2 * lane;
+    /* the multiplier in a VGPR: v_mad_u32_u24 then reads one scalar operand (the arc's A), not
+     * a literal and an SGPR, which would cost a v_mov per arc */
+    uint32_t KM;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(KM) : "i"((1u << 23) + (1u << 15)));
+#define SRT_DB3(off) ((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(slab, voff, (int)(off), 0))
+    for (int t = tc * tper + wv; t < t1; t += 4) {
+        const uint32_t dst = SRT_DB3(t * 128);
+        const uint32_t dst0 = dst & 0xFFu, dst1 = dst >> 8;
+        const int kb = __builtin_amdgcn_readfirstlane(iptr[t]);
+        const int ke = __builtin_amdgcn_readfirstlane(iptr[t + 1]);
+        uint32_t best0 = 0xFFFFFFFFu, best1 = 0xFFFFFFFFu;
+        int k = kb;
+        for (; k + U <= ke; k += U) {
+            uint2 a[U];
+            uint32_t dd[U];
+#pragma unroll
+            for (int q = 0; q < U; ++q) a[q] = uk[k + q];
+#pragma unroll
+            for (int q = 0; q < U; ++q) dd[q] = SRT_DB3(a[q].x);
+#pragma unroll
+            for (int q = 0; q < U; q += 2) {
+                best0 = min(best0, min(__umul24(dd[q] & 0xFFu, KM) + a[q].y,
+                                       __umul24(dd[q + 1] & 0xFFu, KM) + a[q + 1].y));
+                best1 = min(best1, min(__umul24(dd[q] >> 8, KM) + a[q].y,
+                                       __umul24(dd[q + 1] >> 8, KM) + a[q + 1].y));
+            }
+        }
+        for (; k < ke; ++k) {
+            const uint2 a0 = uk[k];
+            const uint32_t d0 = SRT_DB3(a0.x);
+            best0 = min(best0, __umul24(d0 & 0xFFu, KM) + a0.y);
+            best1 = min(best1, __umul24(d0 >> 8, KM) + a0.y);
+        }
+        /* the winner lies on a shortest path iff its D[s][u] + w is D[s][t] */
+        int bk0 = -1, bk1 = -1;
+        const bool w0 = best0 != 0xFFFFFFFFu && (best0 >> 23) == dst0;
+        const bool w1 = best1 != 0xFFFFFFFFu && (best1 >> 23) == dst1;
+        if (sorted) {
+            if (w0) bk0 = kb + (int)(best0 & 0x7FFFu);
+            if (w1) bk1 = kb + (int)(best1 & 0x7FFFu);
+        } else {
+            const uint32_t u0 = w0 ? ((best0 & 0x7FFFu) << 7) : 0xFFFFFFFFu;
+            const uint32_t u1 = w1 ? ((best1 & 0x7FFFu) << 7) : 0xFFFFFFFFu;
+            for (int q = kb; q < ke; ++q) {
+                const uint32_t u = uk[q].x;
+                bk0 = (u == u0) ? q : bk0;
+                bk1 = (u == u1) ? q : bk1;
+            }
+        }
+        const size_t o = (size_t)t * ldT + sl;
+        const bool h0 = s != t && bk0 >= 0, h1 = s + 1 != t && bk1 >= 0;
+        if (v0 && v1 && (o & 1) == 0) {
+            *reinterpret_cast<int2*>(predT + o) =
+                make_int2(h0 ? (int32_t)(uk[bk0].x >> 7) : -1, h1 ? (int32_t)(uk[bk1].x >> 7) : -1);
+            rT[o] = h0 ? ar[bk0] : 0.0;
+            rT[o + 1] = h1 ? ar[bk1] : 0.0;
+        } else {
+            if (v0) {
+                predT[o] = h0 ? (int32_t)(uk[bk0].x >> 7) : -1;
+                rT[o] = h0 ? ar[bk0] : 0.0;
+            }
+            if (v1) {
+                predT[o + 1] = h1 ? (int32_t)(uk[bk1].x >> 7) : -1;
+                rT[o + 1] = h1 ? ar[bk1] : 0.0;
+            }
+        }
+    }
+#undef SRT_DB3
+}
+
 /* Path-order reliability by sweeps for rows with a large distance range (rel_levels_kernel
  * flagged them), one workgroup per row, same in-place (u, r) input. A target resolves once its
  * predecessor resolved in an earlier sweep (double-buffered LDS bitmaps; the sweeps = the depth
@@ -1061,7 +1173,14 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         ws->predt_cap = c2;
         if ((rc = ws_grow((void**)&ws->uw, &c3, (size_t)total + 1, sizeof(uint2)))) return rc;
         ws->uw_cap = c3;
-        if (total > 0)
+        /* byte distances without the tie count take the one-minimum form (pred_cols3_kernel;
+         * SRT_PRED_KEY=0: pred_cols2_kernel) */
+        static const char* pk_env = getenv("SRT_PRED_KEY");
+        const bool key3 = d16 && srt_fw16_small() && !ties && n <= 32768 &&
+                          !(pk_env && atoi(pk_env) == 0);
+        if (total > 0 && key3)
+            pack_uk_kernel<<<srt_ceil_div(n, 4), 256, 0, st>>>(n, iptr, icol, iw, !directed, ws->uw);
+        else if (total > 0)
             pack_uw_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, icol, iw, ws->uw);
         /* DT[u][sl] = D[row0 + sl][u], from the u16 working matrix when the build kept one
          * (half the bytes per candidate arc: the predecessor search is bound by these reads).
@@ -1084,7 +1203,11 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
                                                      256, 0, st>>>(nrows, ld, d16, (size_t)ld, dt8,
                                                                    (size_t)ld * 128);
             /* 16 candidate arcs in flight per step: 17.3 ms on C4 against 18.7 (8) and 20.0 (32) */
-            if (ties)
+            if (key3)
+                pred_cols3_kernel<16><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
+                    n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
+                    nsb2, tch, tper, !directed);
+            else if (ties)
                 pred_cols2_kernel<16, true><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
                     n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
                     nsb2, tch, tper, !directed, ws->ties);
