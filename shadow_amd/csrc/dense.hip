@@ -412,10 +412,13 @@ __global__ __launch_bounds__(256) void ess_fill_kernel(int n, int ld, int row0,
 }
 
 /* transpose an arc list (directed graphs: In*(t) from Out*(u)) */
+/* (dtotal: the arc count read on the device, when the host did not wait for it) */
 __global__ void arc_count_by_col(int64_t arcs, const int32_t* __restrict__ col,
-                                 int32_t* __restrict__ cnt) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < arcs) atomicAdd(&cnt[col[i]], 1);
+                                 int32_t* __restrict__ cnt, const int32_t* __restrict__ dtotal) {
+    if (dtotal) arcs = *dtotal;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < arcs;
+         i += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&cnt[col[i]], 1);
 }
 
 __global__ void arc_transpose_fill(int n, const int32_t* __restrict__ ptr,
@@ -978,9 +981,12 @@ __global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
 }
 
 __global__ void pack_uw_kernel(int64_t arcs, const int32_t* __restrict__ col,
-                               const uint32_t* __restrict__ w, uint2* __restrict__ uw) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < arcs) uw[i] = make_uint2((uint32_t)col[i], w[i]);
+                               const uint32_t* __restrict__ w, uint2* __restrict__ uw,
+                               const int32_t* __restrict__ dtotal) {
+    if (dtotal) arcs = *dtotal;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < arcs;
+         i += (int64_t)gridDim.x * blockDim.x)
+        uw[i] = make_uint2((uint32_t)col[i], w[i]);
 }
 
 /* Diagonal rule (topology.c:1431-1576): min over incident OUT edges of (self-loop: L,
@@ -1052,6 +1058,8 @@ typedef struct {
     size_t dt_cap, predt_cap;
     double* rt; /* reliability of each predecessor arc, sources across columns */
     size_t rt_cap;
+    int32_t* h_total; /* pinned: the essential-arc total of a post pass that did not wait for it */
+    int total_pending;
 } dense_ws;
 
 static dense_ws g_ws[SRT_STATE_SLOTS];
@@ -1117,9 +1125,17 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
     if (gather && (rc = gather(gctx, ws, n, 0, 0, st))) return rc; /* all-reduce counts */
     scan_kernel<<<1, 1024, 0, st>>>(n, ws->cnt, ws->ptr);
     SRT_HIPCHK(hipGetLastError());
+    /* small graphs (n <= 2,048, one GPU) size the arc arrays for n (n - 1) arcs and let the
+     * kernels read the total on the device: no host round trip in the middle of the pass */
+    const bool nowait = !gather && n <= 2048;
+    const int32_t* dtotal = nowait ? ws->ptr + n : nullptr;
     int32_t total = 0;
-    SRT_HIPCHK(hipMemcpyAsync(&total, ws->ptr + n, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    SRT_HIPCHK(hipStreamSynchronize(st));
+    if (nowait) {
+        total = n * (n - 1);
+    } else {
+        SRT_HIPCHK(hipMemcpyAsync(&total, ws->ptr + n, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipStreamSynchronize(st));
+    }
     if (total < 0) {
         srt_set_error("essential-arc count overflow");
         return SRT_E_RANGE;
@@ -1140,7 +1156,8 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         ws->tarc_cap = t1;
         SRT_HIPCHK(hipMemsetAsync(ws->cnt, 0, (size_t)n * sizeof(int32_t), st));
         if (total > 0)
-            arc_count_by_col<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, ws->col, ws->cnt);
+            arc_count_by_col<<<min(srt_ceil_div(total, 256), 2048), 256, 0, st>>>(total, ws->col,
+                                                                                  ws->cnt, dtotal);
         scan_kernel<<<1, 1024, 0, st>>>(n, ws->cnt, ws->tptr);
         SRT_HIPCHK(hipMemcpyAsync(ws->cursor, ws->tptr, (size_t)n * sizeof(int32_t),
                                   hipMemcpyDeviceToDevice, st));
@@ -1181,7 +1198,8 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         if (total > 0 && key3)
             pack_uk_kernel<<<srt_ceil_div(n, 4), 256, 0, st>>>(n, iptr, icol, iw, !directed, ws->uw);
         else if (total > 0)
-            pack_uw_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, icol, iw, ws->uw);
+            pack_uw_kernel<<<min(srt_ceil_div(total, 256), 2048), 256, 0, st>>>(total, icol, iw,
+                                                                                ws->uw, dtotal);
         /* DT[u][sl] = D[row0 + sl][u], from the u16 working matrix when the build kept one
          * (half the bytes per candidate arc: the predecessor search is bound by these reads).
          * With small distances (every local one <= 64 quanta) the search also emits the arc
@@ -1284,10 +1302,22 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
                 return rc;
         }
     }
-    if (stats) {
+    if (stats && nowait) { /* read after the build's final wait (dense_collect_total) */
+        if (!ws->h_total) SRT_HIPCHK(hipHostMalloc((void**)&ws->h_total, sizeof(int32_t)));
+        SRT_HIPCHK(hipMemcpyAsync(ws->h_total, ws->ptr + n, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        ws->total_pending = 1;
+    } else if (stats) {
         stats->ess_arcs = total;
     }
     return SRT_OK;
+}
+
+/* the essential-arc total of a post pass that did not wait for it (after the stream's work) */
+static void dense_collect_total(int32_t n, srt_build_stats* stats) {
+    dense_ws* ws;
+    if (!stats || ws_get(&ws, n) || !ws->total_pending) return;
+    stats->ess_arcs = *ws->h_total;
+    ws->total_pending = 0;
 }
 
 static int dense_finish_rows(int32_t n, int32_t ld, int32_t row0, int32_t nrows, const uint32_t* w,
@@ -1308,6 +1338,7 @@ static int dense_finish_rows(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
         SRT_HIPCHK(hipStreamSynchronize(st));
         stats->max_depth = depth;
         stats->tied_pairs = (int64_t)nt;
+        dense_collect_total(n, stats);
     }
     return SRT_OK;
 }

@@ -2629,10 +2629,19 @@ static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStrea
         }
     } fr2{part, st};
     unsigned long long prev = ~0ull;
+    /* timing (bench): the passes as one span, the first start to the end of the last checked
+     * pass (evpool group 4, one unit per pass) -- no event records between passes */
+    if (evp) {
+        int rc = evpool_reserve(evp, 4 * 64);
+        if (rc) return rc;
+        evp->group = 4;
+        evp->used = 0;
+        SRT_HIPCHK(hipEventRecord(evp->ev[0], st));
+        SRT_HIPCHK(hipEventRecord(evp->ev[1], st));
+    }
+    int hf[2] = {0, 0};
+    bool finished = false;
     for (int it = 0; it < 64; ++it) {
-        if (evp && evp->used + 2 <= evp->cap) {
-            SRT_HIPCHK(hipEventRecord(evp->ev[evp->used], st));
-        }
         if (split) {
             if (nq8)
                 fwq_update_kernel<false, 20, 8><<<(unsigned)(T * T * nq8), 512, 0, st>>>(
@@ -2659,21 +2668,37 @@ static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStrea
                         d, ld, d + (size_t)k0 * ld, k0, T, 0, -1, nullptr, 0);
             }
         }
-        if (evp && evp->used + 2 <= evp->cap) {
-            SRT_HIPCHK(hipEventRecord(evp->ev[evp->used + 1], st));
-            evp->used += 2;
-        }
         SRT_HIPCHK(hipGetLastError());
         if (split) {
             /* the change flags are read every fourth pass (one host round trip per four
              * passes; complete graphs converge in 3-4): a pass after the fixed point changes
-             * nothing and costs only its time */
+             * nothing and costs only its time. The finish pass (u32 table, exactness and
+             * small-distance flags) is enqueued with the check, so a converged squaring needs
+             * no second round trip; otherwise its output is overwritten later. */
             if ((it & 3) != 3) continue;
+            if (evp) {
+                evp->used = 4 * (it + 1);
+                SRT_HIPCHK(hipEventRecord(evp->ev[evp->used - 2], st));
+                SRT_HIPCHK(hipEventRecord(evp->ev[evp->used - 1], st));
+            }
+            SRT_HIPCHK(hipMemsetAsync(flags, 0, 2 * sizeof(int), st));
+            fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 2048), ld), 256, 0, st>>>(n, ld, 0, d, lat,
+                                                                                flags, CAP_F);
+            SRT_HIPCHK(hipGetLastError());
             int ch[4] = {0, 0, 0, 0};
             SRT_HIPCHK(hipMemcpyAsync(ch, sflag, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
+            SRT_HIPCHK(hipMemcpyAsync(hf, flags, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
             SRT_HIPCHK(hipStreamSynchronize(st));
-            if (!ch[0] || !ch[1] || !ch[2] || !ch[3]) break;
+            if (!ch[0] || !ch[1] || !ch[2] || !ch[3]) {
+                finished = true;
+                break;
+            }
             continue;
+        }
+        if (evp) {
+            evp->used = 4 * (it + 1);
+            SRT_HIPCHK(hipEventRecord(evp->ev[evp->used - 2], st));
+            SRT_HIPCHK(hipEventRecord(evp->ev[evp->used - 1], st));
         }
         SRT_HIPCHK(hipMemsetAsync(dsum, 0, sizeof(unsigned long long), st));
         rows_sum_kernel<<<64, 256, 0, st>>>((size_t)ld * ld, d, dsum);
@@ -2684,12 +2709,13 @@ static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStrea
         if (cur == prev) break;
         prev = cur;
     }
-    SRT_HIPCHK(hipMemsetAsync(flags, 0, 2 * sizeof(int), st));
-    fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 2048), ld), 256, 0, st>>>(n, ld, 0, d, lat, flags, CAP_F);
-    SRT_HIPCHK(hipGetLastError());
-    int hf[2] = {0, 0};
-    SRT_HIPCHK(hipMemcpyAsync(hf, flags, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
-    SRT_HIPCHK(hipStreamSynchronize(st));
+    if (!finished) {
+        SRT_HIPCHK(hipMemsetAsync(flags, 0, 2 * sizeof(int), st));
+        fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 2048), ld), 256, 0, st>>>(n, ld, 0, d, lat, flags, CAP_F);
+        SRT_HIPCHK(hipGetLastError());
+        SRT_HIPCHK(hipMemcpyAsync(hf, flags, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipStreamSynchronize(st));
+    }
     *exact = hf[0] ? 0 : 1;
     fw16_small[dev] = hf[1] ? 0 : 1;
     return SRT_OK;

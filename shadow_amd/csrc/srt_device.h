@@ -95,6 +95,17 @@ static inline int evpool_begin(evpool_t** out, int rounds) {
     return SRT_OK;
 }
 
+/* grow the pool to at least n events without resetting what it holds */
+static inline int evpool_reserve(evpool_t* p, int n) {
+    if (p->cap >= n) return SRT_OK;
+    hipEvent_t* ne = (hipEvent_t*)realloc(p->ev, sizeof(hipEvent_t) * n);
+    if (!ne) return SRT_E_NOMEM;
+    p->ev = ne;
+    for (int i = p->cap; i < n; i++) SRT_HIPCHK(hipEventCreate(&p->ev[i]));
+    p->cap = n;
+    return SRT_OK;
+}
+
 static inline int evpool_sum(evpool_t* p, hipEvent_t last, srt_build_stats* stats) {
     SRT_HIPCHK(hipEventSynchronize(last));
     double tot = 0;
