@@ -78,7 +78,8 @@ typedef struct srt_build_stats {
     int32_t n_update;    /* FW update-kernel launches timed (time_kernels = 1) */
     double ms_update;    /* summed HIP-event duration of those launches */
     double ms_comm;      /* host-observed time of the collective calls (sharded builds) */
-    int32_t dist_enc;    /* sparse builds: 3 = multi-source kernel (64 sources per workgroup),
+    int32_t dist_enc;    /* sparse builds: 4 = u64 distances (wide.hip; the graph's range passes
+                          * SRT_INF quanta), 3 = multi-source kernel (64 sources per workgroup),
                           * 2 = workgroup-per-source kernel (LDS-packed rows),
                           * 1 = wave-per-source kernel, 0 = workgroup kernel for every source.
                           * Dense: the distance encoding the build finished with: 9 = 8 with

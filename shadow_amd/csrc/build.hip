@@ -103,6 +103,7 @@ struct srt_sparse_graph {
     uint64_t quantum_ns;
     uint32_t delta, max_w;
     uint64_t dist_bound; /* srt_canon.dist_bound */
+    int wide;            /* srt_canon.wide: u64 rows (wide.hip) */
     int local; /* relabelled arcs span <= 4096 vertices on average (graph.c CM order) */
     int32_t *rp, *col, *irp, *icol;
     uint32_t *w, *iw, *sw;
@@ -134,6 +135,11 @@ struct srt_sparse_graph {
 };
 
 int srt_wgsssp_max_n(void);
+int srt_wide_rows(int n, const int32_t* rp, const int32_t* col, const uint32_t* w, const double* r,
+                  const int32_t* irp, const int32_t* icol, const uint32_t* iw, const double* ir,
+                  const uint32_t* sw, const double* sr, uint64_t quantum_ns, int src_begin,
+                  int src_end, const int32_t* srcs, uint32_t* lat, double* rel, double* lms,
+                  size_t ldo, hipStream_t st);
 int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r, const int32_t* inv,
                     uint32_t max_w, int src_begin, int src_end, const int32_t* srcs, uint32_t* lat,
                     double* rel, int* ovf, hipStream_t st, const uint8_t* ridx,
@@ -263,6 +269,7 @@ static int sparse_graph_from_canon(const srt_canon* c, int device, srt_sparse_gr
     g->arcs = c->arcs;
     g->quantum_ns = c->quantum_ns;
     g->dist_bound = c->dist_bound;
+    g->wide = c->wide;
     g->max_w = 0;
     for (int64_t k = 0; k < c->arcs; k++) g->max_w = c->w[k] > g->max_w ? c->w[k] : g->max_w;
     /* bucket width of the label-correcting loop: the mean arc weight */
@@ -557,6 +564,34 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
     }
     const int nsrc = src_end - src_begin;
     (void)srt_state_slot(); /* also keeps the device's scratch pool mapped (comm.hip) */
+    if (g->wide) { /* distances may pass u32 quanta: the u64 rows (wide.hip) */
+        struct evs {
+            hipEvent_t e[2] = {nullptr, nullptr};
+            ~evs() {
+                for (hipEvent_t x : e)
+                    if (x) (void)hipEventDestroy(x);
+            }
+        } wev;
+        SRT_HIPCHK(hipEventCreate(&wev.e[0]));
+        SRT_HIPCHK(hipEventCreate(&wev.e[1]));
+        SRT_HIPCHK(hipEventRecord(wev.e[0], st));
+        int wrc;
+        wrc = srt_wide_rows(g->n, g->rp, g->col, g->w, g->r, g->irp, g->icol, g->iw, g->ir, g->sw,
+                            g->sr, g->quantum_ns, src_begin, src_end, srcs, lat_rows, rel_rows, lms,
+                            (size_t)g->n, st);
+        if (wrc) return wrc;
+        SRT_HIPCHK(hipEventRecord(wev.e[1], st));
+        SRT_HIPCHK(hipEventSynchronize(wev.e[1]));
+        float a = 0;
+        SRT_HIPCHK(hipEventElapsedTime(&a, wev.e[0], wev.e[1]));
+        if (stats) {
+            stats->algo = SRT_ALGO_SPARSE_SSSP;
+            stats->ms_fw = a;
+            stats->ms_total = a;
+            stats->dist_enc = 4;
+        }
+        return SRT_OK;
+    }
     /* source i of this call: srcs + i, or the range */
     auto one = [&](int i) { return srcs ? srcs + i : (const int32_t*)NULL; };
     const int b0 = srcs ? 0 : src_begin;
@@ -1474,7 +1509,19 @@ static int build_tables_subset_impl(const srt_edges* g, const srt_build_opts* op
     if (rc) return rc;
     *quantum_ns = c.quantum_ns;
     const int use_sp = opts ? opts->use_shortest_path : 1;
-    const int algo = use_sp ? choose_algo(&c, opts) : SRT_ALGO_DENSE_FW;
+    const int algo = use_sp ? (c.wide && !(opts && opts->algo == SRT_ALGO_DENSE_FW)
+                                   ? SRT_ALGO_SPARSE_SSSP
+                                   : choose_algo(&c, opts))
+                            : SRT_ALGO_DENSE_FW;
+    if (use_sp && c.wide && (algo == SRT_ALGO_DENSE_FW || !lat_ms)) {
+        srt_set_error("shortest-path latencies may pass the u32 range (bound %llu quanta of %llu "
+                      "ns): only the sparse u64 rows build this graph, and its latencies are "
+                      "served from the f64 ms table (%s)",
+                      (unsigned long long)c.dist_bound, (unsigned long long)c.quantum_ns,
+                      algo == SRT_ALGO_DENSE_FW ? "dense requested" : "no lat_ms output");
+        srt_canon_free(&c);
+        return SRT_E_RANGE;
+    }
     const int R = virt ? virt : (ngpus < avail ? ngpus : avail);
     uint32_t mq = 0xFFFFFFFFu;
     if (R > 1 && use_sp)

@@ -295,14 +295,15 @@ int srt_canon_build(const srt_edges* g, srt_canon* c) {
             }
         }
     }
-    if (bound >= SRT_INF || 2ull * c->max_w_q >= SRT_INF) {
+    if (2ull * c->max_w_q >= SRT_INF) {
         free(a);
         srt_canon_free(c);
-        srt_set_error("shortest-path latencies may exceed the u32 table range "
-                      "(bound %llu quanta of %llu ns)",
-                      (unsigned long long)bound, (unsigned long long)q);
+        srt_set_error("an edge latency of %llu quanta of %llu ns passes the u32 arc range",
+                      (unsigned long long)c->max_w_q, (unsigned long long)q);
         return SRT_E_RANGE;
     }
+    /* distances that may pass u32 quanta: the u64 rows (wide.hip) build the graph */
+    c->wide = bound >= SRT_INF;
     c->dist_bound = bound;
     rc = fill_csr(g, a, k, q, &c->rowptr, &c->col, &c->w, &c->r, &c->arcs);
     if (rc == SRT_OK && g->directed) {

@@ -23,8 +23,10 @@ typedef struct srt_canon {
     uint64_t quantum_ns;
     uint32_t max_w_q;
     /* upper bound on every finite shortest distance, in quanta (graph.c: MST, (n - 1) max_w or
-     * the hop bound through the highest-degree vertex); < SRT_INF */
+     * the hop bound through the highest-degree vertex); < SRT_INF unless wide */
     uint64_t dist_bound;
+    /* 1: the bound reaches SRT_INF (2^31 - 1) quanta -- only the u64 rows of wide.hip build this graph */
+    int32_t wide;
     /* CSR of canonical out-arcs (self-loops excluded), columns ascending */
     int64_t arcs;
     int32_t* rowptr;

@@ -39,10 +39,10 @@ static __device__ __forceinline__ void st_wg(double* p, double v) {
  * entry is formed once, in path order. The diagonal is the "path to self" rule: MS writes
  * out[s] = D[s][s] q / 1e6 (self-loop L or 2L, exact doubling) at the end, so the pass runs after
  * the diagonal rule has written D[s][s]. */
-template <bool HAS_PRED, bool MS, bool REL>
+template <bool HAS_PRED, bool MS, bool REL, typename DT = uint32_t>
 __global__ __launch_bounds__(PS_THREADS) void path_sweeps_kernel(
     int n, int nrows, const int32_t* __restrict__ srcs, int src_begin,
-    const uint32_t* __restrict__ D, size_t ldd, const int32_t* __restrict__ pred, size_t ldp,
+    const DT* __restrict__ D, size_t ldd, const int32_t* __restrict__ pred, size_t ldp,
     const int32_t* __restrict__ irp, const int32_t* __restrict__ icol,
     const uint32_t* __restrict__ iw, uint64_t q, double* __restrict__ out, size_t ldo,
     const int32_t* __restrict__ only, int32_t* __restrict__ pws, int32_t* __restrict__ max_depth) {
@@ -56,12 +56,15 @@ __global__ __launch_bounds__(PS_THREADS) void path_sweeps_kernel(
     for (int r = blockIdx.x; r < nrows; r += gridDim.x) {
         if (only && !only[r]) continue;
         const int s = srcs ? srcs[r] : src_begin + r;
-        const uint32_t* Dr = D + (size_t)r * ldd;
+        const DT* Dr = D + (size_t)r * ldd;
         double* o = out + (size_t)r * ldo;
+        /* SRT_INF for u32 rows; the u64 rows of wide.hip mark unreachable with ~0 */
+        constexpr DT INF = sizeof(DT) == 4 ? (DT)SRT_INF : (DT)~(DT)0;
         const int32_t* P;
         if constexpr (HAS_PRED) {
             P = pred + (size_t)r * ldp;
         } else {
+            static_assert(HAS_PRED || sizeof(DT) == 4, "u64 rows come with their predecessors");
             int32_t* pw = pws + (size_t)blockIdx.x * n;
             for (int t = tid; t < n; t += PS_THREADS) {
                 int bu = -1;
@@ -112,7 +115,7 @@ __global__ __launch_bounds__(PS_THREADS) void path_sweeps_kernel(
                     const int p = P[t];
                     if (p < 0 || !((done[p >> 5] >> (p & 31)) & 1u)) continue;
                     if constexpr (MS) {
-                        const uint32_t dp = p == s ? 0u : Dr[p];
+                        const DT dp = p == s ? (DT)0 : Dr[p];
                         const double hop = (double)((uint64_t)(Dr[t] - dp) * q) / 1e6;
                         st_wg(o + t, ld_wg(o + p) + hop);
                     } else {
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(PS_THREADS) void path_sweeps_kernel(
             }
             __syncthreads();
         }
-        if (MS && tid == 0) o[s] = Dr[s] < SRT_INF ? (double)((uint64_t)Dr[s] * q) / 1e6 : 0.0;
+        if (MS && tid == 0) o[s] = Dr[s] < INF ? (double)((uint64_t)Dr[s] * q) / 1e6 : 0.0;
         depth_max = depth > depth_max ? depth : depth_max;
         __syncthreads();
     }
@@ -190,6 +193,37 @@ int srt_path_ms_rows(int n, int nrows, const int32_t* srcs, int src_begin, const
     return SRT_OK;
 }
 
+/* u64 distance rows with their predecessor rows (wide.hip): the reliability product in place
+ * over rel rows holding r(pred, t) (rel != NULL), and/or the f64-ms sums into ms (ms != NULL) */
+int srt_path_rows_u64(int n, int nrows, const int32_t* srcs, int src_begin, const uint64_t* D,
+                      size_t ldd, const int32_t* pred, size_t ldp, uint64_t quantum_ns, double* rel,
+                      size_t ldr, double* ms, size_t ldm, hipStream_t st) {
+    if (nrows <= 0) return SRT_OK;
+    if (n > srt_path_sweeps_max_n() || !pred) {
+        srt_set_error("path-order pass (u64 rows): n = %d beyond its range or no predecessors", n);
+        return SRT_E_RANGE;
+    }
+    const int grid = path_grid(nrows);
+    const size_t lds = 2 * (size_t)((n + 31) / 32) * sizeof(uint32_t);
+    if (rel) {
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)path_sweeps_kernel<true, false, true, uint64_t>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        path_sweeps_kernel<true, false, true, uint64_t><<<grid, PS_THREADS, lds, st>>>(
+            n, nrows, srcs, src_begin, D, ldd, pred, ldp, NULL, NULL, NULL, quantum_ns, rel, ldr,
+            NULL, NULL, NULL);
+        SRT_HIPCHK(hipGetLastError());
+    }
+    if (ms) {
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)path_sweeps_kernel<true, true, false, uint64_t>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        path_sweeps_kernel<true, true, false, uint64_t><<<grid, PS_THREADS, lds, st>>>(
+            n, nrows, srcs, src_begin, D, ldd, pred, ldp, NULL, NULL, NULL, quantum_ns, ms, ldm,
+            NULL, NULL, NULL);
+        SRT_HIPCHK(hipGetLastError());
+    }
+    return SRT_OK;
+}
+
 /* path-order reliability by sweeps with the predecessor rows in HBM (dense rows beyond the LDS
  * form of rel_sweeps_kernel): rel rows arrive holding r(pred, t); rows with only[r] == 0 skip */
 int srt_rel_sweeps_rows(int n, int nrows, int row0, const int32_t* pred, size_t ldp, double* rel,
@@ -204,7 +238,7 @@ int srt_rel_sweeps_rows(int n, int nrows, int row0, const int32_t* pred, size_t 
     SRT_HIPCHK(hipFuncSetAttribute((const void*)path_sweeps_kernel<true, false, true>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     path_sweeps_kernel<true, false, true><<<grid, PS_THREADS, lds, st>>>(
-        n, nrows, NULL, row0, NULL, 0, pred, ldp, NULL, NULL, NULL, 0, rel, ldr, only, NULL,
+        n, nrows, NULL, row0, (const uint32_t*)NULL, 0, pred, ldp, NULL, NULL, NULL, 0, rel, ldr, only, NULL,
         max_depth);
     SRT_HIPCHK(hipGetLastError());
     return SRT_OK;
