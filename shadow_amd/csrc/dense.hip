@@ -729,7 +729,7 @@ __global__ void pack_uk_kernel(int n, const int32_t* __restrict__ iptr, const in
     }
 }
 
-template <int U>
+template <int U, bool NT>
 __global__ __launch_bounds__(256) void pred_cols3_kernel(int n, int row0, int nloc, int ldT,
                                                          size_t bsD, const uint8_t* __restrict__ DT,
                                                          const int32_t* __restrict__ iptr,
@@ -802,10 +802,21 @@ __global__ __launch_bounds__(256) void pred_cols3_kernel(int n, int row0, int nl
         const size_t o = (size_t)t * ldT + sl;
         const bool h0 = s != t && bk0 >= 0, h1 = s + 1 != t && bk1 >= 0;
         if (v0 && v1 && (o & 1) == 0) {
-            *reinterpret_cast<int2*>(predT + o) =
-                make_int2(h0 ? (int32_t)(uk[bk0].x >> 7) : -1, h1 ? (int32_t)(uk[bk1].x >> 7) : -1);
-            rT[o] = h0 ? ar[bk0] : 0.0;
-            rT[o + 1] = h1 ? ar[bk1] : 0.0;
+            const int32_t p0 = h0 ? (int32_t)(uk[bk0].x >> 7) : -1;
+            const int32_t p1 = h1 ? (int32_t)(uk[bk1].x >> 7) : -1;
+            const double r0 = h0 ? ar[bk0] : 0.0, r1 = h1 ? ar[bk1] : 0.0;
+            if constexpr (NT) {
+                /* streaming stores: the 50 MB of outputs per source block do not allocate in
+                 * L2, which holds the block's 4-MB slab */
+                __builtin_nontemporal_store(p0, predT + o);
+                __builtin_nontemporal_store(p1, predT + o + 1);
+                __builtin_nontemporal_store(r0, rT + o);
+                __builtin_nontemporal_store(r1, rT + o + 1);
+            } else {
+                *reinterpret_cast<int2*>(predT + o) = make_int2(p0, p1);
+                rT[o] = r0;
+                rT[o + 1] = r1;
+            }
         } else {
             if (v0) {
                 predT[o] = h0 ? (int32_t)(uk[bk0].x >> 7) : -1;
@@ -1221,8 +1232,15 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
                                                      256, 0, st>>>(nrows, ld, d16, (size_t)ld, dt8,
                                                                    (size_t)ld * 128);
             /* 16 candidate arcs in flight per step: 17.3 ms on C4 against 18.7 (8) and 20.0 (32) */
-            if (key3)
-                pred_cols3_kernel<16><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
+            /* SRT_PRED_NT=1: streaming (non-temporal) output stores (A/B knob) */
+            static const char* nt_env = getenv("SRT_PRED_NT");
+            const bool nt = nt_env && atoi(nt_env) == 1;
+            if (key3 && nt)
+                pred_cols3_kernel<16, true><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
+                    n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
+                    nsb2, tch, tper, !directed);
+            else if (key3)
+                pred_cols3_kernel<16, false><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
                     n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
                     nsb2, tch, tper, !directed);
             else if (ties)
