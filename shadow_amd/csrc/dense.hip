@@ -1232,9 +1232,10 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
                                                      256, 0, st>>>(nrows, ld, d16, (size_t)ld, dt8,
                                                                    (size_t)ld * 128);
             /* 16 candidate arcs in flight per step: 17.3 ms on C4 against 18.7 (8) and 20.0 (32) */
-            /* SRT_PRED_NT=1: streaming (non-temporal) output stores (A/B knob) */
+            /* streaming (non-temporal) output stores: 13.9 against 14.5 ms on C4, post pass
+             * 35.4 against 36.3 ms, same box (SRT_PRED_NT=0 turns them off) */
             static const char* nt_env = getenv("SRT_PRED_NT");
-            const bool nt = nt_env && atoi(nt_env) == 1;
+            const bool nt = !(nt_env && atoi(nt_env) == 0);
             if (key3 && nt)
                 pred_cols3_kernel<16, true><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
                     n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
