@@ -932,7 +932,9 @@ __global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
     for (int i = 0; i < PER; ++i) {
         /* out of range reads 0 (the descriptor's bound): not a target of any pass, like the
          * source itself and unreachable vertices */
-        const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(rd, tid * 4, i * NT * 4, 0);
+        /* read once: non-temporal (aux 2), so the row's distances do not displace the rel
+         * rows that the level passes re-read from L2 */
+        const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(rd, tid * 4, i * NT * 4, 2);
         const uint32_t x = (tid + i * NT != s && d < SRT_INF) ? d : 0u;
         mx = max(mx, x);
         const uint32_t b = min(x, 255u) << (8 * (i & 3));
@@ -975,7 +977,7 @@ __global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
 #pragma unroll
             for (int q = 0; q < QB; ++q) t[q] = j + 64 * q < cnt ? (int)wl[j + 64 * q] : -1;
 #pragma unroll
-            for (int q = 0; q < QB; ++q) u[q] = t[q] >= 0 ? pg[t[q]] : -1;
+            for (int q = 0; q < QB; ++q) u[q] = t[q] >= 0 ? __builtin_nontemporal_load(pg + t[q]) : -1;
 #pragma unroll
             for (int q = 0; q < QB; ++q) rt[q] = t[q] >= 0 ? rr[t[q]] : 0.0;
             /* u < 0: unreachable, cannot happen on a validated graph; the entry is kept */
