@@ -447,7 +447,7 @@ __global__ void arc_transpose_fill(int n, const int32_t* __restrict__ ptr,
 /* ------------------------------------------------------------------------------------------ */
 /* out[c][r] = in[r][c]; BM (block-major, 64 or 128): out[r / BM][c][r % BM], ldo = the stride of
  * a BM-row block, so each block's transpose is one contiguous slab */
-template <typename T, typename TO = T, int BM = 0>
+template <typename T, typename TO = T, int BM = 0, bool NTS = false>
 __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, const T* __restrict__ in,
                                                         size_t ldi, TO* __restrict__ out, size_t ldo) {
     __shared__ T tile[64][65];
@@ -468,6 +468,8 @@ __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, cons
         if (r < rows && c < cols) {
             if constexpr (BM != 0)
                 out[(size_t)(r / BM) * ldo + (size_t)c * BM + (r % BM)] = (TO)tile[tx][a];
+            else if constexpr (NTS) /* streaming: rows read once, by a later pass */
+                __builtin_nontemporal_store((TO)tile[tx][a], out + (size_t)c * ldo + r);
             else
                 out[(size_t)c * ldo + r] = (TO)tile[tx][a];
         }
@@ -1281,11 +1283,23 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         /* predecessor rows pred[sl][t] = predT[t][sl] (reuses the DT buffer) and the arc
          * reliabilities straight into the rel rows, where the passes below finish them in place */
         int32_t* pred = reinterpret_cast<int32_t*>(ws->dt);
-        transpose_kernel<uint32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
-            n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows,
-            reinterpret_cast<uint32_t*>(pred), (size_t)ld);
-        transpose_kernel<double><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
-            n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
+        /* SRT_TRANSPOSE_NT=1: streaming stores for the two row transposes (A/B knob) */
+        static const char* tn_env = getenv("SRT_TRANSPOSE_NT");
+        if (tn_env && atoi(tn_env) == 1) {
+            transpose_kernel<uint32_t, uint32_t, 0, true>
+                <<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+                    n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows,
+                    reinterpret_cast<uint32_t*>(pred), (size_t)ld);
+            transpose_kernel<double, double, 0, true>
+                <<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+                    n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
+        } else {
+            transpose_kernel<uint32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+                n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows,
+                reinterpret_cast<uint32_t*>(pred), (size_t)ld);
+            transpose_kernel<double><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+                n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
+        }
         /* level order for rows whose distances span <= 64 quanta, sweeps for the rest
          * (ws->cursor is free here and carries the per-row hand-over flags) */
         /* 1024 threads per row, one row per CU (128 VGPRs): 12.3 ms on C4 against 13.3 for 512
