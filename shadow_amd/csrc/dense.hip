@@ -290,25 +290,35 @@ int srt_dense_fw_device(int32_t n, int32_t ld, uint32_t* d, hipStream_t st, evpo
 /* (s,t) is essential: D[s][u] + W[u][t] = D[s][t] <= D[s][u] + D[u][t] forces D[u][t] = W.    */
 /* Rows are local (global row = row0 + blockIdx.x); counts go to cnt[global row].            */
 /* ------------------------------------------------------------------------------------------ */
+/* four consecutive distances (u32 table, or the exact u16 FW matrix: half the bytes) */
+static __device__ __forceinline__ uint4 ld_d4(const uint32_t* p) {
+    return *reinterpret_cast<const uint4*>(p);
+}
+static __device__ __forceinline__ uint4 ld_d4(const uint16_t* p) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    return make_uint4(v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16);
+}
+
+template <typename DT>
 __global__ __launch_bounds__(256) void ess_count_kernel(int n, int ld, int row0,
                                                         const uint32_t* __restrict__ w,
-                                                        const uint32_t* __restrict__ d,
+                                                        const DT* __restrict__ d,
                                                         int32_t* __restrict__ cnt) {
     const int u = row0 + blockIdx.x;
     if (u >= n) return;
     const uint32_t* wr = w + (size_t)blockIdx.x * ld;
-    const uint32_t* dr = d + (size_t)blockIdx.x * ld;
+    const DT* dr = d + (size_t)blockIdx.x * ld;
     int c = 0;
     const int n4 = n & ~3; /* rows are 16-B aligned (ld % 64 == 0): 4 columns per load */
     for (int t = threadIdx.x * 4; t < n4; t += blockDim.x * 4) {
         const uint4 x = *reinterpret_cast<const uint4*>(wr + t);
-        const uint4 y = *reinterpret_cast<const uint4*>(dr + t);
+        const uint4 y = ld_d4(dr + t);
         c += (t != u && x.x < SRT_INF && x.x == y.x) + (t + 1 != u && x.y < SRT_INF && x.y == y.y) +
              (t + 2 != u && x.z < SRT_INF && x.z == y.z) + (t + 3 != u && x.w < SRT_INF && x.w == y.w);
     }
     for (int t = n4 + threadIdx.x; t < n; t += blockDim.x) {
         uint32_t x = wr[t];
-        c += (t != u && x < SRT_INF && x == dr[t]) ? 1 : 0;
+        c += (t != u && x < SRT_INF && x == (uint32_t)dr[t]) ? 1 : 0;
     }
     __shared__ int red[256];
     red[threadIdx.x] = c;
@@ -346,10 +356,11 @@ __global__ __launch_bounds__(1024) void scan_kernel(int n, const int32_t* __rest
 }
 
 /* fill essential out-arcs of local row u at ptr[u], ascending t (wave ballot compaction) */
+template <typename DT>
 __global__ __launch_bounds__(256) void ess_fill_kernel(int n, int ld, int row0,
                                                        const uint32_t* __restrict__ w,
                                                        const double* __restrict__ r,
-                                                       const uint32_t* __restrict__ d,
+                                                       const DT* __restrict__ d,
                                                        const int32_t* __restrict__ ptr,
                                                        int32_t* __restrict__ col,
                                                        uint32_t* __restrict__ aw,
@@ -357,7 +368,7 @@ __global__ __launch_bounds__(256) void ess_fill_kernel(int n, int ld, int row0,
     const int u = row0 + blockIdx.x;
     if (u >= n) return;
     const uint32_t* wr = w + (size_t)blockIdx.x * ld;
-    const uint32_t* dr = d + (size_t)blockIdx.x * ld;
+    const DT* dr = d + (size_t)blockIdx.x * ld;
     const double* rr = r + (size_t)blockIdx.x * ld;
     __shared__ int wave_cnt[4];
     __shared__ int base;
@@ -373,7 +384,7 @@ __global__ __launch_bounds__(256) void ess_fill_kernel(int n, int ld, int row0,
         uint32_t x[4] = {0, 0, 0, 0}, y[4] = {1, 1, 1, 1};
         if (t + 4 <= n) {
             const uint4 a = *reinterpret_cast<const uint4*>(wr + t);
-            const uint4 b = *reinterpret_cast<const uint4*>(dr + t);
+            const uint4 b = ld_d4(dr + t);
             x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
             y[0] = b.x; y[1] = b.y; y[2] = b.z; y[3] = b.w;
         } else {
@@ -381,7 +392,7 @@ __global__ __launch_bounds__(256) void ess_fill_kernel(int n, int ld, int row0,
             for (int q = 0; q < 4; ++q)
                 if (t + q < n) {
                     x[q] = wr[t + q];
-                    y[q] = dr[t + q];
+                    y[q] = (uint32_t)dr[t + q];
                 }
         }
         bool ok[4];
@@ -1136,7 +1147,14 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
     if (rc) return rc;
     const int lrows = max(0, min(nrows, n - row0)); /* real (non-padding) local rows */
     SRT_HIPCHK(hipMemsetAsync(ws->cnt, 0, (size_t)(n + 1) * sizeof(int32_t), st));
-    if (lrows > 0) ess_count_kernel<<<lrows, 256, 0, st>>>(n, ld, row0, w, d, ws->cnt);
+    /* SRT_ESS_U16=1: the exact u16 FW matrix when the build kept one (the same values in half
+     * the bytes); off until measured on the GPU */
+    static const char* eu_env = getenv("SRT_ESS_U16");
+    const bool ess16 = d16 && eu_env && atoi(eu_env) == 1;
+    if (lrows > 0 && ess16)
+        ess_count_kernel<uint16_t><<<lrows, 256, 0, st>>>(n, ld, row0, w, d16, ws->cnt);
+    else if (lrows > 0)
+        ess_count_kernel<uint32_t><<<lrows, 256, 0, st>>>(n, ld, row0, w, d, ws->cnt);
     if (gather && (rc = gather(gctx, ws, n, 0, 0, st))) return rc; /* all-reduce counts */
     scan_kernel<<<1, 1024, 0, st>>>(n, ws->cnt, ws->ptr);
     SRT_HIPCHK(hipGetLastError());
@@ -1157,7 +1175,12 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
     }
     if ((rc = grow_arcs(ws, (size_t)total + 1))) return rc;
     if (lrows > 0)
-        ess_fill_kernel<<<lrows, 256, 0, st>>>(n, ld, row0, w, r, d, ws->ptr, ws->col, ws->aw, ws->ar);
+        if (ess16)
+            ess_fill_kernel<uint16_t><<<lrows, 256, 0, st>>>(n, ld, row0, w, r, d16, ws->ptr,
+                                                             ws->col, ws->aw, ws->ar);
+        else
+            ess_fill_kernel<uint32_t><<<lrows, 256, 0, st>>>(n, ld, row0, w, r, d, ws->ptr,
+                                                             ws->col, ws->aw, ws->ar);
     SRT_HIPCHK(hipGetLastError());
     if (gather && (rc = gather(gctx, ws, n, 1, total, st))) return rc; /* share the arcs */
     const int32_t *iptr = ws->ptr, *icol = ws->col;
