@@ -1263,7 +1263,21 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
              * 35.4 against 36.3 ms, same box (SRT_PRED_NT=0 turns them off) */
             static const char* nt_env = getenv("SRT_PRED_NT");
             const bool nt = !(nt_env && atoi(nt_env) == 0);
-            if (key3 && nt)
+            static const char* pu_env = getenv("SRT_PRED_U"); /* A/B: arcs in flight per step */
+            const int pu = pu_env ? atoi(pu_env) : 16;
+            if (key3 && nt && pu == 24)
+                pred_cols3_kernel<24, true><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
+                    n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
+                    nsb2, tch, tper, !directed);
+            else if (key3 && nt && pu == 32)
+                pred_cols3_kernel<32, true><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
+                    n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
+                    nsb2, tch, tper, !directed);
+            else if (key3 && nt && pu == 8)
+                pred_cols3_kernel<8, true><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
+                    n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
+                    nsb2, tch, tper, !directed);
+            else if (key3 && nt)
                 pred_cols3_kernel<16, true><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
                     n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
                     nsb2, tch, tper, !directed);
