@@ -15,7 +15,9 @@ Workloads:
   c5            100,000-node Barabasi-Albert graph (m=3), source-sharded SSSP + ncclAllGather
                 (configs[4]); 120 GB of tables per GPU.
 
-Launch: python bench.py [--gpus 1]  or  torchrun --nproc-per-node N bench.py --gpus N
+Launch: python bench.py [--gpus N]  (N > 1 without torchrun: bench.py starts the N rank processes
+itself, as child processes, before anything touches a GPU)  or  torchrun --nproc-per-node N
+bench.py --gpus N.  --dry-run prints each rank's environment and exits before importing torch.
 """
 from __future__ import annotations
 
@@ -30,10 +32,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402  (before the library: one HIP runtime)
-import torch.distributed as dist  # noqa: E402
 
-from shadow_amd import _lib  # noqa: E402
+# torch, torch.distributed and the native library are imported by _runtime() -- after the
+# launcher has decided whether this process is a rank (the launcher itself never imports them)
+torch = dist = _lib = None
+
+
+def _runtime():
+    global torch, dist, _lib
+    import torch as _torch  # before the library: one HIP runtime
+    import torch.distributed as _dist
+    from shadow_amd import _lib as _l
+    torch, dist, _lib = _torch, _dist, _l
 
 WORKLOADS = {
     "c4": dict(kind="dense", n=32768, seed=4, lat_max=1000, self_max=10, loss_max=500,
@@ -128,6 +138,23 @@ class Ctx:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         return elapsed, stats
+
+    def rccl_ranks(self) -> int:
+        """ranks of the RCCL communicator (ncclCommCount); 0 at N = 1 (no communicator)"""
+        if self.world == 1:
+            return 0
+        k = ctypes.c_int32()
+        _lib.check(self.L.srt_comm_count(self.comm, ctypes.byref(k)), "srt_comm_count")
+        return int(k.value)
+
+    def per_rank(self, vals):
+        """every rank's list of floats, on every rank (one all_gather)"""
+        t = torch.tensor(vals, dtype=torch.float64, device=self.dev)
+        if self.world == 1:
+            return [vals]
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t)
+        return [o.cpu().tolist() for o in out]
 
     def close(self):
         if self.world > 1:
@@ -249,6 +276,8 @@ def run_dense(c: Ctx, wl):
         _lib.check(rc, "build")
 
     elapsed, stats = c.timed(step)
+    c.last = stats[-1]
+    c.ms_comm = [float(st.ms_comm) for st in stats]
     # dominant kernel: the FW update (phase 3) of every round, timed with HIP events on the
     # stream it is launched on (per round: one launch, or two on the owner of the next block
     # under the lookahead schedule)
@@ -443,18 +472,27 @@ def run_sparse(c: Ctx, wl):
     rel = torch.empty((rows_all, n), dtype=torch.float64, device=c.dev)
     torch.cuda.synchronize()
 
+    comm_ms = []
+
     def step(stats):
         lp = lat.data_ptr() + s0 * n * 4
         rp = rel.data_ptr() + s0 * n * 8
         if s1 > s0:
             sg.rows(s0, s1, lp, rp, c.stream.cuda_stream, stats)
         if world > 1:
+            ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ea.record(c.stream)
             _lib.check(L.srt_sparse_allgather(c.comm, n, per, ctypes.c_void_p(lat.data_ptr()),
                                               ctypes.c_void_p(rel.data_ptr()), c.sp),
                        "srt_sparse_allgather")
+            eb.record(c.stream)
         c.stream.synchronize()
+        if world > 1 and stats is not None:
+            comm_ms.append(ea.elapsed_time(eb))
 
     elapsed, stats = c.timed(step)
+    c.last = stats[-1]
+    c.ms_comm = list(comm_ms) if comm_ms else [0.0] * len(stats)
     arcs = sg.arcs
     # algorithmic bytes per source: row pointers, every arc once (col 4 + w 4 +
     # reliability 8), the output row (lat 4 + rel 8)
@@ -557,6 +595,53 @@ def run_sparse(c: Ctx, wl):
     return elapsed, "u32", "strong", config, roofline, cpu, parity
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch(n: int) -> int:
+    """`bench.py --gpus N` from a plain shell: start N rank processes of this same command line
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on 127.0.0.1), one per GPU, as
+    children -- nothing here touches the GPU. Rank 0 prints the JSON line. If a rank fails, the
+    others are stopped (by PID) so a peer waiting in a collective cannot hang the job. Returns the
+    first non-zero exit status, else 0."""
+    import signal
+    import subprocess
+    port = int(os.environ.get("MASTER_PORT") or free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
+                    "LOCAL_WORLD_SIZE": str(n), "GROUP_RANK": "0",
+                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)]
+                                      + sys.argv[1:], env=env))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                print(f"[bench] rank {procs.index(p)} exited with {rc}; stopping the others",
+                      file=sys.stderr, flush=True)
+                stop()
+        time.sleep(0.05)
+    return status
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -566,12 +651,30 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the CPU-baseline sample (rank 0, N=1 only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print this rank's launch environment and exit before importing torch")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args.gpus))
+    if args.dry_run:
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")),
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                          "world_size": int(os.environ.get("WORLD_SIZE", "1")),
+                          "master_addr": os.environ.get("MASTER_ADDR"),
+                          "master_port": os.environ.get("MASTER_PORT"),
+                          "torch_imported": "torch" in sys.modules, "pid": os.getpid()}),
+              flush=True)
+        return
+    _runtime()
     c = Ctx(args)
     wl = WORKLOADS[args.workload]
     runner = run_dense if wl["kind"] == "dense" else run_sparse
     elapsed, dtype, scaling, config, roofline, cpu, parity = runner(c, wl)
     n = wl["n"]
+    # per-rank split of the last timed step and the collectives' device time (all ranks)
+    ms_comm = sum(c.ms_comm) / max(len(c.ms_comm), 1)
+    pr = c.per_rank([float(c.last.ms_total), float(c.last.ms_fw), float(c.last.ms_post), ms_comm])
+    rccl = c.rccl_ranks()
     value = float(n) * float(n) * args.steps / elapsed
     if cpu is not None:
         cpu["speedup"] = round(value / cpu["value"], 1)
@@ -584,6 +687,14 @@ def main():
             "dtype": dtype,  # integer latency quanta
             "data": "synthetic", "config": config, "roofline": roofline,
             "cpu_baseline": cpu, "parity": parity,
+            "rccl_ranks": rccl,
+            # device time the streams spent inside collectives per step (waits for peers
+            # included; the band broadcasts overlap the update, so this is not on the critical
+            # path by itself), mean over the timed steps, max over ranks
+            "ms_comm": round(max(p[3] for p in pr), 3),
+            "per_rank": [{"rank": q, "ms_total": round(p[0], 3), "ms_fw": round(p[1], 3),
+                          "ms_post": round(p[2], 3), "ms_comm": round(p[3], 3)}
+                         for q, p in enumerate(pr)],
         }
         print(json.dumps(line), flush=True)
     c.close()

@@ -77,7 +77,9 @@ typedef struct srt_build_stats {
     int32_t max_depth;   /* deepest shortest-path tree seen by the reliability pass */
     int32_t n_update;    /* FW update-kernel launches timed (time_kernels = 1) */
     double ms_update;    /* summed HIP-event duration of those launches */
-    double ms_comm;      /* host-observed time of the collective calls (sharded builds) */
+    double ms_comm;      /* sharded builds (time_kernels = 1): device time the streams spent inside
+                          * collectives, an event pair around each collective or group, waits for
+                          * the peers included (they overlap the update on their own stream) */
     int32_t dist_enc;    /* sparse builds: 4 = u64 distances (wide.hip; the graph's range passes
                           * SRT_INF quanta), 3 = multi-source kernel (64 sources per workgroup),
                           * 2 = workgroup-per-source kernel (LDS-packed rows),
@@ -214,6 +216,8 @@ int srt_comm_init_solo(int32_t nranks, int32_t rank, int32_t device, srt_comm** 
 int srt_comm_init_solo_wire(int32_t nranks, int32_t rank, int32_t device, double gbps,
                             double lat_us, srt_comm** comm);
 double srt_comm_wire_ms(const srt_comm* comm);
+/* ranks of the communicator: ncclCommCount for RCCL, nranks for virtual / timing-only ranks */
+int srt_comm_count(const srt_comm* comm, int32_t* count);
 int srt_comm_init_virtual(int32_t nranks, int32_t device, srt_comm** comms);
 /* Bind the calling host thread to virtual rank `rank` on `device` (its own workspaces and
  * streams) before it drives that rank's srt_dense_build_sharded / srt_sparse_graph_rows;

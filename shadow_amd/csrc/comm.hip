@@ -39,6 +39,12 @@ struct srt_comm {
     int in_group;
     size_t group_bytes;
     double wire_us_total; /* modelled wire time issued on the streams (ms_comm of a solo build) */
+    /* srt_build_stats.ms_comm: an event pair around every collective (or group) while timing is
+     * on -- the device time the streams spend inside collectives, waits for the peers included */
+    int timing, t_open;
+    hipEvent_t* tev;
+    int tcap, tused;
+    hipStream_t t_stream; /* the stream the open group's first collective named */
 };
 
 static thread_local int t_vslot = -1;
@@ -242,6 +248,75 @@ static int solo_wire(const srt_comm* cc, size_t bytes, hipStream_t st) {
 
 extern "C" double srt_comm_wire_ms(const srt_comm* c) { return c ? c->wire_us_total * 1e-3 : 0.0; }
 
+/* ---- collective timing (srt_build_stats.ms_comm) ----------------------------------------- */
+void srt_comm_timing(const srt_comm* cc, int on) {
+    srt_comm* c = const_cast<srt_comm*>(cc);
+    if (!c) return;
+    c->timing = on;
+    c->tused = 0;
+    c->t_open = 0;
+}
+
+static int t_record(srt_comm* c, hipStream_t st) {
+    if (c->tused == c->tcap) {
+        const int nc = c->tcap ? 2 * c->tcap : 512;
+        hipEvent_t* ne = (hipEvent_t*)realloc(c->tev, sizeof(hipEvent_t) * (size_t)nc);
+        if (!ne) return SRT_E_NOMEM;
+        c->tev = ne;
+        for (int i = c->tcap; i < nc; i++) SRT_HIPCHK(hipEventCreate(&c->tev[i]));
+        c->tcap = nc;
+    }
+    SRT_HIPCHK(hipEventRecord(c->tev[c->tused++], st));
+    return SRT_OK;
+}
+
+/* before a collective on st: opens its span (inside a group, only the group's first one does) */
+static int t_begin(const srt_comm* cc, hipStream_t st) {
+    srt_comm* c = const_cast<srt_comm*>(cc);
+    if (!c->timing) return SRT_OK;
+    if (c->in_group) {
+        if (c->t_open) return SRT_OK;
+        c->t_open = 1;
+        c->t_stream = st;
+    }
+    return t_record(c, st);
+}
+
+/* after a collective on st (outside a group), or at the group's end */
+static int t_end(const srt_comm* cc, hipStream_t st) {
+    srt_comm* c = const_cast<srt_comm*>(cc);
+    if (!c->timing || c->in_group) return SRT_OK;
+    return t_record(c, st);
+}
+
+double srt_comm_timing_ms(const srt_comm* cc) {
+    srt_comm* c = const_cast<srt_comm*>(cc);
+    if (!c || !c->timing || c->tused < 2) return 0.0;
+    if (hipEventSynchronize(c->tev[c->tused - 1]) != hipSuccess) return -1.0;
+    double tot = 0.0;
+    for (int i = 0; i + 1 < c->tused; i += 2) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, c->tev[i], c->tev[i + 1]) == hipSuccess) tot += ms;
+    }
+    return tot;
+}
+
+/* RCCL ranks of the communicator (ncclCommCount); virtual and timing-only ranks report theirs */
+extern "C" int srt_comm_count(const srt_comm* c, int32_t* count) {
+    if (!c || !count) {
+        srt_set_error("srt_comm_count: bad arguments");
+        return SRT_E_ARG;
+    }
+    if (c->loop || c->solo) {
+        *count = c->nranks;
+        return SRT_OK;
+    }
+    int k = 0;
+    SRT_NCCLCHK(ncclCommCount(c->nc, &k));
+    *count = k;
+    return SRT_OK;
+}
+
 extern "C" int srt_virtual_rank_bind(int32_t rank, int32_t device) {
     srt_set_virtual_slot(rank);
     SRT_HIPCHK(hipSetDevice(device));
@@ -272,6 +347,8 @@ extern "C" void srt_comm_free(srt_comm* comm) {
     } else if (!comm->solo) {
         (void)ncclCommDestroy(comm->nc);
     }
+    for (int i = 0; i < comm->tcap; i++) (void)hipEventDestroy(comm->tev[i]);
+    free(comm->tev);
     free(comm);
 }
 
@@ -284,7 +361,7 @@ __global__ void allreduce_i32_kernel(int32_t* __restrict__ dst, const int32_t* _
     if (i < count) dst[i] = op_min ? min(dst[i], src[i]) : dst[i] + src[i];
 }
 
-int srt_coll_bcast(const srt_comm* c, void* buf, size_t bytes, int root, hipStream_t st) {
+static int bcast_impl(const srt_comm* c, void* buf, size_t bytes, int root, hipStream_t st) {
     if (c->solo) return root == c->rank ? solo_wire(c, 0, st) : solo_wire(c, bytes, st);
     if (!c->loop) {
         SRT_NCCLCHK(ncclBroadcast(buf, buf, bytes, ncclUint8, root, c->nc, st));
@@ -308,8 +385,8 @@ int srt_coll_bcast(const srt_comm* c, void* buf, size_t bytes, int root, hipStre
     return SRT_OK;
 }
 
-int srt_coll_allreduce_i32(const srt_comm* c, int32_t* buf, size_t count, int op_min,
-                           hipStream_t st) {
+static int allreduce_impl(const srt_comm* c, int32_t* buf, size_t count, int op_min,
+                          hipStream_t st) {
     /* ring all-reduce: 2 (R - 1) / R of the buffer in */
     if (c->solo)
         return solo_wire(c, 2 * (size_t)(c->nranks - 1) * count * sizeof(int32_t) / c->nranks, st);
@@ -349,9 +426,10 @@ int srt_coll_allreduce_i32(const srt_comm* c, int32_t* buf, size_t count, int op
 
 int srt_coll_group_begin(const srt_comm* c) {
     if (!c->loop && !c->solo) SRT_NCCLCHK(ncclGroupStart());
+    srt_comm* m = const_cast<srt_comm*>(c);
+    m->in_group = 1;
+    m->t_open = 0;
     if (c->solo) {
-        srt_comm* m = const_cast<srt_comm*>(c);
-        m->in_group = 1;
         m->group_bytes = 0;
         t_group_stream = nullptr;
     }
@@ -360,16 +438,22 @@ int srt_coll_group_begin(const srt_comm* c) {
 
 int srt_coll_group_end(const srt_comm* c) {
     if (!c->loop && !c->solo) SRT_NCCLCHK(ncclGroupEnd());
-    if (c->solo && c->in_group) {
-        srt_comm* m = const_cast<srt_comm*>(c);
-        m->in_group = 0;
-        if (t_group_stream) return solo_wire(c, m->group_bytes, t_group_stream);
+    srt_comm* m = const_cast<srt_comm*>(c);
+    const int was = m->in_group;
+    m->in_group = 0;
+    if (c->solo && was && t_group_stream) {
+        const int rc = solo_wire(c, m->group_bytes, t_group_stream);
+        if (rc) return rc;
+    }
+    if (was && m->t_open) { /* close the group's span on its first collective's stream */
+        m->t_open = 0;
+        return t_end(c, m->t_stream);
     }
     return SRT_OK;
 }
 
-int srt_coll_exchange(const srt_comm* c, void* const* send, const size_t* send_bytes,
-                      void* const* recv, const size_t* recv_bytes, hipStream_t st) {
+static int exchange_impl(const srt_comm* c, void* const* send, const size_t* send_bytes,
+                         void* const* recv, const size_t* recv_bytes, hipStream_t st) {
     const int me = c->rank, R = c->nranks;
     if (c->solo) {
         size_t in = 0;
@@ -430,12 +514,12 @@ int srt_comm_rank(const srt_comm* c) { return c ? c->rank : -1; }
 int srt_comm_is_solo(const srt_comm* c) { return c ? c->solo : 0; }
 int srt_comm_size(const srt_comm* c) { return c ? c->nranks : 0; }
 
-int srt_coll_allgather(const srt_comm* c, void* buf, size_t bytes, hipStream_t st) {
+static int allgather_impl(const srt_comm* c, void* buf, size_t bytes, hipStream_t st) {
     if (c->solo) return solo_wire(c, (size_t)(c->nranks - 1) * bytes, st);
     if (bytes == 0) return SRT_OK;
     if (c->loop) { /* every rank broadcasts its block in turn */
         for (int q = 0; q < c->nranks; q++) {
-            const int rc = srt_coll_bcast(c, (uint8_t*)buf + bytes * q, bytes, q, st);
+            const int rc = bcast_impl(c, (uint8_t*)buf + bytes * q, bytes, q, st);
             if (rc) return rc;
         }
         return SRT_OK;
@@ -444,8 +528,8 @@ int srt_coll_allgather(const srt_comm* c, void* buf, size_t bytes, hipStream_t s
     return SRT_OK;
 }
 
-extern "C" int srt_sparse_allgather(srt_comm* comm, int32_t n, int32_t rows_per_rank,
-                                    uint32_t* lat_all, double* rel_all, void* stream) {
+static int sparse_allgather_impl(srt_comm* comm, int32_t n, int32_t rows_per_rank,
+                                 uint32_t* lat_all, double* rel_all, void* stream) {
     if (!comm || n <= 0 || rows_per_rank <= 0 || !lat_all || !rel_all) {
         srt_set_error("srt_sparse_allgather: bad arguments");
         return SRT_E_ARG;
@@ -455,8 +539,8 @@ extern "C" int srt_sparse_allgather(srt_comm* comm, int32_t n, int32_t rows_per_
     if (comm->solo) return solo_wire(comm, (size_t)(comm->nranks - 1) * cnt * 12, st);
     if (comm->loop) { /* every rank broadcasts its block in turn */
         for (int q = 0; q < comm->nranks; q++) {
-            int rc = srt_coll_bcast(comm, lat_all + cnt * q, cnt * sizeof(uint32_t), q, st);
-            if (!rc) rc = srt_coll_bcast(comm, rel_all + cnt * q, cnt * sizeof(double), q, st);
+            int rc = bcast_impl(comm, lat_all + cnt * q, cnt * sizeof(uint32_t), q, st);
+            if (!rc) rc = bcast_impl(comm, rel_all + cnt * q, cnt * sizeof(double), q, st);
             if (rc) return rc;
         }
         return SRT_OK;
@@ -466,4 +550,40 @@ extern "C" int srt_sparse_allgather(srt_comm* comm, int32_t n, int32_t rows_per_
     SRT_NCCLCHK(ncclAllGather(rel_all + cnt * comm->rank, rel_all, cnt, ncclFloat64, comm->nc, st));
     SRT_NCCLCHK(ncclGroupEnd());
     return SRT_OK;
+}
+
+/* ---- timed entry points: each collective (or its group) is one span of ms_comm ----------- */
+#define SRT_TIMED(st, call)                       \
+    do {                                          \
+        int r_ = t_begin(c, st);                  \
+        if (!r_) r_ = (call);                     \
+        if (!r_) r_ = t_end(c, st);               \
+        return r_;                                \
+    } while (0)
+
+int srt_coll_bcast(const srt_comm* c, void* buf, size_t bytes, int root, hipStream_t st) {
+    SRT_TIMED(st, bcast_impl(c, buf, bytes, root, st));
+}
+
+int srt_coll_allreduce_i32(const srt_comm* c, int32_t* buf, size_t count, int op_min,
+                           hipStream_t st) {
+    SRT_TIMED(st, allreduce_impl(c, buf, count, op_min, st));
+}
+
+int srt_coll_exchange(const srt_comm* c, void* const* send, const size_t* send_bytes,
+                      void* const* recv, const size_t* recv_bytes, hipStream_t st) {
+    SRT_TIMED(st, exchange_impl(c, send, send_bytes, recv, recv_bytes, st));
+}
+
+int srt_coll_allgather(const srt_comm* c, void* buf, size_t bytes, hipStream_t st) {
+    SRT_TIMED(st, allgather_impl(c, buf, bytes, st));
+}
+
+extern "C" int srt_sparse_allgather(srt_comm* c, int32_t n, int32_t rows_per_rank,
+                                    uint32_t* lat_all, double* rel_all, void* stream) {
+    if (!c) {
+        srt_set_error("srt_sparse_allgather: bad arguments");
+        return SRT_E_ARG;
+    }
+    SRT_TIMED((hipStream_t)stream, sparse_allgather_impl(c, n, rows_per_rank, lat_all, rel_all, stream));
 }

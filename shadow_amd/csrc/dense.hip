@@ -1909,6 +1909,7 @@ int srt_dense_build_sharded_ms(srt_comm* comm, int32_t n, int32_t ld, int32_t di
     evpool_t* evp = NULL;
     if (stats && stats->time_kernels && (rc = evpool_begin(&evp, ld / B))) return rc;
     shard_ctx ctx = {comm, ld};
+    srt_comm_timing(comm, stats && stats->time_kernels);
     int exact = 0, enc = SRT_DENC_U32;
     const char* sym_env = getenv("SRT_FW_SYM");
     /* symmetric rounds up to 1,024 tile columns (fw16.hip SYM_TMAX, the panel-position table) */
@@ -1984,7 +1985,9 @@ int srt_dense_build_sharded_ms(srt_comm* comm, int32_t n, int32_t ld, int32_t di
         stats->ms_post = c;
         stats->ms_total = a + c;
         if (evp && (rc = evpool_sum(evp, e2, stats))) return rc;
+        stats->ms_comm = srt_comm_timing_ms(comm);
     }
+    srt_comm_timing(comm, 0);
     return SRT_OK;
 }
 

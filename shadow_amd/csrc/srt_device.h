@@ -41,6 +41,10 @@ int srt_coll_exchange(const srt_comm* c, void* const* send, const size_t* send_b
 int srt_comm_rank(const srt_comm* c);
 int srt_comm_is_solo(const srt_comm* c); /* timing-only communicator (srt_comm_init_solo) */
 int srt_comm_size(const srt_comm* c);
+/* ms_comm: on = 1 starts timing every collective (or group) of c with an event pair;
+ * srt_comm_timing_ms waits for the last one and returns the summed spans (ms) */
+void srt_comm_timing(const srt_comm* c, int on);
+double srt_comm_timing_ms(const srt_comm* c);
 
 /* pivot-block edge of the blocked Floyd-Warshall and the output-tile edge of its kernels */
 #define SRT_FW_B 64
