@@ -187,7 +187,9 @@ int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t 
                           uint32_t* lat_rows, double* rel_rows, void* stream,
                           srt_build_stats* stats);
 /* Rows of an arbitrary source list (srcs: nsrc device ints; row r = source srcs[r], stride n),
- * e.g. the attached vertices. lat_ms_rows (optional): the f64 path-order ms rows. */
+ * e.g. the attached vertices. lat_ms_rows (optional): the f64 path-order ms rows -- required when
+ * the graph's distances may pass the u32 range (SRT_E_RANGE without it; srt_sparse_graph_rows
+ * refuses such a graph the same way). */
 int srt_sparse_graph_rows_list(const srt_sparse_graph* g, int32_t nsrc, const int32_t* srcs,
                                uint32_t* lat_rows, double* rel_rows, double* lat_ms_rows,
                                void* stream, srt_build_stats* stats);
@@ -255,11 +257,18 @@ void srt_pair_order_free(srt_pair_order* po);
 /* v joins the attached set (verticesWithAttachedHosts, topology.c:2231); idempotent */
 int srt_pair_order_attach(srt_pair_order* po, int32_t v);
 /* lookup (s, t): the source vertex of the path served (s or t), after recording the run or store
- * a miss causes; SRT_E_UNATTACHED if an end is not attached */
+ * a miss causes; SRT_E_UNATTACHED if an end is not attached, SRT_E_NOPATH if no stored path
+ * joins them (neither end reaches the other) */
 int32_t srt_pair_order_lookup(srt_pair_order* po, int32_t s, int32_t t, srt_pair_store_fn on_store,
                               void* ctx);
 /* the same without recording anything: -1 while the pair is not stored */
 int32_t srt_pair_order_peek(srt_pair_order* po, int32_t s, int32_t t);
+/* optional reachability predicate (1: s reaches t); a source run stores only the targets it reaches
+ * (topology.c:1744-1753), so on a directed graph that is not strongly connected a pair is decided
+ * by the first run from an end that reaches the other. NULL (the default): every pair reachable.
+ * Set before the first lookup. */
+typedef int (*srt_pair_reach_fn)(void* ctx, int32_t s, int32_t t);
+void srt_pair_order_set_reach(srt_pair_order* po, srt_pair_reach_fn fn, void* ctx);
 /* recorded source runs of v (one per attach epoch it ran in) */
 int32_t srt_pair_order_runs(srt_pair_order* po, int32_t v);
 

@@ -92,6 +92,8 @@ class LazyPathCache:
             if t == s:  # a one-vertex result path: skipped (:1744-1753)
                 continue
             latency = self.lat_ms[s, t]
+            if math.isinf(latency):  # unreachable: igraph's empty path is skipped (:1744-1753)
+                continue
             if latency == 0:  # :1787-1791
                 latency = 1.0
             self._store(False, s, t, latency, self.rel[s, t])

@@ -114,6 +114,7 @@ SIGNATURES = {
     "srt_pair_order_lookup": (_I32, [_VP, _I32, _I32, _VP, _VP]),
     "srt_pair_order_peek": (_I32, [_VP, _I32, _I32]),
     "srt_pair_order_runs": (_I32, [_VP, _I32]),
+    "srt_pair_order_set_reach": (None, [_VP, _VP, _VP]),
     "srt_device_count": (ctypes.c_int, []),
     "srt_device_sync": (ctypes.c_int, [_I32]),
     # topology.h (reference signatures)
@@ -154,6 +155,8 @@ SIGNATURES = {
     "srt_topology_last_stats": (ctypes.c_int, [_VP, _VP]),
 }
 
+# srt_pair_reach_fn: (ctx, s, t) -> 1 if s reaches t
+PAIR_REACH_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32)
 # srt_pair_store_fn: (ctx, src, targets, count)
 PAIR_STORE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int32,
                                  ctypes.POINTER(ctypes.c_int32), ctypes.c_int32)

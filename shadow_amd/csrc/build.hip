@@ -563,7 +563,6 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
         return SRT_E_ARG;
     }
     const int nsrc = src_end - src_begin;
-    (void)srt_state_slot(); /* also keeps the device's scratch pool mapped (comm.hip) */
     if (g->wide) { /* distances may pass u32 quanta: the u64 rows (wide.hip) */
         struct evs {
             hipEvent_t e[2] = {nullptr, nullptr};
@@ -699,7 +698,7 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
         }
     } sc;
     sc.st = st;
-    SRT_HIPCHK(hipMallocAsync((void**)&sc.ovf, (size_t)nsrc * sizeof(int), st));
+    SRT_HIPCHK(srt_malloc_async((void**)&sc.ovf, (size_t)nsrc * sizeof(int), st));
     int* const ovf = sc.ovf;
     SRT_HIPCHK(hipEventCreate(&sc.ev[0]));
     SRT_HIPCHK(hipEventCreate(&sc.ev[1]));
@@ -714,7 +713,7 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
     if (ms) {
         const int nb = (int)(ms_bsrc.size() / 64);
         const size_t bb = ms_bsrc.size() * sizeof(int32_t);
-        SRT_HIPCHK(hipMallocAsync((void**)&ms_dev, 2 * bb, st));
+        SRT_HIPCHK(srt_malloc_async((void**)&ms_dev, 2 * bb, st));
         SRT_HIPCHK(hipMemcpyAsync(ms_dev, ms_bsrc.data(), bb, hipMemcpyHostToDevice, st));
         SRT_HIPCHK(hipMemcpyAsync(ms_dev + ms_bsrc.size(), ms_brow.data(), bb,
                                   hipMemcpyHostToDevice, st));
@@ -744,9 +743,9 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
             int32_t* dr = NULL;
             uint32_t* tl = NULL;
             double* tr = NULL;
-            SRT_HIPCHK(hipMallocAsync((void**)&dr, 2 * (size_t)nr * 4, st));
-            SRT_HIPCHK(hipMallocAsync((void**)&tl, (size_t)nr * g->n * 4, st));
-            SRT_HIPCHK(hipMallocAsync((void**)&tr, (size_t)nr * g->n * 8, st));
+            SRT_HIPCHK(srt_malloc_async((void**)&dr, 2 * (size_t)nr * 4, st));
+            SRT_HIPCHK(srt_malloc_async((void**)&tl, (size_t)nr * g->n * 4, st));
+            SRT_HIPCHK(srt_malloc_async((void**)&tr, (size_t)nr * g->n * 8, st));
             SRT_HIPCHK(hipMemcpyAsync(dr, rs.data(), (size_t)nr * 4, hipMemcpyHostToDevice, st));
             SRT_HIPCHK(hipMemcpyAsync(dr + nr, ms_rest.data(), (size_t)nr * 4,
                                       hipMemcpyHostToDevice, st));
@@ -875,6 +874,11 @@ extern "C" int srt_sparse_graph_rows(const srt_sparse_graph* g, int32_t src_begi
         srt_set_error("srt_sparse_graph_rows: null graph");
         return SRT_E_ARG;
     }
+    if (g->wide) { /* the u32 rows would saturate: only the f64 ms rows carry these latencies */
+        srt_set_error("srt_sparse_graph_rows: shortest-path latencies may pass the u32 range; use "
+                      "srt_sparse_graph_rows_list with lat_ms_rows");
+        return SRT_E_RANGE;
+    }
     return sparse_rows(g, src_begin, src_end, NULL, lat_rows, rel_rows, NULL, (hipStream_t)stream,
                        stats);
 }
@@ -886,6 +890,11 @@ extern "C" int srt_sparse_graph_rows_list(const srt_sparse_graph* g, int32_t nsr
     if (!g || nsrc <= 0 || !srcs || !lat_rows || !rel_rows) {
         srt_set_error("srt_sparse_graph_rows_list: bad arguments");
         return SRT_E_ARG;
+    }
+    if (g->wide && !lat_ms_rows) { /* the u32 rows would saturate (SRT_INF - 1) */
+        srt_set_error("srt_sparse_graph_rows_list: shortest-path latencies may pass the u32 range; "
+                      "the f64 lat_ms_rows output is required");
+        return SRT_E_RANGE;
     }
     return sparse_rows(g, 0, nsrc, srcs, lat_rows, rel_rows, lat_ms_rows, (hipStream_t)stream, stats);
 }

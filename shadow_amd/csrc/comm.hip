@@ -49,26 +49,46 @@ struct srt_comm {
 
 static thread_local int t_vslot = -1;
 void srt_set_virtual_slot(int rank) { t_vslot = rank; }
-/* The builds' stream-ordered scratch (hipMallocAsync / hipFreeAsync) comes from the device's
- * default pool. With its default release threshold (0) the pool hands freed memory back at every
- * synchronisation, so each build re-maps its scratch: ~0.2 ms of a 0.9-ms C2 build. The pool keeps
- * it instead (set once per device, on the first build there). */
-static int g_pool_kept[64];
-static void keep_pool(int dev) {
-    if (__atomic_load_n(&g_pool_kept[dev & 63], __ATOMIC_RELAXED)) return;
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-        uint64_t keep = ~0ull;
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+/* The builds' stream-ordered scratch (srt_malloc_async / hipFreeAsync) comes from a private
+ * pool per device, not the device's default pool: its release threshold (SRT_POOL_KEEP) keeps
+ * up to that much freed scratch mapped across synchronisations, so a small build does not re-map
+ * its scratch each time (~0.2 ms of a 0.9-ms C2 build), while the caller's own stream-ordered
+ * frees (the default pool) keep the default release behaviour, and anything above the threshold
+ * goes back to the driver at the next synchronisation. */
+#define SRT_POOL_KEEP (4ull << 30)
+static hipMemPool_t g_pool[64];
+static pthread_mutex_t g_pool_mu = PTHREAD_MUTEX_INITIALIZER;
+
+hipMemPool_t srt_scratch_pool(void) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    hipMemPool_t p = __atomic_load_n(&g_pool[dev & 63], __ATOMIC_ACQUIRE);
+    if (p) return p;
+    pthread_mutex_lock(&g_pool_mu);
+    p = g_pool[dev & 63];
+    if (!p) {
+        hipMemPoolProps props;
+        memset(&props, 0, sizeof(props));
+        props.allocType = hipMemAllocationTypePinned;
+        props.handleTypes = hipMemHandleTypeNone;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = dev;
+        if (hipMemPoolCreate(&p, &props) == hipSuccess) {
+            uint64_t keep = SRT_POOL_KEEP;
+            (void)hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &keep);
+        } else {
+            (void)hipGetLastError();
+            (void)hipDeviceGetDefaultMemPool(&p, dev); /* still correct, only without the cap */
+        }
+        __atomic_store_n(&g_pool[dev & 63], p, __ATOMIC_RELEASE);
     }
-    (void)hipGetLastError();
-    __atomic_store_n(&g_pool_kept[dev & 63], 1, __ATOMIC_RELAXED);
+    pthread_mutex_unlock(&g_pool_mu);
+    return p;
 }
 
 int srt_state_slot(void) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    keep_pool(dev);
     if (t_vslot >= 0) return 64 + (t_vslot & 63);
     return dev & 63;
 }

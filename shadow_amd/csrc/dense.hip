@@ -1561,7 +1561,7 @@ int srt_dense_rows_build_device(int32_t n, int32_t ld, int32_t nsub, const int32
                 if (x) (void)hipFreeAsync(x, s);
         }
         int get(int k, size_t bytes) {
-            if (hipMallocAsync(&p[k], bytes ? bytes : 16, s) != hipSuccess) {
+            if (srt_malloc_async(&p[k], bytes ? bytes : 16, s) != hipSuccess) {
                 (void)hipGetLastError();
                 srt_set_error("dense rows build: scratch of %zu MiB failed", bytes >> 20);
                 return SRT_E_NOMEM;

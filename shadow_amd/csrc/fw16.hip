@@ -2504,7 +2504,7 @@ int srt_fw16_rows(int n, int ld, int nsub, const int32_t* dverts, const uint32_t
     rows_init_kernel<<<dim3(srt_ceil_div(ld, 2048), nsp), 256, 0, st>>>(ld, nsub, dverts, w16, ds, CAP_F);
     SRT_HIPCHK(hipGetLastError());
     unsigned long long* dsum = nullptr;
-    SRT_HIPCHK(hipMallocAsync((void**)&dsum, sizeof(unsigned long long), st));
+    SRT_HIPCHK(srt_malloc_async((void**)&dsum, sizeof(unsigned long long), st));
     struct freer {
         unsigned long long* p;
         hipStream_t s;
@@ -2605,7 +2605,7 @@ static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStrea
     fw16_init_kernel<<<dim3(srt_ceil_div(ld, 2048), ld), 256, 0, st>>>(n, ld, 0, w, d, CAP_F);
     SRT_HIPCHK(hipGetLastError());
     unsigned long long* dsum = nullptr;
-    SRT_HIPCHK(hipMallocAsync((void**)&dsum, 2 * sizeof(unsigned long long), st));
+    SRT_HIPCHK(srt_malloc_async((void**)&dsum, 2 * sizeof(unsigned long long), st));
     struct freer {
         unsigned long long* p;
         hipStream_t s;
@@ -2620,7 +2620,7 @@ static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStrea
     const int nq8 = ld / 256, tail = (ld % 256) ? 1 : 0;
     int* sflag = reinterpret_cast<int*>(dsum); /* four change flags (dsum holds 16 bytes) */
     u16* part = nullptr;
-    if (split) SRT_HIPCHK(hipMallocAsync((void**)&part, (size_t)(nq8 + tail) * ld * ld * 2, st));
+    if (split) SRT_HIPCHK(srt_malloc_async((void**)&part, (size_t)(nq8 + tail) * ld * ld * 2, st));
     struct freer2 {
         u16* p;
         hipStream_t s;

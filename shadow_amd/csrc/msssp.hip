@@ -537,7 +537,7 @@ int srt_msssp_rows(int n, int directed, const int2* orp, const uint2* ocw, const
     const char* penv = getenv("SRT_MSSSP_PROF");
     unsigned long long* prof = NULL;
     if (penv && atoi(penv) > 0 &&
-        hipMallocAsync((void**)&prof, (size_t)nbatch * MS_PROF * sizeof(unsigned long long), st) !=
+        srt_malloc_async((void**)&prof, (size_t)nbatch * MS_PROF * sizeof(unsigned long long), st) !=
             hipSuccess) {
         (void)hipGetLastError();
         prof = NULL;

@@ -22,6 +22,14 @@
  * or y made while both were attached. Reads are lock-free (a seqlock over the per-vertex run
  * lists); runs are recorded under a mutex. Direct mode keeps two bits per unordered pair (stored,
  * and which end stored it), set by compare-and-swap.
+ *
+ * Unreachable targets: a source run stores only the targets it reaches -- igraph returns an empty
+ * path for the others and the store loop skips it (:1744-1753). With a reachability predicate
+ * (srt_pair_order_set_reach), a run of x decides {x, y} only when x reaches y, so on a directed
+ * graph that is not strongly connected the pair is stored by the first run from an end that
+ * reaches the other; a pair neither end reaches is never stored (SRT_E_NOPATH, the reference's
+ * panic at :1970-1976). Without a predicate every pair is reachable, which topology_new guarantees
+ * (it refuses graphs that are not strongly connected, :674).
  */
 #define _GNU_SOURCE
 #include <pthread.h>
@@ -39,9 +47,12 @@ typedef struct {
     int64_t seq;   /* global order of runs */
 } po_run;
 
+/* A vertex's runs, appended in place: an entry is written before the count that publishes it, and
+ * never changes after. A full list is copied into one of twice the capacity and the old one
+ * retired, so a vertex's lists total O(runs) memory. */
 typedef struct {
-    int32_t count;
-    int32_t pad;
+    _Atomic int32_t count;
+    int32_t cap;
     po_run r[];
 } po_list;
 
@@ -60,7 +71,19 @@ struct srt_pair_order {
     int32_t* scratch;            /* targets stored by one run */
     atomic_uchar* self_done;     /* (v, v) stored */
     _Atomic uint64_t* pairbits;  /* direct mode: 2 bits per unordered pair {a < b} */
+    srt_pair_reach_fn reach;     /* NULL: every pair reachable */
+    void* reach_ctx;
 };
+
+void srt_pair_order_set_reach(srt_pair_order* po, srt_pair_reach_fn fn, void* ctx) {
+    if (!po) return;
+    po->reach = fn;
+    po->reach_ctx = ctx;
+}
+
+static int reaches(const srt_pair_order* po, int32_t s, int32_t t) {
+    return !po->reach || po->reach(po->reach_ctx, s, t);
+}
 
 srt_pair_order* srt_pair_order_new(int32_t n, int32_t directed, int32_t per_source) {
     if (n <= 0) return NULL;
@@ -126,7 +149,8 @@ int srt_pair_order_attach(srt_pair_order* po, int32_t v) {
 /* seq of the first run in L made while both ends were attached (epoch >= a), or INT64_MAX */
 static int64_t valid_run(const po_list* L, int32_t a) {
     if (!L) return INT64_MAX;
-    for (int32_t i = 0; i < L->count; i++)
+    const int32_t cnt = atomic_load_explicit(&((po_list*)L)->count, memory_order_acquire);
+    for (int32_t i = 0; i < cnt; i++)
         if (L->r[i].epoch >= a) return L->r[i].seq;
     return INT64_MAX;
 }
@@ -135,12 +159,17 @@ static int32_t att_of(const srt_pair_order* po, int32_t v) {
     return atomic_load_explicit(&po->att_epoch[v], memory_order_acquire);
 }
 
-/* per-source mode: the end whose run stored {x, y} (-1: not stored yet) */
+/* per-source mode: the end whose run stored {x, y} (-1: not stored yet); a run stores the pair
+ * only if its source reaches the other end */
 static int32_t stored_from_raw(const srt_pair_order* po, int32_t x, int32_t y) {
     const int32_t ax = att_of(po, x), ay = att_of(po, y);
     const int32_t a = ax > ay ? ax : ay;
-    const int64_t sx = valid_run(atomic_load_explicit(&po->runs[x], memory_order_acquire), a);
-    const int64_t sy = valid_run(atomic_load_explicit(&po->runs[y], memory_order_acquire), a);
+    const int64_t sx = reaches(po, x, y)
+                           ? valid_run(atomic_load_explicit(&po->runs[x], memory_order_acquire), a)
+                           : INT64_MAX;
+    const int64_t sy = reaches(po, y, x)
+                           ? valid_run(atomic_load_explicit(&po->runs[y], memory_order_acquire), a)
+                           : INT64_MAX;
     if (sx == INT64_MAX && sy == INT64_MAX) return -1;
     return sx < sy ? x : y;
 }
@@ -160,8 +189,9 @@ static int32_t stored_from(srt_pair_order* po, int32_t x, int32_t y) {
 }
 
 static int32_t last_epoch(const srt_pair_order* po, int32_t v) {
-    const po_list* L = atomic_load_explicit(&po->runs[v], memory_order_acquire);
-    return L && L->count ? L->r[L->count - 1].epoch : -1;
+    po_list* L = atomic_load_explicit(&po->runs[v], memory_order_acquire);
+    const int32_t cnt = L ? atomic_load_explicit(&L->count, memory_order_acquire) : 0;
+    return cnt ? L->r[cnt - 1].epoch : -1;
 }
 
 /* Record a source run of x in the current epoch and list the targets it stores (caller holds
@@ -169,40 +199,48 @@ static int32_t last_epoch(const srt_pair_order* po, int32_t v) {
 static int32_t record_run(srt_pair_order* po, int32_t x) {
     const int32_t e = atomic_load_explicit(&po->epoch, memory_order_acquire);
     po_list* old = atomic_load_explicit(&po->runs[x], memory_order_relaxed);
-    const int32_t cnt = old ? old->count : 0;
-    po_list* L = (po_list*)malloc(sizeof(po_list) + (size_t)(cnt + 1) * sizeof(po_run));
-    if (!L) return SRT_E_NOMEM;
-    if (old && po->nretired == po->cap_retired) {
-        const size_t nc = po->cap_retired ? 2 * po->cap_retired : 64;
-        po_list** nr = (po_list**)realloc(po->retired, nc * sizeof(po_list*));
-        if (!nr) {
-            free(L);
-            return SRT_E_NOMEM;
+    const int32_t cnt = old ? atomic_load_explicit(&old->count, memory_order_relaxed) : 0;
+    po_list* L = old;
+    if (!old || cnt == old->cap) { /* grow: a copy with twice the capacity */
+        const int32_t cap = cnt ? 2 * cnt : 4;
+        L = (po_list*)malloc(sizeof(po_list) + (size_t)cap * sizeof(po_run));
+        if (!L) return SRT_E_NOMEM;
+        if (old && po->nretired == po->cap_retired) {
+            const size_t nc = po->cap_retired ? 2 * po->cap_retired : 64;
+            po_list** nr = (po_list**)realloc(po->retired, nc * sizeof(po_list*));
+            if (!nr) {
+                free(L);
+                return SRT_E_NOMEM;
+            }
+            po->retired = nr;
+            po->cap_retired = nc;
         }
-        po->retired = nr;
-        po->cap_retired = nc;
+        L->cap = cap;
+        if (cnt) memcpy(L->r, old->r, (size_t)cnt * sizeof(po_run));
+        atomic_init(&L->count, cnt);
     }
-    L->count = cnt + 1;
-    if (cnt) memcpy(L->r, old->r, (size_t)cnt * sizeof(po_run));
     const int64_t seq = ++po->next_seq;
     L->r[cnt].epoch = e;
     L->r[cnt].pad = 0;
     L->r[cnt].seq = seq;
-    /* seqlock write: readers retry across the swap */
+    /* seqlock write: readers retry across the publication */
     atomic_fetch_add_explicit(&po->version, 1, memory_order_relaxed);
     atomic_thread_fence(memory_order_release);
-    atomic_store_explicit(&po->runs[x], L, memory_order_release);
+    if (L != old) atomic_store_explicit(&po->runs[x], L, memory_order_release);
+    atomic_store_explicit(&L->count, cnt + 1, memory_order_release);
     atomic_fetch_add_explicit(&po->version, 1, memory_order_release);
-    if (old) po->retired[po->nretired++] = old;
-    /* targets stored by this run: attached y != x whose pair this run decides */
+    if (old && L != old) po->retired[po->nretired++] = old;
+    /* targets stored by this run: attached y != x, reached from x, whose pair this run decides */
     int32_t k = 0;
     for (int32_t i = 0; i < po->natt; i++) {
         const int32_t y = po->att_list[i];
-        if (y == x) continue;
+        if (y == x || !reaches(po, x, y)) continue;
         const int32_t ay = att_of(po, y), ax = att_of(po, x);
         const int32_t a = ax > ay ? ax : ay;
         if (valid_run(L, a) != seq) continue; /* stored by an earlier run of x, or y not attached */
-        if (valid_run(atomic_load_explicit(&po->runs[y], memory_order_relaxed), a) < seq) continue;
+        if (reaches(po, y, x) &&
+            valid_run(atomic_load_explicit(&po->runs[y], memory_order_relaxed), a) < seq)
+            continue;
         po->scratch[k++] = y;
     }
     return k;
@@ -261,7 +299,7 @@ int32_t srt_pair_order_lookup(srt_pair_order* po, int32_t s, int32_t t, srt_pair
         f = stored_from_raw(po, s, t);
     }
     pthread_mutex_unlock(&po->mu);
-    return f;
+    return f < 0 ? SRT_E_NOPATH : f; /* neither end reaches the other (:1970-1976) */
 }
 
 int32_t srt_pair_order_peek(srt_pair_order* po, int32_t s, int32_t t) {
@@ -280,6 +318,6 @@ int32_t srt_pair_order_peek(srt_pair_order* po, int32_t s, int32_t t) {
 
 int32_t srt_pair_order_runs(srt_pair_order* po, int32_t v) {
     if (!po || v < 0 || v >= po->n || !po->per_source) return 0;
-    const po_list* L = atomic_load(&po->runs[v]);
-    return L ? L->count : 0;
+    po_list* L = atomic_load(&po->runs[v]);
+    return L ? atomic_load(&L->count) : 0;
 }

@@ -324,7 +324,7 @@ int srt_sparse_block_rows(int32_t n, const int32_t* rowptr, const int32_t* col, 
         const int slots = std::min(nsrc, 2 * cus);
         const size_t slot_words = srt_sparse_lds_bytes(n) / 4 + 64; /* 256-B separated slots */
         uint32_t* ws = NULL;
-        if (hipMallocAsync((void**)&ws, (size_t)slots * slot_words * 4, st) != hipSuccess) {
+        if (srt_malloc_async((void**)&ws, (size_t)slots * slot_words * 4, st) != hipSuccess) {
             (void)hipGetLastError();
             srt_set_error("srt_sparse_build_device: workspace of %zu MiB failed",
                           (size_t)slots * slot_words * 4 >> 20);

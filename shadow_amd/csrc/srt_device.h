@@ -25,6 +25,10 @@
  * one device inside one process (srt_build_tables_multi with SRT_VIRTUAL_RANKS, comm.hip). */
 #define SRT_STATE_SLOTS 128
 int srt_state_slot(void);
+/* stream-ordered scratch from the library's private pool of the current device (comm.hip) */
+hipMemPool_t srt_scratch_pool(void);
+#define srt_malloc_async(ptr, bytes, st) \
+    hipMallocFromPoolAsync((void**)(ptr), (bytes), srt_scratch_pool(), (st))
 void srt_set_virtual_slot(int rank); /* -1: back to the device slot */
 
 /* Collectives over an srt_comm: RCCL, or (virtual ranks on one device) device-to-device copies

@@ -169,7 +169,7 @@ int srt_path_ms_rows(int n, int nrows, const int32_t* srcs, int src_begin, const
     const int grid = path_grid(nrows);
     const size_t lds = 2 * (size_t)((n + 31) / 32) * sizeof(uint32_t);
     int32_t* pws = NULL;
-    if (!pred && hipMallocAsync((void**)&pws, (size_t)grid * n * sizeof(int32_t), st) != hipSuccess) {
+    if (!pred && srt_malloc_async((void**)&pws, (size_t)grid * n * sizeof(int32_t), st) != hipSuccess) {
         (void)hipGetLastError();
         srt_set_error("path-order ms pass: scratch of %zu MiB failed",
                       ((size_t)grid * n * sizeof(int32_t)) >> 20);
@@ -363,7 +363,7 @@ int srt_tie_count_rows(int n, int nrows, const int32_t* srcs, int src_begin, con
                        int64_t* tied, hipStream_t st) {
     if (nrows <= 0) return SRT_OK;
     unsigned long long* d = NULL;
-    SRT_HIPCHK(hipMallocAsync((void**)&d, sizeof(*d), st));
+    SRT_HIPCHK(srt_malloc_async((void**)&d, sizeof(*d), st));
     SRT_HIPCHK(hipMemsetAsync(d, 0, sizeof(*d), st));
     dim3 g((unsigned)(srt_ceil_div(n, 256) < 8 ? srt_ceil_div(n, 256) : 8),
            (unsigned)(nrows < 8192 ? nrows : 8192));

@@ -173,9 +173,9 @@ int srt_wide_rows(int n, const int32_t* rp, const int32_t* col, const uint32_t* 
     const int grid = std::min(chunk, 2 * cus);
     uint64_t* D = nullptr;
     int32_t *P = nullptr, *Q = nullptr;
-    SRT_HIPCHK(hipMallocAsync((void**)&D, (size_t)chunk * n * sizeof(uint64_t), st));
-    SRT_HIPCHK(hipMallocAsync((void**)&P, (size_t)chunk * n * sizeof(int32_t), st));
-    SRT_HIPCHK(hipMallocAsync((void**)&Q, (size_t)grid * n * sizeof(int32_t), st));
+    SRT_HIPCHK(srt_malloc_async((void**)&D, (size_t)chunk * n * sizeof(uint64_t), st));
+    SRT_HIPCHK(srt_malloc_async((void**)&P, (size_t)chunk * n * sizeof(int32_t), st));
+    SRT_HIPCHK(srt_malloc_async((void**)&Q, (size_t)grid * n * sizeof(int32_t), st));
     const size_t lds = 2 * (size_t)((n + 31) / 32) * sizeof(uint32_t);
     SRT_HIPCHK(hipFuncSetAttribute((const void*)wide_sssp_kernel,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -351,7 +351,7 @@ int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, con
     if (slots > (size_t)nsrc) slots = nsrc;
     if (slots < 1) slots = 1;
     uint32_t* ws = NULL;
-    if (hipMallocAsync((void**)&ws, slots * per_slot, st) != hipSuccess) {
+    if (srt_malloc_async((void**)&ws, slots * per_slot, st) != hipSuccess) {
         (void)hipGetLastError();
         srt_set_error("wsssp: bucket workspace of %zu MiB failed", (slots * per_slot) >> 20);
         return SRT_E_NOMEM;
@@ -896,7 +896,7 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     g_sparse_form = 4 | (inv ? 0 : 1) | (cmp ? 2 : 0);
     void* ca = NULL;
     const size_t arc_bytes = cmp ? sizeof(uint2) : sizeof(uint4);
-    if (hipMallocAsync(&ca, ((size_t)last.y + 1) * arc_bytes, st) != hipSuccess) {
+    if (srt_malloc_async(&ca, ((size_t)last.y + 1) * arc_bytes, st) != hipSuccess) {
         (void)hipGetLastError();
         srt_set_error("wgsssp: arc array of %d arcs failed", last.y);
         return SRT_E_NOMEM;
@@ -911,7 +911,7 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     size_t slots = (size_t)cus; /* one workgroup per CU: the packed row takes most of the LDS */
     if (slots > (size_t)nsrc) slots = nsrc;
     uint32_t* ws = NULL;
-    if (hipMallocAsync((void**)&ws, slots * (slot_words + 2) * sizeof(uint32_t), st) != hipSuccess) {
+    if (srt_malloc_async((void**)&ws, slots * (slot_words + 2) * sizeof(uint32_t), st) != hipSuccess) {
         (void)hipGetLastError();
         (void)hipFreeAsync(ca, st);
         srt_set_error("wgsssp: workspace of %zu MiB failed", (slots * slot_words * 4) >> 20);

@@ -102,6 +102,20 @@ def test_wide_refusals(gpu):
                             want_ms=True)
     with pytest.raises(RuntimeError, match="SRT_E_RANGE"):
         build_tables_subset(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss, algo=ALGO_AUTO)
+    # the device-row entry points without an f64 ms output (they used to saturate)
+    import torch
+    from shadow_amd.topology import SparseGraph
+    sg = SparseGraph(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss, device=0)
+    try:
+        lat = torch.empty((4, g.n), dtype=torch.int32, device="cuda")
+        rel = torch.empty((4, g.n), dtype=torch.float64, device="cuda")
+        srcs = torch.arange(4, dtype=torch.int32, device="cuda")
+        with pytest.raises(RuntimeError, match="SRT_E_RANGE"):
+            sg.rows(0, 4, lat.data_ptr(), rel.data_ptr())
+        with pytest.raises(RuntimeError, match="SRT_E_RANGE"):
+            sg.rows_list(srcs.data_ptr(), 4, lat.data_ptr(), rel.data_ptr())
+    finally:
+        sg.free()
 
 
 @pytest.mark.parametrize("directed", [False, True])

@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 from oracle.lazy_cache import LazyPathCache
-from shadow_amd._lib import PAIR_STORE_FN, lib
+from shadow_amd._lib import PAIR_REACH_FN, PAIR_STORE_FN, lib
 
 
 class _Runahead:
@@ -31,14 +31,21 @@ class _Runahead:
             self.minimum = best
 
 
-def _replay(n, directed, use_sp, seed, ops, late_attach):
+def _replay(n, directed, use_sp, seed, ops, late_attach, oneway=False):
     rng = np.random.default_rng(seed)
     lat = rng.integers(1, 50, (n, n)).astype(np.float64)  # ms; ties on purpose
     rel = rng.random((n, n))
+    if oneway:
+        # two strongly connected halves A = [0, n/2), B = [n/2, n) joined by one-way arcs A -> B:
+        # no vertex of B reaches A (the oracle's rows hold INFINITY there)
+        lat[n // 2:, :n // 2] = np.inf
     sim = LazyPathCache({"lat_ms": lat, "rel": rel}, directed, use_sp)
     L = lib()
     po = L.srt_pair_order_new(n, int(directed), int(use_sp))
     assert po
+    reach_cb = PAIR_REACH_FN(lambda _c, s, t: int(np.isfinite(lat[s, t])))
+    if oneway:
+        L.srt_pair_order_set_reach(po, reach_cb, None)
     ra = _Runahead(lat)
     cb = PAIR_STORE_FN(ra)
     hosts = {}
@@ -58,8 +65,15 @@ def _replay(n, directed, use_sp, seed, ops, late_attach):
                 L.srt_pair_order_attach(po, hosts[h])
                 continue
             a, b = (int(x) for x in rng.choice(list(hosts), 2))
-            p = sim.path_entry(a, b)
+            try:
+                p = sim.path_entry(a, b)
+            except RuntimeError:  # the reference's panic: no stored path joins them
+                p = None
             f = L.srt_pair_order_lookup(po, hosts[a], hosts[b], cb, None)
+            if p is None:
+                assert f == -8, (k, hosts[a], hosts[b], f)  # SRT_E_NOPATH
+                assert ra.minimum == sim.minimum_path_latency, k
+                continue
             assert f == p.src, (k, hosts[a], hosts[b], f, p.src)
             assert (hosts[b] if f == hosts[a] else hosts[a]) == p.dst
             assert ra.minimum == sim.minimum_path_latency, k
@@ -90,6 +104,33 @@ def test_pair_order_matches_lazy_cache(directed, use_sp, late_attach):
         sim = _replay(40, directed, use_sp, 100 * seed + 7, 1500, late_attach)
         if use_sp:
             assert sim.source_runs > 0
+
+
+@pytest.mark.parametrize("late_attach", [False, True])
+def test_pair_order_unreachable_targets(late_attach):
+    """a source run stores only the targets it reaches (topology.c:1744-1753). On a
+    directed graph with one-way reachability, the pair {s, t} (t unreachable from s) is stored by
+    t's run even when s ran first, and a lookup whose ends do not reach each other either way
+    finds no path."""
+    for seed in range(4):
+        _replay(40, True, True, 31 * seed + 5, 1500, late_attach, oneway=True)
+
+
+def test_pair_order_unreachable_small():
+    L = lib()
+    po = L.srt_pair_order_new(3, 1, 1)
+    reach = PAIR_REACH_FN(lambda _c, s, t: int(not (s == 1 and t == 0)))  # 1 does not reach 0
+    L.srt_pair_order_set_reach(po, reach, None)
+    try:
+        for v in range(3):
+            L.srt_pair_order_attach(po, v)
+        assert L.srt_pair_order_lookup(po, 1, 2, None, None) == 1  # source 1 runs first
+        assert L.srt_pair_order_peek(po, 1, 0) == -1               # ... but cannot store {0, 1}
+        assert L.srt_pair_order_lookup(po, 0, 2, None, None) == 0  # source 0 runs
+        assert L.srt_pair_order_peek(po, 1, 0) == 0                # {0, 1} is 0's path
+        assert L.srt_pair_order_lookup(po, 1, 0, None, None) == 0  # served 0 -> 1
+    finally:
+        L.srt_pair_order_free(po)
 
 
 def test_pair_order_directed_reverse_serving():
