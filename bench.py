@@ -287,6 +287,8 @@ def run_dense(c: Ctx, wl):
     # 4: u16 + f16-compare mins on upper-triangle tiles (undirected), 3: the same on every tile,
     # 2: u16 pk_min, 1: u32
     enc = int(stats[-1].dist_enc)
+    if enc == 12:
+        return dense_levels_tail(c, wl, step, elapsed, stats, lat, rel, nr, ld)
     s_d = 4 if enc == 1 else 2
     # VALU issue model per wave64 relaxation (cycles per SIMD): full-rate ops (v_add_u32) issue in
     # 2 cycles, packed / 3-input ops (v_pk_minimum3_f16, v_pk_min_u16, v_min3_u32) in 4
@@ -450,6 +452,93 @@ def run_dense(c: Ctx, wl):
               "max_tree_depth": int(s0.max_depth),
               "ms_fw": round(s0.ms_fw, 3), "ms_post": round(s0.ms_post, 3)}
     return elapsed, "u32" if enc == 1 else "u16", "strong", config, roofline, cpu, parity
+
+
+def dense_cpu_and_parity(c: Ctx, wl, step, lat, rel):
+    """untimed: the tied-pair count (check build), the CPU baseline legs and the sampled parity"""
+    n, world, rank = wl["n"], c.world, c.rank
+    chk = _lib.BuildStats()
+    chk.count_ties = 1
+    step(chk)
+    tied = all_sum(c, int(chk.tied_pairs))
+    sample = parity_rows(c, dense_range(c, n), n, k_per_rank=8)
+    glat, grel = gather_rows(c, sample, lambda rr: lat[rr], lambda rr: rel[rr], n, 1_000_000)
+    cpu = parity = None
+    if rank == 0 and not c.args.no_cpu_baseline:
+        import oracle  # cpu_baseline leg and the parity check only
+        if world == 1:
+            one = np.array([17 % n], np.int32)
+            _, _, _, t1 = oracle.complete_sample(n, wl["seed"], wl["lat_max"], wl["self_max"],
+                                                 wl["loss_max"], one, 1)
+            k = int(max(2, min(64, c.args.cpu_seconds / max(t1, 1e-3))))
+            srcs = np.unique(np.linspace(0, n - 1, k).astype(np.int32))
+            _, _, gen_s, sssp_s = oracle.complete_sample(n, wl["seed"], wl["lat_max"],
+                                                         wl["self_max"], wl["loss_max"], srcs, 1)
+            cpu = {"value": round(len(srcs) * n / sssp_s, 1), "unit": "node-pairs/s", "cores": 1,
+                   "kind": "port",
+                   "sample": f"{len(srcs)} of {n} sources, dense O(n^2) Dijkstra per source "
+                             f"(oracle/oracle.c orc_complete_sample), {sssp_s:.1f} s, 1 thread "
+                             f"(the reference serializes Dijkstra on graphLock, topology.c:130-148); "
+                             f"matrix generation ({gen_s:.1f} s) excluded"}
+            nt = cpu_threads()
+            kk = int(max(nt, min(32 * nt, nt * c.args.cpu_seconds / 2 / max(t1, 1e-3))))
+            msrcs = np.unique(np.linspace(0, n - 1, kk).astype(np.int32))
+            _, _, _, mt_s = oracle.complete_sample(n, wl["seed"], wl["lat_max"], wl["self_max"],
+                                                   wl["loss_max"], msrcs, nt)
+            cpu["all_cores"] = {"value": round(len(msrcs) * n / mt_s, 1), "cores": nt,
+                                "sample": f"{len(msrcs)} of {n} sources over {nt} threads, "
+                                          f"{mt_s:.1f} s (no graphLock: the reference cannot do "
+                                          f"this)"}
+        clat, crel, _, _ = oracle.complete_sample(n, wl["seed"], wl["lat_max"], wl["self_max"],
+                                                  wl["loss_max"], sample, cpu_threads())
+        parity = compare_rows(sample, n, glat, grel, clat, crel)
+    if parity is not None:
+        parity.update({"tied_pairs": tied, "tied_frac": tied / float(n * (n - 1))})
+    return cpu, parity
+
+
+def dense_levels_tail(c: Ctx, wl, step, elapsed, stats, lat, rel, nr, ld):
+    """Dense builds whose distances came from the bit-parallel Dial levels (levels.hip, dist_enc
+    12): the dominant kernel is lvl_step_kernel, one launch per level, each gathering one 4-B
+    word per (arc of weight < d, source word) -- its algorithmic bytes (srt_build_stats.work_bytes,
+    summed over the levels) over the HIP-event time of the launches. HBM-bound gathers; the
+    rocprof trace under profiles/ gives the same per-launch durations."""
+    n, world = wl["n"], c.world
+    n_upd = sum(s.n_update for s in stats)
+    ms_upd = sum(s.ms_update for s in stats)
+    wbytes = sum(float(s.work_bytes) for s in stats)
+    avg_ms = ms_upd / max(n_upd, 1)
+    per_launch = wbytes / max(n_upd, 1)
+    achieved = per_launch / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{c.args.workload}_n{world}.json")
+    if os.path.exists(pmc_path):
+        pmc = json.load(open(pmc_path))
+        if pmc.get("kernel") == "lvl_step_kernel":
+            traffic = pmc.get("hbm_bytes_per_launch")
+    s0 = stats[-1]
+    roofline = {
+        "bound": "hbm", "kernel": "lvl_step_kernel",
+        "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+        "bytes_per_launch": per_launch, "avg_launch_ms": round(avg_ms, 4),
+        "launches_timed": n_upd,
+        "model": "per level d: one 4-B Delta_{d-w}[k] word gathered per (in-arc k->j of weight "
+                 "w < d, target j, 32-source word) -- the bit-parallel Dial recurrence; averaged "
+                 f"over the {int(s0.levels)} levels of a build",
+        "algorithmic_min_bytes": float(nr) * ld * (4 + 8),
+    }
+    cpu, parity = dense_cpu_and_parity(c, wl, step, lat, rel)
+    config = {"workload": wl["desc"], "n": n, "ld": ld, "distances": "bit-parallel Dial levels",
+              "levels": int(s0.levels),
+              "parallelism": f"row-shard x{world}" + (" (no collective during the levels; "
+                                                      "arc segments and the post pass's "
+                                                      "essential arcs over RCCL)"
+                                                      if world > 1 else ""),
+              "rows_per_rank": nr, "ess_arcs": int(s0.ess_arcs),
+              "max_tree_depth": int(s0.max_depth),
+              "ms_fw": round(s0.ms_fw, 3), "ms_post": round(s0.ms_post, 3)}
+    return elapsed, "u32", "strong", config, roofline, cpu, parity
 
 
 # ------------------------------------------------------------------------------------------
@@ -656,14 +745,14 @@ def main():
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch(args.gpus))
-    if args.dry_run:
-        print(json.dumps({"rank": int(os.environ.get("RANK", "0")),
+    if args.dry_run:  # one write per line: the ranks share the launcher's stdout
+        sys.stdout.write(json.dumps({"rank": int(os.environ.get("RANK", "0")),
                           "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
                           "world_size": int(os.environ.get("WORLD_SIZE", "1")),
                           "master_addr": os.environ.get("MASTER_ADDR"),
                           "master_port": os.environ.get("MASTER_PORT"),
-                          "torch_imported": "torch" in sys.modules, "pid": os.getpid()}),
-              flush=True)
+                          "torch_imported": "torch" in sys.modules, "pid": os.getpid()}) + "\n")
+        sys.stdout.flush()
         return
     _runtime()
     c = Ctx(args)

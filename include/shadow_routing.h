@@ -84,7 +84,8 @@ typedef struct srt_build_stats {
                           * SRT_INF quanta), 3 = multi-source kernel (64 sources per workgroup),
                           * 2 = workgroup-per-source kernel (LDS-packed rows),
                           * 1 = wave-per-source kernel, 0 = workgroup kernel for every source.
-                          * Dense: the distance encoding the build finished with: 9 = 8 with
+                          * Dense: the distance encoding the build finished with: 12 = bit-parallel
+                          * Dial levels (no FW rounds; levels.hip), 9 = 8 with
                           * 256-pivot rounds (SRT_FW_SH_KB=256), 8 = u16
                           * f16-compare row-sharded symmetric rounds of 128 pivots (N > 1;
                           * 4 with SRT_FW_SH_KB=64), 7 = 5 with
@@ -99,6 +100,9 @@ typedef struct srt_build_stats {
                           * predecessors u of t is reached by two or more u: igraph's heap order
                           * picks the reference's predecessor there (topology.c:1679-1701), the
                           * build takes the smallest u -- the class where reliability can differ */
+    int32_t levels;      /* dense level builds (dist_enc 12): the Dial level that settled every pair */
+    int64_t work_bytes;  /* algorithmic bytes of the timed launches (level builds: the Delta words
+                          * gathered over all levels), 0 where the bench models them itself */
 } srt_build_stats;
 
 /* Build the full tables for an edge list on one GPU; outputs are host buffers of n*n entries.

@@ -63,6 +63,8 @@ class BuildStats(ctypes.Structure):
         ("dist_enc", ctypes.c_int32),
         ("count_ties", ctypes.c_int32),
         ("tied_pairs", ctypes.c_int64),
+        ("levels", ctypes.c_int32),
+        ("work_bytes", ctypes.c_int64),
     ]
 
 

@@ -1734,6 +1734,36 @@ static int dense_path_ms(int32_t n, int32_t ld, int32_t row0, int32_t nrows, con
                             (size_t)ld, NULL, NULL, NULL, q, lms, (size_t)ld, st);
 }
 
+/* Dial levels (levels.hip) instead of the FW when the graph's distances are small enough for the
+ * level budget to beat the FW's predicted time (61 T relaxations/s, the measured update rate;
+ * symmetric rounds do half the relaxations). n >= 4,096: below that the FW's squaring or rounds
+ * cost less than the levels' launches. SRT_DENSE_LEVELS=0 keeps the FW, =1 tries the levels at any
+ * size. *exact = 1 when the levels settled every pair (the u16 matrix and lat rows are final). */
+static int dense_try_levels(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
+                            const uint32_t* w_rows, uint32_t* lat_rows, hipStream_t st,
+                            evpool_t* evp, srt_build_stats* stats, int* exact) {
+    *exact = 0;
+    const char* env = getenv("SRT_DENSE_LEVELS");
+    const int mode = env ? atoi(env) : -1;
+    if (mode == 0 || (mode < 0 && n < 4096) || ld % 128) return SRT_OK;
+    const double fw_ms = (double)nrows * ld * ld / (directed ? 1.0 : 2.0) / 6.1e10;
+    if (evp) {
+        evp->used = 0;
+        evp->group = 2;
+    }
+    int nlev = 0;
+    int64_t bytes = 0;
+    const int rc = srt_fw16_levels(comm, n, ld, row0, nrows, directed, w_rows, lat_rows, st, evp,
+                                   mode > 0 ? 1e30 : fw_ms, &nlev, &bytes);
+    if (rc) return rc;
+    if (stats) {
+        stats->levels = nlev;
+        stats->work_bytes = nlev ? bytes : 0;
+    }
+    *exact = nlev > 0;
+    return SRT_OK;
+}
+
 int srt_dense_build_device_ms(int32_t n, int32_t ld, int32_t directed, const uint32_t* w,
                               const double* r, uint32_t* lat, double* rel, double* lat_ms,
                               uint64_t quantum_ns, hipStream_t st, int32_t fw_block,
@@ -1757,8 +1787,12 @@ int srt_dense_build_device_ms(int32_t n, int32_t ld, int32_t directed, const uin
     SRT_HIPCHK(hipEventRecord(e0, st));
     evpool_t* evp = NULL;
     if (stats && stats->time_kernels && (rc = evpool_begin(&evp, ld / B))) return rc;
-    /* narrowest exact encoding first: f16-compare u16 -> pk_min u16 -> u32 */
+    /* narrowest exact encoding first: Dial levels (small distances) -> f16-compare u16 -> pk_min
+     * u16 -> u32 */
     int exact = 0, enc = SRT_DENC_U32;
+    if ((rc = dense_try_levels(NULL, n, ld, 0, ld, directed, w, lat, st, evp, stats, &exact)))
+        return rc;
+    if (exact) enc = SRT_DENC_LEVELS;
     for (int fm = 1; fm >= 0 && !exact && ld % 128 == 0; --fm) {
         if (evp) {
             evp->used = 0;
@@ -1914,6 +1948,9 @@ int srt_dense_build_sharded_ms(srt_comm* comm, int32_t n, int32_t ld, int32_t di
     const char* sym_env = getenv("SRT_FW_SYM");
     /* symmetric rounds up to 1,024 tile columns (fw16.hip SYM_TMAX, the panel-position table) */
     const bool sym = !directed && R > 1 && ld <= 1024 * 128 && !(sym_env && atoi(sym_env) == 0);
+    if ((rc = dense_try_levels(comm, n, ld, b, nr, directed, w_rows, lat_rows, st, evp, stats, &exact)))
+        return rc;
+    if (exact) enc = SRT_DENC_LEVELS;
     for (int fm = 1; fm >= 0 && !exact; --fm) {
         if (evp) {
             evp->used = 0;

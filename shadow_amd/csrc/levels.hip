@@ -1,0 +1,428 @@
+/*
+ * levels.hip -- exact all-pairs shortest distances on dense graphs by bit-parallel Dial levels.
+ *
+ * Replaces, when it is cheaper, the blocked Floyd-Warshall of fw16.hip for the distance phase of
+ * _topology_computeSourcePaths (/root/reference/src/main/routing/topology.c:1578-1814, the igraph
+ * Dijkstra of :1679-1701) on complete / dense graphs. Edge weights are integer quanta >= 1, so
+ * Dijkstra's settle order is Dial's bucket order, and one bucket (distance level d) of EVERY source
+ * can be settled at once with bit operations:
+ *
+ *   Delta_d[j] = ( OR over in-arcs (k -> j, w <= d) of Delta_{d-w}[k] )  AND NOT  R_{d-1}[j]
+ *   R_d[j]     = R_{d-1}[j] OR Delta_d[j]
+ *
+ * where Delta_d[j] is the bit set of sources s with D[s][j] == d, R_d[j] those with D[s][j] <= d,
+ * and Delta_0[k] = R_0[k] = {k}. This is the last-hop decomposition D[s][j] = min_k D[s][k] +
+ * w(k, j) (every weight >= 1, so Delta_{d-w} is final when level d is formed), i.e. the same
+ * distances Dijkstra settles; the canonical predecessors and path-order reliabilities are formed
+ * afterwards from the distances by the dense post pass exactly as after Floyd-Warshall.
+ *
+ * Only arcs with w <= lmax take part. If every pair is settled by level D <= lmax, every arc with
+ * w > lmax >= D is longer than the distance it joins, so it lies on no shortest path and the
+ * result is exact. Otherwise the build falls back to Floyd-Warshall (the caller's).
+ *
+ * Layout (HBM). Bit sets run over this rank's sources (nsrc, a multiple of 128): nw = nsrc / 32
+ * words per vertex. lev[d - 1][j][word] for d = 1..lmax, R[j][word]; one wave owns a (target j,
+ * 64-word source chunk) unit, so every arc costs one coalesced 256-B gather of Delta_{d-w}[k].
+ * In-arcs come from the rows of w (undirected: row j holds j's in-arcs, and a row-sharded rank has
+ * them for its rows) or its columns (directed, one GPU), grouped by (target, weight).
+ */
+#include <hipcub/hipcub.hpp>
+
+#include "srt_device.h"
+
+#define LVL_STRIDE 256 /* per-target offsets: weight 0..255 */
+#define LVL_WMAX 254   /* largest level budget (distances stay u8: the post pass's small path) */
+
+/* ---- in-arc extraction ------------------------------------------------------------------- */
+/* COUNT: per (target, weight) histogram of arcs with 1 <= w <= LVL_WMAX; FILL: the arcs (k | w << 16)
+ * at cursor positions from off (weights above lmax were masked out of off). Rows form: local row
+ * jj of w is target row0 + jj's in-arc row (undirected). */
+template <bool FILL>
+__global__ __launch_bounds__(256) void lvl_arcs_rows_kernel(int n, int ld, int row0,
+                                                            const uint32_t* __restrict__ w,
+                                                            int32_t* __restrict__ cnt, int lmax,
+                                                            const int32_t* __restrict__ off,
+                                                            uint32_t* __restrict__ arcs) {
+    __shared__ int h[LVL_STRIDE];
+    const int jj = blockIdx.x, j = row0 + jj;
+    for (int i = threadIdx.x; i < LVL_STRIDE; i += 256)
+        h[i] = FILL ? (j < n ? off[(size_t)j * LVL_STRIDE + i] : 0) : 0;
+    __syncthreads();
+    const int wmax = FILL ? lmax : LVL_WMAX;
+    if (j < n) {
+        const uint32_t* row = w + (size_t)jj * ld;
+        for (int k4 = threadIdx.x * 4; k4 < n; k4 += 1024) {
+            const uint4 v = *reinterpret_cast<const uint4*>(row + k4);
+            const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = k4 + q;
+                if (k < n && k != j && x[q] >= 1u && x[q] <= (uint32_t)wmax) {
+                    if (FILL)
+                        arcs[atomicAdd(&h[x[q]], 1)] = (uint32_t)k | (x[q] << 16);
+                    else
+                        atomicAdd(&h[x[q]], 1);
+                }
+            }
+        }
+    }
+    if (FILL) return;
+    __syncthreads();
+    for (int i = threadIdx.x; i < LVL_STRIDE; i += 256) cnt[(size_t)j * LVL_STRIDE + i] = h[i];
+}
+
+/* Columns form (directed graph on one GPU): workgroup of 64 target columns j0.., lane = column,
+ * the four waves sweep the rows k (one coalesced 256-B segment of a row per wave and step). */
+template <bool FILL>
+__global__ __launch_bounds__(256) void lvl_arcs_cols_kernel(int n, int ld,
+                                                            const uint32_t* __restrict__ w,
+                                                            int32_t* __restrict__ cnt, int lmax,
+                                                            const int32_t* __restrict__ off,
+                                                            uint32_t* __restrict__ arcs) {
+    __shared__ int h[64 * LVL_STRIDE];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int j0 = blockIdx.x * 64, j = j0 + lane;
+    for (int i = threadIdx.x; i < 64 * LVL_STRIDE; i += 256) {
+        const int c = i / LVL_STRIDE, ww = i % LVL_STRIDE;
+        h[i] = FILL ? (j0 + c < n ? off[(size_t)(j0 + c) * LVL_STRIDE + ww] : 0) : 0;
+    }
+    __syncthreads();
+    const int wmax = FILL ? lmax : LVL_WMAX;
+    if (j < n) {
+        for (int k = wv; k < n; k += 4) {
+            const uint32_t x = w[(size_t)k * ld + j];
+            if (k != j && x >= 1u && x <= (uint32_t)wmax) {
+                if (FILL)
+                    arcs[atomicAdd(&h[lane * LVL_STRIDE + x], 1)] = (uint32_t)k | (x << 16);
+                else
+                    atomicAdd(&h[lane * LVL_STRIDE + x], 1);
+            }
+        }
+    }
+    if (FILL) return;
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * LVL_STRIDE; i += 256) {
+        const int c = i / LVL_STRIDE, ww = i % LVL_STRIDE;
+        if (j0 + c < ld) cnt[(size_t)(j0 + c) * LVL_STRIDE + ww] = h[i];
+    }
+}
+
+/* weight histogram over all targets (for the level budget) and the mask w <= lmax before the scan */
+__global__ void lvl_hist_kernel(size_t count, const int32_t* __restrict__ cnt,
+                                unsigned long long* __restrict__ hist) {
+    __shared__ unsigned long long s[LVL_STRIDE];
+    for (int i = threadIdx.x; i < LVL_STRIDE; i += blockDim.x) s[i] = 0;
+    __syncthreads();
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+         i += (size_t)gridDim.x * blockDim.x)
+        if (cnt[i]) atomicAdd(&s[i % LVL_STRIDE], (unsigned long long)cnt[i]);
+    __syncthreads();
+    for (int i = threadIdx.x; i < LVL_STRIDE; i += blockDim.x)
+        if (s[i]) atomicAdd(&hist[i], s[i]);
+}
+
+__global__ void lvl_mask_kernel(size_t count, int lmax, int32_t* __restrict__ cnt) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count && (int)(i % LVL_STRIDE) > lmax) cnt[i] = 0;
+}
+
+/* ---- the levels ---------------------------------------------------------------------------- */
+/* R = {j} for the local sources j (distance 0), everything else empty */
+__global__ void lvl_init_kernel(int n, int src0, int nsrc, int nw, uint32_t* __restrict__ R) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nsrc) return;
+    const int j = src0 + i;
+    if (j < n) R[(size_t)j * nw + (i >> 5)] = 1u << (i & 31);
+}
+
+/* Level d: one wave per (target j, 64-word source chunk c). Units are handed out XCD-major (each
+ * XCD takes a contiguous run of chunk-major units), so an XCD works on one source chunk at a time
+ * and the Delta rows of that chunk are the only gathered data in its L2. */
+__global__ __launch_bounds__(256) void lvl_step_kernel(int d, int n, int nw, int nchunk, int src0,
+                                                       int nsrc, unsigned nblk,
+                                                       const int32_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ arcs,
+                                                       uint32_t* __restrict__ lev,
+                                                       uint32_t* __restrict__ R,
+                                                       uint8_t* __restrict__ done,
+                                                       int* __restrict__ incomplete) {
+    const unsigned b = blockIdx.x;
+    const unsigned g = (b & 7u) * (nblk >> 3) + (b >> 3); /* nblk % 8 == 0 */
+    const int tgrp = (n + 3) >> 2;
+    const int c = (int)(g / (unsigned)tgrp);
+    /* the wave index through readfirstlane: j is then wave-uniform to the compiler, so the offsets
+     * and the arcs come through scalar loads and every gather's row address is an SGPR */
+    const int j = (int)(g % (unsigned)tgrp) * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (c >= nchunk || j >= n) return;
+    const int lane = threadIdx.x & 63, word = c * 64 + lane;
+    const bool valid = word < nw;
+    const size_t plane = (size_t)n * nw; /* words per level */
+    uint32_t* out = lev + (size_t)(d - 1) * plane + (size_t)j * nw + word;
+    const size_t u = (size_t)j * nchunk + c;
+    if (done[u]) {
+        if (valid) *out = 0u;
+        return;
+    }
+    uint32_t acc = 0;
+    const int32_t* oj = off + (size_t)j * LVL_STRIDE;
+    /* arcs of weight d: the path (k, j) itself, Delta_0[k] = {k} */
+    {
+        const int a0 = oj[d], a1 = oj[d + 1];
+        for (int i = a0; i < a1; ++i) {
+            const int ks = (int)(arcs[i] & 0xFFFFu) - src0;
+            if ((unsigned)ks < (unsigned)nsrc && (ks >> 5) == word) acc |= 1u << (ks & 31);
+        }
+    }
+    /* arcs of weight < d: Delta_{d-w}[k], eight gathers in flight; lanes past nw read word 0 of
+     * the row (a valid address) and drop it, so the loop has no per-lane branch and the eight arcs
+     * come in one scalar load */
+    const int b0 = oj[1], b1 = oj[d];
+    const uint32_t* lw = lev + (valid ? word : 0); /* lane base */
+    int i = b0;
+    for (; i + 8 <= b1; i += 8) {
+        uint32_t a[8], v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a[q] = arcs[i + q];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            v[q] = lw[(size_t)(d - (int)(a[q] >> 16) - 1) * plane + (size_t)(a[q] & 0xFFFFu) * nw];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc |= v[q];
+    }
+    for (; i < b1; ++i) {
+        const uint32_t a = arcs[i];
+        acc |= lw[(size_t)(d - (int)(a >> 16) - 1) * plane + (size_t)(a & 0xFFFFu) * nw];
+    }
+    if (!valid) acc = 0;
+    bool inc = false;
+    if (valid) {
+        uint32_t* rp = R + (size_t)j * nw + word;
+        const uint32_t r = *rp;
+        const uint32_t nb = acc & ~r;
+        *out = nb;
+        if (nb) *rp = r | nb;
+        /* sources past n (padding of the last shard) never appear: they count as settled */
+        const int s0 = src0 + word * 32;
+        const uint32_t full = s0 + 32 <= n ? 0xFFFFFFFFu : s0 >= n ? 0u : (1u << (n - s0)) - 1u;
+        inc = ((r | nb) & full) != full;
+    }
+    const unsigned long long m = __ballot(inc);
+    if (lane == 0) {
+        if (m)
+            atomicAdd(incomplete, 1);
+        else
+            done[u] = 1;
+    }
+}
+
+/* distance rows of the local sources (u16, row stride ld, the FW matrix layout: 0 on the diagonal,
+ * cap where nothing was reached, cap on padding). Thread = target t (256 per workgroup), looping
+ * over 16 source words: it reads word (t, sw) of every level (one 64-B line per thread across the
+ * 16 words) and writes its column of the word's 32 source rows (each row a 512-B segment per
+ * workgroup). */
+__global__ __launch_bounds__(256) void lvl_d16_kernel(int n, int ld, int nw, int src0, int nlev,
+                                                      const uint32_t* __restrict__ lev,
+                                                      uint16_t* __restrict__ d16, uint32_t cap) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= ld) return;
+    const size_t plane = (size_t)n * nw;
+    const int sw1 = min(nw, (int)(blockIdx.y + 1) * 16);
+    for (int sw = blockIdx.y * 16; sw < sw1; ++sw) {
+        uint32_t m[8]; /* levels read eight at a time */
+        uint16_t v[32];
+#pragma unroll
+        for (int s = 0; s < 32; ++s) v[s] = (uint16_t)(src0 + sw * 32 + s == t ? 0u : cap);
+        if (t < n) {
+            for (int d0 = 1; d0 <= nlev; d0 += 8) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    m[q] = d0 + q <= nlev ? lev[(size_t)(d0 + q - 1) * plane + (size_t)t * nw + sw] : 0u;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    if (!m[q]) continue;
+#pragma unroll
+                    for (int s = 0; s < 32; ++s)
+                        if ((m[q] >> s) & 1u) v[s] = (uint16_t)(d0 + q);
+                }
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < 32; ++s) d16[(size_t)(sw * 32 + s) * ld + t] = v[s];
+    }
+}
+
+/* ---- host ----------------------------------------------------------------------------------- */
+/* Streaming-gather rate assumed by the level budget (bytes per ms) and the cost of one level's
+ * launch + completion read-back. */
+#define LVL_BYTES_PER_MS 4.0e9
+#define LVL_LEVEL_MS 0.03
+
+/* Estimated time of levels 1..L (ms): every level gathers one 4-B word per (arc of weight < d,
+ * source word) and reads/writes R and Delta once. */
+static double lvl_estimate(const unsigned long long* hist, int L, double ntgt, double nw) {
+    double t = 0, below = 0; /* arcs with weight < d */
+    for (int d = 1; d <= L; ++d) {
+        if (d >= 2) below += (double)hist[d - 1];
+        t += (below * nw * 4.0 + ntgt * nw * 4.0 * 3.0) / LVL_BYTES_PER_MS + LVL_LEVEL_MS;
+    }
+    return t;
+}
+
+/* One build of the local rows' u16 distances into d16 (nrows x ld). comm (NULL on one GPU):
+ * undirected row shards, every rank sees every target's in-arcs after the segment broadcasts.
+ * fw_ms: the predicted Floyd-Warshall time; the level budget keeps the predicted level time under
+ * half of it. *levels = the level that settled every pair (0: not applicable / over budget -- the
+ * caller runs Floyd-Warshall; every rank of a sharded build returns the same verdict).
+ * *gather_bytes: the Delta words gathered (the kernel's algorithmic bytes). */
+int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
+                     const uint32_t* w_rows, uint16_t* d16, uint32_t cap, double fw_ms,
+                     hipStream_t st, evpool_t* evp, int* levels, int64_t* gather_bytes) {
+    *levels = 0;
+    *gather_bytes = 0;
+    const int R = comm ? srt_comm_size(comm) : 1;
+    if (n > 65535 || ld % 128 || nrows % 128 || row0 % 128) return SRT_OK;
+    if (R > 1 && directed) return SRT_OK; /* in-arcs of a directed graph span every rank's rows */
+    const size_t ncnt = (size_t)ld * LVL_STRIDE;
+    int32_t *cnt = NULL, *off = NULL;
+    unsigned long long* dhist = NULL;
+    SRT_HIPCHK(srt_malloc_async(&cnt, (ncnt + 1) * sizeof(int32_t), st));
+    SRT_HIPCHK(srt_malloc_async(&off, (ncnt + 1) * sizeof(int32_t), st));
+    SRT_HIPCHK(srt_malloc_async(&dhist, LVL_STRIDE * sizeof(unsigned long long), st));
+    struct frees {
+        hipStream_t s;
+        void* p[8] = {};
+        int k = 0;
+        ~frees() {
+            for (int i = 0; i < k; i++) (void)hipFreeAsync(p[i], s);
+        }
+    } fr;
+    fr.s = st;
+    fr.p[fr.k++] = cnt;
+    fr.p[fr.k++] = off;
+    fr.p[fr.k++] = dhist;
+    SRT_HIPCHK(hipMemsetAsync(cnt, 0, (ncnt + 1) * sizeof(int32_t), st));
+    SRT_HIPCHK(hipMemsetAsync(dhist, 0, LVL_STRIDE * sizeof(unsigned long long), st));
+    if (directed)
+        lvl_arcs_cols_kernel<false><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, cnt, 0, NULL, NULL);
+    else
+        lvl_arcs_rows_kernel<false><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, cnt, 0, NULL, NULL);
+    SRT_HIPCHK(hipGetLastError());
+    int rc;
+    if (R > 1 && (rc = srt_coll_allreduce_i32(comm, cnt, ncnt, 0, st))) return rc;
+    lvl_hist_kernel<<<1024, 256, 0, st>>>(ncnt, cnt, dhist);
+    SRT_HIPCHK(hipGetLastError());
+    unsigned long long hist[LVL_STRIDE];
+    SRT_HIPCHK(hipMemcpyAsync(hist, dhist, sizeof(hist), hipMemcpyDeviceToHost, st));
+    SRT_HIPCHK(hipStreamSynchronize(st));
+    /* level budget: the largest L whose predicted time stays under half the FW time */
+    const double nw_all = (double)nrows / 32.0;
+    int lmax = 0;
+    for (int L = 1; L <= LVL_WMAX; ++L) {
+        if (lvl_estimate(hist, L, (double)n, nw_all) > 0.5 * fw_ms) break;
+        lmax = L;
+    }
+    int wmin = 0;
+    for (int x = 1; x <= LVL_WMAX && !wmin; ++x)
+        if (hist[x]) wmin = x;
+    if (lmax < 2 || !wmin || wmin > lmax) return SRT_OK;
+    /* offsets over the arcs with w <= lmax, (target, weight)-major */
+    lvl_mask_kernel<<<srt_ceil_div((int64_t)ncnt, 256), 256, 0, st>>>(ncnt, lmax, cnt);
+    SRT_HIPCHK(hipGetLastError());
+    size_t tmp_bytes = 0;
+    SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(NULL, tmp_bytes, cnt, off, (int)(ncnt + 1), st));
+    void* tmp = NULL;
+    SRT_HIPCHK(srt_malloc_async(&tmp, tmp_bytes, st));
+    fr.p[fr.k++] = tmp;
+    SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, (int)(ncnt + 1), st));
+    int32_t total = 0;
+    SRT_HIPCHK(hipMemcpyAsync(&total, off + ncnt, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    SRT_HIPCHK(hipStreamSynchronize(st));
+    uint32_t* arcs = NULL;
+    SRT_HIPCHK(srt_malloc_async(&arcs, ((size_t)total + 8) * sizeof(uint32_t), st));
+    fr.p[fr.k++] = arcs;
+    if (directed)
+        lvl_arcs_cols_kernel<true><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, NULL, lmax, off, arcs);
+    else
+        lvl_arcs_rows_kernel<true><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, NULL, lmax, off, arcs);
+    SRT_HIPCHK(hipGetLastError());
+    if (R > 1) { /* every rank filled its rows' segment: broadcast the segments */
+        int32_t* hoff = (int32_t*)malloc(((size_t)R + 1) * sizeof(int32_t));
+        if (!hoff) return SRT_E_NOMEM;
+        for (int q = 0; q <= R; q++) {
+            int32_t b = ld, e = ld;
+            if (q < R) srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &b, &e);
+            const size_t at = (size_t)b * LVL_STRIDE;
+            if (hipMemcpyAsync(&hoff[q], off + at, sizeof(int32_t), hipMemcpyDeviceToHost, st) !=
+                hipSuccess) {
+                free(hoff);
+                srt_set_error("levels: offset read-back failed");
+                return SRT_E_DEVICE;
+            }
+        }
+        if (hipStreamSynchronize(st) != hipSuccess) {
+            free(hoff);
+            return SRT_E_DEVICE;
+        }
+        rc = srt_coll_group_begin(comm);
+        for (int q = 0; q < R && !rc; q++)
+            if (hoff[q + 1] > hoff[q])
+                rc = srt_coll_bcast(comm, arcs + hoff[q], (size_t)(hoff[q + 1] - hoff[q]) * 4, q, st);
+        const int rc2 = srt_coll_group_end(comm);
+        free(hoff);
+        if (rc || rc2) return rc ? rc : rc2;
+    }
+    /* level state over the local sources */
+    const int nw = nrows / 32, nchunk = (nw + 63) / 64;
+    const size_t plane = (size_t)n * nw;
+    uint32_t *lev = NULL, *Rb = NULL;
+    uint8_t* done = NULL;
+    int* dinc = NULL;
+    SRT_HIPCHK(srt_malloc_async(&lev, (size_t)lmax * plane * sizeof(uint32_t), st));
+    fr.p[fr.k++] = lev;
+    SRT_HIPCHK(srt_malloc_async(&Rb, plane * sizeof(uint32_t), st));
+    fr.p[fr.k++] = Rb;
+    SRT_HIPCHK(srt_malloc_async(&done, (size_t)n * nchunk + 4 * sizeof(int) * (size_t)(LVL_WMAX + 1), st));
+    fr.p[fr.k++] = done;
+    dinc = (int*)(void*)(((uintptr_t)(done + (size_t)n * nchunk) + 15) & ~(uintptr_t)15);
+    SRT_HIPCHK(hipMemsetAsync(Rb, 0, plane * sizeof(uint32_t), st));
+    SRT_HIPCHK(hipMemsetAsync(done, 0, (size_t)n * nchunk, st));
+    SRT_HIPCHK(hipMemsetAsync(dinc, 0, sizeof(int) * (size_t)(LVL_WMAX + 1), st));
+    lvl_init_kernel<<<srt_ceil_div(nrows, 256), 256, 0, st>>>(n, row0, nrows, nw, Rb);
+    SRT_HIPCHK(hipGetLastError());
+    unsigned nblk = (unsigned)(((n + 3) / 4) * nchunk);
+    nblk = (nblk + 7u) & ~7u;
+    int D = 0;
+    int64_t gathered = 0;
+    for (int d = 1; d <= lmax; ++d) {
+        if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
+        lvl_step_kernel<<<nblk, 256, 0, st>>>(d, n, nw, nchunk, row0, nrows, nblk, off, arcs, lev,
+                                              Rb, done, dinc + d);
+        if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
+        SRT_HIPCHK(hipGetLastError());
+        int inc = 0;
+        SRT_HIPCHK(hipMemcpyAsync(&inc, dinc + d, sizeof(int), hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipStreamSynchronize(st));
+        double below = 0;
+        for (int x = 1; x < d; ++x) below += (double)hist[x];
+        gathered += (int64_t)(below * (double)nw * 4.0);
+        if (inc == 0) {
+            D = d;
+            break;
+        }
+    }
+    int ok = D > 0;
+    if (R > 1) { /* one verdict for every rank: all settled, or Floyd-Warshall everywhere */
+        int32_t* flag = (int32_t*)dinc;
+        SRT_HIPCHK(hipMemcpyAsync(flag, &ok, sizeof(int32_t), hipMemcpyHostToDevice, st));
+        if ((rc = srt_coll_allreduce_i32(comm, flag, 1, 1, st))) return rc;
+        SRT_HIPCHK(hipMemcpyAsync(&ok, flag, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipStreamSynchronize(st));
+    }
+    if (!ok) return SRT_OK;
+    lvl_d16_kernel<<<dim3(srt_ceil_div(ld, 256), srt_ceil_div(nw, 16)), 256, 0, st>>>(n, ld, nw, row0, D,
+                                                                                    lev, d16, cap);
+    SRT_HIPCHK(hipGetLastError());
+    *levels = D;
+    *gather_bytes = gathered;
+    return SRT_OK;
+}

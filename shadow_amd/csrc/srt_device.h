@@ -153,6 +153,14 @@ int srt_fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0, in
 int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,
                    hipStream_t st, evpool_t* evp, srt_owner_fn owner_of, srt_panel_bcast_fn bcast,
                    void* ctx, int rank, int fm, int* sym, int* exact);
+/* levels.hip: u16 distance rows of the local sources by bit-parallel Dial levels (see there) */
+int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
+                     const uint32_t* w_rows, uint16_t* d16, uint32_t cap, double fw_ms,
+                     hipStream_t st, evpool_t* evp, int* levels, int64_t* gather_bytes);
+/* the same into this slot's FW matrix + the finish pass (fw16.hip); *nlev = 0: FW instead */
+int srt_fw16_levels(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
+                    const uint32_t* w_rows, uint32_t* lat_rows, hipStream_t st, evpool_t* evp,
+                    double fw_ms, int* nlev, int64_t* bytes);
 /* the u16 working matrix of the last srt_fw16_build on the current device (row shard x ld) */
 const uint16_t* srt_fw16_matrix(void);
 /* 1 when every real distance of that build is <= 254 quanta (the post pass then reads u8) */
@@ -169,7 +177,8 @@ enum {
     SRT_DENC_F16CMP_SYMSH128 = 8, /* 4 (row-sharded, >= 2 ranks) with 128-pivot rounds */
     SRT_DENC_F16CMP_SYMSH256 = 9, /* 4 (row-sharded) with 256-pivot rounds */
     SRT_DENC_ROWS = 10,           /* a few source rows by Bellman-Ford passes, no FW */
-    SRT_DENC_SQUARE = 11          /* ld <= 2048 on one GPU: min-plus squaring to a fixed point */
+    SRT_DENC_SQUARE = 11,         /* ld <= 2048 on one GPU: min-plus squaring to a fixed point */
+    SRT_DENC_LEVELS = 12          /* bit-parallel Dial levels (levels.hip), no FW rounds */
 };
 int srt_dense_rows_build_device(int32_t n, int32_t ld, int32_t nsub, const int32_t* dverts,
                                 const uint32_t* w, const double* r, uint32_t* lat_rows,

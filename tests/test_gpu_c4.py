@@ -22,8 +22,13 @@ REL_TOL = 1e-12
 N, SEED, LAT_MAX, SELF_MAX, LOSS_MAX = 32768, 4, 1000, 10, 500
 
 
-def test_c4_full_size_default_schedule(gpu):
+@pytest.mark.parametrize("mode", ["levels", "fw"])
+def test_c4_full_size_default_schedule(gpu, monkeypatch, mode):
+    """mode levels: the default (bit-parallel Dial levels, encoding 12); fw: SRT_DENSE_LEVELS=0
+    keeps the Floyd-Warshall schedule (encoding 7)."""
     import torch
+    if mode == "fw":
+        monkeypatch.setenv("SRT_DENSE_LEVELS", "0")
     L = _lib.lib()
     n = ld = N
     w = torch.empty((ld, ld), dtype=torch.int32, device="cuda")
@@ -38,7 +43,7 @@ def test_c4_full_size_default_schedule(gpu):
                                         rel.data_ptr(), None, 0, ctypes.byref(st)), "C4 build")
     torch.cuda.synchronize()
     del w, r
-    assert st.dist_enc == 7, "the default one-GPU schedule (two update streams, 256-pivot rounds)"
+    assert st.dist_enc == (12 if mode == "levels" else 7), st.dist_enc
     # 4 rows in each 4k block (first, middle, two in its last 128-row tile) + the last tile row
     rows = sorted({b + o for b in range(0, n, 4096) for o in (0, 2049, 4096 - 128, 4095)}
                   | {32640, 32700, 32767})
@@ -68,8 +73,9 @@ def test_c4_full_size_default_schedule(gpu):
     print(f"C4 tied pairs: {tied} ({tied / (n * (n - 1)):.4f} of the pairs)")
 
 
+@pytest.mark.parametrize("mode", ["levels", "fw"])
 @pytest.mark.parametrize("ranks", [4, 8])
-def test_c4_virtual_ranks_sharded_schedule(gpu, ranks):
+def test_c4_virtual_ranks_sharded_schedule(gpu, monkeypatch, ranks, mode):
     """The N-GPU C4 schedule at full size on ONE GPU (VERDICT r02 "configs_untested"): `ranks`
     host threads, each a virtual rank on device 0 with its own streams and workspaces, generate
     their row block of C4 on the device and run srt_dense_build_sharded over a virtual
@@ -81,6 +87,8 @@ def test_c4_virtual_ranks_sharded_schedule(gpu, ranks):
     boundary."""
     import threading
     import torch
+    if mode == "fw":
+        monkeypatch.setenv("SRT_DENSE_LEVELS", "0")
     L = _lib.lib()
     n = ld = N
     comms = (ctypes.c_void_p * ranks)()
@@ -122,7 +130,7 @@ def test_c4_virtual_ranks_sharded_schedule(gpu, ranks):
         torch.cuda.synchronize()
         for r in range(ranks):
             _lib.check(rcs[r], f"rank {r}")
-            assert stats[r].dist_enc == 8, (r, stats[r].dist_enc)
+            assert stats[r].dist_enc == (12 if mode == "levels" else 8), (r, stats[r].dist_enc)
         rows = set(range(32640, 32768, 37)) | {32767}
         for b, e in shards:
             rows |= {b, e - 1, b + (e - b) // 3, b + 2 * (e - b) // 3}

@@ -1,0 +1,127 @@
+"""Dense distances by bit-parallel Dial levels (shadow_amd/csrc/levels.hip, dist_enc 12) against
+the CPU oracle's Dijkstra (oracle.c, restating topology.c:1578-1814), bit for bit in latency and
+reliability (the post pass forms predecessors and path-order products from the level distances).
+
+SRT_DENSE_LEVELS=1 forces the level search at any size (the default takes it from n >= 4,096 when
+its budget beats the FW); when the graph's distances pass the level budget the build must fall back
+to the FW and still match. Sharded: virtual ranks on one GPU (row shards, arcs broadcast per rank's
+segment, one verdict for all ranks)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+from shadow_amd import _lib, graphs
+from shadow_amd._lib import ALGO_DENSE_FW
+from shadow_amd.topology import build_tables
+
+pytestmark = pytest.mark.gpu
+REL_TOL = 1e-12
+MS = 1_000_000
+LEVELS = 12
+
+
+def _oracle(g):
+    el = oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
+    return oracle.table(el, True, oracle.ORC_INT_NS, 8, raw=True)
+
+
+def _check(g, lat, rel, what):
+    exp = _oracle(g)
+    bad = np.argwhere(lat != np.asarray(exp["lat_int"], np.uint64))
+    assert bad.size == 0, f"{what}: {len(bad)} latency mismatches, first {bad[:5].tolist()}"
+    err = np.abs(rel - exp["rel"]) / np.maximum(np.abs(exp["rel"]), 1e-300)
+    assert float(err.max()) <= REL_TOL, f"{what}: max rel error {err.max()}"
+
+
+def _directed_dense(n, seed, wmax):
+    rng = np.random.default_rng(seed)
+    i, j = np.nonzero(rng.random((n, n)) < 0.35)
+    keep = i != j
+    i, j = i[keep], j[keep]
+    ring = np.arange(n)  # strongly connected
+    src = np.concatenate([i, ring]).astype(np.int32)
+    dst = np.concatenate([j, (ring + 1) % n]).astype(np.int32)
+    lat = (rng.integers(1, wmax + 1, len(src)) * MS).astype(np.int64)
+    loss = rng.integers(0, 300, len(src)) / 10000.0
+    return graphs.Graph(n, True, src, dst, lat, loss, f"directed{n}")
+
+
+@pytest.mark.parametrize("kind", ["complete300", "complete1000", "ties", "directed", "c1like"])
+def test_levels_match_oracle(gpu, monkeypatch, kind):
+    monkeypatch.setenv("SRT_DENSE_LEVELS", "1")
+    if kind == "complete300":
+        g = graphs.complete_graph(300, seed=7)
+    elif kind == "complete1000":  # C2's distribution: distances up to 9 quanta
+        g = graphs.complete_graph(1000, seed=2)
+    elif kind == "ties":  # 1-3 ms arcs: many equal-length paths (the canonical tie rule)
+        g = graphs.complete_graph(640, seed=11, lat_max=3)
+    elif kind == "directed":  # in-arcs from the columns of w
+        g = _directed_dense(500, 5, 40)
+    else:  # C1's distribution at 50 vertices: distances of tens of quanta
+        g = graphs.complete_graph(50, seed=1)
+    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                algo=ALGO_DENSE_FW)
+    assert st.dist_enc == LEVELS and 1 <= st.levels <= 254, (st.dist_enc, st.levels)
+    _check(g, lat, rel, kind)
+
+
+def test_levels_over_budget_falls_back(gpu, monkeypatch):
+    """A ring of 200-ms hops: distances pass the 254-level budget, so the FW builds it."""
+    monkeypatch.setenv("SRT_DENSE_LEVELS", "1")
+    n = 300
+    src = np.arange(n, dtype=np.int32)
+    dst = ((src + 1) % n).astype(np.int32)
+    lat = np.full(n, 200 * MS, np.int64) + (src % 3) * MS
+    loss = (src % 7) / 1000.0
+    g = graphs.Graph(n, False, src, dst, lat, loss, "ring200")
+    lat_t, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                  algo=ALGO_DENSE_FW)
+    assert st.dist_enc != LEVELS and st.levels == 0
+    _check(g, lat_t, rel, "ring fallback")
+
+
+def test_levels_default_at_4096(gpu):
+    """n = 4,096: the default dispatch takes the levels (no environment), rows vs the oracle."""
+    import torch
+    L = _lib.lib()
+    n = ld = 4096
+    w = torch.empty((ld, ld), dtype=torch.int32, device="cuda")
+    r = torch.empty((ld, ld), dtype=torch.float64, device="cuda")
+    _lib.check(L.srt_gen_complete_device(n, ld, 0, ld, 6, 1000, 10, 500, w.data_ptr(),
+                                         r.data_ptr(), None), "generate")
+    lat = torch.empty_like(w)
+    rel = torch.empty_like(r)
+    st = _lib.BuildStats()
+    st.time_kernels = 1
+    _lib.check(L.srt_dense_build_device(n, ld, 0, w.data_ptr(), r.data_ptr(), lat.data_ptr(),
+                                        rel.data_ptr(), None, 0, ctypes.byref(st)), "build")
+    torch.cuda.synchronize()
+    assert st.dist_enc == LEVELS, st.dist_enc
+    assert st.n_update == st.levels and st.work_bytes > 0
+    rows = np.array([0, 1, 777, 2048, 4000, 4095], np.int32)
+    idx = torch.from_numpy(rows.astype(np.int64)).cuda()
+    glat = lat.index_select(0, idx).cpu().numpy().view(np.uint32).astype(np.uint64) * np.uint64(MS)
+    grel = rel.index_select(0, idx).cpu().numpy()
+    clat, crel, _, _ = oracle.complete_sample(n, 6, 1000, 10, 500, rows, 8)
+    off = np.arange(n)[None, :] != rows[:, None]
+    assert np.array_equal(np.where(off, glat, 0), np.where(off, clat, 0))
+    err = np.abs(grel - crel) / np.maximum(crel, 1e-300)
+    assert float(err[off].max()) <= REL_TOL
+
+
+@pytest.mark.parametrize("ranks", [2, 3])
+@pytest.mark.parametrize("kind", ["complete", "ties"])
+def test_levels_virtual_ranks(gpu, monkeypatch, ranks, kind):
+    """Row-sharded level builds: every rank extracts the in-arcs of its rows, broadcasts its
+    segment, settles its own sources, and all ranks agree on the verdict (ld = 1,024: at 3 ranks
+    the row blocks are 384 | 256 | 384)."""
+    monkeypatch.setenv("SRT_DENSE_LEVELS", "1")
+    monkeypatch.setenv("SRT_VIRTUAL_RANKS", str(ranks))
+    g = graphs.complete_graph(1000, seed=2) if kind == "complete" else \
+        graphs.complete_graph(900, seed=4, lat_max=4)
+    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                algo=ALGO_DENSE_FW, ngpus=1)
+    assert st.dist_enc == LEVELS, st.dist_enc
+    _check(g, lat, rel, f"virtual x{ranks} {kind}")
