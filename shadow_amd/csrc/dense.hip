@@ -1736,7 +1736,8 @@ static int dense_path_ms(int32_t n, int32_t ld, int32_t row0, int32_t nrows, con
 
 /* Dial levels (levels.hip) instead of the FW when the graph's distances are small enough for the
  * level budget to beat the FW's predicted time (61 T relaxations/s, the measured update rate;
- * symmetric rounds do half the relaxations). n >= 4,096: below that the FW's squaring or rounds
+ * symmetric rounds do half the relaxations, plus the rounds' chain). n >= 4,096: below that the
+ * FW's squaring or rounds
  * cost less than the levels' launches. SRT_DENSE_LEVELS=0 keeps the FW, =1 tries the levels at any
  * size. *exact = 1 when the levels settled every pair (the u16 matrix and lat rows are final). */
 static int dense_try_levels(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
@@ -1746,7 +1747,8 @@ static int dense_try_levels(const srt_comm* comm, int n, int ld, int row0, int n
     const char* env = getenv("SRT_DENSE_LEVELS");
     const int mode = env ? atoi(env) : -1;
     if (mode == 0 || (mode < 0 && n < 4096) || ld % 128) return SRT_OK;
-    const double fw_ms = (double)nrows * ld * ld / (directed ? 1.0 : 2.0) / 6.1e10;
+    /* relaxations at the update's rate + ~50 us of round chain per 128 pivots */
+    const double fw_ms = (double)nrows * ld * ld / (directed ? 1.0 : 2.0) / 6.1e10 + ld / 128 * 0.05;
     if (evp) {
         evp->used = 0;
         evp->group = 2;

@@ -7,8 +7,9 @@
  * running lazy Dijkstra under a global lock. Which row serves a pair -- the first source run that
  * stored it, as in the reference's lazy cache (:1189-1215, :1917-1967) -- is decided by
  * pairorder.c. Tables are immutable once built, so lookups are lock-free once their pair is
- * stored; the IP -> vertex map (attach/detach), a first run per source and the packet counters
- * take locks.
+ * stored: the IP -> vertex map is read without a lock (writers -- attach, detach -- serialise among
+ * themselves), the packet counters are atomic, and only a pair's first lookup (a source run)
+ * takes the pair order's lock.
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -34,12 +35,24 @@ extern void worker_updateMinTimeJump(double minPathLatency);
 
 #define TOPOLOGY_MAGIC 0x70b0109au
 
-/* ---- u32 -> i32 map (IP in network order -> vertex) --------------------------------------- */
+/* ---- u32 -> i32 map (IP in network order -> vertex), lock-free reads ----------------------
+ * Open addressing over 64-bit slot words (key << 32 | (u32)value; value -1 = empty, -2 =
+ * tombstone), so a reader sees a key and its value in one atomic load. Writers (attach, detach)
+ * serialise on ip_lock; a resize builds a new table and publishes it with release, and the old one
+ * stays allocated until topology_free, so a reader that loaded it keeps reading valid memory (a
+ * consistent earlier state of the map). Readers take no lock. */
+typedef struct ipmap_tab {
+    size_t cap, used; /* used: live + tombstones (probe-chain length bound) */
+    struct ipmap_tab* retired;
+    _Atomic uint64_t slot[];
+} ipmap_tab;
+
 typedef struct {
-    uint32_t* keys;
-    int32_t* vals; /* -1 empty, -2 tombstone */
-    size_t cap, used;
+    _Atomic(ipmap_tab*) cur;
+    ipmap_tab* retired; /* replaced tables, freed at topology_free */
 } ipmap_t;
+
+#define IPM_EMPTY 0xFFFFFFFFull /* value -1 */
 
 static size_t h32(uint32_t x) {
     x ^= x >> 16;
@@ -50,109 +63,163 @@ static size_t h32(uint32_t x) {
     return x;
 }
 
+static uint64_t ipm_word(uint32_t k, int32_t v) { return ((uint64_t)k << 32) | (uint32_t)v; }
+static int32_t ipm_val(uint64_t w) { return (int32_t)(uint32_t)w; }
+static uint32_t ipm_key(uint64_t w) { return (uint32_t)(w >> 32); }
+
+static ipmap_tab* ipm_alloc(size_t cap) {
+    ipmap_tab* t = (ipmap_tab*)malloc(sizeof(ipmap_tab) + cap * sizeof(uint64_t));
+    if (!t) return NULL;
+    t->cap = cap;
+    t->used = 0;
+    t->retired = NULL;
+    for (size_t i = 0; i < cap; i++) atomic_init(&t->slot[i], IPM_EMPTY);
+    return t;
+}
+
+/* caller holds ip_lock (writer) */
 static int ipmap_put(ipmap_t* m, uint32_t k, int32_t v) {
-    if ((m->used + 1) * 2 > m->cap) {
-        size_t nc = m->cap ? m->cap * 2 : 64;
-        uint32_t* nk = (uint32_t*)malloc(nc * sizeof(uint32_t));
-        int32_t* nv = (int32_t*)malloc(nc * sizeof(int32_t));
-        if (!nk || !nv) {
-            free(nk);
-            free(nv);
-            return -1;
+    ipmap_tab* t = atomic_load_explicit(&m->cur, memory_order_relaxed);
+    if (!t || (t->used + 1) * 2 > t->cap) { /* grow (or drop tombstones): a new table */
+        const size_t nc = t ? t->cap * 2 : 64;
+        ipmap_tab* nt = ipm_alloc(nc);
+        if (!nt) return -1;
+        for (size_t i = 0; t && i < t->cap; i++) {
+            const uint64_t w = atomic_load_explicit(&t->slot[i], memory_order_relaxed);
+            if (ipm_val(w) < 0) continue;
+            size_t h = h32(ipm_key(w)) & (nc - 1);
+            while (ipm_val(atomic_load_explicit(&nt->slot[h], memory_order_relaxed)) != -1)
+                h = (h + 1) & (nc - 1);
+            atomic_store_explicit(&nt->slot[h], w, memory_order_relaxed);
+            nt->used++;
         }
-        for (size_t i = 0; i < nc; i++) nv[i] = -1;
-        size_t used = 0;
-        for (size_t i = 0; i < m->cap; i++)
-            if (m->vals[i] >= 0) {
-                size_t h = h32(m->keys[i]) & (nc - 1);
-                while (nv[h] >= 0) h = (h + 1) & (nc - 1);
-                nk[h] = m->keys[i];
-                nv[h] = m->vals[i];
-                used++;
-            }
-        free(m->keys);
-        free(m->vals);
-        m->keys = nk;
-        m->vals = nv;
-        m->cap = nc;
-        m->used = used;
+        atomic_store_explicit(&m->cur, nt, memory_order_release);
+        if (t) {
+            t->retired = m->retired;
+            m->retired = t;
+        }
+        t = nt;
     }
-    size_t h = h32(k) & (m->cap - 1);
-    size_t tomb = (size_t)-1;
-    while (m->vals[h] != -1) {
-        if (m->vals[h] >= 0 && m->keys[h] == k) {
-            m->vals[h] = v;
+    size_t h = h32(k) & (t->cap - 1), tomb = (size_t)-1;
+    for (;;) {
+        const uint64_t w = atomic_load_explicit(&t->slot[h], memory_order_relaxed);
+        const int32_t x = ipm_val(w);
+        if (x == -1) break;
+        if (x >= 0 && ipm_key(w) == k) {
+            atomic_store_explicit(&t->slot[h], ipm_word(k, v), memory_order_release);
             return 0;
         }
-        if (m->vals[h] == -2 && tomb == (size_t)-1) tomb = h;
-        h = (h + 1) & (m->cap - 1);
+        if (x == -2 && tomb == (size_t)-1) tomb = h;
+        h = (h + 1) & (t->cap - 1);
     }
-    if (tomb != (size_t)-1) h = tomb;
-    else m->used++;
-    m->keys[h] = k;
-    m->vals[h] = v;
+    if (tomb != (size_t)-1)
+        h = tomb;
+    else
+        t->used++;
+    atomic_store_explicit(&t->slot[h], ipm_word(k, v), memory_order_release);
     return 0;
 }
 
+/* no lock: one acquire load of the table, then of each probed slot */
 static int32_t ipmap_get(const ipmap_t* m, uint32_t k) {
-    if (!m->cap) return -1;
-    size_t h = h32(k) & (m->cap - 1);
-    while (m->vals[h] != -1) {
-        if (m->vals[h] >= 0 && m->keys[h] == k) return m->vals[h];
-        h = (h + 1) & (m->cap - 1);
+    const ipmap_tab* t = atomic_load_explicit(&((ipmap_t*)m)->cur, memory_order_acquire);
+    if (!t) return -1;
+    size_t h = h32(k) & (t->cap - 1);
+    for (size_t probes = 0; probes < t->cap; probes++) {
+        const uint64_t w = atomic_load_explicit(&((ipmap_tab*)t)->slot[h], memory_order_acquire);
+        const int32_t x = ipm_val(w);
+        if (x == -1) return -1;
+        if (x >= 0 && ipm_key(w) == k) return x;
+        h = (h + 1) & (t->cap - 1);
     }
     return -1;
 }
 
+/* caller holds ip_lock (writer) */
 static void ipmap_del(ipmap_t* m, uint32_t k) {
-    if (!m->cap) return;
-    size_t h = h32(k) & (m->cap - 1);
-    while (m->vals[h] != -1) {
-        if (m->vals[h] >= 0 && m->keys[h] == k) {
-            m->vals[h] = -2;
+    ipmap_tab* t = atomic_load_explicit(&m->cur, memory_order_relaxed);
+    if (!t) return;
+    size_t h = h32(k) & (t->cap - 1);
+    for (;;) {
+        const uint64_t w = atomic_load_explicit(&t->slot[h], memory_order_relaxed);
+        const int32_t x = ipm_val(w);
+        if (x == -1) return;
+        if (x >= 0 && ipm_key(w) == k) {
+            atomic_store_explicit(&t->slot[h], ipm_word(k, -2), memory_order_release);
             return;
         }
-        h = (h + 1) & (m->cap - 1);
+        h = (h + 1) & (t->cap - 1);
     }
 }
 
-/* ---- packet counters, one per cached Path (the served pair's source, target) ------------ */
+static void ipmap_free(ipmap_t* m) {
+    free(atomic_load(&m->cur));
+    for (ipmap_tab* t = m->retired; t;) {
+        ipmap_tab* nx = t->retired;
+        free(t);
+        t = nx;
+    }
+}
+
+/* ---- packet counters, one per cached Path (the served pair's source, target) ------------
+ * Lock-free: per source vertex a directory of 1,024-counter pages over the targets, both
+ * allocated on first use and installed by compare-and-swap (a loser frees its copy); an increment
+ * is one relaxed fetch-add (topology.c:1983-1993: path_incrementPacketCount on the cached Path). */
+#define CNT_PAGE 1024
 typedef struct {
-    uint64_t* keys;
-    uint64_t* cnt;
-    size_t cap, used;
+    int32_t n, npages;
+    _Atomic(_Atomic(_Atomic uint64_t*)*)* dir; /* n directories of npages page pointers */
 } cntmap_t;
 
-static uint64_t* cnt_slot(cntmap_t* m, uint64_t k) {
-    if ((m->used + 1) * 2 > m->cap) {
-        size_t nc = m->cap ? m->cap * 2 : 1024;
-        uint64_t* nk = (uint64_t*)calloc(nc, sizeof(uint64_t));
-        uint64_t* nv = (uint64_t*)calloc(nc, sizeof(uint64_t));
-        if (!nk || !nv) {
-            free(nk);
-            free(nv);
-            return NULL;
+static int cnt_init(cntmap_t* m, int32_t n) {
+    m->n = n;
+    m->npages = (n + CNT_PAGE - 1) / CNT_PAGE;
+    m->dir = calloc((size_t)n, sizeof(*m->dir));
+    return m->dir ? 0 : -1;
+}
+
+static _Atomic uint64_t* cnt_slot(cntmap_t* m, int32_t from, int32_t to, int create) {
+    _Atomic(_Atomic uint64_t*)* d = atomic_load_explicit(&m->dir[from], memory_order_acquire);
+    if (!d) {
+        if (!create) return NULL;
+        _Atomic(_Atomic uint64_t*)* nd = calloc((size_t)m->npages, sizeof(*nd));
+        if (!nd) return NULL;
+        _Atomic(_Atomic uint64_t*)* exp = NULL;
+        if (atomic_compare_exchange_strong_explicit(&m->dir[from], &exp, nd, memory_order_acq_rel,
+                                                    memory_order_acquire))
+            d = nd;
+        else {
+            free(nd);
+            d = exp;
         }
-        for (size_t i = 0; i < m->cap; i++)
-            if (m->keys[i]) {
-                size_t h = h32((uint32_t)(m->keys[i] ^ (m->keys[i] >> 32))) & (nc - 1);
-                while (nk[h]) h = (h + 1) & (nc - 1);
-                nk[h] = m->keys[i];
-                nv[h] = m->cnt[i];
-            }
-        free(m->keys);
-        free(m->cnt);
-        m->keys = nk;
-        m->cnt = nv;
-        m->cap = nc;
     }
-    size_t h = h32((uint32_t)(k ^ (k >> 32))) & (m->cap - 1);
-    while (m->keys[h] && m->keys[h] != k) h = (h + 1) & (m->cap - 1);
-    if (!m->keys[h]) {
-        m->keys[h] = k;
-        m->used++;
+    _Atomic uint64_t* pg = atomic_load_explicit(&d[to / CNT_PAGE], memory_order_acquire);
+    if (!pg) {
+        if (!create) return NULL;
+        _Atomic uint64_t* np = calloc(CNT_PAGE, sizeof(*np));
+        if (!np) return NULL;
+        _Atomic uint64_t* exp = NULL;
+        if (atomic_compare_exchange_strong_explicit(&d[to / CNT_PAGE], &exp, np,
+                                                    memory_order_acq_rel, memory_order_acquire))
+            pg = np;
+        else {
+            free(np);
+            pg = exp;
+        }
     }
-    return &m->cnt[h];
+    return &pg[to % CNT_PAGE];
+}
+
+static void cnt_free(cntmap_t* m) {
+    if (!m->dir) return;
+    for (int32_t v = 0; v < m->n; v++) {
+        _Atomic(_Atomic uint64_t*)* d = atomic_load(&m->dir[v]);
+        if (!d) continue;
+        for (int32_t p = 0; p < m->npages; p++) free((void*)atomic_load(&d[p]));
+        free((void*)d);
+    }
+    free((void*)m->dir);
+    m->dir = NULL;
 }
 
 /* ---- the topology object -------------------------------------------------------------- */
@@ -196,8 +263,7 @@ struct _Topology {
     double min_path_ms;
     srt_build_opts opts;
     srt_build_stats stats;
-    /* counters */
-    pthread_mutex_t cnt_lock;
+    /* counters (lock-free) */
     cntmap_t counters;
     /* attach index (built on the first attach) */
     pthread_mutex_t ax_lock;
@@ -532,7 +598,6 @@ static Topology* topology_from_text(const char* text, size_t len, int useShortes
     t->use_shortest_path = useShortestPath ? 1 : 0;
     pthread_rwlock_init(&t->ip_lock, NULL);
     pthread_mutex_init(&t->build_lock, NULL);
-    pthread_mutex_init(&t->cnt_lock, NULL);
     pthread_mutex_init(&t->ax_lock, NULL);
     pthread_mutex_init(&t->min_lock, NULL);
     atomic_store(&t->tb, NULL);
@@ -554,7 +619,7 @@ static Topology* topology_from_text(const char* text, size_t len, int useShortes
         return NULL;
     }
     t->po = srt_pair_order_new(t->n, t->directed, t->use_shortest_path);
-    if (!t->po) {
+    if (!t->po || cnt_init(&t->counters, t->n)) {
         srt_log(SRT_LOG_ERROR, "out of memory for the path order of %d vertices", t->n);
         topology_free(t);
         return NULL;
@@ -603,15 +668,12 @@ void topology_free(Topology* t) {
     free(t->attached);
     free(t->elat_ns);
     free(t->eloss);
-    free(t->ipmap.keys);
-    free(t->ipmap.vals);
+    ipmap_free(&t->ipmap);
     tables_free_all(atomic_load(&t->tb));
-    free(t->counters.keys);
-    free(t->counters.cnt);
+    cnt_free(&t->counters);
     gml_free(&t->gml);
     pthread_rwlock_destroy(&t->ip_lock);
     pthread_mutex_destroy(&t->build_lock);
-    pthread_mutex_destroy(&t->cnt_lock);
     attach_index_free(t);
     srt_pair_order_free(t->po);
     pthread_mutex_destroy(&t->ax_lock);
@@ -1015,12 +1077,10 @@ void topology_detach(Topology* t, Address* address) {
     srt_topology_detach_ip(t, address_toNetworkIP(address));
 }
 
+/* lock-free (the packet path's two lookups per call, topology.c:1905-1915) */
 int32_t srt_topology_vertex_of_ip(Topology* t, uint32_t ipNet) {
     if (!magic_ok(t)) return -1;
-    pthread_rwlock_rdlock(&t->ip_lock);
-    int32_t v = ipmap_get(&t->ipmap, ipNet);
-    pthread_rwlock_unlock(&t->ip_lock);
-    return v;
+    return ipmap_get(&t->ipmap, ipNet);
 }
 
 /* ---- build + lookups ------------------------------------------------------------------ */
@@ -1316,16 +1376,11 @@ double srt_topology_reliability_ip(Topology* t, uint32_t srcIp, uint32_t dstIp) 
 
 /* the served Path (source, target) -- path_incrementPacketCount on the cached object (:1983-1993);
  * a pair has one Path whichever direction is looked up */
-static uint64_t counter_key(int64_t from, int64_t to) {
-    return ((uint64_t)from << 32 | (uint64_t)to) + 1; /* 0 = empty slot */
-}
-
 static int increment_pair(Topology* t, int32_t from, int32_t to) {
-    pthread_mutex_lock(&t->cnt_lock);
-    uint64_t* c = cnt_slot(&t->counters, counter_key(from, to));
-    if (c) (*c)++;
-    pthread_mutex_unlock(&t->cnt_lock);
-    return c ? SRT_OK : SRT_E_NOMEM;
+    _Atomic uint64_t* c = cnt_slot(&t->counters, from, to, 1);
+    if (!c) return SRT_E_NOMEM;
+    atomic_fetch_add_explicit(c, 1, memory_order_relaxed);
+    return SRT_OK;
 }
 
 int srt_topology_increment_ip(Topology* t, uint32_t srcIp, uint32_t dstIp) {
@@ -1351,11 +1406,8 @@ uint64_t srt_topology_packet_count_ip(Topology* t, uint32_t srcIp, uint32_t dstI
     if (s < 0 || d < 0) return 0;
     const int32_t from = srt_pair_order_peek(t->po, s, d);
     if (from < 0) return 0;
-    pthread_mutex_lock(&t->cnt_lock);
-    uint64_t* c = cnt_slot(&t->counters, counter_key(from, from == s ? d : s));
-    uint64_t v = c ? *c : 0;
-    pthread_mutex_unlock(&t->cnt_lock);
-    return v;
+    _Atomic uint64_t* c = cnt_slot(&t->counters, from, from == s ? d : s, 0);
+    return c ? atomic_load_explicit(c, memory_order_relaxed) : 0;
 }
 
 /* worker_sendPacket (/root/reference/src/main/core/worker.c:541-555): the fate of one packet on
