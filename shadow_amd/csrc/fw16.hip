@@ -2302,8 +2302,8 @@ static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStrea
                        evpool_t* evp, int* exact);
 
 /* Distances by bit-parallel Dial levels (levels.hip) straight into the u16 FW matrix of this slot
- * (0 on the diagonal, cap on padding), then the same finish pass as the FW: u32 rows, exactness and
- * small-distance flags. *nlev = the level that settled every pair, or 0 when the levels do not
+ * (0 on the diagonal, cap on padding) and the u32 rows -- exact and small by construction (the FW
+ * finish pass's outputs and flags). *nlev = the level that settled every pair, or 0 when the levels do not
  * apply or miss their budget -- the caller then runs the FW. */
 int srt_fw16_levels(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
                     const uint32_t* w_rows, uint32_t* lat_rows, hipStream_t st, evpool_t* evp,
@@ -2320,21 +2320,10 @@ int srt_fw16_levels(const srt_comm* comm, int n, int ld, int row0, int nrows, in
         fw16_caps[dev] = need;
     }
     if (!fw16_flags[dev]) SRT_HIPCHK(hipMalloc(&fw16_flags[dev], 2 * sizeof(int)));
-    int rc = srt_levels_build(comm, n, ld, row0, nrows, directed, w_rows, fw16_bufs[dev], CAP_F,
-                              fw_ms, st, evp, nlev, bytes);
+    int rc = srt_levels_build(comm, n, ld, row0, nrows, directed, w_rows, fw16_bufs[dev], lat_rows,
+                              CAP_F, fw_ms, st, evp, nlev, bytes);
     if (rc || !*nlev) return rc;
-    SRT_HIPCHK(hipMemsetAsync(fw16_flags[dev], 0, 2 * sizeof(int), st));
-    fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 2048), nrows), 256, 0, st>>>(
-        n, ld, row0, fw16_bufs[dev], lat_rows, fw16_flags[dev], CAP_F);
-    SRT_HIPCHK(hipGetLastError());
-    int hf[2] = {0, 0};
-    SRT_HIPCHK(hipMemcpyAsync(hf, fw16_flags[dev], 2 * sizeof(int), hipMemcpyDeviceToHost, st));
-    SRT_HIPCHK(hipStreamSynchronize(st));
-    if (hf[0]) { /* cannot happen: every settled distance is <= the level budget (<= 254) */
-        srt_set_error("levels: a settled distance reached the u16 cap");
-        return SRT_E_RANGE;
-    }
-    fw16_small[dev] = hf[1] ? 0 : 1;
+    fw16_small[dev] = 1; /* every settled distance is <= the level budget (<= 254 quanta) */
     return SRT_OK;
 }
 

@@ -126,6 +126,13 @@ __global__ void lvl_mask_kernel(size_t count, int lmax, int32_t* __restrict__ cn
     if (i < count && (int)(i % LVL_STRIDE) > lmax) cnt[i] = 0;
 }
 
+/* byte offset of each arc's source row inside a level plane (k * nw * 4; nw is this rank's) */
+__global__ void lvl_aoff_kernel(int total, int nw, const uint32_t* __restrict__ arcs,
+                                uint32_t* __restrict__ aoff) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < total) aoff[i] = (arcs[i] & 0xFFFFu) * (uint32_t)nw * 4u;
+}
+
 /* ---- the levels ---------------------------------------------------------------------------- */
 /* R = {j} for the local sources j (distance 0), everything else empty */
 __global__ void lvl_init_kernel(int n, int src0, int nsrc, int nw, uint32_t* __restrict__ R) {
@@ -142,6 +149,7 @@ __global__ __launch_bounds__(256) void lvl_step_kernel(int d, int n, int nw, int
                                                        int nsrc, unsigned nblk,
                                                        const int32_t* __restrict__ off,
                                                        const uint32_t* __restrict__ arcs,
+                                                       const uint32_t* __restrict__ aoff,
                                                        uint32_t* __restrict__ lev,
                                                        uint32_t* __restrict__ R,
                                                        uint8_t* __restrict__ done,
@@ -173,25 +181,25 @@ __global__ __launch_bounds__(256) void lvl_step_kernel(int d, int n, int nw, int
             if ((unsigned)ks < (unsigned)nsrc && (ks >> 5) == word) acc |= 1u << (ks & 31);
         }
     }
-    /* arcs of weight < d: Delta_{d-w}[k], eight gathers in flight; lanes past nw read word 0 of
-     * the row (a valid address) and drop it, so the loop has no per-lane branch and the eight arcs
-     * come in one scalar load */
-    const int b0 = oj[1], b1 = oj[d];
-    const uint32_t* lw = lev + (valid ? word : 0); /* lane base */
-    int i = b0;
-    for (; i + 8 <= b1; i += 8) {
-        uint32_t a[8], v[8];
+    /* arcs of weight w < d: Delta_{d-w}[k], one weight group at a time so the group's plane base is
+     * one scalar pointer and an arc costs one VALU add (its row's byte offset k * nw * 4, aoff, plus
+     * the lane's) and one gather; eight gathers in flight. Lanes past nw read word 0 of the row (a
+     * valid address) and drop it, so the loop has no per-lane branch. */
+    const uint32_t lane4 = (uint32_t)(valid ? word : 0) * 4u;
+    for (int w = 1; w < d; ++w) {
+        const int g1 = oj[w + 1];
+        const char* base = reinterpret_cast<const char*>(lev + (size_t)(d - w - 1) * plane);
+        int i = oj[w];
+        for (; i + 8 <= g1; i += 8) {
+            uint32_t a[8], v[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) a[q] = arcs[i + q];
+            for (int q = 0; q < 8; ++q) a[q] = aoff[i + q];
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-            v[q] = lw[(size_t)(d - (int)(a[q] >> 16) - 1) * plane + (size_t)(a[q] & 0xFFFFu) * nw];
+            for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const uint32_t*>(base + (a[q] + lane4));
 #pragma unroll
-        for (int q = 0; q < 8; ++q) acc |= v[q];
-    }
-    for (; i < b1; ++i) {
-        const uint32_t a = arcs[i];
-        acc |= lw[(size_t)(d - (int)(a >> 16) - 1) * plane + (size_t)(a & 0xFFFFu) * nw];
+            for (int q = 0; q < 8; ++q) acc |= v[q];
+        }
+        for (; i < g1; ++i) acc |= *reinterpret_cast<const uint32_t*>(base + (aoff[i] + lane4));
     }
     if (!valid) acc = 0;
     bool inc = false;
@@ -206,48 +214,67 @@ __global__ __launch_bounds__(256) void lvl_step_kernel(int d, int n, int nw, int
         const uint32_t full = s0 + 32 <= n ? 0xFFFFFFFFu : s0 >= n ? 0u : (1u << (n - s0)) - 1u;
         inc = ((r | nb) & full) != full;
     }
+    /* completion: a flag, not a count -- one same-address atomic per wave serialised at the memory
+     * side (~6 ms per level at C4's 524k units); the flag is read first (an L2 hit once set), so
+     * only the first few waves of a level store it */
     const unsigned long long m = __ballot(inc);
     if (lane == 0) {
-        if (m)
-            atomicAdd(incomplete, 1);
-        else
+        if (!m)
             done[u] = 1;
+        else if (!__hip_atomic_load(incomplete, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            __hip_atomic_store(incomplete, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
-/* distance rows of the local sources (u16, row stride ld, the FW matrix layout: 0 on the diagonal,
- * cap where nothing was reached, cap on padding). Thread = target t (256 per workgroup), looping
- * over 16 source words: it reads word (t, sw) of every level (one 64-B line per thread across the
- * 16 words) and writes its column of the word's 32 source rows (each row a 512-B segment per
- * workgroup). */
-__global__ __launch_bounds__(256) void lvl_d16_kernel(int n, int ld, int nw, int src0, int nlev,
+/* Distance rows of the local sources from the levels, in the FW matrix layout (u16, row stride
+ * ld: 0 on the diagonal, cap on padding) and as the u32 table rows (SRT_INF on padding) -- the FW
+ * finish pass folded in: every settled distance is <= the level budget (<= 254), so the rows are
+ * exact and small by construction. Thread = four consecutive targets t0..t0 + 3 (256 threads = 1,024
+ * targets per workgroup), looping over 16 source words: per word it reads the four targets' word
+ * of every level (the same lines for the 16 words of a workgroup row) and writes 8 B of u16 and
+ * 16 B of u32 per source row. */
+__global__ __launch_bounds__(256) void lvl_out_kernel(int n, int ld, int nw, int src0, int nlev,
                                                       const uint32_t* __restrict__ lev,
-                                                      uint16_t* __restrict__ d16, uint32_t cap) {
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= ld) return;
+                                                      uint16_t* __restrict__ d16,
+                                                      uint32_t* __restrict__ lat, uint32_t cap) {
+    const int t0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (t0 >= ld) return;
     const size_t plane = (size_t)n * nw;
     const int sw1 = min(nw, (int)(blockIdx.y + 1) * 16);
     for (int sw = blockIdx.y * 16; sw < sw1; ++sw) {
-        uint32_t m[8]; /* levels read eight at a time */
-        uint16_t v[32];
+        uint32_t v[32][2]; /* per source: targets t0, t0+1 | t0+2, t0+3 as u16 pairs */
+        const int sg0 = src0 + sw * 32;
 #pragma unroll
-        for (int s = 0; s < 32; ++s) v[s] = (uint16_t)(src0 + sw * 32 + s == t ? 0u : cap);
-        if (t < n) {
-            for (int d0 = 1; d0 <= nlev; d0 += 8) {
+        for (int s = 0; s < 32; ++s) {
+            const int sg = sg0 + s;
+            v[s][0] = (sg == t0 ? 0u : cap) | ((sg == t0 + 1 ? 0u : cap) << 16);
+            v[s][1] = (sg == t0 + 2 ? 0u : cap) | ((sg == t0 + 3 ? 0u : cap) << 16);
+        }
+        for (int d = 1; d <= nlev; ++d) {
+            uint32_t m[4];
 #pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    m[q] = d0 + q <= nlev ? lev[(size_t)(d0 + q - 1) * plane + (size_t)t * nw + sw] : 0u;
+            for (int q = 0; q < 4; ++q)
+                m[q] = t0 + q < n ? lev[(size_t)(d - 1) * plane + (size_t)(t0 + q) * nw + sw] : 0u;
+            if (!(m[0] | m[1] | m[2] | m[3])) continue;
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    if (!m[q]) continue;
+            for (int s = 0; s < 32; ++s) {
 #pragma unroll
-                    for (int s = 0; s < 32; ++s)
-                        if ((m[q] >> s) & 1u) v[s] = (uint16_t)(d0 + q);
-                }
+                for (int q = 0; q < 4; ++q)
+                    if ((m[q] >> s) & 1u) {
+                        const int h = 16 * (q & 1);
+                        v[s][q >> 1] = (v[s][q >> 1] & ~(0xFFFFu << h)) | ((uint32_t)d << h);
+                    }
             }
         }
 #pragma unroll
-        for (int s = 0; s < 32; ++s) d16[(size_t)(sw * 32 + s) * ld + t] = v[s];
+        for (int s = 0; s < 32; ++s) {
+            const size_t o = (size_t)(sw * 32 + s) * ld + t0;
+            *reinterpret_cast<uint2*>(d16 + o) = make_uint2(v[s][0], v[s][1]);
+            uint32_t x[4] = {v[s][0] & 0xFFFFu, v[s][0] >> 16, v[s][1] & 0xFFFFu, v[s][1] >> 16};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) x[q] = x[q] == cap ? SRT_INF : x[q];
+            *reinterpret_cast<uint4*>(lat + o) = make_uint4(x[0], x[1], x[2], x[3]);
+        }
     }
 }
 
@@ -273,10 +300,12 @@ static double lvl_estimate(const unsigned long long* hist, int L, double ntgt, d
  * fw_ms: the predicted Floyd-Warshall time; the level budget keeps the predicted level time under
  * half of it. *levels = the level that settled every pair (0: not applicable / over budget -- the
  * caller runs Floyd-Warshall; every rank of a sharded build returns the same verdict).
- * *gather_bytes: the Delta words gathered (the kernel's algorithmic bytes). */
+ * *gather_bytes: the Delta words gathered (the kernel's algorithmic bytes). On success d16 and
+ * lat_rows hold the rows (the FW finish pass's outputs). */
 int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
-                     const uint32_t* w_rows, uint16_t* d16, uint32_t cap, double fw_ms,
-                     hipStream_t st, evpool_t* evp, int* levels, int64_t* gather_bytes) {
+                     const uint32_t* w_rows, uint16_t* d16, uint32_t* lat_rows, uint32_t cap,
+                     double fw_ms, hipStream_t st, evpool_t* evp, int* levels,
+                     int64_t* gather_bytes) {
     *levels = 0;
     *gather_bytes = 0;
     const int R = comm ? srt_comm_size(comm) : 1;
@@ -290,7 +319,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     SRT_HIPCHK(srt_malloc_async(&dhist, LVL_STRIDE * sizeof(unsigned long long), st));
     struct frees {
         hipStream_t s;
-        void* p[8] = {};
+        void* p[12] = {};
         int k = 0;
         ~frees() {
             for (int i = 0; i < k; i++) (void)hipFreeAsync(p[i], s);
@@ -373,6 +402,14 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     }
     /* level state over the local sources */
     const int nw = nrows / 32, nchunk = (nw + 63) / 64;
+    if ((size_t)n * nw * 4 > 0xFFFFFFFFull) return SRT_OK; /* 32-bit row offsets */
+    uint32_t* aoff = NULL;
+    SRT_HIPCHK(srt_malloc_async(&aoff, ((size_t)total + 8) * sizeof(uint32_t), st));
+    fr.p[fr.k++] = aoff;
+    if (total > 0) {
+        lvl_aoff_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, nw, arcs, aoff);
+        SRT_HIPCHK(hipGetLastError());
+    }
     const size_t plane = (size_t)n * nw;
     uint32_t *lev = NULL, *Rb = NULL;
     uint8_t* done = NULL;
@@ -395,8 +432,8 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     int64_t gathered = 0;
     for (int d = 1; d <= lmax; ++d) {
         if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
-        lvl_step_kernel<<<nblk, 256, 0, st>>>(d, n, nw, nchunk, row0, nrows, nblk, off, arcs, lev,
-                                              Rb, done, dinc + d);
+        lvl_step_kernel<<<nblk, 256, 0, st>>>(d, n, nw, nchunk, row0, nrows, nblk, off, arcs, aoff,
+                                              lev, Rb, done, dinc + d);
         if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
         SRT_HIPCHK(hipGetLastError());
         int inc = 0;
@@ -419,8 +456,8 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         SRT_HIPCHK(hipStreamSynchronize(st));
     }
     if (!ok) return SRT_OK;
-    lvl_d16_kernel<<<dim3(srt_ceil_div(ld, 256), srt_ceil_div(nw, 16)), 256, 0, st>>>(n, ld, nw, row0, D,
-                                                                                    lev, d16, cap);
+    lvl_out_kernel<<<dim3(srt_ceil_div(ld, 1024), srt_ceil_div(nw, 16)), 256, 0, st>>>(
+        n, ld, nw, row0, D, lev, d16, lat_rows, cap);
     SRT_HIPCHK(hipGetLastError());
     *levels = D;
     *gather_bytes = gathered;

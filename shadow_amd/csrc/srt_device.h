@@ -155,8 +155,9 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
                    void* ctx, int rank, int fm, int* sym, int* exact);
 /* levels.hip: u16 distance rows of the local sources by bit-parallel Dial levels (see there) */
 int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
-                     const uint32_t* w_rows, uint16_t* d16, uint32_t cap, double fw_ms,
-                     hipStream_t st, evpool_t* evp, int* levels, int64_t* gather_bytes);
+                     const uint32_t* w_rows, uint16_t* d16, uint32_t* lat_rows, uint32_t cap,
+                     double fw_ms, hipStream_t st, evpool_t* evp, int* levels,
+                     int64_t* gather_bytes);
 /* the same into this slot's FW matrix + the finish pass (fw16.hip); *nlev = 0: FW instead */
 int srt_fw16_levels(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
                     const uint32_t* w_rows, uint32_t* lat_rows, hipStream_t st, evpool_t* evp,
