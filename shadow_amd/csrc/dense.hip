@@ -1138,14 +1138,25 @@ static int grow_arcs(dense_ws* ws, size_t need) {
 typedef int (*ess_gather_fn)(void* ctx, dense_ws* ws, int n, int phase, int32_t total,
                              hipStream_t st);
 
+/* The post pass of a level build (levels.hip): the canonical predecessors and their arc
+ * reliabilities come straight from the level planes and the sorted in-arcs (lvl_pred_kernel,
+ * target-major like pred_cols*_kernel's output), so no essential-arc lists, slab transpose or
+ * predecessor search over the distances; then the same row transposes and path-order reliability
+ * passes as below. */
+static int dense_post_levels(int32_t n, int32_t ld, int32_t row0, int32_t nrows, uint32_t* d,
+                             double* rel, hipStream_t st, srt_build_stats* stats, dense_ws* ws,
+                             int lrows);
+
 static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_t directed,
                       const uint32_t* w, const double* r, uint32_t* d, const uint16_t* d16,
                       double* rel, hipStream_t st, srt_build_stats* stats, ess_gather_fn gather,
-                      void* gctx) {
+                      void* gctx, int lvl = 0) {
     dense_ws* ws;
     int rc = ws_get(&ws, n);
     if (rc) return rc;
     const int lrows = max(0, min(nrows, n - row0)); /* real (non-padding) local rows */
+    if (lvl) /* the distances came from the Dial levels: predecessors from the level planes */
+        return dense_post_levels(n, ld, row0, nrows, d, rel, st, stats, ws, lrows);
     SRT_HIPCHK(hipMemsetAsync(ws->cnt, 0, (size_t)(n + 1) * sizeof(int32_t), st));
     /* the exact u16 FW matrix when the build kept one: the same values in half the bytes
      * (C4: count 1.37 -> 1.08 ms, fill 1.52 -> 1.50 ms; SRT_ESS_U16=0 reads the u32 table) */
@@ -1381,6 +1392,66 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
     } else if (stats) {
         stats->ess_arcs = total;
     }
+    return SRT_OK;
+}
+
+static int dense_post_levels(int32_t n, int32_t ld, int32_t row0, int32_t nrows, uint32_t* d,
+                             double* rel, hipStream_t st, srt_build_stats* stats, dense_ws* ws,
+                             int lrows) {
+    int rc;
+    if (lrows > 0) {
+        const size_t slab = (size_t)ld * nrows;
+        size_t c1 = ws->dt_cap, c2 = ws->predt_cap, c4 = ws->rt_cap;
+        if ((rc = ws_grow((void**)&ws->dt, &c1, slab, sizeof(uint32_t)))) return rc;
+        ws->dt_cap = c1;
+        if ((rc = ws_grow((void**)&ws->predt, &c2, slab, sizeof(int32_t)))) return rc;
+        ws->predt_cap = c2;
+        if ((rc = ws_grow((void**)&ws->rt, &c4, slab, sizeof(double)))) return rc;
+        ws->rt_cap = c4;
+        const bool ties = stats && stats->count_ties;
+        if (ties) SRT_HIPCHK(hipMemsetAsync(ws->ties, 0, sizeof(unsigned long long), st));
+        if ((rc = srt_levels_pred(ws->predt, ws->rt, (size_t)nrows, ties ? ws->ties : NULL, st)))
+            return rc;
+        int32_t* pred = reinterpret_cast<int32_t*>(ws->dt);
+        transpose_kernel<uint32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+            n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows,
+            reinterpret_cast<uint32_t*>(pred), (size_t)ld);
+        transpose_kernel<double><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+            n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
+        SRT_HIPCHK(hipMemsetAsync(ws->depth, 0, sizeof(int32_t), st));
+        /* every level-built distance is <= 254 quanta: level order in place for every row that
+         * spans <= 64 quanta, sweeps for the rest (as dense_post) */
+        if (n <= 1024)
+            rel_levels_kernel<256, 1024><<<lrows, 256, 2048, st>>>(n, ld, row0, d, pred, rel, 64,
+                                                                  ws->depth, ws->cursor);
+        else if (n <= 4096)
+            rel_levels_kernel<512, 4096><<<lrows, 512, 8192, st>>>(n, ld, row0, d, pred, rel, 64,
+                                                                  ws->depth, ws->cursor);
+        else if (n <= 32768) {
+            SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 32768>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
+            rel_levels_kernel<1024, 32768><<<lrows, 1024, 65536, st>>>(n, ld, row0, d, pred, rel, 64,
+                                                                      ws->depth, ws->cursor);
+        } else {
+            SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 65536>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
+            rel_levels_kernel<1024, 65536><<<lrows, 1024, 131072, st>>>(n, ld, row0, d, pred, rel, 64,
+                                                                      ws->depth, ws->cursor);
+        }
+        SRT_HIPCHK(hipGetLastError());
+        if (n <= 32768) {
+            const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
+            SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            rel_sweeps_kernel<<<lrows, 512, lds, st>>>(n, ld, row0, pred, rel, ws->depth, ws->cursor);
+            SRT_HIPCHK(hipGetLastError());
+        } else if ((rc = srt_rel_sweeps_rows(n, lrows, row0, pred, (size_t)ld, rel, (size_t)ld,
+                                             ws->cursor, ws->depth, st))) {
+            return rc;
+        }
+    }
+    srt_levels_release(st);
+    if (stats) stats->ess_arcs = 0; /* no essential-arc lists in this form */
     return SRT_OK;
 }
 
@@ -1697,8 +1768,8 @@ extern "C" int srt_dense_rows_build(int32_t n, int32_t ld, int32_t nsub, const i
 
 int srt_dense_post_device(int32_t n, int32_t ld, int32_t directed, const uint32_t* w, const double* r,
                           uint32_t* d, const uint16_t* d16, double* rel, hipStream_t st,
-                          srt_build_stats* stats) {
-    int rc = dense_post(n, ld, 0, ld, directed, w, r, d, d16, rel, st, stats, NULL, NULL);
+                          srt_build_stats* stats, int lvl) {
+    int rc = dense_post(n, ld, 0, ld, directed, w, r, d, d16, rel, st, stats, NULL, NULL, lvl);
     if (rc) return rc;
     return dense_finish_rows(n, ld, 0, ld, w, r, d, rel, st, stats);
 }
@@ -1741,7 +1812,8 @@ static int dense_path_ms(int32_t n, int32_t ld, int32_t row0, int32_t nrows, con
  * cost less than the levels' launches. SRT_DENSE_LEVELS=0 keeps the FW, =1 tries the levels at any
  * size. *exact = 1 when the levels settled every pair (the u16 matrix and lat rows are final). */
 static int dense_try_levels(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
-                            const uint32_t* w_rows, uint32_t* lat_rows, hipStream_t st,
+                            const uint32_t* w_rows, const double* r_rows, uint32_t* lat_rows,
+                            hipStream_t st,
                             evpool_t* evp, srt_build_stats* stats, int* exact) {
     *exact = 0;
     const char* env = getenv("SRT_DENSE_LEVELS");
@@ -1755,7 +1827,7 @@ static int dense_try_levels(const srt_comm* comm, int n, int ld, int row0, int n
     }
     int nlev = 0;
     int64_t bytes = 0;
-    const int rc = srt_fw16_levels(comm, n, ld, row0, nrows, directed, w_rows, lat_rows, st, evp,
+    const int rc = srt_fw16_levels(comm, n, ld, row0, nrows, directed, w_rows, r_rows, lat_rows, st, evp,
                                    mode > 0 ? 1e30 : fw_ms, &nlev, &bytes);
     if (rc) return rc;
     if (stats) {
@@ -1792,7 +1864,7 @@ int srt_dense_build_device_ms(int32_t n, int32_t ld, int32_t directed, const uin
     /* narrowest exact encoding first: Dial levels (small distances) -> f16-compare u16 -> pk_min
      * u16 -> u32 */
     int exact = 0, enc = SRT_DENC_U32;
-    if ((rc = dense_try_levels(NULL, n, ld, 0, ld, directed, w, lat, st, evp, stats, &exact)))
+    if ((rc = dense_try_levels(NULL, n, ld, 0, ld, directed, w, r, lat, st, evp, stats, &exact)))
         return rc;
     if (exact) enc = SRT_DENC_LEVELS;
     for (int fm = 1; fm >= 0 && !exact && ld % 128 == 0; --fm) {
@@ -1824,7 +1896,7 @@ int srt_dense_build_device_ms(int32_t n, int32_t ld, int32_t directed, const uin
     }
     SRT_HIPCHK(hipEventRecord(e1, st));
     rc = srt_dense_post_device(n, ld, directed, w, r, lat, exact ? srt_fw16_matrix() : NULL, rel,
-                               st, stats);
+                               st, stats, enc == SRT_DENC_LEVELS);
     if (rc) return rc;
     if (lat_ms) {
         if ((rc = dense_path_ms(n, ld, 0, ld, lat, quantum_ns, lat_ms, st))) return rc;
@@ -1950,7 +2022,8 @@ int srt_dense_build_sharded_ms(srt_comm* comm, int32_t n, int32_t ld, int32_t di
     const char* sym_env = getenv("SRT_FW_SYM");
     /* symmetric rounds up to 1,024 tile columns (fw16.hip SYM_TMAX, the panel-position table) */
     const bool sym = !directed && R > 1 && ld <= 1024 * 128 && !(sym_env && atoi(sym_env) == 0);
-    if ((rc = dense_try_levels(comm, n, ld, b, nr, directed, w_rows, lat_rows, st, evp, stats, &exact)))
+    if ((rc = dense_try_levels(comm, n, ld, b, nr, directed, w_rows, r_rows, lat_rows, st, evp, stats,
+                               &exact)))
         return rc;
     if (exact) enc = SRT_DENC_LEVELS;
     for (int fm = 1; fm >= 0 && !exact; --fm) {
@@ -2005,7 +2078,7 @@ int srt_dense_build_sharded_ms(srt_comm* comm, int32_t n, int32_t ld, int32_t di
     SRT_HIPCHK(hipEventRecord(e1, st));
     rc = dense_post(n, ld, b, nr, directed, w_rows, r_rows, lat_rows,
                     exact ? srt_fw16_matrix() : NULL, rel_rows, st, stats,
-                    R > 1 ? shard_gather : NULL, &ctx);
+                    R > 1 ? shard_gather : NULL, &ctx, enc == SRT_DENC_LEVELS);
     if (rc) return rc;
     if ((rc = dense_finish_rows(n, ld, b, nr, w_rows, r_rows, lat_rows, rel_rows, st, stats))) return rc;
     if (lms_rows) {

@@ -476,69 +476,6 @@ static __device__ __forceinline__ uint32_t rowsum16(const uint32_t (&w)[4]) {
     return s;
 }
 
-struct fwh_stage_regs {
-    uint4 a[2], b[2];
-};
-
-static __device__ __forceinline__ void fwh_gload(fwh_stage_regs& g, const u16* __restrict__ A,
-                                                 const u16* __restrict__ B, size_t ld, int tid) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int ia = tid + q * 256, ra = ia & 127, ca = (ia >> 7) * 8; /* 128 rows x 32 pivots */
-        const int ib = tid + q * 256, rb = ib >> 4, cb = (ib & 15) * 8;  /* 32 pivots x 128 cols */
-        g.a[q] = *reinterpret_cast<const uint4*>(A + (size_t)ra * ld + ca);
-        g.b[q] = *reinterpret_cast<const uint4*>(B + (size_t)rb * ld + cb);
-    }
-}
-
-static __device__ __forceinline__ void fwh_swrite(const fwh_stage_regs& g, uint32_t* __restrict__ sA,
-                                                  u16* __restrict__ sB, int tid) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int ia = tid + q * 256, ra = ia & 127, ca = (ia >> 7) * 8;
-        const int ib = tid + q * 256, rb = ib >> 4, cb = (ib & 15) * 8;
-        const uint4 v = g.a[q];
-        uint32_t* d = sA + ((ca >> 1) * 128 + ra) * 2; /* pairs ca/2 .. ca/2+3 of row ra */
-        *reinterpret_cast<uint2*>(d) = make_uint2(splat(v.x & 0xFFFFu), splat(v.x >> 16));
-        *reinterpret_cast<uint2*>(d + 256) = make_uint2(splat(v.y & 0xFFFFu), splat(v.y >> 16));
-        *reinterpret_cast<uint2*>(d + 512) = make_uint2(splat(v.z & 0xFFFFu), splat(v.z >> 16));
-        *reinterpret_cast<uint2*>(d + 768) = make_uint2(splat(v.w & 0xFFFFu), splat(v.w >> 16));
-        *reinterpret_cast<uint4*>(sB + rb * UBS + cb) = g.b[q];
-    }
-}
-
-/* SYM: the A slice of tile row I is the pivot panel transposed, A[r][m] = P[m][I0 + r]; a thread
- * loads 8 rows of pivots 2p and 2p+1 (two coalesced 16-B pieces) and writes them pair-major */
-static __device__ __forceinline__ void fwh_gload_sym(fwh_stage_regs& g, const u16* __restrict__ Ph,
-                                                     int I0, const u16* __restrict__ B, size_t ld,
-                                                     int tid) {
-    const int p = tid >> 4, rg = tid & 15;
-    g.a[0] = *reinterpret_cast<const uint4*>(Ph + (size_t)(2 * p) * ld + I0 + rg * 8);
-    g.a[1] = *reinterpret_cast<const uint4*>(Ph + (size_t)(2 * p + 1) * ld + I0 + rg * 8);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int ib = tid + q * 256, rb = ib >> 4, cb = (ib & 15) * 8;
-        g.b[q] = *reinterpret_cast<const uint4*>(B + (size_t)rb * ld + cb);
-    }
-}
-
-static __device__ __forceinline__ void fwh_swrite_sym(const fwh_stage_regs& g,
-                                                      uint32_t* __restrict__ sA,
-                                                      u16* __restrict__ sB, int tid) {
-    const int p = tid >> 4, rg = tid & 15;
-    const uint32_t a0[4] = {g.a[0].x, g.a[0].y, g.a[0].z, g.a[0].w}; /* pivot 2p, rows 2i, 2i+1 */
-    const uint32_t a1[4] = {g.a[1].x, g.a[1].y, g.a[1].z, g.a[1].w}; /* pivot 2p+1 */
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<uint4*>(sA + ((p * 128) + rg * 8 + 2 * i) * 2) =
-            make_uint4(splat(a0[i] & 0xFFFFu), splat(a1[i] & 0xFFFFu), splat(a0[i] >> 16),
-                       splat(a1[i] >> 16));
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int ib = tid + q * 256, rb = ib >> 4, cb = (ib & 15) * 8;
-        *reinterpret_cast<uint4*>(sB + rb * UBS + cb) = g.b[q];
-    }
-}
 
 /* upper-triangle tile (I <= J) of linear index x among T tile rows: row I holds T - I tiles */
 static __device__ __forceinline__ void tri_decode(int x, int T, int* I, int* J) {
@@ -552,64 +489,7 @@ static __device__ __forceinline__ void tri_decode(int x, int T, int* I, int* J) 
     *J = i + (x - off(i));
 }
 
-/* LDS operand reads: B rows m, m+1 at the thread's 8 columns; A (splat pivots m, m+1) of 4 rows */
-static __device__ __forceinline__ void fwh_readB(uint4 (&b)[2], const u16* __restrict__ pb, int m) {
-    b[0] = *reinterpret_cast<const uint4*>(pb + m * UBS);
-    b[1] = *reinterpret_cast<const uint4*>(pb + (m + 1) * UBS);
-}
-static __device__ __forceinline__ void fwh_readA(uint2 (&a)[4], const uint32_t* __restrict__ pa, int m) {
-    const uint4 q0 = *reinterpret_cast<const uint4*>(pa + (m >> 1) * 256);
-    const uint4 q1 = *reinterpret_cast<const uint4*>(pa + (m >> 1) * 256 + 4);
-    a[0] = make_uint2(q0.x, q0.y);
-    a[1] = make_uint2(q0.z, q0.w);
-    a[2] = make_uint2(q1.x, q1.y);
-    a[3] = make_uint2(q1.z, q1.w);
-}
-/* rows r0..r0+3 of the thread's block, pivots m, m+1: 32 v_add_u32 + 16 v_pk_minimum3_f16 */
-template <int R0>
-static __device__ __forceinline__ void fwh_rows(uint32_t (&acc)[8][4], const uint2 (&a)[4],
-                                                const uint4 (&b)[2]) {
-    const uint32_t b0[4] = {b[0].x, b[0].y, b[0].z, b[0].w};
-    const uint32_t b1[4] = {b[1].x, b[1].y, b[1].z, b[1].w};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) relax_row4(acc[R0 + r], a[r].x, a[r].y, b0, b1);
-}
 
-#define FWH_PHASE __builtin_amdgcn_sched_barrier(0)
-static __device__ __forceinline__ void fwh_stage(uint32_t (&acc)[8][4], const uint32_t* __restrict__ sA,
-                                                 const u16* __restrict__ sB, int tx, int ty) {
-    const uint32_t* pa0 = sA + ty * 8 * 2; /* rows 0-3 of the thread's block (pair 0) */
-    const uint32_t* pa1 = pa0 + 4 * 2;     /* rows 4-7 */
-    const u16* pb = sB + tx * 8;
-    uint4 B0[2], B1[2];
-    uint2 A0[4], A1[4];
-    fwh_readB(B0, pb, 0);
-    fwh_readA(A0, pa0, 0);
-#pragma unroll 1
-    for (int m = 0; m < UKC; m += 4) {
-        /* every phase issues the reads the next phase needs, then computes on registers that
-         * were read one phase earlier (the clamped last reads are harmless re-reads) */
-        const int m2 = m + 2, m4 = min(m + 4, UKC - 2);
-        fwh_readA(A1, pa1, m);
-        FWH_PHASE;
-        fwh_rows<0>(acc, A0, B0);
-        FWH_PHASE;
-        fwh_readB(B1, pb, m2);
-        fwh_readA(A0, pa0, m2);
-        FWH_PHASE;
-        fwh_rows<4>(acc, A1, B0);
-        FWH_PHASE;
-        fwh_readA(A1, pa1, m2);
-        FWH_PHASE;
-        fwh_rows<0>(acc, A0, B1);
-        FWH_PHASE;
-        fwh_readB(B0, pb, m4);
-        fwh_readA(A0, pa0, m4);
-        FWH_PHASE;
-        fwh_rows<4>(acc, A1, B1);
-        FWH_PHASE;
-    }
-}
 
 /* Row-sharded symmetric rounds: of the tile pair (I, J) / (J, I), I != J, the rank owning row I
  * keeps (I, J) when I < J and I + J is even, or I > J and I + J is odd; the other one is its
@@ -630,7 +510,7 @@ static __host__ __device__ __forceinline__ bool sym_kept(int I, int J) {
  * I + J has the parity i0; 7 / 8 = mode 3 restricted to even / odd J (the sharded rounds' two
  * update streams). */
 /* The tile (I, J) the calling block of a mode-XM launch updates and its local tile row Iloc;
- * false when the block has nothing to do (see fwh_update_kernel for the modes). */
+ * false when the block has nothing to do (the modes: the comment above). */
 template <bool SYM, int XM>
 static __device__ __forceinline__ bool fw_tile_of(int ncol_tiles, int i0, int skip,
                                                   const uint32_t* __restrict__ tl, int te, int& I,
@@ -672,61 +552,19 @@ static __device__ __forceinline__ bool fw_tile_of(int ncol_tiles, int i0, int sk
     return true;
 }
 
-template <bool SYM, int XM = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void fwh_update_kernel(
-    u16* __restrict__ D, int ld, const u16* __restrict__ P, int k0, int ncol_tiles, int i0, int skip,
-    const uint32_t* __restrict__ tl, int te) {
-    __shared__ __attribute__((aligned(16))) uint32_t sA[UKC / 2 * 128 * 2];
-    __shared__ __attribute__((aligned(16))) u16 sB[UKC * UBS];
-    if constexpr (XM == 3 || XM == 6 || XM == 7 || XM == 8) FW_CHAIN_PRIO(); /* next-row tiles */
-    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
-    int I, J, Iloc;
-    if (!fw_tile_of<SYM, XM>(ncol_tiles, i0, skip, tl, te, I, J, Iloc)) return;
-    u16* C = D + (size_t)Iloc * 128 * ld + J * 128;
-    const u16* Ag = D + (size_t)I * 128 * ld + k0;
-    const u16* Bg = P + J * 128;
-    fwh_stage_regs g;
-    if (SYM)
-        fwh_gload_sym(g, P, I * 128, Bg, ld, tid);
-    else
-        fwh_gload(g, Ag, Bg, ld, tid);
-    uint32_t acc[8][4];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        const uint4 v = *reinterpret_cast<const uint4*>(C + (size_t)(ty * 8 + r) * ld + tx * 8);
-        acc[r][0] = v.x;
-        acc[r][1] = v.y;
-        acc[r][2] = v.z;
-        acc[r][3] = v.w;
-    }
-    /* unchanged-row test without a 32-VGPR copy of C or a second HBM read of it: values only
-     * decrease, so a row changed iff the sum of its eight u16 values decreased (v_dot2_u32_u16) */
-    uint32_t sum0[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) sum0[r] = rowsum16(acc[r]);
-    if (SYM)
-        fwh_swrite_sym(g, sA, sB, tid);
-    else
-        fwh_swrite(g, sA, sB, tid);
-    __syncthreads();
-    if (SYM) /* in flight during stage 0 */
-        fwh_gload_sym(g, P + (size_t)UKC * ld, I * 128, Bg + (size_t)UKC * ld, ld, tid);
-    else
-        fwh_gload(g, Ag + UKC, Bg + (size_t)UKC * ld, ld, tid);
-    fwh_stage(acc, sA, sB, tx, ty);
-    __syncthreads();
-    if (SYM)
-        fwh_swrite_sym(g, sA, sB, tid);
-    else
-        fwh_swrite(g, sA, sB, tid);
-    __syncthreads();
-    fwh_stage(acc, sA, sB, tx, ty);
-    /* store only the rows that changed */
-#pragma unroll
-    for (int r = 0; r < 8; ++r)
-        if (rowsum16(acc[r]) != sum0[r])
-            *reinterpret_cast<uint4*>(C + (size_t)(ty * 8 + r) * ld + tx * 8) =
-                make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+
+/* LDS operand reads of the update tile (A: 4 x u16 pairs, B: 2 x 8 u16) */
+static __device__ __forceinline__ void fwh_readB(uint4 (&b)[2], const u16* __restrict__ pb, int m) {
+    b[0] = *reinterpret_cast<const uint4*>(pb + m * UBS);
+    b[1] = *reinterpret_cast<const uint4*>(pb + (m + 1) * UBS);
+}
+static __device__ __forceinline__ void fwh_readA(uint2 (&a)[4], const uint32_t* __restrict__ pa, int m) {
+    const uint4 q0 = *reinterpret_cast<const uint4*>(pa + (m >> 1) * 256);
+    const uint4 q1 = *reinterpret_cast<const uint4*>(pa + (m >> 1) * 256 + 4);
+    a[0] = make_uint2(q0.x, q0.y);
+    a[1] = make_uint2(q0.z, q0.w);
+    a[2] = make_uint2(q1.x, q1.y);
+    a[3] = make_uint2(q1.z, q1.w);
 }
 
 /* ---- the same update at 8 waves per SIMD --------------------------------------------------- *
@@ -1331,18 +1169,8 @@ __global__ __launch_bounds__(256) void sym_fill_local_kernel(u16* __restrict__ D
 }
 
 #ifndef SRT_FW16_DEVICE_ONLY
-/* 8-wave update kernel (fwq_update_kernel) unless SRT_FW_WAVES=4 selects the 4-wave one */
-static bool fw_waves8(void) {
-    const char* e = getenv("SRT_FW_WAVES");
-    return !(e && atoi(e) == 4);
-}
-#define FW_UPDATE(SYMV, XMV, GRID, STREAM, ...)                                                   \
-    do {                                                                                          \
-        if (fw_waves8())                                                                          \
-            fwq_update_kernel<SYMV, XMV><<<(GRID), 512, 0, (STREAM)>>>(__VA_ARGS__);              \
-        else                                                                                      \
-            fwh_update_kernel<SYMV, XMV><<<(GRID), 256, 0, (STREAM)>>>(__VA_ARGS__);              \
-    } while (0)
+#define FW_UPDATE(SYMV, XMV, GRID, STREAM, ...) \
+    fwq_update_kernel<SYMV, XMV><<<(GRID), 512, 0, (STREAM)>>>(__VA_ARGS__)
 /* ---- orchestration --------------------------------------------------------------------------- *
  * Lookahead schedule (one row shard per rank; a single GPU is the 1-rank case). Round k uses the
  * 64-row pivot panel P_k (owner: in place in its rows; others: a double-buffered receive panel).
@@ -2292,7 +2120,7 @@ int srt_fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0, in
      * needs ld % 256 == 0) */
     const char* kb_env = getenv("SRT_FW_SH_KB");
     const int want = kb_env ? atoi(kb_env) : 128;
-    const int rp = want == 64 || !fw_waves8() ? 64 : want == 256 && ld % 256 == 0 ? 256 : 128;
+    const int rp = want == 64 ? 64 : 128;
     g_sharded_rp = rp;
     return fw16_build_sym_sharded(comm, n, ld, row0, nrows, w_rows, lat_rows, st, evp, exact, rp);
 }
@@ -2306,8 +2134,8 @@ static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStrea
  * finish pass's outputs and flags). *nlev = the level that settled every pair, or 0 when the levels do not
  * apply or miss their budget -- the caller then runs the FW. */
 int srt_fw16_levels(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
-                    const uint32_t* w_rows, uint32_t* lat_rows, hipStream_t st, evpool_t* evp,
-                    double fw_ms, int* nlev, int64_t* bytes) {
+                    const uint32_t* w_rows, const double* r_rows, uint32_t* lat_rows,
+                    hipStream_t st, evpool_t* evp, double fw_ms, int* nlev, int64_t* bytes) {
     *nlev = 0;
     *bytes = 0;
     const int dev = srt_state_slot();
@@ -2320,8 +2148,8 @@ int srt_fw16_levels(const srt_comm* comm, int n, int ld, int row0, int nrows, in
         fw16_caps[dev] = need;
     }
     if (!fw16_flags[dev]) SRT_HIPCHK(hipMalloc(&fw16_flags[dev], 2 * sizeof(int)));
-    int rc = srt_levels_build(comm, n, ld, row0, nrows, directed, w_rows, fw16_bufs[dev], lat_rows,
-                              CAP_F, fw_ms, st, evp, nlev, bytes);
+    int rc = srt_levels_build(comm, n, ld, row0, nrows, directed, w_rows, r_rows, fw16_bufs[dev],
+                              lat_rows, CAP_F, fw_ms, st, evp, nlev, bytes);
     if (rc || !*nlev) return rc;
     fw16_small[dev] = 1; /* every settled distance is <= the level budget (<= 254 quanta) */
     return SRT_OK;
@@ -2373,7 +2201,7 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
          * 380.1 ms) */
         const char* kb_env = getenv("SRT_FW_KB");
         const int kbw = kb_env ? atoi(kb_env) : 256;
-        const bool big = two && fw_waves8();
+        const bool big = two;
         const int rp = big && kbw >= 256 && ld % 256 == 0 ? 256 : big && kbw >= 128 && ld >= 256 ? 128 : 64;
         *sym = rp == 256 ? 4 : rp == 128 ? 3 : two ? 2 : 1;
         return fw16_build_sym(n, ld, w_rows, lat_rows, st, evp, exact, two, rp);
@@ -2387,10 +2215,8 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
     auto update = [&](unsigned grid, const u16* P, int k0, int ncol, int i0, int skip) {
         if (!fm)
             fw16_update_kernel<false><<<grid, 256, 0, st>>>(d, ld, P, k0, ncol, i0, skip, nullptr, 0);
-        else if (fw_waves8())
-            fwq_update_kernel<false><<<grid, 512, 0, st>>>(d, ld, P, k0, ncol, i0, skip, nullptr, 0);
         else
-            fwh_update_kernel<false><<<grid, 256, 0, st>>>(d, ld, P, k0, ncol, i0, skip, nullptr, 0);
+            fwq_update_kernel<false><<<grid, 512, 0, st>>>(d, ld, P, k0, ncol, i0, skip, nullptr, 0);
     };
     if (nrows > 0) {
         fw16_init_kernel<<<dim3(srt_ceil_div(ld, 2048), nrows), 256, 0, st>>>(n, ld, row0, w_rows, d,

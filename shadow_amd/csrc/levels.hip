@@ -42,7 +42,9 @@ __global__ __launch_bounds__(256) void lvl_arcs_rows_kernel(int n, int ld, int r
                                                             const uint32_t* __restrict__ w,
                                                             int32_t* __restrict__ cnt, int lmax,
                                                             const int32_t* __restrict__ off,
-                                                            uint32_t* __restrict__ arcs) {
+                                                            uint32_t* __restrict__ arcs,
+                                                            const double* __restrict__ r = nullptr,
+                                                            double* __restrict__ ar = nullptr) {
     __shared__ int h[LVL_STRIDE];
     const int jj = blockIdx.x, j = row0 + jj;
     for (int i = threadIdx.x; i < LVL_STRIDE; i += 256)
@@ -58,9 +60,11 @@ __global__ __launch_bounds__(256) void lvl_arcs_rows_kernel(int n, int ld, int r
             for (int q = 0; q < 4; ++q) {
                 const int k = k4 + q;
                 if (k < n && k != j && x[q] >= 1u && x[q] <= (uint32_t)wmax) {
-                    if (FILL)
-                        arcs[atomicAdd(&h[x[q]], 1)] = (uint32_t)k | (x[q] << 16);
-                    else
+                    if (FILL) {
+                        const int p = atomicAdd(&h[x[q]], 1);
+                        arcs[p] = (uint32_t)k | (x[q] << 16);
+                        ar[p] = r[(size_t)jj * ld + k]; /* undirected: r(k -> j) = r(j -> k) */
+                    } else
                         atomicAdd(&h[x[q]], 1);
                 }
             }
@@ -78,7 +82,9 @@ __global__ __launch_bounds__(256) void lvl_arcs_cols_kernel(int n, int ld,
                                                             const uint32_t* __restrict__ w,
                                                             int32_t* __restrict__ cnt, int lmax,
                                                             const int32_t* __restrict__ off,
-                                                            uint32_t* __restrict__ arcs) {
+                                                            uint32_t* __restrict__ arcs,
+                                                            const double* __restrict__ r = nullptr,
+                                                            double* __restrict__ ar = nullptr) {
     __shared__ int h[64 * LVL_STRIDE];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int j0 = blockIdx.x * 64, j = j0 + lane;
@@ -92,9 +98,11 @@ __global__ __launch_bounds__(256) void lvl_arcs_cols_kernel(int n, int ld,
         for (int k = wv; k < n; k += 4) {
             const uint32_t x = w[(size_t)k * ld + j];
             if (k != j && x >= 1u && x <= (uint32_t)wmax) {
-                if (FILL)
-                    arcs[atomicAdd(&h[lane * LVL_STRIDE + x], 1)] = (uint32_t)k | (x << 16);
-                else
+                if (FILL) {
+                    const int p = atomicAdd(&h[lane * LVL_STRIDE + x], 1);
+                    arcs[p] = (uint32_t)k | (x << 16);
+                    ar[p] = r[(size_t)k * ld + j];
+                } else
                     atomicAdd(&h[lane * LVL_STRIDE + x], 1);
             }
         }
@@ -145,8 +153,8 @@ __global__ void lvl_init_kernel(int n, int src0, int nsrc, int nw, uint32_t* __r
 /* Level d: one wave per (target j, 64-word source chunk c). Units are handed out XCD-major (each
  * XCD takes a contiguous run of chunk-major units), so an XCD works on one source chunk at a time
  * and the Delta rows of that chunk are the only gathered data in its L2. */
-__global__ __launch_bounds__(256) void lvl_step_kernel(int d, int n, int nw, int nchunk, int src0,
-                                                       int nsrc, unsigned nblk,
+static __device__ __forceinline__ void lvl_step_unit(unsigned g, int d, int n, int nw, int nchunk,
+                                                     int src0, int nsrc,
                                                        const int32_t* __restrict__ off,
                                                        const uint32_t* __restrict__ arcs,
                                                        const uint32_t* __restrict__ aoff,
@@ -154,8 +162,6 @@ __global__ __launch_bounds__(256) void lvl_step_kernel(int d, int n, int nw, int
                                                        uint32_t* __restrict__ R,
                                                        uint8_t* __restrict__ done,
                                                        int* __restrict__ incomplete) {
-    const unsigned b = blockIdx.x;
-    const unsigned g = (b & 7u) * (nblk >> 3) + (b >> 3); /* nblk % 8 == 0 */
     const int tgrp = (n + 3) >> 2;
     const int c = (int)(g / (unsigned)tgrp);
     /* the wave index through readfirstlane: j is then wave-uniform to the compiler, so the offsets
@@ -226,6 +232,24 @@ __global__ __launch_bounds__(256) void lvl_step_kernel(int d, int n, int nw, int
     }
 }
 
+/* Persistent grid (a few workgroups per CU, each looping over unit blocks): the units live only a
+ * few microseconds, so a one-shot grid of 131k workgroups was bound by workgroup dispatch. Block p
+ * of XCD p % 8 takes that XCD's contiguous run of unit blocks (chunk-major), one every P / 8. */
+__global__ __launch_bounds__(256) void lvl_step_kernel(int d, int n, int nw, int nchunk, int src0,
+                                                       int nsrc, unsigned nblk,
+                                                       const int32_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ arcs,
+                                                       const uint32_t* __restrict__ aoff,
+                                                       uint32_t* __restrict__ lev,
+                                                       uint32_t* __restrict__ R,
+                                                       uint8_t* __restrict__ done,
+                                                       int* __restrict__ incomplete) {
+    const unsigned x = blockIdx.x & 7u, per = nblk >> 3, L = gridDim.x >> 3;
+    for (unsigned u = blockIdx.x >> 3; u < per; u += L)
+        lvl_step_unit(x * per + u, d, n, nw, nchunk, src0, nsrc, off, arcs, aoff, lev, R, done,
+                      incomplete);
+}
+
 /* Distance rows of the local sources from the levels, in the FW matrix layout (u16, row stride
  * ld: 0 on the diagonal, cap on padding) and as the u32 table rows (SRT_INF on padding) -- the FW
  * finish pass folded in: every settled distance is <= the level budget (<= 254), so the rows are
@@ -278,6 +302,164 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(int n, int ld, int nw, int
     }
 }
 
+/* per-target segment starts of the (target, weight) offsets, for the segmented sort */
+__global__ void lvl_segs_kernel(int ld, const int32_t* __restrict__ off, int32_t* __restrict__ seg) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j <= ld) seg[j] = off[(size_t)j * LVL_STRIDE];
+}
+
+/* Canonical predecessors from the levels (the rule of every build kernel: among the tight in-arcs
+ * u -> t, D[s][u] + w = D[s][t], the smallest (D[s][u], u) -- so the largest w, then the smallest u;
+ * Dijkstra with a (dist, vertex) heap, topology.c:1679-1701 up to igraph's tie order).
+ * One wave per (target t, 64-word source chunk), the same units as lvl_step_kernel. For the
+ * sources at level d (Delta_d[t]) the arcs are taken by weight w = d, d - 1, ..., 1 and, inside a
+ * weight, by ascending u (the in-arcs are sorted so): the arc (u, w) is tight for exactly the
+ * sources in Delta_{d-w}[u] (u itself when w = d), and a source takes its first tight arc. A source
+ * hit by two arcs of its winning weight is a tied pair (srt_build_stats.tied_pairs). A level stops
+ * as soon as every source of the wave has its arc. Outputs, target-major as pred_cols*_kernel's
+ * (stride ldp): predT[t][sl] = u (-1 on the diagonal), rT[t][sl] = r(u, t). */
+static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx)[64 * 40], int n,
+                                                     int nw, int nchunk, int src0, int nsrc, int nlev,
+                                                       const int32_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ arcs,
+                                                       const uint32_t* __restrict__ aoff,
+                                                       const double* __restrict__ ar,
+                                                       const uint32_t* __restrict__ lev,
+                                                       int32_t* __restrict__ predT,
+                                                       double* __restrict__ rT, size_t ldp,
+                                                       unsigned long long* __restrict__ ties) {
+    const int tgrp = (n + 3) >> 2;
+    const int c = (int)(g / (unsigned)tgrp);
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int t = (int)(g % (unsigned)tgrp) * 4 + wv;
+    if (c >= nchunk || t >= n) return;
+    const int lane = threadIdx.x & 63, word = c * 64 + lane;
+    const bool valid = word < nw;
+    const size_t plane = (size_t)n * nw;
+    uint16_t* my = &sidx[wv][lane * 40];
+#pragma unroll
+    for (int q = 0; q < 32; q += 8)
+        *reinterpret_cast<uint4*>(my + q) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    const int32_t* ot = off + (size_t)t * LVL_STRIDE;
+    const int a_t = ot[0];
+    const uint32_t lane4 = (uint32_t)(valid ? word : 0) * 4u;
+    unsigned tied = 0;
+    /* one arc's candidates: x = its tight sources among the pending ones */
+    auto take = [&](uint32_t x, uint32_t& H, uint32_t& T, int i) {
+        uint32_t nb = x & ~H;
+        T |= x & H;
+        H |= x;
+        while (nb) {
+            my[__builtin_ctz(nb)] = (uint16_t)(i - a_t);
+            nb &= nb - 1u;
+        }
+    };
+    for (int d = 1; d <= nlev; ++d) {
+        uint32_t pend = valid ? lev[(size_t)(d - 1) * plane + (size_t)t * nw + word] : 0u;
+        if (!__any(pend != 0u)) continue;
+        for (int w = d; w >= 1; --w) {
+            const int g0 = ot[w], g1 = ot[w + 1];
+            if (g0 == g1) continue;
+            uint32_t H = 0, T = 0;
+            if (w == d) { /* the direct arc: tight for the source u itself */
+                for (int i = g0; i < g1; ++i) {
+                    const int us = (int)(arcs[i] & 0xFFFFu) - src0;
+                    if ((unsigned)us < (unsigned)nsrc && (us >> 5) == word)
+                        take(pend & (1u << (us & 31)), H, T, i);
+                }
+            } else { /* eight gathers in flight, then their candidates in arc order */
+                const char* base = reinterpret_cast<const char*>(lev + (size_t)(d - w - 1) * plane);
+                int i = g0;
+                for (; i + 8 <= g1; i += 8) {
+                    uint32_t a[8], v[8];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) a[q] = aoff[i + q];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q)
+                        v[q] = *reinterpret_cast<const uint32_t*>(base + (a[q] + lane4));
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) take(v[q] & pend, H, T, i + q);
+                }
+                for (; i < g1; ++i)
+                    take(*reinterpret_cast<const uint32_t*>(base + (aoff[i] + lane4)) & pend, H, T, i);
+            }
+            tied += __builtin_popcount(T);
+            pend &= ~H;
+            if (!__any(pend != 0u)) break;
+        }
+    }
+    if (ties) {
+        for (int m = 32; m > 0; m >>= 1) tied += __shfl_xor(tied, m);
+        if (lane == 0 && tied) atomicAdd(&ties[blockIdx.x & 1023u], (unsigned long long)tied);
+    }
+    if (!valid) return;
+    /* 32 entries per lane: the indices back from LDS, every arc and reliability gather issued
+     * before the first is used, then 128 B of predecessors and 256 B of reliabilities */
+    uint32_t ix[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint4 v = *reinterpret_cast<const uint4*>(my + 8 * q);
+        ix[4 * q] = v.x;
+        ix[4 * q + 1] = v.y;
+        ix[4 * q + 2] = v.z;
+        ix[4 * q + 3] = v.w;
+    }
+    const int sl0 = word * 32;
+    int32_t pv[32];
+    double rv[32];
+#pragma unroll
+    for (int e = 0; e < 32; ++e) {
+        const uint32_t x = (ix[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+        const int sl = sl0 + e, sg = src0 + sl;
+        const bool h = sl < nsrc && sg < n && sg != t && x != 0xFFFFu;
+        const int k = a_t + (h ? (int)x : 0);
+        pv[e] = h ? (int)(arcs[k] & 0xFFFFu) : -1;
+        rv[e] = h ? ar[k] : 0.0;
+    }
+    int32_t* pp = predT + (size_t)t * ldp + sl0;
+    double* rp = rT + (size_t)t * ldp + sl0;
+#pragma unroll
+    for (int q = 0; q < 32; q += 4) {
+        *reinterpret_cast<int4*>(pp + q) = make_int4(pv[q], pv[q + 1], pv[q + 2], pv[q + 3]);
+        *reinterpret_cast<double2*>(rp + q) = make_double2(rv[q], rv[q + 1]);
+        *reinterpret_cast<double2*>(rp + q + 2) = make_double2(rv[q + 2], rv[q + 3]);
+    }
+}
+
+__global__ __launch_bounds__(256) void lvl_pred_kernel(int n, int nw, int nchunk, int src0, int nsrc,
+                                                       int nlev, unsigned nblk,
+                                                       const int32_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ arcs,
+                                                       const uint32_t* __restrict__ aoff,
+                                                       const double* __restrict__ ar,
+                                                       const uint32_t* __restrict__ lev,
+                                                       int32_t* __restrict__ predT,
+                                                       double* __restrict__ rT, size_t ldp,
+                                                       unsigned long long* __restrict__ ties) {
+    /* per wave and lane: the winning arc of each of its 32 sources (index into t's arcs), 40 u16
+     * per lane so the read-back is four 16-B loads */
+    __shared__ __attribute__((aligned(16))) uint16_t sidx[4][64 * 40];
+    const unsigned x = blockIdx.x & 7u, per = nblk >> 3, L = gridDim.x >> 3;
+    for (unsigned u = blockIdx.x >> 3; u < per; u += L)
+        lvl_pred_unit(x * per + u, sidx, n, nw, nchunk, src0, nsrc, nlev, off, arcs, aoff, ar, lev,
+                      predT, rT, ldp, ties);
+}
+
+__global__ void lvl_sum_kernel(const unsigned long long* __restrict__ v, int k,
+                               unsigned long long* __restrict__ out) {
+    unsigned long long s = 0;
+    for (int i = threadIdx.x; i < k; i += blockDim.x) s += v[i];
+    for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m);
+    __shared__ unsigned long long w[16];
+    if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long x = 0;
+        for (int i = 0; i < (int)(blockDim.x >> 6); i++) x += w[i];
+        *out += x;
+    }
+}
+
 /* ---- host ----------------------------------------------------------------------------------- */
 /* Streaming-gather rate assumed by the level budget (bytes per ms) and the cost of one level's
  * launch + completion read-back. */
@@ -295,40 +477,87 @@ static double lvl_estimate(const unsigned long long* hist, int L, double ntgt, d
     return t;
 }
 
+/* persistent grid of a 256-thread unit kernel: its resident workgroups per CU x the CUs, a multiple
+ * of 8 (one share per XCD), at most the unit blocks */
+static unsigned lvl_grid(const void* fn, unsigned nblk) {
+    int dev = 0, cus = 256, per = 4;
+    if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 256, 0) != hipSuccess || per < 1) per = 4;
+    (void)hipGetLastError();
+    unsigned g = (unsigned)(cus * per) & ~7u;
+    if (g < 8) g = 8;
+    return g < nblk ? g : nblk;
+}
+
+/* The state a successful level build keeps for its post pass (srt_levels_pred), per state slot:
+ * the sorted in-arcs with their reliabilities and the level planes. Freed by srt_levels_release
+ * (stream-ordered). */
+typedef struct {
+    int held;
+    int n, nw, nchunk, row0, nrows, D;
+    unsigned nblk;
+    int32_t* off;
+    uint32_t* arcs;
+    uint32_t* aoff;
+    double* ar;
+    uint32_t* lev;
+    void* p[16];
+    int k;
+    hipStream_t st;
+} lvl_state;
+static lvl_state g_lvl[SRT_STATE_SLOTS];
+
+static void lvl_free(lvl_state* L, hipStream_t st) {
+    for (int i = 0; i < L->k; i++)
+        if (L->p[i]) (void)hipFreeAsync(L->p[i], st);
+    memset(L, 0, sizeof(*L));
+}
+
+void srt_levels_release(hipStream_t st) { lvl_free(&g_lvl[srt_state_slot()], st); }
+
+#define LVL_ALLOC(ptr, bytes)                                      \
+    do {                                                           \
+        SRT_HIPCHK(srt_malloc_async(&(ptr), (bytes), st));         \
+        L->p[L->k++] = (void*)(ptr);                               \
+    } while (0)
+
 /* One build of the local rows' u16 distances into d16 (nrows x ld). comm (NULL on one GPU):
  * undirected row shards, every rank sees every target's in-arcs after the segment broadcasts.
  * fw_ms: the predicted Floyd-Warshall time; the level budget keeps the predicted level time under
  * half of it. *levels = the level that settled every pair (0: not applicable / over budget -- the
  * caller runs Floyd-Warshall; every rank of a sharded build returns the same verdict).
  * *gather_bytes: the Delta words gathered (the kernel's algorithmic bytes). On success d16 and
- * lat_rows hold the rows (the FW finish pass's outputs). */
+ * lat_rows hold the rows (the FW finish pass's outputs) and the slot keeps the arcs and planes
+ * for srt_levels_pred until srt_levels_release. */
 int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
-                     const uint32_t* w_rows, uint16_t* d16, uint32_t* lat_rows, uint32_t cap,
-                     double fw_ms, hipStream_t st, evpool_t* evp, int* levels,
-                     int64_t* gather_bytes) {
+                     const uint32_t* w_rows, const double* r_rows, uint16_t* d16,
+                     uint32_t* lat_rows, uint32_t cap, double fw_ms, hipStream_t st, evpool_t* evp,
+                     int* levels, int64_t* gather_bytes) {
     *levels = 0;
     *gather_bytes = 0;
+    lvl_state* L = &g_lvl[srt_state_slot()];
+    if (L->held) lvl_free(L, st);
     const int R = comm ? srt_comm_size(comm) : 1;
     if (n > 65535 || ld % 128 || nrows % 128 || row0 % 128) return SRT_OK;
     if (R > 1 && directed) return SRT_OK; /* in-arcs of a directed graph span every rank's rows */
+    const int nw = nrows / 32, nchunk = (nw + 63) / 64;
+    if ((size_t)n * nw * 4 > 0xFFFFFFFFull) return SRT_OK; /* 32-bit row offsets */
+    L->st = st;
+    /* on any early return below the allocations go back (lvl_free), unless the build is held */
+    struct guard {
+        lvl_state* L;
+        hipStream_t st;
+        ~guard() {
+            if (!L->held) lvl_free(L, st);
+        }
+    } gd{L, st};
     const size_t ncnt = (size_t)ld * LVL_STRIDE;
     int32_t *cnt = NULL, *off = NULL;
     unsigned long long* dhist = NULL;
-    SRT_HIPCHK(srt_malloc_async(&cnt, (ncnt + 1) * sizeof(int32_t), st));
-    SRT_HIPCHK(srt_malloc_async(&off, (ncnt + 1) * sizeof(int32_t), st));
-    SRT_HIPCHK(srt_malloc_async(&dhist, LVL_STRIDE * sizeof(unsigned long long), st));
-    struct frees {
-        hipStream_t s;
-        void* p[12] = {};
-        int k = 0;
-        ~frees() {
-            for (int i = 0; i < k; i++) (void)hipFreeAsync(p[i], s);
-        }
-    } fr;
-    fr.s = st;
-    fr.p[fr.k++] = cnt;
-    fr.p[fr.k++] = off;
-    fr.p[fr.k++] = dhist;
+    LVL_ALLOC(cnt, (ncnt + 1) * sizeof(int32_t));
+    LVL_ALLOC(off, (ncnt + 1) * sizeof(int32_t));
+    LVL_ALLOC(dhist, LVL_STRIDE * sizeof(unsigned long long));
     SRT_HIPCHK(hipMemsetAsync(cnt, 0, (ncnt + 1) * sizeof(int32_t), st));
     SRT_HIPCHK(hipMemsetAsync(dhist, 0, LVL_STRIDE * sizeof(unsigned long long), st));
     if (directed)
@@ -346,9 +575,9 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     /* level budget: the largest L whose predicted time stays under half the FW time */
     const double nw_all = (double)nrows / 32.0;
     int lmax = 0;
-    for (int L = 1; L <= LVL_WMAX; ++L) {
-        if (lvl_estimate(hist, L, (double)n, nw_all) > 0.5 * fw_ms) break;
-        lmax = L;
+    for (int x = 1; x <= LVL_WMAX; ++x) {
+        if (lvl_estimate(hist, x, (double)n, nw_all) > 0.5 * fw_ms) break;
+        lmax = x;
     }
     int wmin = 0;
     for (int x = 1; x <= LVL_WMAX && !wmin; ++x)
@@ -360,52 +589,64 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     size_t tmp_bytes = 0;
     SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(NULL, tmp_bytes, cnt, off, (int)(ncnt + 1), st));
     void* tmp = NULL;
-    SRT_HIPCHK(srt_malloc_async(&tmp, tmp_bytes, st));
-    fr.p[fr.k++] = tmp;
+    LVL_ALLOC(tmp, tmp_bytes);
     SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, (int)(ncnt + 1), st));
     int32_t total = 0;
     SRT_HIPCHK(hipMemcpyAsync(&total, off + ncnt, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     SRT_HIPCHK(hipStreamSynchronize(st));
-    uint32_t* arcs = NULL;
-    SRT_HIPCHK(srt_malloc_async(&arcs, ((size_t)total + 8) * sizeof(uint32_t), st));
-    fr.p[fr.k++] = arcs;
+    uint32_t *arcs = NULL, *arcs2 = NULL;
+    double *ar = NULL, *ar2 = NULL;
+    LVL_ALLOC(arcs, ((size_t)total + 8) * sizeof(uint32_t));
+    LVL_ALLOC(ar, ((size_t)total + 8) * sizeof(double));
+    LVL_ALLOC(arcs2, ((size_t)total + 8) * sizeof(uint32_t));
+    LVL_ALLOC(ar2, ((size_t)total + 8) * sizeof(double));
     if (directed)
-        lvl_arcs_cols_kernel<true><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, NULL, lmax, off, arcs);
+        lvl_arcs_cols_kernel<true><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, NULL, lmax, off, arcs,
+                                                            r_rows, ar);
     else
-        lvl_arcs_rows_kernel<true><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, NULL, lmax, off, arcs);
+        lvl_arcs_rows_kernel<true><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, NULL, lmax, off, arcs,
+                                                          r_rows, ar);
     SRT_HIPCHK(hipGetLastError());
     if (R > 1) { /* every rank filled its rows' segment: broadcast the segments */
-        int32_t* hoff = (int32_t*)malloc(((size_t)R + 1) * sizeof(int32_t));
-        if (!hoff) return SRT_E_NOMEM;
+        int32_t hoff[65];
+        if (R > 64) return SRT_OK;
         for (int q = 0; q <= R; q++) {
             int32_t b = ld, e = ld;
             if (q < R) srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &b, &e);
-            const size_t at = (size_t)b * LVL_STRIDE;
-            if (hipMemcpyAsync(&hoff[q], off + at, sizeof(int32_t), hipMemcpyDeviceToHost, st) !=
-                hipSuccess) {
-                free(hoff);
-                srt_set_error("levels: offset read-back failed");
-                return SRT_E_DEVICE;
-            }
+            SRT_HIPCHK(hipMemcpyAsync(&hoff[q], off + (size_t)b * LVL_STRIDE, sizeof(int32_t),
+                                      hipMemcpyDeviceToHost, st));
         }
-        if (hipStreamSynchronize(st) != hipSuccess) {
-            free(hoff);
-            return SRT_E_DEVICE;
-        }
+        SRT_HIPCHK(hipStreamSynchronize(st));
         rc = srt_coll_group_begin(comm);
         for (int q = 0; q < R && !rc; q++)
-            if (hoff[q + 1] > hoff[q])
-                rc = srt_coll_bcast(comm, arcs + hoff[q], (size_t)(hoff[q + 1] - hoff[q]) * 4, q, st);
+            if (hoff[q + 1] > hoff[q]) {
+                const size_t c = (size_t)(hoff[q + 1] - hoff[q]);
+                rc = srt_coll_bcast(comm, arcs + hoff[q], c * sizeof(uint32_t), q, st);
+                if (!rc) rc = srt_coll_bcast(comm, ar + hoff[q], c * sizeof(double), q, st);
+            }
         const int rc2 = srt_coll_group_end(comm);
-        free(hoff);
         if (rc || rc2) return rc ? rc : rc2;
     }
+    /* in-arcs of each target sorted by (weight, source vertex): the order the predecessor search
+     * walks them in (the fill's atomics leave the order inside a weight arbitrary) */
+    int32_t* seg = NULL;
+    LVL_ALLOC(seg, ((size_t)ld + 1) * sizeof(int32_t));
+    lvl_segs_kernel<<<srt_ceil_div(ld + 1, 256), 256, 0, st>>>(ld, off, seg);
+    SRT_HIPCHK(hipGetLastError());
+    if (total > 0) {
+        size_t sb = 0;
+        SRT_HIPCHK(hipcub::DeviceSegmentedRadixSort::SortPairs(NULL, sb, arcs, arcs2, ar, ar2, total,
+                                                               ld, seg, seg + 1, 0, 24, st));
+        void* stmp = NULL;
+        LVL_ALLOC(stmp, sb);
+        SRT_HIPCHK(hipcub::DeviceSegmentedRadixSort::SortPairs(stmp, sb, arcs, arcs2, ar, ar2, total,
+                                                               ld, seg, seg + 1, 0, 24, st));
+    }
+    arcs = arcs2;
+    ar = ar2;
     /* level state over the local sources */
-    const int nw = nrows / 32, nchunk = (nw + 63) / 64;
-    if ((size_t)n * nw * 4 > 0xFFFFFFFFull) return SRT_OK; /* 32-bit row offsets */
     uint32_t* aoff = NULL;
-    SRT_HIPCHK(srt_malloc_async(&aoff, ((size_t)total + 8) * sizeof(uint32_t), st));
-    fr.p[fr.k++] = aoff;
+    LVL_ALLOC(aoff, ((size_t)total + 8) * sizeof(uint32_t));
     if (total > 0) {
         lvl_aoff_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, nw, arcs, aoff);
         SRT_HIPCHK(hipGetLastError());
@@ -413,14 +654,10 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     const size_t plane = (size_t)n * nw;
     uint32_t *lev = NULL, *Rb = NULL;
     uint8_t* done = NULL;
-    int* dinc = NULL;
-    SRT_HIPCHK(srt_malloc_async(&lev, (size_t)lmax * plane * sizeof(uint32_t), st));
-    fr.p[fr.k++] = lev;
-    SRT_HIPCHK(srt_malloc_async(&Rb, plane * sizeof(uint32_t), st));
-    fr.p[fr.k++] = Rb;
-    SRT_HIPCHK(srt_malloc_async(&done, (size_t)n * nchunk + 4 * sizeof(int) * (size_t)(LVL_WMAX + 1), st));
-    fr.p[fr.k++] = done;
-    dinc = (int*)(void*)(((uintptr_t)(done + (size_t)n * nchunk) + 15) & ~(uintptr_t)15);
+    LVL_ALLOC(lev, (size_t)lmax * plane * sizeof(uint32_t));
+    LVL_ALLOC(Rb, plane * sizeof(uint32_t));
+    LVL_ALLOC(done, (size_t)n * nchunk + 4 * sizeof(int) * (size_t)(LVL_WMAX + 1));
+    int* dinc = (int*)(void*)(((uintptr_t)(done + (size_t)n * nchunk) + 15) & ~(uintptr_t)15);
     SRT_HIPCHK(hipMemsetAsync(Rb, 0, plane * sizeof(uint32_t), st));
     SRT_HIPCHK(hipMemsetAsync(done, 0, (size_t)n * nchunk, st));
     SRT_HIPCHK(hipMemsetAsync(dinc, 0, sizeof(int) * (size_t)(LVL_WMAX + 1), st));
@@ -428,11 +665,12 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     SRT_HIPCHK(hipGetLastError());
     unsigned nblk = (unsigned)(((n + 3) / 4) * nchunk);
     nblk = (nblk + 7u) & ~7u;
+    const unsigned pgrid = lvl_grid((const void*)lvl_step_kernel, nblk);
     int D = 0;
     int64_t gathered = 0;
     for (int d = 1; d <= lmax; ++d) {
         if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
-        lvl_step_kernel<<<nblk, 256, 0, st>>>(d, n, nw, nchunk, row0, nrows, nblk, off, arcs, aoff,
+        lvl_step_kernel<<<pgrid, 256, 0, st>>>(d, n, nw, nchunk, row0, nrows, nblk, off, arcs, aoff,
                                               lev, Rb, done, dinc + d);
         if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
         SRT_HIPCHK(hipGetLastError());
@@ -461,5 +699,45 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     SRT_HIPCHK(hipGetLastError());
     *levels = D;
     *gather_bytes = gathered;
+    L->held = 1;
+    L->n = n;
+    L->nw = nw;
+    L->nchunk = nchunk;
+    L->row0 = row0;
+    L->nrows = nrows;
+    L->D = D;
+    L->nblk = nblk;
+    L->off = off;
+    L->arcs = arcs;
+    L->aoff = aoff;
+    L->ar = ar;
+    L->lev = lev;
+    return SRT_OK;
+}
+
+/* Canonical predecessors and their arc reliabilities of the held level build, target-major
+ * (predT[t][sl], rT[t][sl], row stride ldp), as pred_cols*_kernel leave them for the transposes
+ * and the reliability passes; ties != NULL adds the tied pairs. */
+int srt_levels_pred(int32_t* predT, double* rT, size_t ldp, unsigned long long* ties,
+                    hipStream_t st) {
+    lvl_state* L = &g_lvl[srt_state_slot()];
+    if (!L->held) {
+        srt_set_error("levels: no held level build for the predecessor pass");
+        return SRT_E_ARG;
+    }
+    unsigned long long* part = NULL;
+    if (ties) {
+        SRT_HIPCHK(srt_malloc_async(&part, 1024 * sizeof(unsigned long long), st));
+        SRT_HIPCHK(hipMemsetAsync(part, 0, 1024 * sizeof(unsigned long long), st));
+    }
+    lvl_pred_kernel<<<lvl_grid((const void*)lvl_pred_kernel, L->nblk), 256, 0, st>>>(L->n, L->nw, L->nchunk, L->row0, L->nrows, L->D,
+                                             L->nblk, L->off, L->arcs, L->aoff, L->ar, L->lev, predT, rT,
+                                             ldp, part);
+    SRT_HIPCHK(hipGetLastError());
+    if (ties) {
+        lvl_sum_kernel<<<1, 1024, 0, st>>>(part, 1024, ties);
+        SRT_HIPCHK(hipGetLastError());
+        SRT_HIPCHK(hipFreeAsync(part, st));
+    }
     return SRT_OK;
 }

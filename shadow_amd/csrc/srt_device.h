@@ -155,13 +155,18 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
                    void* ctx, int rank, int fm, int* sym, int* exact);
 /* levels.hip: u16 distance rows of the local sources by bit-parallel Dial levels (see there) */
 int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
-                     const uint32_t* w_rows, uint16_t* d16, uint32_t* lat_rows, uint32_t cap,
-                     double fw_ms, hipStream_t st, evpool_t* evp, int* levels,
-                     int64_t* gather_bytes);
+                     const uint32_t* w_rows, const double* r_rows, uint16_t* d16,
+                     uint32_t* lat_rows, uint32_t cap, double fw_ms, hipStream_t st, evpool_t* evp,
+                     int* levels, int64_t* gather_bytes);
+/* predecessors + arc reliabilities of the held level build (target-major, row stride ldp) */
+int srt_levels_pred(int32_t* predT, double* rT, size_t ldp, unsigned long long* ties,
+                    hipStream_t st);
+/* frees the held level build (stream-ordered) */
+void srt_levels_release(hipStream_t st);
 /* the same into this slot's FW matrix + the finish pass (fw16.hip); *nlev = 0: FW instead */
 int srt_fw16_levels(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
-                    const uint32_t* w_rows, uint32_t* lat_rows, hipStream_t st, evpool_t* evp,
-                    double fw_ms, int* nlev, int64_t* bytes);
+                    const uint32_t* w_rows, const double* r_rows, uint32_t* lat_rows,
+                    hipStream_t st, evpool_t* evp, double fw_ms, int* nlev, int64_t* bytes);
 /* the u16 working matrix of the last srt_fw16_build on the current device (row shard x ld) */
 const uint16_t* srt_fw16_matrix(void);
 /* 1 when every real distance of that build is <= 254 quanta (the post pass then reads u8) */
@@ -195,7 +200,7 @@ int srt_fw16_rows(int n, int ld, int nsub, const int32_t* dverts, const uint32_t
 
 int srt_dense_post_device(int32_t n, int32_t ld, int32_t directed, const uint32_t* w,
                           const double* r, uint32_t* d, const uint16_t* d16, double* rel,
-                          hipStream_t st, srt_build_stats* stats);
+                          hipStream_t st, srt_build_stats* stats, int lvl);
 
 /* Largest dense n: the predecessor keys pack a 16-bit rank and the essential-arc offsets are
  * int32 (n^2 < 2^31), rounded down to the 128 tile. */

@@ -2,6 +2,7 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Ishadow_amd/csrc tools/fw16_ablate.hip
 #define SRT_FW16_DEVICE_ONLY
 #include "../shadow_amd/csrc/fw16.hip"
+#include "fwh_legacy.h"
 #include <cstdio>
 #include <vector>
 #include <algorithm>

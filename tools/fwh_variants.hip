@@ -5,6 +5,7 @@
 // Run:   tools/fwh_variants [ld]
 #define SRT_FW16_DEVICE_ONLY
 #include "../shadow_amd/csrc/fw16.hip"
+#include "fwh_legacy.h"
 #include <algorithm>
 #include <cstring>
 #include <cstdlib>
