@@ -300,10 +300,8 @@ def run_dense(c: Ctx, wl):
                      1: 4.0}[enc]
     instr_per_relax = {11: 0.75, 9: 0.75, 8: 0.75, 7: 0.75, 6: 0.75, 5: 0.75, 4: 0.75, 3: 0.75,
                        2: 1.0, 1: 1.5}[enc]
-    # the 8-wave update kernel (fwq_update_kernel) unless SRT_FW_WAVES=4 selects the 4-wave one
-    w4 = os.environ.get("SRT_FW_WAVES") == "4"
-    uk = "fwh_update_kernel" if w4 else "fwq_update_kernel"
-    st2 = "" if w4 else ", 2"  # fwq's third template argument: 32-pivot stages per tile
+    # the 8-wave update kernel (fwq_update_kernel; third template argument: 32-pivot stages/tile)
+    uk, st2 = "fwq_update_kernel", ", 2"
     kname = {11: "fwq_update_kernel<false, 20, 8>", 9: "fwq_update_kernel<true, 4, 8>", 8: "fwq_update_kernel<true, 4, 4>", 7: "fwq_update_kernel<true, 4, 8>", 6: "fwq_update_kernel<true, 4, 4>", 5: f"{uk}<true, 4{st2}>",
              4: f"{uk}<true, 0{st2}>" if world == 1 else f"{uk}<true, 4{st2}>",
              3: f"{uk}<false, 0{st2}>",
@@ -311,7 +309,7 @@ def run_dense(c: Ctx, wl):
     # LDS bytes per relaxation: operand reads (fwq: 4 ds_read_b128 per 64 relaxations per lane =
     # 1 B; fwh: 6 per 128 = 0.75 B) + the staged A/B slices (sA 16 KB + sB 8 KB per 32 pivots per
     # 128x128 tile = 0.047 B)
-    lds_b_per_relax = (0.75 if w4 else 1.0) + 24576.0 / (32 * 128 * 128)
+    lds_b_per_relax = 1.0 + 24576.0 / (32 * 128 * 128)
     # elements a timed launch updates: every local row; (enc 4, one GPU) the upper-triangle 128x128
     # tiles; (enc 4, sharded) this rank's kept tiles (fw16.hip sym_kept: one orientation of each
     # tile pair) less the next pivot block's tile row and column, which run in their own launch

@@ -119,9 +119,6 @@ struct srt_sparse_graph {
     uint8_t* ridx;
     uint2 *cw2, *icw2;
     double *r2, *ir2;
-    /* the relabelled in-arcs packed col | w << 24 for the multi-source kernel (max_w < 256,
-     * n < 2^24; 8 words of padding), else NULL */
-    uint32_t* ca2;
     /* host copy of the relabelled out-rows, for the multi-source kernel's source clusters */
     int2* h_rp2;
     uint2* h_cw2;
@@ -174,7 +171,7 @@ extern "C" void srt_sparse_graph_free(srt_sparse_graph* g) {
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(g->device);
     void* ps[] = {g->rp, g->col, g->w, g->r, g->sw, g->sr, g->cw, g->perm, g->inv, g->rp2, g->cw2, g->r2,
-                  g->rpo, g->rtab, g->ridx, g->ca2};
+                  g->rpo, g->rtab, g->ridx};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (g->directed) {
@@ -372,17 +369,6 @@ static int sparse_graph_from_canon(const srt_canon* c, int device, srt_sparse_gr
         if (!rc) rc = up((void**)&g->icw2, hcw, na * sizeof(uint2));
         if (!rc) rc = up((void**)&g->ir2, hr, na * 8);
     }
-    /* packed in-arcs (hcw holds the relabelled in-arcs now: the out-arcs when undirected) */
-    if (!rc && g->max_w < 256 && c->n < (1 << 24)) {
-        uint32_t* pk = (uint32_t*)calloc(na + 8, sizeof(uint32_t));
-        if (!pk) {
-            rc = SRT_E_NOMEM;
-        } else {
-            for (size_t k = 0; k < na; k++) pk[k] = hcw[k].x | (hcw[k].y << 24);
-            rc = up((void**)&g->ca2, pk, (na + 8) * sizeof(uint32_t));
-            free(pk);
-        }
-    }
     if (!rc && !c->directed) {
         g->irp2 = g->rp2;
         g->icw2 = g->cw2;
@@ -431,9 +417,9 @@ int srt_msssp_max_n(void);
 int srt_ms_scatter_rows(int nr, int n, const int32_t* rows, const uint32_t* tl, const double* tr,
                         uint32_t* lat, double* rel, size_t ldo, hipStream_t st);
 int srt_msssp_rows(int n, int directed, const int2* orp, const uint2* ocw, const int2* irp,
-                   const uint2* icw, const uint32_t* ica, const double* ir, const int32_t* inv,
-                   uint32_t delta, int nbatch, const int32_t* bsrc, const int32_t* brow,
-                   uint32_t* lat, double* rel, size_t ldo, int d16, hipStream_t st);
+                   const uint2* icw, const double* ir, const int32_t* inv, uint32_t delta,
+                   int nbatch, const int32_t* bsrc, const int32_t* brow, uint32_t* lat,
+                   double* rel, size_t ldo, int d16, hipStream_t st);
 
 /* Sweep order for the source clusters: breadth-first from a pseudo-peripheral vertex of each
  * component (the far end of a breadth-first search from the component's first vertex), so clusters
@@ -594,16 +580,17 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
     /* source i of this call: srcs + i, or the range */
     auto one = [&](int i) { return srcs ? srcs + i : (const int32_t*)NULL; };
     const int b0 = srcs ? 0 : src_begin;
-    const char* kenv = getenv("SRT_SPARSE_KERNEL");
-    const char* wenv = getenv("SRT_SPARSE_WORKSET");
-    const bool block = (kenv && !strcmp(kenv, "block")) || (wenv && !strcmp(wenv, "hbm"));
+    /* SRT_FORM kernel=block|ms|wg|wave forces one sparse kernel for every source (tests) */
+    const bool block = srt_form_is("kernel", "block") || srt_form_int("hbm", 0) != 0;
     int rc = SRT_OK;
     /* the multi-source kernel (msssp.hip) where the relabelled graph is local (RGG-like, where
      * the 64 frontiers of a source cluster overlap); SRT_SPARSE_MS=0/1 disables / forces it.
      * Sources are clustered here, on the host, before the timed span */
-    const char* menv = getenv("SRT_SPARSE_MS");
+    const bool k_ms = srt_form_is("kernel", "ms"), k_wg = srt_form_is("kernel", "wg"),
+               k_wave = srt_form_is("kernel", "wave");
+    /* SRT_FORM ms=0 / wg=0 take the multi-source / workgroup kernel out of the automatic choice */
     bool ms = allow_ms && !block && g->n <= srt_msssp_max_n() && g->h_rp2 &&
-              (menv ? atoi(menv) != 0 : g->local != 0);
+              (k_ms || (!k_wg && !k_wave && srt_form_int("ms", 1) != 0 && g->local != 0));
     std::vector<int32_t> ms_bsrc, ms_brow, ms_rest, hs;
     if (ms) {
         std::vector<int32_t> rowof((size_t)g->n, -1);
@@ -615,14 +602,12 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
             else rowof[g->h_inv[s]] = i;
         }
         /* SRT_MSSSP_RMAX: the hop radius of a cluster (tests force it to 0 / large) */
-        const char* renv = getenv("SRT_MSSSP_RMAX");
-        const int rmax = renv ? atoi(renv) : 24;
+        const int rmax = srt_form_int("ms_rmax", 24);
         int cus = 256, dev = 0;
         hipDeviceProp_t prop;
         if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
             cus = prop.multiProcessorCount;
-        const char* benv = getenv("SRT_MSSSP_MAXB"); /* tests: the batch budget */
-        const int maxb = benv ? atoi(benv) : 2 * cus;
+        const int maxb = srt_form_int("ms_maxb", 2 * cus); /* tests: the batch budget */
         srt_sparse_graph* gm = const_cast<srt_sparse_graph*>(g); /* the cluster cache */
         pthread_mutex_lock(&gm->ck_mu);
         const bool hit = ms && gm->ck_bsrc && gm->ck_n == nsrc && gm->ck_rmax == rmax &&
@@ -718,18 +703,13 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
         SRT_HIPCHK(hipMemcpyAsync(ms_dev + ms_bsrc.size(), ms_brow.data(), bb,
                                   hipMemcpyHostToDevice, st));
         /* bucket width: 8 mean arc weights (C3: 64 quanta; same-box sweep in DESIGN §5.4) */
-        const char* denv = getenv("SRT_MSSSP_DELTA");
-        const uint32_t delta = denv && atoi(denv) > 0 ? (uint32_t)atoi(denv) : 8u * g->delta;
+        const int fd = srt_form_int("ms_delta", 0);
+        const uint32_t delta = fd > 0 ? (uint32_t)fd : 8u * g->delta;
         /* 16-bit working distances when every finite distance provably fits (half the bytes of
-         * every row access); SRT_MSSSP_U16=0 keeps 32 */
-        const char* uenv = getenv("SRT_MSSSP_U16");
-        const int d16 = g->dist_bound < 0xFFFFull && !(uenv && atoi(uenv) == 0);
+         * every row access; SRT_FORM ms_u16=0 keeps 32 for the tests) */
+        const int d16 = g->dist_bound < 0xFFFFull && srt_form_int("ms_u16", 1) != 0;
         ms_d16 = d16;
-        /* SRT_MSSSP_A32=1: arcs packed in one word (one lane read per arc instead of two, but
-         * a scalar split on the address chain: C3 26.4 vs 25.2 ms for the pairs, same box) */
-        const char* aenv = getenv("SRT_MSSSP_A32");
-        const uint32_t* ca = aenv && atoi(aenv) != 0 ? g->ca2 : NULL;
-        rc = srt_msssp_rows(g->n, g->directed, g->rp2, g->cw2, g->irp2, g->icw2, ca, g->ir2,
+        rc = srt_msssp_rows(g->n, g->directed, g->rp2, g->cw2, g->irp2, g->icw2, g->ir2,
                             g->inv, delta, nb, ms_dev, ms_dev + ms_bsrc.size(), lat_rows, rel_rows,
                             (size_t)g->n, d16, st);
         if (rc) return rc;
@@ -759,14 +739,12 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
             if (rc) return rc;
         }
     }
-    const char* genv = getenv("SRT_SPARSE_WG");
     bool wg = !ms && !g->directed && g->n <= srt_wgsssp_max_n() &&
-              (genv ? atoi(genv) != 0 : (g->n > 32768 && !g->local));
+              (k_wg || (!k_wave && srt_form_int("wg", 1) != 0 && g->n > 32768 && !g->local));
     /* the workgroup kernel keeps its row in LDS (any order serves), so it runs on the original
      * vertex order and writes reliability straight into the output rows; SRT_WG_ORDER=cm runs it
      * on the Cuthill-McKee relabelling with a private row gathered at the end */
-    const char* oenv = getenv("SRT_WG_ORDER");
-    const bool wg_cm = oenv && !strcmp(oenv, "cm");
+    const bool wg_cm = srt_form_is("wg_order", "cm");
     const int2* wrp = wg_cm ? g->rp2 : g->rpo;
     const uint2* wcw = wg_cm ? g->cw2 : g->cw;
     const double* wr = wg_cm ? g->r2 : g->r;
@@ -1021,9 +999,8 @@ static int build_one(const srt_canon* c, const srt_build_opts* opts, int algo, i
         /* a few attached vertices: their rows alone (Bellman-Ford passes, ~6 nsub n^2 work)
          * instead of the all-pairs FW (n^3 / 2), as the reference computes paths from attached
          * sources only (topology.c:1604-1656); SRT_DENSE_ROWS=0 keeps the FW */
-        const char* renv = getenv("SRT_DENSE_ROWS");
         int rows_used = 0;
-        if (use_sp && verts && (size_t)nsub * 12 <= (size_t)n && !(renv && atoi(renv) == 0)) {
+        if (use_sp && verts && (size_t)nsub * 12 <= (size_t)n && srt_form_int("rows", 1) != 0) {
             uint32_t* rl;
             double *rr, *rm = NULL;
             TRY(dalloc(&B, (void**)&rl, (size_t)nsub * ld * sizeof(uint32_t)));

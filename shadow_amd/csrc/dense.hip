@@ -1159,9 +1159,8 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         return dense_post_levels(n, ld, row0, nrows, d, rel, st, stats, ws, lrows);
     SRT_HIPCHK(hipMemsetAsync(ws->cnt, 0, (size_t)(n + 1) * sizeof(int32_t), st));
     /* the exact u16 FW matrix when the build kept one: the same values in half the bytes
-     * (C4: count 1.37 -> 1.08 ms, fill 1.52 -> 1.50 ms; SRT_ESS_U16=0 reads the u32 table) */
-    static const char* eu_env = getenv("SRT_ESS_U16");
-    const bool ess16 = d16 && !(eu_env && atoi(eu_env) == 0);
+     * (C4: count 1.37 -> 1.08 ms, fill 1.52 -> 1.50 ms against the u32 table) */
+    const bool ess16 = d16 != nullptr;
     if (lrows > 0 && ess16)
         ess_count_kernel<uint16_t><<<lrows, 256, 0, st>>>(n, ld, row0, w, d16, ws->cnt);
     else if (lrows > 0)
@@ -1240,10 +1239,8 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         if ((rc = ws_grow((void**)&ws->uw, &c3, (size_t)total + 1, sizeof(uint2)))) return rc;
         ws->uw_cap = c3;
         /* byte distances without the tie count take the one-minimum form (pred_cols3_kernel;
-         * SRT_PRED_KEY=0: pred_cols2_kernel) */
-        static const char* pk_env = getenv("SRT_PRED_KEY");
-        const bool key3 = d16 && srt_fw16_small() && !ties && n <= 32768 &&
-                          !(pk_env && atoi(pk_env) == 0);
+         * C4 post pass 38.1 -> 36.3 ms against pred_cols2_kernel, which the tie count keeps) */
+        const bool key3 = d16 && srt_fw16_small() && !ties && n <= 32768;
         if (total > 0 && key3)
             pack_uk_kernel<<<srt_ceil_div(n, 4), 256, 0, st>>>(n, iptr, icol, iw, !directed, ws->uw);
         else if (total > 0)
@@ -1269,31 +1266,11 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
             transpose_kernel<uint16_t, uint8_t, 128><<<dim3(srt_ceil_div(ld, 64), srt_ceil_div(nrows, 64)),
                                                      256, 0, st>>>(nrows, ld, d16, (size_t)ld, dt8,
                                                                    (size_t)ld * 128);
-            /* 16 candidate arcs in flight per step: 17.3 ms on C4 against 18.7 (8) and 20.0 (32) */
-            /* streaming (non-temporal) output stores: 13.9 against 14.5 ms on C4, post pass
-             * 35.4 against 36.3 ms, same box (SRT_PRED_NT=0 turns them off) */
-            static const char* nt_env = getenv("SRT_PRED_NT");
-            const bool nt = !(nt_env && atoi(nt_env) == 0);
-            static const char* pu_env = getenv("SRT_PRED_U"); /* A/B: arcs in flight per step */
-            const int pu = pu_env ? atoi(pu_env) : 16;
-            if (key3 && nt && pu == 24)
-                pred_cols3_kernel<24, true><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
-                    n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
-                    nsb2, tch, tper, !directed);
-            else if (key3 && nt && pu == 32)
-                pred_cols3_kernel<32, true><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
-                    n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
-                    nsb2, tch, tper, !directed);
-            else if (key3 && nt && pu == 8)
-                pred_cols3_kernel<8, true><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
-                    n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
-                    nsb2, tch, tper, !directed);
-            else if (key3 && nt)
+            /* 16 candidate arcs in flight per step: 17.3 ms on C4 against 18.7 (8) and 20.0 (32);
+             * streaming (non-temporal) output stores: 13.9 against 14.5 ms on C4, post pass 35.4
+             * against 36.3 ms, same box */
+            if (key3)
                 pred_cols3_kernel<16, true><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
-                    n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
-                    nsb2, tch, tper, !directed);
-            else if (key3)
-                pred_cols3_kernel<16, false><<<srt_ceil_div(nsb2, 8) * 8 * tch, 256, 0, st>>>(
                     n, row0, lrows, nrows, (size_t)ld * 128, dt8, iptr, ws->uw, ir, ws->predt, ws->rt,
                     nsb2, tch, tper, !directed);
             else if (ties)
@@ -1331,23 +1308,12 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         /* predecessor rows pred[sl][t] = predT[t][sl] (reuses the DT buffer) and the arc
          * reliabilities straight into the rel rows, where the passes below finish them in place */
         int32_t* pred = reinterpret_cast<int32_t*>(ws->dt);
-        /* SRT_TRANSPOSE_NT=1: streaming stores for the two row transposes (A/B knob) */
-        static const char* tn_env = getenv("SRT_TRANSPOSE_NT");
-        if (tn_env && atoi(tn_env) == 1) {
-            transpose_kernel<uint32_t, uint32_t, 0, true>
-                <<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
-                    n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows,
-                    reinterpret_cast<uint32_t*>(pred), (size_t)ld);
-            transpose_kernel<double, double, 0, true>
-                <<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
-                    n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
-        } else {
-            transpose_kernel<uint32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
-                n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows,
-                reinterpret_cast<uint32_t*>(pred), (size_t)ld);
-            transpose_kernel<double><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
-                n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
-        }
+        /* (streaming stores measured neutral here: these transposes already run at ~5.3 TB/s) */
+        transpose_kernel<uint32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+            n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows,
+            reinterpret_cast<uint32_t*>(pred), (size_t)ld);
+        transpose_kernel<double><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+            n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
         /* level order for rows whose distances span <= 64 quanta, sweeps for the rest
          * (ws->cursor is free here and carries the per-row hand-over flags) */
         /* 1024 threads per row, one row per CU (128 VGPRs): 12.3 ms on C4 against 13.3 for 512
@@ -1816,8 +1782,7 @@ static int dense_try_levels(const srt_comm* comm, int n, int ld, int row0, int n
                             hipStream_t st,
                             evpool_t* evp, srt_build_stats* stats, int* exact) {
     *exact = 0;
-    const char* env = getenv("SRT_DENSE_LEVELS");
-    const int mode = env ? atoi(env) : -1;
+    const int mode = srt_form_int("levels", -1);
     if (mode == 0 || (mode < 0 && n < 4096) || ld % 128) return SRT_OK;
     /* relaxations at the update's rate + ~50 us of round chain per 128 pivots */
     const double fw_ms = (double)nrows * ld * ld / (directed ? 1.0 : 2.0) / 6.1e10 + ld / 128 * 0.05;
@@ -2019,9 +1984,8 @@ int srt_dense_build_sharded_ms(srt_comm* comm, int32_t n, int32_t ld, int32_t di
     shard_ctx ctx = {comm, ld};
     srt_comm_timing(comm, stats && stats->time_kernels);
     int exact = 0, enc = SRT_DENC_U32;
-    const char* sym_env = getenv("SRT_FW_SYM");
     /* symmetric rounds up to 1,024 tile columns (fw16.hip SYM_TMAX, the panel-position table) */
-    const bool sym = !directed && R > 1 && ld <= 1024 * 128 && !(sym_env && atoi(sym_env) == 0);
+    const bool sym = !directed && R > 1 && ld <= 1024 * 128 && srt_form_int("sym", 1) != 0;
     if ((rc = dense_try_levels(comm, n, ld, b, nr, directed, w_rows, r_rows, lat_rows, st, evp, stats,
                                &exact)))
         return rc;

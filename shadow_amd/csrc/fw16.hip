@@ -1354,38 +1354,20 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
                 return SRT_OK;
             };
             const int R = T / 2;
-            /* SRT_FW_NRCS=1: the next round's crosses run on the chain stream after both streams'
-             * rest of the round before (as in the sharded form), not at the head of each update
-             * stream's round */
-            const char* nrenv = getenv("SRT_FW_NRCS");
-            const bool nr_cs = nrenv ? atoi(nrenv) != 0 : false;
             if ((rc = produce4(0))) return rc;
             for (int j = 0; j < R; ++j) {
                 const int ka = 4 * j * KB;
                 u16* Pa = d + (size_t)ka * ld;
                 const bool next = j + 1 < R;
-                if (nr_cs && next) {
-                    /* cs: the crosses of tile rows 2j + 2, 2j + 3 with round j's panels follow
-                     * rest(j - 1) of both streams; round j + 1's panels follow them */
-                    if (j >= 1) {
-                        SRT_HIPCHK(hipStreamWaitEvent(cs, sc->e_set[(j - 1) & 1][0], 0));
-                        SRT_HIPCHK(hipStreamWaitEvent(cs, sc->e_set[(j - 1) & 1][1], 0));
-                    }
-                    for (int p = 0; p < 2; p++)
-                        fwq_update_kernel<true, 13, 8><<<2 * T, 512, 0, cs>>>(d, ld, Pa, ka, T, p,
-                                                                            2 * j + 2, nullptr, 0, -1);
-                    SRT_HIPCHK(hipGetLastError());
-                    if ((rc = produce4(j + 1))) return rc;
-                }
                 for (int p = 0; p < 2; p++) {
                     SRT_HIPCHK(hipStreamWaitEvent(ss[p], sc->ready[j & 1], 0));
-                    if (next && !nr_cs) {
+                    if (next) {
                         fwq_update_kernel<true, 13, 8><<<2 * T, 512, 0, ss[p]>>>(
                             d, ld, Pa, ka, T, p, 2 * j + 2, nullptr, 0, -1);
                         SRT_HIPCHK(hipEventRecord(sc->e_set[j & 1][p], ss[p]));
                     }
                 }
-                if (next && !nr_cs) {
+                if (next) {
                     SRT_HIPCHK(hipStreamWaitEvent(cs, sc->e_set[j & 1][0], 0));
                     SRT_HIPCHK(hipStreamWaitEvent(cs, sc->e_set[j & 1][1], 0));
                     if ((rc = produce4(j + 1))) return rc;
@@ -1404,7 +1386,6 @@ static int fw16_build_sym(int n, int ld, const uint32_t* w, uint32_t* lat, hipSt
                         fwq_update_kernel<true, 5, 8><<<(unsigned)nset[p], 512, 0, ss[p]>>>(
                             d, ld, Pa, ka, T, 0, -1, tls[p], T, 2 * j);
                     if (evp && next) SRT_HIPCHK(hipEventRecord(evp->ev[e0 + 2 + p], ss[p]));
-                    if (nr_cs) SRT_HIPCHK(hipEventRecord(sc->e_set[j & 1][p], ss[p])); /* rest(j) */
                 }
                 SRT_HIPCHK(hipGetLastError());
             }
@@ -1545,7 +1526,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
     const int R = srt_comm_size(comm), me = srt_comm_rank(comm);
     /* kbr = 128: 128-pivot rounds (pivot block = tile row K, panels P_a over P_b, four 32-pivot
      * stages per C-tile residency); kbr = 64: 64-pivot rounds */
-    const bool r128 = kbr == 128, r256 = kbr == 256;
+    const bool r128 = kbr == 128;
     const int T = ld / 128, nb = ld / kbr;
     const int tb = row0 / 128, te = (row0 + nrows) / 128;
     size_t* caps = fw16_caps;
@@ -1603,8 +1584,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
     /* two-deep 128-pivot rounds (N > 1 default; SRT_FW_SH_DEEP=0: one-deep): band k + 3 is staged
      * and broadcast on its own stream right after round k's update, three rounds ahead, and each
      * rank applies the two panels it missed to the staged band itself (fwq_band_kernel) */
-    const char* deep_env = getenv("SRT_FW_SH_DEEP");
-    const bool deep = r128 && R > 1 && T >= 2 && (deep_env ? atoi(deep_env) != 0 : true);
+    const bool deep = r128 && R > 1 && T >= 2 && srt_form_int("deep", 1) != 0;
     const size_t nstage = (size_t)(kbr / KB) * ((size_t)T + 1) * blk * (deep ? 3 : 1);
     bool ok = cnt && hipMalloc(&tl, (nkept + 1) * sizeof(uint32_t)) == hipSuccess &&
               hipMalloc(&down, (size_t)T * sizeof(int)) == hipSuccess &&
@@ -1720,52 +1700,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
             SRT_HIPCHK(hipEventRecord(sc->ready[k & 1], cs));
             return SRT_OK;
         };
-        /* 256-pivot rounds: the band is tile rows K0 = 2j and K1 = 2j + 1 (quarters a, b of K0,
-         * c, d of K1, each staged in its tile row's contributor order: four half-panel
-         * broadcasts per contributor); every rank closes the quarters in order, each one's
-         * closed panel applied to the staged rows of the later quarters first */
-        auto produce256 = [&](int j) -> int {
-            const int k0 = j * 256, K0 = 2 * j;
-            u16* P = pbuf[j & 1];
-            u16* sq[4];
-            for (int q = 0; q < 4; q++) sq[q] = grecv + (size_t)q * ((size_t)T + 1) * blk;
-            int* cq[2] = {cnt, cnt + R};
-            for (int h = 0; h < 2; h++) {
-                const int K = K0 + h, o = own[K];
-                for (int q = 0; q < R; q++) cq[h][q] = 0;
-                for (int J = 0; J < T; J++) cq[h][sym_kept(K, J) ? o : own[J]]++;
-            }
-            for (int q = 0; q < 4; q++)
-                if (cq[q >> 1][me])
-                    sym_contrib_pack_kernel<<<T, 256, 0, cs>>>(d, ld, row0, tb, K0 + (q >> 1),
-                                                               k0 + q * KB, T, down, me, sq[q]);
-            SRT_HIPCHK(hipGetLastError());
-            int r = srt_coll_group_begin(comm);
-            for (int q = 0; q < 4 && !r; q++) {
-                size_t off = 0;
-                for (int x = 0; x < R && !r; x++) {
-                    const int c = cq[q >> 1][x];
-                    if (c) r = srt_coll_bcast(comm, sq[q] + off * blk, (size_t)c * blk * sizeof(u16), x, cs);
-                    off += (size_t)c;
-                }
-            }
-            const int r2 = srt_coll_group_end(comm);
-            if (r || r2) return r ? r : r2;
-            for (int q = 0; q < 4; q++) {
-                const int K = K0 + (q >> 1), kq = k0 + q * KB;
-                u16* Pq = P + (size_t)q * KB * ld;
-                u16* prow = me == own[K] ? d + (size_t)(kq - row0) * ld : nullptr;
-                sym_diag_stage_kernel<<<1, 256, 0, cs>>>(Pq, ld, K, kq, T, down, sq[q], prow);
-                sym_panel_stage_kernel<SYM_RM><<<T, 1024 / SYM_RM, 0, cs>>>(Pq, ld, K, kq, T, down, sq[q], prow);
-                for (int y = q + 1; y < 4; y++) /* P_q into the later quarters' staged rows */
-                    sym_cross_stage_kernel<SYM_RM><<<T, 1024 / SYM_RM, 0, cs>>>(Pq, ld, K0 + (y >> 1), T, down, sq[y], K,
-                                                              (q & 1) * KB);
-            }
-            SRT_HIPCHK(hipGetLastError());
-            SRT_HIPCHK(hipEventRecord(sc->ready[j & 1], cs));
-            return SRT_OK;
-        };
-        auto make = [&](int k) -> int { return r256 ? produce256(k) : r128 ? produce128(k) : produce(k); };
+        auto make = [&](int k) -> int { return r128 ? produce128(k) : produce(k); };
         /* two update streams (st: even J, xs: odd J), as on one GPU (fw16_build_sym): each
          * depends on its own launches and the panel, so their rounds overlap */
         hipStream_t ss[2] = {st, sc->xs};
@@ -1896,31 +1831,12 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
          * back to back instead of NR -> rest with two launch gaps a round: one rank of N = 8
          * 49.2 -> 46.0 ms, N = 4 unchanged (83.5 ms). SRT_FW_SH_NRCS=0 keeps NR on the update
          * streams. */
-        const char* nrenv = getenv("SRT_FW_SH_NRCS");
-        const bool nr_cs = r256 || (nrenv ? atoi(nrenv) != 0 : true); /* 256: only this form */
         for (int k = 0; k < nb; ++k) {
             const int k0 = k * kbr;
             u16* P = panel_of(k);
             const bool next = k + 1 < nb;
             const int K1 = next ? (k + 1) * kbr / 128 : -1;
-            for (int p = 0; p < 2; p++) {
-                SYM_HIP(hipStreamWaitEvent(ss[p], sc->ready[k & 1], 0));
-                if (!next || nr_cs) continue;
-                if (r128) {
-                    if (p == 0)
-                        fwq_update_kernel<true, 7, 4><<<T + (te - tb), 512, 0, ss[p]>>>(
-                            d, ld, P, k0, T, tb, K1, nullptr, te);
-                    else
-                        fwq_update_kernel<true, 8, 4><<<T + (te - tb), 512, 0, ss[p]>>>(
-                            d, ld, P, k0, T, tb, K1, nullptr, te);
-                } else if (p == 0)
-                    FW_UPDATE(true, 7, T + (te - tb), ss[p], d, ld, P, k0, T, tb,
-                                                                                 K1, nullptr, te);
-                else
-                    FW_UPDATE(true, 8, T + (te - tb), ss[p], d, ld, P, k0, T, tb,
-                                                                                 K1, nullptr, te);
-                SYM_HIP(hipEventRecord(sc->e_set[k & 1][p], ss[p]));
-            }
+            for (int p = 0; p < 2; p++) SYM_HIP(hipStreamWaitEvent(ss[p], sc->ready[k & 1], 0));
             /* the unit's period only needs the first round's starts and the last round's ends
              * (evpool_sum, group 4): two records per round fewer on the host's critical path */
             const bool t_first = evp && next && timed == 0, t_last = evp && k + 2 == nb;
@@ -1930,14 +1846,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
             }
             for (int p = 0; p < 2; p++) {
                 if (t_first) SYM_HIP(hipEventRecord(evp->ev[p], ss[p]));
-                if (nset[p] && r256) { /* XM 4 with NST 8 leaves out both crosses K1, K1 + 1 */
-                    if (next)
-                        fwq_update_kernel<true, 4, 8><<<(unsigned)nset[p], 512, 0, ss[p]>>>(
-                            d, ld, P, k0, T, tb, K1, tls[p], te);
-                    else
-                        fwq_update_kernel<true, 5, 8><<<(unsigned)nset[p], 512, 0, ss[p]>>>(
-                            d, ld, P, k0, T, tb, -1, tls[p], te);
-                } else if (nset[p] && r128) {
+                if (nset[p] && r128) {
                     if (next)
                         fwq_update_kernel<true, 4, 4><<<(unsigned)nset[p], 512, 0, ss[p]>>>(
                             d, ld, P, k0, T, tb, K1, tls[p], te);
@@ -1955,29 +1864,21 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
                 if (t_last) SYM_HIP(hipEventRecord(evp->ev[evp->used - 2 + p], ss[p]));
             }
             SYM_HIP(hipGetLastError());
-            if (nr_cs) /* rest(k) done: round k + 1's cross may follow it */
-                for (int p = 0; p < 2; p++) SYM_HIP(hipEventRecord(sc->e_set[k & 1][p], ss[p]));
-            if (next && nr_cs) {
+            /* rest(k) done: round k + 1's cross follows it on the chain stream */
+            for (int p = 0; p < 2; p++) SYM_HIP(hipEventRecord(sc->e_set[k & 1][p], ss[p]));
+            if (next) {
                 /* the cross of K1 was last updated by rest(k - 1); P of round k + 1's buffer was
                  * last read by rest(k - 1) and the cross of round k - 1 (on cs) */
                 if (k >= 1) {
                     SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[(k - 1) & 1][0], 0));
                     SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[(k - 1) & 1][1], 0));
                 }
-                if (r256) /* the next band's two tile rows and columns */
-                    for (int h = 0; h < 2; h++)
-                        fwq_update_kernel<true, 3, 8><<<T + (te - tb), 512, 0, cs>>>(
-                            d, ld, P, k0, T, tb, K1 + h, nullptr, te);
-                else if (r128)
+                if (r128)
                     fwq_update_kernel<true, 3, 4><<<T + (te - tb), 512, 0, cs>>>(d, ld, P, k0, T, tb,
                                                                                 K1, nullptr, te);
                 else
                     FW_UPDATE(true, 3, T + (te - tb), cs, d, ld, P, k0, T, tb, K1, nullptr, te);
                 SYM_HIP(hipGetLastError());
-                if ((rc = make(k + 1))) goto out;
-            } else if (next) {
-                SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[k & 1][0], 0));
-                SYM_HIP(hipStreamWaitEvent(cs, sc->e_set[k & 1][1], 0));
                 if ((rc = make(k + 1))) goto out;
             }
         }
@@ -2116,11 +2017,9 @@ int srt_fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0, in
                       "most %d tile columns", SYM_TMAX);
         return SRT_E_ARG;
     }
-    /* 128-pivot rounds with the 8-wave update; SRT_FW_SH_KB=64 or 256 selects the others (256
-     * needs ld % 256 == 0) */
-    const char* kb_env = getenv("SRT_FW_SH_KB");
-    const int want = kb_env ? atoi(kb_env) : 128;
-    const int rp = want == 64 ? 64 : 128;
+    /* 128-pivot rounds with the 8-wave update; SRT_FW_SH_KB=64 selects 64-pivot rounds (a
+     * 256-pivot form measured slower at N = 8: 57.6 vs 45.9 ms for one rank) */
+    const int rp = srt_form_int("shkb", 128) == 64 ? 64 : 128;
     g_sharded_rp = rp;
     return fw16_build_sym_sharded(comm, n, ld, row0, nrows, w_rows, lat_rows, st, evp, exact, rp);
 }
@@ -2164,9 +2063,8 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
     }
     /* small matrices on one GPU (ld <= 2048, C2's 1,000 vertices): min-plus squaring to a fixed
      * point instead of ld / 64 latency-bound FW rounds; SRT_FW_SQUARE=0 keeps the rounds */
-    const char* sq_env = getenv("SRT_FW_SQUARE");
     if (fm && !bcast && !owner_of && row0 == 0 && nrows == ld && ld <= 2048 &&
-        !(sq_env && atoi(sq_env) == 0)) {
+        srt_form_int("square", 1) != 0) {
         if (sym) *sym = 5;
         return fw16_square(n, ld, w_rows, lat_rows, st, evp, exact);
     }
@@ -2184,23 +2082,21 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
     fw16_sched* sc;
     int rc = sched_get(&sc, dev);
     if (rc) return rc;
-    const char* la_env = getenv("SRT_FW_LOOKAHEAD");
-    const bool lookahead = la_env ? atoi(la_env) != 0 : bcast != NULL;
+    const int la = srt_form_int("lookahead", -1);
+    const bool lookahead = la >= 0 ? la != 0 : bcast != NULL;
     /* upper-triangle rounds: undirected graph, f16-compare path, the whole matrix on one GPU */
-    const char* sym_env = getenv("SRT_FW_SYM");
-    const bool want_sym = sym && *sym && !(sym_env && atoi(sym_env) == 0);
+    const bool want_sym = sym && *sym && srt_form_int("sym", 1) != 0;
     if (sym) *sym = 0;
     if (want_sym && fm && !bcast && !owner_of && row0 == 0 && nrows == ld) {
         /* two update streams once the rounds are long enough to hide their event waits;
          * SRT_FW_LOOKAHEAD=0/1 forces either form */
-        const bool two = la_env ? atoi(la_env) != 0 : ld >= 8192;
+        const bool two = la >= 0 ? la != 0 : ld >= 8192;
         /* 128-pivot rounds on the two update streams (8-wave kernel; SRT_FW_KB=64 selects the
          * 64-pivot rounds). With the update's compute loop at ~85% of the issue model, the per-tile
          * C load, row sums, staging and store are what is left to amortize: C4 332.2 vs 344.1 ms
          * per build on one box (before that loop change the two measured the same, 380.5 vs
          * 380.1 ms) */
-        const char* kb_env = getenv("SRT_FW_KB");
-        const int kbw = kb_env ? atoi(kb_env) : 256;
+        const int kbw = srt_form_int("kb", 256);
         const bool big = two;
         const int rp = big && kbw >= 256 && ld % 256 == 0 ? 256 : big && kbw >= 128 && ld >= 256 ? 128 : 64;
         *sym = rp == 256 ? 4 : rp == 128 ? 3 : two ? 2 : 1;
@@ -2465,14 +2361,12 @@ static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStrea
     } fr{dsum, st};
     /* split-k: one launch per squaring over every (tile, 256-pivot block) -- T^2 ld / 256
      * workgroups, every CU busy at C2's T = 8 -- into per-block partials, then one reduce pass
-     * that also says whether anything changed (SRT_FW_SQUARE_SPLIT=0: the in-place launches per
-     * block, one workgroup per tile) */
-    const char* sp_env = getenv("SRT_FW_SQUARE_SPLIT");
-    const bool split = !(sp_env && atoi(sp_env) == 0);
+     * that also says whether anything changed (an in-place form, one launch per 256-pivot block and
+     * one workgroup per tile, used 64 workgroups on C2 and was retired in round 4) */
     const int nq8 = ld / 256, tail = (ld % 256) ? 1 : 0;
     int* sflag = reinterpret_cast<int*>(dsum); /* four change flags (dsum holds 16 bytes) */
     u16* part = nullptr;
-    if (split) SRT_HIPCHK(srt_malloc_async((void**)&part, (size_t)(nq8 + tail) * ld * ld * 2, st));
+    SRT_HIPCHK(srt_malloc_async((void**)&part, (size_t)(nq8 + tail) * ld * ld * 2, st));
     struct freer2 {
         u16* p;
         hipStream_t s;
@@ -2480,7 +2374,6 @@ static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStrea
             if (p) (void)hipFreeAsync(p, s);
         }
     } fr2{part, st};
-    unsigned long long prev = ~0ull;
     /* timing (bench): the passes as one span, the first start to the end of the last checked
      * pass (evpool group 4, one unit per pass) -- no event records between passes */
     if (evp) {
@@ -2494,72 +2387,43 @@ static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStrea
     int hf[2] = {0, 0};
     bool finished = false;
     for (int it = 0; it < 64; ++it) {
-        if (split) {
-            if (nq8)
-                fwq_update_kernel<false, 20, 8><<<(unsigned)(T * T * nq8), 512, 0, st>>>(
-                    d, ld, d, 0, T, 0, 0, nullptr, 0, -1, part);
-            if (tail)
-                fwq_update_kernel<false, 20, 4><<<(unsigned)(T * T), 512, 0, st>>>(
-                    d, ld, d, nq8 * 256, T, 0, 0, nullptr, 0, -1, part + (size_t)nq8 * ld * ld);
-            if (!(it & 3)) SRT_HIPCHK(hipMemsetAsync(sflag, 0, 4 * sizeof(int), st));
-            const size_t cnt = (size_t)ld * ld;
-            static const char* rg_env = getenv("SRT_SQ_REDUCE_BLOCKS");
-            const unsigned rg = rg_env ? (unsigned)std::max(1, atoi(rg_env))
-                                       : (unsigned)std::min<size_t>(256, srt_ceil_div((long long)(cnt / 8), 256));
-            if (nq8 + tail == 4)
-                sq_reduce_kernel<4><<<rg, 256, 0, st>>>(cnt, 4, part, d, sflag + (it & 3));
-            else
-                sq_reduce_kernel<0><<<rg, 256, 0, st>>>(cnt, nq8 + tail, part, d, sflag + (it & 3));
-        } else {
-            for (int k0 = 0; k0 < ld; k0 += 256) {
-                if (k0 + 256 <= ld)
-                    fwq_update_kernel<false, 0, 8><<<(unsigned)(T * T), 512, 0, st>>>(
-                        d, ld, d + (size_t)k0 * ld, k0, T, 0, -1, nullptr, 0);
-                else
-                    fwq_update_kernel<false, 0, 4><<<(unsigned)(T * T), 512, 0, st>>>(
-                        d, ld, d + (size_t)k0 * ld, k0, T, 0, -1, nullptr, 0);
-            }
-        }
+        if (nq8)
+            fwq_update_kernel<false, 20, 8><<<(unsigned)(T * T * nq8), 512, 0, st>>>(
+                d, ld, d, 0, T, 0, 0, nullptr, 0, -1, part);
+        if (tail)
+            fwq_update_kernel<false, 20, 4><<<(unsigned)(T * T), 512, 0, st>>>(
+                d, ld, d, nq8 * 256, T, 0, 0, nullptr, 0, -1, part + (size_t)nq8 * ld * ld);
+        if (!(it & 3)) SRT_HIPCHK(hipMemsetAsync(sflag, 0, 4 * sizeof(int), st));
+        const size_t cnt = (size_t)ld * ld;
+        const unsigned rg = (unsigned)std::min<size_t>(256, srt_ceil_div((long long)(cnt / 8), 256));
+        if (nq8 + tail == 4)
+            sq_reduce_kernel<4><<<rg, 256, 0, st>>>(cnt, 4, part, d, sflag + (it & 3));
+        else
+            sq_reduce_kernel<0><<<rg, 256, 0, st>>>(cnt, nq8 + tail, part, d, sflag + (it & 3));
         SRT_HIPCHK(hipGetLastError());
-        if (split) {
-            /* the change flags are read every fourth pass (one host round trip per four
-             * passes; complete graphs converge in 3-4): a pass after the fixed point changes
-             * nothing and costs only its time. The finish pass (u32 table, exactness and
-             * small-distance flags) is enqueued with the check, so a converged squaring needs
-             * no second round trip; otherwise its output is overwritten later. */
-            if ((it & 3) != 3) continue;
-            if (evp) {
-                evp->used = 4 * (it + 1);
-                SRT_HIPCHK(hipEventRecord(evp->ev[evp->used - 2], st));
-                SRT_HIPCHK(hipEventRecord(evp->ev[evp->used - 1], st));
-            }
-            SRT_HIPCHK(hipMemsetAsync(flags, 0, 2 * sizeof(int), st));
-            fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 2048), ld), 256, 0, st>>>(n, ld, 0, d, lat,
-                                                                                flags, CAP_F);
-            SRT_HIPCHK(hipGetLastError());
-            int ch[4] = {0, 0, 0, 0};
-            SRT_HIPCHK(hipMemcpyAsync(ch, sflag, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
-            SRT_HIPCHK(hipMemcpyAsync(hf, flags, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
-            SRT_HIPCHK(hipStreamSynchronize(st));
-            if (!ch[0] || !ch[1] || !ch[2] || !ch[3]) {
-                finished = true;
-                break;
-            }
-            continue;
-        }
+        /* the change flags are read every fourth pass (one host round trip per four passes;
+         * complete graphs converge in 3-4): a pass after the fixed point changes nothing and
+         * costs only its time. The finish pass (u32 table, exactness and small-distance flags) is
+         * enqueued with the check, so a converged squaring needs no second round trip; otherwise
+         * its output is overwritten later. */
+        if ((it & 3) != 3) continue;
         if (evp) {
             evp->used = 4 * (it + 1);
             SRT_HIPCHK(hipEventRecord(evp->ev[evp->used - 2], st));
             SRT_HIPCHK(hipEventRecord(evp->ev[evp->used - 1], st));
         }
-        SRT_HIPCHK(hipMemsetAsync(dsum, 0, sizeof(unsigned long long), st));
-        rows_sum_kernel<<<64, 256, 0, st>>>((size_t)ld * ld, d, dsum);
+        SRT_HIPCHK(hipMemsetAsync(flags, 0, 2 * sizeof(int), st));
+        fw16_finish_kernel<<<dim3(srt_ceil_div(ld, 2048), ld), 256, 0, st>>>(n, ld, 0, d, lat,
+                                                                            flags, CAP_F);
         SRT_HIPCHK(hipGetLastError());
-        unsigned long long cur = 0;
-        SRT_HIPCHK(hipMemcpyAsync(&cur, dsum, sizeof(cur), hipMemcpyDeviceToHost, st));
+        int ch[4] = {0, 0, 0, 0};
+        SRT_HIPCHK(hipMemcpyAsync(ch, sflag, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipMemcpyAsync(hf, flags, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
         SRT_HIPCHK(hipStreamSynchronize(st));
-        if (cur == prev) break;
-        prev = cur;
+        if (!ch[0] || !ch[1] || !ch[2] || !ch[3]) {
+            finished = true;
+            break;
+        }
     }
     if (!finished) {
         SRT_HIPCHK(hipMemsetAsync(flags, 0, 2 * sizeof(int), st));

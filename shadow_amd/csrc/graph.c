@@ -27,6 +27,33 @@ static int log_level(void) {
     return g_log_level;
 }
 
+/* SRT_FORM: forcing of internal forms for tests and A/B runs, a comma-separated
+ * list of key=value pairs, re-read at every call (tests change it between builds). Production
+ * builds never set it: every form is chosen from the graph and the device. */
+static const char* form_find(const char* key) {
+    const char* e = getenv("SRT_FORM");
+    if (!e) return NULL;
+    const size_t kl = strlen(key);
+    for (const char* p = e; *p;) {
+        while (*p == ',' || *p == ' ') p++;
+        if (!strncmp(p, key, kl) && p[kl] == '=') return p + kl + 1;
+        while (*p && *p != ',') p++;
+    }
+    return NULL;
+}
+
+int srt_form_int(const char* key, int dflt) {
+    const char* v = form_find(key);
+    return v && *v && *v != ',' ? atoi(v) : dflt;
+}
+
+int srt_form_is(const char* key, const char* value) {
+    const char* v = form_find(key);
+    if (!v) return 0;
+    const size_t l = strlen(value);
+    return !strncmp(v, value, l) && (v[l] == '\0' || v[l] == ',');
+}
+
 void srt_log(int level, const char* fmt, ...) {
     if (level > log_level()) return;
     static const char* names[] = {"error", "warning", "info", "debug"};

@@ -118,11 +118,10 @@ static __device__ __forceinline__ void ms_compact(uint32_t* bm, int nw, int* lis
  * for undirected graphs); inv[original] = relabelled; bsrc / brow: per batch and lane the
  * relabelled source and the output row (-1 = empty lane); ws: per slot D (n x 64 u32), R (n x 64
  * f64) and the lane minimum of every vertex (n u32). */
-template <bool DIRECTED, bool PROF, typename DT, bool A32>
+template <bool DIRECTED, bool PROF, typename DT>
 __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
     int n, const int2* __restrict__ orp, const uint2* __restrict__ ocw,
-    const int2* __restrict__ irp, const uint2* __restrict__ icw, const uint32_t* __restrict__ ica,
-    const double* __restrict__ ir,
+    const int2* __restrict__ irp, const uint2* __restrict__ icw, const double* __restrict__ ir,
     const int32_t* __restrict__ inv, int nbatch, const int32_t* __restrict__ bsrc,
     const int32_t* __restrict__ brow, uint32_t* __restrict__ lat, double* __restrict__ rel,
     size_t ldo, uint32_t* __restrict__ ws, size_t slot_words, uint32_t delta,
@@ -214,16 +213,11 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                  * are loaded while this group's distance rows are in flight, so a group's chain
                  * is its distance rows, then its reliability gathers */
                 constexpr int GS = MS_NWAVE * MS_G;
-                /* a lane's arc of a chunk: A32 one word col | w << 24, else the (col, w) pair */
-                using arc_t = typename std::conditional<A32, uint32_t, uint2>::type;
-                auto arc_at = [&](int k) -> arc_t {
-                    if constexpr (A32) return ica[k];
-                    else return icw[k];
-                };
-                auto arc_none = []() -> arc_t {
-                    if constexpr (A32) return 0u;
-                    else return make_uint2(0u, 0u);
-                };
+                /* a lane's arc of a chunk: the (col, w) pair (one packed word measured slower: the
+                 * scalar split sits on the address chain, C3 26.4 vs 25.2 ms) */
+                using arc_t = uint2;
+                auto arc_at = [&](int k) -> arc_t { return icw[k]; };
+                auto arc_none = []() -> arc_t { return make_uint2(0u, 0u); };
                 int vl_n = 0;
                 int2 bel_n = make_int2(0, 0);
                 arc_t ea_n = arc_none();
@@ -274,14 +268,8 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                     /* the arc in slot j * MS_AC + h of the chunk: its column and weight, as
                      * wave-uniform values (one lane read, the split is scalar) */
                     auto arc_of = [&](const arc_t& e, int slot, uint32_t& col, uint32_t& w) {
-                        if constexpr (A32) {
-                            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)e, slot);
-                            col = x & 0xFFFFFFu;
-                            w = x >> 24;
-                        } else {
-                            col = (uint32_t)__builtin_amdgcn_readlane((int)e.x, slot);
-                            w = (uint32_t)__builtin_amdgcn_readlane((int)e.y, slot);
-                        }
+                        col = (uint32_t)__builtin_amdgcn_readlane((int)e.x, slot);
+                        w = (uint32_t)__builtin_amdgcn_readlane((int)e.y, slot);
                     };
                     arc_t ea = ea0;
                     for (int c0 = 0; c0 < maxdeg; c0 += MS_AC) {
@@ -358,8 +346,7 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                                 for (int k = ob.x + lane; k < ob.y; k += MS_L) ms_set(nxt, ocw[k].x);
                             } else if (maxdeg <= MS_AC) { /* the arcs of the (only) chunk */
                                 if (aj == j && aa < dg[j]) {
-                                    if constexpr (A32) ms_set(nxt, ea & 0xFFFFFFu);
-                                    else ms_set(nxt, ea.x);
+                                    ms_set(nxt, ea.x);
                                 }
                             } else {
                                 for (int k = bx[j] + lane; k < bx[j] + dg[j]; k += MS_L)
@@ -487,7 +474,7 @@ static uint32_t* g_ms_ws[SRT_STATE_SLOTS];
 static size_t g_ms_cap[SRT_STATE_SLOTS];
 
 int srt_msssp_rows(int n, int directed, const int2* orp, const uint2* ocw, const int2* irp,
-                   const uint2* icw, const uint32_t* ica, const double* ir, const int32_t* inv,
+                   const uint2* icw, const double* ir, const int32_t* inv,
                    uint32_t delta, int nbatch, const int32_t* bsrc, const int32_t* brow,
                    uint32_t* lat, double* rel, size_t ldo, int d16, hipStream_t st) {
     if (n > srt_msssp_max_n()) {
@@ -502,8 +489,8 @@ int srt_msssp_rows(int n, int directed, const int2* orp, const uint2* ocw, const
     /* D (u32-sized slots; a u16 row uses half), R and the lane minimum, rounded to 16 bytes */
     const size_t slot_words = ((size_t)n * MS_L * 3 + (size_t)n + 3) & ~(size_t)3;
     const size_t per_slot = slot_words * sizeof(uint32_t);
-    const char* wenv = getenv("SRT_MSSSP_SLOTS");
-    size_t slots = wenv && atoi(wenv) > 0 ? (size_t)atoi(wenv) : 2 * (size_t)cus;
+    const int fs = srt_form_int("ms_slots", 0); /* tests: one or a few persistent slots */
+    size_t slots = fs > 0 ? (size_t)fs : 2 * (size_t)cus;
     if (slots > (size_t)nbatch) slots = nbatch;
     const int sl = srt_state_slot();
     if (g_ms_cap[sl] < slots * per_slot) {
@@ -534,28 +521,25 @@ int srt_msssp_rows(int n, int directed, const int2* orp, const uint2* ocw, const
     uint32_t* ws = g_ms_ws[sl];
     const uint32_t dl = delta < 1 ? 1u : delta;
     const size_t dyn = ms_lds_bytes(n);
-    const char* penv = getenv("SRT_MSSSP_PROF");
-    unsigned long long* prof = NULL;
-    if (penv && atoi(penv) > 0 &&
+    unsigned long long* prof = NULL; /* SRT_FORM prof=1: per-batch phase counts (tools) */
+    if (srt_form_int("prof", 0) > 0 &&
         srt_malloc_async((void**)&prof, (size_t)nbatch * MS_PROF * sizeof(unsigned long long), st) !=
             hipSuccess) {
         (void)hipGetLastError();
         prof = NULL;
     }
-#define SRT_MSSSP_LAUNCH(DIR, PR, DT, A)                                                         \
+#define SRT_MSSSP_LAUNCH(DIR, PR, DT)                                                            \
     do {                                                                                         \
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)msssp_kernel<DIR, PR, DT, A>,                 \
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)msssp_kernel<DIR, PR, DT>,                    \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));    \
-        msssp_kernel<DIR, PR, DT, A><<<(unsigned)slots, MS_WG, dyn, st>>>(                        \
-            n, orp, ocw, irp, icw, ica, ir, inv, nbatch, bsrc, brow, lat, rel, ldo, ws,           \
-            slot_words, dl, prof);                                                                \
+        msssp_kernel<DIR, PR, DT><<<(unsigned)slots, MS_WG, dyn, st>>>(                           \
+            n, orp, ocw, irp, icw, ir, inv, nbatch, bsrc, brow, lat, rel, ldo, ws, slot_words,    \
+            dl, prof);                                                                           \
     } while (0)
 #define SRT_MSSSP_LAUNCH2(DIR, PR)                                                               \
     do {                                                                                         \
-        if (d16 && ica) SRT_MSSSP_LAUNCH(DIR, PR, uint16_t, true);                                \
-        else if (d16) SRT_MSSSP_LAUNCH(DIR, PR, uint16_t, false);                                 \
-        else if (ica) SRT_MSSSP_LAUNCH(DIR, PR, uint32_t, true);                                  \
-        else SRT_MSSSP_LAUNCH(DIR, PR, uint32_t, false);                                          \
+        if (d16) SRT_MSSSP_LAUNCH(DIR, PR, uint16_t);                                             \
+        else SRT_MSSSP_LAUNCH(DIR, PR, uint32_t);                                                 \
     } while (0)
     if (directed && prof) SRT_MSSSP_LAUNCH2(true, true);
     else if (directed) SRT_MSSSP_LAUNCH2(true, false);

@@ -15,6 +15,10 @@ extern "C" {
 enum { SRT_LOG_ERROR = 0, SRT_LOG_WARNING = 1, SRT_LOG_INFO = 2, SRT_LOG_DEBUG = 3 };
 void srt_log(int level, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 void srt_set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+/* SRT_FORM=key=value,... (tests / A/B only): srt_form_int -> the value of key, or dflt when unset;
+ * srt_form_is -> 1 when key is set to exactly value (graph.c) */
+int srt_form_int(const char* key, int dflt);
+int srt_form_is(const char* key, const char* value);
 
 /* Canonical dense / CSR forms of an edge list (host side, see graph.c). */
 typedef struct srt_canon {

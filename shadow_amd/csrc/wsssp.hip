@@ -305,8 +305,8 @@ int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, con
     }
     const int nsrc = src_end - src_begin;
     int bcap = n < 8192 ? n : 8192;
-    const char* env = getenv("SRT_WSSSP_BCAP"); /* tests: force bucket overflows */
-    if (env && atoi(env) > 0) bcap = atoi(env);
+    const int fb = srt_form_int("bcap", 0); /* tests: force bucket overflows */
+    if (fb > 0) bcap = fb;
     int cus = 256;
     int dev = 0;
     hipDeviceProp_t prop;
@@ -316,27 +316,26 @@ int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, con
      * global ones -- the global form is bound by the texture path at one line per lane), else a
      * global row with up to SRT_WSSSP_WAVES (default 16) waves per CU */
     const size_t lds_row = (size_t)n * sizeof(uint32_t), lds_static = 4096;
-    const char* lenv = getenv("SRT_WSSSP_LDS");
     /* the LDS form holds few waves per CU and each wave's bucket steps are a latency chain
      * (C3, n = 20000: 2 waves/CU, 354 ms vs 70 ms for the global form at 16), so it is the
-     * default only while it still fits 8 waves per CU; SRT_WSSSP_LDS=1/0 forces either form */
-    const bool ldsd = lenv ? (atoi(lenv) != 0 && lds_row + lds_static <= 160 * 1024)
-                           : 8 * (lds_row + lds_static) <= 160 * 1024;
+     * default only while it still fits 8 waves per CU; SRT_FORM ws_lds=1/0 forces either form */
+    const int fl = srt_form_int("ws_lds", -1);
+    const bool ldsd = fl >= 0 ? (fl != 0 && lds_row + lds_static <= 160 * 1024)
+                              : 8 * (lds_row + lds_static) <= 160 * 1024;
     /* the kernel's slot layout: f64 reliability row, bucket ring, u32 distance row (global form),
      * padded to 8 bytes */
-    const char* renv = getenv("SRT_WSSSP_RELROW"); /* tests: force either reliability form */
-    const bool relp = renv ? atoi(renv) != 0 : local != 0;
+    const int fr = srt_form_int("ws_relrow", -1); /* tests: force either reliability form */
+    const bool relp = fr >= 0 ? fr != 0 : local != 0;
     g_sparse_form = (ldsd ? 1 : 0) | (relp ? 2 : 0);
     const size_t per_slot =
         (((relp ? 2 * (size_t)n : 0) + (size_t)nb * bcap + (ldsd ? 0 : n) + 1) & ~(size_t)1) *
         sizeof(uint32_t);
-    const char* wenv = getenv("SRT_WSSSP_WAVES");
-    size_t slots = ldsd ? (size_t)cus * ((160 * 1024) / (lds_row + lds_static))
-                        : (size_t)(wenv && atoi(wenv) > 0 ? atoi(wenv) : 16) * cus;
+    /* 16 waves per CU (24 / 32 / 40 measured slower on C3: 65.1 / 66.6 / 65.4 vs 62.0 ms) */
+    size_t slots = ldsd ? (size_t)cus * ((160 * 1024) / (lds_row + lds_static)) : (size_t)16 * cus;
     /* the random gathers into the working rows are served by L2 / Infinity Cache / HBM; past
      * about 1.4 GB of rows in flight more waves only thrash (C5, n = 100,000: 16 waves/CU
      * 2.90 s, 3,500 waves 2.6 s, 8/CU 2.66 s; C3, n = 20,000: 16/CU 73 ms, 8/CU 98 ms) */
-    if (!ldsd && !(wenv && atoi(wenv) > 0)) {
+    if (!ldsd) {
         const size_t cap = ((size_t)1400 << 20) / ((size_t)n * sizeof(uint32_t));
         if (slots > cap) slots = cap > (size_t)cus ? cap : (size_t)cus;
     }
@@ -866,8 +865,7 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
                     double* rel, int* ovf, hipStream_t st, const uint8_t* ridx,
                     const double* rtab) {
     /* two-level steps push up to d + 1 + max_w: the ring then needs max_w + 2 buckets */
-    const char* twoenv = getenv("SRT_WG_TWO");
-    int two = twoenv ? atoi(twoenv) != 0 : 1;
+    int two = srt_form_int("wg_two", 1) != 0; /* tests: one-level steps */
     if (max_w + 2u > 256u) two = 0;
     int nb = 1;
     while ((uint32_t)nb <= max_w + (uint32_t)two) nb <<= 1;
@@ -877,8 +875,8 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     }
     const int nsrc = src_end - src_begin;
     int bcap = n < 32768 ? n : 32768; /* entries per bucket (uint2) */
-    const char* env = getenv("SRT_WSSSP_BCAP"); /* tests: force bucket overflows */
-    if (env && atoi(env) > 0) bcap = atoi(env);
+    const int fb = srt_form_int("bcap", 0); /* tests: force bucket overflows */
+    if (fb > 0) bcap = fb;
     int cus = 256, dev = 0;
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
@@ -888,11 +886,8 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     SRT_HIPCHK(hipMemcpyAsync(&last, rowptr + (n - 1), sizeof(int2), hipMemcpyDeviceToHost, st));
     SRT_HIPCHK(hipStreamSynchronize(st));
     /* compact 8-byte arcs: original order, a reliability table, w < 128, arcs < 2^20 */
-    const char* cenv = getenv("SRT_WG_COMPACT");
-    const char* tenv = getenv("SRT_WGSSSP_THREADS"); /* 512: the 16-byte-arc form only */
-    const bool t512 = tenv && atoi(tenv) == 512;
     const bool cmp = !inv && ridx && rtab && max_w < 128 && last.y < (1 << 20) &&
-                     !(cenv && atoi(cenv) == 0) && !t512;
+                     srt_form_int("wg_compact", 1) != 0; /* tests: the 16-byte arcs */
     g_sparse_form = 4 | (inv ? 0 : 1) | (cmp ? 2 : 0);
     void* ca = NULL;
     const size_t arc_bytes = cmp ? sizeof(uint2) : sizeof(uint4);
@@ -919,8 +914,7 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     }
     SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)nsrc * sizeof(int), st));
     const size_t dyn = (size_t)((n + 2) / 3) * sizeof(uint32_t);
-    const char* penv = getenv("SRT_WGSSSP_PROF"); /* tools: per-phase cycle counts on stderr */
-    if (penv && atoi(penv) > 0) {
+    if (srt_form_int("prof", 0) > 0) { /* tools: per-phase cycle counts on stderr */
         unsigned long long* prof = NULL;
         SRT_HIPCHK(hipMalloc((void**)&prof, slots * 16 * sizeof(unsigned long long)));
         if (cmp) {
@@ -967,20 +961,6 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
                 100 * tot[12] / cyc, 100 * tot[13] / cyc, 100 * tot[14] / cyc, 100 * tot[3] / cyc);
         free(h);
         SRT_HIPCHK(hipFree(prof));
-    } else if (t512) { /* 16-byte arcs; ORIG follows inv as below */
-        if (!inv) {
-            SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<512, false, true>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-            wgsssp_kernel<512, false, true><<<(unsigned)slots, 512, dyn, st>>>(
-                n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf,
-                nullptr, two);
-        } else {
-            SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<512>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-            wgsssp_kernel<512><<<(unsigned)slots, 512, dyn, st>>>(
-                n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf,
-                nullptr, two);
-        }
     } else if (cmp) { /* original order, compact arcs, reliabilities from the table */
         SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, false, true, true>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));

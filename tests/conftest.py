@@ -33,3 +33,41 @@ def gpu():
     L = _lib.lib()
     assert L.srt_device_count() >= 1
     return L
+
+
+# SRT_FORM keys: forcing of internal forms for tests, one environment variable
+def set_form(monkeypatch, **kv):
+    """Merge key=value pairs into SRT_FORM for this test (monkeypatch restores it)."""
+    cur = {}
+    for item in os.environ.get("SRT_FORM", "").split(","):
+        if "=" in item:
+            k, v = item.split("=", 1)
+            cur[k.strip()] = v
+    cur.update({k: str(v) for k, v in kv.items()})
+    monkeypatch.setenv("SRT_FORM", ",".join(f"{k}={v}" for k, v in cur.items()))
+
+
+class form_env:
+    """Context manager: SRT_FORM with key=value pairs merged in, restored on exit (for a part of
+    a test; set_form covers a whole test)."""
+
+    def __init__(self, **kv):
+        self.kv = {k: str(v) for k, v in kv.items()}
+
+    def __enter__(self):
+        self.old = os.environ.get("SRT_FORM")
+        cur = {}
+        for item in (self.old or "").split(","):
+            if "=" in item:
+                k, v = item.split("=", 1)
+                cur[k.strip()] = v
+        cur.update(self.kv)
+        os.environ["SRT_FORM"] = ",".join(f"{k}={v}" for k, v in cur.items())
+        return self
+
+    def __exit__(self, *exc):
+        if self.old is None:
+            os.environ.pop("SRT_FORM", None)
+        else:
+            os.environ["SRT_FORM"] = self.old
+        return False

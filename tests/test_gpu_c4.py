@@ -13,6 +13,7 @@ import ctypes
 
 import numpy as np
 import pytest
+from conftest import set_form
 
 import oracle
 from shadow_amd import _lib
@@ -24,11 +25,11 @@ N, SEED, LAT_MAX, SELF_MAX, LOSS_MAX = 32768, 4, 1000, 10, 500
 
 @pytest.mark.parametrize("mode", ["levels", "fw"])
 def test_c4_full_size_default_schedule(gpu, monkeypatch, mode):
-    """mode levels: the default (bit-parallel Dial levels, encoding 12); fw: SRT_DENSE_LEVELS=0
+    """mode levels: the default (bit-parallel Dial levels, encoding 12); fw: SRT_FORM levels=0
     keeps the Floyd-Warshall schedule (encoding 7)."""
     import torch
     if mode == "fw":
-        monkeypatch.setenv("SRT_DENSE_LEVELS", "0")
+        set_form(monkeypatch, levels="0")
     L = _lib.lib()
     n = ld = N
     w = torch.empty((ld, ld), dtype=torch.int32, device="cuda")
@@ -88,7 +89,7 @@ def test_c4_virtual_ranks_sharded_schedule(gpu, monkeypatch, ranks, mode):
     import threading
     import torch
     if mode == "fw":
-        monkeypatch.setenv("SRT_DENSE_LEVELS", "0")
+        set_form(monkeypatch, levels="0")
     L = _lib.lib()
     n = ld = N
     comms = (ctypes.c_void_p * ranks)()

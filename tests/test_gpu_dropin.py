@@ -446,13 +446,10 @@ def test_dense_rows_few_attached(gpu, kind):
     if kind == "sub_ms":
         assert np.array_equal(ms, full["lat_ms"][sub])
     # the same request with the rows path off takes the FW and agrees
-    import os
-    os.environ["SRT_DENSE_ROWS"] = "0"
-    try:
+    from conftest import form_env
+    with form_env(rows=0):
         lat2, rel2, _, _, st2 = build_tables_subset(g.n, g.directed, g.src, g.dst, g.lat_ns,
                                                     g.loss, verts=verts, algo=ALGO_AUTO)
-    finally:
-        del os.environ["SRT_DENSE_ROWS"]
     assert st2.dist_enc != 10 and np.array_equal(lat, lat2) and np.array_equal(rel, rel2)
 
 

@@ -2,7 +2,7 @@
 the CPU oracle's Dijkstra (oracle.c, restating topology.c:1578-1814), bit for bit in latency and
 reliability (the post pass forms predecessors and path-order products from the level distances).
 
-SRT_DENSE_LEVELS=1 forces the level search at any size (the default takes it from n >= 4,096 when
+SRT_FORM levels=1 forces the level search at any size (the default takes it from n >= 4,096 when
 its budget beats the FW); when the graph's distances pass the level budget the build must fall back
 to the FW and still match. Sharded: virtual ranks on one GPU (row shards, arcs broadcast per rank's
 segment, one verdict for all ranks)."""
@@ -10,6 +10,7 @@ import ctypes
 
 import numpy as np
 import pytest
+from conftest import set_form
 
 import oracle
 from shadow_amd import _lib, graphs
@@ -50,7 +51,7 @@ def _directed_dense(n, seed, wmax):
 
 @pytest.mark.parametrize("kind", ["complete300", "complete1000", "ties", "directed", "c1like"])
 def test_levels_match_oracle(gpu, monkeypatch, kind):
-    monkeypatch.setenv("SRT_DENSE_LEVELS", "1")
+    set_form(monkeypatch, levels="1")
     if kind == "complete300":
         g = graphs.complete_graph(300, seed=7)
     elif kind == "complete1000":  # C2's distribution: distances up to 9 quanta
@@ -69,7 +70,7 @@ def test_levels_match_oracle(gpu, monkeypatch, kind):
 
 def test_levels_over_budget_falls_back(gpu, monkeypatch):
     """A ring of 200-ms hops: distances pass the 254-level budget, so the FW builds it."""
-    monkeypatch.setenv("SRT_DENSE_LEVELS", "1")
+    set_form(monkeypatch, levels="1")
     n = 300
     src = np.arange(n, dtype=np.int32)
     dst = ((src + 1) % n).astype(np.int32)
@@ -117,7 +118,7 @@ def test_levels_virtual_ranks(gpu, monkeypatch, ranks, kind):
     """Row-sharded level builds: every rank extracts the in-arcs of its rows, broadcasts its
     segment, settles its own sources, and all ranks agree on the verdict (ld = 1,024: at 3 ranks
     the row blocks are 384 | 256 | 384)."""
-    monkeypatch.setenv("SRT_DENSE_LEVELS", "1")
+    set_form(monkeypatch, levels="1")
     monkeypatch.setenv("SRT_VIRTUAL_RANKS", str(ranks))
     g = graphs.complete_graph(1000, seed=2) if kind == "complete" else \
         graphs.complete_graph(900, seed=4, lat_max=4)

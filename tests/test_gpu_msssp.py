@@ -1,6 +1,6 @@
 """Multi-source shared-frontier SSSP (shadow_amd/csrc/msssp.hip, srt_build_stats.dist_enc 3):
 64 sources per workgroup, one per lane, pulls to a fixed point with delta-stepping over the lane
-minimum. AUTO takes it for local graphs (C3-shaped RGGs); SRT_SPARSE_MS=1 forces it on any graph.
+minimum. AUTO takes it for local graphs (C3-shaped RGGs); SRT_FORM kernel=ms forces it on any graph.
 
 Every row is its own source's (topology.c:1578-1814, no mirror), compared with oracle/ off the
 diagonal: latency bit-exact in integer ns, reliability bit-exact (the product is formed in path
@@ -8,6 +8,7 @@ order along the canonical predecessor, like the single-source kernels; north_sta
 """
 import numpy as np
 import pytest
+from conftest import form_env, set_form
 
 import oracle
 from shadow_amd import graphs
@@ -80,7 +81,7 @@ def test_msssp_full_tables(gpu, monkeypatch, which):
     """Forced multi-source kernel: the whole raw table (every source's own row) equals the
     oracle's, on undirected / directed / power-law / disconnected graphs and tie-heavy (1..2 ms)
     and wide (1..5000 ms, max weight >= 256) weights."""
-    monkeypatch.setenv("SRT_SPARSE_MS", "1")
+    set_form(monkeypatch, kernel="ms")
     g = _graph(which)
     lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
                                 algo=ALGO_SPARSE_SSSP)
@@ -91,16 +92,13 @@ def test_msssp_full_tables(gpu, monkeypatch, which):
     assert np.array_equal(rel.view(np.uint64), exp["rel"].view(np.uint64)), which
 
 
-@pytest.mark.parametrize("a32", ["0", "1"])
 @pytest.mark.parametrize("u16", ["0", "1"])
-def test_msssp_distance_widths(gpu, monkeypatch, u16, a32):
-    """SRT_MSSSP_U16=0/1: 32-bit working distances, or 16-bit ones (the default when the graph's
-    distance bound is below 0xFFFF; a candidate past it reads as not reached yet), and
-    SRT_MSSSP_A32=0/1: (col, w) pair arcs or col | w << 24 words (the default when every weight is
-    below 256), all four forms give the same tables."""
-    monkeypatch.setenv("SRT_SPARSE_MS", "1")
-    monkeypatch.setenv("SRT_MSSSP_U16", u16)
-    monkeypatch.setenv("SRT_MSSSP_A32", a32)
+def test_msssp_distance_widths(gpu, monkeypatch, u16):
+    """SRT_FORM ms_u16=0/1: 32-bit working distances, or 16-bit ones (the default when the graph's
+    distance bound is below 0xFFFF; a candidate past it reads as not reached yet): the same
+    tables."""
+    set_form(monkeypatch, kernel="ms")
+    set_form(monkeypatch, ms_u16=u16)
     g = graphs.random_geometric(2200, seed=13)
     lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
                                 algo=ALGO_SPARSE_SSSP)
@@ -112,10 +110,10 @@ def test_msssp_distance_widths(gpu, monkeypatch, u16, a32):
 
 @pytest.mark.parametrize("delta", ["1", "3", "100000"])
 def test_msssp_bucket_widths(gpu, monkeypatch, delta):
-    """SRT_MSSSP_DELTA: bucket width 1 (Dial-like), 3, and one bucket for everything (plain
+    """SRT_FORM ms_delta: bucket width 1 (Dial-like), 3, and one bucket for everything (plain
     frontier Bellman-Ford) reach the same fixed point."""
-    monkeypatch.setenv("SRT_SPARSE_MS", "1")
-    monkeypatch.setenv("SRT_MSSSP_DELTA", delta)
+    set_form(monkeypatch, kernel="ms")
+    set_form(monkeypatch, ms_delta=delta)
     g = graphs.random_geometric(2500, seed=11)
     lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
                                 algo=ALGO_SPARSE_SSSP)
@@ -127,10 +125,10 @@ def test_msssp_bucket_widths(gpu, monkeypatch, delta):
 
 @pytest.mark.parametrize("slots", ["1", "3"])
 def test_msssp_persistent_slots(gpu, monkeypatch, slots):
-    """SRT_MSSSP_SLOTS: one workgroup (or three) runs every batch in turn, so every batch after
+    """SRT_FORM ms_slots: one workgroup (or three) runs every batch in turn, so every batch after
     the first starts from the previous batch's working rows (re-initialised to INF)."""
-    monkeypatch.setenv("SRT_SPARSE_MS", "1")
-    monkeypatch.setenv("SRT_MSSSP_SLOTS", slots)
+    set_form(monkeypatch, kernel="ms")
+    set_form(monkeypatch, ms_slots=slots)
     g = graphs.random_geometric(1200, seed=21)
     lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
                                 algo=ALGO_SPARSE_SSSP)
@@ -172,28 +170,21 @@ def test_msssp_c3_compact_sources_and_ties(gpu):
     assert np.array_equal(np.where(off, got, 0), np.where(off, exp["lat_int"], 0))
     r = rel.cpu().numpy()
     assert np.array_equal(r[off].view(np.uint64), exp["rel"][off].view(np.uint64))
-    os.environ["SRT_SPARSE_MS"] = "0"
-    try:
+    with form_env(kernel="wave"):
         st1 = BuildStats()
         st1.count_ties = 1
         sg.rows_list(ds.data_ptr(), len(srcs), lat.data_ptr(), rel.data_ptr(), None, st1)
         torch.cuda.synchronize()
-    finally:
-        del os.environ["SRT_SPARSE_MS"]
     assert st1.dist_enc == 1 and st1.tied_pairs == st.tied_pairs, (st1.tied_pairs, st.tied_pairs)
     # 100 original ids: random positions, so small clusters -- batches of their own within the
     # batch budget, the single-source kernels without one
     exp = oracle.sssp_rows(el, 0, 100, nthreads=16)
     off = np.arange(g.n)[None, :] != np.arange(100)[:, None]
     for maxb, enc in ((None, 3), ("0", 1)):
-        if maxb is not None:
-            os.environ["SRT_MSSSP_MAXB"] = maxb
-        try:
+        with form_env(**({} if maxb is None else {"ms_maxb": maxb})):
             st2 = BuildStats()
             sg.rows(0, 100, lat.data_ptr(), rel.data_ptr(), None, st2)
             torch.cuda.synchronize()
-        finally:
-            os.environ.pop("SRT_MSSSP_MAXB", None)
         assert st2.dist_enc == enc, (maxb, st2.dist_enc)
         got = lat[:100].cpu().numpy().view(np.uint32).astype(np.uint64) * np.uint64(sg.quantum_ns)
         assert np.array_equal(np.where(off, got, 0), np.where(off, exp["lat_int"], 0)), maxb
@@ -208,8 +199,8 @@ def test_msssp_source_list(gpu, monkeypatch, which):
     the last one partial; the hop radius lifted so the scattered sources still share batches):
     row i is source srcs[i]."""
     import torch
-    monkeypatch.setenv("SRT_SPARSE_MS", "1")
-    monkeypatch.setenv("SRT_MSSSP_RMAX", "100000")  # cluster even scattered sources
+    set_form(monkeypatch, kernel="ms")
+    set_form(monkeypatch, ms_rmax="100000")  # cluster even scattered sources
     g = _graph(which)
     rng = np.random.default_rng(77)
     srcs = rng.choice(g.n, 150, replace=False).astype(np.int32)
@@ -235,14 +226,14 @@ def test_msssp_compact_and_scattered_sources(gpu, monkeypatch, rmax, maxb, enc):
     """A source list mixing a compact region (the 200 vertices nearest a point of the unit
     square) with 40 scattered vertices. Clusters that fill 48 lanes within the hop radius take the
     multi-source kernel; the small ones do too while all batches fit the batch budget
-    (SRT_MSSSP_MAXB, default two per CU), else they take the single-source kernels and are
+    (SRT_FORM ms_maxb, default two per CU), else they take the single-source kernels and are
     scattered to their rows: budget 4 splits the set, radius 0 with budget 0 sends every source
     there (dist_enc 1)."""
     import torch
-    monkeypatch.setenv("SRT_SPARSE_MS", "1")
-    monkeypatch.setenv("SRT_MSSSP_RMAX", rmax)
+    set_form(monkeypatch, kernel="ms")
+    set_form(monkeypatch, ms_rmax=rmax)
     if maxb is not None:
-        monkeypatch.setenv("SRT_MSSSP_MAXB", maxb)
+        set_form(monkeypatch, ms_maxb=maxb)
     n = 4000
     g = graphs.random_geometric(n, seed=3)
     idx = np.arange(n, dtype=np.uint64)

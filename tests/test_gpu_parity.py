@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 import oracle
-from conftest import GOLDEN
+from conftest import GOLDEN, set_form
 from shadow_amd import graphs
 from shadow_amd._lib import ALGO_DENSE_FW, ALGO_SPARSE_SSSP
 from shadow_amd.topology import Topology, build_tables
@@ -70,8 +70,8 @@ def test_c1_golden_through_gml(gpu):
                                           (ALGO_SPARSE_SSSP, "1")])
 def test_c2_complete_1000(gpu, monkeypatch, algo, square):
     """C2's full table; the dense build by min-plus squaring (its default at ld <= 2048, encoding
-    11) and by the 256-pivot FW rounds (SRT_FW_SQUARE=0)."""
-    monkeypatch.setenv("SRT_FW_SQUARE", square)
+    11) and by the 256-pivot FW rounds (SRT_FORM square=0)."""
+    set_form(monkeypatch, square=square)
     g = graphs.complete_graph(1000, seed=2)
     lat, rel, st = build_tables(g.n, False, g.src, g.dst, g.lat_ns, g.loss, algo=algo)
     exp = _oracle(g)
@@ -201,13 +201,12 @@ def test_dense_device_api_and_sharded_single_rank(gpu):
 
 
 @pytest.mark.parametrize("hop_ms,enc,sym,la,env", [
-    (1, 4, "1", None, {}), (1, 7, "1", "1", {}), (1, 6, "1", "1", {"SRT_FW_KB": "128"}),
-    (1, 5, "1", "1", {"SRT_FW_KB": "64"}),
-    (1, 5, "1", "1", {"SRT_FW_WAVES": "4"}), (1, 4, "1", None, {"SRT_FW_WAVES": "4"}),
-    (1, 3, "0", None, {}), (1, 3, "0", None, {"SRT_FW_WAVES": "4"}),
+    (1, 4, "1", None, {}), (1, 7, "1", "1", {}), (1, 6, "1", "1", {"kb": "128"}),
+    (1, 5, "1", "1", {"kb": "64"}),
+    (1, 3, "0", None, {}),
     (160, 2, "1", None, {}), (400, 1, "1", None, {}),
-    (1, 11, "1", None, {"SRT_FW_SQUARE": "1"}), (1, 11, "0", None, {"SRT_FW_SQUARE": "1"}),
-    (160, 2, "1", None, {"SRT_FW_SQUARE": "1"})])
+    (1, 11, "1", None, {"square": "1"}), (1, 11, "0", None, {"square": "1"}),
+    (160, 2, "1", None, {"square": "1"})])
 def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym, la, env):
     """Each distance encoding of the dense build (fw16.hip) is exact where it is chosen.
 
@@ -216,21 +215,17 @@ def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym, la, e
     0x3DFF), 160 saturates it and falls back to the u16 pk_min path (cap 0x7FFF), and 400
     saturates both and ends on the u32 kernels. Every tier must match the oracle bit for bit.
     The graph is undirected, so the f16-compare tier runs its upper-triangle form (encoding 4)
-    unless SRT_FW_SYM=0 forces every tile (encoding 3); SRT_FW_LOOKAHEAD=1 forces its two
+    unless SRT_FORM sym=0 forces every tile (encoding 3); lookahead=1 forces its two
     update streams, with 256-pivot rounds (encoding 7, the default from n = 8192), 128-pivot
-    rounds under SRT_FW_KB=128 (encoding 6) or 64-pivot rounds under SRT_FW_KB=64 (encoding 5).
-    SRT_FW_WAVES=4 selects the 4-wave update kernel
-    (fwh_update_kernel) over the 8-wave one (fwq_update_kernel). The round schedules are forced
-    with SRT_FW_SQUARE=0: by default a matrix of ld <= 2048 takes min-plus squaring to a fixed
+    rounds under kb=128 (encoding 6) or 64-pivot rounds under kb=64 (encoding 5). The round
+    schedules are forced with square=0: by default a matrix of ld <= 2048 takes min-plus squaring to a fixed
     point (encoding 11) -- on this ring, ~128-arc paths, so seven or more passes; at hop 160 the
     squaring saturates the f16-compare cap and the build falls back to the u16 rounds (2).
     """
-    monkeypatch.setenv("SRT_FW_SYM", sym)
-    monkeypatch.setenv("SRT_FW_SQUARE", "0")
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    set_form(monkeypatch, sym=sym, square="0")
+    set_form(monkeypatch, **env)
     if la is not None:
-        monkeypatch.setenv("SRT_FW_LOOKAHEAD", la)
+        set_form(monkeypatch, lookahead=la)
     n = 256
     rng = np.random.default_rng(hop_ms)
     src = list(range(n))
@@ -256,10 +251,10 @@ def test_dense_round_sizes_multi_round(gpu, monkeypatch, n, kb):
     """The two-stream schedules with several 256- / 128-pivot rounds (the encoding-tier test has
     one or two): a ring with chords, long enough for distances of a few hundred quanta, against
     the oracle bit for bit. Covers the chain stream's cross updates between a round's panels and
-    the rest launches that start past them (SRT_FW_SQUARE=0: not the small-matrix squaring)."""
-    monkeypatch.setenv("SRT_FW_SQUARE", "0")
-    monkeypatch.setenv("SRT_FW_LOOKAHEAD", "1")
-    monkeypatch.setenv("SRT_FW_KB", kb)
+    the rest launches that start past them (SRT_FORM square=0: not the small-matrix squaring)."""
+    set_form(monkeypatch, square="0")
+    set_form(monkeypatch, lookahead="1")
+    set_form(monkeypatch, kb=kb)
     rng = np.random.default_rng(n)
     src = list(range(n))
     dst = [(i + 1) % n for i in range(n)]
@@ -288,8 +283,8 @@ def test_dense_lookahead_schedule_one_gpu(gpu, monkeypatch, n, seed):
     on the high-priority stream, double-buffered receive panels)."""
     import torch
     from shadow_amd._lib import lib
-    monkeypatch.setenv("SRT_FW_SQUARE", "0")
-    monkeypatch.setenv("SRT_FW_LOOKAHEAD", "1")
+    set_form(monkeypatch, square="0")
+    set_form(monkeypatch, lookahead="1")
     ld = (n + 127) // 128 * 128
     L = lib()
     w = torch.empty((ld, ld), dtype=torch.int32, device="cuda")
@@ -412,13 +407,13 @@ def test_virtual_ranks_sharded_build(gpu, monkeypatch, kind, ranks):
 @pytest.mark.parametrize("ranks", [2, 3])
 @pytest.mark.parametrize("kb", ["64", "256"])
 def test_virtual_ranks_sharded_64_pivot_rounds(gpu, monkeypatch, kind, ranks, kb):
-    """SRT_FW_SH_KB=64 keeps the 64-pivot sharded symmetric rounds (encoding 4), =256 takes
+    """SRT_FORM shkb=64 keeps the 64-pivot sharded symmetric rounds (encoding 4), =256 takes
     256-pivot rounds (encoding 9: the band of tile rows 2j, 2j + 1 as four staged quarters, each
     closed quarter applied to the later ones): same tables. The graphs pad to ld = 768, 2048 and
     1024 (6, 16 and 8 tile rows); at 2 ranks of ld = 768 the band of tile rows 2 and 3 straddles
     the rank boundary (rows 0-383 | 384-767)."""
     monkeypatch.setenv("SRT_VIRTUAL_RANKS", str(ranks))
-    monkeypatch.setenv("SRT_FW_SH_KB", kb)
+    set_form(monkeypatch, shkb=kb)
     if kind == "dense":
         g = graphs.complete_graph(700, seed=9)
     elif kind == "dense2000":

@@ -1,7 +1,7 @@
 """Sparse SSSP through the device C-ABI (srt_sparse_graph_*) and the table builds, every kernel
 form: the wave-per-source bucket kernel (C3-shaped RGG), the workgroup-per-source kernel with the
 distance row packed in LDS (C5-shaped 100k-node Barabasi-Albert graph), and the block kernel
-(sparse.hip, SRT_SPARSE_WORKSET=hbm / bucket overflows).
+(sparse.hip, SRT_FORM hbm=1 / bucket overflows).
 
 Latency bit-exact in integer ns, reliability within 1e-12 relative (north_star). Every row is its
 own source's (no mirror), compared with oracle.sssp_rows / the oracle's raw table off the
@@ -9,6 +9,7 @@ diagonal.
 """
 import numpy as np
 import pytest
+from conftest import set_form
 
 import oracle
 from shadow_amd import graphs
@@ -23,7 +24,7 @@ REL_TOL = 1e-12
 def _single_source_kernels(monkeypatch):
     """These tests pin the single-source kernels; the multi-source kernel that AUTO gives local
     graphs (msssp.hip, dist_enc 3) has its own file, tests/test_gpu_msssp.py."""
-    monkeypatch.setenv("SRT_SPARSE_MS", "0")
+    set_form(monkeypatch, ms="0")
 
 
 def _rows_on_gpu(sg, s0, s1, torch, stats=None):
@@ -67,7 +68,7 @@ def test_c5_shape_ba_100000_workgroup_kernel_rows(gpu):
 
 @pytest.mark.parametrize("which", ["rgg3000", "ba2000", "directed"])
 def test_hbm_workset_forced_full_tables(gpu, monkeypatch, which):
-    monkeypatch.setenv("SRT_SPARSE_WORKSET", "hbm")
+    set_form(monkeypatch, hbm="1")
     if which == "rgg3000":
         g = graphs.random_geometric(3000, seed=3)
     elif which == "ba2000":
@@ -95,7 +96,7 @@ def test_hbm_workset_forced_full_tables(gpu, monkeypatch, which):
 def test_wave_kernel_bucket_overflow_fallback(gpu, monkeypatch, which, bcap):
     """Wave-per-source bucket kernel (wsssp.hip) with tiny bucket capacities: sources whose
     buckets overflow are recomputed by the workgroup kernel, and the table stays exact."""
-    monkeypatch.setenv("SRT_WSSSP_BCAP", bcap)
+    set_form(monkeypatch, bcap=bcap)
     if which == "rgg3000":
         g = graphs.random_geometric(3000, seed=3)
     else:
@@ -120,12 +121,12 @@ def test_wave_kernel_bucket_overflow_fallback(gpu, monkeypatch, which, bcap):
 
 def test_wave_kernel_matches_block_kernel_c3_rows(gpu, monkeypatch):
     """The two sparse kernels agree bit for bit on C3-shaped rows (the wave kernel is the default,
-    SRT_SPARSE_KERNEL=block selects the workgroup kernel)."""
+    SRT_FORM kernel=block selects the block kernel)."""
     import torch
     g = graphs.random_geometric(20000, seed=3)
     sg = SparseGraph(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
     a = _rows_on_gpu(sg, 5000, 5256, torch)
-    monkeypatch.setenv("SRT_SPARSE_KERNEL", "block")
+    set_form(monkeypatch, kernel="block")
     b = _rows_on_gpu(sg, 5000, 5256, torch)
     sg.free()
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
@@ -134,11 +135,10 @@ def test_wave_kernel_matches_block_kernel_c3_rows(gpu, monkeypatch):
 @pytest.mark.parametrize("which", ["rgg3000", "ba2000", "directed"])
 @pytest.mark.parametrize("lds,relrow", [("0", "0"), ("0", "1"), ("1", "0"), ("1", "1")])
 def test_wave_kernel_working_row_forms(gpu, monkeypatch, which, lds, relrow):
-    """SRT_WSSSP_LDS=0/1 (working distance row in global memory or in LDS) x SRT_WSSSP_RELROW=0/1
+    """SRT_FORM ws_lds=0/1 (working distance row in global memory or in LDS) x ws_relrow=0/1
     (reliability written to the output rows at settle time, or kept in a relabelled row and
     gathered at the end): every form gives the same exact tables."""
-    monkeypatch.setenv("SRT_WSSSP_LDS", lds)
-    monkeypatch.setenv("SRT_WSSSP_RELROW", relrow)
+    set_form(monkeypatch, ws_lds=lds, ws_relrow=relrow)
     if which == "rgg3000":
         g = graphs.random_geometric(3000, seed=3)
     elif which == "ba2000":
@@ -163,10 +163,10 @@ def test_wave_kernel_working_row_forms(gpu, monkeypatch, which, lds, relrow):
 
 @pytest.mark.parametrize("which", ["ba2000", "ba3000_w20", "rgg3000"])
 def test_workgroup_kernel_packed_rows(gpu, monkeypatch, which):
-    """SRT_SPARSE_WG=1: the workgroup-per-source kernel (distance row packed 3 x 10 bits in LDS)
+    """SRT_FORM kernel=wg: the workgroup-per-source kernel (distance row packed 3 x 10 bits in LDS)
     on any undirected graph whose probe source shows every distance fits (2 ecc <= 1022); else
     the wave kernel. Either way the exact tables."""
-    monkeypatch.setenv("SRT_SPARSE_WG", "1")
+    set_form(monkeypatch, kernel="wg")
     if which == "ba2000":
         g = graphs.barabasi_albert(2000, seed=5)
     elif which == "ba3000_w20":
@@ -187,8 +187,8 @@ def test_workgroup_kernel_packed_rows(gpu, monkeypatch, which):
 def test_workgroup_kernel_overflow_fallback(gpu, monkeypatch, bcap):
     """Forced bucket overflows in the workgroup kernel: flagged sources go to the wave kernel and,
     when that overflows too, to the block kernel; the tables stay exact."""
-    monkeypatch.setenv("SRT_SPARSE_WG", "1")
-    monkeypatch.setenv("SRT_WSSSP_BCAP", bcap)
+    set_form(monkeypatch, kernel="wg")
+    set_form(monkeypatch, bcap=bcap)
     g = graphs.barabasi_albert(1500, seed=6)
     lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
                                 algo=ALGO_SPARSE_SSSP)
@@ -198,16 +198,14 @@ def test_workgroup_kernel_overflow_fallback(gpu, monkeypatch, bcap):
     assert np.array_equal(rel, exp["rel"])
 
 
-@pytest.mark.parametrize("form", [{}, {"SRT_WG_COMPACT": "0"}, {"SRT_WG_ORDER": "cm"}])
+@pytest.mark.parametrize("form", [{}, {"wg_compact": "0"}, {"wg_order": "cm"}])
 @pytest.mark.parametrize("which", ["ba2000", "ba2500_many_losses"])
 def test_workgroup_kernel_forms(gpu, monkeypatch, form, which):
     """The workgroup kernel's forms give the same exact tables: original vertex order with compact
     8-byte arcs and the table of distinct reliabilities (default when the graph has <= 256 of
-    them), original order with 16-byte arcs (SRT_WG_COMPACT=0, or > 256 distinct losses), and the
-    Cuthill-McKee relabelling with a private reliability row (SRT_WG_ORDER=cm)."""
-    monkeypatch.setenv("SRT_SPARSE_WG", "1")
-    for k, v in form.items():
-        monkeypatch.setenv(k, v)
+    them), original order with 16-byte arcs (SRT_FORM wg_compact=0, or > 256 distinct losses),
+    and the Cuthill-McKee relabelling with a private reliability row (wg_order=cm)."""
+    set_form(monkeypatch, kernel="wg", **form)
     g = graphs.barabasi_albert(2000 if which == "ba2000" else 2500, seed=7)
     if which == "ba2500_many_losses":  # continuous losses: one distinct reliability per edge
         rng = np.random.default_rng(3)
@@ -224,12 +222,11 @@ def test_workgroup_kernel_forms(gpu, monkeypatch, form, which):
 @pytest.mark.parametrize("two", ["0", "1"])
 @pytest.mark.parametrize("lat_max", [1, 2, 20, 127])
 def test_workgroup_kernel_two_level_steps(gpu, monkeypatch, two, lat_max):
-    """SRT_WG_TWO: a Dial step of the workgroup kernel settles buckets d and d + 1 together (the
+    """SRT_FORM wg_two: a Dial step of the workgroup kernel settles buckets d and d + 1 together (the
     default) or bucket d alone. Weights of 1..2 quanta push into d + 1 during nearly every step
     (the consumed-prefix counts); 127 quanta is the largest compact-arc weight, where the bucket
     ring must hold max_w + 2 buckets. Both forms give the exact tables."""
-    monkeypatch.setenv("SRT_SPARSE_WG", "1")
-    monkeypatch.setenv("SRT_WG_TWO", two)
+    set_form(monkeypatch, kernel="wg", wg_two=two)
     g = graphs.barabasi_albert(2000, seed=9, lat_max=lat_max)
     lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
                                 algo=ALGO_SPARSE_SSSP)
@@ -240,17 +237,13 @@ def test_workgroup_kernel_two_level_steps(gpu, monkeypatch, two, lat_max):
     assert np.array_equal(rel, exp["rel"])
 
 
-@pytest.mark.parametrize("knobs", [{"SRT_WGSSSP_THREADS": "512"},
-                                   {"SRT_WGSSSP_PROF": "1"},
-                                   {"SRT_WGSSSP_PROF": "1", "SRT_WG_COMPACT": "0"},
-                                   {"SRT_WGSSSP_THREADS": "512", "SRT_WG_ORDER": "cm"}])
+@pytest.mark.parametrize("knobs", [{"prof": "1"}, {"prof": "1", "wg_compact": "0"},
+                                   {"wg_order": "cm"}, {"prof": "1", "wg_order": "cm"}])
 def test_workgroup_kernel_launch_knobs(gpu, monkeypatch, knobs):
-    """Every launch path of srt_wgsssp_rows once: the 512-thread form and the
-    per-phase profile form run on the original vertex order (ORIG, no inverse permutation) with
-    16-byte arcs, or on the Cuthill-McKee order; exact tables either way."""
-    monkeypatch.setenv("SRT_SPARSE_WG", "1")
-    for k, v in knobs.items():
-        monkeypatch.setenv(k, v)
+    """Every launch path of srt_wgsssp_rows once: the per-phase profile form and the
+    plain form on the original vertex order (ORIG, no inverse permutation) with 8- or 16-byte
+    arcs, or on the Cuthill-McKee order; exact tables either way."""
+    set_form(monkeypatch, kernel="wg", **knobs)
     g = graphs.barabasi_albert(1800, seed=10, lat_max=3)
     lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
                                 algo=ALGO_SPARSE_SSSP)
@@ -265,8 +258,8 @@ def test_workgroup_kernel_two_level_stress(gpu, monkeypatch):
     """Two-level Dial steps with weights of 1..2 quanta on many sources (the skipped
     buckets' reset raced the other waves' bucket search; it now follows the first chunk's scan
     barrier). A race shows up as wrong rows or a hang; the test runs under the suite timeout."""
-    monkeypatch.setenv("SRT_SPARSE_WG", "1")
-    monkeypatch.setenv("SRT_WG_TWO", "1")
+    set_form(monkeypatch, kernel="wg")
+    set_form(monkeypatch, wg_two="1")
     g = graphs.barabasi_albert(12000, seed=11, lat_max=2)
     lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
                                 algo=ALGO_SPARSE_SSSP)

@@ -1,5 +1,5 @@
 """Time the multi-source sparse kernel (msssp.hip) on a bench graph and print its per-batch
-profile (SRT_MSSSP_PROF=1 lines on stderr). python tools/msssp_probe.py c3 [--reps 2]"""
+profile (SRT_FORM prof=1: lines on stderr). python tools/msssp_probe.py c3 [--reps 2]"""
 import argparse
 import os
 import sys
@@ -32,6 +32,5 @@ for r in range(a.reps):
     torch.cuda.synchronize()
     print(f"{a.graph} rows 0..{ns}: {1e3 * (time.perf_counter() - t):.1f} ms wall, kernel "
           f"{st.ms_update:.1f} ms, dist_enc {st.dist_enc} "
-          f"env MS={os.environ.get('SRT_SPARSE_MS')} PROF={os.environ.get('SRT_MSSSP_PROF')} "
-          f"DELTA={os.environ.get('SRT_MSSSP_DELTA')}", flush=True)
+          f"SRT_FORM={os.environ.get('SRT_FORM')}", flush=True)
 sg.free()

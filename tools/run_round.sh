@@ -4,9 +4,11 @@
 # usage: bash tools/run_round.sh <tag> <step> [<step> ...]
 #   tests[:<pytest -k expr>]       the -m gpu suite (or a -k subset)
 #   tfile:<tests/file.py>[:<-k>]   one GPU test file
-#   bench:<wl>[:<steps>[:<VAR=val,VAR=val>]]   one bench.py line (c2 c3 c4 c5) -> bench_<wl>*.json
-#   prof:<wl>[:<VAR=val,...>]      rocprofv3 --kernel-trace --stats of a 3-step bench
-#   solo:<ranks>:<gbps list>[:<VAR=val,...>]   tools/solo_rank.py (one rank of N alone)
+#   bench:<wl>[:<steps>[:<settings>]]   one bench.py line (c2 c3 c4 c5) -> bench_<wl>*.json
+#   prof:<wl>[:<settings>]         rocprofv3 --kernel-trace --stats of a 3-step bench
+#   solo:<ranks>:<gbps list>[:<settings>]   tools/solo_rank.py (one rank of N alone)
+# <settings>: items joined by '+'; an UPPER-case key is an environment variable
+# (SRT_VIRTUAL_RANKS=4), a lower-case one an SRT_FORM key (levels=0+sym=0 -> SRT_FORM=levels=0,sym=0)
 #   py:<script>[:<args with , for spaces>]      python tools/<script>
 # Every step runs under its own timeout; the steps are chained with && (the first failure ends
 # the call). Output lands in gpurun_out/<tag>/.
@@ -18,8 +20,17 @@ mkdir -p $O
 export TMPDIR=/tmp
 PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
 
-envs() { # "A=1,B=2" -> env words
-    [ -n "$1" ] && echo "$1" | tr ',' ' '
+envs() { # "A=1+k=v+j=w" -> env words: A=1 SRT_FORM=k=v,j=w
+    [ -z "$1" ] && return 0
+    local form="" item
+    for item in $(echo "$1" | tr '+' ' '); do
+        case $item in
+        [A-Z]*) echo -n "$item " ;;
+        *) form="${form:+$form,}$item" ;;
+        esac
+    done
+    [ -n "$form" ] && echo -n "SRT_FORM=$form"
+    echo
 }
 
 run_step() {
@@ -41,12 +52,12 @@ run_step() {
         fi ;;
     bench)
         local st=${b:-5} sfx=""
-        [ -n "$c" ] && sfx="_$(echo $c | tr ',=' '__')"
+        [ -n "$c" ] && sfx="_$(echo $c | tr '+=' '__')"
         env $(envs "$c") timeout -k 10 600 python -u bench.py --workload $a --steps $st \
             --warmup 1 > $O/bench_$a$sfx.json 2> $O/bench_$a$sfx.err ;;
     prof)
         local sfx=""
-        [ -n "$b" ] && sfx="_$(echo $b | tr ',=' '__')"
+        [ -n "$b" ] && sfx="_$(echo $b | tr '+=' '__')"
         env $(envs "$b") timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
             -d $O/prof_$a$sfx -o run -- python3 bench.py --workload $a --steps 3 --warmup 1 \
             --no-cpu-baseline > $O/prof_$a$sfx.log 2>&1 ;;

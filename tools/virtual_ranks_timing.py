@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Schedule cost of the row-sharded dense paths on ONE GPU (virtual ranks, SRT_VIRTUAL_RANKS):
 the ranks share the device, so the build time is total work + schedule overhead. Compares the
-single-GPU build, the sharded all-tile rounds (SRT_FW_SYM=0) and the sharded symmetric rounds.
+single-GPU build, the sharded all-tile rounds (SRT_FORM sym=0) and the sharded symmetric rounds.
 usage: python tools/virtual_ranks_timing.py [n]"""
 import os
 import sys
@@ -17,10 +17,10 @@ from shadow_amd.topology import build_tables  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 g = graphs.complete_graph(n, seed=4, lat_max=1000)
 ref = None
-for label, env, ngpus in [("single", {}, None), ("virtual2 all-tile", {"SRT_VIRTUAL_RANKS": "2", "SRT_FW_SYM": "0"}, 1),
+for label, env, ngpus in [("single", {}, None), ("virtual2 all-tile", {"SRT_VIRTUAL_RANKS": "2", "SRT_FORM": "sym=0"}, 1),
                           ("virtual2 symmetric", {"SRT_VIRTUAL_RANKS": "2"}, 1),
                           ("virtual4 symmetric", {"SRT_VIRTUAL_RANKS": "4"}, 1)]:
-    for k in ("SRT_VIRTUAL_RANKS", "SRT_FW_SYM"):
+    for k in ("SRT_VIRTUAL_RANKS", "SRT_FORM"):
         os.environ.pop(k, None)
     os.environ.update(env)
     best = None

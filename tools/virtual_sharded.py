@@ -40,10 +40,10 @@ def main():
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     ap.add_argument("--ranks", type=int, default=2)
     ap.add_argument("--rows", type=int, default=3, help="sampled rows checked against the oracle")
-    ap.add_argument("--sym", default=None, help="SRT_FW_SYM override (0: all-tile rounds)")
+    ap.add_argument("--sym", default=None, help="SRT_FORM sym override (0: all-tile rounds)")
     a = ap.parse_args()
     if a.sym is not None:
-        os.environ["SRT_FW_SYM"] = a.sym
+        os.environ["SRT_FORM"] = f"sym={a.sym}"
     wl = WORKLOADS[a.workload]
     n, R = wl["n"], a.ranks
     L = _lib.lib()
