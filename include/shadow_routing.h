@@ -86,9 +86,9 @@ typedef struct srt_build_stats {
                           * 1 = wave-per-source kernel, 0 = workgroup kernel for every source.
                           * Dense: the distance encoding the build finished with: 12 = bit-parallel
                           * Dial levels (no FW rounds; levels.hip), 9 = 8 with
-                          * 256-pivot rounds (SRT_FW_SH_KB=256), 8 = u16
+                          * 256-pivot rounds (SRT_FORM shkb=256), 8 = u16
                           * f16-compare row-sharded symmetric rounds of 128 pivots (N > 1;
-                          * 4 with SRT_FW_SH_KB=64), 7 = 5 with
+                          * 4 with SRT_FORM shkb=64), 7 = 5 with
                           * 256-pivot rounds (four panels per C-tile residency), 6 = 5 with
                           * 128-pivot rounds (two panels per C-tile residency), 5 = 4 on two
                           * update streams (one GPU, n >= 8192), 4 = u16 with
@@ -169,7 +169,7 @@ int srt_gen_complete_device(int32_t n, int32_t ld, int32_t row0, int32_t nrows, 
  * stride n) with one workgroup per source. The per-source working set (distance row, frontier
  * queue, bitmaps: ~8n + n/8 bytes) is LDS-resident for n <= srt_sparse_max_n() and lives in a
  * per-workgroup HBM slot beyond (persistent grid of 2 workgroups per CU; environment variable
- * SRT_SPARSE_WORKSET=hbm forces the HBM form for testing). delta = bucket width in quanta
+ * SRT_FORM hbm=1 forces the HBM form for testing). delta = bucket width in quanta
  * (0 = default). Each row is its own source's (no symmetry rule is applied: see
  * srt_pair_order). */
 int srt_sparse_max_n(void);

@@ -539,7 +539,7 @@ static void ms_clusters(const srt_sparse_graph* g, const int32_t* rowof, int nsr
  * wave-per-source bucket kernel (wsssp.hip) when the arc weights fit its bucket ring, or the
  * workgroup kernel with the row packed in LDS on large power-law graphs; any source whose buckets
  * overflowed is recomputed (wave kernel, then the workgroup-per-source kernel of sparse.hip).
- * SRT_SPARSE_KERNEL=block (or SRT_SPARSE_WORKSET=hbm) selects the sparse.hip kernel for every
+ * SRT_FORM kernel=block (or SRT_FORM hbm=1) selects the sparse.hip kernel for every
  * source. lms (optional): the f64 path-order ms rows (tables.hip), q the quantum in ns. */
 static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src_end,
                        const int32_t* srcs, uint32_t* lat_rows, double* rel_rows, double* lms,
@@ -584,7 +584,7 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
     const bool block = srt_form_is("kernel", "block") || srt_form_int("hbm", 0) != 0;
     int rc = SRT_OK;
     /* the multi-source kernel (msssp.hip) where the relabelled graph is local (RGG-like, where
-     * the 64 frontiers of a source cluster overlap); SRT_SPARSE_MS=0/1 disables / forces it.
+     * the 64 frontiers of a source cluster overlap); SRT_FORM ms=0 / kernel=ms disables / forces it.
      * Sources are clustered here, on the host, before the timed span */
     const bool k_ms = srt_form_is("kernel", "ms"), k_wg = srt_form_is("kernel", "wg"),
                k_wave = srt_form_is("kernel", "wave");
@@ -601,7 +601,7 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
             if (s < 0 || s >= g->n || rowof[g->h_inv[s]] >= 0) ms = false; /* duplicates */
             else rowof[g->h_inv[s]] = i;
         }
-        /* SRT_MSSSP_RMAX: the hop radius of a cluster (tests force it to 0 / large) */
+        /* SRT_FORM ms_rmax: the hop radius of a cluster (tests force it to 0 / large) */
         const int rmax = srt_form_int("ms_rmax", 24);
         int cus = 256, dev = 0;
         hipDeviceProp_t prop;
@@ -692,7 +692,7 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
     SRT_HIPCHK(hipEventRecord(e0, st));
     /* large power-law graphs (relabelled arcs far apart): the workgroup kernel with the distance
      * row packed in LDS, once a probe source shows every distance fits its 10-bit fields
-     * (d(a, b) <= 2 ecc(s0)); SRT_SPARSE_WG=0/1 disables / allows it at any size */
+     * (d(a, b) <= 2 ecc(s0)); SRT_FORM wg=0 / kernel=wg disables / allows it at any size */
     int32_t* ms_dev = NULL; /* bsrc then brow, freed on the stream after the launch */
     int ms_d16 = 0;
     if (ms) {
@@ -742,7 +742,7 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
     bool wg = !ms && !g->directed && g->n <= srt_wgsssp_max_n() &&
               (k_wg || (!k_wave && srt_form_int("wg", 1) != 0 && g->n > 32768 && !g->local));
     /* the workgroup kernel keeps its row in LDS (any order serves), so it runs on the original
-     * vertex order and writes reliability straight into the output rows; SRT_WG_ORDER=cm runs it
+     * vertex order and writes reliability straight into the output rows; SRT_FORM wg_order=cm runs it
      * on the Cuthill-McKee relabelling with a private row gathered at the end */
     const bool wg_cm = srt_form_is("wg_order", "cm");
     const int2* wrp = wg_cm ? g->rp2 : g->rpo;
@@ -998,7 +998,7 @@ static int build_one(const srt_canon* c, const srt_build_opts* opts, int algo, i
         TRYHIP(hipMemcpyAsync(dr, hr, ll * sizeof(double), hipMemcpyHostToDevice, st));
         /* a few attached vertices: their rows alone (Bellman-Ford passes, ~6 nsub n^2 work)
          * instead of the all-pairs FW (n^3 / 2), as the reference computes paths from attached
-         * sources only (topology.c:1604-1656); SRT_DENSE_ROWS=0 keeps the FW */
+         * sources only (topology.c:1604-1656); SRT_FORM rows=0 keeps the FW */
         int rows_used = 0;
         if (use_sp && verts && (size_t)nsub * 12 <= (size_t)n && srt_form_int("rows", 1) != 0) {
             uint32_t* rl;

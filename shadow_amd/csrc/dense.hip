@@ -1006,6 +1006,188 @@ __global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
     if (tid == 0) atomicMax(max_depth, (int)mx);
 }
 
+/* The same level-order product with the row held on chip: rel_levels_kernel's passes touch the
+ * row's pred and rel lines once per level in scattered 4-8 B pieces (C4: ~2.4x the row bytes,
+ * 12.1 ms). Here every thread loads its PER targets (t = tid + i * NT) once, coalesced: the level
+ * byte and the arc reliability stay in registers, the predecessor goes to LDS as u16. Only the
+ * targets that are some target's predecessor ("parents": C4 rows have ~1-3k of 32k, the vertices
+ * at distance <= 2-3 quanta) get a value slot in LDS, found by a bitmap rank (word prefix +
+ * popcount). Pass L forms rel(s,t) = rel(s,u) * r(u,t) for the targets at distance L from the
+ * parents' slots and files the parents among them; the row is written once at the end. Rows with
+ * more parents than the cap slots (or a distance range beyond maxl) return untouched and flagged
+ * for rel_sweeps_kernel. Dynamic LDS: rel_tree_lds(NT, PER, cap). */
+static constexpr size_t rel_tree_lds(int nt, int per, int cap) {
+    return (size_t)8 * nt + (size_t)2 * nt * per + (size_t)8 * cap;
+}
+
+template <int NT, int PER>
+__global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
+                                                      const uint32_t* __restrict__ lat,
+                                                      const int32_t* __restrict__ pred,
+                                                      double* __restrict__ rel, int maxl, int cap,
+                                                      int32_t* __restrict__ max_depth,
+                                                      int32_t* __restrict__ sweep,
+                                                      const int32_t* __restrict__ srcs = nullptr) {
+    const int s = srcs ? srcs[blockIdx.x] : row0 + blockIdx.x; /* srcs: row i is source srcs[i] */
+    if (s >= n) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int nw = (n + 31) >> 5; /* <= NT (n <= 32 NT) */
+    extern __shared__ __attribute__((aligned(16))) uint32_t tsm[];
+    uint32_t* par = tsm;                                          /* parent bitmap, nw words */
+    uint32_t* pre = tsm + NT;                                     /* parents before each word */
+    uint16_t* spu = reinterpret_cast<uint16_t*>(tsm + 2 * NT);    /* predecessor per target */
+    double* slot = reinterpret_cast<double*>(spu + NT * PER);     /* cap parent values */
+    __shared__ uint32_t red[NT / 64], wsum[NT / 64];
+    for (int q = tid; q < nw; q += NT) par[q] = 0u;
+    const uint32_t* dl = lat + (size_t)blockIdx.x * ld;
+    const int32_t* pg = pred + (size_t)blockIdx.x * ld;
+    double* rr = rel + (size_t)blockIdx.x * ld;
+    const __amdgpu_buffer_rsrc_t rd =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(dl), 0, n * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rp =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(pg), 0, n * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv =
+        __builtin_amdgcn_make_buffer_rsrc(rr, 0, n * 8, 0x00020000);
+    uint32_t lv[PER / 4];
+    double x[PER];
+    uint32_t mx = 0;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        /* out of range reads 0 (the descriptors' bound): no level, like s and unreachable targets */
+        const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(rd, tid * 4, i * NT * 4, 2);
+        const uint32_t p = __builtin_amdgcn_raw_buffer_load_b32(rp, tid * 4, i * NT * 4, 2);
+        const uint32_t l = (tid + i * NT != s && d < SRT_INF) ? d : 0u;
+        mx = max(mx, l);
+        const uint32_t b = min(l, 255u) << (8 * (i & 3));
+        lv[i >> 2] = (i & 3) ? (lv[i >> 2] | b) : b;
+        spu[tid + i * NT] = (uint16_t)p; /* -1 -> 0xFFFF (n <= 32768) */
+    }
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    if (lane == 0) red[tid >> 6] = mx;
+    __syncthreads(); /* par zeroed, red */
+    mx = 0;
+    for (int i = 0; i < NT / 64; ++i) mx = max(mx, red[i]);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) { /* mark the parents */
+        const uint32_t l = (lv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+        const uint32_t u = spu[tid + i * NT];
+        if (l && u != 0xFFFFu && (int)u != s) atomicOr(&par[u >> 5], 1u << (u & 31));
+    }
+    __syncthreads();
+    /* exclusive prefix of the parent counts over the bitmap words (one word per thread) */
+    const uint32_t c = tid < nw ? (uint32_t)__popc(par[tid]) : 0u;
+    uint32_t inc = c;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) wsum[tid >> 6] = inc;
+    __syncthreads();
+    uint32_t base = 0, total = 0;
+    for (int i = 0; i < NT / 64; ++i) {
+        base += i < (tid >> 6) ? wsum[i] : 0u;
+        total += wsum[i];
+    }
+    if (tid < nw) pre[tid] = base + inc - c;
+    const bool bail = (int)mx > maxl || total > (uint32_t)cap;
+    if (tid == 0) sweep[blockIdx.x] = bail;
+    if (bail) return; /* uniform: rel_sweeps_kernel takes the row from its untouched input */
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const uint32_t v0 = __builtin_amdgcn_raw_buffer_load_b32(rv, tid * 8, i * NT * 8, 0);
+        const uint32_t v1 = __builtin_amdgcn_raw_buffer_load_b32(rv, tid * 8 + 4, i * NT * 8, 0);
+        x[i] = __hiloint2double((int)v1, (int)v0);
+    }
+    __syncthreads();
+    auto rank = [&](uint32_t u) {
+        return pre[u >> 5] + (uint32_t)__popc(par[u >> 5] & ((1u << (u & 31)) - 1u));
+    };
+    for (uint32_t L = 1; L <= mx; ++L) {
+        /* opaque per pass: keeps the compiler from hoisting the PER unpacked levels and target
+         * indices out of the loop (they would not fit beside x) */
+#pragma unroll
+        for (int k = 0; k < PER / 4; ++k) asm volatile("" : "+v"(lv[k]));
+        int tl = tid;
+        asm volatile("" : "+v"(tl));
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            if (((lv[i >> 2] >> (8 * (i & 3))) & 0xFFu) != L) continue;
+            const uint32_t t = (uint32_t)(tl + i * NT);
+            const uint32_t u = spu[t];
+            /* u == s: the direct arc (rel(s,s) = 1); u < 0 cannot happen on a validated graph
+             * and keeps the entry, as in rel_levels_kernel */
+            const double ru = (u == 0xFFFFu || (int)u == s) ? 1.0 : slot[rank(u)];
+            x[i] = ru * x[i];
+            if ((par[t >> 5] >> (t & 31)) & 1u) slot[rank(t)] = x[i];
+        }
+        __syncthreads();
+    }
+    int tw = tid;
+    asm volatile("" : "+v"(tw));
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int t = tw + i * NT;
+        if (t < n && ((lv[i >> 2] >> (8 * (i & 3))) & 0xFFu)) __builtin_nontemporal_store(x[i], rr + t);
+    }
+    if (tid == 0) {
+        rr[s] = 1.0;
+        atomicMax(max_depth, (int)mx);
+    }
+}
+
+/* Path-order reliability of lrows rows whose rel rows hold r(pred, t) (pred rows beside them):
+ * rel_tree_kernel for n <= 32768 (rel_levels_kernel past it, or under SRT_FORM reltree=0), then
+ * the sweeps for the rows it flagged. depth, sweep: device scratch (max depth, per-row flags). */
+static int rel_rows_launch(int n, int ld, int row0, int lrows, const uint32_t* d, int32_t* pred,
+                           double* rel, int32_t* depth, int32_t* sweep, const int32_t* srcs,
+                           hipStream_t st) {
+    if (lrows <= 0) return SRT_OK;
+    const bool tree = n <= 32768 && srt_form_int("reltree", 1) != 0;
+    if (tree && n <= 1024) {
+        rel_tree_kernel<256, 4><<<lrows, 256, rel_tree_lds(256, 4, 1024), st>>>(
+            n, ld, row0, d, pred, rel, 64, 1024, depth, sweep, srcs);
+    } else if (tree && n <= 4096) {
+        const int lds = (int)rel_tree_lds(512, 8, 4096);
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_tree_kernel<512, 8>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        rel_tree_kernel<512, 8><<<lrows, 512, lds, st>>>(n, ld, row0, d, pred, rel, 64, 4096, depth,
+                                                         sweep, srcs);
+    } else if (tree) {
+        /* 64 KB of predecessors and 7,168 parent slots (C4 rows have ~1-3k parents): 128 KB */
+        const int cap = 7168, lds = (int)rel_tree_lds(1024, 32, cap);
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_tree_kernel<1024, 32>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        rel_tree_kernel<1024, 32><<<lrows, 1024, lds, st>>>(n, ld, row0, d, pred, rel, 64, cap, depth,
+                                                            sweep, srcs);
+    } else if (n <= 1024) {
+        rel_levels_kernel<256, 1024><<<lrows, 256, 2048, st>>>(n, ld, row0, d, pred, rel, 64, depth,
+                                                              sweep, srcs);
+    } else if (n <= 4096) {
+        rel_levels_kernel<512, 4096><<<lrows, 512, 8192, st>>>(n, ld, row0, d, pred, rel, 64, depth,
+                                                              sweep, srcs);
+    } else if (n <= 32768) {
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 32768>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
+        rel_levels_kernel<1024, 32768><<<lrows, 1024, 65536, st>>>(n, ld, row0, d, pred, rel, 64,
+                                                                  depth, sweep, srcs);
+    } else {
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 65536>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
+        rel_levels_kernel<1024, 65536><<<lrows, 1024, 131072, st>>>(n, ld, row0, d, pred, rel, 64,
+                                                                  depth, sweep, srcs);
+    }
+    SRT_HIPCHK(hipGetLastError());
+    if (n <= 32768) {
+        const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        rel_sweeps_kernel<<<lrows, 512, lds, st>>>(n, ld, row0, pred, rel, depth, sweep, srcs);
+        SRT_HIPCHK(hipGetLastError());
+        return SRT_OK;
+    }
+    return srt_rel_sweeps_rows(n, lrows, row0, pred, (size_t)ld, rel, (size_t)ld, sweep, depth, st);
+}
+
 __global__ void pack_uw_kernel(int64_t arcs, const int32_t* __restrict__ col,
                                const uint32_t* __restrict__ w, uint2* __restrict__ uw,
                                const int32_t* __restrict__ dtotal) {
@@ -1316,40 +1498,9 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
             n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
         /* level order for rows whose distances span <= 64 quanta, sweeps for the rest
          * (ws->cursor is free here and carries the per-row hand-over flags) */
-        /* 1024 threads per row, one row per CU (128 VGPRs): 12.3 ms on C4 against 13.3 for 512
-         * threads at two rows per CU and 13.1 for 1024 at two (64 VGPRs, 4 targets in flight) */
-        if (n <= 32768) {
-            /* small rows take small workgroups (C2, n = 1,000: 256 threads of 4 entries, four
-             * rows per CU, instead of 1,024 threads that scan 32 mostly empty entries per level) */
-            if (n <= 1024)
-                rel_levels_kernel<256, 1024><<<lrows, 256, 2048, st>>>(n, ld, row0, d, pred, rel, 64,
-                                                                      ws->depth, ws->cursor);
-            else if (n <= 4096)
-                rel_levels_kernel<512, 4096><<<lrows, 512, 8192, st>>>(n, ld, row0, d, pred, rel, 64,
-                                                                      ws->depth, ws->cursor);
-            else {
-                SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 32768>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
-                rel_levels_kernel<1024, 32768><<<lrows, 1024, 65536, st>>>(
-                    n, ld, row0, d, pred, rel, 64, ws->depth, ws->cursor);
-            }
-            const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
-            SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            rel_sweeps_kernel<<<lrows, 512, lds, st>>>(n, ld, row0, pred, rel, ws->depth, ws->cursor);
-            SRT_HIPCHK(hipGetLastError());
-        } else {
-            /* n beyond 32768: 64 entries per thread (128 KB of per-wave target lists), and the
-             * flagged rows sweep with their predecessor rows in HBM (tables.hip) */
-            SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 65536>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
-            rel_levels_kernel<1024, 65536><<<lrows, 1024, 131072, st>>>(n, ld, row0, d, pred, rel, 64,
-                                                                      ws->depth, ws->cursor);
-            SRT_HIPCHK(hipGetLastError());
-            if ((rc = srt_rel_sweeps_rows(n, lrows, row0, pred, (size_t)ld, rel, (size_t)ld,
-                                          ws->cursor, ws->depth, st)))
-                return rc;
-        }
+        if ((rc = rel_rows_launch(n, ld, row0, lrows, d, pred, rel, ws->depth, ws->cursor, nullptr,
+                                  st)))
+            return rc;
     }
     if (stats && nowait) { /* read after the build's final wait (dense_collect_total) */
         if (!ws->h_total) SRT_HIPCHK(hipHostMalloc((void**)&ws->h_total, sizeof(int32_t)));
@@ -1387,34 +1538,9 @@ static int dense_post_levels(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
         SRT_HIPCHK(hipMemsetAsync(ws->depth, 0, sizeof(int32_t), st));
         /* every level-built distance is <= 254 quanta: level order in place for every row that
          * spans <= 64 quanta, sweeps for the rest (as dense_post) */
-        if (n <= 1024)
-            rel_levels_kernel<256, 1024><<<lrows, 256, 2048, st>>>(n, ld, row0, d, pred, rel, 64,
-                                                                  ws->depth, ws->cursor);
-        else if (n <= 4096)
-            rel_levels_kernel<512, 4096><<<lrows, 512, 8192, st>>>(n, ld, row0, d, pred, rel, 64,
-                                                                  ws->depth, ws->cursor);
-        else if (n <= 32768) {
-            SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 32768>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
-            rel_levels_kernel<1024, 32768><<<lrows, 1024, 65536, st>>>(n, ld, row0, d, pred, rel, 64,
-                                                                      ws->depth, ws->cursor);
-        } else {
-            SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 65536>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
-            rel_levels_kernel<1024, 65536><<<lrows, 1024, 131072, st>>>(n, ld, row0, d, pred, rel, 64,
-                                                                      ws->depth, ws->cursor);
-        }
-        SRT_HIPCHK(hipGetLastError());
-        if (n <= 32768) {
-            const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
-            SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            rel_sweeps_kernel<<<lrows, 512, lds, st>>>(n, ld, row0, pred, rel, ws->depth, ws->cursor);
-            SRT_HIPCHK(hipGetLastError());
-        } else if ((rc = srt_rel_sweeps_rows(n, lrows, row0, pred, (size_t)ld, rel, (size_t)ld,
-                                             ws->cursor, ws->depth, st))) {
+        if ((rc = rel_rows_launch(n, ld, row0, lrows, d, pred, rel, ws->depth, ws->cursor, nullptr,
+                                  st)))
             return rc;
-        }
     }
     srt_levels_release(st);
     if (stats) stats->ess_arcs = 0; /* no essential-arc lists in this form */
@@ -1672,14 +1798,8 @@ int srt_dense_rows_build_device(int32_t n, int32_t ld, int32_t nsub, const int32
         rows_pred_kernel<false><<<pg, 256, 0, st>>>(n, ld, nsub, dverts, dt, ptr, cand, r, pred,
                                                      rel_rows, ties);
     SRT_HIPCHK(hipGetLastError());
-    SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_levels_kernel<1024, 32768>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
-    rel_levels_kernel<1024, 32768><<<nsub, 1024, 65536, st>>>(n, ld, 0, lat_rows, pred, rel_rows, 64,
-                                                             depth, sweep, dverts);
-    const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
-    SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    rel_sweeps_kernel<<<nsub, 512, lds, st>>>(n, ld, 0, pred, rel_rows, depth, sweep, dverts);
+    if ((rc = rel_rows_launch(n, ld, 0, nsub, lat_rows, pred, rel_rows, depth, sweep, dverts, st)))
+        return rc;
     dense_diag_kernel<<<srt_ceil_div(nsub, 4), 256, 0, st>>>(n, ld, 0, nsub, w, r, lat_rows, rel_rows,
                                                              dverts);
     SRT_HIPCHK(hipGetLastError());
@@ -1775,7 +1895,7 @@ static int dense_path_ms(int32_t n, int32_t ld, int32_t row0, int32_t nrows, con
  * level budget to beat the FW's predicted time (61 T relaxations/s, the measured update rate;
  * symmetric rounds do half the relaxations, plus the rounds' chain). n >= 4,096: below that the
  * FW's squaring or rounds
- * cost less than the levels' launches. SRT_DENSE_LEVELS=0 keeps the FW, =1 tries the levels at any
+ * cost less than the levels' launches. SRT_FORM levels=0 keeps the FW, =1 tries the levels at any
  * size. *exact = 1 when the levels settled every pair (the u16 matrix and lat rows are final). */
 static int dense_try_levels(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
                             const uint32_t* w_rows, const double* r_rows, uint32_t* lat_rows,

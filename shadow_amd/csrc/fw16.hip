@@ -1182,7 +1182,7 @@ __global__ __launch_bounds__(256) void sym_fill_local_kernel(u16* __restrict__ D
  * update that last read it (round k-1) has finished.
  * Without a broadcast to hide (one GPU) the split and the cross-stream events cost more than the
  * overlap returns (C2: 1.01 -> 1.34 ms), so the single-GPU build runs the same rounds on one stream
- * in order; SRT_FW_LOOKAHEAD=1 forces the two-stream schedule (tests exercise it on one GPU). */
+ * in order; SRT_FORM lookahead=1 forces the two-stream schedule (tests exercise it on one GPU). */
 /* per-device u16 working matrix of the last build (rows of the shard, ld columns); the dense
  * post pass reads it transposed for the predecessor search (half the bytes of the u32 table) */
 static u16* fw16_bufs[SRT_STATE_SLOTS];
@@ -1581,7 +1581,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
     u16* grecv = NULL; /* staged panel blocks in (contributor, J) order (r128: rows a, then b) */
     int* cnt = (int*)calloc(2 * (size_t)R, sizeof(int)); /* per contributor (256: two tile rows) */
     const size_t blk = (size_t)KB * 128;
-    /* two-deep 128-pivot rounds (N > 1 default; SRT_FW_SH_DEEP=0: one-deep): band k + 3 is staged
+    /* two-deep 128-pivot rounds (N > 1 default; SRT_FORM deep=0: one-deep): band k + 3 is staged
      * and broadcast on its own stream right after round k's update, three rounds ahead, and each
      * rank applies the two panels it missed to the staged band itself (fwq_band_kernel) */
     const bool deep = r128 && R > 1 && T >= 2 && srt_form_int("deep", 1) != 0;
@@ -1829,7 +1829,7 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
         /* The next pivot row's cross runs on the chain stream (after both streams' rest of the
          * round before, whose tiles it follows), so the update streams run their rest launches
          * back to back instead of NR -> rest with two launch gaps a round: one rank of N = 8
-         * 49.2 -> 46.0 ms, N = 4 unchanged (83.5 ms). SRT_FW_SH_NRCS=0 keeps NR on the update
+         * 49.2 -> 46.0 ms, N = 4 unchanged (83.5 ms). (retired one-GPU NRCS form) keeps NR on the update
          * streams. */
         for (int k = 0; k < nb; ++k) {
             const int k0 = k * kbr;
@@ -2017,7 +2017,7 @@ int srt_fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0, in
                       "most %d tile columns", SYM_TMAX);
         return SRT_E_ARG;
     }
-    /* 128-pivot rounds with the 8-wave update; SRT_FW_SH_KB=64 selects 64-pivot rounds (a
+    /* 128-pivot rounds with the 8-wave update; SRT_FORM shkb=64 selects 64-pivot rounds (a
      * 256-pivot form measured slower at N = 8: 57.6 vs 45.9 ms for one rank) */
     const int rp = srt_form_int("shkb", 128) == 64 ? 64 : 128;
     g_sharded_rp = rp;
@@ -2062,7 +2062,7 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
         return SRT_E_ARG;
     }
     /* small matrices on one GPU (ld <= 2048, C2's 1,000 vertices): min-plus squaring to a fixed
-     * point instead of ld / 64 latency-bound FW rounds; SRT_FW_SQUARE=0 keeps the rounds */
+     * point instead of ld / 64 latency-bound FW rounds; SRT_FORM square=0 keeps the rounds */
     if (fm && !bcast && !owner_of && row0 == 0 && nrows == ld && ld <= 2048 &&
         srt_form_int("square", 1) != 0) {
         if (sym) *sym = 5;
@@ -2089,9 +2089,9 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
     if (sym) *sym = 0;
     if (want_sym && fm && !bcast && !owner_of && row0 == 0 && nrows == ld) {
         /* two update streams once the rounds are long enough to hide their event waits;
-         * SRT_FW_LOOKAHEAD=0/1 forces either form */
+         * SRT_FORM lookahead=0/1 forces either form */
         const bool two = la >= 0 ? la != 0 : ld >= 8192;
-        /* 128-pivot rounds on the two update streams (8-wave kernel; SRT_FW_KB=64 selects the
+        /* 128-pivot rounds on the two update streams (8-wave kernel; SRT_FORM kb=64 selects the
          * 64-pivot rounds). With the update's compute loop at ~85% of the issue model, the per-tile
          * C load, row sums, staging and store are what is left to amortize: C4 332.2 vs 344.1 ms
          * per build on one box (before that loop change the two measured the same, 380.5 vs

@@ -51,7 +51,7 @@
 #define MS_G 4       /* candidates a wave pulls together */
 #define MS_AC 16     /* arcs per candidate and chunk (MS_G x MS_AC lanes) */
 #define MS_AK 8      /* arcs per candidate whose distance rows are loaded together */
-#define MS_PROF 10   /* profile words per batch (SRT_MSSSP_PROF) */
+#define MS_PROF 10   /* profile words per batch (SRT_FORM prof) */
 
 static __device__ __forceinline__ uint32_t ms_ld(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
     double* const R = reinterpret_cast<double*>(wsb + (size_t)n * MS_L);
     uint32_t* const mind = wsb + (size_t)n * MS_L * 3;
 
-    /* PROF (SRT_MSSSP_PROF=1): per batch, passes, pulls, bucket advances, then the cycles of
+    /* PROF (SRT_FORM prof=1): per batch, passes, pulls, bucket advances, then the cycles of
      * wave 0 in the compaction, pull, advance, output and initialisation phases */
     unsigned long long pc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t0 = 0, rt0 = 0;
     auto tick = [&](int slot) {

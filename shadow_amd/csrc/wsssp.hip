@@ -476,7 +476,7 @@ __global__ void wg_arcs_cmp_kernel(int n, const int2* __restrict__ rowptr, const
     }
 }
 
-/* PROF (tools only, SRT_WGSSSP_PROF=1): thread 0 accumulates shader-clock cycles per phase and
+/* PROF (tools only, SRT_FORM prof=1): thread 0 accumulates shader-clock cycles per phase and
  * step counts into prof[block * 16 + k]: 0 init, 1 bucket search, 2 chunk head (sums and the
  * full barrier; 10 entry load, 11 scan barrier), 3 arcs (12 owner search, 13 arc-load wait, 14
  * relaxations; 3 itself: the deferred store and the post-arc barrier),
@@ -501,7 +501,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
     double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ ws, int nb, int bcap,
     int* __restrict__ overflow, unsigned long long* __restrict__ prof = nullptr, int two = 0) {
     /* CMP: cav holds the compact arcs and r the table of distinct reliabilities */
-    /* two (SRT_WG_TWO): a step settles the entries of buckets d and d + 1 present at its start.
+    /* two (SRT_FORM wg_two): a step settles the entries of buckets d and d + 1 present at its start.
      * An entry at d + 1 is final then (every unsettled vertex is at >= d and arcs are >= 1
      * quantum), and its tight predecessors are at <= d: settled, or level 0 of this step. The
      * level-0 entries come first in the step's index order; a chunk holding both levels stores its

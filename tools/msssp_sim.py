@@ -37,7 +37,8 @@ def csr(g):
     d = np.concatenate([g.dst[off], g.src[off]]) if not g.directed else g.dst[off]
     lat = np.concatenate([g.lat_ns[off], g.lat_ns[off]]) if not g.directed else g.lat_ns[off]
     loss = np.concatenate([g.loss[off], g.loss[off]]) if not g.directed else g.loss[off]
-    # canonical arc per ordered pair: (min latency, lowest edge index); r = 1 - (float)loss
+    # canonical arc per ordered pair: (min latency, lowest edge index); r = 1.0 - loss, a full
+    # double (no spare mantissa bits to carry other data)
     eidx = np.concatenate([np.nonzero(off)[0]] * (1 if g.directed else 2))
     o = np.lexsort((eidx, lat, d, s))
     s, d, lat, loss = s[o], d[o], lat[o], loss[o]
