@@ -1020,9 +1020,9 @@ static constexpr size_t rel_tree_lds(int nt, int per, int cap) {
     return (size_t)8 * nt + (size_t)2 * nt * per + (size_t)8 * cap;
 }
 
-template <int NT, int PER>
+template <int NT, int PER, typename LT>
 __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
-                                                      const uint32_t* __restrict__ lat,
+                                                      const LT* __restrict__ lat,
                                                       const int32_t* __restrict__ pred,
                                                       double* __restrict__ rel, int maxl, int cap,
                                                       int32_t* __restrict__ max_depth,
@@ -1039,11 +1039,11 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
     double* slot = reinterpret_cast<double*>(spu + NT * PER);     /* cap parent values */
     __shared__ uint32_t red[NT / 64], wsum[NT / 64];
     for (int q = tid; q < nw; q += NT) par[q] = 0u;
-    const uint32_t* dl = lat + (size_t)blockIdx.x * ld;
+    const LT* dl = lat + (size_t)blockIdx.x * ld;
     const int32_t* pg = pred + (size_t)blockIdx.x * ld;
     double* rr = rel + (size_t)blockIdx.x * ld;
-    const __amdgpu_buffer_rsrc_t rd =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(dl), 0, n * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<LT*>(dl), 0, n * (int)sizeof(LT), 0x00020000);
     const __amdgpu_buffer_rsrc_t rp =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(pg), 0, n * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rv =
@@ -1054,7 +1054,12 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
         /* out of range reads 0 (the descriptors' bound): no level, like s and unreachable targets */
-        const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(rd, tid * 4, i * NT * 4, 2);
+        /* u32 table rows (SRT_INF: unreachable) or a level build's u8 rows (0: s itself) */
+        uint32_t d;
+        if constexpr (sizeof(LT) == 1)
+            d = __builtin_amdgcn_raw_buffer_load_b8(rd, tid, i * NT, 2);
+        else
+            d = __builtin_amdgcn_raw_buffer_load_b32(rd, tid * 4, i * NT * 4, 2);
         const uint32_t p = __builtin_amdgcn_raw_buffer_load_b32(rp, tid * 4, i * NT * 4, 2);
         const uint32_t l = (tid + i * NT != s && d < SRT_INF) ? d : 0u;
         mx = max(mx, l);
@@ -1135,31 +1140,43 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
     }
 }
 
+/* rel_tree_kernel at the row's size class (n <= 32768) */
+template <typename LT>
+static void rel_tree_launch(int n, int ld, int row0, int lrows, const LT* d, int32_t* pred,
+                            double* rel, int32_t* depth, int32_t* sweep, const int32_t* srcs,
+                            hipStream_t st) {
+    if (n <= 1024) {
+        rel_tree_kernel<256, 4, LT><<<lrows, 256, rel_tree_lds(256, 4, 1024), st>>>(
+            n, ld, row0, d, pred, rel, 64, 1024, depth, sweep, srcs);
+    } else if (n <= 4096) {
+        const int lds = (int)rel_tree_lds(512, 8, 4096);
+        (void)hipFuncSetAttribute((const void*)rel_tree_kernel<512, 8, LT>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        rel_tree_kernel<512, 8, LT><<<lrows, 512, lds, st>>>(n, ld, row0, d, pred, rel, 64, 4096,
+                                                             depth, sweep, srcs);
+    } else {
+        /* 64 KB of predecessors and 7,168 parent slots (C4 rows have ~1-3k parents): 128 KB */
+        const int cap = 7168, lds = (int)rel_tree_lds(1024, 32, cap);
+        (void)hipFuncSetAttribute((const void*)rel_tree_kernel<1024, 32, LT>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        rel_tree_kernel<1024, 32, LT><<<lrows, 1024, lds, st>>>(n, ld, row0, d, pred, rel, 64, cap,
+                                                                depth, sweep, srcs);
+    }
+}
+
 /* Path-order reliability of lrows rows whose rel rows hold r(pred, t) (pred rows beside them):
  * rel_tree_kernel for n <= 32768 (rel_levels_kernel past it, or under SRT_FORM reltree=0), then
  * the sweeps for the rows it flagged. depth, sweep: device scratch (max depth, per-row flags). */
 static int rel_rows_launch(int n, int ld, int row0, int lrows, const uint32_t* d, int32_t* pred,
                            double* rel, int32_t* depth, int32_t* sweep, const int32_t* srcs,
-                           hipStream_t st) {
+                           hipStream_t st, const uint8_t* l8 = nullptr) {
     if (lrows <= 0) return SRT_OK;
     const bool tree = n <= 32768 && srt_form_int("reltree", 1) != 0;
-    if (tree && n <= 1024) {
-        rel_tree_kernel<256, 4><<<lrows, 256, rel_tree_lds(256, 4, 1024), st>>>(
-            n, ld, row0, d, pred, rel, 64, 1024, depth, sweep, srcs);
-    } else if (tree && n <= 4096) {
-        const int lds = (int)rel_tree_lds(512, 8, 4096);
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_tree_kernel<512, 8>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        rel_tree_kernel<512, 8><<<lrows, 512, lds, st>>>(n, ld, row0, d, pred, rel, 64, 4096, depth,
-                                                         sweep, srcs);
-    } else if (tree) {
-        /* 64 KB of predecessors and 7,168 parent slots (C4 rows have ~1-3k parents): 128 KB */
-        const int cap = 7168, lds = (int)rel_tree_lds(1024, 32, cap);
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_tree_kernel<1024, 32>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        rel_tree_kernel<1024, 32><<<lrows, 1024, lds, st>>>(n, ld, row0, d, pred, rel, 64, cap, depth,
-                                                            sweep, srcs);
-    } else if (n <= 1024) {
+    if (tree && l8)
+        rel_tree_launch(n, ld, row0, lrows, l8, pred, rel, depth, sweep, srcs, st);
+    else if (tree)
+        rel_tree_launch(n, ld, row0, lrows, d, pred, rel, depth, sweep, srcs, st);
+    else if (n <= 1024) {
         rel_levels_kernel<256, 1024><<<lrows, 256, 2048, st>>>(n, ld, row0, d, pred, rel, 64, depth,
                                                               sweep, srcs);
     } else if (n <= 4096) {
@@ -1537,9 +1554,9 @@ static int dense_post_levels(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
             n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
         SRT_HIPCHK(hipMemsetAsync(ws->depth, 0, sizeof(int32_t), st));
         /* every level-built distance is <= 254 quanta: level order in place for every row that
-         * spans <= 64 quanta, sweeps for the rest (as dense_post) */
+         * spans <= 64 quanta, sweeps for the rest (as dense_post); the level rows as u8 */
         if ((rc = rel_rows_launch(n, ld, row0, lrows, d, pred, rel, ws->depth, ws->cursor, nullptr,
-                                  st)))
+                                  st, srt_levels_l8())))
             return rc;
     }
     srt_levels_release(st);

@@ -2028,30 +2028,17 @@ int srt_fw16_sharded_round_pivots(void) { return g_sharded_rp; }
 static int fw16_square(int n, int ld, const uint32_t* w, uint32_t* lat, hipStream_t st,
                        evpool_t* evp, int* exact);
 
-/* Distances by bit-parallel Dial levels (levels.hip) straight into the u16 FW matrix of this slot
- * (0 on the diagonal, cap on padding) and the u32 rows -- exact and small by construction (the FW
- * finish pass's outputs and flags). *nlev = the level that settled every pair, or 0 when the levels do not
- * apply or miss their budget -- the caller then runs the FW. */
+/* Distances by bit-parallel Dial levels (levels.hip) into the u32 rows (and the level build's own
+ * u8 rows) -- exact and small by construction. *nlev = the level that settled every pair, or 0
+ * when the levels do not apply or miss their budget -- the caller then runs the FW. */
 int srt_fw16_levels(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
                     const uint32_t* w_rows, const double* r_rows, uint32_t* lat_rows,
                     hipStream_t st, evpool_t* evp, double fw_ms, int* nlev, int64_t* bytes) {
     *nlev = 0;
     *bytes = 0;
-    const int dev = srt_state_slot();
-    const size_t need = (size_t)nrows * ld + 2 * (size_t)KB * ld;
-    if (fw16_caps[dev] < need || !fw16_bufs[dev]) {
-        if (fw16_bufs[dev]) SRT_HIPCHK(hipFree(fw16_bufs[dev]));
-        fw16_bufs[dev] = NULL;
-        fw16_caps[dev] = 0;
-        SRT_HIPCHK(hipMalloc(&fw16_bufs[dev], need * sizeof(u16)));
-        fw16_caps[dev] = need;
-    }
-    if (!fw16_flags[dev]) SRT_HIPCHK(hipMalloc(&fw16_flags[dev], 2 * sizeof(int)));
-    int rc = srt_levels_build(comm, n, ld, row0, nrows, directed, w_rows, r_rows, fw16_bufs[dev],
-                              lat_rows, CAP_F, fw_ms, st, evp, nlev, bytes);
-    if (rc || !*nlev) return rc;
-    fw16_small[dev] = 1; /* every settled distance is <= the level budget (<= 254 quanta) */
-    return SRT_OK;
+    /* the level post pass reads the build's own u8 rows, not the u16 FW matrix: none written */
+    return srt_levels_build(comm, n, ld, row0, nrows, directed, w_rows, r_rows, NULL, lat_rows, CAP_F,
+                            fw_ms, st, evp, nlev, bytes);
 }
 
 int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,

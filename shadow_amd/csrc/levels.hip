@@ -250,17 +250,19 @@ __global__ __launch_bounds__(256) void lvl_step_kernel(int d, int n, int nw, int
                       incomplete);
 }
 
-/* Distance rows of the local sources from the levels, in the FW matrix layout (u16, row stride
- * ld: 0 on the diagonal, cap on padding) and as the u32 table rows (SRT_INF on padding) -- the FW
- * finish pass folded in: every settled distance is <= the level budget (<= 254), so the rows are
- * exact and small by construction. Thread = four consecutive targets t0..t0 + 3 (256 threads = 1,024
+/* Distance rows of the local sources from the levels: the u32 table rows (SRT_INF on padding) and
+ * the u8 level rows the reliability pass reads (0 on the diagonal and padding) -- the FW finish
+ * pass folded in: every settled distance is <= the level budget (<= 254), so the rows are exact
+ * and small by construction -- and, when d16 is given, the FW matrix layout (u16, 0 on the
+ * diagonal, cap on padding). Thread = four consecutive targets t0..t0 + 3 (256 threads = 1,024
  * targets per workgroup), looping over 16 source words: per word it reads the four targets' word
- * of every level (the same lines for the 16 words of a workgroup row) and writes 8 B of u16 and
- * 16 B of u32 per source row. */
+ * of every level (the same lines for the 16 words of a workgroup row) and writes 16 B of u32 and
+ * 4 B of u8 per source row. */
 __global__ __launch_bounds__(256) void lvl_out_kernel(int n, int ld, int nw, int src0, int nlev,
                                                       const uint32_t* __restrict__ lev,
                                                       uint16_t* __restrict__ d16,
-                                                      uint32_t* __restrict__ lat, uint32_t cap) {
+                                                      uint32_t* __restrict__ lat,
+                                                      uint8_t* __restrict__ l8, uint32_t cap) {
     const int t0 = (blockIdx.x * 256 + threadIdx.x) * 4;
     if (t0 >= ld) return;
     const size_t plane = (size_t)n * nw;
@@ -293,11 +295,16 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(int n, int ld, int nw, int
 #pragma unroll
         for (int s = 0; s < 32; ++s) {
             const size_t o = (size_t)(sw * 32 + s) * ld + t0;
-            *reinterpret_cast<uint2*>(d16 + o) = make_uint2(v[s][0], v[s][1]);
+            if (d16) *reinterpret_cast<uint2*>(d16 + o) = make_uint2(v[s][0], v[s][1]);
             uint32_t x[4] = {v[s][0] & 0xFFFFu, v[s][0] >> 16, v[s][1] & 0xFFFFu, v[s][1] >> 16};
+            uint32_t b = 0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) x[q] = x[q] == cap ? SRT_INF : x[q];
+            for (int q = 0; q < 4; ++q) {
+                b |= (x[q] == cap ? 0u : x[q]) << (8 * q);
+                x[q] = x[q] == cap ? SRT_INF : x[q];
+            }
             *reinterpret_cast<uint4*>(lat + o) = make_uint4(x[0], x[1], x[2], x[3]);
+            *reinterpret_cast<uint32_t*>(l8 + o) = b;
         }
     }
 }
@@ -502,7 +509,8 @@ typedef struct {
     uint32_t* aoff;
     double* ar;
     uint32_t* lev;
-    void* p[16];
+    uint8_t* l8; /* u8 distance rows (nrows x ld) for the reliability pass */
+    void* p[20];
     int k;
     hipStream_t st;
 } lvl_state;
@@ -515,6 +523,11 @@ static void lvl_free(lvl_state* L, hipStream_t st) {
 }
 
 void srt_levels_release(hipStream_t st) { lvl_free(&g_lvl[srt_state_slot()], st); }
+
+const uint8_t* srt_levels_l8(void) {
+    const lvl_state* L = &g_lvl[srt_state_slot()];
+    return L->held ? L->l8 : NULL;
+}
 
 #define LVL_ALLOC(ptr, bytes)                                      \
     do {                                                           \
@@ -694,8 +707,10 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         SRT_HIPCHK(hipStreamSynchronize(st));
     }
     if (!ok) return SRT_OK;
+    uint8_t* l8 = NULL;
+    LVL_ALLOC(l8, (size_t)nrows * ld);
     lvl_out_kernel<<<dim3(srt_ceil_div(ld, 1024), srt_ceil_div(nw, 16)), 256, 0, st>>>(
-        n, ld, nw, row0, D, lev, d16, lat_rows, cap);
+        n, ld, nw, row0, D, lev, d16, lat_rows, l8, cap);
     SRT_HIPCHK(hipGetLastError());
     *levels = D;
     *gather_bytes = gathered;
@@ -712,6 +727,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     L->aoff = aoff;
     L->ar = ar;
     L->lev = lev;
+    L->l8 = l8;
     return SRT_OK;
 }
 

@@ -153,7 +153,8 @@ int srt_fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0, in
 int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,
                    hipStream_t st, evpool_t* evp, srt_owner_fn owner_of, srt_panel_bcast_fn bcast,
                    void* ctx, int rank, int fm, int* sym, int* exact);
-/* levels.hip: u16 distance rows of the local sources by bit-parallel Dial levels (see there) */
+/* levels.hip: distance rows of the local sources by bit-parallel Dial levels (see there); d16
+ * (the FW matrix layout) may be NULL */
 int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
                      const uint32_t* w_rows, const double* r_rows, uint16_t* d16,
                      uint32_t* lat_rows, uint32_t cap, double fw_ms, hipStream_t st, evpool_t* evp,
@@ -163,6 +164,8 @@ int srt_levels_pred(int32_t* predT, double* rT, size_t ldp, unsigned long long* 
                     hipStream_t st);
 /* frees the held level build (stream-ordered) */
 void srt_levels_release(hipStream_t st);
+/* the held build's u8 distance rows (nrows x ld, 0 on the diagonal), NULL if none */
+const uint8_t* srt_levels_l8(void);
 /* the same into this slot's FW matrix + the finish pass (fw16.hip); *nlev = 0: FW instead */
 int srt_fw16_levels(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
                     const uint32_t* w_rows, const double* r_rows, uint32_t* lat_rows,
