@@ -1097,6 +1097,10 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
     const bool bail = (int)mx > maxl || total > (uint32_t)cap;
     if (tid == 0) sweep[blockIdx.x] = bail;
     if (bail) return; /* uniform: rel_sweeps_kernel takes the row from its untouched input */
+    if (mx == 0) { /* no reachable target: only rel(s, s) */
+        if (tid == 0) rr[s] = 1.0;
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
         const uint32_t v0 = __builtin_amdgcn_raw_buffer_load_b32(rv, tid * 8, i * NT * 8, 0);
@@ -1107,7 +1111,8 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
     auto rank = [&](uint32_t u) {
         return pre[u >> 5] + (uint32_t)__popc(par[u >> 5] & ((1u << (u & 31)) - 1u));
     };
-    for (uint32_t L = 1; L <= mx; ++L) {
+    uint32_t L = 1;
+    do { /* passes 1..mx (mx >= 1: one pass at least, so x needs no second copy for a skip) */
         /* opaque per pass: keeps the compiler from hoisting the PER unpacked levels and target
          * indices out of the loop (they would not fit beside x) */
 #pragma unroll
@@ -1126,7 +1131,7 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
             if ((par[t >> 5] >> (t & 31)) & 1u) slot[rank(t)] = x[i];
         }
         __syncthreads();
-    }
+    } while (++L <= mx);
     int tw = tid;
     asm volatile("" : "+v"(tw));
 #pragma unroll
