@@ -1,8 +1,9 @@
 """C4 at full size in -m gpu: the 32,768-node complete graph through the default one-GPU schedule
-(encoding 7: u16 f16-compare upper-triangle 256-pivot rounds on two update streams, the 8-wave
-update kernel, XCD-remapped grid, u8 predecessor slab, rel_levels_kernel<1024>), against the CPU
-oracle's dense Dijkstra (oracle.complete_sample) on rows spread over every 4k block, including the
-last tile row.
+(encoding 12: distances by bit-parallel Dial levels, predecessors from the level planes, the
+reliability rows on chip in rel_tree_kernel) and through the Floyd-Warshall schedule (SRT_FORM
+levels=0, encoding 7: u16 f16-compare upper-triangle 256-pivot rounds on two update streams),
+against the CPU oracle's dense Dijkstra (oracle.complete_sample) on rows spread over every 4k
+block, including the last tile row.
 
 Latency bit-exact in integer ns; reliability within 1e-12 relative (north_star) on every entry off
 the diagonal: each row is its own source's row (no mirror; the lookup layer serves a pair from the

@@ -480,3 +480,31 @@ def test_packet_path_trace_replay(gpu):
     # single-packet form agrees with the trace form
     ok, d = top.send_packet(src[0], dst[0], chance[0], bool(boot[0]), int(payload[0]))
     assert ok == bool(want[0]) and (not ok or d == want_delay[0])
+
+
+@pytest.mark.parametrize("reltree", ["1", "0"])
+def test_reliability_parent_slots_overflow(gpu, monkeypatch, reltree):
+    """rel_tree_kernel keeps the values of a row's parents (targets that are some target's
+    predecessor) in 7,168 LDS slots for n > 4,096. A comb -- 120 chains of 60 one-ms hops from
+    vertex 0, each ending in a leaf -- gives row 0 7,200 parents (distances <= 61): that row must
+    hand over to the sweeps untouched, the others (distances past 64) take the sweeps anyway.
+    SRT_FORM reltree=0 runs the per-level kernel instead; both exact."""
+    set_form(monkeypatch, reltree=reltree, levels="0")
+    chains, depth = 120, 60
+    src, dst = [], []
+    v = 1
+    for _ in range(chains):
+        prev = 0
+        for _ in range(depth + 1):
+            src.append(prev)
+            dst.append(v)
+            prev = v
+            v += 1
+    n = v
+    rng = np.random.default_rng(21)
+    g = graphs.Graph(n, False, np.array(src, np.int32), np.array(dst, np.int32),
+                     np.full(len(src), MS, np.int64), rng.integers(0, 200, len(src)) * 1e-4)
+    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                algo=ALGO_DENSE_FW)
+    exp = _oracle(g)
+    assert_tables(lat, rel, exp["lat_int"], exp["rel"], f"comb reltree={reltree}")
