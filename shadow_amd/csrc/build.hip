@@ -129,7 +129,15 @@ struct srt_sparse_graph {
     int32_t ck_n, ck_b0, ck_list, ck_rmax, ck_maxb, ck_nb, ck_nrest;
     int32_t *ck_srcs, *ck_bsrc, *ck_brow, *ck_rest;
     pthread_mutex_t ck_mu; /* all-zero (calloc) is the default mutex */
+    /* neighbour-row derivation (derive.hip, undirected): an independent set I of vertices of
+     * degree <= DERIVE_MAXDEG and the rest ("core"), both ascending; crow[v] = v's index in the
+     * core list (-1 for I) */
+    int32_t nI, ncore;
+    int32_t *dI, *dcore, *crow;
+    int32_t ntab; /* entries of rtab */
 };
+
+#define DERIVE_MAXDEG 4 /* <= derive.hip's DV_MAXDEG */
 
 int srt_wgsssp_max_n(void);
 int srt_wide_rows(int n, const int32_t* rp, const int32_t* col, const uint32_t* w, const double* r,
@@ -140,7 +148,11 @@ int srt_wide_rows(int n, const int32_t* rp, const int32_t* col, const uint32_t* 
 int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r, const int32_t* inv,
                     uint32_t max_w, int src_begin, int src_end, const int32_t* srcs, uint32_t* lat,
                     double* rel, int* ovf, hipStream_t st, const uint8_t* ridx,
-                    const double* rtab);
+                    const double* rtab, int place = 0, uint32_t* codes = nullptr);
+int srt_derive_rows(int n, int nI, const int32_t* I, int src_begin, const int2* rowptr,
+                    const uint2* cw, const uint8_t* ridx, const double* rtab, int ntab,
+                    const int32_t* crow, const uint32_t* codes, uint32_t* lat, double* rel,
+                    size_t ldo, hipStream_t st);
 int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, const double* r,
                    const int2* in_rowptr, const uint2* in_cw, const double* in_r,
                    const int32_t* perm, const int32_t* inv, uint32_t max_w, int local,
@@ -171,7 +183,7 @@ extern "C" void srt_sparse_graph_free(srt_sparse_graph* g) {
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(g->device);
     void* ps[] = {g->rp, g->col, g->w, g->r, g->sw, g->sr, g->cw, g->perm, g->inv, g->rp2, g->cw2, g->r2,
-                  g->rpo, g->rtab, g->ridx};
+                  g->rpo, g->rtab, g->ridx, g->dI, g->dcore, g->crow};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (g->directed) {
@@ -254,6 +266,41 @@ static void relabel_csr(int n, const int32_t* rp, const int32_t* col, const uint
         }
         rp2[i] = make_int2(b, o);
     }
+}
+
+/* The independent set of the neighbour-row derivation: vertices of degree 1..DERIVE_MAXDEG taken
+ * greedily in (degree, index) order, each blocking its neighbours (on a BA graph with m = 3 every
+ * degree-3 vertex: they are never adjacent). Undirected graphs only. */
+static int derive_sets(const srt_canon* c, srt_sparse_graph* g) {
+    const int n = c->n;
+    std::vector<int32_t> order((size_t)n), I, core;
+    std::vector<uint8_t> blocked((size_t)n, 0), inI((size_t)n, 0);
+    for (int v = 0; v < n; v++) order[v] = v;
+    auto deg = [&](int v) { return c->rowptr[v + 1] - c->rowptr[v]; };
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return deg(a) < deg(b); });
+    for (int v : order) {
+        const int d = deg(v);
+        if (d > DERIVE_MAXDEG) break;
+        if (d < 1 || blocked[v]) continue;
+        inI[v] = 1;
+        blocked[v] = 1;
+        for (int k = c->rowptr[v]; k < c->rowptr[v + 1]; k++) blocked[c->col[k]] = 1;
+    }
+    std::vector<int32_t> crow((size_t)n, -1);
+    for (int v = 0; v < n; v++) {
+        if (inI[v]) {
+            I.push_back(v);
+        } else {
+            crow[v] = (int32_t)core.size();
+            core.push_back(v);
+        }
+    }
+    g->nI = (int32_t)I.size();
+    g->ncore = (int32_t)core.size();
+    int rc = up((void**)&g->dI, I.data(), I.size() * 4);
+    if (!rc) rc = up((void**)&g->dcore, core.data(), core.size() * 4);
+    if (!rc) rc = up((void**)&g->crow, crow.data(), (size_t)n * 4);
+    return rc;
 }
 
 static int sparse_graph_from_canon(const srt_canon* c, int device, srt_sparse_graph** out) {
@@ -339,6 +386,7 @@ static int sparse_graph_from_canon(const srt_canon* c, int device, srt_sparse_gr
                         idx[k] = (uint8_t)(std::lower_bound(tab, tab + nt, c->r[k]) - tab);
                     rc = up((void**)&g->rtab, tab, nt * sizeof(double));
                     if (!rc) rc = up((void**)&g->ridx, idx, na);
+                    g->ntab = (int32_t)nt;
                 }
             }
             free(tab);
@@ -373,6 +421,7 @@ static int sparse_graph_from_canon(const srt_canon* c, int device, srt_sparse_gr
         g->irp2 = g->rp2;
         g->icw2 = g->cw2;
         g->ir2 = g->r2;
+        rc = derive_sets(c, g);
     }
     free(hperm);
     free(hinv);
@@ -541,6 +590,34 @@ static void ms_clusters(const srt_sparse_graph* g, const int32_t* rowof, int nsr
  * overflowed is recomputed (wave kernel, then the workgroup-per-source kernel of sparse.hip).
  * SRT_FORM kernel=block (or SRT_FORM hbm=1) selects the sparse.hip kernel for every
  * source. lms (optional): the f64 path-order ms rows (tables.hip), q the quantum in ns. */
+/* Every row of an undirected graph, placed by source (row v = v): the core rows by the workgroup
+ * kernel, with their canonical arcs, then the independent set's rows by derivation (derive.hip).
+ * A core source whose buckets overflowed has no codes: then the set's rows take the kernel too. */
+static int sparse_rows_derived(const srt_sparse_graph* g, uint32_t* lat_rows, double* rel_rows,
+                               int* ovf, hipStream_t st) {
+    const int n = g->n;
+    uint32_t* codes = NULL;
+    SRT_HIPCHK(srt_malloc_async(&codes, (size_t)g->ncore * n * sizeof(uint32_t), st));
+    SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)n * sizeof(int), st));
+    int rc = srt_wgsssp_rows(n, g->rpo, g->cw, g->r, NULL, g->max_w, 0, g->ncore, g->dcore, lat_rows,
+                             rel_rows, ovf, st, g->ridx, g->rtab, 1, codes);
+    std::vector<int> hov((size_t)n);
+    if (!rc && hipMemcpyAsync(hov.data(), ovf, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, st) !=
+                   hipSuccess)
+        rc = SRT_E_DEVICE;
+    if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = SRT_E_DEVICE;
+    bool core_ovf = false;
+    for (int v = 0; v < n && !rc; v++) core_ovf |= hov[v] != 0;
+    if (!rc && core_ovf) /* (the set's flags are still 0: every flag is a core row's) */
+        rc = srt_wgsssp_rows(n, g->rpo, g->cw, g->r, NULL, g->max_w, 0, g->nI, g->dI, lat_rows,
+                             rel_rows, ovf, st, g->ridx, g->rtab, 1, NULL);
+    else if (!rc)
+        rc = srt_derive_rows(n, g->nI, g->dI, 0, g->rpo, g->cw, g->ridx, g->rtab, g->ntab, g->crow,
+                             codes, lat_rows, rel_rows, (size_t)n, st);
+    (void)hipFreeAsync(codes, st);
+    return rc;
+}
+
 static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src_end,
                        const int32_t* srcs, uint32_t* lat_rows, double* rel_rows, double* lms,
                        hipStream_t st, srt_build_stats* stats, int allow_ms = 1) {
@@ -739,6 +816,7 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
             if (rc) return rc;
         }
     }
+    bool derived = false;
     bool wg = !ms && !g->directed && g->n <= srt_wgsssp_max_n() &&
               (k_wg || (!k_wave && srt_form_int("wg", 1) != 0 && g->n > 32768 && !g->local));
     /* the workgroup kernel keeps its row in LDS (any order serves), so it runs on the original
@@ -764,7 +842,15 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
         for (int32_t i = 0; i < g->n; i++)
             if (row[i] != SRT_INF && row[i] > ecc) ecc = row[i];
         wg = !pov && 2ull * ecc <= 1022ull;
-        if (wg && nsrc > 1)
+        /* every row of the graph in one call (the full table): the core rows by the kernel with
+         * their canonical arcs, the independent set's rows derived from them (derive.hip;
+         * SRT_FORM derive=0 keeps the kernel for every row) */
+        derived = wg && !srcs && b0 == 0 && nsrc == g->n && !wg_cm && g->nI > 0 && g->ridx &&
+                  g->rtab && g->max_w < 128 && g->arcs < (1 << 20) &&
+                  srt_form_int("wg_compact", 1) != 0 && srt_form_int("derive", 1) != 0;
+        if (derived)
+            rc = sparse_rows_derived(g, lat_rows, rel_rows, ovf, st);
+        else if (wg && nsrc > 1)
             rc = srt_wgsssp_rows(g->n, wrp, wcw, wr, winv, g->max_w, b0 + 1, b0 + nsrc,
                                  one(1), lat_rows + (size_t)g->n, rel_rows + (size_t)g->n, ovf + 1,
                                  st, g->ridx, g->rtab);
@@ -776,7 +862,7 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
                             rel_rows, ovf, st);
     if (rc) return rc;
     /* the multi-source kernel's form: 8, | 16 with 16-bit working distances */
-    const int form = ms ? 8 | (ms_d16 ? 16 : 0) : srt_sparse_last_form();
+    const int form = ms ? 8 | (ms_d16 ? 16 : 0) : srt_sparse_last_form() | (derived ? 64 : 0);
     SRT_HIPCHK(hipEventRecord(e1, st));
     rc = srt_sparse_diag(g->n, b0, b0 + nsrc, srcs, g->rp, g->col, g->w, g->r, g->sw, g->sr,
                          lat_rows, rel_rows, (size_t)g->n, st);

@@ -436,6 +436,13 @@ static __device__ __forceinline__ bool wg_lower(uint32_t* sd, uint32_t v, uint32
         __builtin_amdgcn_s_barrier();                                   \
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); \
     } while (0)
+/* the canonical in-arc of a vertex settled at distance dl from its compact-arc key (D[u] << 40 |
+ * u << 8 | ridx): u | w << 17 | ridx << 24, w = dl - D[u] < 128; ~0 for the source */
+static __device__ __forceinline__ uint32_t wg_code(unsigned long long key, bool src, uint32_t dl) {
+    if (src || key == ~0ull) return ~0u;
+    const uint32_t du = (uint32_t)(key >> 40), u = (uint32_t)(key >> 8) & 0x1FFFFu;
+    return u | ((dl - du) << 17) | ((uint32_t)(key & 0xFFu) << 24);
+}
 static __device__ __forceinline__ uint2 wg_entry(uint32_t v, uint32_t beg, uint32_t deg) {
     return make_uint2(v | (min(deg, WG_DEGC) << 17), beg);
 }
@@ -499,7 +506,12 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
     const int2* __restrict__ rowptr, const void* __restrict__ cav,
     const double* __restrict__ r, const int32_t* __restrict__ inv, uint32_t* __restrict__ lat,
     double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ ws, int nb, int bcap,
-    int* __restrict__ overflow, unsigned long long* __restrict__ prof = nullptr, int two = 0) {
+    int* __restrict__ overflow, unsigned long long* __restrict__ prof = nullptr, int two = 0,
+    int place = 0, uint32_t* __restrict__ codes = nullptr) {
+    /* place: source s0 = srcs[si] writes output row (and overflow flag) s0 - src_begin instead of
+     * si. codes (CMP only): the canonical in-arc of every settled vertex v, row si (stride n):
+     * u | w << 17 | ridx << 24 (~0 for the source) -- the neighbour-row derivation's input
+     * (derive.hip) */
     /* CMP: cav holds the compact arcs and r the table of distinct reliabilities */
     /* two (SRT_FORM wg_two): a step settles the entries of buckets d and d + 1 present at its start.
      * An entry at d + 1 is final then (every unsettled vertex is at >= d and arcs are >= 1
@@ -531,8 +543,10 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
     for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
         const int s0 = srcs ? srcs[si] : src_begin + si;
         const int s = ORIG ? s0 : inv[s0];
-        uint32_t* ol = lat + (size_t)si * ldo;
-        double* rr = rel + (size_t)si * ldo;
+        const int orow = place ? s0 - src_begin : si;
+        uint32_t* ol = lat + (size_t)orow * ldo;
+        double* rr = rel + (size_t)orow * ldo;
+        uint32_t* cd = CMP && codes ? codes + (size_t)si * n : nullptr;
         if (ORIG) relp = rr;
         for (int q = tid; q < words; q += WG) sd[q] = 0x3FFFFFFFu; /* three unreached fields */
         /* ORIG: the output row is written at settle time; unreached entries get their 0 at the
@@ -789,6 +803,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                 if (mixed) {
                     if (v >= 0 && !lvl) {
                         double xa = 1.0, xb = 1.0;
+                        if (cd) cd[v] = wg_code(s_best[tid], v == s, dl);
                         if (v != s) {
                             const unsigned long long key = s_best[tid];
                             xa = 0.0;
@@ -811,6 +826,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                 /* settle: path-order reliability from the canonical predecessor, issued now and
                  * stored one chunk later */
                 if (v >= 0) {
+                    if (cd) cd[v] = wg_code(s_best[tid], v == s, dl);
                     pv = v;
                     pa = 1.0;
                     pb = 1.0;
@@ -846,7 +862,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
             else if (dv == WG_INF)
                 rr[i] = 0.0; /* unreached */
         }
-        if (s_ovf && tid == 0) overflow[si] = 1;
+        if (s_ovf && tid == 0) overflow[orow] = 1;
         __syncthreads();
         WG_PT(5);
     }
@@ -863,7 +879,7 @@ int srt_wgsssp_max_n(void) { return 3 * ((137 * 1024) / 4); }
 int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r, const int32_t* inv,
                     uint32_t max_w, int src_begin, int src_end, const int32_t* srcs, uint32_t* lat,
                     double* rel, int* ovf, hipStream_t st, const uint8_t* ridx,
-                    const double* rtab) {
+                    const double* rtab, int place, uint32_t* codes) {
     /* two-level steps push up to d + 1 + max_w: the ring then needs max_w + 2 buckets */
     int two = srt_form_int("wg_two", 1) != 0; /* tests: one-level steps */
     if (max_w + 2u > 256u) two = 0;
@@ -889,6 +905,10 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     const bool cmp = !inv && ridx && rtab && max_w < 128 && last.y < (1 << 20) &&
                      srt_form_int("wg_compact", 1) != 0; /* tests: the 16-byte arcs */
     g_sparse_form = 4 | (inv ? 0 : 1) | (cmp ? 2 : 0);
+    if (codes && !cmp) {
+        srt_set_error("wgsssp: arc codes need the compact-arc form");
+        return SRT_E_ARG;
+    }
     void* ca = NULL;
     const size_t arc_bytes = cmp ? sizeof(uint2) : sizeof(uint4);
     if (srt_malloc_async(&ca, ((size_t)last.y + 1) * arc_bytes, st) != hipSuccess) {
@@ -912,7 +932,8 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
         srt_set_error("wgsssp: workspace of %zu MiB failed", (slots * slot_words * 4) >> 20);
         return SRT_E_NOMEM;
     }
-    SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)nsrc * sizeof(int), st));
+    /* placed rows flag overflows at their row: the caller clears the flags */
+    if (!place) SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)nsrc * sizeof(int), st));
     const size_t dyn = (size_t)((n + 2) / 3) * sizeof(uint32_t);
     if (srt_form_int("prof", 0) > 0) { /* tools: per-phase cycle counts on stderr */
         unsigned long long* prof = NULL;
@@ -922,19 +943,19 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
             wgsssp_kernel<1024, true, true, true><<<(unsigned)slots, 1024, dyn, st>>>(
                 n, src_begin, srcs, nsrc, rowptr, ca, rtab, inv, lat, rel, (size_t)n, ws, nb, bcap,
-                ovf, prof, two);
+                ovf, prof, two, place, codes);
         } else if (!inv) { /* original order: the output row is the working row */
             SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true, true>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
             wgsssp_kernel<1024, true, true><<<(unsigned)slots, 1024, dyn, st>>>(
                 n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap,
-                ovf, prof, two);
+                ovf, prof, two, place, codes);
         } else {
             SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
             wgsssp_kernel<1024, true><<<(unsigned)slots, 1024, dyn, st>>>(
                 n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap,
-                ovf, prof, two);
+                ovf, prof, two, place, codes);
         }
         SRT_HIPCHK(hipGetLastError());
         unsigned long long* h = (unsigned long long*)calloc(slots * 16, sizeof(*h));
@@ -966,19 +987,19 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
         wgsssp_kernel<1024, false, true, true><<<(unsigned)slots, 1024, dyn, st>>>(
             n, src_begin, srcs, nsrc, rowptr, ca, rtab, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf,
-            nullptr, two);
+            nullptr, two, place, codes);
     } else if (!inv) { /* the graph in original order: reliability straight into the output rows */
         SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, false, true>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
         wgsssp_kernel<1024, false, true><<<(unsigned)slots, 1024, dyn, st>>>(
             n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf,
-            nullptr, two);
+            nullptr, two, place, codes);
     } else {
         SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
         wgsssp_kernel<1024><<<(unsigned)slots, 1024, dyn, st>>>(n, src_begin, srcs, nsrc, rowptr, ca, r,
                                                                inv, lat, rel, (size_t)n, ws, nb, bcap,
-                                                               ovf, nullptr, two);
+                                                               ovf, nullptr, two, place, codes);
     }
     SRT_HIPCHK(hipGetLastError());
     SRT_HIPCHK(hipFreeAsync(ws, st));
