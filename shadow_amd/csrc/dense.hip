@@ -1388,13 +1388,14 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
         return SRT_E_RANGE;
     }
     if ((rc = grow_arcs(ws, (size_t)total + 1))) return rc;
-    if (lrows > 0)
+    if (lrows > 0) {
         if (ess16)
             ess_fill_kernel<uint16_t><<<lrows, 256, 0, st>>>(n, ld, row0, w, r, d16, ws->ptr,
                                                              ws->col, ws->aw, ws->ar);
         else
             ess_fill_kernel<uint32_t><<<lrows, 256, 0, st>>>(n, ld, row0, w, r, d, ws->ptr,
                                                              ws->col, ws->aw, ws->ar);
+    }
     SRT_HIPCHK(hipGetLastError());
     if (gather && (rc = gather(gctx, ws, n, 1, total, st))) return rc; /* share the arcs */
     const int32_t *iptr = ws->ptr, *icol = ws->col;
@@ -1549,12 +1550,19 @@ static int dense_post_levels(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
         ws->rt_cap = c4;
         const bool ties = stats && stats->count_ties;
         if (ties) SRT_HIPCHK(hipMemsetAsync(ws->ties, 0, sizeof(unsigned long long), st));
-        if ((rc = srt_levels_pred(ws->predt, ws->rt, (size_t)nrows, ties ? ws->ties : NULL, st)))
+        /* int16 predecessors while every vertex fits (half the slab's bytes), widened by the
+         * transpose into the int32 rows the reliability passes read */
+        const int p16 = n <= 32768;
+        if ((rc = srt_levels_pred(ws->predt, p16, ws->rt, (size_t)nrows, ties ? ws->ties : NULL, st)))
             return rc;
         int32_t* pred = reinterpret_cast<int32_t*>(ws->dt);
-        transpose_kernel<uint32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
-            n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows,
-            reinterpret_cast<uint32_t*>(pred), (size_t)ld);
+        if (p16)
+            transpose_kernel<int16_t, int32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+                n, nrows, reinterpret_cast<const int16_t*>(ws->predt), (size_t)nrows, pred, (size_t)ld);
+        else
+            transpose_kernel<uint32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+                n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows,
+                reinterpret_cast<uint32_t*>(pred), (size_t)ld);
         transpose_kernel<double><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
             n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
         SRT_HIPCHK(hipMemsetAsync(ws->depth, 0, sizeof(int32_t), st));

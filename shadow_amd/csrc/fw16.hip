@@ -45,15 +45,13 @@ typedef u16 u16x2 __attribute__((ext_vector_type(2)));
 
 static __device__ __forceinline__ u16x2 as2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
 static __device__ __forceinline__ uint32_t as32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
-/* a, b halves <= 0x7FFF: the 32-bit add is two independent 16-bit adds */
-static __device__ __forceinline__ u16x2 relax(u16x2 acc, uint32_t a2, uint32_t b2) {
-    return __builtin_elementwise_min(acc, as2(a2 + b2));
-}
 static __device__ __forceinline__ uint32_t splat(uint32_t h) { return h | (h << 16); }
 /* per half: min(acc, x, y) on u16 bit patterns in [0, 0x7BFF] -> one v_pk_minimum3_f16.
  * Inline asm: written with the generic minimum builtins, LLVM re-associates the chain across
  * pivot pairs into two-input minimum3s with a duplicated operand (1.5x the min instructions). */
-static __device__ __forceinline__ uint32_t min3h(uint32_t acc, uint32_t x, uint32_t y) {
+/* (the FWQ_ROWS_FORM 0 instruction mix of the A/B builds in tools/) */
+__attribute__((unused)) static __device__ __forceinline__ uint32_t min3h(uint32_t acc, uint32_t x,
+                                                                         uint32_t y) {
     uint32_t r;
     asm("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(acc), "v"(x), "v"(y));
     return r;

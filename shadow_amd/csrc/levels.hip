@@ -325,6 +325,7 @@ __global__ void lvl_segs_kernel(int ld, const int32_t* __restrict__ off, int32_t
  * hit by two arcs of its winning weight is a tied pair (srt_build_stats.tied_pairs). A level stops
  * as soon as every source of the wave has its arc. Outputs, target-major as pred_cols*_kernel's
  * (stride ldp): predT[t][sl] = u (-1 on the diagonal), rT[t][sl] = r(u, t). */
+template <typename PT>
 static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx)[64 * 40], int n,
                                                      int nw, int nchunk, int src0, int nsrc, int nlev,
                                                        const int32_t* __restrict__ off,
@@ -332,7 +333,7 @@ static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx
                                                        const uint32_t* __restrict__ aoff,
                                                        const double* __restrict__ ar,
                                                        const uint32_t* __restrict__ lev,
-                                                       int32_t* __restrict__ predT,
+                                                       PT* __restrict__ predT,
                                                        double* __restrict__ rT, size_t ldp,
                                                        unsigned long long* __restrict__ ties) {
     const int tgrp = (n + 3) >> 2;
@@ -423,16 +424,22 @@ static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx
         pv[e] = h ? (int)(arcs[k] & 0xFFFFu) : -1;
         rv[e] = h ? ar[k] : 0.0;
     }
-    int32_t* pp = predT + (size_t)t * ldp + sl0;
+    PT* pp = predT + (size_t)t * ldp + sl0;
     double* rp = rT + (size_t)t * ldp + sl0;
 #pragma unroll
     for (int q = 0; q < 32; q += 4) {
-        *reinterpret_cast<int4*>(pp + q) = make_int4(pv[q], pv[q + 1], pv[q + 2], pv[q + 3]);
+        if constexpr (sizeof(PT) == 2) /* -1 -> 0xFFFF, read back as int16 -1 */
+            *reinterpret_cast<uint2*>(pp + q) =
+                make_uint2(((uint32_t)pv[q] & 0xFFFFu) | ((uint32_t)pv[q + 1] << 16),
+                           ((uint32_t)pv[q + 2] & 0xFFFFu) | ((uint32_t)pv[q + 3] << 16));
+        else
+            *reinterpret_cast<int4*>(pp + q) = make_int4(pv[q], pv[q + 1], pv[q + 2], pv[q + 3]);
         *reinterpret_cast<double2*>(rp + q) = make_double2(rv[q], rv[q + 1]);
         *reinterpret_cast<double2*>(rp + q + 2) = make_double2(rv[q + 2], rv[q + 3]);
     }
 }
 
+template <typename PT>
 __global__ __launch_bounds__(256) void lvl_pred_kernel(int n, int nw, int nchunk, int src0, int nsrc,
                                                        int nlev, unsigned nblk,
                                                        const int32_t* __restrict__ off,
@@ -440,7 +447,7 @@ __global__ __launch_bounds__(256) void lvl_pred_kernel(int n, int nw, int nchunk
                                                        const uint32_t* __restrict__ aoff,
                                                        const double* __restrict__ ar,
                                                        const uint32_t* __restrict__ lev,
-                                                       int32_t* __restrict__ predT,
+                                                       PT* __restrict__ predT,
                                                        double* __restrict__ rT, size_t ldp,
                                                        unsigned long long* __restrict__ ties) {
     /* per wave and lane: the winning arc of each of its 32 sources (index into t's arcs), 40 u16
@@ -448,8 +455,8 @@ __global__ __launch_bounds__(256) void lvl_pred_kernel(int n, int nw, int nchunk
     __shared__ __attribute__((aligned(16))) uint16_t sidx[4][64 * 40];
     const unsigned x = blockIdx.x & 7u, per = nblk >> 3, L = gridDim.x >> 3;
     for (unsigned u = blockIdx.x >> 3; u < per; u += L)
-        lvl_pred_unit(x * per + u, sidx, n, nw, nchunk, src0, nsrc, nlev, off, arcs, aoff, ar, lev,
-                      predT, rT, ldp, ties);
+        lvl_pred_unit<PT>(x * per + u, sidx, n, nw, nchunk, src0, nsrc, nlev, off, arcs, aoff, ar,
+                          lev, predT, rT, ldp, ties);
 }
 
 __global__ void lvl_sum_kernel(const unsigned long long* __restrict__ v, int k,
@@ -733,8 +740,9 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
 
 /* Canonical predecessors and their arc reliabilities of the held level build, target-major
  * (predT[t][sl], rT[t][sl], row stride ldp), as pred_cols*_kernel leave them for the transposes
- * and the reliability passes; ties != NULL adds the tied pairs. */
-int srt_levels_pred(int32_t* predT, double* rT, size_t ldp, unsigned long long* ties,
+ * and the reliability passes; ties != NULL adds the tied pairs. pred16: predT holds int16 (n <=
+ * 32768: half the bytes of the predecessor slab and its transpose), else int32. */
+int srt_levels_pred(void* predT, int pred16, double* rT, size_t ldp, unsigned long long* ties,
                     hipStream_t st) {
     lvl_state* L = &g_lvl[srt_state_slot()];
     if (!L->held) {
@@ -746,9 +754,18 @@ int srt_levels_pred(int32_t* predT, double* rT, size_t ldp, unsigned long long* 
         SRT_HIPCHK(srt_malloc_async(&part, 1024 * sizeof(unsigned long long), st));
         SRT_HIPCHK(hipMemsetAsync(part, 0, 1024 * sizeof(unsigned long long), st));
     }
-    lvl_pred_kernel<<<lvl_grid((const void*)lvl_pred_kernel, L->nblk), 256, 0, st>>>(L->n, L->nw, L->nchunk, L->row0, L->nrows, L->D,
-                                             L->nblk, L->off, L->arcs, L->aoff, L->ar, L->lev, predT, rT,
-                                             ldp, part);
+    if (pred16 && L->n > 32768) {
+        srt_set_error("levels: int16 predecessors need n <= 32768 (n = %d)", L->n);
+        return SRT_E_ARG;
+    }
+    if (pred16)
+        lvl_pred_kernel<int16_t><<<lvl_grid((const void*)lvl_pred_kernel<int16_t>, L->nblk), 256, 0, st>>>(
+            L->n, L->nw, L->nchunk, L->row0, L->nrows, L->D, L->nblk, L->off, L->arcs, L->aoff, L->ar,
+            L->lev, (int16_t*)predT, rT, ldp, part);
+    else
+        lvl_pred_kernel<int32_t><<<lvl_grid((const void*)lvl_pred_kernel<int32_t>, L->nblk), 256, 0, st>>>(
+            L->n, L->nw, L->nchunk, L->row0, L->nrows, L->D, L->nblk, L->off, L->arcs, L->aoff, L->ar,
+            L->lev, (int32_t*)predT, rT, ldp, part);
     SRT_HIPCHK(hipGetLastError());
     if (ties) {
         lvl_sum_kernel<<<1, 1024, 0, st>>>(part, 1024, ties);

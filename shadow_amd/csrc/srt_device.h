@@ -159,8 +159,9 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
                      const uint32_t* w_rows, const double* r_rows, uint16_t* d16,
                      uint32_t* lat_rows, uint32_t cap, double fw_ms, hipStream_t st, evpool_t* evp,
                      int* levels, int64_t* gather_bytes);
-/* predecessors + arc reliabilities of the held level build (target-major, row stride ldp) */
-int srt_levels_pred(int32_t* predT, double* rT, size_t ldp, unsigned long long* ties,
+/* predecessors (int16 when pred16, else int32) + arc reliabilities of the held level build
+ * (target-major, row stride ldp) */
+int srt_levels_pred(void* predT, int pred16, double* rT, size_t ldp, unsigned long long* ties,
                     hipStream_t st);
 /* frees the held level build (stream-ordered) */
 void srt_levels_release(hipStream_t st);
