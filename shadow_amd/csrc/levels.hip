@@ -401,41 +401,46 @@ static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx
         if (lane == 0 && tied) atomicAdd(&ties[blockIdx.x & 1023u], (unsigned long long)tied);
     }
     if (!valid) return;
-    /* 32 entries per lane: the indices back from LDS, every arc and reliability gather issued
-     * before the first is used, then 128 B of predecessors and 256 B of reliabilities */
-    uint32_t ix[16];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint4 v = *reinterpret_cast<const uint4*>(my + 8 * q);
-        ix[4 * q] = v.x;
-        ix[4 * q + 1] = v.y;
-        ix[4 * q + 2] = v.z;
-        ix[4 * q + 3] = v.w;
-    }
+    /* 32 entries per lane in two halves of 16 (the output registers of all 32 held the kernel
+     * to 4 waves per SIMD): the indices back from LDS, every arc and reliability gather of the
+     * half issued before the first is used, then 32 (64) B of predecessors and 128 B of
+     * reliabilities */
     const int sl0 = word * 32;
-    int32_t pv[32];
-    double rv[32];
 #pragma unroll
-    for (int e = 0; e < 32; ++e) {
-        const uint32_t x = (ix[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
-        const int sl = sl0 + e, sg = src0 + sl;
-        const bool h = sl < nsrc && sg < n && sg != t && x != 0xFFFFu;
-        const int k = a_t + (h ? (int)x : 0);
-        pv[e] = h ? (int)(arcs[k] & 0xFFFFu) : -1;
-        rv[e] = h ? ar[k] : 0.0;
-    }
-    PT* pp = predT + (size_t)t * ldp + sl0;
-    double* rp = rT + (size_t)t * ldp + sl0;
+    for (int hf = 0; hf < 2; ++hf) {
+        uint32_t ix[8];
 #pragma unroll
-    for (int q = 0; q < 32; q += 4) {
-        if constexpr (sizeof(PT) == 2) /* -1 -> 0xFFFF, read back as int16 -1 */
-            *reinterpret_cast<uint2*>(pp + q) =
-                make_uint2(((uint32_t)pv[q] & 0xFFFFu) | ((uint32_t)pv[q + 1] << 16),
-                           ((uint32_t)pv[q + 2] & 0xFFFFu) | ((uint32_t)pv[q + 3] << 16));
-        else
-            *reinterpret_cast<int4*>(pp + q) = make_int4(pv[q], pv[q + 1], pv[q + 2], pv[q + 3]);
-        *reinterpret_cast<double2*>(rp + q) = make_double2(rv[q], rv[q + 1]);
-        *reinterpret_cast<double2*>(rp + q + 2) = make_double2(rv[q + 2], rv[q + 3]);
+        for (int q = 0; q < 2; ++q) {
+            const uint4 v = *reinterpret_cast<const uint4*>(my + 16 * hf + 8 * q);
+            ix[4 * q] = v.x;
+            ix[4 * q + 1] = v.y;
+            ix[4 * q + 2] = v.z;
+            ix[4 * q + 3] = v.w;
+        }
+        int32_t pv[16];
+        double rv[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const uint32_t x = (ix[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+            const int sl = sl0 + 16 * hf + e, sg = src0 + sl;
+            const bool h = sl < nsrc && sg < n && sg != t && x != 0xFFFFu;
+            const int k = a_t + (h ? (int)x : 0);
+            pv[e] = h ? (int)(arcs[k] & 0xFFFFu) : -1;
+            rv[e] = h ? ar[k] : 0.0;
+        }
+        PT* pp = predT + (size_t)t * ldp + sl0 + 16 * hf;
+        double* rp = rT + (size_t)t * ldp + sl0 + 16 * hf;
+#pragma unroll
+        for (int q = 0; q < 16; q += 4) {
+            if constexpr (sizeof(PT) == 2) /* -1 -> 0xFFFF, read back as int16 -1 */
+                *reinterpret_cast<uint2*>(pp + q) =
+                    make_uint2(((uint32_t)pv[q] & 0xFFFFu) | ((uint32_t)pv[q + 1] << 16),
+                               ((uint32_t)pv[q + 2] & 0xFFFFu) | ((uint32_t)pv[q + 3] << 16));
+            else
+                *reinterpret_cast<int4*>(pp + q) = make_int4(pv[q], pv[q + 1], pv[q + 2], pv[q + 3]);
+            *reinterpret_cast<double2*>(rp + q) = make_double2(rv[q], rv[q + 1]);
+            *reinterpret_cast<double2*>(rp + q + 2) = make_double2(rv[q + 2], rv[q + 3]);
+        }
     }
 }
 
