@@ -405,13 +405,12 @@ def test_virtual_ranks_sharded_build(gpu, monkeypatch, kind, ranks):
 
 @pytest.mark.parametrize("kind", ["dense", "dense2000", "ring_f16"])
 @pytest.mark.parametrize("ranks", [2, 3])
-@pytest.mark.parametrize("kb", ["64", "256"])
+@pytest.mark.parametrize("kb", ["64", "128"])
 def test_virtual_ranks_sharded_64_pivot_rounds(gpu, monkeypatch, kind, ranks, kb):
-    """SRT_FORM shkb=64 keeps the 64-pivot sharded symmetric rounds (encoding 4), =256 takes
-    256-pivot rounds (encoding 9: the band of tile rows 2j, 2j + 1 as four staged quarters, each
-    closed quarter applied to the later ones): same tables. The graphs pad to ld = 768, 2048 and
-    1024 (6, 16 and 8 tile rows); at 2 ranks of ld = 768 the band of tile rows 2 and 3 straddles
-    the rank boundary (rows 0-383 | 384-767)."""
+    """SRT_FORM shkb=64 keeps the 64-pivot sharded symmetric rounds (encoding 4); the default
+    takes 128-pivot rounds (encoding 8; the 256-pivot form, encoding 9, measured slower and was
+    retired in round 4): same tables. The graphs pad to ld = 768, 2048 and 1024 (6, 16 and 8 tile
+    rows); at 2 ranks of ld = 768 a band straddles the rank boundary (rows 0-383 | 384-767)."""
     monkeypatch.setenv("SRT_VIRTUAL_RANKS", str(ranks))
     set_form(monkeypatch, shkb=kb)
     if kind == "dense":
@@ -424,8 +423,7 @@ def test_virtual_ranks_sharded_64_pivot_rounds(gpu, monkeypatch, kind, ranks, kb
                                 algo=ALGO_DENSE_FW, ngpus=1)
     exp = _oracle(g)
     assert_tables(lat, rel, exp["lat_int"], exp["rel"], f"virtual x{ranks} {kind} {kb}-pivot")
-    ld = (g.n + 127) // 128 * 128
-    want = 4 if kb == "64" else (9 if ld % 256 == 0 else 8)
+    want = 4 if kb == "64" else 8
     assert st.dist_enc == want, f"encoding {st.dist_enc}"
 
 
