@@ -85,8 +85,8 @@ typedef struct srt_build_stats {
                           * 2 = workgroup-per-source kernel (LDS-packed rows),
                           * 1 = wave-per-source kernel, 0 = workgroup kernel for every source.
                           * Dense: the distance encoding the build finished with: 12 = bit-parallel
-                          * Dial levels (no FW rounds; levels.hip), 9 = 8 with
-                          * 256-pivot rounds (SRT_FORM shkb=256), 8 = u16
+                          * Dial levels (no FW rounds; levels.hip), (9: retired 256-pivot
+                          * sharded rounds), 8 = u16
                           * f16-compare row-sharded symmetric rounds of 128 pivots (N > 1;
                           * 4 with SRT_FORM shkb=64), 7 = 5 with
                           * 256-pivot rounds (four panels per C-tile residency), 6 = 5 with
@@ -103,6 +103,10 @@ typedef struct srt_build_stats {
     int32_t levels;      /* dense level builds (dist_enc 12): the Dial level that settled every pair */
     int64_t work_bytes;  /* algorithmic bytes of the timed launches (level builds: the Delta words
                           * gathered over all levels), 0 where the bench models them itself */
+    double ms_pred;      /* level builds (time_kernels = 1): HIP-event time of the predecessor pass
+                          * (lvl_pred_kernel) */
+    double ms_rel;       /* ... and of the path-order reliability pass (rel_tree_kernel and the
+                          * sweeps of the rows it hands over) */
 } srt_build_stats;
 
 /* Build the full tables for an edge list on one GPU; outputs are host buffers of n*n entries.

@@ -65,6 +65,8 @@ class BuildStats(ctypes.Structure):
         ("tied_pairs", ctypes.c_int64),
         ("levels", ctypes.c_int32),
         ("work_bytes", ctypes.c_int64),
+        ("ms_pred", ctypes.c_double),
+        ("ms_rel", ctypes.c_double),
     ]
 
 

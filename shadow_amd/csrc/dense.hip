@@ -1290,6 +1290,10 @@ typedef struct {
     size_t rt_cap;
     int32_t* h_total; /* pinned: the essential-arc total of a post pass that did not wait for it */
     int total_pending;
+    /* time_kernels: events around the level post pass's predecessor and reliability kernels,
+     * read after the build's final wait (dense_finish_rows) */
+    hipEvent_t kev[4];
+    int kev_on;
 } dense_ws;
 
 static dense_ws g_ws[SRT_STATE_SLOTS];
@@ -1550,11 +1554,16 @@ static int dense_post_levels(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
         ws->rt_cap = c4;
         const bool ties = stats && stats->count_ties;
         if (ties) SRT_HIPCHK(hipMemsetAsync(ws->ties, 0, sizeof(unsigned long long), st));
+        const bool kt = stats && stats->time_kernels;
+        if (kt && !ws->kev[0])
+            for (int i = 0; i < 4; i++) SRT_HIPCHK(hipEventCreate(&ws->kev[i]));
+        if (kt) SRT_HIPCHK(hipEventRecord(ws->kev[0], st));
         /* int16 predecessors while every vertex fits (half the slab's bytes), widened by the
          * transpose into the int32 rows the reliability passes read */
         const int p16 = n <= 32768;
         if ((rc = srt_levels_pred(ws->predt, p16, ws->rt, (size_t)nrows, ties ? ws->ties : NULL, st)))
             return rc;
+        if (kt) SRT_HIPCHK(hipEventRecord(ws->kev[1], st));
         int32_t* pred = reinterpret_cast<int32_t*>(ws->dt);
         if (p16)
             transpose_kernel<int16_t, int32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
@@ -1568,9 +1577,14 @@ static int dense_post_levels(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
         SRT_HIPCHK(hipMemsetAsync(ws->depth, 0, sizeof(int32_t), st));
         /* every level-built distance is <= 254 quanta: level order in place for every row that
          * spans <= 64 quanta, sweeps for the rest (as dense_post); the level rows as u8 */
+        if (kt) SRT_HIPCHK(hipEventRecord(ws->kev[2], st));
         if ((rc = rel_rows_launch(n, ld, row0, lrows, d, pred, rel, ws->depth, ws->cursor, nullptr,
                                   st, srt_levels_l8())))
             return rc;
+        if (kt) {
+            SRT_HIPCHK(hipEventRecord(ws->kev[3], st));
+            ws->kev_on = 1;
+        }
     }
     srt_levels_release(st);
     if (stats) stats->ess_arcs = 0; /* no essential-arc lists in this form */
@@ -1604,6 +1618,14 @@ static int dense_finish_rows(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
         stats->max_depth = depth;
         stats->tied_pairs = (int64_t)nt;
         dense_collect_total(n, stats);
+        if (ws->kev_on) {
+            float a = 0, b = 0;
+            SRT_HIPCHK(hipEventElapsedTime(&a, ws->kev[0], ws->kev[1]));
+            SRT_HIPCHK(hipEventElapsedTime(&b, ws->kev[2], ws->kev[3]));
+            stats->ms_pred = a;
+            stats->ms_rel = b;
+            ws->kev_on = 0;
+        }
     }
     return SRT_OK;
 }
