@@ -706,6 +706,10 @@ def run_sparse(c: Ctx, wl):
               "parallelism": f"source-shard x{world}" + (" + RCCL allgather" if world > 1 else ""),
               "sources_per_rank": nsrc,
               "sources_recomputed_after_bucket_overflow": int(s0st.ess_arcs),
+              "kernel_form": int(s0st.fw_block),
+              # srt_build_stats.fw_block bit 64: the independent set's rows derived from their
+              # neighbours' (derive.hip) instead of run by the kernel
+              "derived_rows": bool(int(s0st.fw_block) & 64),
               "ms_sssp": round(s0st.ms_fw, 3)}
     return elapsed, "u32", "strong", config, roofline, cpu, parity
 
