@@ -152,7 +152,7 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
 int srt_derive_rows(int n, int nI, const int32_t* I, int src_begin, const int2* rowptr,
                     const uint2* cw, const uint8_t* ridx, const double* rtab, int ntab,
                     const int32_t* crow, const uint32_t* codes, uint32_t* lat, double* rel,
-                    size_t ldo, hipStream_t st);
+                    size_t ldo, hipStream_t st, int* fallback);
 int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, const double* r,
                    const int2* in_rowptr, const uint2* in_cw, const double* in_r,
                    const int32_t* perm, const int32_t* inv, uint32_t max_w, int local,
@@ -608,12 +608,13 @@ static int sparse_rows_derived(const srt_sparse_graph* g, uint32_t* lat_rows, do
     if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = SRT_E_DEVICE;
     bool core_ovf = false;
     for (int v = 0; v < n && !rc; v++) core_ovf |= hov[v] != 0;
-    if (!rc && core_ovf) /* (the set's flags are still 0: every flag is a core row's) */
+    int fallback = core_ovf;
+    if (!rc && !fallback)
+        rc = srt_derive_rows(n, g->nI, g->dI, 0, g->rpo, g->cw, g->ridx, g->rtab, g->ntab, g->crow,
+                             codes, lat_rows, rel_rows, (size_t)n, st, &fallback);
+    if (!rc && fallback) /* (the set's flags are still 0: every flag is a core row's) */
         rc = srt_wgsssp_rows(n, g->rpo, g->cw, g->r, NULL, g->max_w, 0, g->nI, g->dI, lat_rows,
                              rel_rows, ovf, st, g->ridx, g->rtab, 1, NULL);
-    else if (!rc)
-        rc = srt_derive_rows(n, g->nI, g->dI, 0, g->rpo, g->cw, g->ridx, g->rtab, g->ntab, g->crow,
-                             codes, lat_rows, rel_rows, (size_t)n, st);
     (void)hipFreeAsync(codes, st);
     return rc;
 }

@@ -21,47 +21,47 @@
  */
 #include "srt_device.h"
 
-#define DV_THREADS 1024
-#define DV_MAXDEG 8 /* largest degree the host puts in I */
-#define DV_J 4      /* targets per thread per phase-A step: their loads overlap */
+#define DV_THREADS 256
+#define DV_MAXDEG 4   /* largest degree the host puts in I (build.hip DERIVE_MAXDEG) */
+#define DV_J 2        /* targets per thread per phase-A step: their loads overlap */
+#define DV_LMAX 2048  /* distance levels of the ordered pass (the workgroup kernel's rows end at
+                       * 1,022 quanta, a derived row at 1,022 + 127) */
+#define DV_WG_PER_CU 8
 
-static __device__ __forceinline__ double dv_ld(const double* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-static __device__ __forceinline__ void dv_st(double* p, double v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 /* order of canonical arcs u | w << 17 | ridx << 24: the largest w, then the smallest u */
 static __device__ __forceinline__ uint32_t dv_key(uint32_t code) {
     return ((127u - ((code >> 17) & 0x7Fu)) << 17) | (code & 0x1FFFFu);
 }
 
-/* One workgroup per derived source (persistent grid over I). Rows are placed by source: row of
- * vertex v = v - src_begin, in lat / rel (stride ldo); core vertex k's codes are row crow[k] of
- * codes (stride n). scratch: n words per workgroup (its row of derived codes). */
-__global__ __launch_bounds__(DV_THREADS) void derive_rows_kernel(
+/* One workgroup per derived source (persistent grid over I, DV_WG_PER_CU resident per CU: a
+ * row's ordered pass is a chain of short levels, and the other rows of the CU fill its waits).
+ * Rows are placed by source: row of vertex v = v - src_begin, in lat / rel (stride ldo); core
+ * vertex k's codes are row crow[k] of codes (stride n). Per workgroup scratch: cs (n codes) and
+ * lst (n (target, code) entries, ordered by distance). *bad = 1 if a distance reached DV_LMAX
+ * (the caller then builds these rows with the kernel). */
+__global__ __launch_bounds__(DV_THREADS, 8) void derive_rows_kernel(
     int n, int nI, const int32_t* __restrict__ I, int src_begin, const int2* __restrict__ rowptr,
     const uint2* __restrict__ cw, const uint8_t* __restrict__ ridx, const double* __restrict__ rtab,
     int ntab, const int32_t* __restrict__ crow, const uint32_t* __restrict__ codes,
-    uint32_t* __restrict__ lat, double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ scratch,
-    int32_t* __restrict__ max_depth) {
-    extern __shared__ uint32_t dbm[]; /* done[nw], fresh[nw] */
+    uint32_t* __restrict__ lat, double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ cs_all,
+    uint2* __restrict__ lst_all, size_t lds_n, int* __restrict__ bad) {
+    __shared__ uint32_t s_start[DV_LMAX + 1]; /* first entry of each level in lst */
+    __shared__ uint32_t s_cur[DV_LMAX];       /* counts, then scatter cursors */
     __shared__ double s_tab[256];
     __shared__ int s_nb[DV_MAXDEG], s_w[DV_MAXDEG], s_rx[DV_MAXDEG], s_cr[DV_MAXDEG];
-    __shared__ int s_any;
-    const int tid = threadIdx.x, nw = (n + 31) >> 5;
-    uint32_t* done = dbm;
-    uint32_t* fresh = dbm + nw;
+    __shared__ uint32_t s_maxd;
+    __shared__ int s_big;
+    const int tid = threadIdx.x;
     for (int i = tid; i < ntab; i += DV_THREADS) s_tab[i] = rtab[i];
-    uint32_t* cs = scratch + (size_t)blockIdx.x * (size_t)((n + 3) & ~3); /* 16-B aligned rows */
-    int depth_max = 0;
+    uint32_t* cs = cs_all + (size_t)blockIdx.x * lds_n;
+    uint2* lst = lst_all + (size_t)blockIdx.x * lds_n;
     for (int si = blockIdx.x; si < nI; si += gridDim.x) {
         const int s = I[si];
         uint32_t* ol = lat + (size_t)(s - src_begin) * ldo;
         double* orr = rel + (size_t)(s - src_begin) * ldo;
         const int2 be = rowptr[s];
         const int deg = min(be.y - be.x, DV_MAXDEG);
-        __syncthreads(); /* the previous source is done with s_nb and the bitmaps */
+        __syncthreads(); /* the previous source is done with the shared state */
         if (tid < deg) {
             const uint2 e = cw[be.x + tid];
             s_nb[tid] = (int)e.x;
@@ -69,10 +69,16 @@ __global__ __launch_bounds__(DV_THREADS) void derive_rows_kernel(
             s_rx[tid] = ridx[be.x + tid];
             s_cr[tid] = crow[e.x];
         }
-        for (int q = tid; q < 2 * nw; q += DV_THREADS) dbm[q] = 0u;
+        for (int q = tid; q < DV_LMAX; q += DV_THREADS) s_cur[q] = 0u;
+        if (tid == 0) {
+            s_maxd = 0u;
+            s_big = 0;
+        }
         __syncthreads();
         /* phase A: distances and derived codes, DV_J targets per thread at a time (the deg row
-         * loads of all of them in flight together, then the codes of the tight neighbours) */
+         * loads of all of them in flight together, then the codes of the tight neighbours);
+         * the histogram of the distances */
+        uint32_t mymax = 0;
         for (int t0 = 0; t0 < n; t0 += DV_J * DV_THREADS) {
             uint32_t dk[DV_J][DV_MAXDEG];
 #pragma unroll
@@ -117,112 +123,118 @@ __global__ __launch_bounds__(DV_THREADS) void derive_rows_kernel(
                         bk = dv_key(cd[j][i]);
                         best = cd[j][i];
                     }
-                if (t == s) {
-                    D[j] = 0;
-                    best = ~0u;
-                }
+                if (t == s) D[j] = 0;
                 ol[t] = D[j];
                 cs[t] = best;
-                if (t == s || D[j] >= SRT_INF) { /* resolved: the source, or unreachable */
-                    atomicOr(&done[t >> 5], 1u << (t & 31));
-                    dv_st(orr + t, t == s ? 1.0 : 0.0);
+                if (t == s || D[j] >= SRT_INF) { /* the source, or unreachable */
+                    orr[t] = t == s ? 1.0 : 0.0;
+                } else if (D[j] < DV_LMAX) {
+                    atomicAdd(&s_cur[D[j]], 1u);
+                    mymax = max(mymax, D[j]);
+                } else {
+                    s_big = 1;
                 }
             }
+        }
+        if (mymax) atomicMax(&s_maxd, mymax);
+        __syncthreads();
+        if (s_big) { /* uniform: the caller rebuilds the set's rows with the kernel */
+            if (tid == 0) *bad = 1;
+            continue;
+        }
+        const uint32_t maxd = s_maxd;
+        /* exclusive scan of the level counts into s_start (cursors = starts): DV_LMAX / 256
+         * consecutive levels per thread, a wave scan of the partial sums, then the waves' */
+        {
+            constexpr int PERT = DV_LMAX / DV_THREADS;
+            const int lane = tid & 63, wv = tid >> 6;
+            uint32_t part = 0;
+#pragma unroll
+            for (int q = 0; q < PERT; ++q) part += s_cur[tid * PERT + q];
+            uint32_t inc = part;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+                if (lane >= o) inc += y;
+            }
+            __shared__ uint32_t s_wsum[DV_THREADS / 64];
+            if (lane == 63) s_wsum[wv] = inc;
+            __syncthreads();
+            uint32_t acc = inc - part;
+            for (int i = 0; i < wv; ++i) acc += s_wsum[i];
+#pragma unroll
+            for (int q = 0; q < PERT; ++q) {
+                const int L = tid * PERT + q;
+                const uint32_t c = s_cur[L];
+                s_start[L] = acc;
+                s_cur[L] = acc;
+                acc += c;
+            }
+            if (tid == DV_THREADS - 1) s_start[DV_LMAX] = acc;
+        }
+        __syncthreads();
+        /* phase A2: the reachable targets into lst, grouped by distance (any order inside a
+         * level: every arc is >= 1 quantum, so a target's predecessor is in an earlier level) */
+        for (int t = tid; t < n; t += DV_THREADS) {
+            const uint32_t d = ol[t];
+            if (t == s || d >= SRT_INF) continue;
+            const uint32_t pos = atomicAdd(&s_cur[d], 1u);
+            lst[pos] = make_uint2((uint32_t)t, cs[t]);
         }
         __threadfence_block();
         __syncthreads();
-        /* phase B: rel(s,t) = rel(s,u) * r(u,t) once u has resolved (path order from s), in
-         * sweeps; a thread owns whole bitmap words and reads its 32 targets' codes at once */
-        int depth = 0;
-        for (;;) {
-            if (tid == 0) s_any = 0;
-            __syncthreads();
-            int any = 0;
-            for (int w = tid; w < nw; w += DV_THREADS) {
-                uint32_t pend = ~done[w];
-                if (w == nw - 1 && (n & 31)) pend &= (1u << (n & 31)) - 1u;
-                if (!pend) continue;
-                uint32_t c[32];
-                const uint4* cp = reinterpret_cast<const uint4*>(cs + (size_t)w * 32);
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const uint4 x = (w * 32 + q * 4 + 3 < n) ? cp[q]
-                                    : make_uint4(~0u, ~0u, ~0u, ~0u);
-                    c[4 * q] = x.x;
-                    c[4 * q + 1] = x.y;
-                    c[4 * q + 2] = x.z;
-                    c[4 * q + 3] = x.w;
-                }
-                if (w * 32 + 32 > n) /* the ragged last word: no 16-byte tail reads */
-                    for (int b = 0; b < 32; ++b) c[b] = w * 32 + b < n ? cs[w * 32 + b] : ~0u;
-                uint32_t ready = 0u;
-#pragma unroll
-                for (int b = 0; b < 32; ++b) {
-                    const uint32_t u = c[b] & 0x1FFFFu;
-                    if (((pend >> b) & 1u) && c[b] != ~0u && ((done[u >> 5] >> (u & 31)) & 1u))
-                        ready |= 1u << b;
-                }
-                if (!ready) continue;
-#pragma unroll
-                for (int b0 = 0; b0 < 32; b0 += 8) { /* eight predecessor loads in flight */
-                    if (!((ready >> b0) & 0xFFu)) continue;
-                    double ru[8];
-#pragma unroll
-                    for (int b = 0; b < 8; ++b)
-                        ru[b] = ((ready >> (b0 + b)) & 1u) ? dv_ld(orr + (c[b0 + b] & 0x1FFFFu))
-                                                           : 0.0;
-#pragma unroll
-                    for (int b = 0; b < 8; ++b)
-                        if ((ready >> (b0 + b)) & 1u)
-                            dv_st(orr + w * 32 + b0 + b, ru[b] * s_tab[c[b0 + b] >> 24]);
-                }
-                fresh[w] = ready; /* word w belongs to this thread alone */
-                any = 1;
+        /* phase B: rel(s,t) = rel(s,u) * r(u,t) level by level (path order from s; rel(s,s) = 1
+         * was written in phase A, so the direct arc needs no case) */
+        for (uint32_t L = 1; L <= maxd; ++L) {
+            const uint32_t b = s_start[L], e = s_start[L + 1];
+            if (b == e) continue; /* uniform */
+            for (uint32_t q = b + tid; q < e; q += DV_THREADS) {
+                const uint2 x = lst[q];
+                const double ru = orr[x.y & 0x1FFFFu];
+                orr[x.x] = ru * s_tab[x.y >> 24];
             }
-            if (any) s_any = 1;
             __threadfence_block();
             __syncthreads();
-            if (!s_any) break;
-            ++depth;
-            for (int w = tid; w < nw; w += DV_THREADS) {
-                done[w] |= fresh[w];
-                fresh[w] = 0u;
-            }
-            __syncthreads();
         }
-        depth_max = depth > depth_max ? depth : depth_max;
     }
-    if (max_depth && tid == 0) atomicMax(max_depth, depth_max);
 }
 
 /* The rows of the nI sources I (device list) by derivation, into lat / rel rows placed by source
  * (row v - src_begin, stride ldo), from the core rows already there and their codes (row crow[k]
  * of codes, stride n). rowptr / cw / ridx: the original-order CSR with each arc's index into
  * rtab (ntab <= 256 distinct reliabilities). Every source of I has degree <= DV_MAXDEG and every
- * neighbour is a core vertex (the caller's independent set). */
+ * neighbour is a core vertex (the caller's independent set). Waits for the kernel: *fallback = 1
+ * when a derived distance passed the ordered pass's levels (the caller then builds I's rows with
+ * the SSSP kernel). */
 int srt_derive_rows(int n, int nI, const int32_t* I, int src_begin, const int2* rowptr,
                     const uint2* cw, const uint8_t* ridx, const double* rtab, int ntab,
                     const int32_t* crow, const uint32_t* codes, uint32_t* lat, double* rel,
-                    size_t ldo, hipStream_t st) {
+                    size_t ldo, hipStream_t st, int* fallback) {
+    *fallback = 0;
     if (nI <= 0) return SRT_OK;
-    if (ntab > 256 || n > srt_path_sweeps_max_n()) {
-        srt_set_error("derive: %d reliabilities or n = %d outside the kernel's range", ntab, n);
+    if (ntab > 256) {
+        srt_set_error("derive: %d distinct reliabilities (at most 256)", ntab);
         return SRT_E_ARG;
     }
     int cus = 256, dev = 0;
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
         cus = prop.multiProcessorCount;
-    const int grid = nI < 2 * cus ? nI : 2 * cus;
-    uint32_t* scratch = NULL;
-    SRT_HIPCHK(srt_malloc_async(&scratch, (size_t)grid * ((n + 3) & ~3) * sizeof(uint32_t), st));
-    const size_t lds = 2 * (size_t)((n + 31) / 32) * sizeof(uint32_t);
-    SRT_HIPCHK(hipFuncSetAttribute((const void*)derive_rows_kernel,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    derive_rows_kernel<<<grid, DV_THREADS, lds, st>>>(n, nI, I, src_begin, rowptr, cw, ridx, rtab,
-                                                      ntab, crow, codes, lat, rel, ldo, scratch,
-                                                      NULL);
+    const int grid = nI < DV_WG_PER_CU * cus ? nI : DV_WG_PER_CU * cus;
+    const size_t np = ((size_t)n + 3) & ~(size_t)3;
+    uint32_t* cs = NULL;
+    uint2* lst = NULL;
+    int* bad = NULL;
+    SRT_HIPCHK(srt_malloc_async(&cs, (size_t)grid * np * sizeof(uint32_t), st));
+    SRT_HIPCHK(srt_malloc_async(&lst, (size_t)grid * np * sizeof(uint2), st));
+    SRT_HIPCHK(srt_malloc_async(&bad, sizeof(int), st));
+    SRT_HIPCHK(hipMemsetAsync(bad, 0, sizeof(int), st));
+    derive_rows_kernel<<<grid, DV_THREADS, 0, st>>>(n, nI, I, src_begin, rowptr, cw, ridx, rtab, ntab,
+                                                    crow, codes, lat, rel, ldo, cs, lst, np, bad);
     SRT_HIPCHK(hipGetLastError());
-    SRT_HIPCHK(hipFreeAsync(scratch, st));
+    SRT_HIPCHK(hipMemcpyAsync(fallback, bad, sizeof(int), hipMemcpyDeviceToHost, st));
+    SRT_HIPCHK(hipFreeAsync(cs, st));
+    SRT_HIPCHK(hipFreeAsync(lst, st));
+    SRT_HIPCHK(hipFreeAsync(bad, st));
+    SRT_HIPCHK(hipStreamSynchronize(st));
     return SRT_OK;
 }
