@@ -44,7 +44,7 @@ __global__ __launch_bounds__(DV_THREADS, 8) void derive_rows_kernel(
     const uint2* __restrict__ cw, const uint8_t* __restrict__ ridx, const double* __restrict__ rtab,
     int ntab, const int32_t* __restrict__ crow, const uint32_t* __restrict__ codes,
     uint32_t* __restrict__ lat, double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ cs_all,
-    uint2* __restrict__ lst_all, size_t lds_n, int* __restrict__ bad) {
+    uint2* __restrict__ lst_all, size_t lds_n, int* __restrict__ bad, int phases) {
     __shared__ uint32_t s_start[DV_LMAX + 1]; /* first entry of each level in lst */
     __shared__ uint32_t s_cur[DV_LMAX];       /* counts, then scatter cursors */
     __shared__ double s_tab[256];
@@ -143,6 +143,7 @@ __global__ __launch_bounds__(DV_THREADS, 8) void derive_rows_kernel(
             continue;
         }
         const uint32_t maxd = s_maxd;
+        if (phases < 2) continue; /* tools (SRT_FORM dv_phases=1): phase A alone, for timing */
         /* exclusive scan of the level counts into s_start (cursors = starts): DV_LMAX / 256
          * consecutive levels per thread, a wave scan of the partial sums, then the waves' */
         {
@@ -182,6 +183,7 @@ __global__ __launch_bounds__(DV_THREADS, 8) void derive_rows_kernel(
         }
         __threadfence_block();
         __syncthreads();
+        if (phases < 3) continue; /* tools: phases A and A2 */
         /* phase B: rel(s,t) = rel(s,u) * r(u,t) level by level (path order from s; rel(s,s) = 1
          * was written in phase A, so the direct arc needs no case) */
         for (uint32_t L = 1; L <= maxd; ++L) {
@@ -229,7 +231,8 @@ int srt_derive_rows(int n, int nI, const int32_t* I, int src_begin, const int2* 
     SRT_HIPCHK(srt_malloc_async(&bad, sizeof(int), st));
     SRT_HIPCHK(hipMemsetAsync(bad, 0, sizeof(int), st));
     derive_rows_kernel<<<grid, DV_THREADS, 0, st>>>(n, nI, I, src_begin, rowptr, cw, ridx, rtab, ntab,
-                                                    crow, codes, lat, rel, ldo, cs, lst, np, bad);
+                                                    crow, codes, lat, rel, ldo, cs, lst, np, bad,
+                                                    srt_form_int("dv_phases", 3));
     SRT_HIPCHK(hipGetLastError());
     SRT_HIPCHK(hipMemcpyAsync(fallback, bad, sizeof(int), hipMemcpyDeviceToHost, st));
     SRT_HIPCHK(hipFreeAsync(cs, st));
