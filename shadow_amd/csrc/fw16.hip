@@ -2035,8 +2035,8 @@ int srt_fw16_levels(const srt_comm* comm, int n, int ld, int row0, int nrows, in
     *nlev = 0;
     *bytes = 0;
     /* the level post pass reads the build's own u8 rows, not the u16 FW matrix: none written */
-    return srt_levels_build(comm, n, ld, row0, nrows, directed, w_rows, r_rows, NULL, lat_rows, CAP_F,
-                            fw_ms, st, evp, nlev, bytes);
+    return srt_levels_build(comm, n, ld, row0, nrows, directed, w_rows, r_rows, lat_rows, fw_ms, st,
+                            evp, nlev, bytes);
 }
 
 int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,

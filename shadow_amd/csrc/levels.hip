@@ -253,28 +253,30 @@ __global__ __launch_bounds__(256) void lvl_step_kernel(int d, int n, int nw, int
 /* Distance rows of the local sources from the levels: the u32 table rows (SRT_INF on padding) and
  * the u8 level rows the reliability pass reads (0 on the diagonal and padding) -- the FW finish
  * pass folded in: every settled distance is <= the level budget (<= 254), so the rows are exact
- * and small by construction -- and, when d16 is given, the FW matrix layout (u16, 0 on the
- * diagonal, cap on padding). Thread = four consecutive targets t0..t0 + 3 (256 threads = 1,024
+ * and small by construction. Thread = four consecutive targets t0..t0 + 3 (256 threads = 1,024
  * targets per workgroup), looping over 16 source words: per word it reads the four targets' word
- * of every level (the same lines for the 16 words of a workgroup row) and writes 16 B of u32 and
- * 4 B of u8 per source row. */
+ * of every level (the same lines for the 16 words of a workgroup row), keeps the 32 sources' four
+ * distances as bytes (0xFF: none; 32 VGPRs, 8 waves per SIMD) and writes 16 B of u32 and 4 B of u8
+ * per source row. */
 __global__ __launch_bounds__(256) void lvl_out_kernel(int n, int ld, int nw, int src0, int nlev,
                                                       const uint32_t* __restrict__ lev,
-                                                      uint16_t* __restrict__ d16,
                                                       uint32_t* __restrict__ lat,
-                                                      uint8_t* __restrict__ l8, uint32_t cap) {
+                                                      uint8_t* __restrict__ l8) {
     const int t0 = (blockIdx.x * 256 + threadIdx.x) * 4;
     if (t0 >= ld) return;
     const size_t plane = (size_t)n * nw;
     const int sw1 = min(nw, (int)(blockIdx.y + 1) * 16);
     for (int sw = blockIdx.y * 16; sw < sw1; ++sw) {
-        uint32_t v[32][2]; /* per source: targets t0, t0+1 | t0+2, t0+3 as u16 pairs */
+        uint32_t v[32]; /* per source: the distances to t0..t0 + 3, one byte each */
         const int sg0 = src0 + sw * 32;
 #pragma unroll
         for (int s = 0; s < 32; ++s) {
             const int sg = sg0 + s;
-            v[s][0] = (sg == t0 ? 0u : cap) | ((sg == t0 + 1 ? 0u : cap) << 16);
-            v[s][1] = (sg == t0 + 2 ? 0u : cap) | ((sg == t0 + 3 ? 0u : cap) << 16);
+            uint32_t x = 0xFFFFFFFFu;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (sg == t0 + q) x &= ~(0xFFu << (8 * q));
+            v[s] = x;
         }
         for (int d = 1; d <= nlev; ++d) {
             uint32_t m[4];
@@ -286,22 +288,19 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(int n, int ld, int nw, int
             for (int s = 0; s < 32; ++s) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    if ((m[q] >> s) & 1u) {
-                        const int h = 16 * (q & 1);
-                        v[s][q >> 1] = (v[s][q >> 1] & ~(0xFFFFu << h)) | ((uint32_t)d << h);
-                    }
+                    if ((m[q] >> s) & 1u)
+                        v[s] = (v[s] & ~(0xFFu << (8 * q))) | ((uint32_t)d << (8 * q));
             }
         }
 #pragma unroll
         for (int s = 0; s < 32; ++s) {
             const size_t o = (size_t)(sw * 32 + s) * ld + t0;
-            if (d16) *reinterpret_cast<uint2*>(d16 + o) = make_uint2(v[s][0], v[s][1]);
-            uint32_t x[4] = {v[s][0] & 0xFFFFu, v[s][0] >> 16, v[s][1] & 0xFFFFu, v[s][1] >> 16};
-            uint32_t b = 0;
+            uint32_t x[4], b = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                b |= (x[q] == cap ? 0u : x[q]) << (8 * q);
-                x[q] = x[q] == cap ? SRT_INF : x[q];
+                const uint32_t y = (v[s] >> (8 * q)) & 0xFFu;
+                x[q] = y == 0xFFu ? SRT_INF : y;
+                b |= (y == 0xFFu ? 0u : y) << (8 * q);
             }
             *reinterpret_cast<uint4*>(lat + o) = make_uint4(x[0], x[1], x[2], x[3]);
             *reinterpret_cast<uint32_t*>(l8 + o) = b;
@@ -547,18 +546,17 @@ const uint8_t* srt_levels_l8(void) {
         L->p[L->k++] = (void*)(ptr);                               \
     } while (0)
 
-/* One build of the local rows' u16 distances into d16 (nrows x ld). comm (NULL on one GPU):
- * undirected row shards, every rank sees every target's in-arcs after the segment broadcasts.
- * fw_ms: the predicted Floyd-Warshall time; the level budget keeps the predicted level time under
- * half of it. *levels = the level that settled every pair (0: not applicable / over budget -- the
- * caller runs Floyd-Warshall; every rank of a sharded build returns the same verdict).
- * *gather_bytes: the Delta words gathered (the kernel's algorithmic bytes). On success d16 and
- * lat_rows hold the rows (the FW finish pass's outputs) and the slot keeps the arcs and planes
- * for srt_levels_pred until srt_levels_release. */
+/* One build of the local rows' distances (nrows x ld). comm (NULL on one GPU): undirected row
+ * shards, every rank sees every target's in-arcs after the segment broadcasts. fw_ms: the
+ * predicted Floyd-Warshall time; the level budget keeps the predicted level time under half of
+ * it. *levels = the level that settled every pair (0: not applicable / over budget -- the caller
+ * runs Floyd-Warshall; every rank of a sharded build returns the same verdict). *gather_bytes: the
+ * Delta words gathered (the kernel's algorithmic bytes). On success lat_rows hold the u32 rows
+ * (the FW finish pass's output) and the slot keeps the arcs, the planes and the u8 rows for
+ * srt_levels_pred / srt_levels_l8 until srt_levels_release. */
 int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
-                     const uint32_t* w_rows, const double* r_rows, uint16_t* d16,
-                     uint32_t* lat_rows, uint32_t cap, double fw_ms, hipStream_t st, evpool_t* evp,
-                     int* levels, int64_t* gather_bytes) {
+                     const uint32_t* w_rows, const double* r_rows, uint32_t* lat_rows, double fw_ms,
+                     hipStream_t st, evpool_t* evp, int* levels, int64_t* gather_bytes) {
     *levels = 0;
     *gather_bytes = 0;
     lvl_state* L = &g_lvl[srt_state_slot()];
@@ -722,7 +720,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     uint8_t* l8 = NULL;
     LVL_ALLOC(l8, (size_t)nrows * ld);
     lvl_out_kernel<<<dim3(srt_ceil_div(ld, 1024), srt_ceil_div(nw, 16)), 256, 0, st>>>(
-        n, ld, nw, row0, D, lev, d16, lat_rows, l8, cap);
+        n, ld, nw, row0, D, lev, lat_rows, l8);
     SRT_HIPCHK(hipGetLastError());
     *levels = D;
     *gather_bytes = gathered;

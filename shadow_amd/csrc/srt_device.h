@@ -153,12 +153,10 @@ int srt_fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0, in
 int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, uint32_t* lat_rows,
                    hipStream_t st, evpool_t* evp, srt_owner_fn owner_of, srt_panel_bcast_fn bcast,
                    void* ctx, int rank, int fm, int* sym, int* exact);
-/* levels.hip: distance rows of the local sources by bit-parallel Dial levels (see there); d16
- * (the FW matrix layout) may be NULL */
+/* levels.hip: distance rows of the local sources by bit-parallel Dial levels (see there) */
 int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
-                     const uint32_t* w_rows, const double* r_rows, uint16_t* d16,
-                     uint32_t* lat_rows, uint32_t cap, double fw_ms, hipStream_t st, evpool_t* evp,
-                     int* levels, int64_t* gather_bytes);
+                     const uint32_t* w_rows, const double* r_rows, uint32_t* lat_rows, double fw_ms,
+                     hipStream_t st, evpool_t* evp, int* levels, int64_t* gather_bytes);
 /* predecessors (int16 when pred16, else int32) + arc reliabilities of the held level build
  * (target-major, row stride ldp) */
 int srt_levels_pred(void* predT, int pred16, double* rT, size_t ldp, unsigned long long* ties,
