@@ -200,6 +200,125 @@ __global__ __launch_bounds__(DV_THREADS, 8) void derive_rows_kernel(
     }
 }
 
+/* The same rows with the reliability formed on demand instead of level by level: a thread takes
+ * its targets in index order (coalesced code reads and rel writes) and forms rel(s,t) once its
+ * predecessor's is done; if not, it climbs the predecessor chain to the first vertex whose
+ * predecessor is done, forms that one, and repeats. A done bit (LDS) is set after the value is
+ * stored (workgroup release/acquire), so a value is read only once final; two threads that form
+ * the same vertex store the same product. The ancestors near s are shared by most chains and
+ * stay in cache; no list, no per-level barrier. */
+__global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
+    int n, int nI, const int32_t* __restrict__ I, int src_begin, const int2* __restrict__ rowptr,
+    const uint2* __restrict__ cw, const uint8_t* __restrict__ ridx, const double* __restrict__ rtab,
+    int ntab, const int32_t* __restrict__ crow, const uint32_t* __restrict__ codes,
+    uint32_t* __restrict__ lat, double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ cs_all,
+    size_t lds_n) {
+    extern __shared__ uint32_t cdone[]; /* one bit per target */
+    __shared__ double s_tab[256];
+    __shared__ int s_nb[DV_MAXDEG], s_w[DV_MAXDEG], s_rx[DV_MAXDEG], s_cr[DV_MAXDEG];
+    const int tid = threadIdx.x, nw = (n + 31) >> 5;
+    for (int i = tid; i < ntab; i += DV_THREADS) s_tab[i] = rtab[i];
+    uint32_t* cs = cs_all + (size_t)blockIdx.x * lds_n;
+    auto is_done = [&](uint32_t v) {
+        return (__hip_atomic_load(&cdone[v >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >>
+                (v & 31)) & 1u;
+    };
+    for (int si = blockIdx.x; si < nI; si += gridDim.x) {
+        const int s = I[si];
+        uint32_t* ol = lat + (size_t)(s - src_begin) * ldo;
+        double* orr = rel + (size_t)(s - src_begin) * ldo;
+        const int2 be = rowptr[s];
+        const int deg = min(be.y - be.x, DV_MAXDEG);
+        __syncthreads(); /* the previous source is done with the shared state */
+        if (tid < deg) {
+            const uint2 e = cw[be.x + tid];
+            s_nb[tid] = (int)e.x;
+            s_w[tid] = (int)e.y;
+            s_rx[tid] = ridx[be.x + tid];
+            s_cr[tid] = crow[e.x];
+        }
+        for (int q = tid; q < nw; q += DV_THREADS) cdone[q] = 0u;
+        __syncthreads();
+        /* phase A (as derive_rows_kernel): distances, derived codes; s and the unreachable
+         * targets are done at once */
+        for (int t0 = 0; t0 < n; t0 += DV_J * DV_THREADS) {
+            uint32_t dk[DV_J][DV_MAXDEG];
+#pragma unroll
+            for (int j = 0; j < DV_J; ++j) {
+                const int t = t0 + j * DV_THREADS + tid;
+#pragma unroll
+                for (int i = 0; i < DV_MAXDEG; ++i)
+                    dk[j][i] = (i < deg && t < n)
+                                   ? lat[(size_t)(s_nb[i] - src_begin) * ldo + t]
+                                   : SRT_INF;
+            }
+            uint32_t D[DV_J];
+#pragma unroll
+            for (int j = 0; j < DV_J; ++j) {
+                D[j] = SRT_INF;
+#pragma unroll
+                for (int i = 0; i < DV_MAXDEG; ++i)
+                    if (dk[j][i] < SRT_INF) D[j] = min(D[j], (uint32_t)s_w[i] + dk[j][i]);
+            }
+            uint32_t cd[DV_J][DV_MAXDEG];
+#pragma unroll
+            for (int j = 0; j < DV_J; ++j) {
+                const int t = t0 + j * DV_THREADS + tid;
+#pragma unroll
+                for (int i = 0; i < DV_MAXDEG; ++i) {
+                    cd[j][i] = ~0u;
+                    if (dk[j][i] < SRT_INF && (uint32_t)s_w[i] + dk[j][i] == D[j])
+                        cd[j][i] = t == s_nb[i]
+                                       ? ((uint32_t)s | ((uint32_t)s_w[i] << 17) |
+                                          ((uint32_t)s_rx[i] << 24))
+                                       : codes[(size_t)s_cr[i] * n + t];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < DV_J; ++j) {
+                const int t = t0 + j * DV_THREADS + tid;
+                if (t >= n) continue;
+                uint32_t best = ~0u, bk = ~0u;
+#pragma unroll
+                for (int i = 0; i < DV_MAXDEG; ++i)
+                    if (cd[j][i] != ~0u && dv_key(cd[j][i]) < bk) {
+                        bk = dv_key(cd[j][i]);
+                        best = cd[j][i];
+                    }
+                if (t == s) D[j] = 0;
+                ol[t] = D[j];
+                cs[t] = best;
+                if (t == s || D[j] >= SRT_INF) {
+                    orr[t] = t == s ? 1.0 : 0.0;
+                    atomicOr(&cdone[t >> 5], 1u << (t & 31));
+                }
+            }
+        }
+        __threadfence_block();
+        __syncthreads();
+        /* phase B: on-demand path-order products */
+        for (int t = tid; t < n; t += DV_THREADS) {
+            if (is_done((uint32_t)t)) continue;
+            uint32_t ct = cs[t];
+            for (;;) {
+                uint32_t y = (uint32_t)t, cy = ct;
+                while (!is_done(cy & 0x1FFFFu)) { /* climb to the first formable ancestor */
+                    y = cy & 0x1FFFFu;
+                    cy = cs[y];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                const double rp = __hip_atomic_load(orr + (cy & 0x1FFFFu), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(orr + y, rp * s_tab[cy >> 24], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                atomicOr(&cdone[y >> 5], 1u << (y & 31));
+                if (y == (uint32_t)t) break;
+            }
+        }
+    }
+}
+
 /* The rows of the nI sources I (device list) by derivation, into lat / rel rows placed by source
  * (row v - src_begin, stride ldo), from the core rows already there and their codes (row crow[k]
  * of codes, stride n). rowptr / cw / ridx: the original-order CSR with each arc's index into
@@ -230,9 +349,20 @@ int srt_derive_rows(int n, int nI, const int32_t* I, int src_begin, const int2* 
     SRT_HIPCHK(srt_malloc_async(&lst, (size_t)grid * np * sizeof(uint2), st));
     SRT_HIPCHK(srt_malloc_async(&bad, sizeof(int), st));
     SRT_HIPCHK(hipMemsetAsync(bad, 0, sizeof(int), st));
-    derive_rows_kernel<<<grid, DV_THREADS, 0, st>>>(n, nI, I, src_begin, rowptr, cw, ridx, rtab, ntab,
-                                                    crow, codes, lat, rel, ldo, cs, lst, np, bad,
-                                                    srt_form_int("dv_phases", 3));
+    if (srt_form_int("dv_chain", 1)) {
+        /* on-demand products (derive_chain_kernel): SRT_FORM dv_wg workgroups per CU */
+        const int per = srt_form_int("dv_wg", 4);
+        const int g2 = nI < per * cus ? nI : per * cus;
+        const size_t lds = (size_t)((n + 31) / 32) * sizeof(uint32_t);
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)derive_chain_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        derive_chain_kernel<<<g2 < grid ? g2 : grid, DV_THREADS, lds, st>>>(
+            n, nI, I, src_begin, rowptr, cw, ridx, rtab, ntab, crow, codes, lat, rel, ldo, cs, np);
+    } else {
+        derive_rows_kernel<<<grid, DV_THREADS, 0, st>>>(n, nI, I, src_begin, rowptr, cw, ridx, rtab,
+                                                        ntab, crow, codes, lat, rel, ldo, cs, lst, np,
+                                                        bad, srt_form_int("dv_phases", 3));
+    }
     SRT_HIPCHK(hipGetLastError());
     SRT_HIPCHK(hipMemcpyAsync(fallback, bad, sizeof(int), hipMemcpyDeviceToHost, st));
     SRT_HIPCHK(hipFreeAsync(cs, st));

@@ -179,33 +179,40 @@ static __device__ __forceinline__ void lvl_step_unit(unsigned g, int d, int n, i
     }
     uint32_t acc = 0;
     const int32_t* oj = off + (size_t)j * LVL_STRIDE;
-    /* arcs of weight d: the path (k, j) itself, Delta_0[k] = {k} */
+    /* arcs of weight d: the path (k, j) itself, Delta_0[k] = {k}; 64 arcs per step, one per lane,
+     * and the few whose source lies in this unit's chunk go to the lane owning its word */
     {
-        const int a0 = oj[d], a1 = oj[d + 1];
-        for (int i = a0; i < a1; ++i) {
-            const int ks = (int)(arcs[i] & 0xFFFFu) - src0;
-            if ((unsigned)ks < (unsigned)nsrc && (ks >> 5) == word) acc |= 1u << (ks & 31);
+        const int a0 = oj[d], a1 = oj[d + 1], cw0 = c * 64 * 32;
+        for (int i0 = a0; i0 < a1; i0 += 64) {
+            const int i = i0 + lane;
+            const int ks = i < a1 ? (int)(arcs[i] & 0xFFFFu) - src0 : -1;
+            unsigned long long m = __ballot(ks >= 0 && ks < nsrc && (unsigned)(ks - cw0) < 64u * 32u);
+            while (m) {
+                const int j = __builtin_ctzll(m);
+                m &= m - 1ull;
+                const int kj = __builtin_amdgcn_readlane(ks, j);
+                if ((kj >> 5) == word) acc |= 1u << (kj & 31);
+            }
         }
     }
     /* arcs of weight w < d: Delta_{d-w}[k], one weight group at a time so the group's plane base is
      * one scalar pointer and an arc costs one VALU add (its row's byte offset k * nw * 4, aoff, plus
-     * the lane's) and one gather; eight gathers in flight. Lanes past nw read word 0 of the row (a
-     * valid address) and drop it, so the loop has no per-lane branch. */
+     * the lane's) and one gather; sixteen gathers in flight. Lanes past nw read word 0 of the row
+     * (a valid address) and drop it, so the loop has no per-lane branch. */
     const uint32_t lane4 = (uint32_t)(valid ? word : 0) * 4u;
     for (int w = 1; w < d; ++w) {
         const int g1 = oj[w + 1];
         const char* base = reinterpret_cast<const char*>(lev + (size_t)(d - w - 1) * plane);
-        int i = oj[w];
-        for (; i + 8 <= g1; i += 8) {
-            uint32_t a[8], v[8];
+        for (int i = oj[w]; i < g1; i += 16) { /* sixteen in flight, the tail predicated */
+            uint32_t a[16], v[16];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) a[q] = aoff[i + q];
+            for (int q = 0; q < 16; ++q) a[q] = aoff[min(i + q, g1 - 1)];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const uint32_t*>(base + (a[q] + lane4));
+            for (int q = 0; q < 16; ++q)
+                v[q] = i + q < g1 ? *reinterpret_cast<const uint32_t*>(base + (a[q] + lane4)) : 0u;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) acc |= v[q];
+            for (int q = 0; q < 16; ++q) acc |= v[q];
         }
-        for (; i < g1; ++i) acc |= *reinterpret_cast<const uint32_t*>(base + (aoff[i] + lane4));
     }
     if (!valid) acc = 0;
     bool inc = false;
@@ -368,27 +375,38 @@ static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx
             const int g0 = ot[w], g1 = ot[w + 1];
             if (g0 == g1) continue;
             uint32_t H = 0, T = 0;
-            if (w == d) { /* the direct arc: tight for the source u itself */
-                for (int i = g0; i < g1; ++i) {
-                    const int us = (int)(arcs[i] & 0xFFFFu) - src0;
-                    if ((unsigned)us < (unsigned)nsrc && (us >> 5) == word)
-                        take(pend & (1u << (us & 31)), H, T, i);
+            if (w == d) {
+                /* the direct arc (u, t): tight for the source u itself. 64 arcs per step, one per
+                 * lane; the few whose source lies in this unit's chunk (~2 of C4's ~33 per
+                 * weight) go to the lane owning the source's word. Distinct arcs have distinct
+                 * sources, so there are no ties here and the order does not matter. */
+                const int cw0 = c * 64 * 32; /* the chunk's first source (local index) */
+                for (int i0 = g0; i0 < g1; i0 += 64) {
+                    const int i = i0 + lane;
+                    const int us = i < g1 ? (int)(arcs[i] & 0xFFFFu) - src0 : -1;
+                    unsigned long long m =
+                        __ballot(us >= 0 && us < nsrc && (unsigned)(us - cw0) < 64u * 32u);
+                    while (m) {
+                        const int j = __builtin_ctzll(m);
+                        m &= m - 1ull;
+                        const int uj = __builtin_amdgcn_readlane(us, j);
+                        if ((uj >> 5) == word) take(pend & (1u << (uj & 31)), H, T, i0 + j);
+                    }
                 }
-            } else { /* eight gathers in flight, then their candidates in arc order */
+            } else { /* sixteen gathers in flight (a predicated tail), then their candidates in
+                      * arc order */
                 const char* base = reinterpret_cast<const char*>(lev + (size_t)(d - w - 1) * plane);
-                int i = g0;
-                for (; i + 8 <= g1; i += 8) {
-                    uint32_t a[8], v[8];
+                for (int i = g0; i < g1; i += 16) {
+                    uint32_t a[16], v[16];
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) a[q] = aoff[i + q];
+                    for (int q = 0; q < 16; ++q) a[q] = aoff[min(i + q, g1 - 1)];
 #pragma unroll
-                    for (int q = 0; q < 8; ++q)
-                        v[q] = *reinterpret_cast<const uint32_t*>(base + (a[q] + lane4));
+                    for (int q = 0; q < 16; ++q)
+                        v[q] = i + q < g1 ? *reinterpret_cast<const uint32_t*>(base + (a[q] + lane4))
+                                          : 0u;
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) take(v[q] & pend, H, T, i + q);
+                    for (int q = 0; q < 16; ++q) take(v[q] & pend, H, T, i + q);
                 }
-                for (; i < g1; ++i)
-                    take(*reinterpret_cast<const uint32_t*>(base + (aoff[i] + lane4)) & pend, H, T, i);
             }
             tied += __builtin_popcount(T);
             pend &= ~H;
