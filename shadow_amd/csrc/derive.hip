@@ -27,6 +27,7 @@
 #define DV_LMAX 2048  /* distance levels of the ordered pass (the workgroup kernel's rows end at
                        * 1,022 quanta, a derived row at 1,022 + 127) */
 #define DV_WG_PER_CU 8
+#define DV_JB 4       /* targets per thread per phase-B step of the on-demand form */
 
 /* order of canonical arcs u | w << 17 | ridx << 24: the largest w, then the smallest u */
 static __device__ __forceinline__ uint32_t dv_key(uint32_t code) {
@@ -296,13 +297,12 @@ __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
         }
         __threadfence_block();
         __syncthreads();
-        /* phase B: on-demand path-order products */
-        for (int t = tid; t < n; t += DV_THREADS) {
-            if (is_done((uint32_t)t)) continue;
-            uint32_t ct = cs[t];
+        /* target t (its code ct) once its predecessor is not formed: climb to the first ancestor
+         * whose predecessor is, form it, and repeat until t is formed */
+        auto climb = [&](int t, uint32_t ct) {
             for (;;) {
                 uint32_t y = (uint32_t)t, cy = ct;
-                while (!is_done(cy & 0x1FFFFu)) { /* climb to the first formable ancestor */
+                while (!is_done(cy & 0x1FFFFu)) {
                     y = cy & 0x1FFFFu;
                     cy = cs[y];
                 }
@@ -315,9 +315,49 @@ __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
                 atomicOr(&cdone[y >> 5], 1u << (y & 31));
                 if (y == (uint32_t)t) break;
             }
+        };
+        /* phase B: on-demand path-order products. DV_JB targets per thread per step: their
+         * codes, then the predecessors' values of the ready ones, in flight together; a target
+         * whose predecessor is not formed yet climbs alone */
+        for (int t0 = 0; t0 < n; t0 += DV_JB * DV_THREADS) {
+            uint32_t cj[DV_JB];
+            bool rdy[DV_JB];
+#pragma unroll
+            for (int j = 0; j < DV_JB; ++j) {
+                const int t = t0 + j * DV_THREADS + tid;
+                cj[j] = (t < n && !is_done((uint32_t)t)) ? cs[t] : ~0u;
+            }
+#pragma unroll
+            for (int j = 0; j < DV_JB; ++j) rdy[j] = cj[j] != ~0u && is_done(cj[j] & 0x1FFFFu);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            double rp[DV_JB];
+#pragma unroll
+            for (int j = 0; j < DV_JB; ++j)
+                rp[j] = rdy[j] ? __hip_atomic_load(orr + (cj[j] & 0x1FFFFu), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP)
+                               : 0.0;
+#pragma unroll
+            for (int j = 0; j < DV_JB; ++j)
+                if (rdy[j])
+                    __hip_atomic_store(orr + t0 + j * DV_THREADS + tid, rp[j] * s_tab[cj[j] >> 24],
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#pragma unroll
+            for (int j = 0; j < DV_JB; ++j)
+                if (rdy[j]) {
+                    const int t = t0 + j * DV_THREADS + tid;
+                    atomicOr(&cdone[t >> 5], 1u << (t & 31));
+                }
+#pragma unroll
+            for (int j = 0; j < DV_JB; ++j) {
+                const int t = t0 + j * DV_THREADS + tid;
+                if (cj[j] == ~0u || rdy[j] || is_done((uint32_t)t)) continue;
+                climb(t, cj[j]);
+            }
         }
     }
 }
+
 
 /* The rows of the nI sources I (device list) by derivation, into lat / rel rows placed by source
  * (row v - src_begin, stride ldo), from the core rows already there and their codes (row crow[k]

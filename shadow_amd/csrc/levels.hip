@@ -206,7 +206,7 @@ static __device__ __forceinline__ void lvl_step_unit(unsigned g, int d, int n, i
         for (int i = oj[w]; i < g1; i += 16) { /* sixteen in flight, the tail predicated */
             uint32_t a[16], v[16];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) a[q] = aoff[min(i + q, g1 - 1)];
+            for (int q = 0; q < 16; ++q) a[q] = aoff[i + q]; /* padded: one scalar burst */
 #pragma unroll
             for (int q = 0; q < 16; ++q)
                 v[q] = i + q < g1 ? *reinterpret_cast<const uint32_t*>(base + (a[q] + lane4)) : 0u;
@@ -399,7 +399,7 @@ static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx
                 for (int i = g0; i < g1; i += 16) {
                     uint32_t a[16], v[16];
 #pragma unroll
-                    for (int q = 0; q < 16; ++q) a[q] = aoff[min(i + q, g1 - 1)];
+                    for (int q = 0; q < 16; ++q) a[q] = aoff[i + q]; /* padded: one scalar burst */
 #pragma unroll
                     for (int q = 0; q < 16; ++q)
                         v[q] = i + q < g1 ? *reinterpret_cast<const uint32_t*>(base + (a[q] + lane4))
@@ -687,7 +687,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     ar = ar2;
     /* level state over the local sources */
     uint32_t* aoff = NULL;
-    LVL_ALLOC(aoff, ((size_t)total + 8) * sizeof(uint32_t));
+    LVL_ALLOC(aoff, ((size_t)total + 16) * sizeof(uint32_t)); /* + a 16-arc batch's tail */
     if (total > 0) {
         lvl_aoff_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, nw, arcs, aoff);
         SRT_HIPCHK(hipGetLastError());
