@@ -208,16 +208,20 @@ __global__ __launch_bounds__(DV_THREADS, 8) void derive_rows_kernel(
  * stored (workgroup release/acquire), so a value is read only once final; two threads that form
  * the same vertex store the same product. The ancestors near s are shared by most chains and
  * stay in cache; no list, no per-level barrier. */
+template <bool GDONE>
 __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
     int n, int nI, const int32_t* __restrict__ I, int src_begin, const int2* __restrict__ rowptr,
     const uint2* __restrict__ cw, const uint8_t* __restrict__ ridx, const double* __restrict__ rtab,
     int ntab, const int32_t* __restrict__ crow, const uint32_t* __restrict__ codes,
     uint32_t* __restrict__ lat, double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ cs_all,
-    size_t lds_n) {
-    extern __shared__ uint32_t cdone[]; /* one bit per target */
+    size_t lds_n, uint32_t* __restrict__ done_all) {
+    /* the done bits: LDS, or (GDONE: beside the workgroup SSSP kernel, whose LDS row leaves
+     * ~11 KB of the CU's LDS) a global scratch row per workgroup */
+    extern __shared__ uint32_t ldone[];
     __shared__ double s_tab[256];
     __shared__ int s_nb[DV_MAXDEG], s_w[DV_MAXDEG], s_rx[DV_MAXDEG], s_cr[DV_MAXDEG];
     const int tid = threadIdx.x, nw = (n + 31) >> 5;
+    uint32_t* cdone = GDONE ? done_all + (size_t)blockIdx.x * (size_t)((nw + 31) & ~31) : ldone;
     for (int i = tid; i < ntab; i += DV_THREADS) s_tab[i] = rtab[i];
     uint32_t* cs = cs_all + (size_t)blockIdx.x * lds_n;
     auto is_done = [&](uint32_t v) {
@@ -239,6 +243,7 @@ __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
             s_cr[tid] = crow[e.x];
         }
         for (int q = tid; q < nw; q += DV_THREADS) cdone[q] = 0u;
+        __threadfence_block();
         __syncthreads();
         /* phase A (as derive_rows_kernel): distances, derived codes; s and the unreachable
          * targets are done at once */
@@ -291,7 +296,8 @@ __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
                 cs[t] = best;
                 if (t == s || D[j] >= SRT_INF) {
                     orr[t] = t == s ? 1.0 : 0.0;
-                    atomicOr(&cdone[t >> 5], 1u << (t & 31));
+                    __hip_atomic_fetch_or(&cdone[t >> 5], 1u << (t & 31), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
         }
@@ -312,7 +318,8 @@ __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
                 __hip_atomic_store(orr + y, rp * s_tab[cy >> 24], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                atomicOr(&cdone[y >> 5], 1u << (y & 31));
+                __hip_atomic_fetch_or(&cdone[y >> 5], 1u << (y & 31), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (y == (uint32_t)t) break;
             }
         };
@@ -346,7 +353,8 @@ __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
             for (int j = 0; j < DV_JB; ++j)
                 if (rdy[j]) {
                     const int t = t0 + j * DV_THREADS + tid;
-                    atomicOr(&cdone[t >> 5], 1u << (t & 31));
+                    __hip_atomic_fetch_or(&cdone[t >> 5], 1u << (t & 31), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
 #pragma unroll
             for (int j = 0; j < DV_JB; ++j) {
@@ -363,14 +371,15 @@ __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
  * (row v - src_begin, stride ldo), from the core rows already there and their codes (row crow[k]
  * of codes, stride n). rowptr / cw / ridx: the original-order CSR with each arc's index into
  * rtab (ntab <= 256 distinct reliabilities). Every source of I has degree <= DV_MAXDEG and every
- * neighbour is a core vertex (the caller's independent set). Waits for the kernel: *fallback = 1
- * when a derived distance passed the ordered pass's levels (the caller then builds I's rows with
- * the SSSP kernel). */
-int srt_derive_rows(int n, int nI, const int32_t* I, int src_begin, const int2* rowptr,
-                    const uint2* cw, const uint8_t* ridx, const double* rtab, int ntab,
-                    const int32_t* crow, const uint32_t* codes, uint32_t* lat, double* rel,
-                    size_t ldo, hipStream_t st, int* fallback) {
-    *fallback = 0;
+ * neighbour is a core vertex (the caller's independent set). Stream-ordered, no wait: *bad
+ * (device) becomes 1 when a derived distance passed the ordered form's levels (the caller then
+ * builds I's rows with the SSSP kernel). beside: the SSSP kernel may run at the same time on
+ * another stream (the on-demand form with its done bits in global memory, a few workgroups per
+ * CU). */
+int srt_derive_rows_async(int n, int nI, const int32_t* I, int src_begin, const int2* rowptr,
+                          const uint2* cw, const uint8_t* ridx, const double* rtab, int ntab,
+                          const int32_t* crow, const uint32_t* codes, uint32_t* lat, double* rel,
+                          size_t ldo, hipStream_t st, int* bad, int beside) {
     if (nI <= 0) return SRT_OK;
     if (ntab > 256) {
         srt_set_error("derive: %d distinct reliabilities (at most 256)", ntab);
@@ -380,34 +389,34 @@ int srt_derive_rows(int n, int nI, const int32_t* I, int src_begin, const int2* 
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
         cus = prop.multiProcessorCount;
-    const int grid = nI < DV_WG_PER_CU * cus ? nI : DV_WG_PER_CU * cus;
+    const bool chain = srt_form_int("dv_chain", 1) != 0 || beside;
+    const int per = chain ? srt_form_int("dv_wg", beside ? 2 : 4) : DV_WG_PER_CU;
+    const int grid = nI < per * cus ? nI : per * cus;
     const size_t np = ((size_t)n + 3) & ~(size_t)3;
+    const size_t nwp = ((size_t)((n + 31) / 32) + 31) & ~(size_t)31;
     uint32_t* cs = NULL;
     uint2* lst = NULL;
-    int* bad = NULL;
+    uint32_t* done = NULL;
     SRT_HIPCHK(srt_malloc_async(&cs, (size_t)grid * np * sizeof(uint32_t), st));
-    SRT_HIPCHK(srt_malloc_async(&lst, (size_t)grid * np * sizeof(uint2), st));
-    SRT_HIPCHK(srt_malloc_async(&bad, sizeof(int), st));
-    SRT_HIPCHK(hipMemsetAsync(bad, 0, sizeof(int), st));
-    if (srt_form_int("dv_chain", 1)) {
-        /* on-demand products (derive_chain_kernel): SRT_FORM dv_wg workgroups per CU */
-        const int per = srt_form_int("dv_wg", 4);
-        const int g2 = nI < per * cus ? nI : per * cus;
+    if (chain && beside) {
+        SRT_HIPCHK(srt_malloc_async(&done, (size_t)grid * nwp * sizeof(uint32_t), st));
+        derive_chain_kernel<true><<<grid, DV_THREADS, 0, st>>>(
+            n, nI, I, src_begin, rowptr, cw, ridx, rtab, ntab, crow, codes, lat, rel, ldo, cs, np, done);
+    } else if (chain) {
         const size_t lds = (size_t)((n + 31) / 32) * sizeof(uint32_t);
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)derive_chain_kernel,
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)derive_chain_kernel<false>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        derive_chain_kernel<<<g2 < grid ? g2 : grid, DV_THREADS, lds, st>>>(
-            n, nI, I, src_begin, rowptr, cw, ridx, rtab, ntab, crow, codes, lat, rel, ldo, cs, np);
+        derive_chain_kernel<false><<<grid, DV_THREADS, lds, st>>>(
+            n, nI, I, src_begin, rowptr, cw, ridx, rtab, ntab, crow, codes, lat, rel, ldo, cs, np, NULL);
     } else {
+        SRT_HIPCHK(srt_malloc_async(&lst, (size_t)grid * np * sizeof(uint2), st));
         derive_rows_kernel<<<grid, DV_THREADS, 0, st>>>(n, nI, I, src_begin, rowptr, cw, ridx, rtab,
                                                         ntab, crow, codes, lat, rel, ldo, cs, lst, np,
                                                         bad, srt_form_int("dv_phases", 3));
     }
     SRT_HIPCHK(hipGetLastError());
-    SRT_HIPCHK(hipMemcpyAsync(fallback, bad, sizeof(int), hipMemcpyDeviceToHost, st));
     SRT_HIPCHK(hipFreeAsync(cs, st));
-    SRT_HIPCHK(hipFreeAsync(lst, st));
-    SRT_HIPCHK(hipFreeAsync(bad, st));
-    SRT_HIPCHK(hipStreamSynchronize(st));
+    if (lst) SRT_HIPCHK(hipFreeAsync(lst, st));
+    if (done) SRT_HIPCHK(hipFreeAsync(done, st));
     return SRT_OK;
 }
