@@ -135,13 +135,9 @@ struct srt_sparse_graph {
     int32_t nI, ncore;
     int32_t *dI, *dcore, *crow;
     int32_t ntab; /* entries of rtab */
-    /* pipelining: the core list in DV_CHUNKS chunks [core_chunk[c], core_chunk[c + 1]); I ordered
-     * by the chunk of its last neighbour, group c = [I_group[c], I_group[c + 1]) */
-    int32_t core_chunk[9], I_group[9];
 };
 
 #define DERIVE_MAXDEG 4 /* <= derive.hip's DV_MAXDEG */
-#define DV_CHUNKS 8
 
 int srt_wgsssp_max_n(void);
 int srt_wide_rows(int n, const int32_t* rp, const int32_t* col, const uint32_t* w, const double* r,
@@ -156,7 +152,7 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
 int srt_derive_rows_async(int n, int nI, const int32_t* I, int src_begin, const int2* rowptr,
                           const uint2* cw, const uint8_t* ridx, const double* rtab, int ntab,
                           const int32_t* crow, const uint32_t* codes, uint32_t* lat, double* rel,
-                          size_t ldo, hipStream_t st, int* bad, int beside);
+                          size_t ldo, hipStream_t st);
 int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, const double* r,
                    const int2* in_rowptr, const uint2* in_cw, const double* in_r,
                    const int32_t* perm, const int32_t* inv, uint32_t max_w, int local,
@@ -301,34 +297,7 @@ static int derive_sets(const srt_canon* c, srt_sparse_graph* g) {
     }
     g->nI = (int32_t)I.size();
     g->ncore = (int32_t)core.size();
-    /* the core list in DV_CHUNKS equal chunks (ascending vertex order: BA hubs, the neighbours
-     * of most of I, come first), I sorted by the chunk of its last neighbour */
-    for (int ch = 0; ch <= DV_CHUNKS; ch++)
-        g->core_chunk[ch] = (int32_t)((int64_t)g->ncore * ch / DV_CHUNKS);
-    auto chunk_of = [&](int k) {
-        const int i = crow[k];
-        int ch = 0;
-        while (ch + 1 < DV_CHUNKS && g->core_chunk[ch + 1] <= i) ch++;
-        return ch;
-    };
-    std::vector<int32_t> grp(I.size());
-    for (size_t q = 0; q < I.size(); q++) {
-        const int v = I[q];
-        int ch = 0;
-        for (int k = c->rowptr[v]; k < c->rowptr[v + 1]; k++) ch = std::max(ch, chunk_of(c->col[k]));
-        grp[q] = ch;
-    }
-    std::vector<int32_t> Is(I.size());
-    {
-        int pos = 0;
-        for (int ch = 0; ch < DV_CHUNKS; ch++) {
-            g->I_group[ch] = pos;
-            for (size_t q = 0; q < I.size(); q++)
-                if (grp[q] == ch) Is[pos++] = I[q];
-        }
-        g->I_group[DV_CHUNKS] = pos;
-    }
-    I.swap(Is);
+
     int rc = up((void**)&g->dI, I.data(), I.size() * 4);
     if (!rc) rc = up((void**)&g->dcore, core.data(), core.size() * 4);
     if (!rc) rc = up((void**)&g->crow, crow.data(), (size_t)n * 4);
@@ -624,78 +593,31 @@ static void ms_clusters(const srt_sparse_graph* g, const int32_t* rowof, int nsr
  * source. lms (optional): the f64 path-order ms rows (tables.hip), q the quantum in ns. */
 /* Every row of an undirected graph, placed by source (row v = v): the core rows by the workgroup
  * kernel, with their canonical arcs, then the independent set's rows by derivation (derive.hip).
- * Pipelined: the core list runs in DV_CHUNKS chunks on the build stream; the set's vertices whose
- * neighbours are all in chunks <= c (g->dIg, grouped at graph build) are derived on a second
- * stream as soon as chunk c is done, beside the kernel's next chunk (the workgroup kernel is a
- * latency chain with HBM to spare). A core source whose buckets overflowed has no codes: then
- * the set's rows take the kernel too. */
+ * A core source whose buckets overflowed has no codes: then the set's rows take the kernel too.
+ * (Deriving each chunk's ready set on a second stream beside the kernel's next chunk measured
+ * slower: 829 vs 529 ms on C5.) */
 static int sparse_rows_derived(const srt_sparse_graph* g, uint32_t* lat_rows, double* rel_rows,
                                int* ovf, hipStream_t st) {
     const int n = g->n;
-    struct res {
-        hipStream_t s2 = nullptr;
-        hipEvent_t ev[DV_CHUNKS + 1] = {};
-        uint32_t* codes = nullptr;
-        int* bad = nullptr;
-        hipStream_t st;
-        ~res() {
-            if (codes) (void)hipFreeAsync(codes, st);
-            if (bad) (void)hipFreeAsync(bad, st);
-            for (hipEvent_t e : ev)
-                if (e) (void)hipEventDestroy(e);
-            if (s2) (void)hipStreamDestroy(s2);
-        }
-    } r;
-    r.st = st;
-    SRT_HIPCHK(srt_malloc_async(&r.codes, (size_t)g->ncore * n * sizeof(uint32_t), st));
-    SRT_HIPCHK(srt_malloc_async(&r.bad, sizeof(int), st));
-    SRT_HIPCHK(hipMemsetAsync(r.bad, 0, sizeof(int), st));
+    uint32_t* codes = NULL;
+    SRT_HIPCHK(srt_malloc_async(&codes, (size_t)g->ncore * n * sizeof(uint32_t), st));
     SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)n * sizeof(int), st));
-    const bool pipe = srt_form_int("dv_pipe", 0) != 0; /* measured slower (829 vs 529 ms on C5) */
-    if (pipe) {
-        SRT_HIPCHK(hipStreamCreateWithFlags(&r.s2, hipStreamNonBlocking));
-        for (int c = 0; c <= DV_CHUNKS; c++)
-            SRT_HIPCHK(hipEventCreateWithFlags(&r.ev[c], hipEventDisableTiming));
-    }
-    int rc = SRT_OK;
-    const int nch = pipe ? DV_CHUNKS : 1;
-    for (int c = 0; c < nch && !rc; c++) {
-        const int k0 = pipe ? g->core_chunk[c] : 0, k1 = pipe ? g->core_chunk[c + 1] : g->ncore;
-        if (k1 > k0)
-            rc = srt_wgsssp_rows(n, g->rpo, g->cw, g->r, NULL, g->max_w, 0, k1 - k0, g->dcore + k0,
-                                 lat_rows, rel_rows, ovf, st, g->ridx, g->rtab, 1,
-                                 r.codes + (size_t)k0 * n);
-        if (rc || !pipe) break;
-        /* the set's group c (every neighbour in chunks <= c) beside the next chunk */
-        SRT_HIPCHK(hipEventRecord(r.ev[c], st));
-        SRT_HIPCHK(hipStreamWaitEvent(r.s2, r.ev[c], 0));
-        const int i0 = g->I_group[c], i1 = g->I_group[c + 1];
-        if (i1 > i0)
-            rc = srt_derive_rows_async(n, i1 - i0, g->dI + i0, 0, g->rpo, g->cw, g->ridx, g->rtab,
-                                       g->ntab, g->crow, r.codes, lat_rows, rel_rows, (size_t)n,
-                                       r.s2, r.bad, 1);
-    }
-    if (!rc && pipe) { /* the build stream waits for the last group */
-        SRT_HIPCHK(hipEventRecord(r.ev[DV_CHUNKS], r.s2));
-        SRT_HIPCHK(hipStreamWaitEvent(st, r.ev[DV_CHUNKS], 0));
-    } else if (!rc) {
-        rc = srt_derive_rows_async(n, g->nI, g->dI, 0, g->rpo, g->cw, g->ridx, g->rtab, g->ntab,
-                                   g->crow, r.codes, lat_rows, rel_rows, (size_t)n, st, r.bad, 0);
-    }
-    if (rc) {
-        (void)hipStreamSynchronize(st);
-        return rc;
-    }
+    int rc = srt_wgsssp_rows(n, g->rpo, g->cw, g->r, NULL, g->max_w, 0, g->ncore, g->dcore, lat_rows,
+                             rel_rows, ovf, st, g->ridx, g->rtab, 1, codes);
     std::vector<int> hov((size_t)n);
-    int hbad = 0;
-    SRT_HIPCHK(hipMemcpyAsync(hov.data(), ovf, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, st));
-    SRT_HIPCHK(hipMemcpyAsync(&hbad, r.bad, sizeof(int), hipMemcpyDeviceToHost, st));
-    SRT_HIPCHK(hipStreamSynchronize(st));
-    bool fallback = hbad != 0;
-    for (int v = 0; v < n && !fallback; v++) fallback = hov[v] != 0;
-    if (fallback) /* (the set's flags are still 0: every flag is a core row's) */
+    if (!rc && hipMemcpyAsync(hov.data(), ovf, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, st) !=
+                   hipSuccess)
+        rc = SRT_E_DEVICE;
+    if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = SRT_E_DEVICE;
+    bool core_ovf = false;
+    for (int v = 0; v < n && !rc; v++) core_ovf |= hov[v] != 0;
+    if (!rc && core_ovf) /* (the set's flags are still 0: every flag is a core row's) */
         rc = srt_wgsssp_rows(n, g->rpo, g->cw, g->r, NULL, g->max_w, 0, g->nI, g->dI, lat_rows,
                              rel_rows, ovf, st, g->ridx, g->rtab, 1, NULL);
+    else if (!rc)
+        rc = srt_derive_rows_async(n, g->nI, g->dI, 0, g->rpo, g->cw, g->ridx, g->rtab, g->ntab,
+                                   g->crow, codes, lat_rows, rel_rows, (size_t)n, st);
+    (void)hipFreeAsync(codes, st);
     return rc;
 }
 

@@ -24,9 +24,7 @@
 #define DV_THREADS 256
 #define DV_MAXDEG 4   /* largest degree the host puts in I (build.hip DERIVE_MAXDEG) */
 #define DV_J 2        /* targets per thread per phase-A step: their loads overlap */
-#define DV_LMAX 2048  /* distance levels of the ordered pass (the workgroup kernel's rows end at
-                       * 1,022 quanta, a derived row at 1,022 + 127) */
-#define DV_WG_PER_CU 8
+#define DV_WG_PER_CU 4
 #define DV_JB 4       /* targets per thread per phase-B step of the on-demand form */
 
 /* order of canonical arcs u | w << 17 | ridx << 24: the largest w, then the smallest u */
@@ -34,194 +32,27 @@ static __device__ __forceinline__ uint32_t dv_key(uint32_t code) {
     return ((127u - ((code >> 17) & 0x7Fu)) << 17) | (code & 0x1FFFFu);
 }
 
-/* One workgroup per derived source (persistent grid over I, DV_WG_PER_CU resident per CU: a
- * row's ordered pass is a chain of short levels, and the other rows of the CU fill its waits).
- * Rows are placed by source: row of vertex v = v - src_begin, in lat / rel (stride ldo); core
- * vertex k's codes are row crow[k] of codes (stride n). Per workgroup scratch: cs (n codes) and
- * lst (n (target, code) entries, ordered by distance). *bad = 1 if a distance reached DV_LMAX
- * (the caller then builds these rows with the kernel). */
-__global__ __launch_bounds__(DV_THREADS, 8) void derive_rows_kernel(
-    int n, int nI, const int32_t* __restrict__ I, int src_begin, const int2* __restrict__ rowptr,
-    const uint2* __restrict__ cw, const uint8_t* __restrict__ ridx, const double* __restrict__ rtab,
-    int ntab, const int32_t* __restrict__ crow, const uint32_t* __restrict__ codes,
-    uint32_t* __restrict__ lat, double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ cs_all,
-    uint2* __restrict__ lst_all, size_t lds_n, int* __restrict__ bad, int phases) {
-    __shared__ uint32_t s_start[DV_LMAX + 1]; /* first entry of each level in lst */
-    __shared__ uint32_t s_cur[DV_LMAX];       /* counts, then scatter cursors */
-    __shared__ double s_tab[256];
-    __shared__ int s_nb[DV_MAXDEG], s_w[DV_MAXDEG], s_rx[DV_MAXDEG], s_cr[DV_MAXDEG];
-    __shared__ uint32_t s_maxd;
-    __shared__ int s_big;
-    const int tid = threadIdx.x;
-    for (int i = tid; i < ntab; i += DV_THREADS) s_tab[i] = rtab[i];
-    uint32_t* cs = cs_all + (size_t)blockIdx.x * lds_n;
-    uint2* lst = lst_all + (size_t)blockIdx.x * lds_n;
-    for (int si = blockIdx.x; si < nI; si += gridDim.x) {
-        const int s = I[si];
-        uint32_t* ol = lat + (size_t)(s - src_begin) * ldo;
-        double* orr = rel + (size_t)(s - src_begin) * ldo;
-        const int2 be = rowptr[s];
-        const int deg = min(be.y - be.x, DV_MAXDEG);
-        __syncthreads(); /* the previous source is done with the shared state */
-        if (tid < deg) {
-            const uint2 e = cw[be.x + tid];
-            s_nb[tid] = (int)e.x;
-            s_w[tid] = (int)e.y;
-            s_rx[tid] = ridx[be.x + tid];
-            s_cr[tid] = crow[e.x];
-        }
-        for (int q = tid; q < DV_LMAX; q += DV_THREADS) s_cur[q] = 0u;
-        if (tid == 0) {
-            s_maxd = 0u;
-            s_big = 0;
-        }
-        __syncthreads();
-        /* phase A: distances and derived codes, DV_J targets per thread at a time (the deg row
-         * loads of all of them in flight together, then the codes of the tight neighbours);
-         * the histogram of the distances */
-        uint32_t mymax = 0;
-        for (int t0 = 0; t0 < n; t0 += DV_J * DV_THREADS) {
-            uint32_t dk[DV_J][DV_MAXDEG];
-#pragma unroll
-            for (int j = 0; j < DV_J; ++j) {
-                const int t = t0 + j * DV_THREADS + tid;
-#pragma unroll
-                for (int i = 0; i < DV_MAXDEG; ++i)
-                    dk[j][i] = (i < deg && t < n)
-                                   ? lat[(size_t)(s_nb[i] - src_begin) * ldo + t]
-                                   : SRT_INF;
-            }
-            uint32_t D[DV_J];
-#pragma unroll
-            for (int j = 0; j < DV_J; ++j) {
-                D[j] = SRT_INF;
-#pragma unroll
-                for (int i = 0; i < DV_MAXDEG; ++i)
-                    if (dk[j][i] < SRT_INF) D[j] = min(D[j], (uint32_t)s_w[i] + dk[j][i]);
-            }
-            uint32_t cd[DV_J][DV_MAXDEG];
-#pragma unroll
-            for (int j = 0; j < DV_J; ++j) {
-                const int t = t0 + j * DV_THREADS + tid;
-#pragma unroll
-                for (int i = 0; i < DV_MAXDEG; ++i) {
-                    cd[j][i] = ~0u;
-                    if (dk[j][i] < SRT_INF && (uint32_t)s_w[i] + dk[j][i] == D[j])
-                        cd[j][i] = t == s_nb[i]
-                                       ? ((uint32_t)s | ((uint32_t)s_w[i] << 17) |
-                                          ((uint32_t)s_rx[i] << 24))
-                                       : codes[(size_t)s_cr[i] * n + t];
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < DV_J; ++j) {
-                const int t = t0 + j * DV_THREADS + tid;
-                if (t >= n) continue;
-                uint32_t best = ~0u, bk = ~0u;
-#pragma unroll
-                for (int i = 0; i < DV_MAXDEG; ++i)
-                    if (cd[j][i] != ~0u && dv_key(cd[j][i]) < bk) {
-                        bk = dv_key(cd[j][i]);
-                        best = cd[j][i];
-                    }
-                if (t == s) D[j] = 0;
-                ol[t] = D[j];
-                cs[t] = best;
-                if (t == s || D[j] >= SRT_INF) { /* the source, or unreachable */
-                    orr[t] = t == s ? 1.0 : 0.0;
-                } else if (D[j] < DV_LMAX) {
-                    atomicAdd(&s_cur[D[j]], 1u);
-                    mymax = max(mymax, D[j]);
-                } else {
-                    s_big = 1;
-                }
-            }
-        }
-        if (mymax) atomicMax(&s_maxd, mymax);
-        __syncthreads();
-        if (s_big) { /* uniform: the caller rebuilds the set's rows with the kernel */
-            if (tid == 0) *bad = 1;
-            continue;
-        }
-        const uint32_t maxd = s_maxd;
-        if (phases < 2) continue; /* tools (SRT_FORM dv_phases=1): phase A alone, for timing */
-        /* exclusive scan of the level counts into s_start (cursors = starts): DV_LMAX / 256
-         * consecutive levels per thread, a wave scan of the partial sums, then the waves' */
-        {
-            constexpr int PERT = DV_LMAX / DV_THREADS;
-            const int lane = tid & 63, wv = tid >> 6;
-            uint32_t part = 0;
-#pragma unroll
-            for (int q = 0; q < PERT; ++q) part += s_cur[tid * PERT + q];
-            uint32_t inc = part;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
-                if (lane >= o) inc += y;
-            }
-            __shared__ uint32_t s_wsum[DV_THREADS / 64];
-            if (lane == 63) s_wsum[wv] = inc;
-            __syncthreads();
-            uint32_t acc = inc - part;
-            for (int i = 0; i < wv; ++i) acc += s_wsum[i];
-#pragma unroll
-            for (int q = 0; q < PERT; ++q) {
-                const int L = tid * PERT + q;
-                const uint32_t c = s_cur[L];
-                s_start[L] = acc;
-                s_cur[L] = acc;
-                acc += c;
-            }
-            if (tid == DV_THREADS - 1) s_start[DV_LMAX] = acc;
-        }
-        __syncthreads();
-        /* phase A2: the reachable targets into lst, grouped by distance (any order inside a
-         * level: every arc is >= 1 quantum, so a target's predecessor is in an earlier level) */
-        for (int t = tid; t < n; t += DV_THREADS) {
-            const uint32_t d = ol[t];
-            if (t == s || d >= SRT_INF) continue;
-            const uint32_t pos = atomicAdd(&s_cur[d], 1u);
-            lst[pos] = make_uint2((uint32_t)t, cs[t]);
-        }
-        __threadfence_block();
-        __syncthreads();
-        if (phases < 3) continue; /* tools: phases A and A2 */
-        /* phase B: rel(s,t) = rel(s,u) * r(u,t) level by level (path order from s; rel(s,s) = 1
-         * was written in phase A, so the direct arc needs no case) */
-        for (uint32_t L = 1; L <= maxd; ++L) {
-            const uint32_t b = s_start[L], e = s_start[L + 1];
-            if (b == e) continue; /* uniform */
-            for (uint32_t q = b + tid; q < e; q += DV_THREADS) {
-                const uint2 x = lst[q];
-                const double ru = orr[x.y & 0x1FFFFu];
-                orr[x.x] = ru * s_tab[x.y >> 24];
-            }
-            __threadfence_block();
-            __syncthreads();
-        }
-    }
-}
-
-/* The same rows with the reliability formed on demand instead of level by level: a thread takes
+/* One workgroup per derived source (persistent grid over I, DV_WG_PER_CU per CU). Rows are placed
+ * by source: row of vertex v = v - src_begin, in lat / rel (stride ldo); core vertex k's codes are
+ * row crow[k] of codes (stride n); cs: n codes of scratch per workgroup. Phase A forms the
+ * distances and the derived codes; phase B the reliability on demand: a thread takes
  * its targets in index order (coalesced code reads and rel writes) and forms rel(s,t) once its
  * predecessor's is done; if not, it climbs the predecessor chain to the first vertex whose
  * predecessor is done, forms that one, and repeats. A done bit (LDS) is set after the value is
  * stored (workgroup release/acquire), so a value is read only once final; two threads that form
  * the same vertex store the same product. The ancestors near s are shared by most chains and
- * stay in cache; no list, no per-level barrier. */
-template <bool GDONE>
+ * stay in cache; no list, no per-level barrier (a distance-ordered form -- a per-row list by
+ * distance, one barrier per level -- measured 250 vs 125 ms on C5: ~200 levels per row). */
 __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
     int n, int nI, const int32_t* __restrict__ I, int src_begin, const int2* __restrict__ rowptr,
     const uint2* __restrict__ cw, const uint8_t* __restrict__ ridx, const double* __restrict__ rtab,
     int ntab, const int32_t* __restrict__ crow, const uint32_t* __restrict__ codes,
     uint32_t* __restrict__ lat, double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ cs_all,
-    size_t lds_n, uint32_t* __restrict__ done_all) {
-    /* the done bits: LDS, or (GDONE: beside the workgroup SSSP kernel, whose LDS row leaves
-     * ~11 KB of the CU's LDS) a global scratch row per workgroup */
-    extern __shared__ uint32_t ldone[];
+    size_t lds_n) {
+    extern __shared__ uint32_t cdone[]; /* one bit per target */
     __shared__ double s_tab[256];
     __shared__ int s_nb[DV_MAXDEG], s_w[DV_MAXDEG], s_rx[DV_MAXDEG], s_cr[DV_MAXDEG];
     const int tid = threadIdx.x, nw = (n + 31) >> 5;
-    uint32_t* cdone = GDONE ? done_all + (size_t)blockIdx.x * (size_t)((nw + 31) & ~31) : ldone;
     for (int i = tid; i < ntab; i += DV_THREADS) s_tab[i] = rtab[i];
     uint32_t* cs = cs_all + (size_t)blockIdx.x * lds_n;
     auto is_done = [&](uint32_t v) {
@@ -371,52 +202,31 @@ __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
  * (row v - src_begin, stride ldo), from the core rows already there and their codes (row crow[k]
  * of codes, stride n). rowptr / cw / ridx: the original-order CSR with each arc's index into
  * rtab (ntab <= 256 distinct reliabilities). Every source of I has degree <= DV_MAXDEG and every
- * neighbour is a core vertex (the caller's independent set). Stream-ordered, no wait: *bad
- * (device) becomes 1 when a derived distance passed the ordered form's levels (the caller then
- * builds I's rows with the SSSP kernel). beside: the SSSP kernel may run at the same time on
- * another stream (the on-demand form with its done bits in global memory, a few workgroups per
- * CU). */
+ * neighbour is a core vertex (the caller's independent set). Stream-ordered, no wait. */
 int srt_derive_rows_async(int n, int nI, const int32_t* I, int src_begin, const int2* rowptr,
                           const uint2* cw, const uint8_t* ridx, const double* rtab, int ntab,
                           const int32_t* crow, const uint32_t* codes, uint32_t* lat, double* rel,
-                          size_t ldo, hipStream_t st, int* bad, int beside) {
+                          size_t ldo, hipStream_t st) {
     if (nI <= 0) return SRT_OK;
-    if (ntab > 256) {
-        srt_set_error("derive: %d distinct reliabilities (at most 256)", ntab);
+    if (ntab > 256 || n > (1 << 17)) {
+        srt_set_error("derive: %d distinct reliabilities (at most 256) or n = %d past 2^17", ntab, n);
         return SRT_E_ARG;
     }
     int cus = 256, dev = 0;
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
         cus = prop.multiProcessorCount;
-    const bool chain = srt_form_int("dv_chain", 1) != 0 || beside;
-    const int per = chain ? srt_form_int("dv_wg", beside ? 2 : 4) : DV_WG_PER_CU;
-    const int grid = nI < per * cus ? nI : per * cus;
+    /* 4 workgroups per CU: 181 / 125 / 146 ms on C5 at 2 / 4 / 8 */
+    const int grid = nI < DV_WG_PER_CU * cus ? nI : DV_WG_PER_CU * cus;
     const size_t np = ((size_t)n + 3) & ~(size_t)3;
-    const size_t nwp = ((size_t)((n + 31) / 32) + 31) & ~(size_t)31;
     uint32_t* cs = NULL;
-    uint2* lst = NULL;
-    uint32_t* done = NULL;
     SRT_HIPCHK(srt_malloc_async(&cs, (size_t)grid * np * sizeof(uint32_t), st));
-    if (chain && beside) {
-        SRT_HIPCHK(srt_malloc_async(&done, (size_t)grid * nwp * sizeof(uint32_t), st));
-        derive_chain_kernel<true><<<grid, DV_THREADS, 0, st>>>(
-            n, nI, I, src_begin, rowptr, cw, ridx, rtab, ntab, crow, codes, lat, rel, ldo, cs, np, done);
-    } else if (chain) {
-        const size_t lds = (size_t)((n + 31) / 32) * sizeof(uint32_t);
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)derive_chain_kernel<false>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        derive_chain_kernel<false><<<grid, DV_THREADS, lds, st>>>(
-            n, nI, I, src_begin, rowptr, cw, ridx, rtab, ntab, crow, codes, lat, rel, ldo, cs, np, NULL);
-    } else {
-        SRT_HIPCHK(srt_malloc_async(&lst, (size_t)grid * np * sizeof(uint2), st));
-        derive_rows_kernel<<<grid, DV_THREADS, 0, st>>>(n, nI, I, src_begin, rowptr, cw, ridx, rtab,
-                                                        ntab, crow, codes, lat, rel, ldo, cs, lst, np,
-                                                        bad, srt_form_int("dv_phases", 3));
-    }
+    const size_t lds = (size_t)((n + 31) / 32) * sizeof(uint32_t);
+    SRT_HIPCHK(hipFuncSetAttribute((const void*)derive_chain_kernel,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    derive_chain_kernel<<<grid, DV_THREADS, lds, st>>>(n, nI, I, src_begin, rowptr, cw, ridx, rtab,
+                                                       ntab, crow, codes, lat, rel, ldo, cs, np);
     SRT_HIPCHK(hipGetLastError());
     SRT_HIPCHK(hipFreeAsync(cs, st));
-    if (lst) SRT_HIPCHK(hipFreeAsync(lst, st));
-    if (done) SRT_HIPCHK(hipFreeAsync(done, st));
     return SRT_OK;
 }
