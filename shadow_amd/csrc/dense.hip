@@ -848,8 +848,9 @@ __global__ __launch_bounds__(256) void pred_cols3_kernel(int n, int row0, int nl
  * flagged them), one workgroup per row, same in-place (u, r) input. A target resolves once its
  * predecessor resolved in an earlier sweep (double-buffered LDS bitmaps; the sweeps = the depth
  * of the row's predecessor tree). */
+template <typename PT = int32_t>
 __global__ __launch_bounds__(512) void rel_sweeps_kernel(int n, int ld, int row0,
-                                                         const int32_t* __restrict__ pred,
+                                                         const PT* __restrict__ pred,
                                                          double* __restrict__ rel,
                                                          int32_t* __restrict__ max_depth,
                                                          const int32_t* __restrict__ only,
@@ -861,7 +862,7 @@ __global__ __launch_bounds__(512) void rel_sweeps_kernel(int n, int ld, int row0
     int32_t* pu = smem;                                   /* n predecessor vertices */
     uint32_t* done = reinterpret_cast<uint32_t*>(smem + n); /* resolved before this sweep */
     uint32_t* fresh = done + nw;                           /* resolved during this sweep */
-    const int32_t* pg = pred + (size_t)blockIdx.x * ld;
+    const PT* pg = pred + (size_t)blockIdx.x * ld;
     double* rr = rel + (size_t)blockIdx.x * ld;
     for (int t = threadIdx.x; t < n; t += blockDim.x) pu[t] = pg[t];
     for (int q = threadIdx.x; q < nw; q += blockDim.x) {
@@ -1020,10 +1021,10 @@ static constexpr size_t rel_tree_lds(int nt, int per, int cap) {
     return (size_t)8 * nt + (size_t)2 * nt * per + (size_t)8 * cap;
 }
 
-template <int NT, int PER, typename LT>
+template <int NT, int PER, typename LT, typename PT = int32_t>
 __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
                                                       const LT* __restrict__ lat,
-                                                      const int32_t* __restrict__ pred,
+                                                      const PT* __restrict__ pred,
                                                       double* __restrict__ rel, int maxl, int cap,
                                                       int32_t* __restrict__ max_depth,
                                                       int32_t* __restrict__ sweep,
@@ -1040,12 +1041,12 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
     __shared__ uint32_t red[NT / 64], wsum[NT / 64];
     for (int q = tid; q < nw; q += NT) par[q] = 0u;
     const LT* dl = lat + (size_t)blockIdx.x * ld;
-    const int32_t* pg = pred + (size_t)blockIdx.x * ld;
+    const PT* pg = pred + (size_t)blockIdx.x * ld;
     double* rr = rel + (size_t)blockIdx.x * ld;
     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<LT*>(dl), 0, n * (int)sizeof(LT), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rp =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(pg), 0, n * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<PT*>(pg), 0, n * (int)sizeof(PT), 0x00020000);
     const __amdgpu_buffer_rsrc_t rv =
         __builtin_amdgcn_make_buffer_rsrc(rr, 0, n * 8, 0x00020000);
     uint32_t lv[PER / 4];
@@ -1060,7 +1061,11 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
             d = __builtin_amdgcn_raw_buffer_load_b8(rd, tid, i * NT, 2);
         else
             d = __builtin_amdgcn_raw_buffer_load_b32(rd, tid * 4, i * NT * 4, 2);
-        const uint32_t p = __builtin_amdgcn_raw_buffer_load_b32(rp, tid * 4, i * NT * 4, 2);
+        uint32_t p; /* int32 rows, or int16 (-1 -> 0xFFFF either way below) */
+        if constexpr (sizeof(PT) == 2)
+            p = __builtin_amdgcn_raw_buffer_load_b16(rp, tid * 2, i * NT * 2, 2);
+        else
+            p = __builtin_amdgcn_raw_buffer_load_b32(rp, tid * 4, i * NT * 4, 2);
         const uint32_t l = (tid + i * NT != s && d < SRT_INF) ? d : 0u;
         mx = max(mx, l);
         const uint32_t b = min(l, 255u) << (8 * (i & 3));
@@ -1146,26 +1151,26 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
 }
 
 /* rel_tree_kernel at the row's size class (n <= 32768) */
-template <typename LT>
-static void rel_tree_launch(int n, int ld, int row0, int lrows, const LT* d, int32_t* pred,
+template <typename LT, typename PT>
+static void rel_tree_launch(int n, int ld, int row0, int lrows, const LT* d, const PT* pred,
                             double* rel, int32_t* depth, int32_t* sweep, const int32_t* srcs,
                             hipStream_t st) {
     if (n <= 1024) {
-        rel_tree_kernel<256, 4, LT><<<lrows, 256, rel_tree_lds(256, 4, 1024), st>>>(
+        rel_tree_kernel<256, 4, LT, PT><<<lrows, 256, rel_tree_lds(256, 4, 1024), st>>>(
             n, ld, row0, d, pred, rel, 64, 1024, depth, sweep, srcs);
     } else if (n <= 4096) {
         const int lds = (int)rel_tree_lds(512, 8, 4096);
-        (void)hipFuncSetAttribute((const void*)rel_tree_kernel<512, 8, LT>,
+        (void)hipFuncSetAttribute((const void*)rel_tree_kernel<512, 8, LT, PT>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        rel_tree_kernel<512, 8, LT><<<lrows, 512, lds, st>>>(n, ld, row0, d, pred, rel, 64, 4096,
-                                                             depth, sweep, srcs);
+        rel_tree_kernel<512, 8, LT, PT><<<lrows, 512, lds, st>>>(n, ld, row0, d, pred, rel, 64, 4096,
+                                                                 depth, sweep, srcs);
     } else {
         /* 64 KB of predecessors and 7,168 parent slots (C4 rows have ~1-3k parents): 128 KB */
         const int cap = 7168, lds = (int)rel_tree_lds(1024, 32, cap);
-        (void)hipFuncSetAttribute((const void*)rel_tree_kernel<1024, 32, LT>,
+        (void)hipFuncSetAttribute((const void*)rel_tree_kernel<1024, 32, LT, PT>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        rel_tree_kernel<1024, 32, LT><<<lrows, 1024, lds, st>>>(n, ld, row0, d, pred, rel, 64, cap,
-                                                                depth, sweep, srcs);
+        rel_tree_kernel<1024, 32, LT, PT><<<lrows, 1024, lds, st>>>(n, ld, row0, d, pred, rel, 64,
+                                                                    cap, depth, sweep, srcs);
     }
 }
 
@@ -1174,13 +1179,25 @@ static void rel_tree_launch(int n, int ld, int row0, int lrows, const LT* d, int
  * the sweeps for the rows it flagged. depth, sweep: device scratch (max depth, per-row flags). */
 static int rel_rows_launch(int n, int ld, int row0, int lrows, const uint32_t* d, int32_t* pred,
                            double* rel, int32_t* depth, int32_t* sweep, const int32_t* srcs,
-                           hipStream_t st, const uint8_t* l8 = nullptr) {
+                           hipStream_t st, const uint8_t* l8 = nullptr,
+                           const int16_t* pred16 = nullptr) {
     if (lrows <= 0) return SRT_OK;
     const bool tree = n <= 32768 && srt_form_int("reltree", 1) != 0;
+    if (pred16) { /* a level build's u8 distance rows and int16 predecessor rows (n <= 32768) */
+        rel_tree_launch(n, ld, row0, lrows, l8, pred16, rel, depth, sweep, srcs, st);
+        SRT_HIPCHK(hipGetLastError());
+        const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel<int16_t>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        rel_sweeps_kernel<int16_t><<<lrows, 512, lds, st>>>(n, ld, row0, pred16, rel, depth, sweep,
+                                                            srcs);
+        SRT_HIPCHK(hipGetLastError());
+        return SRT_OK;
+    }
     if (tree && l8)
-        rel_tree_launch(n, ld, row0, lrows, l8, pred, rel, depth, sweep, srcs, st);
+        rel_tree_launch(n, ld, row0, lrows, l8, (const int32_t*)pred, rel, depth, sweep, srcs, st);
     else if (tree)
-        rel_tree_launch(n, ld, row0, lrows, d, pred, rel, depth, sweep, srcs, st);
+        rel_tree_launch(n, ld, row0, lrows, d, (const int32_t*)pred, rel, depth, sweep, srcs, st);
     else if (n <= 1024) {
         rel_levels_kernel<256, 1024><<<lrows, 256, 2048, st>>>(n, ld, row0, d, pred, rel, 64, depth,
                                                               sweep, srcs);
@@ -1201,9 +1218,10 @@ static int rel_rows_launch(int n, int ld, int row0, int lrows, const uint32_t* d
     SRT_HIPCHK(hipGetLastError());
     if (n <= 32768) {
         const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel,
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel<int32_t>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        rel_sweeps_kernel<<<lrows, 512, lds, st>>>(n, ld, row0, pred, rel, depth, sweep, srcs);
+        rel_sweeps_kernel<int32_t><<<lrows, 512, lds, st>>>(n, ld, row0, pred, rel, depth, sweep,
+                                                            srcs);
         SRT_HIPCHK(hipGetLastError());
         return SRT_OK;
     }
@@ -1294,6 +1312,8 @@ typedef struct {
      * read after the build's final wait (dense_finish_rows) */
     hipEvent_t kev[4];
     int kev_on;
+    int diag_done; /* the level post pass applied the diagonal rule itself */
+    int pred16;    /* dt holds int16 predecessor rows (level post pass, n <= 32768) */
 } dense_ws;
 
 static dense_ws g_ws[SRT_STATE_SLOTS];
@@ -1363,6 +1383,7 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
     int rc = ws_get(&ws, n);
     if (rc) return rc;
     const int lrows = max(0, min(nrows, n - row0)); /* real (non-padding) local rows */
+    ws->pred16 = 0;
     if (lvl) /* the distances came from the Dial levels: predecessors from the level planes */
         return dense_post_levels(n, ld, row0, nrows, d, rel, st, stats, ws, lrows);
     SRT_HIPCHK(hipMemsetAsync(ws->cnt, 0, (size_t)(n + 1) * sizeof(int32_t), st));
@@ -1565,9 +1586,11 @@ static int dense_post_levels(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
             return rc;
         if (kt) SRT_HIPCHK(hipEventRecord(ws->kev[1], st));
         int32_t* pred = reinterpret_cast<int32_t*>(ws->dt);
-        if (p16)
-            transpose_kernel<int16_t, int32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
-                n, nrows, reinterpret_cast<const int16_t*>(ws->predt), (size_t)nrows, pred, (size_t)ld);
+        int16_t* pred16 = p16 ? reinterpret_cast<int16_t*>(ws->dt) : nullptr;
+        ws->pred16 = p16;
+        if (p16) /* int16 rows: the reliability passes read them as they are */
+            transpose_kernel<int16_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+                n, nrows, reinterpret_cast<const int16_t*>(ws->predt), (size_t)nrows, pred16, (size_t)ld);
         else
             transpose_kernel<uint32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
                 n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows,
@@ -1579,12 +1602,15 @@ static int dense_post_levels(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
          * spans <= 64 quanta, sweeps for the rest (as dense_post); the level rows as u8 */
         if (kt) SRT_HIPCHK(hipEventRecord(ws->kev[2], st));
         if ((rc = rel_rows_launch(n, ld, row0, lrows, d, pred, rel, ws->depth, ws->cursor, nullptr,
-                                  st, srt_levels_l8())))
+                                  st, srt_levels_l8(), pred16)))
             return rc;
         if (kt) {
             SRT_HIPCHK(hipEventRecord(ws->kev[3], st));
             ws->kev_on = 1;
         }
+        /* the diagonal rule from the keys the level build's count pass took (no second read
+         * of the w rows); directed builds keep dense_diag_kernel */
+        if ((rc = srt_levels_diag(n, ld, d, rel, st, &ws->diag_done))) return rc;
     }
     srt_levels_release(st);
     if (stats) stats->ess_arcs = 0; /* no essential-arc lists in this form */
@@ -1603,7 +1629,12 @@ static int dense_finish_rows(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
                              const double* r, uint32_t* d, double* rel, hipStream_t st,
                              srt_build_stats* stats) {
     const int lrows = max(0, min(nrows, n - row0));
-    if (lrows > 0) dense_diag_kernel<<<srt_ceil_div(lrows, 4), 256, 0, st>>>(n, ld, row0, lrows, w, r, d, rel);
+    dense_ws* wsd;
+    int rcw = ws_get(&wsd, n);
+    if (rcw) return rcw;
+    if (lrows > 0 && !wsd->diag_done)
+        dense_diag_kernel<<<srt_ceil_div(lrows, 4), 256, 0, st>>>(n, ld, row0, lrows, w, r, d, rel);
+    wsd->diag_done = 0;
     SRT_HIPCHK(hipGetLastError());
     if (stats) {
         dense_ws* ws;
@@ -1932,6 +1963,12 @@ struct build_events {
 
 /* f64 path-order ms rows [row0, row0 + lrows) from the predecessor rows the post pass left in the
  * workspace (tables.hip); runs after the diagonal rule */
+__global__ void widen16_kernel(size_t cnt, const int16_t* __restrict__ in, int32_t* __restrict__ out) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt;
+         i += (size_t)gridDim.x * blockDim.x)
+        out[i] = in[i];
+}
+
 static int dense_path_ms(int32_t n, int32_t ld, int32_t row0, int32_t nrows, const uint32_t* d,
                          uint64_t q, double* lms, hipStream_t st) {
     const int lrows = max(0, min(nrows, n - row0));
@@ -1939,8 +1976,17 @@ static int dense_path_ms(int32_t n, int32_t ld, int32_t row0, int32_t nrows, con
     dense_ws* ws;
     int rc = ws_get(&ws, n);
     if (rc) return rc;
-    return srt_path_ms_rows(n, lrows, NULL, row0, d, (size_t)ld, reinterpret_cast<const int32_t*>(ws->dt),
-                            (size_t)ld, NULL, NULL, NULL, q, lms, (size_t)ld, st);
+    const int32_t* pred = reinterpret_cast<const int32_t*>(ws->dt);
+    if (ws->pred16) { /* the level post pass left int16 rows: widened into the free slab */
+        const size_t cnt = (size_t)lrows * ld;
+        const int64_t nb = srt_ceil_div((int64_t)cnt, 256);
+        widen16_kernel<<<(unsigned)(nb < 65536 ? nb : 65536), 256, 0, st>>>(
+            cnt, reinterpret_cast<const int16_t*>(ws->dt), ws->predt);
+        SRT_HIPCHK(hipGetLastError());
+        pred = ws->predt;
+    }
+    return srt_path_ms_rows(n, lrows, NULL, row0, d, (size_t)ld, pred, (size_t)ld, NULL, NULL, NULL, q,
+                            lms, (size_t)ld, st);
 }
 
 /* Dial levels (levels.hip) instead of the FW when the graph's distances are small enough for the

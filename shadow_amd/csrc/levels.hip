@@ -44,9 +44,14 @@ __global__ __launch_bounds__(256) void lvl_arcs_rows_kernel(int n, int ld, int r
                                                             const int32_t* __restrict__ off,
                                                             uint32_t* __restrict__ arcs,
                                                             const double* __restrict__ r = nullptr,
-                                                            double* __restrict__ ar = nullptr) {
+                                                            double* __restrict__ ar = nullptr,
+                                                            unsigned long long* __restrict__ dkey = nullptr) {
     __shared__ int h[LVL_STRIDE];
+    __shared__ unsigned long long s_key[4];
     const int jj = blockIdx.x, j = row0 + jj;
+    /* COUNT also takes the diagonal rule's key from the same row reads (topology.c:1431-1576, as
+     * dense_diag_kernel): min over the row's out-edges of (self-loop L, other 2L) << 32 | u */
+    unsigned long long best = ~0ull;
     for (int i = threadIdx.x; i < LVL_STRIDE; i += 256)
         h[i] = FILL ? (j < n ? off[(size_t)j * LVL_STRIDE + i] : 0) : 0;
     __syncthreads();
@@ -59,6 +64,10 @@ __global__ __launch_bounds__(256) void lvl_arcs_rows_kernel(int n, int ld, int r
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int k = k4 + q;
+                if (!FILL && k < n && x[q] < SRT_INF) {
+                    const unsigned long long lat = k == j ? x[q] : 2ull * x[q];
+                    best = min(best, (lat << 32) | (uint32_t)k);
+                }
                 if (k < n && k != j && x[q] >= 1u && x[q] <= (uint32_t)wmax) {
                     if (FILL) {
                         const int p = atomicAdd(&h[x[q]], 1);
@@ -71,8 +80,37 @@ __global__ __launch_bounds__(256) void lvl_arcs_rows_kernel(int n, int ld, int r
         }
     }
     if (FILL) return;
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long y = __shfl_xor(best, o);
+        best = y < best ? y : best;
+    }
+    if ((threadIdx.x & 63) == 0) s_key[threadIdx.x >> 6] = best;
     __syncthreads();
     for (int i = threadIdx.x; i < LVL_STRIDE; i += 256) cnt[(size_t)j * LVL_STRIDE + i] = h[i];
+    if (threadIdx.x == 0 && dkey)
+        dkey[jj] = min(min(s_key[0], s_key[1]), min(s_key[2], s_key[3]));
+}
+
+/* The diagonal rule of the held rows from the keys the count pass took: D[s][s] = the key's
+ * latency (0 with no out-edge), rel = r or r^2 (0.0), as dense_diag_kernel */
+__global__ void lvl_diag_kernel(int n, int ld, int row0, int lrows,
+                                const unsigned long long* __restrict__ dkey,
+                                const double* __restrict__ r, uint32_t* __restrict__ d,
+                                double* __restrict__ rel) {
+    const int jj = blockIdx.x * blockDim.x + threadIdx.x;
+    if (jj >= lrows) return;
+    const int v = row0 + jj;
+    const unsigned long long best = dkey[jj];
+    const size_t ix = (size_t)jj * ld + v;
+    if (best == ~0ull) {
+        d[ix] = 0;
+        rel[ix] = 0.0;
+    } else {
+        const int u = (int)(best & 0xFFFFFFFFu);
+        const double x = r[(size_t)jj * ld + u];
+        d[ix] = (uint32_t)(best >> 32);
+        rel[ix] = u == v ? x : x * x;
+    }
 }
 
 /* Columns form (directed graph on one GPU): workgroup of 64 target columns j0.., lane = column,
@@ -539,6 +577,8 @@ typedef struct {
     double* ar;
     uint32_t* lev;
     uint8_t* l8; /* u8 distance rows (nrows x ld) for the reliability pass */
+    unsigned long long* dkey; /* the diagonal rule's key per local row (undirected rows form) */
+    const double* r_rows;
     void* p[20];
     int k;
     hipStream_t st;
@@ -552,6 +592,21 @@ static void lvl_free(lvl_state* L, hipStream_t st) {
 }
 
 void srt_levels_release(hipStream_t st) { lvl_free(&g_lvl[srt_state_slot()], st); }
+
+/* the diagonal rule of the held build's rows into d / rel (row stride ld); 0 = applied, 1 = the
+ * build kept no keys (directed: the caller's dense_diag_kernel) */
+int srt_levels_diag(int n, int ld, uint32_t* d, double* rel, hipStream_t st, int* applied) {
+    const lvl_state* L = &g_lvl[srt_state_slot()];
+    *applied = 0;
+    if (!L->held || !L->dkey) return SRT_OK;
+    const int lrows = max(0, min(L->nrows, n - L->row0));
+    if (lrows > 0)
+        lvl_diag_kernel<<<srt_ceil_div(lrows, 256), 256, 0, st>>>(n, ld, L->row0, lrows, L->dkey,
+                                                                  L->r_rows, d, rel);
+    SRT_HIPCHK(hipGetLastError());
+    *applied = 1;
+    return SRT_OK;
+}
 
 const uint8_t* srt_levels_l8(void) {
     const lvl_state* L = &g_lvl[srt_state_slot()];
@@ -599,12 +654,15 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     LVL_ALLOC(cnt, (ncnt + 1) * sizeof(int32_t));
     LVL_ALLOC(off, (ncnt + 1) * sizeof(int32_t));
     LVL_ALLOC(dhist, LVL_STRIDE * sizeof(unsigned long long));
+    unsigned long long* dkey = NULL;
+    if (!directed) LVL_ALLOC(dkey, (size_t)nrows * sizeof(unsigned long long));
     SRT_HIPCHK(hipMemsetAsync(cnt, 0, (ncnt + 1) * sizeof(int32_t), st));
     SRT_HIPCHK(hipMemsetAsync(dhist, 0, LVL_STRIDE * sizeof(unsigned long long), st));
     if (directed)
         lvl_arcs_cols_kernel<false><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, cnt, 0, NULL, NULL);
     else
-        lvl_arcs_rows_kernel<false><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, cnt, 0, NULL, NULL);
+        lvl_arcs_rows_kernel<false><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, cnt, 0, NULL, NULL,
+                                                           NULL, NULL, dkey);
     SRT_HIPCHK(hipGetLastError());
     int rc;
     if (R > 1 && (rc = srt_coll_allreduce_i32(comm, cnt, ncnt, 0, st))) return rc;
@@ -756,6 +814,8 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     L->ar = ar;
     L->lev = lev;
     L->l8 = l8;
+    L->dkey = dkey;
+    L->r_rows = r_rows;
     return SRT_OK;
 }
 

@@ -165,6 +165,9 @@ int srt_levels_pred(void* predT, int pred16, double* rT, size_t ldp, unsigned lo
 void srt_levels_release(hipStream_t st);
 /* the held build's u8 distance rows (nrows x ld, 0 on the diagonal), NULL if none */
 const uint8_t* srt_levels_l8(void);
+/* the diagonal rule of the held build's rows (keys from its row reads); *applied = 0 when it kept
+ * none (directed builds: dense_diag_kernel) */
+int srt_levels_diag(int n, int ld, uint32_t* d, double* rel, hipStream_t st, int* applied);
 /* the same into this slot's FW matrix + the finish pass (fw16.hip); *nlev = 0: FW instead */
 int srt_fw16_levels(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
                     const uint32_t* w_rows, const double* r_rows, uint32_t* lat_rows,

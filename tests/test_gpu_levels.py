@@ -126,3 +126,23 @@ def test_levels_virtual_ranks(gpu, monkeypatch, ranks, kind):
                                 algo=ALGO_DENSE_FW, ngpus=1)
     assert st.dist_enc == LEVELS, st.dist_enc
     _check(g, lat, rel, f"virtual x{ranks} {kind}")
+
+
+def test_levels_sub_ms_path_order(gpu, monkeypatch):
+    """A level build with 0.1-0.3 ms edges (quantum 100 us): the f64 ms table is summed in path
+    order along the level pass's predecessors (int16 rows, widened for the ms pass), bit for bit
+    the reference's (double)ns / 1e6 hop sums."""
+    from shadow_amd.topology import build_tables_subset
+    set_form(monkeypatch, levels="1")
+    rng = np.random.default_rng(42)
+    g0 = graphs.complete_graph(300, seed=3)
+    lat = rng.integers(1, 4, g0.m).astype(np.int64) * 100_000
+    g = graphs.Graph(g0.n, False, g0.src, g0.dst, lat, g0.loss)
+    full = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss), True,
+                        oracle.ORC_INT_NS, 8, raw=True)
+    lat_t, rel, ms, _, st = build_tables_subset(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                                algo=ALGO_DENSE_FW, want_ms=True)
+    assert st.dist_enc == LEVELS, st.dist_enc
+    assert np.array_equal(lat_t, full["lat_int"])
+    assert np.array_equal(rel, full["rel"])
+    assert np.array_equal(ms, full["lat_ms"]), np.argwhere(ms != full["lat_ms"])[:5]
