@@ -278,8 +278,11 @@ static __device__ __forceinline__ void lvl_step_unit(unsigned g, int d, int n, i
 }
 
 /* Persistent grid (a few workgroups per CU, each looping over unit blocks): the units live only a
- * few microseconds, so a one-shot grid of 131k workgroups was bound by workgroup dispatch. Block p
- * of XCD p % 8 takes that XCD's contiguous run of unit blocks (chunk-major), one every P / 8. */
+ * few microseconds, so a one-shot grid of 131k workgroups was bound by workgroup dispatch. The
+ * unit blocks are walked chunk-major by all eight XCDs together (block u * 8 + XCD), so the planes'
+ * gathered slices are one source chunk's at a time for the whole GPU (8 MB per plane: the MALL
+ * holds them) -- an XCD-private run of chunks put 16 chunks' slices in flight at once (~384 MB on
+ * C4, past the 256-MB MALL). */
 __global__ __launch_bounds__(256) void lvl_step_kernel(int d, int n, int nw, int nchunk, int src0,
                                                        int nsrc, unsigned nblk,
                                                        const int32_t* __restrict__ off,
@@ -291,7 +294,7 @@ __global__ __launch_bounds__(256) void lvl_step_kernel(int d, int n, int nw, int
                                                        int* __restrict__ incomplete) {
     const unsigned x = blockIdx.x & 7u, per = nblk >> 3, L = gridDim.x >> 3;
     for (unsigned u = blockIdx.x >> 3; u < per; u += L)
-        lvl_step_unit(x * per + u, d, n, nw, nchunk, src0, nsrc, off, arcs, aoff, lev, R, done,
+        lvl_step_unit(u * 8u + x, d, n, nw, nchunk, src0, nsrc, off, arcs, aoff, lev, R, done,
                       incomplete);
 }
 
@@ -349,6 +352,65 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(int n, int ld, int nw, int
             }
             *reinterpret_cast<uint4*>(lat + o) = make_uint4(x[0], x[1], x[2], x[3]);
             *reinterpret_cast<uint32_t*>(l8 + o) = b;
+        }
+    }
+}
+
+/* The same rows for builds of at most LVL_OUT_L levels, without lvl_out_kernel's re-fetches (its
+ * 4-B plane reads come back 16 times per 64-B sector: C4 fetched 8.9 GB for 0.65 GB of planes).
+ * Workgroup = 256 targets x 8 source words: every level's 8 words of every target are staged in
+ * LDS with one 32-B read per (target, level), then thread = one target runs over the 8 words (256
+ * sources) from LDS, keeping a word's 32 distances as bytes, and writes 4 B of u32 and 1 B of u8
+ * per source row (a wave's 64 consecutive targets: 256 B / 64 B runs). */
+#define LVL_OUT_L 16
+__global__ __launch_bounds__(256) void lvl_out8_kernel(int n, int ld, int nw, int src0, int nlev,
+                                                       const uint32_t* __restrict__ lev,
+                                                       uint32_t* __restrict__ lat,
+                                                       uint8_t* __restrict__ l8) {
+    extern __shared__ uint4 smo[]; /* [level][half][target]: words w0..w0+3 | +4..+7 (8 KB per level) */
+    auto sm = reinterpret_cast<uint4(*)[2][256]>(smo);
+    const int tid = threadIdx.x, t = blockIdx.x * 256 + tid;
+    const int w0 = blockIdx.y * 8;
+    const size_t plane = (size_t)n * nw;
+    const bool tv = t < n;
+    for (int d = 0; d < nlev; ++d) {
+        uint4 a = make_uint4(0u, 0u, 0u, 0u), b = a;
+        if (tv) { /* nw is a multiple of 4 (nsrc % 128 == 0): 16-B aligned words */
+            const uint4* p = reinterpret_cast<const uint4*>(lev + (size_t)d * plane + (size_t)t * nw + w0);
+            a = p[0];
+            b = w0 + 4 < nw ? p[1] : make_uint4(0u, 0u, 0u, 0u);
+        }
+        sm[d][0][tid] = a;
+        sm[d][1][tid] = b;
+    }
+    /* (thread tid reads back only its own entries: no barrier needed) */
+    if (t >= ld) return;
+    const int k1 = min(8, nw - w0);
+    for (int k = 0; k < k1; ++k) {
+        uint32_t v[8]; /* sources 4i..4i+3 of the word, one byte each (0xFF: none) */
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = 0xFFFFFFFFu;
+        const int sg0 = src0 + (w0 + k) * 32;
+        if (t >= sg0 && t < sg0 + 32) { /* the diagonal */
+            const int sd = t - sg0;
+            v[sd >> 2] &= ~(0xFFu << (8 * (sd & 3)));
+        }
+        for (int d = 0; d < nlev; ++d) {
+            const uint4 q = sm[d][k >> 2][tid];
+            const uint32_t m = (k & 3) == 0 ? q.x : (k & 3) == 1 ? q.y : (k & 3) == 2 ? q.z : q.w;
+            if (!m) continue;
+#pragma unroll
+            for (int sidx = 0; sidx < 32; ++sidx)
+                if ((m >> sidx) & 1u)
+                    v[sidx >> 2] = (v[sidx >> 2] & ~(0xFFu << (8 * (sidx & 3)))) |
+                                   ((uint32_t)(d + 1) << (8 * (sidx & 3)));
+        }
+#pragma unroll
+        for (int sidx = 0; sidx < 32; ++sidx) {
+            const size_t o = (size_t)((w0 + k) * 32 + sidx) * ld + t;
+            const uint32_t y = (v[sidx >> 2] >> (8 * (sidx & 3))) & 0xFFu;
+            lat[o] = y == 0xFFu ? SRT_INF : y;
+            l8[o] = (uint8_t)(y == 0xFFu ? 0u : y);
         }
     }
 }
@@ -515,7 +577,7 @@ __global__ __launch_bounds__(256) void lvl_pred_kernel(int n, int nw, int nchunk
     __shared__ __attribute__((aligned(16))) uint16_t sidx[4][64 * 40];
     const unsigned x = blockIdx.x & 7u, per = nblk >> 3, L = gridDim.x >> 3;
     for (unsigned u = blockIdx.x >> 3; u < per; u += L)
-        lvl_pred_unit<PT>(x * per + u, sidx, n, nw, nchunk, src0, nsrc, nlev, off, arcs, aoff, ar,
+        lvl_pred_unit<PT>(u * 8u + x, sidx, n, nw, nchunk, src0, nsrc, nlev, off, arcs, aoff, ar,
                           lev, predT, rT, ldp, ties);
 }
 
@@ -795,8 +857,16 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     if (!ok) return SRT_OK;
     uint8_t* l8 = NULL;
     LVL_ALLOC(l8, (size_t)nrows * ld);
-    lvl_out_kernel<<<dim3(srt_ceil_div(ld, 1024), srt_ceil_div(nw, 16)), 256, 0, st>>>(
-        n, ld, nw, row0, D, lev, lat_rows, l8);
+    if (D <= LVL_OUT_L) {
+        const int lds = D * 2 * 256 * (int)sizeof(uint4);
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)lvl_out8_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        lvl_out8_kernel<<<dim3(srt_ceil_div(ld, 256), srt_ceil_div(nw, 8)), 256, lds, st>>>(
+            n, ld, nw, row0, D, lev, lat_rows, l8);
+    } else {
+        lvl_out_kernel<<<dim3(srt_ceil_div(ld, 1024), srt_ceil_div(nw, 16)), 256, 0, st>>>(
+            n, ld, nw, row0, D, lev, lat_rows, l8);
+    }
     SRT_HIPCHK(hipGetLastError());
     *levels = D;
     *gather_bytes = gathered;
