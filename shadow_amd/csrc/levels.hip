@@ -515,47 +515,47 @@ static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx
         for (int m = 32; m > 0; m >>= 1) tied += __shfl_xor(tied, m);
         if (lane == 0 && tied) atomicAdd(&ties[blockIdx.x & 1023u], (unsigned long long)tied);
     }
-    if (!valid) return;
-    /* 32 entries per lane in two halves of 16 (the output registers of all 32 held the kernel
-     * to 4 waves per SIMD): the indices back from LDS, every arc and reliability gather of the
-     * half issued before the first is used, then 32 (64) B of predecessors and 128 B of
-     * reliabilities */
-    const int sl0 = word * 32;
+    /* Output, coalesced: the wave writes its 2,048 sources in four quarters of 512, lane l taking
+     * 8 consecutive sources (another lane's entries, back from LDS), so every store instruction
+     * covers one contiguous run (1 KB of int16 predecessors, 4 KB of reliabilities per quarter)
+     * instead of 64 strided 16-B pieces. The walk's LDS writes are the wave's own. */
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int cs0 = c * 64 * 32; /* the chunk's first local source */
 #pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-        uint32_t ix[8];
+    for (int q = 0; q < 4; ++q) {
+        const int sl0 = cs0 + q * 512 + lane * 8;
+        if (sl0 >= nsrc) continue; /* nsrc is a multiple of 128: whole groups of 8 */
+        const uint4 raw =
+            *reinterpret_cast<const uint4*>(&sidx[wv][(q * 16 + (lane >> 2)) * 40 + (lane & 3) * 8]);
+        const uint32_t ix[4] = {raw.x, raw.y, raw.z, raw.w};
+        int32_t pv[8];
+        double rv[8];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint4 v = *reinterpret_cast<const uint4*>(my + 16 * hf + 8 * q);
-            ix[4 * q] = v.x;
-            ix[4 * q + 1] = v.y;
-            ix[4 * q + 2] = v.z;
-            ix[4 * q + 3] = v.w;
-        }
-        int32_t pv[16];
-        double rv[16];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
+        for (int e = 0; e < 8; ++e) {
             const uint32_t x = (ix[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
-            const int sl = sl0 + 16 * hf + e, sg = src0 + sl;
-            const bool h = sl < nsrc && sg < n && sg != t && x != 0xFFFFu;
+            const int sg = src0 + sl0 + e;
+            const bool h = sg < n && sg != t && x != 0xFFFFu;
             const int k = a_t + (h ? (int)x : 0);
             pv[e] = h ? (int)(arcs[k] & 0xFFFFu) : -1;
             rv[e] = h ? ar[k] : 0.0;
         }
-        PT* pp = predT + (size_t)t * ldp + sl0 + 16 * hf;
-        double* rp = rT + (size_t)t * ldp + sl0 + 16 * hf;
+        PT* pp = predT + (size_t)t * ldp + sl0;
+        double* rp = rT + (size_t)t * ldp + sl0;
+        if constexpr (sizeof(PT) == 2) { /* -1 -> 0xFFFF, read back as int16 -1 */
+            uint32_t w2[4];
 #pragma unroll
-        for (int q = 0; q < 16; q += 4) {
-            if constexpr (sizeof(PT) == 2) /* -1 -> 0xFFFF, read back as int16 -1 */
-                *reinterpret_cast<uint2*>(pp + q) =
-                    make_uint2(((uint32_t)pv[q] & 0xFFFFu) | ((uint32_t)pv[q + 1] << 16),
-                               ((uint32_t)pv[q + 2] & 0xFFFFu) | ((uint32_t)pv[q + 3] << 16));
-            else
-                *reinterpret_cast<int4*>(pp + q) = make_int4(pv[q], pv[q + 1], pv[q + 2], pv[q + 3]);
-            *reinterpret_cast<double2*>(rp + q) = make_double2(rv[q], rv[q + 1]);
-            *reinterpret_cast<double2*>(rp + q + 2) = make_double2(rv[q + 2], rv[q + 3]);
+            for (int e = 0; e < 4; ++e)
+                w2[e] = ((uint32_t)pv[2 * e] & 0xFFFFu) | ((uint32_t)pv[2 * e + 1] << 16);
+            *reinterpret_cast<uint4*>(pp) = make_uint4(w2[0], w2[1], w2[2], w2[3]);
+        } else {
+            *reinterpret_cast<int4*>(pp) = make_int4(pv[0], pv[1], pv[2], pv[3]);
+            *reinterpret_cast<int4*>(pp + 4) = make_int4(pv[4], pv[5], pv[6], pv[7]);
         }
+#pragma unroll
+        for (int e = 0; e < 8; e += 2)
+            *reinterpret_cast<double2*>(rp + e) = make_double2(rv[e], rv[e + 1]);
     }
 }
 
