@@ -25,7 +25,7 @@
 #define DV_MAXDEG 4   /* largest degree the host puts in I (build.hip DERIVE_MAXDEG) */
 #define DV_J 2        /* targets per thread per phase-A step: their loads overlap */
 #define DV_WG_PER_CU 4
-#define DV_JB 4       /* targets per thread per phase-B step of the on-demand form */
+#define DV_JB 1       /* targets per thread per phase-B step (4: 138 vs 125 ms on C5) */
 
 /* order of canonical arcs u | w << 17 | ridx << 24: the largest w, then the smallest u */
 static __device__ __forceinline__ uint32_t dv_key(uint32_t code) {
@@ -43,18 +43,30 @@ static __device__ __forceinline__ uint32_t dv_key(uint32_t code) {
  * the same vertex store the same product. The ancestors near s are shared by most chains and
  * stay in cache; no list, no per-level barrier (a distance-ordered form -- a per-row list by
  * distance, one barrier per level -- measured 250 vs 125 ms on C5: ~200 levels per row). */
-__global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
+template <int NT, int CACHE>
+__global__ __launch_bounds__(NT) void derive_chain_kernel(
     int n, int nI, const int32_t* __restrict__ I, int src_begin, const int2* __restrict__ rowptr,
     const uint2* __restrict__ cw, const uint8_t* __restrict__ ridx, const double* __restrict__ rtab,
     int ntab, const int32_t* __restrict__ crow, const uint32_t* __restrict__ codes,
     uint32_t* __restrict__ lat, double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ cs_all,
     size_t lds_n) {
-    extern __shared__ uint32_t cdone[]; /* one bit per target */
+    /* dynamic LDS: one done bit per target, then (CACHE) the reliability of vertices < CACHE --
+     * the oldest vertices of a BA graph are its hubs, the parents of most targets */
+    extern __shared__ __attribute__((aligned(16))) uint32_t cdone[];
+    double* cache = reinterpret_cast<double*>(cdone + (((n + 31) / 32 + 3) & ~3));
     __shared__ double s_tab[256];
     __shared__ int s_nb[DV_MAXDEG], s_w[DV_MAXDEG], s_rx[DV_MAXDEG], s_cr[DV_MAXDEG];
     const int tid = threadIdx.x, nw = (n + 31) >> 5;
-    for (int i = tid; i < ntab; i += DV_THREADS) s_tab[i] = rtab[i];
+    for (int i = tid; i < ntab; i += NT) s_tab[i] = rtab[i];
     uint32_t* cs = cs_all + (size_t)blockIdx.x * lds_n;
+    auto rel_of = [&](uint32_t u, const double* orr) -> double {
+        if (CACHE && u < (uint32_t)CACHE) return cache[u];
+        return __hip_atomic_load(orr + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto put = [&](uint32_t y, double v, double* orr) {
+        __hip_atomic_store(orr + y, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (CACHE && y < (uint32_t)CACHE) cache[y] = v;
+    };
     auto is_done = [&](uint32_t v) {
         return (__hip_atomic_load(&cdone[v >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >>
                 (v & 31)) & 1u;
@@ -73,16 +85,16 @@ __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
             s_rx[tid] = ridx[be.x + tid];
             s_cr[tid] = crow[e.x];
         }
-        for (int q = tid; q < nw; q += DV_THREADS) cdone[q] = 0u;
+        for (int q = tid; q < nw; q += NT) cdone[q] = 0u;
         __threadfence_block();
         __syncthreads();
         /* phase A (as derive_rows_kernel): distances, derived codes; s and the unreachable
          * targets are done at once */
-        for (int t0 = 0; t0 < n; t0 += DV_J * DV_THREADS) {
+        for (int t0 = 0; t0 < n; t0 += DV_J * NT) {
             uint32_t dk[DV_J][DV_MAXDEG];
 #pragma unroll
             for (int j = 0; j < DV_J; ++j) {
-                const int t = t0 + j * DV_THREADS + tid;
+                const int t = t0 + j * NT + tid;
 #pragma unroll
                 for (int i = 0; i < DV_MAXDEG; ++i)
                     dk[j][i] = (i < deg && t < n)
@@ -100,7 +112,7 @@ __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
             uint32_t cd[DV_J][DV_MAXDEG];
 #pragma unroll
             for (int j = 0; j < DV_J; ++j) {
-                const int t = t0 + j * DV_THREADS + tid;
+                const int t = t0 + j * NT + tid;
 #pragma unroll
                 for (int i = 0; i < DV_MAXDEG; ++i) {
                     cd[j][i] = ~0u;
@@ -113,7 +125,7 @@ __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
             }
 #pragma unroll
             for (int j = 0; j < DV_J; ++j) {
-                const int t = t0 + j * DV_THREADS + tid;
+                const int t = t0 + j * NT + tid;
                 if (t >= n) continue;
                 uint32_t best = ~0u, bk = ~0u;
 #pragma unroll
@@ -126,7 +138,7 @@ __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
                 ol[t] = D[j];
                 cs[t] = best;
                 if (t == s || D[j] >= SRT_INF) {
-                    orr[t] = t == s ? 1.0 : 0.0;
+                    put((uint32_t)t, t == s ? 1.0 : 0.0, orr);
                     __hip_atomic_fetch_or(&cdone[t >> 5], 1u << (t & 31), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
@@ -144,10 +156,8 @@ __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
                     cy = cs[y];
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                const double rp = __hip_atomic_load(orr + (cy & 0x1FFFFu), __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_store(orr + y, rp * s_tab[cy >> 24], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                const double rp = rel_of(cy & 0x1FFFFu, orr);
+                put(y, rp * s_tab[cy >> 24], orr);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __hip_atomic_fetch_or(&cdone[y >> 5], 1u << (y & 31), __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -157,12 +167,12 @@ __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
         /* phase B: on-demand path-order products. DV_JB targets per thread per step: their
          * codes, then the predecessors' values of the ready ones, in flight together; a target
          * whose predecessor is not formed yet climbs alone */
-        for (int t0 = 0; t0 < n; t0 += DV_JB * DV_THREADS) {
+        for (int t0 = 0; t0 < n; t0 += DV_JB * NT) {
             uint32_t cj[DV_JB];
             bool rdy[DV_JB];
 #pragma unroll
             for (int j = 0; j < DV_JB; ++j) {
-                const int t = t0 + j * DV_THREADS + tid;
+                const int t = t0 + j * NT + tid;
                 cj[j] = (t < n && !is_done((uint32_t)t)) ? cs[t] : ~0u;
             }
 #pragma unroll
@@ -170,26 +180,21 @@ __global__ __launch_bounds__(DV_THREADS) void derive_chain_kernel(
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             double rp[DV_JB];
 #pragma unroll
-            for (int j = 0; j < DV_JB; ++j)
-                rp[j] = rdy[j] ? __hip_atomic_load(orr + (cj[j] & 0x1FFFFu), __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP)
-                               : 0.0;
+            for (int j = 0; j < DV_JB; ++j) rp[j] = rdy[j] ? rel_of(cj[j] & 0x1FFFFu, orr) : 0.0;
 #pragma unroll
             for (int j = 0; j < DV_JB; ++j)
-                if (rdy[j])
-                    __hip_atomic_store(orr + t0 + j * DV_THREADS + tid, rp[j] * s_tab[cj[j] >> 24],
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (rdy[j]) put((uint32_t)(t0 + j * NT + tid), rp[j] * s_tab[cj[j] >> 24], orr);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 #pragma unroll
             for (int j = 0; j < DV_JB; ++j)
                 if (rdy[j]) {
-                    const int t = t0 + j * DV_THREADS + tid;
+                    const int t = t0 + j * NT + tid;
                     __hip_atomic_fetch_or(&cdone[t >> 5], 1u << (t & 31), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
 #pragma unroll
             for (int j = 0; j < DV_JB; ++j) {
-                const int t = t0 + j * DV_THREADS + tid;
+                const int t = t0 + j * NT + tid;
                 if (cj[j] == ~0u || rdy[j] || is_done((uint32_t)t)) continue;
                 climb(t, cj[j]);
             }
@@ -216,16 +221,31 @@ int srt_derive_rows_async(int n, int nI, const int32_t* I, int src_begin, const 
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
         cus = prop.multiProcessorCount;
-    /* 4 workgroups per CU: 181 / 125 / 146 ms on C5 at 2 / 4 / 8 */
-    const int grid = nI < DV_WG_PER_CU * cus ? nI : DV_WG_PER_CU * cus;
+    /* forms (SRT_FORM dv_var, A/B): 0 = 256 threads x 4 per CU, no cache (181 / 125 / 146 ms on
+     * C5 at 2 / 4 / 8 per CU); 1 = 512 x 2 with 8,192 cached; 2 = 1,024 x 1 with 16,384 cached */
+    const int var = srt_form_int("dv_var", 0);
+    const int per = var == 0 ? DV_WG_PER_CU : var == 1 ? 2 : 1;
+    const int nt = var == 0 ? 256 : var == 1 ? 512 : 1024, cache = var == 0 ? 0 : var == 1 ? 8192 : 16384;
+    const int grid = nI < per * cus ? nI : per * cus;
     const size_t np = ((size_t)n + 3) & ~(size_t)3;
     uint32_t* cs = NULL;
     SRT_HIPCHK(srt_malloc_async(&cs, (size_t)grid * np * sizeof(uint32_t), st));
-    const size_t lds = (size_t)((n + 31) / 32) * sizeof(uint32_t);
-    SRT_HIPCHK(hipFuncSetAttribute((const void*)derive_chain_kernel,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    derive_chain_kernel<<<grid, DV_THREADS, lds, st>>>(n, nI, I, src_begin, rowptr, cw, ridx, rtab,
-                                                       ntab, crow, codes, lat, rel, ldo, cs, np);
+    const size_t lds = (size_t)((((n + 31) / 32) + 3) & ~3) * sizeof(uint32_t) + (size_t)cache * 8;
+    const void* fn = var == 0 ? (const void*)derive_chain_kernel<256, 0>
+                     : var == 1 ? (const void*)derive_chain_kernel<512, 8192>
+                                : (const void*)derive_chain_kernel<1024, 16384>;
+    SRT_HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (var == 0)
+        derive_chain_kernel<256, 0><<<grid, nt, lds, st>>>(n, nI, I, src_begin, rowptr, cw, ridx, rtab,
+                                                           ntab, crow, codes, lat, rel, ldo, cs, np);
+    else if (var == 1)
+        derive_chain_kernel<512, 8192><<<grid, nt, lds, st>>>(n, nI, I, src_begin, rowptr, cw, ridx,
+                                                              rtab, ntab, crow, codes, lat, rel, ldo,
+                                                              cs, np);
+    else
+        derive_chain_kernel<1024, 16384><<<grid, nt, lds, st>>>(n, nI, I, src_begin, rowptr, cw, ridx,
+                                                                rtab, ntab, crow, codes, lat, rel, ldo,
+                                                                cs, np);
     SRT_HIPCHK(hipGetLastError());
     SRT_HIPCHK(hipFreeAsync(cs, st));
     return SRT_OK;
