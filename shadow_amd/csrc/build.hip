@@ -135,8 +135,6 @@ struct srt_sparse_graph {
     int32_t nI, ncore;
     int32_t *dI, *dcore, *crow;
     int32_t ntab; /* entries of rtab */
-    int32_t nheavy;  /* vertices of degree > 64 (their in-arcs scanned by whole waves) */
-    int32_t* dheavy;
 };
 
 #define DERIVE_MAXDEG 4 /* <= derive.hip's DV_MAXDEG */
@@ -154,7 +152,7 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
 int srt_derive_rows_async(int n, int nI, const int32_t* I, int src_begin, const int2* rowptr,
                           const uint2* cw, const uint8_t* ridx, const double* rtab, int ntab,
                           const int32_t* crow, const uint32_t* codes, uint32_t* lat, double* rel,
-                          size_t ldo, hipStream_t st, const int32_t* heavy, int nheavy);
+                          size_t ldo, hipStream_t st);
 int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, const double* r,
                    const int2* in_rowptr, const uint2* in_cw, const double* in_r,
                    const int32_t* perm, const int32_t* inv, uint32_t max_w, int local,
@@ -185,7 +183,7 @@ extern "C" void srt_sparse_graph_free(srt_sparse_graph* g) {
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(g->device);
     void* ps[] = {g->rp, g->col, g->w, g->r, g->sw, g->sr, g->cw, g->perm, g->inv, g->rp2, g->cw2, g->r2,
-                  g->rpo, g->rtab, g->ridx, g->dI, g->dcore, g->crow, g->dheavy};
+                  g->rpo, g->rtab, g->ridx, g->dI, g->dcore, g->crow};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (g->directed) {
@@ -300,12 +298,7 @@ static int derive_sets(const srt_canon* c, srt_sparse_graph* g) {
     g->nI = (int32_t)I.size();
     g->ncore = (int32_t)core.size();
 
-    std::vector<int32_t> hv;
-    for (int v = 0; v < n; v++)
-        if (deg(v) > 64) hv.push_back(v);
-    g->nheavy = (int32_t)hv.size();
-    int rc = up((void**)&g->dheavy, hv.data(), hv.size() * 4);
-    if (!rc) rc = up((void**)&g->dI, I.data(), I.size() * 4);
+    int rc = up((void**)&g->dI, I.data(), I.size() * 4);
     if (!rc) rc = up((void**)&g->dcore, core.data(), core.size() * 4);
     if (!rc) rc = up((void**)&g->crow, crow.data(), (size_t)n * 4);
     return rc;
@@ -606,11 +599,8 @@ static void ms_clusters(const srt_sparse_graph* g, const int32_t* rowof, int nsr
 static int sparse_rows_derived(const srt_sparse_graph* g, uint32_t* lat_rows, double* rel_rows,
                                int* ovf, hipStream_t st) {
     const int n = g->n;
-    /* SRT_FORM dv_own=0: the core kernel stores each settled vertex's canonical arc and the set's
-     * rows take their neighbours'; by default the set's rows find their own from their distances */
-    const bool own = srt_form_int("dv_own", 1) != 0;
     uint32_t* codes = NULL;
-    if (!own) SRT_HIPCHK(srt_malloc_async(&codes, (size_t)g->ncore * n * sizeof(uint32_t), st));
+    SRT_HIPCHK(srt_malloc_async(&codes, (size_t)g->ncore * n * sizeof(uint32_t), st));
     SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)n * sizeof(int), st));
     int rc = srt_wgsssp_rows(n, g->rpo, g->cw, g->r, NULL, g->max_w, 0, g->ncore, g->dcore, lat_rows,
                              rel_rows, ovf, st, g->ridx, g->rtab, 1, codes);
@@ -626,9 +616,8 @@ static int sparse_rows_derived(const srt_sparse_graph* g, uint32_t* lat_rows, do
                              rel_rows, ovf, st, g->ridx, g->rtab, 1, NULL);
     else if (!rc)
         rc = srt_derive_rows_async(n, g->nI, g->dI, 0, g->rpo, g->cw, g->ridx, g->rtab, g->ntab,
-                                   g->crow, codes, lat_rows, rel_rows, (size_t)n, st, g->dheavy,
-                                   g->nheavy);
-    if (codes) (void)hipFreeAsync(codes, st);
+                                   g->crow, codes, lat_rows, rel_rows, (size_t)n, st);
+    (void)hipFreeAsync(codes, st);
     return rc;
 }
 

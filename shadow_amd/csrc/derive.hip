@@ -19,14 +19,10 @@
  * target resolves once its predecessor has) -- never taken from k's row, whose product associates
  * from k.
  */
-#include <algorithm>
-
 #include "srt_device.h"
 
-#define DV_THREADS 256
 #define DV_MAXDEG 4   /* largest degree the host puts in I (build.hip DERIVE_MAXDEG) */
 #define DV_J 2        /* targets per thread per phase-A step: their loads overlap */
-#define DV_WG_PER_CU 4
 #define DV_JB 1       /* targets per thread per phase-B step (4: 138 vs 125 ms on C5) */
 
 /* order of canonical arcs u | w << 17 | ridx << 24: the largest w, then the smallest u */
@@ -34,7 +30,7 @@ static __device__ __forceinline__ uint32_t dv_key(uint32_t code) {
     return ((127u - ((code >> 17) & 0x7Fu)) << 17) | (code & 0x1FFFFu);
 }
 
-/* One workgroup per derived source (persistent grid over I, DV_WG_PER_CU per CU). Rows are placed
+/* One workgroup per derived source (persistent grid over I, one per CU). Rows are placed
  * by source: row of vertex v = v - src_begin, in lat / rel (stride ldo); core vertex k's codes are
  * row crow[k] of codes (stride n); cs: n codes of scratch per workgroup. Phase A forms the
  * distances and the derived codes; phase B the reliability on demand: a thread takes
@@ -45,21 +41,17 @@ static __device__ __forceinline__ uint32_t dv_key(uint32_t code) {
  * the same vertex store the same product. The ancestors near s are shared by most chains and
  * stay in cache; no list, no per-level barrier (a distance-ordered form -- a per-row list by
  * distance, one barrier per level -- measured 250 vs 125 ms on C5: ~200 levels per row). */
-template <int NT, int CACHE, bool OWN>
+template <int NT, int CACHE>
 __global__ __launch_bounds__(NT) void derive_chain_kernel(
     int n, int nI, const int32_t* __restrict__ I, int src_begin, const int2* __restrict__ rowptr,
     const uint2* __restrict__ cw, const uint8_t* __restrict__ ridx, const double* __restrict__ rtab,
     int ntab, const int32_t* __restrict__ crow, const uint32_t* __restrict__ codes,
     uint32_t* __restrict__ lat, double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ cs_all,
-    size_t lds_n, const int32_t* __restrict__ heavy = nullptr, int nheavy = 0) {
+    size_t lds_n) {
     /* dynamic LDS: one done bit per target, then (CACHE) the reliability of vertices < CACHE --
-     * the oldest vertices of a BA graph are its hubs, the parents of most targets. OWN: the
-     * codes come from this row's own distances, packed 3 x 10 bits in the same region before
-     * phase B (the core rows then carry no codes) */
+     * the oldest vertices of a BA graph are its hubs, the parents of most targets */
     extern __shared__ __attribute__((aligned(16))) uint32_t cdone[];
     double* cache = reinterpret_cast<double*>(cdone + (((n + 31) / 32 + 3) & ~3));
-    uint32_t* dpk = reinterpret_cast<uint32_t*>(cache);
-    __shared__ int s_big;
     __shared__ double s_tab[256];
     __shared__ int s_nb[DV_MAXDEG], s_w[DV_MAXDEG], s_rx[DV_MAXDEG], s_cr[DV_MAXDEG];
     const int tid = threadIdx.x, nw = (n + 31) >> 5;
@@ -92,10 +84,6 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
             s_cr[tid] = crow[e.x];
         }
         for (int q = tid; q < nw; q += NT) cdone[q] = 0u;
-        if constexpr (OWN) {
-            for (int q = tid; q < (n + 2) / 3; q += NT) dpk[q] = 0u;
-            if (tid == 0) s_big = 0;
-        }
         __threadfence_block();
         __syncthreads();
         /* phase A (as derive_rows_kernel): distances, derived codes; s and the unreachable
@@ -126,7 +114,7 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
 #pragma unroll
                 for (int i = 0; i < DV_MAXDEG; ++i) {
                     cd[j][i] = ~0u;
-                    if (!OWN && dk[j][i] < SRT_INF && (uint32_t)s_w[i] + dk[j][i] == D[j])
+                    if (dk[j][i] < SRT_INF && (uint32_t)s_w[i] + dk[j][i] == D[j])
                         cd[j][i] = t == s_nb[i]
                                        ? ((uint32_t)s | ((uint32_t)s_w[i] << 17) |
                                           ((uint32_t)s_rx[i] << 24))
@@ -146,19 +134,9 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
                     }
                 if (t == s) D[j] = 0;
                 ol[t] = D[j];
-                if constexpr (OWN) {
-                    const uint32_t f = D[j] < 1023u ? D[j] : 1023u; /* 1023: none / past 10 bits */
-                    if (D[j] >= 1023u && D[j] < SRT_INF) s_big = 1;
-                    atomicOr(&dpk[t / 3], f << (10 * (t % 3)));
-                } else {
-                    cs[t] = best;
-                }
+                cs[t] = best;
                 if (t == s || D[j] >= SRT_INF) {
-                    if (OWN) /* the cache region holds the packed distances until phase B */
-                        __hip_atomic_store(orr + t, t == s ? 1.0 : 0.0, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                    else
-                        put((uint32_t)t, t == s ? 1.0 : 0.0, orr);
+                    put((uint32_t)t, t == s ? 1.0 : 0.0, orr);
                     __hip_atomic_fetch_or(&cdone[t >> 5], 1u << (t & 31), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
@@ -166,64 +144,6 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
         }
         __threadfence_block();
         __syncthreads();
-        if constexpr (OWN) {
-            /* the canonical in-arc of every target from this row's distances: the largest w,
-             * then the smallest u among u -> t with D[u] + w == D[t] (D from LDS, or from the
-             * row just written when a distance passed 10 bits); targets of degree > 64 by
-             * whole waves (their in-arcs across the lanes) */
-            const bool big = s_big != 0;
-            auto dget = [&](uint32_t u) -> uint32_t {
-                if (big) return ol[u];
-                const uint32_t f = (dpk[u / 3] >> (10 * (u % 3))) & 1023u;
-                return f == 1023u ? SRT_INF : f;
-            };
-            for (int t = tid; t < n; t += NT) {
-                const int2 tb = rowptr[t];
-                if (tb.y - tb.x > 64) continue;
-                const uint32_t dt = dget((uint32_t)t);
-                uint32_t best = ~0u, bk = ~0u;
-                if (t != s && dt < SRT_INF)
-                    for (int k = tb.x; k < tb.y; ++k) {
-                        const uint2 e = cw[k];
-                        const uint32_t du = e.x == (uint32_t)s ? 0u : dget(e.x);
-                        if (du < SRT_INF && du + e.y == dt) {
-                            const uint32_t key = ((127u - e.y) << 17) | e.x;
-                            if (key < bk) {
-                                bk = key;
-                                best = e.x | (e.y << 17) | ((uint32_t)ridx[k] << 24);
-                            }
-                        }
-                    }
-                cs[t] = best;
-            }
-            const int lane = tid & 63, wv = tid >> 6;
-            for (int h = wv; h < nheavy; h += NT / 64) {
-                const int t = heavy[h];
-                const int2 tb = rowptr[t];
-                const uint32_t dt = dget((uint32_t)t);
-                unsigned long long best = ~0ull; /* key << 32 | code */
-                if (t != s && dt < SRT_INF)
-                    for (int k = tb.x + lane; k < tb.y; k += 64) {
-                        const uint2 e = cw[k];
-                        const uint32_t du = e.x == (uint32_t)s ? 0u : dget(e.x);
-                        if (du < SRT_INF && du + e.y == dt) {
-                            const unsigned long long key =
-                                ((unsigned long long)(((127u - e.y) << 17) | e.x) << 32) |
-                                (e.x | (e.y << 17) | ((uint32_t)ridx[k] << 24));
-                            best = key < best ? key : best;
-                        }
-                    }
-                for (int o = 32; o > 0; o >>= 1) {
-                    const unsigned long long y = __shfl_xor(best, o);
-                    best = y < best ? y : best;
-                }
-                if (lane == 0) cs[t] = best == ~0ull ? ~0u : (uint32_t)best;
-            }
-            __threadfence_block();
-            __syncthreads();
-            if (tid == 0 && CACHE && s < CACHE) cache[s] = 1.0; /* rel(s, s) for the cache */
-            __syncthreads();
-        }
         /* target t (its code ct) once its predecessor is not formed: climb to the first ancestor
          * whose predecessor is, form it, and repeat until t is formed */
         auto climb = [&](int t, uint32_t ct) {
@@ -289,7 +209,7 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
 int srt_derive_rows_async(int n, int nI, const int32_t* I, int src_begin, const int2* rowptr,
                           const uint2* cw, const uint8_t* ridx, const double* rtab, int ntab,
                           const int32_t* crow, const uint32_t* codes, uint32_t* lat, double* rel,
-                          size_t ldo, hipStream_t st, const int32_t* heavy, int nheavy) {
+                          size_t ldo, hipStream_t st) {
     if (nI <= 0) return SRT_OK;
     if (ntab > 256 || n > (1 << 17)) {
         srt_set_error("derive: %d distinct reliabilities (at most 256) or n = %d past 2^17", ntab, n);
@@ -299,49 +219,21 @@ int srt_derive_rows_async(int n, int nI, const int32_t* I, int src_begin, const 
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
         cus = prop.multiProcessorCount;
-    /* forms (SRT_FORM dv_var, A/B): 0 = 256 threads x 4 per CU, no cache (181 / 125 / 146 ms on
-     * C5 at 2 / 4 / 8 per CU); 1 = 512 x 2 with 8,192 cached; 2 = 1,024 x 1 with 16,384 cached
-     * (133 / 125 / 118 ms); codes == NULL: the codes from the row's own distances (1,024 x 1,
-     * 16,384 cached, the packed distances in the same LDS) */
-    if (!codes) {
-        const size_t lds = (size_t)((((n + 31) / 32) + 3) & ~3) * sizeof(uint32_t) +
-                           std::max((size_t)16384 * 8, (size_t)((n + 2) / 3) * 4);
-        const int grid = nI < cus ? nI : cus;
-        const size_t np = ((size_t)n + 3) & ~(size_t)3;
-        uint32_t* cs = NULL;
-        SRT_HIPCHK(srt_malloc_async(&cs, (size_t)grid * np * sizeof(uint32_t), st));
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)derive_chain_kernel<1024, 16384, true>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        derive_chain_kernel<1024, 16384, true><<<grid, 1024, lds, st>>>(
-            n, nI, I, src_begin, rowptr, cw, ridx, rtab, ntab, crow, codes, lat, rel, ldo, cs, np,
-            heavy, nheavy);
-        SRT_HIPCHK(hipGetLastError());
-        SRT_HIPCHK(hipFreeAsync(cs, st));
-        return SRT_OK;
-    }
-    const int var = srt_form_int("dv_var", 2);
-    const int per = var == 0 ? DV_WG_PER_CU : var == 1 ? 2 : 1;
-    const int nt = var == 0 ? 256 : var == 1 ? 512 : 1024, cache = var == 0 ? 0 : var == 1 ? 8192 : 16384;
-    const int grid = nI < per * cus ? nI : per * cus;
+    /* 1,024 threads, one workgroup per CU, 16,384 cached parents: 118 ms on C5 against 125 (512
+     * threads x 2, 8,192 cached) and 133 (256 x 4, no cache). Deriving the codes from the row's
+     * own distances in LDS instead of the core kernel's stores: core 391 -> 338 ms but derive
+     * 116 -> 202 ms (the in-arc scans), dropped */
+    constexpr int NTD = 1024, CACHED = 16384;
+    const int grid = nI < cus ? nI : cus;
     const size_t np = ((size_t)n + 3) & ~(size_t)3;
     uint32_t* cs = NULL;
     SRT_HIPCHK(srt_malloc_async(&cs, (size_t)grid * np * sizeof(uint32_t), st));
-    const size_t lds = (size_t)((((n + 31) / 32) + 3) & ~3) * sizeof(uint32_t) + (size_t)cache * 8;
-    const void* fn = var == 0 ? (const void*)derive_chain_kernel<256, 0, false>
-                     : var == 1 ? (const void*)derive_chain_kernel<512, 8192, false>
-                                : (const void*)derive_chain_kernel<1024, 16384, false>;
-    SRT_HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    if (var == 0)
-        derive_chain_kernel<256, 0, false><<<grid, nt, lds, st>>>(n, nI, I, src_begin, rowptr, cw, ridx, rtab,
-                                                           ntab, crow, codes, lat, rel, ldo, cs, np);
-    else if (var == 1)
-        derive_chain_kernel<512, 8192, false><<<grid, nt, lds, st>>>(n, nI, I, src_begin, rowptr, cw, ridx,
-                                                              rtab, ntab, crow, codes, lat, rel, ldo,
-                                                              cs, np);
-    else
-        derive_chain_kernel<1024, 16384, false><<<grid, nt, lds, st>>>(n, nI, I, src_begin, rowptr, cw, ridx,
-                                                                rtab, ntab, crow, codes, lat, rel, ldo,
-                                                                cs, np);
+    const size_t lds = (size_t)((((n + 31) / 32) + 3) & ~3) * sizeof(uint32_t) + (size_t)CACHED * 8;
+    SRT_HIPCHK(hipFuncSetAttribute((const void*)derive_chain_kernel<NTD, CACHED>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    derive_chain_kernel<NTD, CACHED><<<grid, NTD, lds, st>>>(n, nI, I, src_begin, rowptr, cw, ridx,
+                                                             rtab, ntab, crow, codes, lat, rel, ldo,
+                                                             cs, np);
     SRT_HIPCHK(hipGetLastError());
     SRT_HIPCHK(hipFreeAsync(cs, st));
     return SRT_OK;
