@@ -637,6 +637,27 @@ def run_sparse(c: Ctx, wl):
                  "and read once, the graph once ((n+1)*8 + arcs*16 B); per source its output row "
                  "(n*12 B)")
         achieved_gbs = bytes_launch / (k_ms * 1e-3) / 1e9
+    others = None
+    nder = int(stats[-1].n_derived)
+    if nder:
+        # derived build (fw_block bit 64): the core rows' kernel over n - nder sources (each also
+        # stores its canonical arcs, 4 B per target), then derive_chain_kernel over nder rows
+        # (srt_build_stats.work_bytes: the neighbours' distance rows, one neighbour's arcs, the
+        # output rows). The roofline names the core kernel, the derivation is listed beside it
+        ncore = nsrc - nder
+        core_ms = sum(s.ms_core for s in stats) / len(stats)
+        der_ms = sum(s.ms_derive for s in stats) / len(stats)
+        bytes_launch = float(ncore * (bytes_per_src + n * 4))
+        achieved_gbs = bytes_launch / (core_ms * 1e-3) / 1e9
+        k_ms = core_ms
+        model = (f"core rows ({ncore} sources): per source (n+1)*4 + arcs*16 + n*12 B (SURVEY §8d) "
+                 f"+ n*4 B of canonical arcs; the other {nder} rows derived (derive_chain_kernel)")
+        dbytes = float(stats[-1].work_bytes)
+        others = [{"kernel": "derive_chain_kernel<1024, 16384>", "rows": nder,
+                   "bytes_per_launch": dbytes, "avg_launch_ms": round(der_ms, 3),
+                   "achieved": round(dbytes / (der_ms * 1e-3) / 1e9, 1),
+                   "model": "per derived row: deg * n*4 B (neighbour distance rows) + n*4 B (one "
+                            "optimal neighbour's canonical arcs) + n*12 B (lat + rel rows out)"}]
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{c.args.workload}_n{world}.json")
     if os.path.exists(pmc_path):
@@ -649,7 +670,9 @@ def run_sparse(c: Ctx, wl):
         "bytes_per_launch": bytes_launch, "avg_launch_ms": round(k_ms, 3),
         "launches_timed": len(stats),
         "model": model,
-        "relax_per_launch": float(nsrc) * arcs}
+        "relax_per_launch": float(nsrc - nder) * arcs}
+    if others:
+        roofline["kernels"] = others
     # untimed check build: the tied-pair count over this rank's rows, summed over ranks
     chk = _lib.BuildStats()
     chk.count_ties = 1

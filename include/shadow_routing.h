@@ -107,6 +107,12 @@ typedef struct srt_build_stats {
                           * (lvl_pred_kernel) */
     double ms_rel;       /* ... and of the path-order reliability pass (rel_tree_kernel and the
                           * sweeps of the rows it hands over) */
+    int32_t n_derived;   /* sparse full-table builds with derived rows (fw_block bit 64): the rows
+                          * formed from their neighbours' (derive.hip), the rest by the kernel;
+                          * work_bytes = the derivation's algorithmic bytes */
+    double ms_core;      /* ... HIP-event time of the core rows' kernel (with their canonical arcs) */
+    double ms_derive;    /* ... and of the derivation (or of the kernel for the set's rows, when a
+                          * core row overflowed its buckets: n_derived = 0) */
 } srt_build_stats;
 
 /* Build the full tables for an edge list on one GPU; outputs are host buffers of n*n entries.

@@ -67,6 +67,9 @@ class BuildStats(ctypes.Structure):
         ("work_bytes", ctypes.c_int64),
         ("ms_pred", ctypes.c_double),
         ("ms_rel", ctypes.c_double),
+        ("n_derived", ctypes.c_int32),
+        ("ms_core", ctypes.c_double),
+        ("ms_derive", ctypes.c_double),
     ]
 
 

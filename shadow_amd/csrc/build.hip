@@ -133,6 +133,7 @@ struct srt_sparse_graph {
      * degree <= DERIVE_MAXDEG and the rest ("core"), both ascending; crow[v] = v's index in the
      * core list (-1 for I) */
     int32_t nI, ncore;
+    int64_t degI; /* summed degree of I (the derivation's neighbour-row reads) */
     int32_t *dI, *dcore, *crow;
     int32_t ntab; /* entries of rtab */
 };
@@ -297,6 +298,8 @@ static int derive_sets(const srt_canon* c, srt_sparse_graph* g) {
     }
     g->nI = (int32_t)I.size();
     g->ncore = (int32_t)core.size();
+    g->degI = 0;
+    for (int v : I) g->degI += deg(v);
 
     int rc = up((void**)&g->dI, I.data(), I.size() * 4);
     if (!rc) rc = up((void**)&g->dcore, core.data(), core.size() * 4);
@@ -596,14 +599,29 @@ static void ms_clusters(const srt_sparse_graph* g, const int32_t* rowof, int nsr
  * A core source whose buckets overflowed has no codes: then the set's rows take the kernel too.
  * (Deriving each chunk's ready set on a second stream beside the kernel's next chunk measured
  * slower: 829 vs 529 ms on C5.) */
+struct derived_times {
+    float core = 0, derive = 0; /* HIP-event ms of the core rows' kernel and of the derivation */
+    bool fallback = false;      /* a core row overflowed: the set's rows took the kernel */
+};
+
 static int sparse_rows_derived(const srt_sparse_graph* g, uint32_t* lat_rows, double* rel_rows,
-                               int* ovf, hipStream_t st) {
+                               int* ovf, hipStream_t st, derived_times* tm) {
     const int n = g->n;
+    struct evs {
+        hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+        ~evs() {
+            for (hipEvent_t x : e)
+                if (x) (void)hipEventDestroy(x);
+        }
+    } ev;
+    for (hipEvent_t& x : ev.e) SRT_HIPCHK(hipEventCreate(&x));
     uint32_t* codes = NULL;
     SRT_HIPCHK(srt_malloc_async(&codes, (size_t)g->ncore * n * sizeof(uint32_t), st));
     SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)n * sizeof(int), st));
+    SRT_HIPCHK(hipEventRecord(ev.e[0], st));
     int rc = srt_wgsssp_rows(n, g->rpo, g->cw, g->r, NULL, g->max_w, 0, g->ncore, g->dcore, lat_rows,
                              rel_rows, ovf, st, g->ridx, g->rtab, 1, codes);
+    if (!rc && hipEventRecord(ev.e[1], st) != hipSuccess) rc = SRT_E_DEVICE;
     std::vector<int> hov((size_t)n);
     if (!rc && hipMemcpyAsync(hov.data(), ovf, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, st) !=
                    hipSuccess)
@@ -617,7 +635,13 @@ static int sparse_rows_derived(const srt_sparse_graph* g, uint32_t* lat_rows, do
     else if (!rc)
         rc = srt_derive_rows_async(n, g->nI, g->dI, 0, g->rpo, g->cw, g->ridx, g->rtab, g->ntab,
                                    g->crow, codes, lat_rows, rel_rows, (size_t)n, st);
+    if (!rc && hipEventRecord(ev.e[2], st) != hipSuccess) rc = SRT_E_DEVICE;
     (void)hipFreeAsync(codes, st);
+    if (!rc && hipEventSynchronize(ev.e[2]) == hipSuccess) {
+        (void)hipEventElapsedTime(&tm->core, ev.e[0], ev.e[1]);
+        (void)hipEventElapsedTime(&tm->derive, ev.e[1], ev.e[2]);
+        tm->fallback = core_ovf;
+    }
     return rc;
 }
 
@@ -820,6 +844,7 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
         }
     }
     bool derived = false;
+    derived_times dtm;
     bool wg = !ms && !g->directed && g->n <= srt_wgsssp_max_n() &&
               (k_wg || (!k_wave && srt_form_int("wg", 1) != 0 && g->n > 32768 && !g->local));
     /* the workgroup kernel keeps its row in LDS (any order serves), so it runs on the original
@@ -852,7 +877,7 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
                   g->rtab && g->max_w < 128 && g->arcs < (1 << 20) &&
                   srt_form_int("wg_compact", 1) != 0 && srt_form_int("derive", 1) != 0;
         if (derived)
-            rc = sparse_rows_derived(g, lat_rows, rel_rows, ovf, st);
+            rc = sparse_rows_derived(g, lat_rows, rel_rows, ovf, st, &dtm);
         else if (wg && nsrc > 1)
             rc = srt_wgsssp_rows(g->n, wrp, wcw, wr, winv, g->max_w, b0 + 1, b0 + nsrc,
                                  one(1), lat_rows + (size_t)g->n, rel_rows + (size_t)g->n, ovf + 1,
@@ -930,6 +955,13 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
         stats->dist_enc = ms ? 3 : wg ? 2 : 1;
         stats->fw_block = form;       /* sparse builds: the kernel's form (srt_sparse_last_form) */
         stats->tied_pairs = tied;
+        /* derived builds: the split of the timed span, and the derivation's algorithmic bytes per
+         * row -- the neighbours' distance rows (4 B per target each), one optimal neighbour's
+         * canonical arcs (4 B) and the output rows (4 + 8 B) */
+        stats->n_derived = derived && !dtm.fallback ? g->nI : 0;
+        stats->ms_core = derived ? dtm.core : 0.0;
+        stats->ms_derive = derived ? dtm.derive : 0.0;
+        stats->work_bytes = stats->n_derived ? (g->degI + 4 * (int64_t)g->nI) * 4 * (int64_t)g->n : 0;
     }
     return SRT_OK;
 }
