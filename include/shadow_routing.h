@@ -285,6 +285,10 @@ typedef int (*srt_pair_reach_fn)(void* ctx, int32_t s, int32_t t);
 void srt_pair_order_set_reach(srt_pair_order* po, srt_pair_reach_fn fn, void* ctx);
 /* recorded source runs of v (one per attach epoch it ran in) */
 int32_t srt_pair_order_runs(srt_pair_order* po, int32_t v);
+/* the reference's path counters (topology.c:78-79): lookups that would have run a source's
+ * Dijkstra (shortestPathCount, :1719; on a directed graph every lookup not served s's own path) and
+ * the self paths computed (selfPathCount, :1536); shortest-path mode only */
+void srt_pair_order_counts(srt_pair_order* po, uint32_t* source_runs, uint32_t* self_paths);
 
 int srt_device_count(void);
 int srt_device_sync(int32_t device);

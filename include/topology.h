@@ -67,6 +67,13 @@ int topology_getTable(Topology* top, const uint32_t** latQ, uint64_t* quantumNs,
  * when every edge latency is whole ms: lat_q * quantum / 1e6 is then the reference's value). */
 int srt_topology_table_info(Topology* top, const int32_t** verts, int32_t* nslot,
                             const double** latMs);
+/* The reference's diagnostics (topology.c:78-79, logged by _topology_clearCache at :1142-1164,
+ * which topology_free also logs): lookups that would have run a source's Dijkstra
+ * (shortestPathCount) and self paths computed (selfPathCount); and the table builds this
+ * topology ran with their device time (HIP events, the analogue of USE_PERF_TIMERS'
+ * shortestPathTotalTime). Any pointer may be NULL. */
+int srt_topology_path_counts(Topology* top, uint32_t* shortestPathCount, uint32_t* selfPathCount,
+                             int32_t* builds, double* buildSeconds);
 /* Receive the runahead minimum instead of worker_updateMinTimeJump (tests, embedders); NULL
  * restores the Shadow call. Process-wide. */
 void srt_set_min_time_jump_hook(void (*fn)(double minPathLatencyMs));

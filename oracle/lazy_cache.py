@@ -51,6 +51,7 @@ class LazyPathCache:
         self.minimum_path_latency = 0.0  # :1254
         self.exports = []                # worker_updateMinTimeJump arguments, in order
         self.source_runs = 0             # shortestPathCount (:1719)
+        self.self_runs = 0               # selfPathCount (:1536)
 
     # -- attach / detach ------------------------------------------------------------------
     def attach(self, ip, vertex: int) -> None:
@@ -85,6 +86,7 @@ class LazyPathCache:
 
     def _compute_source(self, s, d) -> bool:
         if s == d:  # _topology_computeShortestPathToSelf
+            self.self_runs += 1
             self._store(True, s, s, self.lat_ms[s, s], self.rel[s, s])
             return True
         self.source_runs += 1

@@ -121,6 +121,7 @@ SIGNATURES = {
     "srt_pair_order_lookup": (_I32, [_VP, _I32, _I32, _VP, _VP]),
     "srt_pair_order_peek": (_I32, [_VP, _I32, _I32]),
     "srt_pair_order_runs": (_I32, [_VP, _I32]),
+    "srt_pair_order_counts": (None, [_VP, _VP, _VP]),
     "srt_pair_order_set_reach": (None, [_VP, _VP, _VP]),
     "srt_device_count": (ctypes.c_int, []),
     "srt_device_sync": (ctypes.c_int, [_I32]),
@@ -157,6 +158,7 @@ SIGNATURES = {
     "srt_topology_edges": (ctypes.c_int, [_VP, _VP]),
     "srt_topology_min_latency_ms": (_D, [_VP]),
     "srt_topology_table_info": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
+    "srt_topology_path_counts": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
     "srt_set_min_time_jump_hook": (None, [_VP]),
     "srt_topology_set_build_opts": (None, [_VP, _VP]),
     "srt_topology_last_stats": (ctypes.c_int, [_VP, _VP]),

@@ -73,6 +73,9 @@ struct srt_pair_order {
     _Atomic uint64_t* pairbits;  /* direct mode: 2 bits per unordered pair {a < b} */
     srt_pair_reach_fn reach;     /* NULL: every pair reachable */
     void* reach_ctx;
+    /* the reference's diagnostics (topology.c:78-79): lookups that miss its cache and run a
+     * source (shortestPathCount, :1719) or the self path (selfPathCount, :1536) */
+    atomic_uint source_runs, self_runs;
 };
 
 void srt_pair_order_set_reach(srt_pair_order* po, srt_pair_reach_fn fn, void* ctx) {
@@ -260,8 +263,11 @@ int32_t srt_pair_order_lookup(srt_pair_order* po, int32_t s, int32_t t, srt_pair
     if (!po || s < 0 || t < 0 || s >= po->n || t >= po->n) return SRT_E_ARG;
     if (att_of(po, s) == INT32_MAX || att_of(po, t) == INT32_MAX) return SRT_E_UNATTACHED;
     if (s == t) { /* (s, s): the self path, stored on its first lookup (:1597-1599, :1573) */
-        if (!atomic_exchange_explicit(&po->self_done[s], 1, memory_order_acq_rel) && on_store)
-            on_store(ctx, s, &s, 1);
+        if (!atomic_exchange_explicit(&po->self_done[s], 1, memory_order_acq_rel)) {
+            if (po->per_source) /* direct mode takes the self-loop edge, uncounted (:1816) */
+                atomic_fetch_add_explicit(&po->self_runs, 1u, memory_order_relaxed);
+            if (on_store) on_store(ctx, s, &s, 1);
+        }
         return s;
     }
     if (!po->per_source) { /* direct mode: the pair itself (:1816-1858) */
@@ -283,12 +289,17 @@ int32_t srt_pair_order_lookup(srt_pair_order* po, int32_t s, int32_t t, srt_pair
     }
     int32_t f = stored_from(po, s, t);
     if (f == s) return s;
+    /* directed: the reference's cache probe is (s, t) only (:1917-1921), so every lookup not
+     * served s's own path runs source s again (:1923-1961), storing nothing new after the first
+     * run of an attach epoch */
+    if (po->directed) atomic_fetch_add_explicit(&po->source_runs, 1u, memory_order_relaxed);
     if (f == t && (!po->directed || last_epoch(po, s) == atomic_load(&po->epoch))) return t;
     /* a miss: source s runs (undirected: the pair is not stored; directed: (s, t) is not, and s
      * has not run since the attached set last grew) */
     pthread_mutex_lock(&po->mu);
     f = stored_from_raw(po, s, t);
     const int run = po->directed ? (f != s && last_epoch(po, s) != atomic_load(&po->epoch)) : f < 0;
+    if (run && !po->directed) atomic_fetch_add_explicit(&po->source_runs, 1u, memory_order_relaxed);
     if (run) {
         const int32_t k = record_run(po, s);
         if (k < 0) {
@@ -314,6 +325,11 @@ int32_t srt_pair_order_peek(srt_pair_order* po, int32_t s, int32_t t) {
         return (bits & 1u) ? ((bits & 2u) ? hi : lo) : -1;
     }
     return stored_from(po, s, t);
+}
+
+void srt_pair_order_counts(srt_pair_order* po, uint32_t* source_runs, uint32_t* self_paths) {
+    if (source_runs) *source_runs = po ? atomic_load(&po->source_runs) : 0u;
+    if (self_paths) *self_paths = po ? atomic_load(&po->self_runs) : 0u;
 }
 
 int32_t srt_pair_order_runs(srt_pair_order* po, int32_t v) {

@@ -263,6 +263,8 @@ struct _Topology {
     double min_path_ms;
     srt_build_opts opts;
     srt_build_stats stats;
+    int32_t builds;       /* table generations built */
+    double build_seconds; /* their device time (srt_build_stats.ms_total) */
     /* counters (lock-free) */
     cntmap_t counters;
     /* attach index (built on the first attach) */
@@ -657,8 +659,27 @@ Topology* topology_new(const char* graphPath, int useShortestPath) {
     return t;
 }
 
+int srt_topology_path_counts(Topology* t, uint32_t* shortestPathCount, uint32_t* selfPathCount,
+                             int32_t* builds, double* buildSeconds) {
+    if (!magic_ok(t)) return SRT_E_ARG;
+    srt_pair_order_counts(t->po, shortestPathCount, selfPathCount);
+    pthread_mutex_lock(&t->build_lock);
+    if (builds) *builds = t->builds;
+    if (buildSeconds) *buildSeconds = t->build_seconds;
+    pthread_mutex_unlock(&t->build_lock);
+    return SRT_OK;
+}
+
 void topology_free(Topology* t) {
     if (!t) return;
+    if (t->po) { /* _topology_clearCache's summary (topology.c:1142-1164) */
+        uint32_t sp = 0, self = 0;
+        srt_pair_order_counts(t->po, &sp, &self);
+        srt_log(SRT_LOG_INFO, "path cache cleared, computed %u shortest paths with dijkstra, and %u "
+                "shortest self paths", sp, self);
+        srt_log(SRT_LOG_INFO, "routing tables: %d builds, %f seconds of device time", t->builds,
+                t->build_seconds);
+    }
     free(t->vid);
     free(t->vip);
     free(t->vcity);
@@ -1258,6 +1279,8 @@ static int build_generation(Topology* t, int nGPUs) {
     }
     tb->prev = atomic_load(&t->tb);
     atomic_store_explicit(&t->tb, tb, memory_order_release);
+    t->builds++;
+    t->build_seconds += t->stats.ms_total * 1e-3;
     srt_log(SRT_LOG_INFO, "routing tables built over %d of %d vertices (%s)", k, n,
             tb->all ? "all" : "attached");
     return SRT_OK;

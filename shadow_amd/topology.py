@@ -201,6 +201,17 @@ class Topology:
         yet); the lazy-cache order of topology.c:1189-1215, :1900-1981."""
         return lib().srt_topology_path_source_ip(self._h, ip_to_net(src), ip_to_net(dst))
 
+    def path_counts(self) -> dict:
+        """The reference's diagnostics (topology.c:78-79, logged at :1142-1164): lookups that
+        would have run a source's Dijkstra, self paths computed, and the table builds run here
+        with their device seconds."""
+        sp, sf, nb, sec = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int32(), ctypes.c_double()
+        check(lib().srt_topology_path_counts(self._h, ctypes.byref(sp), ctypes.byref(sf),
+                                             ctypes.byref(nb), ctypes.byref(sec)),
+              "srt_topology_path_counts")
+        return {"shortest_paths": sp.value, "self_paths": sf.value, "builds": nb.value,
+                "build_seconds": sec.value}
+
     def send_packet(self, src, dst, chance: float, bootstrapping: bool = False,
                     payload_length: int = 1):
         """worker_sendPacket's decision (worker.c:541-555): (delivered, delay_ns or None)."""

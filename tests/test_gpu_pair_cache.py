@@ -106,6 +106,11 @@ def _replay(g, gml, use_sp=True, algo=ALGO_AUTO, ops=2500, hosts=None, late=0, s
                     stats["differs"] += int(raw["rel"][x, y] != raw["rel"][y, x] or
                                             raw["lat_ms"][x, y] != raw["lat_ms"][y, x])
         stats["runs"] = sim.source_runs
+        # the reference's diagnostics (topology.c:78-79): Dijkstra runs and self paths
+        pc = top.path_counts()
+        want = (sim.source_runs, sim.self_runs) if use_sp else (0, 0)
+        assert (pc["shortest_paths"], pc["self_paths"]) == want, (pc, want)
+        assert pc["builds"] >= 1 and pc["build_seconds"] > 0
         return stats
     finally:
         top.free()

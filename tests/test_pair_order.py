@@ -86,6 +86,10 @@ def _replay(n, directed, use_sp, seed, ops, late_attach, oneway=False):
                     p = sim._get(x, x)
                 want = -1 if p is None else p.src
                 assert L.srt_pair_order_peek(po, x, y) == want, (x, y)
+        # the reference's diagnostics (topology.c:78-79): Dijkstra runs and self paths
+        runs, selfs = ctypes.c_uint32(), ctypes.c_uint32()
+        L.srt_pair_order_counts(po, ctypes.byref(runs), ctypes.byref(selfs))
+        assert (runs.value, selfs.value) == ((sim.source_runs, sim.self_runs) if use_sp else (0, 0))
         if use_sp:
             # one recorded run per source per attach epoch it ran in (directed sources re-run on
             # every miss in the reference; those re-runs store nothing new)
