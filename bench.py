@@ -504,9 +504,11 @@ def dense_levels_tail(c: Ctx, wl, step, elapsed, stats, lat, rel, nr, ld):
         weight w < d, target j, 32-source word) -- srt_build_stats.work_bytes (mostly L2/MALL
         hits: the planes are re-read by every in-arc);
       lvl_pred_kernel: every level plane read once (levels x n x nsrc / 8 B) and the
-        target-major predecessor (2 B while n <= 32768) and arc reliability (8 B) of every pair;
-      rel_tree_kernel: per pair the u8 level, the int32 predecessor and the arc reliability read
-        and the reliability written once (1 + 4 + 8 + 8 B)."""
+        target-major predecessor (2 B while n <= 32768) and arc reliability (8 B) of every pair,
+        or one packed 4-B word (predecessor | index into the build's table of distinct arc
+        reliabilities, srt_build_stats.rel_table > 0);
+      rel_tree_kernel: per pair the u8 level, the predecessor and the arc reliability read and
+        the reliability written once (1 + 4 + 8 + 8 B; packed: 1 + 4 + 8 B)."""
     n, world = wl["n"], c.world
     n_upd = sum(s.n_update for s in stats)
     ms_upd = sum(s.ms_update for s in stats)
@@ -516,19 +518,26 @@ def dense_levels_tail(c: Ctx, wl, step, elapsed, stats, lat, rel, nr, ld):
     levels = int(s0.levels)
     pairs = float(nr) * n
     pbytes = 2.0 if n <= 32768 else 4.0
+    ntab = int(s0.rel_table)
+    pair_pred = 4.0 if ntab else pbytes + 8
+    pair_rel = 13.0 if ntab else 21.0
     kern = {
         "lvl_step_kernel": (ms_upd / max(n_upd, 1), wbytes / max(n_upd, 1), n_upd,
                             "per level d: one 4-B Delta_{d-w}[k] word gathered per (in-arc k->j "
                             "of weight w < d, target j, 32-source word); averaged over the "
                             f"{levels} levels of a build"),
         "lvl_pred_kernel": (sum(s.ms_pred for s in stats) / k,
-                            levels * n * nr / 8.0 + pairs * (pbytes + 8), k,
-                            "every level plane read once (levels x n x nsrc / 8 B) + the "
-                            f"target-major predecessor ({int(pbytes)} B) and arc reliability "
-                            "(8 B) of every pair"),
-        "rel_tree_kernel": (sum(s.ms_rel for s in stats) / k, pairs * 21.0, k,
-                            "per pair: u8 level + int32 predecessor + f64 arc reliability read, "
-                            "f64 reliability written (21 B)"),
+                            levels * n * nr / 8.0 + pairs * pair_pred, k,
+                            "every level plane read once (levels x n x nsrc / 8 B) + per pair "
+                            + (f"one packed word (u16 predecessor | u16 index into the {ntab} "
+                               "distinct arc reliabilities, 4 B)" if ntab else
+                               f"the target-major predecessor ({int(pbytes)} B) and arc "
+                               "reliability (8 B)")),
+        "rel_tree_kernel": (sum(s.ms_rel for s in stats) / k, pairs * pair_rel, k,
+                            ("per pair: u8 level + packed predecessor/index word read, f64 "
+                             "reliability written (13 B)" if ntab else
+                             "per pair: u8 level + int32 predecessor + f64 arc reliability read, "
+                             "f64 reliability written (21 B)")),
     }
     total = {name: v[0] * v[2] / k for name, v in kern.items()}  # ms per build
     dom = max(total, key=total.get)
@@ -557,6 +566,8 @@ def dense_levels_tail(c: Ctx, wl, step, elapsed, stats, lat, rel, nr, ld):
     cpu, parity = dense_cpu_and_parity(c, wl, step, lat, rel)
     config = {"workload": wl["desc"], "n": n, "ld": ld, "distances": "bit-parallel Dial levels",
               "levels": int(s0.levels),
+              # distinct arc reliabilities of the packed post pass (0: f64 rows)
+              "rel_table": int(s0.rel_table),
               "parallelism": f"row-shard x{world}" + (" (no collective during the levels: "
                                                       "each rank's in-arc segment broadcast "
                                                       "once, one verdict all-reduce)"

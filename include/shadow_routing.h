@@ -113,6 +113,8 @@ typedef struct srt_build_stats {
     double ms_core;      /* ... HIP-event time of the core rows' kernel (with their canonical arcs) */
     double ms_derive;    /* ... and of the derivation (or of the kernel for the set's rows, when a
                           * core row overflowed its buckets: n_derived = 0) */
+    int32_t rel_table;   /* dense level builds: the distinct arc reliabilities of the packed post
+                          * pass (predecessor | reliability index words); 0 = f64 rows */
 } srt_build_stats;
 
 /* Build the full tables for an edge list on one GPU; outputs are host buffers of n*n entries.

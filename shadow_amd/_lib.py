@@ -70,6 +70,7 @@ class BuildStats(ctypes.Structure):
         ("n_derived", ctypes.c_int32),
         ("ms_core", ctypes.c_double),
         ("ms_derive", ctypes.c_double),
+        ("rel_table", ctypes.c_int32),
     ]
 
 

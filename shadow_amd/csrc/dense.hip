@@ -864,7 +864,12 @@ __global__ __launch_bounds__(512) void rel_sweeps_kernel(int n, int ld, int row0
     uint32_t* fresh = done + nw;                           /* resolved during this sweep */
     const PT* pg = pred + (size_t)blockIdx.x * ld;
     double* rr = rel + (size_t)blockIdx.x * ld;
-    for (int t = threadIdx.x; t < n; t += blockDim.x) pu[t] = pg[t];
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        if constexpr (std::is_same_v<PT, uint32_t>) /* packed rows: the low half, int16 */
+            pu[t] = (int32_t)(int16_t)(pg[t] & 0xFFFFu);
+        else
+            pu[t] = pg[t];
+    }
     for (int q = threadIdx.x; q < nw; q += blockDim.x) {
         done[q] = 0u;
         fresh[q] = 0u;
@@ -1017,10 +1022,13 @@ __global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
  * parents' slots and files the parents among them; the row is written once at the end. Rows with
  * more parents than the cap slots (or a distance range beyond maxl) return untouched and flagged
  * for rel_sweeps_kernel. Dynamic LDS: rel_tree_lds(NT, PER, cap). */
-static constexpr size_t rel_tree_lds(int nt, int per, int cap) {
-    return (size_t)8 * nt + (size_t)2 * nt * per + (size_t)8 * cap;
+static constexpr size_t rel_tree_lds(int nt, int per, int cap, int ntab = 0) {
+    return (size_t)8 * nt + (size_t)2 * nt * per + (size_t)8 * cap + (size_t)8 * ntab;
 }
 
+/* PT = uint32_t: the packed rows of the level build (predecessor | reliability index << 16,
+ * srt_levels_rtab): the arc reliability comes from the table (in LDS) instead of the rel row, which
+ * is then written, not read -- every entry, 0.0 for the unreachable ones. */
 template <int NT, int PER, typename LT, typename PT = int32_t>
 __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
                                                       const LT* __restrict__ lat,
@@ -1028,7 +1036,10 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
                                                       double* __restrict__ rel, int maxl, int cap,
                                                       int32_t* __restrict__ max_depth,
                                                       int32_t* __restrict__ sweep,
-                                                      const int32_t* __restrict__ srcs = nullptr) {
+                                                      const int32_t* __restrict__ srcs = nullptr,
+                                                      const double* __restrict__ rtab = nullptr,
+                                                      int ntab = 0) {
+    constexpr bool PK = std::is_same_v<PT, uint32_t>;
     const int s = srcs ? srcs[blockIdx.x] : row0 + blockIdx.x; /* srcs: row i is source srcs[i] */
     if (s >= n) return;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1038,8 +1049,14 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
     uint32_t* pre = tsm + NT;                                     /* parents before each word */
     uint16_t* spu = reinterpret_cast<uint16_t*>(tsm + 2 * NT);    /* predecessor per target */
     double* slot = reinterpret_cast<double*>(spu + NT * PER);     /* cap parent values */
+    double* srt = slot + cap;                                     /* PK: the ntab reliabilities */
     __shared__ uint32_t red[NT / 64], wsum[NT / 64];
     for (int q = tid; q < nw; q += NT) par[q] = 0u;
+    /* PK: each target's table index is stashed in the slot area until x is formed (the slots
+     * take parent values only after that; cap * 8 >= 2 * NT * PER) */
+    uint16_t* stash = reinterpret_cast<uint16_t*>(slot);
+    if constexpr (PK) /* the table, and 0.0 at ntab: the index of s and of unreachable targets */
+        for (int q = tid; q <= ntab; q += NT) srt[q] = q < ntab ? rtab[q] : 0.0;
     const LT* dl = lat + (size_t)blockIdx.x * ld;
     const PT* pg = pred + (size_t)blockIdx.x * ld;
     double* rr = rel + (size_t)blockIdx.x * ld;
@@ -1066,6 +1083,13 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
             p = __builtin_amdgcn_raw_buffer_load_b16(rp, tid * 2, i * NT * 2, 2);
         else
             p = __builtin_amdgcn_raw_buffer_load_b32(rp, tid * 4, i * NT * 4, 2);
+        if constexpr (PK) {
+            const uint32_t t = (uint32_t)(tid + i * NT);
+            const uint32_t hi = ((p & 0xFFFFu) == 0xFFFFu || t == (uint32_t)s || t >= (uint32_t)n)
+                                    ? (uint32_t)ntab : p >> 16;
+            stash[t] = (uint16_t)hi;
+            p &= 0xFFFFu;
+        }
         const uint32_t l = (tid + i * NT != s && d < SRT_INF) ? d : 0u;
         mx = max(mx, l);
         const uint32_t b = min(l, 255u) << (8 * (i & 3));
@@ -1101,16 +1125,36 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
     if (tid < nw) pre[tid] = base + inc - c;
     const bool bail = (int)mx > maxl || total > (uint32_t)cap;
     if (tid == 0) sweep[blockIdx.x] = bail;
-    if (bail) return; /* uniform: rel_sweeps_kernel takes the row from its untouched input */
-    if (mx == 0) { /* no reachable target: only rel(s, s) */
-        if (tid == 0) rr[s] = 1.0;
-        return;
-    }
+    if constexpr (PK) { /* the arc reliabilities from the table (0.0: s, unreachable) */
+        /* the levels packed before the 64 registers of x are loaded (else the compiler keeps the
+         * 32 unpacked level bytes beside them and spills) */
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const uint32_t v0 = __builtin_amdgcn_raw_buffer_load_b32(rv, tid * 8, i * NT * 8, 0);
-        const uint32_t v1 = __builtin_amdgcn_raw_buffer_load_b32(rv, tid * 8 + 4, i * NT * 8, 0);
-        x[i] = __hiloint2double((int)v1, (int)v0);
+        for (int k = 0; k < PER / 4; ++k) asm volatile("" : "+v"(lv[k]));
+        int tx = tid; /* opaque: no stash addresses kept from the load loop */
+        asm volatile("" : "+v"(tx));
+        if (bail || mx == 0) { /* rel_sweeps_kernel's input: r(pred, t) in the rel row (mx = 0:
+                                * every entry 0.0, and rel(s, s) = 1) */
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int t = tx + i * NT;
+                if (t < n) rr[t] = !bail && t == s ? 1.0 : srt[stash[t]];
+            }
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < PER; ++i) x[i] = srt[stash[tx + i * NT]];
+    } else {
+        if (bail) return; /* uniform: rel_sweeps_kernel takes the row from its untouched input */
+        if (mx == 0) { /* no reachable target: only rel(s, s) */
+            if (tid == 0) rr[s] = 1.0;
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const uint32_t v0 = __builtin_amdgcn_raw_buffer_load_b32(rv, tid * 8, i * NT * 8, 0);
+            const uint32_t v1 = __builtin_amdgcn_raw_buffer_load_b32(rv, tid * 8 + 4, i * NT * 8, 0);
+            x[i] = __hiloint2double((int)v1, (int)v0);
+        }
     }
     __syncthreads();
     auto rank = [&](uint32_t u) {
@@ -1142,7 +1186,9 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
         const int t = tw + i * NT;
-        if (t < n && ((lv[i >> 2] >> (8 * (i & 3))) & 0xFFu)) __builtin_nontemporal_store(x[i], rr + t);
+        /* PK: every entry (the row was not pre-filled); rel(s, s) = 1 */
+        if (t < n && (PK || ((lv[i >> 2] >> (8 * (i & 3))) & 0xFFu)))
+            __builtin_nontemporal_store(PK && t == s ? 1.0 : x[i], rr + t);
     }
     if (tid == 0) {
         rr[s] = 1.0;
@@ -1154,23 +1200,28 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
 template <typename LT, typename PT>
 static void rel_tree_launch(int n, int ld, int row0, int lrows, const LT* d, const PT* pred,
                             double* rel, int32_t* depth, int32_t* sweep, const int32_t* srcs,
-                            hipStream_t st) {
+                            hipStream_t st, const double* rtab = nullptr, int ntab = 0) {
     if (n <= 1024) {
-        rel_tree_kernel<256, 4, LT, PT><<<lrows, 256, rel_tree_lds(256, 4, 1024), st>>>(
-            n, ld, row0, d, pred, rel, 64, 1024, depth, sweep, srcs);
+        const int lds = (int)rel_tree_lds(256, 4, 1024, ntab + 1);
+        (void)hipFuncSetAttribute((const void*)rel_tree_kernel<256, 4, LT, PT>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        rel_tree_kernel<256, 4, LT, PT><<<lrows, 256, lds, st>>>(
+            n, ld, row0, d, pred, rel, 64, 1024, depth, sweep, srcs, rtab, ntab);
     } else if (n <= 4096) {
-        const int lds = (int)rel_tree_lds(512, 8, 4096);
+        const int lds = (int)rel_tree_lds(512, 8, 4096, ntab + 1);
         (void)hipFuncSetAttribute((const void*)rel_tree_kernel<512, 8, LT, PT>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         rel_tree_kernel<512, 8, LT, PT><<<lrows, 512, lds, st>>>(n, ld, row0, d, pred, rel, 64, 4096,
-                                                                 depth, sweep, srcs);
+                                                                 depth, sweep, srcs, rtab, ntab);
     } else {
-        /* 64 KB of predecessors and 7,168 parent slots (C4 rows have ~1-3k parents): 128 KB */
-        const int cap = 7168, lds = (int)rel_tree_lds(1024, 32, cap);
+        /* 64 KB of predecessors and 7,168 parent slots (C4 rows have ~1-3k parents): 128 KB; the
+         * packed form: 8,192 slots (its index stash) and the table (<= 2,049 values): 152 KB */
+        const int cap = rtab ? 8192 : 7168, lds = (int)rel_tree_lds(1024, 32, cap, ntab + 1);
         (void)hipFuncSetAttribute((const void*)rel_tree_kernel<1024, 32, LT, PT>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         rel_tree_kernel<1024, 32, LT, PT><<<lrows, 1024, lds, st>>>(n, ld, row0, d, pred, rel, 64,
-                                                                    cap, depth, sweep, srcs);
+                                                                    cap, depth, sweep, srcs, rtab,
+                                                                    ntab);
     }
 }
 
@@ -1180,9 +1231,21 @@ static void rel_tree_launch(int n, int ld, int row0, int lrows, const LT* d, con
 static int rel_rows_launch(int n, int ld, int row0, int lrows, const uint32_t* d, int32_t* pred,
                            double* rel, int32_t* depth, int32_t* sweep, const int32_t* srcs,
                            hipStream_t st, const uint8_t* l8 = nullptr,
-                           const int16_t* pred16 = nullptr) {
+                           const int16_t* pred16 = nullptr, const uint32_t* pk = nullptr,
+                           const double* rtab = nullptr, int ntab = 0) {
     if (lrows <= 0) return SRT_OK;
     const bool tree = n <= 32768 && srt_form_int("reltree", 1) != 0;
+    if (pk) { /* a level build's u8 rows and packed (predecessor | reliability index) rows */
+        rel_tree_launch(n, ld, row0, lrows, l8, pk, rel, depth, sweep, srcs, st, rtab, ntab);
+        SRT_HIPCHK(hipGetLastError());
+        const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel<uint32_t>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        rel_sweeps_kernel<uint32_t><<<lrows, 512, lds, st>>>(n, ld, row0, pk, rel, depth, sweep,
+                                                             srcs);
+        SRT_HIPCHK(hipGetLastError());
+        return SRT_OK;
+    }
     if (pred16) { /* a level build's u8 distance rows and int16 predecessor rows (n <= 32768) */
         rel_tree_launch(n, ld, row0, lrows, l8, pred16, rel, depth, sweep, srcs, st);
         SRT_HIPCHK(hipGetLastError());
@@ -1313,7 +1376,8 @@ typedef struct {
     hipEvent_t kev[4];
     int kev_on;
     int diag_done; /* the level post pass applied the diagonal rule itself */
-    int pred16;    /* dt holds int16 predecessor rows (level post pass, n <= 32768) */
+    int pred16;    /* dt holds int16 predecessor rows (level post pass, n <= 32768; 2: packed
+                    * predecessor | reliability index words) */
 } dense_ws;
 
 static dense_ws g_ws[SRT_STATE_SLOTS];
@@ -1580,29 +1644,39 @@ static int dense_post_levels(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
             for (int i = 0; i < 4; i++) SRT_HIPCHK(hipEventCreate(&ws->kev[i]));
         if (kt) SRT_HIPCHK(hipEventRecord(ws->kev[0], st));
         /* int16 predecessors while every vertex fits (half the slab's bytes), widened by the
-         * transpose into the int32 rows the reliability passes read */
-        const int p16 = n <= 32768;
+         * transpose into the int32 rows the reliability passes read; with the build's table of
+         * distinct arc reliabilities, one packed word per pair (predecessor | index << 16): 4 B
+         * written, transposed and read instead of 2 + 8 */
+        int ntab = 0;
+        const double* rtab = n <= 32768 ? srt_levels_rtab(&ntab) : nullptr;
+        const int p16 = rtab ? 2 : n <= 32768;
+        if (stats) stats->rel_table = rtab ? ntab : 0;
         if ((rc = srt_levels_pred(ws->predt, p16, ws->rt, (size_t)nrows, ties ? ws->ties : NULL, st)))
             return rc;
         if (kt) SRT_HIPCHK(hipEventRecord(ws->kev[1], st));
         int32_t* pred = reinterpret_cast<int32_t*>(ws->dt);
-        int16_t* pred16 = p16 ? reinterpret_cast<int16_t*>(ws->dt) : nullptr;
+        int16_t* pred16 = p16 == 1 ? reinterpret_cast<int16_t*>(ws->dt) : nullptr;
+        uint32_t* pk = p16 == 2 ? reinterpret_cast<uint32_t*>(ws->dt) : nullptr;
         ws->pred16 = p16;
-        if (p16) /* int16 rows: the reliability passes read them as they are */
+        if (pk)
+            transpose_kernel<uint32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+                n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows, pk, (size_t)ld);
+        else if (p16) /* int16 rows: the reliability passes read them as they are */
             transpose_kernel<int16_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
                 n, nrows, reinterpret_cast<const int16_t*>(ws->predt), (size_t)nrows, pred16, (size_t)ld);
         else
             transpose_kernel<uint32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
                 n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows,
                 reinterpret_cast<uint32_t*>(pred), (size_t)ld);
-        transpose_kernel<double><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
-            n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
+        if (!pk)
+            transpose_kernel<double><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+                n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
         SRT_HIPCHK(hipMemsetAsync(ws->depth, 0, sizeof(int32_t), st));
         /* every level-built distance is <= 254 quanta: level order in place for every row that
          * spans <= 64 quanta, sweeps for the rest (as dense_post); the level rows as u8 */
         if (kt) SRT_HIPCHK(hipEventRecord(ws->kev[2], st));
         if ((rc = rel_rows_launch(n, ld, row0, lrows, d, pred, rel, ws->depth, ws->cursor, nullptr,
-                                  st, srt_levels_l8(), pred16)))
+                                  st, srt_levels_l8(), pred16, pk, rtab, ntab)))
             return rc;
         if (kt) {
             SRT_HIPCHK(hipEventRecord(ws->kev[3], st));
@@ -1963,10 +2037,11 @@ struct build_events {
 
 /* f64 path-order ms rows [row0, row0 + lrows) from the predecessor rows the post pass left in the
  * workspace (tables.hip); runs after the diagonal rule */
-__global__ void widen16_kernel(size_t cnt, const int16_t* __restrict__ in, int32_t* __restrict__ out) {
+template <typename T>
+__global__ void widen16_kernel(size_t cnt, const T* __restrict__ in, int32_t* __restrict__ out) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt;
          i += (size_t)gridDim.x * blockDim.x)
-        out[i] = in[i];
+        out[i] = (int16_t)(in[i] & 0xFFFF); /* int16 rows, or the packed words' low half */
 }
 
 static int dense_path_ms(int32_t n, int32_t ld, int32_t row0, int32_t nrows, const uint32_t* d,
@@ -1980,8 +2055,13 @@ static int dense_path_ms(int32_t n, int32_t ld, int32_t row0, int32_t nrows, con
     if (ws->pred16) { /* the level post pass left int16 rows: widened into the free slab */
         const size_t cnt = (size_t)lrows * ld;
         const int64_t nb = srt_ceil_div((int64_t)cnt, 256);
-        widen16_kernel<<<(unsigned)(nb < 65536 ? nb : 65536), 256, 0, st>>>(
-            cnt, reinterpret_cast<const int16_t*>(ws->dt), ws->predt);
+        const unsigned g = (unsigned)(nb < 65536 ? nb : 65536);
+        if (ws->pred16 == 2)
+            widen16_kernel<uint32_t><<<g, 256, 0, st>>>(cnt, reinterpret_cast<const uint32_t*>(ws->dt),
+                                                        ws->predt);
+        else
+            widen16_kernel<int16_t><<<g, 256, 0, st>>>(cnt, reinterpret_cast<const int16_t*>(ws->dt),
+                                                       ws->predt);
         SRT_HIPCHK(hipGetLastError());
         pred = ws->predt;
     }

@@ -172,6 +172,77 @@ __global__ void lvl_mask_kernel(size_t count, int lmax, int32_t* __restrict__ cn
     if (i < count && (int)(i % LVL_STRIDE) > lmax) cnt[i] = 0;
 }
 
+/* ---- the arcs' distinct reliabilities (packed post pass) ------------------------------------ *
+ * The post pass carries r(pred, t) per pair as a 16-bit index into a table of the distinct arc
+ * reliabilities instead of the f64 itself (C4: 501 values): the predecessor and the index share one
+ * 4-B word (10 B per pair before, plus their two transposes). The table is exact -- each entry is
+ * an arc's double, bit for bit. An open-addressing hash over the value bits (LVL_RT_SLOTS slots,
+ * linear probing) gives each arc a slot, one workgroup numbers the occupied slots in slot order,
+ * and the arcs' slots become dense indices. More than LVL_RT_CAP distinct values (or a probe run
+ * past LVL_RT_PROBE) keeps the f64 form. */
+#define LVL_RT_SLOTS 65536
+#define LVL_RT_PROBE 256
+#define LVL_RT_CAP 2048
+static __device__ __forceinline__ unsigned lvl_rt_hash(unsigned long long b) {
+    b ^= b >> 33;
+    b *= 0xff51afd7ed558ccdull;
+    b ^= b >> 33;
+    return (unsigned)b & (LVL_RT_SLOTS - 1u);
+}
+__global__ void lvl_rt_hash_kernel(int total, const double* __restrict__ ar,
+                                   unsigned long long* __restrict__ H, uint16_t* __restrict__ rix,
+                                   int* __restrict__ ovf) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const unsigned long long b = (unsigned long long)__double_as_longlong(ar[i]);
+    unsigned h = lvl_rt_hash(b);
+    for (int p = 0; p < LVL_RT_PROBE; ++p, h = (h + 1u) & (LVL_RT_SLOTS - 1u)) {
+        unsigned long long v = __hip_atomic_load(&H[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v == ~0ull) v = atomicCAS(&H[h], ~0ull, b); /* ~0: empty (a NaN, never a reliability) */
+        if (v == ~0ull || v == b) {
+            rix[i] = (uint16_t)h;
+            return;
+        }
+    }
+    *ovf = 1;
+}
+/* one workgroup: dense index of every occupied slot (slot order), the table, its size */
+__global__ __launch_bounds__(1024) void lvl_rt_compact_kernel(const unsigned long long* __restrict__ H,
+                                                              uint16_t* __restrict__ map,
+                                                              double* __restrict__ rtab,
+                                                              int* __restrict__ ntab) {
+    constexpr int PER = LVL_RT_SLOTS / 1024;
+    __shared__ int wsum[16];
+    const int tid = threadIdx.x, lane = tid & 63;
+    int c = 0;
+    for (int k = 0; k < PER; ++k) c += H[tid * PER + k] != ~0ull;
+    int inc = c;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) wsum[tid >> 6] = inc;
+    __syncthreads();
+    int base = inc - c, total = 0;
+    for (int w = 0; w < 16; ++w) {
+        base += w < (tid >> 6) ? wsum[w] : 0;
+        total += wsum[w];
+    }
+    for (int k = 0; k < PER; ++k) {
+        const unsigned long long v = H[tid * PER + k];
+        if (v == ~0ull) continue;
+        map[tid * PER + k] = (uint16_t)base;
+        if (base < LVL_RT_CAP) rtab[base] = __longlong_as_double((long long)v);
+        ++base;
+    }
+    if (tid == 0) *ntab = total;
+}
+__global__ void lvl_rt_remap_kernel(int total, const uint16_t* __restrict__ map,
+                                    uint16_t* __restrict__ rix) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < total) rix[i] = map[rix[i]];
+}
+
 /* byte offset of each arc's source row inside a level plane (k * nw * 4; nw is this rank's) */
 __global__ void lvl_aoff_kernel(int total, int nw, const uint32_t* __restrict__ arcs,
                                 uint32_t* __restrict__ aoff) {
@@ -419,6 +490,8 @@ __global__ void lvl_segs_kernel(int ld, const int32_t* __restrict__ off, int32_t
     if (j <= ld) seg[j] = off[(size_t)j * LVL_STRIDE];
 }
 
+/* PT = uint32_t: the packed form -- one word per pair, (u16) predecessor | reliability index << 16
+ * (the arc's reliability is rtab[index], lvl_rtab_*), written into predT; rT and ar unused */
 /* Canonical predecessors from the levels (the rule of every build kernel: among the tight in-arcs
  * u -> t, D[s][u] + w = D[s][t], the smallest (D[s][u], u) -- so the largest w, then the smallest u;
  * Dijkstra with a (dist, vertex) heap, topology.c:1679-1701 up to igraph's tie order).
@@ -436,10 +509,12 @@ static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx
                                                        const uint32_t* __restrict__ arcs,
                                                        const uint32_t* __restrict__ aoff,
                                                        const double* __restrict__ ar,
+                                                       const uint16_t* __restrict__ rix,
                                                        const uint32_t* __restrict__ lev,
                                                        PT* __restrict__ predT,
                                                        double* __restrict__ rT, size_t ldp,
                                                        unsigned long long* __restrict__ ties) {
+    constexpr bool PK = std::is_same_v<PT, uint32_t>;
     const int tgrp = (n + 3) >> 2;
     const int c = (int)(g / (unsigned)tgrp);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -532,6 +607,7 @@ static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx
         const uint32_t ix[4] = {raw.x, raw.y, raw.z, raw.w};
         int32_t pv[8];
         double rv[8];
+        uint32_t kv[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const uint32_t x = (ix[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
@@ -539,9 +615,17 @@ static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx
             const bool h = sg < n && sg != t && x != 0xFFFFu;
             const int k = a_t + (h ? (int)x : 0);
             pv[e] = h ? (int)(arcs[k] & 0xFFFFu) : -1;
-            rv[e] = h ? ar[k] : 0.0;
+            if constexpr (PK)
+                kv[e] = ((uint32_t)pv[e] & 0xFFFFu) | (h ? (uint32_t)rix[k] << 16 : 0u);
+            else
+                rv[e] = h ? ar[k] : 0.0;
         }
         PT* pp = predT + (size_t)t * ldp + sl0;
+        if constexpr (PK) { /* 32 B per lane: a wave's quarter is one 2-KB run */
+            *reinterpret_cast<uint4*>(pp) = make_uint4(kv[0], kv[1], kv[2], kv[3]);
+            *reinterpret_cast<uint4*>(pp + 4) = make_uint4(kv[4], kv[5], kv[6], kv[7]);
+            continue;
+        }
         double* rp = rT + (size_t)t * ldp + sl0;
         if constexpr (sizeof(PT) == 2) { /* -1 -> 0xFFFF, read back as int16 -1 */
             uint32_t w2[4];
@@ -570,6 +654,7 @@ __global__ __launch_bounds__(256) void lvl_pred_kernel(int n, int nw, int nchunk
                                                        const uint32_t* __restrict__ arcs,
                                                        const uint32_t* __restrict__ aoff,
                                                        const double* __restrict__ ar,
+                                                       const uint16_t* __restrict__ rix,
                                                        const uint32_t* __restrict__ lev,
                                                        PT* __restrict__ predT,
                                                        double* __restrict__ rT, size_t ldp,
@@ -580,7 +665,7 @@ __global__ __launch_bounds__(256) void lvl_pred_kernel(int n, int nw, int nchunk
     const unsigned x = blockIdx.x & 7u, per = nblk >> 3, L = gridDim.x >> 3;
     for (unsigned u = blockIdx.x >> 3; u < per; u += L)
         lvl_pred_unit<PT>(u * 8u + x, sidx, n, nw, nchunk, src0, nsrc, nlev, off, arcs, aoff, ar,
-                          lev, predT, rT, ldp, ties);
+                          rix, lev, predT, rT, ldp, ties);
 }
 
 __global__ void lvl_sum_kernel(const unsigned long long* __restrict__ v, int k,
@@ -639,11 +724,14 @@ typedef struct {
     uint32_t* arcs;
     uint32_t* aoff;
     double* ar;
+    uint16_t* rix; /* packed form: each arc's index into rtab (NULL: more than LVL_RT_CAP values) */
+    double* rtab;
+    int ntab;
     uint32_t* lev;
     uint8_t* l8; /* u8 distance rows (nrows x ld) for the reliability pass */
     unsigned long long* dkey; /* the diagonal rule's key per local row (undirected rows form) */
     const double* r_rows;
-    void* p[20];
+    void* p[32]; /* every allocation of the build (LVL_ALLOC), freed together */
     int k;
     hipStream_t st;
 } lvl_state;
@@ -672,6 +760,13 @@ int srt_levels_diag(int n, int ld, uint32_t* d, double* rel, hipStream_t st, int
     return SRT_OK;
 }
 
+/* the held build's table of distinct arc reliabilities (packed form), NULL when it has none */
+const double* srt_levels_rtab(int* ntab) {
+    const lvl_state* L = &g_lvl[srt_state_slot()];
+    *ntab = L->held && L->rix ? L->ntab : 0;
+    return L->held && L->rix ? L->rtab : NULL;
+}
+
 const uint8_t* srt_levels_l8(void) {
     const lvl_state* L = &g_lvl[srt_state_slot()];
     return L->held ? L->l8 : NULL;
@@ -679,6 +774,10 @@ const uint8_t* srt_levels_l8(void) {
 
 #define LVL_ALLOC(ptr, bytes)                                      \
     do {                                                           \
+        if (L->k >= (int)(sizeof(L->p) / sizeof(L->p[0]))) {       \
+            srt_set_error("levels: allocation table full");        \
+            return SRT_E_NOMEM;                                    \
+        }                                                          \
         SRT_HIPCHK(srt_malloc_async(&(ptr), (bytes), st));         \
         L->p[L->k++] = (void*)(ptr);                               \
     } while (0)
@@ -814,6 +913,35 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         lvl_aoff_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, nw, arcs, aoff);
         SRT_HIPCHK(hipGetLastError());
     }
+    /* the distinct arc reliabilities (packed post pass, n <= 32768; SRT_FORM pk=0 keeps f64) */
+    uint16_t* rix = NULL;
+    double* rtab = NULL;
+    int ntab = 0;
+    if (total > 0 && n <= 32768 && srt_form_int("pk", 1) != 0) {
+        unsigned long long* H = NULL;
+        uint16_t* map = NULL;
+        int* dflag = NULL;
+        LVL_ALLOC(H, LVL_RT_SLOTS * sizeof(unsigned long long));
+        LVL_ALLOC(map, LVL_RT_SLOTS * sizeof(uint16_t));
+        LVL_ALLOC(rix, ((size_t)total + 8) * sizeof(uint16_t));
+        LVL_ALLOC(rtab, LVL_RT_CAP * sizeof(double));
+        LVL_ALLOC(dflag, 2 * sizeof(int));
+        SRT_HIPCHK(hipMemsetAsync(H, 0xFF, LVL_RT_SLOTS * sizeof(unsigned long long), st));
+        SRT_HIPCHK(hipMemsetAsync(dflag, 0, 2 * sizeof(int), st));
+        lvl_rt_hash_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, ar, H, rix, dflag);
+        lvl_rt_compact_kernel<<<1, 1024, 0, st>>>(H, map, rtab, dflag + 1);
+        lvl_rt_remap_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, map, rix);
+        SRT_HIPCHK(hipGetLastError());
+        int hf[2] = {0, 0};
+        SRT_HIPCHK(hipMemcpyAsync(hf, dflag, sizeof(hf), hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipStreamSynchronize(st));
+        if (hf[0] || hf[1] > LVL_RT_CAP) {
+            rix = NULL; /* (freed with the state) */
+            rtab = NULL;
+        } else {
+            ntab = hf[1];
+        }
+    }
     const size_t plane = (size_t)n * nw;
     uint32_t *lev = NULL, *Rb = NULL;
     uint8_t* done = NULL;
@@ -884,6 +1012,9 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     L->arcs = arcs;
     L->aoff = aoff;
     L->ar = ar;
+    L->rix = rix;
+    L->rtab = rtab;
+    L->ntab = ntab;
     L->lev = lev;
     L->l8 = l8;
     L->dkey = dkey;
@@ -897,6 +1028,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
  * 32768: half the bytes of the predecessor slab and its transpose), else int32. */
 int srt_levels_pred(void* predT, int pred16, double* rT, size_t ldp, unsigned long long* ties,
                     hipStream_t st) {
+    /* pred16 == 2: the packed form (srt_levels_rtab) */
     lvl_state* L = &g_lvl[srt_state_slot()];
     if (!L->held) {
         srt_set_error("levels: no held level build for the predecessor pass");
@@ -911,14 +1043,22 @@ int srt_levels_pred(void* predT, int pred16, double* rT, size_t ldp, unsigned lo
         srt_set_error("levels: int16 predecessors need n <= 32768 (n = %d)", L->n);
         return SRT_E_ARG;
     }
-    if (pred16)
+    if (pred16 == 2 && !L->rix) {
+        srt_set_error("levels: the packed form needs the reliability table");
+        return SRT_E_ARG;
+    }
+    if (pred16 == 2)
+        lvl_pred_kernel<uint32_t><<<lvl_grid((const void*)lvl_pred_kernel<uint32_t>, L->nblk), 256, 0, st>>>(
+            L->n, L->nw, L->nchunk, L->row0, L->nrows, L->D, L->nblk, L->off, L->arcs, L->aoff, L->ar,
+            L->rix, L->lev, (uint32_t*)predT, rT, ldp, part);
+    else if (pred16)
         lvl_pred_kernel<int16_t><<<lvl_grid((const void*)lvl_pred_kernel<int16_t>, L->nblk), 256, 0, st>>>(
             L->n, L->nw, L->nchunk, L->row0, L->nrows, L->D, L->nblk, L->off, L->arcs, L->aoff, L->ar,
-            L->lev, (int16_t*)predT, rT, ldp, part);
+            L->rix, L->lev, (int16_t*)predT, rT, ldp, part);
     else
         lvl_pred_kernel<int32_t><<<lvl_grid((const void*)lvl_pred_kernel<int32_t>, L->nblk), 256, 0, st>>>(
             L->n, L->nw, L->nchunk, L->row0, L->nrows, L->D, L->nblk, L->off, L->arcs, L->aoff, L->ar,
-            L->lev, (int32_t*)predT, rT, ldp, part);
+            L->rix, L->lev, (int32_t*)predT, rT, ldp, part);
     SRT_HIPCHK(hipGetLastError());
     if (ties) {
         lvl_sum_kernel<<<1, 1024, 0, st>>>(part, 1024, ties);

@@ -165,6 +165,9 @@ int srt_levels_pred(void* predT, int pred16, double* rT, size_t ldp, unsigned lo
 void srt_levels_release(hipStream_t st);
 /* the held build's u8 distance rows (nrows x ld, 0 on the diagonal), NULL if none */
 const uint8_t* srt_levels_l8(void);
+/* the held level build's distinct arc reliabilities (the packed post pass: predecessor | index << 16
+ * words, srt_levels_pred with pred16 = 2); NULL (ntab 0) when the build keeps the f64 form */
+const double* srt_levels_rtab(int* ntab);
 /* the diagonal rule of the held build's rows (keys from its row reads); *applied = 0 when it kept
  * none (directed builds: dense_diag_kernel) */
 int srt_levels_diag(int n, int ld, uint32_t* d, double* rel, hipStream_t st, int* applied);

@@ -49,10 +49,17 @@ def _directed_dense(n, seed, wmax):
     return graphs.Graph(n, True, src, dst, lat, loss, f"directed{n}")
 
 
-@pytest.mark.parametrize("kind", ["complete300", "complete1000", "ties", "directed", "c1like"])
+@pytest.mark.parametrize("kind", ["complete300", "complete1000", "ties", "directed", "c1like",
+                                  "f64form", "manyrel"])
 def test_levels_match_oracle(gpu, monkeypatch, kind):
+    """The post pass carries r(pred, t) as an index into the build's table of distinct arc
+    reliabilities (one packed word with the predecessor); "f64form" (SRT_FORM pk=0) and "manyrel"
+    (more distinct values than the table holds) take the f64 rows. "c1like" has distances past
+    64 quanta: its rows leave rel_tree_kernel for the sweeps."""
     set_form(monkeypatch, levels="1")
-    if kind == "complete300":
+    if kind == "f64form":
+        set_form(monkeypatch, levels="1", pk="0")
+    if kind in ("complete300", "f64form"):
         g = graphs.complete_graph(300, seed=7)
     elif kind == "complete1000":  # C2's distribution: distances up to 9 quanta
         g = graphs.complete_graph(1000, seed=2)
@@ -60,6 +67,10 @@ def test_levels_match_oracle(gpu, monkeypatch, kind):
         g = graphs.complete_graph(640, seed=11, lat_max=3)
     elif kind == "directed":  # in-arcs from the columns of w
         g = _directed_dense(500, 5, 40)
+    elif kind == "manyrel":  # 44,850 distinct loss values: past the table's 2,048
+        g0 = graphs.complete_graph(300, seed=9)
+        loss = np.random.default_rng(9).random(g0.m) * 0.05
+        g = graphs.Graph(g0.n, False, g0.src, g0.dst, g0.lat_ns, loss, "manyrel")
     else:  # C1's distribution at 50 vertices: distances of tens of quanta
         g = graphs.complete_graph(50, seed=1)
     lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
