@@ -1196,166 +1196,6 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
     }
 }
 
-/* The packed rows' form of rel_tree_kernel (a level build's u8 level rows and predecessor |
- * reliability-index words), restructured around what the general kernel spends its time on: a
- * pass there walks a thread's PER targets one by one, and every target of level L runs a chain of
- * four dependent LDS round trips (predecessor, its rank words, its slot, the parent test) -- with
- * ~6 passes of 32 targets that chain, not the row's 160 KB in / 256 KB out, set the time.
- * Here the predecessor of each own target stays in registers (u16 pairs) and, once the parents
- * are numbered, is replaced by its slot index; the targets that are parents are a register bit
- * mask. A pass is then one LDS read per target (the predecessor's slot), issued QB targets at a
- * time, plus the rare parent write. LDS: parent bitmap + prefix, the slots (which first hold the
- * table index of each target, cap * 8 >= 2 * NT * PER) and the reliability table (+ 0.0, 1.0). */
-static constexpr size_t rel_tree_pk_lds(int nt, int cap, int ntab1) {
-    return (size_t)8 * nt + (size_t)8 * cap + (size_t)8 * ntab1;
-}
-
-template <int NT, int PER>
-__global__ __launch_bounds__(NT) void rel_tree_pk_kernel(int n, int ld, int row0,
-                                                         const uint8_t* __restrict__ lat,
-                                                         const uint32_t* __restrict__ pred,
-                                                         double* __restrict__ rel, int maxl, int cap,
-                                                         int32_t* __restrict__ max_depth,
-                                                         int32_t* __restrict__ sweep,
-                                                         const int32_t* __restrict__ srcs,
-                                                         const double* __restrict__ rtab, int ntab) {
-    static_assert(PER <= 32, "parent mask: one bit per target of the thread");
-    constexpr int QB = 4; /* targets whose slot reads are in flight together */
-    const int s = srcs ? srcs[blockIdx.x] : row0 + blockIdx.x;
-    if (s >= n) return;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int nw = (n + 31) >> 5; /* <= NT */
-    extern __shared__ __attribute__((aligned(16))) uint32_t tsm[];
-    uint32_t* par = tsm;                                          /* parent bitmap, nw words */
-    uint32_t* pre = tsm + NT;                                     /* parents before each word */
-    double* slot = reinterpret_cast<double*>(tsm + 2 * NT);       /* cap parent values */
-    uint16_t* stash = reinterpret_cast<uint16_t*>(slot);          /* first: table index per target */
-    double* srt = slot + cap;                                     /* the ntab reliabilities, 0.0 */
-    __shared__ uint32_t red[NT / 64], wsum[NT / 64];
-    for (int q = tid; q < nw; q += NT) par[q] = 0u;
-    for (int q = tid; q <= ntab + 1; q += NT) srt[q] = q < ntab ? rtab[q] : q == ntab ? 0.0 : 1.0;
-    __syncthreads(); /* par zeroed: the parents are marked as the row loads */
-    const uint8_t* dl = lat + (size_t)blockIdx.x * ld;
-    const uint32_t* pg = pred + (size_t)blockIdx.x * ld;
-    double* rr = rel + (size_t)blockIdx.x * ld;
-    const __amdgpu_buffer_rsrc_t rd =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(dl), 0, n, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rp =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(pg), 0, n * 4, 0x00020000);
-    uint32_t lv[PER / 4];
-    uint32_t pu[PER / 2]; /* predecessors, then their slot indices (0xFFFF: rel(s, u) = 1) */
-    double x[PER];
-    uint32_t mx = 0;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const uint32_t t = (uint32_t)(tid + i * NT);
-        const uint32_t d = __builtin_amdgcn_raw_buffer_load_b8(rd, tid, i * NT, 2);
-        const uint32_t p = __builtin_amdgcn_raw_buffer_load_b32(rp, tid * 4, i * NT * 4, 2);
-        const uint32_t l = (t != (uint32_t)s) ? d : 0u; /* out of range: 0 (descriptor bound) */
-        mx = max(mx, l);
-        const uint32_t b = min(l, 255u) << (8 * (i & 3));
-        lv[i >> 2] = (i & 3) ? (lv[i >> 2] | b) : b;
-        const uint32_t u = p & 0xFFFFu;
-        const bool none = u == 0xFFFFu || t == (uint32_t)s || t >= (uint32_t)n;
-        stash[t] = (uint16_t)(none ? (uint32_t)ntab : p >> 16);
-        const uint32_t pv = (none || u == (uint32_t)s) ? 0xFFFFu : u;
-        pu[i >> 1] = (i & 1) ? (pu[i >> 1] | (pv << 16)) : pv;
-        if (l && pv != 0xFFFFu) atomicOr(&par[pv >> 5], 1u << (pv & 31));
-    }
-    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-    if (lane == 0) red[tid >> 6] = mx;
-    __syncthreads(); /* parents marked, red */
-    mx = 0;
-    for (int i = 0; i < NT / 64; ++i) mx = max(mx, red[i]);
-    const uint32_t c = tid < nw ? (uint32_t)__popc(par[tid]) : 0u;
-    uint32_t inc = c;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
-        if (lane >= o) inc += y;
-    }
-    if (lane == 63) wsum[tid >> 6] = inc;
-    __syncthreads();
-    uint32_t base = 0, total = 0;
-    for (int i = 0; i < NT / 64; ++i) {
-        base += i < (tid >> 6) ? wsum[i] : 0u;
-        total += wsum[i];
-    }
-    if (tid < nw) pre[tid] = base + inc - c;
-    const bool bail = (int)mx > maxl || total > (uint32_t)cap;
-    if (tid == 0) sweep[blockIdx.x] = bail;
-    /* the levels packed before x is formed (else the unpacked bytes stay beside x and spill) */
-#pragma unroll
-    for (int k = 0; k < PER / 4; ++k) asm volatile("" : "+v"(lv[k]));
-    int tx = tid; /* opaque: no stash addresses kept from the load loop */
-    asm volatile("" : "+v"(tx));
-    if (bail || mx == 0) { /* rel_sweeps_kernel's input: r(pred, t) (mx = 0: 0.0, rel(s, s) = 1) */
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int t = tx + i * NT;
-            if (t < n) rr[t] = !bail && t == s ? 1.0 : srt[stash[t]];
-        }
-        return;
-    }
-    __syncthreads(); /* pre written */
-    auto rank = [&](uint32_t u) {
-        return pre[u >> 5] + (uint32_t)__popc(par[u >> 5] & ((1u << (u & 31)) - 1u));
-    };
-    /* the predecessors' slot indices, and which own targets are parents (before x is formed:
-     * x, the indices and the levels together would not fit beside the rank temporaries) */
-    uint32_t pm = 0;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const uint32_t t = (uint32_t)(tx + i * NT);
-        const uint32_t u = (pu[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-        const uint32_t su = u == 0xFFFFu ? 0xFFFFu : rank(u);
-        pu[i >> 1] = (i & 1) ? ((pu[i >> 1] & 0xFFFFu) | (su << 16)) : ((pu[i >> 1] & 0xFFFF0000u) | su);
-        if (t < (uint32_t)n && ((par[t >> 5] >> (t & 31)) & 1u)) pm |= 1u << i;
-    }
-#pragma unroll
-    for (int i = 0; i < PER; ++i) x[i] = srt[stash[tx + i * NT]];
-    __syncthreads(); /* every stash read done before the slots take values */
-    uint32_t L = 1;
-    do {
-#pragma unroll
-        for (int k = 0; k < PER / 4; ++k) asm volatile("" : "+v"(lv[k]));
-        int tl = tid;
-        asm volatile("" : "+v"(tl));
-        uint32_t hm = 0; /* own targets at level L */
-#pragma unroll
-        for (int i = 0; i < PER; ++i)
-            hm |= (((lv[i >> 2] >> (8 * (i & 3))) & 0xFFu) == L ? 1u : 0u) << i;
-#pragma unroll
-        for (int i0 = 0; i0 < PER; i0 += QB) {
-            constexpr uint32_t bm = (QB >= 32) ? 0xFFFFFFFFu : ((1u << QB) - 1u);
-            if (!__any((hm >> i0) & bm)) continue; /* wave-uniform: no target of the bundle here */
-            double ru[QB];
-#pragma unroll
-            for (int q = 0; q < QB; ++q) { /* the bundle's slot reads (its targets of this pass) */
-                const int i = i0 + q;
-                const uint32_t su = (pu[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-                ru[q] = 1.0;
-                if (((hm >> i) & 1u) && su != 0xFFFFu) ru[q] = slot[su];
-            }
-#pragma unroll
-            for (int q = 0; q < QB; ++q) x[i0 + q] = ru[q] * x[i0 + q]; /* ru = 1 off the pass */
-            if (((pm & hm) >> i0) & bm) { /* a parent among them (rare): its slot */
-#pragma unroll
-                for (int q = 0; q < QB; ++q)
-                    if (((pm & hm) >> (i0 + q)) & 1u) slot[rank((uint32_t)(tl + (i0 + q) * NT))] = x[i0 + q];
-            }
-        }
-        __syncthreads();
-    } while (++L <= mx);
-    int tw = tid;
-    asm volatile("" : "+v"(tw));
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int t = tw + i * NT;
-        if (t < n) __builtin_nontemporal_store(t == s ? 1.0 : x[i], rr + t);
-    }
-    if (tid == 0) atomicMax(max_depth, (int)mx);
-}
-
 /* rel_tree_kernel at the row's size class (n <= 32768) */
 template <typename LT, typename PT>
 static void rel_tree_launch(int n, int ld, int row0, int lrows, const LT* d, const PT* pred,
@@ -1385,31 +1225,6 @@ static void rel_tree_launch(int n, int ld, int row0, int lrows, const LT* d, con
     }
 }
 
-/* rel_tree_pk_kernel at the row's size class (n <= 32768) */
-static void rel_tree_pk_launch(int n, int ld, int row0, int lrows, const uint8_t* d,
-                               const uint32_t* pk, double* rel, int32_t* depth, int32_t* sweep,
-                               const int32_t* srcs, hipStream_t st, const double* rtab, int ntab) {
-    if (n <= 1024) {
-        const int lds = (int)rel_tree_pk_lds(256, 1024, ntab + 2);
-        (void)hipFuncSetAttribute((const void*)rel_tree_pk_kernel<256, 4>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        rel_tree_pk_kernel<256, 4><<<lrows, 256, lds, st>>>(n, ld, row0, d, pk, rel, 64, 1024, depth,
-                                                            sweep, srcs, rtab, ntab);
-    } else if (n <= 4096) {
-        const int lds = (int)rel_tree_pk_lds(512, 4096, ntab + 2);
-        (void)hipFuncSetAttribute((const void*)rel_tree_pk_kernel<512, 8>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        rel_tree_pk_kernel<512, 8><<<lrows, 512, lds, st>>>(n, ld, row0, d, pk, rel, 64, 4096, depth,
-                                                            sweep, srcs, rtab, ntab);
-    } else { /* 8,192 slots (64 KB, first the index stash) and the table: 88 KB */
-        const int lds = (int)rel_tree_pk_lds(1024, 8192, ntab + 2);
-        (void)hipFuncSetAttribute((const void*)rel_tree_pk_kernel<1024, 32>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        rel_tree_pk_kernel<1024, 32><<<lrows, 1024, lds, st>>>(n, ld, row0, d, pk, rel, 64, 8192,
-                                                               depth, sweep, srcs, rtab, ntab);
-    }
-}
-
 /* Path-order reliability of lrows rows whose rel rows hold r(pred, t) (pred rows beside them):
  * rel_tree_kernel for n <= 32768 (rel_levels_kernel past it, or under SRT_FORM reltree=0), then
  * the sweeps for the rows it flagged. depth, sweep: device scratch (max depth, per-row flags). */
@@ -1421,10 +1236,7 @@ static int rel_rows_launch(int n, int ld, int row0, int lrows, const uint32_t* d
     if (lrows <= 0) return SRT_OK;
     const bool tree = n <= 32768 && srt_form_int("reltree", 1) != 0;
     if (pk) { /* a level build's u8 rows and packed (predecessor | reliability index) rows */
-        if (srt_form_int("pktree", 0) == 0)
-            rel_tree_launch(n, ld, row0, lrows, l8, pk, rel, depth, sweep, srcs, st, rtab, ntab);
-        else
-            rel_tree_pk_launch(n, ld, row0, lrows, l8, pk, rel, depth, sweep, srcs, st, rtab, ntab);
+        rel_tree_launch(n, ld, row0, lrows, l8, pk, rel, depth, sweep, srcs, st, rtab, ntab);
         SRT_HIPCHK(hipGetLastError());
         const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
         SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel<uint32_t>,

@@ -40,6 +40,11 @@
 /* COUNT: per (target, weight) histogram of arcs with 1 <= w <= LVL_WMAX; FILL: the arcs (k | w << 16)
  * at cursor positions from off (weights above lmax were masked out of off). Rows form: local row
  * jj of w is target row0 + jj's in-arc row (undirected). */
+/* The count pass also keeps each row's light arcs (w <= LVL_STASH_W, up to LVL_STASH_CAP of them;
+ * C4: ~1,050 per row) in a stash, so the fill reads them instead of the whole w row again (when
+ * lmax <= LVL_STASH_W and the row's arcs fit). */
+#define LVL_STASH_W 32
+#define LVL_STASH_CAP 2048
 template <bool FILL>
 __global__ __launch_bounds__(256) void lvl_arcs_rows_kernel(int n, int ld, int row0,
                                                             const uint32_t* __restrict__ w,
@@ -48,10 +53,28 @@ __global__ __launch_bounds__(256) void lvl_arcs_rows_kernel(int n, int ld, int r
                                                             uint32_t* __restrict__ arcs,
                                                             const double* __restrict__ r = nullptr,
                                                             double* __restrict__ ar = nullptr,
-                                                            unsigned long long* __restrict__ dkey = nullptr) {
+                                                            unsigned long long* __restrict__ dkey = nullptr,
+                                                            uint32_t* __restrict__ stash = nullptr,
+                                                            int32_t* __restrict__ scnt = nullptr) {
     __shared__ int h[LVL_STRIDE];
     __shared__ unsigned long long s_key[4];
+    __shared__ int s_n;
     const int jj = blockIdx.x, j = row0 + jj;
+    if (FILL && stash && j < n && lmax <= LVL_STASH_W && scnt[jj] <= LVL_STASH_CAP) {
+        for (int i = threadIdx.x; i <= lmax; i += 256) h[i] = off[(size_t)j * LVL_STRIDE + i];
+        __syncthreads();
+        const uint32_t* sr = stash + (size_t)jj * LVL_STASH_CAP;
+        const int m = scnt[jj];
+        for (int q = threadIdx.x; q < m; q += 256) {
+            const uint32_t e = sr[q], x = e >> 16, k = e & 0xFFFFu;
+            if (x > (uint32_t)lmax) continue;
+            const int p = atomicAdd(&h[x], 1);
+            arcs[p] = e;
+            ar[p] = r[(size_t)jj * ld + k]; /* undirected: r(k -> j) = r(j -> k) */
+        }
+        return;
+    }
+    if (!FILL && threadIdx.x == 0) s_n = 0;
     /* COUNT also takes the diagonal rule's key from the same row reads (topology.c:1431-1576, as
      * dense_diag_kernel): min over the row's out-edges of (self-loop L, other 2L) << 32 | u */
     unsigned long long best = ~0ull;
@@ -76,8 +99,14 @@ __global__ __launch_bounds__(256) void lvl_arcs_rows_kernel(int n, int ld, int r
                         const int p = atomicAdd(&h[x[q]], 1);
                         arcs[p] = (uint32_t)k | (x[q] << 16);
                         ar[p] = r[(size_t)jj * ld + k]; /* undirected: r(k -> j) = r(j -> k) */
-                    } else
+                    } else {
                         atomicAdd(&h[x[q]], 1);
+                        if (stash && x[q] <= LVL_STASH_W) {
+                            const int sq = atomicAdd(&s_n, 1);
+                            if (sq < LVL_STASH_CAP)
+                                stash[(size_t)jj * LVL_STASH_CAP + sq] = (uint32_t)k | (x[q] << 16);
+                        }
+                    }
                 }
             }
         }
@@ -89,6 +118,7 @@ __global__ __launch_bounds__(256) void lvl_arcs_rows_kernel(int n, int ld, int r
     }
     if ((threadIdx.x & 63) == 0) s_key[threadIdx.x >> 6] = best;
     __syncthreads();
+    if (stash && threadIdx.x == 0) scnt[jj] = s_n;
     for (int i = threadIdx.x; i < LVL_STRIDE; i += 256) cnt[(size_t)j * LVL_STRIDE + i] = h[i];
     if (threadIdx.x == 0 && dkey)
         dkey[jj] = min(min(s_key[0], s_key[1]), min(s_key[2], s_key[3]));
@@ -842,14 +872,20 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     LVL_ALLOC(off, (ncnt + 1) * sizeof(int32_t));
     LVL_ALLOC(dhist, LVL_STRIDE * sizeof(unsigned long long));
     unsigned long long* dkey = NULL;
-    if (!directed) LVL_ALLOC(dkey, (size_t)nrows * sizeof(unsigned long long));
+    uint32_t* stash = NULL;
+    int32_t* scnt = NULL;
+    if (!directed) {
+        LVL_ALLOC(dkey, (size_t)nrows * sizeof(unsigned long long));
+        LVL_ALLOC(stash, (size_t)nrows * LVL_STASH_CAP * sizeof(uint32_t));
+        LVL_ALLOC(scnt, (size_t)nrows * sizeof(int32_t));
+    }
     SRT_HIPCHK(hipMemsetAsync(cnt, 0, (ncnt + 1) * sizeof(int32_t), st));
     SRT_HIPCHK(hipMemsetAsync(dhist, 0, LVL_STRIDE * sizeof(unsigned long long), st));
     if (directed)
         lvl_arcs_cols_kernel<false><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, cnt, 0, NULL, NULL);
     else
         lvl_arcs_rows_kernel<false><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, cnt, 0, NULL, NULL,
-                                                           NULL, NULL, dkey);
+                                                           NULL, NULL, dkey, stash, scnt);
     SRT_HIPCHK(hipGetLastError());
     int rc;
     if (R > 1 && (rc = srt_coll_allreduce_i32(comm, cnt, ncnt, 0, st))) return rc;
@@ -891,7 +927,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
                                                             r_rows, ar);
     else
         lvl_arcs_rows_kernel<true><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, NULL, lmax, off, arcs,
-                                                          r_rows, ar);
+                                                          r_rows, ar, NULL, stash, scnt);
     SRT_HIPCHK(hipGetLastError());
     if (R > 1) { /* every rank filled its rows' segment: broadcast the segments */
         int32_t hoff[65];
