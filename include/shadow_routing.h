@@ -291,6 +291,11 @@ int32_t srt_pair_order_runs(srt_pair_order* po, int32_t v);
  * Dijkstra (shortestPathCount, :1719; on a directed graph every lookup not served s's own path) and
  * the self paths computed (selfPathCount, :1536); shortest-path mode only */
 void srt_pair_order_counts(srt_pair_order* po, uint32_t* source_runs, uint32_t* self_paths);
+/* k more source runs (shortest-path mode): a caller that answers with one lookup what the
+ * reference does with several -- worker_sendPacket's getReliability, getLatency and
+ * incrementPathPacketCounter (worker.c:541-555), each a cache probe that, on a directed graph,
+ * runs the source again while the pair is served the other end's path */
+void srt_pair_order_add_source_runs(srt_pair_order* po, uint32_t k);
 
 int srt_device_count(void);
 int srt_device_sync(int32_t device);

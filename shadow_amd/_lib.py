@@ -123,6 +123,7 @@ SIGNATURES = {
     "srt_pair_order_peek": (_I32, [_VP, _I32, _I32]),
     "srt_pair_order_runs": (_I32, [_VP, _I32]),
     "srt_pair_order_counts": (None, [_VP, _VP, _VP]),
+    "srt_pair_order_add_source_runs": (None, [_VP, _U32]),
     "srt_pair_order_set_reach": (None, [_VP, _VP, _VP]),
     "srt_device_count": (ctypes.c_int, []),
     "srt_device_sync": (ctypes.c_int, [_I32]),

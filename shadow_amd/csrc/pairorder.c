@@ -327,6 +327,10 @@ int32_t srt_pair_order_peek(srt_pair_order* po, int32_t s, int32_t t) {
     return stored_from(po, s, t);
 }
 
+void srt_pair_order_add_source_runs(srt_pair_order* po, uint32_t k) {
+    if (po && po->per_source) atomic_fetch_add_explicit(&po->source_runs, k, memory_order_relaxed);
+}
+
 void srt_pair_order_counts(srt_pair_order* po, uint32_t* source_runs, uint32_t* self_paths) {
     if (source_runs) *source_runs = po ? atomic_load(&po->source_runs) : 0u;
     if (self_paths) *self_paths = po ? atomic_load(&po->self_runs) : 0u;

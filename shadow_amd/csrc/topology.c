@@ -1448,6 +1448,10 @@ int srt_topology_send_packet_ip(Topology* t, uint32_t srcIp, uint32_t dstIp, dou
     if (!tb) return err;
     const double reliability = tb->rel[i];
     if (bootstrapping || chance <= reliability || payloadLength == 0) {
+        /* the reference's getLatency and incrementPathPacketCounter probe the cache again: on a
+         * directed graph served d's path, each runs source s once more (its diagnostics count) */
+        if (t->directed && s != d && s != srt_topology_vertex_of_ip(t, srcIp)) /* (s: the path's) */
+            srt_pair_order_add_source_runs(t->po, 2u);
         const double latency = tables_latency_ms(t, tb, i);
         if (delayNs) *delayNs = (uint64_t)ceil(latency * 1000000.0);
         const int rc = increment_pair(t, s, d);

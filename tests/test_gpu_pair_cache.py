@@ -110,7 +110,7 @@ def _replay(g, gml, use_sp=True, algo=ALGO_AUTO, ops=2500, hosts=None, late=0, s
         pc = top.path_counts()
         want = (sim.source_runs, sim.self_runs) if use_sp else (0, 0)
         assert (pc["shortest_paths"], pc["self_paths"]) == want, (pc, want)
-        assert pc["builds"] >= 1 and pc["build_seconds"] > 0
+        assert pc["builds"] >= 1 and pc["build_seconds"] >= 0  # (direct mode: a gather, untimed)
         return stats
     finally:
         top.free()
