@@ -544,17 +544,20 @@ def dense_levels_tail(c: Ctx, wl, step, elapsed, stats, lat, rel, nr, ld):
     avg_ms, per_launch, launches, model = kern[dom]
     achieved = per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic = None
+    pmc_k = {}  # per-kernel PMC HBM bytes per launch (profiles/pmc_traffic_<wl>_n<N>.json)
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{c.args.workload}_n{world}.json")
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
-        if pmc.get("kernel") == dom:
-            traffic = pmc.get("hbm_bytes_per_launch")
+        pmc_k = {k: v.get("hbm_bytes_per_launch") for k, v in pmc.get("kernels", {}).items()}
+        if pmc.get("kernel"):
+            pmc_k[pmc["kernel"]] = pmc.get("hbm_bytes_per_launch")
+        traffic = pmc_k.get(dom)
     others = {}
     for name, (ms, b, nl, _) in kern.items():
         gbs = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         others[name] = {"ms_per_build": round(total[name], 3), "avg_launch_ms": round(ms, 4),
                         "bytes_per_launch": b, "achieved": round(gbs, 1),
-                        "frac": round(gbs / HBM_PEAK_GBS, 4)}
+                        "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": pmc_k.get(name)}
     roofline = {
         "bound": "hbm", "kernel": dom,
         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
