@@ -21,7 +21,9 @@
  */
 #include "srt_device.h"
 
+#ifndef DV_MAXDEG
 #define DV_MAXDEG 4   /* largest degree the host puts in I (build.hip DERIVE_MAXDEG) */
+#endif
 #define DV_J 2        /* targets per thread per phase-A step: their loads overlap */
 #define DV_JB 1       /* targets per thread per phase-B step (4: 138 vs 125 ms on C5) */
 

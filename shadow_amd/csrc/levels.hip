@@ -346,7 +346,7 @@ static __device__ __forceinline__ void lvl_step_unit(unsigned g, int d, int n, i
         const int g1 = oj[w + 1];
         const char* base = reinterpret_cast<const char*>(lev + (size_t)(d - w - 1) * plane);
 #ifndef LVL_SB
-#define LVL_SB 16
+#define LVL_SB 16 /* (8 measured the same, 32/48 slower; pipelined batches did not help here) */
 #endif
         for (int i = oj[w]; i < g1; i += LVL_SB) { /* LVL_SB in flight, the tail predicated */
             uint32_t a[LVL_SB], v[LVL_SB];
