@@ -1040,6 +1040,9 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
                                                       const double* __restrict__ rtab = nullptr,
                                                       int ntab = 0) {
     constexpr bool PK = std::is_same_v<PT, uint32_t>;
+    /* the rows' loads: non-temporal (aux 2) on the FW path; cached for the packed rows, measured
+     * 5.27-5.38 against 5.48-5.57 ms on C4 (`profiles/r04/exp/`) */
+    constexpr int AUX = PK ? 0 : 2;
     const int s = srcs ? srcs[blockIdx.x] : row0 + blockIdx.x; /* srcs: row i is source srcs[i] */
     if (s >= n) return;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1075,14 +1078,14 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
         /* u32 table rows (SRT_INF: unreachable) or a level build's u8 rows (0: s itself) */
         uint32_t d;
         if constexpr (sizeof(LT) == 1)
-            d = __builtin_amdgcn_raw_buffer_load_b8(rd, tid, i * NT, 2);
+            d = __builtin_amdgcn_raw_buffer_load_b8(rd, tid, i * NT, AUX);
         else
             d = __builtin_amdgcn_raw_buffer_load_b32(rd, tid * 4, i * NT * 4, 2);
         uint32_t p; /* int32 rows, or int16 (-1 -> 0xFFFF either way below) */
         if constexpr (sizeof(PT) == 2)
             p = __builtin_amdgcn_raw_buffer_load_b16(rp, tid * 2, i * NT * 2, 2);
         else
-            p = __builtin_amdgcn_raw_buffer_load_b32(rp, tid * 4, i * NT * 4, 2);
+            p = __builtin_amdgcn_raw_buffer_load_b32(rp, tid * 4, i * NT * 4, AUX);
         if constexpr (PK) {
             const uint32_t t = (uint32_t)(tid + i * NT);
             const uint32_t hi = ((p & 0xFFFFu) == 0xFFFFu || t == (uint32_t)s || t >= (uint32_t)n)
