@@ -93,6 +93,9 @@ int32_t srt_topology_attach_batch_ip(Topology* top, int32_t nhosts, const uint32
                                      const char* const* countrycodeHints, int32_t* outVertex,
                                      uint64_t* bwDownOut, uint64_t* bwUpOut);
 void srt_topology_detach_ip(Topology* top, uint32_t ipNet);
+/* tables the IP -> vertex map holds (the current one + replaced ones not yet reclaimed); stays
+ * bounded under attach / detach cycles (diagnostic) */
+int64_t srt_topology_ipmap_tables(Topology* top);
 int32_t srt_topology_vertex_of_ip(Topology* top, uint32_t ipNet);
 double srt_topology_latency_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet);
 double srt_topology_reliability_ip(Topology* top, uint32_t srcIpNet, uint32_t dstIpNet);

@@ -143,6 +143,7 @@ SIGNATURES = {
     "srt_topology_attach_ip": (_I32, [_VP, _U32, _VP, _CP, _CP, _CP, _VP, _VP]),
     "srt_topology_attach_batch_ip": (_I32, [_VP, _I32, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "srt_topology_detach_ip": (None, [_VP, _U32]),
+    "srt_topology_ipmap_tables": (ctypes.c_int64, [_VP]),
     "srt_topology_vertex_of_ip": (_I32, [_VP, _U32]),
     "srt_topology_latency_ip": (_D, [_VP, _U32, _U32]),
     "srt_topology_reliability_ip": (_D, [_VP, _U32, _U32]),

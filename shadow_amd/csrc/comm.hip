@@ -461,15 +461,15 @@ int srt_coll_group_end(const srt_comm* c) {
     srt_comm* m = const_cast<srt_comm*>(c);
     const int was = m->in_group;
     m->in_group = 0;
-    if (c->solo && was && t_group_stream) {
-        const int rc = solo_wire(c, m->group_bytes, t_group_stream);
-        if (rc) return rc;
-    }
-    if (was && m->t_open) { /* close the group's span on its first collective's stream */
+    int rc = SRT_OK;
+    if (c->solo && was && t_group_stream) rc = solo_wire(c, m->group_bytes, t_group_stream);
+    if (was && m->t_open) { /* close the group's span on its first collective's stream, also
+                             * after a failed wire span */
         m->t_open = 0;
-        return t_end(c, m->t_stream);
+        const int e = t_end(c, m->t_stream);
+        if (!rc) rc = e;
     }
-    return SRT_OK;
+    return rc;
 }
 
 static int exchange_impl(const srt_comm* c, void* const* send, const size_t* send_bytes,
@@ -573,12 +573,15 @@ static int sparse_allgather_impl(srt_comm* comm, int32_t n, int32_t rows_per_ran
 }
 
 /* ---- timed entry points: each collective (or its group) is one span of ms_comm ----------- */
+/* the closing event is recorded whatever the call returns, so a failed collective cannot leave
+ * the begin/end events of later spans paired across collectives */
 #define SRT_TIMED(st, call)                       \
     do {                                          \
         int r_ = t_begin(c, st);                  \
-        if (!r_) r_ = (call);                     \
-        if (!r_) r_ = t_end(c, st);               \
-        return r_;                                \
+        if (r_) return r_;                        \
+        r_ = (call);                              \
+        const int e_ = t_end(c, st);              \
+        return r_ ? r_ : e_;                      \
     } while (0)
 
 int srt_coll_bcast(const srt_comm* c, void* buf, size_t bytes, int root, hipStream_t st) {

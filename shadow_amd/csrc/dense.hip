@@ -1228,6 +1228,213 @@ static void rel_tree_launch(int n, int ld, int row0, int lrows, const LT* d, con
     }
 }
 
+/* Round 5: the reliability pass of the source-major packed words (srt_levels_pkw: pred | rix << 16
+ * | level << 27 per pair). rel(s,t) = rel(s,pred) * r(pred,t) needs, besides the pair's own word,
+ * only rel(s,pred) -- and the predecessors of a row are few (its "parents": C4 rows have ~1-3k of
+ * 32k targets, the vertices at distance <= 2-3 quanta). So a row's pass computes the parents alone,
+ * in level order (a parent's own predecessor is a parent one level down, topology.c:1364-1365's
+ * left-to-right product), then streams every pair once: 4 B read, the u32 distance and the f64
+ * reliability written (16 B per pair, nothing else). rel_tree_kernel kept every target's
+ * predecessor and value on chip (152 KB of LDS, one 1,024-thread row per CU); here only the
+ * parents' words and values are in LDS (~72 KB: two rows per CU, one row's stores under the other's
+ * loads), the row's words in registers (thread = 4 consecutive targets per 16-B piece, K pieces).
+ * A row with more parents than the cap slots takes rel_sweeps_kernel from the r(pred, t) it
+ * leaves in the rel row (sweep[row] = 1). */
+#define REL_PK_NT 512
+template <int K>
+__global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int row0,
+                                                           const uint32_t* __restrict__ pk,
+                                                           uint32_t* __restrict__ lat,
+                                                           double* __restrict__ rel,
+                                                           const double* __restrict__ rtab, int ntab,
+                                                           int cap, int32_t* __restrict__ max_depth,
+                                                           int32_t* __restrict__ sweep) {
+    constexpr int NT = REL_PK_NT;
+    const int s = row0 + (int)blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int nwb = ld >> 5; /* parent bitmap words (ld % 128 == 0) */
+    extern __shared__ __attribute__((aligned(16))) uint32_t psm[];
+    uint32_t* par = psm;                                         /* parent bitmap */
+    uint32_t* pre = psm + nwb;                                   /* parents before each word */
+    double* srt = reinterpret_cast<double*>(psm + 2 * nwb);      /* the ntab reliabilities, 0.0 */
+    double* pval = srt + ((ntab + 2) & ~1);                      /* cap parent values */
+    uint32_t* pinfo = reinterpret_cast<uint32_t*>(pval + cap);   /* cap parent words */
+    __shared__ uint32_t wsum[NT / 64], red[NT / 64];
+    for (int q = tid; q < nwb; q += NT) par[q] = 0u;
+    for (int q = tid; q <= ntab; q += NT) srt[q] = q < ntab ? rtab[q] : 0.0;
+    /* the row through a buffer descriptor: one 32-bit offset per piece, and pieces past the row
+     * read 0 (level 0: written as "no path", and never stored: t0 >= ld) */
+    const __amdgpu_buffer_rsrc_t rrow = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t*>(pk + (size_t)blockIdx.x * ld), 0, ld * 4, 0x00020000);
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    uint4 wd[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rrow, tid * 16, k * NT * 16, 0);
+        wd[k] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+    __syncthreads(); /* par zeroed */
+    uint32_t mx = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t e4[4] = {wd[k].x, wd[k].y, wd[k].z, wd[k].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t w = e4[e], l = w >> 27, u = w & 0xFFFFu;
+            mx = max(mx, l);
+            if (l && (int)u != s) atomicOr(&par[u >> 5], 1u << (u & 31));
+        }
+    }
+    /* opaque words from here on: else the compiler keeps every word's decoded fields live
+     * across the phases (3 registers per target, one row per CU) */
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        asm volatile("" : "+v"(wd[k].x), "+v"(wd[k].y), "+v"(wd[k].z), "+v"(wd[k].w));
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    if (lane == 0) red[tid >> 6] = mx;
+    __syncthreads(); /* par, red */
+    mx = 0;
+    for (int i = 0; i < NT / 64; ++i) mx = max(mx, red[i]);
+    /* exclusive prefix of the parent counts; thread tid owns bitmap words tid * wpt.. */
+    const int wpt = (nwb + NT - 1) / NT;
+    uint32_t c = 0;
+    for (int i = 0; i < wpt; ++i) {
+        const int q = tid * wpt + i;
+        if (q < nwb) c += (uint32_t)__popc(par[q]);
+    }
+    uint32_t inc = c;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) wsum[tid >> 6] = inc;
+    __syncthreads();
+    uint32_t base = 0, total = 0;
+    for (int i = 0; i < NT / 64; ++i) {
+        base += i < (tid >> 6) ? wsum[i] : 0u;
+        total += wsum[i];
+    }
+    uint32_t run = base + inc - c;
+    for (int i = 0; i < wpt; ++i) {
+        const int q = tid * wpt + i;
+        if (q < nwb) {
+            pre[q] = run;
+            run += (uint32_t)__popc(par[q]);
+        }
+    }
+    const bool bail = total > (uint32_t)cap;
+    if (tid == 0) sweep[blockIdx.x] = bail;
+    __syncthreads(); /* pre */
+    auto rank = [&](uint32_t u) {
+        return pre[u >> 5] + (uint32_t)__popc(par[u >> 5] & ((1u << (u & 31)) - 1u));
+    };
+    if (!bail) {
+        /* the parents' own words into their slots */
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t e4[4] = {wd[k].x, wd[k].y, wd[k].z, wd[k].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t t = 4u * (uint32_t)(tid + k * NT) + e;
+                if ((int)t < n && ((par[t >> 5] >> (t & 31)) & 1u)) pinfo[rank(t)] = e4[e];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();
+        /* the parents' values by level: a level-L parent's predecessor is s or a parent of level
+         * L - 1 (every arc >= 1 quantum); parents sit below the row's largest level */
+        for (uint32_t lv = 1; lv < mx; ++lv) {
+            for (int q = tid; q < (int)total; q += NT) {
+                const uint32_t w = pinfo[q];
+                if ((w >> 27) != lv) continue;
+                const uint32_t u = w & 0xFFFFu;
+                const double ru = (int)u == s ? 1.0 : pval[rank(u)];
+                pval[q] = ru * srt[(w >> 16) & 0x7FFu];
+            }
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        asm volatile("" : "+v"(wd[k].x), "+v"(wd[k].y), "+v"(wd[k].z), "+v"(wd[k].w));
+    uint32_t* lr = lat + (size_t)blockIdx.x * ld;
+    double* rr = rel + (size_t)blockIdx.x * ld;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int t0 = 4 * (tid + k * NT);
+        if (t0 >= ld) continue;
+        const uint32_t e4[4] = {wd[k].x, wd[k].y, wd[k].z, wd[k].w};
+        uint32_t lv[4];
+        double x[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t w = e4[e], l = w >> 27, u = w & 0xFFFFu;
+            const int t = t0 + e;
+            if (!l) { /* s itself (the diagonal rule follows), or no path / padding */
+                lv[e] = t == s ? 0u : SRT_INF;
+                x[e] = t == s ? 1.0 : 0.0;
+            } else {
+                lv[e] = l;
+                const double r = srt[(w >> 16) & 0x7FFu];
+                /* bail: r(pred, t) for rel_sweeps_kernel */
+                x[e] = bail ? r : ((int)u == s ? 1.0 : pval[rank(u)]) * r;
+            }
+        }
+        __builtin_nontemporal_store(lv[0], lr + t0);
+        __builtin_nontemporal_store(lv[1], lr + t0 + 1);
+        __builtin_nontemporal_store(lv[2], lr + t0 + 2);
+        __builtin_nontemporal_store(lv[3], lr + t0 + 3);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) __builtin_nontemporal_store(x[e], rr + t0 + e);
+        /* one piece at a time: hoisting every piece's LDS reads costs the second row per CU */
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (tid == 0) atomicMax(max_depth, (int)mx);
+}
+
+/* rel_pk_kernel at the row's width, then the sweeps for the rows over the parent cap */
+static int rel_pk_launch(int n, int ld, int row0, int lrows, const uint32_t* pk, uint32_t* lat,
+                         double* rel, const double* rtab, int ntab, int32_t* depth, int32_t* sweep,
+                         hipStream_t st) {
+    if (lrows <= 0) return SRT_OK;
+    if (ld > 32768 || ntab > 2048) {
+        srt_set_error("rel_pk_launch: ld %d / %d reliabilities beyond the packed form", ld, ntab);
+        return SRT_E_ARG;
+    }
+    /* two rows per CU: ~80 KB of LDS per workgroup, the rest of it parent slots (12 B each) */
+    const int fixed = 8 * (ld >> 5) + 8 * ((ntab + 2) & ~1);
+    const int cap = min(n, (80 * 1024 - fixed) / 12) & ~63;
+    const int lds = fixed + 12 * cap;
+    const void* fn;
+    const int K = ld <= 2048 ? 1 : ld <= 4096 ? 2 : ld <= 8192 ? 4 : ld <= 16384 ? 8 : 16;
+    switch (K) {
+    case 1: fn = (const void*)rel_pk_kernel<1>; break;
+    case 2: fn = (const void*)rel_pk_kernel<2>; break;
+    case 4: fn = (const void*)rel_pk_kernel<4>; break;
+    case 8: fn = (const void*)rel_pk_kernel<8>; break;
+    default: fn = (const void*)rel_pk_kernel<16>; break;
+    }
+    SRT_HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+#define REL_PK_GO(KK)                                                                          \
+    rel_pk_kernel<KK><<<lrows, REL_PK_NT, lds, st>>>(n, ld, row0, pk, lat, rel, rtab, ntab, cap, \
+                                                     depth, sweep)
+    switch (K) {
+    case 1: REL_PK_GO(1); break;
+    case 2: REL_PK_GO(2); break;
+    case 4: REL_PK_GO(4); break;
+    case 8: REL_PK_GO(8); break;
+    default: REL_PK_GO(16); break;
+    }
+#undef REL_PK_GO
+    SRT_HIPCHK(hipGetLastError());
+    const size_t slds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
+    SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel<uint32_t>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)slds));
+    rel_sweeps_kernel<uint32_t><<<lrows, 512, slds, st>>>(n, ld, row0, pk, rel, depth, sweep, nullptr);
+    SRT_HIPCHK(hipGetLastError());
+    return SRT_OK;
+}
+
 /* Path-order reliability of lrows rows whose rel rows hold r(pred, t) (pred rows beside them):
  * rel_tree_kernel for n <= 32768 (rel_levels_kernel past it, or under SRT_FORM reltree=0), then
  * the sweeps for the rows it flagged. depth, sweep: device scratch (max depth, per-row flags). */
@@ -1631,7 +1838,37 @@ static int dense_post_levels(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
                              double* rel, hipStream_t st, srt_build_stats* stats, dense_ws* ws,
                              int lrows) {
     int rc;
-    if (lrows > 0) {
+    if (lrows > 0 && srt_levels_pkw_ready()) {
+        /* source-major packed words (lvl_pkw_kernel) + rel_pk_kernel, which writes the u32 rows
+         * too: 4 B per pair written and read between them, no transposes, no u8 rows */
+        const size_t slab = (size_t)ld * nrows;
+        size_t c1 = ws->dt_cap;
+        if ((rc = ws_grow((void**)&ws->dt, &c1, slab, sizeof(uint32_t)))) return rc;
+        ws->dt_cap = c1;
+        const bool ties = stats && stats->count_ties;
+        if (ties) SRT_HIPCHK(hipMemsetAsync(ws->ties, 0, sizeof(unsigned long long), st));
+        const bool kt = stats && stats->time_kernels;
+        if (kt && !ws->kev[0])
+            for (int i = 0; i < 4; i++) SRT_HIPCHK(hipEventCreate(&ws->kev[i]));
+        int ntab = 0;
+        const double* rtab = srt_levels_rtab(&ntab);
+        if (stats) stats->rel_table = ntab;
+        uint32_t* pk = reinterpret_cast<uint32_t*>(ws->dt);
+        if (kt) SRT_HIPCHK(hipEventRecord(ws->kev[0], st));
+        if ((rc = srt_levels_pkw(pk, ld, ties ? ws->ties : NULL, st))) return rc;
+        if (kt) SRT_HIPCHK(hipEventRecord(ws->kev[1], st));
+        ws->pred16 = 2; /* dense_path_ms reads the packed words' low half */
+        SRT_HIPCHK(hipMemsetAsync(ws->depth, 0, sizeof(int32_t), st));
+        if (kt) SRT_HIPCHK(hipEventRecord(ws->kev[2], st));
+        if ((rc = rel_pk_launch(n, ld, row0, lrows, pk, d, rel, rtab, ntab, ws->depth, ws->cursor,
+                                st)))
+            return rc;
+        if (kt) {
+            SRT_HIPCHK(hipEventRecord(ws->kev[3], st));
+            ws->kev_on = 1;
+        }
+        if ((rc = srt_levels_diag(n, ld, d, rel, st, &ws->diag_done))) return rc;
+    } else if (lrows > 0) {
         const size_t slab = (size_t)ld * nrows;
         size_t c1 = ws->dt_cap, c2 = ws->predt_cap, c4 = ws->rt_cap;
         if ((rc = ws_grow((void**)&ws->dt, &c1, slab, sizeof(uint32_t)))) return rc;
@@ -2085,8 +2322,16 @@ static int dense_try_levels(const srt_comm* comm, int n, int ld, int row0, int n
     *exact = 0;
     const int mode = srt_form_int("levels", -1);
     if (mode == 0 || (mode < 0 && n < 4096) || ld % 128) return SRT_OK;
-    /* relaxations at the update's rate + ~50 us of round chain per 128 pivots */
-    const double fw_ms = (double)nrows * ld * ld / (directed ? 1.0 : 2.0) / 6.1e10 + ld / 128 * 0.05;
+    /* relaxations at the update's rate + ~50 us of round chain per 128 pivots, for the largest
+     * shard (the same on every rank; srt_levels_build also agrees the budget by a min all-reduce) */
+    int max_rows = nrows;
+    const int R = comm ? srt_comm_size(comm) : 1;
+    for (int q = 0; q < R && R > 1; q++) {
+        int32_t qb = 0, qe = 0;
+        srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &qb, &qe);
+        max_rows = max(max_rows, qe - qb);
+    }
+    const double fw_ms = (double)max_rows * ld * ld / (directed ? 1.0 : 2.0) / 6.1e10 + ld / 128 * 0.05;
     if (evp) {
         evp->used = 0;
         evp->group = 2;

@@ -396,7 +396,11 @@ __global__ __launch_bounds__(256) void lvl_step_kernel(int d, int n, int nw, int
                                                        uint32_t* __restrict__ lev,
                                                        uint32_t* __restrict__ R,
                                                        uint8_t* __restrict__ done,
-                                                       int* __restrict__ incomplete) {
+                                                       int* __restrict__ incomplete,
+                                                       const int* __restrict__ prev) {
+    /* the levels are enqueued in batches without a host round trip per level: a level whose
+     * predecessor settled every pair (prev == 0) has nothing to do */
+    if (prev && !__hip_atomic_load(prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     const unsigned x = blockIdx.x & 7u, per = nblk >> 3, L = gridDim.x >> 3;
     for (unsigned u = blockIdx.x >> 3; u < per; u += L)
         lvl_step_unit(x * per + u, d, n, nw, nchunk, src0, nsrc, off, arcs, aoff, lev, R, done,
@@ -722,6 +726,256 @@ __global__ __launch_bounds__(256) void lvl_pred_kernel(int n, int nw, int nchunk
                           rix, lev, predT, rT, ldp, ties);
 }
 
+#ifndef LVL_PKW_CW
+#define LVL_PKW_CW 16 /* source words per target group: 64 B per gathered arc */
+#endif
+#ifndef LVL_PKW_PB
+#define LVL_PKW_PB 12 /* gathers per lane and batch */
+#endif
+#ifndef LVL_PKW_W
+#define LVL_PKW_W 4 /* waves per workgroup */
+#endif
+#ifndef LVL_PKW_WAVE
+#define LVL_PKW_WAVE 1 /* 1: every wave on its own units (lvl_pkw_wave_kernel) */
+#endif
+/* ---- predecessor words, source-major, with the level (round 5) ---------------------------------
+ * The same canonical rule as lvl_pred_kernel, on a unit shape that keeps the gathered plane slices
+ * in one XCD's L2 and writes its output source-major (no transpose):
+ *  - a wave runs G = 64 / CW targets at once, one per CW-lane group; lane p of a group owns source
+ *    word c * CW + p, so one arc's gather is CW * 4 B (64 B for CW = 16) of Delta_{d-w}[u];
+ *  - a workgroup (8 waves) owns a tile of TT = 8 G targets x S = 32 CW sources, and the units are
+ *    handed out XCD-major, chunk-major: an XCD's CUs work on one source chunk at a time, whose
+ *    plane slices (n x CW x 4 B per level: 2 MB at C4) are the only gathered data in its L2
+ *    (lvl_pred_kernel's 64-word chunks had 8 MB per level, served by the MALL at 6.3x its bytes);
+ *  - the winning arc of each (source, target) lands in an LDS tile as the finished output word
+ *    pred | rix << 16 | level << 27 (rix < 2,048, level <= 31), and the tile is written source-
+ *    major, TT x 4 B per source row, after the tile's targets are done.
+ * arcw[i] = u | rix[i] << 16 for the sorted in-arcs (built by lvl_aw_kernel). Without TIES the walk
+ * of a weight stops once every pending source of every group has its arc (the arcs of a weight are
+ * in ascending u, so the first tight arc wins either way); TIES walks them all and counts the
+ * sources hit twice. Entries with no level (the diagonal, padding) stay 0xFFFF (predecessor -1). */
+/* The walk of one lane group's target t over the chunk's source words (lane p owns word c * CW + p):
+ * every level d of the pending sources, weights w = d .. 1, arcs of a weight in ascending u. The
+ * winning arc of chunk source r = p * 32 + b goes to tile[slot(r)] as pred | rix << 16 | d << 27. */
+template <int CW, int PB, bool TIES, class Slot>
+static __device__ __forceinline__ void pkw_walk(int t, bool tv, bool valid, int word, int g, int p,
+                                                int cs0, int n, int nw, int nlev,
+                                                const int32_t* __restrict__ off,
+                                                const uint32_t* __restrict__ arcw,
+                                                const uint32_t* __restrict__ lev,
+                                                uint32_t* __restrict__ tile, Slot slot,
+                                                unsigned& tied) {
+    constexpr int S = 32 * CW;
+    const size_t plane = (size_t)n * nw;
+    const uint32_t nw4 = (uint32_t)nw * 4u;
+    const int32_t* ot = off + (size_t)(tv ? t : 0) * LVL_STRIDE;
+    const uint32_t lane4 = (uint32_t)(valid ? word : 0) * 4u;
+    for (int d = 1; d <= nlev; ++d) {
+        uint32_t pend = valid ? lev[(size_t)(d - 1) * plane + (size_t)t * nw + word] : 0u;
+        if (!__any(pend != 0u)) continue;
+        const uint32_t dbits = (uint32_t)d << 27;
+        for (int w = d; w >= 1; --w) {
+            const int g0 = tv ? ot[w] : 0, g1 = tv ? ot[w + 1] : 0;
+            uint32_t H = 0, T = 0;
+            if (w == d) {
+                /* the direct arcs (u, t): tight for the source u itself; CW arcs per group and
+                 * step, the few whose u lies in the chunk go to the lane owning its word */
+                for (int k = 0; __any(g0 + k < g1); k += CW) {
+                    const int i = g0 + k + p;
+                    const uint32_t a = i < g1 ? arcw[i] : 0u;
+                    const int us = i < g1 ? (int)(a & 0xFFFFu) - cs0 : -1;
+                    unsigned long long m = __ballot(us >= 0 && us < S);
+                    while (m) {
+                        const int jl = __builtin_ctzll(m);
+                        m &= m - 1ull;
+                        const int uj = __builtin_amdgcn_readlane(us, jl);
+                        const uint32_t aj = (uint32_t)__builtin_amdgcn_readlane((int)a, jl);
+                        const uint32_t b = 1u << (uj & 31);
+                        if (g == jl / CW && p == (uj >> 5) && (pend & b)) {
+                            H |= b;
+                            tile[slot(uj)] = aj | dbits; /* row uj = p * 32 + bit */
+                        }
+                    }
+                }
+            } else {
+                const char* base = reinterpret_cast<const char*>(lev + (size_t)(d - w - 1) * plane);
+                uint32_t a[PB], v[PB];
+#pragma unroll
+                for (int q = 0; q < PB; ++q) a[q] = g0 + q < g1 ? arcw[g0 + q] : 0u;
+#pragma unroll
+                for (int q = 0; q < PB; ++q)
+                    v[q] = g0 + q < g1 ? *reinterpret_cast<const uint32_t*>(
+                                             base + ((a[q] & 0xFFFFu) * nw4 + lane4))
+                                       : 0u;
+                for (int i = g0; __any(i < g1); i += PB) {
+                    /* the next batch in flight while this one's candidates are taken */
+                    const int i2 = i + PB;
+                    uint32_t an[PB], vn[PB];
+#pragma unroll
+                    for (int q = 0; q < PB; ++q) an[q] = i2 + q < g1 ? arcw[i2 + q] : 0u;
+#pragma unroll
+                    for (int q = 0; q < PB; ++q)
+                        vn[q] = i2 + q < g1 ? *reinterpret_cast<const uint32_t*>(
+                                                  base + ((an[q] & 0xFFFFu) * nw4 + lane4))
+                                            : 0u;
+#pragma unroll
+                    for (int q = 0; q < PB; ++q) {
+                        const uint32_t xq = v[q] & pend;
+                        uint32_t nb = xq & ~H;
+                        if (TIES) T |= xq & H;
+                        H |= xq;
+                        const uint32_t val = a[q] | dbits;
+                        while (nb) {
+                            const int bb = __builtin_ctz(nb);
+                            nb &= nb - 1u;
+                            tile[slot(p * 32 + bb)] = val;
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < PB; ++q) {
+                        a[q] = an[q];
+                        v[q] = vn[q];
+                    }
+                    if (!TIES && !__any((pend & ~H) != 0u)) break;
+                }
+            }
+            if (TIES) tied += __builtin_popcount(T);
+            pend &= ~H;
+            if (!__any(pend != 0u)) break;
+        }
+    }
+}
+
+template <int CW, int PB, int NWV, bool TIES>
+__global__ __launch_bounds__(64 * NWV) void lvl_pkw_kernel(int n, int ld, int nw, int src0,
+                                                             int nsrc, int nlev, int ntile,
+                                                             unsigned nunit,
+                                                             const int32_t* __restrict__ off,
+                                                             const uint32_t* __restrict__ arcw,
+                                                             const uint32_t* __restrict__ lev,
+                                                             uint32_t* __restrict__ pk,
+                                                             unsigned long long* __restrict__ ties) {
+    constexpr int G = 64 / CW, TT = NWV * G, S = 32 * CW, LVL_PKW_NT = 64 * NWV;
+    extern __shared__ __attribute__((aligned(16))) uint32_t tile[]; /* [S][TT], columns swizzled */
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane / CW, p = lane % CW;
+    /* XCD x takes units [x * per, (x + 1) * per), chunk-major */
+    const unsigned x = blockIdx.x & 7u, L = gridDim.x >> 3, per = (nunit + 7u) >> 3;
+    unsigned tied = 0;
+    for (unsigned j = blockIdx.x >> 3; j < per; j += L) {
+        const unsigned u = x * per + j;
+        if (u >= nunit) break;
+        const int c = (int)(u / (unsigned)ntile), tb = (int)(u % (unsigned)ntile);
+        for (int q = tid; q < S * TT / 4; q += LVL_PKW_NT)
+            reinterpret_cast<uint4*>(tile)[q] = make_uint4(0xFFFFu, 0xFFFFu, 0xFFFFu, 0xFFFFu);
+        __syncthreads();
+        const int tl = wv * G + g, t = tb * TT + tl;
+        const bool tv = t < n;
+        const int word = c * CW + p;
+        const bool valid = tv && word < nw;
+        /* this lane's tile column: target tl, swizzled by the source word (two-way LDS conflicts at
+         * most among a take step's stores; 4-aligned groups stay whole for the write-out) */
+        const int tcol = tl ^ (((p & 7) << 2) & (TT - 1));
+        const int cs0 = src0 + c * S; /* global index of the chunk's first source */
+        pkw_walk<CW, PB, TIES>(t, tv, valid, word, g, p, cs0, n, nw, nlev, off, arcw, lev, tile,
+                               [&](int r) { return r * TT + tcol; }, tied);
+        __syncthreads();
+        /* write-out: source row r of the chunk, TT x 4 B from column tb * TT */
+        constexpr int GPR = TT / 4; /* 16-B pieces per row */
+        for (int q = tid; q < S * GPR; q += LVL_PKW_NT) {
+            const int r = q / GPR, a4 = q % GPR;
+            const int sl = c * S + r;
+            if (sl >= nsrc) break; /* rows are in order: the rest are past too */
+            const int col = (4 * a4) ^ ((((r >> 5) & 7) << 2) & (TT - 1));
+            const uint4 val = *reinterpret_cast<const uint4*>(&tile[r * TT + col]);
+            uint32_t* o = pk + (size_t)sl * ld + (size_t)tb * TT + 4 * a4;
+            __builtin_nontemporal_store(val.x, o);
+            __builtin_nontemporal_store(val.y, o + 1);
+            __builtin_nontemporal_store(val.z, o + 2);
+            __builtin_nontemporal_store(val.w, o + 3);
+        }
+        __syncthreads();
+    }
+    if (TIES) {
+        for (int m = 32; m > 0; m >>= 1) tied += __shfl_xor(tied, m);
+        if (lane == 0 && tied) atomicAdd(&ties[blockIdx.x & 1023u], (unsigned long long)tied);
+    }
+}
+
+/* The same walk with every wave on its own units (no workgroup barriers: a workgroup's waves
+ * finish their targets at different times): a unit is (G targets, one chunk), the wave's tile is
+ * S rows x G words of LDS (8 KB), and its write-out is G x 4 B per source row (16 B for CW = 16);
+ * the eight waves holding a 128-B line's 32 targets write it within a short time, so the L2 merges
+ * the pieces into whole lines. Rows are swizzled by their word (r ^ (p & 7)): a take step's lanes
+ * hit different banks. */
+template <int CW, int PB, int NWV, bool TIES>
+__global__ __launch_bounds__(64 * NWV) void lvl_pkw_wave_kernel(int n, int ld, int nw, int src0,
+                                                               int nsrc, int nlev, int ntg,
+                                                               unsigned nunit,
+                                                               const int32_t* __restrict__ off,
+                                                               const uint32_t* __restrict__ arcw,
+                                                               const uint32_t* __restrict__ lev,
+                                                               uint32_t* __restrict__ pk,
+                                                               unsigned long long* __restrict__ ties) {
+    constexpr int G = 64 / CW, S = 32 * CW;
+    extern __shared__ __attribute__((aligned(16))) uint32_t wtile[];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    uint32_t* tile = wtile + wv * (S * G);
+    const int g = lane / CW, p = lane % CW;
+    /* XCD x's waves take units [x * per, (x + 1) * per), chunk-major */
+    const unsigned x = blockIdx.x & 7u, per = (nunit + 7u) >> 3;
+    const unsigned wid = (blockIdx.x >> 3) * NWV + wv, wpx = (gridDim.x >> 3) * NWV;
+    unsigned tied = 0;
+    auto phys = [](int r) { return r ^ ((r >> 5) & 7); }; /* row swizzle within the word's 32 rows */
+    for (unsigned j = wid; j < per; j += wpx) {
+        const unsigned u = x * per + j;
+        if (u >= nunit) break;
+        const int c = (int)(u / (unsigned)ntg), tg = (int)(u % (unsigned)ntg);
+#pragma unroll
+        for (int q = 0; q < S * G / 256; ++q)
+            reinterpret_cast<uint4*>(tile)[q * 64 + lane] = make_uint4(0xFFFFu, 0xFFFFu, 0xFFFFu, 0xFFFFu);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int t = tg * G + g;
+        const bool tv = t < n;
+        const int word = c * CW + p;
+        const bool valid = tv && word < nw;
+        const int cs0 = src0 + c * S;
+        pkw_walk<CW, PB, TIES>(t, tv, valid, word, g, p, cs0, n, nw, nlev, off, arcw, lev, tile,
+                               [&](int r) { return phys(r) * G + g; }, tied);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        /* write-out: physical row rp holds chunk row phys(rp) (the swizzle is an involution) */
+        constexpr int LPR = G / 4; /* lanes per row (16 B each) */
+#pragma unroll
+        for (int q = 0; q < S * LPR / 64; ++q) {
+            const int rp = q * (64 / LPR) + lane / LPR, h = lane % LPR;
+            const int sl = c * S + phys(rp);
+            const uint4 val = reinterpret_cast<const uint4*>(tile)[rp * LPR + h];
+            if (sl < nsrc)
+                *reinterpret_cast<uint4*>(pk + (size_t)sl * ld + (size_t)tg * G + 4 * h) = val;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (TIES) {
+        for (int m = 32; m > 0; m >>= 1) tied += __shfl_xor(tied, m);
+        if (lane == 0 && tied) atomicAdd(&ties[blockIdx.x & 1023u], (unsigned long long)tied);
+    }
+}
+
+/* arcw[i] = u | rix[i] << 16 (the in-arcs' tail and reliability index) */
+__global__ void lvl_aw_kernel(int total, const uint32_t* __restrict__ arcs,
+                              const uint16_t* __restrict__ rix, uint32_t* __restrict__ arcw) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < total) arcw[i] = (arcs[i] & 0xFFFFu) | ((uint32_t)rix[i] << 16);
+}
+
 __global__ void lvl_sum_kernel(const unsigned long long* __restrict__ v, int k,
                                unsigned long long* __restrict__ out) {
     unsigned long long s = 0;
@@ -783,6 +1037,8 @@ typedef struct {
     int ntab;
     uint32_t* lev;
     uint8_t* l8; /* u8 distance rows (nrows x ld) for the reliability pass */
+    int pkw;     /* the post pass takes srt_levels_pkw (no lat / l8 rows written by the build) */
+    int total;   /* in-arcs held (w <= lmax) */
     unsigned long long* dkey; /* the diagonal rule's key per local row (undirected rows form) */
     const double* r_rows;
     void* p[32]; /* every allocation of the build (LVL_ALLOC), freed together */
@@ -835,15 +1091,64 @@ const uint8_t* srt_levels_l8(void) {
         SRT_HIPCHK(srt_malloc_async(&(ptr), (bytes), st));         \
         L->p[L->k++] = (void*)(ptr);                               \
     } while (0)
+/* the same, but a failed allocation only clears *ok (the caller agrees on a verdict first) */
+#define LVL_TRY_ALLOC(ptr, bytes, ok)                                                   \
+    do {                                                                                \
+        (ptr) = NULL;                                                                   \
+        if (*(ok) && L->k < (int)(sizeof(L->p) / sizeof(L->p[0])) &&                    \
+            srt_malloc_async(&(ptr), (bytes), st) == hipSuccess) {                      \
+            L->p[L->k++] = (void*)(ptr);                                                \
+        } else {                                                                        \
+            (void)hipGetLastError();                                                    \
+            (ptr) = NULL;                                                               \
+            *(ok) = 0;                                                                  \
+        }                                                                               \
+    } while (0)
+
+/* a min all-reduce of one host int over the ranks (R > 1), through a device word */
+static int lvl_agree_min(const srt_comm* comm, int32_t* dword, int* v, hipStream_t st) {
+    SRT_HIPCHK(hipMemcpyAsync(dword, v, sizeof(int32_t), hipMemcpyHostToDevice, st));
+    int rc = srt_coll_allreduce_i32(comm, dword, 1, 1, st);
+    if (rc) return rc;
+    SRT_HIPCHK(hipMemcpyAsync(v, dword, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    SRT_HIPCHK(hipStreamSynchronize(st));
+    return SRT_OK;
+}
+
+/* bytes the build can still take from the device: free memory plus what the library's scratch
+ * pool holds unused (its release threshold keeps freed blocks mapped) */
+static size_t lvl_avail_bytes(void) {
+    const int cap_mb = srt_form_int("memcap", -1); /* test hook: a nearly full device */
+    if (cap_mb >= 0) return (size_t)cap_mb << 20;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    uint64_t res = 0, used = 0;
+    hipMemPool_t pool = srt_scratch_pool();
+    if (hipMemPoolGetAttribute(pool, hipMemPoolAttrReservedMemCurrent, &res) == hipSuccess &&
+        hipMemPoolGetAttribute(pool, hipMemPoolAttrUsedMemCurrent, &used) == hipSuccess && res > used)
+        fr += (size_t)(res - used);
+    (void)hipGetLastError();
+    return fr;
+}
+
+/* levels enqueued per host round trip: a batch's levels past the one that settles every pair
+ * return at once (lvl_step_kernel's prev test) */
+#define LVL_BATCH 8
 
 /* One build of the local rows' distances (nrows x ld). comm (NULL on one GPU): undirected row
  * shards, every rank sees every target's in-arcs after the segment broadcasts. fw_ms: the
- * predicted Floyd-Warshall time; the level budget keeps the predicted level time under half of
- * it. *levels = the level that settled every pair (0: not applicable / over budget -- the caller
- * runs Floyd-Warshall; every rank of a sharded build returns the same verdict). *gather_bytes: the
- * Delta words gathered (the kernel's algorithmic bytes). On success lat_rows hold the u32 rows
- * (the FW finish pass's output) and the slot keeps the arcs, the planes and the u8 rows for
- * srt_levels_pred / srt_levels_l8 until srt_levels_release. */
+ * predicted Floyd-Warshall time (of the largest shard); the level budget keeps the predicted level
+ * time under half of it. *levels = the level that settled every pair (0: not applicable / over
+ * budget / out of memory -- the caller runs Floyd-Warshall). Every rank of a sharded build takes
+ * the same decisions in the same order: the budget is agreed (min all-reduce) before the first
+ * rank-dependent branch, so is the outcome of the allocations, and the verdict at the end; a rank
+ * never leaves while its peers wait in a collective. *gather_bytes: the Delta words gathered (the
+ * kernel's algorithmic bytes). On success the slot keeps the arcs and the planes for the post pass
+ * until srt_levels_release; lat_rows hold the u32 rows, unless the post pass writes them itself
+ * (srt_levels_pkw_ready). */
 int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
                      const uint32_t* w_rows, const double* r_rows, uint32_t* lat_rows, double fw_ms,
                      hipStream_t st, evpool_t* evp, int* levels, int64_t* gather_bytes) {
@@ -852,10 +1157,19 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     lvl_state* L = &g_lvl[srt_state_slot()];
     if (L->held) lvl_free(L, st);
     const int R = comm ? srt_comm_size(comm) : 1;
-    if (n > 65535 || ld % 128 || nrows % 128 || row0 % 128) return SRT_OK;
+    /* rank-independent applicability: the shards are SRT_SHARD_ALIGN (128) aligned, so nrows %
+     * 128 == 0 on every rank once ld % 128 == 0; the 32-bit plane offsets are checked against the
+     * largest shard */
+    if (n > 65535 || ld % 128 || nrows % 128 || row0 % 128 || R > 64) return SRT_OK;
     if (R > 1 && directed) return SRT_OK; /* in-arcs of a directed graph span every rank's rows */
+    int max_rows = nrows;
+    for (int q = 0; q < R && R > 1; q++) {
+        int32_t b = 0, e = 0;
+        srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &b, &e);
+        max_rows = max(max_rows, e - b);
+    }
+    if ((size_t)n * (size_t)(max_rows / 32) * 4 > 0xFFFFFFFFull) return SRT_OK; /* 32-bit offsets */
     const int nw = nrows / 32, nchunk = (nw + 63) / 64;
-    if ((size_t)n * nw * 4 > 0xFFFFFFFFull) return SRT_OK; /* 32-bit row offsets */
     L->st = st;
     /* on any early return below the allocations go back (lvl_free), unless the build is held */
     struct guard {
@@ -870,7 +1184,10 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     unsigned long long* dhist = NULL;
     LVL_ALLOC(cnt, (ncnt + 1) * sizeof(int32_t));
     LVL_ALLOC(off, (ncnt + 1) * sizeof(int32_t));
-    LVL_ALLOC(dhist, LVL_STRIDE * sizeof(unsigned long long));
+    /* the histogram, then LVL_WMAX + 1 completion flags, then the agreement word */
+    LVL_ALLOC(dhist, (2 * LVL_STRIDE + 8) * sizeof(unsigned long long));
+    int* dinc = reinterpret_cast<int*>(dhist + LVL_STRIDE);
+    int32_t* dagree = reinterpret_cast<int32_t*>(dhist + 2 * LVL_STRIDE);
     unsigned long long* dkey = NULL;
     uint32_t* stash = NULL;
     int32_t* scnt = NULL;
@@ -880,7 +1197,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         LVL_ALLOC(scnt, (size_t)nrows * sizeof(int32_t));
     }
     SRT_HIPCHK(hipMemsetAsync(cnt, 0, (ncnt + 1) * sizeof(int32_t), st));
-    SRT_HIPCHK(hipMemsetAsync(dhist, 0, LVL_STRIDE * sizeof(unsigned long long), st));
+    SRT_HIPCHK(hipMemsetAsync(dhist, 0, (2 * LVL_STRIDE + 8) * sizeof(unsigned long long), st));
     if (directed)
         lvl_arcs_cols_kernel<false><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, cnt, 0, NULL, NULL);
     else
@@ -894,34 +1211,70 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     unsigned long long hist[LVL_STRIDE];
     SRT_HIPCHK(hipMemcpyAsync(hist, dhist, sizeof(hist), hipMemcpyDeviceToHost, st));
     SRT_HIPCHK(hipStreamSynchronize(st));
-    /* level budget: the largest L whose predicted time stays under half the FW time */
-    const double nw_all = (double)nrows / 32.0;
+    /* level budget from global quantities (the summed histogram, the largest shard's words): the
+     * largest L whose predicted time stays under half the FW time */
+    const double nw_all = (double)max_rows / 32.0;
     int lmax = 0;
     for (int x = 1; x <= LVL_WMAX; ++x) {
         if (lvl_estimate(hist, x, (double)n, nw_all) > 0.5 * fw_ms) break;
         lmax = x;
     }
+    /* and by memory: the planes (lmax x n x nw words) within half of what the device has left */
+    const size_t plane = (size_t)n * nw;
+    if (plane > 0) {
+        const size_t cap = lvl_avail_bytes() / 2 / (plane * sizeof(uint32_t));
+        if ((size_t)lmax > cap) lmax = (int)cap;
+    }
+    if (R > 1 && (rc = lvl_agree_min(comm, dagree, &lmax, st))) return rc;
     int wmin = 0;
     for (int x = 1; x <= LVL_WMAX && !wmin; ++x)
         if (hist[x]) wmin = x;
-    if (lmax < 2 || !wmin || wmin > lmax) return SRT_OK;
+    if (lmax < 2 || !wmin || wmin > lmax) return SRT_OK; /* the same on every rank */
+    /* in-arcs with w <= lmax: their count from the histogram (no read-back of the scan) */
+    int64_t total64 = 0;
+    for (int x = 1; x <= lmax; ++x) total64 += (int64_t)hist[x];
+    if (total64 > 0x7FFFFFF0ll) return SRT_OK; /* int32 arc offsets (global) */
+    const int32_t total = (int32_t)total64;
+    /* every allocation of the build up front, softly: one agreed outcome, then the work */
+    int ok = 1;
+    uint32_t *arcs = NULL, *arcs2 = NULL, *aoff = NULL, *lev = NULL, *Rb = NULL;
+    double *ar = NULL, *ar2 = NULL;
+    int32_t* seg = NULL;
+    void *tmp = NULL, *stmp = NULL;
+    uint8_t* done = NULL;
+    size_t tmp_bytes = 0, sb = 0;
+    SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(NULL, tmp_bytes, cnt, off, (int)(ncnt + 1), st));
+    if (total > 0)
+        SRT_HIPCHK(hipcub::DeviceSegmentedRadixSort::SortPairs(NULL, sb, arcs, arcs2, ar, ar2, total,
+                                                               ld, seg, seg + 1, 0, 24, st));
+    LVL_TRY_ALLOC(tmp, tmp_bytes, &ok);
+    LVL_TRY_ALLOC(arcs, ((size_t)total + 8) * sizeof(uint32_t), &ok);
+    LVL_TRY_ALLOC(ar, ((size_t)total + 8) * sizeof(double), &ok);
+    LVL_TRY_ALLOC(arcs2, ((size_t)total + 8) * sizeof(uint32_t), &ok);
+    LVL_TRY_ALLOC(ar2, ((size_t)total + 8) * sizeof(double), &ok);
+    LVL_TRY_ALLOC(seg, ((size_t)ld + 1) * sizeof(int32_t), &ok);
+    if (total > 0) LVL_TRY_ALLOC(stmp, sb, &ok);
+    LVL_TRY_ALLOC(aoff, ((size_t)total + 64) * sizeof(uint32_t), &ok); /* + a gather batch's tail */
+    LVL_TRY_ALLOC(lev, (size_t)lmax * plane * sizeof(uint32_t) + 16, &ok);
+    LVL_TRY_ALLOC(Rb, plane * sizeof(uint32_t) + 16, &ok);
+    LVL_TRY_ALLOC(done, (size_t)n * nchunk + 16, &ok);
+    /* the distinct arc reliabilities (packed post pass, n <= 32768; SRT_FORM pk=0 keeps f64) */
+    const bool want_rt = total > 0 && n <= 32768 && srt_form_int("pk", 1) != 0;
+    unsigned long long* H = NULL;
+    uint16_t *map = NULL, *rix = NULL;
+    double* rtab = NULL;
+    if (want_rt) {
+        LVL_TRY_ALLOC(H, LVL_RT_SLOTS * sizeof(unsigned long long), &ok);
+        LVL_TRY_ALLOC(map, LVL_RT_SLOTS * sizeof(uint16_t), &ok);
+        LVL_TRY_ALLOC(rix, ((size_t)total + 8) * sizeof(uint16_t), &ok);
+        LVL_TRY_ALLOC(rtab, LVL_RT_CAP * sizeof(double), &ok);
+    }
+    if (R > 1 && (rc = lvl_agree_min(comm, dagree, &ok, st))) return rc;
+    if (!ok) return SRT_OK; /* out of device memory somewhere: Floyd-Warshall on every rank */
     /* offsets over the arcs with w <= lmax, (target, weight)-major */
     lvl_mask_kernel<<<srt_ceil_div((int64_t)ncnt, 256), 256, 0, st>>>(ncnt, lmax, cnt);
     SRT_HIPCHK(hipGetLastError());
-    size_t tmp_bytes = 0;
-    SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(NULL, tmp_bytes, cnt, off, (int)(ncnt + 1), st));
-    void* tmp = NULL;
-    LVL_ALLOC(tmp, tmp_bytes);
     SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, (int)(ncnt + 1), st));
-    int32_t total = 0;
-    SRT_HIPCHK(hipMemcpyAsync(&total, off + ncnt, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    SRT_HIPCHK(hipStreamSynchronize(st));
-    uint32_t *arcs = NULL, *arcs2 = NULL;
-    double *ar = NULL, *ar2 = NULL;
-    LVL_ALLOC(arcs, ((size_t)total + 8) * sizeof(uint32_t));
-    LVL_ALLOC(ar, ((size_t)total + 8) * sizeof(double));
-    LVL_ALLOC(arcs2, ((size_t)total + 8) * sizeof(uint32_t));
-    LVL_ALLOC(ar2, ((size_t)total + 8) * sizeof(double));
     if (directed)
         lvl_arcs_cols_kernel<true><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, NULL, lmax, off, arcs,
                                                             r_rows, ar);
@@ -931,7 +1284,6 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     SRT_HIPCHK(hipGetLastError());
     if (R > 1) { /* every rank filled its rows' segment: broadcast the segments */
         int32_t hoff[65];
-        if (R > 64) return SRT_OK;
         for (int q = 0; q <= R; q++) {
             int32_t b = ld, e = ld;
             if (q < R) srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &b, &e);
@@ -951,113 +1303,89 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     }
     /* in-arcs of each target sorted by (weight, source vertex): the order the predecessor search
      * walks them in (the fill's atomics leave the order inside a weight arbitrary) */
-    int32_t* seg = NULL;
-    LVL_ALLOC(seg, ((size_t)ld + 1) * sizeof(int32_t));
     lvl_segs_kernel<<<srt_ceil_div(ld + 1, 256), 256, 0, st>>>(ld, off, seg);
     SRT_HIPCHK(hipGetLastError());
-    if (total > 0) {
-        size_t sb = 0;
-        SRT_HIPCHK(hipcub::DeviceSegmentedRadixSort::SortPairs(NULL, sb, arcs, arcs2, ar, ar2, total,
-                                                               ld, seg, seg + 1, 0, 24, st));
-        void* stmp = NULL;
-        LVL_ALLOC(stmp, sb);
+    if (total > 0)
         SRT_HIPCHK(hipcub::DeviceSegmentedRadixSort::SortPairs(stmp, sb, arcs, arcs2, ar, ar2, total,
                                                                ld, seg, seg + 1, 0, 24, st));
-    }
     arcs = arcs2;
     ar = ar2;
     /* level state over the local sources */
-    uint32_t* aoff = NULL;
-    LVL_ALLOC(aoff, ((size_t)total + 64) * sizeof(uint32_t)); /* + a gather batch's tail */
     if (total > 0) {
         lvl_aoff_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, nw, arcs, aoff);
         SRT_HIPCHK(hipGetLastError());
     }
-    /* the distinct arc reliabilities (packed post pass, n <= 32768; SRT_FORM pk=0 keeps f64) */
-    uint16_t* rix = NULL;
-    double* rtab = NULL;
-    int ntab = 0;
-    if (total > 0 && n <= 32768 && srt_form_int("pk", 1) != 0) {
-        unsigned long long* H = NULL;
-        uint16_t* map = NULL;
-        int* dflag = NULL;
-        LVL_ALLOC(H, LVL_RT_SLOTS * sizeof(unsigned long long));
-        LVL_ALLOC(map, LVL_RT_SLOTS * sizeof(uint16_t));
-        LVL_ALLOC(rix, ((size_t)total + 8) * sizeof(uint16_t));
-        LVL_ALLOC(rtab, LVL_RT_CAP * sizeof(double));
-        LVL_ALLOC(dflag, 2 * sizeof(int));
+    /* the reliability table: its flags are read with the levels' completion (no round trip) */
+    int* dflag = dinc + LVL_WMAX + 1; /* [0] probe overflow, [1] distinct values */
+    if (want_rt) {
         SRT_HIPCHK(hipMemsetAsync(H, 0xFF, LVL_RT_SLOTS * sizeof(unsigned long long), st));
-        SRT_HIPCHK(hipMemsetAsync(dflag, 0, 2 * sizeof(int), st));
         lvl_rt_hash_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, ar, H, rix, dflag);
         lvl_rt_compact_kernel<<<1, 1024, 0, st>>>(H, map, rtab, dflag + 1);
         lvl_rt_remap_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, map, rix);
         SRT_HIPCHK(hipGetLastError());
-        int hf[2] = {0, 0};
-        SRT_HIPCHK(hipMemcpyAsync(hf, dflag, sizeof(hf), hipMemcpyDeviceToHost, st));
-        SRT_HIPCHK(hipStreamSynchronize(st));
-        if (hf[0] || hf[1] > LVL_RT_CAP) {
-            rix = NULL; /* (freed with the state) */
-            rtab = NULL;
-        } else {
-            ntab = hf[1];
-        }
     }
-    const size_t plane = (size_t)n * nw;
-    uint32_t *lev = NULL, *Rb = NULL;
-    uint8_t* done = NULL;
-    LVL_ALLOC(lev, (size_t)lmax * plane * sizeof(uint32_t));
-    LVL_ALLOC(Rb, plane * sizeof(uint32_t));
-    LVL_ALLOC(done, (size_t)n * nchunk + 4 * sizeof(int) * (size_t)(LVL_WMAX + 1));
-    int* dinc = (int*)(void*)(((uintptr_t)(done + (size_t)n * nchunk) + 15) & ~(uintptr_t)15);
     SRT_HIPCHK(hipMemsetAsync(Rb, 0, plane * sizeof(uint32_t), st));
     SRT_HIPCHK(hipMemsetAsync(done, 0, (size_t)n * nchunk, st));
-    SRT_HIPCHK(hipMemsetAsync(dinc, 0, sizeof(int) * (size_t)(LVL_WMAX + 1), st));
     lvl_init_kernel<<<srt_ceil_div(nrows, 256), 256, 0, st>>>(n, row0, nrows, nw, Rb);
     SRT_HIPCHK(hipGetLastError());
     unsigned nblk = (unsigned)(((n + 3) / 4) * nchunk);
     nblk = (nblk + 7u) & ~7u;
     const unsigned pgrid = lvl_grid((const void*)lvl_step_kernel, nblk);
-    int D = 0;
-    int64_t gathered = 0;
-    for (int d = 1; d <= lmax; ++d) {
-        if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
-        lvl_step_kernel<<<pgrid, 256, 0, st>>>(d, n, nw, nchunk, row0, nrows, nblk, off, arcs, aoff,
-                                              lev, Rb, done, dinc + d);
-        if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
+    /* the levels in batches of LVL_BATCH, one host round trip per batch */
+    int D = 0, hflag[2] = {0, 0};
+    const int ev0 = evp ? evp->used : 0;
+    if (evp && (rc = evpool_reserve(evp, ev0 + 2 * lmax))) return rc;
+    for (int d0 = 1; d0 <= lmax && !D; d0 += LVL_BATCH) {
+        const int d1 = min(lmax, d0 + LVL_BATCH - 1);
+        for (int d = d0; d <= d1; ++d) {
+            if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
+            lvl_step_kernel<<<pgrid, 256, 0, st>>>(d, n, nw, nchunk, row0, nrows, nblk, off, arcs,
+                                                  aoff, lev, Rb, done, dinc + d,
+                                                  d > 1 ? dinc + d - 1 : NULL);
+            if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
+        }
         SRT_HIPCHK(hipGetLastError());
-        int inc = 0;
-        SRT_HIPCHK(hipMemcpyAsync(&inc, dinc + d, sizeof(int), hipMemcpyDeviceToHost, st));
+        int inc[LVL_BATCH];
+        SRT_HIPCHK(hipMemcpyAsync(inc, dinc + d0, sizeof(int) * (d1 - d0 + 1), hipMemcpyDeviceToHost,
+                                  st));
+        SRT_HIPCHK(hipMemcpyAsync(hflag, dflag, sizeof(hflag), hipMemcpyDeviceToHost, st));
         SRT_HIPCHK(hipStreamSynchronize(st));
+        for (int d = d0; d <= d1 && !D; ++d)
+            if (inc[d - d0] == 0) D = d;
+    }
+    if (evp && D) evp->used = ev0 + 2 * D; /* the levels that did work */
+    int64_t gathered = 0;
+    for (int d = 1; d <= D; ++d) {
         double below = 0;
         for (int x = 1; x < d; ++x) below += (double)hist[x];
         gathered += (int64_t)(below * (double)nw * 4.0);
-        if (inc == 0) {
-            D = d;
-            break;
-        }
     }
-    int ok = D > 0;
-    if (R > 1) { /* one verdict for every rank: all settled, or Floyd-Warshall everywhere */
-        int32_t* flag = (int32_t*)dinc;
-        SRT_HIPCHK(hipMemcpyAsync(flag, &ok, sizeof(int32_t), hipMemcpyHostToDevice, st));
-        if ((rc = srt_coll_allreduce_i32(comm, flag, 1, 1, st))) return rc;
-        SRT_HIPCHK(hipMemcpyAsync(&ok, flag, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-        SRT_HIPCHK(hipStreamSynchronize(st));
-    }
+    ok = D > 0;
+    if (R > 1 && (rc = lvl_agree_min(comm, dagree, &ok, st))) return rc; /* one verdict */
     if (!ok) return SRT_OK;
+    int ntab = 0;
+    if (want_rt && !hflag[0] && hflag[1] <= LVL_RT_CAP)
+        ntab = hflag[1];
+    else
+        rix = NULL, rtab = NULL; /* (freed with the state) */
+    /* the fused post pass (srt_levels_pkw) writes the u32 rows itself: the table of distinct arc
+     * reliabilities, 5-bit levels and u16 vertices (n <= 32768) */
+    const int pkw = rix && D <= 31 && n <= 32768 && srt_form_int("pkw", 1) != 0;
     uint8_t* l8 = NULL;
-    LVL_ALLOC(l8, (size_t)nrows * ld);
-    if (D <= LVL_OUT_L) {
-        const int lds = D * 2 * 256 * (int)sizeof(uint4);
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)lvl_out8_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        lvl_out8_kernel<<<dim3(srt_ceil_div(ld, 256), srt_ceil_div(nw, 8)), 256, lds, st>>>(
-            n, ld, nw, row0, D, lev, lat_rows, l8);
-    } else {
-        lvl_out_kernel<<<dim3(srt_ceil_div(ld, 1024), srt_ceil_div(nw, 16)), 256, 0, st>>>(
-            n, ld, nw, row0, D, lev, lat_rows, l8);
+    if (!pkw) {
+        LVL_ALLOC(l8, (size_t)nrows * ld);
+        if (D <= LVL_OUT_L) {
+            const int lds = D * 2 * 256 * (int)sizeof(uint4);
+            SRT_HIPCHK(hipFuncSetAttribute((const void*)lvl_out8_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+            lvl_out8_kernel<<<dim3(srt_ceil_div(ld, 256), srt_ceil_div(nw, 8)), 256, lds, st>>>(
+                n, ld, nw, row0, D, lev, lat_rows, l8);
+        } else {
+            lvl_out_kernel<<<dim3(srt_ceil_div(ld, 1024), srt_ceil_div(nw, 16)), 256, 0, st>>>(
+                n, ld, nw, row0, D, lev, lat_rows, l8);
+        }
+        SRT_HIPCHK(hipGetLastError());
     }
-    SRT_HIPCHK(hipGetLastError());
     *levels = D;
     *gather_bytes = gathered;
     L->held = 1;
@@ -1077,8 +1405,78 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     L->ntab = ntab;
     L->lev = lev;
     L->l8 = l8;
+    L->pkw = pkw;
+    L->total = total;
     L->dkey = dkey;
     L->r_rows = r_rows;
+    return SRT_OK;
+}
+
+/* 1 when the held build's post pass is srt_levels_pkw + the packed reliability pass */
+int srt_levels_pkw_ready(void) {
+    const lvl_state* L = &g_lvl[srt_state_slot()];
+    return L->held && L->pkw;
+}
+
+/* Source-major packed words of the held build (lvl_pkw_kernel): pk[sl][t] (row stride ld, nrows
+ * rows) = pred | rix << 16 | level << 27, 0xFFFF where there is no level. ties != NULL adds the
+ * tied pairs (the walk then visits every arc of a weight). */
+int srt_levels_pkw(uint32_t* pk, int ld, unsigned long long* ties, hipStream_t st) {
+    lvl_state* L = &g_lvl[srt_state_slot()];
+    if (!L->held || !L->pkw) {
+        srt_set_error("levels: no held level build in the packed-word form");
+        return SRT_E_ARG;
+    }
+    const int total = L->total;
+    /* the arcs' (tail | reliability index) words, into the gather offsets' buffer (free now) */
+    uint32_t* arcw = L->aoff;
+    if (total > 0) {
+        lvl_aw_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, L->arcs, L->rix, arcw);
+        SRT_HIPCHK(hipGetLastError());
+    }
+    unsigned long long* part = NULL;
+    if (ties) {
+        SRT_HIPCHK(srt_malloc_async(&part, 1024 * sizeof(unsigned long long), st));
+        SRT_HIPCHK(hipMemsetAsync(part, 0, 1024 * sizeof(unsigned long long), st));
+    }
+    constexpr int CW = LVL_PKW_CW, PB = LVL_PKW_PB, NWV = LVL_PKW_W, NT = 64 * NWV;
+    constexpr int G = 64 / CW, S = 32 * CW;
+    constexpr bool WAVE = LVL_PKW_WAVE != 0;
+    constexpr int TT = WAVE ? G : NWV * G; /* targets per unit */
+    const int lds = S * NWV * G * (int)sizeof(uint32_t);
+    const int ntile = ld / TT, nchunkw = (L->nw + CW - 1) / CW;
+    const unsigned nunit = (unsigned)ntile * (unsigned)nchunkw;
+    const void* fn = WAVE ? (ties ? (const void*)lvl_pkw_wave_kernel<CW, PB, NWV, true>
+                                  : (const void*)lvl_pkw_wave_kernel<CW, PB, NWV, false>)
+                          : (ties ? (const void*)lvl_pkw_kernel<CW, PB, NWV, true>
+                                  : (const void*)lvl_pkw_kernel<CW, PB, NWV, false>);
+    SRT_HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    int dev = 0, cus = 256, per = 2;
+    if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, NT, lds) != hipSuccess || per < 1)
+        per = 1;
+    (void)hipGetLastError();
+    unsigned grid = (unsigned)(cus * per) & ~7u;
+    if (grid < 8) grid = 8;
+    if (WAVE && ties)
+        lvl_pkw_wave_kernel<CW, PB, NWV, true><<<grid, NT, lds, st>>>(
+            L->n, ld, L->nw, L->row0, L->nrows, L->D, ntile, nunit, L->off, arcw, L->lev, pk, part);
+    else if (WAVE)
+        lvl_pkw_wave_kernel<CW, PB, NWV, false><<<grid, NT, lds, st>>>(
+            L->n, ld, L->nw, L->row0, L->nrows, L->D, ntile, nunit, L->off, arcw, L->lev, pk, NULL);
+    else if (ties)
+        lvl_pkw_kernel<CW, PB, NWV, true><<<grid, NT, lds, st>>>(
+            L->n, ld, L->nw, L->row0, L->nrows, L->D, ntile, nunit, L->off, arcw, L->lev, pk, part);
+    else
+        lvl_pkw_kernel<CW, PB, NWV, false><<<grid, NT, lds, st>>>(
+            L->n, ld, L->nw, L->row0, L->nrows, L->D, ntile, nunit, L->off, arcw, L->lev, pk, NULL);
+    SRT_HIPCHK(hipGetLastError());
+    if (ties) {
+        lvl_sum_kernel<<<1, 1024, 0, st>>>(part, 1024, ties);
+        SRT_HIPCHK(hipGetLastError());
+        SRT_HIPCHK(hipFreeAsync(part, st));
+    }
     return SRT_OK;
 }
 

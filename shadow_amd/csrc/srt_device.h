@@ -161,6 +161,11 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
  * (target-major, row stride ldp) */
 int srt_levels_pred(void* predT, int pred16, double* rT, size_t ldp, unsigned long long* ties,
                     hipStream_t st);
+/* 1 when the held level build's post pass is the source-major packed-word form (srt_levels_pkw:
+ * pred | reliability index << 16 | level << 27 per pair, then the reliability pass writes the u32
+ * rows too); 0: srt_levels_pred + the transposes */
+int srt_levels_pkw_ready(void);
+int srt_levels_pkw(uint32_t* pk, int ld, unsigned long long* ties, hipStream_t st);
 /* frees the held level build (stream-ordered) */
 void srt_levels_release(hipStream_t st);
 /* the held build's u8 distance rows (nrows x ld, 0 on the diagonal), NULL if none */

@@ -38,21 +38,37 @@ extern void worker_updateMinTimeJump(double minPathLatency);
 /* ---- u32 -> i32 map (IP in network order -> vertex), lock-free reads ----------------------
  * Open addressing over 64-bit slot words (key << 32 | (u32)value; value -1 = empty, -2 =
  * tombstone), so a reader sees a key and its value in one atomic load. Writers (attach, detach)
- * serialise on ip_lock; a resize builds a new table and publishes it with release, and the old one
- * stays allocated until topology_free, so a reader that loaded it keeps reading valid memory (a
- * consistent earlier state of the map). Readers take no lock. */
+ * serialise on ip_lock; a rehash builds a new table and publishes it. Readers take no lock: each
+ * one counts itself in a per-thread stripe around its probe, so a writer that finds every stripe
+ * at zero right after publishing a new table knows no reader still holds an older one, and frees
+ * the retired tables then (otherwise they wait for a later rehash, or topology_free). A rehash of
+ * a table that is mostly tombstones keeps its capacity, so attach/detach cycles do not grow it. */
 typedef struct ipmap_tab {
     size_t cap, used; /* used: live + tombstones (probe-chain length bound) */
     struct ipmap_tab* retired;
     _Atomic uint64_t slot[];
 } ipmap_tab;
 
+#define IPM_STRIPES 64
+typedef struct {
+    _Atomic long n;
+    char pad[64 - sizeof(long)];
+} ipm_stripe;
+
 typedef struct {
     _Atomic(ipmap_tab*) cur;
-    ipmap_tab* retired; /* replaced tables, freed at topology_free */
+    ipmap_tab* retired; /* replaced tables not yet known to be unread */
+    ipm_stripe rd[IPM_STRIPES];
 } ipmap_t;
 
 #define IPM_EMPTY 0xFFFFFFFFull /* value -1 */
+
+static _Thread_local int ipm_tid = -1;
+static _Atomic int ipm_next_tid;
+static int ipm_stripe_of_thread(void) {
+    if (ipm_tid < 0) ipm_tid = atomic_fetch_add(&ipm_next_tid, 1) & (IPM_STRIPES - 1);
+    return ipm_tid;
+}
 
 static size_t h32(uint32_t x) {
     x ^= x >> 16;
@@ -77,11 +93,23 @@ static ipmap_tab* ipm_alloc(size_t cap) {
     return t;
 }
 
+static void ipm_free_list(ipmap_tab* t) {
+    while (t) {
+        ipmap_tab* nx = t->retired;
+        free(t);
+        t = nx;
+    }
+}
+
 /* caller holds ip_lock (writer) */
 static int ipmap_put(ipmap_t* m, uint32_t k, int32_t v) {
     ipmap_tab* t = atomic_load_explicit(&m->cur, memory_order_relaxed);
-    if (!t || (t->used + 1) * 2 > t->cap) { /* grow (or drop tombstones): a new table */
-        const size_t nc = t ? t->cap * 2 : 64;
+    if (!t || (t->used + 1) * 2 > t->cap) { /* grow, or drop the tombstones: a new table */
+        size_t live = 0;
+        for (size_t i = 0; t && i < t->cap; i++)
+            live += ipm_val(atomic_load_explicit(&t->slot[i], memory_order_relaxed)) >= 0;
+        size_t nc = t ? t->cap : 64; /* mostly tombstones: the same capacity */
+        while ((live + 1) * 4 > nc) nc *= 2;
         ipmap_tab* nt = ipm_alloc(nc);
         if (!nt) return -1;
         for (size_t i = 0; t && i < t->cap; i++) {
@@ -93,10 +121,18 @@ static int ipmap_put(ipmap_t* m, uint32_t k, int32_t v) {
             atomic_store_explicit(&nt->slot[h], w, memory_order_relaxed);
             nt->used++;
         }
-        atomic_store_explicit(&m->cur, nt, memory_order_release);
+        atomic_store_explicit(&m->cur, nt, memory_order_seq_cst); /* publish */
         if (t) {
             t->retired = m->retired;
             m->retired = t;
+        }
+        /* a reader counted in no stripe now will load nt: every retired table is unread */
+        long busy = 0;
+        for (int i = 0; i < IPM_STRIPES && !busy; i++)
+            busy = atomic_load_explicit(&m->rd[i].n, memory_order_seq_cst);
+        if (!busy) {
+            ipm_free_list(m->retired);
+            m->retired = NULL;
         }
         t = nt;
     }
@@ -120,19 +156,28 @@ static int ipmap_put(ipmap_t* m, uint32_t k, int32_t v) {
     return 0;
 }
 
-/* no lock: one acquire load of the table, then of each probed slot */
-static int32_t ipmap_get(const ipmap_t* m, uint32_t k) {
-    const ipmap_tab* t = atomic_load_explicit(&((ipmap_t*)m)->cur, memory_order_acquire);
-    if (!t) return -1;
-    size_t h = h32(k) & (t->cap - 1);
-    for (size_t probes = 0; probes < t->cap; probes++) {
-        const uint64_t w = atomic_load_explicit(&((ipmap_tab*)t)->slot[h], memory_order_acquire);
-        const int32_t x = ipm_val(w);
-        if (x == -1) return -1;
-        if (x >= 0 && ipm_key(w) == k) return x;
-        h = (h + 1) & (t->cap - 1);
+/* no lock: count this reader in its stripe, one load of the table, then of each probed slot */
+static int32_t ipmap_get(const ipmap_t* cm, uint32_t k) {
+    ipmap_t* m = (ipmap_t*)cm;
+    _Atomic long* rd = &m->rd[ipm_stripe_of_thread()].n;
+    atomic_fetch_add_explicit(rd, 1, memory_order_seq_cst);
+    const ipmap_tab* t = atomic_load_explicit(&m->cur, memory_order_seq_cst);
+    int32_t r = -1;
+    if (t) {
+        size_t h = h32(k) & (t->cap - 1);
+        for (size_t probes = 0; probes < t->cap; probes++) {
+            const uint64_t w = atomic_load_explicit(&((ipmap_tab*)t)->slot[h], memory_order_acquire);
+            const int32_t x = ipm_val(w);
+            if (x == -1) break;
+            if (x >= 0 && ipm_key(w) == k) {
+                r = x;
+                break;
+            }
+            h = (h + 1) & (t->cap - 1);
+        }
     }
-    return -1;
+    atomic_fetch_sub_explicit(rd, 1, memory_order_release);
+    return r;
 }
 
 /* caller holds ip_lock (writer) */
@@ -154,11 +199,15 @@ static void ipmap_del(ipmap_t* m, uint32_t k) {
 
 static void ipmap_free(ipmap_t* m) {
     free(atomic_load(&m->cur));
-    for (ipmap_tab* t = m->retired; t;) {
-        ipmap_tab* nx = t->retired;
-        free(t);
-        t = nx;
-    }
+    ipm_free_list(m->retired);
+    m->retired = NULL;
+}
+
+/* the tables an ipmap holds (live + retired), for the growth test */
+static size_t ipmap_tables(const ipmap_t* m) {
+    size_t k = atomic_load(&((ipmap_t*)m)->cur) ? 1 : 0;
+    for (const ipmap_tab* t = m->retired; t; t = t->retired) k++;
+    return k;
 }
 
 /* ---- packet counters, one per cached Path (the served pair's source, target) ------------
@@ -1096,6 +1145,15 @@ void srt_topology_detach_ip(Topology* t, uint32_t ipNet) {
 
 void topology_detach(Topology* t, Address* address) {
     srt_topology_detach_ip(t, address_toNetworkIP(address));
+}
+
+/* tables the IP map holds (current + retired): bounded under attach / detach cycles */
+int64_t srt_topology_ipmap_tables(Topology* t) {
+    if (!magic_ok(t)) return -1;
+    pthread_rwlock_rdlock(&t->ip_lock);
+    const int64_t k = (int64_t)ipmap_tables(&t->ipmap);
+    pthread_rwlock_unlock(&t->ip_lock);
+    return k;
 }
 
 /* lock-free (the packet path's two lookups per call, topology.c:1905-1915) */

@@ -72,6 +72,8 @@ def test_c4_full_size_default_schedule(gpu, monkeypatch, mode):
     # tied pairs (canonical rule vs igraph's heap order) are counted: on C4 about half of the
     # pairs have two or more tight predecessors at the same smallest D[s][u] (many 1-2 ms arcs)
     assert 0 < tied < n * (n - 1)
+    if mode == "levels":  # the canonical rule's count is a property of the graph (BENCH_r04)
+        assert tied == 509871915, tied
     print(f"C4 tied pairs: {tied} ({tied / (n * (n - 1)):.4f} of the pairs)")
 
 

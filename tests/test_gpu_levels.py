@@ -50,20 +50,24 @@ def _directed_dense(n, seed, wmax):
 
 
 @pytest.mark.parametrize("kind", ["complete300", "complete1000", "ties", "directed", "c1like",
-                                  "f64form", "manyrel"])
+                                  "f64form", "manyrel", "transposed", "ties_transposed"])
 def test_levels_match_oracle(gpu, monkeypatch, kind):
     """The post pass carries r(pred, t) as an index into the build's table of distinct arc
-    reliabilities (one packed word with the predecessor); "f64form" (SRT_FORM pk=0) and "manyrel"
-    (more distinct values than the table holds) take the f64 rows. "c1like" has distances past
-    64 quanta: its rows leave rel_tree_kernel for the sweeps."""
+    reliabilities: by default one source-major word per pair with the level beside it
+    (lvl_pkw_kernel + rel_pk_kernel); "transposed" (SRT_FORM pkw=0) keeps the target-major words,
+    the transpose and rel_tree_kernel; "f64form" (SRT_FORM pk=0) and "manyrel" (more distinct values
+    than the table holds) take the f64 rows. "c1like" has distances past 31 quanta: the packed
+    words cannot hold its levels (the transposed form, then the sweeps past 64)."""
     set_form(monkeypatch, levels="1")
     if kind == "f64form":
         set_form(monkeypatch, levels="1", pk="0")
-    if kind in ("complete300", "f64form"):
+    if kind in ("transposed", "ties_transposed"):
+        set_form(monkeypatch, levels="1", pkw="0")
+    if kind in ("complete300", "f64form", "transposed"):
         g = graphs.complete_graph(300, seed=7)
     elif kind == "complete1000":  # C2's distribution: distances up to 9 quanta
         g = graphs.complete_graph(1000, seed=2)
-    elif kind == "ties":  # 1-3 ms arcs: many equal-length paths (the canonical tie rule)
+    elif kind in ("ties", "ties_transposed"):  # 1-3 ms arcs: many equal-length paths
         g = graphs.complete_graph(640, seed=11, lat_max=3)
     elif kind == "directed":  # in-arcs from the columns of w
         g = _directed_dense(500, 5, 40)
@@ -157,3 +161,93 @@ def test_levels_sub_ms_path_order(gpu, monkeypatch):
     assert np.array_equal(lat_t, full["lat_int"])
     assert np.array_equal(rel, full["rel"])
     assert np.array_equal(ms, full["lat_ms"]), np.argwhere(ms != full["lat_ms"])[:5]
+
+
+def _virtual_dense(L, n, ld, ranks, seed, lat_max=1000):
+    """srt_dense_build_sharded on `ranks` virtual ranks of device 0 (row blocks generated on the
+    device); returns {row: (lat_ns, rel)} for every row and each rank's stats."""
+    import threading
+    import torch
+    comms = (ctypes.c_void_p * ranks)()
+    _lib.check(L.srt_comm_init_virtual(ranks, 0, comms), "srt_comm_init_virtual")
+    shards, bufs, streams = [], [], []
+    try:
+        for r in range(ranks):
+            b, e = ctypes.c_int32(), ctypes.c_int32()
+            L.srt_shard_rows(ld, 128, ranks, r, ctypes.byref(b), ctypes.byref(e))
+            b, e = b.value, e.value
+            w = torch.empty((e - b, ld), dtype=torch.int32, device="cuda")
+            rr = torch.empty((e - b, ld), dtype=torch.float64, device="cuda")
+            st = torch.cuda.Stream()
+            _lib.check(L.srt_gen_complete_device(n, ld, b, e - b, seed, lat_max, 10, 500,
+                                                 w.data_ptr(), rr.data_ptr(),
+                                                 ctypes.c_void_p(st.cuda_stream)), "generate")
+            shards.append((b, e))
+            bufs.append((w, rr, torch.empty_like(w), torch.empty_like(rr)))
+            streams.append(st)
+        torch.cuda.synchronize()
+        rcs = [None] * ranks
+        stats = [_lib.BuildStats() for _ in range(ranks)]
+
+        def work(r):
+            L.srt_virtual_rank_bind(r, 0)
+            w, rr, lat, rel = bufs[r]
+            rcs[r] = L.srt_dense_build_sharded(ctypes.c_void_p(comms[r]), n, ld, 0, w.data_ptr(),
+                                               rr.data_ptr(), lat.data_ptr(), rel.data_ptr(),
+                                               ctypes.c_void_p(streams[r].cuda_stream), 0,
+                                               ctypes.byref(stats[r]))
+            L.srt_virtual_rank_bind(-1, 0)
+
+        th = [threading.Thread(target=work, args=(r,)) for r in range(ranks)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        torch.cuda.synchronize()
+        for r in range(ranks):
+            _lib.check(rcs[r], f"rank {r}")
+        lat = np.concatenate([bufs[r][2].cpu().numpy() for r in range(ranks)])[:n, :n]
+        rel = np.concatenate([bufs[r][3].cpu().numpy() for r in range(ranks)])[:n, :n]
+    finally:
+        for r in range(ranks):
+            L.srt_comm_free(ctypes.c_void_p(comms[r]))
+    return lat.view(np.uint32).astype(np.uint64) * np.uint64(MS), rel, stats, shards
+
+
+def test_levels_uneven_shards_default_budget(gpu, monkeypatch):
+    """three virtual ranks with uneven row blocks (ld 4,096 = 32 tiles: 1,280 |
+    1,408 | 1,408 rows) and the default, unforced level budget. The budget is taken from global
+    quantities and agreed by a min all-reduce, so every rank takes the same path (no rank leaves for
+    Floyd-Warshall while its peers wait in a broadcast); every row against the oracle."""
+    monkeypatch.delenv("SRT_FORM", raising=False)
+    L = _lib.lib()
+    n = ld = 4096
+    glat, grel, stats, shards = _virtual_dense(L, n, ld, 3, seed=12)
+    assert len({e - b for b, e in shards}) > 1, shards
+    assert {int(s.dist_enc) for s in stats} == {LEVELS}, [int(s.dist_enc) for s in stats]
+    # one verdict for all ranks; each rank's own sources settle at their own last level
+    assert all(int(s.levels) >= 1 for s in stats), [int(s.levels) for s in stats]
+    rows = np.array([0, 1, 1279, 1280, 2000, 2687, 2688, 4095], np.int32)
+    clat, crel, _, _ = oracle.complete_sample(n, 12, 1000, 10, 500, rows, 8)
+    off = np.arange(n)[None, :] != rows[:, None]
+    assert np.array_equal(np.where(off, glat[rows], 0), np.where(off, clat, 0))
+    err = np.abs(grel[rows] - crel) / np.maximum(crel, 1e-300)
+    assert float(err[off].max()) <= REL_TOL
+
+
+def test_levels_memory_cap_falls_back(gpu, monkeypatch):
+    """the level planes are capped by the memory the device has left
+    (srt_levels_build: half of free + the scratch pool's unused bytes). SRT_FORM memcap (MiB, a
+    test hook) stands in for a nearly full device: the budget drops below two levels and the build
+    falls back to Floyd-Warshall instead of failing an allocation; the tables stay exact."""
+    set_form(monkeypatch, levels="1", memcap="0")
+    g = graphs.complete_graph(1000, seed=2)
+    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                algo=ALGO_DENSE_FW)
+    assert st.dist_enc != LEVELS and st.levels == 0, (st.dist_enc, st.levels)
+    _check(g, lat, rel, "memory-capped")
+    set_form(monkeypatch, levels="1", memcap="1")  # 1 MiB: 0.5 MiB of 128-KiB planes -> 4 levels
+    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                algo=ALGO_DENSE_FW)
+    assert st.levels <= 4, st.levels
+    _check(g, lat, rel, "memory-capped 1 MiB")

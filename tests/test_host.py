@@ -139,6 +139,27 @@ def test_attach_detach_lookup(native):
     assert not top.is_routable("11.0.0.9", "11.0.0.10")
 
 
+def test_ipmap_bounded_under_attach_detach_cycles(native):
+    """20,000 attach / detach cycles of fresh addresses leave the IP map at a
+    bounded number of tables (a rehash of a mostly-tombstone table keeps its capacity, and replaced
+    tables are reclaimed once no reader holds them), and lookups stay right throughout."""
+    from shadow_amd.topology import ip_to_net
+    top = Topology.from_gml(tri())
+    keep = [f"12.0.0.{i}" for i in range(1, 9)]
+    for ip in keep:
+        top.attach(ip, 1, None, None, None)
+    for i in range(20000):
+        ip = f"13.{(i >> 16) & 255}.{(i >> 8) & 255}.{i & 255}"
+        top.attach(ip, 1, None, None, None)
+        assert top.vertex_of(ip) >= 0
+        top.detach(ip)
+        assert top.vertex_of(ip) == -1
+    assert all(top.vertex_of(ip) >= 0 for ip in keep)
+    k = native.srt_topology_ipmap_tables(top._h)
+    assert 1 <= k <= 2, k
+    assert ip_to_net("12.0.0.1") != 0
+
+
 def _attach_world(rng, n):
     """Vertex attributes with duplicates, gaps and the special addresses the reference treats as
     unusable (0.0.0.0, 255.255.255.255, an unparsable string, and 1.0.0.127, whose network-order
