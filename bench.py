@@ -7,10 +7,15 @@ canonical predecessors, path-order reliabilities, the undirected symmetry rule a
 rule. value = whole-job node-pairs/s = n^2 * steps / (max over ranks of the timed region).
 
 Workloads:
-  c4 (default)  32,768-node complete graph, blocked Floyd-Warshall. The north-star config; it fits
-                one MI355X (w 4 GiB + r 8 GiB + lat 4 GiB + rel 8 GiB), so the same graph runs at
-                1/2/4/8 GPUs (strong scaling: rows sharded, pivot panels broadcast over RCCL).
-  c2            1,000-node complete graph (configs[1]), blocked Floyd-Warshall.
+  c4 (default)  32,768-node complete graph (configs[3]). The north-star config; it fits one
+                MI355X (w 4 GiB + r 8 GiB + lat 4 GiB + rel 8 GiB), so the same graph runs at
+                1/2/4/8 GPUs (strong scaling: rows sharded). Its distances end at 5 quanta, so the
+                build takes the bit-parallel Dial levels (dist_enc 12); graphs whose distances pass
+                the level budget take the blocked Floyd-Warshall (e.g. c4metric).
+  c4metric      32,768 points in the unit square, complete graph, latency max(1, round(300 *
+                dist)) ms (Tor-atlas-like metric latencies, distances of hundreds of ms): the
+                blocked Floyd-Warshall regime of the same n.
+  c2            1,000-node complete graph (configs[1]), min-plus squaring / blocked FW.
   c3            20,000-node random geometric graph (deg ~8), multi-source SSSP (configs[2]).
   c5            100,000-node Barabasi-Albert graph (m=3), source-sharded SSSP + ncclAllGather
                 (configs[4]); 120 GB of tables per GPU.
@@ -48,6 +53,11 @@ def _runtime():
 WORKLOADS = {
     "c4": dict(kind="dense", n=32768, seed=4, lat_max=1000, self_max=10, loss_max=500,
                desc="C4: 32768-node complete graph, latency U{1..1000} ms, loss U{0..500}e-4"),
+    "c4metric": dict(kind="dense", n=32768, seed=44, lat_max=0, metric=300, self_max=10,
+                     loss_max=500,
+                     desc="C4metric: 32768 points in the unit square, complete graph, latency "
+                          "max(1, round(300*dist)) ms, loss U{0..500}e-4 (Tor-atlas-like metric "
+                          "latencies)"),
     "c2": dict(kind="dense", n=1000, seed=2, lat_max=300, self_max=10, loss_max=500,
                desc="C2: 1000-node complete graph, latency U{1..300} ms, loss U{0..500}e-4"),
     "c3": dict(kind="sparse", n=20000, seed=3, gen="rgg",
@@ -245,7 +255,7 @@ def compare_rows(sample, n, glat, grel, clat, crel) -> dict:
 
 
 # ------------------------------------------------------------------------------------------
-# dense: blocked Floyd-Warshall (C2, C4)
+# dense: Dial levels or blocked Floyd-Warshall (C2, C4, C4metric)
 # ------------------------------------------------------------------------------------------
 def run_dense(c: Ctx, wl):
     L, world, rank = c.L, c.world, c.rank
@@ -260,9 +270,9 @@ def run_dense(c: Ctx, wl):
     r = torch.empty((max(nr, 1), ld), dtype=torch.float64, device=c.dev)
     lat = torch.empty_like(w)
     rel = torch.empty_like(r)
-    _lib.check(L.srt_gen_complete_device(n, ld, b, nr, wl["seed"], wl["lat_max"], wl["self_max"],
-                                         wl["loss_max"], w.data_ptr(), r.data_ptr(), c.sp),
-               "srt_gen_complete_device")
+    gen = L.srt_gen_metric_device if wl.get("metric") else L.srt_gen_complete_device
+    _lib.check(gen(n, ld, b, nr, wl["seed"], wl.get("metric") or wl["lat_max"], wl["self_max"],
+                   wl["loss_max"], w.data_ptr(), r.data_ptr(), c.sp), "generate")
     torch.cuda.synchronize()
 
     def step(stats):
@@ -411,11 +421,12 @@ def run_dense(c: Ctx, wl):
         if world == 1:
             one = np.array([17 % n], np.int32)
             _, _, _, t1 = oracle.complete_sample(n, wl["seed"], wl["lat_max"], wl["self_max"],
-                                                 wl["loss_max"], one, 1)
+                                                 wl["loss_max"], one, 1, metric=wl.get("metric", 0))
             k = int(max(2, min(64, c.args.cpu_seconds / max(t1, 1e-3))))
             srcs = np.unique(np.linspace(0, n - 1, k).astype(np.int32))
             _, _, gen_s, sssp_s = oracle.complete_sample(n, wl["seed"], wl["lat_max"],
-                                                         wl["self_max"], wl["loss_max"], srcs, 1)
+                                                         wl["self_max"], wl["loss_max"], srcs, 1,
+                                                         metric=wl.get("metric", 0))
             cpu = {"value": round(len(srcs) * n / sssp_s, 1), "unit": "node-pairs/s", "cores": 1,
                    "kind": "port",
                    "sample": f"{len(srcs)} of {n} sources, dense O(n^2) Dijkstra per source "
@@ -427,14 +438,16 @@ def run_dense(c: Ctx, wl):
             kk = int(max(nt, min(32 * nt, nt * c.args.cpu_seconds / 2 / max(t1, 1e-3))))
             msrcs = np.unique(np.linspace(0, n - 1, kk).astype(np.int32))
             _, _, _, mt_s = oracle.complete_sample(n, wl["seed"], wl["lat_max"], wl["self_max"],
-                                                   wl["loss_max"], msrcs, nt)
+                                                   wl["loss_max"], msrcs, nt,
+                                                   metric=wl.get("metric", 0))
             cpu["all_cores"] = {"value": round(len(msrcs) * n / mt_s, 1), "cores": nt,
                                 "sample": f"{len(msrcs)} of {n} sources over {nt} threads, "
                                           f"{mt_s:.1f} s (no graphLock: the reference cannot do "
                                           f"this)"}
         # full-size parity of the last build's rows against the oracle
         clat, crel, _, _ = oracle.complete_sample(n, wl["seed"], wl["lat_max"], wl["self_max"],
-                                                  wl["loss_max"], sample, cpu_threads())
+                                                  wl["loss_max"], sample, cpu_threads(),
+                                                  metric=wl.get("metric", 0))
         parity = compare_rows(sample, n, glat, grel, clat, crel)
     if parity is not None:
         parity.update({"tied_pairs": tied, "tied_frac": tied / float(n * (n - 1))})
@@ -467,11 +480,12 @@ def dense_cpu_and_parity(c: Ctx, wl, step, lat, rel):
         if world == 1:
             one = np.array([17 % n], np.int32)
             _, _, _, t1 = oracle.complete_sample(n, wl["seed"], wl["lat_max"], wl["self_max"],
-                                                 wl["loss_max"], one, 1)
+                                                 wl["loss_max"], one, 1, metric=wl.get("metric", 0))
             k = int(max(2, min(64, c.args.cpu_seconds / max(t1, 1e-3))))
             srcs = np.unique(np.linspace(0, n - 1, k).astype(np.int32))
             _, _, gen_s, sssp_s = oracle.complete_sample(n, wl["seed"], wl["lat_max"],
-                                                         wl["self_max"], wl["loss_max"], srcs, 1)
+                                                         wl["self_max"], wl["loss_max"], srcs, 1,
+                                                         metric=wl.get("metric", 0))
             cpu = {"value": round(len(srcs) * n / sssp_s, 1), "unit": "node-pairs/s", "cores": 1,
                    "kind": "port",
                    "sample": f"{len(srcs)} of {n} sources, dense O(n^2) Dijkstra per source "
@@ -482,13 +496,15 @@ def dense_cpu_and_parity(c: Ctx, wl, step, lat, rel):
             kk = int(max(nt, min(32 * nt, nt * c.args.cpu_seconds / 2 / max(t1, 1e-3))))
             msrcs = np.unique(np.linspace(0, n - 1, kk).astype(np.int32))
             _, _, _, mt_s = oracle.complete_sample(n, wl["seed"], wl["lat_max"], wl["self_max"],
-                                                   wl["loss_max"], msrcs, nt)
+                                                   wl["loss_max"], msrcs, nt,
+                                                   metric=wl.get("metric", 0))
             cpu["all_cores"] = {"value": round(len(msrcs) * n / mt_s, 1), "cores": nt,
                                 "sample": f"{len(msrcs)} of {n} sources over {nt} threads, "
                                           f"{mt_s:.1f} s (no graphLock: the reference cannot do "
                                           f"this)"}
         clat, crel, _, _ = oracle.complete_sample(n, wl["seed"], wl["lat_max"], wl["self_max"],
-                                                  wl["loss_max"], sample, cpu_threads())
+                                                  wl["loss_max"], sample, cpu_threads(),
+                                                  metric=wl.get("metric", 0))
         parity = compare_rows(sample, n, glat, grel, clat, crel)
     if parity is not None:
         parity.update({"tied_pairs": tied, "tied_frac": tied / float(n * (n - 1))})

@@ -175,6 +175,12 @@ int srt_dense_rows_build(int32_t n, int32_t ld, int32_t nsub, const int32_t* dve
 int srt_gen_complete_device(int32_t n, int32_t ld, int32_t row0, int32_t nrows, uint64_t seed,
                             uint32_t lat_max_ms, uint32_t self_max_ms, uint32_t loss_max_e4,
                             uint32_t* w, double* r, void* stream);
+/* the metric complete graph (Tor-atlas-like): n points of the unit square, latency
+ * max(1, round(scale_ms * dist)) ms (scale_ms <= 1024), loss and self-loops as above;
+ * oracle/oracle.c orc_metric_sample generates the same weights */
+int srt_gen_metric_device(int32_t n, int32_t ld, int32_t row0, int32_t nrows, uint64_t seed,
+                          uint32_t scale_ms, uint32_t self_max_ms, uint32_t loss_max_e4,
+                          uint32_t* w, double* r, void* stream);
 
 /* ---- device-resident sparse build (CSR of canonical arcs, self-loops excluded) ----------
  * Computes rows [src_begin, src_end) (row r of lat_rows/rel_rows = source src_begin + r, row

@@ -148,24 +148,36 @@ def table(g: EdgeList, use_shortest_path: bool = True, mode: int = ORC_INT_NS,
 
 
 def complete_sample(n: int, seed: int, lat_max: int, self_max: int, loss_max: int, sources,
-                    nthreads: int = 1):
-    """Dense Dijkstra rows of the synthetic complete graph for the given sources.
+                    nthreads: int = 1, metric: int = 0):
+    """Dense Dijkstra rows of the synthetic complete graph for the given sources (metric > 0: the
+    metric graph of scale `metric` ms instead of U{1..lat_max}).
     Returns (lat_ns [k,n] u64, rel [k,n] f64, matrix_gen_seconds, sssp_seconds)."""
     L = lib()
     if not hasattr(L, "_cs_set"):
-        L.orc_complete_sample.restype = ctypes.c_int
-        L.orc_complete_sample.argtypes = [ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32,
-                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
-                                          ctypes.c_int32, ctypes.c_int, ctypes.c_void_p,
-                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        for f in (L.orc_complete_sample, L.orc_metric_sample):
+            f.restype = ctypes.c_int
+            f.argtypes = [ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32,
+                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                          ctypes.c_int32, ctypes.c_int, ctypes.c_void_p,
+                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_dense_weight.restype = ctypes.c_uint32
+        L.orc_dense_weight.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
         L._cs_set = True
     src = np.ascontiguousarray(sources, dtype=np.int32)
     k = len(src)
     lat = np.empty((k, n), np.uint64)
     rel = np.empty((k, n), np.float64)
     gs, ss = ctypes.c_double(), ctypes.c_double()
-    rc = L.orc_complete_sample(n, seed, lat_max, self_max, loss_max, src.ctypes.data, k, nthreads,
-                               lat.ctypes.data, rel.ctypes.data, ctypes.byref(gs), ctypes.byref(ss))
+    fn, p = (L.orc_metric_sample, metric) if metric else (L.orc_complete_sample, lat_max)
+    rc = fn(n, seed, p, self_max, loss_max, src.ctypes.data, k, nthreads,
+            lat.ctypes.data, rel.ctypes.data, ctypes.byref(gs), ctypes.byref(ss))
     if rc:
         raise RuntimeError("orc_complete_sample failed")
     return lat, rel, gs.value, ss.value
+
+
+def dense_weight(seed: int, lat_max: int, metric: int, self_max: int, i: int, j: int) -> int:
+    """one weight (ms) of the synthetic dense generators (metric > 0: the metric graph)"""
+    complete_sample(1, 0, 1, 1, 0, [0])  # binds the signatures
+    return int(lib().orc_dense_weight(seed, lat_max, metric, self_max, i, j))

@@ -463,7 +463,29 @@ typedef struct {
     uint64_t seed;
     uint32_t lat_max, self_max;
     uint32_t* W;
+    uint32_t metric; /* 0: U{1..lat_max}; else the metric graph with scale `metric` ms */
 } genjob_t;
+
+/* The metric graph (bench workload c4metric; shadow_amd/csrc/dense.hip gen_metric_kernel restates
+ * it on the device): point i at 16-bit grid coordinates of the unit square, latency
+ * max(1, round(scale * dist)) ms with the rounding decided in exact integer arithmetic, so the two
+ * generators agree bit for bit: L = the largest L with ((2L - 1) 2^15)^2 <= scale^2 d2, where d2 is
+ * the squared grid distance (scale * sqrt(d2) / 2^16 >= L - 1/2). */
+static inline uint32_t metric_coord(uint64_t seed, uint32_t i, int axis) {
+    return (uint32_t)(ghash(seed, 0, i, 0xFFFFFFFFu - (uint32_t)axis) & 0xFFFFu);
+}
+static inline uint32_t metric_lat(uint64_t seed, uint32_t scale, uint32_t a, uint32_t b) {
+    const int64_t dx = (int64_t)metric_coord(seed, a, 0) - metric_coord(seed, b, 0);
+    const int64_t dy = (int64_t)metric_coord(seed, a, 1) - metric_coord(seed, b, 1);
+    const uint64_t d2 = (uint64_t)(dx * dx + dy * dy);
+    const uint64_t A = (uint64_t)scale * scale * d2;
+    uint64_t L = (uint64_t)((double)scale * sqrt((double)d2) / 65536.0 + 0.5);
+#define METRIC_F(L) (((2ull * (L) - 1ull) << 15) * ((2ull * (L) - 1ull) << 15))
+    while (L > 0 && METRIC_F(L) > A) L--;
+    while (METRIC_F(L + 1) <= A) L++;
+#undef METRIC_F
+    return L > 0 ? (uint32_t)L : 1u;
+}
 
 static void* gen_worker(void* a) {
     genjob_t* j = (genjob_t*)a;
@@ -471,8 +493,9 @@ static void* gen_worker(void* a) {
         for (int32_t k = 0; k < j->n; k++) {
             uint32_t x = i < k ? i : k, y = i < k ? k : i;
             j->W[(size_t)i * j->n + k] =
-                (x == y) ? 1u + (uint32_t)(ghash(j->seed, 2, x, x) % j->self_max)
-                         : 1u + (uint32_t)(ghash(j->seed, 0, x, y) % j->lat_max);
+                (x == y)    ? 1u + (uint32_t)(ghash(j->seed, 2, x, x) % j->self_max)
+                : j->metric ? metric_lat(j->seed, j->metric, x, y)
+                            : 1u + (uint32_t)(ghash(j->seed, 0, x, y) % j->lat_max);
         }
     return NULL;
 }
@@ -549,9 +572,39 @@ static void* dense_worker(void* a) {
     return NULL;
 }
 
+static int dense_sample(int32_t n, uint64_t seed, uint32_t lat_max, uint32_t metric,
+                        uint32_t self_max, uint32_t loss_max, const int32_t* sources, int32_t k,
+                        int nthreads, uint64_t* lat_out, double* rel_out, double* gen_seconds,
+                        double* sssp_seconds);
+
 int orc_complete_sample(int32_t n, uint64_t seed, uint32_t lat_max, uint32_t self_max,
                         uint32_t loss_max, const int32_t* sources, int32_t k, int nthreads,
                         uint64_t* lat_out, double* rel_out, double* gen_seconds,
+                        double* sssp_seconds) {
+    return dense_sample(n, seed, lat_max, 0, self_max, loss_max, sources, k, nthreads, lat_out,
+                        rel_out, gen_seconds, sssp_seconds);
+}
+
+int orc_metric_sample(int32_t n, uint64_t seed, uint32_t scale_ms, uint32_t self_max,
+                      uint32_t loss_max, const int32_t* sources, int32_t k, int nthreads,
+                      uint64_t* lat_out, double* rel_out, double* gen_seconds,
+                      double* sssp_seconds) {
+    if (scale_ms == 0 || scale_ms > 1024) return -1;
+    return dense_sample(n, seed, 0, scale_ms, self_max, loss_max, sources, k, nthreads, lat_out,
+                        rel_out, gen_seconds, sssp_seconds);
+}
+
+/* the weight of one pair of the generators (tests pin the device generator against it) */
+uint32_t orc_dense_weight(uint64_t seed, uint32_t lat_max, uint32_t metric, uint32_t self_max,
+                          uint32_t i, uint32_t j) {
+    const uint32_t x = i < j ? i : j, y = i < j ? j : i;
+    if (x == y) return 1u + (uint32_t)(ghash(seed, 2, x, x) % self_max);
+    return metric ? metric_lat(seed, metric, x, y) : 1u + (uint32_t)(ghash(seed, 0, x, y) % lat_max);
+}
+
+static int dense_sample(int32_t n, uint64_t seed, uint32_t lat_max, uint32_t metric,
+                        uint32_t self_max, uint32_t loss_max, const int32_t* sources, int32_t k,
+                        int nthreads, uint64_t* lat_out, double* rel_out, double* gen_seconds,
                         double* sssp_seconds) {
     if (n <= 0 || k <= 0 || !sources || !lat_out || !rel_out) return -1;
     uint32_t* W = (uint32_t*)malloc((size_t)n * (size_t)n * sizeof(uint32_t));
@@ -562,7 +615,7 @@ int orc_complete_sample(int32_t n, uint64_t seed, uint32_t lat_max, uint32_t sel
     genjob_t gj[64];
     for (int i = 0; i < gt; i++) {
         gj[i] = (genjob_t){n, (int32_t)((int64_t)n * i / gt), (int32_t)((int64_t)n * (i + 1) / gt),
-                           seed, lat_max, self_max, W};
+                           seed, lat_max, self_max, W, metric};
         pthread_create(&th[i], NULL, gen_worker, &gj[i]);
     }
     for (int i = 0; i < gt; i++) pthread_join(th[i], NULL);

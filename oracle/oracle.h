@@ -94,6 +94,14 @@ int orc_complete_sample(int32_t n, uint64_t seed, uint32_t lat_max, uint32_t sel
                         uint32_t loss_max, const int32_t* sources, int32_t k, int nthreads,
                         uint64_t* lat_out, double* rel_out, double* gen_seconds,
                         double* sssp_seconds);
+/* the same on the metric complete graph (points in the unit square, latency
+ * max(1, round(scale_ms * dist)) ms; bench workload c4metric) */
+int orc_metric_sample(int32_t n, uint64_t seed, uint32_t scale_ms, uint32_t self_max,
+                      uint32_t loss_max, const int32_t* sources, int32_t k, int nthreads,
+                      uint64_t* lat_out, double* rel_out, double* gen_seconds,
+                      double* sssp_seconds);
+uint32_t orc_dense_weight(uint64_t seed, uint32_t lat_max, uint32_t metric, uint32_t self_max,
+                          uint32_t i, uint32_t j);
 
 #ifdef __cplusplus
 }

@@ -92,6 +92,8 @@ SIGNATURES = {
     "srt_dense_rows_build": (ctypes.c_int, [_I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "srt_gen_complete_device": (ctypes.c_int, [_I32, _I32, _I32, _I32, _U64, _U32, _U32, _U32,
                                                 _VP, _VP, _VP]),
+    "srt_gen_metric_device": (ctypes.c_int, [_I32, _I32, _I32, _I32, _U64, _U32, _U32, _U32,
+                                              _VP, _VP, _VP]),
     "srt_sparse_max_n": (ctypes.c_int, []),
     "srt_sparse_build_device": (ctypes.c_int, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
                                                _VP, _VP, _I32, _I32, _U32, _VP, _VP, _VP, _VP]),

@@ -70,6 +70,63 @@ extern "C" int srt_gen_complete_device(int32_t n, int32_t ld, int32_t row0, int3
     return SRT_OK;
 }
 
+/* The metric complete graph (bench workload c4metric; oracle/oracle.c metric_lat restates it):
+ * point i at 16-bit grid coordinates of the unit square from the counter hash, latency
+ * max(1, round(scale * dist)) ms with the rounding settled in exact integers (a double estimate,
+ * corrected against ((2L - 1) 2^15)^2 <= scale^2 d2), loss and self-loops as gen_complete_kernel.
+ * Distances reach hundreds of quanta: past the level budget, the FW builds it (Tor-atlas regime). */
+static __device__ __forceinline__ uint32_t metric_coord(uint64_t seed, uint32_t i, int axis) {
+    return (uint32_t)(srt_hash(seed, 0, i, 0xFFFFFFFFu - (uint32_t)axis) & 0xFFFFu);
+}
+__global__ void gen_metric_kernel(int n, int ld, int row0, uint64_t seed, uint32_t scale,
+                                  uint32_t self_max, uint32_t loss_max, uint32_t* __restrict__ w,
+                                  double* __restrict__ r) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = row0 + blockIdx.y;
+    if (j >= ld) return;
+    const size_t ix = (size_t)blockIdx.y * ld + j;
+    if (i >= n || j >= n) {
+        w[ix] = SRT_INF;
+        r[ix] = 0.0;
+        return;
+    }
+    const uint32_t a = i < j ? i : j, b = i < j ? j : i;
+    uint32_t lat, k;
+    if (a == b) {
+        lat = 1u + (uint32_t)(srt_hash(seed, 2, a, a) % self_max);
+        k = (uint32_t)(srt_hash(seed, 3, a, a) % (loss_max + 1u));
+    } else {
+        const int64_t dx = (int64_t)metric_coord(seed, a, 0) - metric_coord(seed, b, 0);
+        const int64_t dy = (int64_t)metric_coord(seed, a, 1) - metric_coord(seed, b, 1);
+        const uint64_t d2 = (uint64_t)(dx * dx + dy * dy);
+        const uint64_t A = (uint64_t)scale * scale * d2;
+        uint64_t L = (uint64_t)((double)scale * sqrt((double)d2) / 65536.0 + 0.5);
+        auto f = [](uint64_t x) { return ((2ull * x - 1ull) << 15) * ((2ull * x - 1ull) << 15); };
+        while (L > 0 && f(L) > A) L--;
+        while (f(L + 1) <= A) L++;
+        lat = L > 0 ? (uint32_t)L : 1u;
+        k = (uint32_t)(srt_hash(seed, 1, a, b) % (loss_max + 1u));
+    }
+    w[ix] = lat;
+    r[ix] = 1.0 - (double)k / 10000.0;
+}
+
+extern "C" int srt_gen_metric_device(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
+                                     uint64_t seed, uint32_t scale_ms, uint32_t self_max_ms,
+                                     uint32_t loss_max_e4, uint32_t* w, double* r, void* stream) {
+    if (n <= 0 || n > 65535 || ld < n || ld % B || !w || !r || scale_ms == 0 || scale_ms > 1024 ||
+        self_max_ms == 0 || row0 < 0 || nrows < 0 || row0 + nrows > ld) {
+        srt_set_error("srt_gen_metric_device: bad arguments");
+        return SRT_E_ARG;
+    }
+    if (nrows == 0) return SRT_OK;
+    dim3 grid(srt_ceil_div(ld, 256), nrows);
+    gen_metric_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(n, ld, row0, seed, scale_ms,
+                                                             self_max_ms, loss_max_e4, w, r);
+    SRT_HIPCHK(hipGetLastError());
+    return SRT_OK;
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* D <- W with a zero diagonal and INF padding                                                */
 /* ------------------------------------------------------------------------------------------ */
@@ -1089,7 +1146,7 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
         if constexpr (PK) {
             const uint32_t t = (uint32_t)(tid + i * NT);
             const uint32_t hi = ((p & 0xFFFFu) == 0xFFFFu || t == (uint32_t)s || t >= (uint32_t)n)
-                                    ? (uint32_t)ntab : p >> 16;
+                                    ? (uint32_t)ntab : (p >> 16) & 0x7FFu; /* (level above) */
             stash[t] = (uint16_t)hi;
             p &= 0xFFFFu;
         }
@@ -1272,6 +1329,14 @@ __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int ro
     for (int k = 0; k < K; ++k) {
         const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rrow, tid * 16, k * NT * 16, 0);
         wd[k] = make_uint4(v.x, v.y, v.z, v.w);
+        /* targets past n (the row's padding) carry no word: a transpose leaves them as they were */
+        const int t4 = 4 * (tid + k * NT);
+        if (t4 + 3 >= n) {
+            if (t4 + 0 >= n) wd[k].x = 0xFFFFu;
+            if (t4 + 1 >= n) wd[k].y = 0xFFFFu;
+            if (t4 + 2 >= n) wd[k].z = 0xFFFFu;
+            if (t4 + 3 >= n) wd[k].w = 0xFFFFu;
+        }
     }
     __syncthreads(); /* par zeroed */
     uint32_t mx = 0;
@@ -1435,15 +1500,150 @@ static int rel_pk_launch(int n, int ld, int row0, int lrows, const uint32_t* pk,
     return SRT_OK;
 }
 
+/* Rows with deep predecessor trees (metric / Tor-atlas-like graphs: ~100 hops, hundreds of distinct
+ * distances, ~8k parents of 32k targets -- too deep for rel_tree_kernel's level passes, too many
+ * parents for its slots). rel_sweeps_kernel rescans the whole row once per tree level (C4metric:
+ * 221 ms). Here one wave owns a row: a counting sort of its targets by distance (every arc >= 1
+ * quantum, so a predecessor is strictly nearer: distance order is a topological order of the tree),
+ * then the targets in that order, 64 at a time, rel(s,t) = rel(s,pred) * r(pred,t) -- the
+ * left-to-right product of topology.c:1364-1365 -- with one dependent round trip per distance
+ * value present in a 64-entry chunk. The rel row arrives holding r(pred, t) (in place); the
+ * sorted list goes to `ord` (ld u32 per row: dist << 16 | t). Rows with a distance past
+ * ORD_NB - 1 stay flagged for the sweeps. */
+#define ORD_NB 1024
+#define ORD_WAVES 4
+template <typename PT>
+__global__ __launch_bounds__(64 * ORD_WAVES) void rel_order_kernel(int n, int ld, int row0, int lrows,
+                                                                   const uint32_t* __restrict__ d,
+                                                                   const PT* __restrict__ pred,
+                                                                   double* __restrict__ rel,
+                                                                   uint32_t* __restrict__ ord,
+                                                                   int32_t* __restrict__ only,
+                                                                   int32_t* __restrict__ max_depth) {
+    __shared__ uint32_t cnt_all[ORD_WAVES][ORD_NB];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    uint32_t* cnt = cnt_all[wv];
+    const int waves = (int)gridDim.x * ORD_WAVES;
+    for (int row = (int)blockIdx.x * ORD_WAVES + wv; row < lrows; row += waves) {
+        if (!only[row]) continue;
+        const int s = row0 + row;
+        const uint32_t* dr = d + (size_t)row * ld;
+        const PT* pr = pred + (size_t)row * ld;
+        double* rr = rel + (size_t)row * ld;
+        uint32_t* od = ord + (size_t)row * ld;
+        for (int i = lane; i < ORD_NB; i += 64) cnt[i] = 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        /* histogram of the reachable targets' distances (s itself and no-path entries left out) */
+        uint32_t mx = 0;
+        for (int t = lane; t < n; t += 64) {
+            const uint32_t x = dr[t];
+            if (t == s || x >= SRT_INF) continue;
+            mx = max(mx, x);
+            if (x < ORD_NB) atomicAdd(&cnt[x], 1u);
+        }
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        if (mx >= ORD_NB) continue; /* stays flagged: rel_sweeps_kernel */
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        /* exclusive prefix in place: lane l owns buckets [16 l, 16 l + 16) */
+        constexpr int PER = ORD_NB / 64;
+        uint32_t loc = 0;
+        for (int k = 0; k < PER; ++k) loc += cnt[lane * PER + k];
+        uint32_t inc = loc;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+            if (lane >= o) inc += y;
+        }
+        uint32_t run = inc - loc;
+        for (int k = 0; k < PER; ++k) {
+            const uint32_t c = cnt[lane * PER + k];
+            cnt[lane * PER + k] = run;
+            run += c;
+        }
+        const int total = (int)__shfl(inc, 63);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int t = lane; t < n; t += 64) {
+            const uint32_t x = dr[t];
+            if (t == s || x >= SRT_INF) continue;
+            const uint32_t pos = atomicAdd(&cnt[x], 1u);
+            od[pos] = (x << 16) | (uint32_t)t;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); /* the list, then read back */
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        /* the targets in distance order; inside a chunk, one step per distance value */
+        for (int base = 0; base < total; base += 64) {
+            const int i = base + lane;
+            const bool act = i < total;
+            const uint32_t e = act ? __hip_atomic_load(od + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                                   : 0xFFFFFFFFu;
+            const int t = (int)(e & 0xFFFFu);
+            const uint32_t dist = e >> 16;
+            int p = act ? (int)pr[t] : -1;
+            const double r = act ? rr[t] : 0.0;
+            uint32_t cur = act ? dist : 0xFFFFu;
+            for (int o = 32; o > 0; o >>= 1) cur = min(cur, (uint32_t)__shfl_xor((int)cur, o));
+            bool pend = act;
+            while (__any(pend)) {
+                if (pend && dist == cur) {
+                    /* p < 0 cannot happen on a reachable target of a validated graph: kept */
+                    const double ru = p == s ? 1.0
+                                    : p < 0  ? 1.0
+                                             : __hip_atomic_load(rr + p, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_store(rr + t, ru * r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    pend = false;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                uint32_t nx = pend ? dist : 0xFFFFu;
+                for (int o = 32; o > 0; o >>= 1) nx = min(nx, (uint32_t)__shfl_xor((int)nx, o));
+                cur = nx;
+            }
+        }
+        if (lane == 0) {
+            __hip_atomic_store(rr + s, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            only[row] = 0;
+            atomicMax(max_depth, (int)mx);
+        }
+    }
+}
+
 /* Path-order reliability of lrows rows whose rel rows hold r(pred, t) (pred rows beside them):
  * rel_tree_kernel for n <= 32768 (rel_levels_kernel past it, or under SRT_FORM reltree=0), then
  * the sweeps for the rows it flagged. depth, sweep: device scratch (max depth, per-row flags). */
+/* the rows rel_tree_kernel handed over (sweep[row] != 0) through rel_order_kernel first: the
+ * sweeps then see only rows with distances past ORD_NB - 1 */
+template <typename PT>
+static int rel_order_launch(int n, int ld, int row0, int lrows, const uint32_t* d, const PT* pred,
+                            double* rel, uint32_t* ord, int32_t* sweep, int32_t* depth,
+                            hipStream_t st) {
+    if (!ord || !d || lrows <= 0 || n > 65535) return SRT_OK;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetLastError();
+    const int grid = min(srt_ceil_div(lrows, ORD_WAVES), cus * 8);
+    rel_order_kernel<PT><<<grid, 64 * ORD_WAVES, 0, st>>>(n, ld, row0, lrows, d, pred, rel, ord,
+                                                          sweep, depth);
+    SRT_HIPCHK(hipGetLastError());
+    return SRT_OK;
+}
+
 static int rel_rows_launch(int n, int ld, int row0, int lrows, const uint32_t* d, int32_t* pred,
                            double* rel, int32_t* depth, int32_t* sweep, const int32_t* srcs,
                            hipStream_t st, const uint8_t* l8 = nullptr,
                            const int16_t* pred16 = nullptr, const uint32_t* pk = nullptr,
-                           const double* rtab = nullptr, int ntab = 0) {
+                           const double* rtab = nullptr, int ntab = 0, uint32_t* ord = nullptr) {
     if (lrows <= 0) return SRT_OK;
+    int rc;
     const bool tree = n <= 32768 && srt_form_int("reltree", 1) != 0;
     if (pk) { /* a level build's u8 rows and packed (predecessor | reliability index) rows */
         rel_tree_launch(n, ld, row0, lrows, l8, pk, rel, depth, sweep, srcs, st, rtab, ntab);
@@ -1489,6 +1689,10 @@ static int rel_rows_launch(int n, int ld, int row0, int lrows, const uint32_t* d
                                                                   depth, sweep, srcs);
     }
     SRT_HIPCHK(hipGetLastError());
+    /* deep rows (distance range past the level passes' 64): distance order, one wave per row */
+    if (tree && !srcs && !l8 &&
+        (rc = rel_order_launch<int32_t>(n, ld, row0, lrows, d, pred, rel, ord, sweep, depth, st)))
+        return rc;
     if (n <= 32768) {
         const size_t lds = (size_t)n * sizeof(int32_t) + 2 * (size_t)((n + 31) / 32) * 4;
         SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_sweeps_kernel<int32_t>,
@@ -1820,8 +2024,11 @@ static int dense_post(int32_t n, int32_t ld, int32_t row0, int32_t nrows, int32_
             n, nrows, ws->rt, (size_t)nrows, rel, (size_t)ld);
         /* level order for rows whose distances span <= 64 quanta, sweeps for the rest
          * (ws->cursor is free here and carries the per-row hand-over flags) */
+        /* the target-major predecessors (predt) are free after the transpose: the order kernel's
+         * per-row lists */
         if ((rc = rel_rows_launch(n, ld, row0, lrows, d, pred, rel, ws->depth, ws->cursor, nullptr,
-                                  st)))
+                                  st, nullptr, nullptr, nullptr, nullptr, 0,
+                                  reinterpret_cast<uint32_t*>(ws->predt))))
             return rc;
     }
     if (stats && nowait) { /* read after the build's final wait (dense_collect_total) */
@@ -1854,9 +2061,22 @@ static int dense_post_levels(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
         const double* rtab = srt_levels_rtab(&ntab);
         if (stats) stats->rel_table = ntab;
         uint32_t* pk = reinterpret_cast<uint32_t*>(ws->dt);
+        const int mode = srt_levels_pkw_ready();
         if (kt) SRT_HIPCHK(hipEventRecord(ws->kev[0], st));
-        if ((rc = srt_levels_pkw(pk, ld, ties ? ws->ties : NULL, st))) return rc;
+        if (mode == 1) {
+            if ((rc = srt_levels_pkw(pk, ld, ties ? ws->ties : NULL, st))) return rc;
+        } else { /* target-major packed words (with the level), then one u32 transpose */
+            size_t c2 = ws->predt_cap;
+            if ((rc = ws_grow((void**)&ws->predt, &c2, slab, sizeof(int32_t)))) return rc;
+            ws->predt_cap = c2;
+            if ((rc = srt_levels_pred(ws->predt, 2, nullptr, (size_t)nrows, ties ? ws->ties : NULL,
+                                      st)))
+                return rc;
+        }
         if (kt) SRT_HIPCHK(hipEventRecord(ws->kev[1], st));
+        if (mode != 1)
+            transpose_kernel<uint32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+                n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows, pk, (size_t)ld);
         ws->pred16 = 2; /* dense_path_ms reads the packed words' low half */
         SRT_HIPCHK(hipMemsetAsync(ws->depth, 0, sizeof(int32_t), st));
         if (kt) SRT_HIPCHK(hipEventRecord(ws->kev[2], st));

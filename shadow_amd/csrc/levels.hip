@@ -295,7 +295,7 @@ __global__ void lvl_init_kernel(int n, int src0, int nsrc, int nw, uint32_t* __r
 /* Level d: one wave per (target j, 64-word source chunk c). Units are handed out XCD-major (each
  * XCD takes a contiguous run of chunk-major units), so an XCD works on one source chunk at a time
  * and the Delta rows of that chunk are the only gathered data in its L2. */
-static __device__ __forceinline__ void lvl_step_unit(unsigned g, int d, int n, int nw, int nchunk,
+static __device__ __forceinline__ uint32_t lvl_step_unit(unsigned g, int d, int n, int nw, int nchunk,
                                                      int src0, int nsrc,
                                                        const int32_t* __restrict__ off,
                                                        const uint32_t* __restrict__ arcs,
@@ -309,7 +309,7 @@ static __device__ __forceinline__ void lvl_step_unit(unsigned g, int d, int n, i
     /* the wave index through readfirstlane: j is then wave-uniform to the compiler, so the offsets
      * and the arcs come through scalar loads and every gather's row address is an SGPR */
     const int j = (int)(g % (unsigned)tgrp) * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    if (c >= nchunk || j >= n) return;
+    if (c >= nchunk || j >= n) return 0u;
     const int lane = threadIdx.x & 63, word = c * 64 + lane;
     const bool valid = word < nw;
     const size_t plane = (size_t)n * nw; /* words per level */
@@ -317,7 +317,7 @@ static __device__ __forceinline__ void lvl_step_unit(unsigned g, int d, int n, i
     const size_t u = (size_t)j * nchunk + c;
     if (done[u]) {
         if (valid) *out = 0u;
-        return;
+        return 0u;
     }
     uint32_t acc = 0;
     const int32_t* oj = off + (size_t)j * LVL_STRIDE;
@@ -361,10 +361,12 @@ static __device__ __forceinline__ void lvl_step_unit(unsigned g, int d, int n, i
     }
     if (!valid) acc = 0;
     bool inc = false;
+    uint32_t settled = 0;
     if (valid) {
         uint32_t* rp = R + (size_t)j * nw + word;
         const uint32_t r = *rp;
         const uint32_t nb = acc & ~r;
+        settled = (uint32_t)__builtin_popcount(nb);
         *out = nb;
         if (nb) *rp = r | nb;
         /* sources past n (padding of the last shard) never appear: they count as settled */
@@ -382,6 +384,7 @@ static __device__ __forceinline__ void lvl_step_unit(unsigned g, int d, int n, i
         else if (!__hip_atomic_load(incomplete, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
             __hip_atomic_store(incomplete, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    return settled;
 }
 
 /* Persistent grid (a few workgroups per CU, each looping over unit blocks): the units live only a
@@ -397,14 +400,23 @@ __global__ __launch_bounds__(256) void lvl_step_kernel(int d, int n, int nw, int
                                                        uint32_t* __restrict__ R,
                                                        uint8_t* __restrict__ done,
                                                        int* __restrict__ incomplete,
-                                                       const int* __restrict__ prev) {
+                                                       const int* __restrict__ prev,
+                                                       unsigned long long* __restrict__ nset) {
     /* the levels are enqueued in batches without a host round trip per level: a level whose
      * predecessor settled every pair (prev == 0) has nothing to do */
     if (prev && !__hip_atomic_load(prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     const unsigned x = blockIdx.x & 7u, per = nblk >> 3, L = gridDim.x >> 3;
+    uint32_t settled = 0; /* pairs this lane settled (one add per block at the end) */
     for (unsigned u = blockIdx.x >> 3; u < per; u += L)
-        lvl_step_unit(x * per + u, d, n, nw, nchunk, src0, nsrc, off, arcs, aoff, lev, R, done,
-                      incomplete);
+        settled += lvl_step_unit(x * per + u, d, n, nw, nchunk, src0, nsrc, off, arcs, aoff, lev, R,
+                                 done, incomplete);
+    unsigned long long c = settled;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    __shared__ unsigned long long s_c[4];
+    if ((threadIdx.x & 63) == 0) s_c[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0 && (s_c[0] | s_c[1] | s_c[2] | s_c[3]))
+        atomicAdd(nset, s_c[0] + s_c[1] + s_c[2] + s_c[3]);
 }
 
 /* Distance rows of the local sources from the levels: the u32 table rows (SRT_INF on padding) and
@@ -581,8 +593,16 @@ static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx
             nb &= nb - 1u;
         }
     };
+    /* PK: the level of each of the lane's 32 sources as five bit planes (level <= 31), so the
+     * packed word carries it (pred | rix << 16 | level << 27) for rel_pk_kernel */
+    uint32_t lvb[5] = {0u, 0u, 0u, 0u, 0u};
     for (int d = 1; d <= nlev; ++d) {
         uint32_t pend = valid ? lev[(size_t)(d - 1) * plane + (size_t)t * nw + word] : 0u;
+        if constexpr (PK) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+                if ((d >> k) & 1) lvb[k] |= pend;
+        }
         if (!__any(pend != 0u)) continue;
         for (int w = d; w >= 1; --w) {
             const int g0 = ot[w], g1 = ot[w + 1];
@@ -636,6 +656,9 @@ static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx
                     for (int q = 0; q < LVL_PB; ++q) take(v[q] & pend, H, T, i + q);
 #pragma unroll
                     for (int q = 0; q < LVL_PB; ++q) v[q] = vn[q];
+                    /* without the tie count the first tight arc is all a source needs: the walk
+                     * of the weight ends once every pending source has one */
+                    if (!ties && !__any((pend & ~H) != 0u)) break;
                 }
 
             }
@@ -659,6 +682,12 @@ static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int sl0 = cs0 + q * 512 + lane * 8;
+        /* the levels of sources sl0 .. sl0 + 7: bits (lane & 3) * 8.. of word q * 16 + lane / 4,
+         * which lane q * 16 + lane / 4 holds (every lane takes part in the shuffles) */
+        uint32_t lq[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            lq[k] = PK ? ((uint32_t)__shfl((int)lvb[k], q * 16 + (lane >> 2)) >> ((lane & 3) * 8)) : 0u;
         if (sl0 >= nsrc) continue; /* nsrc is a multiple of 128: whole groups of 8 */
         const uint4 raw =
             *reinterpret_cast<const uint4*>(&sidx[wv][(q * 16 + (lane >> 2)) * 40 + (lane & 3) * 8]);
@@ -673,8 +702,13 @@ static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx
             const bool h = sg < n && sg != t && x != 0xFFFFu;
             const int k = a_t + (h ? (int)x : 0);
             pv[e] = h ? (int)(arcs[k] & 0xFFFFu) : -1;
-            if constexpr (PK)
-                kv[e] = ((uint32_t)pv[e] & 0xFFFFu) | (h ? (uint32_t)rix[k] << 16 : 0u);
+            if constexpr (PK) {
+                uint32_t l = 0;
+#pragma unroll
+                for (int kk = 0; kk < 5; ++kk) l |= ((lq[kk] >> e) & 1u) << kk;
+                kv[e] = ((uint32_t)pv[e] & 0xFFFFu) | (h ? (uint32_t)rix[k] << 16 : 0u) |
+                        (h ? l << 27 : 0u);
+            }
             else
                 rv[e] = h ? ar[k] : 0.0;
         }
@@ -730,13 +764,13 @@ __global__ __launch_bounds__(256) void lvl_pred_kernel(int n, int nw, int nchunk
 #define LVL_PKW_CW 16 /* source words per target group: 64 B per gathered arc */
 #endif
 #ifndef LVL_PKW_PB
-#define LVL_PKW_PB 12 /* gathers per lane and batch */
+#define LVL_PKW_PB 8 /* gathers per lane and batch */
 #endif
 #ifndef LVL_PKW_W
-#define LVL_PKW_W 4 /* waves per workgroup */
+#define LVL_PKW_W 8 /* waves per workgroup */
 #endif
 #ifndef LVL_PKW_WAVE
-#define LVL_PKW_WAVE 1 /* 1: every wave on its own units (lvl_pkw_wave_kernel) */
+#define LVL_PKW_WAVE 0 /* 1: every wave on its own units (lvl_pkw_wave_kernel) */
 #endif
 /* ---- predecessor words, source-major, with the level (round 5) ---------------------------------
  * The same canonical rule as lvl_pred_kernel, on a unit shape that keeps the gathered plane slices
@@ -878,8 +912,10 @@ __global__ __launch_bounds__(64 * NWV) void lvl_pkw_kernel(int n, int ld, int nw
          * most among a take step's stores; 4-aligned groups stay whole for the write-out) */
         const int tcol = tl ^ (((p & 7) << 2) & (TT - 1));
         const int cs0 = src0 + c * S; /* global index of the chunk's first source */
+#if !defined(LVL_PKW_DIAG) || LVL_PKW_DIAG != 2
         pkw_walk<CW, PB, TIES>(t, tv, valid, word, g, p, cs0, n, nw, nlev, off, arcw, lev, tile,
                                [&](int r) { return r * TT + tcol; }, tied);
+#endif
         __syncthreads();
         /* write-out: source row r of the chunk, TT x 4 B from column tb * TT */
         constexpr int GPR = TT / 4; /* 16-B pieces per row */
@@ -889,6 +925,9 @@ __global__ __launch_bounds__(64 * NWV) void lvl_pkw_kernel(int n, int ld, int nw
             if (sl >= nsrc) break; /* rows are in order: the rest are past too */
             const int col = (4 * a4) ^ ((((r >> 5) & 7) << 2) & (TT - 1));
             const uint4 val = *reinterpret_cast<const uint4*>(&tile[r * TT + col]);
+#if defined(LVL_PKW_DIAG) && LVL_PKW_DIAG == 1
+            if (val.x != 0x12345678u) continue; /* timing diagnostic: no write-out */
+#endif
             uint32_t* o = pk + (size_t)sl * ld + (size_t)tb * TT + 4 * a4;
             __builtin_nontemporal_store(val.x, o);
             __builtin_nontemporal_store(val.y, o + 1);
@@ -1137,6 +1176,8 @@ static size_t lvl_avail_bytes(void) {
 /* levels enqueued per host round trip: a batch's levels past the one that settles every pair
  * return at once (lvl_step_kernel's prev test) */
 #define LVL_BATCH 8
+/* settled fraction of the local pairs the first batch must reach for the build to go on */
+#define LVL_MIN_SETTLED 0.25
 
 /* One build of the local rows' distances (nrows x ld). comm (NULL on one GPU): undirected row
  * shards, every rank sees every target's in-arcs after the segment broadcasts. fw_ms: the
@@ -1331,8 +1372,14 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     unsigned nblk = (unsigned)(((n + 3) / 4) * nchunk);
     nblk = (nblk + 7u) & ~7u;
     const unsigned pgrid = lvl_grid((const void*)lvl_step_kernel, nblk);
-    /* the levels in batches of LVL_BATCH, one host round trip per batch */
+    /* the levels in batches of LVL_BATCH, one host round trip per batch. After the first batch
+     * the settled fraction decides whether the rest is worth it: a graph with far-apart vertices
+     * (metric latencies, C4metric: 0.2% settled after 8 levels, distances of hundreds of quanta)
+     * goes to the FW at once instead of spending its whole budget first (77 ms there) */
     int D = 0, hflag[2] = {0, 0};
+    unsigned long long* nset = reinterpret_cast<unsigned long long*>(dagree + 4);
+    const int lsrc = min(nrows, max(0, n - row0)); /* the local sources (rows past n are padding) */
+    const double pairs = (double)n * (double)lsrc;
     const int ev0 = evp ? evp->used : 0;
     if (evp && (rc = evpool_reserve(evp, ev0 + 2 * lmax))) return rc;
     for (int d0 = 1; d0 <= lmax && !D; d0 += LVL_BATCH) {
@@ -1341,17 +1388,24 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
             lvl_step_kernel<<<pgrid, 256, 0, st>>>(d, n, nw, nchunk, row0, nrows, nblk, off, arcs,
                                                   aoff, lev, Rb, done, dinc + d,
-                                                  d > 1 ? dinc + d - 1 : NULL);
+                                                  d > 1 ? dinc + d - 1 : NULL, nset);
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
         }
         SRT_HIPCHK(hipGetLastError());
         int inc[LVL_BATCH];
+        unsigned long long settled = 0;
         SRT_HIPCHK(hipMemcpyAsync(inc, dinc + d0, sizeof(int) * (d1 - d0 + 1), hipMemcpyDeviceToHost,
                                   st));
         SRT_HIPCHK(hipMemcpyAsync(hflag, dflag, sizeof(hflag), hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipMemcpyAsync(&settled, nset, sizeof(settled), hipMemcpyDeviceToHost, st));
         SRT_HIPCHK(hipStreamSynchronize(st));
         for (int d = d0; d <= d1 && !D; ++d)
             if (inc[d - d0] == 0) D = d;
+        /* every source's own vertex counts as settled at level 0 (n - row0 of them are local) */
+        const double frac = pairs > 0 ? ((double)settled + (double)lsrc) / pairs : 1.0;
+        /* (a forced level build, fw_ms = 1e30 from SRT_FORM levels=1, runs its whole budget) */
+        if (!D && d0 == 1 && d1 < lmax && frac < LVL_MIN_SETTLED && fw_ms < 1e29)
+            break; /* -> Floyd-Warshall */
     }
     if (evp && D) evp->used = ev0 + 2 * D; /* the levels that did work */
     int64_t gathered = 0;
@@ -1370,7 +1424,10 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         rix = NULL, rtab = NULL; /* (freed with the state) */
     /* the fused post pass (srt_levels_pkw) writes the u32 rows itself: the table of distinct arc
      * reliabilities, 5-bit levels and u16 vertices (n <= 32768) */
-    const int pkw = rix && D <= 31 && n <= 32768 && srt_form_int("pkw", 1) != 0;
+    /* 2: the walk of lvl_pred_kernel (target-major packed words with the level), one transpose;
+     * 1: lvl_pkw_kernel (source-major words from an LDS tile); both then rel_pk_kernel, which
+     * writes the u32 rows too; 0: lvl_out8 rows + rel_tree_kernel (and past the packed form) */
+    const int pkw = rix && D <= 31 && n <= 32768 ? srt_form_int("pkw", 2) : 0;
     uint8_t* l8 = NULL;
     if (!pkw) {
         LVL_ALLOC(l8, (size_t)nrows * ld);
@@ -1412,10 +1469,11 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     return SRT_OK;
 }
 
-/* 1 when the held build's post pass is srt_levels_pkw + the packed reliability pass */
+/* the held build's packed-word post pass: 0 none, 1 srt_levels_pkw, 2 srt_levels_pred packed
+ * with levels + a transpose; rel_pk_kernel after either */
 int srt_levels_pkw_ready(void) {
     const lvl_state* L = &g_lvl[srt_state_slot()];
-    return L->held && L->pkw;
+    return L->held ? L->pkw : 0;
 }
 
 /* Source-major packed words of the held build (lvl_pkw_kernel): pk[sl][t] (row stride ld, nrows

@@ -50,15 +50,17 @@ typedef struct ipmap_tab {
 } ipmap_tab;
 
 #define IPM_STRIPES 64
+/* one reader count per 128 B (two cache lines: no false sharing through the adjacent-line
+ * prefetch either); the array is allocated 128-B aligned on first use (ipm_stripes) */
 typedef struct {
     _Atomic long n;
-    char pad[64 - sizeof(long)];
+    char pad[128 - sizeof(long)];
 } ipm_stripe;
 
 typedef struct {
     _Atomic(ipmap_tab*) cur;
     ipmap_tab* retired; /* replaced tables not yet known to be unread */
-    ipm_stripe rd[IPM_STRIPES];
+    ipm_stripe* rd;     /* IPM_STRIPES reader counts (set before the first table is published) */
 } ipmap_t;
 
 #define IPM_EMPTY 0xFFFFFFFFull /* value -1 */
@@ -103,6 +105,11 @@ static void ipm_free_list(ipmap_tab* t) {
 
 /* caller holds ip_lock (writer) */
 static int ipmap_put(ipmap_t* m, uint32_t k, int32_t v) {
+    if (!m->rd) { /* before any table exists: no reader can be counting yet */
+        m->rd = (ipm_stripe*)aligned_alloc(128, sizeof(ipm_stripe) * IPM_STRIPES);
+        if (!m->rd) return -1;
+        for (int i = 0; i < IPM_STRIPES; i++) atomic_init(&m->rd[i].n, 0);
+    }
     ipmap_tab* t = atomic_load_explicit(&m->cur, memory_order_relaxed);
     if (!t || (t->used + 1) * 2 > t->cap) { /* grow, or drop the tombstones: a new table */
         size_t live = 0;
@@ -159,6 +166,7 @@ static int ipmap_put(ipmap_t* m, uint32_t k, int32_t v) {
 /* no lock: count this reader in its stripe, one load of the table, then of each probed slot */
 static int32_t ipmap_get(const ipmap_t* cm, uint32_t k) {
     ipmap_t* m = (ipmap_t*)cm;
+    if (!atomic_load_explicit(&m->cur, memory_order_acquire)) return -1; /* (rd set before cur) */
     _Atomic long* rd = &m->rd[ipm_stripe_of_thread()].n;
     atomic_fetch_add_explicit(rd, 1, memory_order_seq_cst);
     const ipmap_tab* t = atomic_load_explicit(&m->cur, memory_order_seq_cst);
@@ -201,6 +209,8 @@ static void ipmap_free(ipmap_t* m) {
     free(atomic_load(&m->cur));
     ipm_free_list(m->retired);
     m->retired = NULL;
+    free(m->rd);
+    m->rd = NULL;
 }
 
 /* the tables an ipmap holds (live + retired), for the growth test */
