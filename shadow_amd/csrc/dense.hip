@@ -1619,6 +1619,160 @@ __global__ __launch_bounds__(64 * ORD_WAVES) void rel_order_kernel(int n, int ld
 /* Path-order reliability of lrows rows whose rel rows hold r(pred, t) (pred rows beside them):
  * rel_tree_kernel for n <= 32768 (rel_levels_kernel past it, or under SRT_FORM reltree=0), then
  * the sweeps for the rows it flagged. depth, sweep: device scratch (max depth, per-row flags). */
+/* Deep rows, parents only (rel_pk_kernel's idea on the FW path's int32 predecessor rows): only the
+ * parents' values must be readable by other targets, and a metric row has ~8k of them among 32k
+ * targets. One workgroup per row:
+ *   A. the row's predecessors, coalesced: the parent bitmap (LDS atomics), its prefix ranks;
+ *   B. the parents' own (distance, predecessor, r(pred, t)) into rank slots, a histogram of their
+ *      distances, and a counting sort of the slots by distance;
+ *   C. the parents' values in distance order (every arc >= 1 quantum: a parent's predecessor is a
+ *      nearer parent), one barrier per distance present, LDS only;
+ *   D. every target once, coalesced: rel(s,t) = rel(s,pred) * r(pred,t) from the slots -- the
+ *      left-to-right product of topology.c:1364-1365.
+ * 24 B of HBM per pair (d and pred twice, r in, rel out) and no scattered global access. Rows with
+ * more parents than the cap (or distances past DEEP_NB - 1) stay flagged for rel_order_kernel. */
+#define DEEP_NT 512
+#define DEEP_NB 1024
+__global__ __launch_bounds__(DEEP_NT) void rel_deep_kernel(int n, int ld, int row0, int lrows,
+                                                           const uint32_t* __restrict__ d,
+                                                           const int32_t* __restrict__ pred,
+                                                           double* __restrict__ rel, int cap,
+                                                           int32_t* __restrict__ only,
+                                                           int32_t* __restrict__ max_depth) {
+    const int row = blockIdx.x;
+    if (row >= lrows || !only[row]) return;
+    const int s = row0 + row, tid = threadIdx.x, lane = tid & 63;
+    const int nwb = ld >> 5;
+    extern __shared__ __attribute__((aligned(16))) uint32_t dsm[];
+    uint32_t* par = dsm;                                       /* parent bitmap (nwb words) */
+    uint32_t* pre = dsm + nwb;                                 /* parents before each word */
+    uint32_t* hist = dsm + 2 * nwb;                            /* DEEP_NB bucket offsets */
+    double* pval = reinterpret_cast<double*>(hist + DEEP_NB);  /* cap values (r(pred,t) first) */
+    uint16_t* pp = reinterpret_cast<uint16_t*>(pval + cap);    /* the slot's predecessor */
+    uint16_t* pd = pp + cap;                                   /* the slot's distance */
+    uint16_t* ord = pd + cap;                                  /* slots in distance order */
+    __shared__ uint32_t wsum[DEEP_NT / 64], red[DEEP_NT / 64];
+    const uint32_t* dr = d + (size_t)row * ld;
+    const int32_t* pr = pred + (size_t)row * ld;
+    double* rr = rel + (size_t)row * ld;
+    for (int q = tid; q < nwb; q += DEEP_NT) par[q] = 0u;
+    for (int q = tid; q < DEEP_NB; q += DEEP_NT) hist[q] = 0u;
+    __syncthreads();
+    /* A */
+    uint32_t mx = 0;
+    for (int t = tid; t < n; t += DEEP_NT) {
+        const uint32_t x = dr[t];
+        const int p = pr[t];
+        if (t == s || x >= SRT_INF || p < 0) continue;
+        mx = max(mx, x);
+        if (p != s) atomicOr(&par[p >> 5], 1u << (p & 31));
+    }
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    if (lane == 0) red[tid >> 6] = mx;
+    __syncthreads();
+    mx = 0;
+    for (int i = 0; i < DEEP_NT / 64; ++i) mx = max(mx, red[i]);
+    const int wpt = (nwb + DEEP_NT - 1) / DEEP_NT;
+    uint32_t c = 0;
+    for (int i = 0; i < wpt; ++i) {
+        const int q = tid * wpt + i;
+        if (q < nwb) c += (uint32_t)__popc(par[q]);
+    }
+    uint32_t inc = c;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) wsum[tid >> 6] = inc;
+    __syncthreads();
+    uint32_t base = 0, total = 0;
+    for (int i = 0; i < DEEP_NT / 64; ++i) {
+        base += i < (tid >> 6) ? wsum[i] : 0u;
+        total += wsum[i];
+    }
+    uint32_t run = base + inc - c;
+    for (int i = 0; i < wpt; ++i) {
+        const int q = tid * wpt + i;
+        if (q < nwb) {
+            pre[q] = run;
+            run += (uint32_t)__popc(par[q]);
+        }
+    }
+    if (total > (uint32_t)cap || mx >= DEEP_NB) return; /* uniform: stays flagged */
+    __syncthreads();
+    auto rank = [&](uint32_t u) {
+        return pre[u >> 5] + (uint32_t)__popc(par[u >> 5] & ((1u << (u & 31)) - 1u));
+    };
+    /* B: the parents' own entries (every parent is a reachable target: its own predecessor is
+     * s or another parent) */
+    for (int t = tid; t < n; t += DEEP_NT) {
+        if (!((par[t >> 5] >> (t & 31)) & 1u)) continue;
+        const uint32_t k = rank((uint32_t)t);
+        const uint32_t x = dr[t];
+        pd[k] = (uint16_t)x;
+        pp[k] = (uint16_t)pr[t];
+        pval[k] = rr[t];
+        atomicAdd(&hist[x], 1u);
+    }
+    __syncthreads();
+    /* exclusive prefix of the distance histogram (DEEP_NB / DEEP_NT buckets per thread) */
+    {
+        constexpr int PB = DEEP_NB / DEEP_NT;
+        uint32_t loc = 0, v[PB];
+#pragma unroll
+        for (int k = 0; k < PB; ++k) loc += (v[k] = hist[tid * PB + k]);
+        uint32_t in2 = loc;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)in2, o);
+            if (lane >= o) in2 += y;
+        }
+        __syncthreads(); /* wsum reuse */
+        if (lane == 63) wsum[tid >> 6] = in2;
+        __syncthreads();
+        uint32_t b2 = 0;
+        for (int i = 0; i < (tid >> 6); ++i) b2 += wsum[i];
+        uint32_t r2 = b2 + in2 - loc;
+#pragma unroll
+        for (int k = 0; k < PB; ++k) {
+            hist[tid * PB + k] = r2;
+            r2 += v[k];
+        }
+    }
+    __syncthreads();
+    for (int k = tid; k < (int)total; k += DEEP_NT) ord[atomicAdd(&hist[pd[k]], 1u)] = (uint16_t)k;
+    __syncthreads();
+    /* C: hist[x] is now the end of bucket x; bucket 1's start is 0 (no parent at distance 0) */
+    uint32_t b0 = 0;
+    for (uint32_t x = 1; x < mx && b0 < total; ++x) {
+        const uint32_t b1 = hist[x];
+        if (b1 == b0) continue; /* uniform: hist is shared */
+        for (uint32_t i = b0 + tid; i < b1; i += DEEP_NT) {
+            const uint32_t k = ord[i];
+            const uint32_t p = pp[k];
+            const double ru = (int)p == s ? 1.0 : pval[rank(p)];
+            pval[k] = ru * pval[k];
+        }
+        b0 = b1;
+        __syncthreads();
+    }
+    /* D: every target, in index order */
+    for (int t = tid; t < n; t += DEEP_NT) {
+        const uint32_t x = dr[t];
+        const int p = pr[t];
+        if (t == s) {
+            rr[t] = 1.0;
+            continue;
+        }
+        if (x >= SRT_INF || p < 0) continue; /* kept, as rel_sweeps_kernel keeps it */
+        const double r = rr[t];
+        rr[t] = (p == s ? 1.0 : pval[rank((uint32_t)p)]) * r;
+    }
+    if (tid == 0) {
+        only[row] = 0;
+        atomicMax(max_depth, (int)mx);
+    }
+}
+
 /* the rows rel_tree_kernel handed over (sweep[row] != 0) through rel_order_kernel first: the
  * sweeps then see only rows with distances past ORD_NB - 1 */
 template <typename PT>
@@ -1689,7 +1843,18 @@ static int rel_rows_launch(int n, int ld, int row0, int lrows, const uint32_t* d
                                                                   depth, sweep, srcs);
     }
     SRT_HIPCHK(hipGetLastError());
-    /* deep rows (distance range past the level passes' 64): distance order, one wave per row */
+    /* deep rows (distance range past the level passes' 64): parents only in distance order
+     * (rel_deep_kernel), then what it left (more parents than its slots) one wave per row */
+    if (tree && !srcs && !l8 && n <= 65535) {
+        const int fixed = 8 * (ld >> 5) + 4 * DEEP_NB;
+        const int cap = min(n, (160 * 1024 - 1024 - fixed) / 14) & ~63;
+        const int lds = fixed + 14 * cap;
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)rel_deep_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        rel_deep_kernel<<<lrows, DEEP_NT, lds, st>>>(n, ld, row0, lrows, d, pred, rel, cap, sweep,
+                                                     depth);
+        SRT_HIPCHK(hipGetLastError());
+    }
     if (tree && !srcs && !l8 &&
         (rc = rel_order_launch<int32_t>(n, ld, row0, lrows, d, pred, rel, ord, sweep, depth, st)))
         return rc;
