@@ -115,6 +115,10 @@ typedef struct srt_build_stats {
                           * core row overflowed its buckets: n_derived = 0) */
     int32_t rel_table;   /* dense level builds: the distinct arc reliabilities of the packed post
                           * pass (predecessor | reliability index words); 0 = f64 rows */
+    double ms_canon;     /* host clock: the canonical graph (srt_canon_build) */
+    double ms_upload;    /* ... the dense matrices filled from it and moved to the device (pinned
+                          * two-slot staging; the slowest rank of a sharded build) */
+    double ms_download;  /* ... the tables moved into the caller's buffers (same staging) */
 } srt_build_stats;
 
 /* Build the full tables for an edge list on one GPU; outputs are host buffers of n*n entries.

@@ -71,6 +71,9 @@ class BuildStats(ctypes.Structure):
         ("ms_core", ctypes.c_double),
         ("ms_derive", ctypes.c_double),
         ("rel_table", ctypes.c_int32),
+        ("ms_canon", ctypes.c_double),
+        ("ms_upload", ctypes.c_double),
+        ("ms_download", ctypes.c_double),
     ]
 
 

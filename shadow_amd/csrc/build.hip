@@ -19,6 +19,8 @@
 #include <string.h>
 
 #include <pthread.h>
+#include <time.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <vector>
@@ -1049,20 +1051,430 @@ static size_t chunk_budget(size_t reserved, int sharers) {
     return budget / (size_t)(sharers > 1 ? sharers : 1);
 }
 
-static void dense_host_matrices(const srt_canon* c, int ld, uint32_t* hw, double* hr) {
-    const size_t ll = (size_t)ld * ld;
-    for (size_t i = 0; i < ll; i++) {
-        hw[i] = SRT_INF;
-        hr[i] = 0.0;
+/* ------------------------------------------------------------------------------------------ */
+/* Host <-> device staging of the dense matrices and the tables. No n x n host matrix is built:  */
+/* host threads fill (or drain) one pinned slot of a two-slot ring while the DMA engine moves    */
+/* the other, so the 12 B/pair cross PCIe once at the link's rate and the first touch of the     */
+/* caller's pageable table pages is spread over the threads. Slots are cached for the process.   */
+/* ------------------------------------------------------------------------------------------ */
+#define STG_SLOT ((size_t)64 << 20)
+#define STG_CACHE 16
+
+static pthread_mutex_t stg_mu = PTHREAD_MUTEX_INITIALIZER;
+static void* stg_free_slots[STG_CACHE];
+static int stg_nfree = 0;
+
+static void* stg_get(void) {
+    void* p = NULL;
+    pthread_mutex_lock(&stg_mu);
+    if (stg_nfree > 0) p = stg_free_slots[--stg_nfree];
+    pthread_mutex_unlock(&stg_mu);
+    if (!p && hipHostMalloc(&p, STG_SLOT, hipHostMallocPortable) != hipSuccess) p = NULL;
+    return p;
+}
+
+static void stg_put(void* p) {
+    if (!p) return;
+    pthread_mutex_lock(&stg_mu);
+    if (stg_nfree < STG_CACHE) {
+        stg_free_slots[stg_nfree++] = p;
+        p = NULL;
     }
-    for (int u = 0; u < c->n; u++) {
-        for (int k = c->rowptr[u]; k < c->rowptr[u + 1]; k++) {
-            hw[(size_t)u * ld + c->col[k]] = c->w[k];
-            hr[(size_t)u * ld + c->col[k]] = c->r[k];
+    pthread_mutex_unlock(&stg_mu);
+    if (p) (void)hipHostFree(p);
+}
+
+static double host_ms(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
+/* host threads for one rank's staging: the CPUs (at most 16) shared by `sharers` ranks */
+static int stg_threads(int sharers) {
+    long c = sysconf(_SC_NPROCESSORS_ONLN);
+    c = c < 1 ? 1 : c > 16 ? 16 : c;
+    c /= sharers > 1 ? sharers : 1;
+    return c < 1 ? 1 : (int)c;
+}
+
+typedef struct {
+    void (*fn)(void* ctx, int part, int nparts);
+    void* ctx;
+    int part, nparts;
+} par_arg;
+
+static void* par_main(void* p) {
+    par_arg* a = (par_arg*)p;
+    a->fn(a->ctx, a->part, a->nparts);
+    return NULL;
+}
+
+/* fn(ctx, i, nt) for i < nt, part 0 on the calling thread */
+static void par_run(int nt, void (*fn)(void*, int, int), void* ctx) {
+    pthread_t th[16];
+    par_arg arg[16];
+    int started[16] = {0};
+    nt = nt < 1 ? 1 : nt > 16 ? 16 : nt;
+    for (int i = 1; i < nt; i++) {
+        arg[i] = {fn, ctx, i, nt};
+        started[i] = pthread_create(&th[i], NULL, par_main, &arg[i]) == 0;
+        if (!started[i]) fn(ctx, i, nt); /* no thread: do the part here */
+    }
+    fn(ctx, 0, nt);
+    for (int i = 1; i < nt; i++)
+        if (started[i]) pthread_join(th[i], NULL);
+}
+
+typedef struct {
+    const srt_canon* c;
+    int ld, r0, rows;
+    uint32_t* w;
+    double* r;
+} fill_ctx;
+
+/* rows [r0, r0 + rows) of the dense matrices: SRT_INF / 0 off the arcs, the arcs' quanta and
+ * reliabilities, the self-loop on the diagonal (rows >= n stay SRT_INF / 0) */
+static void fill_part(void* p, int part, int nparts) {
+    const fill_ctx* f = (const fill_ctx*)p;
+    const srt_canon* c = f->c;
+    const int a = (int)((int64_t)f->rows * part / nparts), b = (int)((int64_t)f->rows * (part + 1) / nparts);
+    for (int i = a; i < b; i++) {
+        uint32_t* wr = f->w + (size_t)i * f->ld;
+        double* rr = f->r + (size_t)i * f->ld;
+        for (int t = 0; t < f->ld; t++) {
+            wr[t] = SRT_INF;
+            rr[t] = 0.0;
         }
-        hw[(size_t)u * ld + u] = c->self_w[u];
-        hr[(size_t)u * ld + u] = c->self_r[u];
+        const int u = f->r0 + i;
+        if (u >= c->n) continue;
+        for (int k = c->rowptr[u]; k < c->rowptr[u + 1]; k++) {
+            wr[c->col[k]] = c->w[k];
+            rr[c->col[k]] = c->r[k];
+        }
+        wr[u] = c->self_w[u];
+        rr[u] = c->self_r[u];
     }
+}
+
+typedef struct {
+    char* dst;
+    size_t dpitch, width;
+    const char* src;
+    int rows;
+} drain_ctx;
+
+static void drain_part(void* p, int part, int nparts) {
+    const drain_ctx* d = (const drain_ctx*)p;
+    const int a = (int)((int64_t)d->rows * part / nparts), b = (int)((int64_t)d->rows * (part + 1) / nparts);
+    if (d->dpitch == d->width)
+        memcpy(d->dst + (size_t)a * d->width, d->src + (size_t)a * d->width, (size_t)(b - a) * d->width);
+    else
+        for (int i = a; i < b; i++) memcpy(d->dst + (size_t)i * d->dpitch, d->src + (size_t)i * d->width, d->width);
+}
+
+/* ---- the edge-list form: the edges themselves go to the device and are scattered there ---- */
+#define SRT_FALLBACK_CANON (-1000) /* internal: redo the build from the host canonical form */
+
+typedef struct {
+    const srt_edges* g;
+    uint64_t q[16], mx[16];
+    int64_t selfl[16];
+    int bad[16];
+} scan_ctx;
+
+static uint64_t gcd_u64(uint64_t a, uint64_t b) {
+    while (b) {
+        const uint64_t t = a % b;
+        a = b;
+        b = t;
+    }
+    return a;
+}
+
+/* the gcd, the maximum and the self-loops of a slice of the edges; bad = a non-positive latency
+ * or an endpoint out of range (the host canonical form then reports it) */
+static void scan_part(void* p, int part, int nparts) {
+    scan_ctx* s = (scan_ctx*)p;
+    const srt_edges* g = s->g;
+    const int64_t a = g->m * part / nparts, b = g->m * (part + 1) / nparts;
+    uint64_t q = 0, mx = 0;
+    int64_t sl = 0;
+    int bad = 0;
+    /* divisibility by the running gcd q = 2^t d (d odd) without a division: l % q == 0 iff
+     * ctz(l) >= t and (l >> t) * d^-1 (mod 2^64) <= (2^64 - 1) / d */
+    int t = 0;
+    uint64_t dinv = 1, lim = ~0ull;
+    for (int64_t e = a; e < b; e++) {
+        const int64_t l = g->lat_ns[e];
+        const int32_t u = g->src[e], v = g->dst[e];
+        bad |= (l <= 0) | ((uint32_t)u >= (uint32_t)g->n) | ((uint32_t)v >= (uint32_t)g->n);
+        sl += u == v;
+        const uint64_t x = (uint64_t)l;
+        mx = x > mx ? x : mx;
+        if (q == 0 || __builtin_ctzll(x | (1ull << 63)) < t || (x >> t) * dinv > lim) {
+            if (l <= 0) continue;
+            q = gcd_u64(q, x);
+            t = __builtin_ctzll(q);
+            const uint64_t d = q >> t;
+            dinv = d; /* Newton: d * dinv == 1 (mod 2^64) after five steps from d */
+            for (int i = 0; i < 5; i++) dinv *= 2 - d * dinv;
+            lim = ~0ull / d;
+        }
+    }
+    s->q[part] = q;
+    s->mx[part] = mx;
+    s->selfl[part] = sl;
+    s->bad[part] = bad;
+}
+
+/* the edge-list form of a graph whose dense build can start from its edges: 0 = built, 1 = take
+ * the host canonical form (invalid edges, a distance bound that may pass u32 quanta, too many
+ * edges for the device copy, edge indices past u32) */
+static int canon_from_edges(const srt_edges* g, srt_canon* c) {
+    memset(c, 0, sizeof(*c));
+    if (!g || g->n <= 0 || g->m <= 0 || g->m >= 0xFFFFFFFFll ||
+        (size_t)g->m * 24 > ((size_t)96 << 30))
+        return 1;
+    scan_ctx s;
+    memset(&s, 0, sizeof(s));
+    s.g = g;
+    const int nt = g->m >= (1 << 20) ? stg_threads(1) : 1;
+    par_run(nt, scan_part, &s);
+    uint64_t q = 0, mx = 0;
+    int64_t sl = 0;
+    for (int i = 0; i < nt; i++) {
+        if (s.bad[i]) return 1;
+        q = gcd_u64(q, s.q[i]);
+        mx = s.mx[i] > mx ? s.mx[i] : mx;
+        sl += s.selfl[i];
+    }
+    const uint64_t mq = mx / q;
+    if (mq >= SRT_INF / 2 || (uint64_t)(g->n - 1) * mq >= SRT_INF) return 1;
+    c->n = g->n;
+    c->directed = g->directed;
+    c->quantum_ns = q;
+    c->max_w_q = (uint32_t)mq;
+    c->dist_bound = (uint64_t)(g->n - 1) * mq;
+    c->arcs = (g->m - sl) * (g->directed ? 1 : 2); /* upper bound until the scatter counts them */
+    c->edges = g;
+    return 0;
+}
+
+/* rows [row0, row0 + nrows) of the dense matrices from the edge list: the edges staged to the
+ * device through the pinned ring (each chunk's minima scattered as it lands), the lowest-index
+ * pass, then quanta / reliabilities in place */
+static int dense_scatter(const srt_canon* c, int ld, int row0, int nrows, uint32_t* dw, double* dr,
+                         hipStream_t st, int sharers) {
+    const srt_edges* g = c->edges;
+    const int64_t m = g->m;
+    const int64_t per = (int64_t)(STG_SLOT / 24);
+    dbufs B;
+    B.k = 0;
+    int rc = SRT_OK;
+    int32_t *es = NULL, *ed = NULL;
+    int64_t* el = NULL;
+    double* eloss = NULL;
+    unsigned long long* darcs = NULL;
+    void* slot[2] = {stg_get(), stg_get()};
+    hipEvent_t ev[2] = {NULL, NULL};
+    const int nt = stg_threads(sharers);
+    unsigned long long arcs = 0;
+    if (!slot[0] || !slot[1]) {
+        srt_set_error("dense staging: pinned slots unavailable");
+        rc = SRT_E_DEVICE;
+        goto out;
+    }
+    TRY(dalloc(&B, (void**)&es, (size_t)m * sizeof(int32_t)));
+    TRY(dalloc(&B, (void**)&ed, (size_t)m * sizeof(int32_t)));
+    TRY(dalloc(&B, (void**)&el, (size_t)m * sizeof(int64_t)));
+    TRY(dalloc(&B, (void**)&eloss, (size_t)m * sizeof(double)));
+    TRY(dalloc(&B, (void**)&darcs, sizeof(unsigned long long)));
+    TRYHIP(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+    TRYHIP(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+    TRYHIP(hipMemsetAsync(darcs, 0, sizeof(unsigned long long), st));
+    TRY(srt_scatter_prepare(nrows, ld, dw, dr, st));
+    for (int64_t k = 0, e0 = 0; e0 < m; k++, e0 += per) {
+        const int s = (int)(k & 1);
+        const int64_t cnt = m - e0 < per ? m - e0 : per;
+        if (k >= 2) TRYHIP(hipEventSynchronize(ev[s]));
+        char* b = (char*)slot[s];
+        drain_ctx parts[4] = {
+            {b, (size_t)cnt * 4, (size_t)cnt * 4, (const char*)(g->src + e0), 1},
+            {b + (size_t)per * 4, (size_t)cnt * 4, (size_t)cnt * 4, (const char*)(g->dst + e0), 1},
+            {b + (size_t)per * 8, (size_t)cnt * 8, (size_t)cnt * 8, (const char*)(g->lat_ns + e0), 1},
+            {b + (size_t)per * 16, (size_t)cnt * 8, (size_t)cnt * 8, (const char*)(g->loss + e0), 1}};
+        for (int a = 0; a < 4; a++) { /* each array as rows of 64 KiB, split over the threads */
+            drain_ctx d = parts[a];
+            const size_t row = (size_t)64 << 10;
+            const size_t full = d.width / row;
+            if (full > 0) {
+                drain_ctx dd = {d.dst, row, row, d.src, (int)full};
+                par_run(nt, drain_part, &dd);
+            }
+            const size_t done = full * row;
+            if (done < d.width) memcpy(d.dst + done, d.src + done, d.width - done);
+        }
+        TRYHIP(hipMemcpyAsync(es + e0, b, (size_t)cnt * 4, hipMemcpyHostToDevice, st));
+        TRYHIP(hipMemcpyAsync(ed + e0, b + (size_t)per * 4, (size_t)cnt * 4, hipMemcpyHostToDevice, st));
+        TRYHIP(hipMemcpyAsync(el + e0, b + (size_t)per * 8, (size_t)cnt * 8, hipMemcpyHostToDevice, st));
+        TRYHIP(hipMemcpyAsync(eloss + e0, b + (size_t)per * 16, (size_t)cnt * 8, hipMemcpyHostToDevice, st));
+        TRYHIP(hipEventRecord(ev[s], st));
+        TRY(srt_scatter_min(cnt, es + e0, ed + e0, el + e0, c->directed, row0, nrows, ld, dr, st));
+    }
+    TRY(srt_scatter_idx(m, es, ed, el, c->directed, row0, nrows, ld, dr, dw, st));
+    TRY(srt_scatter_final(row0, nrows, ld, c->quantum_ns, eloss, dw, dr, darcs, st));
+    TRYHIP(hipMemcpyAsync(&arcs, darcs, sizeof(arcs), hipMemcpyDeviceToHost, st));
+    TRYHIP(hipStreamSynchronize(st));
+    /* the auto choice took the dense build on an upper bound of the arcs: confirm it (one rank's
+     * rows suffice for the whole graph only when they are all of them) */
+    if (c->verify_dense && row0 == 0 && nrows >= c->n) {
+        const double n = c->n;
+        if (!(c->n <= 2048 || (double)arcs * 16.0 >= n * n)) rc = SRT_FALLBACK_CANON;
+    }
+out:
+    if (st) (void)hipStreamSynchronize(st);
+    for (int s = 0; s < 2; s++) {
+        if (ev[s]) (void)hipEventDestroy(ev[s]);
+        stg_put(slot[s]);
+    }
+    dfree(&B);
+    return rc;
+}
+
+/* rows [row0, row0 + nrows) of the ld x ld matrices into dw / dr (row row0 at dw[0]) */
+static int dense_upload(const srt_canon* c, int ld, int row0, int nrows, uint32_t* dw, double* dr,
+                        hipStream_t st, int sharers) {
+    if (nrows <= 0) return SRT_OK;
+    if (!c->rowptr) return dense_scatter(c, ld, row0, nrows, dw, dr, st, sharers);
+    const size_t row_b = (size_t)ld * (sizeof(uint32_t) + sizeof(double));
+    const int per = (int)(STG_SLOT / row_b);
+    if (per < 1) {
+        srt_set_error("dense staging: a row of %d entries passes the %zu-byte slot", ld, STG_SLOT);
+        return SRT_E_RANGE;
+    }
+    void* slot[2] = {stg_get(), stg_get()};
+    hipEvent_t ev[2] = {NULL, NULL};
+    int rc = SRT_OK;
+    const int nt = stg_threads(sharers);
+    if (!slot[0] || !slot[1] || hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) != hipSuccess) {
+        srt_set_error("dense staging: pinned slots or events unavailable");
+        rc = SRT_E_DEVICE;
+    }
+    for (int k = 0, r = 0; !rc && r < nrows; k++, r += per) {
+        const int s = k & 1, rows = nrows - r < per ? nrows - r : per;
+        if (k >= 2 && hipEventSynchronize(ev[s]) != hipSuccess) rc = SRT_E_DEVICE;
+        if (rc) break;
+        fill_ctx f = {c, ld, row0 + r, rows, (uint32_t*)slot[s],
+                      (double*)((char*)slot[s] + (size_t)per * ld * sizeof(uint32_t))};
+        par_run(nt, fill_part, &f);
+        if (hipMemcpyAsync(dw + (size_t)r * ld, f.w, (size_t)rows * ld * sizeof(uint32_t),
+                           hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(dr + (size_t)r * ld, f.r, (size_t)rows * ld * sizeof(double),
+                           hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipEventRecord(ev[s], st) != hipSuccess)
+            rc = SRT_E_DEVICE;
+    }
+    /* the slots go back to the cache only once their copies are done */
+    if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = SRT_E_DEVICE;
+    if (rc == SRT_E_DEVICE) srt_set_error("dense staging upload failed");
+    for (int s = 0; s < 2; s++) {
+        if (ev[s]) (void)hipEventDestroy(ev[s]);
+        stg_put(slot[s]);
+    }
+    return rc;
+}
+
+/* rows x width bytes from device src (pitch spitch) into host dst (pitch dpitch), after the work
+ * already on `st`; returns when dst holds them */
+static int table_download(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width,
+                          int rows, hipStream_t st, int sharers) {
+    if (rows <= 0 || width == 0) return SRT_OK;
+    {   /* a page-locked destination (hipHostMalloc / hipHostRegister by the caller): one DMA */
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, dst) == hipSuccess && at.type == hipMemoryTypeHost) {
+            if (hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, hipMemcpyDeviceToHost, st) !=
+                    hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess) {
+                srt_set_error("table download to pinned memory failed");
+                return SRT_E_DEVICE;
+            }
+            return SRT_OK;
+        }
+        (void)hipGetLastError(); /* a pageable pointer is "invalid value" to the query */
+    }
+    /* a contiguous table is moved as rows of up to 1 MiB */
+    int64_t R = rows;
+    if (dpitch == width && spitch == width && (size_t)rows * width > STG_SLOT) {
+        size_t w = width;
+        while (w * 2 <= ((size_t)1 << 20) && (R & 1) == 0) {
+            w *= 2;
+            R /= 2;
+        }
+        width = dpitch = spitch = w;
+    }
+    const int per = (int)(STG_SLOT / width);
+    if (per < 1) {
+        srt_set_error("table staging: a row of %zu bytes passes the slot", width);
+        return SRT_E_RANGE;
+    }
+    void* slot[2] = {stg_get(), stg_get()};
+    hipEvent_t ev[2] = {NULL, NULL};
+    int rc = SRT_OK;
+    const int nt = stg_threads(sharers);
+    if (!slot[0] || !slot[1] || hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) != hipSuccess) {
+        srt_set_error("table staging: pinned slots or events unavailable");
+        rc = SRT_E_DEVICE;
+    }
+    int64_t prev_r = -1;
+    int prev_rows = 0;
+    for (int64_t k = 0, r = 0; !rc; k++) {
+        const int s = (int)(k & 1);
+        const int rows_k = r < R ? (int)(R - r < per ? R - r : per) : 0;
+        if (rows_k > 0 &&
+            (hipMemcpy2DAsync(slot[s], width, (const char*)src + (size_t)r * spitch, spitch, width,
+                              rows_k, hipMemcpyDeviceToHost, st) != hipSuccess ||
+             hipEventRecord(ev[s], st) != hipSuccess)) {
+            rc = SRT_E_DEVICE;
+            break;
+        }
+        if (prev_r >= 0) { /* drain the previous chunk while this one moves */
+            if (hipEventSynchronize(ev[s ^ 1]) != hipSuccess) {
+                rc = SRT_E_DEVICE;
+                break;
+            }
+            drain_ctx d = {(char*)dst + (size_t)prev_r * dpitch, dpitch, width,
+                           (const char*)slot[s ^ 1], prev_rows};
+            par_run(nt, drain_part, &d);
+        }
+        prev_r = rows_k > 0 ? r : -1;
+        prev_rows = rows_k;
+        if (rows_k == 0) break;
+        r += rows_k;
+    }
+    if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = SRT_E_DEVICE;
+    if (rc == SRT_E_DEVICE) srt_set_error("table staging download failed");
+    for (int s = 0; s < 2; s++) {
+        if (ev[s]) (void)hipEventDestroy(ev[s]);
+        stg_put(slot[s]);
+    }
+    return rc;
+}
+
+/* the nsub x nsub sub-tables (contiguous on the device) into the caller's buffers */
+static int download_sub(int nsub, const uint32_t* slat, const double* srel, const double* sms,
+                        uint32_t* lat_q, double* rel, double* lat_ms, hipStream_t st,
+                        srt_build_stats* local) {
+    SRT_HIPCHK(hipStreamSynchronize(st)); /* the transfer alone is timed */
+    const double t0 = host_ms();
+    const size_t w4 = (size_t)nsub * sizeof(uint32_t), w8 = (size_t)nsub * sizeof(double);
+    int rc = table_download(lat_q, w4, slat, w4, w4, nsub, st, 1);
+    if (!rc) rc = table_download(rel, w8, srel, w8, w8, nsub, st, 1);
+    if (!rc && sms) rc = table_download(lat_ms, w8, sms, w8, w8, nsub, st, 1);
+    local->ms_download = host_ms() - t0;
+    return rc;
 }
 
 /* one GPU */
@@ -1081,8 +1493,6 @@ static int build_one(const srt_canon* c, const srt_build_opts* opts, int algo, i
     dbufs B;
     B.k = 0;
     hipStream_t st = NULL;
-    uint32_t* hw = NULL;
-    double* hr = NULL;
     int32_t* dverts = NULL;
     uint32_t* dmin = NULL;
     uint32_t *slat = NULL, *dlat = NULL;
@@ -1106,19 +1516,15 @@ static int build_one(const srt_canon* c, const srt_build_opts* opts, int algo, i
         }
         const int ld = srt_ceil_div(n, 128) * 128; /* the u16 FW tiles need ld % 128 == 0 */
         const size_t ll = (size_t)ld * ld;
-        hw = (uint32_t*)malloc(ll * sizeof(uint32_t));
-        hr = (double*)malloc(ll * sizeof(double));
-        if (!hw || !hr) {
-            rc = SRT_E_NOMEM;
-            goto out;
-        }
-        dense_host_matrices(c, ld, hw, hr);
         uint32_t* dw;
         double* dr;
         TRY(dalloc(&B, (void**)&dw, ll * sizeof(uint32_t)));
         TRY(dalloc(&B, (void**)&dr, ll * sizeof(double)));
-        TRYHIP(hipMemcpyAsync(dw, hw, ll * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-        TRYHIP(hipMemcpyAsync(dr, hr, ll * sizeof(double), hipMemcpyHostToDevice, st));
+        {
+            const double t0 = host_ms();
+            TRY(dense_upload(c, ld, 0, ld, dw, dr, st, 1));
+            local.ms_upload = host_ms() - t0;
+        }
         /* a few attached vertices: their rows alone (Bellman-Ford passes, ~6 nsub n^2 work)
          * instead of the all-pairs FW (n^3 / 2), as the reference computes paths from attached
          * sources only (topology.c:1604-1656); SRT_FORM rows=0 keeps the FW */
@@ -1141,10 +1547,7 @@ static int build_one(const srt_canon* c, const srt_build_opts* opts, int algo, i
                     TRY(srt_gather_sub_f64(nsub, nsub, NULL, dverts, rm, ld, sms, nsub, st));
                 }
                 TRY(srt_table_min(nsub, nsub, slat, nsub, dmin, st));
-                TRYHIP(hipMemcpyAsync(lat_q, slat, ns2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-                TRYHIP(hipMemcpyAsync(rel, srel, ns2 * sizeof(double), hipMemcpyDeviceToHost, st));
-                if (sms)
-                    TRYHIP(hipMemcpyAsync(lat_ms, sms, ns2 * sizeof(double), hipMemcpyDeviceToHost, st));
+                TRY(download_sub(nsub, slat, srel, sms, lat_q, rel, lat_ms, st, &local));
                 TRYHIP(hipMemcpyAsync(min_q, dmin, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
                 TRYHIP(hipStreamSynchronize(st));
             }
@@ -1178,18 +1581,19 @@ static int build_one(const srt_canon* c, const srt_build_opts* opts, int algo, i
                 TRY(srt_gather_sub_f64(nsub, nsub, dverts, dverts, dms, ld, sms, nsub, st));
             }
             TRY(srt_table_min(nsub, nsub, slat, nsub, dmin, st));
-            TRYHIP(hipMemcpyAsync(lat_q, slat, ns2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-            TRYHIP(hipMemcpyAsync(rel, srel, ns2 * sizeof(double), hipMemcpyDeviceToHost, st));
-            if (sms) TRYHIP(hipMemcpyAsync(lat_ms, sms, ns2 * sizeof(double), hipMemcpyDeviceToHost, st));
+            TRY(download_sub(nsub, slat, srel, sms, lat_q, rel, lat_ms, st, &local));
         } else {
             TRY(srt_table_min(n, n, dlat, ld, dmin, st));
-            TRYHIP(hipMemcpy2DAsync(lat_q, (size_t)n * sizeof(uint32_t), dlat, (size_t)ld * sizeof(uint32_t),
-                                    (size_t)n * sizeof(uint32_t), n, hipMemcpyDeviceToHost, st));
-            TRYHIP(hipMemcpy2DAsync(rel, (size_t)n * sizeof(double), drel, (size_t)ld * sizeof(double),
-                                    (size_t)n * sizeof(double), n, hipMemcpyDeviceToHost, st));
+            TRYHIP(hipStreamSynchronize(st)); /* the transfer alone is timed */
+            const double t0 = host_ms();
+            TRY(table_download(lat_q, (size_t)n * sizeof(uint32_t), dlat, (size_t)ld * sizeof(uint32_t),
+                               (size_t)n * sizeof(uint32_t), n, st, 1));
+            TRY(table_download(rel, (size_t)n * sizeof(double), drel, (size_t)ld * sizeof(double),
+                               (size_t)n * sizeof(double), n, st, 1));
             if (dms)
-                TRYHIP(hipMemcpy2DAsync(lat_ms, (size_t)n * sizeof(double), dms, (size_t)ld * sizeof(double),
-                                        (size_t)n * sizeof(double), n, hipMemcpyDeviceToHost, st));
+                TRY(table_download(lat_ms, (size_t)n * sizeof(double), dms, (size_t)ld * sizeof(double),
+                                   (size_t)n * sizeof(double), n, st, 1));
+            local.ms_download = host_ms() - t0;
         }
         if (!rows_used) {
             TRYHIP(hipMemcpyAsync(min_q, dmin, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -1239,9 +1643,7 @@ static int build_one(const srt_canon* c, const srt_build_opts* opts, int algo, i
         if (!rc) rc = srt_table_min(nsub, nsub, slat, nsub, dmin, st);
         srt_sparse_graph_free(sg);
         if (rc) goto out;
-        TRYHIP(hipMemcpyAsync(lat_q, slat, ns2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        TRYHIP(hipMemcpyAsync(rel, srel, ns2 * sizeof(double), hipMemcpyDeviceToHost, st));
-        if (sms) TRYHIP(hipMemcpyAsync(lat_ms, sms, ns2 * sizeof(double), hipMemcpyDeviceToHost, st));
+        TRY(download_sub(nsub, slat, srel, sms, lat_q, rel, lat_ms, st, &local));
         TRYHIP(hipMemcpyAsync(min_q, dmin, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         TRYHIP(hipStreamSynchronize(st));
     }
@@ -1252,8 +1654,6 @@ out:
         (void)hipStreamDestroy(st);
     }
     dfree(&B);
-    free(hw);
-    free(hr);
     return rc;
 }
 
@@ -1262,7 +1662,6 @@ out:
 /* communicators from ncclCommInitAll, the same sharded kernels as the one-process-per-GPU     */
 /* path (dense: row shards + pivot-panel broadcast; sparse: source shards + all-gather).       */
 /* ------------------------------------------------------------------------------------------ */
-#include <pthread.h>
 
 typedef struct {
     pthread_mutex_t mu;
@@ -1276,8 +1675,6 @@ typedef struct {
     start_gate* gate;
     srt_comm* comm;
     const srt_canon* c;
-    const uint32_t* hw; /* dense: host w/r matrices, ld x ld */
-    const double* hr;
     int nsub;
     const int32_t* verts; /* host subset (NULL: all vertices) */
     uint32_t* lat_q;      /* host outputs, nsub x nsub */
@@ -1327,11 +1724,10 @@ static void* mjob_dense(void* p) {
     TRY(dalloc(&B, (void**)&dmin, sizeof(uint32_t)));
     if (j->lat_ms) TRY(dalloc(&B, (void**)&dms, rows * sizeof(double)));
     TRYHIP(hipMemsetAsync(dmin, 0xFF, sizeof(uint32_t), st));
-    if (nr > 0) {
-        TRYHIP(hipMemcpyAsync(dw, j->hw + (size_t)b * j->ld, (size_t)nr * j->ld * sizeof(uint32_t),
-                              hipMemcpyHostToDevice, st));
-        TRYHIP(hipMemcpyAsync(dr, j->hr + (size_t)b * j->ld, (size_t)nr * j->ld * sizeof(double),
-                              hipMemcpyHostToDevice, st));
+    {
+        const double t0 = host_ms();
+        TRY(dense_upload(j->c, j->ld, b, nr, dw, dr, st, j->R));
+        j->st.ms_upload = host_ms() - t0;
     }
     TRY(srt_dense_build_sharded_ms(j->comm, n, j->ld, j->directed, dw, dr, dlat, drel, dms,
                                    j->c->quantum_ns, st, 0, &j->st));
@@ -1376,25 +1772,24 @@ static void* mjob_dense(void* p) {
                 TRY(srt_gather_sub_f64(cnt, nsub, drows, dcols, dms, j->ld, sm, nsub, st));
             }
             TRY(srt_table_min(cnt, nsub, sl, nsub, dmin, st));
-            TRYHIP(hipMemcpyAsync(j->lat_q + (size_t)i0 * nsub, sl, (size_t)cnt * nsub * sizeof(uint32_t),
-                                  hipMemcpyDeviceToHost, st));
-            TRYHIP(hipMemcpyAsync(j->rel + (size_t)i0 * nsub, sr, (size_t)cnt * nsub * sizeof(double),
-                                  hipMemcpyDeviceToHost, st));
-            if (sm)
-                TRYHIP(hipMemcpyAsync(j->lat_ms + (size_t)i0 * nsub, sm, (size_t)cnt * nsub * sizeof(double),
-                                      hipMemcpyDeviceToHost, st));
+            const double t0 = host_ms();
+            const size_t w4 = (size_t)nsub * sizeof(uint32_t), w8 = (size_t)nsub * sizeof(double);
+            TRY(table_download(j->lat_q + (size_t)i0 * nsub, w4, sl, w4, w4, cnt, st, j->R));
+            TRY(table_download(j->rel + (size_t)i0 * nsub, w8, sr, w8, w8, cnt, st, j->R));
+            if (sm) TRY(table_download(j->lat_ms + (size_t)i0 * nsub, w8, sm, w8, w8, cnt, st, j->R));
+            j->st.ms_download = host_ms() - t0;
         } else if (cnt > 0) {
             TRY(srt_table_min(cnt, n, dlat, j->ld, dmin, st));
-            TRYHIP(hipMemcpy2DAsync(j->lat_q + (size_t)i0 * n, (size_t)n * sizeof(uint32_t), dlat,
-                                    (size_t)j->ld * sizeof(uint32_t), (size_t)n * sizeof(uint32_t),
-                                    cnt, hipMemcpyDeviceToHost, st));
-            TRYHIP(hipMemcpy2DAsync(j->rel + (size_t)i0 * n, (size_t)n * sizeof(double), drel,
-                                    (size_t)j->ld * sizeof(double), (size_t)n * sizeof(double), cnt,
-                                    hipMemcpyDeviceToHost, st));
+            const double t0 = host_ms();
+            const size_t w4 = (size_t)n * sizeof(uint32_t), w8 = (size_t)n * sizeof(double);
+            TRY(table_download(j->lat_q + (size_t)i0 * n, w4, dlat, (size_t)j->ld * sizeof(uint32_t), w4,
+                               cnt, st, j->R));
+            TRY(table_download(j->rel + (size_t)i0 * n, w8, drel, (size_t)j->ld * sizeof(double), w8, cnt,
+                               st, j->R));
             if (dms)
-                TRYHIP(hipMemcpy2DAsync(j->lat_ms + (size_t)i0 * n, (size_t)n * sizeof(double), dms,
-                                        (size_t)j->ld * sizeof(double), (size_t)n * sizeof(double),
-                                        cnt, hipMemcpyDeviceToHost, st));
+                TRY(table_download(j->lat_ms + (size_t)i0 * n, w8, dms, (size_t)j->ld * sizeof(double), w8,
+                                   cnt, st, j->R));
+            j->st.ms_download = host_ms() - t0;
         }
         TRYHIP(hipMemcpyAsync(&j->min_q, dmin, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         TRYHIP(hipStreamSynchronize(st));
@@ -1486,8 +1881,6 @@ static int build_multi(const srt_canon* c, const srt_build_opts* opts, int algo,
     const int n = c->n;
     const int ld = srt_ceil_div(n, SRT_SHARD_ALIGN) * SRT_SHARD_ALIGN;
     int rc = SRT_OK;
-    uint32_t* hw = NULL;
-    double* hr = NULL;
     start_gate gate;
     pthread_mutex_init(&gate.mu, NULL);
     pthread_cond_init(&gate.cv, NULL);
@@ -1508,14 +1901,6 @@ static int build_multi(const srt_canon* c, const srt_build_opts* opts, int algo,
             rc = SRT_E_RANGE;
             goto done;
         }
-        const size_t ll = (size_t)ld * ld;
-        hw = (uint32_t*)malloc(ll * sizeof(uint32_t));
-        hr = (double*)malloc(ll * sizeof(double));
-        if (!hw || !hr) {
-            rc = SRT_E_NOMEM;
-            goto done;
-        }
-        dense_host_matrices(c, ld, hw, hr);
     }
     for (int i = 0; i < R; i++) devs[i] = virt ? 0 : i;
     if ((rc = virt ? srt_comm_init_virtual(R, 0, comms) : srt_comm_init_all(R, devs, comms)))
@@ -1533,8 +1918,6 @@ static int build_multi(const srt_canon* c, const srt_build_opts* opts, int algo,
         j->gate = &gate;
         j->comm = comms[i];
         j->c = c;
-        j->hw = hw;
-        j->hr = hr;
         j->nsub = nsub;
         j->verts = verts;
         j->lat_q = lat_q;
@@ -1570,7 +1953,12 @@ static int build_multi(const srt_canon* c, const srt_build_opts* opts, int algo,
         *min_q = m;
         if (stats) {
             *stats = jobs[0].st;
-            for (int i = 1; i < R; i++) stats->tied_pairs += jobs[i].st.tied_pairs;
+            for (int i = 1; i < R; i++) {
+                stats->tied_pairs += jobs[i].st.tied_pairs;
+                if (jobs[i].st.ms_upload > stats->ms_upload) stats->ms_upload = jobs[i].st.ms_upload;
+                if (jobs[i].st.ms_download > stats->ms_download)
+                    stats->ms_download = jobs[i].st.ms_download;
+            }
         }
     }
 done:
@@ -1583,8 +1971,6 @@ done:
     free(jobs);
     free(th);
     free(devs);
-    free(hw);
-    free(hr);
     return rc;
 }
 
@@ -1613,32 +1999,53 @@ static int build_tables_subset_impl(const srt_edges* g, const srt_build_opts* op
         srt_set_error("srt_build_tables: no HIP device");
         return SRT_E_DEVICE;
     }
-    srt_canon c;
-    int rc = srt_canon_build(g, &c);
-    if (rc) return rc;
-    *quantum_ns = c.quantum_ns;
     const int use_sp = opts ? opts->use_shortest_path : 1;
-    const int algo = use_sp ? (c.wide && !(opts && opts->algo == SRT_ALGO_DENSE_FW)
-                                   ? SRT_ALGO_SPARSE_SSSP
-                                   : choose_algo(&c, opts))
-                            : SRT_ALGO_DENSE_FW;
-    if (use_sp && c.wide && (algo == SRT_ALGO_DENSE_FW || !lat_ms)) {
-        srt_set_error("shortest-path latencies may pass the u32 range (bound %llu quanta of %llu "
-                      "ns): only the sparse u64 rows build this graph, and its latencies are "
-                      "served from the f64 ms table (%s)",
-                      (unsigned long long)c.dist_bound, (unsigned long long)c.quantum_ns,
-                      algo == SRT_ALGO_DENSE_FW ? "dense requested" : "no lat_ms output");
-        srt_canon_free(&c);
-        return SRT_E_RANGE;
+    const int forced = opts ? opts->algo : SRT_ALGO_AUTO;
+    /* a dense-shaped graph (by its edge count, an upper bound on its arcs) goes to the device as
+     * its edge list; every other graph, and one the edge form refuses, through the host canonical
+     * CSR (graph.c). The dense auto choice is confirmed on the exact arcs by a one-rank scatter. */
+    int edge_form = 0;
+    if (forced != SRT_ALGO_SPARSE_SSSP && g->n <= SRT_DENSE_MAX_N && g->m > 0) {
+        const double n = g->n, ub = (double)g->m * (g->directed ? 1 : 2);
+        edge_form = g->n <= 2048 || ub * 16.0 >= n * n || forced == SRT_ALGO_DENSE_FW || !use_sp;
     }
-    const int R = virt ? virt : (ngpus < avail ? ngpus : avail);
-    uint32_t mq = 0xFFFFFFFFu;
-    if (R > 1 && use_sp)
-        rc = build_multi(&c, opts, algo, R, virt, nsub, verts, lat_q, rel, lat_ms, &mq, stats);
-    else
-        rc = build_one(&c, opts, algo, nsub, verts, lat_q, rel, lat_ms, &mq, stats);
-    if (!rc && min_lat_q) *min_lat_q = mq;
-    srt_canon_free(&c);
+    int rc = SRT_OK;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        srt_canon c;
+        const double t0 = host_ms();
+        if (edge_form && attempt == 0 && canon_from_edges(g, &c) == 0) {
+            c.verify_dense = use_sp && forced != SRT_ALGO_DENSE_FW;
+        } else {
+            if (attempt == 0) edge_form = 0;
+            rc = srt_canon_build(g, &c);
+            if (rc) return rc;
+        }
+        const double ms_canon = host_ms() - t0;
+        *quantum_ns = c.quantum_ns;
+        const int algo = use_sp ? (c.wide && forced != SRT_ALGO_DENSE_FW ? SRT_ALGO_SPARSE_SSSP
+                                                                          : choose_algo(&c, opts))
+                                : SRT_ALGO_DENSE_FW;
+        if (use_sp && c.wide && (algo == SRT_ALGO_DENSE_FW || !lat_ms)) {
+            srt_set_error("shortest-path latencies may pass the u32 range (bound %llu quanta of %llu "
+                          "ns): only the sparse u64 rows build this graph, and its latencies are "
+                          "served from the f64 ms table (%s)",
+                          (unsigned long long)c.dist_bound, (unsigned long long)c.quantum_ns,
+                          algo == SRT_ALGO_DENSE_FW ? "dense requested" : "no lat_ms output");
+            srt_canon_free(&c);
+            return SRT_E_RANGE;
+        }
+        const int R = virt ? virt : (ngpus < avail ? ngpus : avail);
+        uint32_t mq = 0xFFFFFFFFu;
+        if (R > 1 && use_sp)
+            rc = build_multi(&c, opts, algo, R, virt, nsub, verts, lat_q, rel, lat_ms, &mq, stats);
+        else
+            rc = build_one(&c, opts, algo, nsub, verts, lat_q, rel, lat_ms, &mq, stats);
+        if (!rc && min_lat_q) *min_lat_q = mq;
+        if (!rc && stats) stats->ms_canon = ms_canon;
+        srt_canon_free(&c);
+        if (rc != SRT_FALLBACK_CANON) break;
+        srt_log(SRT_LOG_INFO, "edge-list dense build: too few distinct arcs, the host canonical form decides");
+    }
     return rc;
 }
 

@@ -1285,7 +1285,7 @@ static void rel_tree_launch(int n, int ld, int row0, int lrows, const LT* d, con
     }
 }
 
-/* Round 5: the reliability pass of the source-major packed words (srt_levels_pkw: pred | rix << 16
+/* Round 5: the reliability pass of the source-major packed words (srt_levels_pred's, transposed: pred | rix << 16
  * | level << 27 per pair). rel(s,t) = rel(s,pred) * r(pred,t) needs, besides the pair's own word,
  * only rel(s,pred) -- and the predecessors of a row are few (its "parents": C4 rows have ~1-3k of
  * 32k targets, the vertices at distance <= 2-3 quanta). So a row's pass computes the parents alone,
@@ -2226,11 +2226,8 @@ static int dense_post_levels(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
         const double* rtab = srt_levels_rtab(&ntab);
         if (stats) stats->rel_table = ntab;
         uint32_t* pk = reinterpret_cast<uint32_t*>(ws->dt);
-        const int mode = srt_levels_pkw_ready();
         if (kt) SRT_HIPCHK(hipEventRecord(ws->kev[0], st));
-        if (mode == 1) {
-            if ((rc = srt_levels_pkw(pk, ld, ties ? ws->ties : NULL, st))) return rc;
-        } else { /* target-major packed words (with the level), then one u32 transpose */
+        {   /* target-major packed words (with the level), then one u32 transpose */
             size_t c2 = ws->predt_cap;
             if ((rc = ws_grow((void**)&ws->predt, &c2, slab, sizeof(int32_t)))) return rc;
             ws->predt_cap = c2;
@@ -2239,8 +2236,7 @@ static int dense_post_levels(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
                 return rc;
         }
         if (kt) SRT_HIPCHK(hipEventRecord(ws->kev[1], st));
-        if (mode != 1)
-            transpose_kernel<uint32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
+        transpose_kernel<uint32_t><<<dim3(srt_ceil_div(nrows, 64), srt_ceil_div(n, 64)), 256, 0, st>>>(
                 n, nrows, reinterpret_cast<const uint32_t*>(ws->predt), (size_t)nrows, pk, (size_t)ld);
         ws->pred16 = 2; /* dense_path_ms reads the packed words' low half */
         SRT_HIPCHK(hipMemsetAsync(ws->depth, 0, sizeof(int32_t), st));

@@ -760,261 +760,6 @@ __global__ __launch_bounds__(256) void lvl_pred_kernel(int n, int nw, int nchunk
                           rix, lev, predT, rT, ldp, ties);
 }
 
-#ifndef LVL_PKW_CW
-#define LVL_PKW_CW 16 /* source words per target group: 64 B per gathered arc */
-#endif
-#ifndef LVL_PKW_PB
-#define LVL_PKW_PB 8 /* gathers per lane and batch */
-#endif
-#ifndef LVL_PKW_W
-#define LVL_PKW_W 8 /* waves per workgroup */
-#endif
-#ifndef LVL_PKW_WAVE
-#define LVL_PKW_WAVE 0 /* 1: every wave on its own units (lvl_pkw_wave_kernel) */
-#endif
-/* ---- predecessor words, source-major, with the level (round 5) ---------------------------------
- * The same canonical rule as lvl_pred_kernel, on a unit shape that keeps the gathered plane slices
- * in one XCD's L2 and writes its output source-major (no transpose):
- *  - a wave runs G = 64 / CW targets at once, one per CW-lane group; lane p of a group owns source
- *    word c * CW + p, so one arc's gather is CW * 4 B (64 B for CW = 16) of Delta_{d-w}[u];
- *  - a workgroup (8 waves) owns a tile of TT = 8 G targets x S = 32 CW sources, and the units are
- *    handed out XCD-major, chunk-major: an XCD's CUs work on one source chunk at a time, whose
- *    plane slices (n x CW x 4 B per level: 2 MB at C4) are the only gathered data in its L2
- *    (lvl_pred_kernel's 64-word chunks had 8 MB per level, served by the MALL at 6.3x its bytes);
- *  - the winning arc of each (source, target) lands in an LDS tile as the finished output word
- *    pred | rix << 16 | level << 27 (rix < 2,048, level <= 31), and the tile is written source-
- *    major, TT x 4 B per source row, after the tile's targets are done.
- * arcw[i] = u | rix[i] << 16 for the sorted in-arcs (built by lvl_aw_kernel). Without TIES the walk
- * of a weight stops once every pending source of every group has its arc (the arcs of a weight are
- * in ascending u, so the first tight arc wins either way); TIES walks them all and counts the
- * sources hit twice. Entries with no level (the diagonal, padding) stay 0xFFFF (predecessor -1). */
-/* The walk of one lane group's target t over the chunk's source words (lane p owns word c * CW + p):
- * every level d of the pending sources, weights w = d .. 1, arcs of a weight in ascending u. The
- * winning arc of chunk source r = p * 32 + b goes to tile[slot(r)] as pred | rix << 16 | d << 27. */
-template <int CW, int PB, bool TIES, class Slot>
-static __device__ __forceinline__ void pkw_walk(int t, bool tv, bool valid, int word, int g, int p,
-                                                int cs0, int n, int nw, int nlev,
-                                                const int32_t* __restrict__ off,
-                                                const uint32_t* __restrict__ arcw,
-                                                const uint32_t* __restrict__ lev,
-                                                uint32_t* __restrict__ tile, Slot slot,
-                                                unsigned& tied) {
-    constexpr int S = 32 * CW;
-    const size_t plane = (size_t)n * nw;
-    const uint32_t nw4 = (uint32_t)nw * 4u;
-    const int32_t* ot = off + (size_t)(tv ? t : 0) * LVL_STRIDE;
-    const uint32_t lane4 = (uint32_t)(valid ? word : 0) * 4u;
-    for (int d = 1; d <= nlev; ++d) {
-        uint32_t pend = valid ? lev[(size_t)(d - 1) * plane + (size_t)t * nw + word] : 0u;
-        if (!__any(pend != 0u)) continue;
-        const uint32_t dbits = (uint32_t)d << 27;
-        for (int w = d; w >= 1; --w) {
-            const int g0 = tv ? ot[w] : 0, g1 = tv ? ot[w + 1] : 0;
-            uint32_t H = 0, T = 0;
-            if (w == d) {
-                /* the direct arcs (u, t): tight for the source u itself; CW arcs per group and
-                 * step, the few whose u lies in the chunk go to the lane owning its word */
-                for (int k = 0; __any(g0 + k < g1); k += CW) {
-                    const int i = g0 + k + p;
-                    const uint32_t a = i < g1 ? arcw[i] : 0u;
-                    const int us = i < g1 ? (int)(a & 0xFFFFu) - cs0 : -1;
-                    unsigned long long m = __ballot(us >= 0 && us < S);
-                    while (m) {
-                        const int jl = __builtin_ctzll(m);
-                        m &= m - 1ull;
-                        const int uj = __builtin_amdgcn_readlane(us, jl);
-                        const uint32_t aj = (uint32_t)__builtin_amdgcn_readlane((int)a, jl);
-                        const uint32_t b = 1u << (uj & 31);
-                        if (g == jl / CW && p == (uj >> 5) && (pend & b)) {
-                            H |= b;
-                            tile[slot(uj)] = aj | dbits; /* row uj = p * 32 + bit */
-                        }
-                    }
-                }
-            } else {
-                const char* base = reinterpret_cast<const char*>(lev + (size_t)(d - w - 1) * plane);
-                uint32_t a[PB], v[PB];
-#pragma unroll
-                for (int q = 0; q < PB; ++q) a[q] = g0 + q < g1 ? arcw[g0 + q] : 0u;
-#pragma unroll
-                for (int q = 0; q < PB; ++q)
-                    v[q] = g0 + q < g1 ? *reinterpret_cast<const uint32_t*>(
-                                             base + ((a[q] & 0xFFFFu) * nw4 + lane4))
-                                       : 0u;
-                for (int i = g0; __any(i < g1); i += PB) {
-                    /* the next batch in flight while this one's candidates are taken */
-                    const int i2 = i + PB;
-                    uint32_t an[PB], vn[PB];
-#pragma unroll
-                    for (int q = 0; q < PB; ++q) an[q] = i2 + q < g1 ? arcw[i2 + q] : 0u;
-#pragma unroll
-                    for (int q = 0; q < PB; ++q)
-                        vn[q] = i2 + q < g1 ? *reinterpret_cast<const uint32_t*>(
-                                                  base + ((an[q] & 0xFFFFu) * nw4 + lane4))
-                                            : 0u;
-#pragma unroll
-                    for (int q = 0; q < PB; ++q) {
-                        const uint32_t xq = v[q] & pend;
-                        uint32_t nb = xq & ~H;
-                        if (TIES) T |= xq & H;
-                        H |= xq;
-                        const uint32_t val = a[q] | dbits;
-                        while (nb) {
-                            const int bb = __builtin_ctz(nb);
-                            nb &= nb - 1u;
-                            tile[slot(p * 32 + bb)] = val;
-                        }
-                    }
-#pragma unroll
-                    for (int q = 0; q < PB; ++q) {
-                        a[q] = an[q];
-                        v[q] = vn[q];
-                    }
-                    if (!TIES && !__any((pend & ~H) != 0u)) break;
-                }
-            }
-            if (TIES) tied += __builtin_popcount(T);
-            pend &= ~H;
-            if (!__any(pend != 0u)) break;
-        }
-    }
-}
-
-template <int CW, int PB, int NWV, bool TIES>
-__global__ __launch_bounds__(64 * NWV) void lvl_pkw_kernel(int n, int ld, int nw, int src0,
-                                                             int nsrc, int nlev, int ntile,
-                                                             unsigned nunit,
-                                                             const int32_t* __restrict__ off,
-                                                             const uint32_t* __restrict__ arcw,
-                                                             const uint32_t* __restrict__ lev,
-                                                             uint32_t* __restrict__ pk,
-                                                             unsigned long long* __restrict__ ties) {
-    constexpr int G = 64 / CW, TT = NWV * G, S = 32 * CW, LVL_PKW_NT = 64 * NWV;
-    extern __shared__ __attribute__((aligned(16))) uint32_t tile[]; /* [S][TT], columns swizzled */
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g = lane / CW, p = lane % CW;
-    /* XCD x takes units [x * per, (x + 1) * per), chunk-major */
-    const unsigned x = blockIdx.x & 7u, L = gridDim.x >> 3, per = (nunit + 7u) >> 3;
-    unsigned tied = 0;
-    for (unsigned j = blockIdx.x >> 3; j < per; j += L) {
-        const unsigned u = x * per + j;
-        if (u >= nunit) break;
-        const int c = (int)(u / (unsigned)ntile), tb = (int)(u % (unsigned)ntile);
-        for (int q = tid; q < S * TT / 4; q += LVL_PKW_NT)
-            reinterpret_cast<uint4*>(tile)[q] = make_uint4(0xFFFFu, 0xFFFFu, 0xFFFFu, 0xFFFFu);
-        __syncthreads();
-        const int tl = wv * G + g, t = tb * TT + tl;
-        const bool tv = t < n;
-        const int word = c * CW + p;
-        const bool valid = tv && word < nw;
-        /* this lane's tile column: target tl, swizzled by the source word (two-way LDS conflicts at
-         * most among a take step's stores; 4-aligned groups stay whole for the write-out) */
-        const int tcol = tl ^ (((p & 7) << 2) & (TT - 1));
-        const int cs0 = src0 + c * S; /* global index of the chunk's first source */
-#if !defined(LVL_PKW_DIAG) || LVL_PKW_DIAG != 2
-        pkw_walk<CW, PB, TIES>(t, tv, valid, word, g, p, cs0, n, nw, nlev, off, arcw, lev, tile,
-                               [&](int r) { return r * TT + tcol; }, tied);
-#endif
-        __syncthreads();
-        /* write-out: source row r of the chunk, TT x 4 B from column tb * TT */
-        constexpr int GPR = TT / 4; /* 16-B pieces per row */
-        for (int q = tid; q < S * GPR; q += LVL_PKW_NT) {
-            const int r = q / GPR, a4 = q % GPR;
-            const int sl = c * S + r;
-            if (sl >= nsrc) break; /* rows are in order: the rest are past too */
-            const int col = (4 * a4) ^ ((((r >> 5) & 7) << 2) & (TT - 1));
-            const uint4 val = *reinterpret_cast<const uint4*>(&tile[r * TT + col]);
-#if defined(LVL_PKW_DIAG) && LVL_PKW_DIAG == 1
-            if (val.x != 0x12345678u) continue; /* timing diagnostic: no write-out */
-#endif
-            uint32_t* o = pk + (size_t)sl * ld + (size_t)tb * TT + 4 * a4;
-            __builtin_nontemporal_store(val.x, o);
-            __builtin_nontemporal_store(val.y, o + 1);
-            __builtin_nontemporal_store(val.z, o + 2);
-            __builtin_nontemporal_store(val.w, o + 3);
-        }
-        __syncthreads();
-    }
-    if (TIES) {
-        for (int m = 32; m > 0; m >>= 1) tied += __shfl_xor(tied, m);
-        if (lane == 0 && tied) atomicAdd(&ties[blockIdx.x & 1023u], (unsigned long long)tied);
-    }
-}
-
-/* The same walk with every wave on its own units (no workgroup barriers: a workgroup's waves
- * finish their targets at different times): a unit is (G targets, one chunk), the wave's tile is
- * S rows x G words of LDS (8 KB), and its write-out is G x 4 B per source row (16 B for CW = 16);
- * the eight waves holding a 128-B line's 32 targets write it within a short time, so the L2 merges
- * the pieces into whole lines. Rows are swizzled by their word (r ^ (p & 7)): a take step's lanes
- * hit different banks. */
-template <int CW, int PB, int NWV, bool TIES>
-__global__ __launch_bounds__(64 * NWV) void lvl_pkw_wave_kernel(int n, int ld, int nw, int src0,
-                                                               int nsrc, int nlev, int ntg,
-                                                               unsigned nunit,
-                                                               const int32_t* __restrict__ off,
-                                                               const uint32_t* __restrict__ arcw,
-                                                               const uint32_t* __restrict__ lev,
-                                                               uint32_t* __restrict__ pk,
-                                                               unsigned long long* __restrict__ ties) {
-    constexpr int G = 64 / CW, S = 32 * CW;
-    extern __shared__ __attribute__((aligned(16))) uint32_t wtile[];
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    uint32_t* tile = wtile + wv * (S * G);
-    const int g = lane / CW, p = lane % CW;
-    /* XCD x's waves take units [x * per, (x + 1) * per), chunk-major */
-    const unsigned x = blockIdx.x & 7u, per = (nunit + 7u) >> 3;
-    const unsigned wid = (blockIdx.x >> 3) * NWV + wv, wpx = (gridDim.x >> 3) * NWV;
-    unsigned tied = 0;
-    auto phys = [](int r) { return r ^ ((r >> 5) & 7); }; /* row swizzle within the word's 32 rows */
-    for (unsigned j = wid; j < per; j += wpx) {
-        const unsigned u = x * per + j;
-        if (u >= nunit) break;
-        const int c = (int)(u / (unsigned)ntg), tg = (int)(u % (unsigned)ntg);
-#pragma unroll
-        for (int q = 0; q < S * G / 256; ++q)
-            reinterpret_cast<uint4*>(tile)[q * 64 + lane] = make_uint4(0xFFFFu, 0xFFFFu, 0xFFFFu, 0xFFFFu);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int t = tg * G + g;
-        const bool tv = t < n;
-        const int word = c * CW + p;
-        const bool valid = tv && word < nw;
-        const int cs0 = src0 + c * S;
-        pkw_walk<CW, PB, TIES>(t, tv, valid, word, g, p, cs0, n, nw, nlev, off, arcw, lev, tile,
-                               [&](int r) { return phys(r) * G + g; }, tied);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        /* write-out: physical row rp holds chunk row phys(rp) (the swizzle is an involution) */
-        constexpr int LPR = G / 4; /* lanes per row (16 B each) */
-#pragma unroll
-        for (int q = 0; q < S * LPR / 64; ++q) {
-            const int rp = q * (64 / LPR) + lane / LPR, h = lane % LPR;
-            const int sl = c * S + phys(rp);
-            const uint4 val = reinterpret_cast<const uint4*>(tile)[rp * LPR + h];
-            if (sl < nsrc)
-                *reinterpret_cast<uint4*>(pk + (size_t)sl * ld + (size_t)tg * G + 4 * h) = val;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    if (TIES) {
-        for (int m = 32; m > 0; m >>= 1) tied += __shfl_xor(tied, m);
-        if (lane == 0 && tied) atomicAdd(&ties[blockIdx.x & 1023u], (unsigned long long)tied);
-    }
-}
-
-/* arcw[i] = u | rix[i] << 16 (the in-arcs' tail and reliability index) */
-__global__ void lvl_aw_kernel(int total, const uint32_t* __restrict__ arcs,
-                              const uint16_t* __restrict__ rix, uint32_t* __restrict__ arcw) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < total) arcw[i] = (arcs[i] & 0xFFFFu) | ((uint32_t)rix[i] << 16);
-}
-
 __global__ void lvl_sum_kernel(const unsigned long long* __restrict__ v, int k,
                                unsigned long long* __restrict__ out) {
     unsigned long long s = 0;
@@ -1076,7 +821,7 @@ typedef struct {
     int ntab;
     uint32_t* lev;
     uint8_t* l8; /* u8 distance rows (nrows x ld) for the reliability pass */
-    int pkw;     /* the post pass takes srt_levels_pkw (no lat / l8 rows written by the build) */
+    int pkw;     /* the post pass is the packed words with levels + rel_pk (no lat / l8 rows) */
     int total;   /* in-arcs held (w <= lmax) */
     unsigned long long* dkey; /* the diagonal rule's key per local row (undirected rows form) */
     const double* r_rows;
@@ -1422,12 +1167,12 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         ntab = hflag[1];
     else
         rix = NULL, rtab = NULL; /* (freed with the state) */
-    /* the fused post pass (srt_levels_pkw) writes the u32 rows itself: the table of distinct arc
+    /* the packed post pass writes the u32 rows itself (rel_pk_kernel): the table of distinct arc
      * reliabilities, 5-bit levels and u16 vertices (n <= 32768) */
-    /* 2: the walk of lvl_pred_kernel (target-major packed words with the level), one transpose;
-     * 1: lvl_pkw_kernel (source-major words from an LDS tile); both then rel_pk_kernel, which
-     * writes the u32 rows too; 0: lvl_out8 rows + rel_tree_kernel (and past the packed form) */
-    const int pkw = rix && D <= 31 && n <= 32768 ? srt_form_int("pkw", 2) : 0;
+    /* 1: lvl_pred_kernel's target-major packed words with the level, one transpose, then
+     * rel_pk_kernel, which writes the u32 rows too; 0 (past the packed form, or SRT_FORM pkw=0):
+     * lvl_out8 rows + the predecessor rows + rel_tree_kernel */
+    const int pkw = rix && D <= 31 && n <= 32768 ? (srt_form_int("pkw", 1) != 0) : 0;
     uint8_t* l8 = NULL;
     if (!pkw) {
         LVL_ALLOC(l8, (size_t)nrows * ld);
@@ -1469,73 +1214,11 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     return SRT_OK;
 }
 
-/* the held build's packed-word post pass: 0 none, 1 srt_levels_pkw, 2 srt_levels_pred packed
- * with levels + a transpose; rel_pk_kernel after either */
+/* the held build's post pass: 1 srt_levels_pred's packed words with levels + a transpose +
+ * rel_pk_kernel, 0 the u8 level rows + rel_tree_kernel */
 int srt_levels_pkw_ready(void) {
     const lvl_state* L = &g_lvl[srt_state_slot()];
     return L->held ? L->pkw : 0;
-}
-
-/* Source-major packed words of the held build (lvl_pkw_kernel): pk[sl][t] (row stride ld, nrows
- * rows) = pred | rix << 16 | level << 27, 0xFFFF where there is no level. ties != NULL adds the
- * tied pairs (the walk then visits every arc of a weight). */
-int srt_levels_pkw(uint32_t* pk, int ld, unsigned long long* ties, hipStream_t st) {
-    lvl_state* L = &g_lvl[srt_state_slot()];
-    if (!L->held || !L->pkw) {
-        srt_set_error("levels: no held level build in the packed-word form");
-        return SRT_E_ARG;
-    }
-    const int total = L->total;
-    /* the arcs' (tail | reliability index) words, into the gather offsets' buffer (free now) */
-    uint32_t* arcw = L->aoff;
-    if (total > 0) {
-        lvl_aw_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, L->arcs, L->rix, arcw);
-        SRT_HIPCHK(hipGetLastError());
-    }
-    unsigned long long* part = NULL;
-    if (ties) {
-        SRT_HIPCHK(srt_malloc_async(&part, 1024 * sizeof(unsigned long long), st));
-        SRT_HIPCHK(hipMemsetAsync(part, 0, 1024 * sizeof(unsigned long long), st));
-    }
-    constexpr int CW = LVL_PKW_CW, PB = LVL_PKW_PB, NWV = LVL_PKW_W, NT = 64 * NWV;
-    constexpr int G = 64 / CW, S = 32 * CW;
-    constexpr bool WAVE = LVL_PKW_WAVE != 0;
-    constexpr int TT = WAVE ? G : NWV * G; /* targets per unit */
-    const int lds = S * NWV * G * (int)sizeof(uint32_t);
-    const int ntile = ld / TT, nchunkw = (L->nw + CW - 1) / CW;
-    const unsigned nunit = (unsigned)ntile * (unsigned)nchunkw;
-    const void* fn = WAVE ? (ties ? (const void*)lvl_pkw_wave_kernel<CW, PB, NWV, true>
-                                  : (const void*)lvl_pkw_wave_kernel<CW, PB, NWV, false>)
-                          : (ties ? (const void*)lvl_pkw_kernel<CW, PB, NWV, true>
-                                  : (const void*)lvl_pkw_kernel<CW, PB, NWV, false>);
-    SRT_HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    int dev = 0, cus = 256, per = 2;
-    if (hipGetDevice(&dev) == hipSuccess)
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, NT, lds) != hipSuccess || per < 1)
-        per = 1;
-    (void)hipGetLastError();
-    unsigned grid = (unsigned)(cus * per) & ~7u;
-    if (grid < 8) grid = 8;
-    if (WAVE && ties)
-        lvl_pkw_wave_kernel<CW, PB, NWV, true><<<grid, NT, lds, st>>>(
-            L->n, ld, L->nw, L->row0, L->nrows, L->D, ntile, nunit, L->off, arcw, L->lev, pk, part);
-    else if (WAVE)
-        lvl_pkw_wave_kernel<CW, PB, NWV, false><<<grid, NT, lds, st>>>(
-            L->n, ld, L->nw, L->row0, L->nrows, L->D, ntile, nunit, L->off, arcw, L->lev, pk, NULL);
-    else if (ties)
-        lvl_pkw_kernel<CW, PB, NWV, true><<<grid, NT, lds, st>>>(
-            L->n, ld, L->nw, L->row0, L->nrows, L->D, ntile, nunit, L->off, arcw, L->lev, pk, part);
-    else
-        lvl_pkw_kernel<CW, PB, NWV, false><<<grid, NT, lds, st>>>(
-            L->n, ld, L->nw, L->row0, L->nrows, L->D, ntile, nunit, L->off, arcw, L->lev, pk, NULL);
-    SRT_HIPCHK(hipGetLastError());
-    if (ties) {
-        lvl_sum_kernel<<<1, 1024, 0, st>>>(part, 1024, ties);
-        SRT_HIPCHK(hipGetLastError());
-        SRT_HIPCHK(hipFreeAsync(part, st));
-    }
-    return SRT_OK;
 }
 
 /* Canonical predecessors and their arc reliabilities of the held level build, target-major

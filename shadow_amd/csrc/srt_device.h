@@ -161,11 +161,10 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
  * (target-major, row stride ldp) */
 int srt_levels_pred(void* predT, int pred16, double* rT, size_t ldp, unsigned long long* ties,
                     hipStream_t st);
-/* 1 when the held level build's post pass is the source-major packed-word form (srt_levels_pkw:
- * pred | reliability index << 16 | level << 27 per pair, then the reliability pass writes the u32
- * rows too); 0: srt_levels_pred + the transposes */
+/* 1 when the held level build's post pass is the packed-word form (srt_levels_pred with pred16 = 2:
+ * pred | reliability index << 16 | level << 27 per pair, one transpose, then rel_pk_kernel writes
+ * the u32 rows too); 0: the u8 level rows + srt_levels_pred + rel_tree_kernel */
 int srt_levels_pkw_ready(void);
-int srt_levels_pkw(uint32_t* pk, int ld, unsigned long long* ties, hipStream_t st);
 /* frees the held level build (stream-ordered) */
 void srt_levels_release(hipStream_t st);
 /* the held build's u8 distance rows (nrows x ld, 0 on the diagonal), NULL if none */
@@ -243,6 +242,16 @@ int srt_gather_sub_u32(int nr, int nc, const int32_t* rows, const int32_t* cols,
 int srt_gather_sub_f64(int nr, int nc, const int32_t* rows, const int32_t* cols, const double* in,
                        size_t ldi, double* out, size_t ldo, hipStream_t st);
 int srt_table_min(int rows, int cols, const uint32_t* t, size_t ld, uint32_t* dmin, hipStream_t st);
+/* dense matrices from the edge list on the device (tables.hip): prepare (all-ones), the minimum
+ * latency per pair into r's bits, the lowest index among the minima into w, then in place the
+ * quanta / reliabilities (SRT_INF / 0 where no edge) with the off-diagonal arcs counted */
+int srt_scatter_prepare(int nrows, int ld, uint32_t* w, double* r, hipStream_t st);
+int srt_scatter_min(int64_t m, const int32_t* src, const int32_t* dst, const int64_t* lat, int directed,
+                    int32_t row0, int nrows, int ld, double* r, hipStream_t st);
+int srt_scatter_idx(int64_t m, const int32_t* src, const int32_t* dst, const int64_t* lat, int directed,
+                    int32_t row0, int nrows, int ld, const double* r, uint32_t* w, hipStream_t st);
+int srt_scatter_final(int32_t row0, int nrows, int ld, uint64_t q, const double* loss, uint32_t* w,
+                      double* r, unsigned long long* arcs, hipStream_t st);
 /* adds the tied pairs of nrows distance rows (diagonal rule applied) to *tied */
 int srt_tie_count_rows(int n, int nrows, const int32_t* srcs, int src_begin, const uint32_t* D,
                        size_t ldd, const int32_t* irp, const int32_t* icol, const uint32_t* iw,

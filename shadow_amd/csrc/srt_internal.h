@@ -45,6 +45,11 @@ typedef struct srt_canon {
     /* canonical self-loop per vertex (SRT_INF if none) */
     uint32_t* self_w;
     double* self_r;
+    /* edge-list form (build.hip, dense builds): no CSR (rowptr NULL); the dense matrices are
+     * scattered from these edges on the device, arcs holds an upper bound until then and
+     * verify_dense asks the scatter to confirm the auto choice of the dense build */
+    const srt_edges* edges;
+    int32_t verify_dense;
 } srt_canon;
 
 int srt_canon_build(const srt_edges* g, srt_canon* c);

@@ -376,3 +376,105 @@ int srt_tie_count_rows(int n, int nrows, const int32_t* srcs, int src_begin, con
     *tied += (int64_t)h;
     return SRT_OK;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* Dense matrices straight from the edge list (the canonical arc rule of graph.c on the device: */
+/* per ordered pair the minimum-latency edge, the lowest edge index among equal latencies, both */
+/* directions of an undirected edge, self-loops on the diagonal). Rows [row0, row0 + nrows) of  */
+/* an ld-wide matrix; the f64 matrix holds the u64 minimum latency and the u32 matrix the edge  */
+/* index until srt_scatter_final turns them into quanta and reliabilities in place.            */
+/* ------------------------------------------------------------------------------------------ */
+__global__ __launch_bounds__(256) void scatter_min_kernel(int64_t m, const int32_t* __restrict__ src,
+                                                          const int32_t* __restrict__ dst,
+                                                          const int64_t* __restrict__ lat, int directed,
+                                                          int32_t row0, uint32_t nrows, int ld,
+                                                          unsigned long long* __restrict__ minlat) {
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (int64_t)gridDim.x * 256) {
+        const int32_t u = src[e], v = dst[e];
+        const unsigned long long l = (unsigned long long)lat[e];
+        if ((uint32_t)(u - row0) < nrows) atomicMin(minlat + (size_t)(u - row0) * ld + v, l);
+        if (!directed && u != v && (uint32_t)(v - row0) < nrows)
+            atomicMin(minlat + (size_t)(v - row0) * ld + u, l);
+    }
+}
+
+__global__ __launch_bounds__(256) void scatter_idx_kernel(int64_t m, const int32_t* __restrict__ src,
+                                                          const int32_t* __restrict__ dst,
+                                                          const int64_t* __restrict__ lat, int directed,
+                                                          int32_t row0, uint32_t nrows, int ld,
+                                                          const unsigned long long* __restrict__ minlat,
+                                                          uint32_t* __restrict__ eidx) {
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (int64_t)gridDim.x * 256) {
+        const int32_t u = src[e], v = dst[e];
+        const unsigned long long l = (unsigned long long)lat[e];
+        if ((uint32_t)(u - row0) < nrows) {
+            const size_t o = (size_t)(u - row0) * ld + v;
+            if (minlat[o] == l) atomicMin(eidx + o, (uint32_t)e);
+        }
+        if (!directed && u != v && (uint32_t)(v - row0) < nrows) {
+            const size_t o = (size_t)(v - row0) * ld + u;
+            if (minlat[o] == l) atomicMin(eidx + o, (uint32_t)e);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void scatter_final_kernel(int32_t row0, int nrows, int ld, uint64_t q,
+                                                            const double* __restrict__ loss,
+                                                            uint32_t* __restrict__ w, double* __restrict__ r,
+                                                            unsigned long long* __restrict__ arcs) {
+    const size_t total = (size_t)nrows * ld;
+    unsigned long long cnt = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+        const unsigned long long k = __builtin_bit_cast(unsigned long long, r[i]);
+        const uint32_t e = w[i];
+        if (k == ~0ull) {
+            w[i] = SRT_INF;
+            r[i] = 0.0;
+        } else {
+            w[i] = (uint32_t)(k / q);
+            r[i] = 1.0f - loss[e]; /* topology.c:396, as graph.c's canonical arcs */
+            cnt += (size_t)row0 + i / ld != i % ld;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(arcs, cnt);
+}
+
+int srt_scatter_prepare(int nrows, int ld, uint32_t* w, double* r, hipStream_t st) {
+    SRT_HIPCHK(hipMemsetAsync(w, 0xFF, (size_t)nrows * ld * sizeof(uint32_t), st));
+    SRT_HIPCHK(hipMemsetAsync(r, 0xFF, (size_t)nrows * ld * sizeof(double), st));
+    return SRT_OK;
+}
+
+static unsigned scatter_grid(int64_t m) {
+    const int64_t b = (m + 255) / 256;
+    return (unsigned)(b < 8192 ? (b > 0 ? b : 1) : 8192);
+}
+
+int srt_scatter_min(int64_t m, const int32_t* src, const int32_t* dst, const int64_t* lat, int directed,
+                    int32_t row0, int nrows, int ld, double* r, hipStream_t st) {
+    if (m <= 0 || nrows <= 0) return SRT_OK;
+    scatter_min_kernel<<<scatter_grid(m), 256, 0, st>>>(m, src, dst, lat, directed, row0, (uint32_t)nrows,
+                                                        ld, (unsigned long long*)r);
+    SRT_HIPCHK(hipGetLastError());
+    return SRT_OK;
+}
+
+int srt_scatter_idx(int64_t m, const int32_t* src, const int32_t* dst, const int64_t* lat, int directed,
+                    int32_t row0, int nrows, int ld, const double* r, uint32_t* w, hipStream_t st) {
+    if (m <= 0 || nrows <= 0) return SRT_OK;
+    scatter_idx_kernel<<<scatter_grid(m), 256, 0, st>>>(m, src, dst, lat, directed, row0, (uint32_t)nrows,
+                                                        ld, (const unsigned long long*)r, w);
+    SRT_HIPCHK(hipGetLastError());
+    return SRT_OK;
+}
+
+int srt_scatter_final(int32_t row0, int nrows, int ld, uint64_t q, const double* loss, uint32_t* w,
+                      double* r, unsigned long long* arcs, hipStream_t st) {
+    if (nrows <= 0) return SRT_OK;
+    const size_t total = (size_t)nrows * ld;
+    const size_t b = (total + 255) / 256;
+    scatter_final_kernel<<<(unsigned)(b < 8192 ? b : 8192), 256, 0, st>>>(row0, nrows, ld, q, loss, w, r, arcs);
+    SRT_HIPCHK(hipGetLastError());
+    return SRT_OK;
+}

@@ -50,14 +50,13 @@ def _directed_dense(n, seed, wmax):
 
 
 @pytest.mark.parametrize("kind", ["complete300", "complete1000", "ties", "directed", "c1like",
-                                  "f64form", "manyrel", "transposed", "ties_transposed", "wgtile",
-                                  "ties_wgtile"])
+                                  "f64form", "manyrel", "transposed", "ties_transposed"])
 def test_levels_match_oracle(gpu, monkeypatch, kind):
     """The post pass carries r(pred, t) as an index into the build's table of distinct arc
     reliabilities: by default one target-major word per pair with the level beside it
-    (lvl_pred_kernel), one transpose, then rel_pk_kernel; "wgtile" (SRT_FORM pkw=1) writes the
-    words source-major from an LDS tile (lvl_pkw_kernel); "transposed" (pkw=0) keeps the u8 level
-    rows and rel_tree_kernel; "f64form" (SRT_FORM pk=0) and "manyrel" (more distinct values
+    (lvl_pred_kernel), one transpose, then rel_pk_kernel, which writes the u32 rows too;
+    "transposed" (SRT_FORM pkw=0) keeps the u8 level rows and rel_tree_kernel; "f64form"
+    (SRT_FORM pk=0) and "manyrel" (more distinct values
     than the table holds) take the f64 rows. "c1like" has distances past 31 quanta: the packed
     words cannot hold its levels (the transposed form, then the sweeps past 64)."""
     set_form(monkeypatch, levels="1")
@@ -65,13 +64,11 @@ def test_levels_match_oracle(gpu, monkeypatch, kind):
         set_form(monkeypatch, levels="1", pk="0")
     if kind in ("transposed", "ties_transposed"):
         set_form(monkeypatch, levels="1", pkw="0")
-    if kind in ("wgtile", "ties_wgtile"):
-        set_form(monkeypatch, levels="1", pkw="1")
-    if kind in ("complete300", "f64form", "transposed", "wgtile"):
+    if kind in ("complete300", "f64form", "transposed"):
         g = graphs.complete_graph(300, seed=7)
     elif kind == "complete1000":  # C2's distribution: distances up to 9 quanta
         g = graphs.complete_graph(1000, seed=2)
-    elif kind in ("ties", "ties_transposed", "ties_wgtile"):  # 1-3 ms arcs: equal-length paths
+    elif kind in ("ties", "ties_transposed"):  # 1-3 ms arcs: equal-length paths
         g = graphs.complete_graph(640, seed=11, lat_max=3)
     elif kind == "directed":  # in-arcs from the columns of w
         g = _directed_dense(500, 5, 40)
