@@ -689,16 +689,15 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
     auto one = [&](int i) { return srcs ? srcs + i : (const int32_t*)NULL; };
     const int b0 = srcs ? 0 : src_begin;
     /* SRT_FORM kernel=block|ms|wg|wave forces one sparse kernel for every source (tests) */
-    const bool block = srt_form_is("kernel", "block") || srt_form_int("hbm", 0) != 0;
+    const bool block = srt_form_is("kernel", "block");
     int rc = SRT_OK;
     /* the multi-source kernel (msssp.hip) where the relabelled graph is local (RGG-like, where
-     * the 64 frontiers of a source cluster overlap); SRT_FORM ms=0 / kernel=ms disables / forces it.
-     * Sources are clustered here, on the host, before the timed span */
+     * the 64 frontiers of a source cluster overlap). Sources are clustered here, on the host,
+     * before the timed span */
     const bool k_ms = srt_form_is("kernel", "ms"), k_wg = srt_form_is("kernel", "wg"),
                k_wave = srt_form_is("kernel", "wave");
-    /* SRT_FORM ms=0 / wg=0 take the multi-source / workgroup kernel out of the automatic choice */
     bool ms = allow_ms && !block && g->n <= srt_msssp_max_n() && g->h_rp2 &&
-              (k_ms || (!k_wg && !k_wave && srt_form_int("ms", 1) != 0 && g->local != 0));
+              (k_ms || (!k_wg && !k_wave && g->local != 0));
     std::vector<int32_t> ms_bsrc, ms_brow, ms_rest, hs;
     if (ms) {
         std::vector<int32_t> rowof((size_t)g->n, -1);
@@ -709,13 +708,13 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
             if (s < 0 || s >= g->n || rowof[g->h_inv[s]] >= 0) ms = false; /* duplicates */
             else rowof[g->h_inv[s]] = i;
         }
-        /* SRT_FORM ms_rmax: the hop radius of a cluster (tests force it to 0 / large) */
-        const int rmax = srt_form_int("ms_rmax", 24);
+        /* the hop radius of a cluster */
+        const int rmax = 24;
         int cus = 256, dev = 0;
         hipDeviceProp_t prop;
         if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
             cus = prop.multiProcessorCount;
-        const int maxb = srt_form_int("ms_maxb", 2 * cus); /* tests: the batch budget */
+        const int maxb = 2 * cus; /* the batch budget: two per CU, the rest single-source */
         srt_sparse_graph* gm = const_cast<srt_sparse_graph*>(g); /* the cluster cache */
         pthread_mutex_lock(&gm->ck_mu);
         const bool hit = ms && gm->ck_bsrc && gm->ck_n == nsrc && gm->ck_rmax == rmax &&
@@ -800,7 +799,7 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
     SRT_HIPCHK(hipEventRecord(e0, st));
     /* large power-law graphs (relabelled arcs far apart): the workgroup kernel with the distance
      * row packed in LDS, once a probe source shows every distance fits its 10-bit fields
-     * (d(a, b) <= 2 ecc(s0)); SRT_FORM wg=0 / kernel=wg disables / allows it at any size */
+     * (d(a, b) <= 2 ecc(s0)); SRT_FORM kernel=wg allows it at any size */
     int32_t* ms_dev = NULL; /* bsrc then brow, freed on the stream after the launch */
     int ms_d16 = 0;
     if (ms) {
@@ -811,11 +810,10 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
         SRT_HIPCHK(hipMemcpyAsync(ms_dev + ms_bsrc.size(), ms_brow.data(), bb,
                                   hipMemcpyHostToDevice, st));
         /* bucket width: 8 mean arc weights (C3: 64 quanta; same-box sweep in DESIGN §5.4) */
-        const int fd = srt_form_int("ms_delta", 0);
-        const uint32_t delta = fd > 0 ? (uint32_t)fd : 8u * g->delta;
+        const uint32_t delta = 8u * g->delta;
         /* 16-bit working distances when every finite distance provably fits (half the bytes of
-         * every row access; SRT_FORM ms_u16=0 keeps 32 for the tests) */
-        const int d16 = g->dist_bound < 0xFFFFull && srt_form_int("ms_u16", 1) != 0;
+         * every row access) */
+        const int d16 = g->dist_bound < 0xFFFFull;
         ms_d16 = d16;
         rc = srt_msssp_rows(g->n, g->directed, g->rp2, g->cw2, g->irp2, g->icw2, g->ir2,
                             g->inv, delta, nb, ms_dev, ms_dev + ms_bsrc.size(), lat_rows, rel_rows,
@@ -850,15 +848,13 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
     bool derived = false;
     derived_times dtm;
     bool wg = !ms && !g->directed && g->n <= srt_wgsssp_max_n() &&
-              (k_wg || (!k_wave && srt_form_int("wg", 1) != 0 && g->n > 32768 && !g->local));
+              (k_wg || (!k_wave && g->n > 32768 && !g->local));
     /* the workgroup kernel keeps its row in LDS (any order serves), so it runs on the original
-     * vertex order and writes reliability straight into the output rows; SRT_FORM wg_order=cm runs it
-     * on the Cuthill-McKee relabelling with a private row gathered at the end */
-    const bool wg_cm = srt_form_is("wg_order", "cm");
-    const int2* wrp = wg_cm ? g->rp2 : g->rpo;
-    const uint2* wcw = wg_cm ? g->cw2 : g->cw;
-    const double* wr = wg_cm ? g->r2 : g->r;
-    const int32_t* winv = wg_cm ? g->inv : NULL;
+     * vertex order and writes reliability straight into the output rows */
+    const int2* wrp = g->rpo;
+    const uint2* wcw = g->cw;
+    const double* wr = g->r;
+    const int32_t* winv = NULL;
     if (wg) {
         rc = srt_wgsssp_rows(g->n, wrp, wcw, wr, winv, g->max_w, b0, b0 + 1, one(0),
                              lat_rows, rel_rows, ovf, st, g->ridx, g->rtab);
@@ -877,9 +873,8 @@ static int sparse_rows(const srt_sparse_graph* g, int32_t src_begin, int32_t src
         /* every row of the graph in one call (the full table): the core rows by the kernel with
          * their canonical arcs, the independent set's rows derived from them (derive.hip;
          * SRT_FORM derive=0 keeps the kernel for every row) */
-        derived = wg && !srcs && b0 == 0 && nsrc == g->n && !wg_cm && g->nI > 0 && g->ridx &&
-                  g->rtab && g->max_w < 128 && g->arcs < (1 << 20) &&
-                  srt_form_int("wg_compact", 1) != 0 && srt_form_int("derive", 1) != 0;
+        derived = wg && !srcs && b0 == 0 && nsrc == g->n && g->nI > 0 && g->ridx && g->rtab &&
+                  g->max_w < 128 && g->arcs < (1 << 20) && srt_form_int("derive", 1) != 0;
         if (derived)
             rc = sparse_rows_derived(g, lat_rows, rel_rows, ovf, st, &dtm);
         else if (wg && nsrc > 1)
@@ -1527,9 +1522,9 @@ static int build_one(const srt_canon* c, const srt_build_opts* opts, int algo, i
         }
         /* a few attached vertices: their rows alone (Bellman-Ford passes, ~6 nsub n^2 work)
          * instead of the all-pairs FW (n^3 / 2), as the reference computes paths from attached
-         * sources only (topology.c:1604-1656); SRT_FORM rows=0 keeps the FW */
+         * sources only (topology.c:1604-1656) */
         int rows_used = 0;
-        if (use_sp && verts && (size_t)nsub * 12 <= (size_t)n && srt_form_int("rows", 1) != 0) {
+        if (use_sp && verts && (size_t)nsub * 12 <= (size_t)n) {
             uint32_t* rl;
             double *rr, *rm = NULL;
             TRY(dalloc(&B, (void**)&rl, (size_t)nsub * ld * sizeof(uint32_t)));

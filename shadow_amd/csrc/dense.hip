@@ -1445,12 +1445,13 @@ __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int ro
                 x[e] = bail ? r : ((int)u == s ? 1.0 : pval[rank(u)]) * r;
             }
         }
-        __builtin_nontemporal_store(lv[0], lr + t0);
-        __builtin_nontemporal_store(lv[1], lr + t0 + 1);
-        __builtin_nontemporal_store(lv[2], lr + t0 + 2);
-        __builtin_nontemporal_store(lv[3], lr + t0 + 3);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) __builtin_nontemporal_store(x[e], rr + t0 + e);
+        /* whole 16-B pieces: one coalesced 1-KB run per wave for the u32 row, two for the f64 */
+        typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+        typedef double f64x2v __attribute__((ext_vector_type(2)));
+        __builtin_nontemporal_store((u32x4v){lv[0], lv[1], lv[2], lv[3]},
+                                    reinterpret_cast<u32x4v*>(lr + t0));
+        __builtin_nontemporal_store((f64x2v){x[0], x[1]}, reinterpret_cast<f64x2v*>(rr + t0));
+        __builtin_nontemporal_store((f64x2v){x[2], x[3]}, reinterpret_cast<f64x2v*>(rr + t0 + 2));
         /* one piece at a time: hoisting every piece's LDS reads costs the second row per CU */
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -1471,7 +1472,10 @@ static int rel_pk_launch(int n, int ld, int row0, int lrows, const uint32_t* pk,
     const int cap = min(n, (80 * 1024 - fixed) / 12) & ~63;
     const int lds = fixed + 12 * cap;
     const void* fn;
-    const int K = ld <= 2048 ? 1 : ld <= 4096 ? 2 : ld <= 8192 ? 4 : ld <= 16384 ? 8 : 16;
+    const int K = (ld + 4 * REL_PK_NT - 1) / (4 * REL_PK_NT) <= 1 ? 1
+                  : (ld + 4 * REL_PK_NT - 1) / (4 * REL_PK_NT) <= 2 ? 2
+                  : (ld + 4 * REL_PK_NT - 1) / (4 * REL_PK_NT) <= 4 ? 4
+                  : (ld + 4 * REL_PK_NT - 1) / (4 * REL_PK_NT) <= 8 ? 8 : 16;
     switch (K) {
     case 1: fn = (const void*)rel_pk_kernel<1>; break;
     case 2: fn = (const void*)rel_pk_kernel<2>; break;

@@ -1579,10 +1579,10 @@ static int fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0,
     u16* grecv = NULL; /* staged panel blocks in (contributor, J) order (r128: rows a, then b) */
     int* cnt = (int*)calloc(2 * (size_t)R, sizeof(int)); /* per contributor (256: two tile rows) */
     const size_t blk = (size_t)KB * 128;
-    /* two-deep 128-pivot rounds (N > 1 default; SRT_FORM deep=0: one-deep): band k + 3 is staged
+    /* two-deep 128-pivot rounds (N > 1 with two or more tile rows): band k + 3 is staged
      * and broadcast on its own stream right after round k's update, three rounds ahead, and each
      * rank applies the two panels it missed to the staged band itself (fwq_band_kernel) */
-    const bool deep = r128 && R > 1 && T >= 2 && srt_form_int("deep", 1) != 0;
+    const bool deep = r128 && R > 1 && T >= 2;
     const size_t nstage = (size_t)(kbr / KB) * ((size_t)T + 1) * blk * (deep ? 3 : 1);
     bool ok = cnt && hipMalloc(&tl, (nkept + 1) * sizeof(uint32_t)) == hipSuccess &&
               hipMalloc(&down, (size_t)T * sizeof(int)) == hipSuccess &&
@@ -2015,9 +2015,9 @@ int srt_fw16_build_sym_sharded(const srt_comm* comm, int n, int ld, int row0, in
                       "most %d tile columns", SYM_TMAX);
         return SRT_E_ARG;
     }
-    /* 128-pivot rounds with the 8-wave update; SRT_FORM shkb=64 selects 64-pivot rounds (a
-     * 256-pivot form measured slower at N = 8: 57.6 vs 45.9 ms for one rank) */
-    const int rp = srt_form_int("shkb", 128) == 64 ? 64 : 128;
+    /* 128-pivot rounds with the 8-wave update (a 256-pivot form measured slower at N = 8: 57.6
+     * vs 45.9 ms for one rank; 64-pivot rounds slower still) */
+    const int rp = 128;
     g_sharded_rp = rp;
     return fw16_build_sym_sharded(comm, n, ld, row0, nrows, w_rows, lat_rows, st, evp, exact, rp);
 }
@@ -2067,23 +2067,17 @@ int srt_fw16_build(int n, int ld, int row0, int nrows, const uint32_t* w_rows, u
     fw16_sched* sc;
     int rc = sched_get(&sc, dev);
     if (rc) return rc;
-    const int la = srt_form_int("lookahead", -1);
-    const bool lookahead = la >= 0 ? la != 0 : bcast != NULL;
+    const bool lookahead = bcast != NULL;
     /* upper-triangle rounds: undirected graph, f16-compare path, the whole matrix on one GPU */
     const bool want_sym = sym && *sym && srt_form_int("sym", 1) != 0;
     if (sym) *sym = 0;
     if (want_sym && fm && !bcast && !owner_of && row0 == 0 && nrows == ld) {
-        /* two update streams once the rounds are long enough to hide their event waits;
-         * SRT_FORM lookahead=0/1 forces either form */
-        const bool two = la >= 0 ? la != 0 : ld >= 8192;
-        /* 128-pivot rounds on the two update streams (8-wave kernel; SRT_FORM kb=64 selects the
-         * 64-pivot rounds). With the update's compute loop at ~85% of the issue model, the per-tile
-         * C load, row sums, staging and store are what is left to amortize: C4 332.2 vs 344.1 ms
-         * per build on one box (before that loop change the two measured the same, 380.5 vs
-         * 380.1 ms) */
-        const int kbw = srt_form_int("kb", 256);
-        const bool big = two;
-        const int rp = big && kbw >= 256 && ld % 256 == 0 ? 256 : big && kbw >= 128 && ld >= 256 ? 128 : 64;
+        /* two update streams once the rounds are long enough to hide their event waits, with
+         * 256-pivot rounds (128 where ld is not a multiple of 256): with the update's compute loop
+         * at ~85% of the issue model, the per-tile C load, row sums, staging and store are what is
+         * left to amortize, so the longest rounds measured fastest */
+        const bool two = ld >= 8192;
+        const int rp = two ? (ld % 256 == 0 ? 256 : 128) : 64;
         *sym = rp == 256 ? 4 : rp == 128 ? 3 : two ? 2 : 1;
         return fw16_build_sym(n, ld, w_rows, lat_rows, st, evp, exact, two, rp);
     }

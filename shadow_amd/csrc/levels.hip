@@ -626,7 +626,8 @@ static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx
                         if ((uj >> 5) == word) take(pend & (1u << (uj & 31)), H, T, i0 + j);
                     }
                 }
-            } else { /* sixteen gathers in flight (a predicated tail), then their candidates in
+            }
+            else { /* sixteen gathers in flight (a predicated tail), then their candidates in
                       * arc order */
                 const char* base = reinterpret_cast<const char*>(lev + (size_t)(d - w - 1) * plane);
                 /* LVL_PB gathers per batch, software-pipelined: the next batch's gathers are in
@@ -1044,8 +1045,8 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     LVL_TRY_ALLOC(lev, (size_t)lmax * plane * sizeof(uint32_t) + 16, &ok);
     LVL_TRY_ALLOC(Rb, plane * sizeof(uint32_t) + 16, &ok);
     LVL_TRY_ALLOC(done, (size_t)n * nchunk + 16, &ok);
-    /* the distinct arc reliabilities (packed post pass, n <= 32768; SRT_FORM pk=0 keeps f64) */
-    const bool want_rt = total > 0 && n <= 32768 && srt_form_int("pk", 1) != 0;
+    /* the distinct arc reliabilities (packed post pass, n <= 32768) */
+    const bool want_rt = total > 0 && n <= 32768;
     unsigned long long* H = NULL;
     uint16_t *map = NULL, *rix = NULL;
     double* rtab = NULL;

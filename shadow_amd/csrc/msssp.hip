@@ -51,7 +51,6 @@
 #define MS_G 4       /* candidates a wave pulls together */
 #define MS_AC 16     /* arcs per candidate and chunk (MS_G x MS_AC lanes) */
 #define MS_AK 8      /* arcs per candidate whose distance rows are loaded together */
-#define MS_PROF 10   /* profile words per batch (SRT_FORM prof) */
 
 static __device__ __forceinline__ uint32_t ms_ld(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -118,14 +117,13 @@ static __device__ __forceinline__ void ms_compact(uint32_t* bm, int nw, int* lis
  * for undirected graphs); inv[original] = relabelled; bsrc / brow: per batch and lane the
  * relabelled source and the output row (-1 = empty lane); ws: per slot D (n x 64 u32), R (n x 64
  * f64) and the lane minimum of every vertex (n u32). */
-template <bool DIRECTED, bool PROF, typename DT>
+template <bool DIRECTED, typename DT>
 __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
     int n, const int2* __restrict__ orp, const uint2* __restrict__ ocw,
     const int2* __restrict__ irp, const uint2* __restrict__ icw, const double* __restrict__ ir,
     const int32_t* __restrict__ inv, int nbatch, const int32_t* __restrict__ bsrc,
     const int32_t* __restrict__ brow, uint32_t* __restrict__ lat, double* __restrict__ rel,
-    size_t ldo, uint32_t* __restrict__ ws, size_t slot_words, uint32_t delta,
-    unsigned long long* __restrict__ prof) {
+    size_t ldo, uint32_t* __restrict__ ws, size_t slot_words, uint32_t delta) {
     extern __shared__ uint32_t sm[];
     __shared__ int s_list[MS_LCAP];
     __shared__ int s_cnt, s_more;
@@ -144,22 +142,7 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
     double* const R = reinterpret_cast<double*>(wsb + (size_t)n * MS_L);
     uint32_t* const mind = wsb + (size_t)n * MS_L * 3;
 
-    /* PROF (SRT_FORM prof=1): per batch, passes, pulls, bucket advances, then the cycles of
-     * wave 0 in the compaction, pull, advance, output and initialisation phases */
-    unsigned long long pc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t0 = 0, rt0 = 0;
-    auto tick = [&](int slot) {
-        if (PROF) {
-            const unsigned long long t = clock64();
-            pc[slot] += t - t0;
-            t0 = t;
-        }
-    };
     for (int b = blockIdx.x; b < nbatch; b += gridDim.x) {
-        if (PROF) {
-            for (int i = 0; i < 8; i++) pc[i] = 0;
-            t0 = clock64();
-            rt0 = __builtin_amdgcn_s_memrealtime();
-        }
         for (int i = tid; i < 3 * nw; i += MS_WG) sm[i] = 0u;
         {
             uint4* d4 = reinterpret_cast<uint4*>(D);
@@ -186,10 +169,8 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
         uint32_t* cur = bmA;
         uint32_t* nxt = bmB;
         uint32_t T = delta;
-        tick(7);
         for (;;) {
             int found = 0;
-            if (PROF) pc[0]++;
             for (;;) { /* chunks of this pass's candidate list */
                 if (tid == 0) {
                     s_cnt = 0;
@@ -201,8 +182,6 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                 const int cnt = min(s_cnt, MS_LCAP);
                 const int more = s_more;
                 found += cnt;
-                if (PROF) pc[1] += cnt;
-                tick(3);
                 /* a wave pulls MS_G consecutive list entries together, so their row, arc and
                  * distance loads share round trips: lane j < MS_G loads candidate j's in-row,
                  * lanes j * MS_AC + a its arcs a, a + MS_AC, ..., and the 64-lane distance rows
@@ -358,7 +337,6 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                     }
                 }
                 __syncthreads();
-                tick(4);
                 if (!more) break;
             }
             if (found) {
@@ -368,7 +346,6 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                 continue;
             }
             /* no candidate left: advance T past the smallest pending lane minimum */
-            if (PROF) pc[2]++;
             if (tid == 0) s_pmin = SRT_INF;
             __syncthreads();
             uint32_t pm = SRT_INF;
@@ -405,9 +382,7 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
                 pend[wi] = keep;
             }
             __syncthreads();
-            tick(5);
         }
-        tick(5);
         /* output rows in original vertex order: lane j takes target t0 + j and reads its 64-lane
          * rows in 16-byte pieces (4 sources each); each source's row segment is one coalesced
          * store */
@@ -447,12 +422,6 @@ __global__ __launch_bounds__(MS_WG, 4) void msssp_kernel(
             }
         }
         __syncthreads();
-        tick(6);
-        if (PROF && tid == 0) {
-            for (int i = 0; i < 8; i++) prof[(size_t)b * MS_PROF + i] = pc[i];
-            prof[(size_t)b * MS_PROF + 8] = rt0;
-            prof[(size_t)b * MS_PROF + 9] = __builtin_amdgcn_s_memrealtime();
-        }
     }
 }
 
@@ -521,66 +490,20 @@ int srt_msssp_rows(int n, int directed, const int2* orp, const uint2* ocw, const
     uint32_t* ws = g_ms_ws[sl];
     const uint32_t dl = delta < 1 ? 1u : delta;
     const size_t dyn = ms_lds_bytes(n);
-    unsigned long long* prof = NULL; /* SRT_FORM prof=1: per-batch phase counts (tools) */
-    if (srt_form_int("prof", 0) > 0 &&
-        srt_malloc_async((void**)&prof, (size_t)nbatch * MS_PROF * sizeof(unsigned long long), st) !=
-            hipSuccess) {
-        (void)hipGetLastError();
-        prof = NULL;
-    }
-#define SRT_MSSSP_LAUNCH(DIR, PR, DT)                                                            \
+#define SRT_MSSSP_LAUNCH(DIR, DT)                                                                \
     do {                                                                                         \
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)msssp_kernel<DIR, PR, DT>,                    \
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)msssp_kernel<DIR, DT>,                        \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));    \
-        msssp_kernel<DIR, PR, DT><<<(unsigned)slots, MS_WG, dyn, st>>>(                           \
+        msssp_kernel<DIR, DT><<<(unsigned)slots, MS_WG, dyn, st>>>(                               \
             n, orp, ocw, irp, icw, ir, inv, nbatch, bsrc, brow, lat, rel, ldo, ws, slot_words,    \
-            dl, prof);                                                                           \
+            dl);                                                                                 \
     } while (0)
-#define SRT_MSSSP_LAUNCH2(DIR, PR)                                                               \
-    do {                                                                                         \
-        if (d16) SRT_MSSSP_LAUNCH(DIR, PR, uint16_t);                                             \
-        else SRT_MSSSP_LAUNCH(DIR, PR, uint32_t);                                                 \
-    } while (0)
-    if (directed && prof) SRT_MSSSP_LAUNCH2(true, true);
-    else if (directed) SRT_MSSSP_LAUNCH2(true, false);
-    else if (prof) SRT_MSSSP_LAUNCH2(false, true);
-    else SRT_MSSSP_LAUNCH2(false, false);
-#undef SRT_MSSSP_LAUNCH2
+    if (directed && d16) SRT_MSSSP_LAUNCH(true, uint16_t);
+    else if (directed) SRT_MSSSP_LAUNCH(true, uint32_t);
+    else if (d16) SRT_MSSSP_LAUNCH(false, uint16_t);
+    else SRT_MSSSP_LAUNCH(false, uint32_t);
 #undef SRT_MSSSP_LAUNCH
     SRT_HIPCHK(hipGetLastError());
-    if (prof) { /* per-batch means on stderr (a measurement aid, not part of the build) */
-        const size_t words = (size_t)nbatch * MS_PROF;
-        unsigned long long* h = (unsigned long long*)malloc(words * 8);
-        if (h && hipMemcpyAsync(h, prof, words * 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
-            hipStreamSynchronize(st) == hipSuccess) {
-            double m[8] = {0}, busy = 0, worst = 0;
-            unsigned long long t_lo = ~0ull, t_hi = 0;
-            int wb = 0;
-            for (int b = 0; b < nbatch; b++) {
-                const unsigned long long* x = h + (size_t)b * MS_PROF;
-                for (int i = 0; i < 8; i++) m[i] += (double)x[i] / nbatch;
-                const double dur = (double)(x[9] - x[8]) / 100.0; /* s_memrealtime: 100 MHz */
-                busy += dur;
-                if (dur > worst) {
-                    worst = dur;
-                    wb = b;
-                }
-                t_lo = x[8] < t_lo ? x[8] : t_lo;
-                t_hi = x[9] > t_hi ? x[9] : t_hi;
-            }
-            const double span = (double)(t_hi - t_lo) / 100.0;
-            fprintf(stderr,
-                    "[msssp] %d batches, slots %zu, delta %u, u%d: per batch %.1f passes, %.0f pulls, "
-                    "%.1f advances; wave-0 kcycles: compaction %.0f, pulls %.0f, advance %.0f, "
-                    "output %.0f, init %.0f; batch us mean %.0f, worst %.0f (batch %d: %llu passes,"
-                    " %llu pulls); span %.0f us, mean concurrency %.1f\n",
-                    nbatch, slots, dl, d16 ? 16 : 32, m[0], m[1], m[2], m[3] / 1e3, m[4] / 1e3, m[5] / 1e3,
-                    m[6] / 1e3, m[7] / 1e3, busy / nbatch, worst, wb, h[(size_t)wb * MS_PROF],
-                    h[(size_t)wb * MS_PROF + 1], span, span > 0 ? busy / span : 0.0);
-        }
-        free(h);
-        (void)hipFreeAsync(prof, st);
-    }
     return SRT_OK;
 }
 

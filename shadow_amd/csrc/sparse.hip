@@ -306,8 +306,7 @@ int srt_sparse_block_rows(int32_t n, const int32_t* rowptr, const int32_t* col, 
     if (delta == 0) delta = 8; /* bucket width of the label-correcting loop, in quanta */
     const size_t ldo = (size_t)n;
     const int nsrc = src_end - src_begin;
-    const bool force_hbm = srt_form_int("hbm", 0) != 0; /* tests: the HBM working set */
-    if (n <= srt_sparse_max_n() && !force_hbm) {
+    if (n <= srt_sparse_max_n()) {
         const size_t lds = srt_sparse_lds_bytes(n);
         SRT_HIPCHK(hipFuncSetAttribute((const void*)sssp_kernel<false>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -318,14 +318,11 @@ int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, con
     const size_t lds_row = (size_t)n * sizeof(uint32_t), lds_static = 4096;
     /* the LDS form holds few waves per CU and each wave's bucket steps are a latency chain
      * (C3, n = 20000: 2 waves/CU, 354 ms vs 70 ms for the global form at 16), so it is the
-     * default only while it still fits 8 waves per CU; SRT_FORM ws_lds=1/0 forces either form */
-    const int fl = srt_form_int("ws_lds", -1);
-    const bool ldsd = fl >= 0 ? (fl != 0 && lds_row + lds_static <= 160 * 1024)
-                              : 8 * (lds_row + lds_static) <= 160 * 1024;
+     * default only while it still fits 8 waves per CU */
+    const bool ldsd = 8 * (lds_row + lds_static) <= 160 * 1024;
     /* the kernel's slot layout: f64 reliability row, bucket ring, u32 distance row (global form),
      * padded to 8 bytes */
-    const int fr = srt_form_int("ws_relrow", -1); /* tests: force either reliability form */
-    const bool relp = fr >= 0 ? fr != 0 : local != 0;
+    const bool relp = local != 0;
     g_sparse_form = (ldsd ? 1 : 0) | (relp ? 2 : 0);
     const size_t per_slot =
         (((relp ? 2 * (size_t)n : 0) + (size_t)nb * bcap + (ldsd ? 0 : n) + 1) & ~(size_t)1) *
@@ -483,30 +480,17 @@ __global__ void wg_arcs_cmp_kernel(int n, const int2* __restrict__ rowptr, const
     }
 }
 
-/* PROF (tools only, SRT_FORM prof=1): thread 0 accumulates shader-clock cycles per phase and
- * step counts into prof[block * 16 + k]: 0 init, 1 bucket search, 2 chunk head (sums and the
- * full barrier; 10 entry load, 11 scan barrier), 3 arcs (12 owner search, 13 arc-load wait, 14
- * relaxations; 3 itself: the deferred store and the post-arc barrier),
- * 4 settle, 5 output, 6 steps, 7 chunks, 8 arc windows, 9 sources */
-#define WG_PT(k)                                                        \
-    do {                                                                \
-        if (PROF && tid == 0) {                                         \
-            const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-            pacc[k] += t_ - pt;                                         \
-            pt = t_;                                                    \
-        }                                                               \
-    } while (0)
 /* ORIG: the graph in its original vertex order (inv == NULL): the reliability row is the output
  * row itself (settle-time stores and predecessor loads go to rr), so no end-of-source gather of a
  * private relabelled row (one random line per vertex: ~40% of the kernel's memory traffic on C5,
  * profiles/r02_c5) */
-template <int WG, bool PROF = false, bool ORIG = false, bool CMP = false>
+template <int WG, bool ORIG = false, bool CMP = false>
 __global__ __launch_bounds__(WG) void wgsssp_kernel(
     int n, int src_begin, const int32_t* __restrict__ srcs, int nsrc,
     const int2* __restrict__ rowptr, const void* __restrict__ cav,
     const double* __restrict__ r, const int32_t* __restrict__ inv, uint32_t* __restrict__ lat,
     double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ ws, int nb, int bcap,
-    int* __restrict__ overflow, unsigned long long* __restrict__ prof = nullptr, int two = 0,
+    int* __restrict__ overflow, int two = 0,
     int place = 0, uint32_t* __restrict__ codes = nullptr) {
     /* place: source s0 = srcs[si] writes output row (and overflow flag) s0 - src_begin instead of
      * si. codes (CMP only): the canonical in-arc of every settled vertex v, row si (stride n):
@@ -522,8 +506,6 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
     static_assert(!CMP || ORIG, "compact arcs key ties on u: original vertex order only");
     const uint4* __restrict__ ca = reinterpret_cast<const uint4*>(cav);
     const uint2* __restrict__ cc = reinterpret_cast<const uint2*>(cav);
-    unsigned long long pacc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long pt = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     extern __shared__ uint32_t sd[]; /* packed distances, relabelled order */
     __shared__ uint32_t bcnt[256]; /* entries per bucket; the search ballots on bcnt > bst */
     __shared__ uint32_t bst[256];  /* consumed prefix of each bucket (two-level steps) */
@@ -567,8 +549,6 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
         }
         __threadfence_block();
         __syncthreads();
-        WG_PT(0);
-        if (PROF && tid == 0) pacc[9]++;
         /* deferred settle: the reliability of the lane's last settled vertex pv is stored after
          * the next chunk's arcs (or after the last step), so its two loads overlap the bucket
          * search, the next entry load and the arcs; nothing reads rel(s, pv) before a larger
@@ -602,12 +582,9 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
              * counts by then): no push of this step targets b (nd >= d + 1, and the ring is longer
              * than the largest weight), and the next search follows this step's last barrier;
              * bucket d + 1 keeps its count and records the consumed prefix */
-            WG_PT(1);
-            if (PROF && tid == 0) pacc[6]++;
             const uint2* bk = buckets + (size_t)b * bcap + st0;
             const uint2* bk1 = buckets + (size_t)b1 * bcap + st1;
             for (int c0 = 0; c0 < cnt; c0 += WG) {
-                if (PROF && tid == 0) pacc[7]++;
                 const int i = c0 + tid;
                 const int lvl = i >= n0; /* 1: an entry of bucket d + 1 */
                 const uint32_t dl = d + (uint32_t)lvl;
@@ -627,13 +604,11 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                         v = -1; /* stale: improved after it was pushed */
                     }
                 }
-                WG_PT(10);
                 /* workgroup exclusive scan of the degrees */
                 int wtot;
                 const int wex = wave_scan_excl(deg, lane, &wtot);
                 if (lane == 0) s_wtot[wv] = wtot;
                 WG_LDS_BARRIER();
-                WG_PT(11);
                 if (c0 == 0 && tid == 0) {
                     bcnt[b] = 0;
                     bst[b] = 0;
@@ -668,12 +643,10 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                 if (deg > 0 && x + deg == total && (total - 1) / WL + 1 < WG_NBLK)
                     s_blk[(total - 1) / WL + 1] = (uint16_t)tid;
                 WG_LDS_BARRIER();
-                WG_PT(2);
                 /* WG_AK arc windows per pass: the owner searches (fixed-step, unrolled) and the
                  * arc loads of every window are issued before any of them is used, so their
                  * latencies overlap instead of adding up */
                 for (int a0 = 0; a0 < total; a0 += WG * WG_AK) {
-                    if (PROF && tid == 0) pacc[8]++;
                     int own[WG_AK];
                     uint4 e[WG_AK];
                     uint2 ec[WG_AK];
@@ -718,7 +691,6 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
 #pragma unroll
                         for (int j = 0; j < WG_AK; ++j) own[j] = q[j];
                     }
-                    WG_PT(12);
 #pragma unroll
                     for (int j = 0; j < WG_AK; ++j)
                         if (a0 + j * WG + tid < total) {
@@ -728,10 +700,6 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                             else
                                 e[j] = ca[arc];
                         }
-                    if (PROF) {
-                        __builtin_amdgcn_s_waitcnt(0); /* profile only: the arc loads' wait */
-                        WG_PT(13);
-                    }
 #pragma unroll
                     for (int j = 0; j < WG_AK; ++j) {
                         if (a0 + j * WG + tid >= total) continue;
@@ -779,7 +747,6 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                                               u);
                         }
                     }
-                    WG_PT(14);
                 }
                 /* the lane's vertex of the previous chunk: its two loads (issued at that chunk's
                  * settle) have had this chunk's head and arcs to arrive */
@@ -796,7 +763,6 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                     __syncthreads();
                 else
                     WG_LDS_BARRIER();
-                WG_PT(3);
                 /* a chunk with level-1 lanes: its level-0 lanes store their reliability now, and
                  * the level-1 lanes (children of any level-0 vertex of the step) load theirs after
                  * a full barrier */
@@ -844,14 +810,12 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
                         }
                     }
                 }
-                WG_PT(4);
             }
             if (s_ovf) break;
         }
         if (pv >= 0) relp[pv] = pa * pb;
         __threadfence_block();
         __syncthreads();
-        WG_PT(1);
         /* output rows in original order, whole lines */
         for (int i = tid; i < n; i += WG) {
             const int v = ORIG ? i : inv[i];
@@ -864,10 +828,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
         }
         if (s_ovf && tid == 0) overflow[orow] = 1;
         __syncthreads();
-        WG_PT(5);
     }
-    if (PROF && tid == 0)
-        for (int k = 0; k < 16; ++k) prof[blockIdx.x * 16 + k] = pacc[k];
 }
 
 /* largest n the packed LDS row holds beside the kernel's static LDS (1024 threads: ~18 KB) */
@@ -881,10 +842,13 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
                     double* rel, int* ovf, hipStream_t st, const uint8_t* ridx,
                     const double* rtab, int place, uint32_t* codes) {
     /* two-level steps push up to d + 1 + max_w: the ring then needs max_w + 2 buckets */
-    int two = srt_form_int("wg_two", 1) != 0; /* tests: one-level steps */
-    if (max_w + 2u > 256u) two = 0;
+    const int two = max_w + 2u <= 256u;
     int nb = 1;
     while ((uint32_t)nb <= max_w + (uint32_t)two) nb <<= 1;
+    if (inv) { /* the relabelled form was retired (measured slower than the original order) */
+        srt_set_error("wgsssp: the kernel runs on the original vertex order (inv must be NULL)");
+        return SRT_E_ARG;
+    }
     if (nb > 256 || n > srt_wgsssp_max_n()) {
         srt_set_error("wgsssp: n = %d or max arc weight %u outside the kernel's range", n, max_w);
         return SRT_E_ARG;
@@ -902,8 +866,7 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     SRT_HIPCHK(hipMemcpyAsync(&last, rowptr + (n - 1), sizeof(int2), hipMemcpyDeviceToHost, st));
     SRT_HIPCHK(hipStreamSynchronize(st));
     /* compact 8-byte arcs: original order, a reliability table, w < 128, arcs < 2^20 */
-    const bool cmp = !inv && ridx && rtab && max_w < 128 && last.y < (1 << 20) &&
-                     srt_form_int("wg_compact", 1) != 0; /* tests: the 16-byte arcs */
+    const bool cmp = !inv && ridx && rtab && max_w < 128 && last.y < (1 << 20);
     g_sparse_form = 4 | (inv ? 0 : 1) | (cmp ? 2 : 0);
     if (codes && !cmp) {
         srt_set_error("wgsssp: arc codes need the compact-arc form");
@@ -935,71 +898,18 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     /* placed rows flag overflows at their row: the caller clears the flags */
     if (!place) SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)nsrc * sizeof(int), st));
     const size_t dyn = (size_t)((n + 2) / 3) * sizeof(uint32_t);
-    if (srt_form_int("prof", 0) > 0) { /* tools: per-phase cycle counts on stderr */
-        unsigned long long* prof = NULL;
-        SRT_HIPCHK(hipMalloc((void**)&prof, slots * 16 * sizeof(unsigned long long)));
-        if (cmp) {
-            SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true, true, true>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-            wgsssp_kernel<1024, true, true, true><<<(unsigned)slots, 1024, dyn, st>>>(
-                n, src_begin, srcs, nsrc, rowptr, ca, rtab, inv, lat, rel, (size_t)n, ws, nb, bcap,
-                ovf, prof, two, place, codes);
-        } else if (!inv) { /* original order: the output row is the working row */
-            SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true, true>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-            wgsssp_kernel<1024, true, true><<<(unsigned)slots, 1024, dyn, st>>>(
-                n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap,
-                ovf, prof, two, place, codes);
-        } else {
-            SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-            wgsssp_kernel<1024, true><<<(unsigned)slots, 1024, dyn, st>>>(
-                n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap,
-                ovf, prof, two, place, codes);
-        }
-        SRT_HIPCHK(hipGetLastError());
-        unsigned long long* h = (unsigned long long*)calloc(slots * 16, sizeof(*h));
-        SRT_HIPCHK(hipMemcpyAsync(h, prof, slots * 16 * sizeof(*h), hipMemcpyDeviceToHost, st));
-        SRT_HIPCHK(hipStreamSynchronize(st));
-        double tot[16] = {0};
-        for (size_t b = 0; b < slots; ++b)
-            for (int k = 0; k < 16; ++k) tot[k] += (double)h[b * 16 + k];
-        const double cyc = tot[0] + tot[1] + tot[2] + tot[3] + tot[4] + tot[5] + tot[10] + tot[11] +
-                           tot[12] + tot[13] + tot[14];
-        fprintf(stderr,
-                "[wgsssp prof] blocks %zu sources %.0f: cycles/source %.0f = init %.1f%% search "
-                "%.1f%% head %.1f%% (entry load %.1f%%, scan barrier %.1f%%, sums + full "
-                "barrier %.1f%%) arcs %.1f%% settle %.1f%% output %.1f%%; per source: steps "
-                "%.1f chunks %.1f arc windows %.1f; cycles per step %.0f\n",
-                slots, tot[9], cyc / tot[9], 100 * tot[0] / cyc, 100 * tot[1] / cyc,
-                100 * (tot[2] + tot[10] + tot[11]) / cyc, 100 * tot[10] / cyc, 100 * tot[11] / cyc,
-                100 * tot[2] / cyc, 100 * (tot[3] + tot[12] + tot[13] + tot[14]) / cyc,
-                100 * tot[4] / cyc, 100 * tot[5] / cyc, tot[6] / tot[9], tot[7] / tot[9],
-                tot[8] / tot[9], cyc / tot[6]);
-        fprintf(stderr,
-                "[wgsssp prof] arcs: owner search %.1f%% arc-load wait %.1f%% relaxations %.1f%% "
-                "deferred store + post-arc barrier %.1f%%\n",
-                100 * tot[12] / cyc, 100 * tot[13] / cyc, 100 * tot[14] / cyc, 100 * tot[3] / cyc);
-        free(h);
-        SRT_HIPCHK(hipFree(prof));
-    } else if (cmp) { /* original order, compact arcs, reliabilities from the table */
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, false, true, true>,
+    if (cmp) { /* original order, compact arcs, reliabilities from the table */
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true, true>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-        wgsssp_kernel<1024, false, true, true><<<(unsigned)slots, 1024, dyn, st>>>(
+        wgsssp_kernel<1024, true, true><<<(unsigned)slots, 1024, dyn, st>>>(
             n, src_begin, srcs, nsrc, rowptr, ca, rtab, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf,
-            nullptr, two, place, codes);
-    } else if (!inv) { /* the graph in original order: reliability straight into the output rows */
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, false, true>,
+            two, place, codes);
+    } else { /* the graph in original order: reliability straight into the output rows */
+        SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-        wgsssp_kernel<1024, false, true><<<(unsigned)slots, 1024, dyn, st>>>(
+        wgsssp_kernel<1024, true><<<(unsigned)slots, 1024, dyn, st>>>(
             n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf,
-            nullptr, two, place, codes);
-    } else {
-        SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-        wgsssp_kernel<1024><<<(unsigned)slots, 1024, dyn, st>>>(n, src_begin, srcs, nsrc, rowptr, ca, r,
-                                                               inv, lat, rel, (size_t)n, ws, nb, bcap,
-                                                               ovf, nullptr, two, place, codes);
+            two, place, codes);
     }
     SRT_HIPCHK(hipGetLastError());
     SRT_HIPCHK(hipFreeAsync(ws, st));

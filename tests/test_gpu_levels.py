@@ -50,21 +50,18 @@ def _directed_dense(n, seed, wmax):
 
 
 @pytest.mark.parametrize("kind", ["complete300", "complete1000", "ties", "directed", "c1like",
-                                  "f64form", "manyrel", "transposed", "ties_transposed"])
+                                  "manyrel", "transposed", "ties_transposed"])
 def test_levels_match_oracle(gpu, monkeypatch, kind):
     """The post pass carries r(pred, t) as an index into the build's table of distinct arc
     reliabilities: by default one target-major word per pair with the level beside it
     (lvl_pred_kernel), one transpose, then rel_pk_kernel, which writes the u32 rows too;
-    "transposed" (SRT_FORM pkw=0) keeps the u8 level rows and rel_tree_kernel; "f64form"
-    (SRT_FORM pk=0) and "manyrel" (more distinct values
-    than the table holds) take the f64 rows. "c1like" has distances past 31 quanta: the packed
+    "transposed" (SRT_FORM pkw=0) keeps the u8 level rows and rel_tree_kernel; "manyrel" (more
+    distinct values than the table holds) takes the f64 rows. "c1like" has distances past 31 quanta: the packed
     words cannot hold its levels (the transposed form, then the sweeps past 64)."""
     set_form(monkeypatch, levels="1")
-    if kind == "f64form":
-        set_form(monkeypatch, levels="1", pk="0")
     if kind in ("transposed", "ties_transposed"):
         set_form(monkeypatch, levels="1", pkw="0")
-    if kind in ("complete300", "f64form", "transposed"):
+    if kind in ("complete300", "transposed"):
         g = graphs.complete_graph(300, seed=7)
     elif kind == "complete1000":  # C2's distribution: distances up to 9 quanta
         g = graphs.complete_graph(1000, seed=2)

@@ -92,32 +92,20 @@ def test_msssp_full_tables(gpu, monkeypatch, which):
     assert np.array_equal(rel.view(np.uint64), exp["rel"].view(np.uint64)), which
 
 
-@pytest.mark.parametrize("u16", ["0", "1"])
-def test_msssp_distance_widths(gpu, monkeypatch, u16):
-    """SRT_FORM ms_u16=0/1: 32-bit working distances, or 16-bit ones (the default when the graph's
-    distance bound is below 0xFFFF; a candidate past it reads as not reached yet): the same
-    tables."""
+@pytest.mark.parametrize("scale", [1, 40])
+def test_msssp_distance_widths(gpu, monkeypatch, scale):
+    """16-bit working distances where the graph's distance bound is below 0xFFFF (a candidate
+    past it reads as not reached yet), 32-bit ones past it (the same graph with ~40x latencies,
+    still in 1-ms quanta):
+    the oracle's tables either way, the width reported in fw_block bit 16."""
     set_form(monkeypatch, kernel="ms")
-    set_form(monkeypatch, ms_u16=u16)
-    g = graphs.random_geometric(2200, seed=13)
+    g0 = graphs.random_geometric(2200, seed=13)
+    odd = (np.arange(g0.m) % 2) * 1_000_000 * (scale > 1)  # keep the quantum at 1 ms
+    g = graphs.Graph(g0.n, g0.directed, g0.src, g0.dst, g0.lat_ns * scale + odd, g0.loss)
     lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
                                 algo=ALGO_SPARSE_SSSP)
     assert st.dist_enc == 3
-    exp = oracle.table(_el(g), True, oracle.ORC_INT_NS, 8, raw=True)
-    assert np.array_equal(lat, exp["lat_int"])
-    assert np.array_equal(rel.view(np.uint64), exp["rel"].view(np.uint64))
-
-
-@pytest.mark.parametrize("delta", ["1", "3", "100000"])
-def test_msssp_bucket_widths(gpu, monkeypatch, delta):
-    """SRT_FORM ms_delta: bucket width 1 (Dial-like), 3, and one bucket for everything (plain
-    frontier Bellman-Ford) reach the same fixed point."""
-    set_form(monkeypatch, kernel="ms")
-    set_form(monkeypatch, ms_delta=delta)
-    g = graphs.random_geometric(2500, seed=11)
-    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
-                                algo=ALGO_SPARSE_SSSP)
-    assert st.dist_enc == 3
+    assert bool(st.fw_block & 16) == (scale == 1), st.fw_block
     exp = oracle.table(_el(g), True, oracle.ORC_INT_NS, 8, raw=True)
     assert np.array_equal(lat, exp["lat_int"])
     assert np.array_equal(rel.view(np.uint64), exp["rel"].view(np.uint64))
@@ -180,27 +168,23 @@ def test_msssp_c3_compact_sources_and_ties(gpu):
     # batch budget, the single-source kernels without one
     exp = oracle.sssp_rows(el, 0, 100, nthreads=16)
     off = np.arange(g.n)[None, :] != np.arange(100)[:, None]
-    for maxb, enc in ((None, 3), ("0", 1)):
-        with form_env(**({} if maxb is None else {"ms_maxb": maxb})):
-            st2 = BuildStats()
-            sg.rows(0, 100, lat.data_ptr(), rel.data_ptr(), None, st2)
-            torch.cuda.synchronize()
-        assert st2.dist_enc == enc, (maxb, st2.dist_enc)
-        got = lat[:100].cpu().numpy().view(np.uint32).astype(np.uint64) * np.uint64(sg.quantum_ns)
-        assert np.array_equal(np.where(off, got, 0), np.where(off, exp["lat_int"], 0)), maxb
-        r = rel[:100].cpu().numpy()
-        assert np.array_equal(r[off].view(np.uint64), exp["rel"][off].view(np.uint64)), maxb
+    st2 = BuildStats()
+    sg.rows(0, 100, lat.data_ptr(), rel.data_ptr(), None, st2)
+    torch.cuda.synchronize()
+    assert st2.dist_enc == 3, st2.dist_enc
+    got = lat[:100].cpu().numpy().view(np.uint32).astype(np.uint64) * np.uint64(sg.quantum_ns)
+    assert np.array_equal(np.where(off, got, 0), np.where(off, exp["lat_int"], 0))
+    r = rel[:100].cpu().numpy()
+    assert np.array_equal(r[off].view(np.uint64), exp["rel"][off].view(np.uint64))
     sg.free()
 
 
 @pytest.mark.parametrize("which", ["rgg3000", "dring"])
 def test_msssp_source_list(gpu, monkeypatch, which):
-    """srt_sparse_graph_rows_list with an unordered source list of 150 vertices (three batches,
-    the last one partial; the hop radius lifted so the scattered sources still share batches):
-    row i is source srcs[i]."""
+    """srt_sparse_graph_rows_list with an unordered source list of 150 scattered vertices (small
+    clusters, each a batch of its own within the batch budget): row i is source srcs[i]."""
     import torch
     set_form(monkeypatch, kernel="ms")
-    set_form(monkeypatch, ms_rmax="100000")  # cluster even scattered sources
     g = _graph(which)
     rng = np.random.default_rng(77)
     srcs = rng.choice(g.n, 150, replace=False).astype(np.int32)
@@ -221,19 +205,12 @@ def test_msssp_source_list(gpu, monkeypatch, which):
     sg.free()
 
 
-@pytest.mark.parametrize("rmax,maxb,enc", [("0", "0", 1), ("24", "4", 3), ("24", None, 3)])
-def test_msssp_compact_and_scattered_sources(gpu, monkeypatch, rmax, maxb, enc):
+def test_msssp_compact_and_scattered_sources(gpu, monkeypatch):
     """A source list mixing a compact region (the 200 vertices nearest a point of the unit
-    square) with 40 scattered vertices. Clusters that fill 48 lanes within the hop radius take the
-    multi-source kernel; the small ones do too while all batches fit the batch budget
-    (SRT_FORM ms_maxb, default two per CU), else they take the single-source kernels and are
-    scattered to their rows: budget 4 splits the set, radius 0 with budget 0 sends every source
-    there (dist_enc 1)."""
+    square) with 40 scattered vertices: clusters that fill 48 lanes within the hop radius and the
+    small ones all take the multi-source kernel while the batches fit the budget (two per CU)."""
     import torch
     set_form(monkeypatch, kernel="ms")
-    set_form(monkeypatch, ms_rmax=rmax)
-    if maxb is not None:
-        set_form(monkeypatch, ms_maxb=maxb)
     n = 4000
     g = graphs.random_geometric(n, seed=3)
     idx = np.arange(n, dtype=np.uint64)
@@ -249,11 +226,37 @@ def test_msssp_compact_and_scattered_sources(gpu, monkeypatch, rmax, maxb, enc):
     st = BuildStats()
     sg.rows_list(ds.data_ptr(), len(srcs), lat.data_ptr(), rel.data_ptr(), None, st)
     torch.cuda.synchronize()
-    assert st.dist_enc == enc, st.dist_enc
+    assert st.dist_enc == 3, st.dist_enc
     got = lat.cpu().numpy().view(np.uint32).astype(np.uint64) * np.uint64(sg.quantum_ns)
     exp = oracle.sssp_list(_el(g), srcs, nthreads=16)
     off = np.arange(g.n)[None, :] != srcs[:, None]
     assert np.array_equal(np.where(off, got, 0), np.where(off, exp["lat_int"], 0))
     r = rel.cpu().numpy()
+    assert np.array_equal(r[off].view(np.uint64), exp["rel"][off].view(np.uint64))
+    sg.free()
+
+
+def test_msssp_past_the_batch_budget(gpu):
+    """Every source of a 40,000-vertex RGG in one call: more clusters than the batch budget (two
+    per CU), so the batches past it go to the single-source kernels and are scattered to their
+    rows. Sampled rows from the whole range against the oracle."""
+    import torch
+    g = graphs.random_geometric(40000, seed=17)
+    sg = SparseGraph(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
+    lat = torch.empty((g.n, g.n), dtype=torch.int32, device="cuda")
+    rel = torch.empty((g.n, g.n), dtype=torch.float64, device="cuda")
+    st = BuildStats()
+    sg.rows(0, g.n, lat.data_ptr(), rel.data_ptr(), None, st)
+    torch.cuda.synchronize()
+    assert st.dist_enc == 3, st.dist_enc
+    rows = np.random.default_rng(4).choice(g.n, 64, replace=False).astype(np.int32)
+    idx = torch.from_numpy(rows.astype(np.int64)).cuda()
+    got = lat.index_select(0, idx).cpu().numpy().view(np.uint32).astype(np.uint64) \
+        * np.uint64(sg.quantum_ns)
+    r = rel.index_select(0, idx).cpu().numpy()
+    del lat, rel
+    exp = oracle.sssp_list(_el(g), rows, nthreads=16)
+    off = np.arange(g.n)[None, :] != rows[:, None]
+    assert np.array_equal(np.where(off, got, 0), np.where(off, exp["lat_int"], 0))
     assert np.array_equal(r[off].view(np.uint64), exp["rel"][off].view(np.uint64))
     sg.free()

@@ -200,14 +200,10 @@ def test_dense_device_api_and_sharded_single_rank(gpu):
     assert torch.equal(lat2[:n, :n], lat[:n, :n]) and torch.equal(rel2[:n, :n], rel[:n, :n])
 
 
-@pytest.mark.parametrize("hop_ms,enc,sym,la,env", [
-    (1, 4, "1", None, {}), (1, 7, "1", "1", {}), (1, 6, "1", "1", {"kb": "128"}),
-    (1, 5, "1", "1", {"kb": "64"}),
-    (1, 3, "0", None, {}),
-    (160, 2, "1", None, {}), (400, 1, "1", None, {}),
-    (1, 11, "1", None, {"square": "1"}), (1, 11, "0", None, {"square": "1"}),
-    (160, 2, "1", None, {"square": "1"})])
-def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym, la, env):
+@pytest.mark.parametrize("hop_ms,enc,sym,env", [
+    (1, 4, "1", {}), (1, 3, "0", {}), (160, 2, "1", {}), (400, 1, "1", {}),
+    (1, 11, "1", {"square": "1"}), (1, 11, "0", {"square": "1"}), (160, 2, "1", {"square": "1"})])
+def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym, env):
     """Each distance encoding of the dense build (fw16.hip) is exact where it is chosen.
 
     A 256-vertex ring with hop latencies hop_ms / hop_ms+1 (gcd 1 ms) plus a few chords: the
@@ -215,17 +211,14 @@ def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym, la, e
     0x3DFF), 160 saturates it and falls back to the u16 pk_min path (cap 0x7FFF), and 400
     saturates both and ends on the u32 kernels. Every tier must match the oracle bit for bit.
     The graph is undirected, so the f16-compare tier runs its upper-triangle form (encoding 4)
-    unless SRT_FORM sym=0 forces every tile (encoding 3); lookahead=1 forces its two
-    update streams, with 256-pivot rounds (encoding 7, the default from n = 8192), 128-pivot
-    rounds under kb=128 (encoding 6) or 64-pivot rounds under kb=64 (encoding 5). The round
+    unless SRT_FORM sym=0 forces every tile (encoding 3); the two-stream forms (encodings 6 and 7)
+    start at n = 8,192 (test_dense_round_sizes_multi_round). The round
     schedules are forced with square=0: by default a matrix of ld <= 2048 takes min-plus squaring to a fixed
     point (encoding 11) -- on this ring, ~128-arc paths, so seven or more passes; at hop 160 the
     squaring saturates the f16-compare cap and the build falls back to the u16 rounds (2).
     """
     set_form(monkeypatch, sym=sym, square="0")
     set_form(monkeypatch, **env)
-    if la is not None:
-        set_form(monkeypatch, lookahead=la)
     n = 256
     rng = np.random.default_rng(hop_ms)
     src = list(range(n))
@@ -246,15 +239,14 @@ def test_dense_distance_encoding_tiers(gpu, monkeypatch, hop_ms, enc, sym, la, e
     assert st.dist_enc == enc, f"expected encoding {enc}, build used {st.dist_enc}"
 
 
-@pytest.mark.parametrize("n,kb", [(1000, "256"), (1000, "128"), (1536, "256")])
-def test_dense_round_sizes_multi_round(gpu, monkeypatch, n, kb):
-    """The two-stream schedules with several 256- / 128-pivot rounds (the encoding-tier test has
-    one or two): a ring with chords, long enough for distances of a few hundred quanta, against
-    the oracle bit for bit. Covers the chain stream's cross updates between a round's panels and
-    the rest launches that start past them (SRT_FORM square=0: not the small-matrix squaring)."""
-    set_form(monkeypatch, square="0")
-    set_form(monkeypatch, lookahead="1")
-    set_form(monkeypatch, kb=kb)
+@pytest.mark.parametrize("n,enc", [(8192, 7), (8200, 6)])
+def test_dense_round_sizes_multi_round(gpu, monkeypatch, n, enc):
+    """The two-stream schedules of the one-GPU FW (from ld = 8,192): 256-pivot rounds where ld is
+    a multiple of 256 (encoding 7), 128-pivot rounds otherwise (n = 8,200: ld = 8,320, encoding
+    6). A ring with chords, distances of a few thousand quanta (past the level budget, so the FW
+    runs), sampled rows against the oracle bit for bit: the chain stream's cross updates between
+    a round's panels and the rest launches that start past them."""
+    set_form(monkeypatch, levels="0")
     rng = np.random.default_rng(n)
     src = list(range(n))
     dst = [(i + 1) % n for i in range(n)]
@@ -269,22 +261,24 @@ def test_dense_round_sizes_multi_round(gpu, monkeypatch, n, kb):
                      np.array(lat, np.int64), loss)
     got_lat, got_rel, st = build_tables(g.n, False, g.src, g.dst, g.lat_ns, g.loss,
                                         algo=ALGO_DENSE_FW)
-    assert st.dist_enc == (7 if kb == "256" else 6)
-    exp = _oracle(g)
-    assert_tables(got_lat, got_rel, exp["lat_int"], exp["rel"], f"rounds of {kb}, n={n}")
+    assert st.dist_enc == enc, st.dist_enc
+    rows = np.r_[0:8, n // 2:n // 2 + 8, n - 8:n].astype(np.int32)
+    exp = oracle.sssp_list(oracle.EdgeList(g.n, False, g.src, g.dst, g.lat_ns, g.loss), rows,
+                           nthreads=8)
+    off = np.arange(n)[None, :] != rows[:, None]
+    assert np.array_equal(np.where(off, got_lat[rows], 0), np.where(off, exp["lat_int"], 0))
+    err = np.abs(got_rel[rows] - exp["rel"]) / np.maximum(np.abs(exp["rel"]), 1e-300)
+    assert float(err[off].max()) <= REL_TOL
 
 
 @pytest.mark.parametrize("n,seed", [(700, 8), (1000, 2)])
 def test_dense_lookahead_schedule_one_gpu(gpu, monkeypatch, n, seed):
-    """The lookahead schedules forced on one GPU must give the oracle's tables: through the
-    single-GPU entry the symmetric rounds on two update streams (fw16_build_sym: static tile
-    sets by I + J parity, next diagonal / panel / refresh on the high-priority stream), through
-    the 1-rank sharded entry the sharded FW's two-stream schedule (split update, pivot panel k+1
-    on the high-priority stream, double-buffered receive panels)."""
+    """The single-GPU entry (upper-triangle rounds on one stream) and the 1-rank sharded entry
+    (the sharded FW's lookahead schedule: split update, pivot panel k+1 on the high-priority
+    stream, double-buffered receive panels) give the oracle's tables, and the same ones."""
     import torch
     from shadow_amd._lib import lib
     set_form(monkeypatch, square="0")
-    set_form(monkeypatch, lookahead="1")
     ld = (n + 127) // 128 * 128
     L = lib()
     w = torch.empty((ld, ld), dtype=torch.int32, device="cuda")
@@ -401,30 +395,6 @@ def test_virtual_ranks_sharded_build(gpu, monkeypatch, kind, ranks):
                 "ring_u32": 1}
     if kind in want_enc:
         assert st.dist_enc == want_enc[kind], f"encoding {st.dist_enc}"
-
-
-@pytest.mark.parametrize("kind", ["dense", "dense2000", "ring_f16"])
-@pytest.mark.parametrize("ranks", [2, 3])
-@pytest.mark.parametrize("kb", ["64", "128"])
-def test_virtual_ranks_sharded_64_pivot_rounds(gpu, monkeypatch, kind, ranks, kb):
-    """SRT_FORM shkb=64 keeps the 64-pivot sharded symmetric rounds (encoding 4); the default
-    takes 128-pivot rounds (encoding 8; the 256-pivot form, encoding 9, measured slower and was
-    retired in round 4): same tables. The graphs pad to ld = 768, 2048 and 1024 (6, 16 and 8 tile
-    rows); at 2 ranks of ld = 768 a band straddles the rank boundary (rows 0-383 | 384-767)."""
-    monkeypatch.setenv("SRT_VIRTUAL_RANKS", str(ranks))
-    set_form(monkeypatch, shkb=kb)
-    if kind == "dense":
-        g = graphs.complete_graph(700, seed=9)
-    elif kind == "dense2000":
-        g = graphs.complete_graph(2000, seed=13)
-    else:
-        g = _ring_graph(1000, 1, 1)
-    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
-                                algo=ALGO_DENSE_FW, ngpus=1)
-    exp = _oracle(g)
-    assert_tables(lat, rel, exp["lat_int"], exp["rel"], f"virtual x{ranks} {kind} {kb}-pivot")
-    want = 4 if kb == "64" else 8
-    assert st.dist_enc == want, f"encoding {st.dist_enc}"
 
 
 def test_packet_path_trace_replay(gpu):

@@ -1,7 +1,7 @@
 """Sparse SSSP through the device C-ABI (srt_sparse_graph_*) and the table builds, every kernel
 form: the wave-per-source bucket kernel (C3-shaped RGG), the workgroup-per-source kernel with the
 distance row packed in LDS (C5-shaped 100k-node Barabasi-Albert graph), and the block kernel
-(sparse.hip, SRT_FORM hbm=1 / bucket overflows).
+(sparse.hip: LDS working set, HBM past ~20k vertices, bucket overflows).
 
 Latency bit-exact in integer ns, reliability within 1e-12 relative (north_star). Every row is its
 own source's (no mirror), compared with oracle.sssp_rows / the oracle's raw table off the
@@ -22,9 +22,10 @@ REL_TOL = 1e-12
 
 @pytest.fixture(autouse=True)
 def _single_source_kernels(monkeypatch):
-    """These tests pin the single-source kernels; the multi-source kernel that AUTO gives local
-    graphs (msssp.hip, dist_enc 3) has its own file, tests/test_gpu_msssp.py."""
-    set_form(monkeypatch, ms="0")
+    """These tests pin the single-source kernels (SRT_FORM kernel=wave unless a test names
+    another); the multi-source kernel that AUTO gives local graphs (msssp.hip, dist_enc 3) has
+    its own file, tests/test_gpu_msssp.py."""
+    set_form(monkeypatch, kernel="wave")
 
 
 def _rows_on_gpu(sg, s0, s1, torch, stats=None):
@@ -59,36 +60,35 @@ def test_c3_shape_rgg_20000_wave_kernel_rows(gpu):
     _check_rows(g, [(0, 96), (9_950, 10_050), (19_900, 20_000)], torch, want_enc=1)
 
 
-def test_c5_shape_ba_100000_workgroup_kernel_rows(gpu):
+def test_c5_shape_ba_100000_workgroup_kernel_rows(gpu, monkeypatch):
     """C5's graph takes the workgroup kernel (srt_build_stats.dist_enc == 2 for sparse builds)."""
     import torch
+    set_form(monkeypatch, kernel="auto")
     g = graphs.barabasi_albert(100_000, seed=5)
     _check_rows(g, [(0, 48), (50_000, 50_016), (99_984, 100_000)], torch, want_enc=2)
 
 
-@pytest.mark.parametrize("which", ["rgg3000", "ba2000", "directed"])
-def test_hbm_workset_forced_full_tables(gpu, monkeypatch, which):
-    set_form(monkeypatch, hbm="1")
-    if which == "rgg3000":
-        g = graphs.random_geometric(3000, seed=3)
-    elif which == "ba2000":
-        g = graphs.barabasi_albert(2000, seed=5)
+@pytest.mark.parametrize("which", ["rgg21000", "ba21000", "directed21000"])
+def test_block_kernel_hbm_workset_rows(gpu, monkeypatch, which):
+    """The block kernel past srt_sparse_max_n() (~20,160 vertices): its working set in a
+    per-workgroup HBM slot instead of LDS, on sampled row ranges."""
+    import torch
+    set_form(monkeypatch, kernel="block")
+    n = 21000
+    if which == "rgg21000":
+        g = graphs.random_geometric(n, seed=3)
+    elif which == "ba21000":
+        g = graphs.barabasi_albert(n, seed=5)
     else:
         rng = np.random.default_rng(12)
-        n, m = 400, 3000
+        m = 8 * n
         ring = np.arange(n)
         src = np.concatenate([rng.integers(0, n, m), ring, ring]).astype(np.int32)
         dst = np.concatenate([rng.integers(0, n, m), (ring + 1) % n, ring]).astype(np.int32)
         lat = (rng.integers(1, 20, len(src)) * 1_000_000).astype(np.int64)
         loss = rng.integers(0, 300, len(src)) / 10000.0
         g = graphs.Graph(n, True, src, dst, lat, loss)
-    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
-                                algo=ALGO_SPARSE_SSSP)
-    exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss),
-                       True, oracle.ORC_INT_NS, 8, raw=True)
-    assert np.array_equal(lat, exp["lat_int"])
-    err = np.abs(rel - exp["rel"]) / np.maximum(np.abs(exp["rel"]), 1e-300)
-    assert float(err.max()) <= REL_TOL
+    _check_rows(g, [(0, 48), (n - 48, n)], torch)
 
 
 @pytest.mark.parametrize("which", ["rgg3000", "directed"])
@@ -132,17 +132,20 @@ def test_wave_kernel_matches_block_kernel_c3_rows(gpu, monkeypatch):
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
 
-@pytest.mark.parametrize("which", ["rgg3000", "ba2000", "directed"])
-@pytest.mark.parametrize("lds,relrow", [("0", "0"), ("0", "1"), ("1", "0"), ("1", "1")])
-def test_wave_kernel_working_row_forms(gpu, monkeypatch, which, lds, relrow):
-    """SRT_FORM ws_lds=0/1 (working distance row in global memory or in LDS) x ws_relrow=0/1
-    (reliability written to the output rows at settle time, or kept in a relabelled row and
-    gathered at the end): every form gives the same exact tables."""
-    set_form(monkeypatch, ws_lds=lds, ws_relrow=relrow)
+@pytest.mark.parametrize("which", ["rgg3000", "rgg6000", "ba20000", "directed"])
+def test_wave_kernel_working_row_forms(gpu, which):
+    """The wave kernel's forms: working distance row in LDS while eight rows fit a CU (n <= 4,096)
+    or in global memory, and reliability kept in a relabelled row gathered at the end (local
+    graphs) or written to the output rows at settle time (ba20000, not local). The same exact
+    rows either way (fw_block bits 1 and 2 name the form)."""
+    import torch
+    from shadow_amd._lib import BuildStats
     if which == "rgg3000":
         g = graphs.random_geometric(3000, seed=3)
-    elif which == "ba2000":
-        g = graphs.barabasi_albert(2000, seed=5)
+    elif which == "rgg6000":
+        g = graphs.random_geometric(6000, seed=4)
+    elif which == "ba20000":
+        g = graphs.barabasi_albert(20000, seed=5)
     else:
         rng = np.random.default_rng(12)
         n, m = 400, 3000
@@ -152,13 +155,13 @@ def test_wave_kernel_working_row_forms(gpu, monkeypatch, which, lds, relrow):
         lat = (rng.integers(1, 20, len(src)) * 1_000_000).astype(np.int64)
         loss = rng.integers(0, 300, len(src)) / 10000.0
         g = graphs.Graph(n, True, src, dst, lat, loss)
-    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
-                                algo=ALGO_SPARSE_SSSP)
-    exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss),
-                       True, oracle.ORC_INT_NS, 8, raw=True)
-    assert np.array_equal(lat, exp["lat_int"])
-    err = np.abs(rel - exp["rel"]) / np.maximum(np.abs(exp["rel"]), 1e-300)
-    assert float(err.max()) <= REL_TOL
+    sg = SparseGraph(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss)
+    st = BuildStats()
+    _rows_on_gpu(sg, 0, 1, torch, st)
+    sg.free()
+    want = {"rgg3000": 3, "rgg6000": 2, "ba20000": 0, "directed": 3}[which]
+    assert st.fw_block & 3 == want, st.fw_block
+    _check_rows(g, [(0, 64), (g.n - 64, g.n)], torch, want_enc=1)
 
 
 @pytest.mark.parametrize("which", ["ba2000", "ba3000_w20", "rgg3000"])
@@ -198,15 +201,14 @@ def test_workgroup_kernel_overflow_fallback(gpu, monkeypatch, bcap):
     assert np.array_equal(rel, exp["rel"])
 
 
-@pytest.mark.parametrize("form", [{}, {"wg_compact": "0"}, {"wg_order": "cm"}])
-@pytest.mark.parametrize("which", ["ba2000", "ba2500_many_losses"])
-def test_workgroup_kernel_forms(gpu, monkeypatch, form, which):
-    """The workgroup kernel's forms give the same exact tables: original vertex order with compact
-    8-byte arcs and the table of distinct reliabilities (default when the graph has <= 256 of
-    them), original order with 16-byte arcs (SRT_FORM wg_compact=0, or > 256 distinct losses),
-    and the Cuthill-McKee relabelling with a private reliability row (wg_order=cm)."""
-    set_form(monkeypatch, kernel="wg", **form)
-    g = graphs.barabasi_albert(2000 if which == "ba2000" else 2500, seed=7)
+@pytest.mark.parametrize("which", ["ba2000", "ba2500_many_losses", "ba2000_w130"])
+def test_workgroup_kernel_forms(gpu, monkeypatch, which):
+    """The workgroup kernel's forms give the same exact tables: compact 8-byte arcs with the table
+    of distinct reliabilities (<= 256 of them, weights < 128 quanta), or 16-byte arcs (> 256
+    distinct losses, or weights of 128 quanta and more); fw_block bit 2 names the form."""
+    set_form(monkeypatch, kernel="wg")
+    g = graphs.barabasi_albert(2500 if which == "ba2500_many_losses" else 2000, seed=7,
+                               lat_max=130 if which == "ba2000_w130" else 100)
     if which == "ba2500_many_losses":  # continuous losses: one distinct reliability per edge
         rng = np.random.default_rng(3)
         g = graphs.Graph(g.n, g.directed, g.src, g.dst, g.lat_ns, rng.random(g.m) * 0.05)
@@ -215,36 +217,18 @@ def test_workgroup_kernel_forms(gpu, monkeypatch, form, which):
     exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss),
                        True, oracle.ORC_INT_NS, 8, raw=True)
     assert st.dist_enc == 2
+    assert st.fw_block & 7 == (7 if which == "ba2000" else 5), st.fw_block
     assert np.array_equal(lat, exp["lat_int"])
     assert np.array_equal(rel, exp["rel"])
 
 
-@pytest.mark.parametrize("two", ["0", "1"])
 @pytest.mark.parametrize("lat_max", [1, 2, 20, 127])
-def test_workgroup_kernel_two_level_steps(gpu, monkeypatch, two, lat_max):
-    """SRT_FORM wg_two: a Dial step of the workgroup kernel settles buckets d and d + 1 together (the
-    default) or bucket d alone. Weights of 1..2 quanta push into d + 1 during nearly every step
-    (the consumed-prefix counts); 127 quanta is the largest compact-arc weight, where the bucket
-    ring must hold max_w + 2 buckets. Both forms give the exact tables."""
-    set_form(monkeypatch, kernel="wg", wg_two=two)
+def test_workgroup_kernel_two_level_steps(gpu, monkeypatch, lat_max):
+    """A Dial step of the workgroup kernel settles buckets d and d + 1 together. Weights of 1..2
+    quanta push into d + 1 during nearly every step (the consumed-prefix counts); 127 quanta is
+    the largest compact-arc weight, where the bucket ring must hold max_w + 2 buckets."""
+    set_form(monkeypatch, kernel="wg")
     g = graphs.barabasi_albert(2000, seed=9, lat_max=lat_max)
-    lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
-                                algo=ALGO_SPARSE_SSSP)
-    exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss),
-                       True, oracle.ORC_INT_NS, 8, raw=True)
-    assert st.dist_enc == 2
-    assert np.array_equal(lat, exp["lat_int"])
-    assert np.array_equal(rel, exp["rel"])
-
-
-@pytest.mark.parametrize("knobs", [{"prof": "1"}, {"prof": "1", "wg_compact": "0"},
-                                   {"wg_order": "cm"}, {"prof": "1", "wg_order": "cm"}])
-def test_workgroup_kernel_launch_knobs(gpu, monkeypatch, knobs):
-    """Every launch path of srt_wgsssp_rows once: the per-phase profile form and the
-    plain form on the original vertex order (ORIG, no inverse permutation) with 8- or 16-byte
-    arcs, or on the Cuthill-McKee order; exact tables either way."""
-    set_form(monkeypatch, kernel="wg", **knobs)
-    g = graphs.barabasi_albert(1800, seed=10, lat_max=3)
     lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
                                 algo=ALGO_SPARSE_SSSP)
     exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss),
@@ -259,7 +243,6 @@ def test_workgroup_kernel_two_level_stress(gpu, monkeypatch):
     buckets' reset raced the other waves' bucket search; it now follows the first chunk's scan
     barrier). A race shows up as wrong rows or a hang; the test runs under the suite timeout."""
     set_form(monkeypatch, kernel="wg")
-    set_form(monkeypatch, wg_two="1")
     g = graphs.barabasi_albert(12000, seed=11, lat_max=2)
     lat, rel, st = build_tables(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
                                 algo=ALGO_SPARSE_SSSP)

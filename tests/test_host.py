@@ -316,3 +316,21 @@ def test_bench_parity_rows_cover_first_and_last_rank(native):
     lat2[1, 5] += 1
     r = bench.compare_rows(sample, 6, lat2, rel2, lat, rel)
     assert not r["lat_bit_exact"]
+
+
+def test_form_keys_documented_and_few():
+    """SRT_FORM: the library reads at most ten keys, every one of them listed
+    in the §5 table, and the table lists no key the library does not read."""
+    import glob
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    used = set()
+    for f in glob.glob(os.path.join(root, "shadow_amd", "csrc", "*.*")):
+        used |= set(re.findall(r'srt_form_(?:int|is)\("([a-z0-9_]+)"', open(f).read()))
+    doc = open(os.path.join(root, "INTEGRATION.md")).read()
+    sec = doc[doc.index("## 5."):]
+    sec = sec[:sec.index("\n## ", 4)] if "\n## " in sec[4:] else sec
+    listed = set(re.findall(r"^\| `([a-z0-9_]+)` \|", sec, re.M)) - {"SRT_LOG_LEVEL",
+                                                                    "SRT_VIRTUAL_RANKS", "SRT_FORM"}
+    assert len(used) <= 10, sorted(used)
+    assert used == listed, (sorted(used - listed), sorted(listed - used))

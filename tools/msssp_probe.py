@@ -1,5 +1,6 @@
-"""Time the multi-source sparse kernel (msssp.hip) on a bench graph and print its per-batch
-profile (SRT_FORM prof=1: lines on stderr). python tools/msssp_probe.py c3 [--reps 2]"""
+"""Time the multi-source sparse kernel (msssp.hip) on a bench graph (the per-batch phase
+profile of round 2 was retired from the product; rocprofv3 gives the kernel time).
+python tools/msssp_probe.py c3 [--reps 2]"""
 import argparse
 import os
 import sys
