@@ -969,7 +969,7 @@ __global__ __launch_bounds__(512) void rel_sweeps_kernel(int n, int ld, int row0
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) atomicMax(max_depth, depth);
+    if (threadIdx.x == 0) srt_max_once(max_depth, depth);
 }
 
 /* Reliability in increasing-distance order, one workgroup per local source row, in place: the
@@ -1066,7 +1066,7 @@ __global__ __launch_bounds__(NT) void rel_levels_kernel(int n, int ld, int row0,
         __threadfence_block();
         __syncthreads();
     }
-    if (tid == 0) atomicMax(max_depth, (int)mx);
+    if (tid == 0) srt_max_once(max_depth, (int)mx);
 }
 
 /* The same level-order product with the row held on chip: rel_levels_kernel's passes touch the
@@ -1165,7 +1165,8 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
     for (int i = 0; i < PER; ++i) { /* mark the parents */
         const uint32_t l = (lv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
         const uint32_t u = spu[tid + i * NT];
-        if (l && u != 0xFFFFu && (int)u != s) atomicOr(&par[u >> 5], 1u << (u & 31));
+        const uint32_t bit = 1u << (u & 31); /* tested first: ~one atomic per parent */
+        if (l && u != 0xFFFFu && (int)u != s && !(par[u >> 5] & bit)) atomicOr(&par[u >> 5], bit);
     }
     __syncthreads();
     /* exclusive prefix of the parent counts over the bitmap words (one word per thread) */
@@ -1252,7 +1253,7 @@ __global__ __launch_bounds__(NT) void rel_tree_kernel(int n, int ld, int row0,
     }
     if (tid == 0) {
         rr[s] = 1.0;
-        atomicMax(max_depth, (int)mx);
+        srt_max_once(max_depth, (int)mx);
     }
 }
 
@@ -1347,7 +1348,11 @@ __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int ro
         for (int e = 0; e < 4; ++e) {
             const uint32_t w = e4[e], l = w >> 27, u = w & 0xFFFFu;
             mx = max(mx, l);
-            if (l && (int)u != s) atomicOr(&par[u >> 5], 1u << (u & 31));
+            /* a row's 32k targets name only its ~1-3k parents: test before the atomic, so the
+             * LDS atomics are ~one per parent instead of one per target (hub parents' words
+             * would otherwise serialise thousands of them) */
+            const uint32_t bit = 1u << (u & 31);
+            if (l && (int)u != s && !(par[u >> 5] & bit)) atomicOr(&par[u >> 5], bit);
         }
     }
     /* opaque words from here on: else the compiler keeps every word's decoded fields live
@@ -1455,7 +1460,7 @@ __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int ro
         /* one piece at a time: hoisting every piece's LDS reads costs the second row per CU */
         __builtin_amdgcn_sched_barrier(0);
     }
-    if (tid == 0) atomicMax(max_depth, (int)mx);
+    if (tid == 0) srt_max_once(max_depth, (int)mx);
 }
 
 /* rel_pk_kernel at the row's width, then the sweeps for the rows over the parent cap */
@@ -1615,7 +1620,7 @@ __global__ __launch_bounds__(64 * ORD_WAVES) void rel_order_kernel(int n, int ld
         if (lane == 0) {
             __hip_atomic_store(rr + s, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             only[row] = 0;
-            atomicMax(max_depth, (int)mx);
+            srt_max_once(max_depth, (int)mx);
         }
     }
 }
@@ -1669,7 +1674,8 @@ __global__ __launch_bounds__(DEEP_NT) void rel_deep_kernel(int n, int ld, int ro
         const int p = pr[t];
         if (t == s || x >= SRT_INF || p < 0) continue;
         mx = max(mx, x);
-        if (p != s) atomicOr(&par[p >> 5], 1u << (p & 31));
+        const uint32_t bit = 1u << (p & 31); /* tested first: ~one atomic per parent */
+        if (p != s && !(par[p >> 5] & bit)) atomicOr(&par[p >> 5], bit);
     }
     for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
     if (lane == 0) red[tid >> 6] = mx;
@@ -1773,7 +1779,7 @@ __global__ __launch_bounds__(DEEP_NT) void rel_deep_kernel(int n, int ld, int ro
     }
     if (tid == 0) {
         only[row] = 0;
-        atomicMax(max_depth, (int)mx);
+        srt_max_once(max_depth, (int)mx);
     }
 }
 

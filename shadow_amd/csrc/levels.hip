@@ -40,11 +40,17 @@
 /* COUNT: per (target, weight) histogram of arcs with 1 <= w <= LVL_WMAX; FILL: the arcs (k | w << 16)
  * at cursor positions from off (weights above lmax were masked out of off). Rows form: local row
  * jj of w is target row0 + jj's in-arc row (undirected). */
-/* The count pass also keeps each row's light arcs (w <= LVL_STASH_W, up to LVL_STASH_CAP of them;
- * C4: ~1,050 per row) in a stash, so the fill reads them instead of the whole w row again (when
- * lmax <= LVL_STASH_W and the row's arcs fit). */
+/* The count pass also keeps each row's light arcs (w <= LVL_STASH_W; C4: ~1,050 per row) in a
+ * stash, so the fill reads them instead of the whole w row again (when lmax <= LVL_STASH_W and
+ * the row's arcs fit). Wave q of the row's workgroup scans the row's q-th quarter and appends
+ * its light arcs in vertex order (a ballot prefix per step) to its own LVL_STASH_SEG-entry
+ * segment, so the stash holds the row's light arcs in vertex order. The fill then places them by
+ * weight in that order (per-wave counts, then a ballot rank per weight): every target's in-arcs
+ * come out sorted by (weight, source) with no sort pass. A segment that overflows marks the
+ * row (-1) and counts in *sovf: that build takes the full-row fill and the segmented sort. */
 #define LVL_STASH_W 32
-#define LVL_STASH_CAP 2048
+#define LVL_STASH_SEG 512
+#define LVL_STASH_CAP (4 * LVL_STASH_SEG)
 template <bool FILL>
 __global__ __launch_bounds__(256) void lvl_arcs_rows_kernel(int n, int ld, int row0,
                                                             const uint32_t* __restrict__ w,
@@ -55,72 +61,132 @@ __global__ __launch_bounds__(256) void lvl_arcs_rows_kernel(int n, int ld, int r
                                                             double* __restrict__ ar = nullptr,
                                                             unsigned long long* __restrict__ dkey = nullptr,
                                                             uint32_t* __restrict__ stash = nullptr,
-                                                            int32_t* __restrict__ scnt = nullptr) {
+                                                            int32_t* __restrict__ scnt = nullptr,
+                                                            unsigned long long* __restrict__ sovf = nullptr) {
     __shared__ int h[LVL_STRIDE];
     __shared__ unsigned long long s_key[4];
-    __shared__ int s_n;
+    __shared__ int wc[4][LVL_STASH_W + 1];
     const int jj = blockIdx.x, j = row0 + jj;
-    if (FILL && stash && j < n && lmax <= LVL_STASH_W && scnt[jj] <= LVL_STASH_CAP) {
-        for (int i = threadIdx.x; i <= lmax; i += 256) h[i] = off[(size_t)j * LVL_STRIDE + i];
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    if (FILL && stash && j < n && lmax <= LVL_STASH_W &&
+        min(min(scnt[(size_t)jj * 4], scnt[(size_t)jj * 4 + 1]),
+            min(scnt[(size_t)jj * 4 + 2], scnt[(size_t)jj * 4 + 3])) >= 0) {
+        for (int i = tid; i <= lmax; i += 256) h[i] = off[(size_t)j * LVL_STRIDE + i];
+        for (int i = tid; i < 4 * (LVL_STASH_W + 1); i += 256) wc[i / (LVL_STASH_W + 1)][i % (LVL_STASH_W + 1)] = 0;
         __syncthreads();
-        const uint32_t* sr = stash + (size_t)jj * LVL_STASH_CAP;
-        const int m = scnt[jj];
-        for (int q = threadIdx.x; q < m; q += 256) {
-            const uint32_t e = sr[q], x = e >> 16, k = e & 0xFFFFu;
-            if (x > (uint32_t)lmax) continue;
-            const int p = atomicAdd(&h[x], 1);
-            arcs[p] = e;
-            ar[p] = r[(size_t)jj * ld + k]; /* undirected: r(k -> j) = r(j -> k) */
+        const uint32_t* sr = stash + (size_t)jj * LVL_STASH_CAP + wv * LVL_STASH_SEG;
+        const int m = scnt[(size_t)jj * 4 + wv];
+        for (int q = lane; q < m; q += 64) {
+            const uint32_t x = sr[q] >> 16;
+            if (x <= (uint32_t)lmax) atomicAdd(&wc[wv][x], 1);
+        }
+        __syncthreads();
+        /* lane x (x <= lmax <= 32) keeps this wave's next position for weight x: the weight's
+         * start plus the earlier waves' arcs of that weight */
+        int run = 0;
+        if (lane <= lmax) {
+            run = h[lane];
+            for (int v = 0; v < wv; ++v) run += wc[v][lane];
+        }
+        for (int q0 = 0; q0 < m; q0 += 64) {
+            const int q = q0 + lane;
+            const uint32_t e = q < m ? sr[q] : 0u, x = e >> 16;
+            const bool valid = q < m && x >= 1u && x <= (uint32_t)lmax;
+            unsigned long long pend = __ballot(valid);
+            int pos = 0;
+            while (pend) {
+                const int x0 = __builtin_amdgcn_readlane((int)x, __builtin_ctzll(pend));
+                const unsigned long long mm = __ballot(valid && (int)x == x0);
+                const int base = __builtin_amdgcn_readlane(run, x0);
+                if (valid && (int)x == x0) pos = base + __popcll(mm & lt);
+                if (lane == x0) run += __popcll(mm);
+                pend &= ~mm;
+            }
+            if (valid) {
+                arcs[pos] = e;
+                ar[pos] = r[(size_t)jj * ld + (e & 0xFFFFu)]; /* undirected: r(k -> j) = r(j -> k) */
+            }
         }
         return;
     }
-    if (!FILL && threadIdx.x == 0) s_n = 0;
     /* COUNT also takes the diagonal rule's key from the same row reads (topology.c:1431-1576, as
      * dense_diag_kernel): min over the row's out-edges of (self-loop L, other 2L) << 32 | u */
     unsigned long long best = ~0ull;
-    for (int i = threadIdx.x; i < LVL_STRIDE; i += 256)
+    for (int i = tid; i < LVL_STRIDE; i += 256)
         h[i] = FILL ? (j < n ? off[(size_t)j * LVL_STRIDE + i] : 0) : 0;
     __syncthreads();
     const int wmax = FILL ? lmax : LVL_WMAX;
-    if (j < n) {
-        const uint32_t* row = w + (size_t)jj * ld;
-        for (int k4 = threadIdx.x * 4; k4 < n; k4 += 1024) {
-            const uint4 v = *reinterpret_cast<const uint4*>(row + k4);
-            const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+    if (FILL) {
+        if (j < n) {
+            const uint32_t* row = w + (size_t)jj * ld;
+            for (int k4 = tid * 4; k4 < n; k4 += 1024) {
+                const uint4 v = *reinterpret_cast<const uint4*>(row + k4);
+                const uint32_t x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int k = k4 + q;
-                if (!FILL && k < n && x[q] < SRT_INF) {
-                    const unsigned long long lat = k == j ? x[q] : 2ull * x[q];
-                    best = min(best, (lat << 32) | (uint32_t)k);
-                }
-                if (k < n && k != j && x[q] >= 1u && x[q] <= (uint32_t)wmax) {
-                    if (FILL) {
+                for (int q = 0; q < 4; ++q) {
+                    const int k = k4 + q;
+                    if (k < n && k != j && x[q] >= 1u && x[q] <= (uint32_t)wmax) {
                         const int p = atomicAdd(&h[x[q]], 1);
                         arcs[p] = (uint32_t)k | (x[q] << 16);
                         ar[p] = r[(size_t)jj * ld + k]; /* undirected: r(k -> j) = r(j -> k) */
-                    } else {
-                        atomicAdd(&h[x[q]], 1);
-                        if (stash && x[q] <= LVL_STASH_W) {
-                            const int sq = atomicAdd(&s_n, 1);
-                            if (sq < LVL_STASH_CAP)
-                                stash[(size_t)jj * LVL_STASH_CAP + sq] = (uint32_t)k | (x[q] << 16);
-                        }
                     }
                 }
             }
         }
+        return;
     }
-    if (FILL) return;
+    int run = 0;
+    if (j < n) {
+        const uint32_t* row = w + (size_t)jj * ld;
+        const int Q = ((n + 1023) >> 10) << 8; /* a wave's quarter of the row, 256-aligned */
+        const int lo = wv * Q, hi = min(n, lo + Q);
+        uint32_t* seg = stash ? stash + (size_t)jj * LVL_STASH_CAP + wv * LVL_STASH_SEG : nullptr;
+        for (int b0 = lo; b0 < hi; b0 += 256) {
+            const int k4 = b0 + lane * 4;
+            uint4 v = make_uint4(SRT_INF, SRT_INF, SRT_INF, SRT_INF);
+            if (k4 < hi) v = *reinterpret_cast<const uint4*>(row + k4);
+            const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+            int c = 0;
+            bool cand[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = k4 + q;
+                if (k < n && x[q] < SRT_INF) {
+                    const unsigned long long lat = k == j ? x[q] : 2ull * x[q];
+                    best = min(best, (lat << 32) | (uint32_t)k);
+                }
+                const bool arc = k < n && k != j && x[q] >= 1u && x[q] <= (uint32_t)wmax;
+                if (arc) atomicAdd(&h[x[q]], 1);
+                cand[q] = arc && x[q] <= LVL_STASH_W;
+                c += cand[q];
+            }
+            if (seg) { /* vertex order: the lane's exclusive prefix of the counts (0..4) */
+                const unsigned long long b1 = __ballot(c & 1), b2 = __ballot(c & 2), b4 = __ballot(c & 4);
+                int p = run + __popcll(b1 & lt) + 2 * __popcll(b2 & lt) + 4 * __popcll(b4 & lt);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (cand[q]) {
+                        if (p < LVL_STASH_SEG) seg[p] = (uint32_t)(k4 + q) | (x[q] << 16);
+                        ++p;
+                    }
+                run += __popcll(b1) + 2 * __popcll(b2) + 4 * __popcll(b4);
+            }
+        }
+    }
+    if (stash && lane == 0) {
+        const bool over = run > LVL_STASH_SEG;
+        scnt[(size_t)jj * 4 + wv] = over ? -1 : run;
+        if (over) atomicAdd(sovf, 1ull);
+    }
     for (int o = 32; o > 0; o >>= 1) {
         const unsigned long long y = __shfl_xor(best, o);
         best = y < best ? y : best;
     }
-    if ((threadIdx.x & 63) == 0) s_key[threadIdx.x >> 6] = best;
+    if (lane == 0) s_key[wv] = best;
     __syncthreads();
-    if (stash && threadIdx.x == 0) scnt[jj] = s_n;
-    for (int i = threadIdx.x; i < LVL_STRIDE; i += 256) cnt[(size_t)j * LVL_STRIDE + i] = h[i];
-    if (threadIdx.x == 0 && dkey)
+    for (int i = tid; i < LVL_STRIDE; i += 256) cnt[(size_t)j * LVL_STRIDE + i] = h[i];
+    if (tid == 0 && dkey)
         dkey[jj] = min(min(s_key[0], s_key[1]), min(s_key[2], s_key[3]));
 }
 
@@ -290,6 +356,42 @@ __global__ void lvl_init_kernel(int n, int src0, int nsrc, int nw, uint32_t* __r
     if (i >= nsrc) return;
     const int j = src0 + i;
     if (j < n) R[(size_t)j * nw + (i >> 5)] = 1u << (i & 31);
+}
+
+/* Level 1 without the unit walk: Delta_1[j] = {s : w(s, j) = 1} (every arc is >= 1 quantum), so
+ * the level is j's weight-1 in-arcs set as bits (~33 per C4 target) in a zeroed plane and in R.
+ * A wave owns target j (its row of both), a lane an arc; the arcs are sorted by source, so lanes
+ * of one word are adjacent: a segmented OR (shuffle-up scan) leaves each word's bits in its last
+ * lane, which stores them. No atomics: a same-address counter atomic per wave alone cost 0.40 ms
+ * on C4 (serialised at the memory side), so the host counts the level's pairs from the weight
+ * histogram instead. */
+__global__ __launch_bounds__(256) void lvl_first_kernel(int n, int nw, int src0, int nsrc,
+                                                        const int32_t* __restrict__ off,
+                                                        const uint32_t* __restrict__ arcs,
+                                                        uint32_t* __restrict__ lev0,
+                                                        uint32_t* __restrict__ R) {
+    const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (j < n) {
+        const int a0 = off[(size_t)j * LVL_STRIDE + 1], a1 = off[(size_t)j * LVL_STRIDE + 2];
+        for (int i0 = a0; i0 < a1; i0 += 64) {
+            const int i = i0 + lane;
+            const int ks = i < a1 ? (int)(arcs[i] & 0xFFFFu) - src0 : -1;
+            const bool in = ks >= 0 && ks < nsrc;
+            const int wd = in ? ks >> 5 : -1 - lane; /* out-of-range lanes: words of their own */
+            uint32_t bits = in ? 1u << (ks & 31) : 0u;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t yb = (uint32_t)__shfl_up((int)bits, o);
+                const int yw = __shfl_up(wd, o);
+                if (lane >= o && yw == wd) bits |= yb;
+            }
+            const int nwd = __shfl_down(wd, 1);
+            if (in && (lane == 63 || nwd != wd)) {
+                const size_t o = (size_t)j * nw + wd;
+                lev0[o] |= bits;
+                R[o] |= bits;
+            }
+        }
+    }
 }
 
 /* Level d: one wave per (target j, 64-word source chunk c). Units are handed out XCD-major (each
@@ -981,7 +1083,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     if (!directed) {
         LVL_ALLOC(dkey, (size_t)nrows * sizeof(unsigned long long));
         LVL_ALLOC(stash, (size_t)nrows * LVL_STASH_CAP * sizeof(uint32_t));
-        LVL_ALLOC(scnt, (size_t)nrows * sizeof(int32_t));
+        LVL_ALLOC(scnt, (size_t)nrows * 4 * sizeof(int32_t));
     }
     SRT_HIPCHK(hipMemsetAsync(cnt, 0, (ncnt + 1) * sizeof(int32_t), st));
     SRT_HIPCHK(hipMemsetAsync(dhist, 0, (2 * LVL_STRIDE + 8) * sizeof(unsigned long long), st));
@@ -989,7 +1091,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         lvl_arcs_cols_kernel<false><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, cnt, 0, NULL, NULL);
     else
         lvl_arcs_rows_kernel<false><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, cnt, 0, NULL, NULL,
-                                                           NULL, NULL, dkey, stash, scnt);
+                                                           NULL, NULL, dkey, stash, scnt, dhist);
     SRT_HIPCHK(hipGetLastError());
     int rc;
     if (R > 1 && (rc = srt_coll_allreduce_i32(comm, cnt, ncnt, 0, st))) return rc;
@@ -1013,6 +1115,9 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         if ((size_t)lmax > cap) lmax = (int)cap;
     }
     if (R > 1 && (rc = lvl_agree_min(comm, dagree, &lmax, st))) return rc;
+    /* in-arcs already in (weight, source) order from the ordered stash, on every rank: no sort */
+    int sorted_fill = !directed && lmax <= LVL_STASH_W && hist[0] == 0;
+    if (R > 1 && (rc = lvl_agree_min(comm, dagree, &sorted_fill, st))) return rc;
     int wmin = 0;
     for (int x = 1; x <= LVL_WMAX && !wmin; ++x)
         if (hist[x]) wmin = x;
@@ -1031,16 +1136,19 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     uint8_t* done = NULL;
     size_t tmp_bytes = 0, sb = 0;
     SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(NULL, tmp_bytes, cnt, off, (int)(ncnt + 1), st));
-    if (total > 0)
+    const bool need_sort = total > 0 && !sorted_fill;
+    if (need_sort)
         SRT_HIPCHK(hipcub::DeviceSegmentedRadixSort::SortPairs(NULL, sb, arcs, arcs2, ar, ar2, total,
                                                                ld, seg, seg + 1, 0, 24, st));
     LVL_TRY_ALLOC(tmp, tmp_bytes, &ok);
     LVL_TRY_ALLOC(arcs, ((size_t)total + 8) * sizeof(uint32_t), &ok);
     LVL_TRY_ALLOC(ar, ((size_t)total + 8) * sizeof(double), &ok);
-    LVL_TRY_ALLOC(arcs2, ((size_t)total + 8) * sizeof(uint32_t), &ok);
-    LVL_TRY_ALLOC(ar2, ((size_t)total + 8) * sizeof(double), &ok);
-    LVL_TRY_ALLOC(seg, ((size_t)ld + 1) * sizeof(int32_t), &ok);
-    if (total > 0) LVL_TRY_ALLOC(stmp, sb, &ok);
+    if (need_sort) {
+        LVL_TRY_ALLOC(arcs2, ((size_t)total + 8) * sizeof(uint32_t), &ok);
+        LVL_TRY_ALLOC(ar2, ((size_t)total + 8) * sizeof(double), &ok);
+        LVL_TRY_ALLOC(seg, ((size_t)ld + 1) * sizeof(int32_t), &ok);
+        LVL_TRY_ALLOC(stmp, sb, &ok);
+    }
     LVL_TRY_ALLOC(aoff, ((size_t)total + 64) * sizeof(uint32_t), &ok); /* + a gather batch's tail */
     LVL_TRY_ALLOC(lev, (size_t)lmax * plane * sizeof(uint32_t) + 16, &ok);
     LVL_TRY_ALLOC(Rb, plane * sizeof(uint32_t) + 16, &ok);
@@ -1089,14 +1197,16 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         if (rc || rc2) return rc ? rc : rc2;
     }
     /* in-arcs of each target sorted by (weight, source vertex): the order the predecessor search
-     * walks them in (the fill's atomics leave the order inside a weight arbitrary) */
-    lvl_segs_kernel<<<srt_ceil_div(ld + 1, 256), 256, 0, st>>>(ld, off, seg);
-    SRT_HIPCHK(hipGetLastError());
-    if (total > 0)
+     * walks them in (the full-row fill's atomics leave the order inside a weight arbitrary; the
+     * ordered stash fill needs no sort) */
+    if (need_sort) {
+        lvl_segs_kernel<<<srt_ceil_div(ld + 1, 256), 256, 0, st>>>(ld, off, seg);
+        SRT_HIPCHK(hipGetLastError());
         SRT_HIPCHK(hipcub::DeviceSegmentedRadixSort::SortPairs(stmp, sb, arcs, arcs2, ar, ar2, total,
                                                                ld, seg, seg + 1, 0, 24, st));
-    arcs = arcs2;
-    ar = ar2;
+        arcs = arcs2;
+        ar = ar2;
+    }
     /* level state over the local sources */
     if (total > 0) {
         lvl_aoff_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, nw, arcs, aoff);
@@ -1132,9 +1242,20 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         const int d1 = min(lmax, d0 + LVL_BATCH - 1);
         for (int d = d0; d <= d1; ++d) {
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
-            lvl_step_kernel<<<pgrid, 256, 0, st>>>(d, n, nw, nchunk, row0, nrows, nblk, off, arcs,
-                                                  aoff, lev, Rb, done, dinc + d,
-                                                  d > 1 ? dinc + d - 1 : NULL, nset);
+#ifndef LVL_FIRST
+#define LVL_FIRST 1
+#endif
+            if (LVL_FIRST && d == 1) { /* the weight-1 arcs as bits; level 2 takes up the completion flags
+                           * (dinc[1] stays set: a graph settled at level 1 reports 2 levels) */
+                SRT_HIPCHK(hipMemsetAsync(lev, 0, plane * sizeof(uint32_t), st));
+                SRT_HIPCHK(hipMemsetAsync(dinc + 1, 0xFF, sizeof(int), st));
+                lvl_first_kernel<<<srt_ceil_div(n, 4), 256, 0, st>>>(n, nw, row0, nrows, off, arcs,
+                                                                      lev, Rb);
+            } else {
+                lvl_step_kernel<<<pgrid, 256, 0, st>>>(d, n, nw, nchunk, row0, nrows, nblk, off,
+                                                      arcs, aoff, lev, Rb, done, dinc + d,
+                                                      d > 1 ? dinc + d - 1 : NULL, nset);
+            }
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
         }
         SRT_HIPCHK(hipGetLastError());
@@ -1147,7 +1268,9 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         SRT_HIPCHK(hipStreamSynchronize(st));
         for (int d = d0; d <= d1 && !D; ++d)
             if (inc[d - d0] == 0) D = d;
-        /* every source's own vertex counts as settled at level 0 (n - row0 of them are local) */
+        /* every source's own vertex counts as settled at level 0 (n - row0 of them are local);
+         * level 1 (lvl_first_kernel) counts no pairs: its weight-1 arcs, this rank's share of them */
+        if (LVL_FIRST && d0 == 1) settled += (unsigned long long)((double)hist[1] * lsrc / n);
         const double frac = pairs > 0 ? ((double)settled + (double)lsrc) / pairs : 1.0;
         /* (a forced level build, fw_ms = 1e30 from SRT_FORM levels=1, runs its whole budget) */
         if (!D && d0 == 1 && d1 < lmax && frac < LVL_MIN_SETTLED && fw_ms < 1e29)

@@ -211,7 +211,7 @@ __global__ __launch_bounds__(SP_THREADS) void sssp_kernel(
     }
     depth = max(depth, sdepth);
   }
-    if (tid == 0) atomicMax(max_depth, depth);
+    if (tid == 0) srt_max_once(max_depth, depth);
 }
 
 /* Diagonal rule (topology.c:1431-1576) from the canonical CSR: min over (self-loop L, v) and

@@ -10,6 +10,12 @@
 
 #include "srt_internal.h"
 
+/* a running maximum many workgroups raise once each (per-row depth counters): read it first, so
+ * the same-address atomic -- serialised at the memory side, ~12 ns each -- runs only to raise it */
+static __device__ __forceinline__ void srt_max_once(int32_t* p, int v) {
+    if (v > __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(p, v);
+}
+
 #define SRT_HIPCHK(expr)                                                                   \
     do {                                                                                   \
         hipError_t e_ = (expr);                                                            \

@@ -143,7 +143,7 @@ __global__ __launch_bounds__(PS_THREADS) void path_sweeps_kernel(
         depth_max = depth > depth_max ? depth : depth_max;
         __syncthreads();
     }
-    if (max_depth && tid == 0) atomicMax(max_depth, depth_max);
+    if (max_depth && tid == 0) srt_max_once(max_depth, depth_max);
 }
 
 /* largest n whose two row bitmaps fit the LDS */
