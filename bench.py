@@ -655,8 +655,8 @@ def run_sparse(c: Ctx, wl):
     # the kernel's form from the build (srt_build_stats.fw_block of sparse builds)
     form = int(stats[-1].fw_block)
     tf = lambda b: "true" if b else "false"
-    kname = {3: f"msssp_kernel<{tf(g.directed)}>",
-             2: f"wgsssp_kernel<1024, false, {tf(form & 1)}, {tf(form & 2)}>",
+    kname = {3: f"msssp_kernel<{tf(g.directed)}, {'unsigned short' if form & 16 else 'unsigned int'}>",
+             2: f"wgsssp_kernel<1024, true, {tf(form & 2)}>",
              1: f"wsssp_kernel<{tf(g.directed)}, {tf(form & 1)}, {tf(form & 2)}>"
              }.get(enc, "sssp_kernel")
     model = "per source: (n+1)*4 + arcs*16 + n*12 B (SURVEY §8d work-efficient gather model)"
