@@ -1059,6 +1059,13 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     }
     if ((size_t)n * (size_t)(max_rows / 32) * 4 > 0xFFFFFFFFull) return SRT_OK; /* 32-bit offsets */
     const int nw = nrows / 32, nchunk = (nw + 63) / 64;
+    /* a timing-only communicator (srt_comm_init_solo*, tools/solo_rank.py) hands the rank the
+     * whole matrix around its shard: it extracts every row's in-arcs itself, so the collectives it
+     * skips (their bytes charged to the wire model) leave it the arcs the real ranks exchange */
+    const bool xfull = R > 1 && srt_comm_is_solo(comm);
+    const int xrow0 = xfull ? 0 : row0, xrows = xfull ? ld : nrows;
+    const uint32_t* xw = xfull ? w_rows - (size_t)row0 * ld : w_rows;
+    const double* xr = xfull ? r_rows - (size_t)row0 * ld : r_rows;
     L->st = st;
     /* on any early return below the allocations go back (lvl_free), unless the build is held */
     struct guard {
@@ -1081,16 +1088,16 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     uint32_t* stash = NULL;
     int32_t* scnt = NULL;
     if (!directed) {
-        LVL_ALLOC(dkey, (size_t)nrows * sizeof(unsigned long long));
-        LVL_ALLOC(stash, (size_t)nrows * LVL_STASH_CAP * sizeof(uint32_t));
-        LVL_ALLOC(scnt, (size_t)nrows * 4 * sizeof(int32_t));
+        LVL_ALLOC(dkey, (size_t)xrows * sizeof(unsigned long long));
+        LVL_ALLOC(stash, (size_t)xrows * LVL_STASH_CAP * sizeof(uint32_t));
+        LVL_ALLOC(scnt, (size_t)xrows * 4 * sizeof(int32_t));
     }
     SRT_HIPCHK(hipMemsetAsync(cnt, 0, (ncnt + 1) * sizeof(int32_t), st));
     SRT_HIPCHK(hipMemsetAsync(dhist, 0, (2 * LVL_STRIDE + 8) * sizeof(unsigned long long), st));
     if (directed)
         lvl_arcs_cols_kernel<false><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, cnt, 0, NULL, NULL);
     else
-        lvl_arcs_rows_kernel<false><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, cnt, 0, NULL, NULL,
+        lvl_arcs_rows_kernel<false><<<xrows, 256, 0, st>>>(n, ld, xrow0, xw, cnt, 0, NULL, NULL,
                                                            NULL, NULL, dkey, stash, scnt, dhist);
     SRT_HIPCHK(hipGetLastError());
     int rc;
@@ -1174,8 +1181,8 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         lvl_arcs_cols_kernel<true><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, NULL, lmax, off, arcs,
                                                             r_rows, ar);
     else
-        lvl_arcs_rows_kernel<true><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, NULL, lmax, off, arcs,
-                                                          r_rows, ar, NULL, stash, scnt);
+        lvl_arcs_rows_kernel<true><<<xrows, 256, 0, st>>>(n, ld, xrow0, xw, NULL, lmax, off, arcs,
+                                                          xr, ar, NULL, stash, scnt);
     SRT_HIPCHK(hipGetLastError());
     if (R > 1) { /* every rank filled its rows' segment: broadcast the segments */
         int32_t hoff[65];
@@ -1333,7 +1340,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     L->l8 = l8;
     L->pkw = pkw;
     L->total = total;
-    L->dkey = dkey;
+    L->dkey = dkey && xfull ? dkey + row0 : dkey; /* the diagonal keys of this rank's rows */
     L->r_rows = r_rows;
     return SRT_OK;
 }
