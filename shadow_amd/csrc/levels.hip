@@ -266,6 +266,32 @@ __global__ void lvl_hist_kernel(size_t count, const int32_t* __restrict__ cnt,
         if (s[i]) atomicAdd(&hist[i], s[i]);
 }
 
+/* N > 1: the histogram all-reduced in 20-bit limbs (int32 sums of R ranks cannot overflow), then
+ * only the (target, weight <= lmax) counts -- the in-arc offsets need no heavier weight: 2.9 MB
+ * on C4 instead of the 33.5-MB (target x 256 weights) block */
+__global__ void lvl_hist_limbs_kernel(int to, unsigned long long* __restrict__ hist,
+                                      int32_t* __restrict__ limbs) {
+    const int i = threadIdx.x;
+    if (i >= LVL_STRIDE) return;
+    if (to) {
+        limbs[i] = (int32_t)(hist[i] & 0xFFFFFull);
+        limbs[LVL_STRIDE + i] = (int32_t)(hist[i] >> 20);
+    } else {
+        hist[i] = (unsigned long long)(uint32_t)limbs[i] +
+                  ((unsigned long long)(uint32_t)limbs[LVL_STRIDE + i] << 20);
+    }
+}
+__global__ void lvl_cnt_pack_kernel(int ld, int cols, int to, int32_t* __restrict__ cnt,
+                                    int32_t* __restrict__ packed) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)ld * cols) return;
+    const size_t j = i / cols, w = i % cols;
+    if (to)
+        packed[i] = cnt[j * LVL_STRIDE + w];
+    else
+        cnt[j * LVL_STRIDE + w] = packed[i];
+}
+
 __global__ void lvl_mask_kernel(size_t count, int lmax, int32_t* __restrict__ cnt) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count && (int)(i % LVL_STRIDE) > lmax) cnt[i] = 0;
@@ -1078,7 +1104,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     const size_t ncnt = (size_t)ld * LVL_STRIDE;
     int32_t *cnt = NULL, *off = NULL;
     unsigned long long* dhist = NULL;
-    LVL_ALLOC(cnt, (ncnt + 1) * sizeof(int32_t));
+    LVL_ALLOC(cnt, (ncnt + 1 + 2 * LVL_STRIDE) * sizeof(int32_t)); /* + the histogram limbs */
     LVL_ALLOC(off, (ncnt + 1) * sizeof(int32_t));
     /* the histogram, then LVL_WMAX + 1 completion flags, then the agreement word */
     LVL_ALLOC(dhist, (2 * LVL_STRIDE + 8) * sizeof(unsigned long long));
@@ -1101,9 +1127,15 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
                                                            NULL, NULL, dkey, stash, scnt, dhist);
     SRT_HIPCHK(hipGetLastError());
     int rc;
-    if (R > 1 && (rc = srt_coll_allreduce_i32(comm, cnt, ncnt, 0, st))) return rc;
-    lvl_hist_kernel<<<1024, 256, 0, st>>>(ncnt, cnt, dhist);
+    lvl_hist_kernel<<<1024, 256, 0, st>>>(ncnt, cnt, dhist); /* this rank's rows (N > 1) */
     SRT_HIPCHK(hipGetLastError());
+    int32_t* limbs = reinterpret_cast<int32_t*>(cnt + ncnt + 1); /* 2 x 256 int32 past the counts */
+    if (R > 1) {
+        lvl_hist_limbs_kernel<<<1, LVL_STRIDE, 0, st>>>(1, dhist, limbs);
+        if ((rc = srt_coll_allreduce_i32(comm, limbs, 2 * LVL_STRIDE, 0, st))) return rc;
+        lvl_hist_limbs_kernel<<<1, LVL_STRIDE, 0, st>>>(0, dhist, limbs);
+        SRT_HIPCHK(hipGetLastError());
+    }
     unsigned long long hist[LVL_STRIDE];
     SRT_HIPCHK(hipMemcpyAsync(hist, dhist, sizeof(hist), hipMemcpyDeviceToHost, st));
     SRT_HIPCHK(hipStreamSynchronize(st));
@@ -1129,6 +1161,16 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     for (int x = 1; x <= LVL_WMAX && !wmin; ++x)
         if (hist[x]) wmin = x;
     if (lmax < 2 || !wmin || wmin > lmax) return SRT_OK; /* the same on every rank */
+    if (R > 1) { /* every target's counts up to lmax on every rank (one owner row each) */
+        const int cols = lmax + 2;
+        int32_t* packed = NULL;
+        LVL_ALLOC(packed, (size_t)ld * cols * sizeof(int32_t));
+        const int gb = srt_ceil_div((int64_t)ld * cols, 256);
+        lvl_cnt_pack_kernel<<<gb, 256, 0, st>>>(ld, cols, 1, cnt, packed);
+        if ((rc = srt_coll_allreduce_i32(comm, packed, (size_t)ld * cols, 0, st))) return rc;
+        lvl_cnt_pack_kernel<<<gb, 256, 0, st>>>(ld, cols, 0, cnt, packed);
+        SRT_HIPCHK(hipGetLastError());
+    }
     /* in-arcs with w <= lmax: their count from the histogram (no read-back of the scan) */
     int64_t total64 = 0;
     for (int x = 1; x <= lmax; ++x) total64 += (int64_t)hist[x];
@@ -1173,61 +1215,88 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     }
     if (R > 1 && (rc = lvl_agree_min(comm, dagree, &ok, st))) return rc;
     if (!ok) return SRT_OK; /* out of device memory somewhere: Floyd-Warshall on every rank */
-    /* offsets over the arcs with w <= lmax, (target, weight)-major */
-    lvl_mask_kernel<<<srt_ceil_div((int64_t)ncnt, 256), 256, 0, st>>>(ncnt, lmax, cnt);
-    SRT_HIPCHK(hipGetLastError());
-    SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, (int)(ncnt + 1), st));
-    if (directed)
-        lvl_arcs_cols_kernel<true><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, NULL, lmax, off, arcs,
-                                                            r_rows, ar);
-    else
-        lvl_arcs_rows_kernel<true><<<xrows, 256, 0, st>>>(n, ld, xrow0, xw, NULL, lmax, off, arcs,
-                                                          xr, ar, NULL, stash, scnt);
-    SRT_HIPCHK(hipGetLastError());
-    if (R > 1) { /* every rank filled its rows' segment: broadcast the segments */
-        int32_t hoff[65];
-        for (int q = 0; q <= R; q++) {
-            int32_t b = ld, e = ld;
-            if (q < R) srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &b, &e);
-            SRT_HIPCHK(hipMemcpyAsync(&hoff[q], off + (size_t)b * LVL_STRIDE, sizeof(int32_t),
-                                      hipMemcpyDeviceToHost, st));
-        }
-        SRT_HIPCHK(hipStreamSynchronize(st));
-        rc = srt_coll_group_begin(comm);
-        for (int q = 0; q < R && !rc; q++)
-            if (hoff[q + 1] > hoff[q]) {
-                const size_t c = (size_t)(hoff[q + 1] - hoff[q]);
-                rc = srt_coll_bcast(comm, arcs + hoff[q], c * sizeof(uint32_t), q, st);
-                if (!rc) rc = srt_coll_bcast(comm, ar + hoff[q], c * sizeof(double), q, st);
-            }
-        const int rc2 = srt_coll_group_end(comm);
-        if (rc || rc2) return rc ? rc : rc2;
-    }
-    /* in-arcs of each target sorted by (weight, source vertex): the order the predecessor search
-     * walks them in (the full-row fill's atomics leave the order inside a weight arbitrary; the
-     * ordered stash fill needs no sort) */
-    if (need_sort) {
-        lvl_segs_kernel<<<srt_ceil_div(ld + 1, 256), 256, 0, st>>>(ld, off, seg);
-        SRT_HIPCHK(hipGetLastError());
-        SRT_HIPCHK(hipcub::DeviceSegmentedRadixSort::SortPairs(stmp, sb, arcs, arcs2, ar, ar2, total,
-                                                               ld, seg, seg + 1, 0, 24, st));
-        arcs = arcs2;
-        ar = ar2;
-    }
-    /* level state over the local sources */
-    if (total > 0) {
-        lvl_aoff_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, nw, arcs, aoff);
-        SRT_HIPCHK(hipGetLastError());
-    }
-    /* the reliability table: its flags are read with the levels' completion (no round trip) */
+    /* The in-arcs are extracted for the first batch of levels only (w <= lx = min(lmax, LVL_BATCH):
+     * levels d <= lx use no heavier arc) and again up to lmax if the levels run past it: C4 ends
+     * at level 5, and its ~20-quantum budget would extract, number and (N > 1) broadcast 2.5x the
+     * arcs it uses. The counts are kept for the second extraction. */
+    const int lx = min(lmax, LVL_BATCH);
+    int32_t* cnt_keep = NULL;
+    if (lx < lmax) LVL_ALLOC(cnt_keep, (ncnt + 1) * sizeof(int32_t));
+    if (cnt_keep)
+        SRT_HIPCHK(hipMemcpyAsync(cnt_keep, cnt, (ncnt + 1) * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    uint32_t* const arcsA = arcs;
+    double* const arA = ar;
     int* dflag = dinc + LVL_WMAX + 1; /* [0] probe overflow, [1] distinct values */
-    if (want_rt) {
-        SRT_HIPCHK(hipMemsetAsync(H, 0xFF, LVL_RT_SLOTS * sizeof(unsigned long long), st));
-        lvl_rt_hash_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, ar, H, rix, dflag);
-        lvl_rt_compact_kernel<<<1, 1024, 0, st>>>(H, map, rtab, dflag + 1);
-        lvl_rt_remap_kernel<<<srt_ceil_div(total, 256), 256, 0, st>>>(total, map, rix);
+    int32_t total_x = 0;          /* the arcs of the current extraction */
+    auto extract = [&](int lw) -> int {
+        int64_t t64 = 0;
+        for (int x = 1; x <= lw; ++x) t64 += (int64_t)hist[x];
+        total_x = (int32_t)t64;
+        int sorted_w = !directed && lw <= LVL_STASH_W && hist[0] == 0;
+        int rc_ = 0;
+        if (R > 1 && (rc_ = lvl_agree_min(comm, dagree, &sorted_w, st))) return rc_;
+        if (cnt_keep && lw != lx)
+            SRT_HIPCHK(hipMemcpyAsync(cnt, cnt_keep, (ncnt + 1) * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+        /* offsets over the arcs with w <= lw, (target, weight)-major */
+        lvl_mask_kernel<<<srt_ceil_div((int64_t)ncnt, 256), 256, 0, st>>>(ncnt, lw, cnt);
         SRT_HIPCHK(hipGetLastError());
-    }
+        SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, (int)(ncnt + 1), st));
+        if (directed)
+            lvl_arcs_cols_kernel<true><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, NULL, lw, off, arcsA,
+                                                                r_rows, arA);
+        else
+            lvl_arcs_rows_kernel<true><<<xrows, 256, 0, st>>>(n, ld, xrow0, xw, NULL, lw, off, arcsA,
+                                                              xr, arA, NULL, stash, scnt);
+        SRT_HIPCHK(hipGetLastError());
+        if (R > 1) { /* every rank filled its rows' segment: broadcast the segments */
+            int32_t hoff[65];
+            for (int q = 0; q <= R; q++) {
+                int32_t b = ld, e = ld;
+                if (q < R) srt_shard_rows(ld, SRT_SHARD_ALIGN, R, q, &b, &e);
+                SRT_HIPCHK(hipMemcpyAsync(&hoff[q], off + (size_t)b * LVL_STRIDE, sizeof(int32_t),
+                                          hipMemcpyDeviceToHost, st));
+            }
+            SRT_HIPCHK(hipStreamSynchronize(st));
+            rc_ = srt_coll_group_begin(comm);
+            for (int q = 0; q < R && !rc_; q++)
+                if (hoff[q + 1] > hoff[q]) {
+                    const size_t c = (size_t)(hoff[q + 1] - hoff[q]);
+                    rc_ = srt_coll_bcast(comm, arcsA + hoff[q], c * sizeof(uint32_t), q, st);
+                    if (!rc_) rc_ = srt_coll_bcast(comm, arA + hoff[q], c * sizeof(double), q, st);
+                }
+            const int rc2 = srt_coll_group_end(comm);
+            if (rc_ || rc2) return rc_ ? rc_ : rc2;
+        }
+        /* in-arcs of each target sorted by (weight, source vertex): the order the predecessor
+         * search walks them in (the full-row fill's atomics leave the order inside a weight
+         * arbitrary; the ordered stash fill needs no sort) */
+        arcs = arcsA;
+        ar = arA;
+        if (total_x > 0 && !sorted_w) {
+            lvl_segs_kernel<<<srt_ceil_div(ld + 1, 256), 256, 0, st>>>(ld, off, seg);
+            SRT_HIPCHK(hipGetLastError());
+            SRT_HIPCHK(hipcub::DeviceSegmentedRadixSort::SortPairs(stmp, sb, arcsA, arcs2, arA, ar2,
+                                                                   total_x, ld, seg, seg + 1, 0, 24,
+                                                                   st));
+            arcs = arcs2;
+            ar = ar2;
+        }
+        if (total_x > 0) {
+            lvl_aoff_kernel<<<srt_ceil_div(total_x, 256), 256, 0, st>>>(total_x, nw, arcs, aoff);
+            SRT_HIPCHK(hipGetLastError());
+        }
+        /* the reliability table: its flags are read with the levels' completion (no round trip) */
+        if (want_rt && total_x > 0) {
+            SRT_HIPCHK(hipMemsetAsync(dflag, 0, 2 * sizeof(int), st));
+            SRT_HIPCHK(hipMemsetAsync(H, 0xFF, LVL_RT_SLOTS * sizeof(unsigned long long), st));
+            lvl_rt_hash_kernel<<<srt_ceil_div(total_x, 256), 256, 0, st>>>(total_x, ar, H, rix, dflag);
+            lvl_rt_compact_kernel<<<1, 1024, 0, st>>>(H, map, rtab, dflag + 1);
+            lvl_rt_remap_kernel<<<srt_ceil_div(total_x, 256), 256, 0, st>>>(total_x, map, rix);
+            SRT_HIPCHK(hipGetLastError());
+        }
+        return 0;
+    };
+    if ((rc = extract(lx))) return rc;
     SRT_HIPCHK(hipMemsetAsync(Rb, 0, plane * sizeof(uint32_t), st));
     SRT_HIPCHK(hipMemsetAsync(done, 0, (size_t)n * nchunk, st));
     lvl_init_kernel<<<srt_ceil_div(nrows, 256), 256, 0, st>>>(n, row0, nrows, nw, Rb);
@@ -1282,6 +1351,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         /* (a forced level build, fw_ms = 1e30 from SRT_FORM levels=1, runs its whole budget) */
         if (!D && d0 == 1 && d1 < lmax && frac < LVL_MIN_SETTLED && fw_ms < 1e29)
             break; /* -> Floyd-Warshall */
+        if (!D && d1 == lx && lx < lmax && (rc = extract(lmax))) return rc; /* the heavier arcs */
     }
     if (evp && D) evp->used = ev0 + 2 * D; /* the levels that did work */
     int64_t gathered = 0;
@@ -1339,7 +1409,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     L->lev = lev;
     L->l8 = l8;
     L->pkw = pkw;
-    L->total = total;
+    L->total = total_x;
     L->dkey = dkey && xfull ? dkey + row0 : dkey; /* the diagonal keys of this rank's rows */
     L->r_rows = r_rows;
     return SRT_OK;
