@@ -24,7 +24,15 @@
 #ifndef DV_MAXDEG
 #define DV_MAXDEG 4   /* largest degree the host puts in I (build.hip DERIVE_MAXDEG) */
 #endif
+#ifndef DV_J
 #define DV_J 2        /* targets per thread per phase-A step: their loads overlap */
+#endif
+#ifndef DV_SPEC
+#define DV_SPEC 1     /* phase A loads every neighbour's code with its distance (no second trip) */
+#endif
+#ifndef DV_PROBE
+#define DV_PROBE 0    /* 1: phase A alone (timing probe, wrong reliabilities) */
+#endif
 #define DV_JB 1       /* targets per thread per phase-B step (4: 138 vs 125 ms on C5) */
 
 /* order of canonical arcs u | w << 17 | ridx << 24: the largest w, then the smallest u */
@@ -101,6 +109,16 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
                                    ? lat[(size_t)(s_nb[i] - src_begin) * ldo + t]
                                    : SRT_INF;
             }
+            uint32_t cv[DV_J][DV_MAXDEG];
+            if (DV_SPEC) {
+#pragma unroll
+                for (int j = 0; j < DV_J; ++j) {
+                    const int t = t0 + j * NT + tid;
+#pragma unroll
+                    for (int i = 0; i < DV_MAXDEG; ++i)
+                        cv[j][i] = (i < deg && t < n) ? codes[(size_t)s_cr[i] * n + t] : ~0u;
+                }
+            }
             uint32_t D[DV_J];
 #pragma unroll
             for (int j = 0; j < DV_J; ++j) {
@@ -120,7 +138,7 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
                         cd[j][i] = t == s_nb[i]
                                        ? ((uint32_t)s | ((uint32_t)s_w[i] << 17) |
                                           ((uint32_t)s_rx[i] << 24))
-                                       : codes[(size_t)s_cr[i] * n + t];
+                                       : DV_SPEC ? cv[j][i] : codes[(size_t)s_cr[i] * n + t];
                 }
             }
 #pragma unroll
@@ -167,7 +185,7 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
         /* phase B: on-demand path-order products. DV_JB targets per thread per step: their
          * codes, then the predecessors' values of the ready ones, in flight together; a target
          * whose predecessor is not formed yet climbs alone */
-        for (int t0 = 0; t0 < n; t0 += DV_JB * NT) {
+        for (int t0 = 0; t0 < n && !DV_PROBE; t0 += DV_JB * NT) {
             uint32_t cj[DV_JB];
             bool rdy[DV_JB];
 #pragma unroll

@@ -11,8 +11,8 @@ for v in "$@"; do
     if [ "$v" = default ]; then LP=""; else LP=$(pwd)/shadow_amd/ab_$v.so; fi
     # variants named x*: timing diagnostics (wrong tables), no parity tests
     [ "${v#x}" = "$v" ] && SRT_LIB_PATH=$LP timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
-        tests/test_gpu_levels.py -m gpu -k match_oracle > $O/tests_$v.log 2>&1 || [ "${v#x}" != "$v" ] || { echo "$v tests failed"; exit 1; }
+        ${AB_TESTS:-tests/test_gpu_levels.py -k match_oracle} -m gpu > $O/tests_$v.log 2>&1 || [ "${v#x}" != "$v" ] || { echo "$v tests failed"; exit 1; }
     SRT_LIB_PATH=$LP timeout -k 10 300 python -u bench.py --workload $WL --steps 5 --warmup 1 \
         --no-cpu-baseline > $O/bench_${WL}_$v.json 2> $O/bench_${WL}_$v.err || { echo "$v bench failed"; exit 1; }
-    echo "$v $(python3 -c "import json,sys;d=json.loads(open('$O/bench_${WL}_$v.json').read().strip().splitlines()[-1]);print(d['ms_per_step'], {k:v['ms_per_build'] for k,v in d['roofline'].get('kernels',{}).items()})")"
+    echo "$v $(python3 -c "import json,sys;d=json.loads(open('$O/bench_${WL}_$v.json').read().strip().splitlines()[-1]);r=d['roofline'];ks=r.get('kernels',{});print(d['ms_per_step'], r.get('kernel'), r.get('avg_launch_ms'), {k:v['ms_per_build'] for k,v in ks.items()} if isinstance(ks,dict) else [(k['kernel'],k['avg_launch_ms']) for k in ks])")"
 done
