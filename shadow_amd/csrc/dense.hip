@@ -1299,6 +1299,9 @@ static void rel_tree_launch(int n, int ld, int row0, int lrows, const LT* d, con
  * A row with more parents than the cap slots takes rel_sweeps_kernel from the r(pred, t) it
  * leaves in the rel row (sweep[row] = 1). */
 #define REL_PK_NT 512
+#ifndef REL_PK_PROF
+#define REL_PK_PROF 0 /* 1: phase wall clock of a few rows, printed */
+#endif
 template <int K>
 __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int row0,
                                                            const uint32_t* __restrict__ pk,
@@ -1309,6 +1312,13 @@ __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int ro
                                                            int32_t* __restrict__ sweep) {
     constexpr int NT = REL_PK_NT;
     const int s = row0 + (int)blockIdx.x;
+#if REL_PK_PROF
+    unsigned long long pt[6];
+    pt[0] = wall_clock64();
+#define REL_PK_T(i) do { if (threadIdx.x == 0) pt[i] = wall_clock64(); } while (0)
+#else
+#define REL_PK_T(i) ((void)0)
+#endif
     const int tid = threadIdx.x, lane = tid & 63;
     const int nwb = ld >> 5; /* parent bitmap words (ld % 128 == 0) */
     extern __shared__ __attribute__((aligned(16))) uint32_t psm[];
@@ -1363,6 +1373,7 @@ __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int ro
     for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
     if (lane == 0) red[tid >> 6] = mx;
     __syncthreads(); /* par, red */
+    REL_PK_T(1);
     mx = 0;
     for (int i = 0; i < NT / 64; ++i) mx = max(mx, red[i]);
     /* exclusive prefix of the parent counts; thread tid owns bitmap words tid * wpt.. */
@@ -1395,6 +1406,7 @@ __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int ro
     const bool bail = total > (uint32_t)cap;
     if (tid == 0) sweep[blockIdx.x] = bail;
     __syncthreads(); /* pre */
+    REL_PK_T(2);
     auto rank = [&](uint32_t u) {
         return pre[u >> 5] + (uint32_t)__popc(par[u >> 5] & ((1u << (u & 31)) - 1u));
     };
@@ -1424,6 +1436,7 @@ __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int ro
             __syncthreads();
         }
     }
+    REL_PK_T(3);
 #pragma unroll
     for (int k = 0; k < K; ++k)
         asm volatile("" : "+v"(wd[k].x), "+v"(wd[k].y), "+v"(wd[k].z), "+v"(wd[k].w));
@@ -1461,6 +1474,15 @@ __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int ro
         __builtin_amdgcn_sched_barrier(0);
     }
     if (tid == 0) srt_max_once(max_depth, (int)mx);
+#if REL_PK_PROF
+    __syncthreads();
+    if (tid == 0) {
+        pt[4] = wall_clock64();
+        if (blockIdx.x % 4096 == 17)
+            printf("[rel_pk prof] row %d start %llu load+mark %llu prefix %llu levels %llu out %llu (x10 ns) parents %u\n",
+                   (int)blockIdx.x, pt[0], pt[1] - pt[0], pt[2] - pt[1], pt[3] - pt[2], pt[4] - pt[3], total);
+    }
+#endif
 }
 
 /* rel_pk_kernel at the row's width, then the sweeps for the rows over the parent cap */
