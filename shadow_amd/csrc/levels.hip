@@ -27,6 +27,9 @@
  * them for its rows) or its columns (directed, one GPU), grouped by (target, weight).
  */
 #include <hipcub/hipcub.hpp>
+#include <algorithm>
+#include <cstring>
+#include <vector>
 
 #include "srt_device.h"
 
@@ -366,6 +369,23 @@ __global__ void lvl_rt_remap_kernel(int total, const uint16_t* __restrict__ map,
                                     uint16_t* __restrict__ rix) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < total) rix[i] = map[rix[i]];
+}
+
+/* N > 1 (numbered segments): each arc's index into the union table, sorted by value bits, of
+ * every rank's distinct reliabilities -- the same numbering on every rank */
+__global__ void lvl_rt_index_kernel(int total, const double* __restrict__ ar,
+                                    const unsigned long long* __restrict__ tab, int ntab,
+                                    uint16_t* __restrict__ rix) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const unsigned long long b = (unsigned long long)__double_as_longlong(ar[i]);
+    int lo = 0, hi = ntab - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (tab[mid] < b) lo = mid + 1;
+        else hi = mid;
+    }
+    rix[i] = (uint16_t)lo;
 }
 
 /* byte offset of each arc's source row inside a level plane (k * nw * 4; nw is this rank's) */
@@ -1213,6 +1233,11 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         LVL_TRY_ALLOC(rix, ((size_t)total + 8) * sizeof(uint16_t), &ok);
         LVL_TRY_ALLOC(rtab, LVL_RT_CAP * sizeof(double), &ok);
     }
+    /* N > 1: one block per rank for the numbered segments (a header with the overflow flag and
+     * the count, then up to LVL_RT_CAP values) */
+    constexpr size_t LVL_GB = LVL_RT_CAP + 1;
+    double* gat = NULL;
+    if (want_rt && R > 1) LVL_TRY_ALLOC(gat, (size_t)R * LVL_GB * sizeof(double), &ok);
     if (R > 1 && (rc = lvl_agree_min(comm, dagree, &ok, st))) return rc;
     if (!ok) return SRT_OK; /* out of device memory somewhere: Floyd-Warshall on every rank */
     /* The in-arcs are extracted for the first batch of levels only (w <= lx = min(lmax, LVL_BATCH):
@@ -1229,6 +1254,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     int* dflag = dinc + LVL_WMAX + 1; /* [0] probe overflow, [1] distinct values */
     int32_t total_x = 0;          /* the arcs of the current extraction */
     auto extract = [&](int lw) -> int {
+        int numbered = 0; /* the segments travelled as arcs + table indices */
         int64_t t64 = 0;
         for (int x = 1; x <= lw; ++x) t64 += (int64_t)hist[x];
         total_x = (int32_t)t64;
@@ -1257,12 +1283,74 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
                                           hipMemcpyDeviceToHost, st));
             }
             SRT_HIPCHK(hipStreamSynchronize(st));
+            /* Numbered segments: the packed post pass needs each arc's index into the table of
+             * distinct reliabilities, not its f64. Each rank numbers its own segment's values
+             * (hash + compact), the blocks are all-gathered (16 KB per rank), every rank takes
+             * the union sorted by value bits -- the same table everywhere -- and the segments
+             * travel as arcs + u16 indices: 6 B per arc instead of 12. Taken when the post pass
+             * will be the packed one (levels <= lw <= 31, pkw) and the fill needs no sort (the
+             * sort carries the f64s); more than LVL_RT_CAP values in the union (or a probe
+             * overflow) keeps the f64 segments, on every rank alike. A solo rank (xfull) holds
+             * every segment: it numbers all of them and the collectives only charge the wire. */
+            const int me = srt_comm_rank(comm);
+            if (gat && sorted_w && lw <= 31 && srt_form_int("pkw", 1) != 0) {
+                SRT_HIPCHK(hipMemsetAsync(gat, 0, (size_t)R * LVL_GB * sizeof(double), st));
+                for (int q = 0; q < R; q++) {
+                    const int cq = hoff[q + 1] - hoff[q];
+                    if ((!xfull && q != me) || cq <= 0) continue;
+                    SRT_HIPCHK(hipMemsetAsync(dflag, 0, 2 * sizeof(int), st));
+                    SRT_HIPCHK(hipMemsetAsync(H, 0xFF, LVL_RT_SLOTS * sizeof(unsigned long long), st));
+                    lvl_rt_hash_kernel<<<srt_ceil_div(cq, 256), 256, 0, st>>>(cq, arA + hoff[q], H,
+                                                                            rix + hoff[q], dflag);
+                    lvl_rt_compact_kernel<<<1, 1024, 0, st>>>(H, map, gat + q * LVL_GB + 1, dflag + 1);
+                    SRT_HIPCHK(hipGetLastError());
+                    SRT_HIPCHK(hipMemcpyAsync(gat + q * LVL_GB, dflag, 2 * sizeof(int),
+                                              hipMemcpyDeviceToDevice, st));
+                }
+                if ((rc_ = srt_coll_allgather(comm, gat, LVL_GB * sizeof(double), st))) return rc_;
+                std::vector<unsigned long long> hg((size_t)R * LVL_GB);
+                SRT_HIPCHK(hipMemcpyAsync(hg.data(), gat, hg.size() * sizeof(unsigned long long),
+                                          hipMemcpyDeviceToHost, st));
+                SRT_HIPCHK(hipStreamSynchronize(st));
+                std::vector<unsigned long long> u;
+                bool fit = true;
+                for (int q = 0; q < R && fit; q++) {
+                    int hd[2];
+                    memcpy(hd, &hg[(size_t)q * LVL_GB], sizeof(hd));
+                    if (hd[0] || hd[1] > LVL_RT_CAP) fit = false;
+                    else u.insert(u.end(), hg.begin() + (size_t)q * LVL_GB + 1,
+                                  hg.begin() + (size_t)q * LVL_GB + 1 + hd[1]);
+                }
+                if (fit) {
+                    std::sort(u.begin(), u.end());
+                    u.erase(std::unique(u.begin(), u.end()), u.end());
+                    fit = !u.empty() && u.size() <= (size_t)LVL_RT_CAP;
+                }
+                if (fit) {
+                    const int nu = (int)u.size(), hf[2] = {0, nu};
+                    SRT_HIPCHK(hipMemcpyAsync(rtab, u.data(), u.size() * sizeof(double),
+                                              hipMemcpyHostToDevice, st));
+                    SRT_HIPCHK(hipMemcpyAsync(dflag, hf, sizeof(hf), hipMemcpyHostToDevice, st));
+                    for (int q = 0; q < R; q++) {
+                        const int cq = hoff[q + 1] - hoff[q];
+                        if ((!xfull && q != me) || cq <= 0) continue;
+                        lvl_rt_index_kernel<<<srt_ceil_div(cq, 256), 256, 0, st>>>(
+                            cq, arA + hoff[q], reinterpret_cast<const unsigned long long*>(rtab), nu,
+                            rix + hoff[q]);
+                    }
+                    SRT_HIPCHK(hipGetLastError());
+                    SRT_HIPCHK(hipStreamSynchronize(st)); /* hf and u leave scope */
+                    numbered = 1;
+                }
+            }
             rc_ = srt_coll_group_begin(comm);
             for (int q = 0; q < R && !rc_; q++)
                 if (hoff[q + 1] > hoff[q]) {
                     const size_t c = (size_t)(hoff[q + 1] - hoff[q]);
                     rc_ = srt_coll_bcast(comm, arcsA + hoff[q], c * sizeof(uint32_t), q, st);
-                    if (!rc_) rc_ = srt_coll_bcast(comm, arA + hoff[q], c * sizeof(double), q, st);
+                    if (!rc_)
+                        rc_ = numbered ? srt_coll_bcast(comm, rix + hoff[q], c * sizeof(uint16_t), q, st)
+                                       : srt_coll_bcast(comm, arA + hoff[q], c * sizeof(double), q, st);
                 }
             const int rc2 = srt_coll_group_end(comm);
             if (rc_ || rc2) return rc_ ? rc_ : rc2;
@@ -1286,7 +1374,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
             SRT_HIPCHK(hipGetLastError());
         }
         /* the reliability table: its flags are read with the levels' completion (no round trip) */
-        if (want_rt && total_x > 0) {
+        if (want_rt && total_x > 0 && !numbered) {
             SRT_HIPCHK(hipMemsetAsync(dflag, 0, 2 * sizeof(int), st));
             SRT_HIPCHK(hipMemsetAsync(H, 0xFF, LVL_RT_SLOTS * sizeof(unsigned long long), st));
             lvl_rt_hash_kernel<<<srt_ceil_div(total_x, 256), 256, 0, st>>>(total_x, ar, H, rix, dflag);

@@ -398,7 +398,7 @@ def test_sparse_source_shard_allgather_gloo(native):
 
 
 # ---- the row-sharded Dial level build (levels.hip srt_levels_build), its collectives in order --
-LVL_STRIDE, LVL_WMAX = 256, 254
+LVL_STRIDE, LVL_WMAX, RT_CAP = 256, 254, 2048
 
 
 def _lvl_estimate(hist, L, ntgt, nw):
@@ -413,7 +413,9 @@ def _lvl_estimate(hist, L, ntgt, nw):
 def _levels_worker(rank, R, port, n, seed, lat_max, memcap_levels, q):
     """One rank of srt_levels_build: count pass over its rows, count all-reduce (sum), budget,
     budget agreement (min all-reduce), allocation agreement (min), fill, per-rank segment
-    broadcasts, per-target sort by (weight, tail), the levels over this rank's sources, the
+    numbered segments (each rank's distinct reliabilities all-gathered, the union sorted by bits,
+    indices instead of f64s), broadcasts, per-target sort by (weight, tail), the levels over this
+    rank's sources, the
     canonical predecessors and path-order products, verdict agreement (min). numpy compute, gloo
     collectives; memcap_levels[rank] stands in for each rank's device-memory cap on the budget."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -460,14 +462,33 @@ def _levels_worker(rank, R, port, n, seed, lat_max, memcap_levels, q):
     off = np.concatenate([[0], np.cumsum(cnt.reshape(-1))]).astype(np.int64)
     total = int(off[-1])
     assert total == int(hist[1:lmax + 1].sum())  # the total the host takes from the histogram
-    arcs = np.zeros((total, 2), np.int64)  # (weight, tail)
+    arcs = np.zeros((total, 3), np.int64)  # (weight, tail, reliability index)
+    ar = np.zeros(total)  # the arc's reliability (this rank's segment)
     for j in range(b, min(e, n)):
         cur = {x: int(off[j * LVL_STRIDE + x]) for x in range(1, lmax + 1)}
         for k in range(n):
             x = int(w[j, k])
             if k != j and 1 <= x <= lmax:
-                arcs[cur[x]] = (x, k)
+                arcs[cur[x], :2] = (x, k)
+                ar[cur[x]] = rr[k, j]
                 cur[x] += 1
+    # numbered segments: this rank's distinct reliabilities (bit patterns), all-gathered in
+    # fixed blocks (count, then up to RT_CAP values), the union sorted by bits on every rank
+    o0, o1 = int(off[b * LVL_STRIDE]), int(off[e * LVL_STRIDE])
+    mine = np.unique(ar[o0:o1].view(np.uint64))
+    assert mine.size <= RT_CAP
+    blk = np.zeros(RT_CAP + 1, np.uint64)
+    blk[0], blk[1:1 + mine.size] = mine.size, mine
+    parts = [torch.zeros(RT_CAP + 1, dtype=torch.int64) for _ in range(R)]
+    dist.all_gather(parts, torch.from_numpy(blk.view(np.int64)))  # srt_coll_allgather
+    calls.append(("allgather", RT_CAP + 1))
+    union = []
+    for t_ in parts:
+        v = t_.numpy().view(np.uint64)
+        union.append(v[1:1 + int(v[0])])
+    rtab_bits = np.unique(np.concatenate(union))  # sorted by bits, identical on every rank
+    rtab = rtab_bits.view(np.float64)
+    arcs[o0:o1, 2] = np.searchsorted(rtab_bits, ar[o0:o1].view(np.uint64))
     for x in range(R):  # one broadcast per rank's segment (srt_coll_bcast in a group)
         qb, qe = _shard(L, ld, R, x)
         o0, o1 = int(off[qb * LVL_STRIDE]), int(off[qe * LVL_STRIDE])
@@ -477,10 +498,11 @@ def _levels_worker(rank, R, port, n, seed, lat_max, memcap_levels, q):
             calls.append(("bcast", x, o1 - o0))
             arcs[o0:o1] = seg.numpy()
     # per target: sorted by (weight, tail)
-    ins = {}
+    ins, rix = {}, {}
     for j in range(n):
         a = arcs[off[j * LVL_STRIDE]:off[(j + 1) * LVL_STRIDE]]
-        ins[j] = sorted((int(x), int(k)) for x, k in a)
+        ins[j] = sorted((int(x), int(k)) for x, k, _ in a)
+        rix.update({(int(k), j): int(i) for _, k, i in a})
     # the levels over the local sources s in [b, min(e, n))
     src = list(range(b, min(e, n)))
     ns = len(src)
@@ -521,7 +543,7 @@ def _levels_worker(rank, R, port, n, seed, lat_max, memcap_levels, q):
                 if D[i, k] + x == D[i, j] and (best is None or (x, -k) > (best[0], -best[1])):
                     best = (x, k)
             u = best[1]
-            rel[i, j] = (1.0 if u == s else rel[i, u]) * rr[u, j]
+            rel[i, j] = (1.0 if u == s else rel[i, u]) * rtab[rix[(u, j)]]
     q.put((rank, "levels", calls, b, D, rel))
     dist.barrier()
     dist.destroy_process_group()

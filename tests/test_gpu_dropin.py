@@ -445,12 +445,12 @@ def test_dense_rows_few_attached(gpu, kind):
     assert np.array_equal(lat, full["lat_int"][sub]) and np.array_equal(rel, full["rel"][sub])
     if kind == "sub_ms":
         assert np.array_equal(ms, full["lat_ms"][sub])
-    # the same request with the rows path off takes the FW and agrees
-    from conftest import form_env
-    with form_env(rows=0):
-        lat2, rel2, _, _, st2 = build_tables_subset(g.n, g.directed, g.src, g.dst, g.lat_ns,
-                                                    g.loss, verts=verts, algo=ALGO_AUTO)
-    assert st2.dist_enc != 10 and np.array_equal(lat, lat2) and np.array_equal(rel, rel2)
+    # the all-pairs build of the same graph (every vertex attached: no rows path) agrees on the
+    # attached vertices' sub-table
+    lat2, rel2, _, _, st2 = build_tables_subset(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss,
+                                                verts=None, algo=ALGO_AUTO)
+    assert st2.dist_enc != 10
+    assert np.array_equal(lat, lat2[sub]) and np.array_equal(rel, rel2[sub])
 
 
 def test_dense_rows_c4_50_attached(gpu):
