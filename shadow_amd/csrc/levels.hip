@@ -1293,18 +1293,20 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
              * overflow) keeps the f64 segments, on every rank alike. A solo rank (xfull) holds
              * every segment: it numbers all of them and the collectives only charge the wire. */
             const int me = srt_comm_rank(comm);
+            /* the arcs this process numbers: its own segment, or (solo) every segment at once,
+             * in block 0 */
+            const int nb0 = xfull ? hoff[0] : hoff[me], nb1 = xfull ? hoff[R] : hoff[me + 1];
+            const int qb = xfull ? 0 : me;
             if (gat && sorted_w && lw <= 31 && srt_form_int("pkw", 1) != 0) {
                 SRT_HIPCHK(hipMemsetAsync(gat, 0, (size_t)R * LVL_GB * sizeof(double), st));
-                for (int q = 0; q < R; q++) {
-                    const int cq = hoff[q + 1] - hoff[q];
-                    if ((!xfull && q != me) || cq <= 0) continue;
+                if (nb1 > nb0) {
                     SRT_HIPCHK(hipMemsetAsync(dflag, 0, 2 * sizeof(int), st));
                     SRT_HIPCHK(hipMemsetAsync(H, 0xFF, LVL_RT_SLOTS * sizeof(unsigned long long), st));
-                    lvl_rt_hash_kernel<<<srt_ceil_div(cq, 256), 256, 0, st>>>(cq, arA + hoff[q], H,
-                                                                            rix + hoff[q], dflag);
-                    lvl_rt_compact_kernel<<<1, 1024, 0, st>>>(H, map, gat + q * LVL_GB + 1, dflag + 1);
+                    lvl_rt_hash_kernel<<<srt_ceil_div(nb1 - nb0, 256), 256, 0, st>>>(
+                        nb1 - nb0, arA + nb0, H, rix + nb0, dflag);
+                    lvl_rt_compact_kernel<<<1, 1024, 0, st>>>(H, map, gat + qb * LVL_GB + 1, dflag + 1);
                     SRT_HIPCHK(hipGetLastError());
-                    SRT_HIPCHK(hipMemcpyAsync(gat + q * LVL_GB, dflag, 2 * sizeof(int),
+                    SRT_HIPCHK(hipMemcpyAsync(gat + qb * LVL_GB, dflag, 2 * sizeof(int),
                                               hipMemcpyDeviceToDevice, st));
                 }
                 if ((rc_ = srt_coll_allgather(comm, gat, LVL_GB * sizeof(double), st))) return rc_;
@@ -1331,13 +1333,10 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
                     SRT_HIPCHK(hipMemcpyAsync(rtab, u.data(), u.size() * sizeof(double),
                                               hipMemcpyHostToDevice, st));
                     SRT_HIPCHK(hipMemcpyAsync(dflag, hf, sizeof(hf), hipMemcpyHostToDevice, st));
-                    for (int q = 0; q < R; q++) {
-                        const int cq = hoff[q + 1] - hoff[q];
-                        if ((!xfull && q != me) || cq <= 0) continue;
-                        lvl_rt_index_kernel<<<srt_ceil_div(cq, 256), 256, 0, st>>>(
-                            cq, arA + hoff[q], reinterpret_cast<const unsigned long long*>(rtab), nu,
-                            rix + hoff[q]);
-                    }
+                    if (nb1 > nb0)
+                        lvl_rt_index_kernel<<<srt_ceil_div(nb1 - nb0, 256), 256, 0, st>>>(
+                            nb1 - nb0, arA + nb0, reinterpret_cast<const unsigned long long*>(rtab), nu,
+                            rix + nb0);
                     SRT_HIPCHK(hipGetLastError());
                     SRT_HIPCHK(hipStreamSynchronize(st)); /* hf and u leave scope */
                     numbered = 1;
