@@ -2,7 +2,8 @@
 # A/B of side-by-side library builds (make ... OUT=../ab_<v>.so EXTRA=-D...) on the GPU box:
 # per variant, the level parity tests, then a C4 bench line.
 # usage: bash tools/ab_libs.sh <tag> <workload> <variant> [<variant> ...]   (variant "default" or
-# the <v> of shadow_amd/ab_<v>.so)
+# the <v> of shadow_amd/ab_<v>.so); AB_TESTS overrides the parity tests run per variant
+# (default: tests/test_gpu_levels.py -k match_oracle)
 set -o pipefail
 TAG=$1; WL=$2; shift 2
 O=gpurun_out/$TAG
