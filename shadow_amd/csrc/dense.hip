@@ -1299,6 +1299,9 @@ static void rel_tree_launch(int n, int ld, int row0, int lrows, const LT* d, con
  * A row with more parents than the cap slots takes rel_sweeps_kernel from the r(pred, t) it
  * leaves in the rel row (sweep[row] = 1). */
 #define REL_PK_NT 512
+#ifndef REL_PK_NTS
+#define REL_PK_NTS 0 /* 1: the rows' stores non-temporal (4.47-4.53 against 3.83 ms plain, r05nt) */
+#endif
 #ifndef REL_PK_PROF
 #define REL_PK_PROF 0 /* 1: phase wall clock of a few rows, printed */
 #endif
@@ -1466,10 +1469,16 @@ __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int ro
         /* whole 16-B pieces: one coalesced 1-KB run per wave for the u32 row, two for the f64 */
         typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
         typedef double f64x2v __attribute__((ext_vector_type(2)));
+#if REL_PK_NTS
         __builtin_nontemporal_store((u32x4v){lv[0], lv[1], lv[2], lv[3]},
                                     reinterpret_cast<u32x4v*>(lr + t0));
         __builtin_nontemporal_store((f64x2v){x[0], x[1]}, reinterpret_cast<f64x2v*>(rr + t0));
         __builtin_nontemporal_store((f64x2v){x[2], x[3]}, reinterpret_cast<f64x2v*>(rr + t0 + 2));
+#else
+        *reinterpret_cast<u32x4v*>(lr + t0) = (u32x4v){lv[0], lv[1], lv[2], lv[3]};
+        *reinterpret_cast<f64x2v*>(rr + t0) = (f64x2v){x[0], x[1]};
+        *reinterpret_cast<f64x2v*>(rr + t0 + 2) = (f64x2v){x[2], x[3]};
+#endif
         /* one piece at a time: hoisting every piece's LDS reads costs the second row per CU */
         __builtin_amdgcn_sched_barrier(0);
     }
