@@ -38,6 +38,10 @@
 #ifndef LVL_PB
 #define LVL_PB 12 /* lvl_pred_kernel: gathers per pipelined batch */
 #endif
+#ifndef LVL_PNT
+#define LVL_PNT 1 /* lvl_pred_kernel's packed words stored non-temporal, so they do not displace the
+                   * gathered plane slices from the MALL: 5.16 against 5.31-5.36 ms (r05pn) */
+#endif
 
 /* ---- in-arc extraction ------------------------------------------------------------------- */
 /* COUNT: per (target, weight) histogram of arcs with 1 <= w <= LVL_WMAX; FILL: the arcs (k | w << 16)
@@ -863,8 +867,14 @@ static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx
         }
         PT* pp = predT + (size_t)t * ldp + sl0;
         if constexpr (PK) { /* 32 B per lane: a wave's quarter is one 2-KB run */
+#if LVL_PNT
+            typedef unsigned u32x4n __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store((u32x4n){kv[0], kv[1], kv[2], kv[3]}, reinterpret_cast<u32x4n*>(pp));
+            __builtin_nontemporal_store((u32x4n){kv[4], kv[5], kv[6], kv[7]}, reinterpret_cast<u32x4n*>(pp + 4));
+#else
             *reinterpret_cast<uint4*>(pp) = make_uint4(kv[0], kv[1], kv[2], kv[3]);
             *reinterpret_cast<uint4*>(pp + 4) = make_uint4(kv[4], kv[5], kv[6], kv[7]);
+#endif
             continue;
         }
         double* rp = rT + (size_t)t * ldp + sl0;
