@@ -244,6 +244,13 @@ int srt_comm_init_solo(int32_t nranks, int32_t rank, int32_t device, srt_comm** 
 int srt_comm_init_solo_wire(int32_t nranks, int32_t rank, int32_t device, double gbps,
                             double lat_us, srt_comm** comm);
 double srt_comm_wire_ms(const srt_comm* comm);
+/* Collective log: with on != 0 every srt_coll_* call of the communicator appends (op, a, b) --
+ * 1 broadcast (bytes, root), 2 all-reduce (count, op_min), 3 all-gather (bytes per rank, 0),
+ * 4 exchange (0, 0), 5 group begin, 6 group end, 7 sparse all-gather (rows per rank, n).
+ * Enabling clears the log. srt_comm_log_read copies up to cap entries (3 int64 each) into out
+ * and returns the number logged. The ranks' logs of one build must be identical (SPMD). */
+int srt_comm_log_enable(srt_comm* comm, int32_t on);
+int64_t srt_comm_log_read(const srt_comm* comm, int64_t* out, int64_t cap);
 /* ranks of the communicator: ncclCommCount for RCCL, nranks for virtual / timing-only ranks */
 int srt_comm_count(const srt_comm* comm, int32_t* count);
 int srt_comm_init_virtual(int32_t nranks, int32_t device, srt_comm** comms);

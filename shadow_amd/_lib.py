@@ -112,6 +112,8 @@ SIGNATURES = {
     "srt_comm_init_solo": (ctypes.c_int, [_I32, _I32, _I32, _VP]),
     "srt_comm_init_solo_wire": (ctypes.c_int, [_I32, _I32, _I32, _D, _D, _VP]),
     "srt_comm_wire_ms": (_D, [_VP]),
+    "srt_comm_log_enable": (ctypes.c_int, [_VP, _I32]),
+    "srt_comm_log_read": (_I64, [_VP, _VP, _I64]),
     "srt_comm_count": (ctypes.c_int, [_VP, _VP]),
     "srt_virtual_rank_bind": (ctypes.c_int, [_I32, _I32]),
     "srt_comm_free": (None, [_VP]),

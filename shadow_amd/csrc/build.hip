@@ -140,9 +140,7 @@ struct srt_sparse_graph {
     int32_t ntab; /* entries of rtab */
 };
 
-#ifndef DERIVE_MAXDEG
-#define DERIVE_MAXDEG 4 /* <= derive.hip's DV_MAXDEG */
-#endif
+#define DERIVE_MAXDEG SRT_DERIVE_MAXDEG /* derive.hip's DV_MAXDEG */
 
 int srt_wgsssp_max_n(void);
 int srt_wide_rows(int n, const int32_t* rp, const int32_t* col, const uint32_t* w, const double* r,

@@ -45,7 +45,50 @@ struct srt_comm {
     hipEvent_t* tev;
     int tcap, tused;
     hipStream_t t_stream; /* the stream the open group's first collective named */
+    /* collective log (srt_comm_log_enable): (op, a, b) per call, in call order -- what the ranks'
+     * sequences are compared by (tests/test_gpu_protocol.py against the gloo rehearsal) */
+    int log_on;
+    int64_t* logv;
+    size_t log_n, log_cap;
 };
+
+enum { SRT_LOG_BCAST = 1, SRT_LOG_ALLREDUCE, SRT_LOG_ALLGATHER, SRT_LOG_EXCHANGE, SRT_LOG_GROUP_BEGIN,
+       SRT_LOG_GROUP_END, SRT_LOG_SPARSE_ALLGATHER };
+
+static void c_log(const srt_comm* cc, int op, int64_t a, int64_t b) {
+    srt_comm* c = const_cast<srt_comm*>(cc);
+    if (!c->log_on) return;
+    if (c->log_n == c->log_cap) {
+        const size_t nc = c->log_cap ? 2 * c->log_cap : 256;
+        int64_t* nv = (int64_t*)realloc(c->logv, nc * 3 * sizeof(int64_t));
+        if (!nv) return; /* the log stops growing; the comparison then fails on its length */
+        c->logv = nv;
+        c->log_cap = nc;
+    }
+    int64_t* e = c->logv + 3 * c->log_n++;
+    e[0] = op;
+    e[1] = a;
+    e[2] = b;
+}
+
+extern "C" int srt_comm_log_enable(srt_comm* c, int32_t on) {
+    if (!c) {
+        srt_set_error("srt_comm_log_enable: bad arguments");
+        return SRT_E_ARG;
+    }
+    c->log_on = on != 0;
+    c->log_n = 0;
+    return SRT_OK;
+}
+
+extern "C" int64_t srt_comm_log_read(const srt_comm* c, int64_t* out, int64_t cap) {
+    if (!c) return -1;
+    const int64_t k = (int64_t)c->log_n;
+    if (out)
+        for (int64_t i = 0; i < k && i < cap; i++)
+            for (int f = 0; f < 3; f++) out[3 * i + f] = c->logv[3 * i + f];
+    return k;
+}
 
 static thread_local int t_vslot = -1;
 void srt_set_virtual_slot(int rank) { t_vslot = rank; }
@@ -369,6 +412,7 @@ extern "C" void srt_comm_free(srt_comm* comm) {
     }
     for (int i = 0; i < comm->tcap; i++) (void)hipEventDestroy(comm->tev[i]);
     free(comm->tev);
+    free(comm->logv);
     free(comm);
 }
 
@@ -445,6 +489,7 @@ static int allreduce_impl(const srt_comm* c, int32_t* buf, size_t count, int op_
 }
 
 int srt_coll_group_begin(const srt_comm* c) {
+    c_log(c, SRT_LOG_GROUP_BEGIN, 0, 0);
     if (!c->loop && !c->solo) SRT_NCCLCHK(ncclGroupStart());
     srt_comm* m = const_cast<srt_comm*>(c);
     m->in_group = 1;
@@ -457,6 +502,7 @@ int srt_coll_group_begin(const srt_comm* c) {
 }
 
 int srt_coll_group_end(const srt_comm* c) {
+    c_log(c, SRT_LOG_GROUP_END, 0, 0);
     if (!c->loop && !c->solo) SRT_NCCLCHK(ncclGroupEnd());
     srt_comm* m = const_cast<srt_comm*>(c);
     const int was = m->in_group;
@@ -585,20 +631,24 @@ static int sparse_allgather_impl(srt_comm* comm, int32_t n, int32_t rows_per_ran
     } while (0)
 
 int srt_coll_bcast(const srt_comm* c, void* buf, size_t bytes, int root, hipStream_t st) {
+    c_log(c, SRT_LOG_BCAST, (int64_t)bytes, root);
     SRT_TIMED(st, bcast_impl(c, buf, bytes, root, st));
 }
 
 int srt_coll_allreduce_i32(const srt_comm* c, int32_t* buf, size_t count, int op_min,
                            hipStream_t st) {
+    c_log(c, SRT_LOG_ALLREDUCE, (int64_t)count, op_min);
     SRT_TIMED(st, allreduce_impl(c, buf, count, op_min, st));
 }
 
 int srt_coll_exchange(const srt_comm* c, void* const* send, const size_t* send_bytes,
                       void* const* recv, const size_t* recv_bytes, hipStream_t st) {
+    c_log(c, SRT_LOG_EXCHANGE, 0, 0); /* (the byte counts differ per rank) */
     SRT_TIMED(st, exchange_impl(c, send, send_bytes, recv, recv_bytes, st));
 }
 
 int srt_coll_allgather(const srt_comm* c, void* buf, size_t bytes, hipStream_t st) {
+    c_log(c, SRT_LOG_ALLGATHER, (int64_t)bytes, 0);
     SRT_TIMED(st, allgather_impl(c, buf, bytes, st));
 }
 
@@ -608,5 +658,6 @@ extern "C" int srt_sparse_allgather(srt_comm* c, int32_t n, int32_t rows_per_ran
         srt_set_error("srt_sparse_allgather: bad arguments");
         return SRT_E_ARG;
     }
+    c_log(c, SRT_LOG_SPARSE_ALLGATHER, rows_per_rank, n);
     SRT_TIMED((hipStream_t)stream, sparse_allgather_impl(c, n, rows_per_rank, lat_all, rel_all, stream));
 }

@@ -1299,12 +1299,8 @@ static void rel_tree_launch(int n, int ld, int row0, int lrows, const LT* d, con
  * A row with more parents than the cap slots takes rel_sweeps_kernel from the r(pred, t) it
  * leaves in the rel row (sweep[row] = 1). */
 #define REL_PK_NT 512
-#ifndef REL_PK_NTS
-#define REL_PK_NTS 0 /* 1: the rows' stores non-temporal (4.47-4.53 against 3.83 ms plain, r05nt) */
-#endif
-#ifndef REL_PK_PROF
-#define REL_PK_PROF 0 /* 1: phase wall clock of a few rows, printed */
-#endif
+/* (plain row stores: non-temporal ones measured 4.47-4.53 against 3.83 ms, r05nt; the per-phase
+ * wall-clock profile of round 5 is in DESIGN §5.8b) */
 template <int K>
 __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int row0,
                                                            const uint32_t* __restrict__ pk,
@@ -1315,13 +1311,6 @@ __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int ro
                                                            int32_t* __restrict__ sweep) {
     constexpr int NT = REL_PK_NT;
     const int s = row0 + (int)blockIdx.x;
-#if REL_PK_PROF
-    unsigned long long pt[6];
-    pt[0] = wall_clock64();
-#define REL_PK_T(i) do { if (threadIdx.x == 0) pt[i] = wall_clock64(); } while (0)
-#else
-#define REL_PK_T(i) ((void)0)
-#endif
     const int tid = threadIdx.x, lane = tid & 63;
     const int nwb = ld >> 5; /* parent bitmap words (ld % 128 == 0) */
     extern __shared__ __attribute__((aligned(16))) uint32_t psm[];
@@ -1376,7 +1365,6 @@ __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int ro
     for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
     if (lane == 0) red[tid >> 6] = mx;
     __syncthreads(); /* par, red */
-    REL_PK_T(1);
     mx = 0;
     for (int i = 0; i < NT / 64; ++i) mx = max(mx, red[i]);
     /* exclusive prefix of the parent counts; thread tid owns bitmap words tid * wpt.. */
@@ -1409,7 +1397,6 @@ __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int ro
     const bool bail = total > (uint32_t)cap;
     if (tid == 0) sweep[blockIdx.x] = bail;
     __syncthreads(); /* pre */
-    REL_PK_T(2);
     auto rank = [&](uint32_t u) {
         return pre[u >> 5] + (uint32_t)__popc(par[u >> 5] & ((1u << (u & 31)) - 1u));
     };
@@ -1439,7 +1426,6 @@ __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int ro
             __syncthreads();
         }
     }
-    REL_PK_T(3);
 #pragma unroll
     for (int k = 0; k < K; ++k)
         asm volatile("" : "+v"(wd[k].x), "+v"(wd[k].y), "+v"(wd[k].z), "+v"(wd[k].w));
@@ -1469,29 +1455,13 @@ __global__ __launch_bounds__(REL_PK_NT) void rel_pk_kernel(int n, int ld, int ro
         /* whole 16-B pieces: one coalesced 1-KB run per wave for the u32 row, two for the f64 */
         typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
         typedef double f64x2v __attribute__((ext_vector_type(2)));
-#if REL_PK_NTS
-        __builtin_nontemporal_store((u32x4v){lv[0], lv[1], lv[2], lv[3]},
-                                    reinterpret_cast<u32x4v*>(lr + t0));
-        __builtin_nontemporal_store((f64x2v){x[0], x[1]}, reinterpret_cast<f64x2v*>(rr + t0));
-        __builtin_nontemporal_store((f64x2v){x[2], x[3]}, reinterpret_cast<f64x2v*>(rr + t0 + 2));
-#else
         *reinterpret_cast<u32x4v*>(lr + t0) = (u32x4v){lv[0], lv[1], lv[2], lv[3]};
         *reinterpret_cast<f64x2v*>(rr + t0) = (f64x2v){x[0], x[1]};
         *reinterpret_cast<f64x2v*>(rr + t0 + 2) = (f64x2v){x[2], x[3]};
-#endif
         /* one piece at a time: hoisting every piece's LDS reads costs the second row per CU */
         __builtin_amdgcn_sched_barrier(0);
     }
     if (tid == 0) srt_max_once(max_depth, (int)mx);
-#if REL_PK_PROF
-    __syncthreads();
-    if (tid == 0) {
-        pt[4] = wall_clock64();
-        if (blockIdx.x % 4096 == 17)
-            printf("[rel_pk prof] row %d start %llu load+mark %llu prefix %llu levels %llu out %llu (x10 ns) parents %u\n",
-                   (int)blockIdx.x, pt[0], pt[1] - pt[0], pt[2] - pt[1], pt[3] - pt[2], pt[4] - pt[3], total);
-    }
-#endif
 }
 
 /* rel_pk_kernel at the row's width, then the sweeps for the rows over the parent cap */
@@ -2251,6 +2221,13 @@ static int dense_post_levels(int32_t n, int32_t ld, int32_t row0, int32_t nrows,
                              double* rel, hipStream_t st, srt_build_stats* stats, dense_ws* ws,
                              int lrows) {
     int rc;
+    if (lrows < nrows && srt_levels_pkw_ready()) { /* the padding rows of the last shard (or a
+        * shard past n): rel_pk_kernel writes the real rows only, so these take SRT_INF / 0 here,
+        * as lvl_out8_kernel's rows do on the other form */
+        SRT_HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d + (size_t)lrows * ld), (int)SRT_INF,
+                                     (size_t)(nrows - lrows) * ld, st));
+        SRT_HIPCHK(hipMemsetAsync(rel + (size_t)lrows * ld, 0, (size_t)(nrows - lrows) * ld * sizeof(double), st));
+    }
     if (lrows > 0 && srt_levels_pkw_ready()) {
         /* source-major packed words (lvl_pkw_kernel) + rel_pk_kernel, which writes the u32 rows
          * too: 4 B per pair written and read between them, no transposes, no u8 rows */

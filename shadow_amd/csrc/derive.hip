@@ -21,22 +21,11 @@
  */
 #include "srt_device.h"
 
-#ifndef DV_MAXDEG
-#define DV_MAXDEG 4   /* largest degree the host puts in I (build.hip DERIVE_MAXDEG) */
-#endif
-#ifndef DV_J
-#define DV_J 2        /* targets per thread per phase-A step: their loads overlap */
-#endif
-#ifndef DV_SPEC
-#define DV_SPEC 1     /* phase A loads every neighbour's code with its distance (no second trip) */
-#endif
-#ifndef DV_PROF
-#define DV_PROF 0     /* 1: per-phase wall-clock and counts of block 0 and 1, printed */
-#endif
-#ifndef DV_PROBE
-#define DV_PROBE 0    /* 1: phase A alone (timing probe, wrong reliabilities) */
-#endif
-#define DV_JB 1       /* targets per thread per phase-B step (4: 138 vs 125 ms on C5) */
+#define DV_MAXDEG SRT_DERIVE_MAXDEG /* largest degree the host puts in I (build.hip) */
+#define DV_J 2  /* targets per thread per phase-A step: their loads overlap */
+#define DV_JB 1 /* targets per thread per phase-B step (4: 138 vs 125 ms on C5) */
+/* (round-5 A/B forms -- phase A without the speculative code loads, per-phase wall-clock
+ * profiles, the phase-A-only probe -- were measured and left the library: DESIGN §5.9) */
 
 /* order of canonical arcs u | w << 17 | ridx << 24: the largest w, then the smallest u */
 static __device__ __forceinline__ uint32_t dv_key(uint32_t code) {
@@ -82,14 +71,6 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
         return (__hip_atomic_load(&cdone[v >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >>
                 (v & 31)) & 1u;
     };
-#if DV_PROF
-    __shared__ unsigned long long p_climb, p_glob, p_rdy;
-    unsigned long long tA = 0, tB = 0, tq = 0, nrow = 0;
-    if (tid == 0) p_climb = p_glob = p_rdy = 0;
-#define DV_CNT(x, v) atomicAdd(&(x), (unsigned long long)(v))
-#else
-#define DV_CNT(x, v) ((void)0)
-#endif
     for (int si = blockIdx.x; si < nI; si += gridDim.x) {
         const int s = I[si];
         uint32_t* ol = lat + (size_t)(s - src_begin) * ldo;
@@ -107,9 +88,6 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
         for (int q = tid; q < nw; q += NT) cdone[q] = 0u;
         __threadfence_block();
         __syncthreads();
-#if DV_PROF
-        if (tid == 0) tq = wall_clock64();
-#endif
         /* phase A (as derive_rows_kernel): distances, derived codes; s and the unreachable
          * targets are done at once */
         for (int t0 = 0; t0 < n; t0 += DV_J * NT) {
@@ -123,15 +101,14 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
                                    ? lat[(size_t)(s_nb[i] - src_begin) * ldo + t]
                                    : SRT_INF;
             }
+            /* every neighbour's code with its distance: no second round trip */
             uint32_t cv[DV_J][DV_MAXDEG];
-            if (DV_SPEC) {
 #pragma unroll
-                for (int j = 0; j < DV_J; ++j) {
-                    const int t = t0 + j * NT + tid;
+            for (int j = 0; j < DV_J; ++j) {
+                const int t = t0 + j * NT + tid;
 #pragma unroll
-                    for (int i = 0; i < DV_MAXDEG; ++i)
-                        cv[j][i] = (i < deg && t < n) ? codes[(size_t)s_cr[i] * n + t] : ~0u;
-                }
+                for (int i = 0; i < DV_MAXDEG; ++i)
+                    cv[j][i] = (i < deg && t < n) ? codes[(size_t)s_cr[i] * n + t] : ~0u;
             }
             uint32_t D[DV_J];
 #pragma unroll
@@ -152,7 +129,7 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
                         cd[j][i] = t == s_nb[i]
                                        ? ((uint32_t)s | ((uint32_t)s_w[i] << 17) |
                                           ((uint32_t)s_rx[i] << 24))
-                                       : DV_SPEC ? cv[j][i] : codes[(size_t)s_cr[i] * n + t];
+                                       : cv[j][i];
                 }
             }
 #pragma unroll
@@ -178,13 +155,6 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
         }
         __threadfence_block();
         __syncthreads();
-#if DV_PROF
-        if (tid == 0) {
-            const unsigned long long x = wall_clock64();
-            tA += x - tq;
-            tq = x;
-        }
-#endif
         /* target t (its code ct) once its predecessor is not formed: climb to the first ancestor
          * whose predecessor is, form it, and repeat until t is formed */
         auto climb = [&](int t, uint32_t ct) {
@@ -193,7 +163,6 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
                 while (!is_done(cy & 0x1FFFFu)) {
                     y = cy & 0x1FFFFu;
                     cy = cs[y];
-                    DV_CNT(p_climb, 1);
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 const double rp = rel_of(cy & 0x1FFFFu, orr);
@@ -207,7 +176,7 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
         /* phase B: on-demand path-order products. DV_JB targets per thread per step: their
          * codes, then the predecessors' values of the ready ones, in flight together; a target
          * whose predecessor is not formed yet climbs alone */
-        for (int t0 = 0; t0 < n && !DV_PROBE; t0 += DV_JB * NT) {
+        for (int t0 = 0; t0 < n; t0 += DV_JB * NT) {
             uint32_t cj[DV_JB];
             bool rdy[DV_JB];
 #pragma unroll
@@ -238,29 +207,8 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
                 if (cj[j] == ~0u || rdy[j] || is_done((uint32_t)t)) continue;
                 climb(t, cj[j]);
             }
-#if DV_PROF
-#pragma unroll
-            for (int j = 0; j < DV_JB; ++j)
-                if (rdy[j]) {
-                    DV_CNT(p_rdy, 1);
-                    if (!CACHE || (cj[j] & 0x1FFFFu) >= (uint32_t)CACHE) DV_CNT(p_glob, 1);
-                }
-#endif
         }
-#if DV_PROF
-        __syncthreads();
-        if (tid == 0) {
-            tB += wall_clock64() - tq;
-            ++nrow;
-        }
-#endif
     }
-#if DV_PROF
-    if (tid == 0 && blockIdx.x < 2)
-        printf("[derive prof] block %d rows %llu phaseA %.1f us/row phaseB %.1f us/row climbs %.0f/row ready %.0f/row ready-global %.0f/row\n",
-               (int)blockIdx.x, nrow, tA * 0.01 / nrow, tB * 0.01 / nrow, (double)p_climb / nrow,
-               (double)p_rdy / nrow, (double)p_glob / nrow);
-#endif
 }
 
 

@@ -49,7 +49,7 @@ static __device__ __forceinline__ uint32_t splat(uint32_t h) { return h | (h << 
 /* per half: min(acc, x, y) on u16 bit patterns in [0, 0x7BFF] -> one v_pk_minimum3_f16.
  * Inline asm: written with the generic minimum builtins, LLVM re-associates the chain across
  * pivot pairs into two-input minimum3s with a duplicated operand (1.5x the min instructions). */
-/* (the FWQ_ROWS_FORM 0 instruction mix of the A/B builds in tools/) */
+/* (the plain-C row step's instruction mix of the A/B builds in tools/) */
 __attribute__((unused)) static __device__ __forceinline__ uint32_t min3h(uint32_t acc, uint32_t x,
                                                                          uint32_t y) {
     uint32_t r;
@@ -621,37 +621,14 @@ static __device__ __forceinline__ void fwq_swrite(const fwq_stage_regs& g, uint3
     *reinterpret_cast<uint4*>(sB + rb * UBS + cb) = g.b;
 }
 
-/* rows 0..3 of the thread's 4x8 block, pivots m, m+1: 32 v_add_u32 + 16 v_pk_minimum3_f16.
- * FWQ_ROWS_FORM (build-time A/B): 1 = fixed add, add, min3 triples; 2 = one asm block per row;
- * 0 = plain C (the scheduler hoists the adds) */
-#ifndef FWQ_ROWS_FORM
-#define FWQ_ROWS_FORM 2
-#endif
+/* rows 0..3 of the thread's 4x8 block, pivots m, m+1: 32 v_add_u32 + 16 v_pk_minimum3_f16, one
+ * asm block per row (relax_row4; the fixed-triple and plain-C forms measured slower, §5.1) */
 static __device__ __forceinline__ void fwq_rows(uint32_t (&acc)[4][4], const uint2 (&a)[4],
                                                 const uint4 (&b)[2]) {
     const uint32_t b0[4] = {b[0].x, b[0].y, b[0].z, b[0].w};
     const uint32_t b1[4] = {b[1].x, b[1].y, b[1].z, b[1].w};
-#if FWQ_ROWS_FORM == 2
 #pragma unroll
     for (int r = 0; r < 4; ++r) relax_row4(acc[r], a[r].x, a[r].y, b0, b1);
-#elif FWQ_ROWS_FORM == 1
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[r][c] = relax2h(acc[r][c], a[r].x, b0[c], a[r].y, b1[c]);
-#else
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        uint32_t t0[4], t1[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            t0[c] = a[r].x + b0[c];
-            t1[c] = a[r].y + b1[c];
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[r][c] = min3h(acc[r][c], t0[c], t1[c]);
-    }
-#endif
 }
 
 static __device__ __forceinline__ void fwq_stage(uint32_t (&acc)[4][4], const uint32_t* __restrict__ sA,
@@ -845,9 +822,7 @@ static __device__ int sym_contrib_pos(int K, int J, int T, const int* __restrict
 
 /* rows of the staged-panel chain kernels per thread (sym_panel_stage_kernel, sym_cross_stage_kernel:
  * 1024 / SYM_RM threads per workgroup) */
-#ifndef SYM_RM
 #define SYM_RM 2
-#endif
 
 /* this rank's blocks of panel k into the staging buffer (64 x 128 each); with stage_b, a grid of
  * 2T also packs the band's second half (rows k0 + 64..) into stage_b (128-pivot rounds: one launch) */

@@ -35,13 +35,7 @@
 
 #define LVL_STRIDE 256 /* per-target offsets: weight 0..255 */
 #define LVL_WMAX 254   /* largest level budget (distances stay u8: the post pass's small path) */
-#ifndef LVL_PB
 #define LVL_PB 12 /* lvl_pred_kernel: gathers per pipelined batch */
-#endif
-#ifndef LVL_PNT
-#define LVL_PNT 1 /* lvl_pred_kernel's packed words stored non-temporal, so they do not displace the
-                   * gathered plane slices from the MALL: 5.16 against 5.31-5.36 ms (r05pn) */
-#endif
 
 /* ---- in-arc extraction ------------------------------------------------------------------- */
 /* COUNT: per (target, weight) histogram of arcs with 1 <= w <= LVL_WMAX; FILL: the arcs (k | w << 16)
@@ -494,12 +488,10 @@ static __device__ __forceinline__ uint32_t lvl_step_unit(unsigned g, int d, int 
      * the lane's) and one gather; sixteen gathers in flight. Lanes past nw read word 0 of the row
      * (a valid address) and drop it, so the loop has no per-lane branch. */
     const uint32_t lane4 = (uint32_t)(valid ? word : 0) * 4u;
+    constexpr int LVL_SB = 16; /* (8 measured the same, 32/48 slower; pipelined batches did not help) */
     for (int w = 1; w < d; ++w) {
         const int g1 = oj[w + 1];
         const char* base = reinterpret_cast<const char*>(lev + (size_t)(d - w - 1) * plane);
-#ifndef LVL_SB
-#define LVL_SB 16 /* (8 measured the same, 32/48 slower; pipelined batches did not help here) */
-#endif
         for (int i = oj[w]; i < g1; i += LVL_SB) { /* LVL_SB in flight, the tail predicated */
             uint32_t a[LVL_SB], v[LVL_SB];
 #pragma unroll
@@ -867,14 +859,11 @@ static __device__ __forceinline__ void lvl_pred_unit(unsigned g, uint16_t (*sidx
         }
         PT* pp = predT + (size_t)t * ldp + sl0;
         if constexpr (PK) { /* 32 B per lane: a wave's quarter is one 2-KB run */
-#if LVL_PNT
+            /* non-temporal: the words do not displace the gathered plane slices from the MALL
+             * (5.16 against 5.31-5.36 ms with plain stores, r05pn) */
             typedef unsigned u32x4n __attribute__((ext_vector_type(4)));
             __builtin_nontemporal_store((u32x4n){kv[0], kv[1], kv[2], kv[3]}, reinterpret_cast<u32x4n*>(pp));
             __builtin_nontemporal_store((u32x4n){kv[4], kv[5], kv[6], kv[7]}, reinterpret_cast<u32x4n*>(pp + 4));
-#else
-            *reinterpret_cast<uint4*>(pp) = make_uint4(kv[0], kv[1], kv[2], kv[3]);
-            *reinterpret_cast<uint4*>(pp + 4) = make_uint4(kv[4], kv[5], kv[6], kv[7]);
-#endif
             continue;
         }
         double* rp = rT + (size_t)t * ldp + sl0;
@@ -1080,20 +1069,53 @@ static size_t lvl_avail_bytes(void) {
 /* levels enqueued per host round trip: a batch's levels past the one that settles every pair
  * return at once (lvl_step_kernel's prev test) */
 #define LVL_BATCH 8
-/* settled fraction of the local pairs the first batch must reach for the build to go on */
+/* settled fraction of all pairs the first batch must reach for the build to go on */
 #define LVL_MIN_SETTLED 0.25
+
+/* The host-side words of a build (one allocation, zeroed): the weight histogram, the completion
+ * flags, the agreement word and the settled-pair counter, the histogram limbs of the N > 1 count
+ * exchange (+ the allocation-failure count), and the batch vote. Offsets in u64. */
+#define LVL_H_INC 256                            /* int dinc[LVL_WMAX + 1], then dflag[2] */
+#define LVL_H_AGREE 512                          /* int32 agreement word; u64 nset at +2 */
+#define LVL_H_LIMBS 520                          /* int32 [2 * LVL_STRIDE + 1] */
+#define LVL_H_VOTE (LVL_H_LIMBS + LVL_STRIDE + 1) /* int32 [4] */
+#define LVL_H_WORDS (LVL_H_VOTE + 2)
+
+/* N > 1, the end of a batch of levels: this rank's vote -- not done (its last level left a pair
+ * unsettled) and its settled-pair count in 21-bit limbs -- for one sum all-reduce, so every rank
+ * takes the batch's decision (stop, continue, extract heavier arcs, or Floyd-Warshall) from the
+ * same numbers */
+__global__ void lvl_vote_kernel(const int* __restrict__ inc_last,
+                                const unsigned long long* __restrict__ nset,
+                                int32_t* __restrict__ vote) {
+    if (threadIdx.x) return;
+    const unsigned long long s = *nset;
+    vote[0] = *inc_last != 0;
+    vote[1] = (int32_t)(s & 0x1FFFFFull);
+    vote[2] = (int32_t)((s >> 21) & 0x1FFFFFull);
+    vote[3] = (int32_t)(s >> 42);
+}
 
 /* One build of the local rows' distances (nrows x ld). comm (NULL on one GPU): undirected row
  * shards, every rank sees every target's in-arcs after the segment broadcasts. fw_ms: the
  * predicted Floyd-Warshall time (of the largest shard); the level budget keeps the predicted level
  * time under half of it. *levels = the level that settled every pair (0: not applicable / over
- * budget / out of memory -- the caller runs Floyd-Warshall). Every rank of a sharded build takes
- * the same decisions in the same order: the budget is agreed (min all-reduce) before the first
- * rank-dependent branch, so is the outcome of the allocations, and the verdict at the end; a rank
- * never leaves while its peers wait in a collective. *gather_bytes: the Delta words gathered (the
- * kernel's algorithmic bytes). On success the slot keeps the arcs and the planes for the post pass
- * until srt_levels_release; lat_rows hold the u32 rows, unless the post pass writes them itself
- * (srt_levels_pkw_ready). */
+ * budget / out of memory -- the caller runs Floyd-Warshall). *gather_bytes: the Delta words
+ * gathered (the kernel's algorithmic bytes). On success the slot keeps the arcs and the planes for
+ * the post pass until srt_levels_release; lat_rows hold the u32 rows, unless the post pass writes
+ * them itself (srt_levels_pkw_ready).
+ *
+ * The N > 1 protocol. Every branch after the first collective is taken on values every rank holds
+ * alike -- the summed histogram, the agreed budget, the agreed allocation outcome, the gathered
+ * reliability blocks, and each batch's summed vote -- so every rank makes the same collective calls
+ * in the same order and no rank leaves while its peers wait in one. In order: the histogram limbs
+ * with each rank's allocation-failure count (sum), the budget (min), the allocation outcome (min),
+ * the (target, weight <= lmax) counts (sum), the arcs of the first batch (the reliability blocks'
+ * all-gather, then one broadcast group of every rank's segment), then per batch of levels the vote
+ * (sum); a batch that leaves pairs unsettled at the first batch's last level fetches the heavier
+ * arcs the same way. The vote's "all done" is the verdict: no separate agreement.
+ * tests/test_dist_gloo.py rehearses this sequence over gloo and tests/test_gpu_protocol.py checks
+ * every rank's collective log (srt_comm_log_*) against it. */
 int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
                      const uint32_t* w_rows, const double* r_rows, uint32_t* lat_rows, double fw_ms,
                      hipStream_t st, evpool_t* evp, int* levels, int64_t* gather_bytes) {
@@ -1132,43 +1154,52 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         }
     } gd{L, st};
     const size_t ncnt = (size_t)ld * LVL_STRIDE;
+    unsigned long long* dhist = NULL; /* the host-side words (LVL_H_*), a few KB */
+    LVL_ALLOC(dhist, LVL_H_WORDS * sizeof(unsigned long long));
+    SRT_HIPCHK(hipMemsetAsync(dhist, 0, LVL_H_WORDS * sizeof(unsigned long long), st));
+    int* dinc = reinterpret_cast<int*>(dhist + LVL_H_INC);
+    int32_t* dagree = reinterpret_cast<int32_t*>(dhist + LVL_H_AGREE);
+    int32_t* limbs = reinterpret_cast<int32_t*>(dhist + LVL_H_LIMBS);
+    int32_t* dvote = reinterpret_cast<int32_t*>(dhist + LVL_H_VOTE);
+    /* the count pass's buffers, softly: a rank short of memory sends every rank to the FW through
+     * the failure count it adds to the histogram exchange (its limbs stay zero) */
+    int ok = 1;
     int32_t *cnt = NULL, *off = NULL;
-    unsigned long long* dhist = NULL;
-    LVL_ALLOC(cnt, (ncnt + 1 + 2 * LVL_STRIDE) * sizeof(int32_t)); /* + the histogram limbs */
-    LVL_ALLOC(off, (ncnt + 1) * sizeof(int32_t));
-    /* the histogram, then LVL_WMAX + 1 completion flags, then the agreement word */
-    LVL_ALLOC(dhist, (2 * LVL_STRIDE + 8) * sizeof(unsigned long long));
-    int* dinc = reinterpret_cast<int*>(dhist + LVL_STRIDE);
-    int32_t* dagree = reinterpret_cast<int32_t*>(dhist + 2 * LVL_STRIDE);
     unsigned long long* dkey = NULL;
     uint32_t* stash = NULL;
     int32_t* scnt = NULL;
+    LVL_TRY_ALLOC(cnt, (ncnt + 1) * sizeof(int32_t), &ok);
+    LVL_TRY_ALLOC(off, (ncnt + 1) * sizeof(int32_t), &ok);
     if (!directed) {
-        LVL_ALLOC(dkey, (size_t)xrows * sizeof(unsigned long long));
-        LVL_ALLOC(stash, (size_t)xrows * LVL_STASH_CAP * sizeof(uint32_t));
-        LVL_ALLOC(scnt, (size_t)xrows * 4 * sizeof(int32_t));
+        LVL_TRY_ALLOC(dkey, (size_t)xrows * sizeof(unsigned long long), &ok);
+        LVL_TRY_ALLOC(stash, (size_t)xrows * LVL_STASH_CAP * sizeof(uint32_t), &ok);
+        LVL_TRY_ALLOC(scnt, (size_t)xrows * 4 * sizeof(int32_t), &ok);
     }
-    SRT_HIPCHK(hipMemsetAsync(cnt, 0, (ncnt + 1) * sizeof(int32_t), st));
-    SRT_HIPCHK(hipMemsetAsync(dhist, 0, (2 * LVL_STRIDE + 8) * sizeof(unsigned long long), st));
-    if (directed)
-        lvl_arcs_cols_kernel<false><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, cnt, 0, NULL, NULL);
-    else
-        lvl_arcs_rows_kernel<false><<<xrows, 256, 0, st>>>(n, ld, xrow0, xw, cnt, 0, NULL, NULL,
-                                                           NULL, NULL, dkey, stash, scnt, dhist);
-    SRT_HIPCHK(hipGetLastError());
+    if (ok) {
+        SRT_HIPCHK(hipMemsetAsync(cnt, 0, (ncnt + 1) * sizeof(int32_t), st));
+        if (directed)
+            lvl_arcs_cols_kernel<false><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, cnt, 0, NULL, NULL);
+        else
+            lvl_arcs_rows_kernel<false><<<xrows, 256, 0, st>>>(n, ld, xrow0, xw, cnt, 0, NULL, NULL,
+                                                               NULL, NULL, dkey, stash, scnt, dhist);
+        SRT_HIPCHK(hipGetLastError());
+        lvl_hist_kernel<<<1024, 256, 0, st>>>(ncnt, cnt, dhist); /* this rank's rows (N > 1) */
+        SRT_HIPCHK(hipGetLastError());
+    }
     int rc;
-    lvl_hist_kernel<<<1024, 256, 0, st>>>(ncnt, cnt, dhist); /* this rank's rows (N > 1) */
-    SRT_HIPCHK(hipGetLastError());
-    int32_t* limbs = reinterpret_cast<int32_t*>(cnt + ncnt + 1); /* 2 x 256 int32 past the counts */
+    int failed = !ok;
     if (R > 1) {
         lvl_hist_limbs_kernel<<<1, LVL_STRIDE, 0, st>>>(1, dhist, limbs);
-        if ((rc = srt_coll_allreduce_i32(comm, limbs, 2 * LVL_STRIDE, 0, st))) return rc;
+        SRT_HIPCHK(hipMemcpyAsync(limbs + 2 * LVL_STRIDE, &failed, sizeof(int32_t), hipMemcpyHostToDevice, st));
+        if ((rc = srt_coll_allreduce_i32(comm, limbs, 2 * LVL_STRIDE + 1, 0, st))) return rc;
         lvl_hist_limbs_kernel<<<1, LVL_STRIDE, 0, st>>>(0, dhist, limbs);
         SRT_HIPCHK(hipGetLastError());
+        SRT_HIPCHK(hipMemcpyAsync(&failed, limbs + 2 * LVL_STRIDE, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     }
     unsigned long long hist[LVL_STRIDE];
     SRT_HIPCHK(hipMemcpyAsync(hist, dhist, sizeof(hist), hipMemcpyDeviceToHost, st));
     SRT_HIPCHK(hipStreamSynchronize(st));
+    if (failed) return SRT_OK; /* out of device memory somewhere: Floyd-Warshall on every rank */
     /* level budget from global quantities (the summed histogram, the largest shard's words): the
      * largest L whose predicted time stays under half the FW time */
     const double nw_all = (double)max_rows / 32.0;
@@ -1183,31 +1214,27 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         const size_t cap = lvl_avail_bytes() / 2 / (plane * sizeof(uint32_t));
         if ((size_t)lmax > cap) lmax = (int)cap;
     }
+    if (R > 1) { /* test hook: this rank's memory stands in for a smaller budget (lcap_r<rank>) */
+        char key[32];
+        snprintf(key, sizeof(key), "lcap_r%d", srt_comm_rank(comm));
+        const int lc = srt_form_int(key, -1);
+        if (lc >= 0 && lc < lmax) lmax = lc;
+    }
     if (R > 1 && (rc = lvl_agree_min(comm, dagree, &lmax, st))) return rc;
-    /* in-arcs already in (weight, source) order from the ordered stash, on every rank: no sort */
-    int sorted_fill = !directed && lmax <= LVL_STASH_W && hist[0] == 0;
-    if (R > 1 && (rc = lvl_agree_min(comm, dagree, &sorted_fill, st))) return rc;
+    /* From here every branch reads global values only: hist is summed over the ranks (hist[0] is
+     * the stash-overflow count), lmax agreed. In-arcs come out of the ordered stash already in
+     * (weight, source) order, on every rank, when no row overflowed its stash: no sort. */
+    const int sorted_fill = !directed && lmax <= LVL_STASH_W && hist[0] == 0;
     int wmin = 0;
     for (int x = 1; x <= LVL_WMAX && !wmin; ++x)
         if (hist[x]) wmin = x;
-    if (lmax < 2 || !wmin || wmin > lmax) return SRT_OK; /* the same on every rank */
-    if (R > 1) { /* every target's counts up to lmax on every rank (one owner row each) */
-        const int cols = lmax + 2;
-        int32_t* packed = NULL;
-        LVL_ALLOC(packed, (size_t)ld * cols * sizeof(int32_t));
-        const int gb = srt_ceil_div((int64_t)ld * cols, 256);
-        lvl_cnt_pack_kernel<<<gb, 256, 0, st>>>(ld, cols, 1, cnt, packed);
-        if ((rc = srt_coll_allreduce_i32(comm, packed, (size_t)ld * cols, 0, st))) return rc;
-        lvl_cnt_pack_kernel<<<gb, 256, 0, st>>>(ld, cols, 0, cnt, packed);
-        SRT_HIPCHK(hipGetLastError());
-    }
+    if (lmax < 2 || !wmin || wmin > lmax) return SRT_OK;
     /* in-arcs with w <= lmax: their count from the histogram (no read-back of the scan) */
     int64_t total64 = 0;
     for (int x = 1; x <= lmax; ++x) total64 += (int64_t)hist[x];
     if (total64 > 0x7FFFFFF0ll) return SRT_OK; /* int32 arc offsets (global) */
     const int32_t total = (int32_t)total64;
     /* every allocation of the build up front, softly: one agreed outcome, then the work */
-    int ok = 1;
     uint32_t *arcs = NULL, *arcs2 = NULL, *aoff = NULL, *lev = NULL, *Rb = NULL;
     double *ar = NULL, *ar2 = NULL;
     int32_t* seg = NULL;
@@ -1244,19 +1271,29 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         LVL_TRY_ALLOC(rtab, LVL_RT_CAP * sizeof(double), &ok);
     }
     /* N > 1: one block per rank for the numbered segments (a header with the overflow flag and
-     * the count, then up to LVL_RT_CAP values) */
+     * the count, then up to LVL_RT_CAP values), and the count exchange's packed block */
     constexpr size_t LVL_GB = LVL_RT_CAP + 1;
     double* gat = NULL;
     if (want_rt && R > 1) LVL_TRY_ALLOC(gat, (size_t)R * LVL_GB * sizeof(double), &ok);
-    if (R > 1 && (rc = lvl_agree_min(comm, dagree, &ok, st))) return rc;
-    if (!ok) return SRT_OK; /* out of device memory somewhere: Floyd-Warshall on every rank */
+    const int cols = lmax + 2;
+    int32_t* packed = NULL;
+    if (R > 1) LVL_TRY_ALLOC(packed, (size_t)ld * cols * sizeof(int32_t), &ok);
     /* The in-arcs are extracted for the first batch of levels only (w <= lx = min(lmax, LVL_BATCH):
      * levels d <= lx use no heavier arc) and again up to lmax if the levels run past it: C4 ends
      * at level 5, and its ~20-quantum budget would extract, number and (N > 1) broadcast 2.5x the
      * arcs it uses. The counts are kept for the second extraction. */
     const int lx = min(lmax, LVL_BATCH);
     int32_t* cnt_keep = NULL;
-    if (lx < lmax) LVL_ALLOC(cnt_keep, (ncnt + 1) * sizeof(int32_t));
+    if (lx < lmax) LVL_TRY_ALLOC(cnt_keep, (ncnt + 1) * sizeof(int32_t), &ok);
+    if (R > 1 && (rc = lvl_agree_min(comm, dagree, &ok, st))) return rc;
+    if (!ok) return SRT_OK; /* out of device memory somewhere: Floyd-Warshall on every rank */
+    if (R > 1) { /* every target's counts up to lmax on every rank (one owner row each) */
+        const int gb = srt_ceil_div((int64_t)ld * cols, 256);
+        lvl_cnt_pack_kernel<<<gb, 256, 0, st>>>(ld, cols, 1, cnt, packed);
+        if ((rc = srt_coll_allreduce_i32(comm, packed, (size_t)ld * cols, 0, st))) return rc;
+        lvl_cnt_pack_kernel<<<gb, 256, 0, st>>>(ld, cols, 0, cnt, packed);
+        SRT_HIPCHK(hipGetLastError());
+    }
     if (cnt_keep)
         SRT_HIPCHK(hipMemcpyAsync(cnt_keep, cnt, (ncnt + 1) * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     uint32_t* const arcsA = arcs;
@@ -1268,9 +1305,8 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         int64_t t64 = 0;
         for (int x = 1; x <= lw; ++x) t64 += (int64_t)hist[x];
         total_x = (int32_t)t64;
-        int sorted_w = !directed && lw <= LVL_STASH_W && hist[0] == 0;
+        const int sorted_w = !directed && lw <= LVL_STASH_W && hist[0] == 0; /* global values */
         int rc_ = 0;
-        if (R > 1 && (rc_ = lvl_agree_min(comm, dagree, &sorted_w, st))) return rc_;
         if (cnt_keep && lw != lx)
             SRT_HIPCHK(hipMemcpyAsync(cnt, cnt_keep, (ncnt + 1) * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
         /* offsets over the arcs with w <= lw, (target, weight)-major */
@@ -1404,21 +1440,19 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     /* the levels in batches of LVL_BATCH, one host round trip per batch. After the first batch
      * the settled fraction decides whether the rest is worth it: a graph with far-apart vertices
      * (metric latencies, C4metric: 0.2% settled after 8 levels, distances of hundreds of quanta)
-     * goes to the FW at once instead of spending its whole budget first (77 ms there) */
-    int D = 0, hflag[2] = {0, 0};
+     * goes to the FW at once instead of spending its whole budget first (77 ms there). At N > 1
+     * the decision is taken from the summed vote (lvl_vote_kernel): the fraction of all n^2 pairs,
+     * the same number on every rank and the one a single GPU would see. A rank whose own sources
+     * settled early runs the later levels as no-ops (lvl_step_kernel's prev test) and keeps its D. */
+    int D = 0, all_done = 0, hflag[2] = {0, 0};
     unsigned long long* nset = reinterpret_cast<unsigned long long*>(dagree + 4);
-    const int lsrc = min(nrows, max(0, n - row0)); /* the local sources (rows past n are padding) */
-    const double pairs = (double)n * (double)lsrc;
     const int ev0 = evp ? evp->used : 0;
     if (evp && (rc = evpool_reserve(evp, ev0 + 2 * lmax))) return rc;
-    for (int d0 = 1; d0 <= lmax && !D; d0 += LVL_BATCH) {
+    for (int d0 = 1; d0 <= lmax; d0 += LVL_BATCH) {
         const int d1 = min(lmax, d0 + LVL_BATCH - 1);
         for (int d = d0; d <= d1; ++d) {
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
-#ifndef LVL_FIRST
-#define LVL_FIRST 1
-#endif
-            if (LVL_FIRST && d == 1) { /* the weight-1 arcs as bits; level 2 takes up the completion flags
+            if (d == 1) { /* the weight-1 arcs as bits; level 2 takes up the completion flags
                            * (dinc[1] stays set: a graph settled at level 1 reports 2 levels) */
                 SRT_HIPCHK(hipMemsetAsync(lev, 0, plane * sizeof(uint32_t), st));
                 SRT_HIPCHK(hipMemsetAsync(dinc + 1, 0xFF, sizeof(int), st));
@@ -1427,11 +1461,18 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
             } else {
                 lvl_step_kernel<<<pgrid, 256, 0, st>>>(d, n, nw, nchunk, row0, nrows, nblk, off,
                                                       arcs, aoff, lev, Rb, done, dinc + d,
-                                                      d > 1 ? dinc + d - 1 : NULL, nset);
+                                                      dinc + d - 1, nset);
             }
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
         }
         SRT_HIPCHK(hipGetLastError());
+        int32_t vote[4] = {0, 0, 0, 0};
+        if (R > 1) {
+            lvl_vote_kernel<<<1, 64, 0, st>>>(dinc + d1, nset, dvote);
+            SRT_HIPCHK(hipGetLastError());
+            if ((rc = srt_coll_allreduce_i32(comm, dvote, 4, 0, st))) return rc;
+            SRT_HIPCHK(hipMemcpyAsync(vote, dvote, sizeof(vote), hipMemcpyDeviceToHost, st));
+        }
         int inc[LVL_BATCH];
         unsigned long long settled = 0;
         SRT_HIPCHK(hipMemcpyAsync(inc, dinc + d0, sizeof(int) * (d1 - d0 + 1), hipMemcpyDeviceToHost,
@@ -1441,14 +1482,21 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         SRT_HIPCHK(hipStreamSynchronize(st));
         for (int d = d0; d <= d1 && !D; ++d)
             if (inc[d - d0] == 0) D = d;
-        /* every source's own vertex counts as settled at level 0 (n - row0 of them are local);
-         * level 1 (lvl_first_kernel) counts no pairs: its weight-1 arcs, this rank's share of them */
-        if (LVL_FIRST && d0 == 1) settled += (unsigned long long)((double)hist[1] * lsrc / n);
-        const double frac = pairs > 0 ? ((double)settled + (double)lsrc) / pairs : 1.0;
+        if (R > 1) {
+            all_done = vote[0] == 0;
+            settled = (unsigned long long)(uint32_t)vote[1] + ((unsigned long long)(uint32_t)vote[2] << 21) +
+                      ((unsigned long long)(uint32_t)vote[3] << 42);
+        } else {
+            all_done = D != 0;
+        }
+        if (all_done) break;
+        /* settled pairs of all sources: the levels >= 2 counted by lvl_step_kernel, every source's
+         * own vertex (level 0) and the weight-1 arcs (level 1, lvl_first_kernel counts none) */
+        const double frac = ((double)settled + (double)n + (double)hist[1]) / ((double)n * (double)n);
         /* (a forced level build, fw_ms = 1e30 from SRT_FORM levels=1, runs its whole budget) */
-        if (!D && d0 == 1 && d1 < lmax && frac < LVL_MIN_SETTLED && fw_ms < 1e29)
-            break; /* -> Floyd-Warshall */
-        if (!D && d1 == lx && lx < lmax && (rc = extract(lmax))) return rc; /* the heavier arcs */
+        if (d0 == 1 && d1 < lmax && frac < LVL_MIN_SETTLED && fw_ms < 1e29)
+            break; /* -> Floyd-Warshall, every rank */
+        if (d1 == lx && lx < lmax && (rc = extract(lmax))) return rc; /* the heavier arcs */
     }
     if (evp && D) evp->used = ev0 + 2 * D; /* the levels that did work */
     int64_t gathered = 0;
@@ -1457,9 +1505,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         for (int x = 1; x < d; ++x) below += (double)hist[x];
         gathered += (int64_t)(below * (double)nw * 4.0);
     }
-    ok = D > 0;
-    if (R > 1 && (rc = lvl_agree_min(comm, dagree, &ok, st))) return rc; /* one verdict */
-    if (!ok) return SRT_OK;
+    if (!all_done) return SRT_OK; /* the verdict, alike on every rank (the summed vote) */
     int ntab = 0;
     if (want_rt && !hflag[0] && hflag[1] <= LVL_RT_CAP)
         ntab = hflag[1];

@@ -30,6 +30,9 @@ static __device__ __forceinline__ void srt_max_once(int32_t* p, int v) {
  * streams): the current device (0..63), or 64 + r for virtual rank r when several ranks share
  * one device inside one process (srt_build_tables_multi with SRT_VIRTUAL_RANKS, comm.hip). */
 #define SRT_STATE_SLOTS 128
+/* the neighbour-row derivation's largest source degree (build.hip picks I, derive.hip sizes its
+ * per-thread neighbour arrays by it) */
+#define SRT_DERIVE_MAXDEG 4
 int srt_state_slot(void);
 /* stream-ordered scratch from the library's private pool of the current device (comm.hip) */
 hipMemPool_t srt_scratch_pool(void);

@@ -396,11 +396,9 @@ int srt_wsssp_rows(int n, int directed, const int2* rowptr, const uint2* cw, con
  * distance fits (d(a, b) <= 2 ecc(s0)). Undirected graphs only.
  * ------------------------------------------------------------------------------------------ */
 #define WG_INF 1023u
-#ifndef WG_AK
 /* arc windows in flight per lane. Same-box C5 A/Bs: 3 beat 4 by 1.1%, 2 beat 3 by 0.3%, and 1 and
  * 6 lost 1.9% and 4.5% (profiles/r02g/ab_ak_*) */
 #define WG_AK 2
-#endif
 #define WG_NBLK 256 /* 64-arc blocks indexed per chunk (arcs beyond: whole-chunk search) */
 
 static __device__ __forceinline__ uint32_t wg_get(const uint32_t* sd, uint32_t v) {

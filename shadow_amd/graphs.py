@@ -85,6 +85,41 @@ def complete_dense(n: int, seed: int, lat_max: int = 300, self_max: int = 10,
     return lat.astype(np.uint32), 1.0 - k.astype(np.float64) / 10000.0
 
 
+def hub_leaf(n: int, hubs: int, seed: int, hub_max: int = 3, spoke: int = 5,
+             loss_max: int = 500) -> Graph:
+    """Hubs 0..hubs-1 joined to each other (U{1..hub_max} ms) and to every leaf (`spoke` ms); no
+    leaf-leaf edges; every vertex with a self-loop. A hub reaches everything within `spoke` quanta,
+    a leaf needs 2 * spoke for another leaf: row shards of hubs and of leaves settle their sources
+    at different levels (tests/levels_protocol.py: on either side of the level build's batch)."""
+    iu, ju = np.triu_indices(n)
+    keep = (iu == ju) | (iu < hubs)
+    iu, ju = iu[keep].astype(np.uint64), ju[keep].astype(np.uint64)
+    self_loop = iu == ju
+    lat = np.where(self_loop, np.uint64(1) + hash_u64(seed, 2, iu, ju) % np.uint64(10),
+                   np.where(ju < np.uint64(hubs),
+                            np.uint64(1) + hash_u64(seed, 0, iu, ju) % np.uint64(hub_max),
+                            np.uint64(spoke)))
+    k = hash_u64(seed, 1, iu, ju) % np.uint64(loss_max + 1)
+    return Graph(n, False, iu.astype(np.int32), ju.astype(np.int32), lat.astype(np.int64) * MS,
+                 k.astype(np.float64) / 10000.0, f"hubleaf{n}_{hubs}")
+
+
+def dense_of(g: Graph):
+    """(w_ms u32, r f64) matrices of a simple undirected whole-millisecond graph, the dense build's
+    input form: SRT_INF (0x7FFFFFFF) and 0.0 where there is no edge, self-loops on the diagonal,
+    r = 1.0 - loss (topology.c:396)."""
+    assert not g.directed
+    w = np.full((g.n, g.n), 0x7FFFFFFF, np.uint32)
+    r = np.zeros((g.n, g.n))
+    q = (g.lat_ns // MS).astype(np.uint32)
+    assert np.all(q.astype(np.int64) * MS == g.lat_ns)
+    w[g.src, g.dst] = q
+    w[g.dst, g.src] = q
+    r[g.src, g.dst] = 1.0 - g.loss
+    r[g.dst, g.src] = 1.0 - g.loss
+    return w, r
+
+
 def _rand01(seed: int, stream: int, i) -> np.ndarray:
     return (hash_u64(seed, stream, i, 0) >> np.uint64(11)).astype(np.float64) * (2.0 ** -53)
 

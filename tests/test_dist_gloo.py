@@ -398,163 +398,23 @@ def test_sparse_source_shard_allgather_gloo(native):
 
 
 # ---- the row-sharded Dial level build (levels.hip srt_levels_build), its collectives in order --
-LVL_STRIDE, LVL_WMAX, RT_CAP = 256, 254, 2048
+# The protocol is restated in tests/levels_protocol.py; its sequences are the fixture the C
+# library's collective logs are checked against (tests/test_gpu_protocol.py).
+import json  # noqa: E402
+import sys  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import levels_protocol as lp  # noqa: E402
+
+_GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels_protocol.json")
 
 
-def _lvl_estimate(hist, L, ntgt, nw):
-    t, below = 0.0, 0.0
-    for d in range(1, L + 1):
-        if d >= 2:
-            below += float(hist[d - 1])
-        t += (below * nw * 4.0 + ntgt * nw * 4.0 * 3.0) / 4.0e9 + 0.03
-    return t
-
-
-def _levels_worker(rank, R, port, n, seed, lat_max, memcap_levels, q):
-    """One rank of srt_levels_build: count pass over its rows, count all-reduce (sum), budget,
-    budget agreement (min all-reduce), allocation agreement (min), fill, per-rank segment
-    numbered segments (each rank's distinct reliabilities all-gathered, the union sorted by bits,
-    indices instead of f64s), broadcasts, per-target sort by (weight, tail), the levels over this
-    rank's sources, the
-    canonical predecessors and path-order products, verdict agreement (min). numpy compute, gloo
-    collectives; memcap_levels[rank] stands in for each rank's device-memory cap on the budget."""
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=R)
-    from shadow_amd._lib import lib
-    L = lib()
-    ld = (n + ALIGN - 1) // ALIGN * ALIGN
-    b, e = _shard(L, ld, R, rank)
-    max_rows = max(_shard(L, ld, R, x)[1] - _shard(L, ld, R, x)[0] for x in range(R))
-    w, rr = graphs.complete_dense(n, seed, lat_max=lat_max)
-    calls = []
-    # count pass over this rank's rows (row j holds j's in-arcs: undirected)
-    cnt = np.zeros((ld, LVL_STRIDE), np.int32)
-    for j in range(b, min(e, n)):
-        for k in range(n):
-            x = int(w[j, k])
-            if k != j and 1 <= x <= LVL_WMAX:
-                cnt[j, x] += 1
-    tc = torch.from_numpy(cnt.reshape(-1).copy())
-    dist.all_reduce(tc)  # srt_coll_allreduce_i32(cnt, ld * 256, sum)
-    calls.append(("allreduce_sum", tc.numel()))
-    cnt = tc.numpy().reshape(ld, LVL_STRIDE)
-    hist = cnt.sum(axis=0).astype(np.int64)
-    lmax = 0  # the forced budget (fw_ms = 1e30), then this rank's memory cap
-    for x in range(1, LVL_WMAX + 1):
-        if _lvl_estimate(hist, x, n, max_rows / 32.0) > 0.5 * 1e30:
-            break
-        lmax = x
-    lmax = min(lmax, memcap_levels[rank])  # the memory cap differs per rank
-    t = torch.tensor([lmax], dtype=torch.int32)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN)  # lvl_agree_min(lmax)
-    calls.append(("allreduce_min", 1))
-    lmax = int(t.item())
-    wmin = int(np.nonzero(hist[1:])[0][0]) + 1
-    if lmax < 2 or wmin > lmax:
-        q.put((rank, "fw", calls, None, None, None))
-        dist.barrier()
-        dist.destroy_process_group()
-        return
-    t = torch.tensor([1], dtype=torch.int32)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN)  # lvl_agree_min(allocations ok)
-    calls.append(("allreduce_min", 1))
-    cnt[:, lmax + 1:] = 0
-    off = np.concatenate([[0], np.cumsum(cnt.reshape(-1))]).astype(np.int64)
-    total = int(off[-1])
-    assert total == int(hist[1:lmax + 1].sum())  # the total the host takes from the histogram
-    arcs = np.zeros((total, 3), np.int64)  # (weight, tail, reliability index)
-    ar = np.zeros(total)  # the arc's reliability (this rank's segment)
-    for j in range(b, min(e, n)):
-        cur = {x: int(off[j * LVL_STRIDE + x]) for x in range(1, lmax + 1)}
-        for k in range(n):
-            x = int(w[j, k])
-            if k != j and 1 <= x <= lmax:
-                arcs[cur[x], :2] = (x, k)
-                ar[cur[x]] = rr[k, j]
-                cur[x] += 1
-    # numbered segments: this rank's distinct reliabilities (bit patterns), all-gathered in
-    # fixed blocks (count, then up to RT_CAP values), the union sorted by bits on every rank
-    o0, o1 = int(off[b * LVL_STRIDE]), int(off[e * LVL_STRIDE])
-    mine = np.unique(ar[o0:o1].view(np.uint64))
-    assert mine.size <= RT_CAP
-    blk = np.zeros(RT_CAP + 1, np.uint64)
-    blk[0], blk[1:1 + mine.size] = mine.size, mine
-    parts = [torch.zeros(RT_CAP + 1, dtype=torch.int64) for _ in range(R)]
-    dist.all_gather(parts, torch.from_numpy(blk.view(np.int64)))  # srt_coll_allgather
-    calls.append(("allgather", RT_CAP + 1))
-    union = []
-    for t_ in parts:
-        v = t_.numpy().view(np.uint64)
-        union.append(v[1:1 + int(v[0])])
-    rtab_bits = np.unique(np.concatenate(union))  # sorted by bits, identical on every rank
-    rtab = rtab_bits.view(np.float64)
-    arcs[o0:o1, 2] = np.searchsorted(rtab_bits, ar[o0:o1].view(np.uint64))
-    for x in range(R):  # one broadcast per rank's segment (srt_coll_bcast in a group)
-        qb, qe = _shard(L, ld, R, x)
-        o0, o1 = int(off[qb * LVL_STRIDE]), int(off[qe * LVL_STRIDE])
-        if o1 > o0:
-            seg = torch.from_numpy(np.ascontiguousarray(arcs[o0:o1]))
-            dist.broadcast(seg, x)
-            calls.append(("bcast", x, o1 - o0))
-            arcs[o0:o1] = seg.numpy()
-    # per target: sorted by (weight, tail)
-    ins, rix = {}, {}
-    for j in range(n):
-        a = arcs[off[j * LVL_STRIDE]:off[(j + 1) * LVL_STRIDE]]
-        ins[j] = sorted((int(x), int(k)) for x, k, _ in a)
-        rix.update({(int(k), j): int(i) for _, k, i in a})
-    # the levels over the local sources s in [b, min(e, n))
-    src = list(range(b, min(e, n)))
-    ns = len(src)
-    INFD = 1 << 30
-    D = np.full((ns, n), INFD, np.int64)
-    for i, s in enumerate(src):
-        D[i, s] = 0
-    Dl = 0
-    for d in range(1, lmax + 1):
-        for j in range(n):
-            for x, k in ins[j]:
-                if x > d:
-                    break
-                hit = D[:, k] == d - x
-                D[hit & (D[:, j] == INFD), j] = d  # settled at level d (first time)
-        if (D < INFD).all():
-            Dl = d
-            break
-    ok = 1 if Dl else 0
-    t = torch.tensor([ok], dtype=torch.int32)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN)  # the verdict
-    calls.append(("allreduce_min", 1))
-    if not int(t.item()):
-        q.put((rank, "fw", calls, None, None, None))
-        dist.barrier()
-        dist.destroy_process_group()
-        return
-    # canonical predecessor (largest w, then smallest tail among tight in-arcs) and the
-    # path-order reliability product, in increasing distance
-    rel = np.zeros((ns, n))
-    for i, s in enumerate(src):
-        rel[i, s] = 1.0
-        for j in np.argsort(D[i], kind="stable"):
-            if j == s:
-                continue
-            best = None
-            for x, k in ins[j]:
-                if D[i, k] + x == D[i, j] and (best is None or (x, -k) > (best[0], -best[1])):
-                    best = (x, k)
-            u = best[1]
-            rel[i, j] = (1.0 if u == s else rel[i, u]) * rtab[rix[(u, j)]]
-    q.put((rank, "levels", calls, b, D, rel))
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-def _run_levels(n, seed, lat_max, R, memcap):
+def _run_levels(name):
+    R = lp.CASES[name][1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_levels_worker, args=(r, R, port, n, seed, lat_max, memcap, q))
-             for r in range(R)]
+    procs = [ctx.Process(target=lp.gloo_worker, args=(r, R, port, name, q)) for r in range(R)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=500) for _ in range(R)], key=lambda x: x[0])
@@ -564,32 +424,34 @@ def _run_levels(n, seed, lat_max, R, memcap):
     return res
 
 
-@pytest.mark.timeout(900)
-@pytest.mark.parametrize("R", [2, 3])
-def test_dense_level_build_protocol_gloo(native, R):
-    """the level build's N-rank protocol over gloo -- uneven row shards (R = 2:
-    ld 384 = 128 | 256 rows; R = 3: ld 640 = 128 | 256 | 256) and ranks with different memory
-    caps on the level budget (the forced budget of SRT_FORM levels=1 otherwise): every rank makes
-    the same collective calls in the same order with the same sizes, agrees on one verdict, and
-    its rows equal the oracle's."""
-    n, seed, lat_max = 300 if R == 2 else 600, 5, 4
-    res = _run_levels(n, seed, lat_max, R, memcap=[254] + [12] * (R - 1))
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", list(lp.CASES))
+def test_dense_level_build_protocol_gloo(native, name):
+    """VERDICT r04 #4 / r05 #4, ADVICE r05 (high): the level build's N-rank protocol over gloo --
+    uneven row shards, ranks with different level caps (complete*: the min agreement; capfall: a
+    budget of 1 sends every rank to the FW together), and ranks whose own sources settle on either
+    side of the first batch of levels (hubleaf*: hubs at level 5, leaves at 10 -- every rank takes
+    the batch decision from the summed vote, fetches the heavier arcs and runs batch 2). Every rank
+    makes the same collective calls in the same order with the same sizes, the sequence is the
+    committed fixture's (the one the C library's log must equal), and the rows equal the oracle's."""
+    spec, R, _, outcome = lp.CASES[name]
+    res = _run_levels(name)
     assert len({str(x[2]) for x in res}) == 1, [x[2] for x in res]  # identical collective sequence
-    assert {x[1] for x in res} == {"levels"}
-    g = graphs.complete_graph(n, seed=seed, lat_max=lat_max)
+    assert {x[1] for x in res} == {outcome}
+    with open(_GOLDEN) as f:
+        gold = json.load(f)[name]
+    assert [list(c) for c in res[0][2]] == gold["calls"]
+    assert [int(x[6]) for x in res] == gold["own_levels"]
+    if name.startswith("hubleaf"):  # the ranks' own sources settle on either side of level 8
+        assert min(gold["own_levels"]) <= lp.BATCH < max(gold["own_levels"])
+    if outcome != "levels":
+        return
+    g, _, _ = lp.case_graph(spec)
     exp = oracle.table(oracle.EdgeList(g.n, g.directed, g.src, g.dst, g.lat_ns, g.loss), raw=True)
-    for _, _, _, b, D, rel in res:
+    n = g.n
+    for _, _, _, b, D, rel, _ in res:
         rows = slice(b, b + D.shape[0])
         off = np.arange(n)[None, :] != np.arange(b, b + D.shape[0])[:, None]
         lat = D.astype(np.uint64) * np.uint64(1_000_000)
         assert np.array_equal(np.where(off, lat, 0), np.where(off, exp["lat_int"][rows], 0))
         assert np.array_equal(rel[off], exp["rel"][rows][off])
-
-
-@pytest.mark.timeout(600)
-def test_dense_level_build_budget_divergence_falls_back_together(native):
-    """One rank's memory cap leaves a budget of 1 level: the min agreement sends every rank to
-    Floyd-Warshall at the same point (no rank waits in a broadcast its peers skip)."""
-    res = _run_levels(300, 5, 4, 2, memcap=[254, 1])
-    assert {x[1] for x in res} == {"fw"}
-    assert len({str(x[2]) for x in res}) == 1
