@@ -138,6 +138,13 @@ struct srt_sparse_graph {
     int64_t degI; /* summed degree of I (the derivation's neighbour-row reads) */
     int32_t *dI, *dcore, *crow;
     int32_t ntab; /* entries of rtab */
+    /* the derived build's canonical-arc codes of the core rows (ncore x n u32; C5: 21.6 GB), kept
+     * across builds: from the scratch pool they were re-mapped by every build (past the pool's
+     * release threshold), and builds whose fresh mapping came out fragmented ran wgsssp_kernel at
+     * 620-765 ms instead of ~396 */
+    uint32_t* codes;
+    size_t codes_cap;
+    pthread_mutex_t codes_mu;
 };
 
 #define DERIVE_MAXDEG SRT_DERIVE_MAXDEG /* derive.hip's DV_MAXDEG */
@@ -186,7 +193,7 @@ extern "C" void srt_sparse_graph_free(srt_sparse_graph* g) {
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(g->device);
     void* ps[] = {g->rp, g->col, g->w, g->r, g->sw, g->sr, g->cw, g->perm, g->inv, g->rp2, g->cw2, g->r2,
-                  g->rpo, g->rtab, g->ridx, g->dI, g->dcore, g->crow};
+                  g->rpo, g->rtab, g->ridx, g->dI, g->dcore, g->crow, g->codes};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (g->directed) {
@@ -617,8 +624,35 @@ static int sparse_rows_derived(const srt_sparse_graph* g, uint32_t* lat_rows, do
         }
     } ev;
     for (hipEvent_t& x : ev.e) SRT_HIPCHK(hipEventCreate(&x));
+    /* the codes: the graph's own buffer (one allocation, same placement every build) when no other
+     * build of this graph holds it, else stream-ordered scratch */
+    srt_sparse_graph* gm = const_cast<srt_sparse_graph*>(g);
+    const size_t cbytes = (size_t)g->ncore * n * sizeof(uint32_t);
     uint32_t* codes = NULL;
-    SRT_HIPCHK(srt_malloc_async(&codes, (size_t)g->ncore * n * sizeof(uint32_t), st));
+    const bool own = pthread_mutex_trylock(&gm->codes_mu) == 0;
+    struct unlock {
+        pthread_mutex_t* m;
+        ~unlock() {
+            if (m) pthread_mutex_unlock(m);
+        }
+    } ul{own ? &gm->codes_mu : nullptr};
+    if (own) {
+        if (gm->codes_cap < cbytes) {
+            SRT_HIPCHK(hipStreamSynchronize(st)); /* earlier builds on st are done with the old one */
+            if (gm->codes) (void)hipFree(gm->codes);
+            gm->codes = NULL;
+            gm->codes_cap = 0;
+            if (hipMalloc((void**)&gm->codes, cbytes) != hipSuccess) {
+                (void)hipGetLastError();
+                gm->codes = NULL;
+            } else {
+                gm->codes_cap = cbytes;
+            }
+        }
+        codes = gm->codes;
+    }
+    const bool scratch = codes == NULL;
+    if (scratch) SRT_HIPCHK(srt_malloc_async(&codes, cbytes, st));
     SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)n * sizeof(int), st));
     SRT_HIPCHK(hipEventRecord(ev.e[0], st));
     int rc = srt_wgsssp_rows(n, g->rpo, g->cw, g->r, NULL, g->max_w, 0, g->ncore, g->dcore, lat_rows,
@@ -638,12 +672,13 @@ static int sparse_rows_derived(const srt_sparse_graph* g, uint32_t* lat_rows, do
         rc = srt_derive_rows_async(n, g->nI, g->dI, 0, g->rpo, g->cw, g->ridx, g->rtab, g->ntab,
                                    g->crow, codes, lat_rows, rel_rows, (size_t)n, st);
     if (!rc && hipEventRecord(ev.e[2], st) != hipSuccess) rc = SRT_E_DEVICE;
-    (void)hipFreeAsync(codes, st);
+    if (scratch) (void)hipFreeAsync(codes, st);
     if (!rc && hipEventSynchronize(ev.e[2]) == hipSuccess) {
         (void)hipEventElapsedTime(&tm->core, ev.e[0], ev.e[1]);
         (void)hipEventElapsedTime(&tm->derive, ev.e[1], ev.e[2]);
         tm->fallback = core_ovf;
     }
+    if (own && rc) (void)hipStreamSynchronize(st); /* the buffer is free before it is unlocked */
     return rc;
 }
 

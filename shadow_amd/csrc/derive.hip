@@ -49,7 +49,7 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
     const uint2* __restrict__ cw, const uint8_t* __restrict__ ridx, const double* __restrict__ rtab,
     int ntab, const int32_t* __restrict__ crow, const uint32_t* __restrict__ codes,
     uint32_t* __restrict__ lat, double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ cs_all,
-    size_t lds_n) {
+    size_t lds_n, unsigned* __restrict__ queue) {
     /* dynamic LDS: one done bit per target, then (CACHE) the reliability of vertices < CACHE --
      * the oldest vertices of a BA graph are its hubs, the parents of most targets */
     extern __shared__ __attribute__((aligned(16))) uint32_t cdone[];
@@ -71,7 +71,12 @@ __global__ __launch_bounds__(NT) void derive_chain_kernel(
         return (__hip_atomic_load(&cdone[v >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >>
                 (v & 31)) & 1u;
     };
-    for (int si = blockIdx.x; si < nI; si += gridDim.x) {
+    __shared__ int s_next; /* rows from a work queue (a late workgroup does not hold the end back) */
+    for (;;) {
+        if (tid == 0) s_next = (int)atomicAdd(queue, 1u);
+        __syncthreads();
+        const int si = s_next;
+        if (si >= nI) break;
         const int s = I[si];
         uint32_t* ol = lat + (size_t)(s - src_begin) * ldo;
         double* orr = rel + (size_t)(s - src_begin) * ldo;
@@ -238,13 +243,15 @@ int srt_derive_rows_async(int n, int nI, const int32_t* I, int src_begin, const 
     const int grid = nI < cus ? nI : cus;
     const size_t np = ((size_t)n + 3) & ~(size_t)3;
     uint32_t* cs = NULL;
-    SRT_HIPCHK(srt_malloc_async(&cs, (size_t)grid * np * sizeof(uint32_t), st));
+    SRT_HIPCHK(srt_malloc_async(&cs, ((size_t)grid * np + 4) * sizeof(uint32_t), st));
+    unsigned* queue = cs + (size_t)grid * np;
+    SRT_HIPCHK(hipMemsetAsync(queue, 0, sizeof(unsigned), st));
     const size_t lds = (size_t)((((n + 31) / 32) + 3) & ~3) * sizeof(uint32_t) + (size_t)CACHED * 8;
     SRT_HIPCHK(hipFuncSetAttribute((const void*)derive_chain_kernel<NTD, CACHED>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     derive_chain_kernel<NTD, CACHED><<<grid, NTD, lds, st>>>(n, nI, I, src_begin, rowptr, cw, ridx,
                                                              rtab, ntab, crow, codes, lat, rel, ldo,
-                                                             cs, np);
+                                                             cs, np, queue);
     SRT_HIPCHK(hipGetLastError());
     SRT_HIPCHK(hipFreeAsync(cs, st));
     return SRT_OK;

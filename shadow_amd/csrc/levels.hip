@@ -34,6 +34,9 @@
 #include "srt_device.h"
 
 #define LVL_STRIDE 256 /* per-target offsets: weight 0..255 */
+/* levels enqueued per host round trip: a batch's levels past the one that settles every pair
+ * return at once (lvl_step_kernel's prev test) */
+#define LVL_BATCH 8
 #define LVL_WMAX 254   /* largest level budget (distances stay u8: the post pass's small path) */
 #define LVL_PB 12 /* lvl_pred_kernel: gathers per pipelined batch */
 
@@ -306,31 +309,78 @@ __global__ void lvl_mask_kernel(size_t count, int lmax, int32_t* __restrict__ cn
  * linear probing) gives each arc a slot, one workgroup numbers the occupied slots in slot order,
  * and the arcs' slots become dense indices. More than LVL_RT_CAP distinct values (or a probe run
  * past LVL_RT_PROBE) keeps the f64 form. */
-#define LVL_RT_SLOTS 65536
+#define LVL_RT_SLOTS 8192 /* global slots: <= 2048 values at a load of 1/4 */
 #define LVL_RT_PROBE 256
 #define LVL_RT_CAP 2048
+#define LVL_RT_LDS 2048 /* a workgroup's private table */
 static __device__ __forceinline__ unsigned lvl_rt_hash(unsigned long long b) {
     b ^= b >> 33;
     b *= 0xff51afd7ed558ccdull;
     b ^= b >> 33;
     return (unsigned)b & (LVL_RT_SLOTS - 1u);
 }
-__global__ void lvl_rt_hash_kernel(int total, const double* __restrict__ ar,
-                                   unsigned long long* __restrict__ H, uint16_t* __restrict__ rix,
-                                   int* __restrict__ ovf) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= total) return;
-    const unsigned long long b = (unsigned long long)__double_as_longlong(ar[i]);
-    unsigned h = lvl_rt_hash(b);
+static __device__ __forceinline__ int lvl_rt_global_slot(unsigned long long v, unsigned long long* H) {
+    unsigned h = lvl_rt_hash(v);
     for (int p = 0; p < LVL_RT_PROBE; ++p, h = (h + 1u) & (LVL_RT_SLOTS - 1u)) {
-        unsigned long long v = __hip_atomic_load(&H[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (v == ~0ull) v = atomicCAS(&H[h], ~0ull, b); /* ~0: empty (a NaN, never a reliability) */
-        if (v == ~0ull || v == b) {
-            rix[i] = (uint16_t)h;
-            return;
-        }
+        unsigned long long x = __hip_atomic_load(&H[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (x == ~0ull) x = atomicCAS(&H[h], ~0ull, v); /* ~0: empty (a NaN, never a reliability) */
+        if (x == ~0ull || x == v) return (int)h;
     }
-    *ovf = 1;
+    return -1;
+}
+/* Each arc of [lo, hi) (device-held bounds when lo_p / hi_p are given) gets its value's global
+ * slot. A workgroup takes a contiguous run of arcs and dedupes it in a private LDS table first, so
+ * the global table sees each distinct value once per workgroup instead of once per arc: every arc
+ * probing the global table hammered its ~500 hot lines (C4: 87 us for 1.07 M arcs). Values past
+ * the LDS table's probe go to the global table directly (marked 0x8000 in the first pass). */
+__global__ __launch_bounds__(256) void lvl_rt_hash_kernel(const int32_t* __restrict__ lo_p,
+                                                          const int32_t* __restrict__ hi_p, int lo, int hi,
+                                                          const double* __restrict__ ar,
+                                                          unsigned long long* __restrict__ H,
+                                                          uint16_t* __restrict__ rix, int* __restrict__ ovf) {
+    __shared__ unsigned long long key[LVL_RT_LDS];
+    __shared__ uint16_t gs[LVL_RT_LDS];
+    const int a = lo_p ? *lo_p : lo, b = hi_p ? *hi_p : hi, tid = threadIdx.x;
+    const int per = max(0, (b - a + (int)gridDim.x - 1) / (int)gridDim.x);
+    const int c0 = a + (int)blockIdx.x * per, c1 = min(b, c0 + per);
+    for (int s = tid; s < LVL_RT_LDS; s += 256) key[s] = ~0ull;
+    __syncthreads();
+    bool bad = false;
+    for (int i = c0 + tid; i < c1; i += 256) {
+        const unsigned long long v = (unsigned long long)__double_as_longlong(ar[i]);
+        unsigned h = lvl_rt_hash(v) & (LVL_RT_LDS - 1u);
+        int p = 0;
+        for (; p < 64; ++p, h = (h + 1u) & (LVL_RT_LDS - 1u)) {
+            unsigned long long x = __hip_atomic_load(&key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (x == ~0ull) x = atomicCAS(&key[h], ~0ull, v);
+            if (x == ~0ull || x == v) break;
+        }
+        uint16_t out = (uint16_t)h;
+        if (p == 64) {
+            const int g = lvl_rt_global_slot(v, H);
+            bad |= g < 0;
+            out = (uint16_t)(0x8000u | (unsigned)max(g, 0));
+        }
+        rix[i] = out;
+    }
+    __syncthreads();
+    for (int s = tid; s < LVL_RT_LDS; s += 256) {
+        const unsigned long long v = key[s];
+        if (v == ~0ull) continue;
+        const int g = lvl_rt_global_slot(v, H);
+        bad |= g < 0;
+        gs[s] = (uint16_t)max(g, 0);
+    }
+    if (bad) *ovf = 1;
+    __syncthreads();
+    for (int i = c0 + tid; i < c1; i += 256) { /* (this thread's own first-pass entries) */
+        const uint16_t x = rix[i];
+        rix[i] = (x & 0x8000u) ? (uint16_t)(x & 0x7FFFu) : gs[x];
+    }
+}
+static unsigned lvl_rt_grid(int64_t count) {
+    const int64_t g = (count + 4095) / 4096;
+    return (unsigned)(g < 1 ? 1 : g > 512 ? 512 : g);
 }
 /* one workgroup: dense index of every occupied slot (slot order), the table, its size */
 __global__ __launch_bounds__(1024) void lvl_rt_compact_kernel(const unsigned long long* __restrict__ H,
@@ -385,6 +435,163 @@ __global__ void lvl_rt_index_kernel(int total, const double* __restrict__ ar,
     }
     rix[i] = (uint16_t)lo;
 }
+
+/* ---- timing-only solo rank (srt_comm_init_solo*, tools/solo_rank.py) ------------------------ *
+ * A solo rank runs exactly one real rank's work on its own rows; what a real rank would receive
+ * from its peers it synthesises from its own rows instead (the collectives only charge the wire
+ * model). Peer target j = js + shift (js one of the rank's own rows) takes js's counts, then js's
+ * in-arc segment with every source moved by the same shift (mod n; each weight's run rotated so
+ * it stays sorted by source). The graph is then a union of shifted copies of the rank's rows:
+ * every vertex keeps distinct random in-neighbours, and on C4 its distances match the real
+ * graph's (sampled: max 4, mean 3.292 against 3.290); plain copies (no shift) collapsed the
+ * vertices onto the rank's rows and stretched the distances to 6. */
+__global__ void lvl_solo_counts_kernel(int n, int row0, int nrows, int lrows, int32_t* __restrict__ cnt) {
+    const int j = blockIdx.x;
+    if (j >= n || (j >= row0 && j < row0 + nrows)) return;
+    const int js = row0 + ((j - row0) % lrows + lrows) % lrows;
+    for (int x = threadIdx.x; x < LVL_STRIDE; x += blockDim.x)
+        cnt[(size_t)j * LVL_STRIDE + x] = cnt[(size_t)js * LVL_STRIDE + x];
+}
+__global__ void lvl_solo_arcs_kernel(int n, int row0, int nrows, int lrows, int w0, int w1, int nw,
+                                     const int32_t* __restrict__ off, uint32_t* __restrict__ arcs,
+                                     uint16_t* __restrict__ rix, double* __restrict__ ar,
+                                     uint32_t* __restrict__ aoff) {
+    const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (j >= n || (j >= row0 && j < row0 + nrows)) return;
+    const int js = row0 + ((j - row0) % lrows + lrows) % lrows;
+    const int shift = ((j - js) % n + n) % n;
+    for (int x = w0; x <= w1; ++x) {
+        const int g0 = off[(size_t)j * LVL_STRIDE + x], c = off[(size_t)j * LVL_STRIDE + x + 1] - g0;
+        if (c <= 0) continue;
+        const int s0 = off[(size_t)js * LVL_STRIDE + x];
+        int nwr = 0; /* sources that wrap past n: the run's tail, which goes first */
+        for (int i0 = 0; i0 < c; i0 += 64) {
+            const int i = i0 + lane;
+            nwr += __popcll(__ballot(i < c && (int)(arcs[s0 + i] & 0xFFFFu) + shift >= n));
+        }
+        for (int i = lane; i < c; i += 64) {
+            const uint32_t e = arcs[s0 + i];
+            int k = (int)(e & 0xFFFFu) + shift;
+            const bool wr = k >= n;
+            if (wr) k -= n;
+            const int d = g0 + (wr ? i - (c - nwr) : nwr + i);
+            arcs[d] = (uint32_t)k | (e & 0xFFFF0000u);
+            if (rix) rix[d] = rix[s0 + i];
+            if (ar) ar[d] = ar[s0 + i];
+            if (aoff) aoff[d] = (uint32_t)k * (uint32_t)nw * 4u;
+        }
+    }
+}
+
+/* ---- N > 1: the first batch's in-arcs streamed weight by weight ----------------------------- *
+ * Level d reads the arcs of weight <= d only, so the segments travel one weight at a time on a
+ * second stream and level d waits for weight d alone: the wire of weight d + 1 runs under level
+ * d's gathers. On the wire the arcs of one weight are rank-major, target-major within (offw: the
+ * exclusive scan of the counts in [weight][target] order), one u32 per arc -- its source and its
+ * index into the union table of distinct reliabilities (or the source alone, with the f64 beside
+ * it when the union passes the table) -- and each receiver places them into its (target,
+ * weight)-major arcs (4 B per arc on the wire instead of 6). */
+__global__ void lvl_wcols_kernel(int ld, int lw, const int32_t* __restrict__ cnt, int32_t* __restrict__ cw) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x, tot = (size_t)lw * ld;
+    if (i > tot) return;
+    cw[i] = i == tot ? 0 : cnt[(i % ld) * LVL_STRIDE + i / ld + 1];
+}
+/* the wire offsets the host needs: offw at every shard start, per weight (q == R: the end) */
+__global__ void lvl_wire_sizes_kernel(int ld, int lw, int R, const int32_t* __restrict__ offw,
+                                      int32_t* __restrict__ sz) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= lw * (R + 1)) return;
+    const int w = i / (R + 1), q = i % (R + 1);
+    const long long nb = ld / SRT_SHARD_ALIGN;
+    const int b = q == R ? ld : (int)(nb * q / R) * SRT_SHARD_ALIGN; /* srt_shard_rows */
+    sz[i] = offw[(size_t)w * ld + b];
+}
+/* The wire of weight w: one block of maxc[w] u32 per rank (rank q's arcs of weight w, its targets
+ * in order, then padding), all-gathered; wtab[2 (w - 1)] = the weight's base in the wire,
+ * wtab[2 (w - 1) + 1] = maxc[w]; zw[(w - 1) (R + 1) + q] = offw at rank q's first target */
+__global__ void lvl_wire_pack_kernel(int ld, int row0, int lrows, int lw, int R, int me,
+                                     const int32_t* __restrict__ off, const int32_t* __restrict__ offw,
+                                     const int32_t* __restrict__ zw, const int32_t* __restrict__ wtab,
+                                     const uint32_t* __restrict__ arcs, const uint16_t* __restrict__ rix,
+                                     const double* __restrict__ ar, uint32_t* __restrict__ wire,
+                                     double* __restrict__ wire64) {
+    const int jj = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (jj >= lrows) return;
+    const int j = row0 + jj;
+    for (int w = 1; w <= lw; ++w) {
+        const int a0 = off[(size_t)j * LVL_STRIDE + w], c = off[(size_t)j * LVL_STRIDE + w + 1] - a0;
+        const size_t o = (size_t)wtab[2 * (w - 1)] + (size_t)me * wtab[2 * (w - 1) + 1] +
+                         (offw[(size_t)(w - 1) * ld + j] - zw[(w - 1) * (R + 1) + me]);
+        for (int i = lane; i < c; i += 64) {
+            wire[o + i] = (arcs[a0 + i] & 0xFFFFu) | (rix ? (uint32_t)rix[a0 + i] << 16 : 0u);
+            if (wire64) wire64[o + i] = ar[a0 + i];
+        }
+    }
+}
+__global__ void lvl_wire_unpack_kernel(int n, int ld, int row0, int nrows, int w, int nw, int R,
+                                       const int32_t* __restrict__ off, const int32_t* __restrict__ offw,
+                                       const int32_t* __restrict__ zw, const int32_t* __restrict__ wtab,
+                                       const uint32_t* __restrict__ wire, const double* __restrict__ wire64,
+                                       uint32_t* __restrict__ arcs, uint16_t* __restrict__ rix,
+                                       double* __restrict__ ar, uint32_t* __restrict__ aoff) {
+    const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (j >= n || (j >= row0 && j < row0 + nrows)) return;
+    const long long nb = ld / SRT_SHARD_ALIGN; /* the owner of row j (srt_shard_rows) */
+    int q = 0;
+    while (q + 1 < R && (int)(nb * (q + 1) / R) * SRT_SHARD_ALIGN <= j) ++q;
+    const int a0 = off[(size_t)j * LVL_STRIDE + w], c = off[(size_t)j * LVL_STRIDE + w + 1] - a0;
+    const size_t o = (size_t)wtab[2 * (w - 1)] + (size_t)q * wtab[2 * (w - 1) + 1] +
+                     (offw[(size_t)(w - 1) * ld + j] - zw[(w - 1) * (R + 1) + q]);
+    for (int i = lane; i < c; i += 64) {
+        const uint32_t e = wire[o + i], k = e & 0xFFFFu;
+        arcs[a0 + i] = k | ((uint32_t)w << 16);
+        if (rix) rix[a0 + i] = (uint16_t)(e >> 16);
+        if (wire64) ar[a0 + i] = wire64[o + i];
+        aoff[a0 + i] = k * (uint32_t)nw * 4u;
+    }
+}
+/* the numbering kernels over a device-held range [*lo, *hi) (no read-back of the bounds) */
+__global__ void lvl_rt_index_range_kernel(const int32_t* __restrict__ lo, const int32_t* __restrict__ hi,
+                                          const double* __restrict__ ar,
+                                          const unsigned long long* __restrict__ tab, int ntab,
+                                          uint16_t* __restrict__ rix) {
+    const int a = *lo, b = *hi;
+    for (int i = a + blockIdx.x * blockDim.x + threadIdx.x; i < b; i += gridDim.x * blockDim.x) {
+        const unsigned long long v = (unsigned long long)__double_as_longlong(ar[i]);
+        int l = 0, h = ntab - 1;
+        while (l < h) {
+            const int mid = (l + h) >> 1;
+            if (tab[mid] < v) l = mid + 1;
+            else h = mid;
+        }
+        rix[i] = (uint16_t)l;
+    }
+}
+/* byte offsets of the arcs in [*lo, *hi) */
+__global__ void lvl_aoff_range_kernel(const int32_t* __restrict__ lo, const int32_t* __restrict__ hi, int nw,
+                                      const uint32_t* __restrict__ arcs, uint32_t* __restrict__ aoff) {
+    const int a = *lo, b = *hi;
+    for (int i = a + blockIdx.x * blockDim.x + threadIdx.x; i < b; i += gridDim.x * blockDim.x)
+        aoff[i] = (arcs[i] & 0xFFFFu) * (uint32_t)nw * 4u;
+}
+
+/* the second stream and the per-weight events of the streamed extraction, per state slot (made
+ * once, kept: a stream's creation costs more than a build's host work) */
+static hipStream_t g_lvl_cs[SRT_STATE_SLOTS];
+static hipEvent_t g_lvl_ev[SRT_STATE_SLOTS][LVL_BATCH + 2];
+static int lvl_side_stream(hipStream_t* cs, hipEvent_t** ev) {
+    const int k = srt_state_slot();
+    if (!g_lvl_cs[k]) {
+        SRT_HIPCHK(hipStreamCreateWithFlags(&g_lvl_cs[k], hipStreamNonBlocking));
+        for (int i = 0; i < LVL_BATCH + 2; i++)
+            SRT_HIPCHK(hipEventCreateWithFlags(&g_lvl_ev[k][i], hipEventDisableTiming));
+    }
+    *cs = g_lvl_cs[k];
+    *ev = g_lvl_ev[k];
+    return SRT_OK;
+}
+/* host staging of the union table and the wire offsets, per slot (alive until the build syncs) */
+static std::vector<unsigned long long> g_lvl_hbuf[SRT_STATE_SLOTS];
 
 /* byte offset of each arc's source row inside a level plane (k * nw * 4; nw is this rank's) */
 __global__ void lvl_aoff_kernel(int total, int nw, const uint32_t* __restrict__ arcs,
@@ -942,10 +1149,11 @@ static double lvl_estimate(const unsigned long long* hist, int L, double ntgt, d
 
 /* persistent grid of a 256-thread unit kernel: its resident workgroups per CU x the CUs, a multiple
  * of 8 (one share per XCD), at most the unit blocks */
-static unsigned lvl_grid(const void* fn, unsigned nblk) {
+static unsigned lvl_grid(const void* fn, unsigned nblk, int reserve_cus = 0) {
     int dev = 0, cus = 256, per = 4;
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    cus = max(8, cus - reserve_cus);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 256, 0) != hipSuccess || per < 1) per = 4;
     (void)hipGetLastError();
     unsigned g = (unsigned)(cus * per) & ~7u;
@@ -1066,9 +1274,6 @@ static size_t lvl_avail_bytes(void) {
     return fr;
 }
 
-/* levels enqueued per host round trip: a batch's levels past the one that settles every pair
- * return at once (lvl_step_kernel's prev test) */
-#define LVL_BATCH 8
 /* settled fraction of all pairs the first batch must reach for the build to go on */
 #define LVL_MIN_SETTLED 0.25
 
@@ -1137,13 +1342,10 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     }
     if ((size_t)n * (size_t)(max_rows / 32) * 4 > 0xFFFFFFFFull) return SRT_OK; /* 32-bit offsets */
     const int nw = nrows / 32, nchunk = (nw + 63) / 64;
-    /* a timing-only communicator (srt_comm_init_solo*, tools/solo_rank.py) hands the rank the
-     * whole matrix around its shard: it extracts every row's in-arcs itself, so the collectives it
-     * skips (their bytes charged to the wire model) leave it the arcs the real ranks exchange */
-    const bool xfull = R > 1 && srt_comm_is_solo(comm);
-    const int xrow0 = xfull ? 0 : row0, xrows = xfull ? ld : nrows;
-    const uint32_t* xw = xfull ? w_rows - (size_t)row0 * ld : w_rows;
-    const double* xr = xfull ? r_rows - (size_t)row0 * ld : r_rows;
+    /* a timing-only communicator (srt_comm_init_solo*, tools/solo_rank.py): the rank does a real
+     * rank's work on its own rows and synthesises what its peers would send (lvl_solo_*) */
+    const bool solo = R > 1 && srt_comm_is_solo(comm);
+    const int lrows = min(nrows, max(0, n - row0));
     L->st = st;
     /* on any early return below the allocations go back (lvl_free), unless the build is held */
     struct guard {
@@ -1171,17 +1373,18 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     LVL_TRY_ALLOC(cnt, (ncnt + 1) * sizeof(int32_t), &ok);
     LVL_TRY_ALLOC(off, (ncnt + 1) * sizeof(int32_t), &ok);
     if (!directed) {
-        LVL_TRY_ALLOC(dkey, (size_t)xrows * sizeof(unsigned long long), &ok);
-        LVL_TRY_ALLOC(stash, (size_t)xrows * LVL_STASH_CAP * sizeof(uint32_t), &ok);
-        LVL_TRY_ALLOC(scnt, (size_t)xrows * 4 * sizeof(int32_t), &ok);
+        LVL_TRY_ALLOC(dkey, (size_t)nrows * sizeof(unsigned long long), &ok);
+        LVL_TRY_ALLOC(stash, (size_t)nrows * LVL_STASH_CAP * sizeof(uint32_t), &ok);
+        LVL_TRY_ALLOC(scnt, (size_t)nrows * 4 * sizeof(int32_t), &ok);
     }
     if (ok) {
         SRT_HIPCHK(hipMemsetAsync(cnt, 0, (ncnt + 1) * sizeof(int32_t), st));
         if (directed)
             lvl_arcs_cols_kernel<false><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, cnt, 0, NULL, NULL);
         else
-            lvl_arcs_rows_kernel<false><<<xrows, 256, 0, st>>>(n, ld, xrow0, xw, cnt, 0, NULL, NULL,
+            lvl_arcs_rows_kernel<false><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, cnt, 0, NULL, NULL,
                                                                NULL, NULL, dkey, stash, scnt, dhist);
+        if (solo && lrows > 0) lvl_solo_counts_kernel<<<n, 256, 0, st>>>(n, row0, nrows, lrows, cnt);
         SRT_HIPCHK(hipGetLastError());
         lvl_hist_kernel<<<1024, 256, 0, st>>>(ncnt, cnt, dhist); /* this rank's rows (N > 1) */
         SRT_HIPCHK(hipGetLastError());
@@ -1285,6 +1488,22 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     const int lx = min(lmax, LVL_BATCH);
     int32_t* cnt_keep = NULL;
     if (lx < lmax) LVL_TRY_ALLOC(cnt_keep, (ncnt + 1) * sizeof(int32_t), &ok);
+    /* the streamed first extraction's wire (extract_streamed): every rank's block of a weight
+     * padded to the largest, so at most R x the first batch's arcs -- within 2 GB (a global
+     * quantity: the same choice on every rank), else the segment broadcasts of extract() */
+    int64_t total_lx = 0;
+    for (int x = 1; x <= lx; ++x) total_lx += (int64_t)hist[x];
+    int32_t* offw = NULL;
+    uint32_t* wire = NULL;
+    double* wire64 = NULL;
+    const bool can_stream = R > 1 && !directed && lx <= LVL_STASH_W && hist[0] == 0 && gat &&
+                            srt_form_int("pkw", 1) != 0 && (double)R * (double)total_lx * 12.0 < 2e9;
+    if (can_stream) {
+        LVL_TRY_ALLOC(offw, ((size_t)lx * ld + 1) * sizeof(int32_t), &ok);
+        /* (also the [weight][target] counts before their scan) */
+        LVL_TRY_ALLOC(wire, max((size_t)R * (size_t)total_lx + 8, (size_t)lx * ld + 1) * sizeof(uint32_t), &ok);
+        LVL_TRY_ALLOC(wire64, ((size_t)R * (size_t)total_lx + 8) * sizeof(double), &ok);
+    }
     if (R > 1 && (rc = lvl_agree_min(comm, dagree, &ok, st))) return rc;
     if (!ok) return SRT_OK; /* out of device memory somewhere: Floyd-Warshall on every rank */
     if (R > 1) { /* every target's counts up to lmax on every rank (one owner row each) */
@@ -1317,8 +1536,8 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
             lvl_arcs_cols_kernel<true><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, NULL, lw, off, arcsA,
                                                                 r_rows, arA);
         else
-            lvl_arcs_rows_kernel<true><<<xrows, 256, 0, st>>>(n, ld, xrow0, xw, NULL, lw, off, arcsA,
-                                                              xr, arA, NULL, stash, scnt);
+            lvl_arcs_rows_kernel<true><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, NULL, lw, off, arcsA,
+                                                              r_rows, arA, NULL, stash, scnt);
         SRT_HIPCHK(hipGetLastError());
         if (R > 1) { /* every rank filled its rows' segment: broadcast the segments */
             int32_t hoff[65];
@@ -1336,20 +1555,18 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
              * travel as arcs + u16 indices: 6 B per arc instead of 12. Taken when the post pass
              * will be the packed one (levels <= lw <= 31, pkw) and the fill needs no sort (the
              * sort carries the f64s); more than LVL_RT_CAP values in the union (or a probe
-             * overflow) keeps the f64 segments, on every rank alike. A solo rank (xfull) holds
-             * every segment: it numbers all of them and the collectives only charge the wire. */
+             * overflow) keeps the f64 segments, on every rank alike. */
             const int me = srt_comm_rank(comm);
             /* the arcs this process numbers: its own segment, or (solo) every segment at once,
              * in block 0 */
-            const int nb0 = xfull ? hoff[0] : hoff[me], nb1 = xfull ? hoff[R] : hoff[me + 1];
-            const int qb = xfull ? 0 : me;
+            const int nb0 = hoff[me], nb1 = hoff[me + 1], qb = me;
             if (gat && sorted_w && lw <= 31 && srt_form_int("pkw", 1) != 0) {
                 SRT_HIPCHK(hipMemsetAsync(gat, 0, (size_t)R * LVL_GB * sizeof(double), st));
                 if (nb1 > nb0) {
                     SRT_HIPCHK(hipMemsetAsync(dflag, 0, 2 * sizeof(int), st));
                     SRT_HIPCHK(hipMemsetAsync(H, 0xFF, LVL_RT_SLOTS * sizeof(unsigned long long), st));
-                    lvl_rt_hash_kernel<<<srt_ceil_div(nb1 - nb0, 256), 256, 0, st>>>(
-                        nb1 - nb0, arA + nb0, H, rix + nb0, dflag);
+                    lvl_rt_hash_kernel<<<lvl_rt_grid(nb1 - nb0), 256, 0, st>>>(NULL, NULL, nb0, nb1, arA, H,
+                                                                              rix, dflag);
                     lvl_rt_compact_kernel<<<1, 1024, 0, st>>>(H, map, gat + qb * LVL_GB + 1, dflag + 1);
                     SRT_HIPCHK(hipGetLastError());
                     SRT_HIPCHK(hipMemcpyAsync(gat + qb * LVL_GB, dflag, 2 * sizeof(int),
@@ -1399,6 +1616,12 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
                 }
             const int rc2 = srt_coll_group_end(comm);
             if (rc_ || rc2) return rc_ ? rc_ : rc2;
+            if (solo && lrows > 0) {
+                lvl_solo_arcs_kernel<<<srt_ceil_div(n, 4), 256, 0, st>>>(n, row0, nrows, lrows, 1, lw, nw, off,
+                                                                         arcsA, numbered ? rix : NULL,
+                                                                         numbered ? NULL : arA, NULL);
+                SRT_HIPCHK(hipGetLastError());
+            }
         }
         /* in-arcs of each target sorted by (weight, source vertex): the order the predecessor
          * search walks them in (the full-row fill's atomics leave the order inside a weight
@@ -1422,21 +1645,159 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         if (want_rt && total_x > 0 && !numbered) {
             SRT_HIPCHK(hipMemsetAsync(dflag, 0, 2 * sizeof(int), st));
             SRT_HIPCHK(hipMemsetAsync(H, 0xFF, LVL_RT_SLOTS * sizeof(unsigned long long), st));
-            lvl_rt_hash_kernel<<<srt_ceil_div(total_x, 256), 256, 0, st>>>(total_x, ar, H, rix, dflag);
+            lvl_rt_hash_kernel<<<lvl_rt_grid(total_x), 256, 0, st>>>(NULL, NULL, 0, total_x, ar, H, rix, dflag);
             lvl_rt_compact_kernel<<<1, 1024, 0, st>>>(H, map, rtab, dflag + 1);
             lvl_rt_remap_kernel<<<srt_ceil_div(total_x, 256), 256, 0, st>>>(total_x, map, rix);
             SRT_HIPCHK(hipGetLastError());
         }
         return 0;
     };
-    if ((rc = extract(lx))) return rc;
+    hipEvent_t* wev = NULL; /* wev[w]: the arcs of weight w are in place on this rank */
+    hipStream_t wcs = NULL; /* the side stream */
+    int streamed = 0;       /* the weights the streamed extraction delivers on the side stream */
+    int wnum = 0;           /* its arcs carry table indices (else their f64s travel beside) */
+    const int32_t* wsz = NULL; /* host: offw at the shard starts per weight, then wtab */
+    /* N > 1, the first extraction: the arcs of weight <= lw streamed weight by weight on the side
+     * stream (the kernels above); level d then waits for ev[d] only. Taken when the fill is the
+     * ordered stash (sorted_w) and the reliabilities can be numbered; otherwise extract(). One
+     * host round trip: the gathered reliability blocks and the wire offsets come back together. */
+    auto extract_streamed = [&](int lw) -> int {
+        int64_t t64 = 0;
+        for (int x = 1; x <= lw; ++x) t64 += (int64_t)hist[x];
+        total_x = (int32_t)t64;
+        int rc_ = lvl_side_stream(&wcs, &wev);
+        if (rc_) return rc_;
+        const int me = srt_comm_rank(comm);
+        /* offsets over the arcs with w <= lw, (target, weight)-major, and the own rows' arcs */
+        lvl_mask_kernel<<<srt_ceil_div((int64_t)ncnt, 256), 256, 0, st>>>(ncnt, lw, cnt);
+        SRT_HIPCHK(hipGetLastError());
+        SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, (int)(ncnt + 1), st));
+        lvl_arcs_rows_kernel<true><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, NULL, lw, off, arcsA,
+                                                          r_rows, arA, NULL, stash, scnt);
+        const int32_t* lo = off + (size_t)row0 * LVL_STRIDE;
+        const int32_t* hi = off + (size_t)(row0 + nrows) * LVL_STRIDE;
+        lvl_aoff_range_kernel<<<512, 256, 0, st>>>(lo, hi, nw, arcsA, aoff);
+        /* this rank's distinct reliabilities into its block */
+        SRT_HIPCHK(hipMemsetAsync(gat, 0, (size_t)R * LVL_GB * sizeof(double), st));
+        SRT_HIPCHK(hipMemsetAsync(dflag, 0, 2 * sizeof(int), st));
+        SRT_HIPCHK(hipMemsetAsync(H, 0xFF, LVL_RT_SLOTS * sizeof(unsigned long long), st));
+        lvl_rt_hash_kernel<<<lvl_rt_grid(total_x / R), 256, 0, st>>>(lo, hi, 0, 0, arA, H, rix, dflag);
+        lvl_rt_compact_kernel<<<1, 1024, 0, st>>>(H, map, gat + (size_t)me * LVL_GB + 1, dflag + 1);
+        SRT_HIPCHK(hipGetLastError());
+        SRT_HIPCHK(hipMemcpyAsync(gat + (size_t)me * LVL_GB, dflag, 2 * sizeof(int), hipMemcpyDeviceToDevice, st));
+        /* the wire offsets: [weight][target] scan, and its values at the shard starts */
+        const size_t nwo = (size_t)lx * ld + 1;
+        lvl_wcols_kernel<<<srt_ceil_div((int64_t)nwo, 256), 256, 0, st>>>(ld, lw, cnt,
+                                                                       reinterpret_cast<int32_t*>(wire));
+        SRT_HIPCHK(hipGetLastError());
+        SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, reinterpret_cast<int32_t*>(wire), offw,
+                                                    (int)((size_t)lw * ld + 1), st));
+        int32_t* dsz = packed; /* (free since the count exchange): offw at the shard starts, then wtab */
+        lvl_wire_sizes_kernel<<<srt_ceil_div(lw * (R + 1), 256), 256, 0, st>>>(ld, lw, R, offw, dsz);
+        SRT_HIPCHK(hipGetLastError());
+        if ((rc_ = srt_coll_allgather(comm, gat, LVL_GB * sizeof(double), st))) return rc_;
+        std::vector<unsigned long long>& hb = g_lvl_hbuf[srt_state_slot()];
+        const size_t nz = (size_t)lw * (R + 1);
+        hb.assign((size_t)R * LVL_GB + LVL_RT_CAP + 2 + (nz + 2 * (size_t)lw) / 2 + 2, 0ull);
+        unsigned long long* hg = hb.data();
+        int32_t* hsz = reinterpret_cast<int32_t*>(hg + (size_t)R * LVL_GB + LVL_RT_CAP + 2);
+        int32_t* hwt = hsz + nz; /* wtab: per weight its base in the wire and its block size */
+        SRT_HIPCHK(hipMemcpyAsync(hg, gat, (size_t)R * LVL_GB * sizeof(unsigned long long),
+                                  hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipMemcpyAsync(hsz, dsz, nz * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipStreamSynchronize(st));
+        std::vector<unsigned long long> u;
+        bool fit = true;
+        for (int q = 0; q < R && fit; q++) {
+            int hd[2];
+            memcpy(hd, &hg[(size_t)q * LVL_GB], sizeof(hd));
+            if (hd[0] || hd[1] > LVL_RT_CAP) fit = false;
+            else u.insert(u.end(), hg + (size_t)q * LVL_GB + 1, hg + (size_t)q * LVL_GB + 1 + hd[1]);
+        }
+        if (fit) {
+            std::sort(u.begin(), u.end());
+            u.erase(std::unique(u.begin(), u.end()), u.end());
+            fit = !u.empty() && u.size() <= (size_t)LVL_RT_CAP;
+        }
+        wnum = fit ? 1 : 0; /* the same on every rank: every rank gathered the same */
+        size_t base = 0;
+        for (int w = 1; w <= lw; ++w) {
+            const int32_t* zq = hsz + (size_t)(w - 1) * (R + 1);
+            int mx = 0;
+            for (int q = 0; q < R; q++) mx = max(mx, zq[q + 1] - zq[q]);
+            hwt[2 * (w - 1)] = (int32_t)base;
+            hwt[2 * (w - 1) + 1] = mx;
+            base += (size_t)R * mx;
+        }
+        int32_t* dwt = dsz + nz;
+        SRT_HIPCHK(hipMemcpyAsync(dwt, hwt, 2 * (size_t)lw * sizeof(int32_t), hipMemcpyHostToDevice, st));
+        if (wnum) {
+            const int nu = (int)u.size();
+            unsigned long long* ht = hg + (size_t)R * LVL_GB; /* the table, then the flags */
+            memcpy(ht, u.data(), u.size() * sizeof(unsigned long long));
+            const int hf[2] = {0, nu};
+            memcpy(ht + LVL_RT_CAP, hf, sizeof(hf));
+            SRT_HIPCHK(hipMemcpyAsync(rtab, ht, (size_t)nu * sizeof(double), hipMemcpyHostToDevice, st));
+            SRT_HIPCHK(hipMemcpyAsync(dflag, ht + LVL_RT_CAP, 2 * sizeof(int), hipMemcpyHostToDevice, st));
+            lvl_rt_index_range_kernel<<<512, 256, 0, st>>>(lo, hi, arA,
+                                                           reinterpret_cast<const unsigned long long*>(rtab),
+                                                           nu, rix);
+            SRT_HIPCHK(hipGetLastError());
+        }
+        if (lrows > 0)
+            lvl_wire_pack_kernel<<<srt_ceil_div(lrows, 4), 256, 0, st>>>(ld, row0, lrows, lw, R, me, off, offw, dsz,
+                                                                        dwt, arcsA, wnum ? rix : NULL, arA, wire,
+                                                                        wnum ? NULL : wire64);
+        SRT_HIPCHK(hipGetLastError());
+        SRT_HIPCHK(hipEventRecord(wev[0], st));
+        SRT_HIPCHK(hipStreamWaitEvent(wcs, wev[0], 0));
+        wsz = hsz;
+        arcs = arcsA;
+        ar = arA;
+        streamed = lw;
+        return 0;
+    };
+    /* weight w of the streamed extraction on the side stream: the all-gather of the blocks, their
+     * placement (the solo rank synthesises its peers' arcs instead), and, after the last weight of
+     * a build whose reliabilities were not numbered, the local table over every arc. Enqueued just
+     * before level w, so the host's calls for weight w + 1 overlap the levels on the GPU. */
+    auto stream_weight = [&](int w) -> int {
+        const int32_t* hwt = wsz + (size_t)streamed * (R + 1);
+        const size_t base = (size_t)hwt[2 * (w - 1)], mx = (size_t)hwt[2 * (w - 1) + 1];
+        const int32_t* dsz = packed;
+        const int32_t* dwt = dsz + (size_t)streamed * (R + 1);
+        int rc_ = srt_coll_allgather(comm, wire + base, mx * sizeof(uint32_t), wcs);
+        if (!rc_ && !wnum) rc_ = srt_coll_allgather(comm, wire64 + base, mx * sizeof(double), wcs);
+        if (rc_) return rc_;
+        if (solo && lrows > 0)
+            lvl_solo_arcs_kernel<<<srt_ceil_div(n, 4), 256, 0, wcs>>>(n, row0, nrows, lrows, w, w, nw, off, arcs,
+                                                                      wnum ? rix : NULL, wnum ? NULL : ar, aoff);
+        else if (!solo)
+            lvl_wire_unpack_kernel<<<srt_ceil_div(n, 4), 256, 0, wcs>>>(n, ld, row0, nrows, w, nw, R, off, offw,
+                                                                        dsz, dwt, wire, wnum ? NULL : wire64, arcs,
+                                                                        wnum ? rix : NULL, ar, aoff);
+        SRT_HIPCHK(hipGetLastError());
+        if (w == streamed && !wnum) {
+            SRT_HIPCHK(hipMemsetAsync(dflag, 0, 2 * sizeof(int), wcs));
+            SRT_HIPCHK(hipMemsetAsync(H, 0xFF, LVL_RT_SLOTS * sizeof(unsigned long long), wcs));
+            lvl_rt_hash_kernel<<<lvl_rt_grid(total_x), 256, 0, wcs>>>(NULL, NULL, 0, total_x, ar, H, rix, dflag);
+            lvl_rt_compact_kernel<<<1, 1024, 0, wcs>>>(H, map, rtab, dflag + 1);
+            lvl_rt_remap_kernel<<<srt_ceil_div(total_x, 256), 256, 0, wcs>>>(total_x, map, rix);
+            SRT_HIPCHK(hipGetLastError());
+        }
+        SRT_HIPCHK(hipEventRecord(wev[w], wcs));
+        return SRT_OK;
+    };
     SRT_HIPCHK(hipMemsetAsync(Rb, 0, plane * sizeof(uint32_t), st));
     SRT_HIPCHK(hipMemsetAsync(done, 0, (size_t)n * nchunk, st));
     lvl_init_kernel<<<srt_ceil_div(nrows, 256), 256, 0, st>>>(n, row0, nrows, nw, Rb);
     SRT_HIPCHK(hipGetLastError());
+    if ((rc = can_stream ? extract_streamed(lx) : extract(lx))) return rc;
     unsigned nblk = (unsigned)(((n + 3) / 4) * nchunk);
     nblk = (nblk + 7u) & ~7u;
-    const unsigned pgrid = lvl_grid((const void*)lvl_step_kernel, nblk);
+    /* while the streamed arcs are still arriving, one CU per XCD stays free for the broadcast
+     * (RCCL's kernels, the unpack) beside the persistent level grid */
+    const unsigned pgrid = lvl_grid((const void*)lvl_step_kernel, nblk, streamed ? 8 : 0);
     /* the levels in batches of LVL_BATCH, one host round trip per batch. After the first batch
      * the settled fraction decides whether the rest is worth it: a graph with far-apart vertices
      * (metric latencies, C4metric: 0.2% settled after 8 levels, distances of hundreds of quanta)
@@ -1451,6 +1812,10 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     for (int d0 = 1; d0 <= lmax; d0 += LVL_BATCH) {
         const int d1 = min(lmax, d0 + LVL_BATCH - 1);
         for (int d = d0; d <= d1; ++d) {
+            if (d <= streamed) { /* weight d goes out now; level d waits for it alone */
+                if ((rc = stream_weight(d))) return rc;
+                SRT_HIPCHK(hipStreamWaitEvent(st, wev[d], 0));
+            }
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
             if (d == 1) { /* the weight-1 arcs as bits; level 2 takes up the completion flags
                            * (dinc[1] stays set: a graph settled at level 1 reports 2 levels) */
@@ -1553,7 +1918,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     L->l8 = l8;
     L->pkw = pkw;
     L->total = total_x;
-    L->dkey = dkey && xfull ? dkey + row0 : dkey; /* the diagonal keys of this rank's rows */
+    L->dkey = dkey; /* the diagonal keys of this rank's rows */
     L->r_rows = r_rows;
     return SRT_OK;
 }

@@ -489,7 +489,7 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
     const double* __restrict__ r, const int32_t* __restrict__ inv, uint32_t* __restrict__ lat,
     double* __restrict__ rel, size_t ldo, uint32_t* __restrict__ ws, int nb, int bcap,
     int* __restrict__ overflow, int two = 0,
-    int place = 0, uint32_t* __restrict__ codes = nullptr) {
+    int place = 0, uint32_t* __restrict__ codes = nullptr, unsigned* __restrict__ queue = nullptr) {
     /* place: source s0 = srcs[si] writes output row (and overflow flag) s0 - src_begin instead of
      * si. codes (CMP only): the canonical in-arc of every settled vertex v, row si (stride n):
      * u | w << 17 | ridx << 24 (~0 for the source) -- the neighbour-row derivation's input
@@ -520,7 +520,15 @@ __global__ __launch_bounds__(WG) void wgsssp_kernel(
     uint2* buckets = reinterpret_cast<uint2*>(ws + (size_t)blockIdx.x * slot_words);
     double* relp = ORIG ? nullptr : reinterpret_cast<double*>(buckets + (size_t)nb * bcap);
     const uint32_t bm = (uint32_t)nb - 1u;
-    for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
+    /* sources from a work queue, not a fixed stride: with one workgroup per CU, a workgroup that
+     * started late (its CU still busy at launch) or ran slowly left its whole stride to the end:
+     * single C5 launches took 620-1,008 ms against ~390 */
+    __shared__ int s_next;
+    for (;;) {
+        if (tid == 0) s_next = queue ? (int)atomicAdd(queue, 1u) : -1;
+        __syncthreads();
+        const int si = s_next;
+        if (si >= nsrc || si < 0) break;
         const int s0 = srcs ? srcs[si] : src_begin + si;
         const int s = ORIG ? s0 : inv[s0];
         const int orow = place ? s0 - src_begin : si;
@@ -887,7 +895,8 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     size_t slots = (size_t)cus; /* one workgroup per CU: the packed row takes most of the LDS */
     if (slots > (size_t)nsrc) slots = nsrc;
     uint32_t* ws = NULL;
-    if (srt_malloc_async((void**)&ws, slots * (slot_words + 2) * sizeof(uint32_t), st) != hipSuccess) {
+    /* + the work queue's counter, past the slots */
+    if (srt_malloc_async((void**)&ws, (slots * (slot_words + 2) + 2) * sizeof(uint32_t), st) != hipSuccess) {
         (void)hipGetLastError();
         (void)hipFreeAsync(ca, st);
         srt_set_error("wgsssp: workspace of %zu MiB failed", (slots * slot_words * 4) >> 20);
@@ -895,19 +904,21 @@ int srt_wgsssp_rows(int n, const int2* rowptr, const uint2* cw, const double* r,
     }
     /* placed rows flag overflows at their row: the caller clears the flags */
     if (!place) SRT_HIPCHK(hipMemsetAsync(ovf, 0, (size_t)nsrc * sizeof(int), st));
+    unsigned* queue = ws + slots * (slot_words + 2);
+    SRT_HIPCHK(hipMemsetAsync(queue, 0, sizeof(unsigned), st));
     const size_t dyn = (size_t)((n + 2) / 3) * sizeof(uint32_t);
     if (cmp) { /* original order, compact arcs, reliabilities from the table */
         SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true, true>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
         wgsssp_kernel<1024, true, true><<<(unsigned)slots, 1024, dyn, st>>>(
             n, src_begin, srcs, nsrc, rowptr, ca, rtab, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf,
-            two, place, codes);
+            two, place, codes, queue);
     } else { /* the graph in original order: reliability straight into the output rows */
         SRT_HIPCHK(hipFuncSetAttribute((const void*)wgsssp_kernel<1024, true>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
         wgsssp_kernel<1024, true><<<(unsigned)slots, 1024, dyn, st>>>(
             n, src_begin, srcs, nsrc, rowptr, ca, r, inv, lat, rel, (size_t)n, ws, nb, bcap, ovf,
-            two, place, codes);
+            two, place, codes, queue);
     }
     SRT_HIPCHK(hipGetLastError());
     SRT_HIPCHK(hipFreeAsync(ws, st));

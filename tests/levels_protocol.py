@@ -10,11 +10,14 @@ library's collective log does (srt_comm_log_read: (op, a, b) -- 1 broadcast (byt
   2. the level budget (forced: the whole 254-level budget, or this rank's lcap), agreed (min);
   3. the allocation outcome, agreed (min);
   4. the (target, weight <= lmax) counts (sum all-reduce of ld * (lmax + 2) int32);
-  5. extract(lx = min(lmax, 8)): the reliability blocks' all-gather (numbered segments, when the
-     arcs came out of the stash and lw <= 31), then one broadcast group: every rank's segment as
-     the arcs' 4-B words and either u16 table indices or the f64 reliabilities;
+  5. the first extraction (w <= lx = min(lmax, 8)), streamed: the reliability blocks' all-gather,
+     then per weight w (just before level w) one all-gather of every rank's arcs of weight w, one
+     u32 each (source | table index; the source alone, plus an all-gather of the f64s, when the
+     union passes the table), each rank's block padded to the largest;
   6. per batch of 8 levels: the vote (sum all-reduce of 4 int32: not-done, settled-pair limbs);
-     all ranks done -> the levels stand; after the batch ending at lx < lmax, extract(lmax) as in 5.
+     all ranks done -> the levels stand; after the batch ending at lx < lmax, extract(lmax): the
+     all-gather (when lw <= 31 and the arcs came out of the stash), then one broadcast group of
+     every rank's segment as the arcs' 4-B words and either u16 table indices or the f64s.
 
 The distances, canonical predecessors (largest weight, then smallest tail) and path-order
 reliabilities of the rank's rows are computed too, so the caller can check them against the
@@ -134,7 +137,7 @@ def rank_protocol(rank, R, g, w, r, lcaps, fw_ms=1e30):
     cnt = allreduce(cnt.ravel()).reshape(ld, lmax + 2)
     lx = min(lmax, BATCH)
 
-    def extract(lw):
+    def extract(lw, streamed=False):
         sorted_w = lw <= STASH_W and hist[0] == 0
         numbered = False
         if sorted_w and lw <= 31:  # numbered segments (the reliability blocks)
@@ -160,6 +163,15 @@ def rank_protocol(rank, R, g, w, r, lcaps, fw_ms=1e30):
             if fit:
                 u = np.unique(np.concatenate(union)) if union else np.zeros(0, np.uint64)
                 numbered = 0 < u.size <= RT_CAP
+        if streamed:  # per weight, every rank's block padded to the largest: one all-gather of
+            # one u32 per arc (+ one of the f64s when not numbered)
+            for x in range(1, lw + 1):
+                mx = max(int(cnt[shard(ld, R, q)[0]:min(shard(ld, R, q)[1], n), x].sum())
+                         for q in range(R))
+                calls.append((ALLGATHER, mx * 4, 0))
+                if not numbered:
+                    calls.append((ALLGATHER, mx * 8, 0))
+            return
         calls.append((GBEGIN, 0, 0))
         for q in range(R):
             qb, qe = shard(ld, R, q)
@@ -169,7 +181,8 @@ def rank_protocol(rank, R, g, w, r, lcaps, fw_ms=1e30):
                 calls.append((BCAST, c * (2 if numbered else 8), q))
         calls.append((GEND, 0, 0))
 
-    extract(lx)
+    # the first extraction streams when the arcs come out of the stash (n <= 32768: a table)
+    extract(lx, streamed=lx <= STASH_W and hist[0] == 0 and n <= 32768)
     lw = lx
     # the levels of the local sources (bit-parallel Dial levels restated as boolean matmuls)
     src = np.arange(b, min(e, n))

@@ -4,14 +4,15 @@
 srt_comm_init_solo gives rank r of R a communicator whose collectives return at once: the rank
 runs exactly its own schedule of the sharded build -- its row block, its kept tiles, the
 next-row tiles first, panel assembly + closure on the high-priority stream, the final fill and
-its share of the post pass -- on an otherwise idle GPU. The level build (C4's default, dist_enc
-12) runs its own sources over every target; on a solo communicator it extracts every row's
-in-arcs itself from the whole matrix this tool allocates (the real ranks exchange them: one
-count all-reduce and one segment broadcast per rank, charged by the wire model), so its in-arc
-extraction is N times a real rank's (~1.2 ms more at N = 8 on C4) and its rows are exact. Blocks other ranks would send stay a
-small constant, so the tables are NOT correct and nothing is checked; what it measures is one
-rank's compute plus its round-to-round critical chain at N ranks, i.e. the N-GPU build time
-minus the collectives' own cost. The N-GPU runs themselves are the driver's.
+its share of the post pass -- on an otherwise idle GPU. The rank holds only its own rows, as a
+real rank does. The level build (C4's default, dist_enc 12) counts and extracts its own rows'
+in-arcs and synthesises what its peers would send from them (the counts and the in-arc segments
+of peer target j are those of own row row0 + j % rows, levels.hip lvl_solo_*; C4's in-arcs are
+uniformly random, so each target's level and predecessor work matches a real rank's). Blocks
+other ranks would send are synthetic or a small constant, so the tables are NOT correct and
+nothing is checked; what it measures is one rank's compute plus its critical chain at N ranks,
+i.e. the N-GPU build time minus the collectives' own cost. The N-GPU runs themselves are the
+driver's.
 
 --wire-gbps 0,50,64,100,150 adds a wire model (srt_comm_init_solo_wire): each collective holds
 its stream for --wire-lat-us + the bytes this rank would receive / GB/s, so the schedule feels
@@ -65,15 +66,12 @@ def main():
         comm = ctypes.c_void_p()
         _lib.check(L.srt_comm_init_solo_wire(R, r, 0, gbps, a.wire_lat_us if gbps > 0 else 0.0,
                                              ctypes.byref(comm)), "srt_comm_init_solo_wire")
-        # the whole matrix, the rank's shard passed as its rows: the FW reads only those, the
-        # level build (dist_enc 12) extracts every row's in-arcs itself on a solo communicator,
-        # standing in for the count all-reduce and segment broadcasts the wire model charges
-        wf = torch.empty((ld, ld), dtype=torch.int32, device="cuda")
-        rf = torch.empty((ld, ld), dtype=torch.float64, device="cuda")
-        _lib.check(L.srt_gen_complete_device(n, ld, 0, ld, wl["seed"], wl["lat_max"],
-                                             wl["self_max"], wl["loss_max"], wf.data_ptr(),
-                                             rf.data_ptr(), sp), "gen")
-        w, rr = wf[b:e], rf[b:e]
+        # the rank's own rows only (a real rank's footprint)
+        w = torch.empty((nr, ld), dtype=torch.int32, device="cuda")
+        rr = torch.empty((nr, ld), dtype=torch.float64, device="cuda")
+        _lib.check(L.srt_gen_complete_device(n, ld, b, nr, wl["seed"], wl["lat_max"],
+                                             wl["self_max"], wl["loss_max"], w.data_ptr(),
+                                             rr.data_ptr(), sp), "gen")
         lat = torch.empty((nr, ld), dtype=torch.int32, device="cuda")
         rel = torch.empty((nr, ld), dtype=torch.float64, device="cuda")
         torch.cuda.synchronize()
@@ -98,9 +96,13 @@ def main():
             "ms_total": round(best.ms_total, 2),
             "ms_fw": round(best.ms_fw, 2), "ms_post": round(best.ms_post, 2),
             "us_per_round": round(best.ms_fw * 1e3 / rounds, 1),
-            "update_unit_us": round(best.ms_update * 1e3 / max(best.n_update, 1), 1)}), flush=True)
+            "update_unit_us": round(best.ms_update * 1e3 / max(best.n_update, 1), 1),
+            # level build (dist_enc 12): the lvl_step launches, the predecessor pass and rel_pk
+            "ms_levels": round(best.ms_update, 3), "n_levels_timed": int(best.n_update),
+            "ms_pred": round(best.ms_pred, 3), "ms_rel": round(best.ms_rel, 3),
+            "ms_comm": round(best.ms_comm, 3)}), flush=True)
         L.srt_comm_free(comm)
-        del w, rr, wf, rf, lat, rel
+        del w, rr, lat, rel
         torch.cuda.empty_cache()
 
 
