@@ -75,6 +75,8 @@ LDS_PEAK_TBS = 256 * 256 * 2.4e9 / 1e12  # 256 B/clk/CU x 256 CUs x 2.4 GHz = 15
 # `cyc_per_relax` SIMD cycles under the issue model below, so the relaxation roof is
 # 157.3 T / cyc_per_relax.
 VALU_LANE_CYCLES_T = 256 * 4 * 64 * 2.4e9 / 1e12
+# full-rate VALU issue: one wave64 instruction per SIMD every 2 cycles (T instructions/s)
+VALU_ISSUE_T = 256 * 4 * 2.4e9 / 2 / 1e12
 FW_B = 64
 SHARD_ALIGN = 128  # row-shard / update-tile alignment (srt_device.h SRT_SHARD_ALIGN)
 
@@ -562,10 +564,13 @@ def dense_levels_tail(c: Ctx, wl, step, elapsed, stats, lat, rel, nr, ld):
     avg_ms, per_launch, launches, bound, model = kern[dom]
     achieved = per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     pmc_k = {}  # per-kernel PMC HBM bytes per launch (profiles/pmc_traffic_<wl>_n<N>.json)
+    pmc_tcc = {}  # per-kernel L2 (TCC) hits and misses per launch, same file
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{c.args.workload}_n{world}.json")
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
         pmc_k = {kk: v.get("hbm_bytes_per_launch") for kk, v in pmc.get("kernels", {}).items()}
+        pmc_tcc = {kk: (v["TCC_HIT_sum"], v["TCC_MISS_sum"]) for kk, v in pmc.get("kernels", {}).items()
+                   if "TCC_HIT_sum" in v and "TCC_MISS_sum" in v}
     others = {}
     for name, (ms, b, nl, bd, _) in kern.items():
         gbs = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
@@ -576,6 +581,20 @@ def dense_levels_tail(c: Ctx, wl, step, elapsed, stats, lat, rel, nr, ld):
             hb = step_hbm / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
             o["hbm_compulsory"] = {"bytes_per_launch": step_hbm, "achieved": round(hb, 1),
                                    "peak": HBM_PEAK_GBS, "frac": round(hb / HBM_PEAK_GBS, 4)}
+        if name in pmc_tcc and ms > 0:
+            # the L2's side of the kernel: its TCC requests (hits + misses, PMC,
+            # per launch) at 64 B each, over the live launch time, against the L2 peak
+            hit, miss = pmc_tcc[name]
+            req_b = (hit + miss) * 64.0
+            l2 = req_b / (ms * 1e-3) / 1e9
+            o["l2_requests"] = {"bytes_per_launch": req_b, "bytes_per_request": 64,
+                                "achieved": round(l2, 1), "peak": L2_PEAK_GBS,
+                                "frac": round(l2 / L2_PEAK_GBS, 4),
+                                "hit_rate": round(hit / max(hit + miss, 1), 3), "source": "pmc"}
+        if name == "lvl_pred_kernel":
+            # neither roof binds it: its plane-slice gathers come from the L2 / MALL at a small
+            # fraction of either peak, each batch waiting on the previous one
+            o["limiter"] = "gather latency (L2 / MALL), below both the HBM and the L2 peak"
         others[name] = o
     amin = float(nr) * ld * (4 + 8)
     roofline = {
@@ -693,11 +712,23 @@ def run_sparse(c: Ctx, wl):
                    "model": "per derived row: deg * n*4 B (neighbour distance rows) + n*4 B (one "
                             "optimal neighbour's canonical arcs) + n*12 B (lat + rel rows out)"}]
     traffic = None
+    valu = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{c.args.workload}_n{world}.json")
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
         if pmc.get("kernel") == kname:
             traffic = pmc.get("hbm_bytes_per_launch")
+            vi = pmc.get("SQ_INSTS_VALU_per_launch")
+            if vi and k_ms > 0:
+                # the VALU side: wave64 VALU instructions per launch (PMC) over
+                # the live launch time, against the full-rate issue peak (256 CU x 4 SIMD, one
+                # wave64 instruction per 2 cycles at 2.4 GHz)
+                t = vi / (k_ms * 1e-3) / 1e12
+                valu = {"instructions_per_launch": vi, "achieved": round(t, 4),
+                        "peak": round(VALU_ISSUE_T, 4), "unit": "T wave-instr/s",
+                        "frac": round(t / VALU_ISSUE_T, 4), "source": "pmc SQ_INSTS_VALU"}
+                if pmc.get("SQ_INSTS_VALU_per_pull"):
+                    valu["per_pull"] = pmc["SQ_INSTS_VALU_per_pull"]
     roofline = {"bound": "hbm", "kernel": kname,
         "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -705,6 +736,8 @@ def run_sparse(c: Ctx, wl):
         "launches_timed": len(stats),
         "model": model,
         "relax_per_launch": float(nsrc - nder) * arcs}
+    if valu:
+        roofline["valu"] = valu
     if others:
         roofline["kernels"] = others
     # untimed check build: the tied-pair count over this rank's rows, summed over ranks

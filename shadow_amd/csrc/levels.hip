@@ -35,8 +35,10 @@
 
 #define LVL_STRIDE 256 /* per-target offsets: weight 0..255 */
 /* levels enqueued per host round trip: a batch's levels past the one that settles every pair
- * return at once (lvl_step_kernel's prev test) */
+ * return at once (lvl_step_kernel's prev test); the first batch is LVL_B1 levels, then one level
+ * per batch up to LVL_BATCH, then LVL_BATCH per batch */
 #define LVL_BATCH 8
+#define LVL_B1 4
 #define LVL_WMAX 254   /* largest level budget (distances stay u8: the post pass's small path) */
 #define LVL_PB 12 /* lvl_pred_kernel: gathers per pipelined batch */
 
@@ -256,7 +258,7 @@ __global__ __launch_bounds__(256) void lvl_arcs_cols_kernel(int n, int ld,
     }
 }
 
-/* weight histogram over all targets (for the level budget) and the mask w <= lmax before the scan */
+/* weight histogram over the count rows (for the level budget) */
 __global__ void lvl_hist_kernel(size_t count, const int32_t* __restrict__ cnt,
                                 unsigned long long* __restrict__ hist) {
     __shared__ unsigned long long s[LVL_STRIDE];
@@ -296,10 +298,6 @@ __global__ void lvl_cnt_pack_kernel(int ld, int cols, int to, int32_t* __restric
         cnt[j * LVL_STRIDE + w] = packed[i];
 }
 
-__global__ void lvl_mask_kernel(size_t count, int lmax, int32_t* __restrict__ cnt) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < count && (int)(i % LVL_STRIDE) > lmax) cnt[i] = 0;
-}
 
 /* ---- the arcs' distinct reliabilities (packed post pass) ------------------------------------ *
  * The post pass carries r(pred, t) per pair as a 16-bit index into a table of the distinct arc
@@ -550,6 +548,99 @@ __global__ void lvl_wire_unpack_kernel(int n, int ld, int row0, int nrows, int w
         aoff[a0 + i] = k * (uint32_t)nw * 4u;
     }
 }
+/* Offsets of the (target, weight <= lw) in-arcs without masking the counts or scanning all 256
+ * weight columns: per target its arcs up to lw (lvl_tot_kernel), one scan over the targets, then
+ * the target's weight prefixes (lvl_off_kernel writes off[j][0 .. lw + 1]; columns past lw + 1
+ * are never read: every reader stops at lw + 1). The counts stay whole for a later, heavier
+ * extraction. */
+__global__ void lvl_tot_kernel(int ld, int lw, const int32_t* __restrict__ cnt, int32_t* __restrict__ tot) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > ld) return;
+    int t = 0;
+    if (j < ld)
+        for (int w = 1; w <= lw; ++w) t += cnt[(size_t)j * LVL_STRIDE + w];
+    tot[j] = t;
+}
+__global__ void lvl_off_kernel(int ld, int lw, const int32_t* __restrict__ cnt, const int32_t* __restrict__ base,
+                               int32_t* __restrict__ off) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > ld) return;
+    int run = base[j];
+    off[(size_t)j * LVL_STRIDE] = run;
+    if (j == ld) return;
+    for (int w = 1; w <= lw; ++w) {
+        off[(size_t)j * LVL_STRIDE + w] = run;
+        run += cnt[(size_t)j * LVL_STRIDE + w];
+    }
+    off[(size_t)j * LVL_STRIDE + lw + 1] = run;
+}
+
+/* N > 1, the one exchange ahead of every decision (a sum all-reduce of int32; each rank fills
+ * its own slots, the others stay zero): the weight histogram's 20-bit limbs (512) and the
+ * allocation-failure count (+1 pad), every rank's own arcs per weight w <= LVL_BATCH as 16-bit
+ * halves (R x 16), and every rank's distinct light reliabilities -- a header (probe overflow,
+ * count) then up to LVL_RT_CAP values, as int32 pairs (R x (LVL_RT_CAP + 1) x 2). */
+#define LVL_X_LIMBS (2 * LVL_STRIDE + 2)
+#define LVL_X_CNT (2 * LVL_BATCH)
+static size_t lvl_x_words(int R) { return LVL_X_LIMBS + (size_t)R * LVL_X_CNT + (size_t)R * (LVL_RT_CAP + 1) * 2; }
+/* per rank q in [q0, q1) and weight w <= LVL_BATCH: its shard's arcs of weight w, into the
+ * exchange as 16-bit halves (a rank counts its own shard; a solo rank every shard of its
+ * synthesised counts) */
+__global__ void lvl_rank_counts_kernel(int n, int ld, int R, int q0, const int32_t* __restrict__ cnt,
+                                       int32_t* __restrict__ xcnt) {
+    const int q = q0 + (int)blockIdx.y, w = 1 + (int)blockIdx.x;
+    const long long nb = ld / SRT_SHARD_ALIGN;
+    const int b = (int)(nb * q / R) * SRT_SHARD_ALIGN, e = min(n, (int)(nb * (q + 1) / R) * SRT_SHARD_ALIGN);
+    unsigned s = 0;
+    for (int j = b + threadIdx.x; j < e; j += blockDim.x) s += (unsigned)cnt[(size_t)j * LVL_STRIDE + w];
+    for (int o = 32; o > 0; o >>= 1) s += (unsigned)__shfl_xor((int)s, o);
+    __shared__ unsigned ws[4];
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned t = ws[0] + ws[1] + ws[2] + ws[3];
+        xcnt[(size_t)q * LVL_X_CNT + (w - 1) * 2] = (int32_t)(t & 0xFFFFu);
+        xcnt[(size_t)q * LVL_X_CNT + (w - 1) * 2 + 1] = (int32_t)(t >> 16);
+    }
+}
+/* the distinct reliabilities of this rank's light arcs (1 <= w <= wl) straight from the count
+ * pass's stash, deduped per workgroup in LDS, into the global table H */
+__global__ __launch_bounds__(256) void lvl_rt_hash_stash_kernel(int nrows, int ld, int wl,
+                                                                const uint32_t* __restrict__ stash,
+                                                                const int32_t* __restrict__ scnt,
+                                                                const double* __restrict__ r,
+                                                                unsigned long long* __restrict__ H,
+                                                                int* __restrict__ ovf) {
+    __shared__ unsigned long long key[LVL_RT_LDS];
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int per = (nrows + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int r0 = (int)blockIdx.x * per, r1 = min(nrows, r0 + per);
+    for (int k = tid; k < LVL_RT_LDS; k += 256) key[k] = ~0ull;
+    __syncthreads();
+    bool bad = false;
+    for (int jj = r0; jj < r1; ++jj) { /* wave wv: the row's segment wv */
+        const int m = scnt[(size_t)jj * 4 + wv];
+        const uint32_t* sg = stash + (size_t)jj * LVL_STASH_CAP + wv * LVL_STASH_SEG;
+        for (int i = lane; i < m; i += 64) {
+            const uint32_t e = sg[i], x = e >> 16;
+            if (x < 1u || x > (uint32_t)wl) continue;
+            const unsigned long long v = (unsigned long long)__double_as_longlong(r[(size_t)jj * ld + (e & 0xFFFFu)]);
+            unsigned h = lvl_rt_hash(v) & (LVL_RT_LDS - 1u);
+            int p = 0;
+            for (; p < 64; ++p, h = (h + 1u) & (LVL_RT_LDS - 1u)) {
+                unsigned long long y = __hip_atomic_load(&key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (y == ~0ull) y = atomicCAS(&key[h], ~0ull, v);
+                if (y == ~0ull || y == v) break;
+            }
+            if (p == 64) bad |= lvl_rt_global_slot(v, H) < 0;
+        }
+    }
+    __syncthreads();
+    for (int k = tid; k < LVL_RT_LDS; k += 256)
+        if (key[k] != ~0ull) bad |= lvl_rt_global_slot(key[k], H) < 0;
+    if (bad) *ovf = 1;
+}
+
 /* the numbering kernels over a device-held range [*lo, *hi) (no read-back of the bounds) */
 __global__ void lvl_rt_index_range_kernel(const int32_t* __restrict__ lo, const int32_t* __restrict__ hi,
                                           const double* __restrict__ ar,
@@ -1181,13 +1272,15 @@ typedef struct {
     int total;   /* in-arcs held (w <= lmax) */
     unsigned long long* dkey; /* the diagonal rule's key per local row (undirected rows form) */
     const double* r_rows;
-    void* p[32]; /* every allocation of the build (LVL_ALLOC), freed together */
+    void* p[40]; /* every allocation of the build (LVL_ALLOC), freed together */
     int k;
     hipStream_t st;
+    hipEvent_t wlast; /* the streamed extraction's last weight (side stream), or NULL */
 } lvl_state;
 static lvl_state g_lvl[SRT_STATE_SLOTS];
 
 static void lvl_free(lvl_state* L, hipStream_t st) {
+    if (L->wlast) (void)hipStreamWaitEvent(st, L->wlast, 0); /* the side stream is done with them */
     for (int i = 0; i < L->k; i++)
         if (L->p[i]) (void)hipFreeAsync(L->p[i], st);
     memset(L, 0, sizeof(*L));
@@ -1245,16 +1338,6 @@ const uint8_t* srt_levels_l8(void) {
         }                                                                               \
     } while (0)
 
-/* a min all-reduce of one host int over the ranks (R > 1), through a device word */
-static int lvl_agree_min(const srt_comm* comm, int32_t* dword, int* v, hipStream_t st) {
-    SRT_HIPCHK(hipMemcpyAsync(dword, v, sizeof(int32_t), hipMemcpyHostToDevice, st));
-    int rc = srt_coll_allreduce_i32(comm, dword, 1, 1, st);
-    if (rc) return rc;
-    SRT_HIPCHK(hipMemcpyAsync(v, dword, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    SRT_HIPCHK(hipStreamSynchronize(st));
-    return SRT_OK;
-}
-
 /* bytes the build can still take from the device: free memory plus what the library's scratch
  * pool holds unused (its release threshold keeps freed blocks mapped) */
 static size_t lvl_avail_bytes(void) {
@@ -1278,12 +1361,10 @@ static size_t lvl_avail_bytes(void) {
 #define LVL_MIN_SETTLED 0.25
 
 /* The host-side words of a build (one allocation, zeroed): the weight histogram, the completion
- * flags, the agreement word and the settled-pair counter, the histogram limbs of the N > 1 count
- * exchange (+ the allocation-failure count), and the batch vote. Offsets in u64. */
+ * flags, the agreement words and the settled-pair counter, and the batch vote. Offsets in u64. */
 #define LVL_H_INC 256                            /* int dinc[LVL_WMAX + 1], then dflag[2] */
-#define LVL_H_AGREE 512                          /* int32 agreement word; u64 nset at +2 */
-#define LVL_H_LIMBS 520                          /* int32 [2 * LVL_STRIDE + 1] */
-#define LVL_H_VOTE (LVL_H_LIMBS + LVL_STRIDE + 1) /* int32 [4] */
+#define LVL_H_AGREE 512                          /* int32 agreement words [3]; u64 nset at +2 */
+#define LVL_H_VOTE 520                           /* int32 [4] */
 #define LVL_H_WORDS (LVL_H_VOTE + 2)
 
 /* N > 1, the end of a batch of levels: this rank's vote -- not done (its last level left a pair
@@ -1311,16 +1392,23 @@ __global__ void lvl_vote_kernel(const int* __restrict__ inc_last,
  * them itself (srt_levels_pkw_ready).
  *
  * The N > 1 protocol. Every branch after the first collective is taken on values every rank holds
- * alike -- the summed histogram, the agreed budget, the agreed allocation outcome, the gathered
- * reliability blocks, and each batch's summed vote -- so every rank makes the same collective calls
- * in the same order and no rank leaves while its peers wait in one. In order: the histogram limbs
- * with each rank's allocation-failure count (sum), the budget (min), the allocation outcome (min),
- * the (target, weight <= lmax) counts (sum), the arcs of the first batch (the reliability blocks'
- * all-gather, then one broadcast group of every rank's segment), then per batch of levels the vote
- * (sum); a batch that leaves pairs unsettled at the first batch's last level fetches the heavier
- * arcs the same way. The vote's "all done" is the verdict: no separate agreement.
- * tests/test_dist_gloo.py rehearses this sequence over gloo and tests/test_gpu_protocol.py checks
- * every rank's collective log (srt_comm_log_*) against it. */
+ * alike -- the exchanged histogram and blocks, the agreed budget, allocation outcome and wire, and
+ * each batch's summed vote -- so every rank makes the same collective calls in the same order and
+ * no rank leaves while its peers wait in one. In order:
+ *   1. one sum all-reduce of the exchange (lvl_x_words): the histogram limbs, the allocation-
+ *      failure count, every rank's arcs per weight w <= LVL_BATCH, every rank's distinct light
+ *      reliabilities (so the union table and the wire's block sizes need no later round trip);
+ *   2. one min all-reduce of (budget, allocation outcome, wire allocated) -- each rank allocated
+ *      for its own budget, which is at least the agreed one;
+ *   3. the (target, weight <= lmax) counts (sum);
+ *   4. the first batch's arcs: streamed, one all-gather per weight w <= lx (every rank's block
+ *      padded to the largest), sent one weight ahead of the levels on the side stream; or, where
+ *      that form does not apply, extract(): the reliability blocks' all-gather and one broadcast
+ *      group of the segments;
+ *   5. per batch of levels (1-4, then 5, 6, 7, 8 one at a time, then 8 at a time) the vote
+ *      (sum); after the batch ending at lx < lmax, extract(lmax) as in 4's second form.
+ * The vote's "all done" is the verdict. tests/test_dist_gloo.py rehearses this sequence over gloo
+ * and tests/test_gpu_protocol.py checks every rank's collective log (srt_comm_log_*) against it. */
 int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, int directed,
                      const uint32_t* w_rows, const double* r_rows, uint32_t* lat_rows, double fw_ms,
                      hipStream_t st, evpool_t* evp, int* levels, int64_t* gather_bytes) {
@@ -1361,22 +1449,34 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     SRT_HIPCHK(hipMemsetAsync(dhist, 0, LVL_H_WORDS * sizeof(unsigned long long), st));
     int* dinc = reinterpret_cast<int*>(dhist + LVL_H_INC);
     int32_t* dagree = reinterpret_cast<int32_t*>(dhist + LVL_H_AGREE);
-    int32_t* limbs = reinterpret_cast<int32_t*>(dhist + LVL_H_LIMBS);
     int32_t* dvote = reinterpret_cast<int32_t*>(dhist + LVL_H_VOTE);
+    int* dflag = dinc + LVL_WMAX + 1; /* [0] probe overflow, [1] distinct values */
+    const int me = R > 1 ? srt_comm_rank(comm) : 0;
     /* the count pass's buffers, softly: a rank short of memory sends every rank to the FW through
-     * the failure count it adds to the histogram exchange (its limbs stay zero) */
+     * the failure count it adds to the exchange (its slots stay zero) */
     int ok = 1;
-    int32_t *cnt = NULL, *off = NULL;
+    int32_t *cnt = NULL, *off = NULL, *tb = NULL, *xbuf = NULL;
     unsigned long long* dkey = NULL;
     uint32_t* stash = NULL;
     int32_t* scnt = NULL;
+    unsigned long long* H = NULL;
+    uint16_t* map = NULL;
     LVL_TRY_ALLOC(cnt, (ncnt + 1) * sizeof(int32_t), &ok);
     LVL_TRY_ALLOC(off, (ncnt + 1) * sizeof(int32_t), &ok);
+    LVL_TRY_ALLOC(tb, 2 * ((size_t)ld + 1) * sizeof(int32_t), &ok); /* per-target totals, their scan */
+    LVL_TRY_ALLOC(H, LVL_RT_SLOTS * sizeof(unsigned long long), &ok);
+    LVL_TRY_ALLOC(map, LVL_RT_SLOTS * sizeof(uint16_t), &ok);
     if (!directed) {
         LVL_TRY_ALLOC(dkey, (size_t)nrows * sizeof(unsigned long long), &ok);
         LVL_TRY_ALLOC(stash, (size_t)nrows * LVL_STASH_CAP * sizeof(uint32_t), &ok);
         LVL_TRY_ALLOC(scnt, (size_t)nrows * 4 * sizeof(int32_t), &ok);
     }
+    const size_t xn = R > 1 ? lvl_x_words(R) : 0;
+    if (R > 1) LVL_TRY_ALLOC(xbuf, xn * sizeof(int32_t), &ok);
+    constexpr size_t LVL_GB = LVL_RT_CAP + 1;
+    int32_t* const xlimbs = xbuf;
+    int32_t* const xcnt = xbuf ? xbuf + LVL_X_LIMBS : NULL;
+    int32_t* const xblk = xbuf ? xcnt + (size_t)R * LVL_X_CNT : NULL; /* R blocks of LVL_GB u64 */
     if (ok) {
         SRT_HIPCHK(hipMemsetAsync(cnt, 0, (ncnt + 1) * sizeof(int32_t), st));
         if (directed)
@@ -1386,23 +1486,62 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
                                                                NULL, NULL, dkey, stash, scnt, dhist);
         if (solo && lrows > 0) lvl_solo_counts_kernel<<<n, 256, 0, st>>>(n, row0, nrows, lrows, cnt);
         SRT_HIPCHK(hipGetLastError());
-        lvl_hist_kernel<<<1024, 256, 0, st>>>(ncnt, cnt, dhist); /* this rank's rows (N > 1) */
+        /* this rank's rows (a solo rank: every row of its synthesised counts) */
+        const bool own = R > 1 && !solo;
+        lvl_hist_kernel<<<own ? 256 : 1024, 256, 0, st>>>(own ? (size_t)nrows * LVL_STRIDE : ncnt,
+                                                         own ? cnt + (size_t)row0 * LVL_STRIDE : cnt, dhist);
         SRT_HIPCHK(hipGetLastError());
+        if (R > 1) {
+            SRT_HIPCHK(hipMemsetAsync(xbuf, 0, xn * sizeof(int32_t), st));
+            lvl_hist_limbs_kernel<<<1, LVL_STRIDE, 0, st>>>(1, dhist, xlimbs);
+            lvl_rank_counts_kernel<<<dim3(LVL_BATCH, solo ? R : 1), 256, 0, st>>>(n, ld, R, solo ? 0 : me, cnt, xcnt);
+            if (!directed && lrows > 0) { /* this rank's distinct light reliabilities, its block */
+                int32_t* hd = xblk + (size_t)me * LVL_GB * 2;
+                SRT_HIPCHK(hipMemsetAsync(H, 0xFF, LVL_RT_SLOTS * sizeof(unsigned long long), st));
+                lvl_rt_hash_stash_kernel<<<min(512, lrows), 256, 0, st>>>(lrows, ld, LVL_BATCH, stash, scnt,
+                                                                          r_rows, H, hd);
+                lvl_rt_compact_kernel<<<1, 1024, 0, st>>>(H, map, reinterpret_cast<double*>(hd + 2), hd + 1);
+            }
+            SRT_HIPCHK(hipGetLastError());
+        }
     }
     int rc;
+    std::vector<unsigned long long>& hb = g_lvl_hbuf[srt_state_slot()];
+    hb.assign(R > 1 ? (xn + 1) / 2 + LVL_RT_CAP + 2 * LVL_BATCH + 4 : 4, 0ull);
+    int32_t* hx = reinterpret_cast<int32_t*>(hb.data()); /* the exchange, back on the host */
+    unsigned long long* ht = hb.data() + (xn + 1) / 2;   /* the union table, then its flags */
+    int32_t* hwt = reinterpret_cast<int32_t*>(ht + LVL_RT_CAP + 2); /* the wire's per-weight base, block */
     int failed = !ok;
     if (R > 1) {
-        lvl_hist_limbs_kernel<<<1, LVL_STRIDE, 0, st>>>(1, dhist, limbs);
-        SRT_HIPCHK(hipMemcpyAsync(limbs + 2 * LVL_STRIDE, &failed, sizeof(int32_t), hipMemcpyHostToDevice, st));
-        if ((rc = srt_coll_allreduce_i32(comm, limbs, 2 * LVL_STRIDE + 1, 0, st))) return rc;
-        lvl_hist_limbs_kernel<<<1, LVL_STRIDE, 0, st>>>(0, dhist, limbs);
+        SRT_HIPCHK(hipMemcpyAsync(xlimbs + 2 * LVL_STRIDE, &failed, sizeof(int32_t), hipMemcpyHostToDevice, st));
+        if ((rc = srt_coll_allreduce_i32(comm, xbuf, xn, 0, st))) return rc;
+        lvl_hist_limbs_kernel<<<1, LVL_STRIDE, 0, st>>>(0, dhist, xlimbs);
         SRT_HIPCHK(hipGetLastError());
-        SRT_HIPCHK(hipMemcpyAsync(&failed, limbs + 2 * LVL_STRIDE, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipMemcpyAsync(hx, xbuf, xn * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     }
     unsigned long long hist[LVL_STRIDE];
     SRT_HIPCHK(hipMemcpyAsync(hist, dhist, sizeof(hist), hipMemcpyDeviceToHost, st));
     SRT_HIPCHK(hipStreamSynchronize(st));
+    if (R > 1) failed = hx[2 * LVL_STRIDE];
     if (failed) return SRT_OK; /* out of device memory somewhere: Floyd-Warshall on every rank */
+    /* the union of every rank's distinct light reliabilities (sorted by bits: the same table on
+     * every rank) and, per weight <= LVL_BATCH, the largest rank's arcs (the streamed wire's
+     * block): both from the exchange, so the streamed extraction needs no further round trip */
+    std::vector<unsigned long long> u;
+    bool fit = R > 1;
+    for (int q = 0; q < R && fit; q++) {
+        const int32_t* hd = hx + LVL_X_LIMBS + (size_t)R * LVL_X_CNT + (size_t)q * LVL_GB * 2;
+        if (hd[0] || hd[1] > LVL_RT_CAP) fit = false;
+        else {
+            const unsigned long long* v = reinterpret_cast<const unsigned long long*>(hd + 2);
+            u.insert(u.end(), v, v + hd[1]);
+        }
+    }
+    if (fit) {
+        std::sort(u.begin(), u.end());
+        u.erase(std::unique(u.begin(), u.end()), u.end());
+        fit = !u.empty() && u.size() <= (size_t)LVL_RT_CAP;
+    }
     /* level budget from global quantities (the summed histogram, the largest shard's words): the
      * largest L whose predicted time stays under half the FW time */
     const double nw_all = (double)max_rows / 32.0;
@@ -1419,25 +1558,17 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     }
     if (R > 1) { /* test hook: this rank's memory stands in for a smaller budget (lcap_r<rank>) */
         char key[32];
-        snprintf(key, sizeof(key), "lcap_r%d", srt_comm_rank(comm));
+        snprintf(key, sizeof(key), "lcap_r%d", me);
         const int lc = srt_form_int(key, -1);
         if (lc >= 0 && lc < lmax) lmax = lc;
     }
-    if (R > 1 && (rc = lvl_agree_min(comm, dagree, &lmax, st))) return rc;
-    /* From here every branch reads global values only: hist is summed over the ranks (hist[0] is
-     * the stash-overflow count), lmax agreed. In-arcs come out of the ordered stash already in
-     * (weight, source) order, on every rank, when no row overflowed its stash: no sort. */
-    const int sorted_fill = !directed && lmax <= LVL_STASH_W && hist[0] == 0;
-    int wmin = 0;
-    for (int x = 1; x <= LVL_WMAX && !wmin; ++x)
-        if (hist[x]) wmin = x;
-    if (lmax < 2 || !wmin || wmin > lmax) return SRT_OK;
-    /* in-arcs with w <= lmax: their count from the histogram (no read-back of the scan) */
+    /* Every allocation of the build up front, softly, sized by THIS rank's budget: the agreed
+     * budget is the ranks' minimum, so the buffers fit it. Then one min all-reduce agrees the
+     * budget, the allocation outcome and whether the wire could be allocated. */
+    const int lmax_own = max(lmax, 0);
     int64_t total64 = 0;
-    for (int x = 1; x <= lmax; ++x) total64 += (int64_t)hist[x];
-    if (total64 > 0x7FFFFFF0ll) return SRT_OK; /* int32 arc offsets (global) */
-    const int32_t total = (int32_t)total64;
-    /* every allocation of the build up front, softly: one agreed outcome, then the work */
+    for (int x = 1; x <= lmax_own; ++x) total64 += (int64_t)hist[x];
+    const int32_t total_own = (int32_t)(total64 < 0x7FFFFFF0ll ? total64 : 0x7FFFFFF0ll);
     uint32_t *arcs = NULL, *arcs2 = NULL, *aoff = NULL, *lev = NULL, *Rb = NULL;
     double *ar = NULL, *ar2 = NULL;
     int32_t* seg = NULL;
@@ -1445,67 +1576,90 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     uint8_t* done = NULL;
     size_t tmp_bytes = 0, sb = 0;
     SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(NULL, tmp_bytes, cnt, off, (int)(ncnt + 1), st));
-    const bool need_sort = total > 0 && !sorted_fill;
-    if (need_sort)
-        SRT_HIPCHK(hipcub::DeviceSegmentedRadixSort::SortPairs(NULL, sb, arcs, arcs2, ar, ar2, total,
+    const bool need_sort_own = total_own > 0 && !(!directed && lmax_own <= LVL_STASH_W && hist[0] == 0);
+    if (need_sort_own)
+        SRT_HIPCHK(hipcub::DeviceSegmentedRadixSort::SortPairs(NULL, sb, arcs, arcs2, ar, ar2, total_own,
                                                                ld, seg, seg + 1, 0, 24, st));
-    LVL_TRY_ALLOC(tmp, tmp_bytes, &ok);
-    LVL_TRY_ALLOC(arcs, ((size_t)total + 8) * sizeof(uint32_t), &ok);
-    LVL_TRY_ALLOC(ar, ((size_t)total + 8) * sizeof(double), &ok);
-    if (need_sort) {
-        LVL_TRY_ALLOC(arcs2, ((size_t)total + 8) * sizeof(uint32_t), &ok);
-        LVL_TRY_ALLOC(ar2, ((size_t)total + 8) * sizeof(double), &ok);
-        LVL_TRY_ALLOC(seg, ((size_t)ld + 1) * sizeof(int32_t), &ok);
-        LVL_TRY_ALLOC(stmp, sb, &ok);
+    if (total64 <= 0x7FFFFFF0ll && lmax_own >= 2) {
+        LVL_TRY_ALLOC(tmp, tmp_bytes, &ok);
+        LVL_TRY_ALLOC(arcs, ((size_t)total_own + 8) * sizeof(uint32_t), &ok);
+        LVL_TRY_ALLOC(ar, ((size_t)total_own + 8) * sizeof(double), &ok);
+        if (need_sort_own) {
+            LVL_TRY_ALLOC(arcs2, ((size_t)total_own + 8) * sizeof(uint32_t), &ok);
+            LVL_TRY_ALLOC(ar2, ((size_t)total_own + 8) * sizeof(double), &ok);
+            LVL_TRY_ALLOC(seg, ((size_t)ld + 1) * sizeof(int32_t), &ok);
+            LVL_TRY_ALLOC(stmp, sb, &ok);
+        }
+        LVL_TRY_ALLOC(aoff, ((size_t)total_own + 64) * sizeof(uint32_t), &ok); /* + a gather batch's tail */
+        LVL_TRY_ALLOC(lev, (size_t)lmax_own * plane * sizeof(uint32_t) + 16, &ok);
+        LVL_TRY_ALLOC(Rb, plane * sizeof(uint32_t) + 16, &ok);
+        LVL_TRY_ALLOC(done, (size_t)n * nchunk + 16, &ok);
     }
-    LVL_TRY_ALLOC(aoff, ((size_t)total + 64) * sizeof(uint32_t), &ok); /* + a gather batch's tail */
-    LVL_TRY_ALLOC(lev, (size_t)lmax * plane * sizeof(uint32_t) + 16, &ok);
-    LVL_TRY_ALLOC(Rb, plane * sizeof(uint32_t) + 16, &ok);
-    LVL_TRY_ALLOC(done, (size_t)n * nchunk + 16, &ok);
     /* the distinct arc reliabilities (packed post pass, n <= 32768) */
-    const bool want_rt = total > 0 && n <= 32768;
-    unsigned long long* H = NULL;
-    uint16_t *map = NULL, *rix = NULL;
+    uint16_t* rix = NULL;
     double* rtab = NULL;
-    if (want_rt) {
-        LVL_TRY_ALLOC(H, LVL_RT_SLOTS * sizeof(unsigned long long), &ok);
-        LVL_TRY_ALLOC(map, LVL_RT_SLOTS * sizeof(uint16_t), &ok);
-        LVL_TRY_ALLOC(rix, ((size_t)total + 8) * sizeof(uint16_t), &ok);
+    if (total_own > 0 && n <= 32768) {
+        LVL_TRY_ALLOC(rix, ((size_t)total_own + 8) * sizeof(uint16_t), &ok);
         LVL_TRY_ALLOC(rtab, LVL_RT_CAP * sizeof(double), &ok);
     }
-    /* N > 1: one block per rank for the numbered segments (a header with the overflow flag and
-     * the count, then up to LVL_RT_CAP values), and the count exchange's packed block */
-    constexpr size_t LVL_GB = LVL_RT_CAP + 1;
+    /* N > 1: the segments' reliability blocks (extract()), and the count exchange's packed block */
     double* gat = NULL;
-    if (want_rt && R > 1) LVL_TRY_ALLOC(gat, (size_t)R * LVL_GB * sizeof(double), &ok);
-    const int cols = lmax + 2;
+    if (total_own > 0 && n <= 32768 && R > 1) LVL_TRY_ALLOC(gat, (size_t)R * LVL_GB * sizeof(double), &ok);
     int32_t* packed = NULL;
-    if (R > 1) LVL_TRY_ALLOC(packed, (size_t)ld * cols * sizeof(int32_t), &ok);
-    /* The in-arcs are extracted for the first batch of levels only (w <= lx = min(lmax, LVL_BATCH):
-     * levels d <= lx use no heavier arc) and again up to lmax if the levels run past it: C4 ends
-     * at level 5, and its ~20-quantum budget would extract, number and (N > 1) broadcast 2.5x the
-     * arcs it uses. The counts are kept for the second extraction. */
-    const int lx = min(lmax, LVL_BATCH);
-    int32_t* cnt_keep = NULL;
-    if (lx < lmax) LVL_TRY_ALLOC(cnt_keep, (ncnt + 1) * sizeof(int32_t), &ok);
+    if (R > 1) LVL_TRY_ALLOC(packed, ((size_t)ld * (lmax_own + 2) + 4 * LVL_BATCH * 65) * sizeof(int32_t), &ok);
     /* the streamed first extraction's wire (extract_streamed): every rank's block of a weight
-     * padded to the largest, so at most R x the first batch's arcs -- within 2 GB (a global
-     * quantity: the same choice on every rank), else the segment broadcasts of extract() */
-    int64_t total_lx = 0;
-    for (int x = 1; x <= lx; ++x) total_lx += (int64_t)hist[x];
+     * padded to the largest; needs the union table (fit) and at most 2 GB */
+    const int lx_own = min(lmax_own, LVL_BATCH);
+    size_t wire_words = 0;
+    for (int x = 1; x <= lx_own && R > 1; ++x) {
+        int mx = 0;
+        for (int q = 0; q < R; q++) {
+            const int32_t* c = hx + LVL_X_LIMBS + (size_t)q * LVL_X_CNT + (x - 1) * 2;
+            mx = max(mx, (int)((uint32_t)c[0] | ((uint32_t)c[1] << 16)));
+        }
+        wire_words += (size_t)R * mx;
+    }
     int32_t* offw = NULL;
     uint32_t* wire = NULL;
-    double* wire64 = NULL;
-    const bool can_stream = R > 1 && !directed && lx <= LVL_STASH_W && hist[0] == 0 && gat &&
-                            srt_form_int("pkw", 1) != 0 && (double)R * (double)total_lx * 12.0 < 2e9;
-    if (can_stream) {
-        LVL_TRY_ALLOC(offw, ((size_t)lx * ld + 1) * sizeof(int32_t), &ok);
+    int stream_ok = R > 1 && !directed && hist[0] == 0 && fit && n <= 32768 && lx_own >= 1 &&
+                    srt_form_int("pkw", 1) != 0 && (double)wire_words * 4.0 < 2e9;
+    if (stream_ok && ok) {
+        int sok = 1;
+        LVL_TRY_ALLOC(offw, ((size_t)lx_own * ld + 1) * sizeof(int32_t), &sok);
         /* (also the [weight][target] counts before their scan) */
-        LVL_TRY_ALLOC(wire, max((size_t)R * (size_t)total_lx + 8, (size_t)lx * ld + 1) * sizeof(uint32_t), &ok);
-        LVL_TRY_ALLOC(wire64, ((size_t)R * (size_t)total_lx + 8) * sizeof(double), &ok);
+        LVL_TRY_ALLOC(wire, max(wire_words + 8, (size_t)lx_own * ld + 1) * sizeof(uint32_t), &sok);
+        stream_ok = sok;
     }
-    if (R > 1 && (rc = lvl_agree_min(comm, dagree, &ok, st))) return rc;
+    int ag[3] = {lmax, ok, stream_ok};
+    if (R > 1) {
+        SRT_HIPCHK(hipMemcpyAsync(dagree, ag, sizeof(ag), hipMemcpyHostToDevice, st));
+        if ((rc = srt_coll_allreduce_i32(comm, dagree, 3, 1, st))) return rc;
+        SRT_HIPCHK(hipMemcpyAsync(ag, dagree, sizeof(ag), hipMemcpyDeviceToHost, st));
+        SRT_HIPCHK(hipStreamSynchronize(st));
+        lmax = ag[0];
+        ok = ag[1];
+        stream_ok = ag[2];
+    }
+    /* From here every branch reads agreed or global values only: hist is summed over the ranks
+     * (hist[0] is the stash-overflow count), the budget, the allocation outcome and the wire are
+     * agreed. In-arcs come out of the ordered stash already in (weight, source) order, on every
+     * rank, when no row overflowed its stash: no sort. */
+    int wmin = 0;
+    for (int x = 1; x <= LVL_WMAX && !wmin; ++x)
+        if (hist[x]) wmin = x;
+    if (lmax < 2 || !wmin || wmin > lmax) return SRT_OK;
+    total64 = 0;
+    for (int x = 1; x <= lmax; ++x) total64 += (int64_t)hist[x];
+    if (total64 > 0x7FFFFFF0ll) return SRT_OK; /* int32 arc offsets (global) */
     if (!ok) return SRT_OK; /* out of device memory somewhere: Floyd-Warshall on every rank */
+    const int32_t total = (int32_t)total64;
+    const bool want_rt = total > 0 && n <= 32768;
+    /* The in-arcs are extracted for the first batch of levels only (w <= lx = min(lmax, LVL_BATCH):
+     * levels d <= lx use no heavier arc) and again up to lmax if the levels run past it: C4 ends
+     * at level 5, and its ~20-quantum budget would extract, number and (N > 1) send 2.5x the arcs
+     * it uses. The counts stay whole (narrow offsets) for the second extraction. */
+    const int lx = min(lmax, LVL_BATCH);
+    const int cols = lmax + 2;
     if (R > 1) { /* every target's counts up to lmax on every rank (one owner row each) */
         const int gb = srt_ceil_div((int64_t)ld * cols, 256);
         lvl_cnt_pack_kernel<<<gb, 256, 0, st>>>(ld, cols, 1, cnt, packed);
@@ -1513,11 +1667,17 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         lvl_cnt_pack_kernel<<<gb, 256, 0, st>>>(ld, cols, 0, cnt, packed);
         SRT_HIPCHK(hipGetLastError());
     }
-    if (cnt_keep)
-        SRT_HIPCHK(hipMemcpyAsync(cnt_keep, cnt, (ncnt + 1) * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    /* offsets of the (target, weight <= lw) in-arcs: narrow scan, counts untouched */
+    auto offsets = [&](int lw) -> int {
+        lvl_tot_kernel<<<srt_ceil_div(ld + 1, 256), 256, 0, st>>>(ld, lw, cnt, tb);
+        SRT_HIPCHK(hipGetLastError());
+        SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, tb, tb + ld + 1, ld + 1, st));
+        lvl_off_kernel<<<srt_ceil_div(ld + 1, 256), 256, 0, st>>>(ld, lw, cnt, tb + ld + 1, off);
+        SRT_HIPCHK(hipGetLastError());
+        return SRT_OK;
+    };
     uint32_t* const arcsA = arcs;
     double* const arA = ar;
-    int* dflag = dinc + LVL_WMAX + 1; /* [0] probe overflow, [1] distinct values */
     int32_t total_x = 0;          /* the arcs of the current extraction */
     auto extract = [&](int lw) -> int {
         int numbered = 0; /* the segments travelled as arcs + table indices */
@@ -1525,13 +1685,8 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         for (int x = 1; x <= lw; ++x) t64 += (int64_t)hist[x];
         total_x = (int32_t)t64;
         const int sorted_w = !directed && lw <= LVL_STASH_W && hist[0] == 0; /* global values */
-        int rc_ = 0;
-        if (cnt_keep && lw != lx)
-            SRT_HIPCHK(hipMemcpyAsync(cnt, cnt_keep, (ncnt + 1) * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
-        /* offsets over the arcs with w <= lw, (target, weight)-major */
-        lvl_mask_kernel<<<srt_ceil_div((int64_t)ncnt, 256), 256, 0, st>>>(ncnt, lw, cnt);
-        SRT_HIPCHK(hipGetLastError());
-        SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, (int)(ncnt + 1), st));
+        int rc_ = offsets(lw); /* (target, weight <= lw)-major */
+        if (rc_) return rc_;
         if (directed)
             lvl_arcs_cols_kernel<true><<<ld / 64, 256, 0, st>>>(n, ld, w_rows, NULL, lw, off, arcsA,
                                                                 r_rows, arA);
@@ -1656,7 +1811,6 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     hipStream_t wcs = NULL; /* the side stream */
     int streamed = 0;       /* the weights the streamed extraction delivers on the side stream */
     int wnum = 0;           /* its arcs carry table indices (else their f64s travel beside) */
-    const int32_t* wsz = NULL; /* host: offw at the shard starts per weight, then wtab */
     /* N > 1, the first extraction: the arcs of weight <= lw streamed weight by weight on the side
      * stream (the kernels above); level d then waits for ev[d] only. Taken when the fill is the
      * ordered stash (sorted_w) and the reliabilities can be numbered; otherwise extract(). One
@@ -1667,91 +1821,53 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         total_x = (int32_t)t64;
         int rc_ = lvl_side_stream(&wcs, &wev);
         if (rc_) return rc_;
-        const int me = srt_comm_rank(comm);
         /* offsets over the arcs with w <= lw, (target, weight)-major, and the own rows' arcs */
-        lvl_mask_kernel<<<srt_ceil_div((int64_t)ncnt, 256), 256, 0, st>>>(ncnt, lw, cnt);
-        SRT_HIPCHK(hipGetLastError());
-        SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, (int)(ncnt + 1), st));
+        if ((rc_ = offsets(lw))) return rc_;
         lvl_arcs_rows_kernel<true><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, NULL, lw, off, arcsA,
                                                           r_rows, arA, NULL, stash, scnt);
         const int32_t* lo = off + (size_t)row0 * LVL_STRIDE;
         const int32_t* hi = off + (size_t)(row0 + nrows) * LVL_STRIDE;
         lvl_aoff_range_kernel<<<512, 256, 0, st>>>(lo, hi, nw, arcsA, aoff);
-        /* this rank's distinct reliabilities into its block */
-        SRT_HIPCHK(hipMemsetAsync(gat, 0, (size_t)R * LVL_GB * sizeof(double), st));
-        SRT_HIPCHK(hipMemsetAsync(dflag, 0, 2 * sizeof(int), st));
-        SRT_HIPCHK(hipMemsetAsync(H, 0xFF, LVL_RT_SLOTS * sizeof(unsigned long long), st));
-        lvl_rt_hash_kernel<<<lvl_rt_grid(total_x / R), 256, 0, st>>>(lo, hi, 0, 0, arA, H, rix, dflag);
-        lvl_rt_compact_kernel<<<1, 1024, 0, st>>>(H, map, gat + (size_t)me * LVL_GB + 1, dflag + 1);
-        SRT_HIPCHK(hipGetLastError());
-        SRT_HIPCHK(hipMemcpyAsync(gat + (size_t)me * LVL_GB, dflag, 2 * sizeof(int), hipMemcpyDeviceToDevice, st));
-        /* the wire offsets: [weight][target] scan, and its values at the shard starts */
-        const size_t nwo = (size_t)lx * ld + 1;
-        lvl_wcols_kernel<<<srt_ceil_div((int64_t)nwo, 256), 256, 0, st>>>(ld, lw, cnt,
-                                                                       reinterpret_cast<int32_t*>(wire));
-        SRT_HIPCHK(hipGetLastError());
-        SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, reinterpret_cast<int32_t*>(wire), offw,
-                                                    (int)((size_t)lw * ld + 1), st));
-        int32_t* dsz = packed; /* (free since the count exchange): offw at the shard starts, then wtab */
-        lvl_wire_sizes_kernel<<<srt_ceil_div(lw * (R + 1), 256), 256, 0, st>>>(ld, lw, R, offw, dsz);
-        SRT_HIPCHK(hipGetLastError());
-        if ((rc_ = srt_coll_allgather(comm, gat, LVL_GB * sizeof(double), st))) return rc_;
-        std::vector<unsigned long long>& hb = g_lvl_hbuf[srt_state_slot()];
-        const size_t nz = (size_t)lw * (R + 1);
-        hb.assign((size_t)R * LVL_GB + LVL_RT_CAP + 2 + (nz + 2 * (size_t)lw) / 2 + 2, 0ull);
-        unsigned long long* hg = hb.data();
-        int32_t* hsz = reinterpret_cast<int32_t*>(hg + (size_t)R * LVL_GB + LVL_RT_CAP + 2);
-        int32_t* hwt = hsz + nz; /* wtab: per weight its base in the wire and its block size */
-        SRT_HIPCHK(hipMemcpyAsync(hg, gat, (size_t)R * LVL_GB * sizeof(unsigned long long),
-                                  hipMemcpyDeviceToHost, st));
-        SRT_HIPCHK(hipMemcpyAsync(hsz, dsz, nz * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-        SRT_HIPCHK(hipStreamSynchronize(st));
-        std::vector<unsigned long long> u;
-        bool fit = true;
-        for (int q = 0; q < R && fit; q++) {
-            int hd[2];
-            memcpy(hd, &hg[(size_t)q * LVL_GB], sizeof(hd));
-            if (hd[0] || hd[1] > LVL_RT_CAP) fit = false;
-            else u.insert(u.end(), hg + (size_t)q * LVL_GB + 1, hg + (size_t)q * LVL_GB + 1 + hd[1]);
-        }
-        if (fit) {
-            std::sort(u.begin(), u.end());
-            u.erase(std::unique(u.begin(), u.end()), u.end());
-            fit = !u.empty() && u.size() <= (size_t)LVL_RT_CAP;
-        }
-        wnum = fit ? 1 : 0; /* the same on every rank: every rank gathered the same */
+        /* the union table (from the exchange): each own arc's index by binary search */
+        const int nu = (int)u.size();
+        memcpy(ht, u.data(), u.size() * sizeof(unsigned long long));
+        const int hf[2] = {0, nu};
+        memcpy(ht + LVL_RT_CAP, hf, sizeof(hf));
+        SRT_HIPCHK(hipMemcpyAsync(rtab, ht, (size_t)nu * sizeof(double), hipMemcpyHostToDevice, st));
+        SRT_HIPCHK(hipMemcpyAsync(dflag, ht + LVL_RT_CAP, 2 * sizeof(int), hipMemcpyHostToDevice, st));
+        lvl_rt_index_range_kernel<<<512, 256, 0, st>>>(lo, hi, arA, reinterpret_cast<const unsigned long long*>(rtab),
+                                                       nu, rix);
+        /* the wire: per weight every rank's block padded to the largest rank's arcs (from the
+         * exchange's per-rank counts), a rank's arcs inside its block in target order (offw: the
+         * [weight][target] scan, zw its values at the shard starts) */
         size_t base = 0;
         for (int w = 1; w <= lw; ++w) {
-            const int32_t* zq = hsz + (size_t)(w - 1) * (R + 1);
             int mx = 0;
-            for (int q = 0; q < R; q++) mx = max(mx, zq[q + 1] - zq[q]);
+            for (int q = 0; q < R; q++) {
+                const int32_t* c = hx + LVL_X_LIMBS + (size_t)q * LVL_X_CNT + (w - 1) * 2;
+                mx = max(mx, (int)((uint32_t)c[0] | ((uint32_t)c[1] << 16)));
+            }
             hwt[2 * (w - 1)] = (int32_t)base;
             hwt[2 * (w - 1) + 1] = mx;
             base += (size_t)R * mx;
         }
-        int32_t* dwt = dsz + nz;
+        const size_t nwo = (size_t)lw * ld + 1;
+        lvl_wcols_kernel<<<srt_ceil_div((int64_t)nwo, 256), 256, 0, st>>>(ld, lw, cnt,
+                                                                       reinterpret_cast<int32_t*>(wire));
+        SRT_HIPCHK(hipGetLastError());
+        SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, reinterpret_cast<int32_t*>(wire), offw,
+                                                    (int)nwo, st));
+        int32_t* dsz = packed; /* (free since the count exchange): offw at the shard starts, then wtab */
+        int32_t* dwt = dsz + (size_t)lw * (R + 1);
+        lvl_wire_sizes_kernel<<<srt_ceil_div(lw * (R + 1), 256), 256, 0, st>>>(ld, lw, R, offw, dsz);
         SRT_HIPCHK(hipMemcpyAsync(dwt, hwt, 2 * (size_t)lw * sizeof(int32_t), hipMemcpyHostToDevice, st));
-        if (wnum) {
-            const int nu = (int)u.size();
-            unsigned long long* ht = hg + (size_t)R * LVL_GB; /* the table, then the flags */
-            memcpy(ht, u.data(), u.size() * sizeof(unsigned long long));
-            const int hf[2] = {0, nu};
-            memcpy(ht + LVL_RT_CAP, hf, sizeof(hf));
-            SRT_HIPCHK(hipMemcpyAsync(rtab, ht, (size_t)nu * sizeof(double), hipMemcpyHostToDevice, st));
-            SRT_HIPCHK(hipMemcpyAsync(dflag, ht + LVL_RT_CAP, 2 * sizeof(int), hipMemcpyHostToDevice, st));
-            lvl_rt_index_range_kernel<<<512, 256, 0, st>>>(lo, hi, arA,
-                                                           reinterpret_cast<const unsigned long long*>(rtab),
-                                                           nu, rix);
-            SRT_HIPCHK(hipGetLastError());
-        }
         if (lrows > 0)
             lvl_wire_pack_kernel<<<srt_ceil_div(lrows, 4), 256, 0, st>>>(ld, row0, lrows, lw, R, me, off, offw, dsz,
-                                                                        dwt, arcsA, wnum ? rix : NULL, arA, wire,
-                                                                        wnum ? NULL : wire64);
+                                                                        dwt, arcsA, rix, arA, wire, NULL);
         SRT_HIPCHK(hipGetLastError());
         SRT_HIPCHK(hipEventRecord(wev[0], st));
         SRT_HIPCHK(hipStreamWaitEvent(wcs, wev[0], 0));
-        wsz = hsz;
+        wnum = 1;
         arcs = arcsA;
         ar = arA;
         streamed = lw;
@@ -1762,29 +1878,18 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
      * a build whose reliabilities were not numbered, the local table over every arc. Enqueued just
      * before level w, so the host's calls for weight w + 1 overlap the levels on the GPU. */
     auto stream_weight = [&](int w) -> int {
-        const int32_t* hwt = wsz + (size_t)streamed * (R + 1);
         const size_t base = (size_t)hwt[2 * (w - 1)], mx = (size_t)hwt[2 * (w - 1) + 1];
         const int32_t* dsz = packed;
         const int32_t* dwt = dsz + (size_t)streamed * (R + 1);
         int rc_ = srt_coll_allgather(comm, wire + base, mx * sizeof(uint32_t), wcs);
-        if (!rc_ && !wnum) rc_ = srt_coll_allgather(comm, wire64 + base, mx * sizeof(double), wcs);
         if (rc_) return rc_;
         if (solo && lrows > 0)
             lvl_solo_arcs_kernel<<<srt_ceil_div(n, 4), 256, 0, wcs>>>(n, row0, nrows, lrows, w, w, nw, off, arcs,
                                                                       wnum ? rix : NULL, wnum ? NULL : ar, aoff);
         else if (!solo)
             lvl_wire_unpack_kernel<<<srt_ceil_div(n, 4), 256, 0, wcs>>>(n, ld, row0, nrows, w, nw, R, off, offw,
-                                                                        dsz, dwt, wire, wnum ? NULL : wire64, arcs,
-                                                                        wnum ? rix : NULL, ar, aoff);
+                                                                        dsz, dwt, wire, NULL, arcs, rix, ar, aoff);
         SRT_HIPCHK(hipGetLastError());
-        if (w == streamed && !wnum) {
-            SRT_HIPCHK(hipMemsetAsync(dflag, 0, 2 * sizeof(int), wcs));
-            SRT_HIPCHK(hipMemsetAsync(H, 0xFF, LVL_RT_SLOTS * sizeof(unsigned long long), wcs));
-            lvl_rt_hash_kernel<<<lvl_rt_grid(total_x), 256, 0, wcs>>>(NULL, NULL, 0, total_x, ar, H, rix, dflag);
-            lvl_rt_compact_kernel<<<1, 1024, 0, wcs>>>(H, map, rtab, dflag + 1);
-            lvl_rt_remap_kernel<<<srt_ceil_div(total_x, 256), 256, 0, wcs>>>(total_x, map, rix);
-            SRT_HIPCHK(hipGetLastError());
-        }
         SRT_HIPCHK(hipEventRecord(wev[w], wcs));
         return SRT_OK;
     };
@@ -1792,7 +1897,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     SRT_HIPCHK(hipMemsetAsync(done, 0, (size_t)n * nchunk, st));
     lvl_init_kernel<<<srt_ceil_div(nrows, 256), 256, 0, st>>>(n, row0, nrows, nw, Rb);
     SRT_HIPCHK(hipGetLastError());
-    if ((rc = can_stream ? extract_streamed(lx) : extract(lx))) return rc;
+    if ((rc = stream_ok ? extract_streamed(lx) : extract(lx))) return rc;
     unsigned nblk = (unsigned)(((n + 3) / 4) * nchunk);
     nblk = (nblk + 7u) & ~7u;
     /* while the streamed arcs are still arriving, one CU per XCD stays free for the broadcast
@@ -1809,11 +1914,17 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     unsigned long long* nset = reinterpret_cast<unsigned long long*>(dagree + 4);
     const int ev0 = evp ? evp->used : 0;
     if (evp && (rc = evpool_reserve(evp, ev0 + 2 * lmax))) return rc;
-    for (int d0 = 1; d0 <= lmax; d0 += LVL_BATCH) {
-        const int d1 = min(lmax, d0 + LVL_BATCH - 1);
+    int wq = 0; /* the streamed weights enqueued so far */
+    for (int d0 = 1, d1 = 0; d0 <= lmax; d0 = d1 + 1) {
+        /* batches: levels 1-4 (C4's distances end at 4-5), then one level at a time up to
+         * LVL_BATCH (a level nobody needs is never launched, nor its weight waited for), then
+         * LVL_BATCH at a time */
+        d1 = d0 == 1 ? min(lmax, LVL_B1) : d0 <= LVL_BATCH ? d0 : min(lmax, d0 + LVL_BATCH - 1);
         for (int d = d0; d <= d1; ++d) {
-            if (d <= streamed) { /* weight d goes out now; level d waits for it alone */
-                if ((rc = stream_weight(d))) return rc;
+            if (D && d > D) continue; /* this rank's sources are settled: nothing to run */
+            if (d <= streamed) { /* weights go out one ahead; level d waits for weight d alone */
+                while (wq < min(streamed, d + 1))
+                    if ((rc = stream_weight(++wq))) return rc;
                 SRT_HIPCHK(hipStreamWaitEvent(st, wev[d], 0));
             }
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
@@ -1830,6 +1941,10 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
             }
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
         }
+        /* the rest of the streamed weights go out now, under the vote and the next levels (every
+         * rank sends them: a rank that is done still serves its peers) */
+        while (wq < streamed)
+            if ((rc = stream_weight(++wq))) return rc;
         SRT_HIPCHK(hipGetLastError());
         int32_t vote[4] = {0, 0, 0, 0};
         if (R > 1) {
@@ -1858,11 +1973,14 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         /* settled pairs of all sources: the levels >= 2 counted by lvl_step_kernel, every source's
          * own vertex (level 0) and the weight-1 arcs (level 1, lvl_first_kernel counts none) */
         const double frac = ((double)settled + (double)n + (double)hist[1]) / ((double)n * (double)n);
-        /* (a forced level build, fw_ms = 1e30 from SRT_FORM levels=1, runs its whole budget) */
-        if (d0 == 1 && d1 < lmax && frac < LVL_MIN_SETTLED && fw_ms < 1e29)
+        /* at the end of the first LVL_BATCH levels (a forced level build, fw_ms = 1e30 from
+         * SRT_FORM levels=1, runs its whole budget) */
+        if (d1 == lx && d1 < lmax && frac < LVL_MIN_SETTLED && fw_ms < 1e29)
             break; /* -> Floyd-Warshall, every rank */
         if (d1 == lx && lx < lmax && (rc = extract(lmax))) return rc; /* the heavier arcs */
     }
+    /* the side stream's last weight before anything frees the wire (lvl_free waits for it too) */
+    if (streamed) L->wlast = wev[streamed];
     if (evp && D) evp->used = ev0 + 2 * D; /* the levels that did work */
     int64_t gathered = 0;
     for (int d = 1; d <= D; ++d) {

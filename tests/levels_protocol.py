@@ -5,16 +5,17 @@ Each rank does what srt_levels_build does with its row shard and logs every coll
 library's collective log does (srt_comm_log_read: (op, a, b) -- 1 broadcast (bytes, root),
 2 all-reduce (count, op_min), 3 all-gather (bytes per rank, 0), 5/6 group begin/end):
 
-  1. count pass over its rows; the weight histogram in 20-bit limbs + the allocation-failure count
-     (sum all-reduce of 2 * 256 + 1 int32);
-  2. the level budget (forced: the whole 254-level budget, or this rank's lcap), agreed (min);
-  3. the allocation outcome, agreed (min);
-  4. the (target, weight <= lmax) counts (sum all-reduce of ld * (lmax + 2) int32);
-  5. the first extraction (w <= lx = min(lmax, 8)), streamed: the reliability blocks' all-gather,
-     then per weight w (just before level w) one all-gather of every rank's arcs of weight w, one
-     u32 each (source | table index; the source alone, plus an all-gather of the f64s, when the
-     union passes the table), each rank's block padded to the largest;
-  6. per batch of 8 levels: the vote (sum all-reduce of 4 int32: not-done, settled-pair limbs);
+  1. count pass over its rows; one sum all-reduce of the exchange: the weight histogram in 20-bit
+     limbs + the allocation-failure count, every rank's arcs per weight <= 8, every rank's
+     distinct reliabilities of its arcs of weight <= 8 (the union table, from the exchange);
+  2. its level budget (forced: the whole 254-level budget, or this rank's lcap); one min
+     all-reduce of (budget, allocations, wire allocated);
+  3. (4 below) the (target, weight <= lmax) counts (sum all-reduce of ld * (lmax + 2) int32);
+  5. the first extraction (w <= lx = min(lmax, 8)), streamed when the union fits the table: per
+     weight w one all-gather of every rank's arcs of weight w, one u32 each (source | table
+     index), each rank's block padded to the largest; else extract() below;
+  6. per batch (levels 1-4, then 5, 6, 7, 8 one at a time, then 8 at a time): the vote (sum
+     all-reduce of 4 int32: not-done, settled-pair limbs);
      all ranks done -> the levels stand; after the batch ending at lx < lmax, extract(lmax): the
      all-gather (when lw <= 31 and the arcs came out of the stash), then one broadcast group of
      every rank's segment as the arcs' 4-B words and either u16 table indices or the f64s.
@@ -33,7 +34,8 @@ import torch.distributed as dist
 
 from shadow_amd import graphs
 
-ALIGN, LVL_STRIDE, LVL_WMAX, RT_CAP, STASH_W, STASH_SEG, BATCH = 128, 256, 254, 2048, 32, 512, 8
+ALIGN, LVL_STRIDE, LVL_WMAX, RT_CAP, STASH_W, STASH_SEG, BATCH, B1 = 128, 256, 254, 2048, 32, 512, 8, 4
+X_LIMBS, X_CNT = 2 * 256 + 2, 2 * 8  # levels.hip LVL_X_LIMBS, LVL_X_CNT
 INF = 0x7FFFFFFF
 BCAST, ALLREDUCE, ALLGATHER, GBEGIN, GEND = 1, 2, 3, 5, 6
 
@@ -111,11 +113,35 @@ def rank_protocol(rank, R, g, w, r, lcaps, fw_ms=1e30):
             lo, hi = wv * Q, min(n, wv * Q + Q)
             if lo < hi:
                 hist[0] += int((light[:, lo:hi].sum(axis=1) > STASH_SEG).sum())
+    # the one sum exchange: limbs + failure count (+ pad), each rank's arcs per weight <= 8 (its
+    # own slot, 16-bit halves), each rank's distinct light reliabilities (w <= 8) as int32 pairs
+    xcnt = np.zeros((R, X_CNT), np.int64)
+    for x in range(1, BATCH + 1):
+        c = int((arcw[rows] == x).sum()) if rows.size else 0
+        xcnt[rank, 2 * (x - 1)], xcnt[rank, 2 * (x - 1) + 1] = c & 0xFFFF, c >> 16
+    xblk = np.zeros((R, (RT_CAP + 1) * 2), np.int64)
+    if rows.size:
+        vals = np.unique(r[rows][(arcw[rows] >= 1) & (arcw[rows] <= BATCH)].view(np.uint64))
+        k = min(vals.size, RT_CAP)
+        xblk[rank, 1] = vals.size
+        xblk[rank, 2:2 + 2 * k] = vals[:k].view(np.int32).astype(np.int64)
     lo20, hi20 = _limbs(hist, 20, 2)
-    red = allreduce(np.concatenate([lo20, hi20, [0]]))
+    red = allreduce(np.concatenate([lo20, hi20, [0, 0], xcnt.ravel(), xblk.ravel()]))
     hist = red[:LVL_STRIDE] + (red[LVL_STRIDE:2 * LVL_STRIDE] << 20)
     assert red[2 * LVL_STRIDE] == 0
-    # 2. budget
+    xc = red[X_LIMBS:X_LIMBS + R * X_CNT].reshape(R, X_CNT)
+    pcnt = xc[:, 0::2] | (xc[:, 1::2] << 16)  # [rank][weight - 1]
+    xb = red[X_LIMBS + R * X_CNT:].reshape(R, (RT_CAP + 1) * 2)
+    union, fit = [], True
+    for q in range(R):
+        if xb[q, 0] or xb[q, 1] > RT_CAP:
+            fit = False
+        else:
+            union.append(xb[q, 2:2 + 2 * xb[q, 1]].astype(np.int32).view(np.uint64))
+    if fit:
+        u = np.unique(np.concatenate(union))
+        fit = 0 < u.size <= RT_CAP
+    # 2. the budget (this rank's), then one min agreement of (budget, allocations, wire)
     lmax = 0
     for x in range(1, LVL_WMAX + 1):
         if _lvl_estimate(hist, x, n, max_rows / 32.0) > 0.5 * fw_ms:
@@ -123,21 +149,24 @@ def rank_protocol(rank, R, g, w, r, lcaps, fw_ms=1e30):
         lmax = x
     if rank in lcaps:
         lmax = min(lmax, lcaps[rank])
-    lmax = int(allreduce([lmax], 1)[0])
+    lx_own = min(lmax, BATCH)
+    wire_words = sum(R * int(pcnt[:, x - 1].max()) for x in range(1, lx_own + 1))
+    stream_ok = int(R > 1 and hist[0] == 0 and fit and n <= 32768 and lx_own >= 1
+                    and wire_words * 4.0 < 2e9)
+    ag = allreduce([lmax, 1, stream_ok], 1)
+    lmax, stream_ok = int(ag[0]), int(ag[2])
     nz = np.nonzero(hist[1:])[0]
     wmin = int(nz[0]) + 1 if nz.size else 0
     if lmax < 2 or not wmin or wmin > lmax:
         return "fw", calls, b, None, None, 0
-    # 3. allocations
-    allreduce([1], 1)
-    # 4. counts up to lmax
+    # 3. counts up to lmax
     cnt = np.zeros((ld, lmax + 2), np.int64)
     for x in range(1, lmax + 2):
         cnt[rows, x] = (arcw[rows] == x).sum(axis=1)
     cnt = allreduce(cnt.ravel()).reshape(ld, lmax + 2)
     lx = min(lmax, BATCH)
 
-    def extract(lw, streamed=False):
+    def extract(lw):
         sorted_w = lw <= STASH_W and hist[0] == 0
         numbered = False
         if sorted_w and lw <= 31:  # numbered segments (the reliability blocks)
@@ -163,15 +192,6 @@ def rank_protocol(rank, R, g, w, r, lcaps, fw_ms=1e30):
             if fit:
                 u = np.unique(np.concatenate(union)) if union else np.zeros(0, np.uint64)
                 numbered = 0 < u.size <= RT_CAP
-        if streamed:  # per weight, every rank's block padded to the largest: one all-gather of
-            # one u32 per arc (+ one of the f64s when not numbered)
-            for x in range(1, lw + 1):
-                mx = max(int(cnt[shard(ld, R, q)[0]:min(shard(ld, R, q)[1], n), x].sum())
-                         for q in range(R))
-                calls.append((ALLGATHER, mx * 4, 0))
-                if not numbered:
-                    calls.append((ALLGATHER, mx * 8, 0))
-            return
         calls.append((GBEGIN, 0, 0))
         for q in range(R):
             qb, qe = shard(ld, R, q)
@@ -181,8 +201,13 @@ def rank_protocol(rank, R, g, w, r, lcaps, fw_ms=1e30):
                 calls.append((BCAST, c * (2 if numbered else 8), q))
         calls.append((GEND, 0, 0))
 
-    # the first extraction streams when the arcs come out of the stash (n <= 32768: a table)
-    extract(lx, streamed=lx <= STASH_W and hist[0] == 0 and n <= 32768)
+    # 4. the first extraction: streamed (per weight, every rank's block padded to the largest:
+    # one all-gather of one u32 per arc, all of them sent before the first vote), or extract()
+    if stream_ok:
+        for x in range(1, lx + 1):
+            calls.append((ALLGATHER, int(pcnt[:, x - 1].max()) * 4, 0))
+    else:
+        extract(lx)
     lw = lx
     # the levels of the local sources (bit-parallel Dial levels restated as boolean matmuls)
     src = np.arange(b, min(e, n))
@@ -191,8 +216,9 @@ def rank_protocol(rank, R, g, w, r, lcaps, fw_ms=1e30):
     D[np.arange(ns), src] = 0
     M = {x: (arcw.T == x).astype(np.float32) for x in range(1, lmax + 1) if hist[x]}  # M[k, j]
     Dl, all_done, settled = 0, False, 0
-    for d0 in range(1, lmax + 1, BATCH):
-        d1 = min(lmax, d0 + BATCH - 1)
+    d0 = 1
+    while d0 <= lmax:  # batches: levels 1-4, then 5, 6, 7, 8 one at a time, then 8 at a time
+        d1 = min(lmax, B1) if d0 == 1 else d0 if d0 <= BATCH else min(lmax, d0 + BATCH - 1)
         for d in range(d0, d1 + 1):
             hit = np.zeros((ns, n), bool)
             for x, Mx in M.items():
@@ -210,11 +236,12 @@ def rank_protocol(rank, R, g, w, r, lcaps, fw_ms=1e30):
             break
         sg = int(vote[1]) + (int(vote[2]) << 21) + (int(vote[3]) << 42)
         frac = (sg + n + int(hist[1])) / float(n * n)
-        if d0 == 1 and d1 < lmax and frac < 0.25 and fw_ms < 1e29:
+        if d1 == lx and d1 < lmax and frac < 0.25 and fw_ms < 1e29:
             break
         if d1 == lx and lx < lmax:
             extract(lmax)
             lw = lmax
+        d0 = d1 + 1
     if not all_done:
         return "fw", calls, b, None, None, Dl
     # canonical predecessors and path-order reliabilities, level by level

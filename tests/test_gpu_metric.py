@@ -70,3 +70,39 @@ def test_metric_build_takes_fw_and_matches_oracle(gpu, n):
     err = np.abs(grel - crel) / np.maximum(crel, 1e-300)
     assert float(err[off].max()) <= REL_TOL
     assert clat.max() > 200 * 1_000_000  # the regime: distances of hundreds of ms
+
+
+def test_metric_full_size_c4metric(gpu):
+    """the C4metric workload itself (n = 32,768, seed 44, the bench's config)
+    through the default dispatch: the level build settles too few pairs in its first batch and
+    hands over to the u16 FW rounds and rel_deep_kernel; 24 rows spread over the matrix (the first,
+    the last, row-block edges and random ones) against the oracle's dense Dijkstra."""
+    import torch
+    L = _lib.lib()
+    n = ld = 32768
+    w, r = _gen(L, n, ld, seed=44)
+    lat = torch.empty_like(w)
+    rel = torch.empty_like(r)
+    st = _lib.BuildStats()
+    _lib.check(L.srt_dense_build_device(n, ld, 0, w.data_ptr(), r.data_ptr(), lat.data_ptr(),
+                                        rel.data_ptr(), None, 0, ctypes.byref(st)), "build")
+    torch.cuda.synchronize()
+    assert st.dist_enc != 12 and st.levels == 0, (st.dist_enc, st.levels)
+    del w, r
+    rng = np.random.default_rng(7)
+    rows = np.unique(np.concatenate([[0, 1, 127, 128, 16383, 16384, 32640, n - 1],
+                                     rng.integers(0, n, 16)])).astype(np.int32)
+    assert len(rows) >= 16
+    idx = torch.from_numpy(rows.astype(np.int64)).cuda()
+    glat = lat.index_select(0, idx).cpu().numpy().view(np.uint32).astype(np.uint64) \
+        * np.uint64(1_000_000)
+    grel = rel.index_select(0, idx).cpu().numpy()
+    del lat, rel
+    torch.cuda.empty_cache()
+    clat, crel, _, _ = oracle.complete_sample(n, 44, 0, SELF_MAX, LOSS_MAX, rows, 16, metric=SCALE)
+    off = np.arange(n)[None, :] != rows[:, None]
+    bad = np.argwhere(np.where(off, glat, 0) != np.where(off, clat, 0))
+    assert bad.size == 0, f"{len(bad)} latency mismatches, first {bad[:5].tolist()}"
+    err = np.abs(grel - crel) / np.maximum(crel, 1e-300)
+    assert float(err[off].max()) <= REL_TOL
+    assert clat.max() > 300 * 1_000_000
