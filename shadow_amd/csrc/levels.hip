@@ -35,10 +35,10 @@
 
 #define LVL_STRIDE 256 /* per-target offsets: weight 0..255 */
 /* levels enqueued per host round trip: a batch's levels past the one that settles every pair
- * return at once (lvl_step_kernel's prev test); the first batch is LVL_B1 levels, then one level
- * per batch up to LVL_BATCH, then LVL_BATCH per batch */
+ * return at once (lvl_step_kernel's prev test); the first batch is LVL_B1 levels (C4's distances
+ * end at 4-5: one vote), then one level per batch up to LVL_BATCH, then LVL_BATCH per batch */
 #define LVL_BATCH 8
-#define LVL_B1 4
+#define LVL_B1 5
 #define LVL_WMAX 254   /* largest level budget (distances stay u8: the post pass's small path) */
 #define LVL_PB 12 /* lvl_pred_kernel: gathers per pipelined batch */
 
@@ -287,17 +287,28 @@ __global__ void lvl_hist_limbs_kernel(int to, unsigned long long* __restrict__ h
                   ((unsigned long long)(uint32_t)limbs[LVL_STRIDE + i] << 20);
     }
 }
-__global__ void lvl_cnt_pack_kernel(int ld, int cols, int to, int32_t* __restrict__ cnt,
-                                    int32_t* __restrict__ packed) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (size_t)ld * cols) return;
-    const size_t j = i / cols, w = i % cols;
-    if (to)
-        packed[i] = cnt[j * LVL_STRIDE + w];
-    else
-        cnt[j * LVL_STRIDE + w] = packed[i];
+/* N > 1: every target's counts of weights w0..w1 from its owner: each rank's block holds its own
+ * targets' counts as u16 ([weight][row], padded to the largest shard), all-gathered (2 B per
+ * (target, weight) instead of the int32 sum all-reduce of every column up to lmax + 1) */
+__global__ void lvl_cnt_gpack_kernel(int row0, int nrows, int max_rows, int w0, int w1, int me,
+                                     const int32_t* __restrict__ cnt, uint16_t* __restrict__ cg) {
+    const int jj = blockIdx.x * blockDim.x + threadIdx.x;
+    if (jj >= nrows) return;
+    uint16_t* blk = cg + (size_t)me * max_rows * (w1 - w0 + 1);
+    for (int w = w0; w <= w1; ++w)
+        blk[(size_t)(w - w0) * max_rows + jj] = (uint16_t)cnt[(size_t)(row0 + jj) * LVL_STRIDE + w];
 }
-
+__global__ void lvl_cnt_gunpack_kernel(int ld, int R, int max_rows, int w0, int w1,
+                                       const uint16_t* __restrict__ cg, int32_t* __restrict__ cnt) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ld) return;
+    const long long nb = ld / SRT_SHARD_ALIGN; /* the owner of row j (srt_shard_rows) */
+    int q = 0;
+    while (q + 1 < R && (int)(nb * (q + 1) / R) * SRT_SHARD_ALIGN <= j) ++q;
+    const int jj = j - (int)(nb * q / R) * SRT_SHARD_ALIGN;
+    const uint16_t* blk = cg + (size_t)q * max_rows * (w1 - w0 + 1);
+    for (int w = w0; w <= w1; ++w) cnt[(size_t)j * LVL_STRIDE + w] = blk[(size_t)(w - w0) * max_rows + jj];
+}
 
 /* ---- the arcs' distinct reliabilities (packed post pass) ------------------------------------ *
  * The post pass carries r(pred, t) per pair as a 16-bit index into a table of the distinct arc
@@ -604,12 +615,16 @@ __global__ void lvl_rank_counts_kernel(int n, int ld, int R, int q0, const int32
     }
 }
 /* the distinct reliabilities of this rank's light arcs (1 <= w <= wl) straight from the count
- * pass's stash, deduped per workgroup in LDS, into the global table H */
+ * pass's stash: each workgroup dedupes a run of rows in its LDS table and writes the table out
+ * whole (tabs[block], coalesced); lvl_rt_merge_kernel folds the tables into the global table H.
+ * Inserting each workgroup's values straight into H (agent-scope atomics on ~500 hot lines, from
+ * every workgroup) took 72 us on a rank of C4 at N = 8. */
 __global__ __launch_bounds__(256) void lvl_rt_hash_stash_kernel(int nrows, int ld, int wl,
                                                                 const uint32_t* __restrict__ stash,
                                                                 const int32_t* __restrict__ scnt,
                                                                 const double* __restrict__ r,
                                                                 unsigned long long* __restrict__ H,
+                                                                unsigned long long* __restrict__ tabs,
                                                                 int* __restrict__ ovf) {
     __shared__ unsigned long long key[LVL_RT_LDS];
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
@@ -618,26 +633,62 @@ __global__ __launch_bounds__(256) void lvl_rt_hash_stash_kernel(int nrows, int l
     for (int k = tid; k < LVL_RT_LDS; k += 256) key[k] = ~0ull;
     __syncthreads();
     bool bad = false;
+    constexpr int PL = LVL_STASH_SEG / 64; /* a segment's entries per lane, loaded together */
     for (int jj = r0; jj < r1; ++jj) { /* wave wv: the row's segment wv */
         const int m = scnt[(size_t)jj * 4 + wv];
         const uint32_t* sg = stash + (size_t)jj * LVL_STASH_CAP + wv * LVL_STASH_SEG;
-        for (int i = lane; i < m; i += 64) {
-            const uint32_t e = sg[i], x = e >> 16;
-            if (x < 1u || x > (uint32_t)wl) continue;
-            const unsigned long long v = (unsigned long long)__double_as_longlong(r[(size_t)jj * ld + (e & 0xFFFFu)]);
-            unsigned h = lvl_rt_hash(v) & (LVL_RT_LDS - 1u);
+        uint32_t e[PL];
+#pragma unroll
+        for (int q = 0; q < PL; ++q) e[q] = q * 64 + lane < m ? sg[q * 64 + lane] : 0u;
+        unsigned long long v[PL];
+#pragma unroll
+        for (int q = 0; q < PL; ++q) {
+            const uint32_t x = e[q] >> 16;
+            v[q] = x >= 1u && x <= (uint32_t)wl
+                       ? (unsigned long long)__double_as_longlong(r[(size_t)jj * ld + (e[q] & 0xFFFFu)])
+                       : ~0ull;
+        }
+#pragma unroll
+        for (int q = 0; q < PL; ++q) {
+            if (v[q] == ~0ull) continue;
+            unsigned h = lvl_rt_hash(v[q]) & (LVL_RT_LDS - 1u);
             int p = 0;
             for (; p < 64; ++p, h = (h + 1u) & (LVL_RT_LDS - 1u)) {
                 unsigned long long y = __hip_atomic_load(&key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (y == ~0ull) y = atomicCAS(&key[h], ~0ull, v);
-                if (y == ~0ull || y == v) break;
+                if (y == ~0ull) y = atomicCAS(&key[h], ~0ull, v[q]);
+                if (y == ~0ull || y == v[q]) break;
             }
-            if (p == 64) bad |= lvl_rt_global_slot(v, H) < 0;
+            if (p == 64) bad |= lvl_rt_global_slot(v[q], H) < 0;
         }
     }
     __syncthreads();
-    for (int k = tid; k < LVL_RT_LDS; k += 256)
-        if (key[k] != ~0ull) bad |= lvl_rt_global_slot(key[k], H) < 0;
+    for (int k = tid; k < LVL_RT_LDS; k += 256) tabs[(size_t)blockIdx.x * LVL_RT_LDS + k] = key[k];
+    if (bad) *ovf = 1;
+}
+/* slot k of every workgroup table mostly holds the same value (the same hash, the same probe):
+ * thread (k, chunk) walks LVL_RT_MC tables' slot k (independent loads) and inserts each value it
+ * has not just inserted into H -- a few inserts per slot and chunk instead of one per table */
+#define LVL_RT_MC 16
+__global__ __launch_bounds__(256) void lvl_rt_merge_kernel(int ntab, const unsigned long long* __restrict__ tabs,
+                                                           unsigned long long* __restrict__ H,
+                                                           int* __restrict__ ovf) {
+    const int k = (blockIdx.x * 256 + threadIdx.x) % LVL_RT_LDS;
+    const int t0 = (blockIdx.x * 256 + threadIdx.x) / LVL_RT_LDS * LVL_RT_MC;
+    if (t0 >= ntab) return;
+    unsigned long long v[LVL_RT_MC];
+#pragma unroll
+    for (int t = 0; t < LVL_RT_MC; ++t) v[t] = t0 + t < ntab ? tabs[(size_t)(t0 + t) * LVL_RT_LDS + k] : ~0ull;
+    unsigned long long seen[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+    bool bad = false;
+#pragma unroll
+    for (int t = 0; t < LVL_RT_MC; ++t) {
+        if (v[t] == ~0ull || v[t] == seen[0] || v[t] == seen[1] || v[t] == seen[2] || v[t] == seen[3]) continue;
+        bad |= lvl_rt_global_slot(v[t], H) < 0;
+        seen[3] = seen[2];
+        seen[2] = seen[1];
+        seen[1] = seen[0];
+        seen[0] = v[t];
+    }
     if (bad) *ovf = 1;
 }
 
@@ -1338,6 +1389,30 @@ const uint8_t* srt_levels_l8(void) {
         }                                                                               \
     } while (0)
 
+/* One stream-ordered allocation for a group of buffers (each 256-B aligned): a build's ~20
+ * scratch buffers cost one pool call instead of twenty on the host's critical path */
+struct lvl_arena {
+    void** p[24];
+    size_t b[24];
+    int k = 0;
+    template <typename T>
+    void add(T** ptr, size_t bytes) {
+        p[k] = reinterpret_cast<void**>(ptr);
+        b[k++] = bytes;
+    }
+    size_t total() const {
+        size_t t = 0;
+        for (int i = 0; i < k; i++) t += (b[i] + 255) & ~(size_t)255;
+        return t;
+    }
+    void carve(char* base) const {
+        for (int i = 0; i < k; i++) {
+            *p[i] = base;
+            base += (b[i] + 255) & ~(size_t)255;
+        }
+    }
+};
+
 /* bytes the build can still take from the device: free memory plus what the library's scratch
  * pool holds unused (its release threshold keeps freed blocks mapped) */
 static size_t lvl_avail_bytes(void) {
@@ -1405,7 +1480,7 @@ __global__ void lvl_vote_kernel(const int* __restrict__ inc_last,
  *      padded to the largest), sent one weight ahead of the levels on the side stream; or, where
  *      that form does not apply, extract(): the reliability blocks' all-gather and one broadcast
  *      group of the segments;
- *   5. per batch of levels (1-4, then 5, 6, 7, 8 one at a time, then 8 at a time) the vote
+ *   5. per batch of levels (1-5, then 6, 7, 8 one at a time, then 8 at a time) the vote
  *      (sum); after the batch ending at lx < lmax, extract(lmax) as in 4's second form.
  * The vote's "all done" is the verdict. tests/test_dist_gloo.py rehearses this sequence over gloo
  * and tests/test_gpu_protocol.py checks every rank's collective log (srt_comm_log_*) against it. */
@@ -1461,18 +1536,26 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     int32_t* scnt = NULL;
     unsigned long long* H = NULL;
     uint16_t* map = NULL;
-    LVL_TRY_ALLOC(cnt, (ncnt + 1) * sizeof(int32_t), &ok);
-    LVL_TRY_ALLOC(off, (ncnt + 1) * sizeof(int32_t), &ok);
-    LVL_TRY_ALLOC(tb, 2 * ((size_t)ld + 1) * sizeof(int32_t), &ok); /* per-target totals, their scan */
-    LVL_TRY_ALLOC(H, LVL_RT_SLOTS * sizeof(unsigned long long), &ok);
-    LVL_TRY_ALLOC(map, LVL_RT_SLOTS * sizeof(uint16_t), &ok);
+    /* a group of buffers in one allocation (soft: a failure clears *okp) */
+    auto commit = [&](const lvl_arena& a, int* okp) {
+        char* base = NULL;
+        if (a.k) LVL_TRY_ALLOC(base, a.total(), okp);
+        if (base) a.carve(base);
+    };
+    lvl_arena a1;
+    a1.add(&cnt, (ncnt + 1) * sizeof(int32_t));
+    a1.add(&off, (ncnt + 1) * sizeof(int32_t));
+    a1.add(&tb, 2 * ((size_t)ld + 1) * sizeof(int32_t)); /* per-target totals, their scan */
+    a1.add(&H, LVL_RT_SLOTS * sizeof(unsigned long long));
+    a1.add(&map, LVL_RT_SLOTS * sizeof(uint16_t));
     if (!directed) {
-        LVL_TRY_ALLOC(dkey, (size_t)nrows * sizeof(unsigned long long), &ok);
-        LVL_TRY_ALLOC(stash, (size_t)nrows * LVL_STASH_CAP * sizeof(uint32_t), &ok);
-        LVL_TRY_ALLOC(scnt, (size_t)nrows * 4 * sizeof(int32_t), &ok);
+        a1.add(&dkey, (size_t)nrows * sizeof(unsigned long long));
+        a1.add(&stash, (size_t)nrows * LVL_STASH_CAP * sizeof(uint32_t));
+        a1.add(&scnt, (size_t)nrows * 4 * sizeof(int32_t));
     }
     const size_t xn = R > 1 ? lvl_x_words(R) : 0;
-    if (R > 1) LVL_TRY_ALLOC(xbuf, xn * sizeof(int32_t), &ok);
+    if (R > 1) a1.add(&xbuf, xn * sizeof(int32_t));
+    commit(a1, &ok);
     constexpr size_t LVL_GB = LVL_RT_CAP + 1;
     int32_t* const xlimbs = xbuf;
     int32_t* const xcnt = xbuf ? xbuf + LVL_X_LIMBS : NULL;
@@ -1498,8 +1581,15 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
             if (!directed && lrows > 0) { /* this rank's distinct light reliabilities, its block */
                 int32_t* hd = xblk + (size_t)me * LVL_GB * 2;
                 SRT_HIPCHK(hipMemsetAsync(H, 0xFF, LVL_RT_SLOTS * sizeof(unsigned long long), st));
-                lvl_rt_hash_stash_kernel<<<min(512, lrows), 256, 0, st>>>(lrows, ld, LVL_BATCH, stash, scnt,
-                                                                          r_rows, H, hd);
+                /* the workgroup tables in the offsets' buffer (free until the offsets) */
+                size_t ntb = (ncnt + 1) * sizeof(int32_t) / (LVL_RT_LDS * sizeof(unsigned long long));
+                ntb = ntb < 512 ? ntb : 512;
+                ntb = ntb < (size_t)lrows ? ntb : (size_t)lrows;
+                const int nt = (int)(ntb > 0 ? ntb : 1);
+                unsigned long long* tabs = reinterpret_cast<unsigned long long*>(off);
+                lvl_rt_hash_stash_kernel<<<nt, 256, 0, st>>>(lrows, ld, LVL_BATCH, stash, scnt, r_rows, H,
+                                                             tabs, hd);
+                lvl_rt_merge_kernel<<<LVL_RT_LDS / 256 * srt_ceil_div(nt, LVL_RT_MC), 256, 0, st>>>(nt, tabs, H, hd);
                 lvl_rt_compact_kernel<<<1, 1024, 0, st>>>(H, map, reinterpret_cast<double*>(hd + 2), hd + 1);
             }
             SRT_HIPCHK(hipGetLastError());
@@ -1580,33 +1670,40 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     if (need_sort_own)
         SRT_HIPCHK(hipcub::DeviceSegmentedRadixSort::SortPairs(NULL, sb, arcs, arcs2, ar, ar2, total_own,
                                                                ld, seg, seg + 1, 0, 24, st));
+    lvl_arena a2;
     if (total64 <= 0x7FFFFFF0ll && lmax_own >= 2) {
-        LVL_TRY_ALLOC(tmp, tmp_bytes, &ok);
-        LVL_TRY_ALLOC(arcs, ((size_t)total_own + 8) * sizeof(uint32_t), &ok);
-        LVL_TRY_ALLOC(ar, ((size_t)total_own + 8) * sizeof(double), &ok);
+        a2.add(&tmp, tmp_bytes);
+        a2.add(&arcs, ((size_t)total_own + 8) * sizeof(uint32_t));
+        a2.add(&ar, ((size_t)total_own + 8) * sizeof(double));
         if (need_sort_own) {
-            LVL_TRY_ALLOC(arcs2, ((size_t)total_own + 8) * sizeof(uint32_t), &ok);
-            LVL_TRY_ALLOC(ar2, ((size_t)total_own + 8) * sizeof(double), &ok);
-            LVL_TRY_ALLOC(seg, ((size_t)ld + 1) * sizeof(int32_t), &ok);
-            LVL_TRY_ALLOC(stmp, sb, &ok);
+            a2.add(&arcs2, ((size_t)total_own + 8) * sizeof(uint32_t));
+            a2.add(&ar2, ((size_t)total_own + 8) * sizeof(double));
+            a2.add(&seg, ((size_t)ld + 1) * sizeof(int32_t));
+            a2.add(&stmp, sb);
         }
-        LVL_TRY_ALLOC(aoff, ((size_t)total_own + 64) * sizeof(uint32_t), &ok); /* + a gather batch's tail */
-        LVL_TRY_ALLOC(lev, (size_t)lmax_own * plane * sizeof(uint32_t) + 16, &ok);
-        LVL_TRY_ALLOC(Rb, plane * sizeof(uint32_t) + 16, &ok);
-        LVL_TRY_ALLOC(done, (size_t)n * nchunk + 16, &ok);
+        a2.add(&aoff, ((size_t)total_own + 64) * sizeof(uint32_t)); /* + a gather batch's tail */
+        a2.add(&lev, (size_t)lmax_own * plane * sizeof(uint32_t) + 16);
+        a2.add(&Rb, plane * sizeof(uint32_t) + 16);
+        a2.add(&done, (size_t)n * nchunk + 16);
     }
     /* the distinct arc reliabilities (packed post pass, n <= 32768) */
     uint16_t* rix = NULL;
     double* rtab = NULL;
     if (total_own > 0 && n <= 32768) {
-        LVL_TRY_ALLOC(rix, ((size_t)total_own + 8) * sizeof(uint16_t), &ok);
-        LVL_TRY_ALLOC(rtab, LVL_RT_CAP * sizeof(double), &ok);
+        a2.add(&rix, ((size_t)total_own + 8) * sizeof(uint16_t));
+        a2.add(&rtab, LVL_RT_CAP * sizeof(double));
     }
-    /* N > 1: the segments' reliability blocks (extract()), and the count exchange's packed block */
+    /* N > 1: the segments' reliability blocks (extract()), the counts' all-gather blocks (u16,
+     * every weight up to the budget), and the streamed wire's offsets at the shard starts */
     double* gat = NULL;
-    if (total_own > 0 && n <= 32768 && R > 1) LVL_TRY_ALLOC(gat, (size_t)R * LVL_GB * sizeof(double), &ok);
+    if (total_own > 0 && n <= 32768 && R > 1) a2.add(&gat, (size_t)R * LVL_GB * sizeof(double));
+    uint16_t* cg = NULL;
     int32_t* packed = NULL;
-    if (R > 1) LVL_TRY_ALLOC(packed, ((size_t)ld * (lmax_own + 2) + 4 * LVL_BATCH * 65) * sizeof(int32_t), &ok);
+    if (R > 1) {
+        a2.add(&cg, ((size_t)R * max_rows * max(lmax_own, 1) + 8) * sizeof(uint16_t));
+        a2.add(&packed, (size_t)4 * LVL_BATCH * 65 * sizeof(int32_t));
+    }
+    commit(a2, &ok);
     /* the streamed first extraction's wire (extract_streamed): every rank's block of a weight
      * padded to the largest; needs the union table (fit) and at most 2 GB */
     const int lx_own = min(lmax_own, LVL_BATCH);
@@ -1625,9 +1722,11 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
                     srt_form_int("pkw", 1) != 0 && (double)wire_words * 4.0 < 2e9;
     if (stream_ok && ok) {
         int sok = 1;
-        LVL_TRY_ALLOC(offw, ((size_t)lx_own * ld + 1) * sizeof(int32_t), &sok);
+        lvl_arena a3;
+        a3.add(&offw, ((size_t)lx_own * ld + 1) * sizeof(int32_t));
         /* (also the [weight][target] counts before their scan) */
-        LVL_TRY_ALLOC(wire, max(wire_words + 8, (size_t)lx_own * ld + 1) * sizeof(uint32_t), &sok);
+        a3.add(&wire, max(wire_words + 8, (size_t)lx_own * ld + 1) * sizeof(uint32_t));
+        commit(a3, &sok);
         stream_ok = sok;
     }
     int ag[3] = {lmax, ok, stream_ok};
@@ -1659,14 +1758,21 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
      * at level 5, and its ~20-quantum budget would extract, number and (N > 1) send 2.5x the arcs
      * it uses. The counts stay whole (narrow offsets) for the second extraction. */
     const int lx = min(lmax, LVL_BATCH);
-    const int cols = lmax + 2;
-    if (R > 1) { /* every target's counts up to lmax on every rank (one owner row each) */
-        const int gb = srt_ceil_div((int64_t)ld * cols, 256);
-        lvl_cnt_pack_kernel<<<gb, 256, 0, st>>>(ld, cols, 1, cnt, packed);
-        if ((rc = srt_coll_allreduce_i32(comm, packed, (size_t)ld * cols, 0, st))) return rc;
-        lvl_cnt_pack_kernel<<<gb, 256, 0, st>>>(ld, cols, 0, cnt, packed);
+    /* every target's counts of weights w0..w1 on every rank (a solo rank has them: synthesised) */
+    auto share_counts = [&](int w0, int w1) -> int {
+        if (R == 1 || w1 < w0) return SRT_OK;
+        const size_t blk = (size_t)max_rows * (w1 - w0 + 1);
+        if (nrows > 0)
+            lvl_cnt_gpack_kernel<<<srt_ceil_div(nrows, 256), 256, 0, st>>>(row0, nrows, max_rows, w0, w1, me,
+                                                                           cnt, cg);
         SRT_HIPCHK(hipGetLastError());
-    }
+        int rc_ = srt_coll_allgather(comm, cg, blk * sizeof(uint16_t), st);
+        if (rc_) return rc_;
+        if (!solo) lvl_cnt_gunpack_kernel<<<srt_ceil_div(ld, 256), 256, 0, st>>>(ld, R, max_rows, w0, w1, cg, cnt);
+        SRT_HIPCHK(hipGetLastError());
+        return SRT_OK;
+    };
+    if ((rc = share_counts(1, lx))) return rc; /* the first extraction's weights */
     /* offsets of the (target, weight <= lw) in-arcs: narrow scan, counts untouched */
     auto offsets = [&](int lw) -> int {
         lvl_tot_kernel<<<srt_ceil_div(ld + 1, 256), 256, 0, st>>>(ld, lw, cnt, tb);
@@ -1916,7 +2022,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     if (evp && (rc = evpool_reserve(evp, ev0 + 2 * lmax))) return rc;
     int wq = 0; /* the streamed weights enqueued so far */
     for (int d0 = 1, d1 = 0; d0 <= lmax; d0 = d1 + 1) {
-        /* batches: levels 1-4 (C4's distances end at 4-5), then one level at a time up to
+        /* batches: levels 1-5 (C4's distances end at 4-5), then one level at a time up to
          * LVL_BATCH (a level nobody needs is never launched, nor its weight waited for), then
          * LVL_BATCH at a time */
         d1 = d0 == 1 ? min(lmax, LVL_B1) : d0 <= LVL_BATCH ? d0 : min(lmax, d0 + LVL_BATCH - 1);
@@ -1946,20 +2052,23 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         while (wq < streamed)
             if ((rc = stream_weight(++wq))) return rc;
         SRT_HIPCHK(hipGetLastError());
-        int32_t vote[4] = {0, 0, 0, 0};
         if (R > 1) {
             lvl_vote_kernel<<<1, 64, 0, st>>>(dinc + d1, nset, dvote);
             SRT_HIPCHK(hipGetLastError());
             if ((rc = srt_coll_allreduce_i32(comm, dvote, 4, 0, st))) return rc;
-            SRT_HIPCHK(hipMemcpyAsync(vote, dvote, sizeof(vote), hipMemcpyDeviceToHost, st));
         }
-        int inc[LVL_BATCH];
-        unsigned long long settled = 0;
-        SRT_HIPCHK(hipMemcpyAsync(inc, dinc + d0, sizeof(int) * (d1 - d0 + 1), hipMemcpyDeviceToHost,
-                                  st));
-        SRT_HIPCHK(hipMemcpyAsync(hflag, dflag, sizeof(hflag), hipMemcpyDeviceToHost, st));
-        SRT_HIPCHK(hipMemcpyAsync(&settled, nset, sizeof(settled), hipMemcpyDeviceToHost, st));
+        /* one read-back: the completion flags, the table flags, the settled pairs and the vote
+         * are neighbours in the host-side words (four copies cost ~20 us each of round trip) */
+        unsigned long long hw[LVL_H_WORDS - LVL_H_INC];
+        SRT_HIPCHK(hipMemcpyAsync(hw, dhist + LVL_H_INC, sizeof(hw), hipMemcpyDeviceToHost, st));
         SRT_HIPCHK(hipStreamSynchronize(st));
+        const int* hinc = reinterpret_cast<const int*>(hw);
+        const int32_t* vote = reinterpret_cast<const int32_t*>(hw + (LVL_H_VOTE - LVL_H_INC));
+        unsigned long long settled = hw[LVL_H_AGREE + 2 - LVL_H_INC];
+        hflag[0] = hinc[LVL_WMAX + 1];
+        hflag[1] = hinc[LVL_WMAX + 2];
+        int inc[LVL_BATCH];
+        for (int d = d0; d <= d1; ++d) inc[d - d0] = hinc[d];
         for (int d = d0; d <= d1 && !D; ++d)
             if (inc[d - d0] == 0) D = d;
         if (R > 1) {
@@ -1977,7 +2086,9 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
          * SRT_FORM levels=1, runs its whole budget) */
         if (d1 == lx && d1 < lmax && frac < LVL_MIN_SETTLED && fw_ms < 1e29)
             break; /* -> Floyd-Warshall, every rank */
-        if (d1 == lx && lx < lmax && (rc = extract(lmax))) return rc; /* the heavier arcs */
+        if (d1 == lx && lx < lmax) { /* the heavier arcs: their counts, then every arc up to lmax */
+            if ((rc = share_counts(lx + 1, lmax)) || (rc = extract(lmax))) return rc;
+        }
     }
     /* the side stream's last weight before anything frees the wire (lvl_free waits for it too) */
     if (streamed) L->wlast = wev[streamed];

@@ -10,11 +10,11 @@ library's collective log does (srt_comm_log_read: (op, a, b) -- 1 broadcast (byt
      distinct reliabilities of its arcs of weight <= 8 (the union table, from the exchange);
   2. its level budget (forced: the whole 254-level budget, or this rank's lcap); one min
      all-reduce of (budget, allocations, wire allocated);
-  3. (4 below) the (target, weight <= lmax) counts (sum all-reduce of ld * (lmax + 2) int32);
+  3. (4 below) every target's counts of the weights <= lx (one all-gather of u16 blocks);
   5. the first extraction (w <= lx = min(lmax, 8)), streamed when the union fits the table: per
      weight w one all-gather of every rank's arcs of weight w, one u32 each (source | table
      index), each rank's block padded to the largest; else extract() below;
-  6. per batch (levels 1-4, then 5, 6, 7, 8 one at a time, then 8 at a time): the vote (sum
+  6. per batch (levels 1-5, then 6, 7, 8 one at a time, then 8 at a time): the vote (sum
      all-reduce of 4 int32: not-done, settled-pair limbs);
      all ranks done -> the levels stand; after the batch ending at lx < lmax, extract(lmax): the
      all-gather (when lw <= 31 and the arcs came out of the stash), then one broadcast group of
@@ -34,7 +34,7 @@ import torch.distributed as dist
 
 from shadow_amd import graphs
 
-ALIGN, LVL_STRIDE, LVL_WMAX, RT_CAP, STASH_W, STASH_SEG, BATCH, B1 = 128, 256, 254, 2048, 32, 512, 8, 4
+ALIGN, LVL_STRIDE, LVL_WMAX, RT_CAP, STASH_W, STASH_SEG, BATCH, B1 = 128, 256, 254, 2048, 32, 512, 8, 5
 X_LIMBS, X_CNT = 2 * 256 + 2, 2 * 8  # levels.hip LVL_X_LIMBS, LVL_X_CNT
 INF = 0x7FFFFFFF
 BCAST, ALLREDUCE, ALLGATHER, GBEGIN, GEND = 1, 2, 3, 5, 6
@@ -159,12 +159,27 @@ def rank_protocol(rank, R, g, w, r, lcaps, fw_ms=1e30):
     wmin = int(nz[0]) + 1 if nz.size else 0
     if lmax < 2 or not wmin or wmin > lmax:
         return "fw", calls, b, None, None, 0
-    # 3. counts up to lmax
+    # 3. every target's counts of the first extraction's weights from its owner: one all-gather
+    # of u16 blocks ([weight][row], padded to the largest shard); the heavier weights' counts
+    # travel the same way before extract(lmax)
     cnt = np.zeros((ld, lmax + 2), np.int64)
-    for x in range(1, lmax + 2):
-        cnt[rows, x] = (arcw[rows] == x).sum(axis=1)
-    cnt = allreduce(cnt.ravel()).reshape(ld, lmax + 2)
     lx = min(lmax, BATCH)
+
+    def share_counts(w0, w1):
+        if w1 < w0:
+            return
+        blk = np.zeros((w1 - w0 + 1, max_rows), np.int32)  # (u16 on the C wire; gloo has no int16)
+        for x in range(w0, w1 + 1):
+            blk[x - w0, :rows.size] = (arcw[rows] == x).sum(axis=1) if rows.size else 0
+        parts = [torch.zeros(blk.size, dtype=torch.int32) for _ in range(R)]
+        dist.all_gather(parts, torch.from_numpy(blk.ravel()))
+        calls.append((ALLGATHER, blk.size * 2, 0))
+        for q in range(R):
+            qb, qe = shard(ld, R, q)
+            pb = parts[q].numpy().reshape(w1 - w0 + 1, max_rows)
+            cnt[qb:qe, w0:w1 + 1] = pb[:, :qe - qb].T
+
+    share_counts(1, lx)
 
     def extract(lw):
         sorted_w = lw <= STASH_W and hist[0] == 0
@@ -217,7 +232,7 @@ def rank_protocol(rank, R, g, w, r, lcaps, fw_ms=1e30):
     M = {x: (arcw.T == x).astype(np.float32) for x in range(1, lmax + 1) if hist[x]}  # M[k, j]
     Dl, all_done, settled = 0, False, 0
     d0 = 1
-    while d0 <= lmax:  # batches: levels 1-4, then 5, 6, 7, 8 one at a time, then 8 at a time
+    while d0 <= lmax:  # batches: levels 1-5, then 6, 7, 8 one at a time, then 8 at a time
         d1 = min(lmax, B1) if d0 == 1 else d0 if d0 <= BATCH else min(lmax, d0 + BATCH - 1)
         for d in range(d0, d1 + 1):
             hit = np.zeros((ns, n), bool)
@@ -239,6 +254,7 @@ def rank_protocol(rank, R, g, w, r, lcaps, fw_ms=1e30):
         if d1 == lx and d1 < lmax and frac < 0.25 and fw_ms < 1e29:
             break
         if d1 == lx and lx < lmax:
+            share_counts(lx + 1, lmax)
             extract(lmax)
             lw = lmax
         d0 = d1 + 1
