@@ -1605,14 +1605,16 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     if (R > 1) {
         SRT_HIPCHK(hipMemcpyAsync(xlimbs + 2 * LVL_STRIDE, &failed, sizeof(int32_t), hipMemcpyHostToDevice, st));
         if ((rc = srt_coll_allreduce_i32(comm, xbuf, xn, 0, st))) return rc;
-        lvl_hist_limbs_kernel<<<1, LVL_STRIDE, 0, st>>>(0, dhist, xlimbs);
-        SRT_HIPCHK(hipGetLastError());
         SRT_HIPCHK(hipMemcpyAsync(hx, xbuf, xn * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     }
     unsigned long long hist[LVL_STRIDE];
-    SRT_HIPCHK(hipMemcpyAsync(hist, dhist, sizeof(hist), hipMemcpyDeviceToHost, st));
+    if (R == 1) SRT_HIPCHK(hipMemcpyAsync(hist, dhist, sizeof(hist), hipMemcpyDeviceToHost, st));
     SRT_HIPCHK(hipStreamSynchronize(st));
-    if (R > 1) failed = hx[2 * LVL_STRIDE];
+    if (R > 1) { /* the summed histogram from its limbs, on the host (one read-back) */
+        failed = hx[2 * LVL_STRIDE];
+        for (int i = 0; i < LVL_STRIDE; i++)
+            hist[i] = (unsigned long long)(uint32_t)hx[i] + ((unsigned long long)(uint32_t)hx[LVL_STRIDE + i] << 20);
+    }
     if (failed) return SRT_OK; /* out of device memory somewhere: Floyd-Warshall on every rank */
     /* the union of every rank's distinct light reliabilities (sorted by bits: the same table on
      * every rank) and, per weight <= LVL_BATCH, the largest rank's arcs (the streamed wire's
@@ -2027,12 +2029,13 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
          * LVL_BATCH at a time */
         d1 = d0 == 1 ? min(lmax, LVL_B1) : d0 <= LVL_BATCH ? d0 : min(lmax, d0 + LVL_BATCH - 1);
         for (int d = d0; d <= d1; ++d) {
+            /* weights go out one ahead of the levels (every rank alike: a settled rank still sends
+             * its arcs), but not past the batch they are for: a weight nobody's level needs is
+             * never sent (C4 ends at level 5) */
+            while (wq < min(streamed, min(d + 1, d1)))
+                if ((rc = stream_weight(++wq))) return rc;
             if (D && d > D) continue; /* this rank's sources are settled: nothing to run */
-            if (d <= streamed) { /* weights go out one ahead; level d waits for weight d alone */
-                while (wq < min(streamed, d + 1))
-                    if ((rc = stream_weight(++wq))) return rc;
-                SRT_HIPCHK(hipStreamWaitEvent(st, wev[d], 0));
-            }
+            if (d <= streamed) SRT_HIPCHK(hipStreamWaitEvent(st, wev[d], 0)); /* weight d alone */
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
             if (d == 1) { /* the weight-1 arcs as bits; level 2 takes up the completion flags
                            * (dinc[1] stays set: a graph settled at level 1 reports 2 levels) */
@@ -2047,10 +2050,6 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
             }
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
         }
-        /* the rest of the streamed weights go out now, under the vote and the next levels (every
-         * rank sends them: a rank that is done still serves its peers) */
-        while (wq < streamed)
-            if ((rc = stream_weight(++wq))) return rc;
         SRT_HIPCHK(hipGetLastError());
         if (R > 1) {
             lvl_vote_kernel<<<1, 64, 0, st>>>(dinc + d1, nset, dvote);
@@ -2087,11 +2086,14 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         if (d1 == lx && d1 < lmax && frac < LVL_MIN_SETTLED && fw_ms < 1e29)
             break; /* -> Floyd-Warshall, every rank */
         if (d1 == lx && lx < lmax) { /* the heavier arcs: their counts, then every arc up to lmax */
+            while (wq < streamed) /* (the first extraction's last weights, for the collectives) */
+                if ((rc = stream_weight(++wq))) return rc;
+            if (wq) SRT_HIPCHK(hipStreamWaitEvent(st, wev[wq], 0)); /* its writes come first */
             if ((rc = share_counts(lx + 1, lmax)) || (rc = extract(lmax))) return rc;
         }
     }
     /* the side stream's last weight before anything frees the wire (lvl_free waits for it too) */
-    if (streamed) L->wlast = wev[streamed];
+    if (wq) L->wlast = wev[wq];
     if (evp && D) evp->used = ev0 + 2 * D; /* the levels that did work */
     int64_t gathered = 0;
     for (int d = 1; d <= D; ++d) {

@@ -13,7 +13,8 @@ library's collective log does (srt_comm_log_read: (op, a, b) -- 1 broadcast (byt
   3. (4 below) every target's counts of the weights <= lx (one all-gather of u16 blocks);
   5. the first extraction (w <= lx = min(lmax, 8)), streamed when the union fits the table: per
      weight w one all-gather of every rank's arcs of weight w, one u32 each (source | table
-     index), each rank's block padded to the largest; else extract() below;
+     index), each rank's block padded to the largest -- sent one weight ahead of the levels but
+     never past the current batch; else extract() below;
   6. per batch (levels 1-5, then 6, 7, 8 one at a time, then 8 at a time): the vote (sum
      all-reduce of 4 int32: not-done, settled-pair limbs);
      all ranks done -> the levels stand; after the batch ending at lx < lmax, extract(lmax): the
@@ -218,12 +219,10 @@ def rank_protocol(rank, R, g, w, r, lcaps, fw_ms=1e30):
 
     # 4. the first extraction: streamed (per weight, every rank's block padded to the largest:
     # one all-gather of one u32 per arc, all of them sent before the first vote), or extract()
-    if stream_ok:
-        for x in range(1, lx + 1):
-            calls.append((ALLGATHER, int(pcnt[:, x - 1].max()) * 4, 0))
-    else:
+    if not stream_ok:
         extract(lx)
     lw = lx
+    wq = 0  # streamed weights sent: one ahead of the levels, never past the current batch
     # the levels of the local sources (bit-parallel Dial levels restated as boolean matmuls)
     src = np.arange(b, min(e, n))
     ns = src.size
@@ -235,6 +234,9 @@ def rank_protocol(rank, R, g, w, r, lcaps, fw_ms=1e30):
     while d0 <= lmax:  # batches: levels 1-5, then 6, 7, 8 one at a time, then 8 at a time
         d1 = min(lmax, B1) if d0 == 1 else d0 if d0 <= BATCH else min(lmax, d0 + BATCH - 1)
         for d in range(d0, d1 + 1):
+            while stream_ok and wq < min(lx, d + 1, d1):
+                wq += 1
+                calls.append((ALLGATHER, int(pcnt[:, wq - 1].max()) * 4, 0))
             hit = np.zeros((ns, n), bool)
             for x, Mx in M.items():
                 if x <= min(d, lw):
