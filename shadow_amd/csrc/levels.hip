@@ -492,10 +492,69 @@ __global__ void lvl_solo_arcs_kernel(int n, int row0, int nrows, int lrows, int 
     }
 }
 
+/* N > 1, streamed: the arcs of weight d from this rank's own sources (Delta_0) set as bits of
+ * plane d - 1 before the levels, so level d needs none of its peers' weight-d arcs. The targets
+ * j0..j1 are this rank's rows and the graph is undirected, so an in-arc (k, w) of own target j is
+ * the arc j -> k: bit j of row k. Weight 1 also goes into R (level 1 is these bits alone). */
+__global__ void lvl_direct_kernel(int j0, int j1, int nw, int lw, size_t plane, const int32_t* __restrict__ off,
+                                  const uint32_t* __restrict__ arcs, uint32_t* __restrict__ lev,
+                                  uint32_t* __restrict__ R) {
+    const int j = j0 + blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (j >= j1) return;
+    const int a0 = off[(size_t)j * LVL_STRIDE + 1], a1 = off[(size_t)j * LVL_STRIDE + lw + 1];
+    const int s = j - j0;
+    const uint32_t bit = 1u << (s & 31);
+    for (int i = a0 + lane; i < a1; i += 64) {
+        const uint32_t e = arcs[i];
+        const int k = (int)(e & 0xFFFFu), w = (int)(e >> 16);
+        const size_t o = (size_t)k * nw + (s >> 5);
+        atomicOr(lev + (size_t)(w - 1) * plane + o, bit);
+        if (w == 1) atomicOr(R + o, bit);
+    }
+}
+
+/* The solo rank's Delta_0 bits without synthesising its peers' segments first: peer target j's
+ * segment of weight w is own row js's, every source moved by shift (lvl_solo_arcs_kernel), so its
+ * own sources are the sources of row js in [row0 - shift, row0 - shift + nrows) (mod n), found by
+ * binary search in the sorted run. One thread per (target, weight). */
+__global__ void lvl_solo_direct_kernel(int n, int row0, int nrows, int lrows, int nw, int lw, size_t plane,
+                                       const int32_t* __restrict__ off, const uint32_t* __restrict__ arcs,
+                                       uint32_t* __restrict__ lev, uint32_t* __restrict__ R) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = t / lw, w = t % lw + 1;
+    if (j >= n) return;
+    const bool own = j >= row0 && j < row0 + nrows;
+    const int js = own ? j : row0 + ((j - row0) % lrows + lrows) % lrows;
+    const int shift = own ? 0 : ((j - js) % n + n) % n;
+    const int a0 = off[(size_t)js * LVL_STRIDE + w], a1 = off[(size_t)js * LVL_STRIDE + w + 1];
+    const int lo = ((row0 - shift) % n + n) % n;
+    for (int part = 0; part < 2; ++part) { /* the range, split where it wraps past n */
+        const int x0 = part ? 0 : lo, x1 = part ? lo + nrows - n : min(n, lo + nrows);
+        if (x1 <= x0) continue;
+        int a = a0, b = a1;
+        while (a < b) {
+            const int m = (a + b) >> 1;
+            if ((int)(arcs[m] & 0xFFFFu) < x0) a = m + 1;
+            else b = m;
+        }
+        for (int i = a; i < a1; ++i) {
+            const int u = (int)(arcs[i] & 0xFFFFu);
+            if (u >= x1) break;
+            int k = u + shift;
+            if (k >= n) k -= n;
+            const int s = k - row0;
+            const size_t o = (size_t)j * nw + (s >> 5);
+            const uint32_t bit = 1u << (s & 31);
+            atomicOr(lev + (size_t)(w - 1) * plane + o, bit);
+            if (w == 1) atomicOr(R + o, bit);
+        }
+    }
+}
+
 /* ---- N > 1: the first batch's in-arcs streamed weight by weight ----------------------------- *
- * Level d reads the arcs of weight <= d only, so the segments travel one weight at a time on a
- * second stream and level d waits for weight d alone: the wire of weight d + 1 runs under level
- * d's gathers. On the wire the arcs of one weight are rank-major, target-major within (offw: the
+ * Level d reads its peers' arcs of weight < d only (an arc of weight d matters to its own source
+ * alone), so the segments travel one weight at a time on a second stream and level d waits for
+ * weight d - 1 alone: the wire of weight d runs under level d's gathers. On the wire the arcs of one weight are rank-major, target-major within (offw: the
  * exclusive scan of the counts in [weight][target] order), one u32 per arc -- its source and its
  * index into the union table of distinct reliabilities (or the source alone, with the f64 beside
  * it when the union passes the table) -- and each receiver places them into its (target,
@@ -732,8 +791,44 @@ static int lvl_side_stream(hipStream_t* cs, hipEvent_t** ev) {
     *ev = g_lvl_ev[k];
     return SRT_OK;
 }
-/* host staging of the union table and the wire offsets, per slot (alive until the build syncs) */
-static std::vector<unsigned long long> g_lvl_hbuf[SRT_STATE_SLOTS];
+/* The build's host round trips (the exchange, the agreement, one vote per batch) go through
+ * pinned staging, per slot, made once and grown when a larger exchange needs it: a copy to or
+ * from pageable memory is staged by the runtime and blocks the calling thread. Layout (u64
+ * words): the one-GPU histogram, the agreement and failure flag, the vote's read-back, then the
+ * exchange, the union table and the wire's per-weight bases. */
+#define LVL_PIN_HIST 0
+#define LVL_PIN_AG LVL_STRIDE
+#define LVL_PIN_HW (LVL_PIN_AG + 4)
+#define LVL_PIN_X (LVL_PIN_HW + LVL_H_WORDS - LVL_H_INC)
+static unsigned long long* g_lvl_pin[SRT_STATE_SLOTS];
+static size_t g_lvl_pin_words[SRT_STATE_SLOTS];
+static hipEvent_t g_lvl_wev[SRT_STATE_SLOTS];
+static int lvl_pinned(size_t words, unsigned long long** p) {
+    const int k = srt_state_slot();
+    if (g_lvl_pin_words[k] < words) {
+        if (g_lvl_pin[k]) SRT_HIPCHK(hipHostFree(g_lvl_pin[k]));
+        g_lvl_pin[k] = NULL;
+        g_lvl_pin_words[k] = 0;
+        SRT_HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&g_lvl_pin[k]), words * sizeof(unsigned long long),
+                                 hipHostMallocDefault));
+        g_lvl_pin_words[k] = words;
+    }
+    *p = g_lvl_pin[k];
+    return SRT_OK;
+}
+/* Wait for the stream with the calling thread spinning on an event. hipStreamSynchronize sleeps
+ * on the completion interrupt past a short active window, and the wake-up cost 30-60 us per round
+ * trip in the traces of one rank of N = 8 (three or four per build). */
+static int lvl_wait(hipStream_t st) {
+    hipEvent_t& e = g_lvl_wev[srt_state_slot()];
+    if (!e) SRT_HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    SRT_HIPCHK(hipEventRecord(e, st));
+    hipError_t r;
+    while ((r = hipEventQuery(e)) == hipErrorNotReady) {
+    }
+    SRT_HIPCHK(r);
+    return SRT_OK;
+}
 
 /* byte offset of each arc's source row inside a level plane (k * nw * 4; nw is this rank's) */
 __global__ void lvl_aoff_kernel(int total, int nw, const uint32_t* __restrict__ arcs,
@@ -790,8 +885,8 @@ __global__ __launch_bounds__(256) void lvl_first_kernel(int n, int nw, int src0,
 /* Level d: one wave per (target j, 64-word source chunk c). Units are handed out XCD-major (each
  * XCD takes a contiguous run of chunk-major units), so an XCD works on one source chunk at a time
  * and the Delta rows of that chunk are the only gathered data in its L2. */
-static __device__ __forceinline__ uint32_t lvl_step_unit(unsigned g, int d, int n, int nw, int nchunk,
-                                                     int src0, int nsrc,
+static __device__ __forceinline__ uint32_t lvl_step_unit(unsigned g, int d, int direct, int n, int nw,
+                                                       int nchunk, int src0, int nsrc,
                                                        const int32_t* __restrict__ off,
                                                        const uint32_t* __restrict__ arcs,
                                                        const uint32_t* __restrict__ aoff,
@@ -817,8 +912,11 @@ static __device__ __forceinline__ uint32_t lvl_step_unit(unsigned g, int d, int 
     uint32_t acc = 0;
     const int32_t* oj = off + (size_t)j * LVL_STRIDE;
     /* arcs of weight d: the path (k, j) itself, Delta_0[k] = {k}; 64 arcs per step, one per lane,
-     * and the few whose source lies in this unit's chunk go to the lane owning its word */
-    {
+     * and the few whose source lies in this unit's chunk go to the lane owning its word (direct:
+     * lvl_direct_kernel left them in the plane) */
+    if (direct) {
+        if (valid) acc = *out;
+    } else {
         const int a0 = oj[d], a1 = oj[d + 1], cw0 = c * 64 * 32;
         for (int i0 = a0; i0 < a1; i0 += 64) {
             const int i = i0 + lane;
@@ -884,7 +982,7 @@ static __device__ __forceinline__ uint32_t lvl_step_unit(unsigned g, int d, int 
  * few microseconds, so a one-shot grid of 131k workgroups was bound by workgroup dispatch. Block p
  * of XCD p % 8 takes that XCD's contiguous run of unit blocks (chunk-major): 0.69 ms per C4 level
  * against 0.80 when all XCDs walk the same chunk together (lvl_pred_kernel's order). */
-__global__ __launch_bounds__(256) void lvl_step_kernel(int d, int n, int nw, int nchunk, int src0,
+__global__ __launch_bounds__(256) void lvl_step_kernel(int d, int direct, int n, int nw, int nchunk, int src0,
                                                        int nsrc, unsigned nblk,
                                                        const int32_t* __restrict__ off,
                                                        const uint32_t* __restrict__ arcs,
@@ -901,7 +999,7 @@ __global__ __launch_bounds__(256) void lvl_step_kernel(int d, int n, int nw, int
     const unsigned x = blockIdx.x & 7u, per = nblk >> 3, L = gridDim.x >> 3;
     uint32_t settled = 0; /* pairs this lane settled (one add per block at the end) */
     for (unsigned u = blockIdx.x >> 3; u < per; u += L)
-        settled += lvl_step_unit(x * per + u, d, n, nw, nchunk, src0, nsrc, off, arcs, aoff, lev, R,
+        settled += lvl_step_unit(x * per + u, d, direct, n, nw, nchunk, src0, nsrc, off, arcs, aoff, lev, R,
                                  done, incomplete);
     unsigned long long c = settled;
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
@@ -1280,13 +1378,20 @@ __global__ void lvl_sum_kernel(const unsigned long long* __restrict__ v, int k,
 
 /* Estimated time of levels 1..L (ms): every level gathers one 4-B word per (arc of weight < d,
  * source word) and reads/writes R and Delta once. */
-static double lvl_estimate(const unsigned long long* hist, int L, double ntgt, double nw) {
+/* the largest level budget L whose predicted time stays within limit_ms: level d gathers a row of
+ * nw words per arc of weight < d and touches three planes (one running sum, not a sum per L: the
+ * budget of a graph like C4 passes 200 levels, and the quadratic form cost ~30 us of host time
+ * on every build's critical path) */
+static int lvl_budget(const unsigned long long* hist, double ntgt, double nw, double limit_ms) {
     double t = 0, below = 0; /* arcs with weight < d */
-    for (int d = 1; d <= L; ++d) {
+    int L = 0;
+    for (int d = 1; d <= LVL_WMAX; ++d) {
         if (d >= 2) below += (double)hist[d - 1];
         t += (below * nw * 4.0 + ntgt * nw * 4.0 * 3.0) / LVL_BYTES_PER_MS + LVL_LEVEL_MS;
+        if (t > limit_ms) break;
+        L = d;
     }
-    return t;
+    return L;
 }
 
 /* persistent grid of a 256-thread unit kernel: its resident workgroups per CU x the CUs, a multiple
@@ -1596,20 +1701,25 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         }
     }
     int rc;
-    std::vector<unsigned long long>& hb = g_lvl_hbuf[srt_state_slot()];
-    hb.assign(R > 1 ? (xn + 1) / 2 + LVL_RT_CAP + 2 * LVL_BATCH + 4 : 4, 0ull);
-    int32_t* hx = reinterpret_cast<int32_t*>(hb.data()); /* the exchange, back on the host */
-    unsigned long long* ht = hb.data() + (xn + 1) / 2;   /* the union table, then its flags */
+    unsigned long long* pin;
+    if ((rc = lvl_pinned(LVL_PIN_X + (R > 1 ? (xn + 1) / 2 + LVL_RT_CAP + 2 * LVL_BATCH + 4 : 4), &pin)))
+        return rc;
+    int32_t* hx = reinterpret_cast<int32_t*>(pin + LVL_PIN_X); /* the exchange, back on the host */
+    unsigned long long* ht = pin + LVL_PIN_X + (xn + 1) / 2;    /* the union table, then its flags */
     int32_t* hwt = reinterpret_cast<int32_t*>(ht + LVL_RT_CAP + 2); /* the wire's per-weight base, block */
+    int32_t* hag = reinterpret_cast<int32_t*>(pin + LVL_PIN_AG);    /* the agreement, the failure flag */
     int failed = !ok;
     if (R > 1) {
-        SRT_HIPCHK(hipMemcpyAsync(xlimbs + 2 * LVL_STRIDE, &failed, sizeof(int32_t), hipMemcpyHostToDevice, st));
+        hag[3] = failed;
+        SRT_HIPCHK(hipMemcpyAsync(xlimbs + 2 * LVL_STRIDE, &hag[3], sizeof(int32_t), hipMemcpyHostToDevice, st));
         if ((rc = srt_coll_allreduce_i32(comm, xbuf, xn, 0, st))) return rc;
         SRT_HIPCHK(hipMemcpyAsync(hx, xbuf, xn * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     }
     unsigned long long hist[LVL_STRIDE];
-    if (R == 1) SRT_HIPCHK(hipMemcpyAsync(hist, dhist, sizeof(hist), hipMemcpyDeviceToHost, st));
-    SRT_HIPCHK(hipStreamSynchronize(st));
+    if (R == 1)
+        SRT_HIPCHK(hipMemcpyAsync(pin + LVL_PIN_HIST, dhist, sizeof(hist), hipMemcpyDeviceToHost, st));
+    if ((rc = lvl_wait(st))) return rc;
+    if (R == 1) memcpy(hist, pin + LVL_PIN_HIST, sizeof(hist));
     if (R > 1) { /* the summed histogram from its limbs, on the host (one read-back) */
         failed = hx[2 * LVL_STRIDE];
         for (int i = 0; i < LVL_STRIDE; i++)
@@ -1637,11 +1747,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     /* level budget from global quantities (the summed histogram, the largest shard's words): the
      * largest L whose predicted time stays under half the FW time */
     const double nw_all = (double)max_rows / 32.0;
-    int lmax = 0;
-    for (int x = 1; x <= LVL_WMAX; ++x) {
-        if (lvl_estimate(hist, x, (double)n, nw_all) > 0.5 * fw_ms) break;
-        lmax = x;
-    }
+    int lmax = lvl_budget(hist, (double)n, nw_all, 0.5 * fw_ms);
     /* and by memory: the planes (lmax x n x nw words) within half of what the device has left */
     const size_t plane = (size_t)n * nw;
     if (plane > 0) {
@@ -1731,15 +1837,17 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         commit(a3, &sok);
         stream_ok = sok;
     }
-    int ag[3] = {lmax, ok, stream_ok};
     if (R > 1) {
-        SRT_HIPCHK(hipMemcpyAsync(dagree, ag, sizeof(ag), hipMemcpyHostToDevice, st));
+        hag[0] = lmax;
+        hag[1] = ok;
+        hag[2] = stream_ok;
+        SRT_HIPCHK(hipMemcpyAsync(dagree, hag, 3 * sizeof(int32_t), hipMemcpyHostToDevice, st));
         if ((rc = srt_coll_allreduce_i32(comm, dagree, 3, 1, st))) return rc;
-        SRT_HIPCHK(hipMemcpyAsync(ag, dagree, sizeof(ag), hipMemcpyDeviceToHost, st));
-        SRT_HIPCHK(hipStreamSynchronize(st));
-        lmax = ag[0];
-        ok = ag[1];
-        stream_ok = ag[2];
+        SRT_HIPCHK(hipMemcpyAsync(hag, dagree, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        if ((rc = lvl_wait(st))) return rc;
+        lmax = hag[0];
+        ok = hag[1];
+        stream_ok = hag[2];
     }
     /* From here every branch reads agreed or global values only: hist is summed over the ranks
      * (hist[0] is the stash-overflow count), the budget, the allocation outcome and the wire are
@@ -1810,7 +1918,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
                 SRT_HIPCHK(hipMemcpyAsync(&hoff[q], off + (size_t)b * LVL_STRIDE, sizeof(int32_t),
                                           hipMemcpyDeviceToHost, st));
             }
-            SRT_HIPCHK(hipStreamSynchronize(st));
+            if ((rc_ = lvl_wait(st))) return rc_;
             /* Numbered segments: the packed post pass needs each arc's index into the table of
              * distinct reliabilities, not its f64. Each rank numbers its own segment's values
              * (hash + compact), the blocks are all-gathered (16 KB per rank), every rank takes
@@ -1839,7 +1947,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
                 std::vector<unsigned long long> hg((size_t)R * LVL_GB);
                 SRT_HIPCHK(hipMemcpyAsync(hg.data(), gat, hg.size() * sizeof(unsigned long long),
                                           hipMemcpyDeviceToHost, st));
-                SRT_HIPCHK(hipStreamSynchronize(st));
+                if ((rc_ = lvl_wait(st))) return rc_;
                 std::vector<unsigned long long> u;
                 bool fit = true;
                 for (int q = 0; q < R && fit; q++) {
@@ -1864,7 +1972,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
                             nb1 - nb0, arA + nb0, reinterpret_cast<const unsigned long long*>(rtab), nu,
                             rix + nb0);
                     SRT_HIPCHK(hipGetLastError());
-                    SRT_HIPCHK(hipStreamSynchronize(st)); /* hf and u leave scope */
+                    if ((rc_ = lvl_wait(st))) return rc_; /* hf and u leave scope */
                     numbered = 1;
                 }
             }
@@ -1920,7 +2028,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     int streamed = 0;       /* the weights the streamed extraction delivers on the side stream */
     int wnum = 0;           /* its arcs carry table indices (else their f64s travel beside) */
     /* N > 1, the first extraction: the arcs of weight <= lw streamed weight by weight on the side
-     * stream (the kernels above); level d then waits for ev[d] only. Taken when the fill is the
+     * stream (the kernels above); level d then waits for ev[d - 1] only. Taken when the fill is the
      * ordered stash (sorted_w) and the reliabilities can be numbered; otherwise extract(). One
      * host round trip: the gathered reliability blocks and the wire offsets come back together. */
     auto extract_streamed = [&](int lw) -> int {
@@ -1975,6 +2083,15 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         SRT_HIPCHK(hipGetLastError());
         SRT_HIPCHK(hipEventRecord(wev[0], st));
         SRT_HIPCHK(hipStreamWaitEvent(wcs, wev[0], 0));
+        /* while weight 1 travels: the own sources' arcs into their planes */
+        SRT_HIPCHK(hipMemsetAsync(lev, 0, (size_t)lw * plane * sizeof(uint32_t), st));
+        if (solo && lrows > 0)
+            lvl_solo_direct_kernel<<<srt_ceil_div(n * lw, 256), 256, 0, st>>>(n, row0, nrows, lrows, nw, lw, plane,
+                                                                             off, arcsA, lev, Rb);
+        else if (!solo && lrows > 0)
+            lvl_direct_kernel<<<srt_ceil_div(lrows, 4), 256, 0, st>>>(row0, row0 + lrows, nw, lw, plane, off,
+                                                                     arcsA, lev, Rb);
+        SRT_HIPCHK(hipGetLastError());
         wnum = 1;
         arcs = arcsA;
         ar = arA;
@@ -1987,18 +2104,28 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
      * before level w, so the host's calls for weight w + 1 overlap the levels on the GPU. */
     auto stream_weight = [&](int w) -> int {
         const size_t base = (size_t)hwt[2 * (w - 1)], mx = (size_t)hwt[2 * (w - 1) + 1];
-        const int32_t* dsz = packed;
-        const int32_t* dwt = dsz + (size_t)streamed * (R + 1);
         int rc_ = srt_coll_allgather(comm, wire + base, mx * sizeof(uint32_t), wcs);
         if (rc_) return rc_;
-        if (solo && lrows > 0)
-            lvl_solo_arcs_kernel<<<srt_ceil_div(n, 4), 256, 0, wcs>>>(n, row0, nrows, lrows, w, w, nw, off, arcs,
-                                                                      wnum ? rix : NULL, wnum ? NULL : ar, aoff);
-        else if (!solo)
-            lvl_wire_unpack_kernel<<<srt_ceil_div(n, 4), 256, 0, wcs>>>(n, ld, row0, nrows, w, nw, R, off, offw,
-                                                                        dsz, dwt, wire, NULL, arcs, rix, ar, aoff);
-        SRT_HIPCHK(hipGetLastError());
         SRT_HIPCHK(hipEventRecord(wev[w], wcs));
+        return SRT_OK;
+    };
+    /* Weight w's placement, on the main stream between two levels: the all-gather finished under
+     * the previous level, and the whole GPU places the arcs in ~12 us. On the side stream the
+     * placement got only the CUs the persistent level grid left free and ended with the level
+     * it ran beside (72-135 us per weight on one rank of N = 8), and the last weight's all-gather
+     * queued behind it. */
+    int wp = 0; /* the streamed weights placed so far */
+    auto place_weight = [&](int w) -> int {
+        const int32_t* dsz = packed;
+        const int32_t* dwt = dsz + (size_t)streamed * (R + 1);
+        SRT_HIPCHK(hipStreamWaitEvent(st, wev[w], 0));
+        if (solo && lrows > 0)
+            lvl_solo_arcs_kernel<<<srt_ceil_div(n, 4), 256, 0, st>>>(n, row0, nrows, lrows, w, w, nw, off, arcs,
+                                                                     wnum ? rix : NULL, wnum ? NULL : ar, aoff);
+        else if (!solo)
+            lvl_wire_unpack_kernel<<<srt_ceil_div(n, 4), 256, 0, st>>>(n, ld, row0, nrows, w, nw, R, off, offw,
+                                                                       dsz, dwt, wire, NULL, arcs, rix, ar, aoff);
+        SRT_HIPCHK(hipGetLastError());
         return SRT_OK;
     };
     SRT_HIPCHK(hipMemsetAsync(Rb, 0, plane * sizeof(uint32_t), st));
@@ -2010,7 +2137,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     nblk = (nblk + 7u) & ~7u;
     /* while the streamed arcs are still arriving, one CU per XCD stays free for the broadcast
      * (RCCL's kernels, the unpack) beside the persistent level grid */
-    const unsigned pgrid = lvl_grid((const void*)lvl_step_kernel, nblk, streamed ? 8 : 0);
+    const unsigned pgrid = lvl_grid((const void*)lvl_step_kernel, nblk, streamed ? srt_form_int("wcu", 8) : 0);
     /* the levels in batches of LVL_BATCH, one host round trip per batch. After the first batch
      * the settled fraction decides whether the rest is worth it: a graph with far-apart vertices
      * (metric latencies, C4metric: 0.2% settled after 8 levels, distances of hundreds of quanta)
@@ -2035,22 +2162,33 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
             while (wq < min(streamed, min(d + 1, d1)))
                 if ((rc = stream_weight(++wq))) return rc;
             if (D && d > D) continue; /* this rank's sources are settled: nothing to run */
-            if (d <= streamed) SRT_HIPCHK(hipStreamWaitEvent(st, wev[d], 0)); /* weight d alone */
+            /* Level d reads the arcs of weight < d only: an arc of weight d counts for its own
+             * source alone (Delta_0), and lvl_direct_kernel put those into the planes from this
+             * rank's rows. So level d waits for weight d - 1, and level 1 for nothing. */
+            while (wp < min(d - 1, wq))
+                if ((rc = place_weight(++wp))) return rc;
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
             if (d == 1) { /* the weight-1 arcs as bits; level 2 takes up the completion flags
-                           * (dinc[1] stays set: a graph settled at level 1 reports 2 levels) */
-                SRT_HIPCHK(hipMemsetAsync(lev, 0, plane * sizeof(uint32_t), st));
+                           * (dinc[1] stays set: a graph settled at level 1 reports 2 levels).
+                           * Streamed: lvl_direct_kernel has set them. */
                 SRT_HIPCHK(hipMemsetAsync(dinc + 1, 0xFF, sizeof(int), st));
-                lvl_first_kernel<<<srt_ceil_div(n, 4), 256, 0, st>>>(n, nw, row0, nrows, off, arcs,
-                                                                      lev, Rb);
+                if (!streamed) {
+                    SRT_HIPCHK(hipMemsetAsync(lev, 0, plane * sizeof(uint32_t), st));
+                    lvl_first_kernel<<<srt_ceil_div(n, 4), 256, 0, st>>>(n, nw, row0, nrows, off, arcs,
+                                                                          lev, Rb);
+                }
             } else {
-                lvl_step_kernel<<<pgrid, 256, 0, st>>>(d, n, nw, nchunk, row0, nrows, nblk, off,
+                lvl_step_kernel<<<pgrid, 256, 0, st>>>(d, d <= streamed, n, nw, nchunk, row0, nrows, nblk, off,
                                                       arcs, aoff, lev, Rb, done, dinc + d,
                                                       dinc + d - 1, nset);
             }
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
         }
         SRT_HIPCHK(hipGetLastError());
+        /* the batch's weights in place before anything after its levels (the post pass reads
+         * every arc up to the last level) */
+        while (wp < wq)
+            if ((rc = place_weight(++wp))) return rc;
         if (R > 1) {
             lvl_vote_kernel<<<1, 64, 0, st>>>(dinc + d1, nset, dvote);
             SRT_HIPCHK(hipGetLastError());
@@ -2058,9 +2196,10 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         }
         /* one read-back: the completion flags, the table flags, the settled pairs and the vote
          * are neighbours in the host-side words (four copies cost ~20 us each of round trip) */
-        unsigned long long hw[LVL_H_WORDS - LVL_H_INC];
-        SRT_HIPCHK(hipMemcpyAsync(hw, dhist + LVL_H_INC, sizeof(hw), hipMemcpyDeviceToHost, st));
-        SRT_HIPCHK(hipStreamSynchronize(st));
+        unsigned long long* const hw = pin + LVL_PIN_HW;
+        SRT_HIPCHK(hipMemcpyAsync(hw, dhist + LVL_H_INC, (LVL_H_WORDS - LVL_H_INC) * sizeof(unsigned long long),
+                                  hipMemcpyDeviceToHost, st));
+        if ((rc = lvl_wait(st))) return rc;
         const int* hinc = reinterpret_cast<const int*>(hw);
         const int32_t* vote = reinterpret_cast<const int32_t*>(hw + (LVL_H_VOTE - LVL_H_INC));
         unsigned long long settled = hw[LVL_H_AGREE + 2 - LVL_H_INC];
@@ -2088,7 +2227,8 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         if (d1 == lx && lx < lmax) { /* the heavier arcs: their counts, then every arc up to lmax */
             while (wq < streamed) /* (the first extraction's last weights, for the collectives) */
                 if ((rc = stream_weight(++wq))) return rc;
-            if (wq) SRT_HIPCHK(hipStreamWaitEvent(st, wev[wq], 0)); /* its writes come first */
+            while (wp < wq) /* its writes come first */
+                if ((rc = place_weight(++wp))) return rc;
             if ((rc = share_counts(lx + 1, lmax)) || (rc = extract(lmax))) return rc;
         }
     }
