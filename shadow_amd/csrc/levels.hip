@@ -2137,7 +2137,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     nblk = (nblk + 7u) & ~7u;
     /* while the streamed arcs are still arriving, one CU per XCD stays free for the broadcast
      * (RCCL's kernels, the unpack) beside the persistent level grid */
-    const unsigned pgrid = lvl_grid((const void*)lvl_step_kernel, nblk, streamed ? srt_form_int("wcu", 8) : 0);
+    const unsigned pgrid = lvl_grid((const void*)lvl_step_kernel, nblk, streamed ? 8 : 0);
     /* the levels in batches of LVL_BATCH, one host round trip per batch. After the first batch
      * the settled fraction decides whether the rest is worth it: a graph with far-apart vertices
      * (metric latencies, C4metric: 0.2% settled after 8 levels, distances of hundreds of quanta)
