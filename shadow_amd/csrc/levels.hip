@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) void lvl_arcs_cols_kernel(int n, int ld,
 
 /* weight histogram over the count rows (for the level budget) */
 __global__ void lvl_hist_kernel(size_t count, const int32_t* __restrict__ cnt,
-                                unsigned long long* __restrict__ hist) {
+                                unsigned long long* __restrict__ hist, unsigned mult = 1) {
     __shared__ unsigned long long s[LVL_STRIDE];
     for (int i = threadIdx.x; i < LVL_STRIDE; i += blockDim.x) s[i] = 0;
     __syncthreads();
@@ -269,7 +269,7 @@ __global__ void lvl_hist_kernel(size_t count, const int32_t* __restrict__ cnt,
         if (cnt[i]) atomicAdd(&s[i % LVL_STRIDE], (unsigned long long)cnt[i]);
     __syncthreads();
     for (int i = threadIdx.x; i < LVL_STRIDE; i += blockDim.x)
-        if (s[i]) atomicAdd(&hist[i], s[i]);
+        if (s[i]) atomicAdd(&hist[i], s[i] * mult);
 }
 
 /* N > 1: the histogram all-reduced in 20-bit limbs (int32 sums of R ranks cannot overflow), then
@@ -1674,10 +1674,13 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
                                                                NULL, NULL, dkey, stash, scnt, dhist);
         if (solo && lrows > 0) lvl_solo_counts_kernel<<<n, 256, 0, st>>>(n, row0, nrows, lrows, cnt);
         SRT_HIPCHK(hipGetLastError());
-        /* this rank's rows (a solo rank: every row of its synthesised counts) */
-        const bool own = R > 1 && !solo;
-        lvl_hist_kernel<<<own ? 256 : 1024, 256, 0, st>>>(own ? (size_t)nrows * LVL_STRIDE : ncnt,
-                                                         own ? cnt + (size_t)row0 * LVL_STRIDE : cnt, dhist);
+        /* this rank's rows (a solo rank: every row of its synthesised counts, which are its own
+         * rows' n / lrows times over when that divides) */
+        const bool rep = solo && lrows > 0 && lrows == nrows && n % lrows == 0;
+        const bool own = R > 1 && (!solo || rep);
+        lvl_hist_kernel<<<own ? 256 : 1024, 256, 0, st>>>(own ? (size_t)(rep ? lrows : nrows) * LVL_STRIDE : ncnt,
+                                                         own ? cnt + (size_t)row0 * LVL_STRIDE : cnt, dhist,
+                                                         rep ? (unsigned)(n / lrows) : 1u);
         SRT_HIPCHK(hipGetLastError());
         if (R > 1) {
             SRT_HIPCHK(hipMemsetAsync(xbuf, 0, xn * sizeof(int32_t), st));
@@ -1837,6 +1840,51 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         commit(a3, &sok);
         stream_ok = sok;
     }
+    /* N > 1: what needs no agreed value is done on the side stream while the main stream
+     * carries the agreement and the count all-gather (on the main stream it delayed them): the
+     * level state's zeroing and, for the streamed extraction, the union table and the wire's
+     * per-weight bases, sized by this rank's budget (lx_own >= the agreed lx; the entries of the
+     * weights up to lx are the same either way). The main stream waits for it (wev[prep]) before
+     * the extraction; wasted when a rank falls back. */
+    hipEvent_t* wev = NULL; /* wev[w]: the arcs of weight w are in place on this rank */
+    hipStream_t wcs = NULL; /* the side stream */
+    const int prep = LVL_BATCH + 1;
+    bool prepped = false;
+    if (R > 1 && ok && Rb && done) { /* (not allocated under a budget below 2) */
+        if ((rc = lvl_side_stream(&wcs, &wev))) return rc;
+        SRT_HIPCHK(hipEventRecord(wev[prep], st)); /* the allocations are ordered on st */
+        SRT_HIPCHK(hipStreamWaitEvent(wcs, wev[prep], 0));
+        prepped = true;
+        SRT_HIPCHK(hipMemsetAsync(Rb, 0, plane * sizeof(uint32_t), wcs));
+        SRT_HIPCHK(hipMemsetAsync(done, 0, (size_t)n * nchunk, wcs));
+        lvl_init_kernel<<<srt_ceil_div(nrows, 256), 256, 0, wcs>>>(n, row0, nrows, nw, Rb);
+        SRT_HIPCHK(hipGetLastError());
+    }
+    if (prepped && stream_ok && lev && rtab) {
+        SRT_HIPCHK(hipMemsetAsync(lev, 0, (size_t)lx_own * plane * sizeof(uint32_t), wcs));
+        const int nu = (int)u.size();
+        memcpy(ht, u.data(), u.size() * sizeof(unsigned long long));
+        const int hf[2] = {0, nu};
+        memcpy(ht + LVL_RT_CAP, hf, sizeof(hf));
+        SRT_HIPCHK(hipMemcpyAsync(rtab, ht, (size_t)nu * sizeof(double), hipMemcpyHostToDevice, wcs));
+        SRT_HIPCHK(hipMemcpyAsync(dflag, ht + LVL_RT_CAP, 2 * sizeof(int), hipMemcpyHostToDevice, wcs));
+        /* the wire: per weight every rank's block padded to the largest rank's arcs (from the
+         * exchange's per-rank counts): the weight's base and that block size */
+        size_t base = 0;
+        for (int w = 1; w <= lx_own; ++w) {
+            int mx = 0;
+            for (int q = 0; q < R; q++) {
+                const int32_t* c = hx + LVL_X_LIMBS + (size_t)q * LVL_X_CNT + (w - 1) * 2;
+                mx = max(mx, (int)((uint32_t)c[0] | ((uint32_t)c[1] << 16)));
+            }
+            hwt[2 * (w - 1)] = (int32_t)base;
+            hwt[2 * (w - 1) + 1] = mx;
+            base += (size_t)R * mx;
+        }
+        SRT_HIPCHK(hipMemcpyAsync(packed + LVL_BATCH * 65, hwt, 2 * (size_t)lx_own * sizeof(int32_t),
+                                  hipMemcpyHostToDevice, wcs));
+    }
+    if (prepped) SRT_HIPCHK(hipEventRecord(wev[prep], wcs));
     if (R > 1) {
         hag[0] = lmax;
         hag[1] = ok;
@@ -2023,8 +2071,6 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         }
         return 0;
     };
-    hipEvent_t* wev = NULL; /* wev[w]: the arcs of weight w are in place on this rank */
-    hipStream_t wcs = NULL; /* the side stream */
     int streamed = 0;       /* the weights the streamed extraction delivers on the side stream */
     int wnum = 0;           /* its arcs carry table indices (else their f64s travel beside) */
     /* N > 1, the first extraction: the arcs of weight <= lw streamed weight by weight on the side
@@ -2035,8 +2081,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         int64_t t64 = 0;
         for (int x = 1; x <= lw; ++x) t64 += (int64_t)hist[x];
         total_x = (int32_t)t64;
-        int rc_ = lvl_side_stream(&wcs, &wev);
-        if (rc_) return rc_;
+        int rc_;
         /* offsets over the arcs with w <= lw, (target, weight)-major, and the own rows' arcs */
         if ((rc_ = offsets(lw))) return rc_;
         lvl_arcs_rows_kernel<true><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, NULL, lw, off, arcsA,
@@ -2044,47 +2089,29 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         const int32_t* lo = off + (size_t)row0 * LVL_STRIDE;
         const int32_t* hi = off + (size_t)(row0 + nrows) * LVL_STRIDE;
         lvl_aoff_range_kernel<<<512, 256, 0, st>>>(lo, hi, nw, arcsA, aoff);
-        /* the union table (from the exchange): each own arc's index by binary search */
+        /* each own arc's index into the union table (on the device since the agreement) */
         const int nu = (int)u.size();
-        memcpy(ht, u.data(), u.size() * sizeof(unsigned long long));
-        const int hf[2] = {0, nu};
-        memcpy(ht + LVL_RT_CAP, hf, sizeof(hf));
-        SRT_HIPCHK(hipMemcpyAsync(rtab, ht, (size_t)nu * sizeof(double), hipMemcpyHostToDevice, st));
-        SRT_HIPCHK(hipMemcpyAsync(dflag, ht + LVL_RT_CAP, 2 * sizeof(int), hipMemcpyHostToDevice, st));
         lvl_rt_index_range_kernel<<<512, 256, 0, st>>>(lo, hi, arA, reinterpret_cast<const unsigned long long*>(rtab),
                                                        nu, rix);
-        /* the wire: per weight every rank's block padded to the largest rank's arcs (from the
-         * exchange's per-rank counts), a rank's arcs inside its block in target order (offw: the
-         * [weight][target] scan, zw its values at the shard starts) */
-        size_t base = 0;
-        for (int w = 1; w <= lw; ++w) {
-            int mx = 0;
-            for (int q = 0; q < R; q++) {
-                const int32_t* c = hx + LVL_X_LIMBS + (size_t)q * LVL_X_CNT + (w - 1) * 2;
-                mx = max(mx, (int)((uint32_t)c[0] | ((uint32_t)c[1] << 16)));
-            }
-            hwt[2 * (w - 1)] = (int32_t)base;
-            hwt[2 * (w - 1) + 1] = mx;
-            base += (size_t)R * mx;
-        }
+        /* offw: the [weight][target] scan of every target's counts (gathered), dsz its values at
+         * the shard starts; the wire's per-weight bases are on the device since the agreement */
         const size_t nwo = (size_t)lw * ld + 1;
         lvl_wcols_kernel<<<srt_ceil_div((int64_t)nwo, 256), 256, 0, st>>>(ld, lw, cnt,
                                                                        reinterpret_cast<int32_t*>(wire));
         SRT_HIPCHK(hipGetLastError());
         SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, reinterpret_cast<int32_t*>(wire), offw,
                                                     (int)nwo, st));
-        int32_t* dsz = packed; /* (free since the count exchange): offw at the shard starts, then wtab */
-        int32_t* dwt = dsz + (size_t)lw * (R + 1);
+        int32_t* const dsz = packed;
+        const int32_t* dwt = packed + LVL_BATCH * 65;
         lvl_wire_sizes_kernel<<<srt_ceil_div(lw * (R + 1), 256), 256, 0, st>>>(ld, lw, R, offw, dsz);
-        SRT_HIPCHK(hipMemcpyAsync(dwt, hwt, 2 * (size_t)lw * sizeof(int32_t), hipMemcpyHostToDevice, st));
         if (lrows > 0)
             lvl_wire_pack_kernel<<<srt_ceil_div(lrows, 4), 256, 0, st>>>(ld, row0, lrows, lw, R, me, off, offw, dsz,
                                                                         dwt, arcsA, rix, arA, wire, NULL);
         SRT_HIPCHK(hipGetLastError());
         SRT_HIPCHK(hipEventRecord(wev[0], st));
         SRT_HIPCHK(hipStreamWaitEvent(wcs, wev[0], 0));
-        /* while weight 1 travels: the own sources' arcs into their planes */
-        SRT_HIPCHK(hipMemsetAsync(lev, 0, (size_t)lw * plane * sizeof(uint32_t), st));
+        /* while weight 1 travels: the own sources' arcs into their planes (zeroed since the
+         * agreement) */
         if (solo && lrows > 0)
             lvl_solo_direct_kernel<<<srt_ceil_div(n * lw, 256), 256, 0, st>>>(n, row0, nrows, lrows, nw, lw, plane,
                                                                              off, arcsA, lev, Rb);
@@ -2117,7 +2144,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     int wp = 0; /* the streamed weights placed so far */
     auto place_weight = [&](int w) -> int {
         const int32_t* dsz = packed;
-        const int32_t* dwt = dsz + (size_t)streamed * (R + 1);
+        const int32_t* dwt = packed + LVL_BATCH * 65;
         SRT_HIPCHK(hipStreamWaitEvent(st, wev[w], 0));
         if (solo && lrows > 0)
             lvl_solo_arcs_kernel<<<srt_ceil_div(n, 4), 256, 0, st>>>(n, row0, nrows, lrows, w, w, nw, off, arcs,
@@ -2128,10 +2155,13 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         SRT_HIPCHK(hipGetLastError());
         return SRT_OK;
     };
-    SRT_HIPCHK(hipMemsetAsync(Rb, 0, plane * sizeof(uint32_t), st));
-    SRT_HIPCHK(hipMemsetAsync(done, 0, (size_t)n * nchunk, st));
-    lvl_init_kernel<<<srt_ceil_div(nrows, 256), 256, 0, st>>>(n, row0, nrows, nw, Rb);
-    SRT_HIPCHK(hipGetLastError());
+    if (R == 1) {
+        SRT_HIPCHK(hipMemsetAsync(Rb, 0, plane * sizeof(uint32_t), st));
+        SRT_HIPCHK(hipMemsetAsync(done, 0, (size_t)n * nchunk, st));
+        lvl_init_kernel<<<srt_ceil_div(nrows, 256), 256, 0, st>>>(n, row0, nrows, nw, Rb);
+        SRT_HIPCHK(hipGetLastError());
+    }
+    if (prepped) SRT_HIPCHK(hipStreamWaitEvent(st, wev[prep], 0));
     if ((rc = stream_ok ? extract_streamed(lx) : extract(lx))) return rc;
     unsigned nblk = (unsigned)(((n + 3) / 4) * nchunk);
     nblk = (nblk + 7u) & ~7u;
