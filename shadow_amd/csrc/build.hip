@@ -1293,7 +1293,7 @@ static int canon_from_edges(const srt_edges* g, srt_canon* c) {
  * device through the pinned ring (each chunk's minima scattered as it lands), the lowest-index
  * pass, then quanta / reliabilities in place */
 static int dense_scatter(const srt_canon* c, int ld, int row0, int nrows, uint32_t* dw, double* dr,
-                         hipStream_t st, int sharers) {
+                         hipStream_t st, int sharers, unsigned long long* arcs_out) {
     const srt_edges* g = c->edges;
     const int64_t m = g->m;
     const int64_t per = (int64_t)(STG_SLOT / 24);
@@ -1354,8 +1354,10 @@ static int dense_scatter(const srt_canon* c, int ld, int row0, int nrows, uint32
     TRY(srt_scatter_final(row0, nrows, ld, c->quantum_ns, eloss, dw, dr, darcs, st));
     TRYHIP(hipMemcpyAsync(&arcs, darcs, sizeof(arcs), hipMemcpyDeviceToHost, st));
     TRYHIP(hipStreamSynchronize(st));
+    if (arcs_out) *arcs_out = arcs;
     /* the auto choice took the dense build on an upper bound of the arcs: confirm it (one rank's
-     * rows suffice for the whole graph only when they are all of them) */
+     * rows suffice for the whole graph only when they are all of them; N ranks sum their counts,
+     * build_rank) */
     if (c->verify_dense && row0 == 0 && nrows >= c->n) {
         const double n = c->n;
         if (!(c->n <= 2048 || (double)arcs * 16.0 >= n * n)) rc = SRT_FALLBACK_CANON;
@@ -1372,9 +1374,9 @@ out:
 
 /* rows [row0, row0 + nrows) of the ld x ld matrices into dw / dr (row row0 at dw[0]) */
 static int dense_upload(const srt_canon* c, int ld, int row0, int nrows, uint32_t* dw, double* dr,
-                        hipStream_t st, int sharers) {
+                        hipStream_t st, int sharers, unsigned long long* arcs_out = NULL) {
     if (nrows <= 0) return SRT_OK;
-    if (!c->rowptr) return dense_scatter(c, ld, row0, nrows, dw, dr, st, sharers);
+    if (!c->rowptr) return dense_scatter(c, ld, row0, nrows, dw, dr, st, sharers, arcs_out);
     const size_t row_b = (size_t)ld * (sizeof(uint32_t) + sizeof(double));
     const int per = (int)(STG_SLOT / row_b);
     if (per < 1) {
@@ -1754,8 +1756,28 @@ static void* mjob_dense(void* p) {
     TRYHIP(hipMemsetAsync(dmin, 0xFF, sizeof(uint32_t), st));
     {
         const double t0 = host_ms();
-        TRY(dense_upload(j->c, j->ld, b, nr, dw, dr, st, j->R));
+        unsigned long long arcs = 0;
+        TRY(dense_upload(j->c, j->ld, b, nr, dw, dr, st, j->R, &arcs));
         j->st.ms_upload = host_ms() - t0;
+        /* the edge form's dense choice rests on an upper bound of the arcs (parallel edges count
+         * once per edge): the ranks sum their exact counts (three 24-bit limbs: an int32 sum of up
+         * to 64 ranks cannot overflow) and every rank takes the same verdict, falling back to the
+         * host canonical form together when the graph is not dense-shaped after all */
+        if (j->R > 1 && j->c->verify_dense && !j->c->rowptr) {
+            int32_t h[3] = {(int32_t)(arcs & 0xFFFFFF), (int32_t)((arcs >> 24) & 0xFFFFFF), (int32_t)(arcs >> 48)};
+            int32_t* dcount;
+            TRY(dalloc(&B, (void**)&dcount, sizeof(h)));
+            TRYHIP(hipMemcpyAsync(dcount, h, sizeof(h), hipMemcpyHostToDevice, st));
+            TRY(srt_coll_allreduce_i32(j->comm, dcount, 3, 0, st));
+            TRYHIP(hipMemcpyAsync(h, dcount, sizeof(h), hipMemcpyDeviceToHost, st));
+            TRYHIP(hipStreamSynchronize(st));
+            const double total = (double)h[0] + (double)h[1] * 16777216.0 + (double)h[2] * 281474976710656.0;
+            const double nn = (double)n * (double)n;
+            if (!(n <= 2048 || total * 16.0 >= nn)) {
+                rc = SRT_FALLBACK_CANON;
+                goto out;
+            }
+        }
     }
     TRY(srt_dense_build_sharded_ms(j->comm, n, j->ld, j->directed, dw, dr, dlat, drel, dms,
                                    j->c->quantum_ns, st, 0, &j->st));

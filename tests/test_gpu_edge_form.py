@@ -77,8 +77,11 @@ def test_edge_form_direct_mode_diagonal_and_ties(gpu):
     assert np.all(rel[i, i] > 0)  # the self-loops on the diagonal
 
 
-def test_edge_form_falls_back_when_arcs_are_few(gpu):
-    """edge count says dense, distinct arcs say sparse: the host canonical form decides"""
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_edge_form_falls_back_when_arcs_are_few(gpu, monkeypatch, ranks):
+    """edge count says dense, distinct arcs say sparse: the host canonical form decides. On 3
+    virtual ranks no rank holds every row, so the ranks sum their exact arc counts and fall back
+    together (before, a multi-rank build kept the dense FW path here)"""
     n = 3000
     ring = np.arange(n)
     rng = np.random.default_rng(3)
@@ -88,7 +91,9 @@ def test_edge_form_falls_back_when_arcs_are_few(gpu):
     dst = np.concatenate([(ring + 1) % n, (pick + 1) % n]).astype(np.int32)
     lat = (rng.integers(1, 30, len(src)) * MS).astype(np.int64)
     loss = rng.integers(0, 300, len(src)) / 10000.0
-    lat_ns, rel, st = build_tables(n, False, src, dst, lat, loss)
+    if ranks > 1:
+        monkeypatch.setenv("SRT_VIRTUAL_RANKS", str(ranks))
+    lat_ns, rel, st = build_tables(n, False, src, dst, lat, loss, ngpus=ranks if ranks > 1 else None)
     assert st.algo == ALGO_SPARSE_SSSP
     el = oracle.EdgeList(n, False, src, dst, lat, loss)
     rows = [0, 1500, n - 1]
