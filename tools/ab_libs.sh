@@ -1,5 +1,7 @@
 #!/bin/bash
-# A/B of side-by-side library builds (make ... OUT=../ab_<v>.so EXTRA=-D...) on the GPU box:
+# A/B of side-by-side library builds on the GPU box: each variant is a copy of shadow_amd/csrc
+# with the change applied (or an older commit's tree, git archive), built with
+# make OUT=<repo>/shadow_amd/ab_<v>.so (the product sources carry no variant macros):
 # per variant, the level parity tests, then a C4 bench line.
 # usage: bash tools/ab_libs.sh <tag> <workload> <variant> [<variant> ...]   (variant "default" or
 # the <v> of shadow_amd/ab_<v>.so); AB_TESTS overrides the parity tests run per variant

@@ -1,3 +1,7 @@
 set -o pipefail
 export TMPDIR=/tmp
-bash tools/run_round.sh r06w tfile:tests/test_gpu_edge_form.py tfile:tests/test_gpu_dropin.py
+O=gpurun_out/r06x
+mkdir -p $O
+bash tools/run_round.sh r06x tests && \
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 && \
+timeout -k 10 600 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err
