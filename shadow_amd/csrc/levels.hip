@@ -514,40 +514,29 @@ __global__ void lvl_direct_kernel(int j0, int j1, int nw, int lw, size_t plane, 
 }
 
 /* The solo rank's Delta_0 bits without synthesising its peers' segments first: peer target j's
- * segment of weight w is own row js's, every source moved by shift (lvl_solo_arcs_kernel), so its
- * own sources are the sources of row js in [row0 - shift, row0 - shift + nrows) (mod n), found by
- * binary search in the sorted run. One thread per (target, weight). */
+ * runs are own row js's, every source moved by shift (lvl_solo_arcs_kernel), so its own-source
+ * arcs are row js's arcs whose moved source falls in [row0, row0 + nrows). A wave per target, a
+ * lane per arc of weight <= lw (as lvl_direct_kernel; a binary search per (target, weight) ran
+ * 63 us on one rank of N = 8). */
 __global__ void lvl_solo_direct_kernel(int n, int row0, int nrows, int lrows, int nw, int lw, size_t plane,
                                        const int32_t* __restrict__ off, const uint32_t* __restrict__ arcs,
                                        uint32_t* __restrict__ lev, uint32_t* __restrict__ R) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    const int j = t / lw, w = t % lw + 1;
+    const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (j >= n) return;
     const bool own = j >= row0 && j < row0 + nrows;
     const int js = own ? j : row0 + ((j - row0) % lrows + lrows) % lrows;
     const int shift = own ? 0 : ((j - js) % n + n) % n;
-    const int a0 = off[(size_t)js * LVL_STRIDE + w], a1 = off[(size_t)js * LVL_STRIDE + w + 1];
-    const int lo = ((row0 - shift) % n + n) % n;
-    for (int part = 0; part < 2; ++part) { /* the range, split where it wraps past n */
-        const int x0 = part ? 0 : lo, x1 = part ? lo + nrows - n : min(n, lo + nrows);
-        if (x1 <= x0) continue;
-        int a = a0, b = a1;
-        while (a < b) {
-            const int m = (a + b) >> 1;
-            if ((int)(arcs[m] & 0xFFFFu) < x0) a = m + 1;
-            else b = m;
-        }
-        for (int i = a; i < a1; ++i) {
-            const int u = (int)(arcs[i] & 0xFFFFu);
-            if (u >= x1) break;
-            int k = u + shift;
-            if (k >= n) k -= n;
-            const int s = k - row0;
-            const size_t o = (size_t)j * nw + (s >> 5);
-            const uint32_t bit = 1u << (s & 31);
-            atomicOr(lev + (size_t)(w - 1) * plane + o, bit);
-            if (w == 1) atomicOr(R + o, bit);
-        }
+    const int a0 = off[(size_t)js * LVL_STRIDE + 1], a1 = off[(size_t)js * LVL_STRIDE + lw + 1];
+    for (int i = a0 + lane; i < a1; i += 64) {
+        const uint32_t e = arcs[i];
+        int k = (int)(e & 0xFFFFu) + shift;
+        if (k >= n) k -= n;
+        const int s = k - row0, w = (int)(e >> 16);
+        if (s < 0 || s >= nrows) continue;
+        const size_t o = (size_t)j * nw + (s >> 5);
+        const uint32_t bit = 1u << (s & 31);
+        atomicOr(lev + (size_t)(w - 1) * plane + o, bit);
+        if (w == 1) atomicOr(R + o, bit);
     }
 }
 
@@ -2113,8 +2102,8 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         /* while weight 1 travels: the own sources' arcs into their planes (zeroed since the
          * agreement) */
         if (solo && lrows > 0)
-            lvl_solo_direct_kernel<<<srt_ceil_div(n * lw, 256), 256, 0, st>>>(n, row0, nrows, lrows, nw, lw, plane,
-                                                                             off, arcsA, lev, Rb);
+            lvl_solo_direct_kernel<<<srt_ceil_div(n, 4), 256, 0, st>>>(n, row0, nrows, lrows, nw, lw, plane, off,
+                                                                       arcsA, lev, Rb);
         else if (!solo && lrows > 0)
             lvl_direct_kernel<<<srt_ceil_div(lrows, 4), 256, 0, st>>>(row0, row0 + lrows, nw, lw, plane, off,
                                                                      arcsA, lev, Rb);
