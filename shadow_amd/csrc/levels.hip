@@ -543,26 +543,12 @@ __global__ void lvl_solo_direct_kernel(int n, int row0, int nrows, int lrows, in
 /* ---- N > 1: the first batch's in-arcs streamed weight by weight ----------------------------- *
  * Level d reads its peers' arcs of weight < d only (an arc of weight d matters to its own source
  * alone), so the segments travel one weight at a time on a second stream and level d waits for
- * weight d - 1 alone: the wire of weight d runs under level d's gathers. On the wire the arcs of one weight are rank-major, target-major within (offw: the
- * exclusive scan of the counts in [weight][target] order), one u32 per arc -- its source and its
+ * weight d - 1 alone: the wire of weight d runs under level d's gathers. On the wire the arcs of
+ * one weight are rank-major, target-major within (offw: the exclusive scan of the counts in
+ * [weight][target] order, lvl_offsets_kernel), one u32 per arc -- its source and its
  * index into the union table of distinct reliabilities (or the source alone, with the f64 beside
  * it when the union passes the table) -- and each receiver places them into its (target,
  * weight)-major arcs (4 B per arc on the wire instead of 6). */
-__global__ void lvl_wcols_kernel(int ld, int lw, const int32_t* __restrict__ cnt, int32_t* __restrict__ cw) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x, tot = (size_t)lw * ld;
-    if (i > tot) return;
-    cw[i] = i == tot ? 0 : cnt[(i % ld) * LVL_STRIDE + i / ld + 1];
-}
-/* the wire offsets the host needs: offw at every shard start, per weight (q == R: the end) */
-__global__ void lvl_wire_sizes_kernel(int ld, int lw, int R, const int32_t* __restrict__ offw,
-                                      int32_t* __restrict__ sz) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= lw * (R + 1)) return;
-    const int w = i / (R + 1), q = i % (R + 1);
-    const long long nb = ld / SRT_SHARD_ALIGN;
-    const int b = q == R ? ld : (int)(nb * q / R) * SRT_SHARD_ALIGN; /* srt_shard_rows */
-    sz[i] = offw[(size_t)w * ld + b];
-}
 /* The wire of weight w: one block of maxc[w] u32 per rank (rank q's arcs of weight w, its targets
  * in order, then padding), all-gathered; wtab[2 (w - 1)] = the weight's base in the wire,
  * wtab[2 (w - 1) + 1] = maxc[w]; zw[(w - 1) (R + 1) + q] = offw at rank q's first target */
@@ -632,6 +618,120 @@ __global__ void lvl_off_kernel(int ld, int lw, const int32_t* __restrict__ cnt, 
         run += cnt[(size_t)j * LVL_STRIDE + w];
     }
     off[(size_t)j * LVL_STRIDE + lw + 1] = run;
+}
+
+/* The offsets of a first extraction (lw <= LVL_BATCH) in two launches: per target the (target,
+ * weight)-major starts off[j][0..lw + 1] and (offw != NULL, the streamed wire) the
+ * [weight][target] scan offw with its values at the shard starts (dsz). A workgroup takes 256
+ * targets, a thread one target. The first kernel sums each workgroup's columns (the target
+ * totals and the lw weights); the second adds the earlier workgroups' sums, scans its targets and
+ * writes. They replace seven launches (totals, two scans, offsets, columns, two scans, sizes).
+ * (One workgroup doing it all ran ~0.4 ms: one CU's latency on a rank's critical path.) */
+static __device__ __forceinline__ void lvl_off_cols(int ld, int lw, int j, const int32_t* __restrict__ cnt,
+                                                    int (&x)[LVL_BATCH + 1]) {
+    x[0] = 0;
+#pragma unroll
+    for (int w = 1; w <= LVL_BATCH; ++w) {
+        x[w] = j < ld && w <= lw ? cnt[(size_t)j * LVL_STRIDE + w] : 0;
+        x[0] += x[w];
+    }
+}
+__global__ __launch_bounds__(256) void lvl_off_part_kernel(int ld, int lw, const int32_t* __restrict__ cnt,
+                                                           int32_t* __restrict__ part) {
+    __shared__ int ws[4][LVL_BATCH + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int x[LVL_BATCH + 1];
+    lvl_off_cols(ld, lw, blockIdx.x * 256 + tid, cnt, x);
+#pragma unroll
+    for (int c = 0; c <= LVL_BATCH; ++c) {
+        int v = x[c];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (lane == 0) ws[wv][c] = v;
+    }
+    __syncthreads();
+    if (tid <= LVL_BATCH) part[blockIdx.x * (LVL_BATCH + 1) + tid] = ws[0][tid] + ws[1][tid] + ws[2][tid] + ws[3][tid];
+}
+__global__ __launch_bounds__(256) void lvl_offsets_kernel(int ld, int lw, int R, const int32_t* __restrict__ cnt,
+                                                          const int32_t* __restrict__ part, int32_t* __restrict__ off,
+                                                          int32_t* __restrict__ offw, int32_t* __restrict__ dsz) {
+    __shared__ int pre[LVL_BATCH + 1], tot[LVL_BATCH + 1], colB[LVL_BATCH + 2], ws[4][LVL_BATCH + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, b = blockIdx.x, nb = gridDim.x;
+    if (tid < 4 * (LVL_BATCH + 1)) { /* four threads per column: the earlier blocks' sums, all sums */
+        const int c = tid >> 2, k = tid & 3;
+        int p = 0, t = 0;
+        for (int q = k; q < nb; q += 4) {
+            const int v = part[q * (LVL_BATCH + 1) + c];
+            t += v;
+            if (q < b) p += v;
+        }
+        p += __shfl_xor(p, 1);
+        p += __shfl_xor(p, 2);
+        t += __shfl_xor(t, 1);
+        t += __shfl_xor(t, 2);
+        if (k == 0) {
+            pre[c] = p;
+            tot[c] = t;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) { /* offw's base of each weight */
+        int r = 0;
+        for (int w = 1; w <= lw; ++w) {
+            colB[w] = r;
+            r += tot[w];
+        }
+        colB[lw + 1] = r;
+    }
+    const int j = b * 256 + tid;
+    int x[LVL_BATCH + 1], ex[LVL_BATCH + 1];
+    lvl_off_cols(ld, lw, j, cnt, x);
+#pragma unroll
+    for (int c = 0; c <= LVL_BATCH; ++c) {
+        int v = x[c];
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(v, o);
+            if (lane >= o) v += y;
+        }
+        ex[c] = v - x[c];
+        if (lane == 63) ws[wv][c] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c <= LVL_BATCH; ++c) {
+        int add = pre[c];
+        for (int v = 0; v < wv; ++v) add += ws[v][c];
+        ex[c] += add;
+    }
+    if (j < ld) {
+        int32_t* oj = off + (size_t)j * LVL_STRIDE;
+        int r = ex[0];
+        oj[0] = r;
+#pragma unroll
+        for (int w = 1; w <= LVL_BATCH; ++w)
+            if (w <= lw) {
+                oj[w] = r;
+                r += x[w];
+            }
+        oj[lw + 1] = r;
+        if (offw) {
+#pragma unroll
+            for (int w = 1; w <= LVL_BATCH; ++w)
+                if (w <= lw) offw[(size_t)(w - 1) * ld + j] = colB[w] + ex[w];
+            if (dsz && j % SRT_SHARD_ALIGN == 0) { /* a shard start (srt_shard_rows) */
+                const long long nbs = ld / SRT_SHARD_ALIGN;
+                for (int q = 0; q < R; ++q)
+                    if ((int)(nbs * q / R) * SRT_SHARD_ALIGN == j)
+                        for (int w = 1; w <= lw; ++w) dsz[(w - 1) * (R + 1) + q] = colB[w] + ex[w];
+            }
+        }
+    } else if (j == ld) {
+        off[(size_t)ld * LVL_STRIDE] = tot[0];
+        if (offw) {
+            offw[(size_t)lw * ld] = colB[lw + 1];
+            if (dsz) /* q == R: the weight's end, the next weight's start */
+                for (int w = 1; w <= lw; ++w) dsz[(w - 1) * (R + 1) + R] = colB[w + 1];
+        }
+    }
 }
 
 /* N > 1, the one exchange ahead of every decision (a sum all-reduce of int32; each rank fills
@@ -1844,6 +1944,16 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         SRT_HIPCHK(hipEventRecord(wev[prep], st)); /* the allocations are ordered on st */
         SRT_HIPCHK(hipStreamWaitEvent(wcs, wev[prep], 0));
         prepped = true;
+    }
+    if (R > 1) { /* the agreement goes out first; the side stream's calls are made under it */
+        hag[0] = lmax;
+        hag[1] = ok;
+        hag[2] = stream_ok;
+        SRT_HIPCHK(hipMemcpyAsync(dagree, hag, 3 * sizeof(int32_t), hipMemcpyHostToDevice, st));
+        if ((rc = srt_coll_allreduce_i32(comm, dagree, 3, 1, st))) return rc;
+        SRT_HIPCHK(hipMemcpyAsync(hag, dagree, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    }
+    if (prepped) {
         SRT_HIPCHK(hipMemsetAsync(Rb, 0, plane * sizeof(uint32_t), wcs));
         SRT_HIPCHK(hipMemsetAsync(done, 0, (size_t)n * nchunk, wcs));
         lvl_init_kernel<<<srt_ceil_div(nrows, 256), 256, 0, wcs>>>(n, row0, nrows, nw, Rb);
@@ -1875,12 +1985,6 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     }
     if (prepped) SRT_HIPCHK(hipEventRecord(wev[prep], wcs));
     if (R > 1) {
-        hag[0] = lmax;
-        hag[1] = ok;
-        hag[2] = stream_ok;
-        SRT_HIPCHK(hipMemcpyAsync(dagree, hag, 3 * sizeof(int32_t), hipMemcpyHostToDevice, st));
-        if ((rc = srt_coll_allreduce_i32(comm, dagree, 3, 1, st))) return rc;
-        SRT_HIPCHK(hipMemcpyAsync(hag, dagree, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
         if ((rc = lvl_wait(st))) return rc;
         lmax = hag[0];
         ok = hag[1];
@@ -1921,7 +2025,14 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     };
     if ((rc = share_counts(1, lx))) return rc; /* the first extraction's weights */
     /* offsets of the (target, weight <= lw) in-arcs: narrow scan, counts untouched */
-    auto offsets = [&](int lw) -> int {
+    auto offsets = [&](int lw, int32_t* ow = NULL, int32_t* osz = NULL) -> int {
+        if (lw <= LVL_BATCH) { /* a first extraction: two launches (with the wire's offsets) */
+            const int nb = (ld + 1 + 255) / 256; /* (the thread of target ld writes the totals) */
+            lvl_off_part_kernel<<<nb, 256, 0, st>>>(ld, lw, cnt, tb);
+            lvl_offsets_kernel<<<nb, 256, 0, st>>>(ld, lw, R, cnt, tb, off, ow, osz);
+            SRT_HIPCHK(hipGetLastError());
+            return SRT_OK;
+        }
         lvl_tot_kernel<<<srt_ceil_div(ld + 1, 256), 256, 0, st>>>(ld, lw, cnt, tb);
         SRT_HIPCHK(hipGetLastError());
         SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, tb, tb + ld + 1, ld + 1, st));
@@ -2071,8 +2182,12 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         for (int x = 1; x <= lw; ++x) t64 += (int64_t)hist[x];
         total_x = (int32_t)t64;
         int rc_;
-        /* offsets over the arcs with w <= lw, (target, weight)-major, and the own rows' arcs */
-        if ((rc_ = offsets(lw))) return rc_;
+        /* offsets over the arcs with w <= lw, (target, weight)-major, and the wire's: offw, the
+         * [weight][target] scan of every target's counts (gathered), dsz its values at the shard
+         * starts; the wire's per-weight bases are on the device since the agreement */
+        int32_t* const dsz = packed;
+        const int32_t* dwt = packed + LVL_BATCH * 65;
+        if ((rc_ = offsets(lw, offw, dsz))) return rc_;
         lvl_arcs_rows_kernel<true><<<nrows, 256, 0, st>>>(n, ld, row0, w_rows, NULL, lw, off, arcsA,
                                                           r_rows, arA, NULL, stash, scnt);
         const int32_t* lo = off + (size_t)row0 * LVL_STRIDE;
@@ -2082,17 +2197,6 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
         const int nu = (int)u.size();
         lvl_rt_index_range_kernel<<<512, 256, 0, st>>>(lo, hi, arA, reinterpret_cast<const unsigned long long*>(rtab),
                                                        nu, rix);
-        /* offw: the [weight][target] scan of every target's counts (gathered), dsz its values at
-         * the shard starts; the wire's per-weight bases are on the device since the agreement */
-        const size_t nwo = (size_t)lw * ld + 1;
-        lvl_wcols_kernel<<<srt_ceil_div((int64_t)nwo, 256), 256, 0, st>>>(ld, lw, cnt,
-                                                                       reinterpret_cast<int32_t*>(wire));
-        SRT_HIPCHK(hipGetLastError());
-        SRT_HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, reinterpret_cast<int32_t*>(wire), offw,
-                                                    (int)nwo, st));
-        int32_t* const dsz = packed;
-        const int32_t* dwt = packed + LVL_BATCH * 65;
-        lvl_wire_sizes_kernel<<<srt_ceil_div(lw * (R + 1), 256), 256, 0, st>>>(ld, lw, R, offw, dsz);
         if (lrows > 0)
             lvl_wire_pack_kernel<<<srt_ceil_div(lrows, 4), 256, 0, st>>>(ld, row0, lrows, lw, R, me, off, offw, dsz,
                                                                         dwt, arcsA, rix, arA, wire, NULL);
