@@ -840,13 +840,15 @@ __global__ __launch_bounds__(256) void lvl_rt_merge_kernel(int ntab, const unsig
     if (bad) *ovf = 1;
 }
 
-/* the numbering kernels over a device-held range [*lo, *hi) (no read-back of the bounds) */
-__global__ void lvl_rt_index_range_kernel(const int32_t* __restrict__ lo, const int32_t* __restrict__ hi,
-                                          const double* __restrict__ ar,
-                                          const unsigned long long* __restrict__ tab, int ntab,
-                                          uint16_t* __restrict__ rix) {
+/* the own arcs in [*lo, *hi): each one's byte offset of its source row (aoff) and its index into
+ * the sorted table of distinct reliabilities (by value bits, binary search) -- one pass */
+__global__ void lvl_own_index_kernel(const int32_t* __restrict__ lo, const int32_t* __restrict__ hi, int nw,
+                                     const uint32_t* __restrict__ arcs, const double* __restrict__ ar,
+                                     const unsigned long long* __restrict__ tab, int ntab,
+                                     uint32_t* __restrict__ aoff, uint16_t* __restrict__ rix) {
     const int a = *lo, b = *hi;
     for (int i = a + blockIdx.x * blockDim.x + threadIdx.x; i < b; i += gridDim.x * blockDim.x) {
+        aoff[i] = (arcs[i] & 0xFFFFu) * (uint32_t)nw * 4u;
         const unsigned long long v = (unsigned long long)__double_as_longlong(ar[i]);
         int l = 0, h = ntab - 1;
         while (l < h) {
@@ -856,13 +858,6 @@ __global__ void lvl_rt_index_range_kernel(const int32_t* __restrict__ lo, const 
         }
         rix[i] = (uint16_t)l;
     }
-}
-/* byte offsets of the arcs in [*lo, *hi) */
-__global__ void lvl_aoff_range_kernel(const int32_t* __restrict__ lo, const int32_t* __restrict__ hi, int nw,
-                                      const uint32_t* __restrict__ arcs, uint32_t* __restrict__ aoff) {
-    const int a = *lo, b = *hi;
-    for (int i = a + blockIdx.x * blockDim.x + threadIdx.x; i < b; i += gridDim.x * blockDim.x)
-        aoff[i] = (arcs[i] & 0xFFFFu) * (uint32_t)nw * 4u;
 }
 
 /* the second stream and the per-weight events of the streamed extraction, per state slot (made
@@ -880,6 +875,8 @@ static int lvl_side_stream(hipStream_t* cs, hipEvent_t** ev) {
     *ev = g_lvl_ev[k];
     return SRT_OK;
 }
+/* the host-side set that deduplicates the exchanged reliability blocks, per slot */
+static std::vector<unsigned long long> g_lvl_uset[SRT_STATE_SLOTS];
 /* The build's host round trips (the exchange, the agreement, one vote per batch) go through
  * pinned staging, per slot, made once and grown when a larger exchange needs it: a copy to or
  * from pageable memory is staged by the runtime and blocks the calling thread. Layout (u64
@@ -1821,20 +1818,42 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     /* the union of every rank's distinct light reliabilities (sorted by bits: the same table on
      * every rank) and, per weight <= LVL_BATCH, the largest rank's arcs (the streamed wire's
      * block): both from the exchange, so the streamed extraction needs no further round trip */
+    /* The blocks come in hash-slot order and mostly repeat each other (C4: ~500 values per rank,
+     * the same ones), so they are deduplicated through an open-addressing set first and only the
+     * distinct values sorted: sorting the concatenation (4,000 values at N = 8) cost ~0.1-0.2 ms of
+     * host time on the critical path. A solo rank's peers hold its own values (their rows are
+     * shifted copies of its rows), so it pays the same. */
     std::vector<unsigned long long> u;
     bool fit = R > 1;
-    for (int q = 0; q < R && fit; q++) {
-        const int32_t* hd = hx + LVL_X_LIMBS + (size_t)R * LVL_X_CNT + (size_t)q * LVL_GB * 2;
-        if (hd[0] || hd[1] > LVL_RT_CAP) fit = false;
-        else {
-            const unsigned long long* v = reinterpret_cast<const unsigned long long*>(hd + 2);
-            u.insert(u.end(), v, v + hd[1]);
-        }
-    }
     if (fit) {
-        std::sort(u.begin(), u.end());
-        u.erase(std::unique(u.begin(), u.end()), u.end());
-        fit = !u.empty() && u.size() <= (size_t)LVL_RT_CAP;
+        size_t all = 0;
+        for (int q = 0; q < R && fit; q++) {
+            const int32_t* hd = hx + LVL_X_LIMBS + (size_t)R * LVL_X_CNT + (size_t)(solo ? me : q) * LVL_GB * 2;
+            if (hd[0] || hd[1] > LVL_RT_CAP) fit = false;
+            all += (size_t)max(hd[1], 0);
+        }
+        size_t cap = 64;
+        while (cap < 2 * all) cap <<= 1;
+        std::vector<unsigned long long>& set = g_lvl_uset[srt_state_slot()];
+        set.assign(cap, ~0ull); /* (a NaN pattern: never a reliability's bits) */
+        int shift = 64;
+        for (size_t c = cap; c > 1; c >>= 1) --shift;
+        for (int q = 0; q < R && fit; q++) {
+            const int32_t* hd = hx + LVL_X_LIMBS + (size_t)R * LVL_X_CNT + (size_t)(solo ? me : q) * LVL_GB * 2;
+            const unsigned long long* v = reinterpret_cast<const unsigned long long*>(hd + 2);
+            for (int k = 0; k < hd[1]; ++k) {
+                size_t h = (size_t)((v[k] * 0x9E3779B97F4A7C15ull) >> shift);
+                while (set[h] != ~0ull && set[h] != v[k]) h = (h + 1) & (cap - 1);
+                if (set[h] == ~0ull) {
+                    set[h] = v[k];
+                    u.push_back(v[k]);
+                }
+            }
+        }
+        if (fit) {
+            std::sort(u.begin(), u.end());
+            fit = !u.empty() && u.size() <= (size_t)LVL_RT_CAP;
+        }
     }
     /* level budget from global quantities (the summed histogram, the largest shard's words): the
      * largest L whose predicted time stays under half the FW time */
@@ -2192,11 +2211,11 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
                                                           r_rows, arA, NULL, stash, scnt);
         const int32_t* lo = off + (size_t)row0 * LVL_STRIDE;
         const int32_t* hi = off + (size_t)(row0 + nrows) * LVL_STRIDE;
-        lvl_aoff_range_kernel<<<512, 256, 0, st>>>(lo, hi, nw, arcsA, aoff);
-        /* each own arc's index into the union table (on the device since the agreement) */
-        const int nu = (int)u.size();
-        lvl_rt_index_range_kernel<<<512, 256, 0, st>>>(lo, hi, arA, reinterpret_cast<const unsigned long long*>(rtab),
-                                                       nu, rix);
+        /* each own arc's row offset and its index into the union table (on the device since the
+         * agreement) */
+        lvl_own_index_kernel<<<512, 256, 0, st>>>(lo, hi, nw, arcsA, arA,
+                                                  reinterpret_cast<const unsigned long long*>(rtab), (int)u.size(),
+                                                  aoff, rix);
         if (lrows > 0)
             lvl_wire_pack_kernel<<<srt_ceil_div(lrows, 4), 256, 0, st>>>(ld, row0, lrows, lw, R, me, off, offw, dsz,
                                                                         dwt, arcsA, rix, arA, wire, NULL);
