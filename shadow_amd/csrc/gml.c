@@ -5,6 +5,8 @@
 #include "gml.h"
 
 #include <math.h>
+#include <pthread.h>
+#include <unistd.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -315,10 +317,19 @@ static int parse_element(ps_t* s, int is_node) {
     return 0;
 }
 
-static int parse_graph(ps_t* s) {
+/* The graph list's items from s->p: node and edge lists, other lists skipped, key-value pairs
+ * (only `directed` is kept; the last one wins). Stops at the graph's closing ']' (*closed = 1) or,
+ * with stop != NULL, at the first item that starts at or after stop (a parallel chunk's end). */
+static int parse_items(ps_t* s, const char* stop, int* closed, int* have_dir, int* dir) {
+    *closed = 0;
     for (;;) {
+        skip_ws(s);
+        if (stop && s->p >= stop) return 0;
         tok_t k = next_tok(s);
-        if (k.kind == T_CLOSE) return 0;
+        if (k.kind == T_CLOSE) {
+            *closed = 1;
+            return 0;
+        }
         if (k.kind != T_KEY) return fail(s, "expected key in graph");
         tok_t v = next_tok(s);
         if (v.kind == T_OPEN) {
@@ -332,8 +343,202 @@ static int parse_graph(ps_t* s) {
             continue;
         }
         if (v.kind != T_NUM && v.kind != T_STR) return fail(s, "bad value in graph");
-        if (keyeq(&k, "directed") && v.kind == T_NUM) s->directed = (v.num != 0.0);
+        if (keyeq(&k, "directed") && v.kind == T_NUM) {
+            *have_dir = 1;
+            *dir = v.num != 0.0;
+        }
     }
+}
+
+static int parse_graph(ps_t* s) {
+    int closed = 0, have_dir = 0, dir = 0;
+    if (parse_items(s, NULL, &closed, &have_dir, &dir)) return -1;
+    if (have_dir) s->directed = dir;
+    return 0;
+}
+
+/* ---- the graph list in parallel (large files) ------------------------------------------------ *
+ * Shadow's own GML and Tor-atlas-derived topologies are one `graph [` list of millions of `node
+ * [...]` / `edge [...]` items; one core tokenises ~140 MB/s. Above GML_PAR_MIN bytes the list is
+ * cut at candidate item starts (a line that begins, after blanks, with `node [` or `edge [`),
+ * each piece is parsed by its own thread into its own records, string pool and attribute tables,
+ * and the pieces are concatenated in file order (attributes keep their first-seen order and are
+ * strings if any piece saw a string). A candidate inside a quoted string or a nested list is
+ * caught because the previous piece, parsing from a true item start, does not stop exactly on
+ * it; then, or on any error, the list is parsed again by one thread, which also writes the error
+ * message with its line. */
+#define GML_PAR_MIN ((size_t)64 << 20)
+#define GML_PAR_MAXT 16
+
+typedef struct {
+    ps_t s;
+    const char* stop;
+    int rc, closed, have_dir, dir;
+} gml_piece;
+
+static void* piece_run(void* arg) {
+    gml_piece* c = (gml_piece*)arg;
+    c->rc = pool_add(&c->s, "", 0, &(size_t){0}) ? -1 : 0;
+    c->s.vstart = (int64_t*)calloc(1, sizeof(int64_t));
+    c->s.estart = (int64_t*)calloc(1, sizeof(int64_t));
+    if (!c->s.vstart || !c->s.estart) c->rc = -1;
+    if (!c->rc) c->rc = parse_items(&c->s, c->stop, &c->closed, &c->have_dir, &c->dir);
+    return NULL;
+}
+
+static void ps_free(ps_t* s) {
+    for (int i = 0; i < s->vt.count; i++) free(s->vt.names[i]);
+    for (int i = 0; i < s->et.count; i++) free(s->et.names[i]);
+    free(s->vt.names);
+    free(s->vt.is_string);
+    free(s->et.names);
+    free(s->et.is_string);
+    free(s->vkv);
+    free(s->ekv);
+    free(s->vstart);
+    free(s->estart);
+    free(s->node_id);
+    free(s->esrc_id);
+    free(s->edst_id);
+    free(s->pool);
+}
+
+/* a candidate item start at or after q: the first line from q that begins with node/edge and '[' */
+static const char* next_item_start(const char* q, const char* end) {
+    while (q < end) {
+        const char* nl = (const char*)memchr(q, '\n', (size_t)(end - q));
+        if (!nl) return NULL;
+        const char* b = nl + 1;
+        while (b < end && (*b == ' ' || *b == '\t' || *b == '\r')) b++;
+        if (end - b > 5 && (memcmp(b, "node", 4) == 0 || memcmp(b, "edge", 4) == 0)) {
+            const char* x = b + 4;
+            while (x < end && (*x == ' ' || *x == '\t' || *x == '\r' || *x == '\n')) x++;
+            if (x < end && *x == '[') return b;
+        }
+        q = b;
+    }
+    return NULL;
+}
+
+/* append piece c's records to s (attribute indices remapped, string offsets moved) */
+static int piece_merge(ps_t* s, ps_t* c) {
+    int vmap[1024], emap[1024];
+    if (c->vt.count > 1024 || c->et.count > 1024) return -1;
+    for (int a = 0; a < c->vt.count; a++)
+        if ((vmap[a] = attr_index(s, &s->vt, c->vt.names[a], strlen(c->vt.names[a]), c->vt.is_string[a])) < 0)
+            return -1;
+    for (int a = 0; a < c->et.count; a++)
+        if ((emap[a] = attr_index(s, &s->et, c->et.names[a], strlen(c->et.names[a]), c->et.is_string[a])) < 0)
+            return -1;
+    const size_t pbase = s->pool_len;
+    if (s->pool_len + c->pool_len > s->pool_cap) {
+        size_t nc = s->pool_cap ? s->pool_cap : 4096;
+        while (nc < s->pool_len + c->pool_len) nc *= 2;
+        char* np = (char*)realloc(s->pool, nc);
+        if (!np) return -1;
+        s->pool = np;
+        s->pool_cap = nc;
+    }
+    memcpy(s->pool + s->pool_len, c->pool, c->pool_len);
+    s->pool_len += c->pool_len;
+#define SRT_GML_APPEND(field, lenf, capf, type, extra)                                         \
+    do {                                                                                    \
+        size_t need_ = (size_t)(s->lenf + c->lenf) + (extra);                              \
+        if (need_ > (size_t)s->capf) {                                                     \
+            type* np_ = (type*)realloc(s->field, need_ * sizeof(type));                    \
+            if (!np_) return -1;                                                           \
+            s->field = np_;                                                                \
+            s->capf = need_;                                                               \
+        }                                                                                   \
+    } while (0)
+    const int64_t vk0 = s->vkv_len, ek0 = s->ekv_len;
+    SRT_GML_APPEND(vkv, vkv_len, vkv_cap, kv_t, 0);
+    for (int64_t k = 0; k < c->vkv_len; k++) {
+        kv_t kv = c->vkv[k];
+        kv.attr = vmap[kv.attr];
+        if (kv.is_str) kv.str += pbase;
+        s->vkv[s->vkv_len++] = kv;
+    }
+    SRT_GML_APPEND(ekv, ekv_len, ekv_cap, kv_t, 0);
+    for (int64_t k = 0; k < c->ekv_len; k++) {
+        kv_t kv = c->ekv[k];
+        kv.attr = emap[kv.attr];
+        if (kv.is_str) kv.str += pbase;
+        s->ekv[s->ekv_len++] = kv;
+    }
+    {
+        const int64_t n0 = s->n;
+        SRT_GML_APPEND(node_id, n, n_cap, double, 0);
+        int64_t* ns = (int64_t*)realloc(s->vstart, (size_t)(s->n_cap + 1) * sizeof(int64_t));
+        if (!ns) return -1;
+        s->vstart = ns;
+        memcpy(s->node_id + n0, c->node_id, (size_t)c->n * sizeof(double));
+        for (int64_t i = 1; i <= c->n; i++) s->vstart[n0 + i] = vk0 + c->vstart[i];
+        s->n += c->n;
+    }
+    {
+        const int64_t m0 = s->m;
+        SRT_GML_APPEND(esrc_id, m, m_cap, double, 0);
+        double* nd = (double*)realloc(s->edst_id, (size_t)s->m_cap * sizeof(double));
+        int64_t* ne = (int64_t*)realloc(s->estart, (size_t)(s->m_cap + 1) * sizeof(int64_t));
+        if (nd) s->edst_id = nd;
+        if (ne) s->estart = ne;
+        if (!nd || !ne) return -1;
+        memcpy(s->esrc_id + m0, c->esrc_id, (size_t)c->m * sizeof(double));
+        memcpy(s->edst_id + m0, c->edst_id, (size_t)c->m * sizeof(double));
+        for (int64_t i = 1; i <= c->m; i++) s->estart[m0 + i] = ek0 + c->estart[i];
+        s->m += c->m;
+    }
+#undef SRT_GML_APPEND
+    return 0;
+}
+
+/* The graph list from s->p (just past its '['), in nt pieces. Returns the number of pieces when it
+ * was parsed (s->p past the closing ']'), 0 when the caller should parse it with one thread
+ * (nothing changed), -1 when merging the pieces ran out of memory. */
+static int parse_graph_parallel(ps_t* s, int nt) {
+    const char* b[GML_PAR_MAXT + 1];
+    int k = 0;
+    b[k++] = s->p;
+    const size_t body = (size_t)(s->end - s->p);
+    for (int i = 1; i < nt; i++) {
+        const char* q = next_item_start(s->p + body / (size_t)nt * (size_t)i, s->end);
+        if (!q) break;
+        if (q > b[k - 1]) b[k++] = q;
+    }
+    if (k < 2) return 0;
+    gml_piece pc[GML_PAR_MAXT];
+    pthread_t th[GML_PAR_MAXT];
+    int started[GML_PAR_MAXT];
+    memset(pc, 0, sizeof(pc));
+    for (int i = 0; i < k; i++) {
+        pc[i].s.p = b[i];
+        pc[i].s.end = s->end;
+        pc[i].s.line = 1;
+        pc[i].stop = i + 1 < k ? b[i + 1] : NULL;
+        started[i] = pthread_create(&th[i], NULL, piece_run, &pc[i]) == 0;
+        if (!started[i]) piece_run(&pc[i]);
+    }
+    for (int i = 0; i < k; i++)
+        if (started[i]) pthread_join(th[i], NULL);
+    int ok = 1;
+    for (int i = 0; i < k && ok; i++) { /* every piece ends exactly where the next begins */
+        if (pc[i].rc || pc[i].s.vt.count > 1024 || pc[i].s.et.count > 1024) ok = 0;
+        else if (i + 1 < k) ok = !pc[i].closed && pc[i].s.p == b[i + 1];
+        else ok = pc[i].closed;
+    }
+    int dir = -1, rc = ok;
+    for (int i = 0; i < k && rc == 1; i++) {
+        if (piece_merge(s, &pc[i].s)) rc = fail(s, "out of memory");
+        if (pc[i].have_dir) dir = pc[i].dir;
+    }
+    if (rc == 1) {
+        if (dir >= 0) s->directed = dir;
+        s->p = pc[k - 1].s.p;
+        rc = k;
+    }
+    for (int i = 0; i < k; i++) ps_free(&pc[i].s);
+    return rc;
 }
 
 /* open-addressing id -> index map */
@@ -407,6 +612,16 @@ static void fix_strings(gml_attr* cols, int na, int64_t count, char* pool) {
 }
 
 int gml_parse(const char* text, size_t len, gml_graph* out, char* err, size_t errlen) {
+    long nc = sysconf(_SC_NPROCESSORS_ONLN);
+    int nt = nc > GML_PAR_MAXT ? GML_PAR_MAXT : nc > 1 ? (int)nc : 1;
+    const size_t per = (size_t)16 << 20; /* at least 16 MB per piece */
+    if ((size_t)nt > len / per) nt = (int)(len / per) > 1 ? (int)(len / per) : 1;
+    return gml_parse_ex(text, len, out, err, errlen, nt, GML_PAR_MIN);
+}
+
+int gml_parse_ex(const char* text, size_t len, gml_graph* out, char* err, size_t errlen, int nthreads,
+                 size_t par_min) {
+    int used_par = 0; /* the graph list was parsed in pieces */
     memset(out, 0, sizeof(*out));
     ps_t st;
     memset(&st, 0, sizeof(st));
@@ -437,7 +652,11 @@ int gml_parse(const char* text, size_t len, gml_graph* out, char* err, size_t er
         tok_t v = next_tok(s);
         if (v.kind == T_OPEN) {
             if (keyeq(&k, "graph") && !found) {
-                if (parse_graph(s)) goto done;
+                int par = 0;
+                if (nthreads > 1 && (size_t)(s->end - s->p) >= par_min)
+                    par = parse_graph_parallel(s, nthreads < GML_PAR_MAXT ? nthreads : GML_PAR_MAXT);
+                used_par = par > 0 ? par : 0;
+                if (par < 0 || (!par && parse_graph(s))) goto done;
                 found = 1;
             } else if (skip_list(s)) {
                 goto done;
@@ -516,6 +735,7 @@ int gml_parse(const char* text, size_t len, gml_graph* out, char* err, size_t er
     out->n = (int32_t)s->n;
     out->m = s->m;
     out->pool = s->pool;
+    out->pieces = used_par > 1 ? used_par : 1;
     s->pool = NULL;
     rc = 0;
 done:
@@ -534,6 +754,8 @@ done:
     free(s->edst_id);
     free(s->pool);
     if (rc) gml_free(out);
+    /* an error after a parallel graph list: one thread again, for the message and its line */
+    if (rc && used_par) return gml_parse_ex(text, len, out, err, errlen, 1, par_min);
     return rc;
 }
 

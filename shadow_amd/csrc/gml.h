@@ -30,10 +30,16 @@ typedef struct gml_graph {
     gml_attr* va;
     gml_attr* ea;
     char* pool; /* string storage */
+    int pieces; /* the graph list was parsed in this many pieces (1: one thread) */
 } gml_graph;
 
 /* Returns 0 on success; on error returns -1 and writes a message into err (if non-NULL). */
 int gml_parse(const char* text, size_t len, gml_graph* out, char* err, size_t errlen);
+/* gml_parse with the graph list cut into up to nthreads pieces parsed in parallel when it holds
+ * at least par_min bytes (gml_parse: the online CPUs up to 16, one per 16 MB, from 64 MB on).
+ * The result, and any error message, is the one-thread parse's. */
+int gml_parse_ex(const char* text, size_t len, gml_graph* out, char* err, size_t errlen, int nthreads,
+                 size_t par_min);
 void gml_free(gml_graph* g);
 /* Exact-name attribute lookup (igraph_cattribute_has_attr semantics). */
 const gml_attr* gml_vattr(const gml_graph* g, const char* name);
