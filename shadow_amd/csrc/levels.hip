@@ -1021,8 +1021,19 @@ static __device__ __forceinline__ uint32_t lvl_step_unit(unsigned g, int d, int 
      * the lane's) and one gather; sixteen gathers in flight. Lanes past nw read word 0 of the row
      * (a valid address) and drop it, so the loop has no per-lane branch. */
     const uint32_t lane4 = (uint32_t)(valid ? word : 0) * 4u;
+    /* The unit's settled sources, read before the gathers: once every source of the unit is
+     * settled or found, the later gathers cannot change the level's new bits (acc & ~r), so the
+     * walk stops. On C4 a source at distance 4 is nearly always found through a weight-1 arc from
+     * a vertex at distance 3, so level 4 needs the first weight group alone wherever the unit
+     * holds no source at distance 5. Sources past n (padding of the last shard) never appear:
+     * they count as settled. */
+    uint32_t* rp = R + (size_t)j * nw + word;
+    const uint32_t r = valid ? *rp : 0u;
+    const int s0 = src0 + word * 32;
+    const uint32_t full = !valid ? 0u : s0 + 32 <= n ? 0xFFFFFFFFu : s0 >= n ? 0u : (1u << (n - s0)) - 1u;
     constexpr int LVL_SB = 16; /* (8 measured the same, 32/48 slower; pipelined batches did not help) */
     for (int w = 1; w < d; ++w) {
+        if (!__any(((acc | r) & full) != full)) break;
         const int g1 = oj[w + 1];
         const char* base = reinterpret_cast<const char*>(lev + (size_t)(d - w - 1) * plane);
         for (int i = oj[w]; i < g1; i += LVL_SB) { /* LVL_SB in flight, the tail predicated */
@@ -1034,21 +1045,17 @@ static __device__ __forceinline__ uint32_t lvl_step_unit(unsigned g, int d, int 
                 v[q] = i + q < g1 ? *reinterpret_cast<const uint32_t*>(base + (a[q] + lane4)) : 0u;
 #pragma unroll
             for (int q = 0; q < LVL_SB; ++q) acc |= v[q];
+            if (i + LVL_SB < g1 && !__any(((acc | r) & full) != full)) break;
         }
     }
     if (!valid) acc = 0;
     bool inc = false;
     uint32_t settled = 0;
     if (valid) {
-        uint32_t* rp = R + (size_t)j * nw + word;
-        const uint32_t r = *rp;
         const uint32_t nb = acc & ~r;
         settled = (uint32_t)__builtin_popcount(nb);
         *out = nb;
         if (nb) *rp = r | nb;
-        /* sources past n (padding of the last shard) never appear: they count as settled */
-        const int s0 = src0 + word * 32;
-        const uint32_t full = s0 + 32 <= n ? 0xFFFFFFFFu : s0 >= n ? 0u : (1u << (n - s0)) - 1u;
         inc = ((r | nb) & full) != full;
     }
     /* completion: a flag, not a count -- one same-address atomic per wave serialised at the memory
