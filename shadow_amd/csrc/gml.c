@@ -420,77 +420,107 @@ static const char* next_item_start(const char* q, const char* end) {
     return NULL;
 }
 
-/* append piece c's records to s (attribute indices remapped, string offsets moved) */
-static int piece_merge(ps_t* s, ps_t* c) {
+/* Merging the pieces: the attribute maps and every piece's offsets into the merged arrays are
+ * planned on one thread (cheap), then each piece copies its records, remapped, on its own thread
+ * (on one thread the merge took ~170 ms of a 200-MB file's ~540). */
+typedef struct {
+    ps_t* s;
+    ps_t* c;
     int vmap[1024], emap[1024];
-    if (c->vt.count > 1024 || c->et.count > 1024) return -1;
-    for (int a = 0; a < c->vt.count; a++)
-        if ((vmap[a] = attr_index(s, &s->vt, c->vt.names[a], strlen(c->vt.names[a]), c->vt.is_string[a])) < 0)
-            return -1;
-    for (int a = 0; a < c->et.count; a++)
-        if ((emap[a] = attr_index(s, &s->et, c->et.names[a], strlen(c->et.names[a]), c->et.is_string[a])) < 0)
-            return -1;
-    const size_t pbase = s->pool_len;
-    if (s->pool_len + c->pool_len > s->pool_cap) {
-        size_t nc = s->pool_cap ? s->pool_cap : 4096;
-        while (nc < s->pool_len + c->pool_len) nc *= 2;
-        char* np = (char*)realloc(s->pool, nc);
-        if (!np) return -1;
-        s->pool = np;
-        s->pool_cap = nc;
-    }
-    memcpy(s->pool + s->pool_len, c->pool, c->pool_len);
-    s->pool_len += c->pool_len;
-#define SRT_GML_APPEND(field, lenf, capf, type, extra)                                         \
-    do {                                                                                    \
-        size_t need_ = (size_t)(s->lenf + c->lenf) + (extra);                              \
-        if (need_ > (size_t)s->capf) {                                                     \
-            type* np_ = (type*)realloc(s->field, need_ * sizeof(type));                    \
-            if (!np_) return -1;                                                           \
-            s->field = np_;                                                                \
-            s->capf = need_;                                                               \
-        }                                                                                   \
-    } while (0)
-    const int64_t vk0 = s->vkv_len, ek0 = s->ekv_len;
-    SRT_GML_APPEND(vkv, vkv_len, vkv_cap, kv_t, 0);
+    size_t pbase;
+    int64_t vk0, ek0, n0, m0;
+} piece_copy_t;
+
+static void* piece_copy(void* arg) {
+    piece_copy_t* q = (piece_copy_t*)arg;
+    ps_t* s = q->s;
+    const ps_t* c = q->c;
+    memcpy(s->pool + q->pbase, c->pool, c->pool_len);
     for (int64_t k = 0; k < c->vkv_len; k++) {
         kv_t kv = c->vkv[k];
-        kv.attr = vmap[kv.attr];
-        if (kv.is_str) kv.str += pbase;
-        s->vkv[s->vkv_len++] = kv;
+        kv.attr = q->vmap[kv.attr];
+        if (kv.is_str) kv.str += q->pbase;
+        s->vkv[q->vk0 + k] = kv;
     }
-    SRT_GML_APPEND(ekv, ekv_len, ekv_cap, kv_t, 0);
     for (int64_t k = 0; k < c->ekv_len; k++) {
         kv_t kv = c->ekv[k];
-        kv.attr = emap[kv.attr];
-        if (kv.is_str) kv.str += pbase;
-        s->ekv[s->ekv_len++] = kv;
+        kv.attr = q->emap[kv.attr];
+        if (kv.is_str) kv.str += q->pbase;
+        s->ekv[q->ek0 + k] = kv;
     }
-    {
-        const int64_t n0 = s->n;
-        SRT_GML_APPEND(node_id, n, n_cap, double, 0);
-        int64_t* ns = (int64_t*)realloc(s->vstart, (size_t)(s->n_cap + 1) * sizeof(int64_t));
-        if (!ns) return -1;
-        s->vstart = ns;
-        memcpy(s->node_id + n0, c->node_id, (size_t)c->n * sizeof(double));
-        for (int64_t i = 1; i <= c->n; i++) s->vstart[n0 + i] = vk0 + c->vstart[i];
-        s->n += c->n;
+    memcpy(s->node_id + q->n0, c->node_id, (size_t)c->n * sizeof(double));
+    for (int64_t i = 1; i <= c->n; i++) s->vstart[q->n0 + i] = q->vk0 + c->vstart[i];
+    memcpy(s->esrc_id + q->m0, c->esrc_id, (size_t)c->m * sizeof(double));
+    memcpy(s->edst_id + q->m0, c->edst_id, (size_t)c->m * sizeof(double));
+    for (int64_t i = 1; i <= c->m; i++) s->estart[q->m0 + i] = q->ek0 + c->estart[i];
+    return NULL;
+}
+
+/* append the k pieces' records to s in order; -1 when out of memory */
+static int pieces_merge(ps_t* s, gml_piece* pc, int k) {
+    piece_copy_t* q = (piece_copy_t*)calloc((size_t)k, sizeof(piece_copy_t));
+    if (!q) return -1;
+    size_t pool = s->pool_len;
+    int64_t vk = s->vkv_len, ek = s->ekv_len, n = s->n, m = s->m;
+    int rc = 0;
+    for (int i = 0; i < k && !rc; i++) {
+        ps_t* c = &pc[i].s;
+        q[i].s = s;
+        q[i].c = c;
+        for (int a = 0; a < c->vt.count && !rc; a++)
+            if ((q[i].vmap[a] = attr_index(s, &s->vt, c->vt.names[a], strlen(c->vt.names[a]), c->vt.is_string[a])) < 0)
+                rc = -1;
+        for (int a = 0; a < c->et.count && !rc; a++)
+            if ((q[i].emap[a] = attr_index(s, &s->et, c->et.names[a], strlen(c->et.names[a]), c->et.is_string[a])) < 0)
+                rc = -1;
+        q[i].pbase = pool;
+        q[i].vk0 = vk;
+        q[i].ek0 = ek;
+        q[i].n0 = n;
+        q[i].m0 = m;
+        pool += c->pool_len;
+        vk += c->vkv_len;
+        ek += c->ekv_len;
+        n += c->n;
+        m += c->m;
     }
-    {
-        const int64_t m0 = s->m;
-        SRT_GML_APPEND(esrc_id, m, m_cap, double, 0);
-        double* nd = (double*)realloc(s->edst_id, (size_t)s->m_cap * sizeof(double));
-        int64_t* ne = (int64_t*)realloc(s->estart, (size_t)(s->m_cap + 1) * sizeof(int64_t));
-        if (nd) s->edst_id = nd;
-        if (ne) s->estart = ne;
-        if (!nd || !ne) return -1;
-        memcpy(s->esrc_id + m0, c->esrc_id, (size_t)c->m * sizeof(double));
-        memcpy(s->edst_id + m0, c->edst_id, (size_t)c->m * sizeof(double));
-        for (int64_t i = 1; i <= c->m; i++) s->estart[m0 + i] = ek0 + c->estart[i];
-        s->m += c->m;
+    /* the merged arrays at their final sizes (the starts one longer) */
+    if (!rc) {
+        char* np = (char*)realloc(s->pool, pool > 0 ? pool : 1);
+        if (np) { s->pool = np; s->pool_cap = pool; }
+        kv_t* nv = (kv_t*)realloc(s->vkv, (size_t)(vk > 0 ? vk : 1) * sizeof(kv_t));
+        if (nv) { s->vkv = nv; s->vkv_cap = vk; }
+        kv_t* ne = (kv_t*)realloc(s->ekv, (size_t)(ek > 0 ? ek : 1) * sizeof(kv_t));
+        if (ne) { s->ekv = ne; s->ekv_cap = ek; }
+        double* ni = (double*)realloc(s->node_id, (size_t)(n > 0 ? n : 1) * sizeof(double));
+        if (ni) { s->node_id = ni; s->n_cap = n; }
+        int64_t* vs = (int64_t*)realloc(s->vstart, (size_t)(n + 1) * sizeof(int64_t));
+        if (vs) s->vstart = vs;
+        double* es = (double*)realloc(s->esrc_id, (size_t)(m > 0 ? m : 1) * sizeof(double));
+        if (es) { s->esrc_id = es; s->m_cap = m; }
+        double* ed = (double*)realloc(s->edst_id, (size_t)(m > 0 ? m : 1) * sizeof(double));
+        if (ed) s->edst_id = ed;
+        int64_t* est = (int64_t*)realloc(s->estart, (size_t)(m + 1) * sizeof(int64_t));
+        if (est) s->estart = est;
+        if (!np || !nv || !ne || !ni || !vs || !es || !ed || !est) rc = -1;
     }
-#undef SRT_GML_APPEND
-    return 0;
+    if (!rc) {
+        pthread_t th[GML_PAR_MAXT];
+        int started[GML_PAR_MAXT];
+        for (int i = 0; i < k; i++) {
+            started[i] = pthread_create(&th[i], NULL, piece_copy, &q[i]) == 0;
+            if (!started[i]) piece_copy(&q[i]);
+        }
+        for (int i = 0; i < k; i++)
+            if (started[i]) pthread_join(th[i], NULL);
+        s->pool_len = pool;
+        s->vkv_len = vk;
+        s->ekv_len = ek;
+        s->n = n;
+        s->m = m;
+    }
+    free(q);
+    return rc;
 }
 
 /* The graph list from s->p (just past its '['), in nt pieces. Returns the number of pieces when it
@@ -528,10 +558,9 @@ static int parse_graph_parallel(ps_t* s, int nt) {
         else ok = pc[i].closed;
     }
     int dir = -1, rc = ok;
-    for (int i = 0; i < k && rc == 1; i++) {
-        if (piece_merge(s, &pc[i].s)) rc = fail(s, "out of memory");
+    for (int i = 0; i < k; i++)
         if (pc[i].have_dir) dir = pc[i].dir;
-    }
+    if (rc == 1 && pieces_merge(s, pc, k)) rc = fail(s, "out of memory");
     if (rc == 1) {
         if (dir >= 0) s->directed = dir;
         s->p = pc[k - 1].s.p;
