@@ -1,6 +1,9 @@
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r06zi
+O=gpurun_out/r06zj
 mkdir -p $O
-SRT_LIB_PATH=$(pwd)/shadow_amd/ab_xp.so timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_xp -o run -- python3 bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline > $O/prof_xp.log 2>&1; \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_def -o run -- python3 bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline > $O/prof_def.log 2>&1
+gcc -O2 -std=gnu11 -Ishadow_amd/csrc -Iinclude tests/gml_parallel_check.c shadow_amd/csrc/gml.c -o /tmp/gmlchk -lpthread -lm && \
+python tools/gml_big.py /tmp/big.gml && \
+/tmp/gmlchk /tmp/big.gml 16 time > $O/gml_check.txt 2> $O/gml_box16.jsonl && \
+/tmp/gmlchk /tmp/big.gml 8 time >> $O/gml_check.txt 2> $O/gml_box8.jsonl && \
+bash tools/run_round.sh r06zj tfile:tests/test_gpu_dropin.py tfile:tests/test_gpu_parity.py
