@@ -1,9 +1,12 @@
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r06zj
+O=gpurun_out/r06zk
 mkdir -p $O
-gcc -O2 -std=gnu11 -Ishadow_amd/csrc -Iinclude tests/gml_parallel_check.c shadow_amd/csrc/gml.c -o /tmp/gmlchk -lpthread -lm && \
-python tools/gml_big.py /tmp/big.gml && \
-/tmp/gmlchk /tmp/big.gml 16 time > $O/gml_check.txt 2> $O/gml_box16.jsonl && \
-/tmp/gmlchk /tmp/big.gml 8 time >> $O/gml_check.txt 2> $O/gml_box8.jsonl && \
-bash tools/run_round.sh r06zj tfile:tests/test_gpu_dropin.py tfile:tests/test_gpu_parity.py
+bash tools/run_round.sh r06zk tfile:tests/test_gpu_levels.py tfile:tests/test_gpu_c4.py && \
+for i in 1 2; do
+for v in prev new; do
+LP=""; [ $v = prev ] && LP=$(pwd)/shadow_amd/ab_prev.so
+SRT_LIB_PATH=$LP timeout -k 10 300 python -u bench.py --workload c4 --steps 10 --warmup 1 --no-cpu-baseline > $O/bench_c4_${v}_$i.json 2> $O/bench_c4_${v}_$i.err || exit 1
+SRT_LIB_PATH=$LP timeout -k 10 300 python -u tools/solo_rank.py --ranks 8 --which 0,3,7 --wire-gbps 64 > $O/solo_n8_${v}_$i.jsonl 2> $O/solo_n8_${v}_$i.err || exit 1
+done
+done
