@@ -521,7 +521,8 @@ def dense_levels_tail(c: Ctx, wl, step, elapsed, stats, lat, rel, nr, ld):
     object names the one with the most time, the others are listed beside it, each against the
     roof that bounds it:
       lvl_step_kernel (per level d): its gathers are one 4-B Delta_{d-w}[k] word per (in-arc k->j
-        of weight w < d, target j, 32-source word) -- srt_build_stats.work_bytes -- served from the
+        of weight w < d, target j, 32-source word) the unit walked before its early exit --
+        srt_build_stats.work_bytes, counted on the device -- served from the
         L2 / MALL (the planes are re-read by every in-arc), so they are priced against the L2 peak
         (34.5 TB/s, MI355X_MICROARCH.md); its compulsory HBM bytes (the level plane written, R read
         and written, the earlier planes read once) are reported beside them;
@@ -547,7 +548,9 @@ def dense_levels_tail(c: Ctx, wl, step, elapsed, stats, lat, rel, nr, ld):
     kern = {
         "lvl_step_kernel": (ms_upd / max(n_upd, 1), wbytes / max(n_upd, 1), n_upd, "l2",
                             "per level d: one 4-B Delta_{d-w}[k] word gathered per (in-arc k->j "
-                            "of weight w < d, target j, 32-source word), served by the L2 / MALL; "
+                            "of weight w < d, target j, 32-source word) that the unit walked -- "
+                            "counted on the device, since a unit stops once its sources are all "
+                            "settled or found -- served by the L2 / MALL; "
                             f"averaged over the {levels} levels of a build"),
         "lvl_pred_kernel": (sum(s.ms_pred for s in stats) / k,
                             levels * plane + pairs * 4.0, k, "hbm",
@@ -610,9 +613,10 @@ def dense_levels_tail(c: Ctx, wl, step, elapsed, stats, lat, rel, nr, ld):
               "levels": int(s0.levels),
               # distinct arc reliabilities of the packed post pass (0: f64 rows)
               "rel_table": int(s0.rel_table),
-              "parallelism": f"row-shard x{world}" + (" (no collective during the levels: "
-                                                      "each rank's in-arc segment broadcast "
-                                                      "once, one verdict all-reduce)"
+              "parallelism": f"row-shard x{world}" + (" (one exchange and one agreement, "
+                                                      "the counts all-gathered, the first "
+                                                      "batch's arcs streamed weight by weight "
+                                                      "under the levels, one vote per batch)"
                                                       if world > 1 else ""),
               "rows_per_rank": nr, "ess_arcs": int(s0.ess_arcs),
               "max_level": int(s0.max_depth),

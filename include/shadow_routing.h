@@ -102,7 +102,8 @@ typedef struct srt_build_stats {
                           * build takes the smallest u -- the class where reliability can differ */
     int32_t levels;      /* dense level builds (dist_enc 12): the Dial level that settled every pair */
     int64_t work_bytes;  /* algorithmic bytes of the timed launches (level builds: the Delta words
-                          * gathered over all levels), 0 where the bench models them itself */
+                          * gathered over all levels, counted on the device -- a unit stops early
+                          * once its sources are settled), 0 where the bench models them itself */
     double ms_pred;      /* level builds (time_kernels = 1): HIP-event time of the predecessor pass
                           * (lvl_pred_kernel) */
     double ms_rel;       /* ... and of the path-order reliability pass (rel_tree_kernel and the

@@ -972,7 +972,7 @@ __global__ __launch_bounds__(256) void lvl_first_kernel(int n, int nw, int src0,
  * XCD takes a contiguous run of chunk-major units), so an XCD works on one source chunk at a time
  * and the Delta rows of that chunk are the only gathered data in its L2. */
 static __device__ __forceinline__ uint32_t lvl_step_unit(unsigned g, int d, int direct, int n, int nw,
-                                                       int nchunk, int src0, int nsrc,
+                                                       int nchunk, int src0, int nsrc, uint32_t& gath,
                                                        const int32_t* __restrict__ off,
                                                        const uint32_t* __restrict__ arcs,
                                                        const uint32_t* __restrict__ aoff,
@@ -1045,6 +1045,7 @@ static __device__ __forceinline__ uint32_t lvl_step_unit(unsigned g, int d, int 
                 v[q] = i + q < g1 ? *reinterpret_cast<const uint32_t*>(base + (a[q] + lane4)) : 0u;
 #pragma unroll
             for (int q = 0; q < LVL_SB; ++q) acc |= v[q];
+            if (valid) gath += (uint32_t)min(LVL_SB, g1 - i); /* the lane's 4-B gathers */
             if (i + LVL_SB < g1 && !__any(((acc | r) & full) != full)) break;
         }
     }
@@ -1085,22 +1086,32 @@ __global__ __launch_bounds__(256) void lvl_step_kernel(int d, int direct, int n,
                                                        uint8_t* __restrict__ done,
                                                        int* __restrict__ incomplete,
                                                        const int* __restrict__ prev,
-                                                       unsigned long long* __restrict__ nset) {
+                                                       unsigned long long* __restrict__ nset,
+                                                       unsigned long long* __restrict__ ngath) {
     /* the levels are enqueued in batches without a host round trip per level: a level whose
      * predecessor settled every pair (prev == 0) has nothing to do */
     if (prev && !__hip_atomic_load(prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     const unsigned x = blockIdx.x & 7u, per = nblk >> 3, L = gridDim.x >> 3;
     uint32_t settled = 0; /* pairs this lane settled (one add per block at the end) */
+    uint32_t gath = 0;    /* 4-B words this lane gathered (the early exit makes it data-dependent) */
     for (unsigned u = blockIdx.x >> 3; u < per; u += L)
-        settled += lvl_step_unit(x * per + u, d, direct, n, nw, nchunk, src0, nsrc, off, arcs, aoff, lev, R,
+        settled += lvl_step_unit(x * per + u, d, direct, n, nw, nchunk, src0, nsrc, gath, off, arcs, aoff, lev, R,
                                  done, incomplete);
-    unsigned long long c = settled;
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-    __shared__ unsigned long long s_c[4];
-    if ((threadIdx.x & 63) == 0) s_c[threadIdx.x >> 6] = c;
+    unsigned long long c = settled, gb = gath;
+    for (int o = 32; o > 0; o >>= 1) {
+        c += __shfl_xor(c, o);
+        gb += __shfl_xor(gb, o);
+    }
+    __shared__ unsigned long long s_c[4], s_g[4];
+    if ((threadIdx.x & 63) == 0) {
+        s_c[threadIdx.x >> 6] = c;
+        s_g[threadIdx.x >> 6] = gb;
+    }
     __syncthreads();
     if (threadIdx.x == 0 && (s_c[0] | s_c[1] | s_c[2] | s_c[3]))
         atomicAdd(nset, s_c[0] + s_c[1] + s_c[2] + s_c[3]);
+    if (threadIdx.x == 0 && (s_g[0] | s_g[1] | s_g[2] | s_g[3]))
+        atomicAdd(ngath, 4ull * (s_g[0] + s_g[1] + s_g[2] + s_g[3]));
 }
 
 /* Distance rows of the local sources from the levels: the u32 table rows (SRT_INF on padding) and
@@ -2296,6 +2307,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
      * settled early runs the later levels as no-ops (lvl_step_kernel's prev test) and keeps its D. */
     int D = 0, all_done = 0, hflag[2] = {0, 0};
     unsigned long long* nset = reinterpret_cast<unsigned long long*>(dagree + 4);
+    unsigned long long* ngath = nset + 1; /* the level kernels' gathered bytes (dhist word 515) */
     const int ev0 = evp ? evp->used : 0;
     if (evp && (rc = evpool_reserve(evp, ev0 + 2 * lmax))) return rc;
     int wq = 0; /* the streamed weights enqueued so far */
@@ -2329,7 +2341,7 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
             } else {
                 lvl_step_kernel<<<pgrid, 256, 0, st>>>(d, d <= streamed, n, nw, nchunk, row0, nrows, nblk, off,
                                                       arcs, aoff, lev, Rb, done, dinc + d,
-                                                      dinc + d - 1, nset);
+                                                      dinc + d - 1, nset, ngath);
             }
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));
         }
@@ -2384,12 +2396,11 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
     /* the side stream's last weight before anything frees the wire (lvl_free waits for it too) */
     if (wq) L->wlast = wev[wq];
     if (evp && D) evp->used = ev0 + 2 * D; /* the levels that did work */
-    int64_t gathered = 0;
-    for (int d = 1; d <= D; ++d) {
-        double below = 0;
-        for (int x = 1; x < d; ++x) below += (double)hist[x];
-        gathered += (int64_t)(below * (double)nw * 4.0);
-    }
+    /* the bytes the level kernels gathered, counted on the device (the early exit skips the
+     * later weight groups of a unit, so the model -- every arc of weight < d for every level --
+     * would overstate them) */
+    const unsigned long long* hw_last = pin + LVL_PIN_HW; /* the last batch's read-back */
+    const int64_t gathered = (int64_t)hw_last[LVL_H_AGREE + 3 - LVL_H_INC];
     if (!all_done) return SRT_OK; /* the verdict, alike on every rank (the summed vote) */
     int ntab = 0;
     if (want_rt && !hflag[0] && hflag[1] <= LVL_RT_CAP)

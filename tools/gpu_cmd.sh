@@ -1,12 +1,3 @@
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r06zk
-mkdir -p $O
-bash tools/run_round.sh r06zk tfile:tests/test_gpu_levels.py tfile:tests/test_gpu_c4.py && \
-for i in 1 2; do
-for v in prev new; do
-LP=""; [ $v = prev ] && LP=$(pwd)/shadow_amd/ab_prev.so
-SRT_LIB_PATH=$LP timeout -k 10 300 python -u bench.py --workload c4 --steps 10 --warmup 1 --no-cpu-baseline > $O/bench_c4_${v}_$i.json 2> $O/bench_c4_${v}_$i.err || exit 1
-SRT_LIB_PATH=$LP timeout -k 10 300 python -u tools/solo_rank.py --ranks 8 --which 0,3,7 --wire-gbps 64 > $O/solo_n8_${v}_$i.jsonl 2> $O/solo_n8_${v}_$i.err || exit 1
-done
-done
+bash tools/pmc_kernel.sh c4 'lvl_pred|rel_pk|lvl_step|transpose|lvl_arcs' r06zm/pmc_c4 'fetch write tcc'
