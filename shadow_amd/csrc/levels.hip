@@ -41,6 +41,8 @@
 #define LVL_B1 5
 #define LVL_WMAX 254   /* largest level budget (distances stay u8: the post pass's small path) */
 #define LVL_PB 12 /* lvl_pred_kernel: gathers per pipelined batch */
+#define LVL_NEAR_NW 2048 /* lvl_near_kernel: a target's plane row in LDS, four per workgroup */
+#define LVL_NEAR_MIN_NW 512 /* ... and only for shares of at least 16,384 sources */
 
 /* ---- in-arc extraction ------------------------------------------------------------------- */
 /* COUNT: per (target, weight) histogram of arcs with 1 <= w <= LVL_WMAX; FILL: the arcs (k | w << 16)
@@ -968,6 +970,52 @@ __global__ __launch_bounds__(256) void lvl_first_kernel(int n, int nw, int src0,
     }
 }
 
+/* Levels 2 and 3, the near part: the bits that arcs of weight d (Delta_0: the own source itself)
+ * and of weight d - 1 (Delta_1) contribute to Delta_d[t], set into plane d - 1 before
+ * lvl_step_kernel, which then skips that weight group (its gathers read a plane that is nearly
+ * empty: Delta_1[u] is u's ~33 weight-1 in-arcs among n sources). Delta_1[u] is exactly u's
+ * weight-1 run of in-arcs, so a wave per target t reads, for each in-arc (u, d - 1), u's run
+ * (~130 B, coalesced) instead of one 256-B plane slice per source chunk, and ORs the sources
+ * into an LDS copy of t's plane row, which it then writes whole. add: the row already holds the
+ * own-arc bits (streamed N > 1, lvl_direct_kernel), so it is read first and the weight-d run is
+ * not scanned. */
+__global__ __launch_bounds__(256) void lvl_near_kernel(int d, int n, int nw, int src0, int nsrc, int add,
+                                                       const int32_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ arcs,
+                                                       uint32_t* __restrict__ lev) {
+    extern __shared__ uint32_t near_row[]; /* per wave: nw words */
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int t = blockIdx.x * 4 + wv;
+    uint32_t* row = near_row + (size_t)wv * nw;
+    const size_t plane = (size_t)n * nw;
+    uint32_t* prow = lev + (size_t)(d - 1) * plane + (size_t)(t < n ? t : 0) * nw;
+    for (int i = lane; i < nw; i += 64) row[i] = t < n && add ? prow[i] : 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (t < n) {
+        const int32_t* ot = off + (size_t)t * LVL_STRIDE;
+        if (!add) /* the own sources' arcs of weight d into t */
+            for (int i = ot[d] + lane; i < ot[d + 1]; i += 64) {
+                const int ks = (int)(arcs[i] & 0xFFFFu) - src0;
+                if (ks >= 0 && ks < nsrc) atomicOr(&row[ks >> 5], 1u << (ks & 31));
+            }
+        for (int a = ot[d - 1]; a < ot[d]; ++a) { /* each in-arc (u, d - 1): u's weight-1 run */
+            const int u = (int)(arcs[a] & 0xFFFFu);
+            const int b0 = off[(size_t)u * LVL_STRIDE + 1], b1 = off[(size_t)u * LVL_STRIDE + 2];
+            for (int i = b0 + lane; i < b1; i += 64) {
+                const int ks = (int)(arcs[i] & 0xFFFFu) - src0;
+                if (ks >= 0 && ks < nsrc) atomicOr(&row[ks >> 5], 1u << (ks & 31));
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (t < n)
+        for (int i = lane; i < nw; i += 64) prow[i] = row[i];
+}
+
 /* Level d: one wave per (target j, 64-word source chunk c). Units are handed out XCD-major (each
  * XCD takes a contiguous run of chunk-major units), so an XCD works on one source chunk at a time
  * and the Delta rows of that chunk are the only gathered data in its L2. */
@@ -1033,6 +1081,7 @@ static __device__ __forceinline__ uint32_t lvl_step_unit(unsigned g, int d, int 
     const uint32_t full = !valid ? 0u : s0 + 32 <= n ? 0xFFFFFFFFu : s0 >= n ? 0u : (1u << (n - s0)) - 1u;
     constexpr int LVL_SB = 16; /* (8 measured the same, 32/48 slower; pipelined batches did not help) */
     for (int w = 1; w < d; ++w) {
+        if (direct == 2 && w == d - 1) continue; /* lvl_near_kernel set this group's bits */
         if (!__any(((acc | r) & full) != full)) break;
         const int g1 = oj[w + 1];
         const char* base = reinterpret_cast<const char*>(lev + (size_t)(d - w - 1) * plane);
@@ -2339,8 +2388,18 @@ int srt_levels_build(const srt_comm* comm, int n, int ld, int row0, int nrows, i
                                                                           lev, Rb);
                 }
             } else {
-                lvl_step_kernel<<<pgrid, 256, 0, st>>>(d, d <= streamed, n, nw, nchunk, row0, nrows, nblk, off,
-                                                      arcs, aoff, lev, Rb, done, dinc + d,
+                /* levels 2 and 3: the weight-d and weight-(d - 1) groups from the in-arc runs
+                 * (lvl_near_kernel); later levels stop after their first group almost
+                 * everywhere (the early exit), so they keep the gathers. The runs are read whole
+                 * for every target whatever a rank's share of the sources, so they pay only for
+                 * a wide share (C4: 14.5 -> 14.1 ms on one GPU; a rank of N = 8, 128 words,
+                 * went 2.55 -> 2.86 ms) */
+                const bool near = d <= 3 && d <= lx && nw >= LVL_NEAR_MIN_NW && nw <= LVL_NEAR_NW;
+                if (near)
+                    lvl_near_kernel<<<srt_ceil_div(n, 4), 256, 4 * (size_t)nw * sizeof(uint32_t), st>>>(
+                        d, n, nw, row0, nrows, d <= streamed, off, arcs, lev);
+                lvl_step_kernel<<<pgrid, 256, 0, st>>>(d, near ? 2 : d <= streamed, n, nw, nchunk, row0, nrows, nblk,
+                                                      off, arcs, aoff, lev, Rb, done, dinc + d,
                                                       dinc + d - 1, nset, ngath);
             }
             if (evp) SRT_HIPCHK(hipEventRecord(evp->ev[evp->used++], st));

@@ -1,7 +1,13 @@
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r06zo
+O=gpurun_out/r06zq
 mkdir -p $O
-bash tools/run_round.sh r06zo tests && \
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 && \
-timeout -k 10 600 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err
+bash tools/run_round.sh r06zq tfile:tests/test_gpu_levels.py tfile:tests/test_gpu_c4.py tfile:tests/test_gpu_protocol.py tfile:tests/test_gpu_metric.py && \
+for i in 1 2; do
+for v in prev new; do
+LP=""; [ $v = prev ] && LP=$(pwd)/shadow_amd/ab_prev.so
+SRT_LIB_PATH=$LP timeout -k 10 300 python -u bench.py --workload c4 --steps 10 --warmup 1 --no-cpu-baseline > $O/bench_c4_${v}_$i.json 2> $O/bench_c4_${v}_$i.err || exit 1
+SRT_LIB_PATH=$LP timeout -k 10 300 python -u tools/solo_rank.py --ranks 8 --which 0,3,7 --wire-gbps 64 > $O/solo_n8_${v}_$i.jsonl 2> $O/solo_n8_${v}_$i.err || exit 1
+SRT_LIB_PATH=$LP timeout -k 10 300 python -u tools/solo_rank.py --ranks 2 --which 0,1 --wire-gbps 64 > $O/solo_n2_${v}_$i.jsonl 2> $O/solo_n2_${v}_$i.err || exit 1
+done
+done
