@@ -1000,12 +1000,36 @@ __global__ __launch_bounds__(256) void lvl_near_kernel(int d, int n, int nw, int
                 const int ks = (int)(arcs[i] & 0xFFFFu) - src0;
                 if (ks >= 0 && ks < nsrc) atomicOr(&row[ks >> 5], 1u << (ks & 31));
             }
-        for (int a = ot[d - 1]; a < ot[d]; ++a) { /* each in-arc (u, d - 1): u's weight-1 run */
-            const int u = (int)(arcs[a] & 0xFFFFu);
-            const int b0 = off[(size_t)u * LVL_STRIDE + 1], b1 = off[(size_t)u * LVL_STRIDE + 2];
-            for (int i = b0 + lane; i < b1; i += 64) {
-                const int ks = (int)(arcs[i] & 0xFFFFu) - src0;
-                if (ks >= 0 && ks < nsrc) atomicOr(&row[ks >> 5], 1u << (ks & 31));
+        /* each in-arc (u, d - 1): u's weight-1 run. The runs' bounds of 64 arcs come in one
+         * vector load per lane, then four runs are read at a time (their first 64 entries in
+         * flight together; a longer run's tail after) */
+        const int a1 = ot[d];
+        for (int c0 = ot[d - 1]; c0 < a1; c0 += 64) {
+            int ub0 = 0, ub1 = 0;
+            if (c0 + lane < a1) {
+                const int u = (int)(arcs[c0 + lane] & 0xFFFFu);
+                ub0 = off[(size_t)u * LVL_STRIDE + 1];
+                ub1 = off[(size_t)u * LVL_STRIDE + 2];
+            }
+            const int na = min(64, a1 - c0);
+            for (int k = 0; k < na; k += 4) {
+                uint32_t e[4];
+                int b0[4], b1[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    b0[q] = k + q < na ? __builtin_amdgcn_readlane(ub0, k + q) : 0;
+                    b1[q] = k + q < na ? __builtin_amdgcn_readlane(ub1, k + q) : 0;
+                    e[q] = b0[q] + lane < b1[q] ? arcs[b0[q] + lane] : 0xFFFFFFFFu;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int ks = (int)(e[q] & 0xFFFFu) - src0;
+                    if (e[q] != 0xFFFFFFFFu && ks >= 0 && ks < nsrc) atomicOr(&row[ks >> 5], 1u << (ks & 31));
+                    for (int i = b0[q] + 64 + lane; i < b1[q]; i += 64) { /* (runs past 64) */
+                        const int kt = (int)(arcs[i] & 0xFFFFu) - src0;
+                        if (kt >= 0 && kt < nsrc) atomicOr(&row[kt >> 5], 1u << (kt & 31));
+                    }
+                }
             }
         }
     }
