@@ -1,13 +1,11 @@
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r06zr
+O=gpurun_out/r06zs
 mkdir -p $O
-bash tools/run_round.sh r06zr tfile:tests/test_gpu_levels.py tfile:tests/test_gpu_c4.py tfile:tests/test_gpu_protocol.py && \
-AB_TESTS="tests/test_gpu_protocol.py tests/test_gpu_levels.py" SRT_LIB_PATH=$(pwd)/shadow_amd/ab_n8.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 tests/test_gpu_protocol.py tests/test_gpu_levels.py -m gpu > $O/tests_n8.log 2>&1 && \
-for i in 1 2; do
-for v in prev new n8; do
-LP=""; [ $v = prev ] && LP=$(pwd)/shadow_amd/ab_prev.so; [ $v = n8 ] && LP=$(pwd)/shadow_amd/ab_n8.so
-SRT_LIB_PATH=$LP timeout -k 10 300 python -u bench.py --workload c4 --steps 10 --warmup 1 --no-cpu-baseline > $O/bench_c4_${v}_$i.json 2> $O/bench_c4_${v}_$i.err || exit 1
-SRT_LIB_PATH=$LP timeout -k 10 300 python -u tools/solo_rank.py --ranks 8 --which 0,3,7 --wire-gbps 64 > $O/solo_n8_${v}_$i.jsonl 2> $O/solo_n8_${v}_$i.err || exit 1
-done
-done
+bash tools/run_round.sh r06zs tests && \
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 && \
+timeout -k 10 600 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err && \
+bash tools/run_round.sh r06zs bench:c4:20 prof:c4 && \
+timeout -k 10 300 python -u tools/solo_rank.py --ranks 8 --which 0,3,7 --wire-gbps 0,64 > $O/solo_n8.jsonl 2> $O/solo_n8.err && \
+timeout -k 10 300 python -u tools/solo_rank.py --ranks 4 --which 0,3 --wire-gbps 0,64 > $O/solo_n4.jsonl 2> $O/solo_n4.err && \
+timeout -k 10 300 python -u tools/solo_rank.py --ranks 2 --which 0,1 --wire-gbps 0,64 > $O/solo_n2.jsonl 2> $O/solo_n2.err
